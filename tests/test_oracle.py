@@ -1,0 +1,89 @@
+"""CPU: pin the oracle (oracle/msda_oracle.c) against the golden vectors generated from the
+reference (tests/golden/make_golden.py) -- the reference test's own inputs (pdvc/ops/test.py:21-44)
+and 1-D PDVC pyramids -- plus finite differences.  No GPU needed."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(G, name + ".npz"), allow_pickle=False)
+
+
+@pytest.mark.parametrize("pad", ["zeros", "border"])
+def test_reftest_inputs(pad):
+    d = load("op_reftest")
+    out = O.msda_forward(d["value"], d["shapes"], d["lsi"], d["loc"], d["attn"], pad)
+    np.testing.assert_allclose(out, d[f"{pad}_out"], rtol=1e-12, atol=1e-14)
+    gv, gl, ga = O.msda_backward(d["value"], d["shapes"], d["lsi"], d["loc"], d["attn"], d["grad_out"], pad)
+    np.testing.assert_allclose(gv, d[f"{pad}_grad_value"], rtol=1e-10, atol=1e-14)
+    np.testing.assert_allclose(gl, d[f"{pad}_grad_loc"], rtol=1e-10, atol=1e-14)
+    np.testing.assert_allclose(ga, d[f"{pad}_grad_attn"], rtol=1e-10, atol=1e-14)
+
+
+def test_reftest_padding_modes_differ():
+    """the fork's CPU core (border) and the CUDA op (zeros) disagree on test.py's inputs."""
+    d = load("op_reftest")
+    assert np.abs(d["zeros_out"] - d["border_out"]).max() > 1e-4
+
+
+@pytest.mark.parametrize("D", [30, 32, 64, 71])
+@pytest.mark.parametrize("pad", ["zeros", "border"])
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+def test_1d_pyramids(D, pad, dt):
+    d = load(f"op_1d_D{D}")
+    npdt = np.float64 if dt == "f64" else np.float32
+    tol = dict(rtol=1e-11, atol=1e-12) if dt == "f64" else dict(rtol=2e-5, atol=2e-5)
+    args = [d["value"].astype(npdt), d["shapes"], d["lsi"], d["loc"].astype(npdt), d["attn"].astype(npdt)]
+    out = O.msda_forward(*args, pad)
+    np.testing.assert_allclose(out, d[f"{pad}_{dt}_out"], **tol)
+    gv, gl, ga = O.msda_backward(*args, d["grad_out"].astype(npdt), pad)
+    np.testing.assert_allclose(gv, d[f"{pad}_{dt}_grad_value"], **tol)
+    np.testing.assert_allclose(ga, d[f"{pad}_{dt}_grad_attn"], **tol)
+    # y-gradients: torch's border clip zeroes them (H=1 => iy clipped); the CUDA op reports H*dval/dh
+    np.testing.assert_allclose(gl[..., 0], d[f"{pad}_{dt}_grad_loc"][..., 0], **tol)
+    if pad == "border":
+        np.testing.assert_allclose(gl[..., 1], d[f"{pad}_{dt}_grad_loc"][..., 1], **tol)
+
+
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+def test_sample_mode(dt):
+    d = load("op_sample")
+    npdt = np.float64 if dt == "f64" else np.float32
+    tol = dict(rtol=1e-11, atol=1e-12) if dt == "f64" else dict(rtol=2e-5, atol=2e-5)
+    v, lo = d["value"].astype(npdt), d["loc"].astype(npdt)
+    s = O.msda_sample(v, d["shapes"], d["lsi"], lo, "border")
+    np.testing.assert_allclose(s, d[f"{dt}_samples"], **tol)
+    gv, gl = O.msda_sample_backward(v, d["shapes"], d["lsi"], lo, d["grad_samples"].astype(npdt), "border")
+    np.testing.assert_allclose(gv, d[f"{dt}_grad_value"], **tol)
+    np.testing.assert_allclose(gl, d[f"{dt}_grad_loc"], **tol)
+
+
+def test_zeros_finite_difference():
+    """Central differences of the zeros oracle (the reference test's gradcheck, test.py:63-86)."""
+    rng = np.random.RandomState(0)
+    shapes = np.array([[6, 4], [3, 2]])
+    lsi = np.array([0, 24])
+    N, M, D, Lq, L, P = 1, 2, 5, 2, 2, 2
+    v = rng.rand(N, 30, M, D) * 0.01
+    loc = rng.uniform(0.05, 0.95, size=(N, Lq, M, L, P, 2))
+    a = rng.rand(N, Lq, M, L, P) + 1e-5
+    g = rng.randn(N, Lq, M * D)
+    gv, gl, ga = O.msda_backward(v, shapes, lsi, loc, a, g, "zeros")
+    f = lambda v_, l_, a_: (O.msda_forward(v_, shapes, lsi, l_, a_, "zeros") * g).sum()
+    eps = 1e-6
+    for arr, grad in ((v, gv), (loc, gl), (a, ga)):
+        flat = arr.reshape(-1)
+        for i in rng.choice(flat.size, 12, replace=False):
+            old = flat[i]
+            flat[i] = old + eps
+            fp = f(v, loc, a)
+            flat[i] = old - eps
+            fm = f(v, loc, a)
+            flat[i] = old
+            assert abs((fp - fm) / (2 * eps) - grad.reshape(-1)[i]) < 1e-6
