@@ -1,0 +1,513 @@
+// msda1d.hip -- fused 1-D multi-scale deformable attention for PDVC on MI355X (gfx950).
+//
+// Replaces the body of MSDeformAttn.forward between its two projections
+// (pdvc/ops/modules/ms_deform_attn.py:167-192): softmax of the attention logits, sampling-location math
+// (ref dim 1: loc = ref + off / T_l; ref dim 2: loc = c + off / P * len * 0.5), the 1-D -> 2-D lift
+// (y = 0.5, H = 1) and the reference CUDA op (ms_deform_im2col_cuda.cuh:238-300, zero padding).
+// PDVC's pyramid is 1-D, so only the two corners on the H=0 row can be in range (for H=1 the CUDA
+// kernel's h_im is exactly 0, so lh = 0 and the two lower corners carry weight 0): the kernels read
+// exactly those two rows.  Results equal the reference op's float arithmetic up to FMA contraction.
+//
+// Layout / mapping (MI355X-first):
+//   * forward and backward-query: one wave64 per (video, query, group of heads).  A lane owns CPL = 8
+//     consecutive channels of one head (two float4 loads per corner: 1 KiB per wave-instruction over
+//     8 heads at D = 64), LPH = D / CPL lanes per head.  A (video, query) row of M*D = 512 floats is
+//     exactly one wave at PDVC's shape, so the 2 KiB output row is written by one wave.
+//   * backward-value: destination-centric.  One workgroup owns a 64-row tile of one (video, head, level)
+//     and accumulates its grad_value rows in LDS (ds_add_f32) from every sample whose two corners touch
+//     the tile, then writes the tile once with plain stores -- no global float atomics (the reference
+//     issues 2 per channel per sample, ~63 MB of atomics per video at T=512, which would cap the kernel
+//     at the ~1.3 TB/s atomic rate) and every grad_value element has exactly one writer.
+//   * blocks are XCD-remapped so that all blocks of one video run on one XCD and share its L2.
+#include "pdvc_common.h"
+
+namespace pdvc {
+
+constexpr int kNS = 16;   // samples per (query, head) = L * P; PDVC: 4 levels x 4 points
+constexpr int kP = 4;     // points per level
+constexpr int kL = 4;     // levels
+constexpr int kTile = 64; // grad_value tile rows per workgroup
+
+struct Levels1d {
+    int T[kL];
+    int start[kL];
+};
+
+template <int CPL>
+__device__ __forceinline__ void load_row(VecF<CPL>& v, const float* __restrict__ p, bool ok) {
+    if (ok) v.load(p);
+    else v.zero();
+}
+
+// -------------------------------------------------------------------------------------------------
+// forward
+// -------------------------------------------------------------------------------------------------
+template <int CPL, int LPH, int RD>
+__global__ __launch_bounds__(256) void msda1d_fwd_kernel(
+    const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
+    int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
+    int D, int waves_per_row, int total_waves, float* __restrict__ out, float* __restrict__ save_attn,
+    float* __restrict__ save_loc) {
+    constexpr int HPW = 64 / LPH;
+    const int lane = threadIdx.x & 63;
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int wave = lb * 4 + (threadIdx.x >> 6);
+    if (wave >= total_waves) return;
+    const int row = wave / waves_per_row;
+    const int hg = wave - row * waves_per_row;
+    const int b = row / Lq;
+    const int sub = lane % LPH;
+    const int m = hg * HPW + lane / LPH;
+    if (m >= M) return;
+    const int c0 = sub * CPL;
+    const float* prow = proj + (size_t)row * proj_stride;
+
+    // softmax over the head's L*P logits (ms_deform_attn.py:168-169)
+    float a[kNS], off[kNS];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < kNS; ++j) {
+        a[j] = prow[logit_base + m * kNS + j];
+        off[j] = prow[off_base + m * kNS + j];
+        mx = fmaxf(mx, a[j]);
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < kNS; ++j) {
+        a[j] = expf(a[j] - mx);
+        sum += a[j];
+    }
+#pragma unroll
+    for (int j = 0; j < kNS; ++j) a[j] = a[j] / sum;
+
+    float r0[kL], r1[kL];
+#pragma unroll
+    for (int l = 0; l < kL; ++l) {
+        r0[l] = ref[((size_t)row * kL + l) * RD];
+        r1[l] = (RD == 2) ? ref[((size_t)row * kL + l) * RD + 1] : 0.f;
+    }
+
+    const size_t MD = (size_t)M * D;
+    const float* vbase = value + (size_t)b * S * MD + (size_t)m * D + c0;
+    const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
+    VecF<CPL> acc;
+    acc.zero();
+#pragma unroll
+    for (int l = 0; l < kL; ++l) {
+        const int T = lv.T[l], st = lv.start[l];
+        const float Tf = (float)T;
+#pragma unroll
+        for (int p = 0; p < kP; ++p) {
+            const int j = l * kP + p;
+            // ms_deform_attn.py:171-177 (same evaluation order)
+            const float loc = (RD == 1) ? r0[l] + off[j] / Tf : r0[l] + ((off[j] / (float)kP) * r1[l]) * 0.5f;
+            if (save_loc && sub == (j % LPH)) {
+                const size_t si = ((size_t)row * M + m) * kNS + j;
+                save_loc[si] = loc;
+                save_attn[si] = a[j];
+            }
+            const float x = loc * Tf - 0.5f;  // w_im (.cuh:284); h_im == 0 for H == 1
+            if (x > -1.f && x < Tf) {
+                const float xf = floorf(x);
+                const int i0 = (int)xf;
+                const float lw = x - xf, hw = 1.f - lw;
+                const bool ok1 = i0 >= 0 && !(mbase && mbase[st + i0]);
+                const bool ok2 = i0 + 1 <= T - 1 && !(mbase && mbase[st + i0 + 1]);
+                VecF<CPL> v1, v2;
+                load_row(v1, vbase + (size_t)(st + i0) * MD, ok1);
+                load_row(v2, vbase + (size_t)(st + i0 + 1) * MD, ok2);
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) acc.v[c] += (hw * v1.v[c] + lw * v2.v[c]) * a[j];
+            }
+        }
+    }
+    acc.store(out + (size_t)row * MD + (size_t)m * D + c0);
+}
+
+// -------------------------------------------------------------------------------------------------
+// backward, query side: grad of the offset and attention logits (+ reference points)
+// -------------------------------------------------------------------------------------------------
+template <int CPL, int LPH, int RD>
+__global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
+    const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
+    int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
+    int D, int waves_per_row, int total_waves, const float* __restrict__ gout, const float* __restrict__ save_attn,
+    const float* __restrict__ save_loc, float* __restrict__ grad_proj, float* __restrict__ grad_ref) {
+    constexpr int HPW = 64 / LPH;
+    constexpr int SPL = kNS / LPH;  // samples owned per lane after the reduce-scatter
+    static_assert(SPL >= 1, "LPH must be <= 16");
+    const int lane = threadIdx.x & 63;
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int wave = lb * 4 + (threadIdx.x >> 6);
+    if (wave >= total_waves) return;  // wave-uniform
+    const int row = wave / waves_per_row;
+    const int hg = wave - row * waves_per_row;
+    const int b = row / Lq;
+    const int sub = lane % LPH;
+    const int m_raw = hg * HPW + lane / LPH;
+    const bool active = m_raw < M;
+    const int m = active ? m_raw : 0;
+    const int c0 = sub * CPL;
+    const size_t MD = (size_t)M * D;
+    const float* vbase = value + (size_t)b * S * MD + (size_t)m * D + c0;
+    const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
+    const size_t sbase = ((size_t)row * M + m) * kNS;
+
+    VecF<CPL> g;
+    load_row(g, gout + (size_t)row * MD + (size_t)m * D + c0, active);
+
+    // part[2j] = sum_c g*val ; part[2j+1] = sum_c g*(v2 - v1)   (this lane's channels)
+    float part[2 * kNS];
+#pragma unroll
+    for (int l = 0; l < kL; ++l) {
+        const int T = lv.T[l], st = lv.start[l];
+        const float Tf = (float)T;
+#pragma unroll
+        for (int p = 0; p < kP; ++p) {
+            const int j = l * kP + p;
+            float s1 = 0.f, s2 = 0.f;
+            const float loc = active ? save_loc[sbase + j] : 0.f;
+            const float x = loc * Tf - 0.5f;
+            if (active && x > -1.f && x < Tf) {
+                const float xf = floorf(x);
+                const int i0 = (int)xf;
+                const float lw = x - xf, hw = 1.f - lw;
+                const bool ok1 = i0 >= 0 && !(mbase && mbase[st + i0]);
+                const bool ok2 = i0 + 1 <= T - 1 && !(mbase && mbase[st + i0 + 1]);
+                VecF<CPL> v1, v2;
+                load_row(v1, vbase + (size_t)(st + i0) * MD, ok1);
+                load_row(v2, vbase + (size_t)(st + i0 + 1) * MD, ok2);
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    s1 += g.v[c] * (hw * v1.v[c] + lw * v2.v[c]);
+                    s2 += g.v[c] * (v2.v[c] - v1.v[c]);
+                }
+            }
+            part[2 * j] = s1;
+            part[2 * j + 1] = s2;
+        }
+    }
+    group_reduce_scatter<2 * kNS, LPH>(part, lane);
+
+    // lane `sub` now owns samples j = sub*SPL + k, k < SPL: part[2k] = grad_attn, part[2k+1] = sum g*(v2-v1)
+    float aj[SPL], ga[SPL];
+    float dpart = 0.f;
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) {
+        const int j = sub * SPL + k;
+        aj[k] = active ? save_attn[sbase + j] : 0.f;
+        ga[k] = part[2 * k];
+        dpart += aj[k] * ga[k];
+    }
+    const float delta = group_allreduce<LPH>(dpart);  // softmax backward: sum_j a_j * grad_a_j
+
+    float gr0[kL], gr1[kL];
+#pragma unroll
+    for (int l = 0; l < kL; ++l) { gr0[l] = 0.f; gr1[l] = 0.f; }
+    const float* prow = proj + (size_t)row * proj_stride;
+    float* gprow = grad_proj + (size_t)row * proj_stride;
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) {
+        const int j = sub * SPL + k;
+        const int l = j / kP;
+        const float Tf = (float)lv.T[l];
+        // CUDA: grad_loc_w = W * grad_w_weight * (top_grad * attn), summed over channels (.cuh:158)
+        const float gloc = Tf * (part[2 * k + 1] * aj[k]);
+        const float glogit = aj[k] * (ga[k] - delta);
+        float goff;
+        if (RD == 1) {
+            goff = gloc / Tf;
+#pragma unroll
+            for (int ll = 0; ll < kL; ++ll) if (ll == l) gr0[ll] += gloc;
+        } else {
+            const float r1 = ref[((size_t)row * kL + l) * 2 + 1];
+            const float t2 = gloc * 0.5f;
+            goff = (t2 * r1) / (float)kP;
+            const float o = active ? prow[off_base + m * kNS + j] : 0.f;
+#pragma unroll
+            for (int ll = 0; ll < kL; ++ll) if (ll == l) { gr0[ll] += gloc; gr1[ll] += t2 * (o / (float)kP); }
+        }
+        if (active) {
+            gprow[off_base + m * kNS + j] = goff;
+            gprow[logit_base + m * kNS + j] = glogit;
+        }
+    }
+    if (grad_ref) {
+        // sum over every head of the row: all lanes of the wave, then (several waves per row) atomics
+#pragma unroll
+        for (int l = 0; l < kL; ++l) {
+            float v0 = gr0[l];
+#pragma unroll
+            for (int d = 32; d > 0; d >>= 1) v0 += __shfl_xor(v0, d, PDVC_WAVE);
+            float v1 = 0.f;
+            if (RD == 2) {
+                v1 = gr1[l];
+#pragma unroll
+                for (int d = 32; d > 0; d >>= 1) v1 += __shfl_xor(v1, d, PDVC_WAVE);
+            }
+            if (lane == 0) {
+                float* dst = grad_ref + ((size_t)row * kL + l) * RD;
+                if (waves_per_row == 1) {
+                    dst[0] = v0;
+                    if (RD == 2) dst[1] = v1;
+                } else {
+                    atomicAdd(dst, v0);
+                    if (RD == 2) atomicAdd(dst + 1, v1);
+                }
+            }
+        }
+    }
+}
+
+// -------------------------------------------------------------------------------------------------
+// backward, value side: destination-centric LDS tiles
+// -------------------------------------------------------------------------------------------------
+struct TileMap {
+    int prefix[kL + 1];  // tiles before level l (per (video, head))
+};
+
+template <int DMAX>
+__global__ __launch_bounds__(256) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
+                                                                TileMap tm, int Lq, int S, int M, int D,
+                                                                const float* __restrict__ gout,
+                                                                const float* __restrict__ save_attn,
+                                                                const float* __restrict__ save_loc,
+                                                                float* __restrict__ grad_value) {
+    __shared__ float acc[kTile * DMAX];
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int ntiles = tm.prefix[kL];
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int bm = lb / ntiles;
+    const int tile = lb - bm * ntiles;
+    const int b = bm / M, m = bm - b * M;
+    int l = 0;
+#pragma unroll
+    for (int i = 1; i < kL; ++i)
+        if (tile >= tm.prefix[i]) l = i;
+    const int r0 = (tile - tm.prefix[l]) * kTile;
+    const int T = lv.T[l], st = lv.start[l];
+    const float Tf = (float)T;
+    const int nrows = min(kTile, T - r0);
+    for (int i = threadIdx.x; i < kTile * D; i += blockDim.x) acc[i] = 0.f;
+    __syncthreads();
+
+    const size_t MD = (size_t)M * D;
+    const int nsamp = Lq * kP;
+    for (int base = wid * 64; base < nsamp; base += 256) {
+        const int i = base + lane;
+        bool rel = false;
+        int q = 0, x0 = 0;
+        float hw = 0.f, lw = 0.f, a = 0.f;
+        if (i < nsamp) {
+            q = i / kP;
+            const int p = i - q * kP;
+            const size_t si = (((size_t)b * Lq + q) * M + m) * kNS + l * kP + p;
+            const float x = save_loc[si] * Tf - 0.5f;
+            if (x > -1.f && x < Tf) {
+                const float xf = floorf(x);
+                x0 = (int)xf;
+                if (x0 >= r0 - 1 && x0 <= r0 + nrows - 1) {
+                    rel = true;
+                    lw = x - xf;
+                    hw = 1.f - lw;
+                    a = save_attn[si];
+                }
+            }
+        }
+        unsigned long long bal = __ballot(rel);
+        while (bal) {
+            // pick up to 8 relevant samples (wave-uniform) and keep their 8 gradient-row loads in flight
+            int qs[8], xs[8];
+            float w1[8], w2[8], aa[8];
+            int cnt = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                qs[k] = 0; xs[k] = -2; w1[k] = 0.f; w2[k] = 0.f; aa[k] = 0.f;
+                if (bal) {
+                    const int src = __ffsll((long long)bal) - 1;
+                    bal &= bal - 1;
+                    qs[k] = __builtin_amdgcn_readlane(q, src);
+                    xs[k] = __builtin_amdgcn_readlane(x0, src);
+                    w1[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hw), src));
+                    w2[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lw), src));
+                    aa[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a), src));
+                    cnt = k + 1;
+                }
+            }
+            for (int c = lane; c < D; c += 64) {
+                float gv[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    gv[k] = (k < cnt) ? gout[(((size_t)b * Lq + qs[k]) * M + m) * D + c] : 0.f;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    if (k < cnt) {
+                        const float tgv = gv[k] * aa[k];  // top_grad * attn_weight (.cuh:116)
+                        const int ra = xs[k] - r0, rb = ra + 1;
+                        if (ra >= 0 && xs[k] >= 0) atomicAdd(&acc[ra * D + c], w1[k] * tgv);
+                        if (rb < nrows && xs[k] + 1 <= T - 1) atomicAdd(&acc[rb * D + c], w2[k] * tgv);
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // write the tile once; padded rows get zero (masked_fill backward)
+    const uint8_t* mrow = vmask ? vmask + (size_t)b * S + st : nullptr;
+    for (int i = threadIdx.x; i < nrows * D; i += blockDim.x) {
+        const int r = i / D, c = i - r * D;
+        const float v = (mrow && mrow[r0 + r]) ? 0.f : acc[i];
+        grad_value[((size_t)b * S + st + r0 + r) * MD + (size_t)m * D + c] = v;
+    }
+}
+
+// -------------------------------------------------------------------------------------------------
+// host side
+// -------------------------------------------------------------------------------------------------
+static int fill_levels(const int32_t* level_T, int num_levels, int num_point, Levels1d& lv, int& S) {
+    PDVC_CHECK_ARG(level_T != nullptr, "level_T must not be NULL");
+    if (num_levels != kL || num_point != kP)
+        return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "fused 1-D path needs %d levels x %d points (got %d x %d)", kL,
+                              kP, num_levels, num_point);
+    S = 0;
+    for (int l = 0; l < kL; ++l) {
+        PDVC_CHECK_ARG(level_T[l] > 0, "level %d has non-positive length %d", l, level_T[l]);
+        lv.T[l] = level_T[l];
+        lv.start[l] = S;
+        S += level_T[l];
+    }
+    return PDVC_OK;
+}
+
+struct Geometry {
+    int cpl, lph, hpw, waves_per_row;
+};
+
+static int pick_geometry(int M, int D, Geometry& g) {
+    if (D == 16) g.cpl = 4;
+    else if (D == 32 || D == 64 || D == 128) g.cpl = 8;
+    else return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "fused 1-D path supports head_dim 16/32/64/128, got %d", D);
+    g.lph = D / g.cpl;
+    g.hpw = 64 / g.lph;
+    g.waves_per_row = (M + g.hpw - 1) / g.hpw;
+    return PDVC_OK;
+}
+
+}  // namespace pdvc
+
+using namespace pdvc;
+
+template <int RD>
+static void launch_fwd1d(const Geometry& g, dim3 grid, hipStream_t s, const float* value, const uint8_t* mask,
+                         const float* proj, int ps, int ob, int lb, const float* ref, Levels1d lv, int Lq, int S,
+                         int M, int D, int tw, float* out, float* sa, float* sl) {
+#define ARGS value, mask, proj, ps, ob, lb, ref, lv, Lq, S, M, D, g.waves_per_row, tw, out, sa, sl
+    if (g.cpl == 4) hipLaunchKernelGGL((msda1d_fwd_kernel<4, 4, RD>), grid, dim3(256), 0, s, ARGS);
+    else if (g.lph == 4) hipLaunchKernelGGL((msda1d_fwd_kernel<8, 4, RD>), grid, dim3(256), 0, s, ARGS);
+    else if (g.lph == 8) hipLaunchKernelGGL((msda1d_fwd_kernel<8, 8, RD>), grid, dim3(256), 0, s, ARGS);
+    else hipLaunchKernelGGL((msda1d_fwd_kernel<8, 16, RD>), grid, dim3(256), 0, s, ARGS);
+#undef ARGS
+}
+
+template <int RD>
+static void launch_bwdq1d(const Geometry& g, dim3 grid, hipStream_t s, const float* value, const uint8_t* mask,
+                          const float* proj, int ps, int ob, int lb, const float* ref, Levels1d lv, int Lq, int S,
+                          int M, int D, int tw, const float* gout, const float* sa, const float* sl, float* gp,
+                          float* gr) {
+#define ARGS value, mask, proj, ps, ob, lb, ref, lv, Lq, S, M, D, g.waves_per_row, tw, gout, sa, sl, gp, gr
+    if (g.cpl == 4) hipLaunchKernelGGL((msda1d_bwd_query_kernel<4, 4, RD>), grid, dim3(256), 0, s, ARGS);
+    else if (g.lph == 4) hipLaunchKernelGGL((msda1d_bwd_query_kernel<8, 4, RD>), grid, dim3(256), 0, s, ARGS);
+    else if (g.lph == 8) hipLaunchKernelGGL((msda1d_bwd_query_kernel<8, 8, RD>), grid, dim3(256), 0, s, ARGS);
+    else hipLaunchKernelGGL((msda1d_bwd_query_kernel<8, 16, RD>), grid, dim3(256), 0, s, ARGS);
+#undef ARGS
+}
+
+extern "C" int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_pad_mask, const float* proj,
+                                       int proj_stride, int off_base, int logit_base, const float* ref, int ref_dim,
+                                       const int32_t* level_T, int num_levels, int batch, int num_query,
+                                       int num_heads, int head_dim, int num_point, float* output, float* save_attn,
+                                       float* save_loc, void* stream) {
+    Levels1d lv;
+    int S = 0;
+    int rc = fill_levels(level_T, num_levels, num_point, lv, S);
+    if (rc) return rc;
+    Geometry g;
+    if ((rc = pick_geometry(num_heads, head_dim, g))) return rc;
+    PDVC_CHECK_ARG(ref_dim == 1 || ref_dim == 2, "ref_dim must be 1 or 2, got %d", ref_dim);
+    PDVC_CHECK_ARG((save_attn == nullptr) == (save_loc == nullptr), "save_attn and save_loc go together");
+    PDVC_CHECK_ARG(batch >= 0 && num_query >= 0, "negative sizes");
+    const int NSM = num_heads * kNS;
+    PDVC_CHECK_ARG(off_base >= 0 && logit_base >= 0 && off_base + NSM <= proj_stride && logit_base + NSM <= proj_stride,
+                   "proj columns out of range (stride %d, off %d, logit %d, need %d)", proj_stride, off_base,
+                   logit_base, NSM);
+    const long rows = (long)batch * num_query;
+    const long tw = rows * g.waves_per_row;
+    if (tw == 0) return PDVC_OK;
+    PDVC_CHECK_ARG(tw < (1L << 31) / 4, "too many rows");
+    dim3 grid((unsigned)((tw + 3) / 4));
+    hipStream_t s = (hipStream_t)stream;
+    if (ref_dim == 1)
+        launch_fwd1d<1>(g, grid, s, value, value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv, num_query,
+                        S, num_heads, head_dim, (int)tw, output, save_attn, save_loc);
+    else
+        launch_fwd1d<2>(g, grid, s, value, value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv, num_query,
+                        S, num_heads, head_dim, (int)tw, output, save_attn, save_loc);
+    PDVC_CHECK_LAUNCH("msda1d_fwd_kernel");
+    return PDVC_OK;
+}
+
+extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value_pad_mask, const float* ref,
+                                        int ref_dim, const float* proj, int proj_stride, int off_base, int logit_base,
+                                        const int32_t* level_T, int num_levels, int batch, int num_query,
+                                        int num_heads, int head_dim, int num_point, const float* grad_output,
+                                        const float* save_attn, const float* save_loc, float* grad_value,
+                                        float* grad_proj, float* grad_ref, void* stream) {
+    Levels1d lv;
+    int S = 0;
+    int rc = fill_levels(level_T, num_levels, num_point, lv, S);
+    if (rc) return rc;
+    Geometry g;
+    if ((rc = pick_geometry(num_heads, head_dim, g))) return rc;
+    PDVC_CHECK_ARG(ref_dim == 1 || ref_dim == 2, "ref_dim must be 1 or 2, got %d", ref_dim);
+    PDVC_CHECK_ARG(save_attn && save_loc, "backward needs save_attn and save_loc from the forward");
+    const int NSM = num_heads * kNS;
+    PDVC_CHECK_ARG(off_base >= 0 && logit_base >= 0 && off_base + NSM <= proj_stride && logit_base + NSM <= proj_stride,
+                   "proj columns out of range");
+    hipStream_t s = (hipStream_t)stream;
+    const long rows = (long)batch * num_query;
+    const long tw = rows * g.waves_per_row;
+    if (grad_ref && g.waves_per_row > 1 && rows > 0) {
+        hipError_t e = hipMemsetAsync(grad_ref, 0, sizeof(float) * rows * kL * ref_dim, s);
+        if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_ref: %s", hipGetErrorString(e));
+    }
+    if (tw > 0) {
+        dim3 grid((unsigned)((tw + 3) / 4));
+        if (ref_dim == 1)
+            launch_bwdq1d<1>(g, grid, s, value, value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv,
+                             num_query, S, num_heads, head_dim, (int)tw, grad_output, save_attn, save_loc, grad_proj,
+                             grad_ref);
+        else
+            launch_bwdq1d<2>(g, grid, s, value, value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv,
+                             num_query, S, num_heads, head_dim, (int)tw, grad_output, save_attn, save_loc, grad_proj,
+                             grad_ref);
+        PDVC_CHECK_LAUNCH("msda1d_bwd_query_kernel");
+    }
+    // grad_value: tiles of kTile rows per (video, head, level)
+    TileMap tm;
+    tm.prefix[0] = 0;
+    for (int l = 0; l < kL; ++l) tm.prefix[l + 1] = tm.prefix[l] + (lv.T[l] + kTile - 1) / kTile;
+    const long nblk = (long)batch * num_heads * tm.prefix[kL];
+    if (nblk > 0) {
+        PDVC_CHECK_ARG(nblk < (1L << 31), "too many tiles");
+        if (head_dim <= 64)
+            hipLaunchKernelGGL((msda1d_bwd_value_kernel<64>), dim3((unsigned)nblk), dim3(256), 0, s, value_pad_mask, lv,
+                               tm, num_query, S, num_heads, head_dim, grad_output, save_attn, save_loc, grad_value);
+        else
+            hipLaunchKernelGGL((msda1d_bwd_value_kernel<128>), dim3((unsigned)nblk), dim3(256), 0, s, value_pad_mask,
+                               lv, tm, num_query, S, num_heads, head_dim, grad_output, save_attn, save_loc,
+                               grad_value);
+        PDVC_CHECK_LAUNCH("msda1d_bwd_value_kernel");
+    }
+    return PDVC_OK;
+}

@@ -1,0 +1,89 @@
+"""ctypes binding of libpdvc_hip.so -- the C ABI declared in include/pdvc_msda.h.
+
+This is the only door from Python into the HIP kernels.  There is deliberately no fallback: if the
+library is missing, or a tensor is not on a GPU, calls raise (the reference likewise raises
+"Not implemented on the CPU", pdvc/ops/src/ms_deform_attn.h:38,60).
+"""
+import ctypes
+import os
+
+import torch
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("PDVC_HIP_LIB", os.path.join(_PKG, "lib", "libpdvc_hip.so"))
+
+_vp, _i, _u8p = ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p
+
+# name -> argtypes (all return int status)
+SIGNATURES = {
+    "pdvc_ms_deform_attn_forward_f32": [_vp] * 5 + [_i] * 8 + [_vp, _vp],
+    "pdvc_ms_deform_attn_forward_f64": [_vp] * 5 + [_i] * 8 + [_vp, _vp],
+    "pdvc_ms_deform_attn_backward_f32": [_vp] * 6 + [_i] * 8 + [_vp] * 4,
+    "pdvc_ms_deform_attn_backward_f64": [_vp] * 6 + [_i] * 8 + [_vp] * 4,
+    "pdvc_ms_deform_sample_f32": [_vp] * 4 + [_i] * 8 + [_vp, _vp],
+    "pdvc_ms_deform_sample_backward_f32": [_vp] * 5 + [_i] * 8 + [_vp] * 3,
+    "pdvc_msda1d_forward_f32": [_vp, _u8p, _vp, _i, _i, _i, _vp, _i, _vp] + [_i] * 6 + [_vp] * 4,
+    "pdvc_msda1d_backward_f32": [_vp, _u8p, _vp, _i, _vp, _i, _i, _i, _vp] + [_i] * 6 + [_vp] * 7,
+    "pdvc_cap_gather_forward_f32": [_vp, _u8p, _vp, _vp, _i, _i, _vp, _i, _vp] + [_i] * 6 + [_vp] * 3,
+    "pdvc_cap_gather_backward_f32": [_vp, _u8p, _vp, _vp, _i, _i, _vp, _i, _vp] + [_i] * 6 + [_vp] * 6,
+}
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libpdvc_hip.so once; raise loudly if it is absent (no CPU fallback exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(f"libpdvc_hip.so not found at {LIB_PATH}: build it with "
+                              f"`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_int
+        L.pdvc_last_error.restype = ctypes.c_char_p
+        L.pdvc_abi_version.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().pdvc_last_error().decode(errors="replace")
+        raise NativeError(f"{name} failed ({rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL).  Tensors must be contiguous and on a GPU."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise NativeError("PDVC HIP ops need GPU tensors (there is no CPU implementation)")
+    if not t.is_contiguous():
+        raise NativeError("PDVC HIP ops need contiguous tensors")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+_INT_ARRAYS = {}
+
+
+def int_array(values):
+    """Host int32 array (kept alive in a cache: these are per-model constants such as level lengths)."""
+    key = tuple(int(v) for v in values)
+    hit = _INT_ARRAYS.get(key)
+    if hit is None:
+        arr = (ctypes.c_int32 * len(key))(*key)
+        hit = (arr, ctypes.cast(arr, ctypes.c_void_p))
+        _INT_ARRAYS[key] = hit
+    return hit[1]

@@ -1,0 +1,180 @@
+"""Autograd functions over the MI355X C ABI (include/pdvc_msda.h).
+
+Mirrors pdvc/ops/functions/ms_deform_attn_func.py of the reference:
+  * MSDeformAttnFunction        -- same signature/semantics as the reference (:20-38), general 2-D op;
+  * ms_deform_attn_core_pytorch -- same signature as the reference core (:41-68, border padding);
+    here it runs on the HIP raw-sample kernel (there is no CPU path);
+and adds the fused 1-D functions PDVC's modules use:
+  * MSDA1dFunction   -- softmax + sampling locations + zero-padded gather-reduce (ms_deform_attn.py:167-192)
+  * CapGatherFunction -- sampling locations + border raw samples (ms_deform_attn_for_caption.py:92-121)
+"""
+import torch
+from torch.autograd import Function
+from torch.autograd.function import once_differentiable
+
+import MultiScaleDeformableAttention as MSDA
+from pdvc import _native as _n
+
+NUM_SAMPLES = 16  # levels x points on the fused paths
+NUM_SAMPLES_FUSED = NUM_SAMPLES
+
+
+class MSDeformAttnFunction(Function):
+    @staticmethod
+    def forward(ctx, value, value_spatial_shapes, value_level_start_index, sampling_locations, attention_weights,
+                im2col_step):
+        ctx.im2col_step = im2col_step
+        output = MSDA.ms_deform_attn_forward(value, value_spatial_shapes, value_level_start_index,
+                                             sampling_locations, attention_weights, ctx.im2col_step)
+        ctx.save_for_backward(value, value_spatial_shapes, value_level_start_index, sampling_locations,
+                              attention_weights)
+        return output
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_output):
+        value, shapes, lsi, loc, attn = ctx.saved_tensors
+        gv, gl, ga = MSDA.ms_deform_attn_backward(value, shapes, lsi, loc, attn, grad_output, ctx.im2col_step)
+        return gv, None, None, gl, ga, None
+
+
+class _SampleFunction(Function):
+    """Raw bilinear samples (N*M, D, Lq, L, P) with border (or zeros) padding, general 2-D."""
+
+    @staticmethod
+    def forward(ctx, value, shapes, lsi, loc, padding):
+        value, loc = value.contiguous(), loc.contiguous()
+        N, S, M, D = value.shape
+        _, Lq, _, L, P, _ = loc.shape
+        out = torch.empty((N * M, D, Lq, L, P), dtype=value.dtype, device=value.device)
+        if value.dtype != torch.float32:
+            raise RuntimeError("ms_deform_attn_core_pytorch on MI355X supports float32")
+        _n.call("pdvc_ms_deform_sample_f32", _n.ptr(value), _n.ptr(shapes), _n.ptr(lsi), _n.ptr(loc), N, S, M, D,
+                L, Lq, P, padding, _n.ptr(out), _n.stream())
+        ctx.save_for_backward(value, shapes, lsi, loc)
+        ctx.padding = padding
+        return out
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad):
+        value, shapes, lsi, loc = ctx.saved_tensors
+        grad = grad.contiguous()
+        N, S, M, D = value.shape
+        _, Lq, _, L, P, _ = loc.shape
+        gv = torch.empty_like(value)
+        gl = torch.empty_like(loc)
+        _n.call("pdvc_ms_deform_sample_backward_f32", _n.ptr(value), _n.ptr(shapes), _n.ptr(lsi), _n.ptr(loc),
+                _n.ptr(grad), N, S, M, D, L, Lq, P, ctx.padding, _n.ptr(gv), _n.ptr(gl), _n.stream())
+        return gv, None, None, gl, None
+
+
+def ms_deform_attn_core_pytorch(value, value_spatial_shapes, sampling_locations, attention_weights,
+                                return_value=False):
+    """The reference core's contract (ms_deform_attn_func.py:41-68: grid_sample bilinear, border,
+    align_corners=False) on the HIP raw-sample kernel."""
+    shapes = torch.as_tensor(value_spatial_shapes, dtype=torch.long, device=value.device).reshape(-1, 2)
+    lsi = torch.cat((shapes.new_zeros((1,)), shapes.prod(1).cumsum(0)[:-1]))
+    samples = _SampleFunction.apply(value, shapes.contiguous(), lsi.contiguous(), sampling_locations,
+                                    _n_pad("border"))
+    if return_value:
+        return samples
+    N, S, M, D = value.shape
+    _, Lq, _, L, P, _ = sampling_locations.shape
+    w = attention_weights.transpose(1, 2).reshape(N * M, 1, Lq, L * P)
+    out = (samples.flatten(-2) * w).sum(-1).view(N, M * D, Lq)
+    return out.transpose(1, 2).contiguous()
+
+
+def _n_pad(name):
+    return {"zeros": 0, "border": 1}[name]
+
+
+def _levels(level_T):
+    return _n.int_array(level_T), len(level_T)
+
+
+class MSDA1dFunction(Function):
+    """Fused MSDeformAttn core for a 1-D temporal pyramid (GPU semantics: zero padding).
+
+    value (N,S,M,D); pad_mask (N,S) uint8 or None; proj (N,Lq,C) holding offsets at [off_base, +M*16)
+    and attention logits at [logit_base, +M*16); ref (N,Lq,L,1|2).  Returns (N,Lq,M*D)."""
+
+    @staticmethod
+    def forward(ctx, value, pad_mask, proj, ref, level_T, off_base, logit_base):
+        value, proj, ref = value.contiguous(), proj.contiguous(), ref.contiguous()
+        N, S, M, D = value.shape
+        Lq, C = proj.shape[1], proj.shape[2]
+        L, RD = ref.shape[2], ref.shape[3]
+        lvl, nl = _levels(level_T)
+        out = torch.empty((N, Lq, M * D), dtype=value.dtype, device=value.device)
+        need = ctx.needs_input_grad[0] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        if need:
+            save_attn = torch.empty((N, Lq, M, NUM_SAMPLES), dtype=value.dtype, device=value.device)
+            save_loc = torch.empty_like(save_attn)
+        else:
+            save_attn = save_loc = None
+        _n.call("pdvc_msda1d_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(proj), C, off_base, logit_base,
+                _n.ptr(ref), RD, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(out), _n.ptr(save_attn),
+                _n.ptr(save_loc), _n.stream())
+        if need:
+            ctx.save_for_backward(value, pad_mask, proj, ref, save_attn, save_loc)
+        ctx.meta = (tuple(level_T), off_base, logit_base)
+        return out
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_out):
+        value, pad_mask, proj, ref, save_attn, save_loc = ctx.saved_tensors
+        level_T, off_base, logit_base = ctx.meta
+        grad_out = grad_out.contiguous()
+        N, S, M, D = value.shape
+        Lq, C = proj.shape[1], proj.shape[2]
+        RD = ref.shape[3]
+        lvl, nl = _levels(level_T)
+        gv = torch.empty_like(value)
+        gp = torch.zeros_like(proj) if C != 2 * M * NUM_SAMPLES else torch.empty_like(proj)
+        gr = torch.empty_like(ref) if ctx.needs_input_grad[3] else None
+        _n.call("pdvc_msda1d_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(ref), RD, _n.ptr(proj), C,
+                off_base, logit_base, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(grad_out), _n.ptr(save_attn),
+                _n.ptr(save_loc), _n.ptr(gv), _n.ptr(gp), _n.ptr(gr), _n.stream())
+        return gv, None, gp, gr, None, None, None
+
+
+class CapGatherFunction(Function):
+    """Caption-head sampling: raw border samples (R, M, 16, D) of value (N,S,M,D) for query rows whose
+    video is row_video (R,) int32; offsets (R, C) with the M*16 offsets at column off_col0; ref (R,L,1|2)."""
+
+    @staticmethod
+    def forward(ctx, value, pad_mask, row_video, offsets, ref, level_T, off_col0):
+        value, offsets, ref = value.contiguous(), offsets.contiguous(), ref.contiguous()
+        N, S, M, D = value.shape
+        R, C = offsets.shape
+        RD = ref.shape[2]
+        lvl, nl = _levels(level_T)
+        samples = torch.empty((R, M, NUM_SAMPLES, D), dtype=value.dtype, device=value.device)
+        save_loc = torch.empty((R, M, NUM_SAMPLES), dtype=value.dtype, device=value.device)
+        _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video), _n.ptr(offsets),
+                C, off_col0, _n.ptr(ref), RD, lvl, nl, N, R, M, D, NUM_SAMPLES // nl, _n.ptr(samples),
+                _n.ptr(save_loc), _n.stream())
+        ctx.save_for_backward(value, pad_mask, row_video, offsets, ref, save_loc)
+        ctx.meta = (tuple(level_T), off_col0)
+        return samples
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_samples):
+        value, pad_mask, row_video, offsets, ref, save_loc = ctx.saved_tensors
+        level_T, off_col0 = ctx.meta
+        grad_samples = grad_samples.contiguous()
+        N, S, M, D = value.shape
+        R, C = offsets.shape
+        RD = ref.shape[2]
+        lvl, nl = _levels(level_T)
+        gv = torch.zeros_like(value)
+        go = torch.zeros_like(offsets) if C != M * NUM_SAMPLES else torch.empty_like(offsets)
+        gr = torch.empty_like(ref) if ctx.needs_input_grad[4] else None
+        _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video),
+                _n.ptr(offsets), C, off_col0, _n.ptr(ref), RD, lvl, nl, N, R, M, D, NUM_SAMPLES // nl,
+                _n.ptr(save_loc), _n.ptr(grad_samples), _n.ptr(gv), _n.ptr(go), _n.ptr(gr), _n.stream())
+        return gv, None, None, go, gr, None, None

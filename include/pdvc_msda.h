@@ -1,0 +1,143 @@
+/*
+ * pdvc_msda.h -- C ABI of the MI355X-native PDVC hot path (libpdvc_hip.so, gfx950).
+ *
+ * Plain pointers and sizes only: every tensor argument is a DEVICE pointer to a contiguous row-major
+ * array, every `stream` is a hipStream_t passed as void*, and every host-side array argument is marked
+ * "host".  Calls are asynchronous on `stream`, never synchronise, never allocate, and are safe to
+ * capture into a hipGraph.  Outputs are fully written (callers need not zero them) unless a parameter
+ * says "accumulated".  Every entry returns PDVC_OK (0) or a negative PDVC_ERR_*; pdvc_last_error()
+ * returns a thread-local message for the last failure (argument checks mirror the reference's
+ * AT_ASSERTM checks, and kernel launch failures are REPORTED here, where the reference only printf'd
+ * them: pdvc/ops/src/cuda/ms_deform_im2col_cuda.cuh:949-953, 1322-1326).
+ *
+ * Reference interfaces replaced (paths relative to the reference repository):
+ *   pdvc_ms_deform_attn_forward_*   <- MultiScaleDeformableAttention.ms_deform_attn_forward
+ *                                      (pdvc/ops/src/vision.cpp:14, ms_deform_attn.h:20-41,
+ *                                       cuda/ms_deform_attn_cuda.cu:20-80)
+ *   pdvc_ms_deform_attn_backward_*  <- MultiScaleDeformableAttention.ms_deform_attn_backward
+ *                                      (vision.cpp:15, ms_deform_attn.h:43-61, ms_deform_attn_cuda.cu:83-153)
+ *   pdvc_ms_deform_sample_*         <- ms_deform_attn_core_pytorch(..., return_value=True)
+ *                                      (pdvc/ops/functions/ms_deform_attn_func.py:41-68), both paddings
+ *   pdvc_msda1d_*                   <- the body of MSDeformAttn.forward between its projections
+ *                                      (pdvc/ops/modules/ms_deform_attn.py:167-192): softmax, sampling
+ *                                      locations, 1-D lift and the op, fused; backward likewise
+ *   pdvc_cap_gather_*               <- the body of MSDeformAttnCap.forward after value_proj
+ *                                      (pdvc/ops/modules/ms_deform_attn_for_caption.py:92-121): sampling
+ *                                      locations + border-padded raw samples
+ *   pdvc_mha_*                      <- nn.MultiheadAttention's core (softmax(QK^T/sqrt(d)) V) used by
+ *                                      DeformableTransformerDecoderLayer.self_attn
+ *                                      (pdvc/deformable_transformer.py:231,256-258)
+ *   pdvc_lstm_cell_*                <- the pointwise part of nn.LSTM (1 layer, 1 step, no bias) in
+ *                                      ShowAttendTellCore.forward (pdvc/CaptioningHead/LSTM_DSA.py:206-207,261)
+ *   pdvc_softattn_*                 <- ShowAttendTellCore's soft attention over the 16 samples
+ *                                      (LSTM_DSA.py:245-258: tanh, alpha_net, softmax, weighted sum)
+ */
+#ifndef PDVC_MSDA_H
+#define PDVC_MSDA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PDVC_ABI_VERSION 1
+#define PDVC_MAX_LEVELS 8
+
+#define PDVC_OK 0
+#define PDVC_ERR_INVALID_ARG (-1)
+#define PDVC_ERR_LAUNCH (-2)
+#define PDVC_ERR_UNSUPPORTED (-3)
+
+#define PDVC_PAD_ZEROS 0  /* reference CUDA op semantics (ms_deform_im2col_cuda.cuh:286-291) */
+#define PDVC_PAD_BORDER 1 /* grid_sample(padding_mode='border', align_corners=False) semantics */
+
+int pdvc_abi_version(void);
+const char* pdvc_last_error(void);
+
+/* ---- drop-in operator: general 2-D multi-scale deformable attention, zero padding -------------------
+ * value (N,S,M,D); spatial_shapes (L,2) int64 (H,W) DEVICE; level_start_index (L,) int64 DEVICE;
+ * sampling_loc (N,Lq,M,L,P,2) [x,y]; attn_weight (N,Lq,M,L,P); output (N,Lq,M*D).
+ * im2col_step is validated like the reference (N % min(N, im2col_step) == 0) but every batch element
+ * is processed in one launch. */
+int pdvc_ms_deform_attn_forward_f32(const float* value, const int64_t* spatial_shapes,
+                                    const int64_t* level_start_index, const float* sampling_loc,
+                                    const float* attn_weight, int batch, int spatial_size, int num_heads,
+                                    int channels, int num_levels, int num_query, int num_point,
+                                    int im2col_step, float* output, void* stream);
+int pdvc_ms_deform_attn_forward_f64(const double* value, const int64_t* spatial_shapes,
+                                    const int64_t* level_start_index, const double* sampling_loc,
+                                    const double* attn_weight, int batch, int spatial_size, int num_heads,
+                                    int channels, int num_levels, int num_query, int num_point,
+                                    int im2col_step, double* output, void* stream);
+/* grad_value (N,S,M,D), grad_sampling_loc (N,Lq,M,L,P,2), grad_attn_weight (N,Lq,M,L,P). */
+int pdvc_ms_deform_attn_backward_f32(const float* value, const int64_t* spatial_shapes,
+                                     const int64_t* level_start_index, const float* sampling_loc,
+                                     const float* attn_weight, const float* grad_output, int batch,
+                                     int spatial_size, int num_heads, int channels, int num_levels,
+                                     int num_query, int num_point, int im2col_step, float* grad_value,
+                                     float* grad_sampling_loc, float* grad_attn_weight, void* stream);
+int pdvc_ms_deform_attn_backward_f64(const double* value, const int64_t* spatial_shapes,
+                                     const int64_t* level_start_index, const double* sampling_loc,
+                                     const double* attn_weight, const double* grad_output, int batch,
+                                     int spatial_size, int num_heads, int channels, int num_levels,
+                                     int num_query, int num_point, int im2col_step, double* grad_value,
+                                     double* grad_sampling_loc, double* grad_attn_weight, void* stream);
+
+/* ---- raw samples (return_value=True), general 2-D, padding PDVC_PAD_* --------------------------------
+ * samples (N*M, D, Lq, L, P) exactly as the reference core returns them. */
+int pdvc_ms_deform_sample_f32(const float* value, const int64_t* spatial_shapes,
+                              const int64_t* level_start_index, const float* sampling_loc, int batch,
+                              int spatial_size, int num_heads, int channels, int num_levels, int num_query,
+                              int num_point, int padding, float* samples, void* stream);
+int pdvc_ms_deform_sample_backward_f32(const float* value, const int64_t* spatial_shapes,
+                                       const int64_t* level_start_index, const float* sampling_loc,
+                                       const float* grad_samples, int batch, int spatial_size,
+                                       int num_heads, int channels, int num_levels, int num_query,
+                                       int num_point, int padding, float* grad_value,
+                                       float* grad_sampling_loc, void* stream);
+
+/* ---- fused 1-D PDVC deformable attention (zero padding = the reference GPU semantics) ----------------
+ * value (N,S,M,D) = value_proj(input_flatten); value_pad_mask (N,S) uint8, 1 = padded (masked_fill 0),
+ * may be NULL; proj (N,Lq,proj_stride) holds the sampling_offsets logits at [off_base + m*L*P + l*P + p]
+ * and the attention_weights logits at [logit_base + ...]; ref (N,Lq,L,ref_dim), ref_dim 1 (centre) or
+ * 2 (centre, length) -- ms_deform_attn.py:171-177; level_T host (L,) temporal lengths, S = sum(level_T).
+ * output (N,Lq,M*D).  save_attn / save_loc (N,Lq,M,L*P): softmaxed weights and sampling locations for
+ * the backward (may be NULL in inference).  Supported: L*P == 16, D in {16,32,64,128}. */
+int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_pad_mask, const float* proj,
+                            int proj_stride, int off_base, int logit_base, const float* ref, int ref_dim,
+                            const int32_t* level_T, int num_levels, int batch, int num_query,
+                            int num_heads, int head_dim, int num_point, float* output, float* save_attn,
+                            float* save_loc, void* stream);
+/* grad_value (N,S,M,D) (zero on padded rows); grad_proj (N,Lq,proj_stride): only the offset and logit
+ * slots are written; grad_ref (N,Lq,L,ref_dim) or NULL.  workspace: NULL (reserved). */
+int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value_pad_mask, const float* ref,
+                             int ref_dim, const float* proj, int proj_stride, int off_base, int logit_base,
+                             const int32_t* level_T, int num_levels, int batch, int num_query, int num_heads,
+                             int head_dim, int num_point, const float* grad_output, const float* save_attn,
+                             const float* save_loc, float* grad_value, float* grad_proj, float* grad_ref,
+                             void* stream);
+
+/* ---- caption-head border gather (MSDeformAttnCap) ----------------------------------------------------
+ * value (N,S,M,D); value_pad_mask (N,S) or NULL; row_video (R,) int32 DEVICE: video of each query row;
+ * offsets (R, off_stride) with the M*L*P sampling offsets at column off_col0; ref (R,L,ref_dim).
+ * samples (R, M, L*P, D) [the layout ShowAttendTellCore consumes after its permute, LSTM_DSA.py:241-242];
+ * save_loc (R, M, L*P) (may be NULL). */
+int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* value_pad_mask, const int32_t* row_video,
+                                const float* offsets, int off_stride, int off_col0, const float* ref,
+                                int ref_dim, const int32_t* level_T, int num_levels, int batch, int rows,
+                                int num_heads, int head_dim, int num_point, float* samples, float* save_loc,
+                                void* stream);
+/* grad_value ACCUMULATED (atomic adds; zero it before the first call); grad_offsets (R, off_stride):
+ * only the offset columns are written; grad_ref (R,L,ref_dim) or NULL. */
+int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* value_pad_mask, const int32_t* row_video,
+                                 const float* offsets, int off_stride, int off_col0, const float* ref,
+                                 int ref_dim, const int32_t* level_T, int num_levels, int batch, int rows,
+                                 int num_heads, int head_dim, int num_point, const float* save_loc,
+                                 const float* grad_samples, float* grad_value, float* grad_offsets,
+                                 float* grad_ref, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PDVC_MSDA_H */

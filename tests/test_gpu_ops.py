@@ -1,0 +1,345 @@
+"""GPU parity of the HIP operators against the CPU oracle (oracle/msda_oracle.c) and the golden vectors
+generated from the reference (tests/golden).  Tolerances: fp64 1e-10, fp32 1e-4 (north star: 1e-4 fp32).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+DEV = "cuda"
+
+
+def load(name):
+    return np.load(os.path.join(G, name + ".npz"), allow_pickle=False)
+
+
+def cu(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.to(DEV)
+
+
+def close(a, b, tol, what=""):
+    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else a
+    b = b.detach().cpu().numpy() if isinstance(b, torch.Tensor) else b
+    err = np.abs(a - b).max() if a.size else 0.0
+    scale = max(1.0, np.abs(b).max() if b.size else 1.0)
+    assert err <= tol * scale, f"{what}: max|diff|={err:.3e} > {tol:.1e}*{scale:.2f}"
+
+
+# ------------------------------------------------------------------------------------------------
+# drop-in operator MultiScaleDeformableAttention (pdvc/ops/src/vision.cpp:13-16)
+# ------------------------------------------------------------------------------------------------
+def test_dropin_reftest_inputs_f64():
+    """The reference test's own inputs (pdvc/ops/test.py:21-44), fp64, vs the zeros golden vectors."""
+    import MultiScaleDeformableAttention as MSDA
+    d = load("op_reftest")
+    v, lo, a = cu(d["value"]), cu(d["loc"]), cu(d["attn"])
+    shapes, lsi = cu(d["shapes"]), cu(d["lsi"])
+    out = MSDA.ms_deform_attn_forward(v, shapes, lsi, lo, a, 2)
+    close(out, d["zeros_out"], 1e-12, "fwd")
+    gv, gl, ga = MSDA.ms_deform_attn_backward(v, shapes, lsi, lo, a, cu(d["grad_out"]), 2)
+    close(gv, d["zeros_grad_value"], 1e-12, "grad_value")
+    close(gl, d["zeros_grad_loc"], 1e-12, "grad_loc")
+    close(ga, d["zeros_grad_attn"], 1e-12, "grad_attn")
+
+
+@pytest.mark.parametrize("D", [30, 32, 64, 71])
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+def test_dropin_1d_pyramids(D, dt):
+    import MultiScaleDeformableAttention as MSDA
+    d = load(f"op_1d_D{D}")
+    tdt = torch.float64 if dt == "f64" else torch.float32
+    tol = 1e-10 if dt == "f64" else 1e-4
+    v, lo, a = cu(d["value"], tdt), cu(d["loc"], tdt), cu(d["attn"], tdt)
+    shapes, lsi = cu(d["shapes"]), cu(d["lsi"])
+    out = MSDA.ms_deform_attn_forward(v, shapes, lsi, lo, a, 64)
+    close(out, d[f"zeros_{dt}_out"], tol, "fwd")
+    gv, gl, ga = MSDA.ms_deform_attn_backward(v, shapes, lsi, lo, a, cu(d["grad_out"], tdt), 64)
+    close(gv, d[f"zeros_{dt}_grad_value"], tol, "grad_value")
+    close(gl, d[f"zeros_{dt}_grad_loc"], tol, "grad_loc")
+    close(ga, d[f"zeros_{dt}_grad_attn"], tol, "grad_attn")
+
+
+@pytest.mark.parametrize("channels", [30, 32, 64, 71, 1025, 2048, 3096])
+def test_dropin_gradient_channels_vs_oracle(channels):
+    """Every channel count of the reference gradcheck (test.py:85), fp64, against the oracle."""
+    import MultiScaleDeformableAttention as MSDA
+    rng = np.random.RandomState(channels)
+    shapes = np.array([(6, 4), (3, 2)], np.int64)
+    lsi = np.array([0, 24], np.int64)
+    N, M, Lq, L, P = 1, 2, 2, 2, 2
+    v = rng.rand(N, 30, M, channels) * 0.01
+    lo = rng.rand(N, Lq, M, L, P, 2)
+    a = rng.rand(N, Lq, M, L, P) + 1e-5
+    a /= a.sum(-1, keepdims=True).sum(-2, keepdims=True)
+    g = rng.randn(N, Lq, M * channels)
+    ev = O.msda_forward(v, shapes, lsi, lo, a, "zeros")
+    egv, egl, ega = O.msda_backward(v, shapes, lsi, lo, a, g, "zeros")
+    out = MSDA.ms_deform_attn_forward(cu(v), cu(shapes), cu(lsi), cu(lo), cu(a), 2)
+    gv, gl, ga = MSDA.ms_deform_attn_backward(cu(v), cu(shapes), cu(lsi), cu(lo), cu(a), cu(g), 2)
+    close(out, ev, 1e-12, "fwd")
+    close(gv, egv, 1e-12, "grad_value")
+    close(gl, egl, 1e-11, "grad_loc")
+    close(ga, ega, 1e-11, "grad_attn")
+
+
+def test_dropin_autograd_gradcheck():
+    """torch.autograd.gradcheck through MSDeformAttnFunction (test.py:63-78), fp64."""
+    from pdvc.ops.functions import MSDeformAttnFunction
+    torch.manual_seed(3)
+    shapes = torch.as_tensor([(6, 4), (3, 2)], dtype=torch.long, device=DEV)
+    lsi = torch.cat((shapes.new_zeros((1,)), shapes.prod(1).cumsum(0)[:-1]))
+    value = (torch.rand(1, 30, 2, 4, device=DEV, dtype=torch.float64) * 0.01).requires_grad_()
+    loc = torch.rand(1, 2, 2, 2, 2, 2, device=DEV, dtype=torch.float64).requires_grad_()
+    attn = torch.rand(1, 2, 2, 2, 2, device=DEV, dtype=torch.float64) + 1e-5
+    attn = (attn / attn.sum(-1, keepdim=True).sum(-2, keepdim=True)).requires_grad_()
+    assert torch.autograd.gradcheck(MSDeformAttnFunction.apply, (value, shapes, lsi, loc, attn, 2))
+
+
+def test_dropin_errors():
+    import MultiScaleDeformableAttention as MSDA
+    d = load("op_reftest")
+    v, lo, a = cu(d["value"]), cu(d["loc"]), cu(d["attn"])
+    shapes, lsi = cu(d["shapes"]), cu(d["lsi"])
+    v3 = torch.cat([v, v, v], 0)
+    lo3, a3 = torch.cat([lo] * 3, 0), torch.cat([a] * 3, 0)
+    with pytest.raises(RuntimeError, match="im2col_step"):
+        MSDA.ms_deform_attn_forward(v3, shapes, lsi, lo3, a3, 2)  # 3 % min(3,2) != 0
+    with pytest.raises(RuntimeError):
+        MSDA.ms_deform_attn_forward(v.cpu(), shapes, lsi, lo, a, 2)
+    with pytest.raises(RuntimeError):
+        MSDA.ms_deform_attn_forward(v.transpose(1, 2), shapes, lsi, lo, a, 2)
+
+
+def test_dropin_empty_queries():
+    import MultiScaleDeformableAttention as MSDA
+    d = load("op_reftest")
+    v = cu(d["value"])
+    shapes, lsi = cu(d["shapes"]), cu(d["lsi"])
+    lo = torch.zeros(1, 0, 2, 2, 2, 2, dtype=v.dtype, device=DEV)
+    a = torch.zeros(1, 0, 2, 2, 2, dtype=v.dtype, device=DEV)
+    out = MSDA.ms_deform_attn_forward(v, shapes, lsi, lo, a, 64)
+    assert out.shape == (1, 0, 4)
+    gv, gl, ga = MSDA.ms_deform_attn_backward(v, shapes, lsi, lo, a, out, 64)
+    assert torch.count_nonzero(gv) == 0
+
+
+# ------------------------------------------------------------------------------------------------
+# border raw-sample core (ms_deform_attn_core_pytorch, return_value=True)
+# ------------------------------------------------------------------------------------------------
+def test_core_border_samples_vs_golden():
+    from pdvc.ops.functions import ms_deform_attn_core_pytorch
+    d = load("op_sample")
+    v = cu(d["value"], torch.float32).requires_grad_()
+    lo = cu(d["loc"], torch.float32).requires_grad_()
+    s = ms_deform_attn_core_pytorch(v, cu(d["shapes"]), lo, None, return_value=True)
+    close(s, d["f32_samples"], 1e-5, "samples")
+    s.backward(cu(d["grad_samples"], torch.float32))
+    close(v.grad, d["f32_grad_value"], 1e-4, "grad_value")
+    close(lo.grad, d["f32_grad_loc"], 1e-4, "grad_loc")
+
+
+@pytest.mark.parametrize("D", [30, 64])
+def test_core_border_weighted_vs_golden(D):
+    from pdvc.ops.functions import ms_deform_attn_core_pytorch
+    d = load(f"op_1d_D{D}")
+    v = cu(d["value"], torch.float32).requires_grad_()
+    lo = cu(d["loc"], torch.float32).requires_grad_()
+    a = cu(d["attn"], torch.float32).requires_grad_()
+    out = ms_deform_attn_core_pytorch(v, cu(d["shapes"]), lo, a)
+    close(out, d["border_f32_out"], 1e-4, "out")
+    out.backward(cu(d["grad_out"], torch.float32))
+    close(v.grad, d["border_f32_grad_value"], 1e-4, "grad_value")
+    close(lo.grad, d["border_f32_grad_loc"], 1e-4, "grad_loc")
+    close(a.grad, d["border_f32_grad_attn"], 1e-4, "grad_attn")
+
+
+# ------------------------------------------------------------------------------------------------
+# fused 1-D kernels vs the oracle + the module math restated in numpy (ms_deform_attn.py:163-192)
+# ------------------------------------------------------------------------------------------------
+def _softmax(x):
+    e = np.exp(x - x.max(-1, keepdims=True))
+    return e / e.sum(-1, keepdims=True)
+
+
+def expected_msda1d(value, mask, proj, ref, T_l, M, grad_out):
+    """numpy/oracle restatement (float64) of the fused forward and its gradients."""
+    N, S, _, D = value.shape
+    Lq = proj.shape[1]
+    L, P = len(T_l), 4
+    NS = L * P
+    off = proj[..., :M * NS].reshape(N, Lq, M, L, P)
+    logit = proj[..., M * NS:2 * M * NS].reshape(N, Lq, M, NS)
+    a = _softmax(logit).reshape(N, Lq, M, L, P)
+    Tn = np.asarray(T_l, np.float64)[None, None, None, :, None]
+    if ref.shape[-1] == 1:
+        loc = ref[:, :, None, :, None, 0] + off / Tn
+    else:
+        loc = ref[:, :, None, :, None, 0] + off / P * ref[:, :, None, :, None, 1] * 0.5
+    v = value * (~mask)[..., None, None] if mask is not None else value
+    loc2, shapes, lsi = O.lift_1d(loc, T_l)
+    out = O.msda_forward(v, shapes, lsi, loc2, a, "zeros")
+    gv, gl, ga = O.msda_backward(v, shapes, lsi, loc2, a, grad_out, "zeros")
+    if mask is not None:
+        gv = gv * (~mask)[..., None, None]
+    glx = gl[..., 0]
+    ga_flat = ga.reshape(N, Lq, M, NS)
+    a_flat = a.reshape(N, Lq, M, NS)
+    glogit = a_flat * (ga_flat - (a_flat * ga_flat).sum(-1, keepdims=True))
+    if ref.shape[-1] == 1:
+        goff = glx / Tn
+        gref = glx.sum(axis=(2, 4))[..., None]
+    else:
+        goff = glx * 0.5 * ref[:, :, None, :, None, 1] / P
+        gc = glx.sum(axis=(2, 4))
+        gln = (glx * 0.5 * off / P).sum(axis=(2, 4))
+        gref = np.stack([gc, gln], -1)
+    gproj = np.concatenate([goff.reshape(N, Lq, M * NS), glogit.reshape(N, Lq, M * NS)], -1)
+    return out, gv, gproj, gref
+
+
+@pytest.mark.parametrize("D", [16, 32, 64, 128])
+@pytest.mark.parametrize("ref_dim", [1, 2])
+@pytest.mark.parametrize("masked", [False, True])
+def test_fused_msda1d_vs_oracle(D, ref_dim, masked):
+    from pdvc.ops.functions import MSDA1dFunction
+    rng = np.random.RandomState(D * 10 + ref_dim + 100 * masked)
+    M = {16: 8, 32: 4, 64: 8, 128: 3}[D]
+    T_l = [40, 20, 10, 5]
+    N, Lq, S = 2, 37, sum(T_l)
+    value = rng.randn(N, S, M, D)
+    proj = np.concatenate([rng.randn(N, Lq, M * 16) * 3.0, rng.randn(N, Lq, M * 16)], -1)
+    if ref_dim == 1:
+        ref = rng.uniform(-0.05, 1.05, size=(N, Lq, 4, 1))
+    else:
+        ref = np.concatenate([rng.uniform(0, 1, size=(N, Lq, 4, 1)), rng.uniform(0.05, 0.9, size=(N, Lq, 4, 1))], -1)
+    mask = None
+    if masked:
+        mask = np.zeros((N, S), bool)
+        mask[1, 30:40] = True
+        mask[1, 55:60] = True
+    gout = rng.randn(N, Lq, M * D)
+    eo, egv, egp, egr = expected_msda1d(value, mask, proj, ref, T_l, M, gout)
+    v = cu(value, torch.float32).requires_grad_()
+    p = cu(proj, torch.float32).requires_grad_()
+    r = cu(ref, torch.float32).requires_grad_()
+    mk = None if mask is None else cu(mask).view(torch.uint8)
+    out = MSDA1dFunction.apply(v, mk, p, r, tuple(T_l), 0, M * 16)
+    close(out, eo, 1e-4, "out")
+    out.backward(cu(gout, torch.float32))
+    close(v.grad, egv, 1e-4, "grad_value")
+    close(p.grad, egp, 1e-4, "grad_proj")
+    close(r.grad, egr, 1e-4, "grad_ref")
+
+
+def test_fused_msda1d_pdvc_shape_vs_oracle():
+    """PDVC encoder shape at T=128 (M=8, D=64, S=240, Lq=S), one video."""
+    from pdvc.ops.functions import MSDA1dFunction
+    rng = np.random.RandomState(1)
+    T_l = [128, 64, 32, 16]
+    S = sum(T_l)
+    M, D, N, Lq = 8, 64, 1, S
+    value = rng.randn(N, S, M, D).astype(np.float32)
+    proj = np.concatenate([rng.randn(N, Lq, M * 16) * 2, rng.randn(N, Lq, M * 16)], -1).astype(np.float32)
+    ref = np.concatenate([(np.arange(t) + 0.5) / t for t in T_l])[None, :, None, None].repeat(4, 2).astype(np.float32)
+    gout = rng.randn(N, Lq, M * D).astype(np.float32)
+    eo, egv, egp, egr = expected_msda1d(value.astype(np.float64), None, proj.astype(np.float64),
+                                        ref.astype(np.float64), T_l, M, gout.astype(np.float64))
+    v, p = cu(value).requires_grad_(), cu(proj).requires_grad_()
+    out = MSDA1dFunction.apply(v, None, p, cu(ref), tuple(T_l), 0, M * 16)
+    close(out, eo, 1e-4, "out")
+    out.backward(cu(gout))
+    close(v.grad, egv, 1e-4, "grad_value")
+    close(p.grad, egp, 1e-4, "grad_proj")
+
+
+# ------------------------------------------------------------------------------------------------
+# caption gather (border raw samples) vs oracle
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("D,M", [(512, 1), (64, 1), (32, 2), (128, 3)])
+@pytest.mark.parametrize("ref_dim", [1, 2])
+def test_cap_gather_vs_oracle(D, M, ref_dim):
+    from pdvc.ops.functions import CapGatherFunction
+    rng = np.random.RandomState(D + M + ref_dim)
+    T_l = [24, 12, 6, 3]
+    S, N, R, L, P = sum(T_l), 3, 11, 4, 4
+    value = rng.randn(N, S, M, D)
+    row_video = rng.randint(0, N, size=R).astype(np.int32)
+    offsets = rng.randn(R, M * 16) * 3.0
+    if ref_dim == 1:
+        ref = rng.uniform(-0.1, 1.1, size=(R, 4, 1))
+    else:
+        ref = np.concatenate([rng.uniform(0, 1, size=(R, 4, 1)), rng.uniform(0.05, 0.9, size=(R, 4, 1))], -1)
+    gs = rng.randn(R, M, 16, D)
+    off = offsets.reshape(R, M, L, P)
+    Tn = np.asarray(T_l, np.float64)[None, None, :, None]
+    if ref_dim == 1:
+        loc = ref[:, None, :, None, 0] + off / Tn
+    else:
+        loc = ref[:, None, :, None, 0] + off / P * ref[:, None, :, None, 1] * 0.5
+    exp_s = np.zeros((R, M, 16, D))
+    exp_gv = np.zeros_like(value)
+    exp_gl = np.zeros((R, M, L, P))
+    for r in range(R):
+        b = row_video[r]
+        loc2, shapes, lsi = O.lift_1d(loc[r][None, None], T_l)  # (1,1,M,L,P,2)
+        s = O.msda_sample(value[b][None], shapes, lsi, loc2, "border")  # (M, D, 1, L, P)
+        exp_s[r] = s[:, :, 0].reshape(M, D, 16).transpose(0, 2, 1)
+        g = gs[r].transpose(0, 2, 1).reshape(M, D, 1, L, P)
+        gv, gl = O.msda_sample_backward(value[b][None], shapes, lsi, loc2, g, "border")
+        exp_gv[b] += gv[0]
+        exp_gl[r] = gl[0, 0, ..., 0]
+    if ref_dim == 1:
+        exp_go = exp_gl / Tn
+        exp_gr = exp_gl.sum(axis=(1, 3))[..., None]
+    else:
+        exp_go = exp_gl * 0.5 * ref[:, None, :, None, 1] / P
+        exp_gr = np.stack([exp_gl.sum(axis=(1, 3)), (exp_gl * 0.5 * off / P).sum(axis=(1, 3))], -1)
+    v = cu(value, torch.float32).requires_grad_()
+    o = cu(offsets, torch.float32).requires_grad_()
+    rf = cu(ref, torch.float32).requires_grad_()
+    s = CapGatherFunction.apply(v, None, cu(row_video), o, rf, tuple(T_l), 0)
+    close(s, exp_s, 1e-5, "samples")
+    s.backward(cu(gs, torch.float32))
+    close(v.grad, exp_gv, 1e-4, "grad_value")
+    close(o.grad, exp_go.reshape(R, M * 16), 1e-4, "grad_offsets")
+    close(rf.grad, exp_gr, 1e-4, "grad_ref")
+
+
+# ------------------------------------------------------------------------------------------------
+# modules vs golden vectors generated from the reference modules
+# ------------------------------------------------------------------------------------------------
+def _fill(module):
+    import sys
+    sys.path.insert(0, G)
+    import weights as W
+    W.fill_module(module, overrides={"sampling_offsets": 0.5})
+
+
+@pytest.mark.parametrize("ref_dim", [1, 2])
+def test_module_msdeformattn_vs_golden(ref_dim):
+    from pdvc.ops.modules import MSDeformAttn
+    d = load(f"module_msdeformattn_ref{ref_dim}")
+    m = MSDeformAttn(64, 4, 4, 4).to(DEV)
+    _fill(m)
+    q = cu(d["query"]).requires_grad_()
+    r = cu(d["ref"]).requires_grad_()
+    x = cu(d["x"]).requires_grad_()
+    T_l = tuple(int(t) for t in d["T_l"])
+    shapes = torch.as_tensor(T_l, device=DEV)
+    lsi = torch.cat([shapes.new_zeros(1), shapes.cumsum(0)[:-1]])
+    out = m(q, r, x, T_l, lsi, cu(d["pad"]))
+    close(out, d["out"], 1e-4, "out")
+    out.backward(cu(d["grad_out"]))
+    close(q.grad, d["grad_query"], 1e-4, "grad_query")
+    close(r.grad, d["grad_ref"], 1e-4, "grad_ref")
+    close(x.grad, d["grad_x"], 1e-4, "grad_x")
+    for n, p in m.named_parameters():
+        close(p.grad, d["grad." + n], 1e-4, n)
