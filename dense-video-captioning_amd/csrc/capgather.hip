@@ -42,9 +42,10 @@ __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __rest
                                                               const uint8_t* __restrict__ vmask,
                                                               const int32_t* __restrict__ row_video,
                                                               const float* __restrict__ offsets, int off_stride,
-                                                              int off_col0, const float* __restrict__ ref, CapLevels lv,
-                                                              int S, int M, int D, int waves_per_row, int total_waves,
-                                                              float* __restrict__ samples, float* __restrict__ save_loc) {
+                                                              int off_col0, const float* __restrict__ ref, int rd1_rows,
+                                                              CapLevels lv, int S, int M, int D, int waves_per_row,
+                                                              int total_waves, float* __restrict__ samples,
+                                                              float* __restrict__ save_loc) {
     constexpr int HPW = 64 / LPH;
     const int lane = threadIdx.x & 63;
     const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -60,6 +61,7 @@ __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __rest
     const float* vbase = value + (size_t)b * S * MD + (size_t)m * D + c0;
     const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
     const float* orow = offsets + (size_t)r * off_stride + off_col0 + m * cNS;
+    const bool centre_only = (RD == 1) || (r < rd1_rows);  // wave-uniform
 #pragma unroll
     for (int l = 0; l < cL; ++l) {
         const int T = lv.T[l], st = lv.start[l];
@@ -69,7 +71,7 @@ __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __rest
         for (int p = 0; p < cP; ++p) {
             const int j = l * cP + p;
             const float off = orow[j];
-            const float loc = (RD == 1) ? r0 + off / (float)T : r0 + ((off / (float)cP) * r1) * 0.5f;
+            const float loc = centre_only ? r0 + off / (float)T : r0 + ((off / (float)cP) * r1) * 0.5f;
             if (save_loc && sub == (j % LPH)) save_loc[((size_t)r * M + m) * cNS + j] = loc;
             float gm;
             const float ix = border_ix(loc, T, gm);
@@ -92,8 +94,8 @@ __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __rest
 template <int CPL, int LPH, int RD>
 __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const int32_t* __restrict__ row_video,
-    const float* __restrict__ offsets, int off_stride, int off_col0, const float* __restrict__ ref, CapLevels lv, int S,
-    int M, int D, int waves_per_row, int total_waves, const float* __restrict__ save_loc,
+    const float* __restrict__ offsets, int off_stride, int off_col0, const float* __restrict__ ref, int rd1_rows,
+    CapLevels lv, int S, int M, int D, int waves_per_row, int total_waves, const float* __restrict__ save_loc,
     const float* __restrict__ gsamp, float* __restrict__ grad_value, float* __restrict__ grad_off,
     float* __restrict__ grad_ref) {
     constexpr int HPW = 64 / LPH;
@@ -157,6 +159,7 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
     for (int l = 0; l < cL; ++l) { gr0[l] = 0.f; gr1[l] = 0.f; }
     const bool owner = active && sub < G;
     const int gsub = sub % G;
+    const bool centre_only = (RD == 1) || (r < rd1_rows);
 #pragma unroll
     for (int k = 0; k < SPL; ++k) {
         const int j = gsub * SPL + k;
@@ -167,7 +170,7 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
         border_ix(loc, T, gm);
         const float gloc = 2.f * (gm * part[k]);  // grid = 2*loc - 1
         float goff;
-        if (RD == 1) {
+        if (centre_only) {
             goff = gloc / (float)T;
 #pragma unroll
             for (int ll = 0; ll < cL; ++ll) if (ll == l && owner) gr0[ll] += gloc;
@@ -237,7 +240,7 @@ using namespace pdvc;
 
 extern "C" int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* value_pad_mask, const int32_t* row_video,
                                            const float* offsets, int off_stride, int off_col0, const float* ref,
-                                           int ref_dim, const int32_t* level_T, int num_levels, int batch, int rows,
+                                           int ref_dim, int rd1_rows, const int32_t* level_T, int num_levels, int batch, int rows,
                                            int num_heads, int head_dim, int num_point, float* samples, float* save_loc,
                                            void* stream) {
     CapLevels lv;
@@ -252,10 +255,10 @@ extern "C" int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* va
     hipStream_t s = (hipStream_t)stream;
     if (ref_dim == 1) {
         CAP_DISPATCH(cap_gather_fwd_kernel, 1, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
-                     ref, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc)
+                     ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc)
     } else {
         CAP_DISPATCH(cap_gather_fwd_kernel, 2, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
-                     ref, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc)
+                     ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc)
     }
     PDVC_CHECK_LAUNCH("cap_gather_fwd_kernel");
     return PDVC_OK;
@@ -263,7 +266,8 @@ extern "C" int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* va
 
 extern "C" int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* value_pad_mask,
                                             const int32_t* row_video, const float* offsets, int off_stride,
-                                            int off_col0, const float* ref, int ref_dim, const int32_t* level_T,
+                                            int off_col0, const float* ref, int ref_dim, int rd1_rows,
+                                            const int32_t* level_T,
                                             int num_levels, int batch, int rows, int num_heads, int head_dim,
                                             int num_point, const float* save_loc, const float* grad_samples,
                                             float* grad_value, float* grad_offsets, float* grad_ref, void* stream) {
@@ -283,12 +287,12 @@ extern "C" int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* v
     dim3 grid((unsigned)((tw + 3) / 4));
     if (ref_dim == 1) {
         CAP_DISPATCH(cap_gather_bwd_kernel, 1, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
-                     ref, lv, S, num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples, grad_value, grad_offsets,
-                     grad_ref)
+                     ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples, grad_value,
+                     grad_offsets, grad_ref)
     } else {
         CAP_DISPATCH(cap_gather_bwd_kernel, 2, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
-                     ref, lv, S, num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples, grad_value, grad_offsets,
-                     grad_ref)
+                     ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples, grad_value,
+                     grad_offsets, grad_ref)
     }
     PDVC_CHECK_LAUNCH("cap_gather_bwd_kernel");
     return PDVC_OK;

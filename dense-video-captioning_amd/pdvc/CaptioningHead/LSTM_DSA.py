@@ -1,0 +1,259 @@
+"""LSTM captioner with deformable soft attention (reference: pdvc/CaptioningHead/LSTM_DSA.py:17-270).
+
+Same parameters/state_dict names (embed, logit, core.rnn.weight_{ih,hh}_l0, core.deformable_att.*,
+core.ctx2att, core.h2att, core.alpha_net) and the same per-step math, restructured for MI355X:
+
+  * every matched (decoder layer, video, event) row of a batch is decoded in ONE recurrence (the reference
+    runs one Python loop per decoder layer per video and asserts batch size 1, LSTM_DSA.py:59);
+  * loop invariants are hoisted out of the recurrence -- value_proj(memory) (the reference recomputes an
+    S x d x d GEMM every step, ms_deform_attn_for_caption.py:94), the embedding lookups and their LSTM
+    input projection (teacher forcing makes every input token known up front), the event-feature part of
+    the sampling-offset and LSTM projections -- and the three h_{t-1} projections (sampling offsets,
+    h2att, W_hh) are one GEMM;
+  * the caption logits (logit + log_softmax) are one GEMM over all steps after the recurrence;
+  * the border-padded deformable sampling is the HIP caption-gather kernel; rows of decoder layer 0 (1-d
+    reference) and later layers ((c, len) references) share one launch.
+The teacher-forced loop length is computed on the host from the caption lengths (the reference stops at the
+first all-zero token column, LSTM_DSA.py:103-104): the same steps are computed, without a per-step sync.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from pdvc.ops.modules import MSDeformAttnCap
+
+
+class LSTMWeights(nn.Module):
+    """The parameters of nn.LSTM(input_size, hidden_size, num_layers=1, bias=False) under nn.LSTM's names
+    and init (uniform +-1/sqrt(hidden)).  Only the weights are used: the cell runs in the decoder loop."""
+
+    def __init__(self, input_size, hidden_size, num_layers=1):
+        super().__init__()
+        if num_layers != 1:
+            raise NotImplementedError("the caption LSTM supports num_layers=1 (every PDVC config)")
+        self.input_size = input_size
+        self.hidden_size = hidden_size
+        self.weight_ih_l0 = nn.Parameter(torch.empty(4 * hidden_size, input_size))
+        self.weight_hh_l0 = nn.Parameter(torch.empty(4 * hidden_size, hidden_size))
+        stdv = 1.0 / math.sqrt(hidden_size)
+        for w in (self.weight_ih_l0, self.weight_hh_l0):
+            nn.init.uniform_(w, -stdv, stdv)
+
+
+def lstm_cell(gates, c):
+    """PyTorch gate order (i, f, g, o); c' = f*c + i*g; h' = o*tanh(c')."""
+    i, f, g, o = gates.chunk(4, 1)
+    c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(g)
+    h = torch.sigmoid(o) * torch.tanh(c)
+    return h, c
+
+
+class Captioner(nn.Module):
+    def __init__(self, opt):
+        super().__init__()
+        self.opt = opt
+        self.vocab_size = opt.vocab_size
+        self.input_encoding_size = opt.input_encoding_size
+        self.rnn_size = opt.rnn_size
+        self.num_layers = opt.num_layers
+        self.drop_prob_lm = opt.drop_prob
+        self.max_caption_len = opt.max_caption_len
+        self.ss_prob = 0.0
+        self.embed = nn.Embedding(self.vocab_size + 1, self.input_encoding_size)
+        self.logit = nn.Linear(self.rnn_size, self.vocab_size + 1)
+        self.dropout = nn.Dropout(self.drop_prob_lm)
+        self.init_weights()
+
+    def init_weights(self):
+        r = 0.1
+        self.embed.weight.data.uniform_(-r, r)
+        self.logit.bias.data.fill_(0)
+        self.logit.weight.data.uniform_(-r, r)
+
+    def init_hidden(self, batch_size):
+        w = next(self.parameters())
+        return (w.new_zeros(self.num_layers, batch_size, self.rnn_size),
+                w.new_zeros(self.num_layers, batch_size, self.rnn_size))
+
+    def build_loss(self, input, target, mask):
+        """-(sum_t logp[t, target_t] * mask_t) / (sum mask + 1e-6) (LSTM_DSA.py:48-52), as a gather
+        instead of a (rows, steps, vocab) one-hot product."""
+        max_len = input.shape[1]
+        picked = input.gather(2, target[:, :max_len, None]).squeeze(2)
+        return -(picked * mask[:, :max_len]).sum(1) / (mask.sum(1) + 1e-6)
+
+
+def caption_steps(cap_tensor_cpu):
+    """Number of decoder steps of the reference's teacher-forced loop for one video's captions:
+    i runs over range(K-1) and stops at the first i >= 1 whose token column is all zero."""
+    K = cap_tensor_cpu.shape[1]
+    for i in range(1, K - 1):
+        if int(cap_tensor_cpu[:, i].abs().sum()) == 0:
+            return i
+    return max(K - 1, 0)
+
+
+class ShowAttendTellCore(nn.Module):
+    def __init__(self, opt):
+        super().__init__()
+        self.input_encoding_size = opt.input_encoding_size
+        self.rnn_size = opt.rnn_size
+        self.num_layers = opt.num_layers
+        self.drop_prob_lm = opt.drop_prob
+        self.att_feat_size = int(opt.clip_context_dim / opt.cap_nheads)
+        self.att_hid_size = opt.att_hid_size
+        self.opt = opt
+        self.wordRNN_input_feats_type = opt.wordRNN_input_feats_type
+        self.input_dim = opt.hidden_dim * 2
+        self.rnn = LSTMWeights(self.input_encoding_size + self.input_dim, self.rnn_size, self.num_layers)
+        self.att_drop = nn.Dropout(0.5)  # owned by the reference, never applied
+        d_model = opt.hidden_dim
+        self.n_levels = opt.cap_num_feature_levels
+        self.n_heads = opt.cap_nheads
+        self.n_points = opt.cap_dec_n_points
+        self.deformable_att = MSDeformAttnCap(d_model, self.n_levels, self.n_heads, self.n_points)
+        if self.att_hid_size > 0:
+            self.ctx2att = nn.Linear(self.att_feat_size, self.att_hid_size)
+            self.h2att = nn.Linear(self.rnn_size, self.att_hid_size)
+            self.alpha_net = nn.Linear(self.att_hid_size, 1)
+
+
+class LSTMDSACaptioner(Captioner):
+    def __init__(self, opt):
+        super().__init__(opt)
+        self.core = ShowAttendTellCore(opt)
+
+    # ------------------------------------------------------------------------------------------------
+    # the batched decode engine
+    # ------------------------------------------------------------------------------------------------
+    def _prepare(self, memory, mask_flatten):
+        core = self.core
+        value = core.deformable_att.value_proj(memory)  # hoisted: identical for every step
+        mask_u8 = None if mask_flatten is None else mask_flatten.contiguous().view(torch.uint8)
+        return value, mask_u8
+
+    def _step_weights(self):
+        core = self.core
+        H = self.rnn_size
+        E = self.input_encoding_size
+        Dm = core.input_dim // 2
+        W_off, b_off = core.deformable_att.sampling_offsets.weight, core.deformable_att.sampling_offsets.bias
+        W_ih, W_hh = core.rnn.weight_ih_l0, core.rnn.weight_hh_l0
+        n_off = W_off.shape[0]
+        A = core.att_hid_size
+        # one GEMM for every h_{t-1} projection: [sampling offsets (h part) ; h2att ; W_hh]
+        W_h = torch.cat([W_off[:, :H], core.h2att.weight, W_hh], 0)
+        b_h = torch.cat([b_off.new_zeros(n_off), core.h2att.bias, W_hh.new_zeros(W_hh.shape[0])], 0)
+        return dict(H=H, E=E, Dm=Dm, n_off=n_off, A=A, W_off_hs=W_off[:, H:], b_off=b_off,
+                    W_x=W_ih[:, :E], W_att=W_ih[:, E:E + Dm], W_hs=W_ih[:, E + Dm:], W_h=W_h, b_h=b_h)
+
+    def _step(self, w, h, c, x_gates, hs_part, off_hs, value, mask_u8, row_video, ref_rows, rd1_rows, level_T):
+        """One decoder step for all rows (LSTM_DSA.py:231-263)."""
+        core = self.core
+        n_off, A = w["n_off"], w["A"]
+        hp = F.linear(h, w["W_h"], w["b_h"])
+        off = hp[:, :n_off] + off_hs
+        att_h = hp[:, n_off:n_off + A]
+        g_hh = hp[:, n_off + A:]
+        clip = core.deformable_att.sample_rows(value, mask_u8, row_video, off.contiguous(), ref_rows, level_T, 0,
+                                               rd1_rows)  # (R, M, L*P, D)
+        R, M, NS, D = clip.shape
+        att = core.ctx2att(clip)  # (R, M, NS, A)
+        dot = torch.tanh(att + att_h[:, None, None, :])
+        dot = core.alpha_net(dot).squeeze(-1)  # (R, M, NS)
+        weight = F.softmax(dot, dim=-1)
+        att_res = torch.bmm(weight.reshape(R * M, 1, NS), clip.reshape(R * M, NS, D)).reshape(R, M * D)
+        gates = x_gates + hs_part + F.linear(att_res, w["W_att"]) + g_hh
+        return lstm_cell(gates, c)
+
+    def decode_teacher_forced(self, hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten, level_T, seq,
+                              n_steps):
+        """hs_rows (R, d) event features; ref_rows (R, L, 2) references (rows < rd1_rows are 1-d: centre in
+        [..., 0]); row_video (R,) int32; memory (N, S, d); seq (R, K) long; returns logprobs (R, n_steps, V)."""
+        R = hs_rows.shape[0]
+        w = self._step_weights()
+        value, mask_u8 = self._prepare(memory, mask_flatten)
+        xt = self.embed(seq[:, :n_steps])  # (R, n, E)
+        x_gates = F.linear(xt, w["W_x"])  # (R, n, 4H)
+        hs_part = F.linear(hs_rows, w["W_hs"])
+        off_hs = F.linear(hs_rows, w["W_off_hs"], w["b_off"])
+        h = hs_rows.new_zeros(R, w["H"])
+        c = hs_rows.new_zeros(R, w["H"])
+        outs = []
+        for i in range(n_steps):
+            h, c = self._step(w, h, c, x_gates[:, i], hs_part, off_hs, value, mask_u8, row_video, ref_rows,
+                              rd1_rows, level_T)
+            outs.append(h)
+        if not outs:
+            return hs_rows.new_zeros(R, 0, self.vocab_size + 1)
+        Hs = torch.stack(outs, 1)
+        return F.log_softmax(self.logit(self.dropout(Hs)), dim=-1)
+
+    @torch.no_grad()
+    def decode_greedy(self, hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten, level_T, max_len=None):
+        """Greedy decoding (sample_max=1, LSTM_DSA.py:118-186) for all rows at once; returns
+        seq (R, T) and seqLogprobs (R, T) with the reference's unfinished-mask semantics, T <= max_len+1 steps."""
+        R = hs_rows.shape[0]
+        max_len = self.max_caption_len if max_len is None else max_len
+        w = self._step_weights()
+        value, mask_u8 = self._prepare(memory, mask_flatten)
+        hs_part = F.linear(hs_rows, w["W_hs"])
+        off_hs = F.linear(hs_rows, w["W_off_hs"], w["b_off"])
+        h = hs_rows.new_zeros(R, w["H"])
+        c = hs_rows.new_zeros(R, w["H"])
+        it = torch.zeros(R, dtype=torch.long, device=hs_rows.device)
+        seq, seqlp = [], []
+        unfinished = None
+        for t in range(max_len + 1):
+            if t > 0:
+                sample_lp, it = torch.max(logprobs, 1)
+            x_gates = F.linear(self.embed(it), w["W_x"])
+            h, c = self._step(w, h, c, x_gates, hs_part, off_hs, value, mask_u8, row_video, ref_rows, rd1_rows,
+                              level_T)
+            logprobs = F.log_softmax(self.logit(self.dropout(h)), dim=1)
+            if t >= 1:
+                unfinished = (it > 0) if t == 1 else (unfinished & (it > 0))
+                if int(unfinished.sum()) == 0:
+                    break
+                seq.append(it * unfinished.type_as(it))
+                seqlp.append(sample_lp.view(-1))
+        if not seq:
+            return None, None
+        return torch.stack(seq, 1), torch.stack(seqlp, 1)
+
+    # ------------------------------------------------------------------------------------------------
+    # reference-compatible entry points (one video: hs (1, E, d))
+    # ------------------------------------------------------------------------------------------------
+    def _rows_from_reference(self, hs, reference, others):
+        vid_num, query_num, _ = hs.shape
+        L = self.core.n_levels
+        vr = others["valid_ratios"]
+        if reference.shape[-1] == 2:
+            ref = reference[:, :, None] * torch.stack([vr] * 2, -1)[:, None]
+            rd1 = 0
+        else:
+            ref = reference[:, :, None] * vr[:, None, :, None]
+            ref = torch.cat([ref, torch.zeros_like(ref)], -1)
+            rd1 = vid_num * query_num
+        ref = ref[:, :, :L].reshape(vid_num * query_num, L, 2)
+        row_video = torch.arange(vid_num, device=hs.device, dtype=torch.int32).repeat_interleave(query_num)
+        T = tuple(int(x) for x in others.get("level_T", others["spatial_shapes"].tolist()))[:L]
+        return hs.reshape(vid_num * query_num, -1), ref, rd1, row_video, T
+
+    def forward(self, hs, reference, others, cap_tensor):
+        hs_rows, ref, rd1, rv, T = self._rows_from_reference(hs, reference, others)
+        seq = cap_tensor.long()
+        n_steps = caption_steps(seq.detach().cpu())
+        return self.decode_teacher_forced(hs_rows, ref, rd1, rv, others["memory"], others["mask_flatten"], T, seq,
+                                          n_steps)
+
+    def sample(self, hs, reference, others, opt={}):
+        if opt.get("sample_max", 1) != 1 or opt.get("beam_size", 1) != 1:
+            raise NotImplementedError("only greedy decoding (sample_max=1, beam_size=1) is supported")
+        hs_rows, ref, rd1, rv, T = self._rows_from_reference(hs, reference, others)
+        seq, lp = self.decode_greedy(hs_rows, ref, rd1, rv, others["memory"], others["mask_flatten"], T)
+        if seq is None:
+            return [], []
+        return seq, lp

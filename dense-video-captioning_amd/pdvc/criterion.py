@@ -1,0 +1,124 @@
+"""Set criterion (reference: pdvc/criterion.py:14-256) with per-video semantics for batches.
+
+For one video every number equals the reference's.  A batch of N videos returns, for every loss key, the
+mean over videos of the per-video values (each video normalised by its own event count, exactly as the
+reference's batch-size-1 training does); gradients are therefore the average of N batch-1 gradients.
+All decoder layers' matchings are solved after ONE device->host copy (the reference syncs once per layer).
+"""
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import box_ops
+
+COUNTER_CLASS_RATE = [0.00000000e+00, 0.00000000e+00, 1.93425917e-01, 4.12129084e-01, 1.88929963e-01,
+                      7.81296833e-02, 5.09541413e-02, 3.12718553e-02, 1.84833650e-02, 8.39244680e-03,
+                      6.59406534e-03, 4.49595364e-03, 2.19802178e-03, 1.79838146e-03, 5.99460486e-04,
+                      4.99550405e-04, 4.99550405e-04, 1.99820162e-04, 2.99730243e-04, 3.99640324e-04,
+                      2.99730243e-04, 0.00000000e+00, 1.99820162e-04, 0.00000000e+00, 0.00000000e+00,
+                      0.00000000e+00, 9.99100809e-05, 9.99100809e-05]
+
+
+def sigmoid_focal_terms(inputs, targets, alpha=0.25, gamma=2):
+    """Elementwise focal loss (criterion.py:222-248 before its reductions)."""
+    prob = inputs.sigmoid()
+    ce = F.binary_cross_entropy_with_logits(inputs, targets, reduction="none")
+    p_t = prob * targets + (1 - prob) * (1 - targets)
+    loss = ce * ((1 - p_t) ** gamma)
+    if alpha >= 0:
+        loss = (alpha * targets + (1 - alpha) * (1 - targets)) * loss
+    return loss
+
+
+def counter_loss_terms(inputs, targets, gau_mask, beta, weight):
+    """cross_entropy_with_gaussian_mask (criterion.py:200-220) up to its batch mean: (N,) per video."""
+    n = targets.shape[1]
+    mu = torch.arange(n, device=inputs.device).unsqueeze(0).expand(n, n).float()
+    x = mu.transpose(0, 1)
+    mask_dict = torch.exp(-(x - mu) ** 2 / (2 * 2 ** 2))
+    _, ind = targets.max(dim=1)
+    mask = mask_dict[ind]
+    loss = F.binary_cross_entropy_with_logits(inputs, targets, reduction="none", weight=1 - weight)
+    coef = targets + ((1 - mask) ** beta) * (1 - targets) if gau_mask else targets + (1 - targets)
+    return (loss * coef).mean(1)
+
+
+class SetCriterion(nn.Module):
+    def __init__(self, num_classes, matcher, weight_dict, losses, focal_alpha=0.25, focal_gamma=2, opt={}):
+        super().__init__()
+        self.num_classes = num_classes
+        self.matcher = matcher
+        self.weight_dict = weight_dict
+        self.losses = losses
+        self.focal_alpha = focal_alpha
+        self.focal_gamma = focal_gamma
+        self.opt = opt
+        self.counter_class_rate = torch.tensor(COUNTER_CLASS_RATE)
+
+    # -------------------------------------------------------------------------------------------------
+    def layer_losses(self, outputs, targets, indices):
+        """Per-video losses of one decoder layer, averaged over the batch.  outputs: pred_logits (N,Q,C),
+        pred_boxes (N,Q,2), pred_count (N,K+1); indices: list of (query ids, target ids) per video."""
+        logits, boxes, count = outputs["pred_logits"], outputs["pred_boxes"], outputs["pred_count"]
+        N, Q, C = logits.shape
+        dev = logits.device
+        nb = torch.tensor([max(float(len(t["labels"])), 1.0) for t in targets], device=dev)  # clamp(min=1)
+        # labels: focal loss over every query and class (criterion.py:46-65)
+        tclass = torch.full((N, Q), self.num_classes, dtype=torch.int64, device=dev)
+        for v, ((qi, ti), t) in enumerate(zip(indices, targets)):
+            tclass[v, qi.to(dev)] = t["labels"][ti.to(t["labels"].device)].to(dev)
+        onehot = torch.zeros((N, Q, C + 1), dtype=logits.dtype, device=dev)
+        onehot.scatter_(2, tclass.unsqueeze(-1), 1)
+        onehot = onehot[:, :, :-1]
+        focal = sigmoid_focal_terms(logits, onehot, self.focal_alpha, self.focal_gamma)  # (N,Q,C)
+        loss_ce = focal.mean(1).sum(1) / nb * Q
+        # counter (criterion.py:67-76)
+        max_length = count.shape[1] - 1
+        ctgt = torch.tensor([min(len(t["boxes"]), max_length) for t in targets], device=dev, dtype=torch.long)
+        ctgt_onehot = torch.zeros_like(count)
+        ctgt_onehot.scatter_(1, ctgt.unsqueeze(-1), 1)
+        weight = self.counter_class_rate[:max_length + 1].to(dev)
+        loss_counter = counter_loss_terms(count, ctgt_onehot, self.opt.lloss_gau_mask, self.opt.lloss_beta, weight)
+        # cardinality (logging only, criterion.py:80-92)
+        card_pred = (logits.argmax(-1) != C - 1).sum(1).float()
+        tlen = torch.tensor([float(len(t["labels"])) for t in targets], device=dev)
+        card_err = (card_pred - tlen).abs()
+        # boxes (criterion.py:94-123), per video
+        lb, lg, ls = [], [], []
+        for v, ((qi, ti), t) in enumerate(zip(indices, targets)):
+            src = boxes[v, qi.to(dev)]
+            tgt = t["boxes"][ti.to(t["boxes"].device)].to(dev)
+            lb.append(F.l1_loss(src, tgt, reduction="none").sum() / nb[v])
+            sxy, txy = box_ops.box_cl_to_xy(src), box_ops.box_cl_to_xy(tgt)
+            lg.append((1 - torch.diag(box_ops.generalized_box_iou(sxy, txy))).sum() / nb[v])
+            n = len(qi)
+            self_iou = torch.triu(box_ops.box_iou(sxy, sxy)[0], diagonal=1)
+            ls.append(self_iou.sum() / (0.5 * n * (n - 1)))
+        return {"loss_ce": loss_ce.mean(), "loss_counter": loss_counter.mean(),
+                "loss_bbox": torch.stack(lb).mean(), "loss_giou": torch.stack(lg).mean(),
+                "loss_self_iou": torch.stack(ls).mean(), "cardinality_error": card_err.mean()}
+
+    def forward(self, outputs, targets):
+        """Reference contract: returns (losses, last_indices[, aux_indices]); indices are
+        (list of per-video (query ids, target ids), None)."""
+        layers = [outputs] + list(outputs.get("aux_outputs", []))
+        blocks, per_layer = [], []
+        for o in layers:
+            b = self.matcher.cost_blocks(o["pred_logits"], o["pred_boxes"], targets)
+            per_layer.append(len(b))
+            blocks.extend(b)
+        solved, _ = self.matcher.solve(blocks)
+        idx, off = [], 0
+        for n in per_layer:
+            idx.append((solved[off:off + n], None))
+            off += n
+        last_indices = idx[0]
+        outputs["matched_indices"] = last_indices
+        losses = self.layer_losses(outputs, targets, last_indices[0])
+        if "aux_outputs" in outputs:
+            aux_indices = idx[1:]
+            for i, aux in enumerate(outputs["aux_outputs"]):
+                l_dict = self.layer_losses(aux, targets, aux_indices[i][0])
+                losses.update({k + f"_{i}": v for k, v in l_dict.items()})
+            return losses, last_indices, aux_indices
+        return losses, last_indices

@@ -143,10 +143,11 @@ class MSDA1dFunction(Function):
 
 class CapGatherFunction(Function):
     """Caption-head sampling: raw border samples (R, M, 16, D) of value (N,S,M,D) for query rows whose
-    video is row_video (R,) int32; offsets (R, C) with the M*16 offsets at column off_col0; ref (R,L,1|2)."""
+    video is row_video (R,) int32; offsets (R, C) with the M*16 offsets at column off_col0; ref (R,L,1|2).
+    With a 2-wide ref, the first rd1_rows rows are 1-d references (centre only, ref[..., 1] unused)."""
 
     @staticmethod
-    def forward(ctx, value, pad_mask, row_video, offsets, ref, level_T, off_col0):
+    def forward(ctx, value, pad_mask, row_video, offsets, ref, level_T, off_col0, rd1_rows=0):
         value, offsets, ref = value.contiguous(), offsets.contiguous(), ref.contiguous()
         N, S, M, D = value.shape
         R, C = offsets.shape
@@ -155,17 +156,17 @@ class CapGatherFunction(Function):
         samples = torch.empty((R, M, NUM_SAMPLES, D), dtype=value.dtype, device=value.device)
         save_loc = torch.empty((R, M, NUM_SAMPLES), dtype=value.dtype, device=value.device)
         _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video), _n.ptr(offsets),
-                C, off_col0, _n.ptr(ref), RD, lvl, nl, N, R, M, D, NUM_SAMPLES // nl, _n.ptr(samples),
-                _n.ptr(save_loc), _n.stream())
+                C, off_col0, _n.ptr(ref), RD, int(rd1_rows), lvl, nl, N, R, M, D, NUM_SAMPLES // nl,
+                _n.ptr(samples), _n.ptr(save_loc), _n.stream())
         ctx.save_for_backward(value, pad_mask, row_video, offsets, ref, save_loc)
-        ctx.meta = (tuple(level_T), off_col0)
+        ctx.meta = (tuple(level_T), off_col0, int(rd1_rows))
         return samples
 
     @staticmethod
     @once_differentiable
     def backward(ctx, grad_samples):
         value, pad_mask, row_video, offsets, ref, save_loc = ctx.saved_tensors
-        level_T, off_col0 = ctx.meta
+        level_T, off_col0, rd1_rows = ctx.meta
         grad_samples = grad_samples.contiguous()
         N, S, M, D = value.shape
         R, C = offsets.shape
@@ -175,6 +176,6 @@ class CapGatherFunction(Function):
         go = torch.zeros_like(offsets) if C != M * NUM_SAMPLES else torch.empty_like(offsets)
         gr = torch.empty_like(ref) if ctx.needs_input_grad[4] else None
         _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video),
-                _n.ptr(offsets), C, off_col0, _n.ptr(ref), RD, lvl, nl, N, R, M, D, NUM_SAMPLES // nl,
+                _n.ptr(offsets), C, off_col0, _n.ptr(ref), RD, rd1_rows, lvl, nl, N, R, M, D, NUM_SAMPLES // nl,
                 _n.ptr(save_loc), _n.ptr(grad_samples), _n.ptr(gv), _n.ptr(go), _n.ptr(gr), _n.stream())
-        return gv, None, None, go, gr, None, None
+        return gv, None, None, go, gr, None, None, None

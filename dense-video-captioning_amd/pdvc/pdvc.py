@@ -1,0 +1,338 @@
+"""PDVC model assembly for MI355X (reference: pdvc/pdvc.py:35-604).
+
+`build(args) -> (model, criterion, {'bbox': PostProcess})` and `PDVC.forward(dt, criterion,
+transformer_input_type, eval_mode=False) -> (out, loss)` keep the reference's contract and state_dict.
+Batches of N videos are supported (the reference asserts N == 1 in its caption head): every loss entry is
+the mean over videos of the reference's batch-1 value, all matched captions of all decoder layers and
+videos are decoded in one recurrence, and all Hungarian matchings share one device->host copy.
+"""
+import copy
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import box_ops
+from .base_encoder import build_base_encoder
+from .box_ops import inverse_sigmoid
+from .CaptioningHead import build_captioner
+from .CaptioningHead.LSTM_DSA import caption_steps
+from .criterion import SetCriterion
+from .deformable_transformer import build_deforamble_transformer
+from .matcher import build_matcher
+
+
+def _get_clones(module, N):
+    return nn.ModuleList([copy.deepcopy(module) for _ in range(N)])
+
+
+def decide_two_stage(transformer_input_type, dt, criterion):
+    """misc/utils.py:31-49 ('queries' mode; the '*_gt' proposal-input variants are out of scope)."""
+    if transformer_input_type == "queries":
+        return False, False, None, None
+    raise NotImplementedError(f"transformer_input_type '{transformer_input_type}' is not supported on the "
+                              f"MI355X path (BASELINE configs use 'queries')")
+
+
+class MLP(nn.Module):
+    def __init__(self, input_dim, hidden_dim, output_dim, num_layers):
+        super().__init__()
+        self.num_layers = num_layers
+        h = [hidden_dim] * (num_layers - 1)
+        self.layers = nn.ModuleList(nn.Linear(n, k) for n, k in zip([input_dim] + h, h + [output_dim]))
+
+    def forward(self, x):
+        for i, layer in enumerate(self.layers):
+            x = F.relu(layer(x)) if i < self.num_layers - 1 else layer(x)
+        return x
+
+
+class PDVC(nn.Module):
+    def __init__(self, base_encoder, transformer, captioner, num_classes, num_queries, num_feature_levels,
+                 aux_loss=True, with_box_refine=False, opt=None, translator=None):
+        super().__init__()
+        self.opt = opt
+        self.base_encoder = base_encoder
+        self.transformer = transformer
+        self.caption_head = captioner
+        hidden_dim = transformer.d_model
+        self.query_embed = nn.Embedding(num_queries, hidden_dim * 2)
+        self.class_head = nn.Linear(hidden_dim, num_classes)
+        self.count_head = nn.Linear(hidden_dim, opt.max_eseq_length + 1)
+        self.bbox_head = MLP(hidden_dim, hidden_dim, 2, 3)
+        self.num_feature_levels = num_feature_levels
+        self.aux_loss = aux_loss
+        self.with_box_refine = with_box_refine
+        self.share_caption_head = opt.share_caption_head
+        prior_prob = 0.01
+        self.class_head.bias.data = torch.ones(num_classes) * -math.log((1 - prior_prob) / prior_prob)
+        nn.init.constant_(self.bbox_head.layers[-1].weight.data, 0)
+        nn.init.constant_(self.bbox_head.layers[-1].bias.data, 0)
+        num_pred = transformer.decoder.num_layers
+        if self.share_caption_head:
+            self.caption_head = nn.ModuleList([self.caption_head for _ in range(num_pred)])
+        else:
+            self.caption_head = _get_clones(self.caption_head, num_pred)
+        if with_box_refine:
+            self.class_head = _get_clones(self.class_head, num_pred)
+            self.count_head = _get_clones(self.count_head, num_pred)
+            self.bbox_head = _get_clones(self.bbox_head, num_pred)
+            nn.init.constant_(self.bbox_head[0].layers[-1].bias.data[1:], -2)
+            self.transformer.decoder.bbox_head = self.bbox_head
+        else:
+            nn.init.constant_(self.bbox_head.layers[-1].bias.data[1:], -2)
+            self.class_head = nn.ModuleList([self.class_head for _ in range(num_pred)])
+            self.count_head = nn.ModuleList([self.count_head for _ in range(num_pred)])
+            self.bbox_head = nn.ModuleList([self.bbox_head for _ in range(num_pred)])
+            self.transformer.decoder.bbox_head = None
+        self.translator = translator
+        self.disable_mid_caption_heads = opt.disable_mid_caption_heads
+
+    # ------------------------------------------------------------------------------------------------
+    def forward(self, dt, criterion, transformer_input_type, eval_mode=False):
+        vf = dt["video_tensor"]
+        mask = ~dt["video_mask"]
+        duration = dt["video_length"][:, 1]
+        N = vf.shape[0]
+        srcs, masks, pos = self.base_encoder(vf, mask, duration)
+        tr = self.transformer
+        src_flatten, temporal_shapes, lsi, valid_ratios, lvl_pos, mask_flatten = tr.prepare_encoder_inputs(
+            srcs, masks, pos)
+        level_T = tr.last_level_T
+        memory = tr.forward_encoder(src_flatten, level_T, lsi, valid_ratios, lvl_pos, mask_flatten)
+        two_stage, disable_refine, proposals, proposals_mask = decide_two_stage(transformer_input_type, dt,
+                                                                                 criterion)
+        query_embed = self.query_embed.weight
+        proposals_mask = torch.ones(N, query_embed.shape[0], device=query_embed.device).bool()
+        init_reference, tgt, reference_points, query_embed = tr.prepare_decoder_input_query(memory, query_embed)
+        hs, inter_references = tr.forward_decoder(tgt, reference_points, memory, level_T, lsi, valid_ratios,
+                                                  query_embed, mask_flatten, proposals_mask, disable_refine)
+        others = {"memory": memory, "mask_flatten": mask_flatten, "spatial_shapes": temporal_shapes,
+                  "level_T": level_T, "level_start_index": lsi, "valid_ratios": valid_ratios,
+                  "proposals_mask": proposals_mask}
+        if eval_mode or self.opt.caption_loss_coef == 0:
+            return self.parallel_prediction_full(dt, criterion, hs, init_reference, inter_references, others,
+                                                 disable_refine)
+        return self.parallel_prediction_matched(dt, criterion, hs, init_reference, inter_references, others,
+                                                disable_refine)
+
+    def predict_event_num(self, counter, hs_lid):
+        return counter(torch.max(hs_lid, dim=1, keepdim=False)[0])
+
+    def _layer_heads(self, hs, init_reference, inter_references, disable_refine):
+        classes, counts, coords = [], [], []
+        for l_id in range(hs.shape[0]):
+            hs_l = hs[l_id]
+            reference = init_reference if l_id == 0 else inter_references[l_id - 1]
+            classes.append(self.class_head[l_id](hs_l))
+            counts.append(self.predict_event_num(self.count_head[l_id], hs_l))
+            tmp = self.bbox_head[l_id](hs_l)
+            if disable_refine:
+                coords.append(reference)
+            else:
+                r = inverse_sigmoid(reference)
+                if r.shape[-1] == 2:
+                    tmp = tmp + r
+                else:
+                    tmp = torch.cat([tmp[..., :1] + r, tmp[..., 1:]], -1)
+                coords.append(tmp.sigmoid())
+        return classes, counts, coords
+
+    def _pack(self, classes, counts, coords, cap_probs, seqs):
+        all_out = {"pred_logits": torch.stack(classes), "pred_count": torch.stack(counts),
+                   "pred_boxes": torch.stack(coords), "caption_probs": cap_probs, "seq": seqs}
+        out = {k: v[-1] for k, v in all_out.items()}
+        if self.aux_loss:
+            ks, vs = list(zip(*all_out.items()))
+            out["aux_outputs"] = [{ks[i]: vs[i][j] for i in range(len(ks))} for j in range(len(classes) - 1)]
+        return out
+
+    def _caption_rows(self, dt, hs, init_reference, inter_references, others, layer_indices):
+        """Gather every matched (layer, video, event) row: features, references (valid-ratio scaled per level,
+        pdvc/CaptioningHead/LSTM_DSA.py:66-70), token rows and the row bookkeeping."""
+        Ld, N, Q, C = hs.shape
+        dev = hs.device
+        L = self.caption_head[0].core.n_levels
+        vr = others["valid_ratios"][:, :L]  # (N, L)
+        cap_tensor = dt["cap_tensor"]
+        cap_cpu = dt.get("cap_tensor_cpu")
+        if cap_cpu is None:
+            cap_cpu = cap_tensor.detach().cpu()
+        gt_counts = [len(t["labels"]) for t in dt["video_target"]]
+        cap_off = [0]
+        for g in gt_counts:
+            cap_off.append(cap_off[-1] + g)
+        rows = []  # (layer, video, flat_hs_index, cap_row)
+        for l_id, indices in enumerate(layer_indices):
+            for v, (qi, gi) in enumerate(indices):
+                for q, g in zip(qi.tolist(), gi.tolist()):
+                    rows.append((l_id, v, (l_id * N + v) * Q + q, cap_off[v] + g))
+        # layer-0 rows first: their reference is 1-d
+        rows.sort(key=lambda r: (0 if r[0] == 0 else 1))
+        flat_idx = torch.tensor([r[2] for r in rows], dtype=torch.long)
+        cap_rows = torch.tensor([r[3] for r in rows], dtype=torch.long)
+        row_video = torch.tensor([r[1] for r in rows], dtype=torch.int32)
+        rd1 = sum(1 for r in rows if r[0] == 0 and init_reference.shape[-1] == 1)
+        hs_rows = hs.reshape(Ld * N * Q, C).index_select(0, flat_idx.to(dev))
+        refs = []
+        for l_id in range(Ld):
+            reference = init_reference if l_id == 0 else inter_references[l_id - 1]
+            if reference.shape[-1] == 2:
+                ref = reference[:, :, None] * torch.stack([vr, vr], -1)[:, None]
+            else:
+                ref = reference[:, :, None] * vr[:, None, :, None]
+                ref = torch.cat([ref, torch.zeros_like(ref)], -1)
+            refs.append(ref)
+        ref_all = torch.stack(refs).reshape(Ld * N * Q, L, 2)
+        ref_rows = ref_all.index_select(0, flat_idx.to(dev))
+        steps_v = []
+        for v in range(N):
+            steps_v.append(caption_steps(cap_cpu[cap_off[v]:cap_off[v + 1]]))
+        return dict(rows=rows, hs_rows=hs_rows, ref_rows=ref_rows.contiguous(), rd1=rd1,
+                    row_video=row_video.to(dev), cap_rows=cap_rows.to(dev), steps_v=steps_v)
+
+    def parallel_prediction_matched(self, dt, criterion, hs, init_reference, inter_references, others,
+                                    disable_refine):
+        classes, counts, coords = self._layer_heads(hs, init_reference, inter_references, disable_refine)
+        N, Q = hs.shape[1], hs.shape[2]
+        zero_probs = {"cap_prob_train": torch.zeros(1, device=hs.device),
+                      "cap_prob_eval": torch.zeros(N, Q, 3, device=hs.device)}
+        zero_seq = torch.zeros(N, Q, 3, device=hs.device)
+        out = self._pack(classes, counts, coords, [zero_probs] * len(classes), [zero_seq] * len(classes))
+        if not self.aux_loss:
+            raise NotImplementedError("aux_loss=False is not supported")
+        loss, last_indices, aux_indices = criterion(out, dt["video_target"])
+        Ld = hs.shape[0]
+        layer_indices = [aux_indices[l][0] for l in range(Ld - 1)] + [last_indices[0]]
+        R = self._caption_rows(dt, hs, init_reference, inter_references, others, layer_indices)
+        n_steps = max(R["steps_v"]) if R["steps_v"] else 0
+        seq_rows = dt["cap_tensor"].index_select(0, R["cap_rows"])
+        cap_mask_rows = dt["cap_mask"].index_select(0, R["cap_rows"])
+        if self.share_caption_head:
+            logprobs = self.caption_head[0].decode_teacher_forced(
+                R["hs_rows"], R["ref_rows"], R["rd1"], R["row_video"], others["memory"], others["mask_flatten"],
+                others["level_T"], seq_rows, n_steps)
+        else:
+            raise NotImplementedError("share_caption_head=0 is not supported on the batched caption path")
+        cap_loss = self.caption_head[0].build_loss(logprobs, seq_rows[:, 1:], cap_mask_rows[:, 1:].float())
+        # per (layer, video) mean over events, then mean over videos (= the reference's batch-1 losses)
+        rows = R["rows"]
+        lay = torch.tensor([r[0] for r in rows], device=hs.device)
+        vid = torch.tensor([r[1] for r in rows], device=hs.device)
+        key = lay * N + vid
+        sums = torch.zeros(Ld * N, device=hs.device, dtype=cap_loss.dtype).index_add_(0, key, cap_loss)
+        cnts = torch.zeros(Ld * N, device=hs.device, dtype=cap_loss.dtype).index_add_(
+            0, key, torch.ones_like(cap_loss))
+        per = (sums / cnts.clamp(min=1)).view(Ld, N).mean(1)
+        for l_id in range(Ld):
+            k = "loss_caption" if l_id == Ld - 1 else f"loss_caption_{l_id}"
+            loss[k] = per[l_id]
+        last_sel = torch.tensor([i for i, r in enumerate(rows) if r[0] == Ld - 1], dtype=torch.long,
+                                device=hs.device)
+        last_v = [r[1] for r in rows if r[0] == Ld - 1]
+        n_last = max([R["steps_v"][v] for v in last_v], default=0)
+        out.update({"caption_probs": {"cap_prob_train": logprobs.index_select(0, last_sel)[:, :n_last]},
+                    "seq": seq_rows.index_select(0, last_sel)})
+        return out, loss
+
+    def parallel_prediction_full(self, dt, criterion, hs, init_reference, inter_references, others,
+                                 disable_refine):
+        classes, counts, coords = self._layer_heads(hs, init_reference, inter_references, disable_refine)
+        Ld, N, Q, C = hs.shape
+        probs, seqs = [], []
+        for l_id in range(Ld):
+            if l_id != Ld - 1:
+                probs.append({"cap_prob_train": torch.zeros(1, device=hs.device),
+                              "cap_prob_eval": torch.zeros(N, Q, 3, device=hs.device)})
+                seqs.append(torch.zeros(N, Q, 3, device=hs.device))
+                continue
+            reference = init_reference if l_id == 0 else inter_references[l_id - 1]
+            head = self.caption_head[l_id]
+            L = head.core.n_levels
+            vr = others["valid_ratios"][:, :L]
+            if reference.shape[-1] == 2:
+                ref = reference[:, :, None] * torch.stack([vr, vr], -1)[:, None]
+                rd1 = 0
+            else:
+                ref = reference[:, :, None] * vr[:, None, :, None]
+                ref = torch.cat([ref, torch.zeros_like(ref)], -1)
+                rd1 = N * Q
+            row_video = torch.arange(N, device=hs.device, dtype=torch.int32).repeat_interleave(Q)
+            seq, lp = head.decode_greedy(hs[l_id].reshape(N * Q, C), ref.reshape(N * Q, L, 2).contiguous(), rd1,
+                                         row_video, others["memory"], others["mask_flatten"], others["level_T"])
+            if seq is None:
+                probs.append({"cap_prob_eval": []})
+                seqs.append([])
+            else:
+                probs.append({"cap_prob_eval": lp.reshape(N, Q, -1)})
+                seqs.append(seq.reshape(N, Q, -1))
+        out = self._pack(classes, counts, coords, probs, seqs)
+        loss, last_indices, aux_indices = criterion(out, dt["video_target"])
+        return out, loss
+
+
+class PostProcess(nn.Module):
+    """Model outputs -> per-video results (pdvc/pdvc.py:493-546): sigmoid scores, top-k query order,
+    (start, end) boxes clipped to [0,1] x duration, predicted event count, detokenised captions."""
+
+    def __init__(self, opt):
+        super().__init__()
+        self.opt = opt
+
+    @torch.no_grad()
+    def forward(self, outputs, target_sizes, loader):
+        out_logits, out_bbox = outputs["pred_logits"], outputs["pred_boxes"]
+        N, N_q, N_class = out_logits.shape
+        assert len(out_logits) == len(target_sizes)
+        prob = out_logits.sigmoid()
+        topk_values, topk_indexes = torch.topk(prob.view(N, -1), N_q, dim=1)
+        scores = topk_values
+        topk_boxes = topk_indexes // N_class
+        labels = topk_indexes % N_class
+        boxes = box_ops.box_cl_to_xy(out_bbox)
+        raw_boxes = boxes.clone()
+        boxes = boxes.clamp(0, 1)
+        boxes = torch.gather(boxes, 1, topk_boxes.unsqueeze(-1).repeat(1, 1, 2))
+        scale = torch.stack([target_sizes, target_sizes], dim=1)
+        boxes = boxes * scale[:, None, :]
+        seq = outputs["seq"]
+        cap_prob = outputs["caption_probs"]["cap_prob_eval"]
+        eseq_lens = outputs["pred_count"].argmax(dim=-1).clamp(min=1)
+        if len(seq):
+            mask = (seq > 0).float()
+            cap_scores = (mask * cap_prob).sum(2).cpu().numpy().astype("float")
+            seq = seq.detach().cpu().numpy().astype("int")
+            caps = [[loader.dataset.translator.rtranslate(s) for s in s_vid] for s_vid in seq]
+            caps = [[caps[b][idx] for idx in row] for b, row in enumerate(topk_boxes)]
+            cap_scores = [[cap_scores[b, idx] for idx in row] for b, row in enumerate(topk_boxes)]
+        else:
+            cap_scores = [[-1e5] * N_q] * N
+            caps = [[""] * N_q] * N
+        return [{"scores": s, "labels": l, "boxes": b, "raw_boxes": b, "captions": c, "caption_scores": cs,
+                 "query_id": qid, "vid_duration": ts, "pred_seq_len": sl}
+                for s, l, b, rb, c, cs, qid, ts, sl in zip(scores, labels, boxes, raw_boxes, caps, cap_scores,
+                                                            topk_boxes, target_sizes, eseq_lens)]
+
+
+def build(args):
+    device = torch.device(args.device)
+    base_encoder = build_base_encoder(args)
+    transformer = build_deforamble_transformer(args)
+    captioner = build_captioner(args)
+    model = PDVC(base_encoder, transformer, captioner, num_classes=args.num_classes, num_queries=args.num_queries,
+                 num_feature_levels=args.num_feature_levels, aux_loss=args.aux_loss,
+                 with_box_refine=args.with_box_refine, opt=args)
+    matcher = build_matcher(args)
+    weight_dict = {"loss_ce": args.cls_loss_coef, "loss_bbox": args.bbox_loss_coef,
+                   "loss_giou": args.giou_loss_coef, "loss_counter": args.count_loss_coef,
+                   "loss_caption": args.caption_loss_coef}
+    if args.aux_loss:
+        aux = {}
+        for i in range(args.dec_layers - 1):
+            aux.update({k + f"_{i}": v for k, v in weight_dict.items()})
+        weight_dict.update(aux)
+    criterion = SetCriterion(args.num_classes, matcher, weight_dict, ["labels", "boxes", "cardinality"],
+                             focal_alpha=args.focal_alpha, focal_gamma=args.focal_gamma, opt=args)
+    criterion.to(device)
+    return model, criterion, {"bbox": PostProcess(args)}

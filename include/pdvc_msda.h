@@ -121,18 +121,21 @@ int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value_pad_mask, 
 /* ---- caption-head border gather (MSDeformAttnCap) ----------------------------------------------------
  * value (N,S,M,D); value_pad_mask (N,S) or NULL; row_video (R,) int32 DEVICE: video of each query row;
  * offsets (R, off_stride) with the M*L*P sampling offsets at column off_col0; ref (R,L,ref_dim).
+ * With ref_dim 2, rows r < rd1_rows use the centre-only formula of a 1-d reference (loc = c + off / T_l;
+ * the caption heads of decoder layer 0 see the 1-d initial reference, later layers the refined (c, len)
+ * boxes -- pdvc/pdvc.py:249,296), so one launch serves every decoder layer's rows.
  * samples (R, M, L*P, D) [the layout ShowAttendTellCore consumes after its permute, LSTM_DSA.py:241-242];
  * save_loc (R, M, L*P) (may be NULL). */
 int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* value_pad_mask, const int32_t* row_video,
                                 const float* offsets, int off_stride, int off_col0, const float* ref,
-                                int ref_dim, const int32_t* level_T, int num_levels, int batch, int rows,
+                                int ref_dim, int rd1_rows, const int32_t* level_T, int num_levels, int batch, int rows,
                                 int num_heads, int head_dim, int num_point, float* samples, float* save_loc,
                                 void* stream);
 /* grad_value ACCUMULATED (atomic adds; zero it before the first call); grad_offsets (R, off_stride):
  * only the offset columns are written; grad_ref (R,L,ref_dim) or NULL. */
 int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* value_pad_mask, const int32_t* row_video,
                                  const float* offsets, int off_stride, int off_col0, const float* ref,
-                                 int ref_dim, const int32_t* level_T, int num_levels, int batch, int rows,
+                                 int ref_dim, int rd1_rows, const int32_t* level_T, int num_levels, int batch, int rows,
                                  int num_heads, int head_dim, int num_point, const float* save_loc,
                                  const float* grad_samples, float* grad_value, float* grad_offsets,
                                  float* grad_ref, void* stream);
