@@ -1,0 +1,122 @@
+"""Data-parallel training over RCCL (torch.distributed backend 'nccl' on ROCm) -- new functionality: the
+reference trains PDVC on one device only (train.py never wraps the model).
+
+Videos shard naturally: every rank runs its own videos through the whole step and the only exchange is the
+gradient average.  GradAllReducer packs gradients into ~bucket_mb flat buckets in reverse registration order
+(roughly the order backward produces them) and launches each bucket's all-reduce as soon as its last
+gradient is accumulated, so communication overlaps the rest of the backward pass; buckets are launched
+strictly in index order so every rank issues the same collective sequence.  Parameters that never receive a
+gradient (8 in PDVC: transformer.pos_trans*, and the caption head's unused attention_weights/output_proj,
+SURVEY.md section 8(e)) are detected on the first step and excluded, keeping `grad is None` as in the
+reference.  Semantics: after finish(), every gradient is the mean over ranks.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def init_distributed(backend=None):
+    """Initialise from torchrun's env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).  Returns
+    (rank, world_size, local_rank); world_size 1 without initialisation when not launched distributed."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend, init_method="env://")
+    return rank, world, local
+
+
+def broadcast_parameters(module, src=0):
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        with torch.no_grad():
+            for t in list(module.parameters()) + list(module.buffers()):
+                dist.broadcast(t.data, src)
+
+
+class GradAllReducer:
+    def __init__(self, params, bucket_mb=25.0, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        seen, uniq = set(), []
+        for p in params:
+            if p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                uniq.append(p)
+        self.params = uniq
+        self.bucket_bytes = int(bucket_mb * 1024 * 1024)
+        self.active = None  # params known to receive gradients (set after the first step)
+        self._hooks = []
+        self._build(self.params)
+
+    # ------------------------------------------------------------------------------------------------
+    def _build(self, params):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        self.buckets, cur, size = [], [], 0
+        for p in reversed(params):
+            nbytes = p.numel() * p.element_size()
+            if cur and size + nbytes > self.bucket_bytes:
+                self.buckets.append(cur)
+                cur, size = [], 0
+            cur.append(p)
+            size += nbytes
+        if cur:
+            self.buckets.append(cur)
+        self.bucket_of = {}
+        for bi, b in enumerate(self.buckets):
+            for p in b:
+                self.bucket_of[id(p)] = bi
+        for p in params:
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        self._reset()
+
+    def _reset(self):
+        self.pending = [len(b) for b in self.buckets]
+        self.next_launch = 0
+        self.works = []  # (bucket index, flat, work)
+
+    def _on_grad(self, p):
+        bi = self.bucket_of.get(id(p))
+        if bi is None:
+            return
+        self.pending[bi] -= 1
+        if self.active is not None:
+            while self.next_launch < len(self.buckets) and self.pending[self.next_launch] == 0:
+                self._launch(self.next_launch)
+                self.next_launch += 1
+
+    def _launch(self, bi):
+        grads = [p.grad for p in self.buckets[bi]]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        work = dist.all_reduce(flat, group=self.group, async_op=True)
+        self.works.append((bi, flat, work))
+
+    def finish(self):
+        """Wait for (and, on the first step, issue) every bucket's all-reduce; average into .grad."""
+        if self.active is None:
+            # first step: learn which params get gradients (identical on every rank), rebuild, reduce now
+            self.active = [p for p in self.params if p.grad is not None]
+            self._build(self.active)
+            self.active = list(self.active)
+            for bi in range(len(self.buckets)):
+                self._launch(bi)
+        else:
+            while self.next_launch < len(self.buckets):
+                self._launch(self.next_launch)
+                self.next_launch += 1
+        inv = 1.0 / self.world
+        for bi, flat, work in self.works:
+            work.wait()
+            flat.mul_(inv)
+            off = 0
+            for p in self.buckets[bi]:
+                n = p.numel()
+                p.grad.copy_(flat[off:off + n].view_as(p.grad))
+                off += n
+        self._reset()

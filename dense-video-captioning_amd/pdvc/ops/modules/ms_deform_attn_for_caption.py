@@ -49,13 +49,15 @@ class MSDeformAttnCap(nn.Module):
         D = self.d_model // self.n_heads
         return (self.n_levels == 4 and self.n_points == 4 and D >= 32 and D <= 512 and _is_power_of_2(D))
 
-    def sample_rows(self, value, pad_mask_u8, row_video, offsets, reference_points, level_T, off_col0=0):
+    def sample_rows(self, value, pad_mask_u8, row_video, offsets, reference_points, level_T, off_col0=0,
+                    rd1_rows=0):
         """value (N,S,d) = value_proj(memory) [hoisted by the caller]; offsets (R, C) with the
-        M*L*P sampling offsets at off_col0; reference_points (R, L, 1|2).  -> (R, M, L*P, D)."""
+        M*L*P sampling offsets at off_col0; reference_points (R, L, 1|2) (with a 2-wide reference the first
+        rd1_rows rows are 1-d references).  -> (R, M, L*P, D)."""
         N, S, _ = value.shape
         M, D = self.n_heads, self.d_model // self.n_heads
         return CapGatherFunction.apply(value.reshape(N, S, M, D), pad_mask_u8, row_video, offsets,
-                                       reference_points, tuple(level_T), off_col0)
+                                       reference_points, tuple(level_T), off_col0, rd1_rows)
 
     def forward(self, query, reference_points, input_flatten, input_spatial_shapes, input_level_start_index,
                 input_padding_mask=None):
