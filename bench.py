@@ -1,0 +1,194 @@
+#!/usr/bin/env python
+"""PDVC training-step throughput on MI355X: videos/sec fwd+bwd (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W --videos-per-gpu B]
+    torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+Workload (BASELINE.json metric config): cfgs/anet_tsp_pdvc.yml with C=768 features, T=512 frames
+(4 levels: 512/256/128/64 -> S=960), Q=100 queries, 2 encoder + 2 decoder layers, vocab 5748, E=4 events of
+13 words per video; synthetic inputs already resident in HBM; random-init weights.
+One step = the reference's training iteration (train.py:181-187) over B videos per GPU: forward, losses,
+backward, RCCL gradient all-reduce (N>1), grad-norm clip (100) and the AdamW step.  Dropout is active.
+Weak scaling: B videos per GPU at every N; value = all ranks' videos / max-over-ranks time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "dense-video-captioning_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--videos-per-gpu", type=int, default=32)
+    p.add_argument("--T", type=int, default=512)
+    p.add_argument("--C", type=int, default=768)
+    p.add_argument("--Q", type=int, default=100)
+    p.add_argument("--events", type=int, default=4)
+    p.add_argument("--words", type=int, default=13)
+    p.add_argument("--cfg", default="cfgs/anet_tsp_pdvc.yml")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
+    p.add_argument("--kernel-report", action="store_true", help="print per-kernel event timings to stderr")
+    return p.parse_args()
+
+
+def build_model(a, device):
+    import opts
+    from pdvc.pdvc import build
+    args = opts.parse_opts(["--cfg_path", a.cfg, "--device", "cuda"], cfg_root=PKG, feature_dim=a.C,
+                           num_queries=a.Q, frame_embedding_num=a.T)
+    model, criterion, _ = build(args)
+    return args, model.to(device), criterion
+
+
+def msda_alg_bytes(meta, kind):
+    """Algorithmic HBM bytes of one MSDA launch, e = 4 (fp32):
+    fwd = N*S*M*D*e + N*Lq*M*L*P*(8+4) + N*Lq*M*D*e;  bwd = 3*N*S*M*D*e + N*Lq*M*D*e + 2*N*Lq*M*L*P*(8+4)."""
+    N, Lq, S, M, D, NS = meta
+    e = 4
+    if kind == "fwd":
+        return N * S * M * D * e + N * Lq * M * NS * 12 + N * Lq * M * D * e
+    return 3 * N * S * M * D * e + N * Lq * M * D * e + 2 * N * Lq * M * NS * 12
+
+
+def cpu_baseline(a, budget_s):
+    """The oracle (a single-threaded C restatement of the reference MSDA op, oracle/msda_oracle.c) timed on
+    this host: MSDA fwd+bwd of the per-video call set (enc_layers x Lq=S + dec_layers x Lq=Q) at T, M=8,
+    D=64, 4 levels x 4 points, zero padding, fp32.  Bounded: whole videos until budget_s is spent."""
+    from oracle import oracle as O
+    T_l = [a.T // (2 ** i) for i in range(4)]
+    S = sum(T_l)
+    M, D, L, P = 8, 64, 4, 4
+    rng = np.random.RandomState(0)
+    loc_fn = lambda Lq: np.stack([rng.uniform(0, 1, (1, Lq, M, L, P)), np.full((1, Lq, M, L, P), 0.5)], -1)
+    shapes = np.stack([np.ones(4, np.int64), np.asarray(T_l, np.int64)], -1)
+    lsi = np.concatenate([[0], np.cumsum(T_l)[:-1]]).astype(np.int64)
+    value = rng.randn(1, S, M, D).astype(np.float32)
+    calls = [S, S, a.Q, a.Q]
+    inputs = []
+    for Lq in calls:
+        at = rng.uniform(size=(1, Lq, M, L, P)).astype(np.float32)
+        inputs.append((loc_fn(Lq).astype(np.float32), at / at.sum((-1, -2), keepdims=True),
+                       rng.randn(1, Lq, M * D).astype(np.float32)))
+    O.msda_forward(value, shapes, lsi, inputs[-1][0], inputs[-1][1])  # load/compile
+    videos, t0 = 0, time.perf_counter()
+    while True:
+        for loc, at, g in inputs:
+            O.msda_forward(value, shapes, lsi, loc, at)
+            O.msda_backward(value, shapes, lsi, loc, at, g)
+        videos += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": videos / el, "unit": "videos/s", "cores": 1, "kind": "port",
+            "sample": f"{videos} video(s) x MSDA fwd+bwd call set (2 x Lq={S} + 2 x Lq={a.Q}), T={a.T}, M=8, D=64, "
+                      f"L=4, P=4, fp32, oracle/msda_oracle.c single thread, {el:.1f} s"}
+
+
+def main():
+    a = parse()
+    from pdvc.distributed import GradAllReducer, broadcast_parameters, init_distributed
+    from pdvc import _native
+    from pdvc.data import synthetic_videos, collate, to_device
+    rank, world, local = init_distributed()
+    if world != a.gpus and rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    device = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(device)
+    torch.manual_seed(0)
+    np.random.seed(0)
+    args, model, criterion = build_model(a, device)
+    model.train()
+    if world > 1:
+        broadcast_parameters(model)
+    params = [p for p in model.parameters() if p.requires_grad]
+    reducer = GradAllReducer(params) if world > 1 else None
+    opt = torch.optim.AdamW(params, lr=args.lr, weight_decay=args.weight_decay)
+    B = a.videos_per_gpu
+    vocab = args.vocab_size + 1
+    dt = to_device(collate(synthetic_videos(B, a.T, a.C, a.events, a.words, vocab, seed=1000 + rank)), device)
+    wd = criterion.weight_dict
+
+    def step():
+        out, loss = model(dt, criterion, "queries")
+        total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
+        opt.zero_grad(set_to_none=True)
+        total.backward()
+        if reducer is not None:
+            reducer.finish()
+        torch.nn.utils.clip_grad_norm_(params, args.grad_clip)
+        opt.step()
+        return total
+
+    for _ in range(a.warmup):
+        step()
+    names = ["pdvc_msda1d_forward_f32", "pdvc_msda1d_backward_f32", "pdvc_cap_gather_forward_f32",
+             "pdvc_cap_gather_backward_f32"]
+    timer = _native.KernelTimer(names)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    _native.TIMER = timer
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    _native.TIMER = None
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([el], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ks = timer.summary()
+    videos = a.steps * B * world
+    result = {
+        "metric": "videos/sec fwd+bwd (PDVC, T=512 C=768 L=4 Q=100) at 1/2/4/8 MI355X",
+        "value": videos / el, "unit": "videos/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": 1000.0 * el / a.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"anet_tsp_pdvc training step (fwd+loss+bwd+allreduce+AdamW): T={a.T} C={a.C} "
+                               f"L=4 Q={a.Q} 2 enc/2 dec layers, E={a.events} events x {a.words} words, "
+                               f"vocab {vocab}, dropout on",
+                   "videos_per_gpu": B, "global_batch": B * world, "seq_len": a.T,
+                   "parallelism": f"dp{world}"},
+    }
+    # roofline: the fused MSDA forward (the gather kernel; algorithmic bytes per launch / avg launch time)
+    kname = "pdvc_msda1d_forward_f32"
+    if kname in ks and ks[kname]["launches"]:
+        k = ks[kname]
+        avg_ms = k["ms"] / k["launches"]
+        avg_bytes = sum(msda_alg_bytes(m, "fwd") for m in k["metas"]) / k["launches"]
+        ach = avg_bytes / (avg_ms * 1e-3) / 1e9
+        result["roofline"] = {"kernel": "msda1d_fwd_kernel (fused MSDeformAttn forward)", "bound": "hbm",
+                              "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                              "traffic": None, "avg_launch_us": avg_ms * 1e3,
+                              "alg_bytes_per_launch": avg_bytes}
+    result["kernels"] = {n: {"launches": v["launches"], "avg_us": 1e3 * v["ms"] / max(v["launches"], 1),
+                             "share_of_step": v["ms"] / (1e3 * el)} for n, v in ks.items()}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(a, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -53,8 +53,39 @@ def lib():
     return _lib
 
 
-def call(name, *args):
-    rc = getattr(lib(), name)(*args)
+class KernelTimer:
+    """Records HIP events around selected C-ABI launches on the launching (current) stream, so a bench can
+    report a kernel's average device duration over its timed region (bench.py's roofline leg)."""
+
+    def __init__(self, names):
+        self.names = set(names)
+        self.records = []
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, e0, e1, meta in self.records:
+            d = out.setdefault(name, {"launches": 0, "ms": 0.0, "metas": []})
+            d["launches"] += 1
+            d["ms"] += e0.elapsed_time(e1)
+            d["metas"].append(meta)
+        return out
+
+
+TIMER = None
+
+
+def call(name, *args, meta=None):
+    t = TIMER
+    if t is not None and name in t.names:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = getattr(lib(), name)(*args)
+        e1.record()
+        t.records.append((name, e0, e1, meta))
+    else:
+        rc = getattr(lib(), name)(*args)
     if rc != 0:
         msg = lib().pdvc_last_error().decode(errors="replace")
         raise NativeError(f"{name} failed ({rc}): {msg}")

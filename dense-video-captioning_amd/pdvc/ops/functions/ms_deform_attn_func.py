@@ -116,7 +116,7 @@ class MSDA1dFunction(Function):
             save_attn = save_loc = None
         _n.call("pdvc_msda1d_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(proj), C, off_base, logit_base,
                 _n.ptr(ref), RD, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(out), _n.ptr(save_attn),
-                _n.ptr(save_loc), _n.stream())
+                _n.ptr(save_loc), _n.stream(), meta=(N, Lq, S, M, D, NUM_SAMPLES))
         if need:
             ctx.save_for_backward(value, pad_mask, proj, ref, save_attn, save_loc)
         ctx.meta = (tuple(level_T), off_base, logit_base)
@@ -137,7 +137,8 @@ class MSDA1dFunction(Function):
         gr = torch.empty_like(ref) if ctx.needs_input_grad[3] else None
         _n.call("pdvc_msda1d_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(ref), RD, _n.ptr(proj), C,
                 off_base, logit_base, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(grad_out), _n.ptr(save_attn),
-                _n.ptr(save_loc), _n.ptr(gv), _n.ptr(gp), _n.ptr(gr), _n.stream())
+                _n.ptr(save_loc), _n.ptr(gv), _n.ptr(gp), _n.ptr(gr), _n.stream(),
+                meta=(N, Lq, S, M, D, NUM_SAMPLES))
         return gv, None, gp, gr, None, None, None
 
 
