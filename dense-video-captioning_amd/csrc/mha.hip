@@ -1,0 +1,263 @@
+// mha.hip -- decoder query self-attention core for MI355X (gfx950).
+//
+// Replaces the attention core of nn.MultiheadAttention as DeformableTransformerDecoderLayer uses it
+// (pdvc/deformable_transformer.py:231,256-258; torch's multi_head_attention_forward with need_weights):
+//   P = softmax(q * sqrt(1/D) . k^T  [+ -inf at padded keys]),  P_d = dropout(P),  O = P_d . v
+// The in/out projections stay GEMMs (hipBLASLt through torch).  PDVC's shape is tiny and latency-bound
+// (Q = 100..300 queries, D = 64, 8 heads per video), so one workgroup owns one (video, head): K and V are
+// staged once in LDS (rows padded to D+1 floats: conflict-free when lanes walk keys), each wave takes whole
+// query rows, a lane owns one key for the scores (exact softmax over <= 5 keys per lane + wave reductions) and
+// one channel for P.V.  No MFMA: the core is ~2.6 MFLOP per head at Q = 100.
+// Backward: phase A (query-major) recomputes P from the saved log-sum-exp, forms dS = P (dP - delta) with
+// delta = dO . O, writes dq, and stages P_d and dS rows in a global workspace; phase B (key-major, same
+// workgroup, after a barrier) forms dK = dS^T q_scaled and dV = P_d^T dO with lanes over channels.
+// Dropout keeps a counter-hash mask of (seed, video, head, query, key) -- regenerated in the backward.
+#include "pdvc_common.h"
+
+namespace pdvc {
+
+constexpr int kHD = 64;      // head dim (PDVC: 512 / 8)
+constexpr int kMaxQ = 300;   // LDS budget: 2 * Q * (D+1) floats + row buffers <= 160 KiB
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+
+__device__ __forceinline__ bool keep_elem(uint64_t seed, uint32_t head_idx, uint32_t q, uint32_t k, uint32_t Q,
+                                          uint32_t thresh) {
+    const uint32_t idx = (head_idx * Q + q) * Q + k;
+    const uint32_t h = mix32(mix32(idx ^ (uint32_t)seed) + (uint32_t)(seed >> 32) * 0x9e3779b9U);
+    return (h >> 8) >= thresh;  // keep with probability 1 - p (24-bit uniform)
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v = fmaxf(v, __shfl_xor(v, d, PDVC_WAVE));
+    return v;
+}
+__device__ __forceinline__ float wave_add(float v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, PDVC_WAVE);
+    return v;
+}
+
+constexpr int kKPL = (kMaxQ + 63) / 64;  // keys per lane
+
+__global__ __launch_bounds__(256) void mha_fwd_kernel(const float* __restrict__ qk, const float* __restrict__ v,
+                                                      const uint8_t* __restrict__ kpm, int Q, int M, float scaling,
+                                                      float p_drop, uint32_t thresh, uint64_t seed,
+                                                      float* __restrict__ out, float* __restrict__ lse) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int E = M * kHD;
+    const int nm = xcd_remap(blockIdx.x, gridDim.x);
+    const int n = nm / M, m = nm - n * M;
+    float* Ks = smem;                      // [Q][65]
+    float* Vs = Ks + Q * (kHD + 1);        // [Q][64]
+    float* Ps = Vs + Q * kHD;              // [4][Q]
+    float* Qrow = Ps + 4 * Q;              // [4][64]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int i = tid; i < Q * kHD; i += 256) {
+        const int r = i >> 6, c = i & 63;
+        Ks[r * (kHD + 1) + c] = qk[((size_t)n * Q + r) * 2 * E + E + m * kHD + c];
+        Vs[r * kHD + c] = v[((size_t)n * Q + r) * E + m * kHD + c];
+    }
+    __syncthreads();
+    const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    float* prow = Ps + w * Q;
+    float* qrow = Qrow + w * kHD;
+    for (int q = w; q < Q; q += 4) {
+        qrow[lane] = qk[((size_t)n * Q + q) * 2 * E + m * kHD + lane] * scaling;
+        __builtin_amdgcn_wave_barrier();
+        float s[kKPL];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < kKPL; ++i) {
+            const int k = lane + 64 * i;
+            s[i] = -INFINITY;
+            if (k < Q) {
+                float acc = 0.f;
+                const float* kr = Ks + k * (kHD + 1);
+#pragma unroll 16
+                for (int d = 0; d < kHD; ++d) acc += qrow[d] * kr[d];
+                s[i] = (kpm && kpm[(size_t)n * Q + k]) ? -INFINITY : acc;
+            }
+            mx = fmaxf(mx, s[i]);
+        }
+        mx = wave_max(mx);
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < kKPL; ++i) {
+            s[i] = (lane + 64 * i < Q) ? expf(s[i] - mx) : 0.f;
+            sum += s[i];
+        }
+        sum = wave_add(sum);
+        const float inv = 1.f / sum;
+#pragma unroll
+        for (int i = 0; i < kKPL; ++i) {
+            const int k = lane + 64 * i;
+            if (k < Q) {
+                float p = s[i] * inv;
+                if (p_drop > 0.f) p = keep_elem(seed, (uint32_t)nm, q, k, Q, thresh) ? p * keep_scale : 0.f;
+                prow[k] = p;
+            }
+        }
+        if (lane == 0) lse[(size_t)nm * Q + q] = mx + logf(sum);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        float o = 0.f;
+        for (int k = 0; k < Q; ++k) o += prow[k] * Vs[k * kHD + lane];
+        out[((size_t)n * Q + q) * E + m * kHD + lane] = o;
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+__global__ __launch_bounds__(256) void mha_bwd_kernel(const float* __restrict__ qk, const float* __restrict__ v,
+                                                      const uint8_t* __restrict__ kpm, const float* __restrict__ out,
+                                                      const float* __restrict__ gout, const float* __restrict__ lse,
+                                                      int Q, int M, float scaling, float p_drop, uint32_t thresh,
+                                                      uint64_t seed, float* __restrict__ ws_p,
+                                                      float* __restrict__ ws_ds, float* __restrict__ dqk,
+                                                      float* __restrict__ dv) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int E = M * kHD;
+    const int nm = xcd_remap(blockIdx.x, gridDim.x);
+    const int n = nm / M, m = nm - n * M;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    float* A = smem;                   // phase A: K [Q][65]; phase B: dO [Q][64]
+    float* B = A + Q * (kHD + 1);      // phase A: V [Q][65]; phase B: q_scaled [Q][64]
+    float* R = B + Q * (kHD + 1);      // [4][Q] per-wave row buffer (dS row)
+    float* Rv = R + 4 * Q;             // [4][64] per-wave q / dO rows
+    float* Ro = Rv + 4 * kHD;          // [4][64]
+    for (int i = tid; i < Q * kHD; i += 256) {
+        const int r = i >> 6, c = i & 63;
+        A[r * (kHD + 1) + c] = qk[((size_t)n * Q + r) * 2 * E + E + m * kHD + c];
+        B[r * (kHD + 1) + c] = v[((size_t)n * Q + r) * E + m * kHD + c];
+    }
+    __syncthreads();
+    const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    float* dsrow = R + w * Q;
+    float* qrow = Rv + w * kHD;
+    float* dorow = Ro + w * kHD;
+    float* wsp = ws_p + (size_t)nm * Q * Q;
+    float* wsd = ws_ds + (size_t)nm * Q * Q;
+    // ---- phase A: query rows ----
+    for (int q = w; q < Q; q += 4) {
+        const size_t orow = ((size_t)n * Q + q) * E + m * kHD;
+        const float go = gout[orow + lane];
+        qrow[lane] = qk[((size_t)n * Q + q) * 2 * E + m * kHD + lane] * scaling;
+        dorow[lane] = go;
+        const float delta = wave_add(go * out[orow + lane]);
+        const float l = lse[(size_t)nm * Q + q];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < kKPL; ++i) {
+            const int k = lane + 64 * i;
+            if (k < Q) {
+                float s = 0.f, dp = 0.f;
+                const float* kr = A + k * (kHD + 1);
+                const float* vr = B + k * (kHD + 1);
+#pragma unroll 16
+                for (int d = 0; d < kHD; ++d) {
+                    s += qrow[d] * kr[d];
+                    dp += dorow[d] * vr[d];
+                }
+                const bool masked = kpm && kpm[(size_t)n * Q + k];
+                const float p = masked ? 0.f : expf(s - l);
+                float z = 1.f;
+                if (p_drop > 0.f) z = keep_elem(seed, (uint32_t)nm, q, k, Q, thresh) ? keep_scale : 0.f;
+                const float ds = p * (dp * z - delta);
+                dsrow[k] = ds;
+                wsp[(size_t)q * Q + k] = p * z;
+                wsd[(size_t)q * Q + k] = ds;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        float dq = 0.f;
+        for (int k = 0; k < Q; ++k) dq += dsrow[k] * A[k * (kHD + 1) + lane];
+        dqk[((size_t)n * Q + q) * 2 * E + m * kHD + lane] = dq * scaling;
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    // ---- phase B: key rows ----
+    for (int i = tid; i < Q * kHD; i += 256) {
+        const int r = i >> 6, c = i & 63;
+        A[r * kHD + c] = gout[((size_t)n * Q + r) * E + m * kHD + c];
+        B[r * kHD + c] = qk[((size_t)n * Q + r) * 2 * E + m * kHD + c] * scaling;
+    }
+    __syncthreads();
+    for (int k = w; k < Q; k += 4) {
+        float gk = 0.f, gv = 0.f;
+#pragma unroll 8
+        for (int q = 0; q < Q; ++q) {
+            const float pd = wsp[(size_t)q * Q + k];
+            const float ds = wsd[(size_t)q * Q + k];
+            gv += pd * A[q * kHD + lane];
+            gk += ds * B[q * kHD + lane];
+        }
+        dqk[((size_t)n * Q + k) * 2 * E + E + m * kHD + lane] = gk;
+        dv[((size_t)n * Q + k) * E + m * kHD + lane] = gv;
+    }
+}
+
+static uint32_t drop_threshold(float p) {
+    double t = (double)p * 16777216.0;
+    if (t < 0) t = 0;
+    if (t > 16777216.0) t = 16777216.0;
+    return (uint32_t)t;
+}
+
+}  // namespace pdvc
+
+using namespace pdvc;
+
+static size_t fwd_lds(int Q) { return sizeof(float) * ((size_t)Q * (kHD + 1) + (size_t)Q * kHD + 4 * Q + 4 * kHD); }
+static size_t bwd_lds(int Q) { return sizeof(float) * (2 * (size_t)Q * (kHD + 1) + 4 * Q + 8 * kHD); }
+
+extern "C" int pdvc_mha_forward_f32(const float* qk, const float* v, const uint8_t* key_padding_mask, int batch,
+                                    int num_query, int num_heads, int head_dim, float dropout_p, uint64_t seed,
+                                    float* out, float* lse, void* stream) {
+    PDVC_CHECK_ARG(head_dim == kHD, "query self-attention kernel needs head_dim %d, got %d", kHD, head_dim);
+    PDVC_CHECK_ARG(num_query > 0 && num_query <= kMaxQ, "num_query must be in [1,%d], got %d", kMaxQ, num_query);
+    PDVC_CHECK_ARG(batch >= 0 && num_heads > 0, "invalid sizes");
+    PDVC_CHECK_ARG(dropout_p >= 0.f && dropout_p < 1.f, "dropout_p must be in [0,1)");
+    const long blocks = (long)batch * num_heads;
+    if (blocks == 0) return PDVC_OK;
+    const float scaling = sqrtf(1.0f / (float)head_dim);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)mha_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)mha_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(mha_fwd_kernel, dim3((unsigned)blocks), dim3(256), fwd_lds(num_query), (hipStream_t)stream, qk,
+                       v, key_padding_mask, num_query, num_heads, scaling, dropout_p, drop_threshold(dropout_p), seed,
+                       out, lse);
+    PDVC_CHECK_LAUNCH("mha_fwd_kernel");
+    return PDVC_OK;
+}
+
+extern "C" int pdvc_mha_backward_f32(const float* qk, const float* v, const uint8_t* key_padding_mask,
+                                     const float* out, const float* grad_out, const float* lse, int batch,
+                                     int num_query, int num_heads, int head_dim, float dropout_p, uint64_t seed,
+                                     float* workspace, float* grad_qk, float* grad_v, void* stream) {
+    PDVC_CHECK_ARG(head_dim == kHD, "query self-attention kernel needs head_dim %d, got %d", kHD, head_dim);
+    PDVC_CHECK_ARG(num_query > 0 && num_query <= kMaxQ, "num_query must be in [1,%d], got %d", kMaxQ, num_query);
+    PDVC_CHECK_ARG(workspace != nullptr, "workspace (2*N*M*Q*Q floats) is required");
+    const long blocks = (long)batch * num_heads;
+    if (blocks == 0) return PDVC_OK;
+    const float scaling = sqrtf(1.0f / (float)head_dim);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)mha_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    float* ws_p = workspace;
+    float* ws_ds = workspace + (size_t)blocks * num_query * num_query;
+    hipLaunchKernelGGL(mha_bwd_kernel, dim3((unsigned)blocks), dim3(256), bwd_lds(num_query), (hipStream_t)stream, qk,
+                       v, key_padding_mask, out, grad_out, lse, num_query, num_heads, scaling, dropout_p,
+                       drop_threshold(dropout_p), seed, ws_p, ws_ds, grad_qk, grad_v);
+    PDVC_CHECK_LAUNCH("mha_bwd_kernel");
+    return PDVC_OK;
+}

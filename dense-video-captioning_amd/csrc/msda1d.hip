@@ -26,7 +26,6 @@ namespace pdvc {
 constexpr int kNS = 16;   // samples per (query, head) = L * P; PDVC: 4 levels x 4 points
 constexpr int kP = 4;     // points per level
 constexpr int kL = 4;     // levels
-constexpr int kTile = 64; // grad_value tile rows per workgroup
 
 struct Levels1d {
     int T[kL];
@@ -260,105 +259,99 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
 }
 
 // -------------------------------------------------------------------------------------------------
-// backward, value side: destination-centric LDS tiles
+// backward, value side: one workgroup per (video, head, level, channel slice), the level's grad_value
+// rows resident in LDS.  Every level receives exactly Lq*P samples per (video, head), so the work per
+// workgroup is balanced by construction; each sample is read once, its two corner rows are accumulated
+// with ds_add_f32, and the level is written back once with plain stores (one writer per element).
+// Lanes: LPS = DC/4 lanes per sample, each owning channels {sub + LPS*k, k < 4} (dword loads coalesced
+// over the LPS lanes; consecutive banks for the LDS adds), 64/LPS samples per wave-pass, 4 passes
+// unrolled so that 16 gradient loads per lane are in flight.
 // -------------------------------------------------------------------------------------------------
-struct TileMap {
-    int prefix[kL + 1];  // tiles before level l (per (video, head))
+struct UnitMap {
+    int nunits;              // units per (video, head)
+    int level[16];
+    int cslice[16];          // channel slice index within the level
+    int csplit[kL];          // slices per level
 };
 
-template <int DMAX>
-__global__ __launch_bounds__(256) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
-                                                                TileMap tm, int Lq, int S, int M, int D,
+template <int DC>
+__global__ __launch_bounds__(512) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
+                                                                UnitMap um, int Lq, int S, int M, int D,
                                                                 const float* __restrict__ gout,
                                                                 const float* __restrict__ save_attn,
                                                                 const float* __restrict__ save_loc,
                                                                 float* __restrict__ grad_value) {
-    __shared__ float acc[kTile * DMAX];
+    extern __shared__ __attribute__((aligned(16))) float acc[];  // [T_l][DC + 1]
+    constexpr int LPS = DC / 4;
+    constexpr int SPP = 64 / LPS;  // samples per wave-pass
+    constexpr int LD = DC + 1;
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
-    const int ntiles = tm.prefix[kL];
+    const int nw = blockDim.x >> 6;
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
-    const int bm = lb / ntiles;
-    const int tile = lb - bm * ntiles;
+    const int bm = lb / um.nunits;
+    const int unit = lb - bm * um.nunits;
     const int b = bm / M, m = bm - b * M;
-    int l = 0;
-#pragma unroll
-    for (int i = 1; i < kL; ++i)
-        if (tile >= tm.prefix[i]) l = i;
-    const int r0 = (tile - tm.prefix[l]) * kTile;
+    const int l = um.level[unit];
+    const int c0 = um.cslice[unit] * DC;
     const int T = lv.T[l], st = lv.start[l];
     const float Tf = (float)T;
-    const int nrows = min(kTile, T - r0);
-    for (int i = threadIdx.x; i < kTile * D; i += blockDim.x) acc[i] = 0.f;
+    for (int i = threadIdx.x; i < T * LD; i += blockDim.x) acc[i] = 0.f;
     __syncthreads();
 
-    const size_t MD = (size_t)M * D;
+    const int sub = lane % LPS;
+    const int slot = lane / LPS;
     const int nsamp = Lq * kP;
-    for (int base = wid * 64; base < nsamp; base += 256) {
-        const int i = base + lane;
-        bool rel = false;
-        int q = 0, x0 = 0;
-        float hw = 0.f, lw = 0.f, a = 0.f;
-        if (i < nsamp) {
-            q = i / kP;
-            const int p = i - q * kP;
-            const size_t si = (((size_t)b * Lq + q) * M + m) * kNS + l * kP + p;
-            const float x = save_loc[si] * Tf - 0.5f;
-            if (x > -1.f && x < Tf) {
-                const float xf = floorf(x);
-                x0 = (int)xf;
-                if (x0 >= r0 - 1 && x0 <= r0 + nrows - 1) {
-                    rel = true;
-                    lw = x - xf;
-                    hw = 1.f - lw;
-                    a = save_attn[si];
+    const size_t MD = (size_t)M * D;
+    const float* gbase = gout + (size_t)b * Lq * MD + (size_t)m * D + c0 + sub;
+    const size_t sbase = ((size_t)b * Lq * M + m) * kNS + l * kP;  // + (q*M)*kNS + p
+    for (int base = wid * SPP * 4; base < nsamp; base += nw * SPP * 4) {
+        float gv[4][4], cw1[4], cw2[4];
+        int r1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = base + u * SPP + slot;
+            r1[u] = -2;
+            cw1[u] = 0.f;
+            cw2[u] = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) gv[u][k] = 0.f;
+            if (i < nsamp) {
+                const int q = i / kP, p = i - q * kP;
+                const size_t si = sbase + (size_t)q * M * kNS + p;
+                const float x = save_loc[si] * Tf - 0.5f;
+                if (x > -1.f && x < Tf) {
+                    const float xf = floorf(x);
+                    const float lw = x - xf;
+                    const float a = save_attn[si];
+                    r1[u] = (int)xf;
+                    cw1[u] = (1.f - lw);
+                    cw2[u] = lw;
+                    const float* gp = gbase + (size_t)q * MD;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) gv[u][k] = gp[LPS * k] * a;  // top_grad * attn (.cuh:116)
                 }
             }
         }
-        unsigned long long bal = __ballot(rel);
-        while (bal) {
-            // pick up to 8 relevant samples (wave-uniform) and keep their 8 gradient-row loads in flight
-            int qs[8], xs[8];
-            float w1[8], w2[8], aa[8];
-            int cnt = 0;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                qs[k] = 0; xs[k] = -2; w1[k] = 0.f; w2[k] = 0.f; aa[k] = 0.f;
-                if (bal) {
-                    const int src = __ffsll((long long)bal) - 1;
-                    bal &= bal - 1;
-                    qs[k] = __builtin_amdgcn_readlane(q, src);
-                    xs[k] = __builtin_amdgcn_readlane(x0, src);
-                    w1[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hw), src));
-                    w2[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lw), src));
-                    aa[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a), src));
-                    cnt = k + 1;
-                }
+        for (int u = 0; u < 4; ++u) {
+            const int x0 = r1[u];
+            if (x0 >= 0) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) atomicAdd(&acc[x0 * LD + sub + LPS * k], cw1[u] * gv[u][k]);
             }
-            for (int c = lane; c < D; c += 64) {
-                float gv[8];
+            if (x0 >= -1 && x0 + 1 <= T - 1) {
 #pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    gv[k] = (k < cnt) ? gout[(((size_t)b * Lq + qs[k]) * M + m) * D + c] : 0.f;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    if (k < cnt) {
-                        const float tgv = gv[k] * aa[k];  // top_grad * attn_weight (.cuh:116)
-                        const int ra = xs[k] - r0, rb = ra + 1;
-                        if (ra >= 0 && xs[k] >= 0) atomicAdd(&acc[ra * D + c], w1[k] * tgv);
-                        if (rb < nrows && xs[k] + 1 <= T - 1) atomicAdd(&acc[rb * D + c], w2[k] * tgv);
-                    }
-                }
+                for (int k = 0; k < 4; ++k) atomicAdd(&acc[(x0 + 1) * LD + sub + LPS * k], cw2[u] * gv[u][k]);
             }
         }
     }
     __syncthreads();
-    // write the tile once; padded rows get zero (masked_fill backward)
     const uint8_t* mrow = vmask ? vmask + (size_t)b * S + st : nullptr;
-    for (int i = threadIdx.x; i < nrows * D; i += blockDim.x) {
-        const int r = i / D, c = i - r * D;
-        const float v = (mrow && mrow[r0 + r]) ? 0.f : acc[i];
-        grad_value[((size_t)b * S + st + r0 + r) * MD + (size_t)m * D + c] = v;
+    for (int i = threadIdx.x; i < T * DC; i += blockDim.x) {
+        const int r = i / DC, c = i - r * DC;
+        const float v = (mrow && mrow[r]) ? 0.f : acc[r * LD + c];
+        grad_value[((size_t)b * S + st + r) * MD + (size_t)m * D + c0 + c] = v;
     }
 }
 
@@ -493,21 +486,62 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
                              grad_ref);
         PDVC_CHECK_LAUNCH("msda1d_bwd_query_kernel");
     }
-    // grad_value: tiles of kTile rows per (video, head, level)
-    TileMap tm;
-    tm.prefix[0] = 0;
-    for (int l = 0; l < kL; ++l) tm.prefix[l + 1] = tm.prefix[l] + (lv.T[l] + kTile - 1) / kTile;
-    const long nblk = (long)batch * num_heads * tm.prefix[kL];
-    if (nblk > 0) {
-        PDVC_CHECK_ARG(nblk < (1L << 31), "too many tiles");
-        if (head_dim <= 64)
-            hipLaunchKernelGGL((msda1d_bwd_value_kernel<64>), dim3((unsigned)nblk), dim3(256), 0, s, value_pad_mask, lv,
-                               tm, num_query, S, num_heads, head_dim, grad_output, save_attn, save_loc, grad_value);
-        else
-            hipLaunchKernelGGL((msda1d_bwd_value_kernel<128>), dim3((unsigned)nblk), dim3(256), 0, s, value_pad_mask,
-                               lv, tm, num_query, S, num_heads, head_dim, grad_output, save_attn, save_loc,
-                               grad_value);
+    // grad_value: one workgroup per (video, head, level, channel slice); a slice keeps <= 64 KiB of LDS
+    UnitMap um;
+    um.nunits = 0;
+    int maxT = 0;
+    for (int l = 0; l < kL; ++l) {
+        int split = 1;
+        while (((long)lv.T[l] * (head_dim / split + 1) * 4 > 64 * 1024 && head_dim / split > 16) ||
+               head_dim / split > 64)
+            split *= 2;
+        if ((long)lv.T[l] * (head_dim / split + 1) * 4 > 160 * 1024)
+            return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "level %d too long for the LDS value-gradient tile", l);
+        um.csplit[l] = split;
+        for (int c = 0; c < split; ++c) {
+            if (um.nunits >= 16) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "too many value-gradient units");
+            um.level[um.nunits] = l;
+            um.cslice[um.nunits] = c;
+            ++um.nunits;
+        }
+        if (lv.T[l] > maxT) maxT = lv.T[l];
+    }
+    // all slices of one launch share one channel width: use the narrowest (largest split)
+    int split = 1;
+    for (int l = 0; l < kL; ++l) split = um.csplit[l] > split ? um.csplit[l] : split;
+    um.nunits = 0;
+    for (int l = 0; l < kL; ++l)
+        for (int c = 0; c < split; ++c) {
+            um.level[um.nunits] = l;
+            um.cslice[um.nunits] = c;
+            ++um.nunits;
+        }
+    const int DC = head_dim / split;
+    const long nblk = (long)batch * num_heads * um.nunits;
+    if (nblk > 0 && num_query > 0) {
+        const size_t lds = sizeof(float) * (size_t)maxT * (DC + 1);
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<16>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<32>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<64>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr = true;
+        }
+#define VALUE_LAUNCH(DCV)                                                                                       \
+    hipLaunchKernelGGL((msda1d_bwd_value_kernel<DCV>), dim3((unsigned)nblk), dim3(512), lds, s, value_pad_mask, \
+                       lv, um, num_query, S, num_heads, head_dim, grad_output, save_attn, save_loc, grad_value)
+        if (DC == 64) VALUE_LAUNCH(64);
+        else if (DC == 32) VALUE_LAUNCH(32);
+        else if (DC == 16) VALUE_LAUNCH(16);
+        else return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "value-gradient slice width %d", DC);
+#undef VALUE_LAUNCH
         PDVC_CHECK_LAUNCH("msda1d_bwd_value_kernel");
+    } else if (nblk > 0) {
+        hipError_t e = hipMemsetAsync(grad_value, 0, sizeof(float) * (size_t)batch * S * num_heads * head_dim, s);
+        if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_value: %s", hipGetErrorString(e));
     }
     return PDVC_OK;
 }

@@ -13,6 +13,7 @@ _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("PDVC_HIP_LIB", os.path.join(_PKG, "lib", "libpdvc_hip.so"))
 
 _vp, _i, _u8p = ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p
+_f, _u64 = ctypes.c_float, ctypes.c_uint64
 
 # name -> argtypes (all return int status)
 SIGNATURES = {
@@ -26,6 +27,8 @@ SIGNATURES = {
     "pdvc_msda1d_backward_f32": [_vp, _u8p, _vp, _i, _vp, _i, _i, _i, _vp] + [_i] * 6 + [_vp] * 7,
     "pdvc_cap_gather_forward_f32": [_vp, _u8p, _vp, _vp, _i, _i, _vp, _i, _i, _vp] + [_i] * 6 + [_vp] * 3,
     "pdvc_cap_gather_backward_f32": [_vp, _u8p, _vp, _vp, _i, _i, _vp, _i, _i, _vp] + [_i] * 6 + [_vp] * 6,
+    "pdvc_mha_forward_f32": [_vp, _vp, _u8p] + [_i] * 4 + [_f, _u64] + [_vp] * 3,
+    "pdvc_mha_backward_f32": [_vp, _vp, _u8p, _vp, _vp, _vp] + [_i] * 4 + [_f, _u64] + [_vp] * 4,
 }
 
 _lib = None

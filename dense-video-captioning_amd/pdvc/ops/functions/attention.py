@@ -1,29 +1,52 @@
-"""Decoder query self-attention core: softmax(Q K^T / sqrt(d) + key_padding) V with dropout on the
-probabilities -- nn.MultiheadAttention's math (torch.nn.functional.multi_head_attention_forward with
-need_weights=True: q scaled by 1/sqrt(d), baddbmm with the -inf padding mask, softmax, dropout, bmm)."""
-import math
-
+"""Decoder query self-attention core on the HIP kernel (pdvc_mha_*): softmax(q*sqrt(1/D) k^T + key padding)
+with dropout on the probabilities, times v -- nn.MultiheadAttention's math as the reference decoder layer
+uses it (pdvc/deformable_transformer.py:256-258; multi_head_attention_forward with need_weights=True)."""
 import torch
-import torch.nn.functional as F
+from torch.autograd import Function
+from torch.autograd.function import once_differentiable
+
+from pdvc import _native as _n
+
+HEAD_DIM = 64
+MAX_QUERIES = 300
+
+
+class QuerySelfAttentionFunction(Function):
+    @staticmethod
+    def forward(ctx, qk, v, kpm_u8, num_heads, dropout_p, seed):
+        qk, v = qk.contiguous(), v.contiguous()
+        N, Q, E2 = qk.shape
+        E = E2 // 2
+        out = torch.empty((N, Q, E), dtype=qk.dtype, device=qk.device)
+        lse = torch.empty((N, num_heads, Q), dtype=qk.dtype, device=qk.device)
+        _n.call("pdvc_mha_forward_f32", _n.ptr(qk), _n.ptr(v), _n.ptr(kpm_u8), N, Q, num_heads, E // num_heads,
+                float(dropout_p), int(seed), _n.ptr(out), _n.ptr(lse), _n.stream(), meta=(N, Q, num_heads))
+        ctx.save_for_backward(qk, v, kpm_u8, out, lse)
+        ctx.meta = (num_heads, float(dropout_p), int(seed))
+        return out
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_out):
+        qk, v, kpm_u8, out, lse = ctx.saved_tensors
+        num_heads, p, seed = ctx.meta
+        grad_out = grad_out.contiguous()
+        N, Q, E2 = qk.shape
+        ws = torch.empty(2 * N * num_heads * Q * Q, dtype=qk.dtype, device=qk.device)
+        gqk = torch.empty_like(qk)
+        gv = torch.empty_like(v)
+        _n.call("pdvc_mha_backward_f32", _n.ptr(qk), _n.ptr(v), _n.ptr(kpm_u8), _n.ptr(out), _n.ptr(grad_out),
+                _n.ptr(lse), N, Q, num_heads, E2 // 2 // num_heads, p, seed, _n.ptr(ws), _n.ptr(gqk), _n.ptr(gv),
+                _n.stream(), meta=(N, Q, num_heads))
+        return gqk, gv, None, None, None, None
 
 
 def query_self_attention(qk, v, key_padding_mask, num_heads, dropout_p):
     """qk (N, Q, 2E) = [q | k] in-projections, v (N, Q, E); key_padding_mask (N, Q) True = ignore."""
     N, Q, E2 = qk.shape
-    E = E2 // 2
-    D = E // num_heads
-    q = qk[..., :E].reshape(N, Q, num_heads, D).transpose(1, 2).reshape(N * num_heads, Q, D)
-    k = qk[..., E:].reshape(N, Q, num_heads, D).transpose(1, 2).reshape(N * num_heads, Q, D)
-    vv = v.reshape(N, Q, num_heads, D).transpose(1, 2).reshape(N * num_heads, Q, D)
-    q = q * math.sqrt(1.0 / float(D))
-    if key_padding_mask is not None:
-        bias = torch.zeros(N, Q, dtype=q.dtype, device=q.device).masked_fill(key_padding_mask, float("-inf"))
-        bias = bias.view(N, 1, 1, Q).expand(-1, num_heads, -1, -1).reshape(N * num_heads, 1, Q)
-        attn = torch.baddbmm(bias, q, k.transpose(-2, -1))
-    else:
-        attn = torch.bmm(q, k.transpose(-2, -1))
-    attn = F.softmax(attn, dim=-1)
-    if dropout_p > 0.0:
-        attn = F.dropout(attn, p=dropout_p)
-    out = torch.bmm(attn, vv)
-    return out.view(N, num_heads, Q, D).transpose(1, 2).reshape(N, Q, E)
+    if E2 // 2 // num_heads != HEAD_DIM or Q > MAX_QUERIES:
+        raise NotImplementedError(f"query self-attention kernel supports head_dim {HEAD_DIM} and <= {MAX_QUERIES} "
+                                  f"queries (got head_dim {E2 // 2 // num_heads}, Q {Q})")
+    kpm = None if key_padding_mask is None else key_padding_mask.contiguous().view(torch.uint8)
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if dropout_p > 0 else 0
+    return QuerySelfAttentionFunction.apply(qk, v, kpm, num_heads, dropout_p, seed)

@@ -140,6 +140,21 @@ int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* value_pad_ma
                                  const float* grad_samples, float* grad_value, float* grad_offsets,
                                  float* grad_ref, void* stream);
 
+/* ---- decoder query self-attention core (nn.MultiheadAttention, batch-first) -------------------------
+ * qk (N,Q,2E) = [q | k] in-projections (E = num_heads*head_dim), v (N,Q,E); key_padding_mask (N,Q) uint8,
+ * 1 = ignored key, may be NULL.  out (N,Q,E) = softmax(q*sqrt(1/D) k^T + mask) [dropout] v per head;
+ * lse (N,M,Q) log-sum-exp of each score row (saved for the backward).  Dropout keeps a deterministic
+ * counter-hash mask of (seed, video, head, query, key), regenerated by the backward.  head_dim must be 64,
+ * Q <= 300. */
+int pdvc_mha_forward_f32(const float* qk, const float* v, const uint8_t* key_padding_mask, int batch, int num_query,
+                         int num_heads, int head_dim, float dropout_p, uint64_t seed, float* out, float* lse,
+                         void* stream);
+/* workspace: 2*N*M*Q*Q floats.  grad_qk (N,Q,2E) and grad_v (N,Q,E) are fully written. */
+int pdvc_mha_backward_f32(const float* qk, const float* v, const uint8_t* key_padding_mask, const float* out,
+                          const float* grad_out, const float* lse, int batch, int num_query, int num_heads,
+                          int head_dim, float dropout_p, uint64_t seed, float* workspace, float* grad_qk,
+                          float* grad_v, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,201 @@
+"""GPU parity of the module-level hot path against golden vectors from the reference modules:
+DeformableTransformerEncoderLayer / DecoderLayer (MSDA + query self-attention kernels) and the
+LSTM-DSA caption head (teacher-forced captioning logits, loss, gradients, greedy decoding); plus the
+query self-attention kernel against a float64 torch restatement of nn.MultiheadAttention's core."""
+import math
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+G = os.path.join(HERE, "golden")
+sys.path.insert(0, G)
+DEV = "cuda"
+
+
+def load(name):
+    return np.load(os.path.join(G, name + ".npz"), allow_pickle=False)
+
+
+def cu(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    return (t.to(dtype) if dtype is not None else t).to(DEV)
+
+
+def close(a, b, tol, what):
+    a = a.detach().double().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    assert a.shape == b.shape, f"{what}: {a.shape} vs {b.shape}"
+    err = np.abs(a - b).max() if a.size else 0.0
+    scale = max(1.0, np.abs(b).max() if b.size else 1.0)
+    assert err <= tol * scale, f"{what}: max|diff| {err:.3e} > {tol:.0e} * {scale:.3g}"
+
+
+def fill(module):
+    import weights as W
+    W.fill_module(module, overrides={"sampling_offsets": 0.5})
+
+
+# ------------------------------------------------------------------------------------------------
+# query self-attention kernel
+# ------------------------------------------------------------------------------------------------
+def torch_mha_core(qk, v, kpm, M):
+    N, Q, E2 = qk.shape
+    E = E2 // 2
+    D = E // M
+    q = qk[..., :E].reshape(N, Q, M, D).transpose(1, 2)
+    k = qk[..., E:].reshape(N, Q, M, D).transpose(1, 2)
+    vv = v.reshape(N, Q, M, D).transpose(1, 2)
+    s = (q * math.sqrt(1.0 / D)) @ k.transpose(-1, -2)
+    if kpm is not None:
+        s = s.masked_fill(kpm[:, None, None, :], float("-inf"))
+    p = torch.softmax(s, -1)
+    return (p @ vv).transpose(1, 2).reshape(N, Q, E), p
+
+
+@pytest.mark.parametrize("Q,masked", [(100, False), (100, True), (37, True), (300, False)])
+def test_query_self_attention_vs_float64(Q, masked):
+    from pdvc.ops.functions.attention import query_self_attention
+    torch.manual_seed(Q)
+    N, M, E = 3, 8, 512
+    qk = torch.randn(N, Q, 2 * E, device=DEV)
+    v = torch.randn(N, Q, E, device=DEV)
+    kpm = None
+    if masked:
+        kpm = torch.zeros(N, Q, dtype=torch.bool, device=DEV)
+        kpm[1, -5:] = True
+        kpm[2, :3] = True
+    g = torch.randn(N, Q, E, device=DEV)
+    a, b = qk.clone().requires_grad_(), v.clone().requires_grad_()
+    out = query_self_attention(a, b, kpm, M, 0.0)
+    out.backward(g)
+    a64, b64 = qk.double().requires_grad_(), v.double().requires_grad_()
+    ref, _ = torch_mha_core(a64, b64, kpm, M)
+    ref.backward(g.double())
+    close(out, ref, 1e-5, "out")
+    close(a.grad, a64.grad, 1e-4, "grad_qk")
+    close(b.grad, b64.grad, 1e-4, "grad_v")
+
+
+def test_query_self_attention_dropout_consistent():
+    """With dropout the kernel's mask is recovered from its own output (v = one-hot keys); the forward
+    equals P_d.v and the backward equals autograd of that expression with the same mask."""
+    from pdvc.ops.functions.attention import QuerySelfAttentionFunction
+    torch.manual_seed(0)
+    N, M, E, Q, p = 2, 8, 512, 64, 0.25
+    qk = torch.randn(N, Q, 2 * E, device=DEV)
+    onehot = torch.eye(Q, device=DEV)[None, :, None, :].expand(N, Q, M, 64).reshape(N, Q, E).contiguous()
+    pd = QuerySelfAttentionFunction.apply(qk, onehot, None, M, p, 1234)  # rows of P_d per head
+    pd = pd.view(N, Q, M, Q).transpose(1, 2)  # (N, M, Q, Q)
+    _, P = torch_mha_core(qk.double(), onehot.double(), None, M)
+    kept = pd > 0
+    frac = kept.float().mean().item()
+    assert abs(frac - (1 - p)) < 0.03, frac
+    Z = kept.double() / (1 - p)
+    close(pd, P * Z, 1e-5, "P_d")
+    v = torch.randn(N, Q, E, device=DEV)
+    g = torch.randn(N, Q, E, device=DEV)
+    a, b = qk.clone().requires_grad_(), v.clone().requires_grad_()
+    out = QuerySelfAttentionFunction.apply(a, b, None, M, p, 1234)
+    out.backward(g)
+    a64, b64 = qk.double().requires_grad_(), v.double().requires_grad_()
+    _, P64 = torch_mha_core(a64, b64, None, M)
+    ref = (P64 * Z) @ b64.view(N, Q, M, 64).transpose(1, 2)
+    ref = ref.transpose(1, 2).reshape(N, Q, E)
+    ref.backward(g.double())
+    close(out, ref, 1e-5, "out")
+    close(a.grad, a64.grad, 1e-4, "grad_qk")
+    close(b.grad, b64.grad, 1e-4, "grad_v")
+
+
+# ------------------------------------------------------------------------------------------------
+# transformer layers vs the reference layers (tests/golden/make_golden.py::module_layers)
+# ------------------------------------------------------------------------------------------------
+def test_decoder_layer_vs_golden():
+    from pdvc.deformable_transformer import DeformableTransformerDecoderLayer
+    d = load("module_decoder_layer")
+    layer = DeformableTransformerDecoderLayer(64, 48, 0.0, "relu", 4, 4, 4).to(DEV)
+    fill(layer)
+    T_l = tuple(int(t) for t in d["T_l"])
+    tgt, pos, ref, src = (cu(d[k]).requires_grad_() for k in ("tgt", "query_pos", "ref", "src"))
+    lsi = torch.tensor([0, 16, 24, 28], device=DEV)
+    # the reference layer hands self_attn's key_padding_mask = ~query_mask (deformable_transformer.py:257)
+    out = layer(tgt, pos, ref, src, T_l, lsi, cu(d["pad"]), cu(d["query_mask"]))
+    close(out, d["out"], 1e-4, "out")
+    out.backward(cu(d["grad_out"]))
+    for k, t in (("grad_tgt", tgt), ("grad_query_pos", pos), ("grad_ref", ref), ("grad_src", src)):
+        close(t.grad, d[k], 1e-4, k)
+    for n, p in layer.named_parameters():
+        close(p.grad, d["grad." + n], 1e-4, n)
+
+
+def test_decoder_layer_parameters_named_like_nn_multiheadattention():
+    from pdvc.deformable_transformer import DeformableTransformerDecoderLayer
+    names = [n for n, _ in DeformableTransformerDecoderLayer(64, 48, 0.0, "relu", 4, 4, 4).named_parameters()]
+    assert "self_attn.in_proj_weight" in names and "self_attn.out_proj.weight" in names
+
+
+def test_encoder_layer_vs_golden():
+    from pdvc.deformable_transformer import DeformableTransformerEncoderLayer
+    d = load("module_encoder_layer")
+    layer = DeformableTransformerEncoderLayer(64, 48, 0.0, "relu", 4, 4, 4).to(DEV)
+    fill(layer)
+    T_l = tuple(int(t) for t in d["T_l"])
+    src, pos = cu(d["src"]).requires_grad_(), cu(d["pos"]).requires_grad_()
+    lsi = torch.tensor([0, 16, 24, 28], device=DEV)
+    out = layer(src, pos, cu(d["ref"]), T_l, lsi, cu(d["pad"]))
+    close(out, d["out"], 1e-4, "out")
+    out.backward(cu(d["grad_out"]))
+    close(src.grad, d["grad_src"], 1e-4, "grad_src")
+    close(pos.grad, d["grad_pos"], 1e-4, "grad_pos")
+    for n, p in layer.named_parameters():
+        close(p.grad, d["grad." + n], 1e-4, n)
+
+
+# ------------------------------------------------------------------------------------------------
+# caption head vs the reference LSTM_DSA (make_golden.py::module_captioner)
+# ------------------------------------------------------------------------------------------------
+def small_opt():
+    import types
+    return types.SimpleNamespace(
+        vocab_size=23, input_encoding_size=32, rnn_size=64, num_layers=1, drop_prob=0.0, max_caption_len=6,
+        clip_context_dim=64, cap_nheads=1, att_hid_size=48, wordRNN_input_feats_type="C", hidden_dim=64,
+        cap_num_feature_levels=4, cap_dec_n_points=4, num_feature_levels=4, event_context_dim=None)
+
+
+@pytest.mark.parametrize("ref_dim", [1, 2])
+def test_captioner_vs_golden(ref_dim):
+    from pdvc.CaptioningHead.LSTM_DSA import LSTMDSACaptioner
+    d = load(f"module_captioner_ref{ref_dim}")
+    cap = LSTMDSACaptioner(small_opt()).to(DEV)
+    fill(cap)
+    cap.train()
+    T_l = tuple(int(t) for t in d["T_l"])
+    hs, ref, mem = (cu(d[k]).requires_grad_() for k in ("hs", "ref", "memory"))
+    others = {"memory": mem, "mask_flatten": cu(d["mask"]), "spatial_shapes": torch.tensor(T_l, device=DEV),
+              "level_T": T_l, "valid_ratios": torch.ones(1, 4, device=DEV)}
+    cap_tensor = cu(d["cap_tensor"])
+    logprobs = cap(hs, ref, others, cap_tensor)
+    close(logprobs, d["logprobs"], 1e-4, "captioning logits (log_softmax)")
+    loss = cap.build_loss(logprobs, cap_tensor[:, 1:], cu(d["cap_mask"])[:, 1:].float()).mean()
+    close(loss, d["loss"], 1e-4, "loss")
+    loss.backward()
+    close(hs.grad, d["grad_hs"], 1e-4, "grad_hs")
+    close(ref.grad, d["grad_ref"], 1e-4, "grad_ref")
+    close(mem.grad, d["grad_memory"], 1e-4, "grad_memory")
+    for n, p in cap.named_parameters():
+        key = "grad." + n
+        if d[key].size == 0:
+            assert p.grad is None, f"{n} must get no gradient"
+        else:
+            close(p.grad, d[key], 1e-4, n)
+    cap.eval()
+    with torch.no_grad():
+        seq, lp = cap.sample(hs.detach(), ref.detach(), {k: (v.detach() if isinstance(v, torch.Tensor) else v)
+                                                         for k, v in others.items()})
+    assert seq.cpu().tolist() == d["sample_seq"].tolist()
+    close(lp, d["sample_logprobs"], 1e-4, "greedy logprobs")
