@@ -5,11 +5,13 @@ mean over videos of the per-video values (each video normalised by its own event
 reference's batch-size-1 training does); gradients are therefore the average of N batch-1 gradients.
 All decoder layers' matchings are solved after ONE device->host copy (the reference syncs once per layer).
 """
+import numpy as np
 import torch
 import torch.nn.functional as F
 from torch import nn
 
 from . import box_ops
+from .matcher import padded_targets
 
 COUNTER_CLASS_RATE = [0.00000000e+00, 0.00000000e+00, 1.93425917e-01, 4.12129084e-01, 1.88929963e-01,
                       7.81296833e-02, 5.09541413e-02, 3.12718553e-02, 1.84833650e-02, 8.39244680e-03,
@@ -56,17 +58,25 @@ class SetCriterion(nn.Module):
         self.counter_class_rate = torch.tensor(COUNTER_CLASS_RATE)
 
     # -------------------------------------------------------------------------------------------------
-    def layer_losses(self, outputs, targets, indices):
-        """Per-video losses of one decoder layer, averaged over the batch.  outputs: pred_logits (N,Q,C),
-        pred_boxes (N,Q,2), pred_count (N,K+1); indices: list of (query ids, target ids) per video."""
+    def layer_losses(self, outputs, pt, indices):
+        """Per-video losses of one decoder layer, averaged over the batch, computed for all videos at once.
+        outputs: pred_logits (N,Q,C), pred_boxes (N,Q,2), pred_count (N,K+1); pt: padded targets;
+        indices: list of (query ids, target ids) per video."""
         logits, boxes, count = outputs["pred_logits"], outputs["pred_boxes"], outputs["pred_count"]
         N, Q, C = logits.shape
         dev = logits.device
-        nb = torch.tensor([max(float(len(t["labels"])), 1.0) for t in targets], device=dev)  # clamp(min=1)
+        sizes = pt["sizes"]
+        nb = torch.tensor([max(float(e), 1.0) for e in sizes], device=dev)  # num_boxes clamp(min=1)
+        # matched pairs of every video, flattened: (video, query, target slot) -- one host->device copy
+        vid = np.concatenate([np.full(len(i), v, np.int64) for v, (i, _) in enumerate(indices)])
+        qid = np.concatenate([i.numpy() for i, _ in indices])
+        tid = np.concatenate([j.numpy() for _, j in indices])
+        rank = np.concatenate([np.arange(len(i)) for i, _ in indices])
+        pairs = torch.from_numpy(np.stack([vid, qid, tid, rank])).to(dev, non_blocking=True)
+        pv, pq, pt_, pr = pairs[0], pairs[1], pairs[2], pairs[3]
         # labels: focal loss over every query and class (criterion.py:46-65)
         tclass = torch.full((N, Q), self.num_classes, dtype=torch.int64, device=dev)
-        for v, ((qi, ti), t) in enumerate(zip(indices, targets)):
-            tclass[v, qi.to(dev)] = t["labels"][ti.to(t["labels"].device)].to(dev)
+        tclass[pv, pq] = pt["labels"][pv, pt_]
         onehot = torch.zeros((N, Q, C + 1), dtype=logits.dtype, device=dev)
         onehot.scatter_(2, tclass.unsqueeze(-1), 1)
         onehot = onehot[:, :, :-1]
@@ -74,51 +84,51 @@ class SetCriterion(nn.Module):
         loss_ce = focal.mean(1).sum(1) / nb * Q
         # counter (criterion.py:67-76)
         max_length = count.shape[1] - 1
-        ctgt = torch.tensor([min(len(t["boxes"]), max_length) for t in targets], device=dev, dtype=torch.long)
+        ctgt = torch.tensor([min(e, max_length) for e in sizes], device=dev, dtype=torch.long)
         ctgt_onehot = torch.zeros_like(count)
         ctgt_onehot.scatter_(1, ctgt.unsqueeze(-1), 1)
         weight = self.counter_class_rate[:max_length + 1].to(dev)
         loss_counter = counter_loss_terms(count, ctgt_onehot, self.opt.lloss_gau_mask, self.opt.lloss_beta, weight)
         # cardinality (logging only, criterion.py:80-92)
         card_pred = (logits.argmax(-1) != C - 1).sum(1).float()
-        tlen = torch.tensor([float(len(t["labels"])) for t in targets], device=dev)
-        card_err = (card_pred - tlen).abs()
-        # boxes (criterion.py:94-123), per video
-        lb, lg, ls = [], [], []
-        for v, ((qi, ti), t) in enumerate(zip(indices, targets)):
-            src = boxes[v, qi.to(dev)]
-            tgt = t["boxes"][ti.to(t["boxes"].device)].to(dev)
-            lb.append(F.l1_loss(src, tgt, reduction="none").sum() / nb[v])
-            sxy, txy = box_ops.box_cl_to_xy(src), box_ops.box_cl_to_xy(tgt)
-            lg.append((1 - torch.diag(box_ops.generalized_box_iou(sxy, txy))).sum() / nb[v])
-            n = len(qi)
-            self_iou = torch.triu(box_ops.box_iou(sxy, sxy)[0], diagonal=1)
-            ls.append(self_iou.sum() / (0.5 * n * (n - 1)))
-        return {"loss_ce": loss_ce.mean(), "loss_counter": loss_counter.mean(),
-                "loss_bbox": torch.stack(lb).mean(), "loss_giou": torch.stack(lg).mean(),
-                "loss_self_iou": torch.stack(ls).mean(), "cardinality_error": card_err.mean()}
+        card_err = (card_pred - torch.tensor([float(e) for e in sizes], device=dev)).abs()
+        # boxes (criterion.py:94-123): L1 and GIoU of matched pairs, per-video sums via index_add
+        src = boxes[pv, pq]
+        tgt = pt["boxes"][pv, pt_]
+        l1 = F.l1_loss(src, tgt, reduction="none").sum(1)
+        sxy, txy = box_ops.box_cl_to_xy(src), box_ops.box_cl_to_xy(tgt)
+        giou = box_ops.generalized_box_iou(sxy[:, None], txy[:, None])[:, 0, 0]
+        loss_bbox = torch.zeros(N, device=dev, dtype=l1.dtype).index_add_(0, pv, l1) / nb
+        loss_giou = torch.zeros(N, device=dev, dtype=l1.dtype).index_add_(0, pv, 1 - giou) / nb
+        # self-IoU among each video's matched predictions, upper triangle, / (n(n-1)/2)
+        emax = max(len(i) for i, _ in indices) if indices else 0
+        padded = torch.zeros(N, max(emax, 1), 2, device=dev, dtype=sxy.dtype)
+        padded[pv, pr] = sxy
+        valid = torch.zeros(N, max(emax, 1), dtype=torch.bool, device=dev)
+        valid[pv, pr] = True
+        iou = box_ops.box_iou(padded, padded)[0]
+        iou = torch.triu(iou, diagonal=1) * (valid[:, :, None] & valid[:, None, :])
+        n = torch.tensor([float(len(i)) for i, _ in indices], device=dev)
+        loss_self_iou = iou.sum((1, 2)) / (0.5 * n * (n - 1))
+        return {"loss_ce": loss_ce.mean(), "loss_counter": loss_counter.mean(), "loss_bbox": loss_bbox.mean(),
+                "loss_giou": loss_giou.mean(), "loss_self_iou": loss_self_iou.mean(),
+                "cardinality_error": card_err.mean()}
 
-    def forward(self, outputs, targets):
+    def forward(self, outputs, targets, padded=None):
         """Reference contract: returns (losses, last_indices[, aux_indices]); indices are
-        (list of per-video (query ids, target ids), None)."""
+        (list of per-video (query ids, target ids), None).  `padded` may carry padded_targets(targets)."""
+        pt = padded if padded is not None else padded_targets(targets, outputs["pred_logits"].device)
         layers = [outputs] + list(outputs.get("aux_outputs", []))
-        blocks, per_layer = [], []
-        for o in layers:
-            b = self.matcher.cost_blocks(o["pred_logits"], o["pred_boxes"], targets)
-            per_layer.append(len(b))
-            blocks.extend(b)
-        solved, _ = self.matcher.solve(blocks)
-        idx, off = [], 0
-        for n in per_layer:
-            idx.append((solved[off:off + n], None))
-            off += n
+        costs = [self.matcher.cost_padded(o["pred_logits"], o["pred_boxes"], pt) for o in layers]
+        solved = self.matcher.solve_padded(costs, pt["sizes"])
+        idx = [(s, None) for s in solved]
         last_indices = idx[0]
         outputs["matched_indices"] = last_indices
-        losses = self.layer_losses(outputs, targets, last_indices[0])
+        losses = self.layer_losses(outputs, pt, last_indices[0])
         if "aux_outputs" in outputs:
             aux_indices = idx[1:]
             for i, aux in enumerate(outputs["aux_outputs"]):
-                l_dict = self.layer_losses(aux, targets, aux_indices[i][0])
+                l_dict = self.layer_losses(aux, pt, aux_indices[i][0])
                 losses.update({k + f"_{i}": v for k, v in l_dict.items()})
             return losses, last_indices, aux_indices
         return losses, last_indices

@@ -80,4 +80,6 @@ def to_device(dt, device):
         else:
             out[k] = v
     out["cap_tensor_cpu"] = dt["cap_tensor"].clone()
+    from .matcher import padded_targets
+    out["video_target_padded"] = padded_targets(out["video_target"], device)
     return out

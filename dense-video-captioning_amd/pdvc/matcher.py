@@ -26,22 +26,41 @@ class HungarianMatcher(nn.Module):
     @torch.no_grad()
     def cost_blocks(self, pred_logits, pred_boxes, targets):
         """Per-video cost matrices (Q, E_v) as a list of device tensors (matcher.py:87-121)."""
+        C = self.cost_padded(pred_logits, pred_boxes, padded_targets(targets, pred_boxes.device))
+        return [C[v, :, :len(t["labels"])] for v, t in enumerate(targets)]
+
+    @torch.no_grad()
+    def cost_padded(self, pred_logits, pred_boxes, pt):
+        """All videos at once: (N, Q, Emax) cost with targets padded to Emax (padding columns are junk and
+        are sliced away by the caller).  Elementwise the same operations as the reference's flat cost."""
         out_prob = pred_logits.sigmoid()  # (N, Q, C)
         alpha, gamma = self.cost_alpha, self.cost_gamma
         neg = (1 - alpha) * (out_prob ** gamma) * (-(1 - out_prob + 1e-8).log())
         pos = alpha * ((1 - out_prob) ** gamma) * (-(out_prob + 1e-8).log())
-        blocks = []
-        for v, t in enumerate(targets):
-            ids, tb = t["labels"], t["boxes"]
-            c_class = pos[v][:, ids] - neg[v][:, ids]
-            c_bbox = torch.cdist(pred_boxes[v], tb, p=1)
-            c_giou = -generalized_box_iou(box_cl_to_xy(pred_boxes[v]), box_cl_to_xy(tb))
-            blocks.append(self.cost_bbox * c_bbox + self.cost_class * c_class + self.cost_giou * c_giou)
-        return blocks
+        N, Q, _ = out_prob.shape
+        ids = pt["labels"][:, None, :].expand(N, Q, pt["labels"].shape[1])
+        c_class = pos.gather(2, ids) - neg.gather(2, ids)
+        c_bbox = torch.cdist(pred_boxes, pt["boxes"], p=1)
+        c_giou = -generalized_box_iou(box_cl_to_xy(pred_boxes), box_cl_to_xy(pt["boxes"]))
+        return self.cost_bbox * c_bbox + self.cost_class * c_class + self.cost_giou * c_giou
 
     @torch.no_grad()
     def forward(self, outputs, targets):
         return self.solve(self.cost_blocks(outputs["pred_logits"], outputs["pred_boxes"], targets))
+
+    @staticmethod
+    def solve_padded(costs, sizes):
+        """costs: list of (N, Q, Emax) device tensors (one per decoder layer) -> per layer, per video
+        (query ids, target ids); ONE device->host copy for everything."""
+        flat = torch.stack(costs).cpu().numpy()  # (Ld, N, Q, Emax)
+        out = []
+        for layer in flat:
+            res = []
+            for v, e in enumerate(sizes):
+                i, j = linear_sum_assignment(layer[v, :, :e])
+                res.append((torch.as_tensor(i, dtype=torch.int64), torch.as_tensor(j, dtype=torch.int64)))
+            out.append(res)
+        return out
 
     @staticmethod
     def solve(blocks):
@@ -55,6 +74,24 @@ class HungarianMatcher(nn.Module):
             i, j = linear_sum_assignment(c)
             out.append((torch.as_tensor(i, dtype=torch.int64), torch.as_tensor(j, dtype=torch.int64)))
         return out, None
+
+
+def padded_targets(targets, device):
+    """Targets of a batch padded to the largest event count: labels (N, Emax) long, boxes (N, Emax, 2)
+    (padding boxes are a harmless (0.5, 0.5) segment), valid (N, Emax) bool, sizes [E_v]."""
+    sizes = [len(t["labels"]) for t in targets]
+    emax = max(max(sizes), 1)
+    N = len(targets)
+    labels = torch.zeros(N, emax, dtype=torch.long, device=device)
+    boxes = torch.full((N, emax, 2), 0.5, device=device)
+    valid = torch.zeros(N, emax, dtype=torch.bool, device=device)
+    for v, t in enumerate(targets):
+        e = sizes[v]
+        if e:
+            labels[v, :e] = t["labels"].to(device)
+            boxes[v, :e] = t["boxes"].to(device)
+            valid[v, :e] = True
+    return {"labels": labels, "boxes": boxes, "valid": valid, "sizes": sizes}
 
 
 def build_matcher(args):

@@ -202,7 +202,7 @@ class PDVC(nn.Module):
         out = self._pack(classes, counts, coords, [zero_probs] * len(classes), [zero_seq] * len(classes))
         if not self.aux_loss:
             raise NotImplementedError("aux_loss=False is not supported")
-        loss, last_indices, aux_indices = criterion(out, dt["video_target"])
+        loss, last_indices, aux_indices = criterion(out, dt["video_target"], dt.get("video_target_padded"))
         Ld = hs.shape[0]
         layer_indices = [aux_indices[l][0] for l in range(Ld - 1)] + [last_indices[0]]
         R = self._caption_rows(dt, hs, init_reference, inter_references, others, layer_indices)
@@ -268,7 +268,7 @@ class PDVC(nn.Module):
                 probs.append({"cap_prob_eval": lp.reshape(N, Q, -1)})
                 seqs.append(seq.reshape(N, Q, -1))
         out = self._pack(classes, counts, coords, probs, seqs)
-        loss, last_indices, aux_indices = criterion(out, dt["video_target"])
+        loss, last_indices, aux_indices = criterion(out, dt["video_target"], dt.get("video_target_padded"))
         return out, loss
 
 

@@ -28,7 +28,7 @@ def cu(a, dtype=None):
 
 def close(a, b, tol, what):
     a = a.detach().double().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a, np.float64)
-    b = np.asarray(b, np.float64)
+    b = b.detach().double().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b, np.float64)
     assert a.shape == b.shape, f"{what}: {a.shape} vs {b.shape}"
     err = np.abs(a - b).max() if a.size else 0.0
     scale = max(1.0, np.abs(b).max() if b.size else 1.0)
