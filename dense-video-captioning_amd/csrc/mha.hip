@@ -16,7 +16,7 @@
 
 namespace pdvc {
 
-constexpr int kHD = 64;      // head dim (PDVC: 512 / 8)
+constexpr int kHD = 64;      // max head dim (PDVC: 512 / 8 = 64); lanes >= D idle in channel phases
 constexpr int kMaxQ = 300;   // LDS budget: 2 * Q * (D+1) floats + row buffers <= 160 KiB
 
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
@@ -45,29 +45,29 @@ __device__ __forceinline__ float wave_add(float v) {
 constexpr int kKPL = (kMaxQ + 63) / 64;  // keys per lane
 
 __global__ __launch_bounds__(256) void mha_fwd_kernel(const float* __restrict__ qk, const float* __restrict__ v,
-                                                      const uint8_t* __restrict__ kpm, int Q, int M, float scaling,
+                                                      const uint8_t* __restrict__ kpm, int Q, int M, int D, float scaling,
                                                       float p_drop, uint32_t thresh, uint64_t seed,
                                                       float* __restrict__ out, float* __restrict__ lse) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int E = M * kHD;
+    const int E = M * D;
     const int nm = xcd_remap(blockIdx.x, gridDim.x);
     const int n = nm / M, m = nm - n * M;
-    float* Ks = smem;                      // [Q][65]
-    float* Vs = Ks + Q * (kHD + 1);        // [Q][64]
-    float* Ps = Vs + Q * kHD;              // [4][Q]
+    float* Ks = smem;                      // [Q][D+1]
+    float* Vs = Ks + Q * (D + 1);          // [Q][D]
+    float* Ps = Vs + Q * D;                // [4][Q]
     float* Qrow = Ps + 4 * Q;              // [4][64]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (int i = tid; i < Q * kHD; i += 256) {
-        const int r = i >> 6, c = i & 63;
-        Ks[r * (kHD + 1) + c] = qk[((size_t)n * Q + r) * 2 * E + E + m * kHD + c];
-        Vs[r * kHD + c] = v[((size_t)n * Q + r) * E + m * kHD + c];
+    for (int i = tid; i < Q * D; i += 256) {
+        const int r = i / D, c = i - r * D;
+        Ks[r * (D + 1) + c] = qk[((size_t)n * Q + r) * 2 * E + E + m * D + c];
+        Vs[r * D + c] = v[((size_t)n * Q + r) * E + m * D + c];
     }
     __syncthreads();
     const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     float* prow = Ps + w * Q;
     float* qrow = Qrow + w * kHD;
     for (int q = w; q < Q; q += 4) {
-        qrow[lane] = qk[((size_t)n * Q + q) * 2 * E + m * kHD + lane] * scaling;
+        if (lane < D) qrow[lane] = qk[((size_t)n * Q + q) * 2 * E + m * D + lane] * scaling;
         __builtin_amdgcn_wave_barrier();
         float s[kKPL];
         float mx = -INFINITY;
@@ -77,9 +77,9 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(const float* __restrict__ 
             s[i] = -INFINITY;
             if (k < Q) {
                 float acc = 0.f;
-                const float* kr = Ks + k * (kHD + 1);
+                const float* kr = Ks + k * (D + 1);
 #pragma unroll 16
-                for (int d = 0; d < kHD; ++d) acc += qrow[d] * kr[d];
+                for (int d = 0; d < D; ++d) acc += qrow[d] * kr[d];
                 s[i] = (kpm && kpm[(size_t)n * Q + k]) ? -INFINITY : acc;
             }
             mx = fmaxf(mx, s[i]);
@@ -105,9 +105,11 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(const float* __restrict__ 
         if (lane == 0) lse[(size_t)nm * Q + q] = mx + logf(sum);
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        float o = 0.f;
-        for (int k = 0; k < Q; ++k) o += prow[k] * Vs[k * kHD + lane];
-        out[((size_t)n * Q + q) * E + m * kHD + lane] = o;
+        if (lane < D) {
+            float o = 0.f;
+            for (int k = 0; k < Q; ++k) o += prow[k] * Vs[k * D + lane];
+            out[((size_t)n * Q + q) * E + m * D + lane] = o;
+        }
         __builtin_amdgcn_wave_barrier();
     }
 }
@@ -115,24 +117,24 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(const float* __restrict__ 
 __global__ __launch_bounds__(256) void mha_bwd_kernel(const float* __restrict__ qk, const float* __restrict__ v,
                                                       const uint8_t* __restrict__ kpm, const float* __restrict__ out,
                                                       const float* __restrict__ gout, const float* __restrict__ lse,
-                                                      int Q, int M, float scaling, float p_drop, uint32_t thresh,
+                                                      int Q, int M, int D, float scaling, float p_drop, uint32_t thresh,
                                                       uint64_t seed, float* __restrict__ ws_p,
                                                       float* __restrict__ ws_ds, float* __restrict__ dqk,
                                                       float* __restrict__ dv) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int E = M * kHD;
+    const int E = M * D;
     const int nm = xcd_remap(blockIdx.x, gridDim.x);
     const int n = nm / M, m = nm - n * M;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    float* A = smem;                   // phase A: K [Q][65]; phase B: dO [Q][64]
-    float* B = A + Q * (kHD + 1);      // phase A: V [Q][65]; phase B: q_scaled [Q][64]
-    float* R = B + Q * (kHD + 1);      // [4][Q] per-wave row buffer (dS row)
+    float* A = smem;                   // phase A: K [Q][D+1]; phase B: dO [Q][D]
+    float* B = A + Q * (D + 1);        // phase A: V [Q][D+1]; phase B: q_scaled [Q][D]
+    float* R = B + Q * (D + 1);        // [4][Q] per-wave row buffer (dS row)
     float* Rv = R + 4 * Q;             // [4][64] per-wave q / dO rows
     float* Ro = Rv + 4 * kHD;          // [4][64]
-    for (int i = tid; i < Q * kHD; i += 256) {
-        const int r = i >> 6, c = i & 63;
-        A[r * (kHD + 1) + c] = qk[((size_t)n * Q + r) * 2 * E + E + m * kHD + c];
-        B[r * (kHD + 1) + c] = v[((size_t)n * Q + r) * E + m * kHD + c];
+    for (int i = tid; i < Q * D; i += 256) {
+        const int r = i / D, c = i - r * D;
+        A[r * (D + 1) + c] = qk[((size_t)n * Q + r) * 2 * E + E + m * D + c];
+        B[r * (D + 1) + c] = v[((size_t)n * Q + r) * E + m * D + c];
     }
     __syncthreads();
     const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
@@ -143,11 +145,13 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const float* __restrict__ 
     float* wsd = ws_ds + (size_t)nm * Q * Q;
     // ---- phase A: query rows ----
     for (int q = w; q < Q; q += 4) {
-        const size_t orow = ((size_t)n * Q + q) * E + m * kHD;
-        const float go = gout[orow + lane];
-        qrow[lane] = qk[((size_t)n * Q + q) * 2 * E + m * kHD + lane] * scaling;
-        dorow[lane] = go;
-        const float delta = wave_add(go * out[orow + lane]);
+        const size_t orow = ((size_t)n * Q + q) * E + m * D;
+        const float go = lane < D ? gout[orow + lane] : 0.f;
+        if (lane < D) {
+            qrow[lane] = qk[((size_t)n * Q + q) * 2 * E + m * D + lane] * scaling;
+            dorow[lane] = go;
+        }
+        const float delta = wave_add(lane < D ? go * out[orow + lane] : 0.f);
         const float l = lse[(size_t)nm * Q + q];
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -155,10 +159,10 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const float* __restrict__ 
             const int k = lane + 64 * i;
             if (k < Q) {
                 float s = 0.f, dp = 0.f;
-                const float* kr = A + k * (kHD + 1);
-                const float* vr = B + k * (kHD + 1);
+                const float* kr = A + k * (D + 1);
+                const float* vr = B + k * (D + 1);
 #pragma unroll 16
-                for (int d = 0; d < kHD; ++d) {
+                for (int d = 0; d < D; ++d) {
                     s += qrow[d] * kr[d];
                     dp += dorow[d] * vr[d];
                 }
@@ -174,30 +178,33 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const float* __restrict__ 
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        float dq = 0.f;
-        for (int k = 0; k < Q; ++k) dq += dsrow[k] * A[k * (kHD + 1) + lane];
-        dqk[((size_t)n * Q + q) * 2 * E + m * kHD + lane] = dq * scaling;
+        if (lane < D) {
+            float dq = 0.f;
+            for (int k = 0; k < Q; ++k) dq += dsrow[k] * A[k * (D + 1) + lane];
+            dqk[((size_t)n * Q + q) * 2 * E + m * D + lane] = dq * scaling;
+        }
         __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
     // ---- phase B: key rows ----
-    for (int i = tid; i < Q * kHD; i += 256) {
-        const int r = i >> 6, c = i & 63;
-        A[r * kHD + c] = gout[((size_t)n * Q + r) * E + m * kHD + c];
-        B[r * kHD + c] = qk[((size_t)n * Q + r) * 2 * E + m * kHD + c] * scaling;
+    for (int i = tid; i < Q * D; i += 256) {
+        const int r = i / D, c = i - r * D;
+        A[r * D + c] = gout[((size_t)n * Q + r) * E + m * D + c];
+        B[r * D + c] = qk[((size_t)n * Q + r) * 2 * E + m * D + c] * scaling;
     }
     __syncthreads();
+    if (lane >= D) return;
     for (int k = w; k < Q; k += 4) {
         float gk = 0.f, gv = 0.f;
 #pragma unroll 8
         for (int q = 0; q < Q; ++q) {
             const float pd = wsp[(size_t)q * Q + k];
             const float ds = wsd[(size_t)q * Q + k];
-            gv += pd * A[q * kHD + lane];
-            gk += ds * B[q * kHD + lane];
+            gv += pd * A[q * D + lane];
+            gk += ds * B[q * D + lane];
         }
-        dqk[((size_t)n * Q + k) * 2 * E + E + m * kHD + lane] = gk;
-        dv[((size_t)n * Q + k) * E + m * kHD + lane] = gv;
+        dqk[((size_t)n * Q + k) * 2 * E + E + m * D + lane] = gk;
+        dv[((size_t)n * Q + k) * E + m * D + lane] = gv;
     }
 }
 
@@ -212,13 +219,14 @@ static uint32_t drop_threshold(float p) {
 
 using namespace pdvc;
 
-static size_t fwd_lds(int Q) { return sizeof(float) * ((size_t)Q * (kHD + 1) + (size_t)Q * kHD + 4 * Q + 4 * kHD); }
-static size_t bwd_lds(int Q) { return sizeof(float) * (2 * (size_t)Q * (kHD + 1) + 4 * Q + 8 * kHD); }
+static size_t fwd_lds(int Q, int D) { return sizeof(float) * ((size_t)Q * (D + 1) + (size_t)Q * D + 4 * Q + 4 * kHD); }
+static size_t bwd_lds(int Q, int D) { return sizeof(float) * (2 * (size_t)Q * (D + 1) + 4 * Q + 8 * kHD); }
 
 extern "C" int pdvc_mha_forward_f32(const float* qk, const float* v, const uint8_t* key_padding_mask, int batch,
                                     int num_query, int num_heads, int head_dim, float dropout_p, uint64_t seed,
                                     float* out, float* lse, void* stream) {
-    PDVC_CHECK_ARG(head_dim == kHD, "query self-attention kernel needs head_dim %d, got %d", kHD, head_dim);
+    PDVC_CHECK_ARG(head_dim > 0 && head_dim <= kHD, "query self-attention kernel needs head_dim <= %d, got %d", kHD,
+                   head_dim);
     PDVC_CHECK_ARG(num_query > 0 && num_query <= kMaxQ, "num_query must be in [1,%d], got %d", kMaxQ, num_query);
     PDVC_CHECK_ARG(batch >= 0 && num_heads > 0, "invalid sizes");
     PDVC_CHECK_ARG(dropout_p >= 0.f && dropout_p < 1.f, "dropout_p must be in [0,1)");
@@ -231,8 +239,8 @@ extern "C" int pdvc_mha_forward_f32(const float* qk, const float* v, const uint8
         (void)hipFuncSetAttribute((const void*)mha_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL(mha_fwd_kernel, dim3((unsigned)blocks), dim3(256), fwd_lds(num_query), (hipStream_t)stream, qk,
-                       v, key_padding_mask, num_query, num_heads, scaling, dropout_p, drop_threshold(dropout_p), seed,
+    hipLaunchKernelGGL(mha_fwd_kernel, dim3((unsigned)blocks), dim3(256), fwd_lds(num_query, head_dim),
+                       (hipStream_t)stream, qk, v, key_padding_mask, num_query, num_heads, head_dim, scaling, dropout_p, drop_threshold(dropout_p), seed,
                        out, lse);
     PDVC_CHECK_LAUNCH("mha_fwd_kernel");
     return PDVC_OK;
@@ -242,7 +250,8 @@ extern "C" int pdvc_mha_backward_f32(const float* qk, const float* v, const uint
                                      const float* out, const float* grad_out, const float* lse, int batch,
                                      int num_query, int num_heads, int head_dim, float dropout_p, uint64_t seed,
                                      float* workspace, float* grad_qk, float* grad_v, void* stream) {
-    PDVC_CHECK_ARG(head_dim == kHD, "query self-attention kernel needs head_dim %d, got %d", kHD, head_dim);
+    PDVC_CHECK_ARG(head_dim > 0 && head_dim <= kHD, "query self-attention kernel needs head_dim <= %d, got %d", kHD,
+                   head_dim);
     PDVC_CHECK_ARG(num_query > 0 && num_query <= kMaxQ, "num_query must be in [1,%d], got %d", kMaxQ, num_query);
     PDVC_CHECK_ARG(workspace != nullptr, "workspace (2*N*M*Q*Q floats) is required");
     const long blocks = (long)batch * num_heads;
@@ -255,8 +264,9 @@ extern "C" int pdvc_mha_backward_f32(const float* qk, const float* v, const uint
     }
     float* ws_p = workspace;
     float* ws_ds = workspace + (size_t)blocks * num_query * num_query;
-    hipLaunchKernelGGL(mha_bwd_kernel, dim3((unsigned)blocks), dim3(256), bwd_lds(num_query), (hipStream_t)stream, qk,
-                       v, key_padding_mask, out, grad_out, lse, num_query, num_heads, scaling, dropout_p,
+    hipLaunchKernelGGL(mha_bwd_kernel, dim3((unsigned)blocks), dim3(256), bwd_lds(num_query, head_dim),
+                       (hipStream_t)stream, qk, v, key_padding_mask, out, grad_out, lse, num_query, num_heads,
+                       head_dim, scaling, dropout_p,
                        drop_threshold(dropout_p), seed, ws_p, ws_ds, grad_qk, grad_v);
     PDVC_CHECK_LAUNCH("mha_bwd_kernel");
     return PDVC_OK;

@@ -7,7 +7,7 @@ from torch.autograd.function import once_differentiable
 
 from pdvc import _native as _n
 
-HEAD_DIM = 64
+MAX_HEAD_DIM = 64
 MAX_QUERIES = 300
 
 
@@ -44,9 +44,9 @@ class QuerySelfAttentionFunction(Function):
 def query_self_attention(qk, v, key_padding_mask, num_heads, dropout_p):
     """qk (N, Q, 2E) = [q | k] in-projections, v (N, Q, E); key_padding_mask (N, Q) True = ignore."""
     N, Q, E2 = qk.shape
-    if E2 // 2 // num_heads != HEAD_DIM or Q > MAX_QUERIES:
-        raise NotImplementedError(f"query self-attention kernel supports head_dim {HEAD_DIM} and <= {MAX_QUERIES} "
-                                  f"queries (got head_dim {E2 // 2 // num_heads}, Q {Q})")
+    if E2 // 2 // num_heads > MAX_HEAD_DIM or Q > MAX_QUERIES:
+        raise NotImplementedError(f"query self-attention kernel supports head_dim <= {MAX_HEAD_DIM} and <= "
+                                  f"{MAX_QUERIES} queries (got head_dim {E2 // 2 // num_heads}, Q {Q})")
     kpm = None if key_padding_mask is None else key_padding_mask.contiguous().view(torch.uint8)
     seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if dropout_p > 0 else 0
     return QuerySelfAttentionFunction.apply(qk, v, kpm, num_heads, dropout_p, seed)
