@@ -271,10 +271,9 @@ struct UnitMap {
     int nunits;              // units per (video, head)
     int level[16];
     int cslice[16];          // channel slice index within the level
-    int csplit[kL];          // slices per level
+    int dc[16];              // channels per slice (16, 32 or 64)
 };
 
-template <int DC>
 __global__ __launch_bounds__(512) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
                                                                 UnitMap um, int Lq, int S, int M, int D,
                                                                 const float* __restrict__ gout,
@@ -282,9 +281,6 @@ __global__ __launch_bounds__(512) void msda1d_bwd_value_kernel(const uint8_t* __
                                                                 const float* __restrict__ save_loc,
                                                                 float* __restrict__ grad_value) {
     extern __shared__ __attribute__((aligned(16))) float acc[];  // [T_l][DC + 1]
-    constexpr int LPS = DC / 4;
-    constexpr int SPP = 64 / LPS;  // samples per wave-pass
-    constexpr int LD = DC + 1;
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int nw = blockDim.x >> 6;
@@ -293,7 +289,11 @@ __global__ __launch_bounds__(512) void msda1d_bwd_value_kernel(const uint8_t* __
     const int unit = lb - bm * um.nunits;
     const int b = bm / M, m = bm - b * M;
     const int l = um.level[unit];
+    const int DC = um.dc[unit];
     const int c0 = um.cslice[unit] * DC;
+    const int LPS = DC >> 2;         // lanes per sample (4 channels each, strided by LPS)
+    const int SPP = 64 / LPS;        // samples per wave-pass
+    const int LD = DC + 1;           // padded row: rows of different samples start on different banks
     const int T = lv.T[l], st = lv.start[l];
     const float Tf = (float)T;
     for (int i = threadIdx.x; i < T * LD; i += blockDim.x) acc[i] = 0.f;
@@ -304,19 +304,25 @@ __global__ __launch_bounds__(512) void msda1d_bwd_value_kernel(const uint8_t* __
     const int nsamp = Lq * kP;
     const size_t MD = (size_t)M * D;
     const float* gbase = gout + (size_t)b * Lq * MD + (size_t)m * D + c0 + sub;
-    const size_t sbase = ((size_t)b * Lq * M + m) * kNS + l * kP;  // + (q*M)*kNS + p
-    for (int base = wid * SPP * 4; base < nsamp; base += nw * SPP * 4) {
+    const size_t sbase = ((size_t)b * Lq * M + m) * kNS + l * kP;
+    // Interleaved assignment: the SPP*nw lanes-groups of one pass take samples nsamp/(SPP*nw) apart, so the
+    // samples of one LDS atomic instruction come from distant queries (distinct rows); neighbouring queries
+    // sample the same rows and would otherwise serialise on same-address ds_add_f32.
+    const int groups = SPP * nw;
+    const int gidx = wid * SPP + slot;
+    const int per = (nsamp + groups - 1) / groups;
+    for (int it = 0; it < per; it += 4) {
         float gv[4][4], cw1[4], cw2[4];
         int r1[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int i = base + u * SPP + slot;
+            const int i = gidx * per + it + u;
             r1[u] = -2;
             cw1[u] = 0.f;
             cw2[u] = 0.f;
 #pragma unroll
             for (int k = 0; k < 4; ++k) gv[u][k] = 0.f;
-            if (i < nsamp) {
+            if (it + u < per && i < nsamp) {
                 const int q = i / kP, p = i - q * kP;
                 const size_t si = sbase + (size_t)q * M * kNS + p;
                 const float x = save_loc[si] * Tf - 0.5f;
@@ -486,58 +492,38 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
                              grad_ref);
         PDVC_CHECK_LAUNCH("msda1d_bwd_query_kernel");
     }
-    // grad_value: one workgroup per (video, head, level, channel slice); a slice keeps <= 64 KiB of LDS
+    // grad_value: one workgroup per (video, head, level, channel slice); slices keep every LDS tile
+    // <= ~68 KiB (two 512-thread workgroups per CU) with 16..64 channels per slice
     UnitMap um;
     um.nunits = 0;
-    int maxT = 0;
+    size_t lds = 0;
     for (int l = 0; l < kL; ++l) {
-        int split = 1;
-        while (((long)lv.T[l] * (head_dim / split + 1) * 4 > 64 * 1024 && head_dim / split > 16) ||
-               head_dim / split > 64)
-            split *= 2;
-        if ((long)lv.T[l] * (head_dim / split + 1) * 4 > 160 * 1024)
-            return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "level %d too long for the LDS value-gradient tile", l);
-        um.csplit[l] = split;
-        for (int c = 0; c < split; ++c) {
+        int dc = head_dim < 64 ? head_dim : 64;
+        while ((size_t)lv.T[l] * (dc + 1) * 4 > 68 * 1024 && dc > 16) dc /= 2;
+        if (head_dim % dc != 0 || dc % 4 != 0 || (64 % (dc / 4)) != 0)
+            return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "head_dim %d cannot be sliced for the value gradient", head_dim);
+        const size_t need = sizeof(float) * (size_t)lv.T[l] * (dc + 1);
+        if (need > 160 * 1024)
+            return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "level %d (T=%d) too long for the LDS value tile", l, lv.T[l]);
+        if (need > lds) lds = need;
+        for (int c = 0; c < head_dim / dc; ++c) {
             if (um.nunits >= 16) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "too many value-gradient units");
             um.level[um.nunits] = l;
             um.cslice[um.nunits] = c;
+            um.dc[um.nunits] = dc;
             ++um.nunits;
         }
-        if (lv.T[l] > maxT) maxT = lv.T[l];
     }
-    // all slices of one launch share one channel width: use the narrowest (largest split)
-    int split = 1;
-    for (int l = 0; l < kL; ++l) split = um.csplit[l] > split ? um.csplit[l] : split;
-    um.nunits = 0;
-    for (int l = 0; l < kL; ++l)
-        for (int c = 0; c < split; ++c) {
-            um.level[um.nunits] = l;
-            um.cslice[um.nunits] = c;
-            ++um.nunits;
-        }
-    const int DC = head_dim / split;
     const long nblk = (long)batch * num_heads * um.nunits;
     if (nblk > 0 && num_query > 0) {
-        const size_t lds = sizeof(float) * (size_t)maxT * (DC + 1);
         static bool attr = false;
         if (!attr) {
-            (void)hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<16>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<32>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<64>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024);
             attr = true;
         }
-#define VALUE_LAUNCH(DCV)                                                                                       \
-    hipLaunchKernelGGL((msda1d_bwd_value_kernel<DCV>), dim3((unsigned)nblk), dim3(512), lds, s, value_pad_mask, \
-                       lv, um, num_query, S, num_heads, head_dim, grad_output, save_attn, save_loc, grad_value)
-        if (DC == 64) VALUE_LAUNCH(64);
-        else if (DC == 32) VALUE_LAUNCH(32);
-        else if (DC == 16) VALUE_LAUNCH(16);
-        else return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "value-gradient slice width %d", DC);
-#undef VALUE_LAUNCH
+        hipLaunchKernelGGL(msda1d_bwd_value_kernel, dim3((unsigned)nblk), dim3(512), lds, s, value_pad_mask, lv, um,
+                           num_query, S, num_heads, head_dim, grad_output, save_attn, save_loc, grad_value);
         PDVC_CHECK_LAUNCH("msda1d_bwd_value_kernel");
     } else if (nblk > 0) {
         hipError_t e = hipMemsetAsync(grad_value, 0, sizeof(float) * (size_t)batch * S * num_heads * head_dim, s);
