@@ -67,6 +67,8 @@ __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __rest
         const int T = lv.T[l], st = lv.start[l];
         const float r0 = ref[((size_t)r * cL + l) * RD];
         const float r1 = (RD == 2) ? ref[((size_t)r * cL + l) * RD + 1] : 0.f;
+        int x0[cP];
+        float nw[cP], ne[cP];
 #pragma unroll
         for (int p = 0; p < cP; ++p) {
             const int j = l * cP + p;
@@ -76,18 +78,30 @@ __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __rest
             float gm;
             const float ix = border_ix(loc, T, gm);
             const float xf = floorf(ix);
-            const int x0 = (int)xf;
+            x0[p] = (int)xf;
             // iy == 0 (H == 1): nw = (x0+1-ix)*1, ne = (ix-x0)*1, the y0+1 row is outside
-            const float nw = ((float)(x0 + 1) - ix), ne = (ix - xf);
-            const bool ok0 = !(mbase && mbase[st + x0]);
-            const bool ok1 = x0 + 1 < T && !(mbase && mbase[st + x0 + 1]);
-            VecF<CPL> v0, v1, o;
-            ld(v0, vbase + (size_t)(st + x0) * MD, ok0);
-            ld(v1, vbase + (size_t)(st + x0 + 1) * MD, ok1);
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) o.v[c] = v0.v[c] * nw + v1.v[c] * ne;
-            o.store(samples + (((size_t)r * M + m) * cNS + j) * D + c0);
+            nw[p] = ((float)(x0[p] + 1) - ix);
+            ne[p] = (ix - xf);
         }
+        VecF<CPL> v0[cP], v1[cP];
+        bool ok0[cP], ok1[cP];
+#pragma unroll
+        for (int p = 0; p < cP; ++p) {  // the level's 2*P rows in flight together (clamped, selected after)
+            const int a1 = min(x0[p] + 1, T - 1);
+            v0[p].load(vbase + (size_t)(st + x0[p]) * MD);
+            v1[p].load(vbase + (size_t)(st + a1) * MD);
+            ok0[p] = !(mbase && mbase[st + x0[p]]);
+            ok1[p] = x0[p] + 1 < T && !(mbase && mbase[st + a1]);
+        }
+#pragma unroll
+        for (int p = 0; p < cP; ++p) {
+            VecF<CPL> o;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+                o.v[c] = (ok0[p] ? v0[p].v[c] : 0.f) * nw[p] + (ok1[p] ? v1[p].v[c] : 0.f) * ne[p];
+            o.store(samples + (((size_t)r * M + m) * cNS + l * cP + p) * D + c0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -121,32 +135,42 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
 #pragma unroll
     for (int l = 0; l < cL; ++l) {
         const int T = lv.T[l], st = lv.start[l];
+        int x0[cP];
+        float nw[cP], ne[cP];
 #pragma unroll
         for (int p = 0; p < cP; ++p) {
-            const int j = l * cP + p;
-            float s = 0.f;
-            if (active) {
-                const float loc = save_loc[((size_t)r * M + m) * cNS + j];
-                float gm;
-                const float ix = border_ix(loc, T, gm);
-                const float xf = floorf(ix);
-                const int x0 = (int)xf;
-                const float nw = ((float)(x0 + 1) - ix), ne = (ix - xf);
-                const bool ok0 = !(mbase && mbase[st + x0]);
-                const bool ok1 = x0 + 1 < T && !(mbase && mbase[st + x0 + 1]);
-                VecF<CPL> g, v0, v1;
-                g.load(gsamp + (((size_t)r * M + m) * cNS + j) * D + c0);
-                ld(v0, vbase + (size_t)(st + x0) * MD, ok0);
-                ld(v1, vbase + (size_t)(st + x0 + 1) * MD, ok1);
-#pragma unroll
-                for (int c = 0; c < CPL; ++c) {
-                    if (ok0) atomicAdd(gvbase + (size_t)(st + x0) * MD + c, nw * g.v[c]);
-                    if (ok1) atomicAdd(gvbase + (size_t)(st + x0 + 1) * MD + c, ne * g.v[c]);
-                    s += g.v[c] * (v1.v[c] - v0.v[c]);  // gix = -vnw + vne (iy == 0)
-                }
-            }
-            part[j] = s;
+            const float loc = active ? save_loc[((size_t)r * M + m) * cNS + l * cP + p] : 0.f;
+            float gm;
+            const float ix = border_ix(loc, T, gm);
+            const float xf = floorf(ix);
+            x0[p] = (int)xf;
+            nw[p] = ((float)(x0[p] + 1) - ix);
+            ne[p] = (ix - xf);
         }
+        VecF<CPL> g[cP], v0[cP], v1[cP];
+        bool ok0[cP], ok1[cP];
+#pragma unroll
+        for (int p = 0; p < cP; ++p) {
+            const int a1 = min(x0[p] + 1, T - 1);
+            g[p].load(gsamp + (((size_t)r * M + m) * cNS + l * cP + p) * D + c0);
+            v0[p].load(vbase + (size_t)(st + x0[p]) * MD);
+            v1[p].load(vbase + (size_t)(st + a1) * MD);
+            ok0[p] = active && !(mbase && mbase[st + x0[p]]);
+            ok1[p] = active && x0[p] + 1 < T && !(mbase && mbase[st + a1]);
+        }
+#pragma unroll
+        for (int p = 0; p < cP; ++p) {
+            float s = 0.f;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const float gv = active ? g[p].v[c] : 0.f;
+                if (ok0[p]) atomicAdd(gvbase + (size_t)(st + x0[p]) * MD + c, nw[p] * gv);
+                if (ok1[p]) atomicAdd(gvbase + (size_t)(st + x0[p] + 1) * MD + c, ne[p] * gv);
+                s += gv * ((ok1[p] ? v1[p].v[c] : 0.f) - (ok0[p] ? v0[p].v[c] : 0.f));  // gix = -vnw + vne
+            }
+            part[l * cP + p] = s;
+        }
+        __builtin_amdgcn_sched_barrier(0);
     }
     group_reduce_scatter<cNS, G>(part, lane);
 #pragma unroll

@@ -38,6 +38,11 @@ __device__ __forceinline__ void load_row(VecF<CPL>& v, const float* __restrict__
     else v.zero();
 }
 
+// select a level's constant without runtime-indexing the (register-resident) struct
+__device__ __forceinline__ int lvl_sel(const int (&v)[kL], int l) {
+    return l == 0 ? v[0] : l == 1 ? v[1] : l == 2 ? v[2] : v[3];
+}
+
 // -------------------------------------------------------------------------------------------------
 // forward
 // -------------------------------------------------------------------------------------------------
@@ -59,64 +64,71 @@ __global__ __launch_bounds__(256) void msda1d_fwd_kernel(
     const int m = hg * HPW + lane / LPH;
     if (m >= M) return;
     const int c0 = sub * CPL;
-    const float* prow = proj + (size_t)row * proj_stride;
+    const float* logits = proj + (size_t)row * proj_stride + logit_base + m * kNS;
+    const float* offs = proj + (size_t)row * proj_stride + off_base + m * kNS;
 
-    // softmax over the head's L*P logits (ms_deform_attn.py:168-169)
-    float a[kNS], off[kNS];
+    // softmax statistics over the head's L*P logits (ms_deform_attn.py:168-169); weights formed per level
     float mx = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < kNS; ++j) {
-        a[j] = prow[logit_base + m * kNS + j];
-        off[j] = prow[off_base + m * kNS + j];
-        mx = fmaxf(mx, a[j]);
-    }
+    for (int j = 0; j < kNS; ++j) mx = fmaxf(mx, logits[j]);
     float sum = 0.f;
 #pragma unroll
-    for (int j = 0; j < kNS; ++j) {
-        a[j] = expf(a[j] - mx);
-        sum += a[j];
-    }
-#pragma unroll
-    for (int j = 0; j < kNS; ++j) a[j] = a[j] / sum;
-
-    float r0[kL], r1[kL];
-#pragma unroll
-    for (int l = 0; l < kL; ++l) {
-        r0[l] = ref[((size_t)row * kL + l) * RD];
-        r1[l] = (RD == 2) ? ref[((size_t)row * kL + l) * RD + 1] : 0.f;
-    }
+    for (int j = 0; j < kNS; ++j) sum += expf(logits[j] - mx);
 
     const size_t MD = (size_t)M * D;
     const float* vbase = value + (size_t)b * S * MD + (size_t)m * D + c0;
     const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
     VecF<CPL> acc;
     acc.zero();
-#pragma unroll
+#pragma unroll 1
     for (int l = 0; l < kL; ++l) {
-        const int T = lv.T[l], st = lv.start[l];
+        const int T = lvl_sel(lv.T, l), st = lvl_sel(lv.start, l);
         const float Tf = (float)T;
+        const float r0 = ref[((size_t)row * kL + l) * RD];
+        const float r1 = (RD == 2) ? ref[((size_t)row * kL + l) * RD + 1] : 0.f;
+        // positions of the level's P points, then all 2*P corner rows loaded together (clamped addresses;
+        // out-of-range corners are selected to 0 after the load: no data-dependent branches around loads)
+        int i0[kP];
+        float lw[kP], aw[kP];
+        bool ok1[kP], ok2[kP];
 #pragma unroll
         for (int p = 0; p < kP; ++p) {
             const int j = l * kP + p;
+            aw[p] = expf(logits[j] - mx) / sum;
+            const float off = offs[j];
             // ms_deform_attn.py:171-177 (same evaluation order)
-            const float loc = (RD == 1) ? r0[l] + off[j] / Tf : r0[l] + ((off[j] / (float)kP) * r1[l]) * 0.5f;
+            const float loc = (RD == 1) ? r0 + off / Tf : r0 + ((off / (float)kP) * r1) * 0.5f;
             if (save_loc && sub == (j % LPH)) {
                 const size_t si = ((size_t)row * M + m) * kNS + j;
                 save_loc[si] = loc;
-                save_attn[si] = a[j];
+                save_attn[si] = aw[p];
             }
             const float x = loc * Tf - 0.5f;  // w_im (.cuh:284); h_im == 0 for H == 1
-            if (x > -1.f && x < Tf) {
-                const float xf = floorf(x);
-                const int i0 = (int)xf;
-                const float lw = x - xf, hw = 1.f - lw;
-                const bool ok1 = i0 >= 0 && !(mbase && mbase[st + i0]);
-                const bool ok2 = i0 + 1 <= T - 1 && !(mbase && mbase[st + i0 + 1]);
-                VecF<CPL> v1, v2;
-                load_row(v1, vbase + (size_t)(st + i0) * MD, ok1);
-                load_row(v2, vbase + (size_t)(st + i0 + 1) * MD, ok2);
+            const bool inside = x > -1.f && x < Tf;
+            const float xf = floorf(inside ? x : 0.f);
+            i0[p] = (int)xf;
+            lw[p] = inside ? x - xf : 0.f;
+            ok1[p] = inside && i0[p] >= 0;
+            ok2[p] = inside && i0[p] + 1 <= T - 1;
+        }
+        VecF<CPL> v1[kP], v2[kP];
 #pragma unroll
-                for (int c = 0; c < CPL; ++c) acc.v[c] += (hw * v1.v[c] + lw * v2.v[c]) * a[j];
+        for (int p = 0; p < kP; ++p) {
+            const int a1 = min(max(i0[p], 0), T - 1), a2 = min(max(i0[p] + 1, 0), T - 1);
+            v1[p].load(vbase + (size_t)(st + a1) * MD);
+            v2[p].load(vbase + (size_t)(st + a2) * MD);
+            if (mbase) {
+                ok1[p] = ok1[p] && !mbase[st + a1];
+                ok2[p] = ok2[p] && !mbase[st + a2];
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < kP; ++p) {
+            const float hw = 1.f - lw[p];
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const float x1 = ok1[p] ? v1[p].v[c] : 0.f, x2 = ok2[p] ? v2[p].v[c] : 0.f;
+                acc.v[c] += (hw * x1 + lw[p] * x2) * aw[p];
             }
         }
     }
@@ -125,16 +137,19 @@ __global__ __launch_bounds__(256) void msda1d_fwd_kernel(
 
 // -------------------------------------------------------------------------------------------------
 // backward, query side: grad of the offset and attention logits (+ reference points)
+// softmax backward uses delta = sum_j a_j dL/da_j = <dL/dout, out> (out = the forward output of this head),
+// so every level's samples are finished as soon as they are reduced -- no state carried across levels.
 // -------------------------------------------------------------------------------------------------
 template <int CPL, int LPH, int RD>
 __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
     int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
-    int D, int waves_per_row, int total_waves, const float* __restrict__ gout, const float* __restrict__ save_attn,
-    const float* __restrict__ save_loc, float* __restrict__ grad_proj, float* __restrict__ grad_ref) {
+    int D, int waves_per_row, int total_waves, const float* __restrict__ gout, const float* __restrict__ fout,
+    const float* __restrict__ save_attn, const float* __restrict__ save_loc, float* __restrict__ grad_proj,
+    float* __restrict__ grad_ref) {
     constexpr int HPW = 64 / LPH;
-    constexpr int SPL = kNS / LPH;  // samples owned per lane after the reduce-scatter
-    static_assert(SPL >= 1, "LPH must be <= 16");
+    constexpr int G = LPH < 8 ? LPH : 8;  // reduce-scatter group for the level's 8 partial sums
+    constexpr int VPL = 8 / G;            // values per lane after it (interleaved (ga, gs) pairs)
     const int lane = threadIdx.x & 63;
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
     const int wave = lb * 4 + (threadIdx.x >> 6);
@@ -152,106 +167,113 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
     const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
     const size_t sbase = ((size_t)row * M + m) * kNS;
 
-    VecF<CPL> g;
+    VecF<CPL> g, o;
     load_row(g, gout + (size_t)row * MD + (size_t)m * D + c0, active);
+    load_row(o, fout + (size_t)row * MD + (size_t)m * D + c0, active);
+    float dl = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) dl += g.v[c] * o.v[c];
+    const float delta = group_allreduce<LPH>(dl);
 
-    // part[2j] = sum_c g*val ; part[2j+1] = sum_c g*(v2 - v1)   (this lane's channels)
-    float part[2 * kNS];
-#pragma unroll
-    for (int l = 0; l < kL; ++l) {
-        const int T = lv.T[l], st = lv.start[l];
-        const float Tf = (float)T;
-#pragma unroll
-        for (int p = 0; p < kP; ++p) {
-            const int j = l * kP + p;
-            float s1 = 0.f, s2 = 0.f;
-            const float loc = active ? save_loc[sbase + j] : 0.f;
-            const float x = loc * Tf - 0.5f;
-            if (active && x > -1.f && x < Tf) {
-                const float xf = floorf(x);
-                const int i0 = (int)xf;
-                const float lw = x - xf, hw = 1.f - lw;
-                const bool ok1 = i0 >= 0 && !(mbase && mbase[st + i0]);
-                const bool ok2 = i0 + 1 <= T - 1 && !(mbase && mbase[st + i0 + 1]);
-                VecF<CPL> v1, v2;
-                load_row(v1, vbase + (size_t)(st + i0) * MD, ok1);
-                load_row(v2, vbase + (size_t)(st + i0 + 1) * MD, ok2);
-#pragma unroll
-                for (int c = 0; c < CPL; ++c) {
-                    s1 += g.v[c] * (hw * v1.v[c] + lw * v2.v[c]);
-                    s2 += g.v[c] * (v2.v[c] - v1.v[c]);
-                }
-            }
-            part[2 * j] = s1;
-            part[2 * j + 1] = s2;
-        }
-    }
-    group_reduce_scatter<2 * kNS, LPH>(part, lane);
-
-    // lane `sub` now owns samples j = sub*SPL + k, k < SPL: part[2k] = grad_attn, part[2k+1] = sum g*(v2-v1)
-    float aj[SPL], ga[SPL];
-    float dpart = 0.f;
-#pragma unroll
-    for (int k = 0; k < SPL; ++k) {
-        const int j = sub * SPL + k;
-        aj[k] = active ? save_attn[sbase + j] : 0.f;
-        ga[k] = part[2 * k];
-        dpart += aj[k] * ga[k];
-    }
-    const float delta = group_allreduce<LPH>(dpart);  // softmax backward: sum_j a_j * grad_a_j
-
-    float gr0[kL], gr1[kL];
-#pragma unroll
-    for (int l = 0; l < kL; ++l) { gr0[l] = 0.f; gr1[l] = 0.f; }
     const float* prow = proj + (size_t)row * proj_stride;
     float* gprow = grad_proj + (size_t)row * proj_stride;
+#pragma unroll 1
+    for (int l = 0; l < kL; ++l) {
+        const int T = lvl_sel(lv.T, l), st = lvl_sel(lv.start, l);
+        const float Tf = (float)T;
+        int i0[kP];
+        float lw[kP];
+        bool ok1[kP], ok2[kP];
 #pragma unroll
-    for (int k = 0; k < SPL; ++k) {
-        const int j = sub * SPL + k;
-        const int l = j / kP;
-        const float Tf = (float)lv.T[l];
-        // CUDA: grad_loc_w = W * grad_w_weight * (top_grad * attn), summed over channels (.cuh:158)
-        const float gloc = Tf * (part[2 * k + 1] * aj[k]);
-        const float glogit = aj[k] * (ga[k] - delta);
-        float goff;
-        if (RD == 1) {
-            goff = gloc / Tf;
+        for (int p = 0; p < kP; ++p) {
+            const float x = (active ? save_loc[sbase + l * kP + p] : 0.f) * Tf - 0.5f;
+            const bool inside = active && x > -1.f && x < Tf;
+            const float xf = floorf(inside ? x : 0.f);
+            i0[p] = (int)xf;
+            lw[p] = inside ? x - xf : 0.f;
+            ok1[p] = inside && i0[p] >= 0;
+            ok2[p] = inside && i0[p] + 1 <= T - 1;
+        }
+        VecF<CPL> v1[kP], v2[kP];
 #pragma unroll
-            for (int ll = 0; ll < kL; ++ll) if (ll == l) gr0[ll] += gloc;
+        for (int p = 0; p < kP; ++p) {  // all 2*P corner loads in flight together (clamped, selected later)
+            const int a1 = min(max(i0[p], 0), T - 1), a2 = min(max(i0[p] + 1, 0), T - 1);
+            v1[p].load(vbase + (size_t)(st + a1) * MD);
+            v2[p].load(vbase + (size_t)(st + a2) * MD);
+            if (mbase) {
+                ok1[p] = ok1[p] && !mbase[st + a1];
+                ok2[p] = ok2[p] && !mbase[st + a2];
+            }
+        }
+        // part[2p] = sum_c g*val ; part[2p+1] = sum_c g*(v2 - v1) over this lane's channels
+        float part[2 * kP];
+#pragma unroll
+        for (int p = 0; p < kP; ++p) {
+            const float hw = 1.f - lw[p];
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const float x1 = ok1[p] ? v1[p].v[c] : 0.f, x2 = ok2[p] ? v2[p].v[c] : 0.f;
+                s1 += g.v[c] * (hw * x1 + lw[p] * x2);
+                s2 += g.v[c] * (x2 - x1);
+            }
+            part[2 * p] = s1;
+            part[2 * p + 1] = s2;
+        }
+        group_reduce_scatter<2 * kP, G>(part, lane);
+#pragma unroll
+        for (int k = 0; k < VPL; ++k) {
+#pragma unroll
+            for (int d = G; d < LPH; d <<= 1) part[k] += __shfl_xor(part[k], d, PDVC_WAVE);
+        }
+        // group lane r (= sub % G) holds values [r*VPL, (r+1)*VPL) of the interleaved (ga, gs) list
+        float ga, gs;
+        int p;
+        const int r = sub % G;
+        if (VPL == 2) {
+            p = r;
+            ga = part[0];
+            gs = part[1];
         } else {
-            const float r1 = ref[((size_t)row * kL + l) * 2 + 1];
-            const float t2 = gloc * 0.5f;
-            goff = (t2 * r1) / (float)kP;
-            const float o = active ? prow[off_base + m * kNS + j] : 0.f;
-#pragma unroll
-            for (int ll = 0; ll < kL; ++ll) if (ll == l) { gr0[ll] += gloc; gr1[ll] += t2 * (o / (float)kP); }
+            const float other = __shfl_xor(part[0], 1, PDVC_WAVE);
+            p = r >> 1;
+            ga = (r & 1) ? other : part[0];
+            gs = (r & 1) ? part[0] : other;
         }
-        if (active) {
+        const bool owner = active && sub < G && (VPL == 2 || (r & 1) == 0);
+        const int j = l * kP + p;
+        const float a = active ? save_attn[sbase + j] : 0.f;
+        // CUDA: grad_loc_w = W * grad_w_weight * (top_grad * attn), summed over channels (.cuh:158)
+        const float gloc = owner ? Tf * (gs * a) : 0.f;
+        float g0 = gloc, g1 = 0.f;
+        if (owner) {
+            float goff;
+            if (RD == 1) {
+                goff = gloc / Tf;
+            } else {
+                const float rr1 = ref[((size_t)row * kL + l) * 2 + 1];
+                const float t2 = gloc * 0.5f;
+                goff = (t2 * rr1) / (float)kP;
+                g1 = t2 * (prow[off_base + m * kNS + j] / (float)kP);
+            }
             gprow[off_base + m * kNS + j] = goff;
-            gprow[logit_base + m * kNS + j] = glogit;
+            gprow[logit_base + m * kNS + j] = a * (ga - delta);
         }
-    }
-    if (grad_ref) {
-        // sum over every head of the row: all lanes of the wave, then (several waves per row) atomics
+        if (grad_ref) {
+            // sum over every head and point of the row (all lanes), then atomics across waves of a row
 #pragma unroll
-        for (int l = 0; l < kL; ++l) {
-            float v0 = gr0[l];
-#pragma unroll
-            for (int d = 32; d > 0; d >>= 1) v0 += __shfl_xor(v0, d, PDVC_WAVE);
-            float v1 = 0.f;
-            if (RD == 2) {
-                v1 = gr1[l];
-#pragma unroll
-                for (int d = 32; d > 0; d >>= 1) v1 += __shfl_xor(v1, d, PDVC_WAVE);
+            for (int d = 32; d > 0; d >>= 1) {
+                g0 += __shfl_xor(g0, d, PDVC_WAVE);
+                if (RD == 2) g1 += __shfl_xor(g1, d, PDVC_WAVE);
             }
             if (lane == 0) {
                 float* dst = grad_ref + ((size_t)row * kL + l) * RD;
                 if (waves_per_row == 1) {
-                    dst[0] = v0;
-                    if (RD == 2) dst[1] = v1;
+                    dst[0] = g0;
+                    if (RD == 2) dst[1] = g1;
                 } else {
-                    atomicAdd(dst, v0);
-                    if (RD == 2) atomicAdd(dst + 1, v1);
+                    atomicAdd(dst, g0);
+                    if (RD == 2) atomicAdd(dst + 1, g1);
                 }
             }
         }
@@ -311,44 +333,44 @@ __global__ __launch_bounds__(512) void msda1d_bwd_value_kernel(const uint8_t* __
     const int groups = SPP * nw;
     const int gidx = wid * SPP + slot;
     const int per = (nsamp + groups - 1) / groups;
-    for (int it = 0; it < per; it += 4) {
-        float gv[4][4], cw1[4], cw2[4];
-        int r1[4];
+    constexpr int U = 8;  // samples per lane per iteration: 8 loc/attn loads, then 32 gradient loads in flight
+    for (int it = 0; it < per; it += U) {
+        float loc[U], att[U];
+        int qv[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = gidx * per + it + u;
-            r1[u] = -2;
-            cw1[u] = 0.f;
-            cw2[u] = 0.f;
+        for (int u = 0; u < U; ++u) {
+            int i = gidx * per + it + u;
+            const bool ok = (it + u < per) && i < nsamp;
+            i = ok ? i : 0;
+            const int q = i / kP, p = i - q * kP;
+            qv[u] = ok ? q : -1;
+            const size_t si = sbase + (size_t)q * M * kNS + p;
+            loc[u] = save_loc[si];
+            att[u] = save_attn[si];
+        }
+        float gv[U][4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) gv[u][k] = 0.f;
-            if (it + u < per && i < nsamp) {
-                const int q = i / kP, p = i - q * kP;
-                const size_t si = sbase + (size_t)q * M * kNS + p;
-                const float x = save_loc[si] * Tf - 0.5f;
-                if (x > -1.f && x < Tf) {
-                    const float xf = floorf(x);
-                    const float lw = x - xf;
-                    const float a = save_attn[si];
-                    r1[u] = (int)xf;
-                    cw1[u] = (1.f - lw);
-                    cw2[u] = lw;
-                    const float* gp = gbase + (size_t)q * MD;
+        for (int u = 0; u < U; ++u) {
+            const float* gp = gbase + (size_t)(qv[u] < 0 ? 0 : qv[u]) * MD;
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) gv[u][k] = gp[LPS * k] * a;  // top_grad * attn (.cuh:116)
-                }
-            }
+            for (int k = 0; k < 4; ++k) gv[u][k] = gp[LPS * k];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int x0 = r1[u];
-            if (x0 >= 0) {
+        for (int u = 0; u < U; ++u) {
+            const float x = loc[u] * Tf - 0.5f;
+            if (qv[u] >= 0 && x > -1.f && x < Tf) {
+                const float xf = floorf(x);
+                const int x0 = (int)xf;
+                const float lw = x - xf, hw = 1.f - lw;
+                if (x0 >= 0) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) atomicAdd(&acc[x0 * LD + sub + LPS * k], cw1[u] * gv[u][k]);
-            }
-            if (x0 >= -1 && x0 + 1 <= T - 1) {
+                    for (int k = 0; k < 4; ++k) atomicAdd(&acc[x0 * LD + sub + LPS * k], hw * (gv[u][k] * att[u]));
+                }
+                if (x0 + 1 <= T - 1) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) atomicAdd(&acc[(x0 + 1) * LD + sub + LPS * k], cw2[u] * gv[u][k]);
+                    for (int k = 0; k < 4; ++k)
+                        atomicAdd(&acc[(x0 + 1) * LD + sub + LPS * k], lw * (gv[u][k] * att[u]));
+                }
             }
         }
     }
@@ -384,8 +406,10 @@ struct Geometry {
 };
 
 static int pick_geometry(int M, int D, Geometry& g) {
-    if (D == 16) g.cpl = 4;
-    else if (D == 32 || D == 64 || D == 128) g.cpl = 8;
+    // 4 channels (one float4) per lane keeps a level's 2*P corner loads in flight within the register budget
+    // of 4 waves/SIMD; D = 128 needs 8 per lane (at most 16 lanes per head).
+    if (D == 16 || D == 32 || D == 64) g.cpl = 4;
+    else if (D == 128) g.cpl = 8;
     else return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "fused 1-D path supports head_dim 16/32/64/128, got %d", D);
     g.lph = D / g.cpl;
     g.hpw = 64 / g.lph;
@@ -402,23 +426,23 @@ static void launch_fwd1d(const Geometry& g, dim3 grid, hipStream_t s, const floa
                          const float* proj, int ps, int ob, int lb, const float* ref, Levels1d lv, int Lq, int S,
                          int M, int D, int tw, float* out, float* sa, float* sl) {
 #define ARGS value, mask, proj, ps, ob, lb, ref, lv, Lq, S, M, D, g.waves_per_row, tw, out, sa, sl
-    if (g.cpl == 4) hipLaunchKernelGGL((msda1d_fwd_kernel<4, 4, RD>), grid, dim3(256), 0, s, ARGS);
-    else if (g.lph == 4) hipLaunchKernelGGL((msda1d_fwd_kernel<8, 4, RD>), grid, dim3(256), 0, s, ARGS);
-    else if (g.lph == 8) hipLaunchKernelGGL((msda1d_fwd_kernel<8, 8, RD>), grid, dim3(256), 0, s, ARGS);
-    else hipLaunchKernelGGL((msda1d_fwd_kernel<8, 16, RD>), grid, dim3(256), 0, s, ARGS);
+    if (g.cpl == 8) hipLaunchKernelGGL((msda1d_fwd_kernel<8, 16, RD>), grid, dim3(256), 0, s, ARGS);
+    else if (g.lph == 4) hipLaunchKernelGGL((msda1d_fwd_kernel<4, 4, RD>), grid, dim3(256), 0, s, ARGS);
+    else if (g.lph == 8) hipLaunchKernelGGL((msda1d_fwd_kernel<4, 8, RD>), grid, dim3(256), 0, s, ARGS);
+    else hipLaunchKernelGGL((msda1d_fwd_kernel<4, 16, RD>), grid, dim3(256), 0, s, ARGS);
 #undef ARGS
 }
 
 template <int RD>
 static void launch_bwdq1d(const Geometry& g, dim3 grid, hipStream_t s, const float* value, const uint8_t* mask,
                           const float* proj, int ps, int ob, int lb, const float* ref, Levels1d lv, int Lq, int S,
-                          int M, int D, int tw, const float* gout, const float* sa, const float* sl, float* gp,
-                          float* gr) {
-#define ARGS value, mask, proj, ps, ob, lb, ref, lv, Lq, S, M, D, g.waves_per_row, tw, gout, sa, sl, gp, gr
-    if (g.cpl == 4) hipLaunchKernelGGL((msda1d_bwd_query_kernel<4, 4, RD>), grid, dim3(256), 0, s, ARGS);
-    else if (g.lph == 4) hipLaunchKernelGGL((msda1d_bwd_query_kernel<8, 4, RD>), grid, dim3(256), 0, s, ARGS);
-    else if (g.lph == 8) hipLaunchKernelGGL((msda1d_bwd_query_kernel<8, 8, RD>), grid, dim3(256), 0, s, ARGS);
-    else hipLaunchKernelGGL((msda1d_bwd_query_kernel<8, 16, RD>), grid, dim3(256), 0, s, ARGS);
+                          int M, int D, int tw, const float* gout, const float* fout, const float* sa, const float* sl,
+                          float* gp, float* gr) {
+#define ARGS value, mask, proj, ps, ob, lb, ref, lv, Lq, S, M, D, g.waves_per_row, tw, gout, fout, sa, sl, gp, gr
+    if (g.cpl == 8) hipLaunchKernelGGL((msda1d_bwd_query_kernel<8, 16, RD>), grid, dim3(256), 0, s, ARGS);
+    else if (g.lph == 4) hipLaunchKernelGGL((msda1d_bwd_query_kernel<4, 4, RD>), grid, dim3(256), 0, s, ARGS);
+    else if (g.lph == 8) hipLaunchKernelGGL((msda1d_bwd_query_kernel<4, 8, RD>), grid, dim3(256), 0, s, ARGS);
+    else hipLaunchKernelGGL((msda1d_bwd_query_kernel<4, 16, RD>), grid, dim3(256), 0, s, ARGS);
 #undef ARGS
 }
 
@@ -460,7 +484,8 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
                                         int ref_dim, const float* proj, int proj_stride, int off_base, int logit_base,
                                         const int32_t* level_T, int num_levels, int batch, int num_query,
                                         int num_heads, int head_dim, int num_point, const float* grad_output,
-                                        const float* save_attn, const float* save_loc, float* grad_value,
+                                        const float* output, const float* save_attn, const float* save_loc,
+                                        float* grad_value,
                                         float* grad_proj, float* grad_ref, void* stream) {
     Levels1d lv;
     int S = 0;
@@ -469,7 +494,7 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
     Geometry g;
     if ((rc = pick_geometry(num_heads, head_dim, g))) return rc;
     PDVC_CHECK_ARG(ref_dim == 1 || ref_dim == 2, "ref_dim must be 1 or 2, got %d", ref_dim);
-    PDVC_CHECK_ARG(save_attn && save_loc, "backward needs save_attn and save_loc from the forward");
+    PDVC_CHECK_ARG(save_attn && save_loc && output, "backward needs the forward's output, save_attn and save_loc");
     const int NSM = num_heads * kNS;
     PDVC_CHECK_ARG(off_base >= 0 && logit_base >= 0 && off_base + NSM <= proj_stride && logit_base + NSM <= proj_stride,
                    "proj columns out of range");
@@ -484,12 +509,12 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
         dim3 grid((unsigned)((tw + 3) / 4));
         if (ref_dim == 1)
             launch_bwdq1d<1>(g, grid, s, value, value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv,
-                             num_query, S, num_heads, head_dim, (int)tw, grad_output, save_attn, save_loc, grad_proj,
-                             grad_ref);
+                             num_query, S, num_heads, head_dim, (int)tw, grad_output, output, save_attn, save_loc,
+                             grad_proj, grad_ref);
         else
             launch_bwdq1d<2>(g, grid, s, value, value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv,
-                             num_query, S, num_heads, head_dim, (int)tw, grad_output, save_attn, save_loc, grad_proj,
-                             grad_ref);
+                             num_query, S, num_heads, head_dim, (int)tw, grad_output, output, save_attn, save_loc,
+                             grad_proj, grad_ref);
         PDVC_CHECK_LAUNCH("msda1d_bwd_query_kernel");
     }
     // grad_value: one workgroup per (video, head, level, channel slice); slices keep every LDS tile

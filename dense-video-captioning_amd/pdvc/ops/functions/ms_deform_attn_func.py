@@ -118,14 +118,14 @@ class MSDA1dFunction(Function):
                 _n.ptr(ref), RD, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(out), _n.ptr(save_attn),
                 _n.ptr(save_loc), _n.stream(), meta=(N, Lq, S, M, D, NUM_SAMPLES))
         if need:
-            ctx.save_for_backward(value, pad_mask, proj, ref, save_attn, save_loc)
+            ctx.save_for_backward(value, pad_mask, proj, ref, save_attn, save_loc, out)
         ctx.meta = (tuple(level_T), off_base, logit_base)
         return out
 
     @staticmethod
     @once_differentiable
     def backward(ctx, grad_out):
-        value, pad_mask, proj, ref, save_attn, save_loc = ctx.saved_tensors
+        value, pad_mask, proj, ref, save_attn, save_loc, out = ctx.saved_tensors
         level_T, off_base, logit_base = ctx.meta
         grad_out = grad_out.contiguous()
         N, S, M, D = value.shape
@@ -136,8 +136,8 @@ class MSDA1dFunction(Function):
         gp = torch.zeros_like(proj) if C != 2 * M * NUM_SAMPLES else torch.empty_like(proj)
         gr = torch.empty_like(ref) if ctx.needs_input_grad[3] else None
         _n.call("pdvc_msda1d_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(ref), RD, _n.ptr(proj), C,
-                off_base, logit_base, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(grad_out), _n.ptr(save_attn),
-                _n.ptr(save_loc), _n.ptr(gv), _n.ptr(gp), _n.ptr(gr), _n.stream(),
+                off_base, logit_base, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(grad_out), _n.ptr(out),
+                _n.ptr(save_attn), _n.ptr(save_loc), _n.ptr(gv), _n.ptr(gp), _n.ptr(gr), _n.stream(),
                 meta=(N, Lq, S, M, D, NUM_SAMPLES))
         return gv, None, gp, gr, None, None, None
 

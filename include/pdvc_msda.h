@@ -110,13 +110,14 @@ int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_pad_mask, c
                             int num_heads, int head_dim, int num_point, float* output, float* save_attn,
                             float* save_loc, void* stream);
 /* grad_value (N,S,M,D) (zero on padded rows); grad_proj (N,Lq,proj_stride): only the offset and logit
- * slots are written; grad_ref (N,Lq,L,ref_dim) or NULL.  workspace: NULL (reserved). */
+ * slots are written; grad_ref (N,Lq,L,ref_dim) or NULL.  `output` is the forward's output (the softmax
+ * backward's row term sum_j a_j dL/da_j is computed as <grad_output, output>). */
 int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value_pad_mask, const float* ref,
                              int ref_dim, const float* proj, int proj_stride, int off_base, int logit_base,
                              const int32_t* level_T, int num_levels, int batch, int num_query, int num_heads,
-                             int head_dim, int num_point, const float* grad_output, const float* save_attn,
-                             const float* save_loc, float* grad_value, float* grad_proj, float* grad_ref,
-                             void* stream);
+                             int head_dim, int num_point, const float* grad_output, const float* output,
+                             const float* save_attn, const float* save_loc, float* grad_value, float* grad_proj,
+                             float* grad_ref, void* stream);
 
 /* ---- caption-head border gather (MSDeformAttnCap) ----------------------------------------------------
  * value (N,S,M,D); value_pad_mask (N,S) or NULL; row_video (R,) int32 DEVICE: video of each query row;
