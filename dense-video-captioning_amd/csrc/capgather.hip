@@ -42,7 +42,8 @@ __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __rest
                                                               const uint8_t* __restrict__ vmask,
                                                               const int32_t* __restrict__ row_video,
                                                               const float* __restrict__ offsets, int off_stride,
-                                                              int off_col0, const float* __restrict__ ref, int rd1_rows,
+                                                              int off_col0, const float* __restrict__ off_add,
+                                                              const float* __restrict__ ref, int rd1_rows,
                                                               CapLevels lv, int S, int M, int D, int waves_per_row,
                                                               int total_waves, float* __restrict__ samples,
                                                               float* __restrict__ save_loc) {
@@ -72,7 +73,7 @@ __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __rest
 #pragma unroll
         for (int p = 0; p < cP; ++p) {
             const int j = l * cP + p;
-            const float off = orow[j];
+            const float off = off_add ? orow[j] + off_add[((size_t)r * M + m) * cNS + j] : orow[j];
             const float loc = centre_only ? r0 + off / (float)T : r0 + ((off / (float)cP) * r1) * 0.5f;
             if (save_loc && sub == (j % LPH)) save_loc[((size_t)r * M + m) * cNS + j] = loc;
             float gm;
@@ -108,8 +109,9 @@ __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __rest
 template <int CPL, int LPH, int RD>
 __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const int32_t* __restrict__ row_video,
-    const float* __restrict__ offsets, int off_stride, int off_col0, const float* __restrict__ ref, int rd1_rows,
-    CapLevels lv, int S, int M, int D, int waves_per_row, int total_waves, const float* __restrict__ save_loc,
+    const float* __restrict__ offsets, int off_stride, int off_col0, const float* __restrict__ off_add,
+    const float* __restrict__ ref, int rd1_rows, CapLevels lv, int S, int M, int D, int waves_per_row,
+    int total_waves, const float* __restrict__ save_loc,
     const float* __restrict__ gsamp, float* __restrict__ grad_value, float* __restrict__ grad_off,
     float* __restrict__ grad_ref) {
     constexpr int HPW = 64 / LPH;
@@ -202,7 +204,8 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
             const float r1 = ref[((size_t)r * cL + l) * 2 + 1];
             const float t2 = gloc * 0.5f;
             goff = (t2 * r1) / (float)cP;
-            const float o = active ? offsets[(size_t)r * off_stride + off_col0 + m * cNS + j] : 0.f;
+            float o = active ? offsets[(size_t)r * off_stride + off_col0 + m * cNS + j] : 0.f;
+            if (active && off_add) o += off_add[((size_t)r * M + m) * cNS + j];
 #pragma unroll
             for (int ll = 0; ll < cL; ++ll)
                 if (ll == l && owner) { gr0[ll] += gloc; gr1[ll] += t2 * (o / (float)cP); }
@@ -263,7 +266,8 @@ using namespace pdvc;
     }
 
 extern "C" int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* value_pad_mask, const int32_t* row_video,
-                                           const float* offsets, int off_stride, int off_col0, const float* ref,
+                                           const float* offsets, int off_stride, int off_col0, const float* off_add,
+                                           const float* ref,
                                            int ref_dim, int rd1_rows, const int32_t* level_T, int num_levels, int batch, int rows,
                                            int num_heads, int head_dim, int num_point, float* samples, float* save_loc,
                                            void* stream) {
@@ -279,10 +283,10 @@ extern "C" int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* va
     hipStream_t s = (hipStream_t)stream;
     if (ref_dim == 1) {
         CAP_DISPATCH(cap_gather_fwd_kernel, 1, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
-                     ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc)
+                     off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc)
     } else {
         CAP_DISPATCH(cap_gather_fwd_kernel, 2, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
-                     ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc)
+                     off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc)
     }
     PDVC_CHECK_LAUNCH("cap_gather_fwd_kernel");
     return PDVC_OK;
@@ -290,7 +294,8 @@ extern "C" int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* va
 
 extern "C" int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* value_pad_mask,
                                             const int32_t* row_video, const float* offsets, int off_stride,
-                                            int off_col0, const float* ref, int ref_dim, int rd1_rows,
+                                            int off_col0, const float* off_add, const float* ref, int ref_dim,
+                                            int rd1_rows,
                                             const int32_t* level_T,
                                             int num_levels, int batch, int rows, int num_heads, int head_dim,
                                             int num_point, const float* save_loc, const float* grad_samples,
@@ -302,21 +307,17 @@ extern "C" int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* v
     PDVC_CHECK_ARG(save_loc != nullptr, "backward needs save_loc from the forward");
     PDVC_CHECK_ARG(off_col0 >= 0 && off_col0 + num_heads * cNS <= off_stride, "offset columns out of range");
     hipStream_t s = (hipStream_t)stream;
-    if (grad_ref && rows > 0) {
-        hipError_t e = hipMemsetAsync(grad_ref, 0, sizeof(float) * (size_t)rows * cL * ref_dim, s);
-        if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_ref: %s", hipGetErrorString(e));
-    }
     const long tw = (long)rows * wpr;
     if (tw == 0) return PDVC_OK;
     dim3 grid((unsigned)((tw + 3) / 4));
     if (ref_dim == 1) {
         CAP_DISPATCH(cap_gather_bwd_kernel, 1, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
-                     ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples, grad_value,
-                     grad_offsets, grad_ref)
+                     off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples,
+                     grad_value, grad_offsets, grad_ref)
     } else {
         CAP_DISPATCH(cap_gather_bwd_kernel, 2, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
-                     ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples, grad_value,
-                     grad_offsets, grad_ref)
+                     off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples,
+                     grad_value, grad_offsets, grad_ref)
     }
     PDVC_CHECK_LAUNCH("cap_gather_bwd_kernel");
     return PDVC_OK;

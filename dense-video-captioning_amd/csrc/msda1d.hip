@@ -19,6 +19,8 @@
 //     issues 2 per channel per sample, ~63 MB of atomics per video at T=512, which would cap the kernel
 //     at the ~1.3 TB/s atomic rate) and every grad_value element has exactly one writer.
 //   * blocks are XCD-remapped so that all blocks of one video run on one XCD and share its L2.
+#include <cstdlib>
+
 #include "pdvc_common.h"
 
 namespace pdvc {
@@ -296,6 +298,7 @@ struct UnitMap {
     int dc[16];              // channels per slice (16, 32 or 64)
 };
 
+template <int ABL>  // diagnostic ablations (0 = the kernel): 1 = plain LDS stores, 2 = no gradient loads
 __global__ __launch_bounds__(512) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
                                                                 UnitMap um, int Lq, int S, int M, int D,
                                                                 const float* __restrict__ gout,
@@ -353,7 +356,7 @@ __global__ __launch_bounds__(512) void msda1d_bwd_value_kernel(const uint8_t* __
         for (int u = 0; u < U; ++u) {
             const float* gp = gbase + (size_t)(qv[u] < 0 ? 0 : qv[u]) * MD;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) gv[u][k] = gp[LPS * k];
+            for (int k = 0; k < 4; ++k) gv[u][k] = (ABL == 2) ? 1.f : gp[LPS * k];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -364,12 +367,17 @@ __global__ __launch_bounds__(512) void msda1d_bwd_value_kernel(const uint8_t* __
                 const float lw = x - xf, hw = 1.f - lw;
                 if (x0 >= 0) {
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) atomicAdd(&acc[x0 * LD + sub + LPS * k], hw * (gv[u][k] * att[u]));
+                    for (int k = 0; k < 4; ++k) {
+                        if (ABL == 1) acc[x0 * LD + sub + LPS * k] = hw * (gv[u][k] * att[u]);
+                        else atomicAdd(&acc[x0 * LD + sub + LPS * k], hw * (gv[u][k] * att[u]));
+                    }
                 }
                 if (x0 + 1 <= T - 1) {
 #pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        atomicAdd(&acc[(x0 + 1) * LD + sub + LPS * k], lw * (gv[u][k] * att[u]));
+                    for (int k = 0; k < 4; ++k) {
+                        if (ABL == 1) acc[(x0 + 1) * LD + sub + LPS * k] = lw * (gv[u][k] * att[u]);
+                        else atomicAdd(&acc[(x0 + 1) * LD + sub + LPS * k], lw * (gv[u][k] * att[u]));
+                    }
                 }
             }
         }
@@ -542,13 +550,27 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
     const long nblk = (long)batch * num_heads * um.nunits;
     if (nblk > 0 && num_query > 0) {
         static bool attr = false;
+        static int abl = 0;
         if (!attr) {
-            (void)hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      160 * 1024);
+            (void)hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<0>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<2>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            const char* e = getenv("PDVC_ABLATE_VALUE");  // diagnostics only (timing builds; wrong results)
+            abl = e ? atoi(e) : 0;
             attr = true;
         }
-        hipLaunchKernelGGL(msda1d_bwd_value_kernel, dim3((unsigned)nblk), dim3(512), lds, s, value_pad_mask, lv, um,
-                           num_query, S, num_heads, head_dim, grad_output, save_attn, save_loc, grad_value);
+        if (abl == 1)
+            hipLaunchKernelGGL(msda1d_bwd_value_kernel<1>, dim3((unsigned)nblk), dim3(512), lds, s, value_pad_mask, lv,
+                               um, num_query, S, num_heads, head_dim, grad_output, save_attn, save_loc, grad_value);
+        else if (abl == 2)
+            hipLaunchKernelGGL(msda1d_bwd_value_kernel<2>, dim3((unsigned)nblk), dim3(512), lds, s, value_pad_mask, lv,
+                               um, num_query, S, num_heads, head_dim, grad_output, save_attn, save_loc, grad_value);
+        else
+            hipLaunchKernelGGL(msda1d_bwd_value_kernel<0>, dim3((unsigned)nblk), dim3(512), lds, s, value_pad_mask, lv,
+                               um, num_query, S, num_heads, head_dim, grad_output, save_attn, save_loc, grad_value);
         PDVC_CHECK_LAUNCH("msda1d_bwd_value_kernel");
     } else if (nblk > 0) {
         hipError_t e = hipMemsetAsync(grad_value, 0, sizeof(float) * (size_t)batch * S * num_heads * head_dim, s);

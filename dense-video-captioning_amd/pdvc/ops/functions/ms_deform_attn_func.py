@@ -157,7 +157,7 @@ class CapGatherFunction(Function):
         samples = torch.empty((R, M, NUM_SAMPLES, D), dtype=value.dtype, device=value.device)
         save_loc = torch.empty((R, M, NUM_SAMPLES), dtype=value.dtype, device=value.device)
         _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video), _n.ptr(offsets),
-                C, off_col0, _n.ptr(ref), RD, int(rd1_rows), lvl, nl, N, R, M, D, NUM_SAMPLES // nl,
+                C, off_col0, None, _n.ptr(ref), RD, int(rd1_rows), lvl, nl, N, R, M, D, NUM_SAMPLES // nl,
                 _n.ptr(samples), _n.ptr(save_loc), _n.stream())
         ctx.save_for_backward(value, pad_mask, row_video, offsets, ref, save_loc)
         ctx.meta = (tuple(level_T), off_col0, int(rd1_rows))
@@ -175,8 +175,8 @@ class CapGatherFunction(Function):
         lvl, nl = _levels(level_T)
         gv = torch.zeros_like(value)
         go = torch.zeros_like(offsets) if C != M * NUM_SAMPLES else torch.empty_like(offsets)
-        gr = torch.empty_like(ref) if ctx.needs_input_grad[4] else None
+        gr = torch.zeros_like(ref) if ctx.needs_input_grad[4] else None
         _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video),
-                _n.ptr(offsets), C, off_col0, _n.ptr(ref), RD, rd1_rows, lvl, nl, N, R, M, D, NUM_SAMPLES // nl,
+                _n.ptr(offsets), C, off_col0, None, _n.ptr(ref), RD, rd1_rows, lvl, nl, N, R, M, D, NUM_SAMPLES // nl,
                 _n.ptr(save_loc), _n.ptr(grad_samples), _n.ptr(gv), _n.ptr(go), _n.ptr(gr), _n.stream())
         return gv, None, None, go, gr, None, None, None

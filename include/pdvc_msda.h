@@ -121,25 +121,27 @@ int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value_pad_mask, 
 
 /* ---- caption-head border gather (MSDeformAttnCap) ----------------------------------------------------
  * value (N,S,M,D); value_pad_mask (N,S) or NULL; row_video (R,) int32 DEVICE: video of each query row;
- * offsets (R, off_stride) with the M*L*P sampling offsets at column off_col0; ref (R,L,ref_dim).
- * With ref_dim 2, rows r < rd1_rows use the centre-only formula of a 1-d reference (loc = c + off / T_l;
- * the caption heads of decoder layer 0 see the 1-d initial reference, later layers the refined (c, len)
- * boxes -- pdvc/pdvc.py:249,296), so one launch serves every decoder layer's rows.
+ * offsets (R, off_stride) with the M*L*P sampling offsets at column off_col0, plus off_add (R, M*L*P) when
+ * not NULL (the caption decoder passes the h-part and the event-part of its offset projection separately);
+ * ref (R,L,ref_dim).  With ref_dim 2, rows r < rd1_rows use the centre-only formula of a 1-d reference
+ * (loc = c + off / T_l; the caption heads of decoder layer 0 see the 1-d initial reference, later layers the
+ * refined (c, len) boxes -- pdvc/pdvc.py:249,296), so one launch serves every decoder layer's rows.
  * samples (R, M, L*P, D) [the layout ShowAttendTellCore consumes after its permute, LSTM_DSA.py:241-242];
  * save_loc (R, M, L*P) (may be NULL). */
 int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* value_pad_mask, const int32_t* row_video,
-                                const float* offsets, int off_stride, int off_col0, const float* ref,
-                                int ref_dim, int rd1_rows, const int32_t* level_T, int num_levels, int batch, int rows,
-                                int num_heads, int head_dim, int num_point, float* samples, float* save_loc,
-                                void* stream);
-/* grad_value ACCUMULATED (atomic adds; zero it before the first call); grad_offsets (R, off_stride):
- * only the offset columns are written; grad_ref (R,L,ref_dim) or NULL. */
+                                const float* offsets, int off_stride, int off_col0, const float* off_add,
+                                const float* ref, int ref_dim, int rd1_rows, const int32_t* level_T, int num_levels,
+                                int batch, int rows, int num_heads, int head_dim, int num_point, float* samples,
+                                float* save_loc, void* stream);
+/* grad_value and grad_ref (R,L,ref_dim, may be NULL) are ACCUMULATED (atomic adds; zero them before the first
+ * call -- the caption decoder accumulates every step into one buffer); grad_offsets (R, off_stride): only the
+ * offset columns are written (it is also the gradient of off_add). */
 int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* value_pad_mask, const int32_t* row_video,
-                                 const float* offsets, int off_stride, int off_col0, const float* ref,
-                                 int ref_dim, int rd1_rows, const int32_t* level_T, int num_levels, int batch, int rows,
-                                 int num_heads, int head_dim, int num_point, const float* save_loc,
-                                 const float* grad_samples, float* grad_value, float* grad_offsets,
-                                 float* grad_ref, void* stream);
+                                 const float* offsets, int off_stride, int off_col0, const float* off_add,
+                                 const float* ref, int ref_dim, int rd1_rows, const int32_t* level_T, int num_levels,
+                                 int batch, int rows, int num_heads, int head_dim, int num_point,
+                                 const float* save_loc, const float* grad_samples, float* grad_value,
+                                 float* grad_offsets, float* grad_ref, void* stream);
 
 /* ---- decoder query self-attention core (nn.MultiheadAttention, batch-first) -------------------------
  * qk (N,Q,2E) = [q | k] in-projections (E = num_heads*head_dim), v (N,Q,E); key_padding_mask (N,Q) uint8,
@@ -155,6 +157,31 @@ int pdvc_mha_backward_f32(const float* qk, const float* v, const uint8_t* key_pa
                           const float* grad_out, const float* lse, int batch, int num_query, int num_heads,
                           int head_dim, float dropout_p, uint64_t seed, float* workspace, float* grad_qk,
                           float* grad_v, void* stream);
+
+/* ---- caption decoder step pieces (ShowAttendTellCore) ------------------------------------------------
+ * softattn: att (R,M,16,A) = ctx2att(samples); att_h (R, ld_att_h) = h2att(h) (A values per row);
+ * alpha_w (A), alpha_b (1) = alpha_net; clip (R,M,16,D) the samples.  att_res (R, M*D) = sum_j p_j clip_j with
+ * p = softmax_j(alpha_net(tanh(att_j + att_h))); probs (R,M,16) saved.  Supported (A, D): (512,512), (64,64),
+ * (128,128), (256,256), (512,256), (64,512). */
+int pdvc_softattn_forward_f32(const float* att, const float* att_h, int ld_att_h, const float* alpha_w,
+                              const float* alpha_b, const float* clip, int rows, int num_heads, int att_hid,
+                              int head_dim, float* att_res, float* probs, void* stream);
+/* grad_att (R,M,16,A); grad_att_h (R, ld) (summed over heads); grad_clip (R,M,16,D) = p_j * grad_res (the
+ * caller adds grad_att @ W_ctx2att); per-(row, head) partials of the alpha_net weight (R*M, A) and bias (R*M). */
+int pdvc_softattn_backward_f32(const float* att, const float* att_h, int ld_att_h, const float* alpha_w,
+                               const float* clip, const float* probs, const float* grad_res, int rows,
+                               int num_heads, int att_hid, int head_dim, float* grad_att, float* grad_att_h,
+                               int ld_grad_att_h, float* grad_clip, float* grad_alpha_w_part,
+                               float* grad_alpha_b_part, void* stream);
+/* lstm cell: gates = gates_a + gates_b + gates_c (rows x 4*hidden, each with its own row stride; b/c may be
+ * NULL), order (i,f,g,o); c_out = f*c_prev + i*g; h_out = o*tanh(c_out) (row stride ld_h_out); acts (R,4H). */
+int pdvc_lstm_cell_forward_f32(const float* gates_a, int lda, const float* gates_b, int ldb, const float* gates_c,
+                               int ldc, const float* c_prev, int rows, int hidden, float* h_out, int ld_h_out,
+                               float* c_out, float* acts, void* stream);
+/* grad_gates (R,4H), grad_c_prev (R,H) from grad_h (+ grad_h2 if not NULL) and grad_c_next (or NULL). */
+int pdvc_lstm_cell_backward_f32(const float* grad_h, int ld_grad_h, const float* grad_h2, int ld_grad_h2,
+                                const float* grad_c_next, const float* acts, const float* c_prev, const float* c,
+                                int rows, int hidden, float* grad_gates, float* grad_c_prev, void* stream);
 
 #ifdef __cplusplus
 }
