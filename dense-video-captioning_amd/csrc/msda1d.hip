@@ -13,14 +13,13 @@
 //     consecutive channels of one head (two float4 loads per corner: 1 KiB per wave-instruction over
 //     8 heads at D = 64), LPH = D / CPL lanes per head.  A (video, query) row of M*D = 512 floats is
 //     exactly one wave at PDVC's shape, so the 2 KiB output row is written by one wave.
-//   * backward-value: destination-centric.  One workgroup owns a 64-row tile of one (video, head, level)
-//     and accumulates its grad_value rows in LDS (ds_add_f32) from every sample whose two corners touch
-//     the tile, then writes the tile once with plain stores -- no global float atomics (the reference
-//     issues 2 per channel per sample, ~63 MB of atomics per video at T=512, which would cap the kernel
-//     at the ~1.3 TB/s atomic rate) and every grad_value element has exactly one writer.
+//   * backward-value: destination-centric.  One workgroup per (video, head, level) builds an inverted index
+//     of its samples in LDS (bucketed by floor of the sampling position) and sums, per grad_value row,
+//     the contributions of exactly the samples whose corners touch it -- no float atomics at all (the
+//     reference issues 2 global atomics per channel per sample, ~63 MB of atomics per video at T=512,
+//     which would cap the kernel at the ~1.3 TB/s atomic rate) and every grad_value element has
+//     exactly one writer.
 //   * blocks are XCD-remapped so that all blocks of one video run on one XCD and share its L2.
-#include <cstdlib>
-
 #include "pdvc_common.h"
 
 namespace pdvc {
@@ -283,112 +282,170 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
 }
 
 // -------------------------------------------------------------------------------------------------
-// backward, value side: one workgroup per (video, head, level, channel slice), the level's grad_value
-// rows resident in LDS.  Every level receives exactly Lq*P samples per (video, head), so the work per
-// workgroup is balanced by construction; each sample is read once, its two corner rows are accumulated
-// with ds_add_f32, and the level is written back once with plain stores (one writer per element).
-// Lanes: LPS = DC/4 lanes per sample, each owning channels {sub + LPS*k, k < 4} (dword loads coalesced
-// over the LPS lanes; consecutive banks for the LDS adds), 64/LPS samples per wave-pass, 4 passes
-// unrolled so that 16 gradient loads per lane are in flight.
+// backward, value side: destination-centric sum over an inverted index, no float atomics.
+// One workgroup per (video, head, level) and chunk of queries.  Row t of the level receives
+//     grad_value[t] = sum_{x0(s) = t} hw_s a_s g_q(s)  +  sum_{x0(s) = t-1} lw_s a_s g_q(s)
+// over the samples s = (q, p) of that level.  The workgroup buckets its samples by key = x0 + 1 in LDS
+// (counting sort: one LDS integer atomic per sample), so row t needs exactly the contiguous sorted
+// range of buckets t (high corner) and t+1 (low corner).  Each wave owns a contiguous row range chosen
+// so that the waves see equal sample counts, walks its buckets in order with two running accumulators
+// (lane = channel, one 256-B gradient row load per sample, 8 in flight) and writes every row exactly
+// once with plain coalesced stores -- rows no sample touches are written as zeros, so grad_value needs
+// no memset.  (The first version accumulated with ds_add_f32 and ran ~7x slower: LDS float atomics
+// were the kernel's whole cost, measured by replacing them with plain stores -- tools/kbench.py.)
 // -------------------------------------------------------------------------------------------------
-struct UnitMap {
-    int nunits;              // units per (video, head)
-    int level[16];
-    int cslice[16];          // channel slice index within the level
-    int dc[16];              // channels per slice (16, 32 or 64)
-};
+constexpr int kVW = 8;  // waves per value-gradient workgroup
 
-template <int ABL>  // diagnostic ablations (0 = the kernel): 1 = plain LDS stores, 2 = no gradient loads
-__global__ __launch_bounds__(512) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
-                                                                UnitMap um, int Lq, int S, int M, int D,
-                                                                const float* __restrict__ gout,
-                                                                const float* __restrict__ save_attn,
-                                                                const float* __restrict__ save_loc,
-                                                                float* __restrict__ grad_value) {
-    extern __shared__ __attribute__((aligned(16))) float acc[];  // [T_l][DC + 1]
+template <int CW>  // channels per lane: D <= 64 -> 1, D = 128 -> 2
+__global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
+                                                                     int Lq, int q0, int nq, int S, int M, int D,
+                                                                     int accumulate,
+                                                                     const float* __restrict__ gout,
+                                                                     const float* __restrict__ save_attn,
+                                                                     const float* __restrict__ save_loc,
+                                                                     float* __restrict__ grad_value) {
+    extern __shared__ __attribute__((aligned(16))) int lds_i[];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
-    const int nw = blockDim.x >> 6;
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
-    const int bm = lb / um.nunits;
-    const int unit = lb - bm * um.nunits;
+    const int l = lb % kL;  // the 4 levels of one (video, head) read the same gradient rows: same XCD
+    const int bm = lb / kL;
     const int b = bm / M, m = bm - b * M;
-    const int l = um.level[unit];
-    const int DC = um.dc[unit];
-    const int c0 = um.cslice[unit] * DC;
-    const int LPS = DC >> 2;         // lanes per sample (4 channels each, strided by LPS)
-    const int SPP = 64 / LPS;        // samples per wave-pass
-    const int LD = DC + 1;           // padded row: rows of different samples start on different banks
-    const int T = lv.T[l], st = lv.start[l];
+    const int T = lvl_sel(lv.T, l), st = lvl_sel(lv.start, l);
     const float Tf = (float)T;
-    for (int i = threadIdx.x; i < T * LD; i += blockDim.x) acc[i] = 0.f;
-    __syncthreads();
+    const int n = nq * kP;  // samples of this (video, head, level, query chunk)
+    int* off = lds_i;                       // [T + 2]: bucket counts, then exclusive offsets
+    int* cur = lds_i + (T + 2);             // [T + 2]: scatter cursors
+    int* sq = lds_i + 2 * (T + 2);          // [n] query of each sorted sample
+    float* clo = (float*)(sq + n);          // [n] hw * a  -> row x0
+    float* chi = clo + n;                   // [n] lw * a  -> row x0 + 1
+    __shared__ int wsum[kVW];
 
-    const int sub = lane % LPS;
-    const int slot = lane / LPS;
-    const int nsamp = Lq * kP;
-    const size_t MD = (size_t)M * D;
-    const float* gbase = gout + (size_t)b * Lq * MD + (size_t)m * D + c0 + sub;
+    for (int i = threadIdx.x; i < T + 2; i += blockDim.x) off[i] = 0;
+    __syncthreads();
     const size_t sbase = ((size_t)b * Lq * M + m) * kNS + l * kP;
-    // Interleaved assignment: the SPP*nw lanes-groups of one pass take samples nsamp/(SPP*nw) apart, so the
-    // samples of one LDS atomic instruction come from distant queries (distinct rows); neighbouring queries
-    // sample the same rows and would otherwise serialise on same-address ds_add_f32.
-    const int groups = SPP * nw;
-    const int gidx = wid * SPP + slot;
-    const int per = (nsamp + groups - 1) / groups;
-    constexpr int U = 8;  // samples per lane per iteration: 8 loc/attn loads, then 32 gradient loads in flight
-    for (int it = 0; it < per; it += U) {
-        float loc[U], att[U];
-        int qv[U];
+    // 1) histogram of key = x0 + 1 in [0, T] (samples outside (-1, T) touch no row, as in the reference)
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int q = q0 + i / kP, p = i % kP;
+        const float x = save_loc[sbase + (size_t)q * M * kNS + p] * Tf - 0.5f;
+        if (x > -1.f && x < Tf) atomicAdd(&off[(int)floorf(x) + 1], 1);
+    }
+    __syncthreads();
+    // 2) exclusive scan of off[0 .. T+1] (off[T+1] = 0 before, total after): per-thread chunks + wave scan
+    {
+        const int len = T + 2;
+        const int per = (len + blockDim.x - 1) / blockDim.x;
+        const int i0 = threadIdx.x * per;
+        int tot = 0;
+        for (int i = i0; i < i0 + per && i < len; ++i) tot += off[i];
+        int inc = tot;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            int i = gidx * per + it + u;
-            const bool ok = (it + u < per) && i < nsamp;
-            i = ok ? i : 0;
-            const int q = i / kP, p = i - q * kP;
-            qv[u] = ok ? q : -1;
-            const size_t si = sbase + (size_t)q * M * kNS + p;
-            loc[u] = save_loc[si];
-            att[u] = save_attn[si];
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += y;
         }
-        float gv[U][4];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const float* gp = gbase + (size_t)(qv[u] < 0 ? 0 : qv[u]) * MD;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) gv[u][k] = (ABL == 2) ? 1.f : gp[LPS * k];
+        if (lane == 63) wsum[wid] = inc;
+        __syncthreads();
+        int base = 0;
+        for (int w = 0; w < wid; ++w) base += wsum[w];
+        int run = base + inc - tot;
+        for (int i = i0; i < i0 + per && i < len; ++i) {
+            const int c = off[i];
+            off[i] = run;
+            cur[i] = run;
+            run += c;
         }
+    }
+    __syncthreads();
+    // 3) scatter the samples into bucket order with their two corner coefficients
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int q = q0 + i / kP, p = i % kP;
+        const size_t si = sbase + (size_t)q * M * kNS + p;
+        const float x = save_loc[si] * Tf - 0.5f;
+        if (x > -1.f && x < Tf) {
+            const float xf = floorf(x);
+            const float lw = x - xf, a = save_attn[si];
+            const int pos = atomicAdd(&cur[(int)xf + 1], 1);
+            sq[pos] = q;
+            clo[pos] = (1.f - lw) * a;
+            chi[pos] = lw * a;
+        }
+    }
+    __syncthreads();
+    // 4) wave wid owns rows [r0, r1): split points balance the sorted samples over the waves
+    const int total = off[T + 1];
+    auto split = [&](int w) -> int {
+        if (w <= 0) return 0;
+        if (w >= kVW) return T;
+        const int target = (int)(((long)total * w) / kVW);
+        int lo = 0, hi = T;  // smallest k in [0, T] with off[k] >= target
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (off[mid] >= target) hi = mid;
+            else lo = mid + 1;
+        }
+        return lo;
+    };
+    const int r0 = split(wid), r1 = split(wid + 1);
+    if (r0 >= r1) return;
+    const size_t MD = (size_t)M * D;
+    const float* gb = gout + (size_t)b * Lq * MD + (size_t)m * D;
+    float* ob = grad_value + ((size_t)b * S + st) * MD + (size_t)m * D;
+    const uint8_t* mrow = vmask ? vmask + (size_t)b * S + st : nullptr;
+    float accp[CW], acch[CW];  // rows k-1 and k
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const float x = loc[u] * Tf - 0.5f;
-            if (qv[u] >= 0 && x > -1.f && x < Tf) {
-                const float xf = floorf(x);
-                const int x0 = (int)xf;
-                const float lw = x - xf, hw = 1.f - lw;
-                if (x0 >= 0) {
+    for (int c = 0; c < CW; ++c) accp[c] = acch[c] = 0.f;
+    int k = r0;
+    auto close_bucket = [&]() {  // bucket k is complete: row k-1 has both its corners
+        const int r = k - 1;
+        if (r >= r0) {
+            const bool zero = mrow && mrow[r];
+            float* orow = ob + (size_t)r * MD;
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        if (ABL == 1) acc[x0 * LD + sub + LPS * k] = hw * (gv[u][k] * att[u]);
-                        else atomicAdd(&acc[x0 * LD + sub + LPS * k], hw * (gv[u][k] * att[u]));
-                    }
-                }
-                if (x0 + 1 <= T - 1) {
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        if (ABL == 1) acc[(x0 + 1) * LD + sub + LPS * k] = lw * (gv[u][k] * att[u]);
-                        else atomicAdd(&acc[(x0 + 1) * LD + sub + LPS * k], lw * (gv[u][k] * att[u]));
-                    }
+            for (int c = 0; c < CW; ++c) {
+                const int ch = lane + 64 * c;
+                if (ch < D) {
+                    float v = zero ? 0.f : accp[c];
+                    if (accumulate) v += orow[ch];
+                    orow[ch] = v;
                 }
             }
         }
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+            accp[c] = acch[c];
+            acch[c] = 0.f;
+        }
+        ++k;
+    };
+    const int jb = off[r0], je = off[r1 + 1];
+    constexpr int U = 8;
+    for (int j0 = jb; j0 < je; j0 += U) {
+        float gv[U][CW];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = (j0 + u < je) ? j0 + u : je - 1;
+            const float* gp = gb + (size_t)sq[j] * MD;
+#pragma unroll
+            for (int c = 0; c < CW; ++c) {
+                const int ch = lane + 64 * c;
+                gv[u][c] = gp[ch < D ? ch : 0];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = j0 + u;
+            if (j >= je) break;
+            while (j >= off[k + 1]) close_bucket();
+            const float cl = clo[j], chh = chi[j];
+#pragma unroll
+            for (int c = 0; c < CW; ++c) {
+                accp[c] = fmaf(cl, gv[u][c], accp[c]);
+                acch[c] = fmaf(chh, gv[u][c], acch[c]);
+            }
+        }
     }
-    __syncthreads();
-    const uint8_t* mrow = vmask ? vmask + (size_t)b * S + st : nullptr;
-    for (int i = threadIdx.x; i < T * DC; i += blockDim.x) {
-        const int r = i / DC, c = i - r * DC;
-        const float v = (mrow && mrow[r]) ? 0.f : acc[r * LD + c];
-        grad_value[((size_t)b * S + st + r) * MD + (size_t)m * D + c0 + c] = v;
-    }
+    while (k <= r1) close_bucket();
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -525,56 +582,48 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
                              grad_proj, grad_ref);
         PDVC_CHECK_LAUNCH("msda1d_bwd_query_kernel");
     }
-    // grad_value: one workgroup per (video, head, level, channel slice); slices keep every LDS tile
-    // <= ~68 KiB (two 512-thread workgroups per CU) with 16..64 channels per slice
-    UnitMap um;
-    um.nunits = 0;
-    size_t lds = 0;
-    for (int l = 0; l < kL; ++l) {
-        int dc = head_dim < 64 ? head_dim : 64;
-        while ((size_t)lv.T[l] * (dc + 1) * 4 > 68 * 1024 && dc > 16) dc /= 2;
-        if (head_dim % dc != 0 || dc % 4 != 0 || (64 % (dc / 4)) != 0)
-            return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "head_dim %d cannot be sliced for the value gradient", head_dim);
-        const size_t need = sizeof(float) * (size_t)lv.T[l] * (dc + 1);
-        if (need > 160 * 1024)
-            return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "level %d (T=%d) too long for the LDS value tile", l, lv.T[l]);
-        if (need > lds) lds = need;
-        for (int c = 0; c < head_dim / dc; ++c) {
-            if (um.nunits >= 16) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "too many value-gradient units");
-            um.level[um.nunits] = l;
-            um.cslice[um.nunits] = c;
-            um.dc[um.nunits] = dc;
-            ++um.nunits;
+    // grad_value: one workgroup per (video, head, level) and query chunk; the chunk keeps the LDS index
+    // (2 (T+2) ints + 12 B per sample) within 96 KiB; later chunks add into the rows the first wrote
+    PDVC_CHECK_ARG(head_dim <= 128, "value gradient supports head_dim <= 128, got %d", head_dim);
+    const long nblk = (long)batch * num_heads * kL;
+    if (nblk > 0) {
+        if (num_query == 0) {
+            hipError_t e = hipMemsetAsync(grad_value, 0, sizeof(float) * (size_t)batch * S * num_heads * head_dim, s);
+            if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_value: %s", hipGetErrorString(e));
+            return PDVC_OK;
         }
-    }
-    const long nblk = (long)batch * num_heads * um.nunits;
-    if (nblk > 0 && num_query > 0) {
+        int Tmax = 0;
+        for (int l = 0; l < kL; ++l) Tmax = lv.T[l] > Tmax ? lv.T[l] : Tmax;
+        const long budget = 96 * 1024 - 8L * (Tmax + 2);
+        if (budget < 12L * kP) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "level length %d too long", Tmax);
+        int qchunk = (int)(budget / (12L * kP));
+        if (qchunk > num_query) qchunk = num_query;
         static bool attr = false;
-        static int abl = 0;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<0>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<2>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            const char* e = getenv("PDVC_ABLATE_VALUE");  // diagnostics only (timing builds; wrong results)
-            abl = e ? atoi(e) : 0;
+        if (!attr) {  // dynamic LDS <= 96 KiB by construction of qchunk (plus 32 B static)
+            hipError_t e1 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+            hipError_t e2 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<2>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+            if (e1 != hipSuccess || e2 != hipSuccess) {
+                (void)hipGetLastError();
+                return pdvc_set_error(PDVC_ERR_LAUNCH, "msda1d_bwd_value_kernel: cannot raise the LDS limit");
+            }
             attr = true;
         }
-        if (abl == 1)
-            hipLaunchKernelGGL(msda1d_bwd_value_kernel<1>, dim3((unsigned)nblk), dim3(512), lds, s, value_pad_mask, lv,
-                               um, num_query, S, num_heads, head_dim, grad_output, save_attn, save_loc, grad_value);
-        else if (abl == 2)
-            hipLaunchKernelGGL(msda1d_bwd_value_kernel<2>, dim3((unsigned)nblk), dim3(512), lds, s, value_pad_mask, lv,
-                               um, num_query, S, num_heads, head_dim, grad_output, save_attn, save_loc, grad_value);
-        else
-            hipLaunchKernelGGL(msda1d_bwd_value_kernel<0>, dim3((unsigned)nblk), dim3(512), lds, s, value_pad_mask, lv,
-                               um, num_query, S, num_heads, head_dim, grad_output, save_attn, save_loc, grad_value);
-        PDVC_CHECK_LAUNCH("msda1d_bwd_value_kernel");
-    } else if (nblk > 0) {
-        hipError_t e = hipMemsetAsync(grad_value, 0, sizeof(float) * (size_t)batch * S * num_heads * head_dim, s);
-        if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_value: %s", hipGetErrorString(e));
+        for (int q0 = 0; q0 < num_query; q0 += qchunk) {
+            const int nq = (num_query - q0) < qchunk ? (num_query - q0) : qchunk;
+            const size_t lds = sizeof(int) * (2 * (size_t)(Tmax + 2) + 3 * (size_t)nq * kP);
+            const int acc = q0 > 0;
+            if (head_dim <= 64)
+                hipLaunchKernelGGL(msda1d_bwd_value_kernel<1>, dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
+                                   value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
+                                   save_attn, save_loc, grad_value);
+            else
+                hipLaunchKernelGGL(msda1d_bwd_value_kernel<2>, dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
+                                   value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
+                                   save_attn, save_loc, grad_value);
+            PDVC_CHECK_LAUNCH("msda1d_bwd_value_kernel");
+        }
     }
     return PDVC_OK;
 }
