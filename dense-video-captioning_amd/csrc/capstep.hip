@@ -18,23 +18,24 @@ constexpr int sNS = 16;
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
-// att (R, M, 16, A) contiguous; att_h (R, ldh) [A values at column 0 of the pointer]; clip (R, M, 16, D)
-template <int APL, int DPL>  // hidden / value floats per lane (A = 64*APL, D = 64*DPL)
+// att (R, M, 16, A) contiguous; att_h (R, ldh) [A values at column 0 of the pointer]; clip (R, M, 16, D).
+// APL / DPL are the per-lane maxima (A <= 64*APL, D <= 64*DPL); columns past A / D are masked.
+template <int APL, int DPL>
 __global__ __launch_bounds__(256) void softattn_fwd_kernel(const float* __restrict__ att, const float* __restrict__ att_h,
                                                            int ldh, const float* __restrict__ aw,
                                                            const float* __restrict__ ab, const float* __restrict__ clip,
-                                                           int R, int M, float* __restrict__ res,
+                                                           int R, int M, int A, int D, float* __restrict__ res,
                                                            float* __restrict__ probs) {
     const int lane = threadIdx.x & 63;
     const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (wave >= R * M) return;
-    const int r = wave / M, m = wave - r * M;
-    constexpr int A = 64 * APL, D = 64 * DPL;
+    const int r = wave / M;
     float hv[APL], wv[APL];
 #pragma unroll
     for (int k = 0; k < APL; ++k) {
-        hv[k] = att_h[(size_t)r * ldh + lane + 64 * k];
-        wv[k] = aw[lane + 64 * k];
+        const int a = lane + 64 * k;
+        hv[k] = a < A ? att_h[(size_t)r * ldh + a] : 0.f;
+        wv[k] = a < A ? aw[a] : 0.f;
     }
     const float* ab_ = att + (size_t)wave * sNS * A;
     float part[sNS];
@@ -42,7 +43,10 @@ __global__ __launch_bounds__(256) void softattn_fwd_kernel(const float* __restri
     for (int j = 0; j < sNS; ++j) {
         float s = 0.f;
 #pragma unroll
-        for (int k = 0; k < APL; ++k) s += tanhf(ab_[j * A + lane + 64 * k] + hv[k]) * wv[k];
+        for (int k = 0; k < APL; ++k) {
+            const int a = lane + 64 * k;
+            if (a < A) s += tanhf(ab_[j * A + a] + hv[k]) * wv[k];
+        }
         part[j] = s;
     }
     group_reduce_scatter<sNS, 16>(part, lane);   // lane%16 -> dot of sample lane%16 (partial over 16-lane group)
@@ -68,10 +72,16 @@ __global__ __launch_bounds__(256) void softattn_fwd_kernel(const float* __restri
     for (int j = 0; j < sNS; ++j) {
         const float pj = __shfl(p, j, PDVC_WAVE);
 #pragma unroll
-        for (int k = 0; k < DPL; ++k) o[k] += pj * cb[j * D + lane + 64 * k];
+        for (int k = 0; k < DPL; ++k) {
+            const int d = lane + 64 * k;
+            if (d < D) o[k] += pj * cb[j * D + d];
+        }
     }
 #pragma unroll
-    for (int k = 0; k < DPL; ++k) res[(size_t)wave * D + lane + 64 * k] = o[k];
+    for (int k = 0; k < DPL; ++k) {
+        const int d = lane + 64 * k;
+        if (d < D) res[(size_t)wave * D + d] = o[k];
+    }
 }
 
 // backward: grad_res (R, M*D) -> grad_att (R,M,16,A), grad_att_h (R,A) (summed over heads), grad_clip
@@ -82,7 +92,7 @@ __global__ __launch_bounds__(256) void softattn_bwd_kernel(const float* __restri
                                                            int ldh, const float* __restrict__ aw,
                                                            const float* __restrict__ clip,
                                                            const float* __restrict__ probs,
-                                                           const float* __restrict__ gres, int R, int M,
+                                                           const float* __restrict__ gres, int R, int M, int A, int D,
                                                            float* __restrict__ gatt, float* __restrict__ gatt_h,
                                                            int ldgh, float* __restrict__ gclip,
                                                            float* __restrict__ gaw_part, float* __restrict__ gab_part) {
@@ -90,14 +100,16 @@ __global__ __launch_bounds__(256) void softattn_bwd_kernel(const float* __restri
     const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (wave >= R * M) return;
     const int r = wave / M;
-    constexpr int A = 64 * APL, D = 64 * DPL;
     const float* cb = clip + (size_t)wave * sNS * D;
     float* gcb = gclip + (size_t)wave * sNS * D;
     float g[DPL];
 #pragma unroll
-    for (int k = 0; k < DPL; ++k) g[k] = gres[(size_t)wave * D + lane + 64 * k];
+    for (int k = 0; k < DPL; ++k) {
+        const int d = lane + 64 * k;
+        g[k] = d < D ? gres[(size_t)wave * D + d] : 0.f;
+    }
     const float p = (lane < sNS) ? probs[(size_t)wave * sNS + lane] : 0.f;
-    // d p_j = sum_d g_d clip_j[d]; grad_clip_j += p_j g
+    // d p_j = sum_d g_d clip_j[d]; grad_clip_j = p_j g
     float part[sNS];
 #pragma unroll
     for (int j = 0; j < sNS; ++j) {
@@ -105,9 +117,12 @@ __global__ __launch_bounds__(256) void softattn_bwd_kernel(const float* __restri
         float s = 0.f;
 #pragma unroll
         for (int k = 0; k < DPL; ++k) {
-            const size_t idx = (size_t)j * D + lane + 64 * k;
-            s += g[k] * cb[idx];
-            gcb[idx] = pj * g[k];
+            const int d = lane + 64 * k;
+            if (d < D) {
+                const size_t idx = (size_t)j * D + d;
+                s += g[k] * cb[idx];
+                gcb[idx] = pj * g[k];
+            }
         }
         part[j] = s;
     }
@@ -128,8 +143,9 @@ __global__ __launch_bounds__(256) void softattn_bwd_kernel(const float* __restri
     float hv[APL], wv[APL], gh[APL], gw[APL];
 #pragma unroll
     for (int k = 0; k < APL; ++k) {
-        hv[k] = att_h[(size_t)r * ldh + lane + 64 * k];
-        wv[k] = aw[lane + 64 * k];
+        const int a = lane + 64 * k;
+        hv[k] = a < A ? att_h[(size_t)r * ldh + a] : 0.f;
+        wv[k] = a < A ? aw[a] : 0.f;
         gh[k] = 0.f;
         gw[k] = 0.f;
     }
@@ -140,18 +156,24 @@ __global__ __launch_bounds__(256) void softattn_bwd_kernel(const float* __restri
         const float dj = __shfl(ddot, j, PDVC_WAVE);
 #pragma unroll
         for (int k = 0; k < APL; ++k) {
-            const float th = tanhf(ab_[j * A + lane + 64 * k] + hv[k]);
-            const float dpre = dj * wv[k] * (1.f - th * th);
-            gab_[j * A + lane + 64 * k] = dpre;
-            gh[k] += dpre;
-            gw[k] += dj * th;
+            const int a = lane + 64 * k;
+            if (a < A) {
+                const float th = tanhf(ab_[j * A + a] + hv[k]);
+                const float dpre = dj * wv[k] * (1.f - th * th);
+                gab_[j * A + a] = dpre;
+                gh[k] += dpre;
+                gw[k] += dj * th;
+            }
         }
     }
 #pragma unroll
     for (int k = 0; k < APL; ++k) {
-        if (M == 1) gatt_h[(size_t)r * ldgh + lane + 64 * k] = gh[k];
-        else atomicAdd(&gatt_h[(size_t)r * ldgh + lane + 64 * k], gh[k]);
-        gaw_part[(size_t)wave * A + lane + 64 * k] = gw[k];
+        const int a = lane + 64 * k;
+        if (a < A) {
+            if (M == 1) gatt_h[(size_t)r * ldgh + a] = gh[k];
+            else atomicAdd(&gatt_h[(size_t)r * ldgh + a], gh[k]);
+            gaw_part[(size_t)wave * A + a] = gw[k];
+        }
     }
 }
 
@@ -190,7 +212,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(const float* __restrict__
                                                        int lddh2, const float* __restrict__ dc_next,
                                                        const float* __restrict__ acts, const float* __restrict__ c_prev,
                                                        const float* __restrict__ c, int R, int H,
-                                                       float* __restrict__ dgates, float* __restrict__ dc_prev) {
+                                                       float* __restrict__ dgates, int ldg, float* __restrict__ dc_prev) {
     const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (long)R * H) return;
     const int r = (int)(idx / H), u = (int)(idx - (long)r * H);
@@ -202,7 +224,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(const float* __restrict__
     float dc = gh * o * (1.f - tc * tc);
     if (dc_next) dc += dc_next[idx];
     const float dO = gh * tc, dI = dc * g, dG = dc * i, dF = dc * c_prev[idx];
-    float* d = dgates + (size_t)r * 4 * H;
+    float* d = dgates + (size_t)r * ldg;
     d[u] = dI * i * (1.f - i);
     d[H + u] = dF * f * (1.f - f);
     d[2 * H + u] = dG * (1.f - g * g);
@@ -214,15 +236,24 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(const float* __restrict__
 
 using namespace pdvc;
 
-#define SA_DISPATCH(KERNEL, A, D, ...)                                                                           \
-    do {                                                                                                         \
-        if (A == 512 && D == 512) hipLaunchKernelGGL((KERNEL<8, 8>), __VA_ARGS__);                              \
-        else if (A == 64 && D == 64) hipLaunchKernelGGL((KERNEL<1, 1>), __VA_ARGS__);                           \
-        else if (A == 128 && D == 128) hipLaunchKernelGGL((KERNEL<2, 2>), __VA_ARGS__);                         \
-        else if (A == 256 && D == 256) hipLaunchKernelGGL((KERNEL<4, 4>), __VA_ARGS__);                         \
-        else if (A == 512 && D == 256) hipLaunchKernelGGL((KERNEL<8, 4>), __VA_ARGS__);                         \
-        else if (A == 64 && D == 512) hipLaunchKernelGGL((KERNEL<1, 8>), __VA_ARGS__);                          \
-        else return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "soft attention: unsupported (A=%d, D=%d)", A, D);     \
+static int pow2_lanes(int n) {  // per-lane maximum for n columns over 64 lanes: 1, 2, 4 or 8 (0 if n > 512)
+    const int k = (n + 63) / 64;
+    return k <= 1 ? 1 : k <= 2 ? 2 : k <= 4 ? 4 : k <= 8 ? 8 : 0;
+}
+
+#define SA_CASE(KERNEL, PA, PD, ...) \
+    else if (pa == PA && pd == PD) hipLaunchKernelGGL((KERNEL<PA, PD>), __VA_ARGS__)
+#define SA_DISPATCH(KERNEL, A, D, ...)                                                                       \
+    do {                                                                                                     \
+        const int pa = pow2_lanes(A), pd = pow2_lanes(D);                                                    \
+        if (A <= 0 || D <= 0 || pa == 0 || pd == 0)                                                          \
+            return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "soft attention: need 0 < A, D <= 512 (A=%d, D=%d)", A, D); \
+        SA_CASE(KERNEL, 1, 1, __VA_ARGS__); SA_CASE(KERNEL, 1, 2, __VA_ARGS__); SA_CASE(KERNEL, 1, 4, __VA_ARGS__); \
+        SA_CASE(KERNEL, 1, 8, __VA_ARGS__); SA_CASE(KERNEL, 2, 1, __VA_ARGS__); SA_CASE(KERNEL, 2, 2, __VA_ARGS__); \
+        SA_CASE(KERNEL, 2, 4, __VA_ARGS__); SA_CASE(KERNEL, 2, 8, __VA_ARGS__); SA_CASE(KERNEL, 4, 1, __VA_ARGS__); \
+        SA_CASE(KERNEL, 4, 2, __VA_ARGS__); SA_CASE(KERNEL, 4, 4, __VA_ARGS__); SA_CASE(KERNEL, 4, 8, __VA_ARGS__); \
+        SA_CASE(KERNEL, 8, 1, __VA_ARGS__); SA_CASE(KERNEL, 8, 2, __VA_ARGS__); SA_CASE(KERNEL, 8, 4, __VA_ARGS__); \
+        SA_CASE(KERNEL, 8, 8, __VA_ARGS__);                                                                  \
     } while (0)
 
 extern "C" int pdvc_softattn_forward_f32(const float* att, const float* att_h, int ld_att_h, const float* alpha_w,
@@ -234,7 +265,7 @@ extern "C" int pdvc_softattn_forward_f32(const float* att, const float* att_h, i
     dim3 grid((unsigned)((waves + 3) / 4)), block(256);
     hipStream_t s = (hipStream_t)stream;
     SA_DISPATCH(softattn_fwd_kernel, att_hid, head_dim, grid, block, 0, s, att, att_h, ld_att_h, alpha_w, alpha_b,
-                clip, rows, num_heads, att_res, probs);
+                clip, rows, num_heads, att_hid, head_dim, att_res, probs);
     PDVC_CHECK_LAUNCH("softattn_fwd_kernel");
     return PDVC_OK;
 }
@@ -255,7 +286,7 @@ extern "C" int pdvc_softattn_backward_f32(const float* att, const float* att_h, 
     }
     dim3 grid((unsigned)((waves + 3) / 4)), block(256);
     SA_DISPATCH(softattn_bwd_kernel, att_hid, head_dim, grid, block, 0, s, att, att_h, ld_att_h, alpha_w, clip, probs,
-                grad_res, rows, num_heads, grad_att, grad_att_h, ld_grad_att_h, grad_clip, grad_alpha_w_part,
+                grad_res, rows, num_heads, att_hid, head_dim, grad_att, grad_att_h, ld_grad_att_h, grad_clip, grad_alpha_w_part,
                 grad_alpha_b_part);
     PDVC_CHECK_LAUNCH("softattn_bwd_kernel");
     return PDVC_OK;
@@ -276,13 +307,13 @@ extern "C" int pdvc_lstm_cell_forward_f32(const float* gates_a, int lda, const f
 extern "C" int pdvc_lstm_cell_backward_f32(const float* grad_h, int ld_grad_h, const float* grad_h2, int ld_grad_h2,
                                            const float* grad_c_next, const float* acts, const float* c_prev,
                                            const float* c, int rows, int hidden, float* grad_gates,
-                                           float* grad_c_prev, void* stream) {
-    PDVC_CHECK_ARG(rows >= 0 && hidden > 0, "invalid sizes");
+                                           int ld_grad_gates, float* grad_c_prev, void* stream) {
+    PDVC_CHECK_ARG(rows >= 0 && hidden > 0 && ld_grad_gates >= 4 * hidden, "invalid sizes");
     const long n = (long)rows * hidden;
     if (n == 0) return PDVC_OK;
     hipLaunchKernelGGL(lstm_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, grad_h,
                        ld_grad_h, grad_h2, ld_grad_h2, grad_c_next, acts, c_prev, c, rows, hidden, grad_gates,
-                       grad_c_prev);
+                       ld_grad_gates, grad_c_prev);
     PDVC_CHECK_LAUNCH("lstm_bwd_kernel");
     return PDVC_OK;
 }

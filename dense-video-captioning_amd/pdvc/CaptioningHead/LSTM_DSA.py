@@ -12,7 +12,10 @@ core.ctx2att, core.h2att, core.alpha_net) and the same per-step math, restructur
     h2att, W_hh) are one GEMM;
   * the caption logits (logit + log_softmax) are one GEMM over all steps after the recurrence;
   * the border-padded deformable sampling is the HIP caption-gather kernel; rows of decoder layer 0 (1-d
-    reference) and later layers ((c, len) references) share one launch.
+    reference) and later layers ((c, len) references) share one launch;
+  * training runs the whole recurrence as one autograd function (ops/functions/caption_decode.py): 6 launches
+    per step forward and backward (GEMMs + the gather, soft-attention and LSTM-cell kernels), weight gradients
+    as single GEMMs over all steps.
 The teacher-forced loop length is computed on the host from the caption lengths (the reference stops at the
 first all-zero token column, LSTM_DSA.py:103-104): the same steps are computed, without a per-step sync.
 """
@@ -22,6 +25,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from pdvc.ops.functions import CaptionDecodeFunction
 from pdvc.ops.modules import MSDeformAttnCap
 
 
@@ -172,23 +176,20 @@ class LSTMDSACaptioner(Captioner):
                               n_steps):
         """hs_rows (R, d) event features; ref_rows (R, L, 2) references (rows < rd1_rows are 1-d: centre in
         [..., 0]); row_video (R,) int32; memory (N, S, d); seq (R, K) long; returns logprobs (R, n_steps, V)."""
-        R = hs_rows.shape[0]
+        core = self.core
         w = self._step_weights()
         value, mask_u8 = self._prepare(memory, mask_flatten)
+        if n_steps == 0:
+            return hs_rows.new_zeros(hs_rows.shape[0], 0, self.vocab_size + 1)
         xt = self.embed(seq[:, :n_steps])  # (R, n, E)
-        x_gates = F.linear(xt, w["W_x"])  # (R, n, 4H)
-        hs_part = F.linear(hs_rows, w["W_hs"])
+        xg = F.linear(xt, w["W_x"]) + F.linear(hs_rows, w["W_hs"])[:, None]  # loop-invariant gate parts
         off_hs = F.linear(hs_rows, w["W_off_hs"], w["b_off"])
-        h = hs_rows.new_zeros(R, w["H"])
-        c = hs_rows.new_zeros(R, w["H"])
-        outs = []
-        for i in range(n_steps):
-            h, c = self._step(w, h, c, x_gates[:, i], hs_part, off_hs, value, mask_u8, row_video, ref_rows,
-                              rd1_rows, level_T)
-            outs.append(h)
-        if not outs:
-            return hs_rows.new_zeros(R, 0, self.vocab_size + 1)
-        Hs = torch.stack(outs, 1)
+        Nv, S, _ = value.shape
+        M = core.deformable_att.n_heads
+        Hs = CaptionDecodeFunction.apply(
+            value.view(Nv, S, M, -1), xg, off_hs, ref_rows, w["W_h"], w["b_h"], core.ctx2att.weight,
+            core.ctx2att.bias, core.alpha_net.weight.view(-1), core.alpha_net.bias, w["W_att"], mask_u8, row_video,
+            tuple(level_T), rd1_rows)
         return F.log_softmax(self.logit(self.dropout(Hs)), dim=-1)
 
     @torch.no_grad()

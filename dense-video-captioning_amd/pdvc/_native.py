@@ -30,7 +30,7 @@ SIGNATURES = {
     "pdvc_softattn_forward_f32": [_vp, _vp, _i, _vp, _vp, _vp] + [_i] * 4 + [_vp] * 3,
     "pdvc_softattn_backward_f32": [_vp, _vp, _i, _vp, _vp, _vp, _vp] + [_i] * 4 + [_vp, _vp, _i, _vp, _vp, _vp, _vp],
     "pdvc_lstm_cell_forward_f32": [_vp, _i, _vp, _i, _vp, _i, _vp, _i, _i, _vp, _i, _vp, _vp, _vp],
-    "pdvc_lstm_cell_backward_f32": [_vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp],
+    "pdvc_lstm_cell_backward_f32": [_vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _i, _vp, _vp],
     "pdvc_mha_forward_f32": [_vp, _vp, _u8p] + [_i] * 4 + [_f, _u64] + [_vp] * 3,
     "pdvc_mha_backward_f32": [_vp, _vp, _u8p, _vp, _vp, _vp] + [_i] * 4 + [_f, _u64] + [_vp] * 4,
 }
@@ -107,6 +107,16 @@ def ptr(t):
     if not t.is_contiguous():
         raise NativeError("PDVC HIP ops need contiguous tensors")
     return ctypes.c_void_p(t.data_ptr())
+
+
+def rows(t):
+    """(pointer, row stride) of a 2-D row-strided view (unit column stride), e.g. a column block of a wider
+    matrix; the kernels take the row stride as an argument."""
+    if not t.is_cuda:
+        raise NativeError("PDVC HIP ops need GPU tensors (there is no CPU implementation)")
+    if t.dim() != 2 or (t.stride(1) != 1 and t.shape[1] > 1):
+        raise NativeError(f"expected a 2-D row-strided view, got shape {tuple(t.shape)} strides {t.stride()}")
+    return ctypes.c_void_p(t.data_ptr()), t.stride(0)
 
 
 def stream():

@@ -1,2 +1,3 @@
 from .ms_deform_attn_func import (MSDeformAttnFunction, ms_deform_attn_core_pytorch, MSDA1dFunction, NUM_SAMPLES_FUSED,
                                   CapGatherFunction)
+from .caption_decode import CaptionDecodeFunction

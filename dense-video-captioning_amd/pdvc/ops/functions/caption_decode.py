@@ -1,0 +1,146 @@
+"""The teacher-forced LSTM-DSA caption recurrence as ONE autograd function (forward and backward).
+
+Reference: ShowAttendTellCore.forward (pdvc/CaptioningHead/LSTM_DSA.py:231-263) called once per token by
+Captioner.forward (LSTM_DSA.py:55-109).  Per step and row (h, c start at zero):
+    hp      = [W_off_h ; W_h2att ; W_hh] h_{t-1} + [0 ; b_h2att ; 0]            (one GEMM)
+    clip    = border samples of value at  ref (+) (hp[:, :16] + off_hs)          (cap-gather kernel)
+    att     = ctx2att(clip)                                                      (one GEMM, R*16 rows)
+    res     = sum_j softmax_j(alpha_net(tanh(att_j + hp[:, h2att]))) clip_j      (soft-attention kernel)
+    gates   = xg_t + W_att res + hp[:, W_hh]                                     (one GEMM + LSTM kernel)
+    h, c    = LSTM cell(gates, c)
+xg_t = W_x embed(token_t) + W_hs hs and off_hs = W_off_hs hs + b_off are loop invariants computed by the
+caller (with autograd).  Autograd of the stock modules issues ~25 kernels per step forward and ~50
+backward; here it is 6 launches per step each way, and every weight gradient is ONE GEMM over all steps
+after the backward loop (the per-step activations are kept: ~0.5 MB per row per step at PDVC's shape).
+"""
+import torch
+from torch.autograd import Function
+from torch.autograd.function import once_differentiable
+
+from pdvc import _native as _n
+from .ms_deform_attn_func import NUM_SAMPLES, _levels
+
+
+class CaptionDecodeFunction(Function):
+    """value (Nv,S,M,D) = value_proj(memory); xg (R,n,4H); off_hs (R, M*16); ref (R,L,1|2) (first rd1_rows rows
+    1-d when 2-wide); W_h (M*16 + A + 4H, H), b_h; W_ctx (A, D), b_ctx (A); alpha_w (A,), alpha_b (1,);
+    W_att (4H, M*D).  Returns the hidden states (R, n, H)."""
+
+    @staticmethod
+    def forward(ctx, value, xg, off_hs, ref, W_h, b_h, W_ctx, b_ctx, alpha_w, alpha_b, W_att, pad_mask, row_video,
+                level_T, rd1_rows):
+        value, xg, off_hs, ref = value.contiguous(), xg.contiguous(), off_hs.contiguous(), ref.contiguous()
+        W_h, W_ctx, W_att = W_h.contiguous(), W_ctx.contiguous(), W_att.contiguous()
+        alpha_w, alpha_b = alpha_w.contiguous(), alpha_b.contiguous()
+        Nv, S, M, D = value.shape
+        R, n, G = xg.shape
+        H = G // 4
+        A = W_ctx.shape[0]
+        NS = NUM_SAMPLES
+        n_off = M * NS
+        Ph = W_h.shape[0]
+        if Ph != n_off + A + G or W_att.shape != (G, M * D) or off_hs.shape != (R, n_off):
+            raise ValueError("caption decode: inconsistent weight shapes")
+        RD = ref.shape[2]
+        lvl, nl = _levels(level_T)
+        kw = dict(dtype=value.dtype, device=value.device)
+        HP = torch.empty((n, R, Ph), **kw)
+        CLIP = torch.empty((n, R, M, NS, D), **kw)
+        LOC = torch.empty((n, R, M, NS), **kw)
+        ATT = torch.empty((n, R * M * NS, A), **kw)
+        PROBS = torch.empty((n, R, M, NS), **kw)
+        RES = torch.empty((n, R, M * D), **kw)
+        ACTS = torch.empty((n, R, G), **kw)
+        CS = torch.empty((n, R, H), **kw)
+        HS = torch.empty((R, n, H), **kw)
+        GATT = torch.empty((R, G), **kw)
+        zero = torch.zeros((R, H), **kw)
+        st = _n.stream()
+        for i in range(n):
+            if i == 0:
+                HP[0].copy_(b_h.expand(R, Ph))  # h_{-1} = 0
+            else:
+                torch.addmm(b_h, HS[:, i - 1], W_h.t(), out=HP[i])
+            _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video), _n.ptr(HP[i]),
+                    Ph, 0, _n.ptr(off_hs), _n.ptr(ref), RD, int(rd1_rows), lvl, nl, Nv, R, M, D, NS // nl,
+                    _n.ptr(CLIP[i]), _n.ptr(LOC[i]), st)
+            torch.addmm(b_ctx, CLIP[i].view(-1, D), W_ctx.t(), out=ATT[i])
+            ah, ldh = _n.rows(HP[i][:, n_off:n_off + A])
+            _n.call("pdvc_softattn_forward_f32", _n.ptr(ATT[i]), ah, ldh, _n.ptr(alpha_w), _n.ptr(alpha_b),
+                    _n.ptr(CLIP[i]), R, M, A, D, _n.ptr(RES[i]), _n.ptr(PROBS[i]), st)
+            torch.mm(RES[i], W_att.t(), out=GATT)
+            xa, ldx = _n.rows(xg[:, i])
+            gh, ldg = _n.rows(HP[i][:, n_off + A:])
+            ho, ldo = _n.rows(HS[:, i])
+            _n.call("pdvc_lstm_cell_forward_f32", xa, ldx, _n.ptr(GATT), G, gh, ldg,
+                    _n.ptr(CS[i - 1] if i > 0 else zero), R, H, ho, ldo, _n.ptr(CS[i]), _n.ptr(ACTS[i]), st)
+        ctx.save_for_backward(value, off_hs, ref, W_h, W_ctx, alpha_w, W_att, pad_mask, row_video, HP, CLIP, LOC,
+                              ATT, PROBS, RES, ACTS, CS, HS)
+        ctx.meta = (tuple(level_T), int(rd1_rows))
+        return HS
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dHS):
+        (value, off_hs, ref, W_h, W_ctx, alpha_w, W_att, pad_mask, row_video, HP, CLIP, LOC, ATT, PROBS, RES, ACTS,
+         CS, HS) = ctx.saved_tensors
+        level_T, rd1_rows = ctx.meta
+        dHS = dHS.contiguous()
+        Nv, S, M, D = value.shape
+        n, R, Ph = HP.shape
+        H = HS.shape[2]
+        G = 4 * H
+        A = W_ctx.shape[0]
+        NS = NUM_SAMPLES
+        n_off = M * NS
+        RD = ref.shape[2]
+        lvl, nl = _levels(level_T)
+        kw = dict(dtype=value.dtype, device=value.device)
+        dHP = torch.empty((n, R, Ph), **kw)
+        dATT = torch.empty((n, R * M * NS, A), **kw)
+        GAW = torch.empty((n, R * M, A), **kw)
+        GAB = torch.empty((n, R * M), **kw)
+        dCLIP = torch.empty((R, M, NS, D), **kw)
+        dRES = torch.empty((R, M * D), **kw)
+        dh = torch.empty((R, H), **kw)
+        dc = [torch.empty((R, H), **kw), torch.empty((R, H), **kw)]
+        zero = torch.zeros((R, H), **kw)
+        gv = torch.zeros_like(value)
+        gr = torch.zeros_like(ref) if ctx.needs_input_grad[3] else None
+        st = _n.stream()
+        for i in reversed(range(n)):
+            last = i == n - 1
+            gh_, ldgh = _n.rows(dHS[:, i])
+            dg, lddg = _n.rows(dHP[i][:, n_off + A:])
+            _n.call("pdvc_lstm_cell_backward_f32", gh_, ldgh, None if last else _n.ptr(dh), H,
+                    None if last else _n.ptr(dc[(i + 1) % 2]), _n.ptr(ACTS[i]),
+                    _n.ptr(CS[i - 1] if i > 0 else zero), _n.ptr(CS[i]), R, H, dg, lddg, _n.ptr(dc[i % 2]), st)
+            torch.mm(dHP[i][:, n_off + A:], W_att, out=dRES)
+            ah, ldh = _n.rows(HP[i][:, n_off:n_off + A])
+            gah, ldgah = _n.rows(dHP[i][:, n_off:n_off + A])
+            _n.call("pdvc_softattn_backward_f32", _n.ptr(ATT[i]), ah, ldh, _n.ptr(alpha_w), _n.ptr(CLIP[i]),
+                    _n.ptr(PROBS[i]), _n.ptr(dRES), R, M, A, D, _n.ptr(dATT[i]), gah, ldgah, _n.ptr(dCLIP),
+                    _n.ptr(GAW[i]), _n.ptr(GAB[i]), st)
+            dCLIP.view(-1, D).addmm_(dATT[i], W_ctx)
+            _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video),
+                    _n.ptr(HP[i]), Ph, 0, _n.ptr(off_hs), _n.ptr(ref), RD, rd1_rows, lvl, nl, Nv, R, M, D, NS // nl,
+                    _n.ptr(LOC[i]), _n.ptr(dCLIP), _n.ptr(gv), _n.ptr(dHP[i]), _n.ptr(gr), st)
+            if i > 0:
+                torch.mm(dHP[i], W_h, out=dh)
+        # weight gradients: one GEMM each over every (step, row)
+        d_gates = dHP[..., n_off + A:]                       # (n, R, 4H), row stride Ph
+        d_xg = d_gates.permute(1, 0, 2).contiguous()
+        d_off_hs = dHP[..., :n_off].sum(0)
+        if n > 1:
+            dW_h = dHP[1:].reshape(-1, Ph).t() @ HS[:, :-1].transpose(0, 1).reshape(-1, H)
+        else:
+            dW_h = torch.zeros_like(W_h)
+        db_h = dHP.sum((0, 1))
+        dA2 = dATT.view(-1, A)
+        dW_ctx = dA2.t() @ CLIP.view(-1, D)
+        db_ctx = dA2.sum(0)
+        dalpha_w = GAW.sum((0, 1))
+        dalpha_b = GAB.sum().reshape(1)
+        dW_att = d_gates.reshape(-1, G).t() @ RES.view(-1, M * D)
+        return (gv, d_xg, d_off_hs, gr, dW_h, db_h, dW_ctx, db_ctx, dalpha_w, dalpha_b, dW_att, None, None, None,
+                None)

@@ -147,7 +147,7 @@ int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* value_pad_ma
  * qk (N,Q,2E) = [q | k] in-projections (E = num_heads*head_dim), v (N,Q,E); key_padding_mask (N,Q) uint8,
  * 1 = ignored key, may be NULL.  out (N,Q,E) = softmax(q*sqrt(1/D) k^T + mask) [dropout] v per head;
  * lse (N,M,Q) log-sum-exp of each score row (saved for the backward).  Dropout keeps a deterministic
- * counter-hash mask of (seed, video, head, query, key), regenerated by the backward.  head_dim must be 64,
+ * counter-hash mask of (seed, video, head, query, key), regenerated by the backward.  head_dim <= 64,
  * Q <= 300. */
 int pdvc_mha_forward_f32(const float* qk, const float* v, const uint8_t* key_padding_mask, int batch, int num_query,
                          int num_heads, int head_dim, float dropout_p, uint64_t seed, float* out, float* lse,
@@ -161,8 +161,7 @@ int pdvc_mha_backward_f32(const float* qk, const float* v, const uint8_t* key_pa
 /* ---- caption decoder step pieces (ShowAttendTellCore) ------------------------------------------------
  * softattn: att (R,M,16,A) = ctx2att(samples); att_h (R, ld_att_h) = h2att(h) (A values per row);
  * alpha_w (A), alpha_b (1) = alpha_net; clip (R,M,16,D) the samples.  att_res (R, M*D) = sum_j p_j clip_j with
- * p = softmax_j(alpha_net(tanh(att_j + att_h))); probs (R,M,16) saved.  Supported (A, D): (512,512), (64,64),
- * (128,128), (256,256), (512,256), (64,512). */
+ * p = softmax_j(alpha_net(tanh(att_j + att_h))); probs (R,M,16) saved.  Any 0 < A, D <= 512. */
 int pdvc_softattn_forward_f32(const float* att, const float* att_h, int ld_att_h, const float* alpha_w,
                               const float* alpha_b, const float* clip, int rows, int num_heads, int att_hid,
                               int head_dim, float* att_res, float* probs, void* stream);
@@ -178,10 +177,12 @@ int pdvc_softattn_backward_f32(const float* att, const float* att_h, int ld_att_
 int pdvc_lstm_cell_forward_f32(const float* gates_a, int lda, const float* gates_b, int ldb, const float* gates_c,
                                int ldc, const float* c_prev, int rows, int hidden, float* h_out, int ld_h_out,
                                float* c_out, float* acts, void* stream);
-/* grad_gates (R,4H), grad_c_prev (R,H) from grad_h (+ grad_h2 if not NULL) and grad_c_next (or NULL). */
+/* grad_gates (R, ld_grad_gates >= 4H; the first 4H columns written), grad_c_prev (R,H) from grad_h (+ grad_h2
+ * if not NULL) and grad_c_next (or NULL). */
 int pdvc_lstm_cell_backward_f32(const float* grad_h, int ld_grad_h, const float* grad_h2, int ld_grad_h2,
                                 const float* grad_c_next, const float* acts, const float* c_prev, const float* c,
-                                int rows, int hidden, float* grad_gates, float* grad_c_prev, void* stream);
+                                int rows, int hidden, float* grad_gates, int ld_grad_gates, float* grad_c_prev,
+                                void* stream);
 
 #ifdef __cplusplus
 }

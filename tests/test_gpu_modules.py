@@ -199,3 +199,66 @@ def test_captioner_vs_golden(ref_dim):
                                                          for k, v in others.items()})
     assert seq.cpu().tolist() == d["sample_seq"].tolist()
     close(lp, d["sample_logprobs"], 1e-4, "greedy logprobs")
+
+
+@pytest.mark.parametrize("heads,rd1", [(1, 3), (2, 0)])
+def test_caption_decode_function_matches_step_loop(heads, rd1):
+    """The fused teacher-forced recurrence (ops/functions/caption_decode.py) against the per-step autograd
+    loop of the same math (LSTMDSACaptioner._step: cap-gather kernel + torch ops), at the PDVC caption shape
+    (d=512, A=512, H=512, 16 samples) with a mix of 1-d and (c, len) reference rows."""
+    import types
+    from pdvc.CaptioningHead.LSTM_DSA import LSTMDSACaptioner
+    opt = types.SimpleNamespace(
+        vocab_size=50, input_encoding_size=512, rnn_size=512, num_layers=1, drop_prob=0.0, max_caption_len=8,
+        clip_context_dim=512, cap_nheads=heads, att_hid_size=512, wordRNN_input_feats_type="C", hidden_dim=512,
+        cap_num_feature_levels=4, cap_dec_n_points=4, num_feature_levels=4, event_context_dim=None)
+    torch.manual_seed(0)
+    cap = LSTMDSACaptioner(opt).to(DEV)
+    with torch.no_grad():
+        for p in cap.parameters():
+            p.normal_(0, 0.03)
+    T_l = (64, 32, 16, 8)
+    Nv, R, n = 2, 9, 7
+    S = sum(T_l)
+    memory = torch.randn(Nv, S, 512, device=DEV)
+    mask = torch.zeros(Nv, S, dtype=torch.bool, device=DEV)
+    mask[1, -5:] = True
+    hs = torch.randn(R, 512, device=DEV)
+    ref = torch.rand(R, 4, 2, device=DEV) * 0.8 + 0.1
+    row_video = torch.tensor([0, 1, 0, 1, 0, 1, 1, 0, 0], dtype=torch.int32, device=DEV)
+    seq = torch.randint(1, 51, (R, n + 1), device=DEV)
+    g = torch.randn(R, n, 51, device=DEV)
+
+    def run(fused):
+        ins = [t.clone().requires_grad_() for t in (hs, ref, memory)]
+        cap.zero_grad(set_to_none=True)
+        if fused:
+            out = cap.decode_teacher_forced(ins[0], ins[1], rd1, row_video, ins[2], mask, T_l, seq, n)
+        else:
+            w = cap._step_weights()
+            value, mask_u8 = cap._prepare(ins[2], mask)
+            xt = cap.embed(seq[:, :n])
+            x_gates = torch.nn.functional.linear(xt, w["W_x"])
+            hs_part = torch.nn.functional.linear(ins[0], w["W_hs"])
+            off_hs = torch.nn.functional.linear(ins[0], w["W_off_hs"], w["b_off"])
+            h = ins[0].new_zeros(R, 512)
+            c = ins[0].new_zeros(R, 512)
+            outs = []
+            for i in range(n):
+                h, c = cap._step(w, h, c, x_gates[:, i], hs_part, off_hs, value, mask_u8, row_video, ins[1], rd1,
+                                 T_l)
+                outs.append(h)
+            out = torch.log_softmax(cap.logit(torch.stack(outs, 1)), -1)
+        loss = (out * g).sum()
+        loss.backward()
+        grads = {k: p.grad.clone() for k, p in cap.named_parameters() if p.grad is not None}
+        return out.detach(), [t.grad.clone() for t in ins], grads
+
+    o1, gi1, gp1 = run(True)
+    o0, gi0, gp0 = run(False)
+    close(o1, o0, 1e-5, "logprobs")
+    for name, a, b in zip(("hs", "ref", "memory"), gi1, gi0):
+        close(a, b, 1e-4, "grad_" + name)
+    assert set(gp1) == set(gp0)
+    for k in gp0:
+        close(gp1[k], gp0[k], 1e-4, k)
