@@ -37,6 +37,12 @@ __device__ __forceinline__ void ld(VecF<CPL>& v, const float* __restrict__ p, bo
     else v.zero();
 }
 
+// One wave per (row, head group, level, pair of points): waves_per_row = head groups x kSplit, so the
+// R ~ 256 caption rows of a step still put >= 2048 waves on the chip (one wave per row left 255 of 256
+// CUs with a single wave).  A head's D channels are spread over LPH lanes, CPL = 8 consecutive floats each.
+constexpr int kSPW = 2;              // samples per wave
+constexpr int kSplit = cNS / kSPW;   // waves per (row, head group)
+
 template <int CPL, int LPH, int RD>
 __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __restrict__ value,
                                                               const uint8_t* __restrict__ vmask,
@@ -52,7 +58,10 @@ __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __rest
     const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (wave >= total_waves) return;
     const int r = wave / waves_per_row;
-    const int hg = wave - r * waves_per_row;
+    const int wr = wave - r * waves_per_row;
+    const int hg = wr / kSplit;
+    const int j0 = (wr - hg * kSplit) * kSPW;
+    const int l = j0 / cP;
     const int sub = lane % LPH;
     const int m = hg * HPW + lane / LPH;
     if (m >= M) return;
@@ -63,46 +72,43 @@ __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __rest
     const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
     const float* orow = offsets + (size_t)r * off_stride + off_col0 + m * cNS;
     const bool centre_only = (RD == 1) || (r < rd1_rows);  // wave-uniform
+    const int T = lv.T[0] * (l == 0) + lv.T[1] * (l == 1) + lv.T[2] * (l == 2) + lv.T[3] * (l == 3);
+    const int st = lv.start[0] * (l == 0) + lv.start[1] * (l == 1) + lv.start[2] * (l == 2) + lv.start[3] * (l == 3);
+    const float r0 = ref[((size_t)r * cL + l) * RD];
+    const float r1 = (RD == 2) ? ref[((size_t)r * cL + l) * RD + 1] : 0.f;
+    int x0[kSPW];
+    float nw[kSPW], ne[kSPW];
 #pragma unroll
-    for (int l = 0; l < cL; ++l) {
-        const int T = lv.T[l], st = lv.start[l];
-        const float r0 = ref[((size_t)r * cL + l) * RD];
-        const float r1 = (RD == 2) ? ref[((size_t)r * cL + l) * RD + 1] : 0.f;
-        int x0[cP];
-        float nw[cP], ne[cP];
+    for (int u = 0; u < kSPW; ++u) {
+        const int j = j0 + u;
+        const float off = off_add ? orow[j] + off_add[((size_t)r * M + m) * cNS + j] : orow[j];
+        const float loc = centre_only ? r0 + off / (float)T : r0 + ((off / (float)cP) * r1) * 0.5f;
+        if (save_loc && sub == 0) save_loc[((size_t)r * M + m) * cNS + j] = loc;
+        float gm;
+        const float ix = border_ix(loc, T, gm);
+        const float xf = floorf(ix);
+        x0[u] = (int)xf;
+        // iy == 0 (H == 1): nw = (x0+1-ix)*1, ne = (ix-x0)*1, the y0+1 row is outside
+        nw[u] = ((float)(x0[u] + 1) - ix);
+        ne[u] = (ix - xf);
+    }
+    VecF<CPL> v0[kSPW], v1[kSPW];
+    bool ok0[kSPW], ok1[kSPW];
 #pragma unroll
-        for (int p = 0; p < cP; ++p) {
-            const int j = l * cP + p;
-            const float off = off_add ? orow[j] + off_add[((size_t)r * M + m) * cNS + j] : orow[j];
-            const float loc = centre_only ? r0 + off / (float)T : r0 + ((off / (float)cP) * r1) * 0.5f;
-            if (save_loc && sub == (j % LPH)) save_loc[((size_t)r * M + m) * cNS + j] = loc;
-            float gm;
-            const float ix = border_ix(loc, T, gm);
-            const float xf = floorf(ix);
-            x0[p] = (int)xf;
-            // iy == 0 (H == 1): nw = (x0+1-ix)*1, ne = (ix-x0)*1, the y0+1 row is outside
-            nw[p] = ((float)(x0[p] + 1) - ix);
-            ne[p] = (ix - xf);
-        }
-        VecF<CPL> v0[cP], v1[cP];
-        bool ok0[cP], ok1[cP];
+    for (int u = 0; u < kSPW; ++u) {  // all corner rows in flight together (clamped, selected after)
+        const int a1 = min(x0[u] + 1, T - 1);
+        v0[u].load(vbase + (size_t)(st + x0[u]) * MD);
+        v1[u].load(vbase + (size_t)(st + a1) * MD);
+        ok0[u] = !(mbase && mbase[st + x0[u]]);
+        ok1[u] = x0[u] + 1 < T && !(mbase && mbase[st + a1]);
+    }
 #pragma unroll
-        for (int p = 0; p < cP; ++p) {  // the level's 2*P rows in flight together (clamped, selected after)
-            const int a1 = min(x0[p] + 1, T - 1);
-            v0[p].load(vbase + (size_t)(st + x0[p]) * MD);
-            v1[p].load(vbase + (size_t)(st + a1) * MD);
-            ok0[p] = !(mbase && mbase[st + x0[p]]);
-            ok1[p] = x0[p] + 1 < T && !(mbase && mbase[st + a1]);
-        }
+    for (int u = 0; u < kSPW; ++u) {
+        VecF<CPL> o;
 #pragma unroll
-        for (int p = 0; p < cP; ++p) {
-            VecF<CPL> o;
-#pragma unroll
-            for (int c = 0; c < CPL; ++c)
-                o.v[c] = (ok0[p] ? v0[p].v[c] : 0.f) * nw[p] + (ok1[p] ? v1[p].v[c] : 0.f) * ne[p];
-            o.store(samples + (((size_t)r * M + m) * cNS + l * cP + p) * D + c0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
+        for (int c = 0; c < CPL; ++c)
+            o.v[c] = (ok0[u] ? v0[u].v[c] : 0.f) * nw[u] + (ok1[u] ? v1[u].v[c] : 0.f) * ne[u];
+        o.store(samples + (((size_t)r * M + m) * cNS + j0 + u) * D + c0);
     }
 }
 
@@ -115,13 +121,14 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
     const float* __restrict__ gsamp, float* __restrict__ grad_value, float* __restrict__ grad_off,
     float* __restrict__ grad_ref) {
     constexpr int HPW = 64 / LPH;
-    constexpr int G = LPH < 16 ? LPH : 16;  // reduce-scatter group; the rest is an all-reduce
-    constexpr int SPL = cNS / G;
     const int lane = threadIdx.x & 63;
     const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (wave >= total_waves) return;
     const int r = wave / waves_per_row;
-    const int hg = wave - r * waves_per_row;
+    const int wr = wave - r * waves_per_row;
+    const int hg = wr / kSplit;
+    const int j0 = (wr - hg * kSplit) * kSPW;
+    const int l = j0 / cP;
     const int sub = lane % LPH;
     const int m_raw = hg * HPW + lane / LPH;
     const bool active = m_raw < M;
@@ -132,99 +139,83 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
     const float* vbase = value + (size_t)b * S * MD + (size_t)m * D + c0;
     float* gvbase = grad_value + (size_t)b * S * MD + (size_t)m * D + c0;
     const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
+    const int T = lv.T[0] * (l == 0) + lv.T[1] * (l == 1) + lv.T[2] * (l == 2) + lv.T[3] * (l == 3);
+    const int st = lv.start[0] * (l == 0) + lv.start[1] * (l == 1) + lv.start[2] * (l == 2) + lv.start[3] * (l == 3);
 
-    float part[cNS];
+    float loc[kSPW], gm[kSPW], nw[kSPW], ne[kSPW];
+    int x0[kSPW];
 #pragma unroll
-    for (int l = 0; l < cL; ++l) {
-        const int T = lv.T[l], st = lv.start[l];
-        int x0[cP];
-        float nw[cP], ne[cP];
-#pragma unroll
-        for (int p = 0; p < cP; ++p) {
-            const float loc = active ? save_loc[((size_t)r * M + m) * cNS + l * cP + p] : 0.f;
-            float gm;
-            const float ix = border_ix(loc, T, gm);
-            const float xf = floorf(ix);
-            x0[p] = (int)xf;
-            nw[p] = ((float)(x0[p] + 1) - ix);
-            ne[p] = (ix - xf);
-        }
-        VecF<CPL> g[cP], v0[cP], v1[cP];
-        bool ok0[cP], ok1[cP];
-#pragma unroll
-        for (int p = 0; p < cP; ++p) {
-            const int a1 = min(x0[p] + 1, T - 1);
-            g[p].load(gsamp + (((size_t)r * M + m) * cNS + l * cP + p) * D + c0);
-            v0[p].load(vbase + (size_t)(st + x0[p]) * MD);
-            v1[p].load(vbase + (size_t)(st + a1) * MD);
-            ok0[p] = active && !(mbase && mbase[st + x0[p]]);
-            ok1[p] = active && x0[p] + 1 < T && !(mbase && mbase[st + a1]);
-        }
-#pragma unroll
-        for (int p = 0; p < cP; ++p) {
-            float s = 0.f;
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                const float gv = active ? g[p].v[c] : 0.f;
-                if (ok0[p]) atomicAdd(gvbase + (size_t)(st + x0[p]) * MD + c, nw[p] * gv);
-                if (ok1[p]) atomicAdd(gvbase + (size_t)(st + x0[p] + 1) * MD + c, ne[p] * gv);
-                s += gv * ((ok1[p] ? v1[p].v[c] : 0.f) - (ok0[p] ? v0[p].v[c] : 0.f));  // gix = -vnw + vne
-            }
-            part[l * cP + p] = s;
-        }
-        __builtin_amdgcn_sched_barrier(0);
+    for (int u = 0; u < kSPW; ++u) {
+        loc[u] = active ? save_loc[((size_t)r * M + m) * cNS + j0 + u] : 0.f;
+        const float ix = border_ix(loc[u], T, gm[u]);
+        const float xf = floorf(ix);
+        x0[u] = (int)xf;
+        nw[u] = ((float)(x0[u] + 1) - ix);
+        ne[u] = (ix - xf);
     }
-    group_reduce_scatter<cNS, G>(part, lane);
+    VecF<CPL> g[kSPW], v0[kSPW], v1[kSPW];
+    bool ok0[kSPW], ok1[kSPW];
 #pragma unroll
-    for (int k = 0; k < SPL; ++k) {
-#pragma unroll
-        for (int d = G; d < LPH; d <<= 1) part[k] += __shfl_xor(part[k], d, PDVC_WAVE);
+    for (int u = 0; u < kSPW; ++u) {
+        const int a1 = min(x0[u] + 1, T - 1);
+        g[u].load(gsamp + (((size_t)r * M + m) * cNS + j0 + u) * D + c0);
+        v0[u].load(vbase + (size_t)(st + x0[u]) * MD);
+        v1[u].load(vbase + (size_t)(st + a1) * MD);
+        ok0[u] = active && !(mbase && mbase[st + x0[u]]);
+        ok1[u] = active && x0[u] + 1 < T && !(mbase && mbase[st + a1]);
     }
-    float gr0[cL], gr1[cL];
+    float part[kSPW];
 #pragma unroll
-    for (int l = 0; l < cL; ++l) { gr0[l] = 0.f; gr1[l] = 0.f; }
-    const bool owner = active && sub < G;
-    const int gsub = sub % G;
+    for (int u = 0; u < kSPW; ++u) {
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const float gv = active ? g[u].v[c] : 0.f;
+            if (ok0[u]) atomicAdd(gvbase + (size_t)(st + x0[u]) * MD + c, nw[u] * gv);
+            if (ok1[u]) atomicAdd(gvbase + (size_t)(st + x0[u] + 1) * MD + c, ne[u] * gv);
+            s += gv * ((ok1[u] ? v1[u].v[c] : 0.f) - (ok0[u] ? v0[u].v[c] : 0.f));  // gix = -vnw + vne
+        }
+        part[u] = s;
+    }
+    // sum over the LPH lanes of the head (all lanes end with the head's totals)
+#pragma unroll
+    for (int u = 0; u < kSPW; ++u) {
+#pragma unroll
+        for (int d = 1; d < LPH; d <<= 1) part[u] += __shfl_xor(part[u], d, PDVC_WAVE);
+    }
+    const bool owner = active && sub == 0;
     const bool centre_only = (RD == 1) || (r < rd1_rows);
+    float gr0 = 0.f, gr1 = 0.f;
+    const float r1 = (RD == 2 && !centre_only) ? ref[((size_t)r * cL + l) * 2 + 1] : 0.f;
 #pragma unroll
-    for (int k = 0; k < SPL; ++k) {
-        const int j = gsub * SPL + k;
-        const int l = j / cP;
-        const int T = lv.T[l];
-        const float loc = active ? save_loc[((size_t)r * M + m) * cNS + j] : 0.f;
-        float gm;
-        border_ix(loc, T, gm);
-        const float gloc = 2.f * (gm * part[k]);  // grid = 2*loc - 1
+    for (int u = 0; u < kSPW; ++u) {
+        const int j = j0 + u;
+        const float gloc = 2.f * (gm[u] * part[u]);  // grid = 2*loc - 1
         float goff;
         if (centre_only) {
             goff = gloc / (float)T;
-#pragma unroll
-            for (int ll = 0; ll < cL; ++ll) if (ll == l && owner) gr0[ll] += gloc;
+            gr0 += gloc;
         } else {
-            const float r1 = ref[((size_t)r * cL + l) * 2 + 1];
             const float t2 = gloc * 0.5f;
             goff = (t2 * r1) / (float)cP;
             float o = active ? offsets[(size_t)r * off_stride + off_col0 + m * cNS + j] : 0.f;
             if (active && off_add) o += off_add[((size_t)r * M + m) * cNS + j];
-#pragma unroll
-            for (int ll = 0; ll < cL; ++ll)
-                if (ll == l && owner) { gr0[ll] += gloc; gr1[ll] += t2 * (o / (float)cP); }
+            gr0 += gloc;
+            gr1 += t2 * (o / (float)cP);
         }
         if (owner) grad_off[(size_t)r * off_stride + off_col0 + m * cNS + j] = goff;
     }
     if (grad_ref) {
+        // heads of this wave: sum the owners' values over the wave, one atomic per (wave, level)
+        float v0 = owner ? gr0 : 0.f, v1 = owner ? gr1 : 0.f;
 #pragma unroll
-        for (int l = 0; l < cL; ++l) {
-            float v0 = gr0[l], v1 = gr1[l];
-#pragma unroll
-            for (int d = 32; d > 0; d >>= 1) {
-                v0 += __shfl_xor(v0, d, PDVC_WAVE);
-                if (RD == 2) v1 += __shfl_xor(v1, d, PDVC_WAVE);
-            }
-            if (lane == 0) {
-                atomicAdd(grad_ref + ((size_t)r * cL + l) * RD, v0);
-                if (RD == 2) atomicAdd(grad_ref + ((size_t)r * cL + l) * RD + 1, v1);
-            }
+        for (int d = LPH; d < 64; d <<= 1) {
+            v0 += __shfl_xor(v0, d, PDVC_WAVE);
+            if (RD == 2) v1 += __shfl_xor(v1, d, PDVC_WAVE);
+        }
+        if (lane == 0) {
+            atomicAdd(grad_ref + ((size_t)r * cL + l) * RD, v0);
+            if (RD == 2) atomicAdd(grad_ref + ((size_t)r * cL + l) * RD + 1, v1);
         }
     }
 }
@@ -248,7 +239,7 @@ static int cap_setup(const int32_t* level_T, int num_levels, int num_point, int 
                               head_dim);
     lph = head_dim / 8;
     const int hpw = 64 / lph;
-    wpr = (num_heads + hpw - 1) / hpw;
+    wpr = ((num_heads + hpw - 1) / hpw) * kSplit;
     return PDVC_OK;
 }
 

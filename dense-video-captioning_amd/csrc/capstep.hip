@@ -4,9 +4,8 @@
 //   (pdvc/CaptioningHead/LSTM_DSA.py:245-258):
 //     dot_j = alpha_net(tanh(att_j + att_h)) = sum_a tanh(att[j,a] + att_h[a]) * w_a + b
 //     p = softmax_j(dot);  att_res = sum_j p_j * clip_j
-//   with att = ctx2att(clip) (a GEMM, hipBLASLt) and att_h = h2att(h) given.  One wave per (row, head):
-//   lanes cover the hidden width for the 16 dots (reduce-scatter over lanes) and the value width for the
-//   weighted sum.  Replaces an add, tanh, the 1-wide alpha_net GEMM, softmax and a bmm (+ their backward).
+//   with att = ctx2att(clip) (a GEMM, hipBLASLt) and att_h = h2att(h) given.  One 512-thread workgroup per
+//   (row, head): threads cover the hidden width for the 16 dots and the value width for the weighted sum.  Replaces an add, tanh, the 1-wide alpha_net GEMM, softmax and a bmm (+ their backward).
 // lstm_cell: nn.LSTM's cell for 1 layer, 1 step, no bias (LSTM_DSA.py:206-207,261): gates = sum of up to
 //   three pre-activation parts (the GEMM outputs of the hoisted input part, the attention part and W_hh h),
 //   gate order (i, f, g, o), c' = f c + i g, h' = o tanh(c').  One lane per (row, unit).
@@ -18,162 +17,138 @@ constexpr int sNS = 16;
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
-// att (R, M, 16, A) contiguous; att_h (R, ldh) [A values at column 0 of the pointer]; clip (R, M, 16, D).
-// APL / DPL are the per-lane maxima (A <= 64*APL, D <= 64*DPL); columns past A / D are masked.
-template <int APL, int DPL>
-__global__ __launch_bounds__(256) void softattn_fwd_kernel(const float* __restrict__ att, const float* __restrict__ att_h,
-                                                           int ldh, const float* __restrict__ aw,
-                                                           const float* __restrict__ ab, const float* __restrict__ clip,
-                                                           int R, int M, int A, int D, float* __restrict__ res,
-                                                           float* __restrict__ probs) {
-    const int lane = threadIdx.x & 63;
-    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (wave >= R * M) return;
-    const int r = wave / M;
-    float hv[APL], wv[APL];
+// One 512-thread workgroup per (row, head); threads run over the hidden (A) and value (D) channels, so every
+// global access is a coalesced row segment and no reduction crosses a thread except the 16 dot products
+// (wave reduce-scatter + an 8-wave LDS sum).  att (R, M, 16, A) contiguous; att_h (R, ldh) [A values at
+// column 0 of the pointer]; clip (R, M, 16, D); any A, D (loops stride 512).
+constexpr int kSAT = 512;            // threads per soft-attention workgroup
+constexpr int kSAW = kSAT / 64;      // waves
+
+// sum over the workgroup of 16 per-thread partials; result (all 16) in red[0..15]
+__device__ __forceinline__ void block_sum16(float (&part)[sNS], float* red, int lane, int wid) {
+    group_reduce_scatter<sNS, 16>(part, lane);  // lane%16 -> partial of sample lane%16 over its 16-lane group
+    float v = part[0];
+    v += __shfl_xor(v, 16, PDVC_WAVE);
+    v += __shfl_xor(v, 32, PDVC_WAVE);
+    if (lane < sNS) red[wid * sNS + lane] = v;
+    __syncthreads();
+    if (threadIdx.x < sNS) {
+        float t = 0.f;
 #pragma unroll
-    for (int k = 0; k < APL; ++k) {
-        const int a = lane + 64 * k;
-        hv[k] = a < A ? att_h[(size_t)r * ldh + a] : 0.f;
-        wv[k] = a < A ? aw[a] : 0.f;
+        for (int w = 0; w < kSAW; ++w) t += red[w * sNS + threadIdx.x];
+        red[kSAW * sNS + threadIdx.x] = t;
     }
-    const float* ab_ = att + (size_t)wave * sNS * A;
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kSAT) void softattn_fwd_kernel(const float* __restrict__ att, const float* __restrict__ att_h,
+                                                            int ldh, const float* __restrict__ aw,
+                                                            const float* __restrict__ ab, const float* __restrict__ clip,
+                                                            int R, int M, int A, int D, float* __restrict__ res,
+                                                            float* __restrict__ probs) {
+    __shared__ float red[(kSAW + 1) * sNS];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wg = blockIdx.x;  // (row, head)
+    const int r = wg / M;
+    const float* ab_ = att + (size_t)wg * sNS * A;
     float part[sNS];
 #pragma unroll
-    for (int j = 0; j < sNS; ++j) {
-        float s = 0.f;
+    for (int j = 0; j < sNS; ++j) part[j] = 0.f;
+    for (int a = threadIdx.x; a < A; a += kSAT) {
+        const float hv = att_h[(size_t)r * ldh + a], wv = aw[a];
 #pragma unroll
-        for (int k = 0; k < APL; ++k) {
-            const int a = lane + 64 * k;
-            if (a < A) s += tanhf(ab_[j * A + a] + hv[k]) * wv[k];
-        }
-        part[j] = s;
+        for (int j = 0; j < sNS; ++j) part[j] += tanhf(ab_[(size_t)j * A + a] + hv) * wv;
     }
-    group_reduce_scatter<sNS, 16>(part, lane);   // lane%16 -> dot of sample lane%16 (partial over 16-lane group)
-    float dot = part[0];
-    dot += __shfl_xor(dot, 16, PDVC_WAVE);
-    dot += __shfl_xor(dot, 32, PDVC_WAVE);
-    dot += ab[0];
-    // softmax over the 16 samples (each value replicated on 4 lanes)
-    float mx = dot;
+    block_sum16(part, red, lane, wid);
+    const float* dots = red + kSAW * sNS;
+    float mx = -INFINITY;
 #pragma unroll
-    for (int d = 8; d > 0; d >>= 1) mx = fmaxf(mx, __shfl_xor(mx, d, PDVC_WAVE));
-    const float e = expf(dot - mx);
-    float sum = e;
-#pragma unroll
-    for (int d = 8; d > 0; d >>= 1) sum += __shfl_xor(sum, d, PDVC_WAVE);
-    const float p = e / sum;
-    if (lane < sNS) probs[(size_t)wave * sNS + lane] = p;
-    float o[DPL];
-#pragma unroll
-    for (int k = 0; k < DPL; ++k) o[k] = 0.f;
-    const float* cb = clip + (size_t)wave * sNS * D;
+    for (int j = 0; j < sNS; ++j) mx = fmaxf(mx, dots[j] + ab[0]);
+    float p[sNS], sum = 0.f;
 #pragma unroll
     for (int j = 0; j < sNS; ++j) {
-        const float pj = __shfl(p, j, PDVC_WAVE);
-#pragma unroll
-        for (int k = 0; k < DPL; ++k) {
-            const int d = lane + 64 * k;
-            if (d < D) o[k] += pj * cb[j * D + d];
-        }
+        p[j] = expf(dots[j] + ab[0] - mx);
+        sum += p[j];
     }
+    const float inv = 1.f / sum;
 #pragma unroll
-    for (int k = 0; k < DPL; ++k) {
-        const int d = lane + 64 * k;
-        if (d < D) res[(size_t)wave * D + d] = o[k];
+    for (int j = 0; j < sNS; ++j) p[j] = p[j] * inv;
+    if (threadIdx.x < sNS) {
+        float pj = 0.f;
+#pragma unroll
+        for (int j = 0; j < sNS; ++j) pj = (j == (int)threadIdx.x) ? p[j] : pj;
+        probs[(size_t)wg * sNS + threadIdx.x] = pj;
+    }
+    const float* cb = clip + (size_t)wg * sNS * D;
+    for (int d = threadIdx.x; d < D; d += kSAT) {
+        float o = 0.f;
+#pragma unroll
+        for (int j = 0; j < sNS; ++j) o += p[j] * cb[(size_t)j * D + d];
+        res[(size_t)wg * D + d] = o;
     }
 }
 
 // backward: grad_res (R, M*D) -> grad_att (R,M,16,A), grad_att_h (R,A) (summed over heads), grad_clip
 // (R,M,16,D) = p_j * grad_res (the caller adds the ctx2att-path term grad_att @ W_ctx2att with a GEMM),
-// per-wave partial sums of the alpha_net weight gradient (R*M, A) and bias gradient (R*M).
-template <int APL, int DPL>
-__global__ __launch_bounds__(256) void softattn_bwd_kernel(const float* __restrict__ att, const float* __restrict__ att_h,
-                                                           int ldh, const float* __restrict__ aw,
-                                                           const float* __restrict__ clip,
-                                                           const float* __restrict__ probs,
-                                                           const float* __restrict__ gres, int R, int M, int A, int D,
-                                                           float* __restrict__ gatt, float* __restrict__ gatt_h,
-                                                           int ldgh, float* __restrict__ gclip,
-                                                           float* __restrict__ gaw_part, float* __restrict__ gab_part) {
-    const int lane = threadIdx.x & 63;
-    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (wave >= R * M) return;
-    const int r = wave / M;
-    const float* cb = clip + (size_t)wave * sNS * D;
-    float* gcb = gclip + (size_t)wave * sNS * D;
-    float g[DPL];
+// per-(row, head) partial sums of the alpha_net weight gradient (R*M, A) and bias gradient (R*M).
+__global__ __launch_bounds__(kSAT) void softattn_bwd_kernel(const float* __restrict__ att, const float* __restrict__ att_h,
+                                                            int ldh, const float* __restrict__ aw,
+                                                            const float* __restrict__ clip,
+                                                            const float* __restrict__ probs,
+                                                            const float* __restrict__ gres, int R, int M, int A, int D,
+                                                            float* __restrict__ gatt, float* __restrict__ gatt_h,
+                                                            int ldgh, float* __restrict__ gclip,
+                                                            float* __restrict__ gaw_part, float* __restrict__ gab_part) {
+    __shared__ float red[(kSAW + 1) * sNS];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wg = blockIdx.x;
+    const int r = wg / M;
+    float p[sNS];
 #pragma unroll
-    for (int k = 0; k < DPL; ++k) {
-        const int d = lane + 64 * k;
-        g[k] = d < D ? gres[(size_t)wave * D + d] : 0.f;
-    }
-    const float p = (lane < sNS) ? probs[(size_t)wave * sNS + lane] : 0.f;
-    // d p_j = sum_d g_d clip_j[d]; grad_clip_j = p_j g
+    for (int j = 0; j < sNS; ++j) p[j] = probs[(size_t)wg * sNS + j];
+    // dp_j = sum_d g_d clip_j[d];  grad_clip_j = p_j g
+    const float* cb = clip + (size_t)wg * sNS * D;
+    float* gcb = gclip + (size_t)wg * sNS * D;
     float part[sNS];
 #pragma unroll
-    for (int j = 0; j < sNS; ++j) {
-        const float pj = __shfl(p, j, PDVC_WAVE);
-        float s = 0.f;
+    for (int j = 0; j < sNS; ++j) part[j] = 0.f;
+    for (int d = threadIdx.x; d < D; d += kSAT) {
+        const float g = gres[(size_t)wg * D + d];
 #pragma unroll
-        for (int k = 0; k < DPL; ++k) {
-            const int d = lane + 64 * k;
-            if (d < D) {
-                const size_t idx = (size_t)j * D + d;
-                s += g[k] * cb[idx];
-                gcb[idx] = pj * g[k];
-            }
+        for (int j = 0; j < sNS; ++j) {
+            part[j] += g * cb[(size_t)j * D + d];
+            gcb[(size_t)j * D + d] = p[j] * g;
         }
-        part[j] = s;
     }
-    group_reduce_scatter<sNS, 16>(part, lane);
-    float dp = part[0];
-    dp += __shfl_xor(dp, 16, PDVC_WAVE);
-    dp += __shfl_xor(dp, 32, PDVC_WAVE);
-    // softmax backward: ddot_j = p_j (dp_j - sum_k p_k dp_k); lanes j (mod 16) hold sample j
-    const float pj_l = __shfl(p, lane & 15, PDVC_WAVE);
-    float t = pj_l * dp;
+    block_sum16(part, red, lane, wid);
+    const float* dp = red + kSAW * sNS;
+    // softmax backward: ddot_j = p_j (dp_j - sum_k p_k dp_k)
+    float t = 0.f;
 #pragma unroll
-    for (int d = 8; d > 0; d >>= 1) t += __shfl_xor(t, d, PDVC_WAVE);
-    const float ddot = pj_l * (dp - t);
-    float sb = ddot;
-#pragma unroll
-    for (int d = 8; d > 0; d >>= 1) sb += __shfl_xor(sb, d, PDVC_WAVE);
-    if (lane == 0) gab_part[wave] = sb;
-    float hv[APL], wv[APL], gh[APL], gw[APL];
-#pragma unroll
-    for (int k = 0; k < APL; ++k) {
-        const int a = lane + 64 * k;
-        hv[k] = a < A ? att_h[(size_t)r * ldh + a] : 0.f;
-        wv[k] = a < A ? aw[a] : 0.f;
-        gh[k] = 0.f;
-        gw[k] = 0.f;
-    }
-    const float* ab_ = att + (size_t)wave * sNS * A;
-    float* gab_ = gatt + (size_t)wave * sNS * A;
+    for (int j = 0; j < sNS; ++j) t += p[j] * dp[j];
+    float dd[sNS], sb = 0.f;
 #pragma unroll
     for (int j = 0; j < sNS; ++j) {
-        const float dj = __shfl(ddot, j, PDVC_WAVE);
-#pragma unroll
-        for (int k = 0; k < APL; ++k) {
-            const int a = lane + 64 * k;
-            if (a < A) {
-                const float th = tanhf(ab_[j * A + a] + hv[k]);
-                const float dpre = dj * wv[k] * (1.f - th * th);
-                gab_[j * A + a] = dpre;
-                gh[k] += dpre;
-                gw[k] += dj * th;
-            }
-        }
+        dd[j] = p[j] * (dp[j] - t);
+        sb += dd[j];
     }
+    if (threadIdx.x == 0) gab_part[wg] = sb;
+    const float* ab_ = att + (size_t)wg * sNS * A;
+    float* gab_ = gatt + (size_t)wg * sNS * A;
+    for (int a = threadIdx.x; a < A; a += kSAT) {
+        const float hv = att_h[(size_t)r * ldh + a], wv = aw[a];
+        float gh = 0.f, gw = 0.f;
 #pragma unroll
-    for (int k = 0; k < APL; ++k) {
-        const int a = lane + 64 * k;
-        if (a < A) {
-            if (M == 1) gatt_h[(size_t)r * ldgh + a] = gh[k];
-            else atomicAdd(&gatt_h[(size_t)r * ldgh + a], gh[k]);
-            gaw_part[(size_t)wave * A + a] = gw[k];
+        for (int j = 0; j < sNS; ++j) {
+            const float th = tanhf(ab_[(size_t)j * A + a] + hv);
+            const float dpre = dd[j] * wv * (1.f - th * th);
+            gab_[(size_t)j * A + a] = dpre;
+            gh += dpre;
+            gw += dd[j] * th;
         }
+        if (M == 1) gatt_h[(size_t)r * ldgh + a] = gh;
+        else atomicAdd(&gatt_h[(size_t)r * ldgh + a], gh);
+        gaw_part[(size_t)wg * A + a] = gw;
     }
 }
 
@@ -236,36 +211,16 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(const float* __restrict__
 
 using namespace pdvc;
 
-static int pow2_lanes(int n) {  // per-lane maximum for n columns over 64 lanes: 1, 2, 4 or 8 (0 if n > 512)
-    const int k = (n + 63) / 64;
-    return k <= 1 ? 1 : k <= 2 ? 2 : k <= 4 ? 4 : k <= 8 ? 8 : 0;
-}
-
-#define SA_CASE(KERNEL, PA, PD, ...) \
-    else if (pa == PA && pd == PD) hipLaunchKernelGGL((KERNEL<PA, PD>), __VA_ARGS__)
-#define SA_DISPATCH(KERNEL, A, D, ...)                                                                       \
-    do {                                                                                                     \
-        const int pa = pow2_lanes(A), pd = pow2_lanes(D);                                                    \
-        if (A <= 0 || D <= 0 || pa == 0 || pd == 0)                                                          \
-            return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "soft attention: need 0 < A, D <= 512 (A=%d, D=%d)", A, D); \
-        SA_CASE(KERNEL, 1, 1, __VA_ARGS__); SA_CASE(KERNEL, 1, 2, __VA_ARGS__); SA_CASE(KERNEL, 1, 4, __VA_ARGS__); \
-        SA_CASE(KERNEL, 1, 8, __VA_ARGS__); SA_CASE(KERNEL, 2, 1, __VA_ARGS__); SA_CASE(KERNEL, 2, 2, __VA_ARGS__); \
-        SA_CASE(KERNEL, 2, 4, __VA_ARGS__); SA_CASE(KERNEL, 2, 8, __VA_ARGS__); SA_CASE(KERNEL, 4, 1, __VA_ARGS__); \
-        SA_CASE(KERNEL, 4, 2, __VA_ARGS__); SA_CASE(KERNEL, 4, 4, __VA_ARGS__); SA_CASE(KERNEL, 4, 8, __VA_ARGS__); \
-        SA_CASE(KERNEL, 8, 1, __VA_ARGS__); SA_CASE(KERNEL, 8, 2, __VA_ARGS__); SA_CASE(KERNEL, 8, 4, __VA_ARGS__); \
-        SA_CASE(KERNEL, 8, 8, __VA_ARGS__);                                                                  \
-    } while (0)
-
 extern "C" int pdvc_softattn_forward_f32(const float* att, const float* att_h, int ld_att_h, const float* alpha_w,
                                          const float* alpha_b, const float* clip, int rows, int num_heads,
                                          int att_hid, int head_dim, float* att_res, float* probs, void* stream) {
     PDVC_CHECK_ARG(rows >= 0 && num_heads > 0, "invalid sizes");
     const long waves = (long)rows * num_heads;
     if (waves == 0) return PDVC_OK;
-    dim3 grid((unsigned)((waves + 3) / 4)), block(256);
+    PDVC_CHECK_ARG(att_hid > 0 && head_dim > 0 && waves < (1L << 31), "invalid sizes");
     hipStream_t s = (hipStream_t)stream;
-    SA_DISPATCH(softattn_fwd_kernel, att_hid, head_dim, grid, block, 0, s, att, att_h, ld_att_h, alpha_w, alpha_b,
-                clip, rows, num_heads, att_hid, head_dim, att_res, probs);
+    hipLaunchKernelGGL(softattn_fwd_kernel, dim3((unsigned)waves), dim3(kSAT), 0, s, att, att_h, ld_att_h, alpha_w,
+                       alpha_b, clip, rows, num_heads, att_hid, head_dim, att_res, probs);
     PDVC_CHECK_LAUNCH("softattn_fwd_kernel");
     return PDVC_OK;
 }
@@ -284,10 +239,10 @@ extern "C" int pdvc_softattn_backward_f32(const float* att, const float* att_h, 
         hipError_t e = hipMemset2DAsync(grad_att_h, sizeof(float) * ld_grad_att_h, 0, sizeof(float) * att_hid, rows, s);
         if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_att_h: %s", hipGetErrorString(e));
     }
-    dim3 grid((unsigned)((waves + 3) / 4)), block(256);
-    SA_DISPATCH(softattn_bwd_kernel, att_hid, head_dim, grid, block, 0, s, att, att_h, ld_att_h, alpha_w, clip, probs,
-                grad_res, rows, num_heads, att_hid, head_dim, grad_att, grad_att_h, ld_grad_att_h, grad_clip, grad_alpha_w_part,
-                grad_alpha_b_part);
+    PDVC_CHECK_ARG(att_hid > 0 && head_dim > 0 && waves < (1L << 31), "invalid sizes");
+    hipLaunchKernelGGL(softattn_bwd_kernel, dim3((unsigned)waves), dim3(kSAT), 0, s, att, att_h, ld_att_h, alpha_w,
+                       clip, probs, grad_res, rows, num_heads, att_hid, head_dim, grad_att, grad_att_h, ld_grad_att_h,
+                       grad_clip, grad_alpha_w_part, grad_alpha_b_part);
     PDVC_CHECK_LAUNCH("softattn_bwd_kernel");
     return PDVC_OK;
 }
