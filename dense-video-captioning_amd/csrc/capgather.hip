@@ -133,7 +133,9 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
     const int m_raw = hg * HPW + lane / LPH;
     const bool active = m_raw < M;
     const int m = active ? m_raw : 0;
-    const int c0 = sub * CPL;
+    // lane-strided channels (sub + LPH*c): every atomic wave-instruction adds one contiguous LPH*4-byte
+    // segment per head (256 B at D = 512), the shape global float atomics run at full rate with
+    const int c0 = sub;
     const int b = row_video[r];
     const size_t MD = (size_t)M * D;
     const float* vbase = value + (size_t)b * S * MD + (size_t)m * D + c0;
@@ -153,14 +155,20 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
         nw[u] = ((float)(x0[u] + 1) - ix);
         ne[u] = (ix - xf);
     }
-    VecF<CPL> g[kSPW], v0[kSPW], v1[kSPW];
+    float g[kSPW][CPL], v0[kSPW][CPL], v1[kSPW][CPL];
     bool ok0[kSPW], ok1[kSPW];
 #pragma unroll
     for (int u = 0; u < kSPW; ++u) {
         const int a1 = min(x0[u] + 1, T - 1);
-        g[u].load(gsamp + (((size_t)r * M + m) * cNS + j0 + u) * D + c0);
-        v0[u].load(vbase + (size_t)(st + x0[u]) * MD);
-        v1[u].load(vbase + (size_t)(st + a1) * MD);
+        const float* gp = gsamp + (((size_t)r * M + m) * cNS + j0 + u) * D + c0;
+        const float* p0 = vbase + (size_t)(st + x0[u]) * MD;
+        const float* p1 = vbase + (size_t)(st + a1) * MD;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            g[u][c] = gp[LPH * c];
+            v0[u][c] = p0[LPH * c];
+            v1[u][c] = p1[LPH * c];
+        }
         ok0[u] = active && !(mbase && mbase[st + x0[u]]);
         ok1[u] = active && x0[u] + 1 < T && !(mbase && mbase[st + a1]);
     }
@@ -170,10 +178,10 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
         float s = 0.f;
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
-            const float gv = active ? g[u].v[c] : 0.f;
-            if (ok0[u]) atomicAdd(gvbase + (size_t)(st + x0[u]) * MD + c, nw[u] * gv);
-            if (ok1[u]) atomicAdd(gvbase + (size_t)(st + x0[u] + 1) * MD + c, ne[u] * gv);
-            s += gv * ((ok1[u] ? v1[u].v[c] : 0.f) - (ok0[u] ? v0[u].v[c] : 0.f));  // gix = -vnw + vne
+            const float gv = active ? g[u][c] : 0.f;
+            if (ok0[u]) atomicAdd(gvbase + (size_t)(st + x0[u]) * MD + LPH * c, nw[u] * gv);
+            if (ok1[u]) atomicAdd(gvbase + (size_t)(st + x0[u] + 1) * MD + LPH * c, ne[u] * gv);
+            s += gv * ((ok1[u] ? v1[u][c] : 0.f) - (ok0[u] ? v0[u][c] : 0.f));  // gix = -vnw + vne
         }
         part[u] = s;
     }

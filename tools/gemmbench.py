@@ -1,0 +1,50 @@
+"""fp32 GEMM rates of the step's dominant shapes under torch's BLAS backends (diagnostic).
+    python tools/gemmbench.py"""
+import torch
+
+
+def rate(M, N, K, ta, tb, reps=20):
+    a = torch.randn((K, M) if ta else (M, K), device="cuda")
+    b = torch.randn((N, K) if tb else (K, N), device="cuda")
+    A = a.t() if ta else a
+    B = b.t() if tb else b
+    for _ in range(3):
+        A @ B
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        A @ B
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / reps * 1e-3
+    return 2 * M * N * K / t / 1e12, t * 1e6
+
+
+SHAPES = [  # (M, N, K, A transposed, B transposed): forward x W^T, dgrad g W, wgrad g^T x
+    (30720, 512, 512, False, True), (30720, 512, 512, False, False), (512, 512, 30720, True, False),
+    (30720, 256, 512, False, True), (4096, 512, 512, False, True), (3584, 5748, 512, False, True),
+    (3584, 512, 5748, False, False), (5748, 512, 3584, True, False), (256, 2576, 512, False, True),
+]
+
+if __name__ == "__main__":
+    libs = ["default"]
+    try:
+        cur = torch.backends.cuda.preferred_blas_library()
+        libs = [str(cur)]
+        for name in ("hipblaslt", "rocblas"):
+            if name not in str(cur).lower():
+                libs.append(name)
+    except Exception as e:  # noqa: BLE001
+        print("preferred_blas_library unavailable:", e)
+    for lib in libs:
+        if lib != libs[0]:
+            try:
+                torch.backends.cuda.preferred_blas_library(lib)
+            except Exception as e:  # noqa: BLE001
+                print(lib, "unavailable:", e)
+                continue
+        for s in SHAPES:
+            tf, us = rate(*s)
+            print(f"{lib:28s} M={s[0]:6d} N={s[1]:5d} K={s[2]:6d} tA={int(s[3])} tB={int(s[4])}: {tf:6.1f} TF/s {us:8.1f} us",
+                  flush=True)
