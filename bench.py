@@ -176,9 +176,15 @@ def main():
         avg_ms = k["ms"] / k["launches"]
         avg_bytes = sum(msda_alg_bytes(m, "fwd") for m in k["metas"]) / k["launches"]
         ach = avg_bytes / (avg_ms * 1e-3) / 1e9
+        traffic, tsrc = None, None
+        tfile = os.path.join(ROOT, "profiles", "r01_msda1d_fwd_traffic.json")
+        if os.path.exists(tfile):  # PMC pass of the same command (tools/pmc_traffic.py): HBM bytes per launch
+            with open(tfile) as f:
+                traffic = json.load(f).get("avg_bytes_per_launch")
+            tsrc = os.path.relpath(tfile, ROOT)
         result["roofline"] = {"kernel": "msda1d_fwd_kernel (fused MSDeformAttn forward)", "bound": "hbm",
                               "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                              "traffic": None, "avg_launch_us": avg_ms * 1e3,
+                              "traffic": traffic, "traffic_source": tsrc, "avg_launch_us": avg_ms * 1e3,
                               "alg_bytes_per_launch": avg_bytes}
     result["kernels"] = {n: {"launches": v["launches"], "avg_us": 1e3 * v["ms"] / max(v["launches"], 1),
                              "share_of_step": v["ms"] / (1e3 * el)} for n, v in ks.items()}

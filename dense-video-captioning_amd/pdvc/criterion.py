@@ -10,7 +10,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from . import box_ops
+from . import box_ops, hostio
 from .matcher import padded_targets
 
 COUNTER_CLASS_RATE = [0.00000000e+00, 0.00000000e+00, 1.93425917e-01, 4.12129084e-01, 1.88929963e-01,
@@ -66,14 +66,15 @@ class SetCriterion(nn.Module):
         N, Q, C = logits.shape
         dev = logits.device
         sizes = pt["sizes"]
-        nb = torch.tensor([max(float(e), 1.0) for e in sizes], device=dev)  # num_boxes clamp(min=1)
-        # matched pairs of every video, flattened: (video, query, target slot) -- one host->device copy
+        nb = pt["num_boxes"]  # (N,) float, clamp(min=1)
+        # matched pairs of every video, flattened: (video, query, target slot, rank) and the per-video match
+        # counts -- one asynchronous host->device copy
         vid = np.concatenate([np.full(len(i), v, np.int64) for v, (i, _) in enumerate(indices)])
         qid = np.concatenate([i.numpy() for i, _ in indices])
         tid = np.concatenate([j.numpy() for _, j in indices])
         rank = np.concatenate([np.arange(len(i)) for i, _ in indices])
-        pairs = torch.from_numpy(np.stack([vid, qid, tid, rank])).to(dev, non_blocking=True)
-        pv, pq, pt_, pr = pairs[0], pairs[1], pairs[2], pairs[3]
+        nmatch = np.asarray([len(i) for i, _ in indices], np.int64)
+        pv, pq, pt_, pr, n_dev = hostio.pack_to_device([vid, qid, tid, rank, nmatch], dev)
         # labels: focal loss over every query and class (criterion.py:46-65)
         tclass = torch.full((N, Q), self.num_classes, dtype=torch.int64, device=dev)
         tclass[pv, pq] = pt["labels"][pv, pt_]
@@ -84,14 +85,15 @@ class SetCriterion(nn.Module):
         loss_ce = focal.mean(1).sum(1) / nb * Q
         # counter (criterion.py:67-76)
         max_length = count.shape[1] - 1
-        ctgt = torch.tensor([min(e, max_length) for e in sizes], device=dev, dtype=torch.long)
+        ctgt = pt["sizes_long"].clamp(max=max_length)
         ctgt_onehot = torch.zeros_like(count)
         ctgt_onehot.scatter_(1, ctgt.unsqueeze(-1), 1)
-        weight = self.counter_class_rate[:max_length + 1].to(dev)
+        weight = hostio.const(("counter_class_rate", max_length), lambda: self.counter_class_rate[:max_length + 1],
+                              dev)
         loss_counter = counter_loss_terms(count, ctgt_onehot, self.opt.lloss_gau_mask, self.opt.lloss_beta, weight)
         # cardinality (logging only, criterion.py:80-92)
         card_pred = (logits.argmax(-1) != C - 1).sum(1).float()
-        card_err = (card_pred - torch.tensor([float(e) for e in sizes], device=dev)).abs()
+        card_err = (card_pred - pt["sizes_long"].float()).abs()
         # boxes (criterion.py:94-123): L1 and GIoU of matched pairs, per-video sums via index_add
         src = boxes[pv, pq]
         tgt = pt["boxes"][pv, pt_]
@@ -108,7 +110,7 @@ class SetCriterion(nn.Module):
         valid[pv, pr] = True
         iou = box_ops.box_iou(padded, padded)[0]
         iou = torch.triu(iou, diagonal=1) * (valid[:, :, None] & valid[:, None, :])
-        n = torch.tensor([float(len(i)) for i, _ in indices], device=dev)
+        n = n_dev.to(l1.dtype)
         loss_self_iou = iou.sum((1, 2)) / (0.5 * n * (n - 1))
         return {"loss_ce": loss_ce.mean(), "loss_counter": loss_counter.mean(), "loss_bbox": loss_bbox.mean(),
                 "loss_giou": loss_giou.mean(), "loss_self_iou": loss_self_iou.mean(),

@@ -81,5 +81,5 @@ def to_device(dt, device):
             out[k] = v
     out["cap_tensor_cpu"] = dt["cap_tensor"].clone()
     from .matcher import padded_targets
-    out["video_target_padded"] = padded_targets(out["video_target"], device)
+    out["video_target_padded"] = padded_targets(dt["video_target"], device)  # from the host copies
     return out

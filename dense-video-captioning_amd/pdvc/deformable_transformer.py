@@ -15,6 +15,8 @@ import torch.nn.functional as F
 from torch import nn
 from torch.nn.init import constant_, normal_, xavier_uniform_
 
+from . import hostio
+
 from .box_ops import inverse_sigmoid
 from .ops.modules import MSDeformAttn
 from .ops.functions.attention import query_self_attention
@@ -77,7 +79,8 @@ class DeformableTransformer(nn.Module):
         src_flatten = torch.cat(src_flatten, 1)
         mask_flatten = torch.cat(mask_flatten, 1)
         lvl_pos = torch.cat(lvl_pos, 1)
-        temporal_shapes = torch.as_tensor(level_T, dtype=torch.long, device=src_flatten.device)
+        temporal_shapes = hostio.const(("level_T", tuple(level_T)), lambda: torch.tensor(level_T, dtype=torch.long),
+                                       src_flatten.device)
         level_start_index = torch.cat((temporal_shapes.new_zeros((1,)), temporal_shapes.cumsum(0)[:-1]))
         valid_ratios = torch.stack([self.get_valid_ratio(m) for m in masks], 1)
         self.last_level_T = tuple(level_T)

@@ -10,6 +10,7 @@ import torch
 from scipy.optimize import linear_sum_assignment
 from torch import nn
 
+from . import hostio
 from .box_ops import box_cl_to_xy, generalized_box_iou
 
 
@@ -82,16 +83,20 @@ def padded_targets(targets, device):
     sizes = [len(t["labels"]) for t in targets]
     emax = max(max(sizes), 1)
     N = len(targets)
-    labels = torch.zeros(N, emax, dtype=torch.long, device=device)
-    boxes = torch.full((N, emax, 2), 0.5, device=device)
-    valid = torch.zeros(N, emax, dtype=torch.bool, device=device)
+    labels = torch.zeros(N, emax, dtype=torch.long)
+    boxes = torch.full((N, emax, 2), 0.5)
+    valid = torch.zeros(N, emax, dtype=torch.bool)
     for v, t in enumerate(targets):
         e = sizes[v]
         if e:
-            labels[v, :e] = t["labels"].to(device)
-            boxes[v, :e] = t["boxes"].to(device)
+            labels[v, :e] = t["labels"].detach().cpu()
+            boxes[v, :e] = t["boxes"].detach().cpu()
             valid[v, :e] = True
-    return {"labels": labels, "boxes": boxes, "valid": valid, "sizes": sizes}
+    sizes_t = torch.tensor(sizes, dtype=torch.long)
+    return {"labels": hostio.to_device(labels, device), "boxes": hostio.to_device(boxes, device),
+            "valid": hostio.to_device(valid, device), "sizes": sizes,
+            "sizes_long": hostio.to_device(sizes_t, device),
+            "num_boxes": hostio.to_device(sizes_t.float().clamp(min=1.0), device)}
 
 
 def build_matcher(args):

@@ -13,7 +13,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from . import box_ops
+from . import box_ops, hostio
 from .base_encoder import build_base_encoder
 from .box_ops import inverse_sigmoid
 from .CaptioningHead import build_captioner
@@ -170,11 +170,15 @@ class PDVC(nn.Module):
                     rows.append((l_id, v, (l_id * N + v) * Q + q, cap_off[v] + g))
         # layer-0 rows first: their reference is 1-d
         rows.sort(key=lambda r: (0 if r[0] == 0 else 1))
-        flat_idx = torch.tensor([r[2] for r in rows], dtype=torch.long)
-        cap_rows = torch.tensor([r[3] for r in rows], dtype=torch.long)
-        row_video = torch.tensor([r[1] for r in rows], dtype=torch.int32)
+        Ld_last = Ld - 1
+        last_sel = [i for i, r in enumerate(rows) if r[0] == Ld_last]
+        # every per-row index array in ONE asynchronous host->device copy
+        flat_idx, cap_rows, row_video, lay, vid, last_sel_d = hostio.pack_to_device(
+            [[r[2] for r in rows], [r[3] for r in rows], [r[1] for r in rows], [r[0] for r in rows],
+             [r[1] for r in rows], last_sel], dev)
+        row_video = row_video.to(torch.int32)
         rd1 = sum(1 for r in rows if r[0] == 0 and init_reference.shape[-1] == 1)
-        hs_rows = hs.reshape(Ld * N * Q, C).index_select(0, flat_idx.to(dev))
+        hs_rows = hs.reshape(Ld * N * Q, C).index_select(0, flat_idx)
         refs = []
         for l_id in range(Ld):
             reference = init_reference if l_id == 0 else inter_references[l_id - 1]
@@ -185,12 +189,12 @@ class PDVC(nn.Module):
                 ref = torch.cat([ref, torch.zeros_like(ref)], -1)
             refs.append(ref)
         ref_all = torch.stack(refs).reshape(Ld * N * Q, L, 2)
-        ref_rows = ref_all.index_select(0, flat_idx.to(dev))
+        ref_rows = ref_all.index_select(0, flat_idx)
         steps_v = []
         for v in range(N):
             steps_v.append(caption_steps(cap_cpu[cap_off[v]:cap_off[v + 1]]))
-        return dict(rows=rows, hs_rows=hs_rows, ref_rows=ref_rows.contiguous(), rd1=rd1,
-                    row_video=row_video.to(dev), cap_rows=cap_rows.to(dev), steps_v=steps_v)
+        return dict(rows=rows, hs_rows=hs_rows, ref_rows=ref_rows.contiguous(), rd1=rd1, row_video=row_video,
+                    cap_rows=cap_rows, lay=lay, vid=vid, last_sel=last_sel_d, steps_v=steps_v)
 
     def parallel_prediction_matched(self, dt, criterion, hs, init_reference, inter_references, others,
                                     disable_refine):
@@ -218,9 +222,7 @@ class PDVC(nn.Module):
         cap_loss = self.caption_head[0].build_loss(logprobs, seq_rows[:, 1:], cap_mask_rows[:, 1:].float())
         # per (layer, video) mean over events, then mean over videos (= the reference's batch-1 losses)
         rows = R["rows"]
-        lay = torch.tensor([r[0] for r in rows], device=hs.device)
-        vid = torch.tensor([r[1] for r in rows], device=hs.device)
-        key = lay * N + vid
+        key = R["lay"] * N + R["vid"]
         sums = torch.zeros(Ld * N, device=hs.device, dtype=cap_loss.dtype).index_add_(0, key, cap_loss)
         cnts = torch.zeros(Ld * N, device=hs.device, dtype=cap_loss.dtype).index_add_(
             0, key, torch.ones_like(cap_loss))
@@ -228,8 +230,7 @@ class PDVC(nn.Module):
         for l_id in range(Ld):
             k = "loss_caption" if l_id == Ld - 1 else f"loss_caption_{l_id}"
             loss[k] = per[l_id]
-        last_sel = torch.tensor([i for i, r in enumerate(rows) if r[0] == Ld - 1], dtype=torch.long,
-                                device=hs.device)
+        last_sel = R["last_sel"]
         last_v = [r[1] for r in rows if r[0] == Ld - 1]
         n_last = max([R["steps_v"][v] for v in last_v], default=0)
         out.update({"caption_probs": {"cap_prob_train": logprobs.index_select(0, last_sel)[:, :n_last]},
