@@ -45,166 +45,213 @@ __device__ __forceinline__ int lvl_sel(const int (&v)[kL], int l) {
 }
 
 // -------------------------------------------------------------------------------------------------
-// forward
+// Mapping shared by the forward and the query-side backward: one wave = QPW = 64/LPH consecutive queries of
+// ONE (video, head); a workgroup = 4 waves = 4*QPW consecutive queries of that head.  Consecutive encoder
+// queries are neighbouring positions of one level, so a workgroup's samples fall in a narrow window of every
+// level: its value rows (256 B per head and position) are re-read from L1 instead of L2.  Within a lane
+// group (LPH lanes = one query), lane `sub` owns samples j = sub + LPH*k for the parameter phase (coalesced
+// logits/offsets, softmax by group shuffles) and hands each sample's row and corner weights to the group by
+// shuffles for the gather phase, which is unrolled over the 16 samples with a scheduling barrier per level
+// (each level's 2*P corner loads in flight together, no cross-level hoisting).
 // -------------------------------------------------------------------------------------------------
+template <int LPH>
+__device__ __forceinline__ float group_max(float v) {
+#pragma unroll
+    for (int d = 1; d < LPH; d <<= 1) v = fmaxf(v, __shfl_xor(v, d, PDVC_WAVE));
+    return v;
+}
+
+struct WaveQuery {
+    int b, m, q, row, sub, gbase;
+    bool active;
+};
+
+template <int LPH>
+__device__ __forceinline__ WaveQuery wave_query(int wave, int lane, int Lq, int M) {
+    constexpr int QPW = 64 / LPH;
+    const int qg_per = (Lq + QPW - 1) / QPW;
+    const int bm = wave / qg_per;
+    const int qg = wave - bm * qg_per;
+    WaveQuery w;
+    w.b = bm / M;
+    w.m = bm - w.b * M;
+    const int q = qg * QPW + lane / LPH;
+    w.active = q < Lq;
+    w.q = w.active ? q : Lq - 1;
+    w.row = w.b * Lq + w.q;
+    w.sub = lane % LPH;
+    w.gbase = lane - w.sub;
+    return w;
+}
+
+// forward
 template <int CPL, int LPH, int RD>
 __global__ __launch_bounds__(256) void msda1d_fwd_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
     int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
-    int D, int waves_per_row, int total_waves, float* __restrict__ out, float* __restrict__ save_attn,
+    int D, int total_waves, float* __restrict__ out, float* __restrict__ save_attn,
     float* __restrict__ save_loc) {
-    constexpr int HPW = 64 / LPH;
+    constexpr int JPL = kNS / LPH;  // samples owned per lane in the parameter phase
     const int lane = threadIdx.x & 63;
-    const int lb = xcd_remap(blockIdx.x, gridDim.x);
-    const int wave = lb * 4 + (threadIdx.x >> 6);
-    if (wave >= total_waves) return;
-    const int row = wave / waves_per_row;
-    const int hg = wave - row * waves_per_row;
-    const int b = row / Lq;
-    const int sub = lane % LPH;
-    const int m = hg * HPW + lane / LPH;
-    if (m >= M) return;
-    const int c0 = sub * CPL;
-    const float* logits = proj + (size_t)row * proj_stride + logit_base + m * kNS;
-    const float* offs = proj + (size_t)row * proj_stride + off_base + m * kNS;
+    const int wave = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    if (wave >= total_waves) return;  // wave-uniform
+    const WaveQuery w = wave_query<LPH>(wave, lane, Lq, M);
+    const size_t MD = (size_t)M * D;
+    const uint8_t* mbase = vmask ? vmask + (size_t)w.b * S : nullptr;
+    const float* prow = proj + (size_t)w.row * proj_stride;
 
-    // softmax statistics over the head's L*P logits (ms_deform_attn.py:168-169); weights formed per level
-    float mx = -INFINITY;
+    // parameter phase (ms_deform_attn.py:168-177, same evaluation order): softmax weight, location, corner
+    // row and the two corner weights (0 where the reference skips the corner or the row is padding)
+    float lg[JPL], mx = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < kNS; ++j) mx = fmaxf(mx, logits[j]);
+    for (int k = 0; k < JPL; ++k) {
+        lg[k] = prow[logit_base + w.m * kNS + w.sub + LPH * k];
+        mx = fmaxf(mx, lg[k]);
+    }
+    mx = group_max<LPH>(mx);
     float sum = 0.f;
 #pragma unroll
-    for (int j = 0; j < kNS; ++j) sum += expf(logits[j] - mx);
-
-    const size_t MD = (size_t)M * D;
-    const float* vbase = value + (size_t)b * S * MD + (size_t)m * D + c0;
-    const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
-    VecF<CPL> acc;
-    acc.zero();
-#pragma unroll 1
-    for (int l = 0; l < kL; ++l) {
+    for (int k = 0; k < JPL; ++k) sum += expf(lg[k] - mx);
+    sum = group_allreduce<LPH>(sum);
+    int i0v[JPL];
+    float w1v[JPL], w2v[JPL];
+#pragma unroll
+    for (int k = 0; k < JPL; ++k) {
+        const int j = w.sub + LPH * k;
+        const int l = j / kP;
         const int T = lvl_sel(lv.T, l), st = lvl_sel(lv.start, l);
         const float Tf = (float)T;
-        const float r0 = ref[((size_t)row * kL + l) * RD];
-        const float r1 = (RD == 2) ? ref[((size_t)row * kL + l) * RD + 1] : 0.f;
-        // positions of the level's P points, then all 2*P corner rows loaded together (clamped addresses;
-        // out-of-range corners are selected to 0 after the load: no data-dependent branches around loads)
-        int i0[kP];
-        float lw[kP], aw[kP];
-        bool ok1[kP], ok2[kP];
+        const float aw = expf(lg[k] - mx) / sum;
+        const float off = prow[off_base + w.m * kNS + j];
+        const float r0 = ref[((size_t)w.row * kL + l) * RD];
+        const float r1 = (RD == 2) ? ref[((size_t)w.row * kL + l) * RD + 1] : 0.f;
+        const float loc = (RD == 1) ? r0 + off / Tf : r0 + ((off / (float)kP) * r1) * 0.5f;
+        if (save_loc && w.active) {
+            const size_t si = ((size_t)w.row * M + w.m) * kNS + j;
+            save_loc[si] = loc;
+            save_attn[si] = aw;
+        }
+        const float x = loc * Tf - 0.5f;  // w_im (.cuh:284); h_im == 0 for H == 1
+        const bool inside = x > -1.f && x < Tf;
+        const float xf = floorf(inside ? x : 0.f);
+        const int i0 = (int)xf;
+        const float lw = inside ? x - xf : 0.f;
+        bool ok1 = inside && i0 >= 0, ok2 = inside && i0 + 1 <= T - 1;
+        if (mbase) {
+            ok1 = ok1 && !mbase[st + min(max(i0, 0), T - 1)];
+            ok2 = ok2 && !mbase[st + min(max(i0 + 1, 0), T - 1)];
+        }
+        i0v[k] = i0;
+        w1v[k] = ok1 ? (1.f - lw) * aw : 0.f;
+        w2v[k] = ok2 ? lw * aw : 0.f;
+    }
+
+    const float* vbase = value + (size_t)w.b * S * MD + (size_t)w.m * D + w.sub * CPL;
+    VecF<CPL> acc;
+    acc.zero();
+#pragma unroll
+    for (int l = 0; l < kL; ++l) {
+        const int T = lv.T[l], st = lv.start[l];
+        VecF<CPL> v1[kP], v2[kP];
+        float c1[kP], c2[kP];
 #pragma unroll
         for (int p = 0; p < kP; ++p) {
             const int j = l * kP + p;
-            aw[p] = expf(logits[j] - mx) / sum;
-            const float off = offs[j];
-            // ms_deform_attn.py:171-177 (same evaluation order)
-            const float loc = (RD == 1) ? r0 + off / Tf : r0 + ((off / (float)kP) * r1) * 0.5f;
-            if (save_loc && sub == (j % LPH)) {
-                const size_t si = ((size_t)row * M + m) * kNS + j;
-                save_loc[si] = loc;
-                save_attn[si] = aw[p];
-            }
-            const float x = loc * Tf - 0.5f;  // w_im (.cuh:284); h_im == 0 for H == 1
-            const bool inside = x > -1.f && x < Tf;
-            const float xf = floorf(inside ? x : 0.f);
-            i0[p] = (int)xf;
-            lw[p] = inside ? x - xf : 0.f;
-            ok1[p] = inside && i0[p] >= 0;
-            ok2[p] = inside && i0[p] + 1 <= T - 1;
-        }
-        VecF<CPL> v1[kP], v2[kP];
-#pragma unroll
-        for (int p = 0; p < kP; ++p) {
-            const int a1 = min(max(i0[p], 0), T - 1), a2 = min(max(i0[p] + 1, 0), T - 1);
+            const int src = w.gbase + j % LPH;
+            const int i0 = __shfl(i0v[j / LPH], src, PDVC_WAVE);
+            c1[p] = __shfl(w1v[j / LPH], src, PDVC_WAVE);
+            c2[p] = __shfl(w2v[j / LPH], src, PDVC_WAVE);
+            const int a1 = min(max(i0, 0), T - 1), a2 = min(max(i0 + 1, 0), T - 1);
             v1[p].load(vbase + (size_t)(st + a1) * MD);
             v2[p].load(vbase + (size_t)(st + a2) * MD);
-            if (mbase) {
-                ok1[p] = ok1[p] && !mbase[st + a1];
-                ok2[p] = ok2[p] && !mbase[st + a2];
-            }
         }
 #pragma unroll
         for (int p = 0; p < kP; ++p) {
-            const float hw = 1.f - lw[p];
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                const float x1 = ok1[p] ? v1[p].v[c] : 0.f, x2 = ok2[p] ? v2[p].v[c] : 0.f;
-                acc.v[c] += (hw * x1 + lw[p] * x2) * aw[p];
-            }
+            for (int c = 0; c < CPL; ++c) acc.v[c] += c1[p] * v1[p].v[c] + c2[p] * v2[p].v[c];
         }
+        __builtin_amdgcn_sched_barrier(0);
     }
-    acc.store(out + (size_t)row * MD + (size_t)m * D + c0);
+    if (w.active) acc.store(out + (size_t)w.row * MD + (size_t)w.m * D + w.sub * CPL);
 }
 
 // -------------------------------------------------------------------------------------------------
 // backward, query side: grad of the offset and attention logits (+ reference points)
 // softmax backward uses delta = sum_j a_j dL/da_j = <dL/dout, out> (out = the forward output of this head),
 // so every level's samples are finished as soon as they are reduced -- no state carried across levels.
+// grad_ref sums over the heads of a query, which live in different waves: atomics (zeroed by the host).
 // -------------------------------------------------------------------------------------------------
 template <int CPL, int LPH, int RD>
 __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
     int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
-    int D, int waves_per_row, int total_waves, const float* __restrict__ gout, const float* __restrict__ fout,
+    int D, int total_waves, const float* __restrict__ gout, const float* __restrict__ fout,
     const float* __restrict__ save_attn, const float* __restrict__ save_loc, float* __restrict__ grad_proj,
     float* __restrict__ grad_ref) {
-    constexpr int HPW = 64 / LPH;
+    constexpr int JPL = kNS / LPH;
     constexpr int G = LPH < 8 ? LPH : 8;  // reduce-scatter group for the level's 8 partial sums
     constexpr int VPL = 8 / G;            // values per lane after it (interleaved (ga, gs) pairs)
     const int lane = threadIdx.x & 63;
-    const int lb = xcd_remap(blockIdx.x, gridDim.x);
-    const int wave = lb * 4 + (threadIdx.x >> 6);
+    const int wave = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
     if (wave >= total_waves) return;  // wave-uniform
-    const int row = wave / waves_per_row;
-    const int hg = wave - row * waves_per_row;
-    const int b = row / Lq;
-    const int sub = lane % LPH;
-    const int m_raw = hg * HPW + lane / LPH;
-    const bool active = m_raw < M;
-    const int m = active ? m_raw : 0;
-    const int c0 = sub * CPL;
+    const WaveQuery w = wave_query<LPH>(wave, lane, Lq, M);
     const size_t MD = (size_t)M * D;
-    const float* vbase = value + (size_t)b * S * MD + (size_t)m * D + c0;
-    const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
-    const size_t sbase = ((size_t)row * M + m) * kNS;
+    const uint8_t* mbase = vmask ? vmask + (size_t)w.b * S : nullptr;
+    const size_t sbase = ((size_t)w.row * M + w.m) * kNS;
+    const int c0 = w.sub * CPL;
 
     VecF<CPL> g, o;
-    load_row(g, gout + (size_t)row * MD + (size_t)m * D + c0, active);
-    load_row(o, fout + (size_t)row * MD + (size_t)m * D + c0, active);
+    g.load(gout + (size_t)w.row * MD + (size_t)w.m * D + c0);
+    o.load(fout + (size_t)w.row * MD + (size_t)w.m * D + c0);
     float dl = 0.f;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) dl += g.v[c] * o.v[c];
     const float delta = group_allreduce<LPH>(dl);
 
-    const float* prow = proj + (size_t)row * proj_stride;
-    float* gprow = grad_proj + (size_t)row * proj_stride;
-#pragma unroll 1
-    for (int l = 0; l < kL; ++l) {
+    // parameter phase: corner row and (masked) corner weights of the lane's samples
+    int i0v[JPL];
+    float lwv[JPL];
+    int okv[JPL];
+#pragma unroll
+    for (int k = 0; k < JPL; ++k) {
+        const int j = w.sub + LPH * k;
+        const int l = j / kP;
         const int T = lvl_sel(lv.T, l), st = lvl_sel(lv.start, l);
         const float Tf = (float)T;
-        int i0[kP];
-        float lw[kP];
-        bool ok1[kP], ok2[kP];
-#pragma unroll
-        for (int p = 0; p < kP; ++p) {
-            const float x = (active ? save_loc[sbase + l * kP + p] : 0.f) * Tf - 0.5f;
-            const bool inside = active && x > -1.f && x < Tf;
-            const float xf = floorf(inside ? x : 0.f);
-            i0[p] = (int)xf;
-            lw[p] = inside ? x - xf : 0.f;
-            ok1[p] = inside && i0[p] >= 0;
-            ok2[p] = inside && i0[p] + 1 <= T - 1;
+        const float x = save_loc[sbase + j] * Tf - 0.5f;
+        const bool inside = x > -1.f && x < Tf;
+        const float xf = floorf(inside ? x : 0.f);
+        const int i0 = (int)xf;
+        bool ok1 = inside && i0 >= 0, ok2 = inside && i0 + 1 <= T - 1;
+        if (mbase) {
+            ok1 = ok1 && !mbase[st + min(max(i0, 0), T - 1)];
+            ok2 = ok2 && !mbase[st + min(max(i0 + 1, 0), T - 1)];
         }
+        i0v[k] = i0;
+        lwv[k] = inside ? x - xf : 0.f;
+        okv[k] = (ok1 ? 1 : 0) | (ok2 ? 2 : 0);
+    }
+
+    const float* vbase = value + (size_t)w.b * S * MD + (size_t)w.m * D + c0;
+    const float* prow = proj + (size_t)w.row * proj_stride;
+    float* gprow = grad_proj + (size_t)w.row * proj_stride;
+#pragma unroll
+    for (int l = 0; l < kL; ++l) {
+        const int T = lv.T[l], st = lv.start[l];
+        const float Tf = (float)T;
         VecF<CPL> v1[kP], v2[kP];
+        float lw[kP];
+        int ok[kP];
 #pragma unroll
         for (int p = 0; p < kP; ++p) {  // all 2*P corner loads in flight together (clamped, selected later)
-            const int a1 = min(max(i0[p], 0), T - 1), a2 = min(max(i0[p] + 1, 0), T - 1);
+            const int j = l * kP + p;
+            const int src = w.gbase + j % LPH;
+            const int i0 = __shfl(i0v[j / LPH], src, PDVC_WAVE);
+            lw[p] = __shfl(lwv[j / LPH], src, PDVC_WAVE);
+            ok[p] = __shfl(okv[j / LPH], src, PDVC_WAVE);
+            const int a1 = min(max(i0, 0), T - 1), a2 = min(max(i0 + 1, 0), T - 1);
             v1[p].load(vbase + (size_t)(st + a1) * MD);
             v2[p].load(vbase + (size_t)(st + a2) * MD);
-            if (mbase) {
-                ok1[p] = ok1[p] && !mbase[st + a1];
-                ok2[p] = ok2[p] && !mbase[st + a2];
-            }
         }
         // part[2p] = sum_c g*val ; part[2p+1] = sum_c g*(v2 - v1) over this lane's channels
         float part[2 * kP];
@@ -214,7 +261,7 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
             float s1 = 0.f, s2 = 0.f;
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
-                const float x1 = ok1[p] ? v1[p].v[c] : 0.f, x2 = ok2[p] ? v2[p].v[c] : 0.f;
+                const float x1 = (ok[p] & 1) ? v1[p].v[c] : 0.f, x2 = (ok[p] & 2) ? v2[p].v[c] : 0.f;
                 s1 += g.v[c] * (hw * x1 + lw[p] * x2);
                 s2 += g.v[c] * (x2 - x1);
             }
@@ -230,7 +277,7 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
         // group lane r (= sub % G) holds values [r*VPL, (r+1)*VPL) of the interleaved (ga, gs) list
         float ga, gs;
         int p;
-        const int r = sub % G;
+        const int r = w.sub % G;
         if (VPL == 2) {
             p = r;
             ga = part[0];
@@ -241,9 +288,9 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
             ga = (r & 1) ? other : part[0];
             gs = (r & 1) ? part[0] : other;
         }
-        const bool owner = active && sub < G && (VPL == 2 || (r & 1) == 0);
+        const bool owner = w.active && w.sub < G && (VPL == 2 || (r & 1) == 0);
         const int j = l * kP + p;
-        const float a = active ? save_attn[sbase + j] : 0.f;
+        const float a = save_attn[sbase + j];
         // CUDA: grad_loc_w = W * grad_w_weight * (top_grad * attn), summed over channels (.cuh:158)
         const float gloc = owner ? Tf * (gs * a) : 0.f;
         float g0 = gloc, g1 = 0.f;
@@ -252,32 +299,25 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
             if (RD == 1) {
                 goff = gloc / Tf;
             } else {
-                const float rr1 = ref[((size_t)row * kL + l) * 2 + 1];
+                const float rr1 = ref[((size_t)w.row * kL + l) * 2 + 1];
                 const float t2 = gloc * 0.5f;
                 goff = (t2 * rr1) / (float)kP;
-                g1 = t2 * (prow[off_base + m * kNS + j] / (float)kP);
+                g1 = t2 * (prow[off_base + w.m * kNS + j] / (float)kP);
             }
-            gprow[off_base + m * kNS + j] = goff;
-            gprow[logit_base + m * kNS + j] = a * (ga - delta);
+            gprow[off_base + w.m * kNS + j] = goff;
+            gprow[logit_base + w.m * kNS + j] = a * (ga - delta);
         }
         if (grad_ref) {
-            // sum over every head and point of the row (all lanes), then atomics across waves of a row
-#pragma unroll
-            for (int d = 32; d > 0; d >>= 1) {
-                g0 += __shfl_xor(g0, d, PDVC_WAVE);
-                if (RD == 2) g1 += __shfl_xor(g1, d, PDVC_WAVE);
-            }
-            if (lane == 0) {
-                float* dst = grad_ref + ((size_t)row * kL + l) * RD;
-                if (waves_per_row == 1) {
-                    dst[0] = g0;
-                    if (RD == 2) dst[1] = g1;
-                } else {
-                    atomicAdd(dst, g0);
-                    if (RD == 2) atomicAdd(dst + 1, g1);
-                }
+            // sum over the query's points of this level (its lane group), one atomic per (query, head, level)
+            g0 = group_allreduce<LPH>(g0);
+            if (RD == 2) g1 = group_allreduce<LPH>(g1);
+            if (w.sub == 0 && w.active) {
+                float* dst = grad_ref + ((size_t)w.row * kL + l) * RD;
+                atomicAdd(dst, g0);
+                if (RD == 2) atomicAdd(dst + 1, g1);
             }
         }
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -467,8 +507,14 @@ static int fill_levels(const int32_t* level_T, int num_levels, int num_point, Le
 }
 
 struct Geometry {
-    int cpl, lph, hpw, waves_per_row;
+    int cpl, lph;
 };
+
+// waves of the query-tile mapping: one per (video, head, group of 64/LPH queries)
+static long query_waves(const Geometry& g, int batch, int num_heads, int num_query) {
+    const int qpw = 64 / g.lph;
+    return (long)batch * num_heads * ((num_query + qpw - 1) / qpw);
+}
 
 static int pick_geometry(int M, int D, Geometry& g) {
     // 4 channels (one float4) per lane keeps a level's 2*P corner loads in flight within the register budget
@@ -477,8 +523,6 @@ static int pick_geometry(int M, int D, Geometry& g) {
     else if (D == 128) g.cpl = 8;
     else return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "fused 1-D path supports head_dim 16/32/64/128, got %d", D);
     g.lph = D / g.cpl;
-    g.hpw = 64 / g.lph;
-    g.waves_per_row = (M + g.hpw - 1) / g.hpw;
     return PDVC_OK;
 }
 
@@ -490,7 +534,7 @@ template <int RD>
 static void launch_fwd1d(const Geometry& g, dim3 grid, hipStream_t s, const float* value, const uint8_t* mask,
                          const float* proj, int ps, int ob, int lb, const float* ref, Levels1d lv, int Lq, int S,
                          int M, int D, int tw, float* out, float* sa, float* sl) {
-#define ARGS value, mask, proj, ps, ob, lb, ref, lv, Lq, S, M, D, g.waves_per_row, tw, out, sa, sl
+#define ARGS value, mask, proj, ps, ob, lb, ref, lv, Lq, S, M, D, tw, out, sa, sl
     if (g.cpl == 8) hipLaunchKernelGGL((msda1d_fwd_kernel<8, 16, RD>), grid, dim3(256), 0, s, ARGS);
     else if (g.lph == 4) hipLaunchKernelGGL((msda1d_fwd_kernel<4, 4, RD>), grid, dim3(256), 0, s, ARGS);
     else if (g.lph == 8) hipLaunchKernelGGL((msda1d_fwd_kernel<4, 8, RD>), grid, dim3(256), 0, s, ARGS);
@@ -503,7 +547,7 @@ static void launch_bwdq1d(const Geometry& g, dim3 grid, hipStream_t s, const flo
                           const float* proj, int ps, int ob, int lb, const float* ref, Levels1d lv, int Lq, int S,
                           int M, int D, int tw, const float* gout, const float* fout, const float* sa, const float* sl,
                           float* gp, float* gr) {
-#define ARGS value, mask, proj, ps, ob, lb, ref, lv, Lq, S, M, D, g.waves_per_row, tw, gout, fout, sa, sl, gp, gr
+#define ARGS value, mask, proj, ps, ob, lb, ref, lv, Lq, S, M, D, tw, gout, fout, sa, sl, gp, gr
     if (g.cpl == 8) hipLaunchKernelGGL((msda1d_bwd_query_kernel<8, 16, RD>), grid, dim3(256), 0, s, ARGS);
     else if (g.lph == 4) hipLaunchKernelGGL((msda1d_bwd_query_kernel<4, 4, RD>), grid, dim3(256), 0, s, ARGS);
     else if (g.lph == 8) hipLaunchKernelGGL((msda1d_bwd_query_kernel<4, 8, RD>), grid, dim3(256), 0, s, ARGS);
@@ -529,8 +573,7 @@ extern "C" int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_
     PDVC_CHECK_ARG(off_base >= 0 && logit_base >= 0 && off_base + NSM <= proj_stride && logit_base + NSM <= proj_stride,
                    "proj columns out of range (stride %d, off %d, logit %d, need %d)", proj_stride, off_base,
                    logit_base, NSM);
-    const long rows = (long)batch * num_query;
-    const long tw = rows * g.waves_per_row;
+    const long tw = query_waves(g, batch, num_heads, num_query);
     if (tw == 0) return PDVC_OK;
     PDVC_CHECK_ARG(tw < (1L << 31) / 4, "too many rows");
     dim3 grid((unsigned)((tw + 3) / 4));
@@ -565,8 +608,8 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
                    "proj columns out of range");
     hipStream_t s = (hipStream_t)stream;
     const long rows = (long)batch * num_query;
-    const long tw = rows * g.waves_per_row;
-    if (grad_ref && g.waves_per_row > 1 && rows > 0) {
+    const long tw = query_waves(g, batch, num_heads, num_query);
+    if (grad_ref && rows > 0) {  // accumulated over the heads with atomics
         hipError_t e = hipMemsetAsync(grad_ref, 0, sizeof(float) * rows * kL * ref_dim, s);
         if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_ref: %s", hipGetErrorString(e));
     }

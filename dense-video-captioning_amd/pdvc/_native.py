@@ -31,6 +31,7 @@ SIGNATURES = {
     "pdvc_softattn_backward_f32": [_vp, _vp, _i, _vp, _vp, _vp, _vp] + [_i] * 4 + [_vp, _vp, _i, _vp, _vp, _vp, _vp],
     "pdvc_lstm_cell_forward_f32": [_vp, _i, _vp, _i, _vp, _i, _vp, _i, _i, _vp, _i, _vp, _vp, _vp],
     "pdvc_lstm_cell_backward_f32": [_vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _i, _vp, _vp],
+    "pdvc_gemm_f32": [_i, _i, _i, _vp, _i, _i, _vp, _i, _i, _vp, _i, _vp, _i, _i, _vp],
     "pdvc_mha_forward_f32": [_vp, _vp, _u8p] + [_i] * 4 + [_f, _u64] + [_vp] * 3,
     "pdvc_mha_backward_f32": [_vp, _vp, _u8p, _vp, _vp, _vp] + [_i] * 4 + [_f, _u64] + [_vp] * 4,
 }
@@ -106,6 +107,13 @@ def ptr(t):
         raise NativeError("PDVC HIP ops need GPU tensors (there is no CPU implementation)")
     if not t.is_contiguous():
         raise NativeError("PDVC HIP ops need contiguous tensors")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def ptr_any(t):
+    """Device pointer of a (possibly strided) GPU tensor; the caller passes its strides to the kernel."""
+    if not t.is_cuda:
+        raise NativeError("PDVC HIP ops need GPU tensors (there is no CPU implementation)")
     return ctypes.c_void_p(t.data_ptr())
 
 

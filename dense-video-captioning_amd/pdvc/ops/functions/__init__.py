@@ -1,3 +1,4 @@
 from .ms_deform_attn_func import (MSDeformAttnFunction, ms_deform_attn_core_pytorch, MSDA1dFunction, NUM_SAMPLES_FUSED,
                                   CapGatherFunction)
 from .caption_decode import CaptionDecodeFunction
+from .linear import LinearFunction, linear, matmul

@@ -1,0 +1,86 @@
+"""fp32 matrix products on the gfx950 matrix cores (csrc/gemm.hip, pdvc_gemm_f32) and nn.Linear on them.
+
+`matmul(a, b)` takes op(A) (M,K) and op(B) (K,N) as logical 2-D views and passes their storage order to the
+kernel (a row-major or a transposed view of row-major memory both go without a copy).  LinearFunction is
+nn.Linear's forward/backward (y = x W^T + b; dx = dy W; dW = dy^T x split over the rows with atomics;
+db = sum dy) -- the projections of MSDeformAttn and the FFNs."""
+import torch
+from torch.autograd import Function
+
+from pdvc import _native as _n
+
+CU = 256  # MI355X compute units
+
+
+def _operand(t):
+    """(tensor, transposed flag, leading dimension) for a logical 2-D operand."""
+    if t.stride(1) == 1 and t.stride(0) >= t.shape[1]:
+        return t, 0, max(t.stride(0), 1)
+    if t.stride(0) == 1 and t.stride(1) >= t.shape[0]:
+        return t, 1, max(t.stride(1), 1)
+    t = t.contiguous()
+    return t, 0, max(t.stride(0), 1)
+
+
+def _split_k(M, N, K):
+    tiles = ((M + 127) // 128) * ((N + 127) // 128)
+    if tiles >= CU or K < 1024:
+        return 1
+    return max(1, min(2 * CU // tiles, K // 512))
+
+
+def matmul(a, b, bias=None, relu=False, out=None, accumulate=False):
+    """op(a) (M,K) @ op(b) (K,N) (+ bias) (ReLU) -> (M,N) fp32.  accumulate=True adds into `out` (split-K)."""
+    if a.dtype != torch.float32 or b.dtype != torch.float32:
+        raise TypeError("pdvc matmul is fp32")
+    M, K = a.shape
+    K2, N = b.shape
+    if K != K2:
+        raise ValueError(f"inner dimensions differ: {tuple(a.shape)} @ {tuple(b.shape)}")
+    a, ta, lda = _operand(a)
+    b, tb, ldb = _operand(b)
+    if accumulate:
+        if out is None or bias is not None or relu:
+            raise ValueError("accumulate needs `out` and no epilogue")
+        epi, split = 3, _split_k(M, N, K)
+    else:
+        epi = 0 if bias is None else (2 if relu else 1)
+        split = 1
+        if out is None:
+            out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    if bias is not None:
+        bias = bias.contiguous()
+    if out.stride(1) != 1:
+        raise ValueError("out must have unit column stride")
+    _n.call("pdvc_gemm_f32", M, N, K, _n.ptr_any(a), lda, ta, _n.ptr_any(b), ldb, tb, _n.ptr_any(out), out.stride(0),
+            _n.ptr(bias), epi, split, _n.stream())
+    return out
+
+
+class LinearFunction(Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        y = matmul(x2, weight.t(), bias=bias)
+        ctx.save_for_backward(x2, weight)
+        ctx.has_bias = bias is not None
+        return y.view(*shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, weight = ctx.saved_tensors
+        gy2 = gy.reshape(-1, weight.shape[0])
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = matmul(gy2, weight).view(*gy.shape[:-1], weight.shape[1])
+        if ctx.needs_input_grad[1]:
+            gw = torch.zeros_like(weight)
+            matmul(gy2.t(), x2, out=gw, accumulate=True)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = gy2.sum(0)
+        return gx, gw, gb
+
+
+def linear(x, weight, bias=None):
+    return LinearFunction.apply(x, weight, bias)

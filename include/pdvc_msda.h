@@ -31,6 +31,10 @@
  *                                      ShowAttendTellCore.forward (pdvc/CaptioningHead/LSTM_DSA.py:206-207,261)
  *   pdvc_softattn_*                 <- ShowAttendTellCore's soft attention over the 16 samples
  *                                      (LSTM_DSA.py:245-258: tanh, alpha_net, softmax, weighted sum)
+ *   pdvc_gemm_f32                   <- the dense projections (nn.Linear forward/backward) of the layers
+ *                                      above: MSDeformAttn value/offset/output projections
+ *                                      (ms_deform_attn.py:79-126), the FFNs (deformable_transformer.py:150-156,
+ *                                      240-243), fp32 on the f32-input matrix cores
  */
 #ifndef PDVC_MSDA_H
 #define PDVC_MSDA_H
@@ -183,6 +187,14 @@ int pdvc_lstm_cell_backward_f32(const float* grad_h, int ld_grad_h, const float*
                                 const float* grad_c_next, const float* acts, const float* c_prev, const float* c,
                                 int rows, int hidden, float* grad_gates, int ld_grad_gates, float* grad_c_prev,
                                 void* stream);
+
+/* ---- fp32 GEMM on the matrix cores ----------------------------------------------------------------
+ * C[M,N] = op(A)[M,K] op(B)[K,N] (+ bias[N]) (ReLU).  op(A): trans_a 0 -> A[m*lda + k], 1 -> A[k*lda + m];
+ * op(B): trans_b 0 -> B[k*ldb + n], 1 -> B[n*ldb + k].  epilogue 0 store, 1 + bias, 2 + bias then ReLU,
+ * 3 atomic accumulate into C (the only epilogue allowed with split_k > 1; C is ACCUMULATED, zero it first).
+ * Exact f32 products (v_mfma_f32_32x32x2_f32); summation order differs from a sequential loop. */
+int pdvc_gemm_f32(int M, int N, int K, const float* A, int lda, int trans_a, const float* B, int ldb, int trans_b,
+                  float* C, int ldc, const float* bias, int epilogue, int split_k, void* stream);
 
 #ifdef __cplusplus
 }
