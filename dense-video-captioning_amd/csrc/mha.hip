@@ -4,13 +4,16 @@
 // (pdvc/deformable_transformer.py:231,256-258; torch's multi_head_attention_forward with need_weights):
 //   P = softmax(q * sqrt(1/D) . k^T  [+ -inf at padded keys]),  P_d = dropout(P),  O = P_d . v
 // The in/out projections stay GEMMs (hipBLASLt through torch).  PDVC's shape is tiny and latency-bound
-// (Q = 100..300 queries, D = 64, 8 heads per video), so one workgroup owns one (video, head): K and V are
-// staged once in LDS (rows padded to D+1 floats: conflict-free when lanes walk keys), each wave takes whole
+// (Q = 100..300 queries, D = 64, 8 heads per video), so a workgroup owns 16 queries of one (video, head): K and V
+// are staged in LDS (rows padded to D+1 floats: conflict-free when lanes walk keys), each wave takes whole
 // query rows, a lane owns one key for the scores (exact softmax over <= 5 keys per lane + wave reductions) and
-// one channel for P.V.  No MFMA: the core is ~2.6 MFLOP per head at Q = 100.
+// one channel for P.V.  The dropout seed may come from device memory (seed_dev), so a captured hipGraph
+// replays with a fresh seed drawn by the graph itself.  No MFMA: the core is ~2.6 MFLOP per head at Q = 100.
 // Backward: phase A (query-major) recomputes P from the saved log-sum-exp, forms dS = P (dP - delta) with
-// delta = dO . O, writes dq, and stages P_d and dS rows in a global workspace; phase B (key-major, same
-// workgroup, after a barrier) forms dK = dS^T q_scaled and dV = P_d^T dO with lanes over channels.
+// delta = dO . O, writes dq, and stages P_d and dS rows in a global workspace; phase B (key-major, a second
+// launch) forms dK = dS^T q_scaled and dV = P_d^T dO with lanes over channels.  Every launch has one
+// workgroup per (video, head, chunk of 16 queries or keys): ~1800 workgroups at PDVC's batch instead of 256,
+// K/V (or dO/q) staged per workgroup from L2.
 // Dropout keeps a counter-hash mask of (seed, video, head, query, key) -- regenerated in the backward.
 #include "pdvc_common.h"
 
@@ -44,14 +47,24 @@ __device__ __forceinline__ float wave_add(float v) {
 
 constexpr int kKPL = (kMaxQ + 63) / 64;  // keys per lane
 
+constexpr int kQB = 16;  // queries (forward / backward phase A) or keys (phase B) per workgroup
+
+__device__ __forceinline__ uint64_t load_seed(uint64_t seed, const uint64_t* seed_dev) {
+    return seed_dev ? *seed_dev : seed;
+}
+
 __global__ __launch_bounds__(256) void mha_fwd_kernel(const float* __restrict__ qk, const float* __restrict__ v,
                                                       const uint8_t* __restrict__ kpm, int Q, int M, int D, float scaling,
-                                                      float p_drop, uint32_t thresh, uint64_t seed,
+                                                      float p_drop, uint32_t thresh, uint64_t seed0,
+                                                      const uint64_t* __restrict__ seed_dev, int qchunks,
                                                       float* __restrict__ out, float* __restrict__ lse) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int E = M * D;
-    const int nm = xcd_remap(blockIdx.x, gridDim.x);
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);  // the chunks of one (video, head) share an XCD
+    const int nm = lb / qchunks;
+    const int q0 = (lb - nm * qchunks) * kQB, q1 = min(Q, q0 + kQB);
     const int n = nm / M, m = nm - n * M;
+    const uint64_t seed = load_seed(seed0, seed_dev);
     float* Ks = smem;                      // [Q][D+1]
     float* Vs = Ks + Q * (D + 1);          // [Q][D]
     float* Ps = Vs + Q * D;                // [4][Q]
@@ -66,7 +79,7 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(const float* __restrict__ 
     const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     float* prow = Ps + w * Q;
     float* qrow = Qrow + w * kHD;
-    for (int q = w; q < Q; q += 4) {
+    for (int q = q0 + w; q < q1; q += 4) {
         if (lane < D) qrow[lane] = qk[((size_t)n * Q + q) * 2 * E + m * D + lane] * scaling;
         __builtin_amdgcn_wave_barrier();
         float s[kKPL];
@@ -114,23 +127,27 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(const float* __restrict__ 
     }
 }
 
-__global__ __launch_bounds__(256) void mha_bwd_kernel(const float* __restrict__ qk, const float* __restrict__ v,
-                                                      const uint8_t* __restrict__ kpm, const float* __restrict__ out,
-                                                      const float* __restrict__ gout, const float* __restrict__ lse,
-                                                      int Q, int M, int D, float scaling, float p_drop, uint32_t thresh,
-                                                      uint64_t seed, float* __restrict__ ws_p,
-                                                      float* __restrict__ ws_ds, float* __restrict__ dqk,
-                                                      float* __restrict__ dv) {
+// backward phase A: one workgroup per (video, head, chunk of kQB queries)
+__global__ __launch_bounds__(256) void mha_bwd_q_kernel(const float* __restrict__ qk, const float* __restrict__ v,
+                                                        const uint8_t* __restrict__ kpm, const float* __restrict__ out,
+                                                        const float* __restrict__ gout, const float* __restrict__ lse,
+                                                        int Q, int M, int D, float scaling, float p_drop, uint32_t thresh,
+                                                        uint64_t seed0, const uint64_t* __restrict__ seed_dev,
+                                                        int qchunks, float* __restrict__ ws_p,
+                                                        float* __restrict__ ws_ds, float* __restrict__ dqk) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int E = M * D;
-    const int nm = xcd_remap(blockIdx.x, gridDim.x);
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int nm = lb / qchunks;
+    const int q0 = (lb - nm * qchunks) * kQB, q1 = min(Q, q0 + kQB);
     const int n = nm / M, m = nm - n * M;
+    const uint64_t seed = load_seed(seed0, seed_dev);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    float* A = smem;                   // phase A: K [Q][D+1]; phase B: dO [Q][D]
-    float* B = A + Q * (D + 1);        // phase A: V [Q][D+1]; phase B: q_scaled [Q][D]
+    float* A = smem;                   // K [Q][D+1]
+    float* B = A + Q * (D + 1);        // V [Q][D+1]
     float* R = B + Q * (D + 1);        // [4][Q] per-wave row buffer (dS row)
-    float* Rv = R + 4 * Q;             // [4][64] per-wave q / dO rows
-    float* Ro = Rv + 4 * kHD;          // [4][64]
+    float* Rv = R + 4 * Q;             // [4][64] per-wave q rows
+    float* Ro = Rv + 4 * kHD;          // [4][64] per-wave dO rows
     for (int i = tid; i < Q * D; i += 256) {
         const int r = i / D, c = i - r * D;
         A[r * (D + 1) + c] = qk[((size_t)n * Q + r) * 2 * E + E + m * D + c];
@@ -143,8 +160,7 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const float* __restrict__ 
     float* dorow = Ro + w * kHD;
     float* wsp = ws_p + (size_t)nm * Q * Q;
     float* wsd = ws_ds + (size_t)nm * Q * Q;
-    // ---- phase A: query rows ----
-    for (int q = w; q < Q; q += 4) {
+    for (int q = q0 + w; q < q1; q += 4) {
         const size_t orow = ((size_t)n * Q + q) * E + m * D;
         const float go = lane < D ? gout[orow + lane] : 0.f;
         if (lane < D) {
@@ -185,26 +201,75 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const float* __restrict__ 
         }
         __builtin_amdgcn_wave_barrier();
     }
-    __syncthreads();
-    // ---- phase B: key rows ----
-    for (int i = tid; i < Q * D; i += 256) {
-        const int r = i / D, c = i - r * D;
-        A[r * D + c] = gout[((size_t)n * Q + r) * E + m * D + c];
-        B[r * D + c] = qk[((size_t)n * Q + r) * 2 * E + m * D + c] * scaling;
+}
+
+// backward phase B: one workgroup per (video, head, chunk of kQB keys); dK = dS^T q_scaled, dV = P_d^T dO.
+// The chunk's P_d / dS columns stay in LDS; dO and q_scaled stream through in 64-query slabs, each wave
+// accumulating its kQB/4 keys with lanes over channels.
+constexpr int kQS = 64;  // query slab
+__global__ __launch_bounds__(256) void mha_bwd_k_kernel(const float* __restrict__ qk, const float* __restrict__ gout,
+                                                        int Q, int M, int D, float scaling, int kchunks,
+                                                        const float* __restrict__ ws_p, const float* __restrict__ ws_ds,
+                                                        float* __restrict__ dqk, float* __restrict__ dv) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int KPW = kQB / 4;  // keys per wave
+    const int E = M * D;
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int nm = lb / kchunks;
+    const int k0 = (lb - nm * kchunks) * kQB, k1 = min(Q, k0 + kQB);
+    const int n = nm / M, m = nm - n * M;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    float* Pc = smem;             // P_d columns of the chunk [kQB][Q]
+    float* Dc = Pc + kQB * Q;     // dS columns [kQB][Q]
+    float* A = Dc + kQB * Q;      // dO slab [kQS][D]
+    float* B = A + kQS * D;       // q_scaled slab [kQS][D]
+    const float* wsp = ws_p + (size_t)nm * Q * Q;
+    const float* wsd = ws_ds + (size_t)nm * Q * Q;
+    const int nk = k1 - k0;
+    for (int i = tid; i < Q * nk; i += 256) {  // coalesced along keys within each query row
+        const int q = i / nk, kk = i - q * nk;
+        Pc[kk * Q + q] = wsp[(size_t)q * Q + k0 + kk];
+        Dc[kk * Q + q] = wsd[(size_t)q * Q + k0 + kk];
     }
-    __syncthreads();
-    if (lane >= D) return;
-    for (int k = w; k < Q; k += 4) {
-        float gk = 0.f, gv = 0.f;
-#pragma unroll 8
-        for (int q = 0; q < Q; ++q) {
-            const float pd = wsp[(size_t)q * Q + k];
-            const float ds = wsd[(size_t)q * Q + k];
-            gv += pd * A[q * D + lane];
-            gk += ds * B[q * D + lane];
+    float gk[KPW], gv[KPW];
+#pragma unroll
+    for (int j = 0; j < KPW; ++j) gk[j] = gv[j] = 0.f;
+    for (int qs = 0; qs < Q; qs += kQS) {
+        const int nq = min(kQS, Q - qs);
+        __syncthreads();
+        for (int i = tid; i < nq * D; i += 256) {
+            const int r = i / D, c = i - r * D;
+            A[r * D + c] = gout[((size_t)n * Q + qs + r) * E + m * D + c];
+            B[r * D + c] = qk[((size_t)n * Q + qs + r) * 2 * E + m * D + c] * scaling;
         }
-        dqk[((size_t)n * Q + k) * 2 * E + E + m * D + lane] = gk;
-        dv[((size_t)n * Q + k) * E + m * D + lane] = gv;
+        __syncthreads();
+        if (lane < D) {
+#pragma unroll
+            for (int j = 0; j < KPW; ++j) {
+                const int kk = w * KPW + j;
+                if (k0 + kk < k1) {
+                    const float* pc = Pc + kk * Q + qs;
+                    const float* dc = Dc + kk * Q + qs;
+                    float a = 0.f, bsum = 0.f;
+#pragma unroll 8
+                    for (int q = 0; q < nq; ++q) {
+                        a += pc[q] * A[q * D + lane];
+                        bsum += dc[q] * B[q * D + lane];
+                    }
+                    gv[j] += a;
+                    gk[j] += bsum;
+                }
+            }
+        }
+    }
+    if (lane >= D) return;
+#pragma unroll
+    for (int j = 0; j < KPW; ++j) {
+        const int k = k0 + w * KPW + j;
+        if (k < k1) {
+            dqk[((size_t)n * Q + k) * 2 * E + E + m * D + lane] = gk[j];
+            dv[((size_t)n * Q + k) * E + m * D + lane] = gv[j];
+        }
     }
 }
 
@@ -220,28 +285,40 @@ static uint32_t drop_threshold(float p) {
 using namespace pdvc;
 
 static size_t fwd_lds(int Q, int D) { return sizeof(float) * ((size_t)Q * (D + 1) + (size_t)Q * D + 4 * Q + 4 * kHD); }
-static size_t bwd_lds(int Q, int D) { return sizeof(float) * (2 * (size_t)Q * (D + 1) + 4 * Q + 8 * kHD); }
+static size_t bwdq_lds(int Q, int D) { return sizeof(float) * (2 * (size_t)Q * (D + 1) + 4 * Q + 8 * kHD); }
+static size_t bwdk_lds(int Q, int D) { return sizeof(float) * (2 * (size_t)kQB * Q + 2 * (size_t)kQS * D); }
+
+static int mha_attrs() {
+    static bool attr = false;
+    if (!attr) {
+        const void* ks[3] = {(const void*)mha_fwd_kernel, (const void*)mha_bwd_q_kernel, (const void*)mha_bwd_k_kernel};
+        for (const void* k : ks)
+            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) {
+                (void)hipGetLastError();
+                return pdvc_set_error(PDVC_ERR_LAUNCH, "mha: cannot raise the LDS limit");
+            }
+        attr = true;
+    }
+    return PDVC_OK;
+}
 
 extern "C" int pdvc_mha_forward_f32(const float* qk, const float* v, const uint8_t* key_padding_mask, int batch,
                                     int num_query, int num_heads, int head_dim, float dropout_p, uint64_t seed,
-                                    float* out, float* lse, void* stream) {
+                                    const uint64_t* seed_dev, float* out, float* lse, void* stream) {
     PDVC_CHECK_ARG(head_dim > 0 && head_dim <= kHD, "query self-attention kernel needs head_dim <= %d, got %d", kHD,
                    head_dim);
     PDVC_CHECK_ARG(num_query > 0 && num_query <= kMaxQ, "num_query must be in [1,%d], got %d", kMaxQ, num_query);
     PDVC_CHECK_ARG(batch >= 0 && num_heads > 0, "invalid sizes");
     PDVC_CHECK_ARG(dropout_p >= 0.f && dropout_p < 1.f, "dropout_p must be in [0,1)");
-    const long blocks = (long)batch * num_heads;
+    const int qchunks = (num_query + kQB - 1) / kQB;
+    const long blocks = (long)batch * num_heads * qchunks;
     if (blocks == 0) return PDVC_OK;
+    int rc = mha_attrs();
+    if (rc) return rc;
     const float scaling = sqrtf(1.0f / (float)head_dim);
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)mha_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void*)mha_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
     hipLaunchKernelGGL(mha_fwd_kernel, dim3((unsigned)blocks), dim3(256), fwd_lds(num_query, head_dim),
-                       (hipStream_t)stream, qk, v, key_padding_mask, num_query, num_heads, head_dim, scaling, dropout_p, drop_threshold(dropout_p), seed,
-                       out, lse);
+                       (hipStream_t)stream, qk, v, key_padding_mask, num_query, num_heads, head_dim, scaling, dropout_p,
+                       drop_threshold(dropout_p), seed, seed_dev, qchunks, out, lse);
     PDVC_CHECK_LAUNCH("mha_fwd_kernel");
     return PDVC_OK;
 }
@@ -249,25 +326,27 @@ extern "C" int pdvc_mha_forward_f32(const float* qk, const float* v, const uint8
 extern "C" int pdvc_mha_backward_f32(const float* qk, const float* v, const uint8_t* key_padding_mask,
                                      const float* out, const float* grad_out, const float* lse, int batch,
                                      int num_query, int num_heads, int head_dim, float dropout_p, uint64_t seed,
-                                     float* workspace, float* grad_qk, float* grad_v, void* stream) {
+                                     const uint64_t* seed_dev, float* workspace, float* grad_qk, float* grad_v,
+                                     void* stream) {
     PDVC_CHECK_ARG(head_dim > 0 && head_dim <= kHD, "query self-attention kernel needs head_dim <= %d, got %d", kHD,
                    head_dim);
     PDVC_CHECK_ARG(num_query > 0 && num_query <= kMaxQ, "num_query must be in [1,%d], got %d", kMaxQ, num_query);
     PDVC_CHECK_ARG(workspace != nullptr, "workspace (2*N*M*Q*Q floats) is required");
-    const long blocks = (long)batch * num_heads;
-    if (blocks == 0) return PDVC_OK;
+    const int chunks = (num_query + kQB - 1) / kQB;
+    const long nm = (long)batch * num_heads;
+    if (nm == 0) return PDVC_OK;
+    int rc = mha_attrs();
+    if (rc) return rc;
     const float scaling = sqrtf(1.0f / (float)head_dim);
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)mha_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
     float* ws_p = workspace;
-    float* ws_ds = workspace + (size_t)blocks * num_query * num_query;
-    hipLaunchKernelGGL(mha_bwd_kernel, dim3((unsigned)blocks), dim3(256), bwd_lds(num_query, head_dim),
-                       (hipStream_t)stream, qk, v, key_padding_mask, out, grad_out, lse, num_query, num_heads,
-                       head_dim, scaling, dropout_p,
-                       drop_threshold(dropout_p), seed, ws_p, ws_ds, grad_qk, grad_v);
-    PDVC_CHECK_LAUNCH("mha_bwd_kernel");
+    float* ws_ds = workspace + (size_t)nm * num_query * num_query;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(mha_bwd_q_kernel, dim3((unsigned)(nm * chunks)), dim3(256), bwdq_lds(num_query, head_dim), s,
+                       qk, v, key_padding_mask, out, grad_out, lse, num_query, num_heads, head_dim, scaling, dropout_p,
+                       drop_threshold(dropout_p), seed, seed_dev, chunks, ws_p, ws_ds, grad_qk);
+    PDVC_CHECK_LAUNCH("mha_bwd_q_kernel");
+    hipLaunchKernelGGL(mha_bwd_k_kernel, dim3((unsigned)(nm * chunks)), dim3(256), bwdk_lds(num_query, head_dim), s,
+                       qk, grad_out, num_query, num_heads, head_dim, scaling, chunks, ws_p, ws_ds, grad_qk, grad_v);
+    PDVC_CHECK_LAUNCH("mha_bwd_k_kernel");
     return PDVC_OK;
 }

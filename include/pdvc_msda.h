@@ -154,13 +154,14 @@ int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* value_pad_ma
  * counter-hash mask of (seed, video, head, query, key), regenerated by the backward.  head_dim <= 64,
  * Q <= 300. */
 int pdvc_mha_forward_f32(const float* qk, const float* v, const uint8_t* key_padding_mask, int batch, int num_query,
-                         int num_heads, int head_dim, float dropout_p, uint64_t seed, float* out, float* lse,
-                         void* stream);
-/* workspace: 2*N*M*Q*Q floats.  grad_qk (N,Q,2E) and grad_v (N,Q,E) are fully written. */
+                         int num_heads, int head_dim, float dropout_p, uint64_t seed, const uint64_t* seed_dev,
+                         float* out, float* lse, void* stream);
+/* workspace: 2*N*M*Q*Q floats (P_d and dS); grad_qk (N,Q,2E) and grad_v (N,Q,E) fully written.  seed_dev
+ * (device, may be NULL) overrides seed -- pass the forward's. */
 int pdvc_mha_backward_f32(const float* qk, const float* v, const uint8_t* key_padding_mask, const float* out,
                           const float* grad_out, const float* lse, int batch, int num_query, int num_heads,
-                          int head_dim, float dropout_p, uint64_t seed, float* workspace, float* grad_qk,
-                          float* grad_v, void* stream);
+                          int head_dim, float dropout_p, uint64_t seed, const uint64_t* seed_dev, float* workspace,
+                          float* grad_qk, float* grad_v, void* stream);
 
 /* ---- caption decoder step pieces (ShowAttendTellCore) ------------------------------------------------
  * softattn: att (R,M,16,A) = ctx2att(samples); att_h (R, ld_att_h) = h2att(h) (A values per row);
