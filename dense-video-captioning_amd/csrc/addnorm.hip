@@ -1,0 +1,300 @@
+// addnorm.hip -- y = LayerNorm(x + dropout(s)) fused, forward and backward, for MI355X (gfx950).
+//
+// The residual epilogue of every transformer sub-layer in PDVC: `norm(src + dropout(src2))`
+// (pdvc/deformable_transformer.py:150-156 encoder, :253-271 decoder -- reference lines cited in DESIGN.md).
+// Eager PyTorch runs it as dropout (mask + scale), add and LayerNorm forward, then LayerNorm input-grad,
+// LayerNorm weight-grad and dropout backward: six passes over a (rows, d) tensor that is 63 MB at the encoder
+// shape.  Here: one forward pass (reads x, s; writes y and 8 bytes of statistics per row) and one backward
+// pass (reads x, s, dy; writes dx, ds), the dropout mask regenerated from a counter hash of
+// (seed, row, column) instead of stored.  One wave per row (d <= 512: <= 8 columns per lane, float4 loads);
+// workgroups walk rows with a grid stride so each lane keeps its columns' gamma/beta-gradient partials in
+// registers, summed over the workgroup in LDS and over workgroups by a second small kernel.
+#include "pdvc_common.h"
+
+namespace pdvc {
+
+constexpr int kAND = 512;              // max row width
+constexpr int kAPL = kAND / 64;        // columns per lane (max)
+constexpr int kANW = 4;                // waves per workgroup
+
+__device__ __forceinline__ uint32_t an_mix(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+
+// keep with probability 1 - p: 24-bit uniform from (seed, row, col)
+__device__ __forceinline__ bool an_keep(uint64_t seed, uint32_t row, uint32_t col, uint32_t thresh) {
+    const uint32_t h = an_mix(an_mix(row * 0x9e3779b9U ^ (uint32_t)seed) + col * 0x85ebca6bU + (uint32_t)(seed >> 32));
+    return (h >> 8) >= thresh;
+}
+
+__device__ __forceinline__ float an_wave_sum(float v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, PDVC_WAVE);
+    return v;
+}
+
+// lane's columns: c = lane*4 + 256*k + {0..3}  (float4 chunks, k < kAPL/4)
+template <int CH>  // float4 chunks per lane
+__global__ __launch_bounds__(kANW * 64) void addnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ s,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, int rows, int d,
+                                                                float p, uint32_t thresh, uint64_t seed0,
+                                                                const uint64_t* __restrict__ seed_dev, float eps,
+                                                                float* __restrict__ y, float* __restrict__ mean_out,
+                                                                float* __restrict__ rstd_out) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t seed = seed_dev ? *seed_dev : seed0;
+    const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+    const float inv_d = 1.f / (float)d;
+    for (int row = blockIdx.x * kANW + (threadIdx.x >> 6); row < rows; row += gridDim.x * kANW) {
+        float z[CH][4];
+        float sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int c = lane * 4 + 256 * k;
+            if (c < d) {
+                const float4 xv = *reinterpret_cast<const float4*>(x + (size_t)row * d + c);
+                const float4 sv = *reinterpret_cast<const float4*>(s + (size_t)row * d + c);
+                const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, ss[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float sd = ss[e];
+                    if (p > 0.f) sd = an_keep(seed, (uint32_t)row, (uint32_t)(c + e), thresh) ? sd * scale : 0.f;
+                    z[k][e] = xs[e] + sd;
+                    sum += z[k][e];
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) z[k][e] = 0.f;
+            }
+        }
+        const float mean = an_wave_sum(sum) * inv_d;
+        float sq = 0.f;
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int c = lane * 4 + 256 * k;
+            if (c < d) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float t = z[k][e] - mean;
+                    sq += t * t;
+                }
+            }
+        }
+        const float rstd = rsqrtf(an_wave_sum(sq) * inv_d + eps);
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int c = lane * 4 + 256 * k;
+            if (c < d) {
+                const float4 g = *reinterpret_cast<const float4*>(gamma + c);
+                const float4 b = *reinterpret_cast<const float4*>(beta + c);
+                float4 o;
+                o.x = (z[k][0] - mean) * rstd * g.x + b.x;
+                o.y = (z[k][1] - mean) * rstd * g.y + b.y;
+                o.z = (z[k][2] - mean) * rstd * g.z + b.z;
+                o.w = (z[k][3] - mean) * rstd * g.w + b.w;
+                *reinterpret_cast<float4*>(y + (size_t)row * d + c) = o;
+            }
+        }
+        if (lane == 0) {
+            mean_out[row] = mean;
+            rstd_out[row] = rstd;
+        }
+    }
+}
+
+template <int CH>
+__global__ __launch_bounds__(kANW * 64) void addnorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ s,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ mean_in,
+                                                                const float* __restrict__ rstd_in,
+                                                                const float* __restrict__ dy, int rows, int d, float p,
+                                                                uint32_t thresh, uint64_t seed0,
+                                                                const uint64_t* __restrict__ seed_dev,
+                                                                float* __restrict__ dx, float* __restrict__ ds,
+                                                                float* __restrict__ dgamma_part,
+                                                                float* __restrict__ dbeta_part) {
+    __shared__ float red[2][kANW][kAND];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t seed = seed_dev ? *seed_dev : seed0;
+    const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+    const float inv_d = 1.f / (float)d;
+    float pg[CH][4], pb[CH][4];
+#pragma unroll
+    for (int k = 0; k < CH; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pg[k][e] = pb[k][e] = 0.f;
+    for (int row = blockIdx.x * kANW + wid; row < rows; row += gridDim.x * kANW) {
+        const float mean = mean_in[row], rstd = rstd_in[row];
+        float xh[CH][4], gg[CH][4];
+        unsigned keep_bits[CH];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int c = lane * 4 + 256 * k;
+            keep_bits[k] = 0xF;
+            if (c < d) {
+                const float4 xv = *reinterpret_cast<const float4*>(x + (size_t)row * d + c);
+                const float4 sv = *reinterpret_cast<const float4*>(s + (size_t)row * d + c);
+                const float4 dv = *reinterpret_cast<const float4*>(dy + (size_t)row * d + c);
+                const float4 gv = *reinterpret_cast<const float4*>(gamma + c);
+                const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, ss[4] = {sv.x, sv.y, sv.z, sv.w};
+                const float dd[4] = {dv.x, dv.y, dv.z, dv.w}, gm[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float sd = ss[e];
+                    if (p > 0.f) {
+                        const bool kp = an_keep(seed, (uint32_t)row, (uint32_t)(c + e), thresh);
+                        if (!kp) keep_bits[k] &= ~(1u << e);
+                        sd = kp ? sd * scale : 0.f;
+                    }
+                    xh[k][e] = (xs[e] + sd - mean) * rstd;
+                    gg[k][e] = dd[e] * gm[e];
+                    s1 += gg[k][e];
+                    s2 += gg[k][e] * xh[k][e];
+                    pg[k][e] += dd[e] * xh[k][e];
+                    pb[k][e] += dd[e];
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) xh[k][e] = gg[k][e] = 0.f;
+            }
+        }
+        const float m1 = an_wave_sum(s1) * inv_d, m2 = an_wave_sum(s2) * inv_d;
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int c = lane * 4 + 256 * k;
+            if (c < d) {
+                float o[4], q[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    o[e] = rstd * (gg[k][e] - m1 - xh[k][e] * m2);
+                    q[e] = ((keep_bits[k] >> e) & 1u) ? o[e] * scale : 0.f;
+                }
+                *reinterpret_cast<float4*>(dx + (size_t)row * d + c) = make_float4(o[0], o[1], o[2], o[3]);
+                *reinterpret_cast<float4*>(ds + (size_t)row * d + c) = make_float4(q[0], q[1], q[2], q[3]);
+            }
+        }
+    }
+    // workgroup sum of the column partials, one row of partials per workgroup
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        const int c = lane * 4 + 256 * k;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (c + e < kAND) {
+                red[0][wid][c + e] = pg[k][e];
+                red[1][wid][c + e] = pb[k][e];
+            }
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < d; c += blockDim.x) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int w = 0; w < kANW; ++w) {
+            a += red[0][w][c];
+            b += red[1][w][c];
+        }
+        dgamma_part[(size_t)blockIdx.x * d + c] = a;
+        dbeta_part[(size_t)blockIdx.x * d + c] = b;
+    }
+}
+
+// column sums of the (parts, d) partials -> dgamma, dbeta: a workgroup per 64 columns, its 4 waves take
+// every 4th partial row, summed in LDS in a fixed order (bitwise reproducible)
+__global__ __launch_bounds__(256) void addnorm_colsum_kernel(const float* __restrict__ gpart,
+                                                             const float* __restrict__ bpart, int parts, int d,
+                                                             float* __restrict__ dgamma, float* __restrict__ dbeta) {
+    __shared__ float red[2][4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane;
+    float a = 0.f, b = 0.f;
+    if (c < d) {
+#pragma unroll 8
+        for (int i = w; i < parts; i += 4) {
+            a += gpart[(size_t)i * d + c];
+            b += bpart[(size_t)i * d + c];
+        }
+    }
+    red[0][w][lane] = a;
+    red[1][w][lane] = b;
+    __syncthreads();
+    if (w == 0 && c < d) {
+        dgamma[c] = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
+        dbeta[c] = red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
+    }
+}
+
+static uint32_t an_threshold(float p) {
+    double t = (double)p * 16777216.0;
+    if (t < 0) t = 0;
+    if (t > 16777216.0) t = 16777216.0;
+    return (uint32_t)t;
+}
+
+static int an_grid(int rows, int cap) {
+    const int want = (rows + kANW - 1) / kANW;
+    return want < cap ? (want > 0 ? want : 1) : cap;
+}
+constexpr int kAnFwdBlocks = 1024;  // 4 per CU
+constexpr int kAnBwdBlocks = 256;   // 1 per CU: fewer gamma/beta partial rows
+
+}  // namespace pdvc
+
+using namespace pdvc;
+
+#define AN_CHECK()                                                                                            \
+    PDVC_CHECK_ARG(rows >= 0 && d > 0 && d <= kAND && d % 4 == 0, "add-norm needs 0 < d <= %d, d %% 4 == 0", \
+                   kAND);                                                                                      \
+    PDVC_CHECK_ARG(p >= 0.f && p < 1.f, "dropout p must be in [0, 1)")
+
+extern "C" int pdvc_add_dropout_layernorm_forward_f32(const float* x, const float* s, const float* gamma,
+                                                      const float* beta, int rows, int d, float p, uint64_t seed,
+                                                      const uint64_t* seed_dev, float eps, float* y, float* mean,
+                                                      float* rstd, void* stream) {
+    AN_CHECK();
+    if (rows == 0) return PDVC_OK;
+    const dim3 grid((unsigned)an_grid(rows, kAnFwdBlocks)), block(kANW * 64);
+    hipStream_t st = (hipStream_t)stream;
+    if (d <= 256)
+        hipLaunchKernelGGL(addnorm_fwd_kernel<1>, grid, block, 0, st, x, s, gamma, beta, rows, d, p, an_threshold(p),
+                           seed, seed_dev, eps, y, mean, rstd);
+    else
+        hipLaunchKernelGGL(addnorm_fwd_kernel<2>, grid, block, 0, st, x, s, gamma, beta, rows, d, p, an_threshold(p),
+                           seed, seed_dev, eps, y, mean, rstd);
+    PDVC_CHECK_LAUNCH("addnorm_fwd_kernel");
+    return PDVC_OK;
+}
+
+extern "C" int pdvc_add_dropout_layernorm_backward_f32(const float* x, const float* s, const float* gamma,
+                                                       const float* mean, const float* rstd, const float* dy, int rows,
+                                                       int d, float p, uint64_t seed, const uint64_t* seed_dev,
+                                                       float* dx, float* ds, float* dgamma, float* dbeta,
+                                                       float* workspace, void* stream) {
+    AN_CHECK();
+    PDVC_CHECK_ARG(workspace != nullptr, "workspace (2 * 256 * d floats) is required");
+    hipStream_t st = (hipStream_t)stream;
+    if (rows == 0) {
+        hipError_t e1 = hipMemsetAsync(dgamma, 0, sizeof(float) * d, st);
+        hipError_t e2 = hipMemsetAsync(dbeta, 0, sizeof(float) * d, st);
+        if (e1 != hipSuccess || e2 != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset failed");
+        return PDVC_OK;
+    }
+    const int parts = an_grid(rows, kAnBwdBlocks);
+    float* gpart = workspace;
+    float* bpart = workspace + (size_t)parts * d;
+    const dim3 grid((unsigned)parts), block(kANW * 64);
+    if (d <= 256)
+        hipLaunchKernelGGL(addnorm_bwd_kernel<1>, grid, block, 0, st, x, s, gamma, mean, rstd, dy, rows, d, p,
+                           an_threshold(p), seed, seed_dev, dx, ds, gpart, bpart);
+    else
+        hipLaunchKernelGGL(addnorm_bwd_kernel<2>, grid, block, 0, st, x, s, gamma, mean, rstd, dy, rows, d, p,
+                           an_threshold(p), seed, seed_dev, dx, ds, gpart, bpart);
+    PDVC_CHECK_LAUNCH("addnorm_bwd_kernel");
+    hipLaunchKernelGGL(addnorm_colsum_kernel, dim3((unsigned)((d + 63) / 64)), dim3(256), 0, st, gpart, bpart, parts,
+                       d, dgamma, dbeta);
+    PDVC_CHECK_LAUNCH("addnorm_colsum_kernel");
+    return PDVC_OK;
+}

@@ -16,6 +16,7 @@ from torch import nn
 from torch.nn.init import constant_, normal_, xavier_uniform_
 
 from . import hostio
+from .ops.functions import add_dropout_layernorm
 
 from .box_ops import inverse_sigmoid
 from .ops.modules import MSDeformAttn
@@ -136,12 +137,12 @@ class DeformableTransformerEncoderLayer(nn.Module):
 
     def forward_ffn(self, src):
         src2 = self.linear2(self.dropout2(self.activation(self.linear1(src))))
-        return self.norm2(src + self.dropout3(src2))
+        return add_dropout_layernorm(src, src2, self.norm2, self.dropout3.p, self.training)
 
     def forward(self, src, pos, reference_points, temporal_shapes, level_start_index, padding_mask=None):
         src2 = self.self_attn(self.with_pos_embed(src, pos), reference_points, src, temporal_shapes,
                               level_start_index, padding_mask)
-        src = self.norm1(src + self.dropout1(src2))
+        src = add_dropout_layernorm(src, src2, self.norm1, self.dropout1.p, self.training)
         return self.forward_ffn(src)
 
 
@@ -223,17 +224,17 @@ class DeformableTransformerDecoderLayer(nn.Module):
 
     def forward_ffn(self, tgt):
         tgt2 = self.linear2(self.dropout3(self.activation(self.linear1(tgt))))
-        return self.norm3(tgt + self.dropout4(tgt2))
+        return add_dropout_layernorm(tgt, tgt2, self.norm3, self.dropout4.p, self.training)
 
     def forward(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,
                 src_padding_mask=None, query_mask=None):
         q = self.with_pos_embed(tgt, query_pos)
         kpm = None if query_mask is None else ~query_mask
         tgt2 = self.self_attn(q, tgt, key_padding_mask=kpm)
-        tgt = self.norm2(tgt + self.dropout2(tgt2))
+        tgt = add_dropout_layernorm(tgt, tgt2, self.norm2, self.dropout2.p, self.training)
         tgt2 = self.cross_attn(self.with_pos_embed(tgt, query_pos), reference_points, src, src_temporal_shapes,
                                level_start_index, src_padding_mask)
-        tgt = self.norm1(tgt + self.dropout1(tgt2))
+        tgt = add_dropout_layernorm(tgt, tgt2, self.norm1, self.dropout1.p, self.training)
         return self.forward_ffn(tgt)
 
 

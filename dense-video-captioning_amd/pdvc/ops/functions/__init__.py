@@ -2,3 +2,4 @@ from .ms_deform_attn_func import (MSDeformAttnFunction, ms_deform_attn_core_pyto
                                   CapGatherFunction)
 from .caption_decode import CaptionDecodeFunction
 from .linear import LinearFunction, linear, matmul
+from .addnorm import AddDropoutLayerNormFunction, add_dropout_layernorm

@@ -31,6 +31,8 @@
  *                                      ShowAttendTellCore.forward (pdvc/CaptioningHead/LSTM_DSA.py:206-207,261)
  *   pdvc_softattn_*                 <- ShowAttendTellCore's soft attention over the 16 samples
  *                                      (LSTM_DSA.py:245-258: tanh, alpha_net, softmax, weighted sum)
+ *   pdvc_add_dropout_layernorm_*    <- the residual epilogue norm(x + dropout(s)) of every transformer sub-layer
+ *                                      (deformable_transformer.py:150-156, 253-271)
  *   pdvc_gemm_f32                   <- the dense projections (nn.Linear forward/backward) of the layers
  *                                      above: MSDeformAttn value/offset/output projections
  *                                      (ms_deform_attn.py:79-126), the FFNs (deformable_transformer.py:150-156,
@@ -188,6 +190,19 @@ int pdvc_lstm_cell_backward_f32(const float* grad_h, int ld_grad_h, const float*
                                 const float* grad_c_next, const float* acts, const float* c_prev, const float* c,
                                 int rows, int hidden, float* grad_gates, int ld_grad_gates, float* grad_c_prev,
                                 void* stream);
+
+/* ---- fused residual epilogue: y = LayerNorm(x + dropout(s)) -----------------------------------------
+ * x, s, y (rows, d) contiguous, d % 4 == 0, d <= 512; gamma, beta (d); mean, rstd (rows) saved for the backward.
+ * Dropout keeps each element with probability 1-p from a counter hash of (seed, row, column), scaled by
+ * 1/(1-p); seed_dev (device, may be NULL) overrides seed.  The backward regenerates the mask:
+ * dx = dL/dx, ds = dL/ds, dgamma/dbeta fully written; workspace 2*256*d floats. */
+int pdvc_add_dropout_layernorm_forward_f32(const float* x, const float* s, const float* gamma, const float* beta,
+                                           int rows, int d, float p, uint64_t seed, const uint64_t* seed_dev,
+                                           float eps, float* y, float* mean, float* rstd, void* stream);
+int pdvc_add_dropout_layernorm_backward_f32(const float* x, const float* s, const float* gamma, const float* mean,
+                                            const float* rstd, const float* dy, int rows, int d, float p,
+                                            uint64_t seed, const uint64_t* seed_dev, float* dx, float* ds,
+                                            float* dgamma, float* dbeta, float* workspace, void* stream);
 
 /* ---- fp32 GEMM on the matrix cores ----------------------------------------------------------------
  * C[M,N] = op(A)[M,K] op(B)[K,N] (+ bias[N]) (ReLU).  op(A): trans_a 0 -> A[m*lda + k], 1 -> A[k*lda + m];
