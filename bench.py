@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     p.add_argument("--kernel-report", action="store_true", help="print per-kernel event timings to stderr")
+    p.add_argument("--gemm", choices=["hip", "torch"], default=None,
+                   help="projection GEMMs on pdvc_gemm_f32 (hip) or torch/hipBLASLt (default: PDVC_GEMM or hip)")
     return p.parse_args()
 
 
@@ -106,6 +108,9 @@ def main():
     from pdvc.distributed import GradAllReducer, broadcast_parameters, init_distributed
     from pdvc import _native
     from pdvc.data import synthetic_videos, collate, to_device
+    from pdvc.ops.functions import linear as _lin
+    if a.gemm:
+        _lin.BACKEND = a.gemm
     rank, world, local = init_distributed()
     if world != a.gpus and rank == 0:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
@@ -166,7 +171,7 @@ def main():
         "config": {"workload": f"anet_tsp_pdvc training step (fwd+loss+bwd+allreduce+AdamW): T={a.T} C={a.C} "
                                f"L=4 Q={a.Q} 2 enc/2 dec layers, E={a.events} events x {a.words} words, "
                                f"vocab {vocab}, dropout on",
-                   "videos_per_gpu": B, "global_batch": B * world, "seq_len": a.T,
+                   "videos_per_gpu": B, "global_batch": B * world, "seq_len": a.T, "gemm": _lin.BACKEND,
                    "parallelism": f"dp{world}"},
     }
     # roofline: the fused MSDA forward (the gather kernel; algorithmic bytes per launch / avg launch time)

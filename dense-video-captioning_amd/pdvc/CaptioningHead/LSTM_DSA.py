@@ -27,6 +27,7 @@ from torch import nn
 
 from pdvc.ops.functions import CaptionDecodeFunction
 from pdvc.ops.modules import MSDeformAttnCap
+from pdvc.ops.modules.linear import Linear
 
 
 class LSTMWeights(nn.Module):
@@ -66,7 +67,7 @@ class Captioner(nn.Module):
         self.max_caption_len = opt.max_caption_len
         self.ss_prob = 0.0
         self.embed = nn.Embedding(self.vocab_size + 1, self.input_encoding_size)
-        self.logit = nn.Linear(self.rnn_size, self.vocab_size + 1)
+        self.logit = Linear(self.rnn_size, self.vocab_size + 1)
         self.dropout = nn.Dropout(self.drop_prob_lm)
         self.init_weights()
 

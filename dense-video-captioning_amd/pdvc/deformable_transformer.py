@@ -19,7 +19,9 @@ from . import hostio
 from .ops.functions import add_dropout_layernorm
 
 from .box_ops import inverse_sigmoid
+from .ops.functions.linear import dense
 from .ops.modules import MSDeformAttn
+from .ops.modules.linear import Linear
 from .ops.functions.attention import query_self_attention
 
 
@@ -124,10 +126,10 @@ class DeformableTransformerEncoderLayer(nn.Module):
         self.self_attn = MSDeformAttn(d_model, n_levels, n_heads, n_points)
         self.dropout1 = nn.Dropout(dropout)
         self.norm1 = nn.LayerNorm(d_model)
-        self.linear1 = nn.Linear(d_model, d_ffn)
+        self.linear1 = Linear(d_model, d_ffn)
         self.activation = _get_activation_fn(activation)
         self.dropout2 = nn.Dropout(dropout)
-        self.linear2 = nn.Linear(d_ffn, d_model)
+        self.linear2 = Linear(d_ffn, d_model)
         self.dropout3 = nn.Dropout(dropout)
         self.norm2 = nn.LayerNorm(d_model)
 
@@ -136,7 +138,10 @@ class DeformableTransformerEncoderLayer(nn.Module):
         return tensor if pos is None else tensor + pos
 
     def forward_ffn(self, src):
-        src2 = self.linear2(self.dropout2(self.activation(self.linear1(src))))
+        if self.activation is F.relu:
+            src2 = self.linear2(self.dropout2(self.linear1(src, relu=True)))
+        else:
+            src2 = self.linear2(self.dropout2(self.activation(self.linear1(src))))
         return add_dropout_layernorm(src, src2, self.norm2, self.dropout3.p, self.training)
 
     def forward(self, src, pos, reference_points, temporal_shapes, level_start_index, padding_mask=None):
@@ -185,7 +190,7 @@ class QuerySelfAttention(nn.Module):
         self.head_dim = embed_dim // num_heads
         self.in_proj_weight = nn.Parameter(torch.empty(3 * embed_dim, embed_dim))
         self.in_proj_bias = nn.Parameter(torch.empty(3 * embed_dim))
-        self.out_proj = nn.Linear(embed_dim, embed_dim)
+        self.out_proj = Linear(embed_dim, embed_dim)
         xavier_uniform_(self.in_proj_weight)
         constant_(self.in_proj_bias, 0.)
         constant_(self.out_proj.bias, 0.)
@@ -195,8 +200,8 @@ class QuerySelfAttention(nn.Module):
         key_padding_mask (N, Q) True = ignore.  Returns (N, Q, E)."""
         E = self.embed_dim
         w, b = self.in_proj_weight, self.in_proj_bias
-        qk = F.linear(qk_in, w[:2 * E], b[:2 * E])
-        v = F.linear(v_in, w[2 * E:], b[2 * E:])
+        qk = dense(qk_in, w[:2 * E], b[:2 * E])
+        v = dense(v_in, w[2 * E:], b[2 * E:])
         p = self.dropout if self.training else 0.0
         out = query_self_attention(qk, v, key_padding_mask, self.num_heads, p)
         return self.out_proj(out)
@@ -211,10 +216,10 @@ class DeformableTransformerDecoderLayer(nn.Module):
         self.self_attn = QuerySelfAttention(d_model, n_heads, dropout=dropout)
         self.dropout2 = nn.Dropout(dropout)
         self.norm2 = nn.LayerNorm(d_model)
-        self.linear1 = nn.Linear(d_model, d_ffn)
+        self.linear1 = Linear(d_model, d_ffn)
         self.activation = _get_activation_fn(activation)
         self.dropout3 = nn.Dropout(dropout)
-        self.linear2 = nn.Linear(d_ffn, d_model)
+        self.linear2 = Linear(d_ffn, d_model)
         self.dropout4 = nn.Dropout(dropout)
         self.norm3 = nn.LayerNorm(d_model)
 
@@ -223,7 +228,10 @@ class DeformableTransformerDecoderLayer(nn.Module):
         return tensor if pos is None else tensor + pos
 
     def forward_ffn(self, tgt):
-        tgt2 = self.linear2(self.dropout3(self.activation(self.linear1(tgt))))
+        if self.activation is F.relu:
+            tgt2 = self.linear2(self.dropout3(self.linear1(tgt, relu=True)))
+        else:
+            tgt2 = self.linear2(self.dropout3(self.activation(self.linear1(tgt))))
         return add_dropout_layernorm(tgt, tgt2, self.norm3, self.dropout4.p, self.training)
 
     def forward(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,

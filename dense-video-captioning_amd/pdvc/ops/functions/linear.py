@@ -4,12 +4,17 @@
 kernel (a row-major or a transposed view of row-major memory both go without a copy).  LinearFunction is
 nn.Linear's forward/backward (y = x W^T + b; dx = dy W; dW = dy^T x split over the rows with atomics;
 db = sum dy) -- the projections of MSDeformAttn and the FFNs."""
+import os
+
 import torch
+import torch.nn.functional as F
 from torch.autograd import Function
 
 from pdvc import _native as _n
 
 CU = 256  # MI355X compute units
+# "hip": the projections run on pdvc_gemm_f32; "torch": F.linear (hipBLASLt) -- an A/B switch for bench.py
+BACKEND = os.environ.get("PDVC_GEMM", "hip")
 
 
 def _operand(t):
@@ -58,19 +63,23 @@ def matmul(a, b, bias=None, relu=False, out=None, accumulate=False):
 
 
 class LinearFunction(Function):
+    """y = x W^T + b (ReLU fused when relu=True: the backward masks dy with y > 0)."""
+
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, relu=False):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
-        y = matmul(x2, weight.t(), bias=bias)
-        ctx.save_for_backward(x2, weight)
+        y = matmul(x2, weight.t(), bias=bias, relu=relu)
+        ctx.save_for_backward(x2, weight, y if relu else None)
         ctx.has_bias = bias is not None
         return y.view(*shape[:-1], weight.shape[0])
 
     @staticmethod
     def backward(ctx, gy):
-        x2, weight = ctx.saved_tensors
+        x2, weight, y = ctx.saved_tensors
         gy2 = gy.reshape(-1, weight.shape[0])
+        if y is not None:
+            gy2 = gy2 * (y > 0)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             gx = matmul(gy2, weight).view(*gy.shape[:-1], weight.shape[1])
@@ -79,8 +88,16 @@ class LinearFunction(Function):
             matmul(gy2.t(), x2, out=gw, accumulate=True)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = gy2.sum(0)
-        return gx, gw, gb
+        return gx, gw, gb, None
 
 
-def linear(x, weight, bias=None):
-    return LinearFunction.apply(x, weight, bias)
+def linear(x, weight, bias=None, relu=False):
+    return LinearFunction.apply(x, weight, bias, relu)
+
+
+def dense(x, weight, bias=None, relu=False):
+    """nn.Linear (+ ReLU) on the backend selected by BACKEND (fp32 CUDA tensors only go to the HIP GEMM)."""
+    if BACKEND == "hip" and x.is_cuda and x.dtype == torch.float32 and weight.dtype == torch.float32:
+        return LinearFunction.apply(x, weight, bias, relu)
+    y = F.linear(x, weight, bias)
+    return F.relu(y) if relu else y

@@ -13,6 +13,8 @@ from torch import nn
 from torch.nn.init import constant_, xavier_uniform_
 
 from ..functions import MSDeformAttnFunction, MSDA1dFunction, NUM_SAMPLES_FUSED
+from ..functions.linear import dense
+from .linear import Linear
 
 FUSED_HEAD_DIMS = (16, 32, 64, 128)
 
@@ -58,10 +60,10 @@ class MSDeformAttn(nn.Module):
         self.n_levels = n_levels
         self.n_heads = n_heads
         self.n_points = n_points
-        self.sampling_offsets = nn.Linear(d_model, n_heads * n_levels * n_points)
-        self.attention_weights = nn.Linear(d_model, n_heads * n_levels * n_points)
-        self.value_proj = nn.Linear(d_model, d_model)
-        self.output_proj = nn.Linear(d_model, d_model)
+        self.sampling_offsets = Linear(d_model, n_heads * n_levels * n_points)
+        self.attention_weights = Linear(d_model, n_heads * n_levels * n_points)
+        self.value_proj = Linear(d_model, d_model)
+        self.output_proj = Linear(d_model, d_model)
         self._reset_parameters()
 
     def _reset_parameters(self):
@@ -85,7 +87,7 @@ class MSDeformAttn(nn.Module):
         """One GEMM for both query projections: [offsets | attention logits] (N, Lq, 2*M*L*P)."""
         w = torch.cat([self.sampling_offsets.weight, self.attention_weights.weight], 0)
         b = torch.cat([self.sampling_offsets.bias, self.attention_weights.bias], 0)
-        return F.linear(query, w, b)
+        return dense(query, w, b)
 
     def forward(self, query, reference_points, input_flatten, input_spatial_shapes, input_level_start_index,
                 input_padding_mask=None, value=None):

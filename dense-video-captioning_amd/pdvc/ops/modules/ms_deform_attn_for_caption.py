@@ -9,6 +9,7 @@ from torch import nn
 from torch.nn.init import constant_, xavier_uniform_
 
 from ..functions import CapGatherFunction, ms_deform_attn_core_pytorch, NUM_SAMPLES_FUSED
+from .linear import Linear
 from .ms_deform_attn import _is_power_of_2, level_lengths, sampling_offsets_init
 
 import warnings
@@ -26,10 +27,10 @@ class MSDeformAttnCap(nn.Module):
         self.n_levels = n_levels
         self.n_heads = n_heads
         self.n_points = n_points
-        self.sampling_offsets = nn.Linear(2 * d_model, n_heads * n_levels * n_points)
-        self.attention_weights = nn.Linear(2 * d_model, n_heads * n_levels * n_points)
-        self.value_proj = nn.Linear(d_model, d_model)
-        self.output_proj = nn.Linear(d_model, d_model)
+        self.sampling_offsets = Linear(2 * d_model, n_heads * n_levels * n_points)
+        self.attention_weights = Linear(2 * d_model, n_heads * n_levels * n_points)
+        self.value_proj = Linear(d_model, d_model)
+        self.output_proj = Linear(d_model, d_model)
         self._reset_parameters()
 
     def _reset_parameters(self):
