@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     p.add_argument("--kernel-report", action="store_true", help="print per-kernel event timings to stderr")
     p.add_argument("--gemm", choices=["hip", "torch"], default=None,
-                   help="projection GEMMs on pdvc_gemm_f32 (hip) or torch/hipBLASLt (default: PDVC_GEMM or hip)")
+                   help="projection GEMMs on pdvc_gemm_f32 (hip) or torch/hipBLASLt (default: PDVC_GEMM or torch)")
     return p.parse_args()
 
 

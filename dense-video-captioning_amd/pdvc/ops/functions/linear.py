@@ -14,7 +14,7 @@ from pdvc import _native as _n
 
 CU = 256  # MI355X compute units
 # "hip": the projections run on pdvc_gemm_f32; "torch": F.linear (hipBLASLt) -- an A/B switch for bench.py
-BACKEND = os.environ.get("PDVC_GEMM", "hip")
+BACKEND = os.environ.get("PDVC_GEMM", "torch")
 
 
 def _operand(t):
