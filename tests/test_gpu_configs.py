@@ -1,0 +1,48 @@
+"""One PDVC training step (forward, losses, backward) at the shape of every BASELINE.json configuration,
+on the GPU path, with a small batch: finite losses, every used parameter gets a finite gradient and the 8
+parameters the reference never uses get none.  (Parity at these shapes is pinned by the kernel tests and the
+two whole-model golden fixtures; this checks the configurations run end to end: T up to 1024, Q up to 300,
+3+3 layers, C = 500/768/3072.)"""
+import os
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(os.path.dirname(HERE), "dense-video-captioning_amd")
+
+# (cfg, T, C, Q, events, words) -- BASELINE.json "configs"
+CONFIGS = [
+    ("cfgs/yc2_tsn_pdvc.yml", 128, 512, 100, 8, 9),
+    ("cfgs/yc2_tsp_pdvc.yml", 256, 768, 100, 8, 9),
+    ("cfgs/anet_tsp_pdvc.yml", 512, 768, 100, 4, 13),
+    ("cfgs/yc2_newModel_sound.yml", 512, 768, 100, 8, 9),
+    ("cfgs/anet_c3d_pdvc.yml", 1024, 500, 300, 4, 13),
+]
+
+
+@pytest.mark.parametrize("cfg,T,C,Q,E,W", CONFIGS)
+def test_training_step_runs_at_config(cfg, T, C, Q, E, W):
+    import opts
+    from pdvc.data import collate, synthetic_videos, to_device
+    from pdvc.pdvc import build
+    torch.manual_seed(0)
+    args = opts.parse_opts(["--cfg_path", cfg, "--device", "cuda"], cfg_root=PKG, feature_dim=C, num_queries=Q,
+                           frame_embedding_num=T)
+    model, criterion, _ = build(args)
+    model = model.cuda().train()
+    dt = to_device(collate(synthetic_videos(2, T, C, E, W, args.vocab_size + 1, seed=3)), "cuda")
+    out, loss = model(dt, criterion, "queries")
+    wd = criterion.weight_dict
+    total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
+    assert torch.isfinite(total).item(), {k: float(v) for k, v in loss.items()}
+    total.backward()
+    n_none = 0
+    for n, p in model.named_parameters():
+        if p.grad is None:
+            n_none += 1
+            continue
+        assert torch.isfinite(p.grad).all().item(), n
+    assert n_none == 8, n_none
