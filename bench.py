@@ -108,7 +108,8 @@ def main():
     from pdvc.distributed import GradAllReducer, broadcast_parameters, init_distributed
     from pdvc import _native
     from pdvc.data import synthetic_videos, collate, to_device
-    from pdvc.ops.functions import linear as _lin
+    import importlib
+    _lin = importlib.import_module("pdvc.ops.functions.linear")
     if a.gemm:
         _lin.BACKEND = a.gemm
     rank, world, local = init_distributed()

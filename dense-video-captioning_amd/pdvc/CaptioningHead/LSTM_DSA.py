@@ -21,6 +21,7 @@ first all-zero token column, LSTM_DSA.py:103-104): the same steps are computed, 
 """
 import math
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 from torch import nn
@@ -93,11 +94,12 @@ class Captioner(nn.Module):
 def caption_steps(cap_tensor_cpu):
     """Number of decoder steps of the reference's teacher-forced loop for one video's captions:
     i runs over range(K-1) and stops at the first i >= 1 whose token column is all zero."""
-    K = cap_tensor_cpu.shape[1]
-    for i in range(1, K - 1):
-        if int(cap_tensor_cpu[:, i].abs().sum()) == 0:
-            return i
-    return max(K - 1, 0)
+    x = cap_tensor_cpu.numpy() if isinstance(cap_tensor_cpu, torch.Tensor) else np.asarray(cap_tensor_cpu)
+    K = x.shape[1]
+    if K < 3:
+        return max(K - 1, 0)
+    zero = np.flatnonzero(np.abs(x[:, 1:K - 1]).sum(0) == 0)
+    return int(zero[0]) + 1 if zero.size else K - 1
 
 
 class ShowAttendTellCore(nn.Module):

@@ -59,10 +59,14 @@ class SetCriterion(nn.Module):
 
     # -------------------------------------------------------------------------------------------------
     def layer_losses(self, outputs, pt, indices):
-        """Per-video losses of one decoder layer, averaged over the batch, computed for all videos at once.
-        outputs: pred_logits (N,Q,C), pred_boxes (N,Q,2), pred_count (N,K+1); pt: padded targets;
-        indices: list of (query ids, target ids) per video."""
-        logits, boxes, count = outputs["pred_logits"], outputs["pred_boxes"], outputs["pred_count"]
+        """Per-video losses of one decoder layer, averaged over the batch (see video_losses)."""
+        v = self.video_losses(outputs["pred_logits"], outputs["pred_boxes"], outputs["pred_count"], pt, indices)
+        return {k: t.mean() for k, t in v.items()}
+
+    def video_losses(self, logits, boxes, count, pt, indices):
+        """Per-video loss vectors (N,) for a batch of N videos -- or of N = layers x videos when the decoder
+        layers are stacked -- computed for all at once.  logits (N,Q,C), boxes (N,Q,2), count (N,K+1); pt:
+        padded targets; indices: list of (query ids, target ids) per video."""
         N, Q, C = logits.shape
         dev = logits.device
         sizes = pt["sizes"]
@@ -112,25 +116,46 @@ class SetCriterion(nn.Module):
         iou = torch.triu(iou, diagonal=1) * (valid[:, :, None] & valid[:, None, :])
         n = n_dev.to(l1.dtype)
         loss_self_iou = iou.sum((1, 2)) / (0.5 * n * (n - 1))
-        return {"loss_ce": loss_ce.mean(), "loss_counter": loss_counter.mean(), "loss_bbox": loss_bbox.mean(),
-                "loss_giou": loss_giou.mean(), "loss_self_iou": loss_self_iou.mean(),
-                "cardinality_error": card_err.mean()}
+        return {"loss_ce": loss_ce, "loss_counter": loss_counter, "loss_bbox": loss_bbox, "loss_giou": loss_giou,
+                "loss_self_iou": loss_self_iou, "cardinality_error": card_err}
 
     def forward(self, outputs, targets, padded=None):
         """Reference contract: returns (losses, last_indices[, aux_indices]); indices are
         (list of per-video (query ids, target ids), None).  `padded` may carry padded_targets(targets)."""
         pt = padded if padded is not None else padded_targets(targets, outputs["pred_logits"].device)
         layers = [outputs] + list(outputs.get("aux_outputs", []))
-        costs = [self.matcher.cost_padded(o["pred_logits"], o["pred_boxes"], pt) for o in layers]
-        solved = self.matcher.solve_padded(costs, pt["sizes"])
-        idx = [(s, None) for s in solved]
+        Ld = len(layers)
+        N = outputs["pred_logits"].shape[0]
+        # every decoder layer at once: the layers are stacked as Ld*N "videos" against repeated targets --
+        # one cost pass, one device->host copy for all matchings, one pass per loss term
+        ptL = repeat_targets(pt, Ld)
+        logits = torch.cat([o["pred_logits"] for o in layers], 0)
+        boxes = torch.cat([o["pred_boxes"] for o in layers], 0)
+        count = torch.cat([o["pred_count"] for o in layers], 0)
+        costs = self.matcher.cost_padded(logits, boxes, ptL)  # (Ld*N, Q, Emax)
+        solved = self.matcher.solve_padded(list(costs.view(Ld, N, *costs.shape[1:])), pt["sizes"])
+        idx = [(s_, None) for s_ in solved]
         last_indices = idx[0]
         outputs["matched_indices"] = last_indices
-        losses = self.layer_losses(outputs, pt, last_indices[0])
+        per = self.video_losses(logits, boxes, count, ptL, [m for s_ in solved for m in s_])
+        per = {k: v.view(Ld, N).mean(1) for k, v in per.items()}
+        losses = {k: v[0] for k, v in per.items()}
         if "aux_outputs" in outputs:
             aux_indices = idx[1:]
-            for i, aux in enumerate(outputs["aux_outputs"]):
-                l_dict = self.layer_losses(aux, pt, aux_indices[i][0])
-                losses.update({k + f"_{i}": v for k, v in l_dict.items()})
+            for i in range(Ld - 1):
+                losses.update({k + f"_{i}": v[i + 1] for k, v in per.items()})
             return losses, last_indices, aux_indices
         return losses, last_indices
+
+
+def repeat_targets(pt, times):
+    """Padded targets repeated for `times` stacked decoder layers (cached on the dict)."""
+    if times == 1:
+        return pt
+    key = ("repeat", times)
+    if key not in pt:
+        rep = {k: (v.repeat(times, *([1] * (v.dim() - 1))) if isinstance(v, torch.Tensor) else v)
+               for k, v in pt.items() if not isinstance(k, tuple)}
+        rep["sizes"] = list(pt["sizes"]) * times
+        pt[key] = rep
+    return pt[key]

@@ -48,7 +48,7 @@ def test_gemm_split_k_accumulate(M, N, K):
 
 
 def test_linear_function_matches_nn_linear():
-    from pdvc.ops.functions import linear
+    from pdvc.ops.functions.linear import linear
     torch.manual_seed(0)
     lin = torch.nn.Linear(512, 256).to(DEV).double()
     x = torch.randn(4, 960, 512, device=DEV, dtype=torch.float64, requires_grad=True)
