@@ -48,6 +48,23 @@ class MLP(nn.Module):
         return x
 
 
+class _TrunkModule(nn.Module):
+    """PDVC.trunk as a module whose parameters are exactly the trunk's (for make_graphed_callables)."""
+
+    def __init__(self, pdvc):
+        super().__init__()
+        self.base_encoder = pdvc.base_encoder
+        self.transformer = pdvc.transformer
+        self.query_embed = pdvc.query_embed
+        self.class_head = pdvc.class_head
+        self.count_head = pdvc.count_head
+        self.bbox_head = pdvc.bbox_head
+        object.__setattr__(self, "_pdvc", pdvc)
+
+    def forward(self, vf, video_mask, duration):
+        return self._pdvc.trunk(vf, video_mask, duration)
+
+
 class PDVC(nn.Module):
     def __init__(self, base_encoder, transformer, captioner, num_classes, num_queries, num_feature_levels,
                  aux_loss=True, with_box_refine=False, opt=None, translator=None):
@@ -90,10 +107,12 @@ class PDVC(nn.Module):
         self.disable_mid_caption_heads = opt.disable_mid_caption_heads
 
     # ------------------------------------------------------------------------------------------------
-    def forward(self, dt, criterion, transformer_input_type, eval_mode=False):
-        vf = dt["video_tensor"]
-        mask = ~dt["video_mask"]
-        duration = dt["video_length"][:, 1]
+    def trunk(self, vf, video_mask, duration):
+        """The static-shape part of PDVC.forward (pdvc/pdvc.py:123-150 in the reference): base encoder,
+        deformable encoder, decoder with iterative refinement and the per-layer class/count/box heads.
+        Tensors in, tensors out, no host synchronisation: it can be captured as one hipGraph forward and
+        one backward (enable_graph)."""
+        mask = ~video_mask
         N = vf.shape[0]
         srcs, masks, pos = self.base_encoder(vf, mask, duration)
         tr = self.transformer
@@ -101,21 +120,49 @@ class PDVC(nn.Module):
             srcs, masks, pos)
         level_T = tr.last_level_T
         memory = tr.forward_encoder(src_flatten, level_T, lsi, valid_ratios, lvl_pos, mask_flatten)
-        two_stage, disable_refine, proposals, proposals_mask = decide_two_stage(transformer_input_type, dt,
-                                                                                 criterion)
         query_embed = self.query_embed.weight
         proposals_mask = torch.ones(N, query_embed.shape[0], device=query_embed.device).bool()
         init_reference, tgt, reference_points, query_embed = tr.prepare_decoder_input_query(memory, query_embed)
         hs, inter_references = tr.forward_decoder(tgt, reference_points, memory, level_T, lsi, valid_ratios,
-                                                  query_embed, mask_flatten, proposals_mask, disable_refine)
+                                                  query_embed, mask_flatten, proposals_mask, False)
+        classes, counts, coords = self._layer_heads(hs, init_reference, inter_references, False)
+        return (memory, mask_flatten, temporal_shapes, lsi, valid_ratios, proposals_mask, hs, init_reference,
+                inter_references, torch.stack(classes), torch.stack(counts), torch.stack(coords))
+
+    def enable_graph(self, dt):
+        """Capture trunk() for the shapes of `dt` (training mode) with torch.cuda.make_graphed_callables:
+        later training forwards of the same shapes replay one forward graph and, inside backward(), one
+        backward graph, instead of launching ~700 kernels from Python.  Dropout inside stays random per
+        replay (graph-safe RNG; the HIP kernels draw their seeds on the device)."""
+        sample = (dt["video_tensor"], dt["video_mask"], dt["video_length"][:, 1].contiguous())
+        mod = _TrunkModule(self)
+        key = tuple((tuple(t.shape), t.dtype) for t in sample)
+        graphed = torch.cuda.make_graphed_callables(mod, sample, allow_unused_input=True)
+        # kept outside the module registry: state_dict keys stay the reference's
+        object.__setattr__(self, "_graph_key", key)
+        object.__setattr__(self, "_graphed_trunk", graphed)
+
+    def _run_trunk(self, dt):
+        args = (dt["video_tensor"], dt["video_mask"], dt["video_length"][:, 1].contiguous())
+        g = self.__dict__.get("_graphed_trunk")
+        if g is not None and self.training and tuple((tuple(t.shape), t.dtype) for t in args) == self._graph_key:
+            return g(*args)
+        return self.trunk(*args)
+
+    def forward(self, dt, criterion, transformer_input_type, eval_mode=False):
+        two_stage, disable_refine, proposals, proposals_mask = decide_two_stage(transformer_input_type, dt,
+                                                                                 criterion)
+        (memory, mask_flatten, temporal_shapes, lsi, valid_ratios, proposals_mask, hs, init_reference,
+         inter_references, classes, counts, coords) = self._run_trunk(dt)
         others = {"memory": memory, "mask_flatten": mask_flatten, "spatial_shapes": temporal_shapes,
-                  "level_T": level_T, "level_start_index": lsi, "valid_ratios": valid_ratios,
+                  "level_T": self.transformer.last_level_T, "level_start_index": lsi, "valid_ratios": valid_ratios,
                   "proposals_mask": proposals_mask}
+        heads = (list(classes.unbind(0)), list(counts.unbind(0)), list(coords.unbind(0)))
         if eval_mode or self.opt.caption_loss_coef == 0:
             return self.parallel_prediction_full(dt, criterion, hs, init_reference, inter_references, others,
-                                                 disable_refine)
+                                                 disable_refine, heads)
         return self.parallel_prediction_matched(dt, criterion, hs, init_reference, inter_references, others,
-                                                disable_refine)
+                                                disable_refine, heads)
 
     def predict_event_num(self, counter, hs_lid):
         return counter(torch.max(hs_lid, dim=1, keepdim=False)[0])
@@ -197,8 +244,9 @@ class PDVC(nn.Module):
                     cap_rows=cap_rows, lay=lay, vid=vid, last_sel=last_sel_d, steps_v=steps_v)
 
     def parallel_prediction_matched(self, dt, criterion, hs, init_reference, inter_references, others,
-                                    disable_refine):
-        classes, counts, coords = self._layer_heads(hs, init_reference, inter_references, disable_refine)
+                                    disable_refine, heads=None):
+        classes, counts, coords = heads if heads is not None else self._layer_heads(hs, init_reference,
+                                                                                    inter_references, disable_refine)
         N, Q = hs.shape[1], hs.shape[2]
         zero_probs = {"cap_prob_train": torch.zeros(1, device=hs.device),
                       "cap_prob_eval": torch.zeros(N, Q, 3, device=hs.device)}
@@ -238,8 +286,9 @@ class PDVC(nn.Module):
         return out, loss
 
     def parallel_prediction_full(self, dt, criterion, hs, init_reference, inter_references, others,
-                                 disable_refine):
-        classes, counts, coords = self._layer_heads(hs, init_reference, inter_references, disable_refine)
+                                 disable_refine, heads=None):
+        classes, counts, coords = heads if heads is not None else self._layer_heads(hs, init_reference,
+                                                                                    inter_references, disable_refine)
         Ld, N, Q, C = hs.shape
         probs, seqs = [], []
         for l_id in range(Ld):

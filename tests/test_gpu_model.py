@@ -140,3 +140,33 @@ def test_eval_forward_matches_reference(case):
     assert out["pred_count"].argmax(-1).clamp(min=1).cpu().tolist() == d["eval.count_argmax"].tolist()
     assert out["seq"].cpu().tolist() == d["eval.seq"].tolist(), "greedy caption tokens differ"
     close(out["caption_probs"]["cap_prob_eval"], d["eval.cap_prob_eval"], 1e-4, 1e-4, "cap_prob_eval")
+
+
+def test_graphed_trunk_matches_eager():
+    """enable_graph: the captured trunk (hipGraph forward + backward) gives the eager step's losses and
+    gradients, over two consecutive replays (static buffers re-used correctly), dropout off."""
+    d = load("pdvc_small_anet")
+    model, criterion = build_filled(d)
+    model.train()
+    dt = fixture_dt(d)
+    dt["video_length"] = dt["video_length"].contiguous()
+    wd = criterion.weight_dict
+
+    def run():
+        model.zero_grad(set_to_none=True)
+        out, loss = model(dt, criterion, "queries")
+        total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
+        total.backward()
+        return total.item(), {n: (p.grad.clone() if p.grad is not None else None) for n, p in model.named_parameters()}
+
+    t0, g0 = run()
+    model.enable_graph(dt)
+    for _ in range(2):
+        t1, g1 = run()
+        assert abs(t1 - t0) <= 1e-5 * max(1.0, abs(t0)), (t1, t0)
+        for n in g0:
+            assert (g0[n] is None) == (g1[n] is None), n
+            if g0[n] is not None:
+                err = (g0[n] - g1[n]).abs().max().item()
+                assert err <= 1e-5 * (g0[n].abs().max().item() + 1e-6), f"{n}: {err}"
+    assert list(model.state_dict().keys()) == [str(k) for k in d["state_keys"]]
