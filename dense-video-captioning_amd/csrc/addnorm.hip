@@ -14,7 +14,6 @@
 namespace pdvc {
 
 constexpr int kAND = 512;              // max row width
-constexpr int kAPL = kAND / 64;        // columns per lane (max)
 constexpr int kANW = 4;                // waves per workgroup
 
 __device__ __forceinline__ uint32_t an_mix(uint32_t x) {

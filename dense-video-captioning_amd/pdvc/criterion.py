@@ -11,7 +11,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import box_ops, hostio
-from .matcher import padded_targets
+from .matcher import LazyIndices, padded_targets
 
 COUNTER_CLASS_RATE = [0.00000000e+00, 0.00000000e+00, 1.93425917e-01, 4.12129084e-01, 1.88929963e-01,
                       7.81296833e-02, 5.09541413e-02, 3.12718553e-02, 1.84833650e-02, 8.39244680e-03,
@@ -73,12 +73,16 @@ class SetCriterion(nn.Module):
         nb = pt["num_boxes"]  # (N,) float, clamp(min=1)
         # matched pairs of every video, flattened: (video, query, target slot, rank) and the per-video match
         # counts -- one asynchronous host->device copy
-        vid = np.concatenate([np.full(len(i), v, np.int64) for v, (i, _) in enumerate(indices)])
-        qid = np.concatenate([i.numpy() for i, _ in indices])
-        tid = np.concatenate([j.numpy() for _, j in indices])
-        rank = np.concatenate([np.arange(len(i)) for i, _ in indices])
-        nmatch = np.asarray([len(i) for i, _ in indices], np.int64)
-        pv, pq, pt_, pr, n_dev = hostio.pack_to_device([vid, qid, tid, rank, nmatch], dev)
+        if pairs is None:
+            vid = np.concatenate([np.full(len(i), v, np.int64) for v, (i, _) in enumerate(indices)])
+            qid = np.concatenate([i.numpy() for i, _ in indices])
+            tid = np.concatenate([j.numpy() for _, j in indices])
+            rank = np.concatenate([np.arange(len(i)) for i, _ in indices])
+            nmatch = np.asarray([len(i) for i, _ in indices], np.int64)
+            pv, pq, pt_, pr, n_dev = hostio.pack_to_device([vid, qid, tid, rank, nmatch], dev)
+            emax = max(len(i) for i, _ in indices) if indices else 0
+        else:
+            pv, pq, pt_, pr, n_dev, emax = pairs
         # labels: focal loss over every query and class (criterion.py:46-65)
         tclass = torch.full((N, Q), self.num_classes, dtype=torch.int64, device=dev)
         tclass[pv, pq] = pt["labels"][pv, pt_]
@@ -107,7 +111,6 @@ class SetCriterion(nn.Module):
         loss_bbox = torch.zeros(N, device=dev, dtype=l1.dtype).index_add_(0, pv, l1) / nb
         loss_giou = torch.zeros(N, device=dev, dtype=l1.dtype).index_add_(0, pv, 1 - giou) / nb
         # self-IoU among each video's matched predictions, upper triangle, / (n(n-1)/2)
-        emax = max(len(i) for i, _ in indices) if indices else 0
         padded = torch.zeros(N, max(emax, 1), 2, device=dev, dtype=sxy.dtype)
         padded[pv, pr] = sxy
         valid = torch.zeros(N, max(emax, 1), dtype=torch.bool, device=dev)
@@ -133,11 +136,19 @@ class SetCriterion(nn.Module):
         boxes = torch.cat([o["pred_boxes"] for o in layers], 0)
         count = torch.cat([o["pred_count"] for o in layers], 0)
         costs = self.matcher.cost_padded(logits, boxes, ptL)  # (Ld*N, Q, Emax)
-        solved = self.matcher.solve_padded(list(costs.view(Ld, N, *costs.shape[1:])), pt["sizes"])
-        idx = [(s_, None) for s_ in solved]
+        if costs.is_cuda and costs.dtype == torch.float32 and max(pt["sizes"], default=0) <= costs.shape[1]:
+            # matching on the GPU (scipy's algorithm): no host round trip anywhere in the training step
+            m = self.matcher.solve_device(costs, ptL["sizes"], ptL["sizes_i32"])
+            pp, pk, nm, emax = static_pairs(ptL)
+            pairs = (pp, m.queries[pp, pk], m.targets[pp, pk], pk, nm, emax)
+            per = self.video_losses(logits, boxes, count, ptL, None, pairs)
+            idx = [(LazyIndices(m, b, N), None) for b in range(Ld)]
+        else:
+            solved = self.matcher.solve_padded(list(costs.view(Ld, N, *costs.shape[1:])), pt["sizes"])
+            idx = [(s_, None) for s_ in solved]
+            per = self.video_losses(logits, boxes, count, ptL, [m_ for s_ in solved for m_ in s_])
         last_indices = idx[0]
         outputs["matched_indices"] = last_indices
-        per = self.video_losses(logits, boxes, count, ptL, [m for s_ in solved for m in s_])
         per = {k: v.view(Ld, N).mean(1) for k, v in per.items()}
         losses = {k: v[0] for k, v in per.items()}
         if "aux_outputs" in outputs:
@@ -146,6 +157,20 @@ class SetCriterion(nn.Module):
                 losses.update({k + f"_{i}": v[i + 1] for k, v in per.items()})
             return losses, last_indices, aux_indices
         return losses, last_indices
+
+
+def static_pairs(pt):
+    """(problem, rank) of every matched pair -- known from the target counts alone, since every target is
+    matched -- plus the per-problem match counts and the largest; device tensors, cached on the dict."""
+    key = ("pairs",)
+    if key not in pt:
+        sizes = pt["sizes"]
+        pp = np.concatenate([np.full(e, p, np.int64) for p, e in enumerate(sizes)] or [np.zeros(0, np.int64)])
+        pk = np.concatenate([np.arange(e) for e in sizes] or [np.zeros(0, np.int64)])
+        dev = pt["sizes_long"].device
+        pp_d, pk_d = hostio.pack_to_device([pp, pk], dev)
+        pt[key] = (pp_d, pk_d, pt["sizes_long"], max(sizes, default=0))
+    return pt[key]
 
 
 def repeat_targets(pt, times):

@@ -1,8 +1,9 @@
 """Hungarian matcher (reference: pdvc/matcher.py:22-152).
 
 Cost = cost_bbox * L1 + cost_class * focal-style class cost + cost_giou * (-GIoU), computed for every video
-of the batch on the GPU in one pass; ONE device->host copy brings all cost blocks over; the assignment is
-scipy's linear_sum_assignment per video (the reference's solver, so matched indices are bit-exact).
+of the batch on the GPU in one pass.  The assignment is solved on the GPU (pdvc_lsap_f32, csrc/lsap.hip: the
+algorithm and tie rule of scipy's linear_sum_assignment, so matched indices are scipy's bit for bit) with no
+host round trip; `solve_padded` keeps the host/scipy route (ONE device->host copy for every block).
 The reference also solves a 4x-replicated "many-to-one" problem whose result no loss uses; it is skipped.
 """
 import numpy as np
@@ -10,6 +11,7 @@ import torch
 from scipy.optimize import linear_sum_assignment
 from torch import nn
 
+from . import _native as _n
 from . import hostio
 from .box_ops import box_cl_to_xy, generalized_box_iou
 
@@ -50,6 +52,18 @@ class HungarianMatcher(nn.Module):
         return self.solve(self.cost_blocks(outputs["pred_logits"], outputs["pred_boxes"], targets))
 
     @staticmethod
+    @torch.no_grad()
+    def solve_device(costs, sizes, sizes_dev):
+        """costs (P, Q, Emax) device float32, sizes host list (P,), sizes_dev the same as a device int32 tensor
+        -> DeviceMatching: per problem the matched queries ascending and their targets, on the device."""
+        P, Q, E = costs.shape
+        qo = torch.zeros((P, max(E, 1)), dtype=torch.int64, device=costs.device)
+        to = torch.zeros_like(qo)
+        _n.call("pdvc_lsap_f32", _n.ptr(costs.contiguous()), P, Q, E, _n.int_array(tuple(sizes)),
+                _n.ptr(sizes_dev), _n.ptr(qo), _n.ptr(to), _n.stream())
+        return DeviceMatching(qo, to, list(sizes))
+
+    @staticmethod
     def solve_padded(costs, sizes):
         """costs: list of (N, Q, Emax) device tensors (one per decoder layer) -> per layer, per video
         (query ids, target ids); ONE device->host copy for everything."""
@@ -77,6 +91,40 @@ class HungarianMatcher(nn.Module):
         return out, None
 
 
+class DeviceMatching:
+    """Matchings of P problems held on the device: queries (P, Emax) ascending, targets (P, Emax)."""
+
+    def __init__(self, queries, targets, sizes):
+        self.queries, self.targets, self.sizes = queries, targets, sizes
+        self._host = None
+
+    def host(self):
+        if self._host is None:  # one device->host copy, only when a caller asks for Python lists
+            q, t = self.queries.cpu(), self.targets.cpu()
+            self._host = [(q[p, :e].clone(), t[p, :e].clone()) for p, e in enumerate(self.sizes)]
+        return self._host
+
+
+class LazyIndices:
+    """The reference's per-video list of (query ids, target ids) for one block of N problems of a
+    DeviceMatching; materialised on the host on first access (the training step never needs it)."""
+
+    def __init__(self, matching, block, n):
+        self.matching, self.block, self.n = matching, block, n
+
+    def __len__(self):
+        return self.n
+
+    def _list(self):
+        return self.matching.host()[self.block * self.n:(self.block + 1) * self.n]
+
+    def __getitem__(self, i):
+        return self._list()[i]
+
+    def __iter__(self):
+        return iter(self._list())
+
+
 def padded_targets(targets, device):
     """Targets of a batch padded to the largest event count: labels (N, Emax) long, boxes (N, Emax, 2)
     (padding boxes are a harmless (0.5, 0.5) segment), valid (N, Emax) bool, sizes [E_v]."""
@@ -95,7 +143,7 @@ def padded_targets(targets, device):
     sizes_t = torch.tensor(sizes, dtype=torch.long)
     return {"labels": hostio.to_device(labels, device), "boxes": hostio.to_device(boxes, device),
             "valid": hostio.to_device(valid, device), "sizes": sizes,
-            "sizes_long": hostio.to_device(sizes_t, device),
+            "sizes_long": hostio.to_device(sizes_t, device), "sizes_i32": hostio.to_device(sizes_t.int(), device),
             "num_boxes": hostio.to_device(sizes_t.float().clamp(min=1.0), device)}
 
 

@@ -20,7 +20,7 @@ from .CaptioningHead import build_captioner
 from .CaptioningHead.LSTM_DSA import caption_steps
 from .criterion import SetCriterion
 from .deformable_transformer import build_deforamble_transformer
-from .matcher import build_matcher
+from .matcher import LazyIndices, build_matcher
 
 
 def _get_clones(module, N):
@@ -210,19 +210,39 @@ class PDVC(nn.Module):
         cap_off = [0]
         for g in gt_counts:
             cap_off.append(cap_off[-1] + g)
-        rows = []  # (layer, video, flat_hs_index, cap_row)
-        for l_id, indices in enumerate(layer_indices):
-            for v, (qi, gi) in enumerate(indices):
-                for q, g in zip(qi.tolist(), gi.tolist()):
-                    rows.append((l_id, v, (l_id * N + v) * Q + q, cap_off[v] + g))
-        # layer-0 rows first: their reference is 1-d
-        rows.sort(key=lambda r: (0 if r[0] == 0 else 1))
         Ld_last = Ld - 1
-        last_sel = [i for i, r in enumerate(rows) if r[0] == Ld_last]
-        # every per-row index array in ONE asynchronous host->device copy
-        flat_idx, cap_rows, row_video, lay, vid, last_sel_d = hostio.pack_to_device(
-            [[r[2] for r in rows], [r[3] for r in rows], [r[1] for r in rows], [r[0] for r in rows],
-             [r[1] for r in rows], last_sel], dev)
+        if all(isinstance(ix, LazyIndices) for ix in layer_indices):
+            # matching on the device: which rows exist is known from the target counts alone (every target is
+            # matched); only the matched query and target of each row come from the device matching
+            m = layer_indices[0].matching
+            rows, r_p, r_k, r_base, r_cap = [], [], [], [], []
+            for l_id, ix in enumerate(layer_indices):  # layer-major: layer 0 (1-d references) first
+                for v in range(N):
+                    for k in range(gt_counts[v]):
+                        rows.append((l_id, v))
+                        r_p.append(ix.block * N + v)
+                        r_k.append(k)
+                        r_base.append((l_id * N + v) * Q)
+                        r_cap.append(cap_off[v])
+            last_sel = [i for i, r in enumerate(rows) if r[0] == Ld_last]
+            rp, rk, rb, rc, row_video, lay, vid, last_sel_d = hostio.pack_to_device(
+                [r_p, r_k, r_base, r_cap, [r[1] for r in rows], [r[0] for r in rows], [r[1] for r in rows],
+                 last_sel], dev)
+            flat_idx = rb + m.queries[rp, rk]
+            cap_rows = rc + m.targets[rp, rk]
+        else:
+            rows = []  # (layer, video, flat_hs_index, cap_row)
+            for l_id, indices in enumerate(layer_indices):
+                for v, (qi, gi) in enumerate(indices):
+                    for q, g in zip(qi.tolist(), gi.tolist()):
+                        rows.append((l_id, v, (l_id * N + v) * Q + q, cap_off[v] + g))
+            # layer-0 rows first: their reference is 1-d
+            rows.sort(key=lambda r: (0 if r[0] == 0 else 1))
+            last_sel = [i for i, r in enumerate(rows) if r[0] == Ld_last]
+            # every per-row index array in ONE asynchronous host->device copy
+            flat_idx, cap_rows, row_video, lay, vid, last_sel_d = hostio.pack_to_device(
+                [[r[2] for r in rows], [r[3] for r in rows], [r[1] for r in rows], [r[0] for r in rows],
+                 [r[1] for r in rows], last_sel], dev)
         row_video = row_video.to(torch.int32)
         rd1 = sum(1 for r in rows if r[0] == 0 and init_reference.shape[-1] == 1)
         hs_rows = hs.reshape(Ld * N * Q, C).index_select(0, flat_idx)

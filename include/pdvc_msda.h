@@ -33,6 +33,8 @@
  *                                      (LSTM_DSA.py:245-258: tanh, alpha_net, softmax, weighted sum)
  *   pdvc_add_dropout_layernorm_*    <- the residual epilogue norm(x + dropout(s)) of every transformer sub-layer
  *                                      (deformable_transformer.py:150-156, 253-271)
+ *   pdvc_lsap_f32                   <- HungarianMatcher's scipy.optimize.linear_sum_assignment per video
+ *                                      (pdvc/matcher.py:119-121), same algorithm and tie rule, on the GPU
  *   pdvc_gemm_f32                   <- the dense projections (nn.Linear forward/backward) of the layers
  *                                      above: MSDeformAttn value/offset/output projections
  *                                      (ms_deform_attn.py:79-126), the FFNs (deformable_transformer.py:150-156,
@@ -203,6 +205,14 @@ int pdvc_add_dropout_layernorm_backward_f32(const float* x, const float* s, cons
                                             const float* rstd, const float* dy, int rows, int d, float p,
                                             uint64_t seed, const uint64_t* seed_dev, float* dx, float* ds,
                                             float* dgamma, float* dbeta, float* workspace, void* stream);
+
+/* ---- linear sum assignment (the set matcher) --------------------------------------------------------
+ * costs (P, Q, max_targets) float32: problem p matches its first sizes[p] targets (rows of scipy's transposed
+ * problem) to the Q queries; sizes given on the host (validated) and on the device.  Outputs (P, max_targets)
+ * int64: the matched queries of problem p in ascending order and the target of each -- scipy's
+ * (row_ind, col_ind) of the (Q, sizes[p]) matrix; entries past sizes[p] are not written. */
+int pdvc_lsap_f32(const float* costs, int num_problems, int num_query, int max_targets, const int32_t* sizes_host,
+                  const int32_t* sizes_dev, int64_t* query_out, int64_t* target_out, void* stream);
 
 /* ---- fp32 GEMM on the matrix cores ----------------------------------------------------------------
  * C[M,N] = op(A)[M,K] op(B)[K,N] (+ bias[N]) (ReLU).  op(A): trans_a 0 -> A[m*lda + k], 1 -> A[k*lda + m];

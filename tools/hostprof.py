@@ -16,7 +16,9 @@ import bench  # noqa: E402
 
 
 def main():
-    sys.argv = [sys.argv[0], "--cpu-seconds", "0"] + sys.argv[1:]
+    graph = "--graph" in sys.argv
+    argv = [x for x in sys.argv[1:] if x != "--graph"]
+    sys.argv = [sys.argv[0], "--cpu-seconds", "0"] + argv
     a = bench.parse()
     from pdvc.data import synthetic_videos, collate, to_device
     device = torch.device("cuda:0")
@@ -37,6 +39,8 @@ def main():
         torch.nn.utils.clip_grad_norm_(params, args.grad_clip)
         opt.step()
 
+    if graph:
+        model.enable_graph(dt)
     for _ in range(3):
         step()
     torch.cuda.synchronize()
