@@ -56,6 +56,7 @@ class SetCriterion(nn.Module):
         self.focal_gamma = focal_gamma
         self.opt = opt
         self.counter_class_rate = torch.tensor(COUNTER_CLASS_RATE)
+        self.device_matching = None  # None: match on the GPU whenever the costs live there
 
     # -------------------------------------------------------------------------------------------------
     def layer_losses(self, outputs, pt, indices):
@@ -63,10 +64,11 @@ class SetCriterion(nn.Module):
         v = self.video_losses(outputs["pred_logits"], outputs["pred_boxes"], outputs["pred_count"], pt, indices)
         return {k: t.mean() for k, t in v.items()}
 
-    def video_losses(self, logits, boxes, count, pt, indices):
+    def video_losses(self, logits, boxes, count, pt, indices, pairs=None):
         """Per-video loss vectors (N,) for a batch of N videos -- or of N = layers x videos when the decoder
         layers are stacked -- computed for all at once.  logits (N,Q,C), boxes (N,Q,2), count (N,K+1); pt:
-        padded targets; indices: list of (query ids, target ids) per video."""
+        padded targets; indices: list of (query ids, target ids) per video, or None with `pairs` = device
+        tensors (video, query, target, rank, per-video match count) and the largest count."""
         N, Q, C = logits.shape
         dev = logits.device
         sizes = pt["sizes"]
@@ -136,7 +138,8 @@ class SetCriterion(nn.Module):
         boxes = torch.cat([o["pred_boxes"] for o in layers], 0)
         count = torch.cat([o["pred_count"] for o in layers], 0)
         costs = self.matcher.cost_padded(logits, boxes, ptL)  # (Ld*N, Q, Emax)
-        if costs.is_cuda and costs.dtype == torch.float32 and max(pt["sizes"], default=0) <= costs.shape[1]:
+        on_device = self.device_matching if self.device_matching is not None else costs.is_cuda
+        if on_device and costs.dtype == torch.float32 and max(pt["sizes"], default=0) <= costs.shape[1]:
             # matching on the GPU (scipy's algorithm): no host round trip anywhere in the training step
             m = self.matcher.solve_device(costs, ptL["sizes"], ptL["sizes_i32"])
             pp, pk, nm, emax = static_pairs(ptL)

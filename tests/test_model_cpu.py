@@ -93,3 +93,59 @@ def test_matcher_solves_like_scipy():
         c = m.cost_blocks(logits, boxes, targets)[v].numpy()
         ei, ej = linear_sum_assignment(c)
         assert i.tolist() == ei.tolist() and j.tolist() == ej.tolist()
+
+
+def test_criterion_device_matching_path_equals_host_path(monkeypatch):
+    """The device-matching bookkeeping of SetCriterion (static pairs, LazyIndices, per-layer means) gives the
+    host path's losses and indices; the GPU solver is stood in for by scipy here (its own parity test is
+    tests/test_gpu_lsap.py)."""
+    import types
+    import numpy as np
+    from scipy.optimize import linear_sum_assignment
+    from pdvc.criterion import SetCriterion
+    from pdvc.matcher import DeviceMatching, HungarianMatcher, padded_targets
+
+    def fake_solve_device(costs, sizes, sizes_dev):
+        P, Q, E = costs.shape
+        q = torch.zeros((P, max(E, 1)), dtype=torch.int64)
+        t = torch.zeros_like(q)
+        for p_, e in enumerate(sizes):
+            i, j = linear_sum_assignment(costs[p_, :, :e].numpy())
+            q[p_, :e] = torch.from_numpy(i)
+            t[p_, :e] = torch.from_numpy(j)
+        return DeviceMatching(q, t, list(sizes))
+
+    monkeypatch.setattr(HungarianMatcher, "solve_device", staticmethod(fake_solve_device))
+    torch.manual_seed(0)
+    N, Q, Ld = 5, 20, 3
+    targets = []
+    for v in range(N):
+        e = 1 + v % 4
+        c = torch.rand(e) * 0.8 + 0.1
+        targets.append({"labels": torch.zeros(e, dtype=torch.long),
+                        "boxes": torch.stack([c, torch.rand(e) * 0.2 + 0.05], -1)})
+    opt = types.SimpleNamespace(lloss_gau_mask=1, lloss_beta=1)
+    weight = {"loss_ce": 2, "loss_bbox": 0, "loss_giou": 4, "loss_counter": 0.5}
+    crit = SetCriterion(1, HungarianMatcher(2, 0, 4), weight, ["labels", "boxes"], opt=opt)
+
+    def outputs():
+        g = torch.Generator().manual_seed(1)
+        layers = [{"pred_logits": torch.randn(N, Q, 1, generator=g), "pred_boxes": torch.rand(N, Q, 2, generator=g),
+                   "pred_count": torch.randn(N, 11, generator=g)} for _ in range(Ld)]
+        out = dict(layers[0])
+        out["aux_outputs"] = layers[1:]
+        return out
+
+    res = {}
+    for dev_match in (False, True):
+        crit.device_matching = dev_match
+        losses, last, aux = crit(outputs(), targets, padded_targets(targets, "cpu"))
+        res[dev_match] = (losses, [list(last[0])] + [list(a[0]) for a in aux])
+    lh, ih = res[False]
+    ld, idd = res[True]
+    assert set(lh) == set(ld)
+    for k in lh:
+        assert torch.allclose(lh[k], ld[k], rtol=1e-6, atol=1e-7, equal_nan=True), k
+    for a, b in zip(ih, idd):
+        for (i1, j1), (i2, j2) in zip(a, b):
+            assert i1.tolist() == i2.tolist() and j1.tolist() == j2.tolist()
