@@ -18,6 +18,7 @@ from torch.autograd import Function
 from torch.autograd.function import once_differentiable
 
 from pdvc import _native as _n
+from .linear import wgrad_mm
 from .ms_deform_attn_func import NUM_SAMPLES, _levels
 
 
@@ -132,15 +133,15 @@ class CaptionDecodeFunction(Function):
         d_xg = d_gates.permute(1, 0, 2).contiguous()
         d_off_hs = dHP[..., :n_off].sum(0)
         if n > 1:
-            dW_h = dHP[1:].reshape(-1, Ph).t() @ HS[:, :-1].transpose(0, 1).reshape(-1, H)
+            dW_h = wgrad_mm(dHP[1:].reshape(-1, Ph), HS[:, :-1].transpose(0, 1).reshape(-1, H))
         else:
             dW_h = torch.zeros_like(W_h)
         db_h = dHP.sum((0, 1))
         dA2 = dATT.view(-1, A)
-        dW_ctx = dA2.t() @ CLIP.view(-1, D)
+        dW_ctx = wgrad_mm(dA2, CLIP.view(-1, D))
         db_ctx = dA2.sum(0)
         dalpha_w = GAW.sum((0, 1))
         dalpha_b = GAB.sum().reshape(1)
-        dW_att = d_gates.reshape(-1, G).t() @ RES.view(-1, M * D)
+        dW_att = wgrad_mm(d_gates.reshape(-1, G), RES.view(-1, M * D))
         return (gv, d_xg, d_off_hs, gr, dW_h, db_h, dW_ctx, db_ctx, dalpha_w, dalpha_b, dW_att, None, None, None,
                 None)

@@ -95,9 +95,61 @@ def linear(x, weight, bias=None, relu=False):
     return LinearFunction.apply(x, weight, bias, relu)
 
 
+def wgrad_splits(rows):
+    """K-chunks for a weight gradient over `rows` rows: hipBLASLt runs dW = dy^T x (512 x 512 outputs, K = N*S
+    = 30720) on 128 workgroups at ~70 TF/s; as a batched GEMM over 16 row chunks plus a sum it fills the
+    chip at ~135 TF/s (tools/gemmbench.py on MI355X).  1 = a plain GEMM."""
+    for s in (16, 8, 4, 2):
+        if rows % s == 0 and rows // s >= 1536:
+            return s
+    return 1
+
+
+def wgrad_mm(gy, x):
+    """gy^T x for row-major gy (rows, O) and x (rows, I): the weight-gradient product, split over K."""
+    rows = gy.shape[0]
+    s = wgrad_splits(rows)
+    if s == 1:
+        return torch.mm(gy.t(), x)
+    return torch.bmm(gy.reshape(s, rows // s, gy.shape[1]).transpose(1, 2), x.reshape(s, rows // s, x.shape[1])).sum(0)
+
+
+class TorchLinearFunction(Function):
+    """nn.Linear (+ fused ReLU) on hipBLASLt with a split-K weight gradient (see wgrad_splits)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu=False):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        y = torch.addmm(bias, x2, weight.t()) if bias is not None else torch.mm(x2, weight.t())
+        if relu:
+            y.relu_()
+        ctx.save_for_backward(x2, weight, y if relu else None)
+        ctx.has_bias = bias is not None
+        return y.view(*shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, weight, y = ctx.saved_tensors
+        O = weight.shape[0]
+        gy2 = gy.reshape(-1, O)
+        if y is not None:
+            gy2 = torch.ops.aten.threshold_backward(gy2, y, 0.0)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.mm(gy2, weight).view(*gy.shape[:-1], weight.shape[1])
+        if ctx.needs_input_grad[1]:
+            gw = wgrad_mm(gy2, x2)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = gy2.sum(0)
+        return gx, gw, gb, None
+
+
 def dense(x, weight, bias=None, relu=False):
     """nn.Linear (+ ReLU) on the backend selected by BACKEND (fp32 CUDA tensors only go to the HIP GEMM)."""
-    if BACKEND == "hip" and x.is_cuda and x.dtype == torch.float32 and weight.dtype == torch.float32:
-        return LinearFunction.apply(x, weight, bias, relu)
+    if x.is_cuda and x.dtype == torch.float32 and weight.dtype == torch.float32:
+        if BACKEND == "hip":
+            return LinearFunction.apply(x, weight, bias, relu)
+        return TorchLinearFunction.apply(x, weight, bias, relu)
     y = F.linear(x, weight, bias)
     return F.relu(y) if relu else y

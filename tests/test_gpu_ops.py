@@ -260,6 +260,64 @@ def test_fused_msda1d_pdvc_shape_vs_oracle():
     close(p.grad, egp, 1e-4, "grad_proj")
 
 
+@pytest.mark.parametrize("ref_dim", [1, 2])
+@pytest.mark.parametrize("masked", [False, True])
+@pytest.mark.parametrize("offset_scale", [2.0, 60.0])
+def test_fused_msda1d_pyramid_tiled_vs_oracle(ref_dim, masked, offset_scale):
+    """Self-attention over the pyramid (Lq == S, D = 64) takes the LDS-windowed kernels (pick_slices in
+    msda1d.hip).  offset_scale 60 scatters samples over whole levels, so windows overflow the LDS budget and
+    levels fall back to global gathers: results must not depend on the windowing."""
+    from pdvc.ops.functions import MSDA1dFunction
+    rng = np.random.RandomState(7 + ref_dim + 10 * masked + int(offset_scale))
+    T_l = [96, 48, 24, 12]
+    S = sum(T_l)
+    M, D, N, Lq = 4, 64, 3, S
+    value = rng.randn(N, S, M, D)
+    proj = np.concatenate([rng.randn(N, Lq, M * 16) * offset_scale, rng.randn(N, Lq, M * 16)], -1)
+    centre = np.concatenate([(np.arange(t) + 0.5) / t for t in T_l])[None, :, None, None].repeat(4, 2)
+    centre = np.repeat(centre, N, 0)
+    if ref_dim == 1:
+        ref = centre
+    else:
+        ref = np.concatenate([centre, rng.uniform(0.05, 0.5, size=(N, Lq, 4, 1))], -1)
+    mask = None
+    if masked:
+        mask = np.zeros((N, S), bool)
+        mask[1, 80:96] = True
+        mask[1, 136:144] = True
+        mask[2, 170:] = True
+    gout = rng.randn(N, Lq, M * D)
+    eo, egv, egp, egr = expected_msda1d(value, mask, proj, ref, T_l, M, gout)
+    v = cu(value, torch.float32).requires_grad_()
+    p = cu(proj, torch.float32).requires_grad_()
+    r = cu(ref, torch.float32).requires_grad_()
+    mk = None if mask is None else cu(mask).view(torch.uint8)
+    out = MSDA1dFunction.apply(v, mk, p, r, tuple(T_l), 0, M * 16)
+    close(out, eo, 1e-4, "out")
+    out.backward(cu(gout, torch.float32))
+    close(v.grad, egv, 1e-4, "grad_value")
+    close(p.grad, egp, 1e-4, "grad_proj")
+    close(r.grad, egr, 1e-4, "grad_ref")
+
+
+def test_fused_msda1d_tiled_equals_untiled():
+    """The tiled and the per-query kernels share their arithmetic (the untiled path runs on the same queries
+    minus the last, so Lq != S): equal up to FMA contraction."""
+    from pdvc.ops.functions import MSDA1dFunction
+    rng = np.random.RandomState(3)
+    T_l = [64, 32, 16, 8]
+    S = sum(T_l)
+    M, D, N = 8, 64, 2
+    value = cu(rng.randn(N, S, M, D), torch.float32)
+    proj = cu(np.concatenate([rng.randn(N, S, M * 16) * 2, rng.randn(N, S, M * 16)], -1), torch.float32)
+    ref = cu(rng.uniform(0, 1, size=(N, S, 4, 1)), torch.float32)
+    full = MSDA1dFunction.apply(value, None, proj, ref, tuple(T_l), 0, M * 16)  # tiled (Lq == S)
+    part = MSDA1dFunction.apply(value, None, proj[:, :S - 1].contiguous(), ref[:, :S - 1].contiguous(), tuple(T_l),
+                                0, M * 16)  # untiled
+    err = (full[:, :S - 1] - part).abs().max().item()
+    assert err <= 1e-6 * (part.abs().max().item() + 1.0), err
+
+
 # ------------------------------------------------------------------------------------------------
 # caption gather (border raw samples) vs oracle
 # ------------------------------------------------------------------------------------------------

@@ -53,7 +53,30 @@ def rate_pdvc(M, N, K, ta, tb, reps=20):
     return 2 * M * N * K / t / 1e12, t * 1e6
 
 
+def rate_splitk_bmm(M, N, K, splits, reps=20):
+    """wgrad dW (M,N) = dy^T (M,K) x (K,N) as a batched GEMM over `splits` K-chunks + a sum (torch)."""
+    dy = torch.randn(K, M, device="cuda")
+    x = torch.randn(K, N, device="cuda")
+    f = lambda: torch.bmm(dy.view(splits, K // splits, M).transpose(1, 2), x.view(splits, K // splits, N)).sum(0)
+    for _ in range(3):
+        f()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        f()
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / reps * 1e-3
+    return 2 * M * N * K / t / 1e12, t * 1e6
+
+
 if __name__ == "__main__":
+    for splits in (2, 4, 8, 16):
+        for (M, N, K) in ((512, 512, 30720), (256, 512, 30720), (512, 768, 16384)):
+            tf, us = rate_splitk_bmm(M, N, K, splits)
+            print(f"{'torch bmm split-K x' + str(splits):28s} M={M:6d} N={N:5d} K={K:6d}: {tf:6.1f} TF/s {us:8.1f} us",
+                  flush=True)
     for s in SHAPES:
         tf, us = rate_pdvc(*s)
         print(f"{'pdvc_gemm_f32':28s} M={s[0]:6d} N={s[1]:5d} K={s[2]:6d} tA={int(s[3])} tB={int(s[4])}: {tf:6.1f} TF/s {us:8.1f} us",
