@@ -45,8 +45,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     p.add_argument("--kernel-report", action="store_true", help="print per-kernel event timings to stderr")
-    p.add_argument("--no-graph", action="store_true",
-                   help="run the static-shape trunk eagerly instead of as a captured hipGraph")
+    p.add_argument("--graph", choices=["step", "trunk", "none"], default="step",
+                   help="step: forward+losses+backward replayed as one captured hipGraph (pdvc/step_graph.py); "
+                        "trunk: only the static-shape trunk graphed (base encoder .. heads); none: eager")
     p.add_argument("--gemm", choices=["hip", "torch"], default=None,
                    help="projection GEMMs on pdvc_gemm_f32 (hip) or torch/hipBLASLt (default: PDVC_GEMM or torch)")
     return p.parse_args()
@@ -133,7 +134,7 @@ def main():
     dt = to_device(collate(synthetic_videos(B, a.T, a.C, a.events, a.words, vocab, seed=1000 + rank)), device)
     wd = criterion.weight_dict
 
-    def step():
+    def eager_step():
         out, loss = model(dt, criterion, "queries")
         total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
         opt.zero_grad(set_to_none=True)
@@ -144,13 +145,34 @@ def main():
         opt.step()
         return total
 
-    if not a.no_graph:
+    step = eager_step
+    if a.graph == "trunk":
         model.enable_graph(dt)  # capture base encoder -> encoder -> decoder -> heads, fwd and bwd
+    elif a.graph == "step":
+        from pdvc.step_graph import StepGraph
+        sg = StepGraph(model, criterion, dt, reducer=reducer)  # forward + losses + backward, one hipGraph
+
+        dbg = os.environ.get("PDVC_DEBUG_SYNC") == "1"
+
+        def step():  # the graph leaves the gradients in place (and averaged over ranks by its reducer)
+            total = sg.replay()
+            if dbg:
+                torch.cuda.synchronize()
+                print("debug: replay ok", file=sys.stderr, flush=True)
+            torch.nn.utils.clip_grad_norm_(params, args.grad_clip)
+            if dbg:
+                torch.cuda.synchronize()
+                print("debug: clip ok", file=sys.stderr, flush=True)
+            opt.step()
+            if dbg:
+                torch.cuda.synchronize()
+                print("debug: adam ok", file=sys.stderr, flush=True)
+            return total
     for _ in range(a.warmup):
         step()
     names = ["pdvc_msda1d_forward_f32", "pdvc_msda1d_backward_f32", "pdvc_cap_gather_forward_f32",
              "pdvc_cap_gather_backward_f32"]
-    graphed = "_graphed_trunk" in model.__dict__
+    graphed = a.graph != "none"
     timer = _native.KernelTimer(names)
     if world > 1:
         dist.barrier()
@@ -170,15 +192,14 @@ def main():
         el = float(t.item())
     timing_note = "HIP events around every launch in the timed steps"
     if graphed:
-        # the timed steps replay the trunk's kernels inside a hipGraph, where no event can bracket one launch:
+        # the timed steps replay the kernels inside a hipGraph, where no event can bracket one launch:
         # time them in 2 untimed eager steps at the same shapes right after (same kernels, same data sizes)
-        g = model.__dict__.pop("_graphed_trunk")
+        model.__dict__.pop("_graphed_trunk", None)
         _native.TIMER = timer
         for _ in range(2):
-            step()
+            eager_step()
         torch.cuda.synchronize()
         _native.TIMER = None
-        model.__dict__["_graphed_trunk"] = g
         timing_note = ("HIP events around every launch in 2 eager steps right after the timed (hipGraph) steps, "
                        "same shapes; step wall time excludes them")
     ks = timer.summary()
@@ -192,7 +213,8 @@ def main():
                                f"L=4 Q={a.Q} 2 enc/2 dec layers, E={a.events} events x {a.words} words, "
                                f"vocab {vocab}, dropout on",
                    "videos_per_gpu": B, "global_batch": B * world, "seq_len": a.T, "gemm": _lin.BACKEND,
-                   "trunk": "hipGraph" if graphed else "eager",
+                   "graph": {"step": "fwd+loss+bwd as one hipGraph", "trunk": "trunk hipGraph",
+                             "none": "eager"}[a.graph],
                    "parallelism": f"dp{world}"},
     }
     # roofline: the fused MSDA forward (the gather kernel; algorithmic bytes per launch / avg launch time)

@@ -31,6 +31,32 @@ from pdvc.ops.modules import MSDeformAttnCap
 from pdvc.ops.modules.linear import Linear
 
 
+class _EmbeddingRows(torch.autograd.Function):
+    """nn.Embedding's lookup with an atomic scatter-add backward (index_add_).  torch's embedding backward
+    sorts the indices and runs rocprim unique-by-key/partition passes; replayed inside a captured hipGraph
+    those faulted on MI355X (illegal address in rocprim's partition kernel), and they are ~6 extra launches."""
+
+    @staticmethod
+    def forward(ctx, weight, idx):
+        ctx.save_for_backward(idx)
+        ctx.rows = weight.shape[0]
+        return weight.index_select(0, idx.reshape(-1)).view(*idx.shape, weight.shape[1])
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        D = g.shape[-1]
+        gw = g.new_zeros((ctx.rows, D)).index_add_(0, idx.reshape(-1), g.reshape(-1, D))
+        return gw, None
+
+
+def embed_rows(embedding, idx):
+    """embedding(idx) for an nn.Embedding without padding_idx/max_norm (the caption head's)."""
+    if embedding.padding_idx is not None or embedding.max_norm is not None or not idx.is_cuda:
+        return embedding(idx)
+    return _EmbeddingRows.apply(embedding.weight, idx)
+
+
 class LSTMWeights(nn.Module):
     """The parameters of nn.LSTM(input_size, hidden_size, num_layers=1, bias=False) under nn.LSTM's names
     and init (uniform +-1/sqrt(hidden)).  Only the weights are used: the cell runs in the decoder loop."""
@@ -184,7 +210,7 @@ class LSTMDSACaptioner(Captioner):
         value, mask_u8 = self._prepare(memory, mask_flatten)
         if n_steps == 0:
             return hs_rows.new_zeros(hs_rows.shape[0], 0, self.vocab_size + 1)
-        xt = self.embed(seq[:, :n_steps])  # (R, n, E)
+        xt = embed_rows(self.embed, seq[:, :n_steps])  # (R, n, E)
         xg = F.linear(xt, w["W_x"]) + F.linear(hs_rows, w["W_hs"])[:, None]  # loop-invariant gate parts
         off_hs = F.linear(hs_rows, w["W_off_hs"], w["b_off"])
         Nv, S, _ = value.shape

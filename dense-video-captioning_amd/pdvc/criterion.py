@@ -116,7 +116,7 @@ class SetCriterion(nn.Module):
         padded = torch.zeros(N, max(emax, 1), 2, device=dev, dtype=sxy.dtype)
         padded[pv, pr] = sxy
         valid = torch.zeros(N, max(emax, 1), dtype=torch.bool, device=dev)
-        valid[pv, pr] = True
+        valid.index_put_((pv, pr), torch.ones(pv.shape, dtype=torch.bool, device=dev))  # no host scalar
         iou = box_ops.box_iou(padded, padded)[0]
         iou = torch.triu(iou, diagonal=1) * (valid[:, :, None] & valid[:, None, :])
         n = n_dev.to(l1.dtype)

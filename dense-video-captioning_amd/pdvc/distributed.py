@@ -50,6 +50,7 @@ class GradAllReducer:
         self.params = uniq
         self.bucket_bytes = int(bucket_mb * 1024 * 1024)
         self.active = None  # params known to receive gradients (set after the first step)
+        self.suspended = False  # True while a step graph is captured: finish() then reduces every bucket
         self._hooks = []
         self._build(self.params)
 
@@ -83,7 +84,7 @@ class GradAllReducer:
 
     def _on_grad(self, p):
         bi = self.bucket_of.get(id(p))
-        if bi is None:
+        if bi is None or self.suspended:
             return
         self.pending[bi] -= 1
         if self.active is not None:

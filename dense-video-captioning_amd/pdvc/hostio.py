@@ -16,6 +16,9 @@ def to_device(x, device, dtype=None):
         t = t.to(dtype)
     if t.device.type != "cpu" or torch.device(device).type == "cpu":
         return t.to(device)
+    if torch.cuda.is_current_stream_capturing():
+        # a copy node would re-read this host buffer at every replay, after it has been freed
+        raise RuntimeError("host->device copy inside a graph capture: cache the device tensor before capturing")
     return t.pin_memory().to(device, non_blocking=True)
 
 

@@ -225,9 +225,14 @@ class PDVC(nn.Module):
                         r_base.append((l_id * N + v) * Q)
                         r_cap.append(cap_off[v])
             last_sel = [i for i, r in enumerate(rows) if r[0] == Ld_last]
-            rp, rk, rb, rc, row_video, lay, vid, last_sel_d = hostio.pack_to_device(
-                [r_p, r_k, r_base, r_cap, [r[1] for r in rows], [r[0] for r in rows], [r[1] for r in rows],
-                 last_sel], dev)
+            # the row bookkeeping depends on the batch's event counts only: one host->device copy per batch
+            # (cached on dt, so a captured step graph re-uses device tensors and copies nothing)
+            key = ("_caption_rows", Ld, N, Q, tuple(ix.block for ix in layer_indices))
+            if key not in dt:
+                dt[key] = hostio.pack_to_device(
+                    [r_p, r_k, r_base, r_cap, [r[1] for r in rows], [r[0] for r in rows], [r[1] for r in rows],
+                     last_sel], dev)
+            rp, rk, rb, rc, row_video, lay, vid, last_sel_d = dt[key]
             flat_idx = rb + m.queries[rp, rk]
             cap_rows = rc + m.targets[rp, rk]
         else:

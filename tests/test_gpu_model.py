@@ -170,3 +170,40 @@ def test_graphed_trunk_matches_eager():
                 err = (g0[n] - g1[n]).abs().max().item()
                 assert err <= 1e-5 * (g0[n].abs().max().item() + 1e-6), f"{n}: {err}"
     assert list(model.state_dict().keys()) == [str(k) for k in d["state_keys"]]
+
+
+def test_step_graph_matches_eager():
+    """StepGraph (forward + losses + backward captured as one hipGraph, pdvc/step_graph.py) replays the eager
+    step: same total loss and gradients, over two replays, dropout off; a batch loaded into the captured
+    inputs is picked up by the next replay."""
+    from pdvc.step_graph import StepGraph
+    d = load("pdvc_small_anet")
+    model, criterion = build_filled(d)
+    model.train()
+    dt = fixture_dt(d)
+    dt["video_length"] = dt["video_length"].contiguous()
+    wd = criterion.weight_dict
+
+    def eager():
+        model.zero_grad(set_to_none=True)
+        out, loss = model(dt, criterion, "queries")
+        total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
+        total.backward()
+        return total.item(), {n: (p.grad.clone() if p.grad is not None else None) for n, p in model.named_parameters()}
+
+    t0, g0 = eager()
+    sg = StepGraph(model, criterion, dt)
+    for _ in range(2):
+        t1 = sg.replay().item()
+        assert abs(t1 - t0) <= 1e-5 * max(1.0, abs(t0)), (t1, t0)
+        for n, p in model.named_parameters():
+            assert (g0[n] is None) == (p.grad is None), n
+            if p.grad is not None:
+                err = (g0[n] - p.grad).abs().max().item()
+                assert err <= 1e-5 * (g0[n].abs().max().item() + 1e-6), f"{n}: {err}"
+    # a new batch of the same shapes: the replay follows the loaded inputs
+    dt2 = dict(dt)
+    dt2["video_tensor"] = dt["video_tensor"] * 0.5
+    sg.load({"video_tensor": dt2["video_tensor"]})
+    t2 = sg.replay().item()
+    assert abs(t2 - t0) > 1e-6, "replay ignored the loaded batch"
