@@ -35,7 +35,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--videos-per-gpu", type=int, default=32)
+    p.add_argument("--videos-per-gpu", type=int, default=256)
     p.add_argument("--T", type=int, default=512)
     p.add_argument("--C", type=int, default=768)
     p.add_argument("--Q", type=int, default=100)
@@ -128,7 +128,8 @@ def main():
         broadcast_parameters(model)
     params = [p for p in model.parameters() if p.requires_grad]
     reducer = GradAllReducer(params) if world > 1 else None
-    opt = torch.optim.AdamW(params, lr=args.lr, weight_decay=args.weight_decay)
+    # the reference's AdamW (train.py) as torch's fused single-kernel implementation (same update rule)
+    opt = torch.optim.AdamW(params, lr=args.lr, weight_decay=args.weight_decay, fused=True)
     B = a.videos_per_gpu
     vocab = args.vocab_size + 1
     dt = to_device(collate(synthetic_videos(B, a.T, a.C, a.events, a.words, vocab, seed=1000 + rank)), device)
@@ -213,6 +214,7 @@ def main():
                                f"L=4 Q={a.Q} 2 enc/2 dec layers, E={a.events} events x {a.words} words, "
                                f"vocab {vocab}, dropout on",
                    "videos_per_gpu": B, "global_batch": B * world, "seq_len": a.T, "gemm": _lin.BACKEND,
+                   "peak_hbm_gb": round(torch.cuda.max_memory_reserved(device) / 2 ** 30, 1),
                    "graph": {"step": "fwd+loss+bwd as one hipGraph", "trunk": "trunk hipGraph",
                              "none": "eager"}[a.graph],
                    "parallelism": f"dp{world}"},

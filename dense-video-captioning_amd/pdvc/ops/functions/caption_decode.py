@@ -18,7 +18,7 @@ from torch.autograd import Function
 from torch.autograd.function import once_differentiable
 
 from pdvc import _native as _n
-from .linear import wgrad_mm
+from .linear import colsum, wgrad_mm
 from .ms_deform_attn_func import NUM_SAMPLES, _levels
 
 
@@ -136,11 +136,11 @@ class CaptionDecodeFunction(Function):
             dW_h = wgrad_mm(dHP[1:].reshape(-1, Ph), HS[:, :-1].transpose(0, 1).reshape(-1, H))
         else:
             dW_h = torch.zeros_like(W_h)
-        db_h = dHP.sum((0, 1))
+        db_h = colsum(dHP.view(-1, Ph))
         dA2 = dATT.view(-1, A)
         dW_ctx = wgrad_mm(dA2, CLIP.view(-1, D))
-        db_ctx = dA2.sum(0)
-        dalpha_w = GAW.sum((0, 1))
+        db_ctx = colsum(dA2)
+        dalpha_w = colsum(GAW.view(-1, A))
         dalpha_b = GAB.sum().reshape(1)
         dW_att = wgrad_mm(d_gates.reshape(-1, G), RES.view(-1, M * D))
         return (gv, d_xg, d_off_hs, gr, dW_h, db_h, dW_ctx, db_ctx, dalpha_w, dalpha_b, dW_att, None, None, None,

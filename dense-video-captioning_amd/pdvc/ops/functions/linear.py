@@ -105,6 +105,21 @@ def wgrad_splits(rows):
     return 1
 
 
+def colsum(x):
+    """x.sum(0) for a 2-D fp32 GPU tensor: pdvc_colsum_f32 (csrc/colsum.hip) when the rows are long and
+    16-byte aligned, else torch.  The bias gradient of every projection."""
+    rows, cols = x.shape
+    if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and cols % 4 == 0 and rows >= 512
+            and x.data_ptr() % 16 == 0):
+        return x.sum(0)
+    cblocks = (cols // 4 + 15) // 16
+    parts = max(1, min(64, (2 * CU) // cblocks, rows // 64))
+    ws = torch.empty(parts * cols, dtype=x.dtype, device=x.device)
+    out = torch.empty(cols, dtype=x.dtype, device=x.device)
+    _n.call("pdvc_colsum_f32", _n.ptr(x), rows, cols, parts, _n.ptr(ws), _n.ptr(out), _n.stream())
+    return out
+
+
 def wgrad_mm(gy, x):
     """gy^T x for row-major gy (rows, O) and x (rows, I): the weight-gradient product, split over K."""
     rows = gy.shape[0]
@@ -141,7 +156,7 @@ class TorchLinearFunction(Function):
         if ctx.needs_input_grad[1]:
             gw = wgrad_mm(gy2, x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = gy2.sum(0)
+            gb = colsum(gy2.contiguous())
         return gx, gw, gb, None
 
 

@@ -35,6 +35,7 @@
  *                                      (deformable_transformer.py:150-156, 253-271)
  *   pdvc_lsap_f32                   <- HungarianMatcher's scipy.optimize.linear_sum_assignment per video
  *                                      (pdvc/matcher.py:119-121), same algorithm and tie rule, on the GPU
+ *   pdvc_colsum_f32                 <- the bias gradients (sum over rows of dY) of those nn.Linear layers
  *   pdvc_gemm_f32                   <- the dense projections (nn.Linear forward/backward) of the layers
  *                                      above: MSDeformAttn value/offset/output projections
  *                                      (ms_deform_attn.py:79-126), the FFNs (deformable_transformer.py:150-156,
@@ -213,6 +214,11 @@ int pdvc_add_dropout_layernorm_backward_f32(const float* x, const float* s, cons
  * (row_ind, col_ind) of the (Q, sizes[p]) matrix; entries past sizes[p] are not written. */
 int pdvc_lsap_f32(const float* costs, int num_problems, int num_query, int max_targets, const int32_t* sizes_host,
                   const int32_t* sizes_dev, int64_t* query_out, int64_t* target_out, void* stream);
+
+/* ---- column sums (bias gradients) ---------------------------------------------------------------------
+ * out[c] = sum_r x[r*cols + c] for a row-major (rows, cols) fp32 matrix, cols % 4 == 0, 16-byte aligned;
+ * workspace: parts*cols floats (partial sums of `parts` row slabs, 1 <= parts).  Deterministic. */
+int pdvc_colsum_f32(const float* x, int rows, int cols, int parts, float* workspace, float* out, void* stream);
 
 /* ---- fp32 GEMM on the matrix cores ----------------------------------------------------------------
  * C[M,N] = op(A)[M,K] op(B)[K,N] (+ bias[N]) (ReLU).  op(A): trans_a 0 -> A[m*lda + k], 1 -> A[k*lda + m];

@@ -64,3 +64,15 @@ def test_linear_function_matches_nn_linear():
     for got, exp, name in ((xf.grad, x.grad, "dx"), (w.grad, lin.weight.grad, "dW"), (b.grad, lin.bias.grad, "db")):
         err = (got.double() - exp).abs().max().item()
         assert err <= 1e-5 * (exp.abs().max().item() + 1.0), f"{name}: {err}"
+
+
+@pytest.mark.parametrize("rows,cols", [(30720, 512), (3200, 512), (3200, 2576), (777, 260), (512, 4), (100000, 12)])
+def test_colsum_matches_torch(rows, cols):
+    """pdvc_colsum_f32 (the bias gradients) against a float64 column sum, ragged slabs and column tiles."""
+    from pdvc.ops.functions.linear import colsum
+    torch.manual_seed(rows + cols)
+    x = torch.randn(rows, cols, device=DEV)
+    got = colsum(x)
+    exp = x.double().sum(0)
+    err = (got.double() - exp).abs().max().item()
+    assert err <= 1e-5 * (x.abs().sum(0).max().item() + 1.0), err
