@@ -178,455 +178,134 @@ __global__ __launch_bounds__(256) void msda1d_fwd_kernel(
 }
 
 // -------------------------------------------------------------------------------------------------
-// Pyramid-tiled variants for the encoder's self-attention (Lq == S: query q is pyramid position q), D = 64.
-// A workgroup takes one (video, head) and one slice k of the normalised time axis, [k/K, (k+1)/K): the
-// queries of EVERY level inside it (about S/K of them).  Their samples fall in a narrow window of each
-// level (the reference +- the learned offsets), so the workgroup stages those windows of the head's value
-// rows in LDS once (coalesced 256-B rows, all loads in flight together) and gathers the 32 corner rows of
-// every query from LDS: each staged row is read ~20x from LDS instead of ~20x through L1/L2.  The windows
-// come from the actual samples (min/max of the used corner rows per level); a level whose window does not
-// fit is gathered from global memory, so results never depend on the locality assumption.  Parameter
-// phase and accumulation order are the untiled kernels' (16 lanes per query): both give the same bits.
+// Whole-pyramid forward for the encoder's self-attention (Lq ~ S queries per (video, head)), D = 64.
+// A 1024-thread workgroup takes one (video, head) and a block of up to 512 queries (16 lanes per query, 8
+// queries per lane group).  The head's value rows (256 B per position) are staged in LDS level by level --
+// level 0 (T_0 <= 512 rows, 128 KiB), then levels 1..3 together -- with coalesced float4 loads, and every
+// corner row is gathered from LDS.  The value slice is read from HBM once per query block (twice per head at
+// S = 960) instead of ~20 times through L1/L2: 0.79x the per-query kernel's time at 256 videos (tools/kbench.py).
+// Parameter phase, corner clamping and accumulation order are msda1d_fwd_kernel's at LPH = 16: the same bits.
+// (A backward-query twin, holding dOut slices for 4 queries per lane group, spilled and ran 2x slower than
+// msda1d_bwd_query_kernel; the backward keeps the per-query mapping.)
 // -------------------------------------------------------------------------------------------------
-constexpr int kTQ = 64;    // queries per slice (at most)
-constexpr int kWin = 128;  // staged value rows per slice (256 B each)
-constexpr int kIntMax = 0x7fffffff, kIntMin = -0x7fffffff - 1;
+constexpr int kPyrThreads = 1024;
+constexpr int kPyrQPS = 8;                                  // queries per 16-lane group
+constexpr int kPyrQ = (kPyrThreads / 16) * kPyrQPS;        // 512 queries per workgroup
+constexpr int kPyrRows = 512;                               // LDS rows (256 B each): 128 KiB
+constexpr size_t kPyrLds = (size_t)kPyrRows * 64 * sizeof(float);
 
-// pyramid slice k of K: level l contributes positions [k*T_l/K, (k+1)*T_l/K).  `first[l]` is the pyramid
-// index of the level's first query in the slice and `end[l]` the slice-local index one past its last.
-struct Slice {
-    int first[kL], end[kL];
-};
-__device__ __forceinline__ Slice make_slice(int k, int K, const Levels1d& lv) {
-    Slice s;
-    int acc = 0;
-#pragma unroll
-    for (int l = 0; l < kL; ++l) {
-        const int b0 = (k * lv.T[l]) / K, n = ((k + 1) * lv.T[l]) / K - b0;
-        s.first[l] = lv.start[l] + b0 - acc;  // pyramid index = first[l] + slice-local index
-        acc += n;
-        s.end[l] = acc;
-    }
-    return s;
-}
-// the ql-th query of the slice (valid = false past its last; the index is then 0, always in range)
-__device__ __forceinline__ int slice_query(const Slice& s, int ql, bool& valid) {
-    valid = ql < s.end[kL - 1];
-    int f = s.first[3];
-    f = ql < s.end[2] ? s.first[2] : f;
-    f = ql < s.end[1] ? s.first[1] : f;
-    f = ql < s.end[0] ? s.first[0] : f;
-    return valid ? f + ql : 0;
-}
-
-struct Window {
-    int lo[kL], n[kL], base[kL], used;
-};
-
-// per-level windows from the min/max of the used corner rows, greedily in level order within kWin rows
-__device__ __forceinline__ Window make_window(const int* s_lo, const int* s_hi) {
-    Window w;
-    w.used = 0;
-#pragma unroll
-    for (int l = 0; l < kL; ++l) {
-        const int lo = __builtin_amdgcn_readfirstlane(s_lo[l]), hi = __builtin_amdgcn_readfirstlane(s_hi[l]);
-        const int n = hi >= lo ? hi - lo + 1 : 0;
-        const bool fit = n > 0 && w.used + n <= kWin;
-        w.lo[l] = fit ? lo : 0;
-        w.n[l] = fit ? n : 0;
-        w.base[l] = w.used;
-        w.used += fit ? n : 0;
-    }
-    return w;
-}
-
-// stage the window rows of one head (vsrc = value + b*S*MD + m*D) in LDS: 16 float4 per row
-__device__ __forceinline__ void stage_window(float4* __restrict__ win, const float* __restrict__ vsrc, size_t MD,
-                                             const Window& w, const Levels1d& lv) {
-    const int total = w.used * 16;
+// stage rows [r0, r0 + n) of one head (vsrc = value + b*S*MD + m*64) into LDS rows [dst, dst + n)
+__device__ __forceinline__ void pyr_stage(float4* __restrict__ lds, const float* __restrict__ vsrc, size_t MD, int r0,
+                                          int n, int dst) {
     const float4* src = reinterpret_cast<const float4*>(vsrc);
     const size_t rs = MD / 4;
-    for (int i0 = threadIdx.x; i0 < total; i0 += 4 * 256) {
-        float4 t[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = i0 + u * 256;
-            if (i < total) {
-                const int r = i >> 4, c = i & 15;
-                int g = 0;
-#pragma unroll
-                for (int l = 0; l < kL; ++l)
-                    if (r >= w.base[l] && r < w.base[l] + w.n[l]) g = lv.start[l] + w.lo[l] + (r - w.base[l]);
-                t[u] = src[(size_t)g * rs + c];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = i0 + u * 256;
-            if (i < total) win[i] = t[u];
-        }
-    }
+    const int total = n * 16;
+#pragma unroll 4
+    for (int i = threadIdx.x; i < total; i += kPyrThreads) lds[(size_t)(dst + (i >> 4)) * 16 + (i & 15)] =
+        src[(size_t)(r0 + (i >> 4)) * rs + (i & 15)];
 }
 
-// one corner row (level-relative row r; -1 = unused corner -> zeros) of this lane's 4 channels c*4..c*4+3
-// from global memory: the path of a level whose corners are not all in the window
-__device__ __forceinline__ void fetch_row(VecF<4>& v, int r, const float* __restrict__ vsrc, size_t MD, int st,
-                                         int c) {
-    VecF<4> t;
-    t.load(vsrc + (size_t)(st + max(r, 0)) * MD + c * 4);
-    const bool use = r >= 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v.v[i] = use ? t.v[i] : 0.f;
-}
-
-// a corner row is servable from the window (or unused)
-__device__ __forceinline__ bool in_window(int r, int l, const Window& w) {
-    return (r < 0) | ((unsigned)(r - w.lo[l]) < (unsigned)w.n[l]);
-}
-
-// fetch_row when the whole wave's corners of this level are in the window: no branches, so a level's 8
-// ds_read_b128 issue back to back (the index is clamped into the array; unused corners read as zeros)
-__device__ __forceinline__ void lds_row(VecF<4>& v, int r, int l, const Window& w, const float4* __restrict__ win,
-                                       int c) {
-    const int i = min(max(w.base[l] + r - w.lo[l], 0), kWin - 1);
-    const float4 t = win[i * 16 + c];
-    const bool use = r >= 0;
-    v.v[0] = use ? t.x : 0.f;
-    v.v[1] = use ? t.y : 0.f;
-    v.v[2] = use ? t.z : 0.f;
-    v.v[3] = use ? t.w : 0.f;
-}
-
-// fold a lane's min/max of used rows (level l = bits 2,3 of its lane) into the workgroup's per-level bounds
-__device__ __forceinline__ void track_rows(int l, int lo, int hi, int* s_lo, int* s_hi) {
-#pragma unroll
-    for (int d = 1; d <= 32; d <<= 1) {
-        if (d == 4 || d == 8) continue;
-        lo = min(lo, __shfl_xor(lo, d, PDVC_WAVE));
-        hi = max(hi, __shfl_xor(hi, d, PDVC_WAVE));
-    }
-    if ((threadIdx.x & 0x33) == 0 && hi >= lo) {
-        atomicMin(&s_lo[l], lo);
-        atomicMax(&s_hi[l], hi);
-    }
-}
-
-// slice id -> (video, head, slice); the K slices of a (video, head) run on one XCD
-struct SliceId {
-    int b, m, k;
-};
-__device__ __forceinline__ SliceId slice_id(int M, int K) {
-    const int t = xcd_remap(blockIdx.x, gridDim.x);
-    SliceId s;
-    s.k = t % K;
-    const int bm = t / K;
-    s.b = bm / M;
-    s.m = bm - s.b * M;
-    return s;
+// LDS row base of level l: level 0 alone, then levels 1..3 packed
+__device__ __forceinline__ int pyr_base(const Levels1d& lv, int l) {
+    return l <= 1 ? 0 : (l == 2 ? lv.T[1] : lv.T[1] + lv.T[2]);
 }
 
 template <int RD>
-__global__ __launch_bounds__(256) void msda1d_fwd_tiled_kernel(
+__global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
-    int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int S, int M, int K,
-    float* __restrict__ out, float* __restrict__ save_attn, float* __restrict__ save_loc) {
-    constexpr int D = 64;
-    __shared__ __attribute__((aligned(16))) float4 win[kWin * 16];  // 32 KiB of value rows
-    __shared__ int2 s_row[kTQ * kNS];                                 // corner rows (-1 = unused)
-    __shared__ float2 s_w[kTQ * kNS];                                 // corner weights
-    __shared__ int s_lo[kL], s_hi[kL];
-    const SliceId id = slice_id(M, K);
-    const int b = id.b, m = id.m;
-    const Slice sl = make_slice(id.k, K, lv);
-    const size_t MD = (size_t)M * D;
+    int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
+    int qblocks, float* __restrict__ out, float* __restrict__ save_attn, float* __restrict__ save_loc) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds4[];
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);  // the query blocks and heads of a video share an XCD
+    const int qb = blk % qblocks, bm = blk / qblocks;
+    const int b = bm / M, m = bm - b * M;
+    const int slot = threadIdx.x >> 4, sub = threadIdx.x & 15, lane = threadIdx.x & 63, gbase = lane - sub;
+    const size_t MD = (size_t)M * 64;
     const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
-    if (threadIdx.x < kL) {
-        s_lo[threadIdx.x] = kIntMax;
-        s_hi[threadIdx.x] = kIntMin;
-    }
-    __syncthreads();
+    const float* vsrc = value + (size_t)b * S * MD + (size_t)m * 64;
 
-    // 1) parameters (ms_deform_attn.py:168-177) -- msda1d_fwd_kernel's arithmetic, 16 lanes per query
-    {
-        const int j = threadIdx.x & 15, l = j >> 2;
-        const int T = lvl_sel(lv.T, l), st = lvl_sel(lv.start, l);
-        const float Tf = (float)T;
-        int lo = kIntMax, hi = kIntMin;
-#pragma unroll 1
-        for (int pass = 0; pass < kTQ / 16; ++pass) {
-            const int ql = pass * 16 + (threadIdx.x >> 4);
-            bool valid;
-            const int q = slice_query(sl, ql, valid);  // uniform over the 16-lane group
-            const size_t row = (size_t)b * S + q;
-            const float* prow = proj + row * proj_stride;
-            // a slot past the slice's queries reads query 0's row (always in range) and stores nothing
-            const float lg = prow[logit_base + m * kNS + j];
-            const float mx = group_max<16>(lg);
-            const float sum = group_allreduce<16>(expf(lg - mx));
-            const float aw = expf(lg - mx) / sum;
-            const float off = prow[off_base + m * kNS + j];
-            const float r0 = ref[(row * kL + l) * RD];
-            const float r1 = (RD == 2) ? ref[(row * kL + l) * RD + 1] : 0.f;
-            const float loc = (RD == 1) ? r0 + off / Tf : r0 + ((off / (float)kP) * r1) * 0.5f;
-            if (save_loc && valid) {
-                const size_t si = (row * M + m) * kNS + j;
-                save_loc[si] = loc;
-                save_attn[si] = aw;
-            }
-            const float x = loc * Tf - 0.5f;
-            const bool inside = x > -1.f && x < Tf;
-            const float xf = floorf(inside ? x : 0.f);
-            const int i0 = (int)xf;
-            const float lw = inside ? x - xf : 0.f;
-            bool ok1 = valid && inside && i0 >= 0, ok2 = valid && inside && i0 + 1 <= T - 1;
-            if (mbase) {
-                ok1 = ok1 && !mbase[st + min(max(i0, 0), T - 1)];
-                ok2 = ok2 && !mbase[st + min(max(i0 + 1, 0), T - 1)];
-            }
-            s_row[ql * kNS + j] = make_int2(ok1 ? i0 : -1, ok2 ? i0 + 1 : -1);
-            s_w[ql * kNS + j] = make_float2(ok1 ? (1.f - lw) * aw : 0.f, ok2 ? lw * aw : 0.f);
-            if (ok1) {
-                lo = min(lo, i0);
-                hi = max(hi, i0);
-            }
-            if (ok2) {
-                lo = min(lo, i0 + 1);
-                hi = max(hi, i0 + 1);
-            }
-        }
-        track_rows(l, lo, hi, s_lo, s_hi);
-    }
-    __syncthreads();
-
-    // 2) stage the per-level windows of this head's value rows
-    const Window w = make_window(s_lo, s_hi);
-    const float* vsrc = value + (size_t)b * S * MD + (size_t)m * D;
-    stage_window(win, vsrc, MD, w, lv);
-    __syncthreads();
-
-    // 3) gather: a wave = 4 queries x 16 lanes of 4 channels
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15;
-#pragma unroll 1
-    for (int pass = 0; pass < kTQ / 16; ++pass) {
-        const int ql = pass * 16 + wid * 4 + (lane >> 4);
-        bool valid;
-        const int q = slice_query(sl, ql, valid);
-        VecF<4> acc;
-        acc.zero();
+    // parameters of this lane's sample j = sub for its 8 queries (msda1d_fwd_kernel's arithmetic)
+    const int l_own = sub >> 2;
+    const int T_own = lvl_sel(lv.T, l_own), st_own = lvl_sel(lv.start, l_own);
+    const float Tf_own = (float)T_own;
+    int i0v[kPyrQPS];
+    float w1v[kPyrQPS], w2v[kPyrQPS];
 #pragma unroll
-        for (int l = 0; l < kL; ++l) {
-            const int st = lv.start[l];
+    for (int i = 0; i < kPyrQPS; ++i) {
+        const int q = qb * kPyrQ + slot + 64 * i;
+        const bool act = q < Lq;
+        const size_t row = (size_t)b * Lq + (act ? q : 0);
+        const float* prow = proj + row * proj_stride;
+        const float lg = prow[logit_base + m * kNS + sub];
+        const float mx = group_max<16>(lg);
+        const float sum = group_allreduce<16>(expf(lg - mx));
+        const float aw = expf(lg - mx) / sum;
+        const float off = prow[off_base + m * kNS + sub];
+        const float r0 = ref[(row * kL + l_own) * RD];
+        const float r1 = (RD == 2) ? ref[(row * kL + l_own) * RD + 1] : 0.f;
+        const float loc = (RD == 1) ? r0 + off / Tf_own : r0 + ((off / (float)kP) * r1) * 0.5f;
+        if (save_loc && act) {
+            const size_t si = (row * M + m) * kNS + sub;
+            save_loc[si] = loc;
+            save_attn[si] = aw;
+        }
+        const float x = loc * Tf_own - 0.5f;
+        const bool inside = x > -1.f && x < Tf_own;
+        const float xf = floorf(inside ? x : 0.f);
+        const int i0 = (int)xf;
+        const float lw = inside ? x - xf : 0.f;
+        bool ok1 = inside && i0 >= 0, ok2 = inside && i0 + 1 <= T_own - 1;
+        if (mbase) {
+            ok1 = ok1 && !mbase[st_own + min(max(i0, 0), T_own - 1)];
+            ok2 = ok2 && !mbase[st_own + min(max(i0 + 1, 0), T_own - 1)];
+        }
+        i0v[i] = i0;
+        w1v[i] = ok1 ? (1.f - lw) * aw : 0.f;
+        w2v[i] = ok2 ? lw * aw : 0.f;
+    }
+
+    VecF<4> acc[kPyrQPS];
+#pragma unroll
+    for (int i = 0; i < kPyrQPS; ++i) acc[i].zero();
+#pragma unroll 1
+    for (int l = 0; l < kL; ++l) {  // rolled: keeps each level's address math out of the others' registers
+        if (l == 0 || l == 1) {  // stage level 0, then levels 1..3 in one round trip
+            __syncthreads();
+            if (l == 0) {
+                pyr_stage(lds4, vsrc, MD, lv.start[0], lv.T[0], 0);
+            } else {
+                pyr_stage(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3], 0);
+            }
+            __syncthreads();
+        }
+        const int T = lvl_sel(lv.T, l), base = pyr_base(lv, l);
+#pragma unroll
+        for (int i = 0; i < kPyrQPS; ++i) {
             VecF<4> v1[kP], v2[kP];
             float c1[kP], c2[kP];
-            int r1[kP], r2[kP];
-            bool in = true;
 #pragma unroll
             for (int p = 0; p < kP; ++p) {
-                const int2 rr = s_row[ql * kNS + l * kP + p];
-                const float2 ww = s_w[ql * kNS + l * kP + p];
-                c1[p] = ww.x;
-                c2[p] = ww.y;
-                r1[p] = rr.x;
-                r2[p] = rr.y;
-                in = in & in_window(rr.x, l, w) & in_window(rr.y, l, w);
-            }
-            if (__all(in)) {
-#pragma unroll
-                for (int p = 0; p < kP; ++p) {
-                    lds_row(v1[p], r1[p], l, w, win, c);
-                    lds_row(v2[p], r2[p], l, w, win, c);
-                }
-            } else {
-#pragma unroll
-                for (int p = 0; p < kP; ++p) {
-                    fetch_row(v1[p], r1[p], vsrc, MD, st, c);
-                    fetch_row(v2[p], r2[p], vsrc, MD, st, c);
-                }
+                const int src = gbase + l * kP + p;
+                const int i0 = __shfl(i0v[i], src, PDVC_WAVE);
+                c1[p] = __shfl(w1v[i], src, PDVC_WAVE);
+                c2[p] = __shfl(w2v[i], src, PDVC_WAVE);
+                const int a1 = min(max(i0, 0), T - 1), a2 = min(max(i0 + 1, 0), T - 1);
+                const float4 t1 = lds4[(base + a1) * 16 + sub], t2 = lds4[(base + a2) * 16 + sub];
+                v1[p].v[0] = t1.x; v1[p].v[1] = t1.y; v1[p].v[2] = t1.z; v1[p].v[3] = t1.w;
+                v2[p].v[0] = t2.x; v2[p].v[1] = t2.y; v2[p].v[2] = t2.z; v2[p].v[3] = t2.w;
             }
 #pragma unroll
             for (int p = 0; p < kP; ++p) {
 #pragma unroll
-                for (int cc = 0; cc < 4; ++cc) acc.v[cc] += c1[p] * v1[p].v[cc] + c2[p] * v2[p].v[cc];
+                for (int c = 0; c < 4; ++c) acc[i].v[c] += c1[p] * v1[p].v[c] + c2[p] * v2[p].v[c];
             }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (valid) acc.store(out + ((size_t)b * S + q) * MD + (size_t)m * D + c * 4);
-    }
-}
-
-// the query-side backward's per-level epilogue at LPH = 16 (D = 64): reduce the 8 partials
-// (sum g*val, sum g*(v2-v1)) of the 4 points over the query's 16 lanes, then write the offset/logit grads
-// and accumulate grad_ref -- msda1d_bwd_query_kernel's code at its <4, 16> instantiation
-template <int RD>
-__device__ __forceinline__ void finish_level16(float (&part)[2 * kP], int lane, int sub, bool active, int l,
-                                               float Tf, float delta, size_t row, size_t sbase, int m, int off_base,
-                                               int logit_base, const float* __restrict__ save_attn,
-                                               const float* __restrict__ prow, float* __restrict__ gprow,
-                                               const float* __restrict__ ref, float* __restrict__ grad_ref) {
-    constexpr int G = 8;
-    group_reduce_scatter<2 * kP, G>(part, lane);
-    part[0] += __shfl_xor(part[0], 8, PDVC_WAVE);
-    const int r = sub % G;
-    const float other = __shfl_xor(part[0], 1, PDVC_WAVE);
-    const int p = r >> 1;
-    const float ga = (r & 1) ? other : part[0];
-    const float gs = (r & 1) ? part[0] : other;
-    const bool owner = active && sub < G && (r & 1) == 0;
-    const int j = l * kP + p;
-    const float a = save_attn[sbase + j];
-    const float gloc = owner ? Tf * (gs * a) : 0.f;
-    float g0 = gloc, g1 = 0.f;
-    if (owner) {
-        float goff;
-        if (RD == 1) {
-            goff = gloc / Tf;
-        } else {
-            const float rr1 = ref[(row * kL + l) * 2 + 1];
-            const float t2 = gloc * 0.5f;
-            goff = (t2 * rr1) / (float)kP;
-            g1 = t2 * (prow[off_base + m * kNS + j] / (float)kP);
-        }
-        gprow[off_base + m * kNS + j] = goff;
-        gprow[logit_base + m * kNS + j] = a * (ga - delta);
-    }
-    if (grad_ref) {
-        g0 = group_allreduce<16>(g0);
-        if (RD == 2) g1 = group_allreduce<16>(g1);
-        if (sub == 0 && active) {
-            float* dst = grad_ref + (row * kL + l) * RD;
-            atomicAdd(dst, g0);
-            if (RD == 2) atomicAdd(dst + 1, g1);
+            __builtin_amdgcn_sched_barrier(0);  // one query's 8 LDS reads in flight at a time: no spills
         }
     }
-}
-
-template <int RD>
-__global__ __launch_bounds__(256) void msda1d_bwd_query_tiled_kernel(
-    const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
-    int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int S, int M, int K,
-    const float* __restrict__ gout, const float* __restrict__ fout, const float* __restrict__ save_attn,
-    const float* __restrict__ save_loc, float* __restrict__ grad_proj, float* __restrict__ grad_ref) {
-    constexpr int D = 64;
-    __shared__ __attribute__((aligned(16))) float4 win[kWin * 16];
-    __shared__ int2 s_row[kTQ * kNS];
-    __shared__ float s_lw[kTQ * kNS];
-    __shared__ int s_lo[kL], s_hi[kL];
-    const SliceId id = slice_id(M, K);
-    const int b = id.b, m = id.m;
-    const Slice sl = make_slice(id.k, K, lv);
-    const size_t MD = (size_t)M * D;
-    const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
-    if (threadIdx.x < kL) {
-        s_lo[threadIdx.x] = kIntMax;
-        s_hi[threadIdx.x] = kIntMin;
-    }
-    __syncthreads();
-
-    // 1) corner rows and interpolation weights from the saved sampling locations
-    {
-        const int j = threadIdx.x & 15, l = j >> 2;
-        const int T = lvl_sel(lv.T, l), st = lvl_sel(lv.start, l);
-        const float Tf = (float)T;
-        int lo = kIntMax, hi = kIntMin;
-#pragma unroll 1
-        for (int pass = 0; pass < kTQ / 16; ++pass) {
-            const int ql = pass * 16 + (threadIdx.x >> 4);
-            bool valid;
-            const int q = slice_query(sl, ql, valid);
-            const size_t row = (size_t)b * S + q;
-            const float x = save_loc[(row * M + m) * kNS + j] * Tf - 0.5f;
-            const bool inside = valid && x > -1.f && x < Tf;
-            const float xf = floorf(inside ? x : 0.f);
-            const int i0 = (int)xf;
-            bool ok1 = inside && i0 >= 0, ok2 = inside && i0 + 1 <= T - 1;
-            if (mbase) {
-                ok1 = ok1 && !mbase[st + min(max(i0, 0), T - 1)];
-                ok2 = ok2 && !mbase[st + min(max(i0 + 1, 0), T - 1)];
-            }
-            s_row[ql * kNS + j] = make_int2(ok1 ? i0 : -1, ok2 ? i0 + 1 : -1);
-            s_lw[ql * kNS + j] = inside ? x - xf : 0.f;
-            if (ok1) {
-                lo = min(lo, i0);
-                hi = max(hi, i0);
-            }
-            if (ok2) {
-                lo = min(lo, i0 + 1);
-                hi = max(hi, i0 + 1);
-            }
-        }
-        track_rows(l, lo, hi, s_lo, s_hi);
-    }
-    __syncthreads();
-    const Window w = make_window(s_lo, s_hi);
-    const float* vsrc = value + (size_t)b * S * MD + (size_t)m * D;
-    stage_window(win, vsrc, MD, w, lv);
-    __syncthreads();
-
-    // 2) per query: delta = <dOut, out>, then per level the 8 partial sums and the epilogue
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = lane & 15, c0 = sub * 4;
-#pragma unroll 1
-    for (int pass = 0; pass < kTQ / 16; ++pass) {
-        const int ql = pass * 16 + wid * 4 + (lane >> 4);
-        bool valid;
-        const int q = slice_query(sl, ql, valid);
-        const size_t row = (size_t)b * S + q;
-        VecF<4> g, o;
-        g.load(gout + row * MD + (size_t)m * D + c0);
-        o.load(fout + row * MD + (size_t)m * D + c0);
-        float dl = 0.f;
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) dl += g.v[cc] * o.v[cc];
-        const float delta = group_allreduce<16>(dl);
-        const size_t sbase = (row * M + m) * kNS;
-        const float* prow = proj + row * proj_stride;
-        float* gprow = grad_proj + row * proj_stride;
-#pragma unroll
-        for (int l = 0; l < kL; ++l) {
-            const int st = lv.start[l];
-            const float Tf = (float)lv.T[l];
-            VecF<4> v1[kP], v2[kP];
-            float lw[kP];
-            int r1[kP], r2[kP];
-            bool in = true;
-#pragma unroll
-            for (int p = 0; p < kP; ++p) {
-                const int2 rr = s_row[ql * kNS + l * kP + p];
-                lw[p] = s_lw[ql * kNS + l * kP + p];
-                r1[p] = rr.x;
-                r2[p] = rr.y;
-                in = in & in_window(rr.x, l, w) & in_window(rr.y, l, w);
-            }
-            if (__all(in)) {
-#pragma unroll
-                for (int p = 0; p < kP; ++p) {
-                    lds_row(v1[p], r1[p], l, w, win, sub);
-                    lds_row(v2[p], r2[p], l, w, win, sub);
-                }
-            } else {
-#pragma unroll
-                for (int p = 0; p < kP; ++p) {
-                    fetch_row(v1[p], r1[p], vsrc, MD, st, sub);
-                    fetch_row(v2[p], r2[p], vsrc, MD, st, sub);
-                }
-            }
-            float part[2 * kP];
-#pragma unroll
-            for (int p = 0; p < kP; ++p) {
-                const float hw = 1.f - lw[p];
-                float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-                for (int cc = 0; cc < 4; ++cc) {
-                    const float x1 = v1[p].v[cc], x2 = v2[p].v[cc];
-                    s1 += g.v[cc] * (hw * x1 + lw[p] * x2);
-                    s2 += g.v[cc] * (x2 - x1);
-                }
-                part[2 * p] = s1;
-                part[2 * p + 1] = s2;
-            }
-            finish_level16<RD>(part, lane, sub, valid, l, Tf, delta, row, sbase, m, off_base, logit_base, save_attn,
-                               prow, gprow, ref, grad_ref);
-            __builtin_amdgcn_sched_barrier(0);
-        }
+    for (int i = 0; i < kPyrQPS; ++i) {
+        const int q = qb * kPyrQ + slot + 64 * i;
+        if (q < Lq) acc[i].store(out + ((size_t)b * Lq + q) * MD + (size_t)m * 64 + sub * 4);
     }
 }
 
@@ -981,20 +660,31 @@ static int pick_geometry(int M, int D, Geometry& g) {
     return PDVC_OK;
 }
 
-// Pyramid slices for the tiled kernels, or 0 when they do not apply: self-attention over the pyramid
-// (Lq == S), D = 64.  K is the smallest count (from S/60 up) whose slices hold at most kTQ queries.
-// Opt-in (PDVC_MSDA_TILED=1) until they beat the per-query kernels on the bench shape (A/B diagnostics).
-static int pick_slices(const Levels1d& lv, int S, int num_query, int head_dim) {
+// Query blocks for the whole-pyramid kernels, or 0 when they do not apply: D = 64, enough queries per
+// (video, head) to amortise staging the head's value rows (4 * Lq >= S: the encoder, Lq == S), level 0 and
+// levels 1..3 each within the 512-row LDS buffer.  PDVC_MSDA_PYR=0 in the environment turns them off (A/B).
+static int pick_pyr(const Levels1d& lv, int S, int num_query, int head_dim, int per_block) {
     static const int enabled = [] {
-        const char* e = getenv("PDVC_MSDA_TILED");
-        return (e && e[0] == '1') ? 1 : 0;
+        const char* e = getenv("PDVC_MSDA_PYR");
+        return (e && e[0] == '0') ? 0 : 1;
     }();
-    if (!enabled || num_query != S || head_dim != 64 || S <= 0) return 0;
-    for (int K = S / 60 > 1 ? S / 60 : 1;; ++K) {
-        int most = 0;
-        for (int l = 0; l < kL; ++l) most += (lv.T[l] + K - 1) / K;
-        if (most <= kTQ) return K;
+    if (!enabled || head_dim != 64 || num_query <= 0 || 4L * num_query < S) return 0;
+    if (lv.T[0] > kPyrRows || lv.T[1] + lv.T[2] + lv.T[3] > kPyrRows) return 0;
+    return (num_query + per_block - 1) / per_block;
+}
+
+static int pyr_attrs() {
+    static int rc = -1;
+    if (rc < 0) {
+        const void* ks[2] = {(const void*)msda1d_fwd_pyr_kernel<1>, (const void*)msda1d_fwd_pyr_kernel<2>};
+        rc = PDVC_OK;
+        for (const void* k : ks)
+            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPyrLds) != hipSuccess) {
+                (void)hipGetLastError();
+                rc = pdvc_set_error(PDVC_ERR_LAUNCH, "msda1d pyramid kernels: cannot raise the LDS limit");
+            }
     }
+    return rc;
 }
 
 }  // namespace pdvc
@@ -1049,16 +739,19 @@ extern "C" int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_
     PDVC_CHECK_ARG(tw < (1L << 31) / 4, "too many rows");
     dim3 grid((unsigned)((tw + 3) / 4));
     hipStream_t s = (hipStream_t)stream;
-    if (const int K = pick_slices(lv, S, num_query, head_dim)) {
-        PDVC_CHECK_ARG((long)batch * num_heads * K < (1L << 31), "too many slices");
-        dim3 tg((unsigned)(batch * num_heads * K));
+    if (const int qb = pick_pyr(lv, S, num_query, head_dim, kPyrQ)) {
+        if ((rc = pyr_attrs())) return rc;
+        PDVC_CHECK_ARG((long)batch * num_heads * qb < (1L << 31), "too many query blocks");
+        dim3 pg((unsigned)(batch * num_heads * qb));
         if (ref_dim == 1)
-            hipLaunchKernelGGL((msda1d_fwd_tiled_kernel<1>), tg, dim3(256), 0, s, value, value_pad_mask, proj,
-                               proj_stride, off_base, logit_base, ref, lv, S, num_heads, K, output, save_attn, save_loc);
+            hipLaunchKernelGGL((msda1d_fwd_pyr_kernel<1>), pg, dim3(kPyrThreads), kPyrLds, s, value, value_pad_mask,
+                               proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, qb, output,
+                               save_attn, save_loc);
         else
-            hipLaunchKernelGGL((msda1d_fwd_tiled_kernel<2>), tg, dim3(256), 0, s, value, value_pad_mask, proj,
-                               proj_stride, off_base, logit_base, ref, lv, S, num_heads, K, output, save_attn, save_loc);
-        PDVC_CHECK_LAUNCH("msda1d_fwd_tiled_kernel");
+            hipLaunchKernelGGL((msda1d_fwd_pyr_kernel<2>), pg, dim3(kPyrThreads), kPyrLds, s, value, value_pad_mask,
+                               proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, qb, output,
+                               save_attn, save_loc);
+        PDVC_CHECK_LAUNCH("msda1d_fwd_pyr_kernel");
         return PDVC_OK;
     }
     if (ref_dim == 1)
@@ -1096,20 +789,7 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
         hipError_t e = hipMemsetAsync(grad_ref, 0, sizeof(float) * rows * kL * ref_dim, s);
         if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_ref: %s", hipGetErrorString(e));
     }
-    const int K = pick_slices(lv, S, num_query, head_dim);
-    if (tw > 0 && K > 0) {
-        PDVC_CHECK_ARG((long)batch * num_heads * K < (1L << 31), "too many slices");
-        dim3 tg((unsigned)(batch * num_heads * K));
-        if (ref_dim == 1)
-            hipLaunchKernelGGL((msda1d_bwd_query_tiled_kernel<1>), tg, dim3(256), 0, s, value, value_pad_mask, proj,
-                               proj_stride, off_base, logit_base, ref, lv, S, num_heads, K, grad_output, output,
-                               save_attn, save_loc, grad_proj, grad_ref);
-        else
-            hipLaunchKernelGGL((msda1d_bwd_query_tiled_kernel<2>), tg, dim3(256), 0, s, value, value_pad_mask, proj,
-                               proj_stride, off_base, logit_base, ref, lv, S, num_heads, K, grad_output, output,
-                               save_attn, save_loc, grad_proj, grad_ref);
-        PDVC_CHECK_LAUNCH("msda1d_bwd_query_tiled_kernel");
-    } else if (tw > 0) {
+    if (tw > 0) {
         dim3 grid((unsigned)((tw + 3) / 4));
         if (ref_dim == 1)
             launch_bwdq1d<1>(g, grid, s, value, value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv,

@@ -263,10 +263,10 @@ def test_fused_msda1d_pdvc_shape_vs_oracle():
 @pytest.mark.parametrize("ref_dim", [1, 2])
 @pytest.mark.parametrize("masked", [False, True])
 @pytest.mark.parametrize("offset_scale", [2.0, 60.0])
-def test_fused_msda1d_pyramid_tiled_vs_oracle(ref_dim, masked, offset_scale):
-    """Self-attention over the pyramid (Lq == S, D = 64) takes the LDS-windowed kernels (pick_slices in
-    msda1d.hip).  offset_scale 60 scatters samples over whole levels, so windows overflow the LDS budget and
-    levels fall back to global gathers: results must not depend on the windowing."""
+def test_fused_msda1d_pyramid_vs_oracle(ref_dim, masked, offset_scale):
+    """Self-attention over the pyramid (Lq == S, D = 64) takes the whole-pyramid forward (pick_pyr in
+    msda1d.hip: the head's value rows staged in LDS); offset_scale 60 scatters samples over whole levels and
+    past both ends (clamped corners, zero padding)."""
     from pdvc.ops.functions import MSDA1dFunction
     rng = np.random.RandomState(7 + ref_dim + 10 * masked + int(offset_scale))
     T_l = [96, 48, 24, 12]
@@ -300,9 +300,9 @@ def test_fused_msda1d_pyramid_tiled_vs_oracle(ref_dim, masked, offset_scale):
     close(r.grad, egr, 1e-4, "grad_ref")
 
 
-def test_fused_msda1d_tiled_equals_untiled():
-    """The tiled and the per-query kernels share their arithmetic (the untiled path runs on the same queries
-    minus the last, so Lq != S): equal up to FMA contraction."""
+def test_fused_msda1d_pyramid_equals_per_query():
+    """The whole-pyramid and the per-query forward share their arithmetic (4 * Lq < S sends a query subset to
+    the per-query kernel): equal up to FMA contraction."""
     from pdvc.ops.functions import MSDA1dFunction
     rng = np.random.RandomState(3)
     T_l = [64, 32, 16, 8]
@@ -311,10 +311,11 @@ def test_fused_msda1d_tiled_equals_untiled():
     value = cu(rng.randn(N, S, M, D), torch.float32)
     proj = cu(np.concatenate([rng.randn(N, S, M * 16) * 2, rng.randn(N, S, M * 16)], -1), torch.float32)
     ref = cu(rng.uniform(0, 1, size=(N, S, 4, 1)), torch.float32)
-    full = MSDA1dFunction.apply(value, None, proj, ref, tuple(T_l), 0, M * 16)  # tiled (Lq == S)
-    part = MSDA1dFunction.apply(value, None, proj[:, :S - 1].contiguous(), ref[:, :S - 1].contiguous(), tuple(T_l),
-                                0, M * 16)  # untiled
-    err = (full[:, :S - 1] - part).abs().max().item()
+    full = MSDA1dFunction.apply(value, None, proj, ref, tuple(T_l), 0, M * 16)  # whole-pyramid (Lq == S)
+    nq = S // 4 - 1
+    part = MSDA1dFunction.apply(value, None, proj[:, :nq].contiguous(), ref[:, :nq].contiguous(), tuple(T_l),
+                                0, M * 16)  # per-query (4 * Lq < S)
+    err = (full[:, :nq] - part).abs().max().item()
     assert err <= 1e-6 * (part.abs().max().item() + 1.0), err
 
 

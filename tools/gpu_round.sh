@@ -2,7 +2,7 @@
 # One GPU-box pass over the steps named on the command line, each under its own time limit; the script
 # stops at the first failure.  Usage (repo root, GPU box):
 #     bash tools/gpu_round.sh TAG [kbench] [tests] [bench] [gemm] [prof] [pmc]
-#   kbench  MSDA kernel timings, pyramid-tiled kernels on (PDVC_MSDA_TILED=1) and default
+#   kbench  MSDA kernel timings, per-query kernels (PDVC_MSDA_PYR=0) and default (whole-pyramid)
 #   tests   pytest -m gpu + smoke()
 #   bench   bench.py (the JSON line)
 #   gemm    bench.py --gemm hip + tools/gemmbench.py
@@ -20,11 +20,11 @@ has() { [[ "$STEPS" == *" $1 "* ]]; }
 
 if has kbench; then
   echo "[$(date +%T)] kbench"
-  PDVC_MSDA_TILED=1 timeout -k 10 300 python -u tools/kbench.py > "$OUT/kbench_tiled.txt" 2>&1 \
-      || { echo "kbench failed"; tail -30 "$OUT/kbench_tiled.txt"; exit 1; }
+  PDVC_MSDA_PYR=0 timeout -k 10 300 python -u tools/kbench.py > "$OUT/kbench_perquery.txt" 2>&1 \
+      || { echo "kbench failed"; tail -30 "$OUT/kbench_perquery.txt"; exit 1; }
   timeout -k 10 300 python -u tools/kbench.py > "$OUT/kbench.txt" 2>&1 \
       || { echo "kbench failed"; tail -30 "$OUT/kbench.txt"; exit 1; }
-  echo "tiled:"; grep -v amdgpu.ids "$OUT/kbench_tiled.txt"
+  echo "per-query kernels:"; grep -v amdgpu.ids "$OUT/kbench_perquery.txt"
   echo "default:"; grep -v amdgpu.ids "$OUT/kbench.txt"
 fi
 if has tests; then
@@ -32,11 +32,11 @@ if has tests; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
       > "$OUT/pytest_gpu.log" 2>&1
   rc=$?
-  if [ $rc -eq 0 ]; then  # the opt-in pyramid-tiled MSDA kernels against the oracle too
-    PDVC_MSDA_TILED=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -m gpu -x -q --timeout 120 \
-        --timeout-method thread -k msda1d > "$OUT/pytest_gpu_tiled.log" 2>&1
+  if [ $rc -eq 0 ]; then  # the per-query MSDA kernels (whole-pyramid ones off) against the oracle too
+    PDVC_MSDA_PYR=0 timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -m gpu -x -q --timeout 120 \
+        --timeout-method thread -k msda1d > "$OUT/pytest_gpu_perquery.log" 2>&1
     rc=$?
-    tail -1 "$OUT/pytest_gpu_tiled.log"
+    tail -1 "$OUT/pytest_gpu_perquery.log"
   fi
   tail -3 "$OUT/pytest_gpu.log"
   if [ $rc -ne 0 ]; then echo "pytest failed rc=$rc"; grep -E "FAILED|Error" "$OUT/pytest_gpu.log" | head -30; exit $rc; fi
