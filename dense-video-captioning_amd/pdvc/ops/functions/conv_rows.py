@@ -1,0 +1,123 @@
+"""The base encoder's Conv1d + GroupNorm pyramid (reference: pdvc/base_encoder.py:23-86) on channels-last rows
+(N, T, C), the layout the deformable transformer consumes -- no transposes on either side.
+
+  * kernel-1 conv = a Linear over rows (ops/functions/linear.py: hipBLASLt, split-K weight gradient);
+  * kernel-3 / stride-2 / pad-1 conv: with T = 2L, the rows (x[2t], x[2t+1]) of a video are one contiguous
+    2C-wide row of x.view(N*L, 2C), so y[t] = [x[2t] | x[2t+1]] [W1 | W2]^T + b + x[2t-1] W0^T is one GEMM plus
+    the W0 tap of the previous odd row, added shifted by one output row (zero at t = 0: the padding);
+  * GroupNorm(G, C) on rows: pdvc_groupnorm_rows_* (csrc/groupnorm.hip).
+Same parameters (nn.Conv1d / nn.GroupNorm), same math."""
+import torch
+import torch.nn.functional as F
+from torch.autograd import Function
+from torch.autograd.function import once_differentiable
+
+from pdvc import _native as _n
+from .linear import colsum, dense, wgrad_mm
+
+GN_ROWS = 64  # rows per stats chunk (csrc/groupnorm.hip kGnRows)
+
+
+class ConvS2RowsFunction(Function):
+    """Conv1d(C, O, kernel 3, stride 2, padding 1) on x (N, T, C) rows -> (N, ceil(T/2), O)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        N, T, C = x.shape
+        Tin = T
+        if T % 2:
+            x = F.pad(x, (0, 0, 0, 1))  # the extra zero row is the right padding of the last odd window
+            T += 1
+        L = T // 2
+        O = weight.shape[0]
+        x = x.contiguous()
+        X2 = x.view(N * L, 2 * C)
+        w12 = torch.cat([weight[:, :, 1], weight[:, :, 2]], 1)  # (O, 2C): taps on x[2t], x[2t+1]
+        w0 = weight[:, :, 0].contiguous()                       # (O, C): tap on x[2t-1]
+        y = torch.addmm(bias, X2, w12.t())
+        z = torch.mm(X2[:, C:], w0.t())                         # x[2t+1] W0^T feeds output row t+1
+        yv = y.view(N, L, O)
+        yv[:, 1:] += z.view(N, L, O)[:, :-1]
+        ctx.save_for_backward(X2, w12, w0)
+        ctx.shape = (N, T, C, L, O, Tin)
+        return yv
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy):
+        X2, w12, w0 = ctx.saved_tensors
+        N, T, C, L, O, Tin = ctx.shape
+        dy2 = dy.reshape(N * L, O).contiguous()
+        dz = torch.zeros_like(dy2).view(N, L, O)
+        dz[:, :-1] = dy2.view(N, L, O)[:, 1:]
+        dz2 = dz.view(N * L, O)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            dX2 = torch.mm(dy2, w12)
+            dX2[:, C:] += torch.mm(dz2, w0)
+            gx = dX2.view(N, T, C)[:, :Tin]
+        if ctx.needs_input_grad[1]:
+            g12 = wgrad_mm(dy2, X2)
+            g0 = wgrad_mm(dz2, X2[:, C:])
+            gw = torch.stack([g0, g12[:, :C], g12[:, C:]], 2)
+        if ctx.needs_input_grad[2]:
+            gb = colsum(dy2)
+        return gx, gw, gb
+
+
+class GroupNormRowsFunction(Function):
+    """nn.GroupNorm(G, C) of x (N, T, C) rows (statistics per video and group over T x C/G values)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, groups, eps):
+        x = x.contiguous()
+        N, T, C = x.shape
+        chunks = (T + GN_ROWS - 1) // GN_ROWS
+        kw = dict(dtype=x.dtype, device=x.device)
+        ws = torch.empty(N * chunks * groups * 3, **kw)
+        y = torch.empty_like(x)
+        mean = torch.empty(N * groups, **kw)
+        rstd = torch.empty(N * groups, **kw)
+        _n.call("pdvc_groupnorm_rows_forward_f32", _n.ptr(x), N, T, C, groups, float(eps), _n.ptr(weight),
+                _n.ptr(bias), _n.ptr(ws), _n.ptr(y), _n.ptr(mean), _n.ptr(rstd), _n.stream())
+        ctx.save_for_backward(x, weight, mean, rstd)
+        ctx.groups = groups
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy):
+        x, weight, mean, rstd = ctx.saved_tensors
+        dy = dy.contiguous()
+        N, T, C = x.shape
+        G = ctx.groups
+        chunks = (T + GN_ROWS - 1) // GN_ROWS
+        kw = dict(dtype=x.dtype, device=x.device)
+        gws = torch.empty(N * chunks * G * 2 + N * G * 2, **kw)
+        cpart = torch.empty(N * chunks, 2 * C, **kw)
+        dx = torch.empty_like(x)
+        _n.call("pdvc_groupnorm_rows_backward_f32", _n.ptr(x), _n.ptr(dy), _n.ptr(mean), _n.ptr(rstd), _n.ptr(weight),
+                N, T, C, G, _n.ptr(gws), _n.ptr(cpart), _n.ptr(dx), _n.stream())
+        gsum = colsum(cpart)
+        return dx, gsum[:C].contiguous(), gsum[C:].contiguous(), None, None
+
+
+def conv1d_rows(conv, x):
+    """nn.Conv1d (kernel 1, or kernel 3 / stride 2 / padding 1) applied to x (N, T, C) rows."""
+    k = conv.weight.shape[2]
+    if k == 1:
+        return dense(x, conv.weight[:, :, 0], conv.bias)
+    if not (k == 3 and conv.stride[0] == 2 and conv.padding[0] == 1 and conv.dilation[0] == 1 and conv.groups == 1):
+        raise NotImplementedError("conv1d_rows supports kernel 1, or kernel 3 with stride 2 / padding 1")
+    return ConvS2RowsFunction.apply(x, conv.weight, conv.bias)
+
+
+def group_norm_rows(gn, x):
+    """nn.GroupNorm applied to x (N, T, C) rows (falls back to torch off the GPU / for other group shapes)."""
+    C = x.shape[-1]
+    cpg = C // gn.num_groups
+    ok = (x.is_cuda and x.dtype == torch.float32 and gn.affine and C % 4 == 0 and 256 % (C // 4) == 0
+          and cpg % 4 == 0 and (cpg // 4) & (cpg // 4 - 1) == 0)
+    if not ok:
+        return F.group_norm(x.transpose(1, 2), gn.num_groups, gn.weight, gn.bias, gn.eps).transpose(1, 2)
+    return GroupNormRowsFunction.apply(x, gn.weight, gn.bias, gn.num_groups, gn.eps)

@@ -29,6 +29,10 @@ class PositionEmbeddingSine(nn.Module):
 
     def embed(self, mask, duration, dtype=torch.float32):
         """mask (N, L) True = padding; duration (N,) seconds -> pos (N, num_pos_feats + 256, L)."""
+        return self.embed_rows(mask, duration, dtype).permute(0, 2, 1)
+
+    def embed_rows(self, mask, duration, dtype=torch.float32):
+        """The same embedding, channels-last: (N, L, num_pos_feats + 256)."""
         not_mask = ~mask
         x_embed = not_mask.cumsum(1, dtype=torch.float32)
         if self.normalize:
@@ -40,7 +44,7 @@ class PositionEmbeddingSine(nn.Module):
         pos_x = torch.stack((pos_x[:, :, 0::2].sin(), pos_x[:, :, 1::2].cos()), dim=3).flatten(2)
         dur = self.duration_embedding(duration).reshape(-1, 1, self.max_duration).expand(
             pos_x.shape[0], pos_x.shape[1], self.max_duration)
-        return torch.cat((pos_x, dur), dim=2).permute(0, 2, 1).to(dtype)
+        return torch.cat((pos_x, dur), dim=2).to(dtype)
 
     def forward(self, tensor_list):
         """Reference calling convention: a NestedTensor-like object with .tensors, .mask, .duration."""

@@ -35,6 +35,8 @@
  *                                      (deformable_transformer.py:150-156, 253-271)
  *   pdvc_lsap_f32                   <- HungarianMatcher's scipy.optimize.linear_sum_assignment per video
  *                                      (pdvc/matcher.py:119-121), same algorithm and tie rule, on the GPU
+ *   pdvc_groupnorm_rows_*           <- nn.GroupNorm(32, d) of the base encoder's pyramid levels
+ *                                      (pdvc/base_encoder.py:32-41), on channels-last rows
  *   pdvc_colsum_f32                 <- the bias gradients (sum over rows of dY) of those nn.Linear layers
  *   pdvc_gemm_f32                   <- the dense projections (nn.Linear forward/backward) of the layers
  *                                      above: MSDeformAttn value/offset/output projections
@@ -214,6 +216,19 @@ int pdvc_add_dropout_layernorm_backward_f32(const float* x, const float* s, cons
  * (row_ind, col_ind) of the (Q, sizes[p]) matrix; entries past sizes[p] are not written. */
 int pdvc_lsap_f32(const float* costs, int num_problems, int num_query, int max_targets, const int32_t* sizes_host,
                   const int32_t* sizes_dev, int64_t* query_out, int64_t* target_out, void* stream);
+
+/* ---- GroupNorm on channels-last rows (the base encoder's nn.GroupNorm(G, C) after each Conv1d) -------------
+ * x, y, dy, dx (N, T, C) row-major; group g = channels [g*C/G, (g+1)*C/G) of every row of a video; mean, rstd
+ * (N, G) saved by the forward (biased variance, as torch).  C/G = 4 x a power of two, C/4 divides 256.
+ * chunks = ceil(T / 64).  Workspaces (floats): forward N*chunks*G*3; backward group_ws N*chunks*G*2 + N*G*2 and
+ * col_partials N*chunks*2*C, whose column sums (pdvc_colsum_f32 over N*chunks rows of 2*C) are
+ * [dgamma | dbeta]. */
+int pdvc_groupnorm_rows_forward_f32(const float* x, int N, int T, int C, int G, float eps, const float* gamma,
+                                    const float* beta, float* workspace, float* y, float* mean, float* rstd,
+                                    void* stream);
+int pdvc_groupnorm_rows_backward_f32(const float* x, const float* dy, const float* mean, const float* rstd,
+                                     const float* gamma, int N, int T, int C, int G, float* group_ws,
+                                     float* col_partials, float* dx, void* stream);
 
 /* ---- column sums (bias gradients) ---------------------------------------------------------------------
  * out[c] = sum_r x[r*cols + c] for a row-major (rows, cols) fp32 matrix, cols % 4 == 0, 16-byte aligned;
