@@ -99,7 +99,7 @@ def wgrad_splits(rows):
     """K-chunks for a weight gradient over `rows` rows: hipBLASLt runs dW = dy^T x (512 x 512 outputs, K = N*S
     = 30720) on 128 workgroups at ~70 TF/s; as a batched GEMM over 16 row chunks plus a sum it fills the
     chip at ~135 TF/s (tools/gemmbench.py on MI355X).  1 = a plain GEMM."""
-    for s in (16, 8, 4, 2):
+    for s in (64, 32, 16, 8, 4, 2):  # 245760 rows (256 videos): 64 chunks, 146 TF/s (tools/gemm_large.py)
         if rows % s == 0 and rows // s >= 1536:
             return s
     return 1
