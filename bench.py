@@ -43,6 +43,9 @@ def parse():
     p.add_argument("--words", type=int, default=13)
     p.add_argument("--cfg", default="cfgs/anet_tsp_pdvc.yml")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--dist-backend", default=None, help="torch.distributed backend (default: nccl = RCCL on GPUs)")
+    p.add_argument("--same-device", action="store_true",
+                   help="rehearsal on a 1-GPU box: every rank on cuda:0 (use with --dist-backend gloo)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     p.add_argument("--kernel-report", action="store_true", help="print per-kernel event timings to stderr")
     p.add_argument("--graph", choices=["step", "trunk", "none"], default="step",
@@ -115,10 +118,10 @@ def main():
     _lin = importlib.import_module("pdvc.ops.functions.linear")
     if a.gemm:
         _lin.BACKEND = a.gemm
-    rank, world, local = init_distributed()
+    rank, world, local = init_distributed(a.dist_backend)
     if world != a.gpus and rank == 0:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    device = torch.device(f"cuda:{local}")
+    device = torch.device("cuda:0" if a.same_device else f"cuda:{local}")
     torch.cuda.set_device(device)
     torch.manual_seed(0)
     np.random.seed(0)

@@ -19,7 +19,7 @@ from . import hostio
 from .ops.functions import add_dropout_layernorm
 
 from .box_ops import inverse_sigmoid
-from .ops.functions.linear import dense
+from .ops.functions.linear import add_row_bias, dense
 from .ops.modules import MSDeformAttn
 from .ops.modules.linear import Linear
 from .ops.functions.attention import query_self_attention
@@ -77,7 +77,7 @@ class DeformableTransformer(nn.Module):
         for lvl, (src, mask, pos) in enumerate(zip(srcs, masks, pos_embeds)):
             level_T.append(int(src.shape[2]))
             src_flatten.append(src.transpose(1, 2))
-            lvl_pos.append(pos.transpose(1, 2) + self.level_embed[lvl].view(1, 1, -1))
+            lvl_pos.append(add_row_bias(pos.transpose(1, 2), self.level_embed[lvl]))
             mask_flatten.append(mask)
         src_flatten = torch.cat(src_flatten, 1)
         mask_flatten = torch.cat(mask_flatten, 1)

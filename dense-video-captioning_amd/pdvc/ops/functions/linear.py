@@ -120,6 +120,26 @@ def colsum(x):
     return out
 
 
+class AddRowBias(Function):
+    """x + bias broadcast over the rows of x (..., C); the bias gradient is a column sum (colsum) instead of
+    torch's generic reduction over the broadcast dims (e.g. the transformer's level embedding added to each
+    level's positional rows, deformable_transformer.py:110 in the reference)."""
+
+    @staticmethod
+    def forward(ctx, x, bias):
+        ctx.C = bias.numel()
+        return x + bias.view(*([1] * (x.dim() - 1)), -1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        gb = colsum(dy.reshape(-1, ctx.C).contiguous()) if ctx.needs_input_grad[1] else None
+        return dy, gb
+
+
+def add_row_bias(x, bias):
+    return AddRowBias.apply(x, bias)
+
+
 def wgrad_mm(gy, x):
     """gy^T x for row-major gy (rows, O) and x (rows, I): the weight-gradient product, split over K."""
     rows = gy.shape[0]
