@@ -17,6 +17,8 @@
 // Dropout keeps a counter-hash mask of (seed, video, head, query, key) -- regenerated in the backward.
 #include "pdvc_common.h"
 
+#include <cstdlib>
+
 namespace pdvc {
 
 constexpr int kHD = 64;      // max head dim (PDVC: 512 / 8 = 64); lanes >= D idle in channel phases
@@ -273,6 +275,291 @@ __global__ __launch_bounds__(256) void mha_bwd_k_kernel(const float* __restrict_
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Matrix-core path (D == 64, Q <= 128: PDVC's decoder).  One 256-thread workgroup per (video, head) with the
+// queries padded to 128 (zero rows / masked keys): wave w owns query rows 32w..32w+31.  Scores, P.V, dP, dq, dk
+// and dv are 32x32 tiles of v_mfma_f32_32x32x2_f32 (exact fp32 products, fp32 accumulation).  Operand layout
+// of one MFMA step kk: lane l supplies A[l%32][2kk + l/32] and B[2kk + l/32][l%32]; accumulator register r of
+// lane l holds C[(r&3) + 8(r>>2) + 4(l/32)][l%32].  Rows of the C tile are spread over 32-lane halves, so a row
+// softmax is a 5-step butterfly inside each half.
+typedef float mha_f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kMQ = 128;   // padded queries / keys
+constexpr int kMLD = 65;   // LDS row stride of [row][channel] images (conflict-free column walks)
+
+__device__ __forceinline__ int crow(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
+
+__device__ __forceinline__ mha_f32x16 mfma32(float a, float b, mha_f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// rows [0, Q) of one head's 64 channels (row stride `ld` floats, x `mul`) -> LDS [128][stride]; rows >= Q zero
+__device__ __forceinline__ void mha_stage(const float* __restrict__ src, size_t ld, int Q, float mul, float* dst,
+                                          int stride, int tid) {
+    for (int i = tid; i < kMQ * 16; i += 256) {
+        const int r = i >> 4, c = (i & 15) * 4;
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r < Q) x = *reinterpret_cast<const float4*>(src + (size_t)r * ld + c);
+        float* d = dst + r * stride + c;
+        d[0] = x.x * mul;
+        d[1] = x.y * mul;
+        d[2] = x.z * mul;
+        d[3] = x.w * mul;
+    }
+}
+
+__global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(const float* __restrict__ qk, const float* __restrict__ v,
+                                                           const uint8_t* __restrict__ kpm, int Q, int M,
+                                                           float scaling, float p_drop, uint32_t thresh, uint64_t seed0,
+                                                           const uint64_t* __restrict__ seed_dev,
+                                                           float* __restrict__ out, float* __restrict__ lse) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int D = 64;
+    constexpr int kPLD = kMQ + 1;               // P tile row stride
+    float* Ks = smem;                           // [128][65]
+    float* Qs = Ks + kMQ * kMLD;                // [128][65] q * scaling
+    float* Vs = Qs + kMQ * kMLD;                // [128][64]
+    const int E = M * D;
+    const int nm = xcd_remap(blockIdx.x, gridDim.x);
+    const int n = nm / M, m = nm - n * M;
+    const uint64_t seed = load_seed(seed0, seed_dev);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, hi = lane >> 5;
+    const float* qbase = qk + (size_t)n * Q * 2 * E + m * D;
+    mha_stage(qbase + E, 2 * (size_t)E, Q, 1.f, Ks, kMLD, tid);
+    mha_stage(qbase, 2 * (size_t)E, Q, scaling, Qs, kMLD, tid);
+    mha_stage(v + (size_t)n * Q * E + m * D, (size_t)E, Q, 1.f, Vs, D, tid);
+    __syncthreads();
+    const int row0 = w * 32;
+    mha_f32x16 s[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) s[kb] = mha_f32x16{};
+    {
+        const float* qa = Qs + (row0 + l32) * kMLD + hi;
+        const float* kbp = Ks + l32 * kMLD + hi;
+#pragma unroll 8
+        for (int kk = 0; kk < D / 2; ++kk) {
+            const float a = qa[2 * kk];
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb) s[kb] = mfma32(a, kbp[kb * 32 * kMLD + 2 * kk], s[kb]);
+        }
+    }
+    bool kval[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+        const int k = kb * 32 + l32;
+        kval[kb] = k < Q && !(kpm && kpm[(size_t)n * Q + k]);
+    }
+    __syncthreads();  // every wave is done with Ks / Qs: the P tiles reuse that space
+    float* Pw = smem + w * 32 * kPLD;  // [32][129] this wave's P_d rows
+    const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int rl = crow(r, hi), q = row0 + rl;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) mx = fmaxf(mx, kval[kb] ? s[kb][r] : -INFINITY);
+#pragma unroll
+        for (int d = 16; d > 0; d >>= 1) mx = fmaxf(mx, __shfl_xor(mx, d, PDVC_WAVE));
+        float e[4], sum = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+            e[kb] = kval[kb] ? expf(s[kb][r] - mx) : 0.f;
+            sum += e[kb];
+        }
+#pragma unroll
+        for (int d = 16; d > 0; d >>= 1) sum += __shfl_xor(sum, d, PDVC_WAVE);
+        const float inv = 1.f / sum;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+            const int k = kb * 32 + l32;
+            float p = e[kb] * inv;
+            if (p_drop > 0.f && q < Q && k < Q)
+                p = keep_elem(seed, (uint32_t)nm, (uint32_t)q, (uint32_t)k, (uint32_t)Q, thresh) ? p * keep_scale : 0.f;
+            Pw[rl * kPLD + k] = p;
+        }
+        if (l32 == 0 && q < Q) lse[(size_t)nm * Q + q] = mx + logf(sum);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    mha_f32x16 o[2] = {mha_f32x16{}, mha_f32x16{}};
+    {
+        const float* pa = Pw + l32 * kPLD + hi;
+        const float* vb = Vs + hi * D + l32;
+#pragma unroll 8
+        for (int kk = 0; kk < kMQ / 2; ++kk) {
+            const float a = pa[2 * kk];
+            o[0] = mfma32(a, vb[2 * kk * D], o[0]);
+            o[1] = mfma32(a, vb[2 * kk * D + 32], o[1]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int q = row0 + crow(r, hi);
+        if (q < Q) {
+            float* orow = out + ((size_t)n * Q + q) * E + m * D + l32;
+            orow[0] = o[0][r];
+            orow[32] = o[1][r];
+        }
+    }
+}
+
+// Backward, one workgroup per (video, head).  Phase A (wave w = query rows 32w..): recompute P from the saved
+// log-sum-exp, dP_d = dO . V^T, dS = P (dP_d z - delta), dq = dS . K; P_d and dS go to the global workspace
+// (stays in L2: this workgroup reads it back).  Phase B (wave w = key rows 32w..): dk = dS^T . q_scaled,
+// dv = P_d^T . dO, A operands read from the workspace, B operands from the LDS images of phase A.
+__global__ __launch_bounds__(256) void mha_bwd_mfma_kernel(const float* __restrict__ qk, const float* __restrict__ v,
+                                                           const uint8_t* __restrict__ kpm,
+                                                           const float* __restrict__ out,
+                                                           const float* __restrict__ gout,
+                                                           const float* __restrict__ lse, int Q, int M, float scaling,
+                                                           float p_drop, uint32_t thresh, uint64_t seed0,
+                                                           const uint64_t* __restrict__ seed_dev,
+                                                           float* __restrict__ ws_p, float* __restrict__ ws_ds,
+                                                           float* __restrict__ dqk, float* __restrict__ dv) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int D = 64;
+    constexpr int kDLD = 33;
+    float* Ks = smem;                     // [128][65]
+    float* Vs = Ks + kMQ * kMLD;          // [128][65]
+    float* Qs = Vs + kMQ * kMLD;          // [128][65] q * scaling
+    float* Os = Qs + kMQ * kMLD;          // [128][65] dO
+    float* Ds = Os + kMQ * kMLD;          // [4][32][33] per-wave dS block
+    float* rowl = Ds + 4 * 32 * kDLD;     // [128] lse
+    float* rowd = rowl + kMQ;             // [128] delta = dO . O
+    const int E = M * D;
+    const int nm = xcd_remap(blockIdx.x, gridDim.x);
+    const int n = nm / M, m = nm - n * M;
+    const uint64_t seed = load_seed(seed0, seed_dev);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, hi = lane >> 5;
+    const float* qbase = qk + (size_t)n * Q * 2 * E + m * D;
+    const size_t hbase = (size_t)n * Q * E + m * D;
+    mha_stage(qbase + E, 2 * (size_t)E, Q, 1.f, Ks, kMLD, tid);
+    mha_stage(v + hbase, (size_t)E, Q, 1.f, Vs, kMLD, tid);
+    mha_stage(qbase, 2 * (size_t)E, Q, scaling, Qs, kMLD, tid);
+    mha_stage(gout + hbase, (size_t)E, Q, 1.f, Os, kMLD, tid);
+    if (tid < kMQ) {
+        float dl = 0.f, l = 0.f;
+        if (tid < Q) {
+            const float4* orow = reinterpret_cast<const float4*>(out + hbase + (size_t)tid * E);
+            const float4* grow = reinterpret_cast<const float4*>(gout + hbase + (size_t)tid * E);
+#pragma unroll 4
+            for (int c = 0; c < D / 4; ++c) {
+                const float4 a = orow[c], b = grow[c];
+                dl += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+            }
+            l = lse[(size_t)nm * Q + tid];
+        }
+        rowd[tid] = dl;
+        rowl[tid] = l;
+    }
+    __syncthreads();
+    const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    float* wsp = ws_p + (size_t)nm * Q * Q;
+    float* wsd = ws_ds + (size_t)nm * Q * Q;
+    const int row0 = w * 32;
+    float* Dw = Ds + w * 32 * kDLD;
+    mha_f32x16 dq[2] = {mha_f32x16{}, mha_f32x16{}};
+#pragma unroll 1
+    for (int kb = 0; kb < 4; ++kb) {
+        const int k = kb * 32 + l32;
+        const bool kv = k < Q && !(kpm && kpm[(size_t)n * Q + k]);
+        mha_f32x16 s = mha_f32x16{}, dp = mha_f32x16{};
+        {
+            const float* qa = Qs + (row0 + l32) * kMLD + hi;
+            const float* oa = Os + (row0 + l32) * kMLD + hi;
+            const float* kbp = Ks + k * kMLD + hi;
+            const float* vbp = Vs + k * kMLD + hi;
+#pragma unroll 8
+            for (int kk = 0; kk < D / 2; ++kk) {
+                s = mfma32(qa[2 * kk], kbp[2 * kk], s);
+                dp = mfma32(oa[2 * kk], vbp[2 * kk], dp);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int rl = crow(r, hi), q = row0 + rl;
+            float ds = 0.f;
+            if (q < Q) {
+                const float p = kv ? expf(s[r] - rowl[q]) : 0.f;
+                float z = 1.f;
+                if (p_drop > 0.f && k < Q)
+                    z = keep_elem(seed, (uint32_t)nm, (uint32_t)q, (uint32_t)k, (uint32_t)Q, thresh) ? keep_scale : 0.f;
+                ds = p * (dp[r] * z - rowd[q]);
+                if (k < Q) {
+                    wsp[(size_t)q * Q + k] = p * z;
+                    wsd[(size_t)q * Q + k] = ds;
+                }
+            }
+            Dw[rl * kDLD + l32] = ds;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        {
+            const float* da = Dw + l32 * kDLD + hi;
+            const float* kb0 = Ks + (kb * 32 + hi) * kMLD + l32;
+#pragma unroll 8
+            for (int kk = 0; kk < 16; ++kk) {
+                const float a = da[2 * kk];
+                dq[0] = mfma32(a, kb0[2 * kk * kMLD], dq[0]);
+                dq[1] = mfma32(a, kb0[2 * kk * kMLD + 32], dq[1]);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int q = row0 + crow(r, hi);
+        if (q < Q) {
+            float* drow = dqk + ((size_t)n * Q + q) * 2 * E + m * D + l32;
+            drow[0] = dq[0][r] * scaling;
+            drow[32] = dq[1][r] * scaling;
+        }
+    }
+    __syncthreads();  // the workspace rows of every wave are written (global writes visible to the workgroup)
+    // phase B: wave w owns keys key0..key0+31
+    const int key0 = w * 32, kl = key0 + l32;
+    mha_f32x16 gk[2] = {mha_f32x16{}, mha_f32x16{}}, gv[2] = {mha_f32x16{}, mha_f32x16{}};
+    if (key0 < Q) {
+        const int half = (Q + 1) >> 1;
+        const bool kin = kl < Q;
+        for (int kk0 = 0; kk0 < half; kk0 += 4) {  // q <= 2 * (half + 3) + 1 < 128: padded LDS rows are zero
+            float ad[4], ap[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int q = 2 * (kk0 + j) + hi;
+                const bool in = kin && q < Q;
+                ad[j] = in ? wsd[(size_t)q * Q + kl] : 0.f;
+                ap[j] = in ? wsp[(size_t)q * Q + kl] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int q = 2 * (kk0 + j) + hi;
+                const float* qb = Qs + q * kMLD + l32;
+                const float* ob = Os + q * kMLD + l32;
+                gk[0] = mfma32(ad[j], qb[0], gk[0]);
+                gk[1] = mfma32(ad[j], qb[32], gk[1]);
+                gv[0] = mfma32(ap[j], ob[0], gv[0]);
+                gv[1] = mfma32(ap[j], ob[32], gv[1]);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int k = key0 + crow(r, hi);
+        if (k < Q) {
+            float* krow = dqk + ((size_t)n * Q + k) * 2 * E + E + m * D + l32;
+            float* vrow = dv + ((size_t)n * Q + k) * E + m * D + l32;
+            krow[0] = gk[0][r];
+            krow[32] = gk[1][r];
+            vrow[0] = gv[0][r];
+            vrow[32] = gv[1][r];
+        }
+    }
+}
+
 static uint32_t drop_threshold(float p) {
     double t = (double)p * 16777216.0;
     if (t < 0) t = 0;
@@ -287,11 +574,23 @@ using namespace pdvc;
 static size_t fwd_lds(int Q, int D) { return sizeof(float) * ((size_t)Q * (D + 1) + (size_t)Q * D + 4 * Q + 4 * kHD); }
 static size_t bwdq_lds(int Q, int D) { return sizeof(float) * (2 * (size_t)Q * (D + 1) + 4 * Q + 8 * kHD); }
 static size_t bwdk_lds(int Q, int D) { return sizeof(float) * (2 * (size_t)kQB * Q + 2 * (size_t)kQS * D); }
+static constexpr size_t kFwdMfmaLds = sizeof(float) * (2 * kMQ * kMLD + kMQ * 64);
+static constexpr size_t kBwdMfmaLds = sizeof(float) * (4 * kMQ * kMLD + 4 * 32 * 33 + 2 * kMQ);
+static_assert(sizeof(float) * 4 * 32 * (kMQ + 1) <= sizeof(float) * 2 * kMQ * kMLD, "P tiles must fit in K/Q images");
+static_assert(kBwdMfmaLds <= 160 * 1024, "backward LDS budget");
+
+// matrix-core kernels for D == 64, Q <= 128 (PDVC_MHA_MFMA=0 selects the scalar kernels, for tests)
+static bool use_mfma(int Q, int D) {
+    if (D != 64 || Q > kMQ) return false;
+    const char* e = getenv("PDVC_MHA_MFMA");
+    return !(e && e[0] == '0');
+}
 
 static int mha_attrs() {
     static bool attr = false;
     if (!attr) {
-        const void* ks[3] = {(const void*)mha_fwd_kernel, (const void*)mha_bwd_q_kernel, (const void*)mha_bwd_k_kernel};
+        const void* ks[5] = {(const void*)mha_fwd_kernel, (const void*)mha_bwd_q_kernel, (const void*)mha_bwd_k_kernel,
+                             (const void*)mha_fwd_mfma_kernel, (const void*)mha_bwd_mfma_kernel};
         for (const void* k : ks)
             if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) {
                 (void)hipGetLastError();
@@ -316,6 +615,13 @@ extern "C" int pdvc_mha_forward_f32(const float* qk, const float* v, const uint8
     int rc = mha_attrs();
     if (rc) return rc;
     const float scaling = sqrtf(1.0f / (float)head_dim);
+    if (use_mfma(num_query, head_dim)) {
+        hipLaunchKernelGGL(mha_fwd_mfma_kernel, dim3((unsigned)((long)batch * num_heads)), dim3(256), kFwdMfmaLds,
+                           (hipStream_t)stream, qk, v, key_padding_mask, num_query, num_heads, scaling, dropout_p,
+                           drop_threshold(dropout_p), seed, seed_dev, out, lse);
+        PDVC_CHECK_LAUNCH("mha_fwd_mfma_kernel");
+        return PDVC_OK;
+    }
     hipLaunchKernelGGL(mha_fwd_kernel, dim3((unsigned)blocks), dim3(256), fwd_lds(num_query, head_dim),
                        (hipStream_t)stream, qk, v, key_padding_mask, num_query, num_heads, head_dim, scaling, dropout_p,
                        drop_threshold(dropout_p), seed, seed_dev, qchunks, out, lse);
@@ -341,6 +647,13 @@ extern "C" int pdvc_mha_backward_f32(const float* qk, const float* v, const uint
     float* ws_p = workspace;
     float* ws_ds = workspace + (size_t)nm * num_query * num_query;
     hipStream_t s = (hipStream_t)stream;
+    if (use_mfma(num_query, head_dim)) {
+        hipLaunchKernelGGL(mha_bwd_mfma_kernel, dim3((unsigned)nm), dim3(256), kBwdMfmaLds, s, qk, v,
+                           key_padding_mask, out, grad_out, lse, num_query, num_heads, scaling, dropout_p,
+                           drop_threshold(dropout_p), seed, seed_dev, ws_p, ws_ds, grad_qk, grad_v);
+        PDVC_CHECK_LAUNCH("mha_bwd_mfma_kernel");
+        return PDVC_OK;
+    }
     hipLaunchKernelGGL(mha_bwd_q_kernel, dim3((unsigned)(nm * chunks)), dim3(256), bwdq_lds(num_query, head_dim), s,
                        qk, v, key_padding_mask, out, grad_out, lse, num_query, num_heads, head_dim, scaling, dropout_p,
                        drop_threshold(dropout_p), seed, seed_dev, chunks, ws_p, ws_ds, grad_qk);

@@ -57,7 +57,7 @@ def torch_mha_core(qk, v, kpm, M):
     return (p @ vv).transpose(1, 2).reshape(N, Q, E), p
 
 
-@pytest.mark.parametrize("Q,masked", [(100, False), (100, True), (37, True), (300, False)])
+@pytest.mark.parametrize("Q,masked", [(100, False), (100, True), (37, True), (128, True), (129, False), (300, False)])
 def test_query_self_attention_vs_float64(Q, masked):
     from pdvc.ops.functions.attention import query_self_attention
     torch.manual_seed(Q)
@@ -110,6 +110,30 @@ def test_query_self_attention_dropout_consistent():
     close(out, ref, 1e-5, "out")
     close(a.grad, a64.grad, 1e-4, "grad_qk")
     close(b.grad, b64.grad, 1e-4, "grad_v")
+
+
+@pytest.mark.parametrize("Q,p", [(100, 0.1), (61, 0.0), (128, 0.3)])
+def test_query_self_attention_matrix_core_matches_scalar(Q, p, monkeypatch):
+    """The MFMA kernels (D = 64, Q <= 128) and the scalar kernels (PDVC_MHA_MFMA=0) draw the same dropout mask
+    from the same seed: outputs and gradients agree to fp32 rounding."""
+    from pdvc.ops.functions.attention import QuerySelfAttentionFunction
+    torch.manual_seed(Q)
+    N, M, E = 3, 8, 512
+    qk = torch.randn(N, Q, 2 * E, device=DEV)
+    v = torch.randn(N, Q, E, device=DEV)
+    kpm = torch.zeros(N, Q, dtype=torch.bool, device=DEV)
+    kpm[0, -7:] = True
+    kpm[2, 1:4] = True
+    g = torch.randn(N, Q, E, device=DEV)
+    res = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PDVC_MHA_MFMA", mode)
+        a, b = qk.clone().requires_grad_(), v.clone().requires_grad_()
+        out = QuerySelfAttentionFunction.apply(a, b, kpm, M, p, 77)
+        out.backward(g)
+        res.append((out.detach(), a.grad, b.grad))
+    for name, x, y in zip(("out", "grad_qk", "grad_v"), res[0], res[1]):
+        close(x, y, 2e-5, name)
 
 
 # ------------------------------------------------------------------------------------------------
