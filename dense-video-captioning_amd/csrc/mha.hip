@@ -3,17 +3,15 @@
 // Replaces the attention core of nn.MultiheadAttention as DeformableTransformerDecoderLayer uses it
 // (pdvc/deformable_transformer.py:231,256-258; torch's multi_head_attention_forward with need_weights):
 //   P = softmax(q * sqrt(1/D) . k^T  [+ -inf at padded keys]),  P_d = dropout(P),  O = P_d . v
-// The in/out projections stay GEMMs (hipBLASLt through torch).  PDVC's shape is tiny and latency-bound
-// (Q = 100..300 queries, D = 64, 8 heads per video), so a workgroup owns 16 queries of one (video, head): K and V
-// are staged in LDS (rows padded to D+1 floats: conflict-free when lanes walk keys), each wave takes whole
-// query rows, a lane owns one key for the scores (exact softmax over <= 5 keys per lane + wave reductions) and
-// one channel for P.V.  The dropout seed may come from device memory (seed_dev), so a captured hipGraph
-// replays with a fresh seed drawn by the graph itself.  No MFMA: the core is ~2.6 MFLOP per head at Q = 100.
+// The in/out projections stay GEMMs (hipBLASLt through torch).  PDVC's decoder (D = 64, Q = 100) takes the
+// matrix-core kernels below (mha_*_mfma_kernel: one workgroup per (video, head), 32x32 fp32 MFMA tiles, the
+// backward in one launch).  The scalar kernels serve any other shape (Q <= 300, D <= 64): a workgroup owns 16
+// queries of one (video, head), K and V staged in LDS (rows padded to D+1 floats), a lane owns one key for the
+// scores (exact softmax over <= 5 keys per lane + wave reductions) and one channel for P.V.  The dropout seed
+// may come from device memory (seed_dev), so a captured hipGraph replays with a fresh seed drawn by the graph.
 // Backward: phase A (query-major) recomputes P from the saved log-sum-exp, forms dS = P (dP - delta) with
-// delta = dO . O, writes dq, and stages P_d and dS rows in a global workspace; phase B (key-major, a second
-// launch) forms dK = dS^T q_scaled and dV = P_d^T dO with lanes over channels.  Every launch has one
-// workgroup per (video, head, chunk of 16 queries or keys): ~1800 workgroups at PDVC's batch instead of 256,
-// K/V (or dO/q) staged per workgroup from L2.
+// delta = dO . O, writes dq, and stages P_d and dS rows in a global workspace; phase B (key-major) forms
+// dK = dS^T q_scaled and dV = P_d^T dO.
 // Dropout keeps a counter-hash mask of (seed, video, head, query, key) -- regenerated in the backward.
 #include "pdvc_common.h"
 
