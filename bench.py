@@ -53,6 +53,8 @@ def parse():
                         "trunk: only the static-shape trunk graphed (base encoder .. heads); none: eager")
     p.add_argument("--gemm", choices=["hip", "torch"], default=None,
                    help="projection GEMMs on pdvc_gemm_f32 (hip) or torch/hipBLASLt (default: PDVC_GEMM or torch)")
+    p.add_argument("--gemm-table", choices=["auto", "off"], default="auto",
+                   help="auto: library GEMMs use the pre-tuned solution table (pdvc/gemm_tuning.py) when present")
     return p.parse_args()
 
 
@@ -123,6 +125,8 @@ def main():
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     device = torch.device("cuda:0" if a.same_device else f"cuda:{local}")
     torch.cuda.set_device(device)
+    from pdvc import gemm_tuning
+    tuned = a.gemm_table == "auto" and gemm_tuning.enable(tag=f"_r{rank}")
     torch.manual_seed(0)
     np.random.seed(0)
     args, model, criterion = build_model(a, device)
@@ -216,7 +220,8 @@ def main():
         "config": {"workload": f"anet_tsp_pdvc training step (fwd+loss+bwd+allreduce+AdamW): T={a.T} C={a.C} "
                                f"L=4 Q={a.Q} 2 enc/2 dec layers, E={a.events} events x {a.words} words, "
                                f"vocab {vocab}, dropout on",
-                   "videos_per_gpu": B, "global_batch": B * world, "seq_len": a.T, "gemm": _lin.BACKEND,
+                   "videos_per_gpu": B, "global_batch": B * world, "seq_len": a.T,
+                   "gemm": _lin.BACKEND + ("+tuned-table" if tuned else ""),
                    "peak_hbm_gb": round(torch.cuda.max_memory_reserved(device) / 2 ** 30, 1),
                    "graph": {"step": "fwd+loss+bwd as one hipGraph", "trunk": "trunk hipGraph",
                              "none": "eager"}[a.graph],

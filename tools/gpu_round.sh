@@ -66,7 +66,7 @@ if has prof; then
       -- python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err" \
       || { echo "rocprof failed"; tail -30 "$OUT/prof.err"; exit 1; }
   ks=$(find "$OUT/prof" -name "*kernel_stats.csv" | head -1)
-  if [ -n "$ks" ]; then python tools/profsum.py "$ks" 9 40 > "$OUT/prof_summary.txt"; cat "$OUT/prof_summary.txt"; fi
+  if [ -n "$ks" ]; then python tools/profsum.py "$ks" 0 45 > "$OUT/prof_summary.txt"; cat "$OUT/prof_summary.txt"; fi
 fi
 if has pmc; then
   for c in FETCH_SIZE WRITE_SIZE; do

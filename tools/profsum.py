@@ -1,4 +1,5 @@
-"""Summarise a rocprofv3 --stats kernel_stats.csv per training step:  python tools/profsum.py CSV STEPS [TOP]"""
+"""Summarise a rocprofv3 --stats kernel_stats.csv per training step:  python tools/profsum.py CSV STEPS [TOP]
+STEPS = 0 counts the steps from the matcher kernel (pdvc::lsap_kernel runs once per training step)."""
 import collections
 import csv
 import sys
@@ -8,6 +9,9 @@ def main():
     path, steps = sys.argv[1], float(sys.argv[2])
     top = int(sys.argv[3]) if len(sys.argv) > 3 else 25
     rows = list(csv.DictReader(open(path)))
+    if steps <= 0:
+        steps = float(sum(int(r["Calls"]) for r in rows if "lsap_kernel" in r["Name"]))
+        print(f"steps (lsap_kernel launches): {steps:.0f}")
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     n = sum(int(r["Calls"]) for r in rows)
     print(f"GPU time {tot / 1e6 / steps:.2f} ms/step, {n / steps:.0f} launches/step")
