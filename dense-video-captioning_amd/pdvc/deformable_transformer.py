@@ -23,6 +23,7 @@ from .ops.functions.linear import add_row_bias, dense
 from .ops.modules import MSDeformAttn
 from .ops.modules.linear import Linear
 from .ops.functions.attention import query_self_attention
+from .ops.functions.ffn import ffn_block, use_ffn_block
 
 
 class DeformableTransformer(nn.Module):
@@ -138,6 +139,9 @@ class DeformableTransformerEncoderLayer(nn.Module):
         return tensor if pos is None else tensor + pos
 
     def forward_ffn(self, src):
+        if self.activation is F.relu and use_ffn_block(src):
+            return ffn_block(src, self.linear1, self.linear2, self.norm2, self.dropout2.p, self.dropout3.p,
+                             self.training)
         if self.activation is F.relu:
             src2 = self.linear2(self.dropout2(self.linear1(src, relu=True)))
         else:
@@ -228,6 +232,9 @@ class DeformableTransformerDecoderLayer(nn.Module):
         return tensor if pos is None else tensor + pos
 
     def forward_ffn(self, tgt):
+        if self.activation is F.relu and use_ffn_block(tgt):
+            return ffn_block(tgt, self.linear1, self.linear2, self.norm3, self.dropout3.p, self.dropout4.p,
+                             self.training)
         if self.activation is F.relu:
             tgt2 = self.linear2(self.dropout3(self.linear1(tgt, relu=True)))
         else:

@@ -1,0 +1,106 @@
+"""The transformer feed-forward sub-layer as one autograd node:
+    out = norm(x + dropout_out(linear2(dropout_act(relu(linear1(x))))))
+(reference: DeformableTransformerEncoderLayer.forward_ffn, deformable_transformer.py:140-145; the decoder's
+forward_ffn, :233-237).  Same arithmetic as the module chain; what changes is where the passes over the
+(rows x d_ffn) and (rows x d) tensors go:
+  * relu + dropout is one in-place HIP pass (csrc/ffn.hip), its backward one pass that also sums linear1's
+    bias gradient (no byte mask: the forward output itself says where relu passed and dropout kept);
+  * the residual gradient from the layer norm and linear1's input gradient meet in the dgrad GEMM's epilogue
+    (dx = dx_residual + dh W1, beta = 1) instead of an autograd add;
+  * the residual epilogue is pdvc_add_dropout_layernorm (csrc/addnorm.hip).
+Both dropout masks are counter hashes of seeds drawn on the GPU (graph-safe), regenerated in the backward.
+"""
+import ctypes
+
+import torch
+import torch.nn.functional as F
+from torch.autograd import Function
+from torch.autograd.function import once_differentiable
+
+from pdvc import _native as _n
+from .addnorm import BWD_PARTS
+from . import linear as _lin
+from .linear import CU, colsum, wgrad_mm
+
+
+def _seed_ptrs(seeds):
+    """(act, out) device pointers of the two int64 seeds drawn by ffn_block, or (NULL, NULL)."""
+    if seeds is None:
+        return None, None
+    base = _n.ptr(seeds).value
+    return ctypes.c_void_p(base), ctypes.c_void_p(base + 8)
+
+
+def _parts(rows, cols):
+    cblocks = (cols // 4 + 15) // 16
+    return max(1, min(256, (8 * CU) // cblocks, rows // 64))
+
+
+class FFNBlockFunction(Function):
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, gamma, beta, p_act, p_out, eps, seeds):
+        shape = x.shape
+        d = shape[-1]
+        x2 = x.reshape(-1, d).contiguous()
+        rows = x2.shape[0]
+        seed_act, seed_out = _seed_ptrs(seeds)
+        h = torch.addmm(b1, x2, w1.t())
+        _n.call("pdvc_relu_dropout_forward_f32", _n.ptr(h), rows, h.shape[1], float(p_act), 0, seed_act, _n.stream())
+        y = torch.addmm(b2, h, w2.t())
+        out = torch.empty_like(x2)
+        mean = torch.empty(rows, dtype=x.dtype, device=x.device)
+        rstd = torch.empty_like(mean)
+        _n.call("pdvc_add_dropout_layernorm_forward_f32", _n.ptr(x2), _n.ptr(y), _n.ptr(gamma), _n.ptr(beta), rows,
+                d, float(p_out), 0, seed_out, float(eps), _n.ptr(out), _n.ptr(mean), _n.ptr(rstd), _n.stream())
+        ctx.save_for_backward(x2, h, y, w1, w2, gamma, mean, rstd, seeds)
+        ctx.meta = (shape, float(p_act), float(p_out))
+        return out.view(shape)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dout):
+        x2, h, y, w1, w2, gamma, mean, rstd, seeds = ctx.saved_tensors
+        shape, p_act, p_out = ctx.meta
+        rows, d = x2.shape
+        fdim = h.shape[1]
+        _, seed_out = _seed_ptrs(seeds)
+        dout2 = dout.reshape(-1, d).contiguous()
+        dx = torch.empty_like(x2)
+        dy = torch.empty_like(y)
+        dgamma = torch.empty_like(gamma)
+        dbeta = torch.empty_like(gamma)
+        ws = torch.empty(2 * BWD_PARTS * d, dtype=x2.dtype, device=x2.device)
+        _n.call("pdvc_add_dropout_layernorm_backward_f32", _n.ptr(x2), _n.ptr(y), _n.ptr(gamma), _n.ptr(mean),
+                _n.ptr(rstd), _n.ptr(dout2), rows, d, p_out, 0, seed_out, _n.ptr(dx), _n.ptr(dy), _n.ptr(dgamma),
+                _n.ptr(dbeta), _n.ptr(ws), _n.stream())
+        db2 = colsum(dy)
+        dw2 = wgrad_mm(dy, h)
+        dh = torch.mm(dy, w2)
+        parts = _parts(rows, fdim)
+        ws1 = torch.empty(parts * fdim, dtype=h.dtype, device=h.device)
+        db1 = torch.empty(fdim, dtype=h.dtype, device=h.device)
+        _n.call("pdvc_relu_dropout_backward_f32", _n.ptr(h), _n.ptr(dh), rows, fdim, p_act, parts, _n.ptr(ws1),
+                _n.ptr(db1), _n.stream())
+        dw1 = wgrad_mm(dh, x2)
+        dx.addmm_(dh, w1)  # residual gradient + linear1's input gradient in one GEMM (beta = 1)
+        return dx.view(shape), dw1, db1, dw2, db2, dgamma, dbeta, None, None, None, None
+
+
+def use_ffn_block(x):
+    """FFNBlockFunction serves fp32 GPU activations on the torch/hipBLASLt GEMM backend."""
+    return x.is_cuda and x.dtype == torch.float32 and _lin.BACKEND != "hip"
+
+
+def ffn_block(x, linear1, linear2, norm, p_act, p_out, training):
+    """norm(x + dropout(linear2(dropout(relu(linear1(x)))))) with nn.Linear-like linear1/linear2 and an
+    nn.LayerNorm norm.  GPU fp32: FFNBlockFunction; CPU (tests of host logic only): the module chain."""
+    if not x.is_cuda:
+        h = F.dropout(F.relu(F.linear(x, linear1.weight, linear1.bias)), p_act, training)
+        return norm(x + F.dropout(F.linear(h, linear2.weight, linear2.bias), p_out, training))
+    p_act = float(p_act) if training else 0.0
+    p_out = float(p_out) if training else 0.0
+    seeds = None
+    if p_act > 0 or p_out > 0:
+        seeds = torch.randint(0, 2 ** 62, (2,), device=x.device, dtype=torch.int64)
+    return FFNBlockFunction.apply(x, linear1.weight, linear1.bias, linear2.weight, linear2.bias, norm.weight,
+                                  norm.bias, p_act, p_out, norm.eps, seeds)

@@ -38,6 +38,8 @@
  *   pdvc_groupnorm_rows_*           <- nn.GroupNorm(32, d) of the base encoder's pyramid levels
  *                                      (pdvc/base_encoder.py:32-41), on channels-last rows
  *   pdvc_colsum_f32                 <- the bias gradients (sum over rows of dY) of those nn.Linear layers
+ *   pdvc_relu_dropout_*             <- dropout(relu(.)) between the two FFN linears of every transformer layer
+ *                                      (deformable_transformer.py:140-145 encoder, :233-237 decoder)
  *   pdvc_gemm_f32                   <- the dense projections (nn.Linear forward/backward) of the layers
  *                                      above: MSDeformAttn value/offset/output projections
  *                                      (ms_deform_attn.py:79-126), the FFNs (deformable_transformer.py:150-156,
@@ -234,6 +236,16 @@ int pdvc_groupnorm_rows_backward_f32(const float* x, const float* dy, const floa
  * out[c] = sum_r x[r*cols + c] for a row-major (rows, cols) fp32 matrix, cols % 4 == 0, 16-byte aligned;
  * workspace: parts*cols floats (partial sums of `parts` row slabs, 1 <= parts).  Deterministic. */
 int pdvc_colsum_f32(const float* x, int rows, int cols, int parts, float* workspace, float* out, void* stream);
+
+/* ---- FFN relu + dropout --------------------------------------------------------------------------------
+ * forward, in place on h (rows x cols, cols % 4 == 0, 16-byte aligned): h = relu(h) * keep / (1 - p), keep a
+ * counter hash of (seed | *seed_dev, row, col) with P(keep) = 1 - p.
+ * backward, in place on grad: grad = (hd > 0) ? grad / (1 - p) : 0 where hd is the forward's output; when
+ * dbias != NULL also dbias[c] = sum_r grad[r, c] (workspace: parts * cols floats, parts >= 1). */
+int pdvc_relu_dropout_forward_f32(float* h, long rows, int cols, float p, uint64_t seed, const uint64_t* seed_dev,
+                                  void* stream);
+int pdvc_relu_dropout_backward_f32(const float* hd, float* grad, int rows, int cols, float p, int parts,
+                                   float* workspace, float* dbias, void* stream);
 
 /* ---- fp32 GEMM on the matrix cores ----------------------------------------------------------------
  * C[M,N] = op(A)[M,K] op(B)[K,N] (+ bias[N]) (ReLU).  op(A): trans_a 0 -> A[m*lda + k], 1 -> A[k*lda + m];
