@@ -12,7 +12,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from .ops.functions.conv_rows import conv1d_rows, group_norm_rows
-from .position_encoding import PositionEmbeddingSine
+from .position_encoding import PositionEmbeddingSine, PyramidPosEmbed
 
 
 class BaseEncoder(nn.Module):
@@ -47,18 +47,17 @@ class BaseEncoder(nn.Module):
     def forward(self, vf, mask, duration):
         """vf (N, L, C); mask (N, L) True = padding; duration (N,).  Returns lists of (N, d, L_l), (N, L_l),
         (N, d, L_l) as the reference -- the (N, d, L_l) tensors are transposed VIEWS of channels-last
-        (N, L_l, d) storage, so the transformer's flattening (src.transpose(1, 2)) costs no copy."""
+        (N, L_l, d) storage, so the transformer's flattening (src.transpose(1, 2)) costs no copy; the position
+        embeddings come as a PyramidPosEmbed (indexable like the reference's list)."""
         x = vf.contiguous()
         rows = [self._proj(0, x)]
         masks = [mask]
-        poses = [self.pos_embed.embed_rows(mask, duration)]
         for lvl in range(1, self.num_feature_levels):
             src = self._proj(lvl, x if lvl == 1 else rows[-1])
             m = F.interpolate(mask[None].float(), size=src.shape[1:2]).to(torch.bool)[0]
             rows.append(src)
             masks.append(m)
-            poses.append(self.pos_embed.embed_rows(m, duration, dtype=src.dtype))
-        return [r.transpose(1, 2) for r in rows], masks, [p_.transpose(1, 2) for p_ in poses]
+        return [r.transpose(1, 2) for r in rows], masks, PyramidPosEmbed(self.pos_embed, masks, duration)
 
 
 def build_base_encoder(args):

@@ -24,6 +24,8 @@ from .ops.modules import MSDeformAttn
 from .ops.modules.linear import Linear
 from .ops.functions.attention import query_self_attention
 from .ops.functions.ffn import ffn_block, use_ffn_block
+from .ops.functions.posembed import level_pos_rows
+from .position_encoding import PyramidPosEmbed
 
 
 class DeformableTransformer(nn.Module):
@@ -75,14 +77,18 @@ class DeformableTransformer(nn.Module):
         reference's (L,) long tensor; the Python tuple is attached as `self.last_level_T`."""
         src_flatten, mask_flatten, lvl_pos = [], [], []
         level_T = []
-        for lvl, (src, mask, pos) in enumerate(zip(srcs, masks, pos_embeds)):
+        fused_pos = (isinstance(pos_embeds, PyramidPosEmbed) and srcs[0].is_cuda and srcs[0].dtype == torch.float32
+                     and self.level_embed.shape[0] == len(srcs))
+        for lvl, (src, mask) in enumerate(zip(srcs, masks)):
             level_T.append(int(src.shape[2]))
             src_flatten.append(src.transpose(1, 2))
-            lvl_pos.append(add_row_bias(pos.transpose(1, 2), self.level_embed[lvl]))
+            if not fused_pos:
+                lvl_pos.append(add_row_bias(pos_embeds[lvl].transpose(1, 2), self.level_embed[lvl]))
             mask_flatten.append(mask)
         src_flatten = torch.cat(src_flatten, 1)
         mask_flatten = torch.cat(mask_flatten, 1)
-        lvl_pos = torch.cat(lvl_pos, 1)
+        # all levels' sine + duration rows + level embeddings in one HIP pass (ops/functions/posembed.py)
+        lvl_pos = level_pos_rows(pos_embeds, self.level_embed) if fused_pos else torch.cat(lvl_pos, 1)
         temporal_shapes = hostio.const(("level_T", tuple(level_T)), lambda: torch.tensor(level_T, dtype=torch.long),
                                        src_flatten.device)
         level_start_index = torch.cat((temporal_shapes.new_zeros((1,)), temporal_shapes.cumsum(0)[:-1]))

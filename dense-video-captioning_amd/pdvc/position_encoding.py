@@ -31,15 +31,25 @@ class PositionEmbeddingSine(nn.Module):
         """mask (N, L) True = padding; duration (N,) seconds -> pos (N, num_pos_feats + 256, L)."""
         return self.embed_rows(mask, duration, dtype).permute(0, 2, 1)
 
-    def embed_rows(self, mask, duration, dtype=torch.float32):
-        """The same embedding, channels-last: (N, L, num_pos_feats + 256)."""
+    def positions(self, mask):
+        """Normalised cumulative positions of the valid frames (N, L): the sine features' argument before the
+        frequency division (position_encoding.py:53-58)."""
         not_mask = ~mask
         x_embed = not_mask.cumsum(1, dtype=torch.float32)
         if self.normalize:
             eps = 1e-6
             x_embed = (x_embed - 0.5) / (x_embed[:, -1:] + eps) * self.scale
-        dim_t = torch.arange(self.num_pos_feats, dtype=torch.float32, device=mask.device)
-        dim_t = self.temperature ** (2 * (dim_t // 2) / self.num_pos_feats)
+        return x_embed
+
+    def freqs(self, device):
+        """The frequency table dim_t (num_pos_feats,) of position_encoding.py:60-61."""
+        dim_t = torch.arange(self.num_pos_feats, dtype=torch.float32, device=device)
+        return self.temperature ** (2 * (dim_t // 2) / self.num_pos_feats)
+
+    def embed_rows(self, mask, duration, dtype=torch.float32):
+        """The same embedding, channels-last: (N, L, num_pos_feats + 256)."""
+        x_embed = self.positions(mask)
+        dim_t = self.freqs(mask.device)
         pos_x = x_embed[:, :, None] / dim_t
         pos_x = torch.stack((pos_x[:, :, 0::2].sin(), pos_x[:, :, 1::2].cos()), dim=3).flatten(2)
         dur = self.duration_embedding(duration).reshape(-1, 1, self.max_duration).expand(
@@ -49,6 +59,28 @@ class PositionEmbeddingSine(nn.Module):
     def forward(self, tensor_list):
         """Reference calling convention: a NestedTensor-like object with .tensors, .mask, .duration."""
         return self.embed(tensor_list.mask, tensor_list.duration)
+
+
+class PyramidPosEmbed:
+    """The pyramid's position embeddings as BaseEncoder hands them to the transformer: indexable like the
+    reference's list of (N, d, T_l) tensors (base_encoder.py:80-85; an element is materialised on access), while
+    DeformableTransformer.prepare_encoder_inputs builds all levels + level embeddings directly into the
+    flattened (N, S, d) rows in one HIP pass from these inputs (ops/functions/posembed.py)."""
+
+    def __init__(self, pe, masks, duration):
+        self.pe = pe
+        self.masks = list(masks)
+        self.duration = duration
+
+    def __len__(self):
+        return len(self.masks)
+
+    def __getitem__(self, i):
+        dt = self.duration.dtype if self.duration.is_floating_point() else torch.float32
+        return self.pe.embed_rows(self.masks[i], self.duration, dtype=dt).transpose(1, 2)
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
 
 
 def build_position_encoding(position_embedding, N_steps):

@@ -38,6 +38,9 @@
  *   pdvc_groupnorm_rows_*           <- nn.GroupNorm(32, d) of the base encoder's pyramid levels
  *                                      (pdvc/base_encoder.py:32-41), on channels-last rows
  *   pdvc_colsum_f32                 <- the bias gradients (sum over rows of dY) of those nn.Linear layers
+ *   pdvc_level_pos_rows_*           <- the encoder's positional input: PositionEmbeddingSine per level
+ *                                      (position_encoding.py:20-75) + level_embed + the concatenation over levels
+ *                                      (deformable_transformer.py:100-112)
  *   pdvc_relu_dropout_*             <- dropout(relu(.)) between the two FFN linears of every transformer layer
  *                                      (deformable_transformer.py:140-145 encoder, :233-237 decoder)
  *   pdvc_gemm_f32                   <- the dense projections (nn.Linear forward/backward) of the layers
@@ -236,6 +239,17 @@ int pdvc_groupnorm_rows_backward_f32(const float* x, const float* dy, const floa
  * out[c] = sum_r x[r*cols + c] for a row-major (rows, cols) fp32 matrix, cols % 4 == 0, 16-byte aligned;
  * workspace: parts*cols floats (partial sums of `parts` row slabs, 1 <= parts).  Deterministic. */
 int pdvc_colsum_f32(const float* x, int rows, int cols, int parts, float* workspace, float* out, void* stream);
+
+/* ---- encoder positional input ------------------------------------------------------------------------
+ * pos[n, s, c] = (c < F ? (c even ? sin : cos)(xe[n*S + s] / dim_t[c]) : dur[n*Dd + c - F])
+ *                + level_embed[l(s)*(F + Dd) + c],   l(s) the level of flattened row s (level_T: host array of
+ * num_levels <= 8 lengths summing to S); F % 4 == Dd % 4 == 0; pos, level_embed, dur 16-byte aligned.
+ * backward: partials[(n*num_levels + l)*C + c] = sum over the rows s of level l of dpos[n, s, c]. */
+int pdvc_level_pos_rows_forward_f32(const float* xe, const float* dim_t, const float* dur, const float* level_embed,
+                                    const int32_t* level_T, int num_levels, int N, int S, int F, int Dd, float* pos,
+                                    void* stream);
+int pdvc_level_pos_rows_backward_f32(const float* dpos, const int32_t* level_T, int num_levels, int N, int S, int C,
+                                     float* partials, void* stream);
 
 /* ---- FFN relu + dropout --------------------------------------------------------------------------------
  * forward, in place on h (rows x cols, cols % 4 == 0, 16-byte aligned): h = relu(h) * keep / (1 - p), keep a
