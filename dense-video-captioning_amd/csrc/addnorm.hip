@@ -113,17 +113,18 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_bwd_kernel(const float* __r
                                                                 const uint64_t* __restrict__ seed_dev,
                                                                 float* __restrict__ dx, float* __restrict__ ds,
                                                                 float* __restrict__ dgamma_part,
-                                                                float* __restrict__ dbeta_part) {
-    __shared__ float red[2][kANW][kAND];
+                                                                float* __restrict__ dbeta_part,
+                                                                float* __restrict__ dsum_part) {
+    __shared__ float red[3][kANW][kAND];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t seed = seed_dev ? *seed_dev : seed0;
     const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
     const float inv_d = 1.f / (float)d;
-    float pg[CH][4], pb[CH][4];
+    float pg[CH][4], pb[CH][4], pd[CH][4];  // column partials of dgamma, dbeta and (optionally) ds
 #pragma unroll
     for (int k = 0; k < CH; ++k)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) pg[k][e] = pb[k][e] = 0.f;
+        for (int e = 0; e < 4; ++e) pg[k][e] = pb[k][e] = pd[k][e] = 0.f;
     for (int row = blockIdx.x * kANW + wid; row < rows; row += gridDim.x * kANW) {
         const float mean = mean_in[row], rstd = rstd_in[row];
         float xh[CH][4], gg[CH][4];
@@ -170,6 +171,7 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_bwd_kernel(const float* __r
                 for (int e = 0; e < 4; ++e) {
                     o[e] = rstd * (gg[k][e] - m1 - xh[k][e] * m2);
                     q[e] = ((keep_bits[k] >> e) & 1u) ? o[e] * scale : 0.f;
+                    pd[k][e] += q[e];
                 }
                 *reinterpret_cast<float4*>(dx + (size_t)row * d + c) = make_float4(o[0], o[1], o[2], o[3]);
                 *reinterpret_cast<float4*>(ds + (size_t)row * d + c) = make_float4(q[0], q[1], q[2], q[3]);
@@ -185,44 +187,52 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_bwd_kernel(const float* __r
             if (c + e < kAND) {
                 red[0][wid][c + e] = pg[k][e];
                 red[1][wid][c + e] = pb[k][e];
+                red[2][wid][c + e] = pd[k][e];
             }
         }
     }
     __syncthreads();
     for (int c = threadIdx.x; c < d; c += blockDim.x) {
-        float a = 0.f, b = 0.f;
+        float a = 0.f, b = 0.f, e = 0.f;
 #pragma unroll
         for (int w = 0; w < kANW; ++w) {
             a += red[0][w][c];
             b += red[1][w][c];
+            e += red[2][w][c];
         }
         dgamma_part[(size_t)blockIdx.x * d + c] = a;
         dbeta_part[(size_t)blockIdx.x * d + c] = b;
+        if (dsum_part) dsum_part[(size_t)blockIdx.x * d + c] = e;
     }
 }
 
-// column sums of the (parts, d) partials -> dgamma, dbeta: a workgroup per 64 columns, its 4 waves take
-// every 4th partial row, summed in LDS in a fixed order (bitwise reproducible)
+// column sums of the (parts, d) partials -> dgamma, dbeta (and dsum when given): a workgroup per 64 columns,
+// its 4 waves take every 4th partial row, summed in LDS in a fixed order (bitwise reproducible)
 __global__ __launch_bounds__(256) void addnorm_colsum_kernel(const float* __restrict__ gpart,
-                                                             const float* __restrict__ bpart, int parts, int d,
-                                                             float* __restrict__ dgamma, float* __restrict__ dbeta) {
-    __shared__ float red[2][4][64];
+                                                             const float* __restrict__ bpart,
+                                                             const float* __restrict__ spart, int parts, int d,
+                                                             float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                             float* __restrict__ dsum) {
+    __shared__ float red[3][4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + lane;
-    float a = 0.f, b = 0.f;
+    float a = 0.f, b = 0.f, e = 0.f;
     if (c < d) {
 #pragma unroll 8
         for (int i = w; i < parts; i += 4) {
             a += gpart[(size_t)i * d + c];
             b += bpart[(size_t)i * d + c];
+            if (spart) e += spart[(size_t)i * d + c];
         }
     }
     red[0][w][lane] = a;
     red[1][w][lane] = b;
+    red[2][w][lane] = e;
     __syncthreads();
     if (w == 0 && c < d) {
         dgamma[c] = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
         dbeta[c] = red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
+        if (dsum) dsum[c] = red[2][0][lane] + red[2][1][lane] + red[2][2][lane] + red[2][3][lane];
     }
 }
 
@@ -271,29 +281,32 @@ extern "C" int pdvc_add_dropout_layernorm_backward_f32(const float* x, const flo
                                                        const float* mean, const float* rstd, const float* dy, int rows,
                                                        int d, float p, uint64_t seed, const uint64_t* seed_dev,
                                                        float* dx, float* ds, float* dgamma, float* dbeta,
-                                                       float* workspace, void* stream) {
+                                                       float* ds_colsum, float* workspace, void* stream) {
     AN_CHECK();
-    PDVC_CHECK_ARG(workspace != nullptr, "workspace (2 * 256 * d floats) is required");
+    PDVC_CHECK_ARG(workspace != nullptr, "workspace (3 * 256 * d floats) is required");
     hipStream_t st = (hipStream_t)stream;
     if (rows == 0) {
         hipError_t e1 = hipMemsetAsync(dgamma, 0, sizeof(float) * d, st);
         hipError_t e2 = hipMemsetAsync(dbeta, 0, sizeof(float) * d, st);
-        if (e1 != hipSuccess || e2 != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset failed");
+        hipError_t e3 = ds_colsum ? hipMemsetAsync(ds_colsum, 0, sizeof(float) * d, st) : hipSuccess;
+        if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess)
+            return pdvc_set_error(PDVC_ERR_LAUNCH, "memset failed");
         return PDVC_OK;
     }
     const int parts = an_grid(rows, kAnBwdBlocks);
     float* gpart = workspace;
     float* bpart = workspace + (size_t)parts * d;
+    float* spart = ds_colsum ? workspace + 2 * (size_t)parts * d : nullptr;
     const dim3 grid((unsigned)parts), block(kANW * 64);
     if (d <= 256)
         hipLaunchKernelGGL(addnorm_bwd_kernel<1>, grid, block, 0, st, x, s, gamma, mean, rstd, dy, rows, d, p,
-                           an_threshold(p), seed, seed_dev, dx, ds, gpart, bpart);
+                           an_threshold(p), seed, seed_dev, dx, ds, gpart, bpart, spart);
     else
         hipLaunchKernelGGL(addnorm_bwd_kernel<2>, grid, block, 0, st, x, s, gamma, mean, rstd, dy, rows, d, p,
-                           an_threshold(p), seed, seed_dev, dx, ds, gpart, bpart);
+                           an_threshold(p), seed, seed_dev, dx, ds, gpart, bpart, spart);
     PDVC_CHECK_LAUNCH("addnorm_bwd_kernel");
-    hipLaunchKernelGGL(addnorm_colsum_kernel, dim3((unsigned)((d + 63) / 64)), dim3(256), 0, st, gpart, bpart, parts,
-                       d, dgamma, dbeta);
+    hipLaunchKernelGGL(addnorm_colsum_kernel, dim3((unsigned)((d + 63) / 64)), dim3(256), 0, st, gpart, bpart, spart,
+                       parts, d, dgamma, dbeta, ds_colsum);
     PDVC_CHECK_LAUNCH("addnorm_colsum_kernel");
     return PDVC_OK;
 }

@@ -24,7 +24,8 @@ from .ops.modules import MSDeformAttn
 from .ops.modules.linear import Linear
 from .ops.functions.attention import query_self_attention
 from .ops.functions.ffn import ffn_block, use_ffn_block
-from .ops.functions.posembed import level_pos_rows
+from .ops.functions.attn_block import encoder_attn_block, use_attn_block
+from .ops.functions.posembed import level_pos_rows, level_pos_rows_split
 from .position_encoding import PyramidPosEmbed
 
 
@@ -87,8 +88,16 @@ class DeformableTransformer(nn.Module):
             mask_flatten.append(mask)
         src_flatten = torch.cat(src_flatten, 1)
         mask_flatten = torch.cat(mask_flatten, 1)
-        # all levels' sine + duration rows + level embeddings in one HIP pass (ops/functions/posembed.py)
-        lvl_pos = level_pos_rows(pos_embeds, self.level_embed) if fused_pos else torch.cat(lvl_pos, 1)
+        # all levels' sine + duration rows + level embeddings in one HIP pass (ops/functions/posembed.py); when every
+        # encoder layer runs the fused attention block, their position gradients come back as per-(video, level)
+        # sums through a small handle instead of a (N, S, d) gradient
+        if fused_pos and not self.no_encoder and all(layer.block_ok(src_flatten) for layer in self.encoder.layers):
+            lvl_pos, handle = level_pos_rows_split(pos_embeds, self.level_embed)
+            lvl_pos._pdvc_level_grad = handle
+        elif fused_pos:
+            lvl_pos = level_pos_rows(pos_embeds, self.level_embed)
+        else:
+            lvl_pos = torch.cat(lvl_pos, 1)
         temporal_shapes = hostio.const(("level_T", tuple(level_T)), lambda: torch.tensor(level_T, dtype=torch.long),
                                        src_flatten.device)
         level_start_index = torch.cat((temporal_shapes.new_zeros((1,)), temporal_shapes.cumsum(0)[:-1]))
@@ -154,7 +163,18 @@ class DeformableTransformerEncoderLayer(nn.Module):
             src2 = self.linear2(self.dropout2(self.activation(self.linear1(src))))
         return add_dropout_layernorm(src, src2, self.norm2, self.dropout3.p, self.training)
 
+    def block_ok(self, src):
+        return use_attn_block(src, self)
+
     def forward(self, src, pos, reference_points, temporal_shapes, level_start_index, padding_mask=None):
+        handle = getattr(pos, "_pdvc_level_grad", None)
+        if pos is not None and self.block_ok(src):
+            # the sub-layer as one autograd node: gradients of src meet in GEMM epilogues (ops/functions/attn_block.py)
+            src = encoder_attn_block(self, src, pos, handle, reference_points, _level_T(temporal_shapes),
+                                     padding_mask)
+            return self.forward_ffn(src)
+        if handle is not None:
+            raise RuntimeError("a level-position gradient handle needs the fused encoder attention block")
         src2 = self.self_attn(self.with_pos_embed(src, pos), reference_points, src, temporal_shapes,
                               level_start_index, padding_mask)
         src = add_dropout_layernorm(src, src2, self.norm1, self.dropout1.p, self.training)

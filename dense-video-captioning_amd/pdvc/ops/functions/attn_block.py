@@ -1,0 +1,115 @@
+"""The encoder's self-attention sub-layer as one autograd node:
+    out = norm(src + dropout(output_proj(MSDA(value_proj(src), proj(src + pos)))))
+(reference: DeformableTransformerEncoderLayer.forward, deformable_transformer.py:147-151, and MSDeformAttn.forward,
+ms_deform_attn.py:79-126).  Same kernels and GEMMs as the module chain; what the single node changes is where the
+gradients of src meet:
+  * src's three gradient paths (residual from the layer norm, value projection, query projection) accumulate in
+    the epilogues of the two input-gradient GEMMs (beta = 1) instead of two autograd adds over (N*S, d);
+  * output_proj's bias gradient comes out of the layer-norm backward pass (pdvc_add_dropout_layernorm ds_colsum);
+  * with a level-position handle (ops/functions/posembed.py) the position gradient is returned as per-(video,
+    level) sums, sum_rows(d_proj) @ W_q, so the (N*S, d) position gradient is never formed nor accumulated over
+    layers.
+"""
+import torch
+from torch.autograd import Function
+from torch.autograd.function import once_differentiable
+
+from pdvc import _native as _n
+from .addnorm import BWD_PARTS
+from .linear import colsum, wgrad_mm
+from .ms_deform_attn_func import NUM_SAMPLES, msda1d_backward, msda1d_forward
+from .posembed import level_row_sums
+
+
+class EncoderAttnBlockFunction(Function):
+    @staticmethod
+    def forward(ctx, src, pos, handle, ref, pad_mask, Wv, bv, Wq, bq, Wo, bo, gamma, beta, p, eps, seed, level_T, M):
+        N, S, d = src.shape
+        R = N * S
+        D = d // M
+        src2 = src.reshape(R, d).contiguous()
+        q = src2 + pos.reshape(R, d)
+        value = torch.addmm(bv, src2, Wv.t())
+        proj = torch.addmm(bq, q, Wq.t())
+        nq = M * NUM_SAMPLES
+        ref = ref.contiguous()
+        out, save_attn, save_loc = msda1d_forward(value.view(N, S, M, D), pad_mask, proj.view(N, S, -1), ref,
+                                                  level_T, 0, nq)
+        s2 = torch.addmm(bo, out.view(R, d), Wo.t())
+        y = torch.empty_like(src2)
+        mean = torch.empty(R, dtype=src.dtype, device=src.device)
+        rstd = torch.empty_like(mean)
+        seed_dev = seed if isinstance(seed, torch.Tensor) else None
+        seed_int = 0 if seed_dev is not None else int(seed)
+        _n.call("pdvc_add_dropout_layernorm_forward_f32", _n.ptr(src2), _n.ptr(s2), _n.ptr(gamma), _n.ptr(beta), R,
+                d, float(p), seed_int, _n.ptr(seed_dev), float(eps), _n.ptr(y), _n.ptr(mean), _n.ptr(rstd),
+                _n.stream())
+        ctx.save_for_backward(src2, q, value, proj, ref, pad_mask, save_attn, save_loc, out, s2, Wv, Wq, Wo, gamma,
+                              mean, rstd, seed_dev)
+        ctx.meta = (N, S, d, M, float(p), seed_int, tuple(level_T), handle is not None)
+        return y.view(N, S, d)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy):
+        (src2, q, value, proj, ref, pad_mask, save_attn, save_loc, out, s2, Wv, Wq, Wo, gamma, mean, rstd,
+         seed_dev) = ctx.saved_tensors
+        N, S, d, M, p, seed_int, level_T, has_handle = ctx.meta
+        R = N * S
+        D = d // M
+        dy2 = dy.reshape(R, d).contiguous()
+        d_src = torch.empty_like(src2)
+        d_s2 = torch.empty_like(s2)
+        dgamma = torch.empty_like(gamma)
+        dbeta = torch.empty_like(gamma)
+        dbo = torch.empty_like(gamma)
+        ws = torch.empty(3 * BWD_PARTS * d, dtype=src2.dtype, device=src2.device)
+        _n.call("pdvc_add_dropout_layernorm_backward_f32", _n.ptr(src2), _n.ptr(s2), _n.ptr(gamma), _n.ptr(mean),
+                _n.ptr(rstd), _n.ptr(dy2), R, d, p, seed_int, _n.ptr(seed_dev), _n.ptr(d_src), _n.ptr(d_s2),
+                _n.ptr(dgamma), _n.ptr(dbeta), _n.ptr(dbo), _n.ptr(ws), _n.stream())
+        dWo = wgrad_mm(d_s2, out.view(R, d))
+        d_out = torch.mm(d_s2, Wo)
+        nq = M * NUM_SAMPLES
+        gv, gp, _ = msda1d_backward(value.view(N, S, M, D), pad_mask, proj.view(N, S, -1), ref, save_attn, save_loc,
+                                    out, d_out.view(N, S, d), level_T, 0, nq)
+        gv2 = gv.view(R, d)
+        gp2 = gp.view(R, -1)
+        dbv = colsum(gv2)
+        dWv = wgrad_mm(gv2, src2)
+        dbq = colsum(gp2)
+        dWq = wgrad_mm(gp2, q)
+        d_pos = d_handle = None
+        if has_handle:
+            d_handle = torch.matmul(level_row_sums(gp.view(N, S, -1), level_T), Wq)
+            d_src.addmm_(gp2, Wq)
+        elif ctx.needs_input_grad[1]:
+            d_q = torch.mm(gp2, Wq)
+            d_pos = d_q.view(N, S, d)
+            d_src.add_(d_q)
+        else:
+            d_src.addmm_(gp2, Wq)
+        d_src.addmm_(gv2, Wv)  # residual + value path + query path, accumulated in the GEMM epilogues
+        return (d_src.view(N, S, d), d_pos, d_handle, None, None, dWv, dbv, dWq, dbq, dWo, dbo, dgamma, dbeta,
+                None, None, None, None, None)
+
+
+def use_attn_block(src, layer):
+    """EncoderAttnBlockFunction serves fp32 GPU rows whose MSDeformAttn takes the fused 1-D kernels, on the
+    torch/hipBLASLt GEMM backend."""
+    from . import linear as _lin
+    return (src.is_cuda and src.dtype == torch.float32 and layer.self_attn.fused and _lin.BACKEND != "hip"
+            and layer.self_attn.d_model % layer.self_attn.n_heads == 0)
+
+
+def encoder_attn_block(layer, src, pos, handle, reference_points, level_T, padding_mask):
+    """norm1(src + dropout1(self_attn(src + pos, ...))) of a DeformableTransformerEncoderLayer."""
+    sa = layer.self_attn
+    mask = None if padding_mask is None else padding_mask.contiguous().view(torch.uint8)
+    Wq = torch.cat([sa.sampling_offsets.weight, sa.attention_weights.weight], 0)
+    bq = torch.cat([sa.sampling_offsets.bias, sa.attention_weights.bias], 0)
+    p = float(layer.dropout1.p) if layer.training else 0.0
+    seed = torch.randint(0, 2 ** 62, (1,), device=src.device, dtype=torch.int64) if p > 0 else 0
+    return EncoderAttnBlockFunction.apply(src, pos, handle, reference_points, mask, sa.value_proj.weight,
+                                          sa.value_proj.bias, Wq, bq, sa.output_proj.weight, sa.output_proj.bias,
+                                          layer.norm1.weight, layer.norm1.bias, p, layer.norm1.eps, seed,
+                                          tuple(level_T), sa.n_heads)

@@ -20,7 +20,7 @@ from torch.autograd.function import once_differentiable
 from pdvc import _native as _n
 from .addnorm import BWD_PARTS
 from . import linear as _lin
-from .linear import CU, colsum, wgrad_mm
+from .linear import CU, wgrad_mm
 
 
 def _seed_ptrs(seeds):
@@ -69,11 +69,11 @@ class FFNBlockFunction(Function):
         dy = torch.empty_like(y)
         dgamma = torch.empty_like(gamma)
         dbeta = torch.empty_like(gamma)
-        ws = torch.empty(2 * BWD_PARTS * d, dtype=x2.dtype, device=x2.device)
+        ws = torch.empty(3 * BWD_PARTS * d, dtype=x2.dtype, device=x2.device)
+        db2 = torch.empty_like(gamma)  # linear2's bias gradient = column sums of dy, summed by the same pass
         _n.call("pdvc_add_dropout_layernorm_backward_f32", _n.ptr(x2), _n.ptr(y), _n.ptr(gamma), _n.ptr(mean),
                 _n.ptr(rstd), _n.ptr(dout2), rows, d, p_out, 0, seed_out, _n.ptr(dx), _n.ptr(dy), _n.ptr(dgamma),
-                _n.ptr(dbeta), _n.ptr(ws), _n.stream())
-        db2 = colsum(dy)
+                _n.ptr(dbeta), _n.ptr(db2), _n.ptr(ws), _n.stream())
         dw2 = wgrad_mm(dy, h)
         dh = torch.mm(dy, w2)
         parts = _parts(rows, fdim)

@@ -94,6 +94,41 @@ def _levels(level_T):
     return _n.int_array(level_T), len(level_T)
 
 
+def msda1d_forward(value, pad_mask, proj, ref, level_T, off_base, logit_base, save=True):
+    """pdvc_msda1d_forward_f32 on contiguous value (N,S,M,D), proj (N,Lq,C), ref (N,Lq,L,1|2): returns
+    (out (N,Lq,M*D), save_attn, save_loc) -- the last two None when save is False."""
+    N, S, M, D = value.shape
+    Lq, C = proj.shape[1], proj.shape[2]
+    RD = ref.shape[3]
+    lvl, nl = _levels(level_T)
+    out = torch.empty((N, Lq, M * D), dtype=value.dtype, device=value.device)
+    save_attn = save_loc = None
+    if save:
+        save_attn = torch.empty((N, Lq, M, NUM_SAMPLES), dtype=value.dtype, device=value.device)
+        save_loc = torch.empty_like(save_attn)
+    _n.call("pdvc_msda1d_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(proj), C, off_base, logit_base,
+            _n.ptr(ref), RD, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(out), _n.ptr(save_attn),
+            _n.ptr(save_loc), _n.stream(), meta=(N, Lq, S, M, D, NUM_SAMPLES))
+    return out, save_attn, save_loc
+
+
+def msda1d_backward(value, pad_mask, proj, ref, save_attn, save_loc, out, grad_out, level_T, off_base, logit_base,
+                    need_ref=False):
+    """pdvc_msda1d_backward_f32: returns (grad_value, grad_proj, grad_ref or None)."""
+    N, S, M, D = value.shape
+    Lq, C = proj.shape[1], proj.shape[2]
+    RD = ref.shape[3]
+    lvl, nl = _levels(level_T)
+    gv = torch.empty_like(value)
+    gp = torch.zeros_like(proj) if C != 2 * M * NUM_SAMPLES else torch.empty_like(proj)
+    gr = torch.empty_like(ref) if need_ref else None
+    _n.call("pdvc_msda1d_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(ref), RD, _n.ptr(proj), C,
+            off_base, logit_base, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(grad_out), _n.ptr(out),
+            _n.ptr(save_attn), _n.ptr(save_loc), _n.ptr(gv), _n.ptr(gp), _n.ptr(gr), _n.stream(),
+            meta=(N, Lq, S, M, D, NUM_SAMPLES))
+    return gv, gp, gr
+
+
 class MSDA1dFunction(Function):
     """Fused MSDeformAttn core for a 1-D temporal pyramid (GPU semantics: zero padding).
 
@@ -103,20 +138,8 @@ class MSDA1dFunction(Function):
     @staticmethod
     def forward(ctx, value, pad_mask, proj, ref, level_T, off_base, logit_base):
         value, proj, ref = value.contiguous(), proj.contiguous(), ref.contiguous()
-        N, S, M, D = value.shape
-        Lq, C = proj.shape[1], proj.shape[2]
-        L, RD = ref.shape[2], ref.shape[3]
-        lvl, nl = _levels(level_T)
-        out = torch.empty((N, Lq, M * D), dtype=value.dtype, device=value.device)
         need = ctx.needs_input_grad[0] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
-        if need:
-            save_attn = torch.empty((N, Lq, M, NUM_SAMPLES), dtype=value.dtype, device=value.device)
-            save_loc = torch.empty_like(save_attn)
-        else:
-            save_attn = save_loc = None
-        _n.call("pdvc_msda1d_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(proj), C, off_base, logit_base,
-                _n.ptr(ref), RD, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(out), _n.ptr(save_attn),
-                _n.ptr(save_loc), _n.stream(), meta=(N, Lq, S, M, D, NUM_SAMPLES))
+        out, save_attn, save_loc = msda1d_forward(value, pad_mask, proj, ref, level_T, off_base, logit_base, need)
         if need:
             ctx.save_for_backward(value, pad_mask, proj, ref, save_attn, save_loc, out)
         ctx.meta = (tuple(level_T), off_base, logit_base)
@@ -127,18 +150,8 @@ class MSDA1dFunction(Function):
     def backward(ctx, grad_out):
         value, pad_mask, proj, ref, save_attn, save_loc, out = ctx.saved_tensors
         level_T, off_base, logit_base = ctx.meta
-        grad_out = grad_out.contiguous()
-        N, S, M, D = value.shape
-        Lq, C = proj.shape[1], proj.shape[2]
-        RD = ref.shape[3]
-        lvl, nl = _levels(level_T)
-        gv = torch.empty_like(value)
-        gp = torch.zeros_like(proj) if C != 2 * M * NUM_SAMPLES else torch.empty_like(proj)
-        gr = torch.empty_like(ref) if ctx.needs_input_grad[3] else None
-        _n.call("pdvc_msda1d_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(ref), RD, _n.ptr(proj), C,
-                off_base, logit_base, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(grad_out), _n.ptr(out),
-                _n.ptr(save_attn), _n.ptr(save_loc), _n.ptr(gv), _n.ptr(gp), _n.ptr(gr), _n.stream(),
-                meta=(N, Lq, S, M, D, NUM_SAMPLES))
+        gv, gp, gr = msda1d_backward(value, pad_mask, proj, ref, save_attn, save_loc, out, grad_out.contiguous(),
+                                     level_T, off_base, logit_base, need_ref=ctx.needs_input_grad[3])
         return gv, None, gp, gr, None, None, None
 
 

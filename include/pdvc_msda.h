@@ -205,14 +205,16 @@ int pdvc_lstm_cell_backward_f32(const float* grad_h, int ld_grad_h, const float*
  * x, s, y (rows, d) contiguous, d % 4 == 0, d <= 512; gamma, beta (d); mean, rstd (rows) saved for the backward.
  * Dropout keeps each element with probability 1-p from a counter hash of (seed, row, column), scaled by
  * 1/(1-p); seed_dev (device, may be NULL) overrides seed.  The backward regenerates the mask:
- * dx = dL/dx, ds = dL/ds, dgamma/dbeta fully written; workspace 2*256*d floats. */
+ * dx = dL/dx, ds = dL/ds, dgamma/dbeta fully written; ds_colsum (may be NULL) = column sums of ds (the bias
+ * gradient of the linear that produced s) from the same pass; workspace 3*256*d floats. */
 int pdvc_add_dropout_layernorm_forward_f32(const float* x, const float* s, const float* gamma, const float* beta,
                                            int rows, int d, float p, uint64_t seed, const uint64_t* seed_dev,
                                            float eps, float* y, float* mean, float* rstd, void* stream);
 int pdvc_add_dropout_layernorm_backward_f32(const float* x, const float* s, const float* gamma, const float* mean,
                                             const float* rstd, const float* dy, int rows, int d, float p,
                                             uint64_t seed, const uint64_t* seed_dev, float* dx, float* ds,
-                                            float* dgamma, float* dbeta, float* workspace, void* stream);
+                                            float* dgamma, float* dbeta, float* ds_colsum, float* workspace,
+                                            void* stream);
 
 /* ---- linear sum assignment (the set matcher) --------------------------------------------------------
  * costs (P, Q, max_targets) float32: problem p matches its first sizes[p] targets (rows of scipy's transposed
