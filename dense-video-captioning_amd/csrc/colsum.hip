@@ -48,11 +48,34 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restric
 
 __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int parts, int cols,
                                                            float* __restrict__ out) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= cols) return;
-    float s = 0.f;
-    for (int p = 0; p < parts; ++p) s += part[(size_t)p * cols + c];
-    out[c] = s;
+    // 16 float4 column groups x 16 lanes over the partial rows, then a fixed-order LDS sum: deterministic
+    __shared__ float4 red[16][16];
+    const int cg = threadIdx.x & 15, rl = threadIdx.x >> 4;
+    const int c4 = blockIdx.x * 16 + cg, cs = cols / 4;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c4 < cs) {
+        const float4* src = reinterpret_cast<const float4*>(part) + c4;
+        for (int p = rl; p < parts; p += 16) {
+            const float4 v = src[(size_t)p * cs];
+            a.x += v.x;
+            a.y += v.y;
+            a.z += v.z;
+            a.w += v.w;
+        }
+    }
+    red[rl][cg] = a;
+    __syncthreads();
+    if (rl == 0 && c4 < cs) {
+        float4 t = red[0][cg];
+#pragma unroll
+        for (int k = 1; k < 16; ++k) {
+            t.x += red[k][cg].x;
+            t.y += red[k][cg].y;
+            t.z += red[k][cg].z;
+            t.w += red[k][cg].w;
+        }
+        reinterpret_cast<float4*>(out)[c4] = t;
+    }
 }
 
 }  // namespace pdvc
@@ -62,13 +85,14 @@ using namespace pdvc;
 extern "C" int pdvc_colsum_f32(const float* x, int rows, int cols, int parts, float* workspace, float* out,
                                void* stream) {
     PDVC_CHECK_ARG(rows >= 0 && cols > 0 && parts >= 1, "invalid sizes");
-    PDVC_CHECK_ARG(cols % 4 == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)workspace % 16) == 0,
+    PDVC_CHECK_ARG(cols % 4 == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)workspace % 16) == 0 &&
+                       ((uintptr_t)out % 16) == 0,
                    "colsum needs 16-byte aligned rows (cols %% 4 == 0)");
     hipStream_t s = (hipStream_t)stream;
     const unsigned cb = (unsigned)((cols / 4 + 15) / 16);
     hipLaunchKernelGGL(colsum_part_kernel, dim3(cb, (unsigned)parts), dim3(256), 0, s, x, rows, cols, parts, workspace);
     PDVC_CHECK_LAUNCH("colsum_part_kernel");
-    hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, s, workspace, parts,
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((cols / 4 + 15) / 16)), dim3(256), 0, s, workspace, parts,
                        cols, out);
     PDVC_CHECK_LAUNCH("colsum_final_kernel");
     return PDVC_OK;

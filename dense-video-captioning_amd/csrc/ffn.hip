@@ -92,12 +92,35 @@ __global__ __launch_bounds__(256) void relu_dropout_bwd_kernel(const float* __re
 }
 
 __global__ __launch_bounds__(256) void ffn_colsum_final_kernel(const float* __restrict__ part, int parts, int cols,
-                                                               float* __restrict__ out) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= cols) return;
-    float s = 0.f;
-    for (int p = 0; p < parts; ++p) s += part[(size_t)p * cols + c];
-    out[c] = s;
+                                                           float* __restrict__ out) {
+    // 16 float4 column groups x 16 lanes over the partial rows, then a fixed-order LDS sum: deterministic
+    __shared__ float4 red[16][16];
+    const int cg = threadIdx.x & 15, rl = threadIdx.x >> 4;
+    const int c4 = blockIdx.x * 16 + cg, cs = cols / 4;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c4 < cs) {
+        const float4* src = reinterpret_cast<const float4*>(part) + c4;
+        for (int p = rl; p < parts; p += 16) {
+            const float4 v = src[(size_t)p * cs];
+            a.x += v.x;
+            a.y += v.y;
+            a.z += v.z;
+            a.w += v.w;
+        }
+    }
+    red[rl][cg] = a;
+    __syncthreads();
+    if (rl == 0 && c4 < cs) {
+        float4 t = red[0][cg];
+#pragma unroll
+        for (int k = 1; k < 16; ++k) {
+            t.x += red[k][cg].x;
+            t.y += red[k][cg].y;
+            t.z += red[k][cg].z;
+            t.w += red[k][cg].w;
+        }
+        reinterpret_cast<float4*>(out)[c4] = t;
+    }
 }
 
 static uint32_t ffn_threshold(float p) {
@@ -133,7 +156,8 @@ extern "C" int pdvc_relu_dropout_backward_f32(const float* hd, float* grad, int 
     PDVC_CHECK_ARG(rows >= 0 && cols > 0 && cols % 4 == 0 && parts >= 1, "invalid sizes");
     PDVC_CHECK_ARG(((uintptr_t)hd % 16) == 0 && ((uintptr_t)grad % 16) == 0, "16-byte aligned rows required");
     PDVC_CHECK_ARG((dbias == nullptr) == (workspace == nullptr), "dbias needs a workspace of parts*cols floats");
-    PDVC_CHECK_ARG(workspace == nullptr || ((uintptr_t)workspace % 16) == 0, "workspace must be 16-byte aligned");
+    PDVC_CHECK_ARG(workspace == nullptr || (((uintptr_t)workspace % 16) == 0 && ((uintptr_t)dbias % 16) == 0),
+                   "workspace and dbias must be 16-byte aligned");
     PDVC_CHECK_ARG(p >= 0.f && p < 1.f, "dropout p must be in [0,1)");
     hipStream_t s = (hipStream_t)stream;
     const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
@@ -142,7 +166,7 @@ extern "C" int pdvc_relu_dropout_backward_f32(const float* hd, float* grad, int 
                        parts, scale, workspace);
     PDVC_CHECK_LAUNCH("relu_dropout_bwd_kernel");
     if (dbias) {
-        hipLaunchKernelGGL(ffn_colsum_final_kernel, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, s, workspace,
+        hipLaunchKernelGGL(ffn_colsum_final_kernel, dim3((unsigned)((cols / 4 + 15) / 16)), dim3(256), 0, s, workspace,
                            parts, cols, dbias);
         PDVC_CHECK_LAUNCH("ffn_colsum_final_kernel");
     }

@@ -15,6 +15,7 @@ from torch import nn
 
 from . import box_ops, hostio
 from .base_encoder import build_base_encoder
+from .ops.functions.linear import dense
 from .box_ops import inverse_sigmoid
 from .CaptioningHead import build_captioner
 from .CaptioningHead.LSTM_DSA import caption_steps
@@ -43,8 +44,9 @@ class MLP(nn.Module):
         self.layers = nn.ModuleList(nn.Linear(n, k) for n, k in zip([input_dim] + h, h + [output_dim]))
 
     def forward(self, x):
+        # nn.Linear parameters (state_dict unchanged) through `dense`: ReLU fused, split-K weight gradients
         for i, layer in enumerate(self.layers):
-            x = F.relu(layer(x)) if i < self.num_layers - 1 else layer(x)
+            x = dense(x, layer.weight, layer.bias, relu=i < self.num_layers - 1)
         return x
 
 

@@ -239,7 +239,8 @@ int pdvc_groupnorm_rows_backward_f32(const float* x, const float* dy, const floa
 
 /* ---- column sums (bias gradients) ---------------------------------------------------------------------
  * out[c] = sum_r x[r*cols + c] for a row-major (rows, cols) fp32 matrix, cols % 4 == 0, 16-byte aligned;
- * workspace: parts*cols floats (partial sums of `parts` row slabs, 1 <= parts).  Deterministic. */
+ * workspace: parts*cols floats (partial sums of `parts` row slabs, 1 <= parts); out 16-byte aligned.
+ * Deterministic. */
 int pdvc_colsum_f32(const float* x, int rows, int cols, int parts, float* workspace, float* out, void* stream);
 
 /* ---- encoder positional input ------------------------------------------------------------------------
