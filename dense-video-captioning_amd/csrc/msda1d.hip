@@ -470,7 +470,10 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
 // -------------------------------------------------------------------------------------------------
 constexpr int kVW = 8;  // waves per value-gradient workgroup
 
-template <int CW>  // channels per lane: D <= 64 -> 1, D = 128 -> 2
+// CW: channels per lane (D <= 64 -> 1, D = 128 -> 2).  G4 (D == 64): the gather phase runs on 16-lane groups
+// with a float4 per lane instead of whole waves with one float per lane -- 32 row ranges per workgroup, and one
+// wave-instruction loads the gradient rows of 4 samples (4x fewer loads, LDS index reads and loop iterations).
+template <int CW, bool G4>
 __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
                                                                      int Lq, int q0, int nq, int S, int M, int D,
                                                                      int accumulate,
@@ -546,12 +549,13 @@ __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_
         }
     }
     __syncthreads();
-    // 4) wave wid owns rows [r0, r1): split points balance the sorted samples over the waves
+    // 4) row ranges: split points balance the sorted samples over the waves (or 16-lane groups)
     const int total = off[T + 1];
+    constexpr int kParts = G4 ? kVW * 4 : kVW;
     auto split = [&](int w) -> int {
         if (w <= 0) return 0;
-        if (w >= kVW) return T;
-        const int target = (int)(((long)total * w) / kVW);
+        if (w >= kParts) return T;
+        const int target = (int)(((long)total * w) / kParts);
         int lo = 0, hi = T;  // smallest k in [0, T] with off[k] >= target
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
@@ -560,12 +564,68 @@ __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_
         }
         return lo;
     };
+    const size_t MD = (size_t)M * D;
+    const uint8_t* mrow = vmask ? vmask + (size_t)b * S + st : nullptr;
+    constexpr int U = 8;
+    if constexpr (G4) {
+        const int grp = lane >> 4, gl = lane & 15;
+        const int vg = wid * 4 + grp;
+        const int r0 = split(vg), r1 = split(vg + 1);
+        if (r0 < r1) {  // per-group control flow below: no cross-lane operations
+            const float* gb = gout + (size_t)b * Lq * MD + (size_t)m * D + gl * 4;
+            float* ob = grad_value + ((size_t)b * S + st) * MD + (size_t)m * D + gl * 4;
+            float4 accp = make_float4(0.f, 0.f, 0.f, 0.f), acch = accp;  // rows k-1 and k
+            int k = r0;
+            auto close_bucket = [&]() {
+                const int r = k - 1;
+                if (r >= r0) {
+                    float4* orow = reinterpret_cast<float4*>(ob + (size_t)r * MD);
+                    float4 v = (mrow && mrow[r]) ? make_float4(0.f, 0.f, 0.f, 0.f) : accp;
+                    if (accumulate) {
+                        const float4 o = *orow;
+                        v.x += o.x;
+                        v.y += o.y;
+                        v.z += o.z;
+                        v.w += o.w;
+                    }
+                    *orow = v;
+                }
+                accp = acch;
+                acch = make_float4(0.f, 0.f, 0.f, 0.f);
+                ++k;
+            };
+            const int jb = off[r0], je = off[r1 + 1];
+            for (int j0 = jb; j0 < je; j0 += U) {
+                float4 gv[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int j = (j0 + u < je) ? j0 + u : je - 1;
+                    gv[u] = *reinterpret_cast<const float4*>(gb + (size_t)sq[j] * MD);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int j = j0 + u;
+                    if (j >= je) break;
+                    while (j >= off[k + 1]) close_bucket();
+                    const float cl = clo[j], chh = chi[j];
+                    accp.x = fmaf(cl, gv[u].x, accp.x);
+                    accp.y = fmaf(cl, gv[u].y, accp.y);
+                    accp.z = fmaf(cl, gv[u].z, accp.z);
+                    accp.w = fmaf(cl, gv[u].w, accp.w);
+                    acch.x = fmaf(chh, gv[u].x, acch.x);
+                    acch.y = fmaf(chh, gv[u].y, acch.y);
+                    acch.z = fmaf(chh, gv[u].z, acch.z);
+                    acch.w = fmaf(chh, gv[u].w, acch.w);
+                }
+            }
+            while (k <= r1) close_bucket();
+        }
+        return;
+    }
     const int r0 = split(wid), r1 = split(wid + 1);
     if (r0 >= r1) return;
-    const size_t MD = (size_t)M * D;
     const float* gb = gout + (size_t)b * Lq * MD + (size_t)m * D;
     float* ob = grad_value + ((size_t)b * S + st) * MD + (size_t)m * D;
-    const uint8_t* mrow = vmask ? vmask + (size_t)b * S + st : nullptr;
     float accp[CW], acch[CW];  // rows k-1 and k
 #pragma unroll
     for (int c = 0; c < CW; ++c) accp[c] = acch[c] = 0.f;
@@ -593,7 +653,6 @@ __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_
         ++k;
     };
     const int jb = off[r0], je = off[r1 + 1];
-    constexpr int U = 8;
     for (int j0 = jb; j0 < je; j0 += U) {
         float gv[U][CW];
 #pragma unroll
@@ -671,6 +730,15 @@ static int pick_pyr(const Levels1d& lv, int S, int num_query, int head_dim, int 
     if (!enabled || head_dim != 64 || num_query <= 0 || 4L * num_query < S) return 0;
     if (lv.T[0] > kPyrRows || lv.T[1] + lv.T[2] + lv.T[3] > kPyrRows) return 0;
     return (num_query + per_block - 1) / per_block;
+}
+
+// 16-lane-group gather for the value gradient at D = 64 (PDVC_MSDA_G4=0 selects the wave-per-range form)
+static bool value_g4() {
+    static const bool on = [] {
+        const char* e = getenv("PDVC_MSDA_G4");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 static int pyr_attrs() {
@@ -819,11 +887,13 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
         if (qchunk > num_query) qchunk = num_query;
         static bool attr = false;
         if (!attr) {  // dynamic LDS <= 96 KiB by construction of qchunk (plus 32 B static)
-            hipError_t e1 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1>,
+            hipError_t e1 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1, false>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-            hipError_t e2 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<2>,
+            hipError_t e2 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<2, false>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-            if (e1 != hipSuccess || e2 != hipSuccess) {
+            hipError_t e3 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1, true>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+            if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
                 (void)hipGetLastError();
                 return pdvc_set_error(PDVC_ERR_LAUNCH, "msda1d_bwd_value_kernel: cannot raise the LDS limit");
             }
@@ -833,12 +903,16 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
             const int nq = (num_query - q0) < qchunk ? (num_query - q0) : qchunk;
             const size_t lds = sizeof(int) * (2 * (size_t)(Tmax + 2) + 3 * (size_t)nq * kP);
             const int acc = q0 > 0;
-            if (head_dim <= 64)
-                hipLaunchKernelGGL(msda1d_bwd_value_kernel<1>, dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
+            if (head_dim == 64 && value_g4())
+                hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
+                                   value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
+                                   save_attn, save_loc, grad_value);
+            else if (head_dim <= 64)
+                hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, false>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
                                    value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
                                    save_attn, save_loc, grad_value);
             else
-                hipLaunchKernelGGL(msda1d_bwd_value_kernel<2>, dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
+                hipLaunchKernelGGL((msda1d_bwd_value_kernel<2, false>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
                                    value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
                                    save_attn, save_loc, grad_value);
             PDVC_CHECK_LAUNCH("msda1d_bwd_value_kernel");
