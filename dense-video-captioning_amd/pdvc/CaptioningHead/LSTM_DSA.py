@@ -163,7 +163,10 @@ class LSTMDSACaptioner(Captioner):
     # ------------------------------------------------------------------------------------------------
     def _prepare(self, memory, mask_flatten):
         core = self.core
-        value = core.deformable_att.value_proj(memory)  # hoisted: identical for every step
+        # hoisted: identical for every step; the trunk may have projected memory for all its consumers at once
+        value = getattr(memory, "_pdvc_values", {}).get(id(core.deformable_att.value_proj))
+        if value is None:
+            value = core.deformable_att.value_proj(memory)
         mask_u8 = None if mask_flatten is None else mask_flatten.contiguous().view(torch.uint8)
         return value, mask_u8
 

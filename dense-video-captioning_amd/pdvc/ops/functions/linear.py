@@ -188,3 +188,48 @@ def dense(x, weight, bias=None, relu=False):
         return TorchLinearFunction.apply(x, weight, bias, relu)
     y = F.linear(x, weight, bias)
     return F.relu(y) if relu else y
+
+
+class MultiLinearFunction(Function):
+    """Several nn.Linear layers applied to the same input x: (x W_0^T + b_0, x W_1^T + b_1, ...).  Forward is
+    one GEMM per layer; the backward accumulates the input gradient of all of them in the epilogues of their
+    data-gradient GEMMs (beta = 1) instead of autograd adds over x's shape -- PDVC's encoder memory feeds the
+    value projections of every decoder layer and of the caption head (deformable_transformer.py:260-262,
+    ms_deform_attn_for_caption.py:70)."""
+
+    @staticmethod
+    def forward(ctx, x, *wb):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        ws, bs = wb[0::2], wb[1::2]
+        outs = tuple(torch.addmm(b, x2, w.t()).view(*shape[:-1], w.shape[0]) for w, b in zip(ws, bs))
+        ctx.save_for_backward(x2, *ws)
+        ctx.shape = shape
+        return outs
+
+    @staticmethod
+    def backward(ctx, *grads):
+        x2, *ws = ctx.saved_tensors
+        gx = None
+        gwb = []
+        for g, w in zip(grads, ws):
+            if g is None:
+                gwb += [None, None]
+                continue
+            g2 = g.reshape(-1, w.shape[0]).contiguous()
+            if gx is None:
+                gx = torch.mm(g2, w)
+            else:
+                gx.addmm_(g2, w)
+            gwb += [wgrad_mm(g2, x2), colsum(g2)]
+        if gx is None:
+            gx = torch.zeros_like(x2)
+        return (gx.view(ctx.shape), *gwb)
+
+
+def multi_dense(x, layers):
+    """[layer(x) for layer in layers] for nn.Linear-like layers (with biases) sharing the input x."""
+    wb = []
+    for layer in layers:
+        wb += [layer.weight, layer.bias]
+    return MultiLinearFunction.apply(x, *wb)

@@ -98,6 +98,8 @@ class MSDeformAttn(nn.Module):
         T = level_lengths(input_spatial_shapes)
         if sum(T) != Len_in:
             raise AssertionError("sum of level lengths must equal the flattened input length")
+        if value is None:  # a caller may have projected input_flatten for several consumers at once (pdvc.py trunk)
+            value = getattr(input_flatten, "_pdvc_values", {}).get(id(self.value_proj))
         if value is None:
             value = self.value_proj(input_flatten)
         M, D = self.n_heads, self.d_model // self.n_heads

@@ -8,6 +8,7 @@ videos are decoded in one recurrence, and all Hungarian matchings share one devi
 """
 import copy
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -15,7 +16,8 @@ from torch import nn
 
 from . import box_ops, hostio
 from .base_encoder import build_base_encoder
-from .ops.functions.linear import dense
+from .ops.functions import linear as _lin
+from .ops.functions.linear import dense, multi_dense
 from .box_ops import inverse_sigmoid
 from .CaptioningHead import build_captioner
 from .CaptioningHead.LSTM_DSA import caption_steps
@@ -122,6 +124,7 @@ class PDVC(nn.Module):
             srcs, masks, pos)
         level_T = tr.last_level_T
         memory = tr.forward_encoder(src_flatten, level_T, lsi, valid_ratios, lvl_pos, mask_flatten)
+        self._project_memory(memory)
         query_embed = self.query_embed.weight
         proposals_mask = torch.ones(N, query_embed.shape[0], device=query_embed.device).bool()
         init_reference, tgt, reference_points, query_embed = tr.prepare_decoder_input_query(memory, query_embed)
@@ -130,6 +133,22 @@ class PDVC(nn.Module):
         classes, counts, coords = self._layer_heads(hs, init_reference, inter_references, False)
         return (memory, mask_flatten, temporal_shapes, lsi, valid_ratios, proposals_mask, hs, init_reference,
                 inter_references, torch.stack(classes), torch.stack(counts), torch.stack(coords))
+
+    def _project_memory(self, memory):
+        """The value projections of every consumer of the encoder memory (each decoder layer's cross-attention
+        and the shared caption head) as one autograd node, attached to `memory` for the consumers to pick up:
+        their input gradients then accumulate in GEMM epilogues instead of autograd adds over (N, S, d)."""
+        if not (memory.is_cuda and memory.dtype == torch.float32 and _lin.BACKEND != "hip"):
+            return
+        if os.environ.get("PDVC_FUSED_MEMORY_PROJ") == "0":  # A/B switch
+            return
+        users = [layer.cross_attn.value_proj for layer in self.transformer.decoder.layers]
+        if self.share_caption_head:
+            att = getattr(getattr(self.caption_head[0], "core", None), "deformable_att", None)
+            if att is not None:
+                users.append(att.value_proj)
+        vals = multi_dense(memory, users)
+        memory._pdvc_values = {id(u): v for u, v in zip(users, vals)}
 
     def enable_graph(self, dt):
         """Capture trunk() for the shapes of `dt` (training mode) with torch.cuda.make_graphed_callables:
