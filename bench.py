@@ -35,7 +35,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--videos-per-gpu", type=int, default=256)
+    p.add_argument("--videos-per-gpu", type=int, default=512)
     p.add_argument("--T", type=int, default=512)
     p.add_argument("--C", type=int, default=768)
     p.add_argument("--Q", type=int, default=100)
