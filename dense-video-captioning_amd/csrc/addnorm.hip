@@ -207,32 +207,49 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_bwd_kernel(const float* __r
 }
 
 // column sums of the (parts, d) partials -> dgamma, dbeta (and dsum when given): a workgroup per 64 columns,
-// its 4 waves take every 4th partial row, summed in LDS in a fixed order (bitwise reproducible)
+// 16 float4 column groups x 16 lanes over the partial rows, then a fixed-order LDS sum (bitwise reproducible)
 __global__ __launch_bounds__(256) void addnorm_colsum_kernel(const float* __restrict__ gpart,
                                                              const float* __restrict__ bpart,
                                                              const float* __restrict__ spart, int parts, int d,
                                                              float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                              float* __restrict__ dsum) {
-    __shared__ float red[3][4][64];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = blockIdx.x * 64 + lane;
-    float a = 0.f, b = 0.f, e = 0.f;
-    if (c < d) {
-#pragma unroll 8
-        for (int i = w; i < parts; i += 4) {
-            a += gpart[(size_t)i * d + c];
-            b += bpart[(size_t)i * d + c];
-            if (spart) e += spart[(size_t)i * d + c];
+    __shared__ float4 red[3][16][16];
+    const int cg = threadIdx.x & 15, rl = threadIdx.x >> 4;
+    const int c4 = blockIdx.x * 16 + cg, cs = d / 4;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, e = a;
+    if (c4 < cs) {
+        const float4* g4 = reinterpret_cast<const float4*>(gpart) + c4;
+        const float4* b4 = reinterpret_cast<const float4*>(bpart) + c4;
+        const float4* s4 = spart ? reinterpret_cast<const float4*>(spart) + c4 : nullptr;
+#pragma unroll 4
+        for (int i = rl; i < parts; i += 16) {
+            const float4 x = g4[(size_t)i * cs], y = b4[(size_t)i * cs];
+            a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+            b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
+            if (s4) {
+                const float4 z = s4[(size_t)i * cs];
+                e.x += z.x; e.y += z.y; e.z += z.z; e.w += z.w;
+            }
         }
     }
-    red[0][w][lane] = a;
-    red[1][w][lane] = b;
-    red[2][w][lane] = e;
+    red[0][rl][cg] = a;
+    red[1][rl][cg] = b;
+    red[2][rl][cg] = e;
     __syncthreads();
-    if (w == 0 && c < d) {
-        dgamma[c] = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
-        dbeta[c] = red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
-        if (dsum) dsum[c] = red[2][0][lane] + red[2][1][lane] + red[2][2][lane] + red[2][3][lane];
+    if (rl < 3 && c4 < cs && (rl < 2 || dsum)) {
+        float4 t = red[rl][0][cg];
+#pragma unroll
+        for (int k = 1; k < 16; ++k) {
+            t.x += red[rl][k][cg].x;
+            t.y += red[rl][k][cg].y;
+            t.z += red[rl][k][cg].z;
+            t.w += red[rl][k][cg].w;
+        }
+        float* dst = rl == 0 ? dgamma : (rl == 1 ? dbeta : dsum);
+        dst[c4 * 4 + 0] = t.x;
+        dst[c4 * 4 + 1] = t.y;
+        dst[c4 * 4 + 2] = t.z;
+        dst[c4 * 4 + 3] = t.w;
     }
 }
 
@@ -247,8 +264,8 @@ static int an_grid(int rows, int cap) {
     const int want = (rows + kANW - 1) / kANW;
     return want < cap ? (want > 0 ? want : 1) : cap;
 }
-constexpr int kAnFwdBlocks = 1024;  // 4 per CU
-constexpr int kAnBwdBlocks = 256;   // 1 per CU: fewer gamma/beta partial rows
+constexpr int kAnFwdBlocks = 2048;  // 8 per CU
+constexpr int kAnBwdBlocks = 1024;  // 4 per CU (16 waves): enough loads in flight to stream at HBM rate
 
 }  // namespace pdvc
 
@@ -283,7 +300,7 @@ extern "C" int pdvc_add_dropout_layernorm_backward_f32(const float* x, const flo
                                                        float* dx, float* ds, float* dgamma, float* dbeta,
                                                        float* ds_colsum, float* workspace, void* stream) {
     AN_CHECK();
-    PDVC_CHECK_ARG(workspace != nullptr, "workspace (3 * 256 * d floats) is required");
+    PDVC_CHECK_ARG(workspace != nullptr, "workspace (3 * 1024 * d floats) is required");
     hipStream_t st = (hipStream_t)stream;
     if (rows == 0) {
         hipError_t e1 = hipMemsetAsync(dgamma, 0, sizeof(float) * d, st);
@@ -305,7 +322,7 @@ extern "C" int pdvc_add_dropout_layernorm_backward_f32(const float* x, const flo
         hipLaunchKernelGGL(addnorm_bwd_kernel<2>, grid, block, 0, st, x, s, gamma, mean, rstd, dy, rows, d, p,
                            an_threshold(p), seed, seed_dev, dx, ds, gpart, bpart, spart);
     PDVC_CHECK_LAUNCH("addnorm_bwd_kernel");
-    hipLaunchKernelGGL(addnorm_colsum_kernel, dim3((unsigned)((d + 63) / 64)), dim3(256), 0, st, gpart, bpart, spart,
+    hipLaunchKernelGGL(addnorm_colsum_kernel, dim3((unsigned)((d / 4 + 15) / 16)), dim3(256), 0, st, gpart, bpart, spart,
                        parts, d, dgamma, dbeta, ds_colsum);
     PDVC_CHECK_LAUNCH("addnorm_colsum_kernel");
     return PDVC_OK;

@@ -206,7 +206,7 @@ int pdvc_lstm_cell_backward_f32(const float* grad_h, int ld_grad_h, const float*
  * Dropout keeps each element with probability 1-p from a counter hash of (seed, row, column), scaled by
  * 1/(1-p); seed_dev (device, may be NULL) overrides seed.  The backward regenerates the mask:
  * dx = dL/dx, ds = dL/ds, dgamma/dbeta fully written; ds_colsum (may be NULL) = column sums of ds (the bias
- * gradient of the linear that produced s) from the same pass; workspace 3*256*d floats. */
+ * gradient of the linear that produced s) from the same pass; workspace 3*1024*d floats. */
 int pdvc_add_dropout_layernorm_forward_f32(const float* x, const float* s, const float* gamma, const float* beta,
                                            int rows, int d, float p, uint64_t seed, const uint64_t* seed_dev,
                                            float eps, float* y, float* mean, float* rstd, void* stream);
