@@ -300,6 +300,30 @@ def test_fused_msda1d_pyramid_vs_oracle(ref_dim, masked, offset_scale):
     close(r.grad, egr, 1e-4, "grad_ref")
 
 
+@pytest.mark.parametrize("offset_scale,ref_dim", [(1.0, 1), (300.0, 1), (300.0, 2)])
+def test_fused_msda1d_windowed_full_size_vs_oracle(offset_scale, ref_dim):
+    """PDVC's full pyramid (T = 512: S = 960, two 512-query blocks of the whole-pyramid forward): offsets of
+    about one cell, and of hundreds of cells (samples over whole levels and past both ends)."""
+    from pdvc.ops.functions import MSDA1dFunction
+    rng = np.random.RandomState(int(offset_scale) + ref_dim)
+    T_l = [512, 256, 128, 64]
+    S = sum(T_l)
+    M, D, N, Lq = 2, 64, 1, S
+    value = rng.randn(N, S, M, D)
+    proj = np.concatenate([rng.randn(N, Lq, M * 16) * offset_scale, rng.randn(N, Lq, M * 16)], -1)
+    centre = np.concatenate([(np.arange(t) + 0.5) / t for t in T_l])[None, :, None, None].repeat(4, 2)
+    ref = centre if ref_dim == 1 else np.concatenate([centre, rng.uniform(0.05, 0.5, size=(N, Lq, 4, 1))], -1)
+    gout = rng.randn(N, Lq, M * D)
+    eo, egv, egp, _ = expected_msda1d(value, None, proj, ref, T_l, M, gout)
+    v = cu(value, torch.float32).requires_grad_()
+    p = cu(proj, torch.float32).requires_grad_()
+    out = MSDA1dFunction.apply(v, None, p, cu(ref, torch.float32), tuple(T_l), 0, M * 16)
+    close(out, eo, 1e-4, "out")
+    out.backward(cu(gout, torch.float32))
+    close(v.grad, egv, 1e-4, "grad_value")
+    close(p.grad, egp, 1e-4, "grad_proj")
+
+
 def test_fused_msda1d_pyramid_equals_per_query():
     """The whole-pyramid and the per-query forward share their arithmetic (4 * Lq < S sends a query subset to
     the per-query kernel): equal up to FMA contraction."""
