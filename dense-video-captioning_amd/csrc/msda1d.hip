@@ -205,6 +205,17 @@ __device__ __forceinline__ void pyr_stage(float4* __restrict__ lds, const float*
         src[(size_t)(r0 + (i >> 4)) * rs + (i & 15)];
 }
 
+// pyr_stage with 2 loads in flight per thread (used while the parameter loads hold registers)
+__device__ __forceinline__ void pyr_stage_lean(float4* __restrict__ lds, const float* __restrict__ vsrc, size_t MD,
+                                               int r0, int n, int dst) {
+    const float4* src = reinterpret_cast<const float4*>(vsrc);
+    const size_t rs = MD / 4;
+    const int total = n * 16;
+#pragma unroll 2
+    for (int i = threadIdx.x; i < total; i += kPyrThreads) lds[(size_t)(dst + (i >> 4)) * 16 + (i & 15)] =
+        src[(size_t)(r0 + (i >> 4)) * rs + (i & 15)];
+}
+
 // LDS row base of level l: level 0 alone, then levels 1..3 packed
 __device__ __forceinline__ int pyr_base(const Levels1d& lv, int l) {
     return l <= 1 ? 0 : (l == 2 ? lv.T[1] : lv.T[1] + lv.T[2]);
@@ -228,6 +239,20 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
     const int l_own = sub >> 2;
     const int T_own = lvl_sel(lv.T, l_own), st_own = lvl_sel(lv.start, l_own);
     const float Tf_own = (float)T_own;
+    // issue every parameter load first, then stage level 0 while they are in flight (neither depends on the
+    // other), then do the parameter math: the loads' latency hides under the staging
+    float lgv[kPyrQPS], offv[kPyrQPS], r0v[kPyrQPS], r1v[kPyrQPS];
+#pragma unroll
+    for (int i = 0; i < kPyrQPS; ++i) {
+        const int q = qb * kPyrQ + slot + 64 * i;
+        const size_t row = (size_t)b * Lq + (q < Lq ? q : 0);
+        const float* prow = proj + row * proj_stride;
+        lgv[i] = prow[logit_base + m * kNS + sub];
+        offv[i] = prow[off_base + m * kNS + sub];
+        r0v[i] = ref[(row * kL + l_own) * RD];
+        r1v[i] = (RD == 2) ? ref[(row * kL + l_own) * RD + 1] : 0.f;
+    }
+    pyr_stage_lean(lds4, vsrc, MD, lv.start[0], lv.T[0], 0);
     int i0v[kPyrQPS];
     float w1v[kPyrQPS], w2v[kPyrQPS];
 #pragma unroll
@@ -235,14 +260,13 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
         const int q = qb * kPyrQ + slot + 64 * i;
         const bool act = q < Lq;
         const size_t row = (size_t)b * Lq + (act ? q : 0);
-        const float* prow = proj + row * proj_stride;
-        const float lg = prow[logit_base + m * kNS + sub];
+        const float lg = lgv[i];
         const float mx = group_max<16>(lg);
         const float sum = group_allreduce<16>(expf(lg - mx));
         const float aw = expf(lg - mx) / sum;
-        const float off = prow[off_base + m * kNS + sub];
-        const float r0 = ref[(row * kL + l_own) * RD];
-        const float r1 = (RD == 2) ? ref[(row * kL + l_own) * RD + 1] : 0.f;
+        const float off = offv[i];
+        const float r0 = r0v[i];
+        const float r1 = r1v[i];
         const float loc = (RD == 1) ? r0 + off / Tf_own : r0 + ((off / (float)kP) * r1) * 0.5f;
         if (save_loc && act) {
             const size_t si = (row * M + m) * kNS + sub;
@@ -269,13 +293,11 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
     for (int i = 0; i < kPyrQPS; ++i) acc[i].zero();
 #pragma unroll 1
     for (int l = 0; l < kL; ++l) {  // rolled: keeps each level's address math out of the others' registers
-        if (l == 0 || l == 1) {  // stage level 0, then levels 1..3 in one round trip
+        if (l == 0) {  // level 0 was staged before the parameter math
             __syncthreads();
-            if (l == 0) {
-                pyr_stage(lds4, vsrc, MD, lv.start[0], lv.T[0], 0);
-            } else {
-                pyr_stage(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3], 0);
-            }
+        } else if (l == 1) {  // levels 1..3 in one round trip
+            __syncthreads();
+            pyr_stage(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3], 0);
             __syncthreads();
         }
         const int T = lvl_sel(lv.T, l), base = pyr_base(lv, l);
