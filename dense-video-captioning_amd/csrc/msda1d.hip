@@ -59,7 +59,7 @@ __device__ __forceinline__ int lvl_sel(const int (&v)[kL], int l) {
 template <int LPH>
 __device__ __forceinline__ float group_max(float v) {
 #pragma unroll
-    for (int d = 1; d < LPH; d <<= 1) v = fmaxf(v, __shfl_xor(v, d, PDVC_WAVE));
+    for (int d = 1; d < LPH; d <<= 1) v = fmaxf(v, d <= 8 ? grp_swap(v, d) : __shfl_xor(v, d, PDVC_WAVE));
     return v;
 }
 
@@ -159,10 +159,9 @@ __global__ __launch_bounds__(256) void msda1d_fwd_kernel(
 #pragma unroll
         for (int p = 0; p < kP; ++p) {
             const int j = l * kP + p;
-            const int src = w.gbase + j % LPH;
-            const int i0 = __shfl(i0v[j / LPH], src, PDVC_WAVE);
-            c1[p] = __shfl(w1v[j / LPH], src, PDVC_WAVE);
-            c2[p] = __shfl(w2v[j / LPH], src, PDVC_WAVE);
+            const int i0 = grp_bcast<LPH>(i0v[j / LPH], j % LPH);
+            c1[p] = grp_bcast<LPH>(w1v[j / LPH], j % LPH);
+            c2[p] = grp_bcast<LPH>(w2v[j / LPH], j % LPH);
             const int a1 = min(max(i0, 0), T - 1), a2 = min(max(i0 + 1, 0), T - 1);
             v1[p].load(vbase + (size_t)(st + a1) * MD);
             v2[p].load(vbase + (size_t)(st + a2) * MD);
@@ -307,7 +306,7 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
             float c1[kP], c2[kP];
 #pragma unroll
             for (int p = 0; p < kP; ++p) {
-                const int src = gbase + l * kP + p;
+                const int src = gbase + l * kP + p;  // l is a runtime level index here: ds_bpermute
                 const int i0 = __shfl(i0v[i], src, PDVC_WAVE);
                 c1[p] = __shfl(w1v[i], src, PDVC_WAVE);
                 c2[p] = __shfl(w2v[i], src, PDVC_WAVE);
@@ -401,10 +400,9 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
 #pragma unroll
         for (int p = 0; p < kP; ++p) {  // all 2*P corner loads in flight together (clamped, selected later)
             const int j = l * kP + p;
-            const int src = w.gbase + j % LPH;
-            const int i0 = __shfl(i0v[j / LPH], src, PDVC_WAVE);
-            lw[p] = __shfl(lwv[j / LPH], src, PDVC_WAVE);
-            ok[p] = __shfl(okv[j / LPH], src, PDVC_WAVE);
+            const int i0 = grp_bcast<LPH>(i0v[j / LPH], j % LPH);
+            lw[p] = grp_bcast<LPH>(lwv[j / LPH], j % LPH);
+            ok[p] = grp_bcast<LPH>(okv[j / LPH], j % LPH);
             const int a1 = min(max(i0, 0), T - 1), a2 = min(max(i0 + 1, 0), T - 1);
             v1[p].load(vbase + (size_t)(st + a1) * MD);
             v2[p].load(vbase + (size_t)(st + a2) * MD);
@@ -428,7 +426,7 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
 #pragma unroll
         for (int k = 0; k < VPL; ++k) {
 #pragma unroll
-            for (int d = G; d < LPH; d <<= 1) part[k] += __shfl_xor(part[k], d, PDVC_WAVE);
+            for (int d = G; d < LPH; d <<= 1) part[k] += grp_swap(part[k], d);  // exact xor for d = 8
         }
         // group lane r (= sub % G) holds values [r*VPL, (r+1)*VPL) of the interleaved (ga, gs) list
         float ga, gs;
@@ -439,7 +437,7 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
             ga = part[0];
             gs = part[1];
         } else {
-            const float other = __shfl_xor(part[0], 1, PDVC_WAVE);
+            const float other = grp_swap(part[0], 1);
             p = r >> 1;
             ga = (r & 1) ? other : part[0];
             gs = (r & 1) ? part[0] : other;

@@ -19,17 +19,56 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
     return base + slot;
 }
 
-// Sum over aligned groups of G lanes (G power of two <= 64) with xor butterflies.
+// Partner exchange for butterfly step d (1, 2, 4, 8) inside aligned 16-lane groups, on the DPP network (a VALU
+// operand modifier: no LDS traffic, no lane-index arithmetic, unlike __shfl_xor's ds_bpermute).  d = 1, 2, 8
+// are exact xors (quad_perm, row_ror:8); d = 4 pairs lane i with 7 - i inside its 8-lane half (row_half_mirror).
+// Any involution that flips bit d and keeps the bits above d inside the group gives the same sums in
+// allreduce / max / reduce-scatter butterflies whose steps run from high d to low or low to high.
+__device__ __forceinline__ float grp_swap(float v, int d) {
+    const int x = __float_as_int(v);
+    int r;
+    switch (d) {
+        case 1: r = __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false); break;   // quad_perm(1,0,3,2)
+        case 2: r = __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false); break;   // quad_perm(2,3,0,1)
+        case 4: r = __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false); break;  // row_half_mirror
+        default: r = __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false); break;  // row_ror:8
+    }
+    return __int_as_float(r);
+}
+
+// the lane with index k inside each aligned group of G (<= 32) lanes, for every lane of the group
+// (ds_swizzle bit mode: lane' = (lane & and_mask) | k within each 32-lane half; k a compile-time constant after
+// unrolling, so the pattern is an immediate -- no address arithmetic)
+template <int G>
+__device__ __forceinline__ int grp_bcast(int v, int k) {
+    static_assert(G == 4 || G == 8 || G == 16 || G == 32, "group of 4..32 lanes");
+    constexpr int and_mask = 0x1F & ~(G - 1);
+#define PDVC_SWZ(K) case K: return __builtin_amdgcn_ds_swizzle(v, and_mask | ((K) << 5));
+    switch (k) {
+        PDVC_SWZ(0) PDVC_SWZ(1) PDVC_SWZ(2) PDVC_SWZ(3) PDVC_SWZ(4) PDVC_SWZ(5) PDVC_SWZ(6) PDVC_SWZ(7)
+        PDVC_SWZ(8) PDVC_SWZ(9) PDVC_SWZ(10) PDVC_SWZ(11) PDVC_SWZ(12) PDVC_SWZ(13) PDVC_SWZ(14) PDVC_SWZ(15)
+        PDVC_SWZ(16) PDVC_SWZ(17) PDVC_SWZ(18) PDVC_SWZ(19) PDVC_SWZ(20) PDVC_SWZ(21) PDVC_SWZ(22) PDVC_SWZ(23)
+        PDVC_SWZ(24) PDVC_SWZ(25) PDVC_SWZ(26) PDVC_SWZ(27) PDVC_SWZ(28) PDVC_SWZ(29) PDVC_SWZ(30) PDVC_SWZ(31)
+        default: return v;
+    }
+#undef PDVC_SWZ
+}
+template <int G>
+__device__ __forceinline__ float grp_bcast(float v, int k) {
+    return __int_as_float(grp_bcast<G>(__float_as_int(v), k));
+}
+
+// Sum over aligned groups of G lanes (G power of two <= 64) with butterflies (DPP inside 16-lane groups).
 template <int G>
 __device__ __forceinline__ float group_allreduce(float v) {
 #pragma unroll
-    for (int d = G >> 1; d > 0; d >>= 1) v += __shfl_xor(v, d, PDVC_WAVE);
+    for (int d = G >> 1; d > 0; d >>= 1) v += (d <= 8) ? grp_swap(v, d) : __shfl_xor(v, d, PDVC_WAVE);
     return v;
 }
 
 // Transposed (reduce-scatter) butterfly inside aligned groups of G lanes: every lane enters with K
 // partial values; after log2(G) halving steps lane r (= lane % G) holds the FULL group sums of the
-// K/G consecutive values [r*K/G, (r+1)*K/G).  Costs K/2 + K/4 + ... shuffles instead of K*log2(G).
+// K/G consecutive values [r*K/G, (r+1)*K/G).  Costs K/2 + K/4 + ... exchanges instead of K*log2(G).
 template <int K, int G>
 __device__ __forceinline__ void group_reduce_scatter(float (&v)[K], int lane) {
     static_assert((K % G) == 0, "K must be a multiple of G");
@@ -43,7 +82,7 @@ __device__ __forceinline__ void group_reduce_scatter(float (&v)[K], int lane) {
             if (i < half) {
                 // value I send = the half I do not keep; value I receive lands on the half I keep
                 const float send = upper ? v[i] : v[i + half];
-                const float recv = __shfl_xor(send, d, PDVC_WAVE);
+                const float recv = (d <= 8) ? grp_swap(send, d) : __shfl_xor(send, d, PDVC_WAVE);
                 const float mine = upper ? v[i + half] : v[i];
                 v[i] = mine + recv;
             }
