@@ -29,7 +29,7 @@ __device__ __forceinline__ bool an_keep(uint64_t seed, uint32_t row, uint32_t co
 
 __device__ __forceinline__ float an_wave_sum(float v) {
 #pragma unroll
-    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, PDVC_WAVE);
+    for (int d = 32; d > 0; d >>= 1) v += lane_swap(v, d);
     return v;
 }
 
@@ -264,7 +264,7 @@ static int an_grid(int rows, int cap) {
     const int want = (rows + kANW - 1) / kANW;
     return want < cap ? (want > 0 ? want : 1) : cap;
 }
-constexpr int kAnFwdBlocks = 2048;  // 8 per CU
+constexpr int kAnFwdBlocks = 1024;  // 4 per CU
 constexpr int kAnBwdBlocks = 1024;  // 4 per CU (16 waves): enough loads in flight to stream at HBM rate
 
 }  // namespace pdvc

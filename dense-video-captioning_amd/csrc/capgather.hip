@@ -189,7 +189,7 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
 #pragma unroll
     for (int u = 0; u < kSPW; ++u) {
 #pragma unroll
-        for (int d = 1; d < LPH; d <<= 1) part[u] += __shfl_xor(part[u], d, PDVC_WAVE);
+        for (int d = 1; d < LPH; d <<= 1) part[u] += lane_swap(part[u], d);
     }
     const bool owner = active && sub == 0;
     const bool centre_only = (RD == 1) || (r < rd1_rows);
@@ -218,8 +218,8 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
         float v0 = owner ? gr0 : 0.f, v1 = owner ? gr1 : 0.f;
 #pragma unroll
         for (int d = LPH; d < 64; d <<= 1) {
-            v0 += __shfl_xor(v0, d, PDVC_WAVE);
-            if (RD == 2) v1 += __shfl_xor(v1, d, PDVC_WAVE);
+            v0 += lane_swap(v0, d);
+            if (RD == 2) v1 += lane_swap(v1, d);
         }
         if (lane == 0) {
             atomicAdd(grad_ref + ((size_t)r * cL + l) * RD, v0);

@@ -28,7 +28,7 @@ constexpr int kSAW = kSAT / 64;      // waves
 __device__ __forceinline__ void block_sum16(float (&part)[sNS], float* red, int lane, int wid) {
     group_reduce_scatter<sNS, 16>(part, lane);  // lane%16 -> partial of sample lane%16 over its 16-lane group
     float v = part[0];
-    v += __shfl_xor(v, 16, PDVC_WAVE);
+    v += lane_swap(v, 16);
     v += __shfl_xor(v, 32, PDVC_WAVE);
     if (lane < sNS) red[wid * sNS + lane] = v;
     __syncthreads();

@@ -6,7 +6,7 @@
 // ~18 us.  Here pass 1 splits the rows into `parts` slabs (enough workgroups to fill the chip); a workgroup sums
 // one slab for 64 consecutive columns (16 lanes own one float4 column group each and 16 row lanes take
 // interleaved rows: a wave-instruction reads 4 rows x 256 B) and writes one partial row; pass 2 adds the
-// `parts` (<= 64) partial rows.  Deterministic (fixed order), no atomics, no memset.  HBM-bound: rows*cols*4 bytes read.
+// `parts` (<= 256) partial rows over 16 lanes per column group.  Deterministic (fixed order), no atomics, no memset.  HBM-bound: rows*cols*4 bytes read.
 #include "pdvc_common.h"
 
 namespace pdvc {

@@ -36,12 +36,12 @@ __device__ __forceinline__ bool keep_elem(uint64_t seed, uint32_t head_idx, uint
 
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
-    for (int d = 32; d > 0; d >>= 1) v = fmaxf(v, __shfl_xor(v, d, PDVC_WAVE));
+    for (int d = 32; d > 0; d >>= 1) v = fmaxf(v, lane_swap(v, d));
     return v;
 }
 __device__ __forceinline__ float wave_add(float v) {
 #pragma unroll
-    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, PDVC_WAVE);
+    for (int d = 32; d > 0; d >>= 1) v += lane_swap(v, d);
     return v;
 }
 
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(const float* __restri
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) mx = fmaxf(mx, kval[kb] ? s[kb][r] : -INFINITY);
 #pragma unroll
-        for (int d = 16; d > 0; d >>= 1) mx = fmaxf(mx, __shfl_xor(mx, d, PDVC_WAVE));
+        for (int d = 16; d > 0; d >>= 1) mx = fmaxf(mx, lane_swap(mx, d));
         float e[4], sum = 0.f;
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) {
@@ -364,7 +364,7 @@ __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(const float* __restri
             sum += e[kb];
         }
 #pragma unroll
-        for (int d = 16; d > 0; d >>= 1) sum += __shfl_xor(sum, d, PDVC_WAVE);
+        for (int d = 16; d > 0; d >>= 1) sum += lane_swap(sum, d);
         const float inv = 1.f / sum;
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) {

@@ -59,7 +59,7 @@ __device__ __forceinline__ int lvl_sel(const int (&v)[kL], int l) {
 template <int LPH>
 __device__ __forceinline__ float group_max(float v) {
 #pragma unroll
-    for (int d = 1; d < LPH; d <<= 1) v = fmaxf(v, d <= 8 ? grp_swap(v, d) : __shfl_xor(v, d, PDVC_WAVE));
+    for (int d = 1; d < LPH; d <<= 1) v = fmaxf(v, lane_swap(v, d));
     return v;
 }
 

@@ -19,21 +19,28 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
     return base + slot;
 }
 
-// Partner exchange for butterfly step d (1, 2, 4, 8) inside aligned 16-lane groups, on the DPP network (a VALU
-// operand modifier: no LDS traffic, no lane-index arithmetic, unlike __shfl_xor's ds_bpermute).  d = 1, 2, 8
-// are exact xors (quad_perm, row_ror:8); d = 4 pairs lane i with 7 - i inside its 8-lane half (row_half_mirror).
-// Any involution that flips bit d and keeps the bits above d inside the group gives the same sums in
-// allreduce / max / reduce-scatter butterflies whose steps run from high d to low or low to high.
+// Exact xor-partner exchange for butterfly step d (1, 2, 4, 8) inside aligned 16-lane groups without
+// ds_bpermute's lane-index arithmetic: d = 1, 2 on DPP quad_perm, d = 8 on DPP row_ror:8 (VALU operand
+// modifiers, no LDS traffic), d = 4 on ds_swizzle's bit mode (gfx9 DPP has no xor-4 pattern; row_half_mirror
+// would pair lanes across more than one bit, which is wrong for partial reductions over the higher bits only).
 __device__ __forceinline__ float grp_swap(float v, int d) {
     const int x = __float_as_int(v);
     int r;
     switch (d) {
         case 1: r = __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false); break;   // quad_perm(1,0,3,2)
         case 2: r = __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false); break;   // quad_perm(2,3,0,1)
-        case 4: r = __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false); break;  // row_half_mirror
-        default: r = __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false); break;  // row_ror:8
+        case 4: r = __builtin_amdgcn_ds_swizzle(x, 0x1F | (0x04 << 10)); break;         // lane ^ 4
+        default: r = __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false); break;  // row_ror:8 = lane ^ 8
     }
     return __int_as_float(r);
+}
+
+// butterfly partner for any step d of a wave-wide reduction: DPP for d <= 8, ds_swizzle (exact xor inside
+// 32-lane halves) for d = 16, ds_bpermute for d = 32
+__device__ __forceinline__ float lane_swap(float v, int d) {
+    if (d <= 8) return grp_swap(v, d);
+    if (d == 16) return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1F | (0x10 << 10)));
+    return __shfl_xor(v, d, PDVC_WAVE);
 }
 
 // the lane with index k inside each aligned group of G (<= 32) lanes, for every lane of the group
@@ -62,7 +69,7 @@ __device__ __forceinline__ float grp_bcast(float v, int k) {
 template <int G>
 __device__ __forceinline__ float group_allreduce(float v) {
 #pragma unroll
-    for (int d = G >> 1; d > 0; d >>= 1) v += (d <= 8) ? grp_swap(v, d) : __shfl_xor(v, d, PDVC_WAVE);
+    for (int d = G >> 1; d > 0; d >>= 1) v += lane_swap(v, d);
     return v;
 }
 
@@ -82,7 +89,7 @@ __device__ __forceinline__ void group_reduce_scatter(float (&v)[K], int lane) {
             if (i < half) {
                 // value I send = the half I do not keep; value I receive lands on the half I keep
                 const float send = upper ? v[i] : v[i + half];
-                const float recv = (d <= 8) ? grp_swap(send, d) : __shfl_xor(send, d, PDVC_WAVE);
+                const float recv = lane_swap(send, d);
                 const float mine = upper ? v[i + half] : v[i];
                 v[i] = mine + recv;
             }
