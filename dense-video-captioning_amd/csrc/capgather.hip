@@ -179,8 +179,10 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const float gv = active ? g[u][c] : 0.f;
-            if (ok0[u]) atomicAdd(gvbase + (size_t)(st + x0[u]) * MD + LPH * c, nw[u] * gv);
-            if (ok1[u]) atomicAdd(gvbase + (size_t)(st + x0[u] + 1) * MD + LPH * c, ne[u] * gv);
+            if (grad_value) {  // NULL: the value gradient comes from cap_value_grad_kernel after all steps
+                if (ok0[u]) atomicAdd(gvbase + (size_t)(st + x0[u]) * MD + LPH * c, nw[u] * gv);
+                if (ok1[u]) atomicAdd(gvbase + (size_t)(st + x0[u] + 1) * MD + LPH * c, ne[u] * gv);
+            }
             s += gv * ((ok1[u] ? v1[u][c] : 0.f) - (ok0[u] ? v0[u][c] : 0.f));  // gix = -vnw + vne
         }
         part[u] = s;
@@ -226,6 +228,169 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
             if (RD == 2) atomicAdd(grad_ref + ((size_t)r * cL + l) * RD + 1, v1);
         }
     }
+}
+
+// -------------------------------------------------------------------------------------------------
+// Value gradient of the caption sampling, all decoder steps at once, destination-sorted (no float atomics).
+// The per-step backward (cap_gather_bwd_kernel with grad_value == NULL) leaves the value gradient out; after
+// the recurrence this kernel sums, for every value row, the contributions of the samples of every step whose
+// border-clipped corners touch it: row t of level l gets  sum_{x0(s) = t} nw_s g_s + sum_{x0(s) = t-1} ne_s g_s
+// over the samples s = (step, row of the video, point of level l), g_s the sample's gradient row (D floats).
+// One 512-thread workgroup per (video, head, level): an LDS counting sort of its samples by key x0 + 1, then
+// each wave walks a contiguous row range (balanced by sample count) with two running accumulators -- the
+// mapping of msda1d_bwd_value_kernel (msda1d.hip) with per-sample gradient rows.  Every row is written once
+// (zeros where no sample lands), so grad_value needs no memset; with `accumulate` a later chunk of steps adds.
+// The per-step kernel's atomics were 2 x 134 MB per step at 512 videos, capped by the ~1.3 TB/s atomic rate.
+// -------------------------------------------------------------------------------------------------
+constexpr int kCVW = 8;  // waves per workgroup
+
+template <int CW>  // channels per lane: D <= 64 * CW, channel = lane + 64 c
+__global__ __launch_bounds__(kCVW * 64) void cap_value_grad_kernel(
+    const uint8_t* __restrict__ vmask, CapLevels lv, int S, int M, int D, int R, int s0, int ns, int accumulate,
+    const int32_t* __restrict__ vr_start, const int32_t* __restrict__ vr_rows, const float* __restrict__ save_loc,
+    const float* __restrict__ gsamp, float* __restrict__ grad_value) {
+    extern __shared__ __attribute__((aligned(16))) int lds_c[];
+    __shared__ int wsum[kCVW];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int l = lb % cL;
+    const int bm = lb / cL;
+    const int b = bm / M, m = bm - b * M;
+    const int T = lv.T[0] * (l == 0) + lv.T[1] * (l == 1) + lv.T[2] * (l == 2) + lv.T[3] * (l == 3);
+    const int st = lv.start[0] * (l == 0) + lv.start[1] * (l == 1) + lv.start[2] * (l == 2) + lv.start[3] * (l == 3);
+    const int rb0 = vr_start[b], nr = vr_start[b + 1] - rb0;
+    const int per_step = nr * cP;
+    const int n = ns * per_step;
+    int* off = lds_c;                // [T + 2]
+    int* cur = lds_c + (T + 2);      // [T + 2]
+    int* sq = lds_c + 2 * (T + 2);   // [n] gradient row of each sorted sample
+    float* clo = (float*)(sq + n);   // [n] nw (0 where the corner is masked) -> row x0
+    float* chi = clo + n;            // [n] ne (0 where x0 + 1 is outside or masked) -> row x0 + 1
+    const uint8_t* mrow = vmask ? vmask + (size_t)b * S + st : nullptr;
+    for (int i = threadIdx.x; i < T + 2; i += blockDim.x) off[i] = 0;
+    __syncthreads();
+    auto sample = [&](int i, int& gidx) -> float {  // clipped pixel coordinate of sample i; gidx its gradient row
+        const int step = s0 + i / per_step, rem = i - (i / per_step) * per_step;
+        const int r = vr_rows[rb0 + rem / cP], j = l * cP + rem % cP;
+        const size_t si = (((size_t)step * R + r) * M + m) * cNS + j;
+        gidx = (int)si;
+        float gm;
+        return border_ix(save_loc[si], T, gm);
+    };
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        int gidx;
+        const float ix = sample(i, gidx);
+        atomicAdd(&off[(int)floorf(ix) + 1], 1);
+    }
+    __syncthreads();
+    {  // exclusive scan of off[0 .. T+1]
+        const int len = T + 2;
+        const int per = (len + blockDim.x - 1) / blockDim.x;
+        const int i0 = threadIdx.x * per;
+        int tot = 0;
+        for (int i = i0; i < i0 + per && i < len; ++i) tot += off[i];
+        int inc = tot;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += y;
+        }
+        if (lane == 63) wsum[wid] = inc;
+        __syncthreads();
+        int base = 0;
+        for (int w = 0; w < wid; ++w) base += wsum[w];
+        int run = base + inc - tot;
+        for (int i = i0; i < i0 + per && i < len; ++i) {
+            const int c = off[i];
+            off[i] = run;
+            cur[i] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        int gidx;
+        const float ix = sample(i, gidx);
+        const float xf = floorf(ix);
+        const int x0 = (int)xf;
+        const bool ok0 = !(mrow && mrow[x0]);
+        const bool ok1 = x0 + 1 < T && !(mrow && mrow[x0 + 1]);
+        const int pos = atomicAdd(&cur[x0 + 1], 1);
+        sq[pos] = gidx;
+        clo[pos] = ok0 ? ((float)(x0 + 1) - ix) : 0.f;
+        chi[pos] = ok1 ? (ix - xf) : 0.f;
+    }
+    __syncthreads();
+    const int total = off[T + 1];
+    auto split = [&](int w) -> int {
+        if (w <= 0) return 0;
+        if (w >= kCVW) return T;
+        const int target = (int)(((long)total * w) / kCVW);
+        int lo = 0, hi = T;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (off[mid] >= target) hi = mid;
+            else lo = mid + 1;
+        }
+        return lo;
+    };
+    const int r0 = split(wid), r1 = split(wid + 1);
+    if (r0 >= r1) return;
+    const size_t MD = (size_t)M * D;
+    float* ob = grad_value + ((size_t)b * S + st) * MD + (size_t)m * D;
+    float accp[CW], acch[CW];
+#pragma unroll
+    for (int c = 0; c < CW; ++c) accp[c] = acch[c] = 0.f;
+    int k = r0;
+    auto close_bucket = [&]() {  // bucket k complete: row k-1 has both its corners
+        const int r = k - 1;
+        if (r >= r0) {
+            float* orow = ob + (size_t)r * MD;
+#pragma unroll
+            for (int c = 0; c < CW; ++c) {
+                const int ch = lane + 64 * c;
+                if (ch < D) {
+                    float v = accp[c];
+                    if (accumulate) v += orow[ch];
+                    orow[ch] = v;
+                }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+            accp[c] = acch[c];
+            acch[c] = 0.f;
+        }
+        ++k;
+    };
+    const int jb = off[r0], je = off[r1 + 1];
+    constexpr int U = 4;
+    for (int j0 = jb; j0 < je; j0 += U) {
+        float gv[U][CW];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = (j0 + u < je) ? j0 + u : je - 1;
+            const float* gp = gsamp + (size_t)sq[j] * D;
+#pragma unroll
+            for (int c = 0; c < CW; ++c) {
+                const int ch = lane + 64 * c;
+                gv[u][c] = gp[ch < D ? ch : 0];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = j0 + u;
+            if (j >= je) break;
+            while (j >= off[k + 1]) close_bucket();
+            const float cl = clo[j], chh = chi[j];
+#pragma unroll
+            for (int c = 0; c < CW; ++c) {
+                accp[c] = fmaf(cl, gv[u][c], accp[c]);
+                acch[c] = fmaf(chh, gv[u][c], acch[c]);
+            }
+        }
+    }
+    while (k <= r1) close_bucket();
 }
 
 static int cap_setup(const int32_t* level_T, int num_levels, int num_point, int head_dim, int num_heads, int ref_dim,
@@ -319,5 +484,65 @@ extern "C" int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* v
                      grad_value, grad_offsets, grad_ref)
     }
     PDVC_CHECK_LAUNCH("cap_gather_bwd_kernel");
+    return PDVC_OK;
+}
+
+extern "C" int pdvc_cap_value_grad_f32(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels,
+                                       int batch, int num_heads, int head_dim, int num_point, int rows, int steps,
+                                       int max_rows_per_video, const int32_t* video_row_start,
+                                       const int32_t* video_rows, const float* save_loc, const float* grad_samples,
+                                       float* grad_value, void* stream) {
+    CapLevels lv;
+    int S = 0;
+    PDVC_CHECK_ARG(level_T != nullptr && num_levels == cL && num_point == cP, "caption value gradient needs %d x %d",
+                   cL, cP);
+    for (int l = 0; l < cL; ++l) {
+        PDVC_CHECK_ARG(level_T[l] > 0, "level %d has non-positive length", l);
+        lv.T[l] = level_T[l];
+        lv.start[l] = S;
+        S += level_T[l];
+    }
+    PDVC_CHECK_ARG(head_dim > 0 && head_dim <= 512, "head_dim must be in [1, 512], got %d", head_dim);
+    PDVC_CHECK_ARG(batch >= 0 && num_heads > 0 && rows >= 0 && steps >= 0 && max_rows_per_video >= 0, "invalid sizes");
+    hipStream_t s = (hipStream_t)stream;
+    const long nblk = (long)batch * num_heads * cL;
+    if (nblk == 0) return PDVC_OK;
+    if (steps == 0 || max_rows_per_video == 0) {
+        hipError_t e = hipMemsetAsync(grad_value, 0, sizeof(float) * (size_t)batch * S * num_heads * head_dim, s);
+        return e == hipSuccess ? PDVC_OK : pdvc_set_error(PDVC_ERR_LAUNCH, "memset: %s", hipGetErrorString(e));
+    }
+    int Tmax = 0;
+    for (int l = 0; l < cL; ++l) Tmax = lv.T[l] > Tmax ? lv.T[l] : Tmax;
+    const long budget = 96 * 1024 - 8L * (Tmax + 2);
+    const long per_step = 12L * max_rows_per_video * cP;  // LDS bytes per step of samples
+    PDVC_CHECK_ARG(budget >= per_step, "too many caption rows per video (%d) for one step in LDS", max_rows_per_video);
+    const int chunk = (int)(budget / per_step);
+    static bool attr = false;
+    if (!attr) {
+        const void* ks[4] = {(const void*)cap_value_grad_kernel<1>, (const void*)cap_value_grad_kernel<2>,
+                             (const void*)cap_value_grad_kernel<4>, (const void*)cap_value_grad_kernel<8>};
+        for (const void* k : ks)
+            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) != hipSuccess) {
+                (void)hipGetLastError();
+                return pdvc_set_error(PDVC_ERR_LAUNCH, "cap_value_grad_kernel: cannot raise the LDS limit");
+            }
+        attr = true;
+    }
+    const int cw = head_dim <= 64 ? 1 : head_dim <= 128 ? 2 : head_dim <= 256 ? 4 : 8;
+    for (int s0 = 0; s0 < steps; s0 += chunk) {
+        const int ns = steps - s0 < chunk ? steps - s0 : chunk;
+        const size_t lds = sizeof(int) * (2 * (size_t)(Tmax + 2) + 3 * (size_t)ns * max_rows_per_video * cP);
+        const int acc = s0 > 0;
+        const dim3 grid((unsigned)nblk), block(kCVW * 64);
+#define CVG(CW) hipLaunchKernelGGL((cap_value_grad_kernel<CW>), grid, block, lds, s, value_pad_mask, lv, S, num_heads, \
+                                   head_dim, rows, s0, ns, acc, video_row_start, video_rows, save_loc, grad_samples,     \
+                                   grad_value)
+        if (cw == 1) CVG(1);
+        else if (cw == 2) CVG(2);
+        else if (cw == 4) CVG(4);
+        else CVG(8);
+#undef CVG
+        PDVC_CHECK_LAUNCH("cap_value_grad_kernel");
+    }
     return PDVC_OK;
 }

@@ -205,9 +205,11 @@ class LSTMDSACaptioner(Captioner):
         return lstm_cell(gates, c)
 
     def decode_teacher_forced(self, hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten, level_T, seq,
-                              n_steps):
+                              n_steps, video_csr=None):
         """hs_rows (R, d) event features; ref_rows (R, L, 2) references (rows < rd1_rows are 1-d: centre in
-        [..., 0]); row_video (R,) int32; memory (N, S, d); seq (R, K) long; returns logprobs (R, n_steps, V)."""
+        [..., 0]); row_video (R,) int32; memory (N, S, d); seq (R, K) long; returns logprobs (R, n_steps, V).
+        video_csr (start, rows, max rows per video) of row_video lets the backward sum the value gradient of all
+        steps in one destination-sorted pass (no float atomics)."""
         core = self.core
         w = self._step_weights()
         value, mask_u8 = self._prepare(memory, mask_flatten)
@@ -221,7 +223,7 @@ class LSTMDSACaptioner(Captioner):
         Hs = CaptionDecodeFunction.apply(
             value.view(Nv, S, M, -1), xg, off_hs, ref_rows, w["W_h"], w["b_h"], core.ctx2att.weight,
             core.ctx2att.bias, core.alpha_net.weight.view(-1), core.alpha_net.bias, w["W_att"], mask_u8, row_video,
-            tuple(level_T), rd1_rows)
+            tuple(level_T), rd1_rows, video_csr)
         return F.log_softmax(self.logit(self.dropout(Hs)), dim=-1)
 
     @torch.no_grad()

@@ -29,7 +29,7 @@ class CaptionDecodeFunction(Function):
 
     @staticmethod
     def forward(ctx, value, xg, off_hs, ref, W_h, b_h, W_ctx, b_ctx, alpha_w, alpha_b, W_att, pad_mask, row_video,
-                level_T, rd1_rows):
+                level_T, rd1_rows, video_csr=None):
         value, xg, off_hs, ref = value.contiguous(), xg.contiguous(), off_hs.contiguous(), ref.contiguous()
         W_h, W_ctx, W_att = W_h.contiguous(), W_ctx.contiguous(), W_att.contiguous()
         alpha_w, alpha_b = alpha_w.contiguous(), alpha_b.contiguous()
@@ -77,7 +77,7 @@ class CaptionDecodeFunction(Function):
                     _n.ptr(CS[i - 1] if i > 0 else zero), R, H, ho, ldo, _n.ptr(CS[i]), _n.ptr(ACTS[i]), st)
         ctx.save_for_backward(value, off_hs, ref, W_h, W_ctx, alpha_w, W_att, pad_mask, row_video, HP, CLIP, LOC,
                               ATT, PROBS, RES, ACTS, CS, HS)
-        ctx.meta = (tuple(level_T), int(rd1_rows))
+        ctx.meta = (tuple(level_T), int(rd1_rows), video_csr)
         return HS
 
     @staticmethod
@@ -85,7 +85,7 @@ class CaptionDecodeFunction(Function):
     def backward(ctx, dHS):
         (value, off_hs, ref, W_h, W_ctx, alpha_w, W_att, pad_mask, row_video, HP, CLIP, LOC, ATT, PROBS, RES, ACTS,
          CS, HS) = ctx.saved_tensors
-        level_T, rd1_rows = ctx.meta
+        level_T, rd1_rows, video_csr = ctx.meta
         dHS = dHS.contiguous()
         Nv, S, M, D = value.shape
         n, R, Ph = HP.shape
@@ -101,16 +101,20 @@ class CaptionDecodeFunction(Function):
         dATT = torch.empty((n, R * M * NS, A), **kw)
         GAW = torch.empty((n, R * M, A), **kw)
         GAB = torch.empty((n, R * M), **kw)
-        dCLIP = torch.empty((R, M, NS, D), **kw)
+        # with the rows' per-video CSR, every step's sample gradient is kept and the value gradient is one
+        # destination-sorted pass after the loop (pdvc_cap_value_grad_f32) instead of per-step atomics
+        deferred = video_csr is not None
+        dCLIP_all = torch.empty((n if deferred else 1, R, M, NS, D), **kw)
         dRES = torch.empty((R, M * D), **kw)
         dh = torch.empty((R, H), **kw)
         dc = [torch.empty((R, H), **kw), torch.empty((R, H), **kw)]
         zero = torch.zeros((R, H), **kw)
-        gv = torch.zeros_like(value)
+        gv = torch.empty_like(value) if deferred else torch.zeros_like(value)
         gr = torch.zeros_like(ref) if ctx.needs_input_grad[3] else None
         st = _n.stream()
         for i in reversed(range(n)):
             last = i == n - 1
+            dCLIP = dCLIP_all[i if deferred else 0]
             gh_, ldgh = _n.rows(dHS[:, i])
             dg, lddg = _n.rows(dHP[i][:, n_off + A:])
             _n.call("pdvc_lstm_cell_backward_f32", gh_, ldgh, None if last else _n.ptr(dh), H,
@@ -125,9 +129,13 @@ class CaptionDecodeFunction(Function):
             dCLIP.view(-1, D).addmm_(dATT[i], W_ctx)
             _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video),
                     _n.ptr(HP[i]), Ph, 0, _n.ptr(off_hs), _n.ptr(ref), RD, rd1_rows, lvl, nl, Nv, R, M, D, NS // nl,
-                    _n.ptr(LOC[i]), _n.ptr(dCLIP), _n.ptr(gv), _n.ptr(dHP[i]), _n.ptr(gr), st)
+                    _n.ptr(LOC[i]), _n.ptr(dCLIP), None if deferred else _n.ptr(gv), _n.ptr(dHP[i]), _n.ptr(gr), st)
             if i > 0:
                 torch.mm(dHP[i], W_h, out=dh)
+        if deferred:
+            vr_start, vr_rows, max_rows = video_csr
+            _n.call("pdvc_cap_value_grad_f32", _n.ptr(pad_mask), lvl, nl, Nv, M, D, NS // nl, R, n, int(max_rows),
+                    _n.ptr(vr_start), _n.ptr(vr_rows), _n.ptr(LOC), _n.ptr(dCLIP_all), _n.ptr(gv), st)
         # weight gradients: one GEMM each over every (step, row)
         d_gates = dHP[..., n_off + A:]                       # (n, R, 4H), row stride Ph
         d_xg = d_gates.permute(1, 0, 2).contiguous()
@@ -144,4 +152,4 @@ class CaptionDecodeFunction(Function):
         dalpha_b = GAB.sum().reshape(1)
         dW_att = wgrad_mm(d_gates.reshape(-1, G), RES.view(-1, M * D))
         return (gv, d_xg, d_off_hs, gr, dW_h, db_h, dW_ctx, db_ctx, dalpha_w, dalpha_b, dW_att, None, None, None,
-                None)
+                None, None)

@@ -113,7 +113,7 @@ def colsum(x):
             and x.data_ptr() % 16 == 0):
         return x.sum(0)
     cblocks = (cols // 4 + 15) // 16
-    parts = max(1, min(64, (2 * CU) // cblocks, rows // 64))
+    parts = max(1, min(256, (8 * CU) // cblocks, rows // 64))  # >= 8 workgroups per CU on wide gradients
     ws = torch.empty(parts * cols, dtype=x.dtype, device=x.device)
     out = torch.empty(cols, dtype=x.dtype, device=x.device)
     _n.call("pdvc_colsum_f32", _n.ptr(x), rows, cols, parts, _n.ptr(ws), _n.ptr(out), _n.stream())

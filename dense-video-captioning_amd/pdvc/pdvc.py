@@ -38,6 +38,23 @@ def decide_two_stage(transformer_input_type, dt, criterion):
                               f"MI355X path (BASELINE configs use 'queries')")
 
 
+# PDVC_CAP_DEFERRED=0: per-step float atomics for the caption value gradient (A/B switch)
+_CAP_DEFERRED = os.environ.get("PDVC_CAP_DEFERRED", "1") != "0"
+
+
+def _video_csr(rows, N):
+    """Host CSR of the caption rows of each video (rows: tuples whose [1] is the video): (start (N+1,),
+    row indices grouped by video, largest row count of a video)."""
+    by_video = [[] for _ in range(N)]
+    for i, r in enumerate(rows):
+        by_video[r[1]].append(i)
+    start = [0]
+    for v in range(N):
+        start.append(start[-1] + len(by_video[v]))
+    flat = [i for v in range(N) for i in by_video[v]]
+    return start, flat, max((len(b) for b in by_video), default=0)
+
+
 class MLP(nn.Module):
     def __init__(self, input_dim, hidden_dim, output_dim, num_layers):
         super().__init__()
@@ -250,10 +267,11 @@ class PDVC(nn.Module):
             # (cached on dt, so a captured step graph re-uses device tensors and copies nothing)
             key = ("_caption_rows", Ld, N, Q, tuple(ix.block for ix in layer_indices))
             if key not in dt:
+                vr_start, vr_rows, max_rows = _video_csr(rows, N)
                 dt[key] = hostio.pack_to_device(
                     [r_p, r_k, r_base, r_cap, [r[1] for r in rows], [r[0] for r in rows], [r[1] for r in rows],
-                     last_sel], dev)
-            rp, rk, rb, rc, row_video, lay, vid, last_sel_d = dt[key]
+                     last_sel, vr_start, vr_rows], dev) + [max_rows]
+            rp, rk, rb, rc, row_video, lay, vid, last_sel_d, vr_start_d, vr_rows_d, max_rows = dt[key]
             flat_idx = rb + m.queries[rp, rk]
             cap_rows = rc + m.targets[rp, rk]
         else:
@@ -266,9 +284,10 @@ class PDVC(nn.Module):
             rows.sort(key=lambda r: (0 if r[0] == 0 else 1))
             last_sel = [i for i, r in enumerate(rows) if r[0] == Ld_last]
             # every per-row index array in ONE asynchronous host->device copy
-            flat_idx, cap_rows, row_video, lay, vid, last_sel_d = hostio.pack_to_device(
+            vr_start, vr_rows, max_rows = _video_csr(rows, N)
+            flat_idx, cap_rows, row_video, lay, vid, last_sel_d, vr_start_d, vr_rows_d = hostio.pack_to_device(
                 [[r[2] for r in rows], [r[3] for r in rows], [r[1] for r in rows], [r[0] for r in rows],
-                 [r[1] for r in rows], last_sel], dev)
+                 [r[1] for r in rows], last_sel, vr_start, vr_rows], dev)
         row_video = row_video.to(torch.int32)
         rd1 = sum(1 for r in rows if r[0] == 0 and init_reference.shape[-1] == 1)
         hs_rows = hs.reshape(Ld * N * Q, C).index_select(0, flat_idx)
@@ -286,8 +305,9 @@ class PDVC(nn.Module):
         steps_v = []
         for v in range(N):
             steps_v.append(caption_steps(cap_cpu[cap_off[v]:cap_off[v + 1]]))
+        video_csr = (vr_start_d.to(torch.int32), vr_rows_d.to(torch.int32), max_rows)
         return dict(rows=rows, hs_rows=hs_rows, ref_rows=ref_rows.contiguous(), rd1=rd1, row_video=row_video,
-                    cap_rows=cap_rows, lay=lay, vid=vid, last_sel=last_sel_d, steps_v=steps_v)
+                    cap_rows=cap_rows, lay=lay, vid=vid, last_sel=last_sel_d, steps_v=steps_v, video_csr=video_csr)
 
     def parallel_prediction_matched(self, dt, criterion, hs, init_reference, inter_references, others,
                                     disable_refine, heads=None):
@@ -310,7 +330,8 @@ class PDVC(nn.Module):
         if self.share_caption_head:
             logprobs = self.caption_head[0].decode_teacher_forced(
                 R["hs_rows"], R["ref_rows"], R["rd1"], R["row_video"], others["memory"], others["mask_flatten"],
-                others["level_T"], seq_rows, n_steps)
+                others["level_T"], seq_rows, n_steps,
+                video_csr=R["video_csr"] if _CAP_DEFERRED else None)
         else:
             raise NotImplementedError("share_caption_head=0 is not supported on the batched caption path")
         cap_loss = self.caption_head[0].build_loss(logprobs, seq_rows[:, 1:], cap_mask_rows[:, 1:].float())

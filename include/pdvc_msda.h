@@ -38,6 +38,8 @@
  *   pdvc_groupnorm_rows_*           <- nn.GroupNorm(32, d) of the base encoder's pyramid levels
  *                                      (pdvc/base_encoder.py:32-41), on channels-last rows
  *   pdvc_colsum_f32                 <- the bias gradients (sum over rows of dY) of those nn.Linear layers
+ *   pdvc_cap_value_grad_f32         <- the value-gradient half of the caption sampling's backward
+ *                                      (grid_sample backward in ms_deform_attn_core_pytorch), all steps at once
  *   pdvc_level_pos_rows_*           <- the encoder's positional input: PositionEmbeddingSine per level
  *                                      (position_encoding.py:20-75) + level_embed + the concatenation over levels
  *                                      (deformable_transformer.py:100-112)
@@ -242,6 +244,17 @@ int pdvc_groupnorm_rows_backward_f32(const float* x, const float* dy, const floa
  * workspace: parts*cols floats (partial sums of `parts` row slabs, 1 <= parts); out 16-byte aligned.
  * Deterministic. */
 int pdvc_colsum_f32(const float* x, int rows, int cols, int parts, float* workspace, float* out, void* stream);
+
+/* ---- caption value gradient over all decoder steps -----------------------------------------------------
+ * grad_value (batch, S, num_heads, head_dim), fully written (accumulation-free, no atomics): the value gradient
+ * of pdvc_cap_gather_* for `steps` teacher-forced steps at once, from save_loc (steps, rows, num_heads, 16) and
+ * grad_samples (steps, rows, num_heads, 16, head_dim) -- pdvc_cap_gather_backward_f32 called with
+ * grad_value == NULL leaves this part out.  video_row_start (batch + 1) / video_rows (rows): DEVICE int32 CSR
+ * of the caption rows of each video; max_rows_per_video bounds its row counts (host). */
+int pdvc_cap_value_grad_f32(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels, int batch,
+                            int num_heads, int head_dim, int num_point, int rows, int steps, int max_rows_per_video,
+                            const int32_t* video_row_start, const int32_t* video_rows, const float* save_loc,
+                            const float* grad_samples, float* grad_value, void* stream);
 
 /* ---- encoder positional input ------------------------------------------------------------------------
  * pos[n, s, c] = (c < F ? (c even ? sin : cos)(xe[n*S + s] / dim_t[c]) : dur[n*Dd + c - F])

@@ -52,3 +52,44 @@ def test_version_and_errors(lib):
 def test_native_binding_table_matches_header():
     from pdvc import _native
     assert set(_native.SIGNATURES) <= set(declared_symbols())
+
+
+def declared_prototypes():
+    """name -> list of parameter kinds ('p' pointer, 'i' integer/enum, 'f' floating) from include/*.h."""
+    protos = {}
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"//[^\n]*", "", src)
+        for name, params in re.findall(r"\b(pdvc_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", src):
+            kinds = []
+            for prm in params.split(","):
+                prm = prm.strip()
+                if not prm or prm == "void":
+                    continue
+                kinds.append("p" if "*" in prm else "f" if re.search(r"\b(float|double)\b", prm) else "i")
+            protos[name] = kinds
+    return protos
+
+
+def test_native_binding_argument_kinds_match_header():
+    """Each ctypes argtypes list in pdvc/_native.py has the header's parameter count, with pointers where the
+    prototype has pointers and scalars where it has scalars."""
+    from pdvc import _native
+    protos = declared_prototypes()
+    bad = []
+    for name, argtypes in _native.SIGNATURES.items():
+        want = protos.get(name)
+        assert want is not None, f"{name}: no prototype parsed"
+        got = []
+        for t in argtypes:
+            if t in (ctypes.c_float, ctypes.c_double):
+                got.append("f")
+            elif t in (ctypes.c_int, ctypes.c_long, ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint32,
+                       ctypes.c_size_t, ctypes.c_longlong, ctypes.c_ulonglong):
+                got.append("i")
+            else:
+                got.append("p")
+        if got != want:
+            bad.append(f"{name}: binding {''.join(got)} vs header {''.join(want)}")
+    assert not bad, "\n".join(bad)

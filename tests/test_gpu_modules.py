@@ -225,11 +225,13 @@ def test_captioner_vs_golden(ref_dim):
     close(lp, d["sample_logprobs"], 1e-4, "greedy logprobs")
 
 
-@pytest.mark.parametrize("heads,rd1", [(1, 3), (2, 0)])
-def test_caption_decode_function_matches_step_loop(heads, rd1):
+@pytest.mark.parametrize("heads,rd1,deferred", [(1, 3, False), (2, 0, False), (1, 3, True), (2, 0, True)])
+def test_caption_decode_function_matches_step_loop(heads, rd1, deferred):
     """The fused teacher-forced recurrence (ops/functions/caption_decode.py) against the per-step autograd
     loop of the same math (LSTMDSACaptioner._step: cap-gather kernel + torch ops), at the PDVC caption shape
-    (d=512, A=512, H=512, 16 samples) with a mix of 1-d and (c, len) reference rows."""
+    (d=512, A=512, H=512, 16 samples) with a mix of 1-d and (c, len) reference rows. deferred: the value
+    gradient of all steps comes from the destination-sorted pass (pdvc_cap_value_grad_f32) over the per-video
+    row CSR instead of per-step atomics; video 2 has no rows."""
     import types
     from pdvc.CaptioningHead.LSTM_DSA import LSTMDSACaptioner
     opt = types.SimpleNamespace(
@@ -242,14 +244,21 @@ def test_caption_decode_function_matches_step_loop(heads, rd1):
         for p in cap.parameters():
             p.normal_(0, 0.03)
     T_l = (64, 32, 16, 8)
-    Nv, R, n = 2, 9, 7
+    Nv, R, n = 3, 9, 7
     S = sum(T_l)
     memory = torch.randn(Nv, S, 512, device=DEV)
     mask = torch.zeros(Nv, S, dtype=torch.bool, device=DEV)
     mask[1, -5:] = True
     hs = torch.randn(R, 512, device=DEV)
     ref = torch.rand(R, 4, 2, device=DEV) * 0.8 + 0.1
-    row_video = torch.tensor([0, 1, 0, 1, 0, 1, 1, 0, 0], dtype=torch.int32, device=DEV)
+    rv = [0, 1, 0, 1, 0, 1, 1, 0, 0]
+    row_video = torch.tensor(rv, dtype=torch.int32, device=DEV)
+    starts, flat = [0], []
+    for v in range(Nv):
+        flat += [i for i in range(R) if rv[i] == v]
+        starts.append(len(flat))
+    video_csr = (torch.tensor(starts, dtype=torch.int32, device=DEV),
+                 torch.tensor(flat, dtype=torch.int32, device=DEV), max(rv.count(v) for v in range(Nv)))
     seq = torch.randint(1, 51, (R, n + 1), device=DEV)
     g = torch.randn(R, n, 51, device=DEV)
 
@@ -257,7 +266,8 @@ def test_caption_decode_function_matches_step_loop(heads, rd1):
         ins = [t.clone().requires_grad_() for t in (hs, ref, memory)]
         cap.zero_grad(set_to_none=True)
         if fused:
-            out = cap.decode_teacher_forced(ins[0], ins[1], rd1, row_video, ins[2], mask, T_l, seq, n)
+            out = cap.decode_teacher_forced(ins[0], ins[1], rd1, row_video, ins[2], mask, T_l, seq, n,
+                                            video_csr=video_csr if deferred else None)
         else:
             w = cap._step_weights()
             value, mask_u8 = cap._prepare(ins[2], mask)
@@ -286,3 +296,45 @@ def test_caption_decode_function_matches_step_loop(heads, rd1):
     assert set(gp1) == set(gp0)
     for k in gp0:
         close(gp1[k], gp0[k], 1e-4, k)
+
+
+def test_caption_value_grad_chunked_steps():
+    """Many caption rows on one video (220 rows x 4 points x 12 B per step) overflow the LDS of one launch of
+    the destination-sorted value-gradient pass, so its steps run in several accumulating chunks; the memory
+    gradient must match the per-step atomic path of the same fused recurrence."""
+    import types
+    from pdvc.CaptioningHead.LSTM_DSA import LSTMDSACaptioner
+    opt = types.SimpleNamespace(
+        vocab_size=30, input_encoding_size=512, rnn_size=512, num_layers=1, drop_prob=0.0, max_caption_len=24,
+        clip_context_dim=512, cap_nheads=1, att_hid_size=512, wordRNN_input_feats_type="C", hidden_dim=512,
+        cap_num_feature_levels=4, cap_dec_n_points=4, num_feature_levels=4, event_context_dim=None)
+    torch.manual_seed(1)
+    cap = LSTMDSACaptioner(opt).to(DEV)
+    with torch.no_grad():
+        for p in cap.parameters():
+            p.normal_(0, 0.03)
+    T_l = (128, 64, 32, 16)
+    Nv, R, n = 2, 240, 20
+    memory = torch.randn(Nv, sum(T_l), 512, device=DEV)
+    mask = torch.zeros(Nv, sum(T_l), dtype=torch.bool, device=DEV)
+    mask[0, -7:] = True
+    hs = torch.randn(R, 512, device=DEV)
+    ref = torch.rand(R, 4, 2, device=DEV) * 0.9 + 0.05
+    rv = [0 if i % 12 else 1 for i in range(R)]
+    row_video = torch.tensor(rv, dtype=torch.int32, device=DEV)
+    starts, flat = [0], []
+    for v in range(Nv):
+        flat += [i for i in range(R) if rv[i] == v]
+        starts.append(len(flat))
+    video_csr = (torch.tensor(starts, dtype=torch.int32, device=DEV),
+                 torch.tensor(flat, dtype=torch.int32, device=DEV), max(rv.count(v) for v in range(Nv)))
+    assert 12 * video_csr[2] * 4 * n > 96 * 1024  # more than one chunk
+    seq = torch.randint(1, 31, (R, n + 1), device=DEV)
+    g = torch.randn(R, n, 31, device=DEV)
+
+    def run(csr):
+        m = memory.clone().requires_grad_()
+        out = cap.decode_teacher_forced(hs, ref, 5, row_video, m, mask, T_l, seq, n, video_csr=csr)
+        (out * g).sum().backward()
+        return m.grad
+    close(run(video_csr), run(None), 1e-4, "grad_memory")
