@@ -28,6 +28,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+F32_MFMA_PEAK_TFS = 157.3  # MI355X dense FP32 matrix peak (MI355X_MICROARCH.md: no xf32 on gfx950)
+GEMM_OPS = ("aten::mm", "aten::addmm", "aten::addmm_", "aten::bmm", "aten::baddbmm")
 
 
 def parse():
@@ -53,6 +55,8 @@ def parse():
                         "trunk: only the static-shape trunk graphed (base encoder .. heads); none: eager")
     p.add_argument("--gemm", choices=["hip", "torch"], default=None,
                    help="projection GEMMs on pdvc_gemm_f32 (hip) or torch/hipBLASLt (default: PDVC_GEMM or torch)")
+    p.add_argument("--no-gemm-roofline", action="store_true",
+                   help="skip the profiled eager step that prices the projection GEMMs against the MFMA peak")
     p.add_argument("--gemm-table", choices=["auto", "off"], default="auto",
                    help="auto: library GEMMs use the pre-tuned solution table (pdvc/gemm_tuning.py) when present")
     return p.parse_args()
@@ -75,6 +79,50 @@ def msda_alg_bytes(meta, kind):
     if kind == "fwd":
         return N * S * M * D * e + N * Lq * M * NS * 12 + N * Lq * M * D * e
     return 3 * N * S * M * D * e + N * Lq * M * D * e + 2 * N * Lq * M * NS * 12
+
+
+def gemm_flops(name, shapes):
+    """2*m*n*k of one aten GEMM call from its recorded input shapes (0 if the shapes are not recorded)."""
+    try:
+        if name == "aten::mm":
+            (m, k), (_, n) = shapes[0], shapes[1]
+            return 2 * m * n * k
+        if name in ("aten::addmm", "aten::addmm_"):
+            (m, k), (_, n) = shapes[1], shapes[2]
+            return 2 * m * n * k
+        if name == "aten::bmm":
+            (b, m, k), (_, _, n) = shapes[0], shapes[1]
+            return 2 * b * m * n * k
+        if name == "aten::baddbmm":
+            (b, m, k), (_, _, n) = shapes[1], shapes[2]
+            return 2 * b * m * n * k
+    except (ValueError, IndexError, TypeError):
+        return 0
+    return 0
+
+
+def gemm_roofline(step_fn):
+    """MFMA roofline of the projection GEMMs: one eager training step under torch.profiler; every aten GEMM's
+    2mnk flops (its recorded shapes) over the device time of the kernels it launched, summed over the step."""
+    from torch.profiler import ProfilerActivity, profile
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+        step_fn()
+        torch.cuda.synchronize()
+    flops, dev_us, calls = 0, 0.0, 0
+    for e in prof.key_averages(group_by_input_shape=True):
+        if e.key in GEMM_OPS:
+            flops += gemm_flops(e.key, e.input_shapes) * e.count
+            dev_us += e.device_time_total
+            calls += e.count
+    if dev_us <= 0:
+        return None
+    ach = flops / (dev_us * 1e-6) / 1e12
+    return {"kernel": "projection / FFN / LSTM / logit GEMMs (hipBLASLt, tuned table)", "bound": "mfma",
+            "achieved": ach, "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": ach / F32_MFMA_PEAK_TFS,
+            "traffic": None, "gemm_calls_per_step": calls, "gflop_per_step": flops / 1e9,
+            "gemm_device_ms_per_step": dev_us / 1e3,
+            "timing": "torch.profiler device time of every aten GEMM in 1 eager step after the timed steps"}
 
 
 def cpu_baseline(a, budget_s):
@@ -211,6 +259,7 @@ def main():
         timing_note = ("HIP events around every launch in 2 eager steps right after the timed (hipGraph) steps, "
                        "same shapes; step wall time excludes them")
     ks = timer.summary()
+    groof = None if a.no_gemm_roofline else gemm_roofline(eager_step)
     videos = a.steps * B * world
     result = {
         "metric": "videos/sec fwd+bwd (PDVC, T=512 C=768 L=4 Q=100) at 1/2/4/8 MI355X",
@@ -245,6 +294,9 @@ def main():
                               "traffic": traffic, "traffic_source": tsrc, "avg_launch_us": avg_ms * 1e3,
                               "timing": timing_note,
                               "alg_bytes_per_launch": avg_bytes}
+    if groof is not None:
+        groof["share_of_step"] = groof["gemm_device_ms_per_step"] / (1e3 * el / a.steps)
+        result["roofline_mfma"] = groof
     ksteps = 2 if graphed else a.steps
     result["kernels"] = {n: {"launches": v["launches"], "avg_us": 1e3 * v["ms"] / max(v["launches"], 1),
                              "share_of_step": v["ms"] / ksteps / (1e3 * el / a.steps)} for n, v in ks.items()}
