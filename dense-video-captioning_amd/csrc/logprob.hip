@@ -1,0 +1,157 @@
+// logprob.hip -- the caption head's word log-probabilities and the log-probability of the target word, both ways
+// (reference: Captioner.get_logprobs_state, LSTM_DSA.py:112-116: logprobs = log_softmax(logit(dropout(h))), and
+// LanguageModelCriterion / build_loss, LSTM_DSA.py:48-52: -sum_t logp[t, target_t] * mask_t / sum mask).
+//
+// Forward: one workgroup per (caption row, step) -- a row of V logits (V = 5748 on ActivityNet, 1609 on YouCook2).
+// One pass keeps a per-lane running (max, sum of exp) pair over the row, the pairs merge across the workgroup,
+// and a second pass (the row is in L2 by then) writes logp = (x - max) - log(sum) -- torch's log_softmax
+// arithmetic -- and the row's target entry picked = logp[target].  torch needed log_softmax, a gather, and in
+// the backward a zero-fill of a (rows, V) tensor, a scatter and log_softmax_backward: ~5 full passes.
+// Backward: the loss reaches the logits only through `picked`, so
+//     dlogits[j] = g * ([j == target] - exp(logp[j]))
+// one read of logp and one write of dlogits per element, no (rows, V) one-hot or zero fill.
+// HBM-bound: forward 12 bytes per element (x read ~2x, the second from L2; logp written), backward 8.
+#include <math.h>
+
+#include "pdvc_common.h"
+
+namespace pdvc {
+
+constexpr int kLpThreads = 256;
+
+// merge two (max, sum of exp(x - max)) pairs
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+    if (m2 > m) {
+        s = s * expf(m - m2) + s2;
+        m = m2;
+    } else if (m2 > -INFINITY) {
+        s += s2 * expf(m2 - m);
+    }
+}
+
+__device__ __forceinline__ void lse_add(float& m, float& s, float x) {
+    if (x > m) {
+        s = s * expf(m - x) + 1.f;
+        m = x;
+    } else {
+        s += expf(x - m);
+    }
+}
+
+template <bool VEC4>
+__global__ __launch_bounds__(kLpThreads) void logprob_pick_fwd_kernel(const float* __restrict__ x,
+                                                                     const int64_t* __restrict__ target, int V,
+                                                                     float* __restrict__ logp,
+                                                                     float* __restrict__ picked) {
+    __shared__ float red_m[kLpThreads / PDVC_WAVE], red_s[kLpThreads / PDVC_WAVE];
+    const long row = blockIdx.x;
+    const float* xr = x + row * (long)V;
+    float* lr = logp + row * (long)V;
+    float m = -INFINITY, s = 0.f;
+    if (VEC4) {
+        const int v4 = V / 4;
+        const float4* x4 = reinterpret_cast<const float4*>(xr);
+        for (int i = threadIdx.x; i < v4; i += kLpThreads) {
+            const float4 a = x4[i];
+            lse_add(m, s, a.x); lse_add(m, s, a.y); lse_add(m, s, a.z); lse_add(m, s, a.w);
+        }
+    } else {
+        for (int i = threadIdx.x; i < V; i += kLpThreads) lse_add(m, s, xr[i]);
+    }
+#pragma unroll
+    for (int d = 1; d < PDVC_WAVE; d <<= 1) {
+        const float m2 = lane_swap(m, d), s2 = lane_swap(s, d);
+        lse_merge(m, s, m2, s2);
+    }
+    const int wave = threadIdx.x / PDVC_WAVE, lane = threadIdx.x % PDVC_WAVE;
+    if (lane == 0) {
+        red_m[wave] = m;
+        red_s[wave] = s;
+    }
+    __syncthreads();
+    m = red_m[0];
+    s = red_s[0];
+#pragma unroll
+    for (int w = 1; w < kLpThreads / PDVC_WAVE; ++w) lse_merge(m, s, red_m[w], red_s[w]);
+    const float ls = logf(s);
+    if (VEC4) {
+        const int v4 = V / 4;
+        const float4* x4 = reinterpret_cast<const float4*>(xr);
+        float4* l4 = reinterpret_cast<float4*>(lr);
+        for (int i = threadIdx.x; i < v4; i += kLpThreads) {
+            const float4 a = x4[i];
+            l4[i] = make_float4((a.x - m) - ls, (a.y - m) - ls, (a.z - m) - ls, (a.w - m) - ls);
+        }
+    } else {
+        for (int i = threadIdx.x; i < V; i += kLpThreads) lr[i] = (xr[i] - m) - ls;
+    }
+    if (threadIdx.x == 0) {
+        const int64_t t = target[row];
+        // an out-of-range target poisons the loss (torch's gather would raise a device-side assert)
+        picked[row] = (t >= 0 && t < V) ? (xr[t] - m) - ls : NAN;
+    }
+}
+
+template <bool VEC4>
+__global__ __launch_bounds__(kLpThreads) void logprob_pick_bwd_kernel(const float* __restrict__ logp,
+                                                                     const int64_t* __restrict__ target,
+                                                                     const float* __restrict__ gpick, int V,
+                                                                     float* __restrict__ dx) {
+    const long row = blockIdx.x;
+    const float g = gpick[row];
+    const int64_t t = target[row];
+    const float* lr = logp + row * (long)V;
+    float* dr = dx + row * (long)V;
+    if (VEC4) {
+        const int v4 = V / 4;
+        const float4* l4 = reinterpret_cast<const float4*>(lr);
+        float4* d4 = reinterpret_cast<float4*>(dr);
+        for (int i = threadIdx.x; i < v4; i += kLpThreads) {
+            const float4 a = l4[i];
+            const int j = 4 * i;
+            d4[i] = make_float4(g * ((j == t ? 1.f : 0.f) - expf(a.x)), g * ((j + 1 == t ? 1.f : 0.f) - expf(a.y)),
+                                g * ((j + 2 == t ? 1.f : 0.f) - expf(a.z)),
+                                g * ((j + 3 == t ? 1.f : 0.f) - expf(a.w)));
+        }
+    } else {
+        for (int j = threadIdx.x; j < V; j += kLpThreads) dr[j] = g * ((j == t ? 1.f : 0.f) - expf(lr[j]));
+    }
+}
+
+}  // namespace pdvc
+
+using namespace pdvc;
+
+extern "C" int pdvc_logprob_pick_forward_f32(const float* logits, const int64_t* target, int rows, int V,
+                                             float* logp, float* picked, void* stream) {
+    PDVC_CHECK_ARG(rows >= 0 && V > 0, "invalid sizes (rows >= 0, V > 0)");
+    PDVC_CHECK_ARG(rows == 0 || (logits && target && logp && picked), "null pointer");
+    if (rows == 0) return PDVC_OK;
+    const bool vec4 = (V % 4) == 0 && ((uintptr_t)logits % 16) == 0 && ((uintptr_t)logp % 16) == 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (vec4)
+        hipLaunchKernelGGL(logprob_pick_fwd_kernel<true>, dim3((unsigned)rows), dim3(kLpThreads), 0, s, logits,
+                           target, V, logp, picked);
+    else
+        hipLaunchKernelGGL(logprob_pick_fwd_kernel<false>, dim3((unsigned)rows), dim3(kLpThreads), 0, s, logits,
+                           target, V, logp, picked);
+    PDVC_CHECK_LAUNCH("logprob_pick_fwd_kernel");
+    return PDVC_OK;
+}
+
+extern "C" int pdvc_logprob_pick_backward_f32(const float* logp, const int64_t* target, const float* grad_picked,
+                                              int rows, int V, float* grad_logits, void* stream) {
+    PDVC_CHECK_ARG(rows >= 0 && V > 0, "invalid sizes (rows >= 0, V > 0)");
+    PDVC_CHECK_ARG(rows == 0 || (logp && target && grad_picked && grad_logits), "null pointer");
+    if (rows == 0) return PDVC_OK;
+    const bool vec4 = (V % 4) == 0 && ((uintptr_t)logp % 16) == 0 && ((uintptr_t)grad_logits % 16) == 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (vec4)
+        hipLaunchKernelGGL(logprob_pick_bwd_kernel<true>, dim3((unsigned)rows), dim3(kLpThreads), 0, s, logp,
+                           target, grad_picked, V, grad_logits);
+    else
+        hipLaunchKernelGGL(logprob_pick_bwd_kernel<false>, dim3((unsigned)rows), dim3(kLpThreads), 0, s, logp,
+                           target, grad_picked, V, grad_logits);
+    PDVC_CHECK_LAUNCH("logprob_pick_bwd_kernel");
+    return PDVC_OK;
+}

@@ -27,6 +27,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from pdvc.ops.functions import CaptionDecodeFunction
+from pdvc.ops.functions.logprob import logprob_pick
 from pdvc.ops.modules import MSDeformAttnCap
 from pdvc.ops.modules.linear import Linear
 
@@ -114,6 +115,13 @@ class Captioner(nn.Module):
         instead of a (rows, steps, vocab) one-hot product."""
         max_len = input.shape[1]
         picked = input.gather(2, target[:, :max_len, None]).squeeze(2)
+        return -(picked * mask[:, :max_len]).sum(1) / (mask.sum(1) + 1e-6)
+
+    @staticmethod
+    def build_loss_picked(picked, mask):
+        """build_loss from the target log-probabilities already gathered (decode_teacher_forced(pick_target=...)):
+        -(sum_t picked_t * mask_t) / (sum mask + 1e-6), the same per-row values (LSTM_DSA.py:48-52)."""
+        max_len = picked.shape[1]
         return -(picked * mask[:, :max_len]).sum(1) / (mask.sum(1) + 1e-6)
 
 
@@ -205,16 +213,19 @@ class LSTMDSACaptioner(Captioner):
         return lstm_cell(gates, c)
 
     def decode_teacher_forced(self, hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten, level_T, seq,
-                              n_steps, video_csr=None):
+                              n_steps, video_csr=None, pick_target=None):
         """hs_rows (R, d) event features; ref_rows (R, L, 2) references (rows < rd1_rows are 1-d: centre in
         [..., 0]); row_video (R,) int32; memory (N, S, d); seq (R, K) long; returns logprobs (R, n_steps, V).
         video_csr (start, rows, max rows per video) of row_video lets the backward sum the value gradient of all
-        steps in one destination-sorted pass (no float atomics)."""
+        steps in one destination-sorted pass (no float atomics).  With pick_target (R, >= n_steps) long, returns
+        (logprobs, picked) where picked (R, n_steps) = logprobs at the target words (csrc/logprob.hip: log_softmax
+        and the loss's gather in one pass, the backward in one pass -- the input of build_loss_picked)."""
         core = self.core
         w = self._step_weights()
         value, mask_u8 = self._prepare(memory, mask_flatten)
         if n_steps == 0:
-            return hs_rows.new_zeros(hs_rows.shape[0], 0, self.vocab_size + 1)
+            empty = hs_rows.new_zeros(hs_rows.shape[0], 0, self.vocab_size + 1)
+            return empty if pick_target is None else (empty, hs_rows.new_zeros(hs_rows.shape[0], 0))
         xt = embed_rows(self.embed, seq[:, :n_steps])  # (R, n, E)
         xg = F.linear(xt, w["W_x"]) + F.linear(hs_rows, w["W_hs"])[:, None]  # loop-invariant gate parts
         off_hs = F.linear(hs_rows, w["W_off_hs"], w["b_off"])
@@ -224,7 +235,10 @@ class LSTMDSACaptioner(Captioner):
             value.view(Nv, S, M, -1), xg, off_hs, ref_rows, w["W_h"], w["b_h"], core.ctx2att.weight,
             core.ctx2att.bias, core.alpha_net.weight.view(-1), core.alpha_net.bias, w["W_att"], mask_u8, row_video,
             tuple(level_T), rd1_rows, video_csr)
-        return F.log_softmax(self.logit(self.dropout(Hs)), dim=-1)
+        logits = self.logit(self.dropout(Hs))
+        if pick_target is not None:
+            return logprob_pick(logits, pick_target[:, :n_steps])
+        return F.log_softmax(logits, dim=-1)
 
     @torch.no_grad()
     def decode_greedy(self, hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten, level_T, max_len=None):

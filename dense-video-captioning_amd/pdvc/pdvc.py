@@ -40,6 +40,9 @@ def decide_two_stage(transformer_input_type, dt, criterion):
 
 # PDVC_CAP_DEFERRED=0: per-step float atomics for the caption value gradient (A/B switch)
 _CAP_DEFERRED = os.environ.get("PDVC_CAP_DEFERRED", "1") != "0"
+# caption log-probabilities and the loss's target gather in one HIP pass each way (csrc/logprob.hip);
+# PDVC_LOGPROB_FUSED=0 keeps torch's log_softmax + gather (same-box A/B)
+_LOGPROB_FUSED = os.environ.get("PDVC_LOGPROB_FUSED", "1") != "0"
 
 
 def _video_csr(rows, N):
@@ -331,10 +334,15 @@ class PDVC(nn.Module):
             logprobs = self.caption_head[0].decode_teacher_forced(
                 R["hs_rows"], R["ref_rows"], R["rd1"], R["row_video"], others["memory"], others["mask_flatten"],
                 others["level_T"], seq_rows, n_steps,
-                video_csr=R["video_csr"] if _CAP_DEFERRED else None)
+                video_csr=R["video_csr"] if _CAP_DEFERRED else None,
+                pick_target=seq_rows[:, 1:] if _LOGPROB_FUSED else None)
         else:
             raise NotImplementedError("share_caption_head=0 is not supported on the batched caption path")
-        cap_loss = self.caption_head[0].build_loss(logprobs, seq_rows[:, 1:], cap_mask_rows[:, 1:].float())
+        if _LOGPROB_FUSED:
+            logprobs, picked = logprobs
+            cap_loss = self.caption_head[0].build_loss_picked(picked, cap_mask_rows[:, 1:].float())
+        else:
+            cap_loss = self.caption_head[0].build_loss(logprobs, seq_rows[:, 1:], cap_mask_rows[:, 1:].float())
         # per (layer, video) mean over events, then mean over videos (= the reference's batch-1 losses)
         rows = R["rows"]
         key = R["lay"] * N + R["vid"]

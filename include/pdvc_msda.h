@@ -45,6 +45,8 @@
  *                                      (deformable_transformer.py:100-112)
  *   pdvc_relu_dropout_*             <- dropout(relu(.)) between the two FFN linears of every transformer layer
  *                                      (deformable_transformer.py:140-145 encoder, :233-237 decoder)
+ *   pdvc_logprob_pick_*             <- log_softmax of the caption logits (LSTM_DSA.py:112-116) fused with the
+ *                                      caption loss's target gather (LSTM_DSA.py:48-52), and its backward
  *   pdvc_gemm_f32                   <- the dense projections (nn.Linear forward/backward) of the layers
  *                                      above: MSDeformAttn value/offset/output projections
  *                                      (ms_deform_attn.py:79-126), the FFNs (deformable_transformer.py:150-156,
@@ -128,8 +130,9 @@ int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_pad_mask, c
                             int num_heads, int head_dim, int num_point, float* output, float* save_attn,
                             float* save_loc, void* stream);
 /* grad_value (N,S,M,D) (zero on padded rows); grad_proj (N,Lq,proj_stride): only the offset and logit
- * slots are written; grad_ref (N,Lq,L,ref_dim) or NULL.  `output` is the forward's output (the softmax
- * backward's row term sum_j a_j dL/da_j is computed as <grad_output, output>). */
+ * slots are written; grad_ref (N,Lq,L,ref_dim) or NULL.  `output` is the forward's output or NULL: the softmax
+ * backward's row term sum_j a_j dL/da_j is computed as <grad_output, output> when it is given, else summed over
+ * the sampled values themselves (no second read of a (N,Lq,M*D) tensor; the default). */
 int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value_pad_mask, const float* ref,
                              int ref_dim, const float* proj, int proj_stride, int off_base, int logit_base,
                              const int32_t* level_T, int num_levels, int batch, int num_query, int num_heads,
@@ -276,6 +279,18 @@ int pdvc_relu_dropout_forward_f32(float* h, long rows, int cols, float p, uint64
                                   void* stream);
 int pdvc_relu_dropout_backward_f32(const float* hd, float* grad, int rows, int cols, float p, int parts,
                                    float* workspace, float* dbias, void* stream);
+
+/* ---- caption word log-probabilities + target pick ----------------------------------------------------
+ * Replaces log_softmax(logit(.)) (LSTM_DSA.py:112-116) and the target gather of the caption loss
+ * (LSTM_DSA.py:48-52) for rows = caption rows x steps, V = vocabulary + 1 (row-major, row stride V).
+ * forward: logp[r, :] = (x[r, :] - max) - log(sum exp(x[r, :] - max)); picked[r] = logp[r, target[r]]
+ *          (NaN when target[r] is outside [0, V)).
+ * backward (the loss depends on the logits only through picked): grad_logits[r, j] =
+ *          grad_picked[r] * ([j == target[r]] - exp(logp[r, j])).  target: int64, one per row. */
+int pdvc_logprob_pick_forward_f32(const float* logits, const int64_t* target, int rows, int V, float* logp,
+                                  float* picked, void* stream);
+int pdvc_logprob_pick_backward_f32(const float* logp, const int64_t* target, const float* grad_picked, int rows,
+                                   int V, float* grad_logits, void* stream);
 
 /* ---- fp32 GEMM on the matrix cores ----------------------------------------------------------------
  * C[M,N] = op(A)[M,K] op(B)[K,N] (+ bias[N]) (ReLU).  op(A): trans_a 0 -> A[m*lda + k], 1 -> A[k*lda + m];

@@ -1,0 +1,68 @@
+"""GPU parity of the fused caption log-probabilities + target pick (pdvc/ops/functions/logprob.py,
+csrc/logprob.hip) against the reference chain log_softmax -> gather -> masked sum (LSTM_DSA.py:48-52,
+112-116) in float64 torch: values, the logits gradient through the loss, and a gradient arriving on logp
+itself.  Both kernel forms: V % 4 == 0 (ActivityNet, 5748, float4 lanes) and V % 4 != 0 (YouCook2, 1609)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL = 1e-5  # fp32 vs float64 reference, relative to max(1, |reference|)
+
+
+def close(a, b, tol, what):
+    a, b = a.detach().double(), b.detach().double()
+    assert a.shape == b.shape, f"{what}: {tuple(a.shape)} vs {tuple(b.shape)}"
+    err = (a - b).abs().max().item() if a.numel() else 0.0
+    scale = max(1.0, b.abs().max().item() if b.numel() else 1.0)
+    assert err <= tol * scale, f"{what}: max|diff| {err:.3e} > {tol:.0e} * {scale:.3g}"
+
+
+@pytest.mark.parametrize("V", [5748, 1609, 7, 300])
+def test_logprob_pick_matches_log_softmax_gather(V):
+    from pdvc.ops.functions.logprob import logprob_pick
+    g = torch.Generator().manual_seed(V)
+    R, n = 37, 6
+    logits = (torch.randn(R, n, V, generator=g) * 4).to(DEV)
+    target = torch.randint(0, V, (R, n), generator=g).to(DEV)
+    target[0, :] = 0
+    target[1, :] = V - 1
+    mask = (torch.rand(R, n, generator=g) > 0.3).float().to(DEV)
+    x = logits.clone().requires_grad_(True)
+    logp, picked = logprob_pick(x, target)
+    loss = (-(picked * mask).sum(1) / (mask.sum(1) + 1e-6)).sum()
+    loss.backward()
+    xr = logits.double().clone().requires_grad_(True)
+    lr = torch.log_softmax(xr, -1)
+    pr = lr.gather(2, target[:, :, None]).squeeze(2)
+    (-(pr * mask.double()).sum(1) / (mask.double().sum(1) + 1e-6)).sum().backward()
+    close(logp, lr, TOL, "logp")
+    close(picked, pr, TOL, "picked")
+    close(x.grad, xr.grad, TOL, "grad logits")
+
+
+def test_logprob_pick_gradient_on_logp_too():
+    from pdvc.ops.functions.logprob import logprob_pick
+    g = torch.Generator().manual_seed(3)
+    R, n, V = 9, 4, 5748
+    logits = torch.randn(R, n, V, generator=g).to(DEV)
+    target = torch.randint(0, V, (R, n), generator=g).to(DEV)
+    w = torch.randn(R, n, V, generator=g).to(DEV)
+    x = logits.clone().requires_grad_(True)
+    logp, picked = logprob_pick(x, target)
+    ((logp * w).sum() + picked.sum()).backward()
+    xr = logits.double().clone().requires_grad_(True)
+    lr = torch.log_softmax(xr, -1)
+    ((lr * w.double()).sum() + lr.gather(2, target[:, :, None]).sum()).backward()
+    close(x.grad, xr.grad, TOL, "grad logits (logp + picked)")
+
+
+def test_logprob_pick_bad_target_poisons_and_empty_rows():
+    from pdvc.ops.functions.logprob import logprob_pick
+    x = torch.randn(2, 3, 16, device=DEV)
+    t = torch.tensor([[0, 16, 3], [-1, 2, 15]], device=DEV)
+    _, picked = logprob_pick(x, t)
+    p = picked.cpu()
+    assert torch.isnan(p[0, 1]) and torch.isnan(p[1, 0]) and torch.isfinite(p[0, 0]) and torch.isfinite(p[1, 2])
+    logp, picked = logprob_pick(torch.randn(0, 3, 16, device=DEV), torch.zeros(0, 3, dtype=torch.long, device=DEV))
+    assert logp.shape == (0, 3, 16) and picked.shape == (0, 3)
