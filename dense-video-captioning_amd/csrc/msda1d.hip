@@ -332,8 +332,11 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
 
 // -------------------------------------------------------------------------------------------------
 // backward, query side: grad of the offset and attention logits (+ reference points)
-// softmax backward uses delta = sum_j a_j dL/da_j = <dL/dout, out> (out = the forward output of this head),
-// so every level's samples are finished as soon as they are reduced -- no state carried across levels.
+// softmax backward needs delta = sum_j a_j dL/da_j over the 16 samples of a (query, head).  Default (fout NULL):
+// each level's owner lanes keep their (a_j, dL/da_j) pair in registers -- one pair per lane per level -- and the
+// lane group sums a_j dL/da_j after the last level (the order of the reference's autograd softmax backward
+// over grad_attn_weight).  With fout: delta = <dL/dout, out> (out = the forward output of this head), read as a
+// second 256-B row per (query, head), which lets every level finish as soon as it is reduced.
 // grad_ref sums over the heads of a query, which live in different waves: atomics (zeroed by the host).
 // -------------------------------------------------------------------------------------------------
 template <int CPL, int LPH, int RD>
@@ -355,13 +358,19 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
     const size_t sbase = ((size_t)w.row * M + w.m) * kNS;
     const int c0 = w.sub * CPL;
 
-    VecF<CPL> g, o;
+    VecF<CPL> g;
     g.load(gout + (size_t)w.row * MD + (size_t)w.m * D + c0);
-    o.load(fout + (size_t)w.row * MD + (size_t)w.m * D + c0);
-    float dl = 0.f;
+    float delta = 0.f;
+    if (fout) {  // wave-uniform
+        VecF<CPL> o;
+        o.load(fout + (size_t)w.row * MD + (size_t)w.m * D + c0);
+        float dl = 0.f;
 #pragma unroll
-    for (int c = 0; c < CPL; ++c) dl += g.v[c] * o.v[c];
-    const float delta = group_allreduce<LPH>(dl);
+        for (int c = 0; c < CPL; ++c) dl += g.v[c] * o.v[c];
+        delta = group_allreduce<LPH>(dl);
+    }
+    float keep_ga[kL];  // dL/da of this lane's owned sample per level, and sum of a dL/da (fout == NULL)
+    float dl_own = 0.f;
 
     // parameter phase: corner row and (masked) corner weights of the lane's samples
     int i0v[JPL];
@@ -459,8 +468,10 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
                 g1 = t2 * (prow[off_base + w.m * kNS + j] / (float)kP);
             }
             gprow[off_base + w.m * kNS + j] = goff;
-            gprow[logit_base + w.m * kNS + j] = a * (ga - delta);
+            if (fout) gprow[logit_base + w.m * kNS + j] = a * (ga - delta);
         }
+        keep_ga[l] = ga;
+        dl_own += owner ? a * ga : 0.f;
         if (grad_ref) {
             // sum over the query's points of this level (its lane group), one atomic per (query, head, level)
             g0 = group_allreduce<LPH>(g0);
@@ -472,6 +483,20 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
             }
         }
         __builtin_amdgcn_sched_barrier(0);
+    }
+    if (!fout) {
+        delta = group_allreduce<LPH>(dl_own);
+        // the owned sample's point index and ownership do not depend on the level (see the loop above)
+        const int r = w.sub % G;
+        const int p = VPL == 2 ? r : r >> 1;
+        if (w.active && w.sub < G && (VPL == 2 || (r & 1) == 0)) {
+#pragma unroll
+            for (int l = 0; l < kL; ++l) {
+                const int j = l * kP + p;
+                const float a = save_attn[sbase + j];  // re-read (cached) rather than held across the levels
+                gprow[logit_base + w.m * kNS + j] = a * (keep_ga[l] - delta);
+            }
+        }
     }
 }
 
@@ -866,7 +891,7 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
     Geometry g;
     if ((rc = pick_geometry(num_heads, head_dim, g))) return rc;
     PDVC_CHECK_ARG(ref_dim == 1 || ref_dim == 2, "ref_dim must be 1 or 2, got %d", ref_dim);
-    PDVC_CHECK_ARG(save_attn && save_loc && output, "backward needs the forward's output, save_attn and save_loc");
+    PDVC_CHECK_ARG(save_attn && save_loc, "backward needs the forward's save_attn and save_loc");
     const int NSM = num_heads * kNS;
     PDVC_CHECK_ARG(off_base >= 0 && logit_base >= 0 && off_base + NSM <= proj_stride && logit_base + NSM <= proj_stride,
                    "proj columns out of range");

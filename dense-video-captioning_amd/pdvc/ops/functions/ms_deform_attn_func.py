@@ -8,6 +8,8 @@ and adds the fused 1-D functions PDVC's modules use:
   * MSDA1dFunction   -- softmax + sampling locations + zero-padded gather-reduce (ms_deform_attn.py:167-192)
   * CapGatherFunction -- sampling locations + border raw samples (ms_deform_attn_for_caption.py:92-121)
 """
+import os
+
 import torch
 from torch.autograd import Function
 from torch.autograd.function import once_differentiable
@@ -112,9 +114,15 @@ def msda1d_forward(value, pad_mask, proj, ref, level_T, off_base, logit_base, sa
     return out, save_attn, save_loc
 
 
+# The softmax backward's row term sum_j a_j dL/da_j: summed over the sampled values inside the kernel (default),
+# or PDVC_MSDA_DELTA_OUT=1: computed as <grad_out, out> from the forward output (one more (N,Lq,M*D) read).
+_DELTA_FROM_OUT = os.environ.get("PDVC_MSDA_DELTA_OUT", "0") == "1"
+
+
 def msda1d_backward(value, pad_mask, proj, ref, save_attn, save_loc, out, grad_out, level_T, off_base, logit_base,
                     need_ref=False):
-    """pdvc_msda1d_backward_f32: returns (grad_value, grad_proj, grad_ref or None)."""
+    """pdvc_msda1d_backward_f32: returns (grad_value, grad_proj, grad_ref or None).  `out` (the forward output)
+    is passed to the kernel only under PDVC_MSDA_DELTA_OUT=1."""
     N, S, M, D = value.shape
     Lq, C = proj.shape[1], proj.shape[2]
     RD = ref.shape[3]
@@ -123,8 +131,8 @@ def msda1d_backward(value, pad_mask, proj, ref, save_attn, save_loc, out, grad_o
     gp = torch.zeros_like(proj) if C != 2 * M * NUM_SAMPLES else torch.empty_like(proj)
     gr = torch.empty_like(ref) if need_ref else None
     _n.call("pdvc_msda1d_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(ref), RD, _n.ptr(proj), C,
-            off_base, logit_base, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(grad_out), _n.ptr(out),
-            _n.ptr(save_attn), _n.ptr(save_loc), _n.ptr(gv), _n.ptr(gp), _n.ptr(gr), _n.stream(),
+            off_base, logit_base, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(grad_out),
+            _n.ptr(out) if _DELTA_FROM_OUT else None, _n.ptr(save_attn), _n.ptr(save_loc), _n.ptr(gv), _n.ptr(gp), _n.ptr(gr), _n.stream(),
             meta=(N, Lq, S, M, D, NUM_SAMPLES))
     return gv, gp, gr
 
