@@ -9,6 +9,8 @@
 // lstm_cell: nn.LSTM's cell for 1 layer, 1 step, no bias (LSTM_DSA.py:206-207,261): gates = sum of up to
 //   three pre-activation parts (the GEMM outputs of the hoisted input part, the attention part and W_hh h),
 //   gate order (i, f, g, o), c' = f c + i g, h' = o tanh(c').  One lane per (row, unit).
+#include <stdlib.h>
+
 #include "pdvc_common.h"
 
 namespace pdvc {
@@ -152,6 +154,188 @@ __global__ __launch_bounds__(kSAT) void softattn_bwd_kernel(const float* __restr
     }
 }
 
+// float4 forms of the two kernels above (A, D, the row strides and the pointers 16-byte aligned -- PDVC's
+// A = D = 512): one 128-thread workgroup per (row, head), a lane owns 4 consecutive channels and issues the 16
+// samples' float4 loads together.  The 512-thread form gave each lane one float per sample row, 8 waves per
+// (row, head) and two workgroup barriers for ~8 KB of reads: latency-bound at ~3x its HBM time.
+template <int NW>
+__device__ __forceinline__ void block_sum16w(float (&part)[sNS], float* red, int lane, int wid) {
+    group_reduce_scatter<sNS, 16>(part, lane);
+    float v = part[0];
+    v += lane_swap(v, 16);
+    v += __shfl_xor(v, 32, PDVC_WAVE);
+    if (lane < sNS) red[wid * sNS + lane] = v;
+    __syncthreads();
+    if (threadIdx.x < sNS) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) t += red[w * sNS + threadIdx.x];
+        red[NW * sNS + threadIdx.x] = t;
+    }
+    __syncthreads();
+}
+
+constexpr int kSA4T = 128;
+constexpr int kSA4W = kSA4T / 64;
+
+__device__ __forceinline__ float dot4(float4 a, float4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
+
+__global__ __launch_bounds__(kSA4T) void softattn_fwd4_kernel(const float* __restrict__ att,
+                                                              const float* __restrict__ att_h, int ldh,
+                                                              const float* __restrict__ aw, const float* __restrict__ ab,
+                                                              const float* __restrict__ clip, int R, int M, int A,
+                                                              int D, float* __restrict__ res,
+                                                              float* __restrict__ probs) {
+    __shared__ float red[(kSA4W + 1) * sNS];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wg = blockIdx.x;
+    const int r = wg / M;
+    const int A4 = A / 4, D4 = D / 4;
+    const float4* at4 = reinterpret_cast<const float4*>(att + (size_t)wg * sNS * A);
+    const float4* h4 = reinterpret_cast<const float4*>(att_h + (size_t)r * ldh);
+    const float4* w4 = reinterpret_cast<const float4*>(aw);
+    float part[sNS];
+#pragma unroll
+    for (int j = 0; j < sNS; ++j) part[j] = 0.f;
+    for (int a = threadIdx.x; a < A4; a += kSA4T) {
+        const float4 hv = h4[a], wv = w4[a];
+        float4 x[sNS];
+#pragma unroll
+        for (int j = 0; j < sNS; ++j) x[j] = at4[(size_t)j * A4 + a];
+#pragma unroll
+        for (int j = 0; j < sNS; ++j)
+            part[j] += tanhf(x[j].x + hv.x) * wv.x + tanhf(x[j].y + hv.y) * wv.y + tanhf(x[j].z + hv.z) * wv.z +
+                       tanhf(x[j].w + hv.w) * wv.w;
+    }
+    block_sum16w<kSA4W>(part, red, lane, wid);
+    const float* dots = red + kSA4W * sNS;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < sNS; ++j) mx = fmaxf(mx, dots[j] + ab[0]);
+    float p[sNS], sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < sNS; ++j) {
+        p[j] = expf(dots[j] + ab[0] - mx);
+        sum += p[j];
+    }
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int j = 0; j < sNS; ++j) p[j] = p[j] * inv;
+    if (threadIdx.x < sNS) {
+        float pj = 0.f;
+#pragma unroll
+        for (int j = 0; j < sNS; ++j) pj = (j == (int)threadIdx.x) ? p[j] : pj;
+        probs[(size_t)wg * sNS + threadIdx.x] = pj;
+    }
+    const float4* c4 = reinterpret_cast<const float4*>(clip + (size_t)wg * sNS * D);
+    float4* r4 = reinterpret_cast<float4*>(res + (size_t)wg * D);
+    for (int d = threadIdx.x; d < D4; d += kSA4T) {
+        float4 x[sNS];
+#pragma unroll
+        for (int j = 0; j < sNS; ++j) x[j] = c4[(size_t)j * D4 + d];
+        float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < sNS; ++j) {
+            o.x += p[j] * x[j].x;
+            o.y += p[j] * x[j].y;
+            o.z += p[j] * x[j].z;
+            o.w += p[j] * x[j].w;
+        }
+        r4[d] = o;
+    }
+}
+
+__global__ __launch_bounds__(kSA4T) void softattn_bwd4_kernel(const float* __restrict__ att,
+                                                              const float* __restrict__ att_h, int ldh,
+                                                              const float* __restrict__ aw,
+                                                              const float* __restrict__ clip,
+                                                              const float* __restrict__ probs,
+                                                              const float* __restrict__ gres, int R, int M, int A,
+                                                              int D, float* __restrict__ gatt,
+                                                              float* __restrict__ gatt_h, int ldgh,
+                                                              float* __restrict__ gclip, float* __restrict__ gaw_part,
+                                                              float* __restrict__ gab_part) {
+    __shared__ float red[(kSA4W + 1) * sNS];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wg = blockIdx.x;
+    const int r = wg / M;
+    const int A4 = A / 4, D4 = D / 4;
+    float p[sNS];
+#pragma unroll
+    for (int j = 0; j < sNS; ++j) p[j] = probs[(size_t)wg * sNS + j];
+    const float4* c4 = reinterpret_cast<const float4*>(clip + (size_t)wg * sNS * D);
+    float4* gc4 = reinterpret_cast<float4*>(gclip + (size_t)wg * sNS * D);
+    const float4* g4 = reinterpret_cast<const float4*>(gres + (size_t)wg * D);
+    float part[sNS];
+#pragma unroll
+    for (int j = 0; j < sNS; ++j) part[j] = 0.f;
+    for (int d = threadIdx.x; d < D4; d += kSA4T) {
+        const float4 g = g4[d];
+        float4 x[sNS];
+#pragma unroll
+        for (int j = 0; j < sNS; ++j) x[j] = c4[(size_t)j * D4 + d];
+#pragma unroll
+        for (int j = 0; j < sNS; ++j) {
+            part[j] += dot4(g, x[j]);
+            gc4[(size_t)j * D4 + d] = make_float4(p[j] * g.x, p[j] * g.y, p[j] * g.z, p[j] * g.w);
+        }
+    }
+    block_sum16w<kSA4W>(part, red, lane, wid);
+    const float* dp = red + kSA4W * sNS;
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < sNS; ++j) t += p[j] * dp[j];
+    float dd[sNS], sb = 0.f;
+#pragma unroll
+    for (int j = 0; j < sNS; ++j) {
+        dd[j] = p[j] * (dp[j] - t);
+        sb += dd[j];
+    }
+    if (threadIdx.x == 0) gab_part[wg] = sb;
+    const float4* at4 = reinterpret_cast<const float4*>(att + (size_t)wg * sNS * A);
+    float4* ga4 = reinterpret_cast<float4*>(gatt + (size_t)wg * sNS * A);
+    const float4* h4 = reinterpret_cast<const float4*>(att_h + (size_t)r * ldh);
+    const float4* w4 = reinterpret_cast<const float4*>(aw);
+    float4* gh4 = reinterpret_cast<float4*>(gatt_h + (size_t)r * ldgh);
+    float4* gw4 = reinterpret_cast<float4*>(gaw_part + (size_t)wg * A);
+    for (int a = threadIdx.x; a < A4; a += kSA4T) {
+        const float4 hv = h4[a], wv = w4[a];
+        float4 x[sNS];
+#pragma unroll
+        for (int j = 0; j < sNS; ++j) x[j] = at4[(size_t)j * A4 + a];
+        float4 gh = make_float4(0.f, 0.f, 0.f, 0.f), gw = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < sNS; ++j) {
+            const float tx = tanhf(x[j].x + hv.x), ty = tanhf(x[j].y + hv.y), tz = tanhf(x[j].z + hv.z),
+                        tw = tanhf(x[j].w + hv.w);
+            const float4 dpre = make_float4(dd[j] * wv.x * (1.f - tx * tx), dd[j] * wv.y * (1.f - ty * ty),
+                                            dd[j] * wv.z * (1.f - tz * tz), dd[j] * wv.w * (1.f - tw * tw));
+            ga4[(size_t)j * A4 + a] = dpre;
+            gh.x += dpre.x; gh.y += dpre.y; gh.z += dpre.z; gh.w += dpre.w;
+            gw.x += dd[j] * tx; gw.y += dd[j] * ty; gw.z += dd[j] * tz; gw.w += dd[j] * tw;
+        }
+        if (M == 1) {
+            gh4[a] = gh;
+        } else {
+            float* gp = gatt_h + (size_t)r * ldgh + 4 * a;
+            atomicAdd(gp, gh.x); atomicAdd(gp + 1, gh.y); atomicAdd(gp + 2, gh.z); atomicAdd(gp + 3, gh.w);
+        }
+        gw4[a] = gw;
+    }
+}
+
+// PDVC_SOFTATTN_SCALAR=1 keeps the 512-thread kernels (same-box A/B)
+static bool sa_vec4(const void* const* ptrs, int n, int A, int D, int ld1, int ld2) {
+    static const bool scalar = [] {
+        const char* e = getenv("PDVC_SOFTATTN_SCALAR");
+        return e && e[0] == '1';
+    }();
+    if (scalar || A % 4 || D % 4 || ld1 % 4 || ld2 % 4) return false;
+    for (int i = 0; i < n; ++i)
+        if (((uintptr_t)ptrs[i]) % 16) return false;
+    return true;
+}
+
 // gates = a + b + c (each (R,4H) with its own row stride; b or c may be NULL); acts <- (i,f,g,o) activations
 __global__ __launch_bounds__(256) void lstm_fwd_kernel(const float* __restrict__ ga, int lda, const float* __restrict__ gb,
                                                        int ldb, const float* __restrict__ gc, int ldc,
@@ -219,8 +403,13 @@ extern "C" int pdvc_softattn_forward_f32(const float* att, const float* att_h, i
     if (waves == 0) return PDVC_OK;
     PDVC_CHECK_ARG(att_hid > 0 && head_dim > 0 && waves < (1L << 31), "invalid sizes");
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(softattn_fwd_kernel, dim3((unsigned)waves), dim3(kSAT), 0, s, att, att_h, ld_att_h, alpha_w,
-                       alpha_b, clip, rows, num_heads, att_hid, head_dim, att_res, probs);
+    const void* fp[] = {att, att_h, alpha_w, clip, att_res};
+    if (sa_vec4(fp, 5, att_hid, head_dim, ld_att_h, 0))
+        hipLaunchKernelGGL(softattn_fwd4_kernel, dim3((unsigned)waves), dim3(kSA4T), 0, s, att, att_h, ld_att_h,
+                           alpha_w, alpha_b, clip, rows, num_heads, att_hid, head_dim, att_res, probs);
+    else
+        hipLaunchKernelGGL(softattn_fwd_kernel, dim3((unsigned)waves), dim3(kSAT), 0, s, att, att_h, ld_att_h, alpha_w,
+                           alpha_b, clip, rows, num_heads, att_hid, head_dim, att_res, probs);
     PDVC_CHECK_LAUNCH("softattn_fwd_kernel");
     return PDVC_OK;
 }
@@ -240,9 +429,15 @@ extern "C" int pdvc_softattn_backward_f32(const float* att, const float* att_h, 
         if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_att_h: %s", hipGetErrorString(e));
     }
     PDVC_CHECK_ARG(att_hid > 0 && head_dim > 0 && waves < (1L << 31), "invalid sizes");
-    hipLaunchKernelGGL(softattn_bwd_kernel, dim3((unsigned)waves), dim3(kSAT), 0, s, att, att_h, ld_att_h, alpha_w,
-                       clip, probs, grad_res, rows, num_heads, att_hid, head_dim, grad_att, grad_att_h, ld_grad_att_h,
-                       grad_clip, grad_alpha_w_part, grad_alpha_b_part);
+    const void* bp[] = {att, att_h, alpha_w, clip, grad_res, grad_att, grad_att_h, grad_clip, grad_alpha_w_part};
+    if (sa_vec4(bp, 9, att_hid, head_dim, ld_att_h, ld_grad_att_h))
+        hipLaunchKernelGGL(softattn_bwd4_kernel, dim3((unsigned)waves), dim3(kSA4T), 0, s, att, att_h, ld_att_h,
+                           alpha_w, clip, probs, grad_res, rows, num_heads, att_hid, head_dim, grad_att, grad_att_h,
+                           ld_grad_att_h, grad_clip, grad_alpha_w_part, grad_alpha_b_part);
+    else
+        hipLaunchKernelGGL(softattn_bwd_kernel, dim3((unsigned)waves), dim3(kSAT), 0, s, att, att_h, ld_att_h, alpha_w,
+                           clip, probs, grad_res, rows, num_heads, att_hid, head_dim, grad_att, grad_att_h,
+                           ld_grad_att_h, grad_clip, grad_alpha_w_part, grad_alpha_b_part);
     PDVC_CHECK_LAUNCH("softattn_bwd_kernel");
     return PDVC_OK;
 }
