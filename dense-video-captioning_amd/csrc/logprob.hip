@@ -3,14 +3,15 @@
 // LanguageModelCriterion / build_loss, LSTM_DSA.py:48-52: -sum_t logp[t, target_t] * mask_t / sum mask).
 //
 // Forward: one workgroup per (caption row, step) -- a row of V logits (V = 5748 on ActivityNet, 1609 on YouCook2).
-// One pass keeps a per-lane running (max, sum of exp) pair over the row, the pairs merge across the workgroup,
-// and a second pass (the row is in L2 by then) writes logp = (x - max) - log(sum) -- torch's log_softmax
-// arithmetic -- and the row's target entry picked = logp[target].  torch needed log_softmax, a gather, and in
+// For V <= 8192 (V % 4 == 0) the row is held in registers: max, then sum exp(x - max), then
+// logp = (x - max) - log(sum) -- torch's log_softmax arithmetic -- and the row's target entry picked = logp[target].
+// Longer or unaligned rows take a streaming form: a per-lane running (max, sum of exp) pair, merged over the
+// workgroup, and a second pass over the row (in L2 by then).  torch needed log_softmax, a gather, and in
 // the backward a zero-fill of a (rows, V) tensor, a scatter and log_softmax_backward: ~5 full passes.
 // Backward: the loss reaches the logits only through `picked`, so
 //     dlogits[j] = g * ([j == target] - exp(logp[j]))
 // one read of logp and one write of dlogits per element, no (rows, V) one-hot or zero fill.
-// HBM-bound: forward 12 bytes per element (x read ~2x, the second from L2; logp written), backward 8.
+// HBM-bound: forward 8 bytes per element (x read once into registers for V <= 8192, logp written), backward 8.
 #include <math.h>
 
 #include "pdvc_common.h"
@@ -118,6 +119,102 @@ __global__ __launch_bounds__(kLpThreads) void logprob_pick_bwd_kernel(const floa
     }
 }
 
+// Register-resident forms for V <= 4 * kLpThreads * KR (KR float4 per lane: 8192 logits at KR = 8): every load
+// of the row is issued before any arithmetic, the max and then sum exp(x - max) are taken from registers (the
+// order torch's log_softmax uses: no running rescale), and logp is written from the same registers -- the row
+// is read once.  The streaming kernels above serialised one float4 load and four expf per loop trip.
+constexpr int kLpKR = 8;
+
+__device__ __forceinline__ float block_max(float v, float* red) {
+#pragma unroll
+    for (int d = 1; d < PDVC_WAVE; d <<= 1) v = fmaxf(v, lane_swap(v, d));
+    const int wave = threadIdx.x / PDVC_WAVE;
+    __syncthreads();
+    if ((threadIdx.x % PDVC_WAVE) == 0) red[wave] = v;
+    __syncthreads();
+    v = red[0];
+#pragma unroll
+    for (int w = 1; w < kLpThreads / PDVC_WAVE; ++w) v = fmaxf(v, red[w]);
+    return v;
+}
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+#pragma unroll
+    for (int d = 1; d < PDVC_WAVE; d <<= 1) v += lane_swap(v, d);
+    const int wave = threadIdx.x / PDVC_WAVE;
+    __syncthreads();
+    if ((threadIdx.x % PDVC_WAVE) == 0) red[wave] = v;
+    __syncthreads();
+    v = red[0];
+#pragma unroll
+    for (int w = 1; w < kLpThreads / PDVC_WAVE; ++w) v += red[w];
+    return v;
+}
+
+__global__ __launch_bounds__(kLpThreads) void logprob_pick_fwd_reg_kernel(const float* __restrict__ x,
+                                                                         const int64_t* __restrict__ target, int V,
+                                                                         float* __restrict__ logp,
+                                                                         float* __restrict__ picked) {
+    __shared__ float red[kLpThreads / PDVC_WAVE];
+    const long row = blockIdx.x;
+    const int v4 = V / 4;
+    const float4* x4 = reinterpret_cast<const float4*>(x + row * (long)V);
+    float4 r[kLpKR];
+#pragma unroll
+    for (int k = 0; k < kLpKR; ++k) {
+        const int i = threadIdx.x + k * kLpThreads;
+        r[k] = i < v4 ? x4[i] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < kLpKR; ++k) m = fmaxf(m, fmaxf(fmaxf(r[k].x, r[k].y), fmaxf(r[k].z, r[k].w)));
+    m = block_max(m, red);
+    float sm = 0.f;
+#pragma unroll
+    for (int k = 0; k < kLpKR; ++k)
+        if (threadIdx.x + k * kLpThreads < v4)
+            sm += expf(r[k].x - m) + expf(r[k].y - m) + expf(r[k].z - m) + expf(r[k].w - m);
+    const float ls = logf(block_sum(sm, red));
+    float4* l4 = reinterpret_cast<float4*>(logp + row * (long)V);
+#pragma unroll
+    for (int k = 0; k < kLpKR; ++k) {
+        const int i = threadIdx.x + k * kLpThreads;
+        if (i < v4) l4[i] = make_float4((r[k].x - m) - ls, (r[k].y - m) - ls, (r[k].z - m) - ls, (r[k].w - m) - ls);
+    }
+    if (threadIdx.x == 0) {
+        const int64_t t = target[row];
+        picked[row] = (t >= 0 && t < V) ? (x[row * (long)V + t] - m) - ls : NAN;
+    }
+}
+
+__global__ __launch_bounds__(kLpThreads) void logprob_pick_bwd_reg_kernel(const float* __restrict__ logp,
+                                                                         const int64_t* __restrict__ target,
+                                                                         const float* __restrict__ gpick, int V,
+                                                                         float* __restrict__ dx) {
+    const long row = blockIdx.x;
+    const int v4 = V / 4;
+    const float g = gpick[row];
+    const int64_t t = target[row];
+    const float4* l4 = reinterpret_cast<const float4*>(logp + row * (long)V);
+    float4* d4 = reinterpret_cast<float4*>(dx + row * (long)V);
+    float4 r[kLpKR];
+#pragma unroll
+    for (int k = 0; k < kLpKR; ++k) {
+        const int i = threadIdx.x + k * kLpThreads;
+        if (i < v4) r[k] = l4[i];
+    }
+#pragma unroll
+    for (int k = 0; k < kLpKR; ++k) {
+        const int i = threadIdx.x + k * kLpThreads;
+        if (i < v4) {
+            const int j = 4 * i;
+            d4[i] = make_float4(g * ((j == t ? 1.f : 0.f) - expf(r[k].x)), g * ((j + 1 == t ? 1.f : 0.f) - expf(r[k].y)),
+                                g * ((j + 2 == t ? 1.f : 0.f) - expf(r[k].z)),
+                                g * ((j + 3 == t ? 1.f : 0.f) - expf(r[k].w)));
+        }
+    }
+}
+
 }  // namespace pdvc
 
 using namespace pdvc;
@@ -129,7 +226,10 @@ extern "C" int pdvc_logprob_pick_forward_f32(const float* logits, const int64_t*
     if (rows == 0) return PDVC_OK;
     const bool vec4 = (V % 4) == 0 && ((uintptr_t)logits % 16) == 0 && ((uintptr_t)logp % 16) == 0;
     hipStream_t s = (hipStream_t)stream;
-    if (vec4)
+    if (vec4 && V / 4 <= kLpThreads * kLpKR)
+        hipLaunchKernelGGL(logprob_pick_fwd_reg_kernel, dim3((unsigned)rows), dim3(kLpThreads), 0, s, logits, target, V,
+                           logp, picked);
+    else if (vec4)
         hipLaunchKernelGGL(logprob_pick_fwd_kernel<true>, dim3((unsigned)rows), dim3(kLpThreads), 0, s, logits,
                            target, V, logp, picked);
     else
@@ -146,7 +246,10 @@ extern "C" int pdvc_logprob_pick_backward_f32(const float* logp, const int64_t* 
     if (rows == 0) return PDVC_OK;
     const bool vec4 = (V % 4) == 0 && ((uintptr_t)logp % 16) == 0 && ((uintptr_t)grad_logits % 16) == 0;
     hipStream_t s = (hipStream_t)stream;
-    if (vec4)
+    if (vec4 && V / 4 <= kLpThreads * kLpKR)
+        hipLaunchKernelGGL(logprob_pick_bwd_reg_kernel, dim3((unsigned)rows), dim3(kLpThreads), 0, s, logp, target,
+                           grad_picked, V, grad_logits);
+    else if (vec4)
         hipLaunchKernelGGL(logprob_pick_bwd_kernel<true>, dim3((unsigned)rows), dim3(kLpThreads), 0, s, logp,
                            target, grad_picked, V, grad_logits);
     else
