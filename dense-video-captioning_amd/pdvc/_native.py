@@ -40,7 +40,11 @@ SIGNATURES = {
     "pdvc_relu_dropout_backward_f32": [_vp, _vp, _i, _i, _f, _i, _vp, _vp, _vp],
     "pdvc_logprob_pick_forward_f32": [_vp, _vp, _i, _i, _vp, _vp, _vp],
     "pdvc_logprob_pick_backward_f32": [_vp, _vp, _vp, _i, _i, _vp, _vp],
-    "pdvc_level_pos_rows_forward_f32":[_vp] * 5 + [_i] * 5 + [_vp, _vp],
+    "pdvc_seq_attention_forward_f32": [_vp, ctypes.c_long, _vp, ctypes.c_long, _vp, ctypes.c_long] + [_i] * 5
+    + [_vp, _vp, _vp],
+    "pdvc_seq_attention_backward_f32": [_vp, ctypes.c_long, _vp, ctypes.c_long, _vp, ctypes.c_long, _vp, _vp, _vp]
+    + [_i] * 5 + [_vp, _vp, ctypes.c_long, _vp, ctypes.c_long, _vp, ctypes.c_long, _vp],
+    "pdvc_level_pos_rows_forward_f32": [_vp] * 5 + [_i] * 5 + [_vp, _vp],
     "pdvc_level_pos_rows_backward_f32": [_vp, _vp] + [_i] * 4 + [_vp, _vp],
     "pdvc_groupnorm_rows_forward_f32": [_vp, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "pdvc_groupnorm_rows_backward_f32": [_vp] * 5 + [_i] * 4 + [_vp] * 4,

@@ -47,6 +47,8 @@
  *                                      (deformable_transformer.py:140-145 encoder, :233-237 decoder)
  *   pdvc_logprob_pick_*             <- log_softmax of the caption logits (LSTM_DSA.py:112-116) fused with the
  *                                      caption loss's target gather (LSTM_DSA.py:48-52), and its backward
+ *   pdvc_seq_attention_*            <- the attention core of NewModel's two nn.MultiheadAttention front-end
+ *                                      blocks over T clips (NewModel.py:41-65, cfgs/yc2_newModel_sound.yml)
  *   pdvc_gemm_f32                   <- the dense projections (nn.Linear forward/backward) of the layers
  *                                      above: MSDeformAttn value/offset/output projections
  *                                      (ms_deform_attn.py:79-126), the FFNs (deformable_transformer.py:150-156,
@@ -291,6 +293,22 @@ int pdvc_logprob_pick_forward_f32(const float* logits, const int64_t* target, in
                                   float* picked, void* stream);
 int pdvc_logprob_pick_backward_f32(const float* logp, const int64_t* target, const float* grad_picked, int rows,
                                    int V, float* grad_logits, void* stream);
+
+/* ---- long-sequence attention core (dual-modality front-end, cfgs/yc2_newModel_sound) --------------------
+ * Replaces the core of the two nn.MultiheadAttention(768, 32, batch_first=True) calls of NewModel
+ * (NewModel.py:41-65): out = softmax(q k^T / sqrt(head_dim)) v per (video, head), no mask, no dropout.
+ * q (N,Tq,*) row stride ldq, k / v (N,Tk,*) row strides ldk / ldv, head h at columns [h*head_dim, +head_dim);
+ * out (N,Tq,num_heads*head_dim) contiguous; lse (N,num_heads,Tq) saved for the backward.  head_dim in
+ * {16,24,32,48,64}; any Tq, Tk (keys streamed through LDS in tiles of 128).
+ * backward: workspace N*num_heads*Tq floats; grad_q / grad_k / grad_v fully written with their row strides. */
+int pdvc_seq_attention_forward_f32(const float* q, long ldq, const float* k, long ldk, const float* v, long ldv,
+                                   int batch, int num_query, int num_key, int num_heads, int head_dim, float* out,
+                                   float* lse, void* stream);
+int pdvc_seq_attention_backward_f32(const float* q, long ldq, const float* k, long ldk, const float* v, long ldv,
+                                    const float* out, const float* grad_out, const float* lse, int batch,
+                                    int num_query, int num_key, int num_heads, int head_dim, float* workspace,
+                                    float* grad_q, long ld_grad_q, float* grad_k, long ld_grad_k, float* grad_v,
+                                    long ld_grad_v, void* stream);
 
 /* ---- fp32 GEMM on the matrix cores ----------------------------------------------------------------
  * C[M,N] = op(A)[M,K] op(B)[K,N] (+ bias[N]) (ReLU).  op(A): trans_a 0 -> A[m*lda + k], 1 -> A[k*lda + m];
