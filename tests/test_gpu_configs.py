@@ -46,3 +46,30 @@ def test_training_step_runs_at_config(cfg, T, C, Q, E, W):
             continue
         assert torch.isfinite(p.grad).all().item(), n
     assert n_none == 8, n_none
+
+
+def test_newmodel_dual_modality_training_step():
+    """cfgs/yc2_newModel_sound.yml through NewModel (pdvc/newmodel.py): front-end (HIP attention core) + PDVC,
+    synthetic clip and sound features (N, T=512, 768); every front-end parameter receives a finite gradient and
+    PDVC's 8 never-used parameters none, as in the plain-PDVC case."""
+    import opts
+    from pdvc.data import collate, synthetic_videos, to_device
+    from pdvc.newmodel import build_newmodel
+    torch.manual_seed(0)
+    args = opts.parse_opts(["--cfg_path", "cfgs/yc2_newModel_sound.yml", "--device", "cuda"], cfg_root=PKG,
+                           feature_dim=768, num_queries=100, frame_embedding_num=512)
+    model, criterion, post = build_newmodel(args)
+    model = model.cuda().train()
+    dt = to_device(collate(synthetic_videos(2, 512, 768, 8, 9, args.vocab_size + 1, seed=5)), "cuda")
+    dt["sound_tensor"] = torch.randn(2, 512, 768, device="cuda")
+    out, loss, los = model(dt)
+    assert los == 0 and "bbox" in post
+    wd = criterion.weight_dict
+    total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
+    assert torch.isfinite(total).item()
+    total.backward()
+    none = [n for n, p in model.named_parameters() if p.grad is None]
+    assert len(none) == 8 and all(n.startswith("pdvcModel.") for n in none), none
+    for n, p in model.named_parameters():
+        if not n.startswith("pdvcModel."):
+            assert torch.isfinite(p.grad).all().item() and p.grad.abs().sum().item() > 0, n
