@@ -28,25 +28,28 @@ __device__ __forceinline__ void sq_stage(float* lds, const float* src, long ld, 
     }
 }
 
-template <int D>
+template <int D, int R>
 __global__ __launch_bounds__(kSqT) void seqattn_fwd_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                            const float* __restrict__ v, int H, int Tq, int Tk,
                                                            long ldq, long ldk, long ldv, float scale,
                                                            float* __restrict__ out, float* __restrict__ lse) {
     __shared__ float ks[kSqTile * D], vs[kSqTile * D];
     const int nh = blockIdx.y, n = nh / H, h = nh - n * H;
-    const int i = blockIdx.x * kSqT + threadIdx.x;
-    const bool act = i < Tq;
     const float* qh = q + (long)n * Tq * ldq + h * D;
     const float* kh = k + (long)n * Tk * ldk + h * D;
     const float* vh = v + (long)n * Tk * ldv + h * D;
-    float qi[D], acc[D];
+    float qi[R][D], acc[R][D], m[R], l[R];
 #pragma unroll
-    for (int c = 0; c < D; ++c) {
-        qi[c] = act ? qh[(long)i * ldq + c] * scale : 0.f;
-        acc[c] = 0.f;
+    for (int r = 0; r < R; ++r) {
+        const int i = blockIdx.x * kSqT * R + r * kSqT + threadIdx.x;
+#pragma unroll
+        for (int c = 0; c < D; ++c) {
+            qi[r][c] = i < Tq ? qh[(long)i * ldq + c] * scale : 0.f;
+            acc[r][c] = 0.f;
+        }
+        m[r] = -INFINITY;
+        l[r] = 0.f;
     }
-    float m = -INFINITY, l = 0.f;
     for (int t0 = 0; t0 < Tk; t0 += kSqTile) {
         const int nt = min(kSqTile, Tk - t0);
         __syncthreads();
@@ -54,28 +57,38 @@ __global__ __launch_bounds__(kSqT) void seqattn_fwd_kernel(const float* __restri
         sq_stage<D>(vs, vh, ldv, t0, nt, Tk);
         __syncthreads();
         for (int j = 0; j < nt; ++j) {
-            float s = 0.f;
+            float kv[D];
 #pragma unroll
-            for (int c = 0; c < D; ++c) s += qi[c] * ks[j * D + c];
-            if (s > m) {
-                const float corr = __expf(m - s);
-                l *= corr;
+            for (int c = 0; c < D; ++c) kv[c] = ks[j * D + c];
 #pragma unroll
-                for (int c = 0; c < D; ++c) acc[c] *= corr;
-                m = s;
+            for (int r = 0; r < R; ++r) {
+                float s = 0.f;
+#pragma unroll
+                for (int c = 0; c < D; ++c) s += qi[r][c] * kv[c];
+                if (s > m[r]) {
+                    const float corr = __expf(m[r] - s);
+                    l[r] *= corr;
+#pragma unroll
+                    for (int c = 0; c < D; ++c) acc[r][c] *= corr;
+                    m[r] = s;
+                }
+                const float p = __expf(s - m[r]);
+                l[r] += p;
+#pragma unroll
+                for (int c = 0; c < D; ++c) acc[r][c] += p * vs[j * D + c];
             }
-            const float p = __expf(s - m);
-            l += p;
-#pragma unroll
-            for (int c = 0; c < D; ++c) acc[c] += p * vs[j * D + c];
         }
     }
-    if (act) {
-        const float inv = 1.f / l;
-        float* o = out + ((long)n * Tq + i) * H * D + h * D;
 #pragma unroll
-        for (int c = 0; c < D; ++c) o[c] = acc[c] * inv;
-        lse[(long)nh * Tq + i] = m + logf(l);
+    for (int r = 0; r < R; ++r) {
+        const int i = blockIdx.x * kSqT * R + r * kSqT + threadIdx.x;
+        if (i < Tq) {
+            const float inv = 1.f / l[r];
+            float* o = out + ((long)n * Tq + i) * H * D + h * D;
+#pragma unroll
+            for (int c = 0; c < D; ++c) o[c] = acc[r][c] * inv;
+            lse[(long)nh * Tq + i] = m[r] + logf(l[r]);
+        }
     }
 }
 
@@ -93,7 +106,7 @@ __global__ void seqattn_delta_kernel(const float* __restrict__ out, const float*
     delta[((long)n * H + h) * Tq + i] = s;
 }
 
-template <int D>
+template <int D, int R>
 __global__ __launch_bounds__(kSqT) void seqattn_bwd_dq_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                               const float* __restrict__ v,
                                                               const float* __restrict__ dout,
@@ -103,20 +116,24 @@ __global__ __launch_bounds__(kSqT) void seqattn_bwd_dq_kernel(const float* __res
                                                               float* __restrict__ dq, long lddq) {
     __shared__ float ks[kSqTile * D], vs[kSqTile * D];
     const int nh = blockIdx.y, n = nh / H, h = nh - n * H;
-    const int i = blockIdx.x * kSqT + threadIdx.x;
-    const bool act = i < Tq;
     const float* qh = q + (long)n * Tq * ldq + h * D;
     const float* kh = k + (long)n * Tk * ldk + h * D;
     const float* vh = v + (long)n * Tk * ldv + h * D;
     const float* gh = dout + (long)n * Tq * H * D + h * D;
-    float qi[D], gi[D], acc[D];
+    float qi[R][D], gi[R][D], acc[R][D], li[R], di[R];
 #pragma unroll
-    for (int c = 0; c < D; ++c) {
-        qi[c] = act ? qh[(long)i * ldq + c] * scale : 0.f;
-        gi[c] = act ? gh[(long)i * H * D + c] : 0.f;
-        acc[c] = 0.f;
+    for (int r = 0; r < R; ++r) {
+        const int i = blockIdx.x * kSqT * R + r * kSqT + threadIdx.x;
+        const bool act = i < Tq;
+#pragma unroll
+        for (int c = 0; c < D; ++c) {
+            qi[r][c] = act ? qh[(long)i * ldq + c] * scale : 0.f;
+            gi[r][c] = act ? gh[(long)i * H * D + c] : 0.f;
+            acc[r][c] = 0.f;
+        }
+        li[r] = act ? lse[(long)nh * Tq + i] : 0.f;
+        di[r] = act ? delta[(long)nh * Tq + i] : 0.f;
     }
-    const float li = act ? lse[(long)nh * Tq + i] : 0.f, di = act ? delta[(long)nh * Tq + i] : 0.f;
     for (int t0 = 0; t0 < Tk; t0 += kSqTile) {
         const int nt = min(kSqTile, Tk - t0);
         __syncthreads();
@@ -124,21 +141,34 @@ __global__ __launch_bounds__(kSqT) void seqattn_bwd_dq_kernel(const float* __res
         sq_stage<D>(vs, vh, ldv, t0, nt, Tk);
         __syncthreads();
         for (int j = 0; j < nt; ++j) {
-            float s = 0.f, dp = 0.f;
+            float kv[D], vv[D];
 #pragma unroll
             for (int c = 0; c < D; ++c) {
-                s += qi[c] * ks[j * D + c];
-                dp += gi[c] * vs[j * D + c];
+                kv[c] = ks[j * D + c];
+                vv[c] = vs[j * D + c];
             }
-            const float ds = __expf(s - li) * (dp - di);
 #pragma unroll
-            for (int c = 0; c < D; ++c) acc[c] += ds * ks[j * D + c];
+            for (int r = 0; r < R; ++r) {
+                float s = 0.f, dp = 0.f;
+#pragma unroll
+                for (int c = 0; c < D; ++c) {
+                    s += qi[r][c] * kv[c];
+                    dp += gi[r][c] * vv[c];
+                }
+                const float ds = __expf(s - li[r]) * (dp - di[r]);
+#pragma unroll
+                for (int c = 0; c < D; ++c) acc[r][c] += ds * kv[c];
+            }
         }
     }
-    if (act) {
-        float* o = dq + ((long)n * Tq + i) * lddq + h * D;
 #pragma unroll
-        for (int c = 0; c < D; ++c) o[c] = acc[c] * scale;
+    for (int r = 0; r < R; ++r) {
+        const int i = blockIdx.x * kSqT * R + r * kSqT + threadIdx.x;
+        if (i < Tq) {
+            float* o = dq + ((long)n * Tq + i) * lddq + h * D;
+#pragma unroll
+            for (int c = 0; c < D; ++c) o[c] = acc[r][c] * scale;
+        }
     }
 }
 
@@ -214,6 +244,10 @@ __global__ __launch_bounds__(kSqT) void seqattn_bwd_dkv_kernel(const float* __re
         default: break;            \
     }
 
+// query rows per lane in the forward and dq kernels: 2 for head_dim <= 32 (each key row read from LDS serves two
+// queries), 1 above (register budget)
+static constexpr int sq_rows_per_lane(int D) { return D <= 32 ? 2 : 1; }
+
 static bool sq_head_dim_ok(int D) { return D == 16 || D == 24 || D == 32 || D == 48 || D == 64; }
 
 }  // namespace pdvc
@@ -230,11 +264,16 @@ extern "C" int pdvc_seq_attention_forward_f32(const float* q, long ldq, const fl
     PDVC_CHECK_ARG((long)batch * num_heads < 65536, "batch * num_heads must be < 65536");
     if (batch == 0 || num_query == 0) return PDVC_OK;
     const float scale = 1.f / sqrtf((float)head_dim);
-    dim3 grid((unsigned)((num_query + kSqT - 1) / kSqT), (unsigned)(batch * num_heads));
+    const int R = sq_rows_per_lane(head_dim);
+    dim3 grid((unsigned)((num_query + kSqT * R - 1) / (kSqT * R)), (unsigned)(batch * num_heads));
     hipStream_t s = (hipStream_t)stream;
 #define PDVC_SQ_FWD(DD)                                                                                              \
-    hipLaunchKernelGGL(seqattn_fwd_kernel<DD>, grid, dim3(kSqT), 0, s, q, k, v, num_heads, num_query, num_key, ldq, \
-                       ldk, ldv, scale, out, lse)
+    if (sq_rows_per_lane(DD) == 2)                                                                                   \
+        hipLaunchKernelGGL((seqattn_fwd_kernel<DD, 2>), grid, dim3(kSqT), 0, s, q, k, v, num_heads, num_query,       \
+                           num_key, ldq, ldk, ldv, scale, out, lse);                                                \
+    else                                                                                                             \
+        hipLaunchKernelGGL((seqattn_fwd_kernel<DD, 1>), grid, dim3(kSqT), 0, s, q, k, v, num_heads, num_query,       \
+                           num_key, ldq, ldk, ldv, scale, out, lse)
     PDVC_SQ_DISPATCH(head_dim, PDVC_SQ_FWD)
 #undef PDVC_SQ_FWD
     PDVC_CHECK_LAUNCH("seqattn_fwd_kernel");
@@ -271,11 +310,16 @@ extern "C" int pdvc_seq_attention_backward_f32(const float* q, long ldq, const f
                            delta);
         PDVC_CHECK_LAUNCH("seqattn_delta_kernel");
     }
-    dim3 gq((unsigned)((num_query + kSqT - 1) / kSqT), (unsigned)(batch * num_heads));
+    const int R = sq_rows_per_lane(head_dim);
+    dim3 gq((unsigned)((num_query + kSqT * R - 1) / (kSqT * R)), (unsigned)(batch * num_heads));
     dim3 gk((unsigned)((num_key + kSqT - 1) / kSqT), (unsigned)(batch * num_heads));
 #define PDVC_SQ_DQ(DD)                                                                                               \
-    hipLaunchKernelGGL(seqattn_bwd_dq_kernel<DD>, gq, dim3(kSqT), 0, s, q, k, v, grad_out, lse, delta, num_heads,    \
-                       num_query, num_key, ldq, ldk, ldv, scale, grad_q, ld_grad_q)
+    if (sq_rows_per_lane(DD) == 2)                                                                                   \
+        hipLaunchKernelGGL((seqattn_bwd_dq_kernel<DD, 2>), gq, dim3(kSqT), 0, s, q, k, v, grad_out, lse, delta,      \
+                           num_heads, num_query, num_key, ldq, ldk, ldv, scale, grad_q, ld_grad_q);                 \
+    else                                                                                                             \
+        hipLaunchKernelGGL((seqattn_bwd_dq_kernel<DD, 1>), gq, dim3(kSqT), 0, s, q, k, v, grad_out, lse, delta,      \
+                           num_heads, num_query, num_key, ldq, ldk, ldv, scale, grad_q, ld_grad_q)
 #define PDVC_SQ_DKV(DD)                                                                                              \
     hipLaunchKernelGGL(seqattn_bwd_dkv_kernel<DD>, gk, dim3(kSqT), 0, s, q, k, v, grad_out, lse, delta, num_heads,   \
                        num_query, num_key, ldq, ldk, ldv, scale, grad_k, ld_grad_k, grad_v, ld_grad_v)
