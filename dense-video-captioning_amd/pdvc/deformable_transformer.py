@@ -115,9 +115,11 @@ class DeformableTransformer(nn.Module):
     def prepare_decoder_input_query(self, memory, query_embed):
         bs = memory.shape[0]
         query_embed, tgt = torch.chunk(query_embed, 2, dim=1)
+        # the Q reference points are the same for every video: one (Q, d) x (d, 1) product, then broadcast
+        # (the reference applies the Linear to the expanded (bs, Q, d) tensor: the same values, bs times the work)
+        reference_points = self.reference_points(query_embed).sigmoid().unsqueeze(0).expand(bs, -1, -1).contiguous()
         query_embed = query_embed.unsqueeze(0).expand(bs, -1, -1)
         tgt = tgt.unsqueeze(0).expand(bs, -1, -1)
-        reference_points = self.reference_points(query_embed).sigmoid()
         return reference_points, tgt, reference_points, query_embed
 
     def prepare_decoder_input_proposal(self, gt_reference_points):

@@ -143,6 +143,8 @@ def add_row_bias(x, bias):
 def wgrad_mm(gy, x):
     """gy^T x for row-major gy (rows, O) and x (rows, I): the weight-gradient product, split over K."""
     rows = gy.shape[0]
+    if gy.shape[1] == 1:  # a 1-wide layer: a weighted column sum, not an (M = 1) GEMM (~1 TB/s on hipBLASLt)
+        return colsum((x * gy).contiguous()).view(1, -1)
     s = wgrad_splits(rows)
     if s == 1:
         return torch.mm(gy.t(), x)

@@ -213,7 +213,8 @@ class PDVC(nn.Module):
         for l_id in range(hs.shape[0]):
             hs_l = hs[l_id]
             reference = init_reference if l_id == 0 else inter_references[l_id - 1]
-            classes.append(self.class_head[l_id](hs_l))
+            ch = self.class_head[l_id]
+            classes.append(dense(hs_l, ch.weight, ch.bias))  # 1-wide head: weight gradient as a column sum
             counts.append(self.predict_event_num(self.count_head[l_id], hs_l))
             tmp = self.bbox_head[l_id](hs_l)
             if disable_refine:
