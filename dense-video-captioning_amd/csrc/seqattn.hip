@@ -172,7 +172,7 @@ __global__ __launch_bounds__(kSqT) void seqattn_bwd_dq_kernel(const float* __res
     }
 }
 
-template <int D>
+template <int D, int R>
 __global__ __launch_bounds__(kSqT) void seqattn_bwd_dkv_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                                const float* __restrict__ v,
                                                                const float* __restrict__ dout,
@@ -183,19 +183,22 @@ __global__ __launch_bounds__(kSqT) void seqattn_bwd_dkv_kernel(const float* __re
                                                                float* __restrict__ dv, long lddv) {
     __shared__ float qs[kSqTile * D], gs[kSqTile * D], ls[kSqTile], dls[kSqTile];
     const int nh = blockIdx.y, n = nh / H, h = nh - n * H;
-    const int j = blockIdx.x * kSqT + threadIdx.x;
-    const bool act = j < Tk;
     const float* qh = q + (long)n * Tq * ldq + h * D;
     const float* kh = k + (long)n * Tk * ldk + h * D;
     const float* vh = v + (long)n * Tk * ldv + h * D;
     const float* gh = dout + (long)n * Tq * H * D + h * D;
-    float kj[D], vj[D], ak[D], av[D];
+    float kj[R][D], vj[R][D], ak[R][D], av[R][D];
 #pragma unroll
-    for (int c = 0; c < D; ++c) {
-        kj[c] = act ? kh[(long)j * ldk + c] * scale : 0.f;
-        vj[c] = act ? vh[(long)j * ldv + c] : 0.f;
-        ak[c] = 0.f;
-        av[c] = 0.f;
+    for (int r = 0; r < R; ++r) {
+        const int j = blockIdx.x * kSqT * R + r * kSqT + threadIdx.x;
+        const bool act = j < Tk;
+#pragma unroll
+        for (int c = 0; c < D; ++c) {
+            kj[r][c] = act ? kh[(long)j * ldk + c] * scale : 0.f;
+            vj[r][c] = act ? vh[(long)j * ldv + c] : 0.f;
+            ak[r][c] = 0.f;
+            av[r][c] = 0.f;
+        }
     }
     for (int t0 = 0; t0 < Tq; t0 += kSqTile) {
         const int nt = min(kSqTile, Tq - t0);
@@ -208,28 +211,42 @@ __global__ __launch_bounds__(kSqT) void seqattn_bwd_dkv_kernel(const float* __re
         }
         __syncthreads();
         for (int i = 0; i < nt; ++i) {
-            float s = 0.f, dp = 0.f;
+            float qv[D], gv[D];
 #pragma unroll
             for (int c = 0; c < D; ++c) {
-                s += kj[c] * qs[i * D + c];
-                dp += vj[c] * gs[i * D + c];
+                qv[c] = qs[i * D + c];
+                gv[c] = gs[i * D + c];
             }
-            const float p = __expf(s - ls[i]);
-            const float ds = p * (dp - dls[i]);
+            const float li = ls[i], di = dls[i];
 #pragma unroll
-            for (int c = 0; c < D; ++c) {
-                av[c] += p * gs[i * D + c];
-                ak[c] += ds * qs[i * D + c];
+            for (int r = 0; r < R; ++r) {
+                float s = 0.f, dp = 0.f;
+#pragma unroll
+                for (int c = 0; c < D; ++c) {
+                    s += kj[r][c] * qv[c];
+                    dp += vj[r][c] * gv[c];
+                }
+                const float p = __expf(s - li);
+                const float ds = p * (dp - di);
+#pragma unroll
+                for (int c = 0; c < D; ++c) {
+                    av[r][c] += p * gv[c];
+                    ak[r][c] += ds * qv[c];
+                }
             }
         }
     }
-    if (act) {
-        float* ok = dk + ((long)n * Tk + j) * lddk + h * D;
-        float* ov = dv + ((long)n * Tk + j) * lddv + h * D;
 #pragma unroll
-        for (int c = 0; c < D; ++c) {
-            ok[c] = ak[c] * scale;
-            ov[c] = av[c];
+    for (int r = 0; r < R; ++r) {
+        const int j = blockIdx.x * kSqT * R + r * kSqT + threadIdx.x;
+        if (j < Tk) {
+            float* ok = dk + ((long)n * Tk + j) * lddk + h * D;
+            float* ov = dv + ((long)n * Tk + j) * lddv + h * D;
+#pragma unroll
+            for (int c = 0; c < D; ++c) {
+                ok[c] = ak[r][c] * scale;
+                ov[c] = av[r][c];
+            }
         }
     }
 }
@@ -247,6 +264,9 @@ __global__ __launch_bounds__(kSqT) void seqattn_bwd_dkv_kernel(const float* __re
 // query rows per lane in the forward and dq kernels: 2 for head_dim <= 32 (each key row read from LDS serves two
 // queries), 1 above (register budget)
 static constexpr int sq_rows_per_lane(int D) { return D <= 32 ? 2 : 1; }
+
+// key rows per lane in the dk/dv kernel: 2 for head_dim <= 24 (four D-vectors per key row live in registers)
+static constexpr int sq_keys_per_lane(int D) { return D <= 24 ? 2 : 1; }
 
 static bool sq_head_dim_ok(int D) { return D == 16 || D == 24 || D == 32 || D == 48 || D == 64; }
 
@@ -312,7 +332,8 @@ extern "C" int pdvc_seq_attention_backward_f32(const float* q, long ldq, const f
     }
     const int R = sq_rows_per_lane(head_dim);
     dim3 gq((unsigned)((num_query + kSqT * R - 1) / (kSqT * R)), (unsigned)(batch * num_heads));
-    dim3 gk((unsigned)((num_key + kSqT - 1) / kSqT), (unsigned)(batch * num_heads));
+    const int RK = sq_keys_per_lane(head_dim);
+    dim3 gk((unsigned)((num_key + kSqT * RK - 1) / (kSqT * RK)), (unsigned)(batch * num_heads));
 #define PDVC_SQ_DQ(DD)                                                                                               \
     if (sq_rows_per_lane(DD) == 2)                                                                                   \
         hipLaunchKernelGGL((seqattn_bwd_dq_kernel<DD, 2>), gq, dim3(kSqT), 0, s, q, k, v, grad_out, lse, delta,      \
@@ -321,8 +342,13 @@ extern "C" int pdvc_seq_attention_backward_f32(const float* q, long ldq, const f
         hipLaunchKernelGGL((seqattn_bwd_dq_kernel<DD, 1>), gq, dim3(kSqT), 0, s, q, k, v, grad_out, lse, delta,      \
                            num_heads, num_query, num_key, ldq, ldk, ldv, scale, grad_q, ld_grad_q)
 #define PDVC_SQ_DKV(DD)                                                                                              \
-    hipLaunchKernelGGL(seqattn_bwd_dkv_kernel<DD>, gk, dim3(kSqT), 0, s, q, k, v, grad_out, lse, delta, num_heads,   \
-                       num_query, num_key, ldq, ldk, ldv, scale, grad_k, ld_grad_k, grad_v, ld_grad_v)
+    if (sq_keys_per_lane(DD) == 2)                                                                                   \
+        hipLaunchKernelGGL((seqattn_bwd_dkv_kernel<DD, 2>), gk, dim3(kSqT), 0, s, q, k, v, grad_out, lse, delta,     \
+                           num_heads, num_query, num_key, ldq, ldk, ldv, scale, grad_k, ld_grad_k, grad_v,          \
+                           ld_grad_v);                                                                              \
+    else                                                                                                             \
+        hipLaunchKernelGGL((seqattn_bwd_dkv_kernel<DD, 1>), gk, dim3(kSqT), 0, s, q, k, v, grad_out, lse, delta,     \
+                           num_heads, num_query, num_key, ldq, ldk, ldv, scale, grad_k, ld_grad_k, grad_v, ld_grad_v)
     PDVC_SQ_DISPATCH(head_dim, PDVC_SQ_DQ)
     PDVC_CHECK_LAUNCH("seqattn_bwd_dq_kernel");
     PDVC_SQ_DISPATCH(head_dim, PDVC_SQ_DKV)
