@@ -95,6 +95,11 @@ def linear(x, weight, bias=None, relu=False):
     return LinearFunction.apply(x, weight, bias, relu)
 
 
+# dense(..., relu=True) asks hipBLASLt for the ReLU epilogue instead of a separate pass (same-box A/B 3277 -> 3292
+# videos/s); PDVC_RELU_EPILOGUE=0 keeps addmm + relu_
+_RELU_EPILOGUE = os.environ.get("PDVC_RELU_EPILOGUE", "1") != "0"
+
+
 def wgrad_splits(rows):
     """K-chunks for a weight gradient over `rows` rows: hipBLASLt runs dW = dy^T x (512 x 512 outputs, K = N*S
     = 30720) on 128 workgroups at ~70 TF/s; as a batched GEMM over 16 row chunks plus a sum it fills the
@@ -158,9 +163,12 @@ class TorchLinearFunction(Function):
     def forward(ctx, x, weight, bias, relu=False):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
-        y = torch.addmm(bias, x2, weight.t()) if bias is not None else torch.mm(x2, weight.t())
-        if relu:
-            y.relu_()
+        if relu and bias is not None and _RELU_EPILOGUE:
+            y = torch._addmm_activation(bias, x2, weight.t(), use_gelu=False)  # ReLU in the GEMM epilogue
+        else:
+            y = torch.addmm(bias, x2, weight.t()) if bias is not None else torch.mm(x2, weight.t())
+            if relu:
+                y.relu_()
         ctx.save_for_backward(x2, weight, y if relu else None)
         ctx.has_bias = bias is not None
         return y.view(*shape[:-1], weight.shape[0])
