@@ -92,26 +92,13 @@ __global__ __launch_bounds__(kSqT) void seqattn_fwd_kernel(const float* __restri
     }
 }
 
-// delta_i = dout_i . out_i per (n, h, i)
-__global__ void seqattn_delta_kernel(const float* __restrict__ out, const float* __restrict__ dout, int H, int Tq,
-                                     int D, float* __restrict__ delta) {
-    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;  // (head, query) of video blockIdx.y
-    if (idx >= (long)H * Tq) return;
-    const int n = blockIdx.y;
-    const int h = (int)(idx / Tq), i = (int)(idx - (long)h * Tq);
-    const float* o = out + ((long)n * Tq + i) * H * D + h * D;
-    const float* g = dout + ((long)n * Tq + i) * H * D + h * D;
-    float s = 0.f;
-    for (int c = 0; c < D; ++c) s += o[c] * g[c];
-    delta[((long)n * H + h) * Tq + i] = s;
-}
-
 template <int D, int R>
 __global__ __launch_bounds__(kSqT) void seqattn_bwd_dq_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                               const float* __restrict__ v,
                                                               const float* __restrict__ dout,
                                                               const float* __restrict__ lse,
-                                                              const float* __restrict__ delta, int H, int Tq, int Tk,
+                                                              const float* __restrict__ out,
+                                                              float* __restrict__ delta, int H, int Tq, int Tk,
                                                               long ldq, long ldk, long ldv, float scale,
                                                               float* __restrict__ dq, long lddq) {
     __shared__ float ks[kSqTile * D], vs[kSqTile * D];
@@ -132,7 +119,15 @@ __global__ __launch_bounds__(kSqT) void seqattn_bwd_dq_kernel(const float* __res
             acc[r][c] = 0.f;
         }
         li[r] = act ? lse[(long)nh * Tq + i] : 0.f;
-        di[r] = act ? delta[(long)nh * Tq + i] : 0.f;
+        // delta_i = dout_i . out_i, from the lane's own rows; published for the dk/dv kernel launched after this
+        float dsum = 0.f;
+        if (act) {
+            const float* oh = out + ((long)n * Tq + i) * H * D + h * D;
+#pragma unroll
+            for (int c = 0; c < D; ++c) dsum += gi[r][c] * oh[c];
+            delta[(long)nh * Tq + i] = dsum;
+        }
+        di[r] = dsum;
     }
     for (int t0 = 0; t0 < Tk; t0 += kSqTile) {
         const int nt = min(kSqTile, Tk - t0);
@@ -322,24 +317,17 @@ extern "C" int pdvc_seq_attention_backward_f32(const float* q, long ldq, const f
         if (e1 != hipSuccess || e2 != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_k/grad_v");
         return PDVC_OK;
     }
-    float* delta = workspace;  // (N, H, Tq)
-    {
-        const long ht = (long)num_heads * num_query;
-        dim3 g((unsigned)((ht + 255) / 256), (unsigned)batch);
-        hipLaunchKernelGGL(seqattn_delta_kernel, g, dim3(256), 0, s, out, grad_out, num_heads, num_query, head_dim,
-                           delta);
-        PDVC_CHECK_LAUNCH("seqattn_delta_kernel");
-    }
+    float* delta = workspace;  // (N, H, Tq): written by the dq kernel, read by the dk/dv kernel
     const int R = sq_rows_per_lane(head_dim);
     dim3 gq((unsigned)((num_query + kSqT * R - 1) / (kSqT * R)), (unsigned)(batch * num_heads));
     const int RK = sq_keys_per_lane(head_dim);
     dim3 gk((unsigned)((num_key + kSqT * RK - 1) / (kSqT * RK)), (unsigned)(batch * num_heads));
 #define PDVC_SQ_DQ(DD)                                                                                               \
     if (sq_rows_per_lane(DD) == 2)                                                                                   \
-        hipLaunchKernelGGL((seqattn_bwd_dq_kernel<DD, 2>), gq, dim3(kSqT), 0, s, q, k, v, grad_out, lse, delta,      \
+        hipLaunchKernelGGL((seqattn_bwd_dq_kernel<DD, 2>), gq, dim3(kSqT), 0, s, q, k, v, grad_out, lse, out, delta, \
                            num_heads, num_query, num_key, ldq, ldk, ldv, scale, grad_q, ld_grad_q);                 \
     else                                                                                                             \
-        hipLaunchKernelGGL((seqattn_bwd_dq_kernel<DD, 1>), gq, dim3(kSqT), 0, s, q, k, v, grad_out, lse, delta,      \
+        hipLaunchKernelGGL((seqattn_bwd_dq_kernel<DD, 1>), gq, dim3(kSqT), 0, s, q, k, v, grad_out, lse, out, delta, \
                            num_heads, num_query, num_key, ldq, ldk, ldv, scale, grad_q, ld_grad_q)
 #define PDVC_SQ_DKV(DD)                                                                                              \
     if (sq_keys_per_lane(DD) == 2)                                                                                   \
