@@ -48,7 +48,7 @@ def parse():
     p.add_argument("--dist-backend", default=None, help="torch.distributed backend (default: nccl = RCCL on GPUs)")
     p.add_argument("--same-device", action="store_true",
                    help="rehearsal on a 1-GPU box: every rank on cuda:0 (use with --dist-backend gloo)")
-    p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
+    p.add_argument("--cpu-seconds", type=float, default=6.0, help="budget of the secondary C-oracle CPU figure")
     p.add_argument("--kernel-report", action="store_true", help="print per-kernel event timings to stderr")
     p.add_argument("--graph", choices=["step", "trunk", "none"], default="step",
                    help="step: forward+losses+backward replayed as one captured hipGraph (pdvc/step_graph.py); "
@@ -125,10 +125,25 @@ def gemm_roofline(step_fn):
             "timing": "torch.profiler device time of every aten GEMM in 1 eager step after the timed steps"}
 
 
-def cpu_baseline(a, budget_s):
-    """The oracle (a single-threaded C restatement of the reference MSDA op, oracle/msda_oracle.c) timed on
-    this host: MSDA fwd+bwd of the per-video call set (enc_layers x Lq=S + dec_layers x Lq=Q) at T, M=8,
-    D=64, 4 levels x 4 points, zero padding, fp32.  Bounded: whole videos until budget_s is spent."""
+def cpu_baseline(a):
+    """The reference's CPU deformable-attention path timed on this host: a torch restatement of
+    ms_deform_attn_core_pytorch (pdvc/ops/functions/ms_deform_attn_func.py:41-68, grid_sample border; pinned to
+    the reference's fixtures by tests/test_oracle.py) over one video's call set -- enc_layers x Lq=S + dec_layers
+    x Lq=Q, forward + backward, M=8 D=64 L=4 P=4 fp32 -- with every CPU this process may use; 3 warm-ups, median
+    of 20 runs."""
+    from oracle.torch_core import time_call_set
+    med, info = time_call_set(T=a.T, Q=a.Q, runs=20, warmup=3)
+    return {"value": 1.0 / med, "unit": "videos/s", "cores": info["threads"], "kind": "port",
+            "cpu_model": info["cpu_model"], "physical_cores": info["physical_cores"],
+            "usable_cpus": info["usable_cpus"], "ms_per_video": 1e3 * med,
+            "sample": f"median of {info['runs']} runs (after {info['warmup']} warm-ups) of one video's MSDeformAttn "
+                      f"call set ({info['calls']}), fwd+bwd, T={a.T}, M=8, D=64, L=4, P=4, fp32, "
+                      f"torch.set_num_threads({info['threads']}): oracle/torch_core.py (grid_sample, border)"}
+
+
+def cpu_baseline_c(a, budget_s):
+    """Secondary CPU figure: the single-threaded C restatement of the CUDA op (oracle/msda_oracle.c, zero
+    padding), whole videos of the same call set until budget_s is spent."""
     from oracle import oracle as O
     T_l = [a.T // (2 ** i) for i in range(4)]
     S = sum(T_l)
@@ -155,8 +170,8 @@ def cpu_baseline(a, budget_s):
         if el >= budget_s:
             break
     return {"value": videos / el, "unit": "videos/s", "cores": 1, "kind": "port",
-            "sample": f"{videos} video(s) x MSDA fwd+bwd call set (2 x Lq={S} + 2 x Lq={a.Q}), T={a.T}, M=8, D=64, "
-                      f"L=4, P=4, fp32, oracle/msda_oracle.c single thread, {el:.1f} s"}
+            "sample": f"{videos} video(s) x MSDA fwd+bwd call set (2 x Lq={S} + 2 x Lq={a.Q}), T={a.T}, fp32, "
+                      f"oracle/msda_oracle.c (zeros), single thread, {el:.1f} s"}
 
 
 def main():
@@ -303,8 +318,18 @@ def main():
     ksteps = 2 if graphed else a.steps
     result["kernels"] = {n: {"launches": v["launches"], "avg_us": 1e3 * v["ms"] / max(v["launches"], 1),
                              "share_of_step": v["ms"] / ksteps / (1e3 * el / a.steps)} for n, v in ks.items()}
+    # the north-star comparison, like for like: MSDeformAttn fwd+bwd (the fused 1-D kernels, encoder + decoder
+    # calls) per step on the GPU, from the HIP-event timings above, as videos/s against the CPU figure
+    msda_ms = sum(ks[n]["ms"] for n in ("pdvc_msda1d_forward_f32", "pdvc_msda1d_backward_f32") if n in ks) / ksteps
+    if msda_ms > 0:
+        result["msda_gpu"] = {"ms_per_step": msda_ms, "videos_per_s": B / (msda_ms * 1e-3) * world,
+                              "what": "fused MSDeformAttn forward + backward kernels of every encoder and decoder "
+                                      "layer, HIP events, per step of B videos per GPU"}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(a, a.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(a)
+        result["cpu_baseline_c_oracle"] = cpu_baseline_c(a, a.cpu_seconds)
+        if "msda_gpu" in result:
+            result["msda_gpu"]["vs_cpu_baseline"] = result["msda_gpu"]["videos_per_s"] / result["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -303,9 +303,9 @@ extern "C" int pdvc_add_dropout_layernorm_backward_f32(const float* x, const flo
     PDVC_CHECK_ARG(workspace != nullptr, "workspace (3 * 1024 * d floats) is required");
     hipStream_t st = (hipStream_t)stream;
     if (rows == 0) {
-        hipError_t e1 = hipMemsetAsync(dgamma, 0, sizeof(float) * d, st);
-        hipError_t e2 = hipMemsetAsync(dbeta, 0, sizeof(float) * d, st);
-        hipError_t e3 = ds_colsum ? hipMemsetAsync(ds_colsum, 0, sizeof(float) * d, st) : hipSuccess;
+        hipError_t e1 = zero_async(dgamma, d, st);
+        hipError_t e2 = zero_async(dbeta, d, st);
+        hipError_t e3 = ds_colsum ? zero_async(ds_colsum, d, st) : hipSuccess;
         if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess)
             return pdvc_set_error(PDVC_ERR_LAUNCH, "memset failed");
         return PDVC_OK;

@@ -508,7 +508,7 @@ extern "C" int pdvc_cap_value_grad_f32(const uint8_t* value_pad_mask, const int3
     const long nblk = (long)batch * num_heads * cL;
     if (nblk == 0) return PDVC_OK;
     if (steps == 0 || max_rows_per_video == 0) {
-        hipError_t e = hipMemsetAsync(grad_value, 0, sizeof(float) * (size_t)batch * S * num_heads * head_dim, s);
+        hipError_t e = zero_async(grad_value, (size_t)batch * S * num_heads * head_dim, s);
         return e == hipSuccess ? PDVC_OK : pdvc_set_error(PDVC_ERR_LAUNCH, "memset: %s", hipGetErrorString(e));
     }
     int Tmax = 0;

@@ -899,7 +899,7 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
     const long rows = (long)batch * num_query;
     const long tw = query_waves(g, batch, num_heads, num_query);
     if (grad_ref && rows > 0) {  // accumulated over the heads with atomics
-        hipError_t e = hipMemsetAsync(grad_ref, 0, sizeof(float) * rows * kL * ref_dim, s);
+        hipError_t e = zero_async(grad_ref, (size_t)rows * kL * ref_dim, s);
         if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_ref: %s", hipGetErrorString(e));
     }
     if (tw > 0) {
@@ -920,7 +920,7 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
     const long nblk = (long)batch * num_heads * kL;
     if (nblk > 0) {
         if (num_query == 0) {
-            hipError_t e = hipMemsetAsync(grad_value, 0, sizeof(float) * (size_t)batch * S * num_heads * head_dim, s);
+            hipError_t e = zero_async(grad_value, (size_t)batch * S * num_heads * head_dim, s);
             if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_value: %s", hipGetErrorString(e));
             return PDVC_OK;
         }

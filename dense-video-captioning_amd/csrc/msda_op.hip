@@ -85,12 +85,17 @@ __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
+// The level table lives in device memory, so the host cannot check it without a sync.  A level whose rows
+// fall outside [0, S) (a malformed table; the reference reads out of bounds there) is given H = W = 0: it
+// contributes no samples, and no value row outside the tensor is ever read.
 __device__ __forceinline__ void load_levels(const int64_t* __restrict__ shapes, const int64_t* __restrict__ lsi,
-                                            int L, int* sH, int* sW, int* sStart) {
+                                            int L, int S, int* sH, int* sW, int* sStart) {
     for (int i = threadIdx.x; i < L; i += blockDim.x) {
-        sH[i] = (int)shapes[2 * i];
-        sW[i] = (int)shapes[2 * i + 1];
-        sStart[i] = (int)lsi[i];
+        const int64_t h = shapes[2 * i], w = shapes[2 * i + 1], st = lsi[i];
+        const bool ok = h >= 0 && w >= 0 && st >= 0 && st + h * w <= (int64_t)S;
+        sH[i] = ok ? (int)h : 0;
+        sW[i] = ok ? (int)w : 0;
+        sStart[i] = ok ? (int)st : 0;
     }
     __syncthreads();
 }
@@ -102,7 +107,7 @@ __global__ __launch_bounds__(256) void msda2d_fwd_kernel(const T* __restrict__ v
                                                           const T* __restrict__ attn, int N, int S, int M, int D, int L,
                                                           int Lq, int P, T* __restrict__ out) {
     __shared__ int sH[kMaxLevels2d], sW[kMaxLevels2d], sStart[kMaxLevels2d];
-    load_levels(shapes, lsi, L, sH, sW, sStart);
+    load_levels(shapes, lsi, L, S, sH, sW, sStart);
     const int lane = threadIdx.x & 63;
     const long wave = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (wave >= (long)N * Lq * M) return;
@@ -136,7 +141,7 @@ __global__ __launch_bounds__(256) void msda2d_bwd_kernel(const T* __restrict__ v
                                                           T* __restrict__ grad_value, T* __restrict__ grad_loc,
                                                           T* __restrict__ grad_attn) {
     __shared__ int sH[kMaxLevels2d], sW[kMaxLevels2d], sStart[kMaxLevels2d];
-    load_levels(shapes, lsi, L, sH, sW, sStart);
+    load_levels(shapes, lsi, L, S, sH, sW, sStart);
     const int lane = threadIdx.x & 63;
     const long wave = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (wave >= (long)N * Lq * M) return;
@@ -195,7 +200,7 @@ static int launch_bwd(const T* value, const int64_t* shapes, const int64_t* lsi,
                       const T* gout, int N, int S, int M, int D, int L, int Lq, int P, T* gv, T* gl, T* ga,
                       hipStream_t stream) {
     if ((long)N * S * M * D > 0) {
-        hipError_t e = hipMemsetAsync(gv, 0, sizeof(T) * (size_t)N * S * M * D, stream);
+        hipError_t e = zero_async(reinterpret_cast<float*>(gv), sizeof(T) / sizeof(float) * (size_t)N * S * M * D, stream);
         if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_value: %s", hipGetErrorString(e));
     }
     const long waves = (long)N * Lq * M;

@@ -141,6 +141,33 @@ struct Levels {
     int start[PDVC_MAX_LEVELS];
 };
 
+// Zero-fill as a kernel (vector stores).  hipMemsetAsync captured into a hipGraph did not re-zero its buffer
+// on replays after the first (tools/diag_refgrad.py: the decoder's atomically accumulated grad_ref kept the
+// previous replay's contents); a kernel node replays like every other launch.
+template <int V>
+__global__ __launch_bounds__(256) void zero_fill_kernel(float* __restrict__ p, size_t n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (V == 4) {
+        float4* q = reinterpret_cast<float4*>(p);
+        for (; i < n / 4; i += stride) q[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+        for (; i < n; i += stride) p[i] = 0.f;
+    }
+}
+
+static inline hipError_t zero_async(float* p, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const bool vec = ((uintptr_t)p % 16 == 0) && (n % 4 == 0);
+    const size_t work = vec ? n / 4 : n;
+    const unsigned blocks = (unsigned)(work / 256 + 1 < 8192 ? work / 256 + 1 : 8192);
+    if (vec)
+        hipLaunchKernelGGL(zero_fill_kernel<4>, dim3(blocks), dim3(256), 0, s, p, n);
+    else
+        hipLaunchKernelGGL(zero_fill_kernel<1>, dim3(blocks), dim3(256), 0, s, p, n);
+    return hipGetLastError();
+}
+
 }  // namespace pdvc
 
 // Host-side status plumbing (defined in pdvc_status.cpp).

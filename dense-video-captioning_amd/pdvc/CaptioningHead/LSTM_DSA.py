@@ -221,6 +221,11 @@ class LSTMDSACaptioner(Captioner):
         (logprobs, picked) where picked (R, n_steps) = logprobs at the target words (csrc/logprob.hip: log_softmax
         and the loss's gather in one pass, the backward in one pass -- the input of build_loss_picked)."""
         core = self.core
+        if self.training and self.ss_prob > 0:
+            # LSTM_DSA.py:89-99 feeds sampled words back when ss_prob > 0; the whole-sequence decode here takes
+            # every input word up front.  (train.py:156 sets ss_prob on the caption_head ModuleList, which no
+            # captioner reads, so the reference's schedule never reaches this point either.)
+            raise NotImplementedError("scheduled sampling (ss_prob > 0) is not supported by the batched decode")
         w = self._step_weights()
         value, mask_u8 = self._prepare(memory, mask_flatten)
         if n_steps == 0:
@@ -241,9 +246,13 @@ class LSTMDSACaptioner(Captioner):
         return F.log_softmax(logits, dim=-1)
 
     @torch.no_grad()
-    def decode_greedy(self, hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten, level_T, max_len=None):
-        """Greedy decoding (sample_max=1, LSTM_DSA.py:118-186) for all rows at once; returns
-        seq (R, T) and seqLogprobs (R, T) with the reference's unfinished-mask semantics, T <= max_len+1 steps."""
+    def decode_greedy(self, hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten, level_T, max_len=None,
+                      sample_max=1, temperature=1.0, generator=None):
+        """Caption decoding for all rows at once (LSTM_DSA.py:118-186); returns seq (R, T) and seqLogprobs
+        (R, T) with the reference's unfinished-mask semantics, T <= max_len + 1 steps.  sample_max=1: greedy
+        (argmax word and its log-probability).  sample_max=0: the next word is drawn from
+        exp(logprobs / temperature) (torch.multinomial, normalised; `generator` seeds it) and its log-probability
+        is the untempered logprobs at the drawn word, as LSTM_DSA.py:160-168."""
         R = hs_rows.shape[0]
         max_len = self.max_caption_len if max_len is None else max_len
         w = self._step_weights()
@@ -257,7 +266,13 @@ class LSTMDSACaptioner(Captioner):
         unfinished = None
         for t in range(max_len + 1):
             if t > 0:
-                sample_lp, it = torch.max(logprobs, 1)
+                if sample_max:
+                    sample_lp, it = torch.max(logprobs, 1)
+                else:
+                    prob = torch.exp(logprobs if temperature == 1.0 else torch.div(logprobs, temperature))
+                    it = torch.multinomial(prob, 1, generator=generator)
+                    sample_lp = logprobs.gather(1, it)
+                    it = it.view(-1)
             x_gates = F.linear(self.embed(it), w["W_x"])
             h, c = self._step(w, h, c, x_gates, hs_part, off_hs, value, mask_u8, row_video, ref_rows, rd1_rows,
                               level_T)
@@ -299,10 +314,12 @@ class LSTMDSACaptioner(Captioner):
                                           n_steps)
 
     def sample(self, hs, reference, others, opt={}):
-        if opt.get("sample_max", 1) != 1 or opt.get("beam_size", 1) != 1:
-            raise NotImplementedError("only greedy decoding (sample_max=1, beam_size=1) is supported")
+        """opt: sample_max (1 greedy, 0 multinomial), temperature, generator (torch.Generator for the draws);
+        beam_size is ignored, as in the reference (read at LSTM_DSA.py:124, never used)."""
         hs_rows, ref, rd1, rv, T = self._rows_from_reference(hs, reference, others)
-        seq, lp = self.decode_greedy(hs_rows, ref, rd1, rv, others["memory"], others["mask_flatten"], T)
+        seq, lp = self.decode_greedy(hs_rows, ref, rd1, rv, others["memory"], others["mask_flatten"], T,
+                                     sample_max=opt.get("sample_max", 1), temperature=opt.get("temperature", 1.0),
+                                     generator=opt.get("generator"))
         if seq is None:
             return [], []
         return seq, lp

@@ -8,7 +8,9 @@ gradient is accumulated, so communication overlaps the rest of the backward pass
 strictly in index order so every rank issues the same collective sequence.  Parameters that never receive a
 gradient (8 in PDVC: transformer.pos_trans*, and the caption head's unused attention_weights/output_proj,
 SURVEY.md section 8(e)) are detected on the first step and excluded, keeping `grad is None` as in the
-reference.  Semantics: after finish(), every gradient is the mean over ranks.
+reference.  A parameter found active on the first step whose gradient is None on a later step (a branch
+not taken on this rank) contributes zeros, so every rank still issues the same collectives, and receives the
+rank mean like every other.  Semantics: after finish(), every active gradient is the mean over ranks.
 """
 import os
 
@@ -93,7 +95,7 @@ class GradAllReducer:
                 self.next_launch += 1
 
     def _launch(self, bi):
-        grads = [p.grad for p in self.buckets[bi]]
+        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.buckets[bi]]
         flat = torch.cat([g.reshape(-1) for g in grads])
         work = dist.all_reduce(flat, group=self.group, async_op=True)
         self.works.append((bi, flat, work))
@@ -118,6 +120,9 @@ class GradAllReducer:
             off = 0
             for p in self.buckets[bi]:
                 n = p.numel()
-                p.grad.copy_(flat[off:off + n].view_as(p.grad))
+                if p.grad is None:
+                    p.grad = flat[off:off + n].view_as(p).clone()
+                else:
+                    p.grad.copy_(flat[off:off + n].view_as(p.grad))
                 off += n
         self._reset()

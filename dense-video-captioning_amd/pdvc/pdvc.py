@@ -399,8 +399,17 @@ class PDVC(nn.Module):
 
 
 class PostProcess(nn.Module):
-    """Model outputs -> per-video results (pdvc/pdvc.py:493-546): sigmoid scores, top-k query order,
-    (start, end) boxes clipped to [0,1] x duration, predicted event count, detokenised captions."""
+    """Eval outputs of a batch -> one result dict per video, in the reference's format (pdvc/pdvc.py:493-546).
+
+    Everything numeric is computed for the whole batch on the device, ranked per video by detection score:
+      scores        sigmoid(pred_logits) over the (query, class) grid, descending (top-k with k = Q);
+      query_id      the query of each ranked entry, labels its class;
+      boxes         (centre, length) -> (start, end), clamped to [0, 1], times the video's duration,
+                    gathered in ranked order (`raw_boxes` is the same tensor, as in the reference);
+      caption_scores  sum of the greedy tokens' log-probabilities over tokens > 0, in ranked order;
+      pred_seq_len  argmax of the count head, at least 1.
+    The caption scores and tokens reach the host in one copy; captions are detokenised there by the
+    loader's translator (`loader.dataset.translator.rtranslate`, data/video_dataset.py:172-180)."""
 
     def __init__(self, opt):
         super().__init__()
@@ -408,37 +417,31 @@ class PostProcess(nn.Module):
 
     @torch.no_grad()
     def forward(self, outputs, target_sizes, loader):
-        out_logits, out_bbox = outputs["pred_logits"], outputs["pred_boxes"]
-        N, N_q, N_class = out_logits.shape
-        assert len(out_logits) == len(target_sizes)
-        prob = out_logits.sigmoid()
-        topk_values, topk_indexes = torch.topk(prob.view(N, -1), N_q, dim=1)
-        scores = topk_values
-        topk_boxes = topk_indexes // N_class
-        labels = topk_indexes % N_class
-        boxes = box_ops.box_cl_to_xy(out_bbox)
-        raw_boxes = boxes.clone()
-        boxes = boxes.clamp(0, 1)
-        boxes = torch.gather(boxes, 1, topk_boxes.unsqueeze(-1).repeat(1, 1, 2))
-        scale = torch.stack([target_sizes, target_sizes], dim=1)
-        boxes = boxes * scale[:, None, :]
+        logits = outputs["pred_logits"]
+        N, Q, K = logits.shape
+        if len(target_sizes) != N:
+            raise ValueError(f"PostProcess: {len(target_sizes)} durations for {N} videos")
+        scores, ranked = logits.sigmoid().reshape(N, Q * K).topk(Q, dim=1)
+        query_id = torch.div(ranked, K, rounding_mode="floor")
+        labels = ranked - query_id * K
+        se = box_ops.box_cl_to_xy(outputs["pred_boxes"]).clamp(0, 1)
+        boxes = se.gather(1, query_id[..., None].expand(N, Q, 2)) * target_sizes.to(se.dtype)[:, None, None]
+        seq_len = outputs["pred_count"].argmax(dim=-1).clamp(min=1)
         seq = outputs["seq"]
-        cap_prob = outputs["caption_probs"]["cap_prob_eval"]
-        eseq_lens = outputs["pred_count"].argmax(dim=-1).clamp(min=1)
         if len(seq):
-            mask = (seq > 0).float()
-            cap_scores = (mask * cap_prob).sum(2).cpu().numpy().astype("float")
-            seq = seq.detach().cpu().numpy().astype("int")
-            caps = [[loader.dataset.translator.rtranslate(s) for s in s_vid] for s_vid in seq]
-            caps = [[caps[b][idx] for idx in row] for b, row in enumerate(topk_boxes)]
-            cap_scores = [[cap_scores[b, idx] for idx in row] for b, row in enumerate(topk_boxes)]
-        else:
-            cap_scores = [[-1e5] * N_q] * N
-            caps = [[""] * N_q] * N
-        return [{"scores": s, "labels": l, "boxes": b, "raw_boxes": b, "captions": c, "caption_scores": cs,
-                 "query_id": qid, "vid_duration": ts, "pred_seq_len": sl}
-                for s, l, b, rb, c, cs, qid, ts, sl in zip(scores, labels, boxes, raw_boxes, caps, cap_scores,
-                                                            topk_boxes, target_sizes, eseq_lens)]
+            cap_scores = (outputs["caption_probs"]["cap_prob_eval"] * (seq > 0)).sum(2).gather(1, query_id)
+            seq_ranked = seq.gather(1, query_id[..., None].expand(N, Q, seq.shape[2]))
+            tr = loader.dataset.translator
+            host_scores = cap_scores.double().cpu().numpy()
+            host_seq = seq_ranked.cpu().numpy().astype("int")
+            caps = [[tr.rtranslate(s) for s in vid] for vid in host_seq]
+            cap_scores = [list(row) for row in host_scores]
+        else:  # no caption decoded (every query finished at once)
+            cap_scores = [[-1e5] * Q for _ in range(N)]
+            caps = [[""] * Q for _ in range(N)]
+        return [{"scores": scores[b], "labels": labels[b], "boxes": boxes[b], "raw_boxes": boxes[b],
+                 "captions": caps[b], "caption_scores": cap_scores[b], "query_id": query_id[b],
+                 "vid_duration": target_sizes[b], "pred_seq_len": seq_len[b]} for b in range(N)]
 
 
 def build(args):

@@ -358,6 +358,42 @@ def ref_args(cfg, **over):
     return args
 
 
+def pack_grad(res, name, g):
+    """Store one full gradient tensor under `name`.  A 2-D gradient of low numerical rank (a Linear weight
+    gradient is a sum of one outer product per GEMM row: rank <= rows, e.g. S = 30 rows per video at T = 16)
+    is stored as float32 factors `name.A` (m, r) @ `name.B` (r, n) of its float64 SVD, with the smallest r
+    whose float32-factor reconstruction is within 1e-6 * max(1, max|g|) of every element; the achieved
+    error is stored as `name.err`.  The tests rebuild the full tensor and compare every element."""
+    g = g.detach().double().cpu().numpy()
+    shape = g.shape
+    if g.ndim > 2:  # conv weights (out, in, k): factored as (out, in*k)
+        g = g.reshape(shape[0], -1)
+    if g.ndim == 2 and min(g.shape) >= 32:
+        m, n = g.shape
+        U, s, Vt = np.linalg.svd(g, full_matrices=False)
+        bound = 1e-6 * max(1.0, float(np.abs(g).max()))
+        # candidate ranks: singular values above a relative noise floor, grown until the bound holds
+        r = int((s > s[0] * 1e-7).sum()) if s[0] > 0 else 1
+        while r <= min(m, n) and (m + n) * r < m * n // 2:
+            A = (U[:, :r] * s[:r]).astype(np.float32)
+            B = Vt[:r].astype(np.float32)
+            err = float(np.abs(A.astype(np.float64) @ B.astype(np.float64) - g).max())
+            if err <= bound:
+                res[name + ".A"], res[name + ".B"], res[name + ".err"] = A, B, np.float64(err)
+                res[name + ".shape"] = np.asarray(shape, np.int64)
+                return
+            r = max(r + 1, int(r * 1.25))
+    res[name] = g.reshape(shape).astype(np.float32)
+
+
+def pack_model_grads(res, model, scale=1.0):
+    for n, p in model.named_parameters():
+        if p.grad is None:
+            res["gradnone." + n] = np.zeros(0)
+        else:
+            pack_grad(res, "grad." + n, p.grad * scale)
+
+
 def whole_model():
     import io
     from pdvc.pdvc import build
@@ -396,15 +432,7 @@ def whole_model():
         for li, (i, j) in enumerate(out["matched_indices"][0]):
             res[f"matched.last.{li}.q"] = i
             res[f"matched.last.{li}.g"] = j
-        for n, p in model.named_parameters():
-            if p.grad is None:
-                res["gradnone." + n] = np.zeros(0)
-                continue
-            g = p.grad.detach().double().reshape(-1)
-            res["gsum." + n] = g.sum()
-            res["gnorm." + n] = g.norm()
-            idx = np.linspace(0, g.numel() - 1, num=min(16, g.numel())).astype(np.int64)
-            res["gsamp." + n] = g[idx]
+        pack_model_grads(res, model)
         res["param_names"] = np.asarray([n for n, _ in model.named_parameters()])
         res["state_keys"] = np.asarray(list(model.state_dict().keys()))
         res["state_shapes"] = np.asarray([",".join(str(s) for s in v.shape) for v in model.state_dict().values()])
@@ -435,6 +463,214 @@ def whole_model():
         save(name, **res)
 
 
+def synthetic_translator(vocab):
+    """The reference Translator (data/video_dataset.py:152-180) over a synthetic vocabulary w1..w{vocab}."""
+    import json
+    import tempfile
+    from data.video_dataset import Translator
+    vocab_json = {"word_to_ix": {f"w{i}": i for i in range(1, vocab + 1)},
+                  "ix_to_word": {str(i): f"w{i}" for i in range(1, vocab + 1)}}
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+        json.dump(vocab_json, f)
+        path = f.name
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        tr = Translator(path, vocab)
+    os.unlink(path)
+    return tr
+
+
+def whole_model_batch():
+    """Reference batch-1 training steps on three different videos (batch_items): per-video losses, matched
+    indices of every decoder layer, captioning log-probabilities and heads; the MEAN of the three per-video
+    gradients as full tensors (what one 3-video batch of the MI355X path must produce: every loss is the mean
+    over videos of the batch-1 value, pdvc/criterion.py:154-198 normalising per video).  Also each video's eval
+    forward (greedy captions) and the reference PostProcess (pdvc/pdvc.py:493-546) on it."""
+    import io
+    import types as _types
+    from pdvc.pdvc import build, PostProcess
+    from data.video_dataset import collate_fn
+    over = dict(feature_dim=32, num_queries=10, enc_layers=2, dec_layers=2, transformer_ff_dim=64,
+                vocab_size=29, transformer_dropout_prob=0.0, drop_prob=0.0, max_caption_len=8)
+    cfg = "cfgs/anet_tsp_pdvc.yml"
+    args = ref_args(cfg, **over)
+    torch.manual_seed(0)
+    with contextlib.redirect_stdout(io.StringIO()):
+        model, criterion, post = build(args)
+    W.fill_module(model, overrides={"sampling_offsets": 0.5})
+    items = W.batch_items(vocab=args.vocab_size)
+    T = max(it[0].shape[0] for it in items)
+    captured = {}
+    orig_forward = criterion.forward
+
+    def capture(*a, **k):
+        r = orig_forward(*a, **k)
+        captured["r"] = r
+        return r
+    criterion.forward = capture
+    tr = synthetic_translator(args.vocab_size)
+    loader = _types.SimpleNamespace(dataset=_types.SimpleNamespace(translator=tr))
+    res = {}
+    grads = {}
+    wd = criterion.weight_dict
+    nv = len(items)
+    for v, item in enumerate(items):
+        dt = collate_fn([item])
+        Tv = dt["video_tensor"].shape[1]
+        if Tv < T:  # the batch's padding of this video (collate_fn pads every video to the longest)
+            dt["video_tensor"] = torch.cat([dt["video_tensor"], dt["video_tensor"].new_zeros(1, T - Tv, 32)], 1)
+            dt["video_mask"] = torch.cat([dt["video_mask"], dt["video_mask"].new_zeros(1, T - Tv)], 1)
+        model.train()
+        model.zero_grad(set_to_none=True)
+        out, loss = model(dt, criterion, "queries")
+        total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
+        total.backward()
+        for n, p in model.named_parameters():
+            if p.grad is not None:
+                grads[n] = grads.get(n, 0) + p.grad.detach().double() / nv
+            else:
+                grads.setdefault(n, None)
+        res[f"v{v}.total_loss"] = total.detach()
+        for k, val in loss.items():
+            res[f"v{v}.loss.{k}"] = val.detach() if isinstance(val, torch.Tensor) else np.asarray(val)
+        res[f"v{v}.pred_logits"] = out["pred_logits"]
+        res[f"v{v}.pred_boxes"] = out["pred_boxes"]
+        res[f"v{v}.pred_count"] = out["pred_count"]
+        res[f"v{v}.cap_prob_train"] = out["caption_probs"]["cap_prob_train"]
+        _, last_indices, aux_indices = captured["r"]
+        layer_idx = [aux_indices[l][0] for l in range(len(aux_indices))] + [last_indices[0]]
+        for l_id, ind in enumerate(layer_idx):
+            i, j = ind[0]
+            res[f"v{v}.matched.{l_id}.q"] = i
+            res[f"v{v}.matched.{l_id}.g"] = j
+        # eval forward + PostProcess on this video
+        model.eval()
+        with torch.no_grad():
+            out_e, _ = model(dt, criterion, "queries", eval_mode=True)
+            pp = post["bbox"](out_e, dt["video_length"][:, 1], loader)[0]
+        res[f"v{v}.eval.pred_logits"] = out_e["pred_logits"]
+        res[f"v{v}.eval.pred_boxes"] = out_e["pred_boxes"]
+        res[f"v{v}.eval.pred_count"] = out_e["pred_count"]
+        res[f"v{v}.eval.seq"] = out_e["seq"]
+        res[f"v{v}.eval.cap_prob_eval"] = out_e["caption_probs"]["cap_prob_eval"]
+        for k in ("scores", "labels", "boxes", "query_id", "vid_duration", "pred_seq_len"):
+            res[f"v{v}.post.{k}"] = pp[k]
+        res[f"v{v}.post.caption_scores"] = np.asarray(pp["caption_scores"], np.float64)
+        res[f"v{v}.post.captions"] = np.asarray(pp["captions"])
+    for n, g in grads.items():
+        if g is None:
+            res["gradnone." + n] = np.zeros(0)
+        else:
+            pack_grad(res, "grad." + n, g)
+    res["param_names"] = np.asarray([n for n, _ in model.named_parameters()])
+    res["args"] = np.asarray([f"{k}={v!r}" for k, v in sorted(over.items())] + [f"cfg={cfg!r}"])
+    res["n_videos"] = np.asarray(nv)
+    save("pdvc_batch3_anet", **res)
+
+
+INGEST_WORDS = ["a", "man", "is", "cutting", "the", "onion", "with", "knife", "woman", "pours", "water", "into",
+                "pot", "and", "stirs", "it", "slowly", "then", "adds", "salt"]
+INGEST_SENTENCES = ["A man is cutting the onion.", "The woman pours water into the pot, and stirs it slowly!",
+                    "then-adds salt/pepper; \"quickly\"", "  ", "UNKNOWN words: zebra_unicorn?",
+                    "a man a man a man a man a man a man a man a man a man", "stirs\\nthe\\pot"]
+
+
+def data_ingestion():
+    """Reference data path (data/video_dataset.py): resizeFeature (:386-397), Translator (:152-180),
+    process_time_step (:210-217) and PropSeqDataset.__getitem__ (:232-293) on feature files written to a
+    temporary folder; the inputs (feature arrays, annotation and vocabulary JSON text) are stored with the
+    outputs so the test rebuilds the same folder."""
+    import io
+    import json
+    import shutil
+    import tempfile
+    from data.video_dataset import resizeFeature, PropSeqDataset, EDVCdataset
+    rng = np.random.RandomState(17)
+    res = {}
+    for c, (t0, n) in enumerate([(1, 5), (7, 16), (16, 7), (10, 10), (33, 100), (100, 33), (2, 3), (513, 512)]):
+        x = rng.randn(t0, 4).astype(np.float32)
+        res[f"resize.{c}.in"] = x
+        res[f"resize.{c}.n"] = np.asarray(n)
+        res[f"resize.{c}.out"] = resizeFeature(x, n, "nearest")
+    vocab = {"word_to_ix": {w: i + 1 for i, w in enumerate(INGEST_WORDS)},
+             "ix_to_word": {str(i + 1): w for i, w in enumerate(INGEST_WORDS)}}
+    vocab_text = json.dumps(vocab)
+    tmp = tempfile.mkdtemp(prefix="pdvc_ingest_")
+    try:
+        vpath = os.path.join(tmp, "vocab.json")
+        with open(vpath, "w") as f:
+            f.write(vocab_text)
+        from data.video_dataset import Translator
+        with contextlib.redirect_stdout(io.StringIO()):
+            tr = Translator(vpath, len(INGEST_WORDS))
+        for i, s in enumerate(INGEST_SENTENCES):
+            for ml in (6, 30):
+                res[f"translate.{i}.{ml}"] = tr.translate(s, ml)
+        ids = [[3, 4, 5, 0, 7], [0, 1], [1, 2, 3], [], [20, 19, 18, 0, 0]]
+        for i, s in enumerate(ids):
+            res[f"rtranslate.{i}.in"] = np.asarray(s, np.int64)
+            res[f"rtranslate.{i}.out"] = np.asarray(tr.rtranslate(np.asarray(s, np.int64)))
+        pts = [(120.0, [[0.0, 10.5], [100.0, 130.0]], 100), (33.3, [[1.0, 2.0], [-5.0, 33.3]], 64)]
+        for i, (dur, ts, fl) in enumerate(pts):
+            res[f"timestep.{i}.out"] = np.asarray(EDVCdataset.process_time_step(None, dur, ts, fl))
+        # a feature folder: 4 videos (vggish npy of different lengths, one missing, one of a single row),
+        # plus tsn_100 csv files for the two-type dataset
+        keys = ["v_QOlSCBRmfWY", "v_ehGHCYKzyZ8", "v_nwznKOuZM7w", "v_missing0000"]
+        lengths = [37, 5, 1, None]
+        anno = {}
+        os.makedirs(os.path.join(tmp, "vgg"))
+        os.makedirs(os.path.join(tmp, "tsn"))
+        for k, T0 in zip(keys, lengths):
+            if T0 is not None:
+                f = rng.randn(T0, 128).astype(np.float32)
+                res[f"feat.{k}"] = f
+                np.save(os.path.join(tmp, "vgg", k[:13] + ".npy"), f)
+                ftsn = rng.randn(T0 + 2, 400).astype(np.float64).round(5)
+                res[f"tsn.{k}"] = ftsn
+                import pandas as pd
+                pd.DataFrame(ftsn).to_csv(os.path.join(tmp, "tsn", k[:13] + ".csv"), index=False)
+            ne = int(rng.randint(1, 14))
+            dur = float(rng.uniform(20, 200))
+            ts = np.sort(rng.uniform(0, dur, size=(ne, 2)), 1).round(2).tolist()
+            anno[k] = {"duration": round(dur, 2), "timestamps": ts,
+                       "sentences": [INGEST_SENTENCES[int(rng.randint(len(INGEST_SENTENCES)))] for _ in range(ne)]}
+        anno_text = json.dumps(anno)
+        apath = os.path.join(tmp, "anno.json")
+        with open(apath, "w") as f:
+            f.write(anno_text)
+        res["anno_json"] = np.asarray(anno_text)
+        res["vocab_json"] = np.asarray(vocab_text)
+        res["keys"] = np.asarray(keys)
+        for name, vtype, folder, fdim, rescale in (
+                ("single", "vggish", os.path.join(tmp, "vgg"), 128, 1),
+                ("multi", ["vggish", "tsn_100"], [os.path.join(tmp, "vgg"), os.path.join(tmp, "tsn")], 528, 1),
+                ("norescale", "vggish", os.path.join(tmp, "vgg"), 128, 0)):
+            opt = types.SimpleNamespace(vocab_size=len(INGEST_WORDS), max_caption_len=8, invalid_video_json=[],
+                                        feature_sample_rate=2, train_proposal_sample_num=24,
+                                        gt_proposal_sample_num=4, feature_dim=fdim, num_queries=10,
+                                        visual_feature_type=vtype, data_rescale=rescale, frame_embedding_num=16,
+                                        data_norm=0, num_classes=1)
+            with contextlib.redirect_stdout(io.StringIO()):
+                ds = PropSeqDataset(apath, folder, vpath, True, "gt", opt)
+                np.random.seed(123)
+                for i in range(len(ds)):
+                    feats, fst, labels, caps, ts, dur, raw, key = ds[i]
+                    p = f"ds.{name}.{i}."
+                    res[p + "feats"] = np.asarray(feats)
+                    res[p + "featstamps"] = np.asarray(fst, np.int64).reshape(-1, 2)
+                    res[p + "labels"] = np.asarray(labels, np.int64)
+                    res[p + "ncaps"] = np.asarray(len(caps))
+                    for j, cp in enumerate(caps):
+                        res[p + f"cap{j}"] = np.asarray(cp, np.int64)
+                    res[p + "timestamps"] = np.asarray(ts, np.float64).reshape(-1, 2)
+                    res[p + "duration"] = np.asarray(dur)
+                    res[p + "raw"] = np.asarray(raw)
+                    res[p + "key"] = np.asarray(key)
+    finally:
+        shutil.rmtree(tmp)
+    save("data_ingestion", **res)
+
+
 def state_dict_keys_full():
     """Key list + shapes of the full-size anet_tsp_pdvc model with BASELINE's overrides (C=768, Q=100)."""
     import io
@@ -454,7 +690,8 @@ def state_dict_keys_full():
 if __name__ == "__main__":
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     which = sys.argv[1:] or ["op_reftest", "op_1d", "op_sample", "module_msdeformattn", "module_layers",
-                             "module_captioner", "whole_model", "state_dict_keys_full"]
+                             "module_captioner", "whole_model", "whole_model_batch", "data_ingestion",
+                             "state_dict_keys_full"]
     for w in which:
         globals()[w]()
     for k, v in OUT.items():

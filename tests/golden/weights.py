@@ -57,3 +57,27 @@ def synthetic_video_batch(n_videos, T, C, n_events, n_words, vocab, duration=120
         batch.append((feat, featstamps, [0] * ne, caps, [list(t) for t in ts], duration,
                       ["w"] * ne, f"v_{seed}_{v}"))
     return batch
+
+
+def batch_items(seed=21, C=32, vocab=29):
+    """Three videos in the reference collate_fn tuple format (data/video_dataset.py:15-149) with different
+    event counts (2, 3, 5), caption lengths and durations; video 1 has 12 frames, so in a batch of 16-frame
+    videos its mask is padded (False) over the last 4 frames."""
+    rng = np.random.RandomState(seed)
+    spec = [(16, [5, 2], 120.0), (12, [3, 6, 4], 90.0), (16, [6, 3, 1, 5, 4], 150.0)]
+    items = []
+    for v, (Tv, words, dur) in enumerate(spec):
+        feat = rng.randn(Tv, C).astype(np.float32)
+        ne = len(words)
+        ts = np.sort(rng.uniform(0, dur, size=(ne, 2)), axis=1)
+        ts[:, 1] = np.minimum(np.maximum(ts[:, 1], ts[:, 0] + 1.0), dur)
+        caps = [np.array([0] + list(rng.randint(1, vocab, size=w)) + [0], dtype=np.int64) for w in words]
+        stamps = [[t[0] / dur * Tv, t[1] / dur * Tv] for t in ts]
+        items.append((feat, stamps, [0] * ne, caps, [list(t) for t in ts], dur, ["w"] * ne, f"b3_{v}"))
+    return items
+
+
+def dp_items(vocab=29):
+    """Four videos for the data-parallel equivalence test: batch_items' three plus a fourth 16-frame video;
+    split over 2 ranks as [0, 1] and [2, 3], every rank's batch pads to the union's 16 frames."""
+    return batch_items(seed=21, vocab=vocab) + batch_items(seed=22, vocab=vocab)[2:]

@@ -1,6 +1,8 @@
 """CPU, world_size 2 over gloo: the data-parallel gradient all-reducer (pdvc/distributed.py) gives every rank
 the mean of the per-rank gradients, keeps never-used parameters at grad None (as the reference's 8 unused
-PDVC parameters), overlaps buckets with backward (several buckets in flight), and survives repeated steps."""
+PDVC parameters), overlaps buckets with backward (several buckets in flight), survives repeated steps, builds
+the same bucket order on every rank, and treats a gradient missing on one rank in a later step (a branch not
+taken there) as zeros -- both ranks still issue identical collectives and receive the mean."""
 import os
 import socket
 
@@ -25,20 +27,27 @@ class Toy(torch.nn.Module):
         self.b = torch.nn.Linear(32, 8)
         self.unused = torch.nn.Linear(8, 8)  # never touched by forward
         self.shared = torch.nn.Linear(8, 8)
+        self.branch = torch.nn.Linear(8, 8)  # used on every step except rank 1's second
 
-    def forward(self, x):
+    def forward(self, x, branch=True):
         h = torch.relu(self.a(x))
         y = self.b(h)
+        if branch:
+            y = y + self.branch(y)
         return (self.shared(y) + self.shared(y * 0.5)).pow(2).mean()
+
+
+def _branch(rank, step):
+    return not (rank == 1 and step == 1)
 
 
 def _grads_single(seed_rank, steps_data):
     torch.manual_seed(0)
     m = Toy()
     out = []
-    for x in steps_data[seed_rank]:
+    for step, x in enumerate(steps_data[seed_rank]):
         m.zero_grad(set_to_none=True)
-        m(x).backward()
+        m(x, _branch(seed_rank, step)).backward()
         out.append({n: (p.grad.clone() if p.grad is not None else None) for n, p in m.named_parameters()})
     return out
 
@@ -56,12 +65,13 @@ def _worker(rank, world, port, data, q):
     broadcast_parameters(m)
     red = GradAllReducer(list(m.parameters()), bucket_mb=0.002)  # tiny buckets: several in flight
     res = []
-    for x in data[rank]:
+    for step, x in enumerate(data[rank]):
         m.zero_grad(set_to_none=True)
-        m(x).backward()
+        m(x, _branch(rank, step)).backward()
         red.finish()
         res.append({n: (p.grad.numpy().copy() if p.grad is not None else None) for n, p in m.named_parameters()})
-    q.put((rank, res, len(red.buckets)))
+    names = {id(p): n for n, p in m.named_parameters()}
+    q.put((rank, res, [[names[id(p)] for p in b] for b in red.buckets]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -76,11 +86,14 @@ def test_grad_allreduce_is_mean_of_ranks():
     procs = [ctx.Process(target=_worker, args=(r, world, port, data, q)) for r in range(world)]
     for p in procs:
         p.start()
-    results = dict()
+    results, orders = dict(), dict()
     for _ in range(world):
-        r, res, nb = q.get(timeout=120)
+        r, res, buckets = q.get(timeout=120)
         results[r] = res
-        assert nb >= 2
+        orders[r] = buckets
+        assert len(buckets) >= 2
+    assert orders[0] == orders[1], "bucket order differs between ranks"
+    assert not any(n.startswith("unused") for b in orders[0] for n in b)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -90,6 +103,10 @@ def test_grad_allreduce_is_mean_of_ranks():
             if name.startswith("unused"):
                 assert results[0][step][name] is None and results[1][step][name] is None
                 continue
-            expect = (singles[0][step][name] + singles[1][step][name]) / 2
+            g0, g1 = singles[0][step][name], singles[1][step][name]
+            if g1 is None:  # rank 1 skipped the branch on this step: it contributes zeros
+                assert name.startswith("branch") and step == 1
+                g1 = torch.zeros_like(g0)
+            expect = (g0 + g1) / 2
             for r in range(world):
                 torch.testing.assert_close(torch.from_numpy(results[r][step][name]), expect, rtol=1e-6, atol=1e-7)

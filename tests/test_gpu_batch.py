@@ -1,0 +1,176 @@
+"""GPU parity of the BATCHED training step -- the path bench.py times at 1024 videos per GPU -- against the
+reference run one video at a time (tests/golden/make_golden.py::whole_model_batch).
+
+The reference cannot batch (pdvc/CaptioningHead/LSTM_DSA.py:59,121 assert one video) and normalises every
+loss by that video's event count (pdvc/criterion.py:167-171).  The MI355X path's batch semantics: every loss
+key is the mean over videos of the reference's batch-1 value, so the gradient of one N-video step is the mean
+of the N batch-1 gradients.  The fixture has 3 videos with 2, 3 and 5 events, ragged caption lengths,
+different durations and one padded (masked) video; it holds each video's losses, matched indices of every
+decoder layer, heads, captioning log-probabilities, eval outputs and PostProcess results, and the mean
+gradient of every parameter as a full tensor.  Tolerance: 1e-4 * max(1, max|ref|) per tensor (fp32);
+matched indices, ranked query ids, labels, counts and greedy tokens bit-exact."""
+import os
+import sys
+import types
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import test_gpu_model as TM  # noqa: E402
+
+DEV = "cuda"
+TOL = 1e-4
+NAME = "pdvc_batch3_anet"
+
+
+def close(got, ref, what, tol=TOL):
+    got = got.detach().double().cpu().numpy() if isinstance(got, torch.Tensor) else np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    assert got.shape == ref.shape, f"{what}: shape {got.shape} vs {ref.shape}"
+    if ref.size == 0:
+        return
+    err = float(np.abs(got - ref).max())
+    scale = max(1.0, float(np.abs(ref).max()))
+    assert err <= tol * scale, f"{what}: max|diff| {err:.3e} > {tol:.0e} * {scale:.3g}"
+
+
+def batch_dt(d):
+    """The 3 fixture videos as ONE batch through our collate (the reference collate_fn's padding)."""
+    import weights as W
+    from pdvc.data import collate, to_device
+    return to_device(collate(W.batch_items(vocab=29)), DEV)
+
+
+class Capture:
+    """Wraps a criterion's forward to keep its (losses, last_indices, aux_indices) return value."""
+
+    def __init__(self, criterion):
+        self.result = None
+        orig = criterion.forward
+
+        def fwd(*a, **k):
+            self.result = orig(*a, **k)
+            return self.result
+        criterion.forward = fwd
+
+    def layer_indices(self):
+        _, last, aux = self.result
+        return [list(aux[l][0]) for l in range(len(aux))] + [list(last[0])]
+
+
+@pytest.fixture(scope="module")
+def fixture():
+    return TM.load(NAME)
+
+
+def _check_forward(d, out, loss, cap, nv):
+    wd_keys = [f[len("v0.loss."):] for f in d.files if f.startswith("v0.loss.")]
+    for k in wd_keys:
+        ref = np.mean([float(d[f"v{v}.loss.{k}"]) for v in range(nv)])
+        got = loss[k].item() if isinstance(loss[k], torch.Tensor) else float(loss[k])
+        assert abs(got - ref) <= TOL * max(1.0, abs(ref)), f"loss {k}: {got} vs mean of batch-1 {ref}"
+    for v in range(nv):
+        close(out["pred_logits"][v:v + 1], d[f"v{v}.pred_logits"], f"video {v} pred_logits")
+        close(out["pred_boxes"][v:v + 1], d[f"v{v}.pred_boxes"], f"video {v} pred_boxes")
+        close(out["pred_count"][v:v + 1], d[f"v{v}.pred_count"], f"video {v} pred_count")
+    for l_id, per_video in enumerate(cap.layer_indices()):
+        for v, (i, j) in enumerate(per_video):
+            assert i.tolist() == d[f"v{v}.matched.{l_id}.q"].tolist(), f"layer {l_id} video {v} matched queries"
+            assert j.tolist() == d[f"v{v}.matched.{l_id}.g"].tolist(), f"layer {l_id} video {v} matched targets"
+    # captioning log-probabilities of the last layer: rows grouped by video, each video's own step count
+    probs = out["caption_probs"]["cap_prob_train"]
+    row = 0
+    for v in range(nv):
+        ref = d[f"v{v}.cap_prob_train"]
+        e, steps = ref.shape[0], ref.shape[1]
+        close(probs[row:row + e, :steps], ref, f"video {v} cap_prob_train")
+        row += e
+    assert row == probs.shape[0]
+
+
+def _check_grads(d, named_params, what):
+    n_checked = 0
+    for n, p in named_params:
+        if "gradnone." + n in d.files:
+            assert p.grad is None, f"{what}: {n} must receive no gradient (as in the reference)"
+            continue
+        assert p.grad is not None, f"{what}: {n} has no gradient"
+        close(p.grad, TM.full_grad(d, n), f"{what}: grad {n}")
+        n_checked += 1
+    assert n_checked > 100
+
+
+def test_batched_step_equals_mean_of_reference_batch1_steps(fixture):
+    d = fixture
+    nv = int(d["n_videos"])
+    model, criterion = TM.build_filled(d)
+    model.train()
+    dt = batch_dt(d)
+    assert dt["video_tensor"].shape[0] == nv and not bool(dt["video_mask"].all()), "fixture must pad one video"
+    cap = Capture(criterion)
+    out, loss = model(dt, criterion, "queries")
+    _check_forward(d, out, loss, cap, nv)
+    wd = criterion.weight_dict
+    total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
+    ref_total = np.mean([float(d[f"v{v}.total_loss"]) for v in range(nv)])
+    assert abs(total.item() - ref_total) <= TOL * max(1.0, abs(ref_total))
+    total.backward()
+    _check_grads(d, model.named_parameters(), "eager batch")
+
+
+def test_batched_step_graph_equals_reference(fixture):
+    """The same batch through StepGraph (forward + losses + backward as one hipGraph replay, the bench path)."""
+    from pdvc.step_graph import StepGraph
+    d = fixture
+    nv = int(d["n_videos"])
+    model, criterion = TM.build_filled(d)
+    model.train()
+    dt = batch_dt(d)
+    sg = StepGraph(model, criterion, dt)
+    for _ in range(2):
+        total = sg.replay().item()
+        ref_total = np.mean([float(d[f"v{v}.total_loss"]) for v in range(nv)])
+        assert abs(total - ref_total) <= TOL * max(1.0, abs(ref_total))
+        _check_grads(d, model.named_parameters(), "step graph")
+
+
+def test_batched_eval_and_postprocess_match_reference(fixture):
+    """Eval forward (greedy captions) of the 3-video batch and our PostProcess on it against each video's
+    reference eval forward and reference PostProcess (pdvc/pdvc.py:493-546)."""
+    from data.video_dataset import Translator
+    d = fixture
+    nv = int(d["n_videos"])
+    model, criterion = TM.build_filled(d)
+    model.eval()
+    dt = batch_dt(d)
+    with torch.no_grad():
+        out, _ = model(dt, criterion, "queries", eval_mode=True)
+    tr = Translator.from_vocab({str(i): f"w{i}" for i in range(1, 30)})
+    loader = types.SimpleNamespace(dataset=types.SimpleNamespace(translator=tr))
+    post = TM.build_post(d)
+    res = post(out, dt["video_length"][:, 1], loader)
+    assert len(res) == nv
+    for v in range(nv):
+        close(out["pred_logits"][v:v + 1], d[f"v{v}.eval.pred_logits"], f"video {v} eval pred_logits")
+        close(out["pred_boxes"][v:v + 1], d[f"v{v}.eval.pred_boxes"], f"video {v} eval pred_boxes")
+        ref_seq = d[f"v{v}.eval.seq"]
+        steps = ref_seq.shape[-1]
+        got_seq = out["seq"][v:v + 1].cpu().numpy()
+        assert got_seq[..., :steps].tolist() == ref_seq.tolist(), f"video {v} greedy tokens"
+        assert not got_seq[..., steps:].any(), f"video {v}: tokens after the video's last step"
+        close(out["caption_probs"]["cap_prob_eval"][v:v + 1, :, :steps], d[f"v{v}.eval.cap_prob_eval"],
+              f"video {v} cap_prob_eval")
+        r = res[v]
+        close(r["scores"], d[f"v{v}.post.scores"], f"video {v} scores")
+        assert r["query_id"].tolist() == d[f"v{v}.post.query_id"].tolist(), f"video {v} ranked query ids"
+        assert r["labels"].tolist() == d[f"v{v}.post.labels"].tolist()
+        close(r["boxes"], d[f"v{v}.post.boxes"], f"video {v} boxes")
+        close(r["raw_boxes"], d[f"v{v}.post.boxes"], f"video {v} raw_boxes (the reference returns boxes)")
+        close(r["vid_duration"], d[f"v{v}.post.vid_duration"], f"video {v} duration")
+        assert int(r["pred_seq_len"]) == int(d[f"v{v}.post.pred_seq_len"])
+        close(np.asarray(r["caption_scores"]), d[f"v{v}.post.caption_scores"], f"video {v} caption scores")
+        assert list(r["captions"]) == [str(s) for s in d[f"v{v}.post.captions"]], f"video {v} captions"

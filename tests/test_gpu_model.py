@@ -1,6 +1,7 @@
 """GPU parity of whole PDVC training fwd+bwd and eval fwd against golden vectors produced by the reference
 model (tests/golden/make_golden.py::whole_model): losses, captioning logits (log-probabilities), boxes,
-matched segment indices (bit-exact), greedy caption tokens, and per-parameter gradient checksums."""
+matched segment indices (bit-exact), greedy caption tokens, and every parameter gradient as a full tensor
+(1e-4 * max(1, max|ref|) per tensor)."""
 import ast
 import os
 import sys
@@ -63,6 +64,22 @@ def build_filled(d):
     return model, criterion
 
 
+def full_grad(d, name):
+    """The reference gradient of parameter `name` as a full float64 tensor: stored whole, or as the float32
+    factors A @ B of its SVD (make_golden.py::pack_grad; reconstruction error <= 1e-6 * max(1, max|g|),
+    recorded as `.err`)."""
+    k = "grad." + name
+    if k in d.files:
+        return d[k].astype(np.float64)
+    g = d[k + ".A"].astype(np.float64) @ d[k + ".B"].astype(np.float64)
+    return g.reshape(tuple(int(x) for x in d[k + ".shape"]))
+
+
+def build_post(d):
+    from pdvc.pdvc import PostProcess
+    return PostProcess(fixture_args(d))
+
+
 def close(a, b, rtol, atol, what):
     a = a.detach().float().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
     b = np.asarray(b)
@@ -116,12 +133,12 @@ def test_training_step_matches_reference(case):
             assert p.grad is None, f"{n} must receive no gradient (as in the reference)"
             continue
         assert p.grad is not None, n
-        g = p.grad.detach().double().reshape(-1).cpu().numpy()
-        gnorm = float(d["gnorm." + n])
-        scale = max(gnorm, 1e-6)
-        assert abs(np.linalg.norm(g) - gnorm) <= 2e-4 * scale + 1e-7, f"{n}: |g| {np.linalg.norm(g)} vs {gnorm}"
-        idx = np.linspace(0, g.size - 1, num=min(16, g.size)).astype(np.int64)
-        np.testing.assert_allclose(g[idx], d["gsamp." + n], rtol=2e-3, atol=2e-4 * scale + 1e-7, err_msg=n)
+        ref = full_grad(d, n)
+        g = p.grad.detach().double().cpu().numpy()
+        assert g.shape == ref.shape, n
+        err = float(np.abs(g - ref).max())
+        scale = max(1.0, float(np.abs(ref).max()))
+        assert err <= 1e-4 * scale, f"grad {n}: max|diff| {err:.3e} > 1e-4 * {scale:.3g}"
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -192,8 +209,12 @@ def test_step_graph_matches_eager():
         return total.item(), {n: (p.grad.clone() if p.grad is not None else None) for n, p in model.named_parameters()}
 
     t0, g0 = eager()
+    # a fresh batch dict (no caches from the eager step) and three replays: a buffer the graph fails to
+    # re-initialise shows up from the second replay on
+    dt = fixture_dt(d)
+    dt["video_length"] = dt["video_length"].contiguous()
     sg = StepGraph(model, criterion, dt)
-    for _ in range(2):
+    for _ in range(3):
         t1 = sg.replay().item()
         assert abs(t1 - t0) <= 1e-5 * max(1.0, abs(t0)), (t1, t0)
         for n, p in model.named_parameters():

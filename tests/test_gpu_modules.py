@@ -225,6 +225,52 @@ def test_captioner_vs_golden(ref_dim):
     close(lp, d["sample_logprobs"], 1e-4, "greedy logprobs")
 
 
+@pytest.mark.parametrize("temperature", [1.0, 0.5])
+def test_captioner_multinomial_sampling(temperature):
+    """sample_max=0 (LSTM_DSA.py:160-168): words drawn from exp(logprobs / temperature).  The draws are
+    random (parity unpinned: torch's device RNG is not the reference's CPU RNG), so the test checks the
+    law: 4096 copies of one event row share the first step's distribution; the frequency ratio of two drawn
+    words must match exp((lp_a - lp_b) / temperature) within 5 standard errors, every returned log-probability
+    must be the untempered log-probability of its word (equal words -> equal values), a seeded generator
+    must reproduce the draws, and the unfinished-mask semantics must hold (zeros after a row's first 0)."""
+    from pdvc.CaptioningHead.LSTM_DSA import LSTMDSACaptioner
+    d = load("module_captioner_ref1")
+    cap = LSTMDSACaptioner(small_opt()).to(DEV)
+    fill(cap)
+    cap.eval()
+    T_l = tuple(int(t) for t in d["T_l"])
+    R = 4096
+    hs = cu(d["hs"])[:, :1].expand(1, R, -1).contiguous()
+    ref = cu(d["ref"])[:, :1].expand(1, R, -1).contiguous()
+    others = {"memory": cu(d["memory"]), "mask_flatten": cu(d["mask"]), "level_T": T_l,
+              "spatial_shapes": torch.tensor(T_l, device=DEV), "valid_ratios": torch.ones(1, 4, device=DEV)}
+    gen = torch.Generator(device=DEV).manual_seed(7)
+    opt = {"sample_max": 0, "temperature": temperature, "generator": gen}
+    with torch.no_grad():
+        seq, lp = cap.sample(hs, ref, others, opt)
+        gen.manual_seed(7)
+        seq2, lp2 = cap.sample(hs, ref, others, opt)
+    assert torch.equal(seq, seq2) and torch.equal(lp, lp2), "seeded draws must repeat"
+    first, lp1 = seq[:, 0].cpu().numpy(), lp[:, 0].double().cpu().numpy()
+    words, counts = np.unique(first, return_counts=True)
+    assert len(words) >= 2, "a tempered draw over 24 words should not be constant"
+    lp_of = {}
+    for w in words:
+        vals = lp1[first == w]
+        assert np.ptp(vals) < 1e-5, f"word {w}: log-probabilities differ across identical rows"
+        lp_of[w] = vals[0]
+    a, b = words[np.argsort(-counts)[:2]]
+    ca, cb = counts[words == a][0], counts[words == b][0]
+    expect = np.exp((lp_of[a] - lp_of[b]) / temperature)
+    se = (ca / cb) * np.sqrt(1.0 / ca + 1.0 / cb)
+    assert abs(ca / cb - expect) <= 5 * se, f"ratio {ca / cb:.3f} vs exp((lp_a-lp_b)/T) {expect:.3f}"
+    s = seq.cpu().numpy()
+    for row in s[:256]:
+        z = np.flatnonzero(row == 0)
+        if z.size:
+            assert not row[z[0]:].any(), "tokens after a finished row"
+
+
 @pytest.mark.parametrize("heads,rd1,deferred", [(1, 3, False), (2, 0, False), (1, 3, True), (2, 0, True)])
 def test_caption_decode_function_matches_step_loop(heads, rd1, deferred):
     """The fused teacher-forced recurrence (ops/functions/caption_decode.py) against the per-step autograd

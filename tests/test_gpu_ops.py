@@ -116,6 +116,45 @@ def test_dropin_errors():
         MSDA.ms_deform_attn_forward(v.cpu(), shapes, lsi, lo, a, 2)
     with pytest.raises(RuntimeError):
         MSDA.ms_deform_attn_forward(v.transpose(1, 2), shapes, lsi, lo, a, 2)
+    # dtypes the reference's data<int64_t>() / data<scalar_t>() accessors reject
+    with pytest.raises(RuntimeError, match="int64"):
+        MSDA.ms_deform_attn_forward(v, shapes.int(), lsi, lo, a, 2)
+    with pytest.raises(RuntimeError, match="int64"):
+        MSDA.ms_deform_attn_forward(v, shapes, lsi.int(), lo, a, 2)
+    with pytest.raises(RuntimeError, match="sampling_loc"):
+        MSDA.ms_deform_attn_forward(v, shapes, lsi, lo.float(), a, 2)
+    with pytest.raises(RuntimeError, match="attn_weight"):
+        MSDA.ms_deform_attn_forward(v.float(), shapes, lsi, lo.float(), a, 2)
+    g = torch.zeros(1, 2, 4, dtype=torch.float32, device=DEV)
+    with pytest.raises(RuntimeError, match="grad_output"):
+        MSDA.ms_deform_attn_backward(v, shapes, lsi, lo, a, g, 2)
+    # shapes inconsistent with value / sampling_loc
+    with pytest.raises(RuntimeError, match="spatial_shapes"):
+        MSDA.ms_deform_attn_forward(v, shapes.reshape(-1), lsi, lo, a, 2)
+    with pytest.raises(RuntimeError, match="attn_weight"):
+        MSDA.ms_deform_attn_forward(v, shapes, lsi, lo, a[..., :1].contiguous(), 2)
+    with pytest.raises(RuntimeError, match="grad_output"):
+        MSDA.ms_deform_attn_backward(v, shapes, lsi, lo, a, g.double()[..., :3].contiguous(), 2)
+
+
+def test_dropin_malformed_level_table_reads_nothing_outside_value():
+    """A level table pointing past the value rows (the host cannot see device-resident shapes without a sync;
+    the reference reads out of bounds) drops that level: no fault, no read outside value."""
+    import MultiScaleDeformableAttention as MSDA
+    d = load("op_reftest")
+    v, lo, a = cu(d["value"]), cu(d["loc"]), cu(d["attn"])
+    shapes, lsi = cu(d["shapes"]), cu(d["lsi"])
+    bad = lsi.clone()
+    bad[1] = 10 ** 9
+    out = MSDA.ms_deform_attn_forward(v, shapes, bad, lo, a, 2)
+    only0 = a.clone()
+    only0[:, :, :, 1] = 0
+    ref = MSDA.ms_deform_attn_forward(v, shapes, lsi, lo, only0, 2)
+    torch.cuda.synchronize()
+    close(out, ref, 1e-12, "level 1 dropped")
+    gv, gl, ga = MSDA.ms_deform_attn_backward(v, shapes, bad, lo, a, out, 2)
+    torch.cuda.synchronize()
+    assert torch.isfinite(gv).all() and torch.count_nonzero(ga[:, :, :, 1]) == 0
 
 
 def test_dropin_empty_queries():

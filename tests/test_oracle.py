@@ -87,3 +87,32 @@ def test_zeros_finite_difference():
             fm = f(v, loc, a)
             flat[i] = old
             assert abs((fp - fm) / (2 * eps) - grad.reshape(-1)[i]) < 1e-6
+
+
+@pytest.mark.parametrize("D", [30, 64])
+def test_torch_cpu_core_matches_reference_border(D):
+    """oracle/torch_core.py (the CPU baseline bench.py times) reproduces the reference's CPU core
+    (ms_deform_attn_core_pytorch, border padding) on its fixtures, forward and every gradient, fp64."""
+    import torch
+    from oracle.torch_core import ms_deform_attn_core_cpu
+    d = load(f"op_1d_D{D}")
+    shapes = [tuple(int(x) for x in s) for s in d["shapes"]]
+    v, lo, a = (torch.tensor(d[k], dtype=torch.float64, requires_grad=True) for k in ("value", "loc", "attn"))
+    out = ms_deform_attn_core_cpu(v, shapes, lo, a)
+    np.testing.assert_allclose(out.detach().numpy(), d["border_f64_out"], rtol=1e-12, atol=1e-13)
+    out.backward(torch.tensor(d["grad_out"]))
+    np.testing.assert_allclose(v.grad.numpy(), d["border_f64_grad_value"], rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(lo.grad.numpy(), d["border_f64_grad_loc"], rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(a.grad.numpy(), d["border_f64_grad_attn"], rtol=1e-12, atol=1e-13)
+    s = load("op_sample")
+    vs = torch.tensor(s["value"], dtype=torch.float64)
+    samp = ms_deform_attn_core_cpu(vs, [tuple(int(x) for x in r) for r in s["shapes"]],
+                                   torch.tensor(s["loc"]), torch.zeros(1, 6, 1, 4, 4, dtype=torch.float64),
+                                   return_value=True)
+    np.testing.assert_allclose(samp.numpy(), s["f64_samples"], rtol=1e-12, atol=1e-13)
+
+
+def test_cpu_baseline_timer_runs():
+    from oracle.torch_core import time_call_set
+    t, info = time_call_set(T=32, Q=10, runs=3, warmup=1, threads=2)
+    assert t > 0 and info["threads"] == 2 and info["runs"] == 3
