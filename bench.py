@@ -10,10 +10,16 @@ Workload (BASELINE.json metric config): cfgs/anet_tsp_pdvc.yml with C=768 featur
 One step = the reference's training iteration (train.py:181-187) over B videos per GPU: forward, losses,
 backward, RCCL gradient all-reduce (N>1), grad-norm clip (100) and the AdamW step.  Dropout is active.
 Weak scaling: B videos per GPU at every N; value = all ranks' videos / max-over-ranks time.
+
+--workload yc2_tsp_bf16 measures BASELINE.json configs[1] instead: cfgs/yc2_tsp_pdvc.yml, T=256, C=768, Q=100,
+E=8 events of 9 words, with every GEMM on bf16 operands and fp32 accumulation (pdvc/precision.py); its line
+carries dtype "bf16" and the GEMM roofline against the bf16 MFMA peak.  The default (no flags) is the
+headline fp32 line.
 """
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -29,7 +35,15 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 F32_MFMA_PEAK_TFS = 157.3  # MI355X dense FP32 matrix peak (MI355X_MICROARCH.md: no xf32 on gfx950)
-GEMM_OPS = ("aten::mm", "aten::addmm", "aten::addmm_", "aten::bmm", "aten::baddbmm")
+BF16_MFMA_PEAK_TFS = 2500.0  # MI355X dense BF16 matrix peak (MI355X_MICROARCH.md; the 5 PF figure is 2:1 sparse)
+GEMM_KERNEL = re.compile(r"^Cijk_|gemm|Gemm")  # hipBLASLt / rocBLAS (Tensile) kernels, pdvc_gemm_f32
+# the two benchmarked workloads: the metric's headline config, and BASELINE.json configs[1] in bf16
+WORKLOADS = {
+    "anet_tsp": dict(cfg="cfgs/anet_tsp_pdvc.yml", T=512, C=768, Q=100, events=4, words=13, precision="fp32",
+                     metric="videos/sec fwd+bwd (PDVC, T=512 C=768 L=4 Q=100) at 1/2/4/8 MI355X"),
+    "yc2_tsp_bf16": dict(cfg="cfgs/yc2_tsp_pdvc.yml", T=256, C=768, Q=100, events=8, words=9, precision="bf16",
+                         metric="videos/sec fwd+bwd (PDVC yc2_tsp_pdvc, T=256 C=768 L=4 Q=100, bf16) on 1 MI355X"),
+}
 
 
 def parse():
@@ -38,12 +52,13 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--videos-per-gpu", type=int, default=1024)
-    p.add_argument("--T", type=int, default=512)
-    p.add_argument("--C", type=int, default=768)
-    p.add_argument("--Q", type=int, default=100)
-    p.add_argument("--events", type=int, default=4)
-    p.add_argument("--words", type=int, default=13)
-    p.add_argument("--cfg", default="cfgs/anet_tsp_pdvc.yml")
+    p.add_argument("--workload", choices=sorted(WORKLOADS), default="anet_tsp",
+                   help="anet_tsp: the metric's config (fp32, the reference's precision); yc2_tsp_bf16: "
+                        "BASELINE.json configs[1] (T=256, bf16 GEMMs, pdvc/precision.py)")
+    for k in ("T", "C", "Q", "events", "words"):
+        p.add_argument(f"--{k}", type=int, default=None, help="override the workload's value")
+    p.add_argument("--cfg", default=None)
+    p.add_argument("--precision", choices=["fp32", "bf16"], default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--dist-backend", default=None, help="torch.distributed backend (default: nccl = RCCL on GPUs)")
     p.add_argument("--same-device", action="store_true",
@@ -59,7 +74,11 @@ def parse():
                    help="skip the profiled eager step that prices the projection GEMMs against the MFMA peak")
     p.add_argument("--gemm-table", choices=["auto", "off"], default="auto",
                    help="auto: library GEMMs use the pre-tuned solution table (pdvc/gemm_tuning.py) when present")
-    return p.parse_args()
+    a = p.parse_args()
+    for k, v in WORKLOADS[a.workload].items():
+        if getattr(a, k, None) is None:
+            setattr(a, k, v)
+    return a
 
 
 def build_model(a, device):
@@ -81,48 +100,73 @@ def msda_alg_bytes(meta, kind):
     return 3 * N * S * M * D * e + N * Lq * M * D * e + 2 * N * Lq * M * NS * 12
 
 
-def gemm_flops(name, shapes):
-    """2*m*n*k of one aten GEMM call from its recorded input shapes (0 if the shapes are not recorded)."""
-    try:
-        if name == "aten::mm":
-            (m, k), (_, n) = shapes[0], shapes[1]
-            return 2 * m * n * k
-        if name in ("aten::addmm", "aten::addmm_"):
-            (m, k), (_, n) = shapes[1], shapes[2]
-            return 2 * m * n * k
-        if name == "aten::bmm":
-            (b, m, k), (_, _, n) = shapes[0], shapes[1]
-            return 2 * b * m * n * k
-        if name == "aten::baddbmm":
-            (b, m, k), (_, _, n) = shapes[1], shapes[2]
-            return 2 * b * m * n * k
-    except (ValueError, IndexError, TypeError):
-        return 0
-    return 0
+class GemmFlops:
+    """Counts 2*m*n*k of every aten GEMM (mm, addmm, addmm_, _addmm_activation, bmm, baddbmm and their out=
+    forms) issued while active, backward included (a TorchDispatchMode is carried into autograd's threads).
+    torch.utils.flop_counter misses the in-place and fused-activation forms the step uses."""
+
+    def __enter__(self):
+        from torch.utils._python_dispatch import TorchDispatchMode
+        aten = torch.ops.aten
+        packets = {aten.mm, aten.addmm, aten.addmm_, aten._addmm_activation, aten.bmm, aten.baddbmm}
+        outer = self
+        self.flops = 0
+
+        class _Mode(TorchDispatchMode):
+            def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+                if func.overloadpacket in packets:
+                    ts = [t for t in args if isinstance(t, torch.Tensor)]
+                    a, b = ts[-2], ts[-1]
+                    batch = a.shape[0] if a.dim() == 3 else 1
+                    outer.flops += 2 * batch * a.shape[-2] * a.shape[-1] * b.shape[-1]
+                return func(*args, **(kwargs or {}))
+
+        self._mode = _Mode()
+        self._mode.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        self._mode.__exit__(*exc)
+        return False
 
 
-def gemm_roofline(step_fn):
-    """MFMA roofline of the projection GEMMs: one eager training step under torch.profiler; every aten GEMM's
-    2mnk flops (its recorded shapes) over the device time of the kernels it launched, summed over the step."""
+def gemm_roofline(flop_step, timed_step, precision, graphed):
+    """MFMA roofline of the projection / FFN / LSTM / logit GEMMs on the TIMED path: their useful flops
+    (GemmFlops over one eager step: 2mnk per GEMM, forward and backward; precision-independent)
+    over the device time of the GEMM kernels (hipBLASLt / rocBLAS Tensile "Cijk_*", pdvc_gemm) in one profiled
+    step of the timed kind -- a hipGraph replay when the bench replays graphs."""
     from torch.profiler import ProfilerActivity, profile
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
-        step_fn()
+    with GemmFlops() as fc:
+        flop_step()
+    torch.cuda.synchronize()
+    flops = fc.flops
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        timed_step()
         torch.cuda.synchronize()
-    flops, dev_us, calls = 0, 0.0, 0
-    for e in prof.key_averages(group_by_input_shape=True):
-        if e.key in GEMM_OPS:
-            flops += gemm_flops(e.key, e.input_shapes) * e.count
-            dev_us += e.device_time_total
-            calls += e.count
-    if dev_us <= 0:
+    gemm_us, cast_us, launches, total_us = 0.0, 0.0, 0, 0.0
+    for e in prof.key_averages():
+        dt = e.device_time_total
+        total_us += dt
+        if GEMM_KERNEL.search(e.key):
+            gemm_us += dt
+            launches += e.count
+        elif precision == "bf16" and "copy" in e.key.lower() and "bfloat16" in e.key.lower():
+            cast_us += dt
+    if gemm_us <= 0:
         return None
-    ach = flops / (dev_us * 1e-6) / 1e12
-    return {"kernel": "projection / FFN / LSTM / logit GEMMs (hipBLASLt, tuned table)", "bound": "mfma",
-            "achieved": ach, "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": ach / F32_MFMA_PEAK_TFS,
-            "traffic": None, "gemm_calls_per_step": calls, "gflop_per_step": flops / 1e9,
-            "gemm_device_ms_per_step": dev_us / 1e3,
-            "timing": "torch.profiler device time of every aten GEMM in 1 eager step after the timed steps"}
+    peak = BF16_MFMA_PEAK_TFS if precision == "bf16" else F32_MFMA_PEAK_TFS
+    ach = flops / (gemm_us * 1e-6) / 1e12
+    r = {"kernel": "projection / FFN / LSTM / logit GEMMs (hipBLASLt, " +
+                   ("bf16 operands, fp32 accumulation)" if precision == "bf16" else "fp32, tuned table)"),
+         "bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak, "traffic": None,
+         "gemm_kernel_launches_per_step": launches, "gflop_per_step": flops / 1e9,
+         "gemm_device_ms_per_step": gemm_us / 1e3, "profiled_device_ms_per_step": total_us / 1e3,
+         "timing": ("kernel device time in 1 profiled hipGraph replay of the step" if graphed else
+                    "kernel device time in 1 profiled eager step") + "; flops: 2mnk of every aten GEMM of 1 eager step (GemmFlops)"}
+    if precision == "bf16":
+        r["bf16_cast_ms_per_step"] = cast_us / 1e3
+    return r
 
 
 def cpu_baseline(a):
@@ -174,6 +218,11 @@ def cpu_baseline_c(a, budget_s):
                       f"oracle/msda_oracle.c (zeros), single thread, {el:.1f} s"}
 
 
+def log(msg):
+    """Progress on stderr (a long GPU run that prints nothing for minutes is taken to be hung)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     a = parse()
     from pdvc.distributed import GradAllReducer, broadcast_parameters, init_distributed
@@ -204,12 +253,19 @@ def main():
     vocab = args.vocab_size + 1
     dt = to_device(collate(synthetic_videos(B, a.T, a.C, a.events, a.words, vocab, seed=1000 + rank)), device)
     wd = criterion.weight_dict
+    from pdvc.precision import bf16_matmul
+    bf16 = a.precision == "bf16"
 
-    def eager_step():
+    def fwd_bwd():
         out, loss = model(dt, criterion, "queries")
         total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
         opt.zero_grad(set_to_none=True)
         total.backward()
+        return total
+
+    def eager_step():
+        with bf16_matmul(bf16):
+            total = fwd_bwd()
         if reducer is not None:
             reducer.finish()
         torch.nn.utils.clip_grad_norm_(params, args.grad_clip)
@@ -221,7 +277,8 @@ def main():
         model.enable_graph(dt)  # capture base encoder -> encoder -> decoder -> heads, fwd and bwd
     elif a.graph == "step":
         from pdvc.step_graph import StepGraph
-        sg = StepGraph(model, criterion, dt, reducer=reducer)  # forward + losses + backward, one hipGraph
+        with bf16_matmul(bf16):  # the bf16 mode reroutes the GEMMs once, at capture
+            sg = StepGraph(model, criterion, dt, reducer=reducer)  # forward + losses + backward, one hipGraph
 
         dbg = os.environ.get("PDVC_DEBUG_SYNC") == "1"
 
@@ -239,8 +296,10 @@ def main():
                 torch.cuda.synchronize()
                 print("debug: adam ok", file=sys.stderr, flush=True)
             return total
+    log(f"{B} videos/GPU, {world} rank(s): warm-up")
     for _ in range(a.warmup):
         step()
+    log("timed steps")
     names = ["pdvc_msda1d_forward_f32", "pdvc_msda1d_backward_f32", "pdvc_cap_gather_forward_f32",
              "pdvc_cap_gather_backward_f32"]
     graphed = a.graph != "none"
@@ -274,16 +333,19 @@ def main():
         timing_note = ("HIP events around every launch in 2 eager steps right after the timed (hipGraph) steps, "
                        "same shapes; step wall time excludes them")
     ks = timer.summary()
-    groof = None if a.no_gemm_roofline else gemm_roofline(eager_step)
+    log("GEMM roofline step")
+    groof = None if a.no_gemm_roofline else gemm_roofline(fwd_bwd, step, a.precision, graphed)
     videos = a.steps * B * world
     result = {
-        "metric": "videos/sec fwd+bwd (PDVC, T=512 C=768 L=4 Q=100) at 1/2/4/8 MI355X",
+        "metric": WORKLOADS[a.workload]["metric"],
         "value": videos / el, "unit": "videos/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": 1000.0 * el / a.steps, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"anet_tsp_pdvc training step (fwd+loss+bwd+allreduce+AdamW): T={a.T} C={a.C} "
-                               f"L=4 Q={a.Q} 2 enc/2 dec layers, E={a.events} events x {a.words} words, "
-                               f"vocab {vocab}, dropout on",
+        "vs_baseline": None, "dtype": "bf16" if bf16 else "f32", "data": "synthetic",
+        "config": {"workload": f"{os.path.basename(a.cfg)[:-4]} training step (fwd+loss+bwd+allreduce+AdamW): "
+                               f"T={a.T} C={a.C} L=4 Q={a.Q} {args.enc_layers} enc/{args.dec_layers} dec layers, "
+                               f"E={a.events} events x {a.words} words, vocab {vocab}, dropout on" +
+                               (", GEMMs on bf16 operands with fp32 accumulation, fp32 storage elsewhere" if bf16
+                                else ", fp32 throughout"),
                    "videos_per_gpu": B, "global_batch": B * world, "seq_len": a.T,
                    "gemm": _lin.BACKEND + ("+tuned-table" if tuned else ""),
                    "peak_hbm_gb": round(torch.cuda.max_memory_reserved(device) / 2 ** 30, 1),
@@ -292,7 +354,7 @@ def main():
                    "parallelism": f"dp{world}"},
     }
     # roofline_gather: the fused MSDA forward (the north star's gather kernel; algorithmic bytes per launch / avg
-    # launch time).  `roofline` is the dominant work, the GEMMs against the fp32 MFMA peak (gemm_roofline)
+    # launch time).  `roofline` is the dominant work, the GEMMs against the MFMA peak of the precision in use
     kname = "pdvc_msda1d_forward_f32"
     if kname in ks and ks[kname]["launches"]:
         k = ks[kname]
@@ -326,7 +388,9 @@ def main():
                               "what": "fused MSDeformAttn forward + backward kernels of every encoder and decoder "
                                       "layer, HIP events, per step of B videos per GPU"}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        log("CPU baseline (reference core, torch)")
         result["cpu_baseline"] = cpu_baseline(a)
+        log("CPU baseline (C oracle)")
         result["cpu_baseline_c_oracle"] = cpu_baseline_c(a, a.cpu_seconds)
         if "msda_gpu" in result:
             result["msda_gpu"]["vs_cpu_baseline"] = result["msda_gpu"]["videos_per_s"] / result["cpu_baseline"]["value"]

@@ -41,9 +41,8 @@ def build(force=False, verbose=True):
             continue
         cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
                "-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc"), "-c", s, "-o", o]
-        if s.endswith(".cpp"):
-            cmd.insert(1, "-x")
-            cmd.insert(2, "c++")
+        if s.endswith(".cpp"):  # host-only C++ (status plumbing)
+            cmd[1:1] = ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"]
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
     failed = False
     for cmd, p in procs:

@@ -18,6 +18,7 @@ from torch.autograd import Function
 from torch.autograd.function import once_differentiable
 
 from pdvc import _native as _n
+from pdvc.precision import fp32_gemms
 from .linear import colsum, wgrad_mm
 from .ms_deform_attn_func import NUM_SAMPLES, _levels
 
@@ -57,24 +58,25 @@ class CaptionDecodeFunction(Function):
         GATT = torch.empty((R, G), **kw)
         zero = torch.zeros((R, H), **kw)
         st = _n.stream()
-        for i in range(n):
-            if i == 0:
-                HP[0].copy_(b_h.expand(R, Ph))  # h_{-1} = 0
-            else:
-                torch.addmm(b_h, HS[:, i - 1], W_h.t(), out=HP[i])
-            _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video), _n.ptr(HP[i]),
-                    Ph, 0, _n.ptr(off_hs), _n.ptr(ref), RD, int(rd1_rows), lvl, nl, Nv, R, M, D, NS // nl,
-                    _n.ptr(CLIP[i]), _n.ptr(LOC[i]), st)
-            torch.addmm(b_ctx, CLIP[i].view(-1, D), W_ctx.t(), out=ATT[i])
-            ah, ldh = _n.rows(HP[i][:, n_off:n_off + A])
-            _n.call("pdvc_softattn_forward_f32", _n.ptr(ATT[i]), ah, ldh, _n.ptr(alpha_w), _n.ptr(alpha_b),
-                    _n.ptr(CLIP[i]), R, M, A, D, _n.ptr(RES[i]), _n.ptr(PROBS[i]), st)
-            torch.mm(RES[i], W_att.t(), out=GATT)
-            xa, ldx = _n.rows(xg[:, i])
-            gh, ldg = _n.rows(HP[i][:, n_off + A:])
-            ho, ldo = _n.rows(HS[:, i])
-            _n.call("pdvc_lstm_cell_forward_f32", xa, ldx, _n.ptr(GATT), G, gh, ldg,
-                    _n.ptr(CS[i - 1] if i > 0 else zero), R, H, ho, ldo, _n.ptr(CS[i]), _n.ptr(ACTS[i]), st)
+        with fp32_gemms():  # the recurrence stays fp32 in the bf16 mode (pdvc/precision.py)
+            for i in range(n):
+                if i == 0:
+                    HP[0].copy_(b_h.expand(R, Ph))  # h_{-1} = 0
+                else:
+                    torch.addmm(b_h, HS[:, i - 1], W_h.t(), out=HP[i])
+                _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video), _n.ptr(HP[i]),
+                        Ph, 0, _n.ptr(off_hs), _n.ptr(ref), RD, int(rd1_rows), lvl, nl, Nv, R, M, D, NS // nl,
+                        _n.ptr(CLIP[i]), _n.ptr(LOC[i]), st)
+                torch.addmm(b_ctx, CLIP[i].view(-1, D), W_ctx.t(), out=ATT[i])
+                ah, ldh = _n.rows(HP[i][:, n_off:n_off + A])
+                _n.call("pdvc_softattn_forward_f32", _n.ptr(ATT[i]), ah, ldh, _n.ptr(alpha_w), _n.ptr(alpha_b),
+                        _n.ptr(CLIP[i]), R, M, A, D, _n.ptr(RES[i]), _n.ptr(PROBS[i]), st)
+                torch.mm(RES[i], W_att.t(), out=GATT)
+                xa, ldx = _n.rows(xg[:, i])
+                gh, ldg = _n.rows(HP[i][:, n_off + A:])
+                ho, ldo = _n.rows(HS[:, i])
+                _n.call("pdvc_lstm_cell_forward_f32", xa, ldx, _n.ptr(GATT), G, gh, ldg,
+                        _n.ptr(CS[i - 1] if i > 0 else zero), R, H, ho, ldo, _n.ptr(CS[i]), _n.ptr(ACTS[i]), st)
         ctx.save_for_backward(value, off_hs, ref, W_h, W_ctx, alpha_w, W_att, pad_mask, row_video, HP, CLIP, LOC,
                               ATT, PROBS, RES, ACTS, CS, HS)
         ctx.meta = (tuple(level_T), int(rd1_rows), video_csr)
@@ -112,26 +114,27 @@ class CaptionDecodeFunction(Function):
         gv = torch.empty_like(value) if deferred else torch.zeros_like(value)
         gr = torch.zeros_like(ref) if ctx.needs_input_grad[3] else None
         st = _n.stream()
-        for i in reversed(range(n)):
-            last = i == n - 1
-            dCLIP = dCLIP_all[i if deferred else 0]
-            gh_, ldgh = _n.rows(dHS[:, i])
-            dg, lddg = _n.rows(dHP[i][:, n_off + A:])
-            _n.call("pdvc_lstm_cell_backward_f32", gh_, ldgh, None if last else _n.ptr(dh), H,
-                    None if last else _n.ptr(dc[(i + 1) % 2]), _n.ptr(ACTS[i]),
-                    _n.ptr(CS[i - 1] if i > 0 else zero), _n.ptr(CS[i]), R, H, dg, lddg, _n.ptr(dc[i % 2]), st)
-            torch.mm(dHP[i][:, n_off + A:], W_att, out=dRES)
-            ah, ldh = _n.rows(HP[i][:, n_off:n_off + A])
-            gah, ldgah = _n.rows(dHP[i][:, n_off:n_off + A])
-            _n.call("pdvc_softattn_backward_f32", _n.ptr(ATT[i]), ah, ldh, _n.ptr(alpha_w), _n.ptr(CLIP[i]),
-                    _n.ptr(PROBS[i]), _n.ptr(dRES), R, M, A, D, _n.ptr(dATT[i]), gah, ldgah, _n.ptr(dCLIP),
-                    _n.ptr(GAW[i]), _n.ptr(GAB[i]), st)
-            dCLIP.view(-1, D).addmm_(dATT[i], W_ctx)
-            _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video),
-                    _n.ptr(HP[i]), Ph, 0, _n.ptr(off_hs), _n.ptr(ref), RD, rd1_rows, lvl, nl, Nv, R, M, D, NS // nl,
-                    _n.ptr(LOC[i]), _n.ptr(dCLIP), None if deferred else _n.ptr(gv), _n.ptr(dHP[i]), _n.ptr(gr), st)
-            if i > 0:
-                torch.mm(dHP[i], W_h, out=dh)
+        with fp32_gemms():  # the recurrence stays fp32 in the bf16 mode
+            for i in reversed(range(n)):
+                last = i == n - 1
+                dCLIP = dCLIP_all[i if deferred else 0]
+                gh_, ldgh = _n.rows(dHS[:, i])
+                dg, lddg = _n.rows(dHP[i][:, n_off + A:])
+                _n.call("pdvc_lstm_cell_backward_f32", gh_, ldgh, None if last else _n.ptr(dh), H,
+                        None if last else _n.ptr(dc[(i + 1) % 2]), _n.ptr(ACTS[i]),
+                        _n.ptr(CS[i - 1] if i > 0 else zero), _n.ptr(CS[i]), R, H, dg, lddg, _n.ptr(dc[i % 2]), st)
+                torch.mm(dHP[i][:, n_off + A:], W_att, out=dRES)
+                ah, ldh = _n.rows(HP[i][:, n_off:n_off + A])
+                gah, ldgah = _n.rows(dHP[i][:, n_off:n_off + A])
+                _n.call("pdvc_softattn_backward_f32", _n.ptr(ATT[i]), ah, ldh, _n.ptr(alpha_w), _n.ptr(CLIP[i]),
+                        _n.ptr(PROBS[i]), _n.ptr(dRES), R, M, A, D, _n.ptr(dATT[i]), gah, ldgah, _n.ptr(dCLIP),
+                        _n.ptr(GAW[i]), _n.ptr(GAB[i]), st)
+                dCLIP.view(-1, D).addmm_(dATT[i], W_ctx)
+                _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video),
+                        _n.ptr(HP[i]), Ph, 0, _n.ptr(off_hs), _n.ptr(ref), RD, rd1_rows, lvl, nl, Nv, R, M, D, NS // nl,
+                        _n.ptr(LOC[i]), _n.ptr(dCLIP), None if deferred else _n.ptr(gv), _n.ptr(dHP[i]), _n.ptr(gr), st)
+                if i > 0:
+                    torch.mm(dHP[i], W_h, out=dh)
         if deferred:
             vr_start, vr_rows, max_rows = video_csr
             _n.call("pdvc_cap_value_grad_f32", _n.ptr(pad_mask), lvl, nl, Nv, M, D, NS // nl, R, n, int(max_rows),

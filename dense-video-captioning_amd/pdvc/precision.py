@@ -1,0 +1,130 @@
+"""The bf16 mode of the training step (BASELINE.json configs[1]: yc2_tsp_pdvc, "1 x MI355X bf16").
+
+The reference computes in fp32 only (pdvc/ops/src/cuda/ms_deform_attn_cuda.cu:64,134 dispatch floating types;
+every nn.Linear is fp32); the fp32 path stays the default and the parity-pinned one.  In the bf16 mode every
+fp32 GEMM of the step -- forward projections, FFNs, LSTM gates, logits, and every input- and weight-gradient
+GEMM autograd issues for them -- runs on the bf16 matrix cores: both operands are rounded to bf16 (one cast
+pass each, ~0.13 ms per 126 M elements) and multiplied by hipBLASLt with fp32 accumulation and an fp32 RESULT
+(aten mm/addmm/bmm/baddbmm .dtype overloads).  Everything else keeps fp32 storage: activations, the HIP kernels
+(MSDA, caption gather, layer norms, attention), parameters, gradients and the optimizer state.
+
+Measured on MI355X (tools/bf16_torch_probe.py), 245760 x 512 x 512: fp32 1.10 ms; bf16 0.25-0.31 ms + the
+0.13 ms cast; logit / LSTM-gate shapes 591 / 1041 TFLOP/s against 132 / 147 in fp32.  (hipBLASLt's
+HIPBLAS_COMPUTE_32F_FAST_16BF -- fp32 operands rounded inside the kernel -- ran 510-785 TFLOP/s with
+/opt/rocm's library, tools/blaslt_probe.cpp, but the hipBLASLt that torch loads ships no such kernels for
+gfx950, so the rounding is an explicit cast here.)
+
+Mechanism: a TorchDispatchMode that reroutes aten mm / addmm / addmm_ / bmm / baddbmm / _addmm_activation
+(and their out= forms) on fp32 GPU tensors.  The mode is thread-local state that autograd carries into its
+backward threads, so the gradient GEMMs are rerouted too; inside a captured step graph the rerouting happens
+once, at capture.  GEMMs below MIN_FLOPS (tiny heads, 1-wide projections) stay fp32: no time to win there.
+
+    with bf16_matmul():
+        out, loss = model(dt, criterion, "queries"); total.backward()
+
+Tolerances against the fp32 path: tests/test_gpu_bf16.py and DESIGN.md.
+"""
+import contextlib
+
+import torch
+from torch.utils._python_dispatch import TorchDispatchMode
+
+aten = torch.ops.aten
+MIN_FLOPS = 1 << 22
+# GEMMs the mode saw: (op, M, N, K) -> [calls on the bf16 path, calls kept in fp32 (below MIN_FLOPS)]
+STATS = {}
+_F32 = torch.float32
+_BF = torch.bfloat16
+
+
+def _bf(t):
+    return t.to(_BF)
+
+
+def _f32_cuda(*ts):
+    return all(isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == _F32 for t in ts)
+
+
+def _mnk(a, b):
+    return a.shape[-2], b.shape[-1], a.shape[-1]
+
+
+def _big(a, b):
+    M, N, K = _mnk(a, b)
+    batch = a.shape[0] if a.dim() == 3 else 1
+    return 2 * M * N * K * batch >= MIN_FLOPS
+
+
+class BF16Matmul(TorchDispatchMode):
+    """fp32 GPU GEMMs -> bf16 operands, fp32 accumulation and result (see the module docstring)."""
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        r = self._route(func, args, kwargs)
+        return func(*args, **kwargs) if r is NotImplemented else r
+
+    @staticmethod
+    def _count(key, routed):
+        s = STATS.setdefault(key, [0, 0])
+        s[0 if routed else 1] += 1
+        return routed
+
+    def _route(self, func, args, kw):
+        if func in (aten.mm.default, aten.mm.out):
+            a, b = args[:2]
+            if not (_f32_cuda(a, b) and self._count(("mm",) + _mnk(a, b), _big(a, b))):
+                return NotImplemented
+            if func is aten.mm.out:
+                return aten.mm.dtype_out(_bf(a), _bf(b), _F32, out=kw["out"])
+            return aten.mm.dtype(_bf(a), _bf(b), _F32)
+        if func in (aten.addmm.default, aten.addmm.out, aten.addmm_.default, aten._addmm_activation.default):
+            inp, a, b = args[:3]
+            if not (_f32_cuda(inp, a, b) and self._count(("addmm",) + _mnk(a, b), _big(a, b))):
+                return NotImplemented
+            if func is aten._addmm_activation.default and kw.get("use_gelu", False):
+                return NotImplemented
+            beta, alpha = kw.get("beta", 1), kw.get("alpha", 1)
+            if func is aten.addmm_.default:
+                return aten.addmm.dtype_out(inp, _bf(a), _bf(b), _F32, beta=beta, alpha=alpha, out=inp)
+            if func is aten.addmm.out:
+                return aten.addmm.dtype_out(inp, _bf(a), _bf(b), _F32, beta=beta, alpha=alpha, out=kw["out"])
+            y = aten.addmm.dtype(inp, _bf(a), _bf(b), _F32, beta=beta, alpha=alpha)
+            return y.relu_() if func is aten._addmm_activation.default else y
+        if func in (aten.bmm.default, aten.baddbmm.default):
+            if func is aten.bmm.default:
+                a, b = args[:2]
+                ok = _f32_cuda(a, b)
+            else:
+                inp, a, b = args[:3]
+                ok = _f32_cuda(inp, a, b)
+            if not (ok and self._count(("bmm",) + _mnk(a, b) + (a.shape[0],), _big(a, b))):
+                return NotImplemented
+            if func is aten.bmm.default:
+                return aten.bmm.dtype(_bf(a), _bf(b), _F32)
+            return aten.baddbmm.dtype(inp, _bf(a), _bf(b), _F32, beta=kw.get("beta", 1), alpha=kw.get("alpha", 1))
+        return NotImplemented
+
+
+@contextlib.contextmanager
+def bf16_matmul(enabled=True):
+    """Route the fp32 GEMMs issued inside the block (and by the backward passes it starts) to bf16 MFMA."""
+    if not enabled:
+        yield
+        return
+    with BF16Matmul():
+        yield
+
+
+@contextlib.contextmanager
+def fp32_gemms():
+    """GEMMs issued inside stay fp32 even under bf16_matmul: for the caption recurrence, whose per-step GEMMs
+    feed the next step (bf16 rounding there compounds over the steps) and are small, latency-bound launches
+    with little to win."""
+    from torch.utils._python_dispatch import _disable_current_modes
+    with _disable_current_modes():
+        yield
+
+
+def routed_summary():
+    """(GEMM calls on the bf16 path, calls kept fp32) over everything the mode saw."""
+    return sum(v[0] for v in STATS.values()), sum(v[1] for v in STATS.values())

@@ -10,8 +10,9 @@ and sum over (level, point).  Autograd supplies the backward, as in the referenc
 
 `time_call_set` times the per-video call set BASELINE.md specifies: enc_layers x (Lq = S) + dec_layers x
 (Lq = Q) calls, each forward + backward, M = 8, D = 64, L = 4, P = 4, fp32, N = 1 (the reference trains one
-video at a time), with torch using every CPU this process may run on; 3 warm-up runs, then the median of
-`runs` timed runs.
+video at a time), with torch using every CPU this process may run on -- capped by OMP_NUM_THREADS when the
+environment sets it (a GPU box exposes the whole machine's CPUs but grants a 16-CPU share and sets it); 3
+warm-up runs, then the median of `runs` timed runs.
 """
 import os
 import statistics
@@ -66,7 +67,10 @@ def cpu_info():
 def time_call_set(T=512, Q=100, enc_layers=2, dec_layers=2, runs=20, warmup=3, threads=None, seed=0):
     """Median seconds of one video's MSDeformAttn call set (fwd+bwd) on the CPU, and the settings used."""
     model, phys, usable = cpu_info()
-    threads = threads or usable
+    if threads is None:
+        threads = usable
+        if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+            threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
     torch.set_num_threads(threads)
     M, D, L, P = 8, 64, 4, 4
     T_l = [T // (2 ** i) for i in range(L)]

@@ -1,0 +1,230 @@
+"""The bf16 mode (pdvc/precision.py) -- BASELINE.json configs[1], yc2_tsp_pdvc on 1 MI355X in
+bf16.  The reference is fp32-only, so the fp32 path (pinned to the reference's fixtures elsewhere) is the
+oracle here.
+
+Stated tolerances (also in DESIGN.md):
+  * every rerouted GEMM form: equal to float64 on operands rounded to bf16 within 1e-5 * sqrt(K) * scale
+    (products of bf16 values are exact in fp32, only the fp32 accumulation differs), scale = max|a| * max|b|,
+    and within 2^-7 * sqrt(K) * scale of float64 on the unrounded operands;
+  * whole training step at the cfg-2 shape (T=256, C=768, Q=100, d=512, 2+2 layers, vocab 5748), dropout off:
+    every loss within 2e-2 * max(1, |loss_fp32|) (the non-caption losses also under the bf16 step's own set
+    matching -- a random-init model's near-tied costs let bf16 rounding flip matches, so gradients and caption
+    losses are compared under the fp32 step's matching); every parameter gradient with ||g_bf16 - g_fp32|| <= 0.1 *
+    ||g_fp32|| (relative L2) and cosine >= 0.995 (gradients that vanish in exact arithmetic -- ||g_fp32|| below
+    1e-3 of the largest gradient norm, e.g. the soft-attention logit bias under its softmax -- within 1e-3 of
+    that largest norm instead); the StepGraph replay of the bf16 step equal to the eager bf16
+    step within 1e-2 relative L2 per gradient (the library may pick other GEMM algorithms under capture: an
+    fp32 summation-order difference of one ulp can flip the bf16 rounding of the next GEMM's operand, so
+    replay-vs-eager noise grows to ~1e-3 -- still 50x below the bf16-vs-fp32 differences); never-used
+    parameters None in both.
+"""
+import math
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(os.path.dirname(HERE), "dense-video-captioning_amd")
+DEV = "cuda"
+
+
+def bf16_round(t):
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+OPS = ["mm", "mm_out", "addmm", "addmm_out", "addmm_", "addmm_relu", "bmm", "baddbmm"]
+
+
+@pytest.mark.parametrize("op", OPS)
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True)])
+def test_mode_gemms_vs_float64(op, ta, tb):
+    """Every rerouted overload equals float64 on bf16-rounded operands within 1e-5 * sqrt(K) * scale (bf16
+    products are exact in fp32; only the fp32 accumulation differs), and float64 on the unrounded operands
+    within 2^-7 * sqrt(K) * scale; the fp32 result of each form (out=, in place) lands where it should."""
+    from pdvc.precision import bf16_matmul, STATS
+    g = torch.Generator(device=DEV).manual_seed(11)
+    M, N, K, B = 300, 200, 512, 3
+    batched = op in ("bmm", "baddbmm")
+    shp = lambda r, c, t: ((B,) if batched else ()) + ((c, r) if t else (r, c))
+    a = torch.randn(shp(M, K, ta), device=DEV, generator=g)
+    b = torch.randn(shp(K, N, tb), device=DEV, generator=g)
+    A = a.transpose(-1, -2) if ta else a
+    Bm = b.transpose(-1, -2) if tb else b
+    bias = torch.randn(N, device=DEV, generator=g)
+    c0 = torch.randn(((B,) if batched else ()) + (M, N), device=DEV, generator=g)
+    out = torch.empty_like(c0)
+    STATS.clear()
+    with bf16_matmul():
+        if op == "mm":
+            y = torch.mm(A, Bm)
+        elif op == "mm_out":
+            y = torch.mm(A, Bm, out=out)
+        elif op == "addmm":
+            y = torch.addmm(bias, A, Bm)
+        elif op == "addmm_out":
+            y = torch.addmm(bias, A, Bm, out=out)
+        elif op == "addmm_":
+            y = c0.clone().addmm_(A, Bm)
+        elif op == "addmm_relu":
+            y = torch._addmm_activation(bias, A, Bm)
+        elif op == "bmm":
+            y = torch.bmm(A, Bm)
+        else:
+            y = torch.baddbmm(c0, A, Bm, beta=0.5, alpha=2.0)
+    assert sum(v[0] for v in STATS.values()) == 1, f"{op}: not routed to bf16 ({STATS})"
+    assert y.dtype == torch.float32
+    if op.endswith("_out"):
+        assert y.data_ptr() == out.data_ptr()
+    r16 = bf16_round(A).double() @ bf16_round(Bm).double()
+    r64 = A.double() @ Bm.double()
+    extra = {"addmm": bias.double(), "addmm_out": bias.double(), "addmm_relu": bias.double(),
+             "addmm_": c0.double()}.get(op, 0)
+    if op == "baddbmm":
+        r16, r64 = 0.5 * c0.double() + 2 * r16, 0.5 * c0.double() + 2 * r64
+    else:
+        r16, r64 = r16 + extra, r64 + extra
+    if op == "addmm_relu":
+        r16, r64 = r16.clamp(min=0), r64.clamp(min=0)
+    scale = math.sqrt(K) * float(a.abs().max()) * float(b.abs().max()) * (2 if op == "baddbmm" else 1)
+    assert (y.double() - r16).abs().max().item() <= 1e-5 * scale
+    assert (y.double() - r64).abs().max().item() <= 2 ** -7 * scale
+
+
+def test_mode_keeps_tiny_gemms_fp32():
+    from pdvc.precision import bf16_matmul, STATS
+    a = torch.randn(100, 512, device=DEV)
+    w = torch.randn(512, 1, device=DEV)
+    STATS.clear()
+    with bf16_matmul():
+        y = torch.mm(a, w)
+    assert torch.equal(y, torch.mm(a, w)) and sum(v[1] for v in STATS.values()) == 1
+
+
+def test_dispatch_mode_routes_linear_forward_and_backward():
+    """nn.Linear forward and both gradient GEMMs under bf16_matmul equal the fp32 results within bf16 rounding,
+    and actually differ from them (the bf16 route ran)."""
+    from pdvc.precision import bf16_matmul
+    g = torch.Generator(device=DEV).manual_seed(5)
+    lin = torch.nn.Linear(512, 384).to(DEV)
+    x = torch.randn(2, 700, 512, device=DEV, generator=g, requires_grad=True)
+    gy = torch.randn(2, 700, 384, device=DEV, generator=g)
+
+    def run():
+        lin.zero_grad()
+        x.grad = None
+        y = lin(x)
+        y.backward(gy)
+        return y.detach().clone(), x.grad.clone(), lin.weight.grad.clone(), lin.bias.grad.clone()
+
+    ref = run()
+    with bf16_matmul():
+        got = run()
+    for r, o, name in zip(ref, got, ("y", "dx", "dW", "db")):
+        rel = ((o - r).norm() / r.norm()).item()
+        assert rel < 1e-2, f"{name}: relative error {rel:.3e}"
+        if name != "db":  # the bias gradient is a reduction, not a GEMM
+            assert rel > 1e-6, f"{name}: identical to fp32 -- the bf16 route did not run"
+
+
+def _cfg2_model_and_batch():
+    sys.path.insert(0, PKG)
+    import opts
+    from pdvc.pdvc import build
+    from pdvc.data import collate, synthetic_videos, to_device
+    torch.manual_seed(0)
+    args = opts.parse_opts(["--cfg_path", "cfgs/yc2_tsp_pdvc.yml", "--device", "cuda"], cfg_root=PKG, feature_dim=768,
+                           num_queries=100, frame_embedding_num=256)
+    args.transformer_dropout_prob = 0.0
+    args.drop_prob = 0.0
+    model, criterion, _ = build(args)
+    model = model.to(DEV).train()
+    dt = to_device(collate(synthetic_videos(2, 256, 768, 8, 9, args.vocab_size + 1, seed=7)), DEV)
+    return model, criterion, dt
+
+
+def _step(model, criterion, dt, matched=None):
+    wd = criterion.weight_dict
+    model.zero_grad(set_to_none=True)
+    orig = criterion.forward
+
+    def capture(*a, **k):
+        r = orig(*a, **k)
+        if matched is not None:
+            _, last, aux = r
+            matched.extend([[(i.tolist(), j.tolist()) for i, j in list(ix[0])] for ix in list(aux) + [last]])
+        return r
+    criterion.forward = capture
+    try:
+        _, loss = model(dt, criterion, "queries")
+    finally:
+        criterion.forward = orig
+    total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
+    total.backward()
+    return ({k: float(v) for k, v in loss.items()},
+            {n: (None if p.grad is None else p.grad.detach().clone()) for n, p in model.named_parameters()})
+
+
+REL_L2, COSINE = 0.1, 0.995
+
+
+def test_cfg2_training_step_bf16_vs_fp32():
+    from pdvc.precision import bf16_matmul
+    from pdvc.step_graph import StepGraph
+    model, criterion, dt = _cfg2_model_and_batch()
+    # A random-init model scores every query almost alike, so the set matching is decided by tiny cost
+    # differences that bf16 rounding flips; the gradients are compared under the fp32 step's matching
+    # (replayed into the bf16 step), the losses under their own.
+    m32, m16 = [], []
+    l32, g32 = _step(model, criterion, dt, m32)
+    with bf16_matmul():
+        l16_own, g16_own = _step(model, criterion, dt, m16)
+    print("bf16 step matched like fp32:", m32 == m16)
+    solve = criterion.matcher.solve_device
+    saved = []
+    criterion.matcher.solve_device = lambda *a, **k: saved.append(solve(*a, **k)) or saved[-1]
+    _step(model, criterion, dt)
+    criterion.matcher.solve_device = lambda *a, **k: saved.pop(0)
+    try:
+        with bf16_matmul():
+            l16, g16 = _step(model, criterion, dt)
+    finally:
+        criterion.matcher.solve_device = solve
+    for k, v in l32.items():
+        if np.isnan(v):
+            continue
+        assert abs(l16[k] - v) <= 2e-2 * max(1.0, abs(v)), f"loss {k}: bf16 {l16[k]} vs fp32 {v}"
+        if "caption" not in k:  # the caption losses follow the matching's rows
+            assert abs(l16_own[k] - v) <= 2e-2 * max(1.0, abs(v)), f"loss {k} (own matching): {l16_own[k]} vs {v}"
+    worst = []
+    gmax = max(r.norm().item() for r in g32.values() if r is not None)
+    for n, r in g32.items():
+        assert (r is None) == (g16[n] is None), n
+        if r is None:
+            continue
+        o = g16[n]
+        if r.norm().item() < 1e-3 * gmax:
+            assert (o - r).norm().item() <= 1e-3 * gmax, n
+            continue
+        rel = ((o - r).norm() / r.norm()).item()
+        cos = torch.nn.functional.cosine_similarity(o.reshape(1, -1).double(), r.reshape(1, -1).double()).item()
+        worst.append((round(rel, 4), round(cos, 5), n))
+    worst.sort(reverse=True)
+    print("largest relative gradient errors (bf16 vs fp32):", worst[:12])
+    bad = [w for w in worst if w[0] > REL_L2 or w[1] < COSINE]
+    assert not bad, f"gradients outside relative L2 {REL_L2} / cosine {COSINE}: {bad}"
+    # the bench path: the bf16 step captured and replayed as one hipGraph
+    with bf16_matmul():
+        sg = StepGraph(model, criterion, dt)
+    for _ in range(2):
+        sg.replay()
+        torch.cuda.synchronize()
+        for n, p in model.named_parameters():  # against the eager bf16 step with its own matching
+            if g16_own[n] is None:
+                assert p.grad is None
+                continue
+            err = (p.grad - g16_own[n]).norm().item()
+            assert err <= 1e-2 * g16_own[n].norm().item() + 1e-7, f"replayed grad {n}: {err:.3e}"
