@@ -17,6 +17,7 @@ carries dtype "bf16" and the GEMM roofline against the bf16 MFMA peak.  The defa
 headline fp32 line.
 """
 import argparse
+import glob
 import json
 import os
 import re
@@ -362,8 +363,9 @@ def main():
         avg_bytes = sum(msda_alg_bytes(m, "fwd") for m in k["metas"]) / k["launches"]
         ach = avg_bytes / (avg_ms * 1e-3) / 1e9
         traffic, tsrc = None, None
-        tfile = os.path.join(ROOT, "profiles", "r01_msda1d_fwd_traffic.json")
-        if os.path.exists(tfile):  # PMC pass of the same command (tools/pmc_traffic.py): HBM bytes per launch
+        tfiles = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_msda1d_fwd_traffic.json")))
+        tfile = tfiles[-1] if tfiles else ""
+        if tfile and os.path.exists(tfile):  # PMC pass of the same command (tools/pmc_traffic.py): HBM bytes per launch
             with open(tfile) as f:
                 traffic = json.load(f).get("avg_bytes_per_launch")
             tsrc = os.path.relpath(tfile, ROOT)
