@@ -49,6 +49,8 @@ def collate(batch):
         targets.append({"boxes": boxes, "labels": torch.tensor(labels[v]).long(), "masks": None,
                         "image_id": keys[v]})
     return {"video_tensor": video, "video_length": length, "video_mask": vmask, "video_key": list(keys),
+            # host-side fact of the batch: no padded frame anywhere (the kernels then skip the padding mask)
+            "video_mask_all_valid": bool(vmask.all()),
             "video_target": targets, "gt_featstamps": list(chain(*_stamps)), "gt_timestamp": list(raw_ts),
             "gt_gather_idx": gather, "gt_boxes": gt_boxes, "gt_boxes_mask": (gt_boxes != 0).sum(2) > 0,
             "cap_tensor": cap, "cap_length": cap_len, "cap_mask": cap_mask, "cap_raw": list(_raw_caps)}

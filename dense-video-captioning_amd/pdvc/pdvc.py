@@ -143,13 +143,16 @@ class PDVC(nn.Module):
         src_flatten, temporal_shapes, lsi, valid_ratios, lvl_pos, mask_flatten = tr.prepare_encoder_inputs(
             srcs, masks, pos)
         level_T = tr.last_level_T
-        memory = tr.forward_encoder(src_flatten, level_T, lsi, valid_ratios, lvl_pos, mask_flatten)
+        # no padded frame in the batch (a host-side fact, dt["video_mask_all_valid"]): the all-False padding mask
+        # changes nothing, so the kernels get none and skip its per-corner byte loads
+        kmask = None if self.__dict__.get("_no_padding", False) else mask_flatten
+        memory = tr.forward_encoder(src_flatten, level_T, lsi, valid_ratios, lvl_pos, kmask)
         self._project_memory(memory)
         query_embed = self.query_embed.weight
         proposals_mask = torch.ones(N, query_embed.shape[0], device=query_embed.device).bool()
         init_reference, tgt, reference_points, query_embed = tr.prepare_decoder_input_query(memory, query_embed)
         hs, inter_references = tr.forward_decoder(tgt, reference_points, memory, level_T, lsi, valid_ratios,
-                                                  query_embed, mask_flatten, proposals_mask, False)
+                                                  query_embed, kmask, proposals_mask, False)
         classes, counts, coords = self._layer_heads(hs, init_reference, inter_references, False)
         return (memory, mask_flatten, temporal_shapes, lsi, valid_ratios, proposals_mask, hs, init_reference,
                 inter_references, torch.stack(classes), torch.stack(counts), torch.stack(coords))
@@ -193,9 +196,11 @@ class PDVC(nn.Module):
     def forward(self, dt, criterion, transformer_input_type, eval_mode=False):
         two_stage, disable_refine, proposals, proposals_mask = decide_two_stage(transformer_input_type, dt,
                                                                                  criterion)
+        object.__setattr__(self, "_no_padding", bool(dt.get("video_mask_all_valid", False)))
         (memory, mask_flatten, temporal_shapes, lsi, valid_ratios, proposals_mask, hs, init_reference,
          inter_references, classes, counts, coords) = self._run_trunk(dt)
-        others = {"memory": memory, "mask_flatten": mask_flatten, "spatial_shapes": temporal_shapes,
+        others = {"memory": memory, "mask_flatten": None if self._no_padding else mask_flatten,
+                  "spatial_shapes": temporal_shapes,
                   "level_T": self.transformer.last_level_T, "level_start_index": lsi, "valid_ratios": valid_ratios,
                   "proposals_mask": proposals_mask}
         heads = (list(classes.unbind(0)), list(counts.unbind(0)), list(coords.unbind(0)))

@@ -57,6 +57,9 @@ class StepGraph:
 
     def load(self, dt):
         """Copy a batch of the captured shapes (same event and caption counts) into the graph's inputs."""
+        if bool(dt.get("video_mask_all_valid", False)) != bool(self.dt.get("video_mask_all_valid", False)):
+            raise ValueError("StepGraph.load: the batch's padding (video_mask_all_valid) differs from the captured "
+                             "batch's; capture a graph for it")
         for k, v in dt.items():
             dst = self.dt.get(k)
             if isinstance(v, torch.Tensor) and isinstance(dst, torch.Tensor) and dst.device.type == "cuda":

@@ -101,11 +101,16 @@ def test_state_dict_names_match_reference(case):
 
 
 @pytest.mark.parametrize("case", CASES)
-def test_training_step_matches_reference(case):
+@pytest.mark.parametrize("no_padding", [False, True])
+def test_training_step_matches_reference(case, no_padding):
+    """no_padding: the batch declares it has no padded frame (dt["video_mask_all_valid"], true of the fixture's
+    video), so the kernels run without the all-False padding mask -- same results."""
     d = load(case)
     model, criterion = build_filled(d)
     model.train()
     dt = fixture_dt(d)
+    assert bool(dt["video_mask"].all())
+    dt["video_mask_all_valid"] = no_padding
     out, loss = model(dt, criterion, "queries")
     wd = criterion.weight_dict
     total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
