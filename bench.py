@@ -60,6 +60,9 @@ def parse():
         p.add_argument(f"--{k}", type=int, default=None, help="override the workload's value")
     p.add_argument("--cfg", default=None)
     p.add_argument("--precision", choices=["fp32", "bf16"], default=None)
+    p.add_argument("--mode", choices=["train", "eval"], default="train",
+                   help="eval: the reference's evaluation pass instead (eval_utils.py:178 -> PDVC.forward(eval_mode="
+                        "True): greedy captions of every query, then PostProcess) -- videos/s, not the headline")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--dist-backend", default=None, help="torch.distributed backend (default: nccl = RCCL on GPUs)")
     p.add_argument("--same-device", action="store_true",
@@ -224,8 +227,58 @@ def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def eval_main(a):
+    """Evaluation throughput: forward with greedy captions for all Q queries (LSTM_DSA.py:118-186, the loop stops
+    when every row has finished, one host check per step as the reference) + PostProcess (pdvc.py:493-546,
+    captions detokenised on the host).  Eager: the decode's length is data-dependent.  One GPU."""
+    import types
+    from pdvc.data import synthetic_videos, collate, to_device
+    from data.video_dataset import Translator
+    device = torch.device("cuda:0")
+    torch.cuda.set_device(device)
+    torch.manual_seed(0)
+    args, model, criterion = build_model(a, device)
+    model.eval()
+    post = __import__("pdvc.pdvc", fromlist=["PostProcess"]).PostProcess(args)
+    B = a.videos_per_gpu
+    vocab = args.vocab_size + 1
+    dt = to_device(collate(synthetic_videos(B, a.T, a.C, a.events, a.words, vocab, seed=1000)), device)
+    tr = Translator.from_vocab({str(i): f"w{i}" for i in range(1, vocab)})
+    loader = types.SimpleNamespace(dataset=types.SimpleNamespace(translator=tr))
+    steps_seen = []
+
+    def step():
+        with torch.no_grad():
+            out, _ = model(dt, criterion, "queries", eval_mode=True)
+            res = post(out, dt["video_length"][:, 1], loader)
+        steps_seen.append(out["seq"].shape[-1] if len(out["seq"]) else 0)
+        return res
+
+    log(f"eval: {B} videos, warm-up")
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    result = {"metric": "videos/sec eval (PDVC forward + greedy captions of all queries + PostProcess, "
+                        f"T={a.T} C={a.C} Q={a.Q}) on 1 MI355X",
+              "value": a.steps * B / el, "unit": "videos/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+              "ms_per_step": 1e3 * el / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+              "dtype": "f32", "data": "synthetic",
+              "config": {"workload": f"{os.path.basename(a.cfg)[:-4]} eval: {B} videos x {a.Q} queries, greedy "
+                                     f"decoding up to max_caption_len {args.max_caption_len} + 1 steps, random-init "
+                                     f"weights (decode length {steps_seen[-1]} steps)",
+                         "videos_per_gpu": B, "global_batch": B, "seq_len": a.T, "parallelism": "dp1"}}
+    print(json.dumps(result), flush=True)
+
+
 def main():
     a = parse()
+    if a.mode == "eval":
+        return eval_main(a)
     from pdvc.distributed import GradAllReducer, broadcast_parameters, init_distributed
     from pdvc import _native
     from pdvc.data import synthetic_videos, collate, to_device

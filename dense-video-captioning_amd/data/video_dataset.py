@@ -82,6 +82,21 @@ class Translator:
         w2i = self.vocab["word_to_ix"]
         return np.array([0] + [w2i[w] for w in words][:max_len - 2] + [0])
 
+    def rtranslate_batch(self, seqs):
+        """rtranslate of every row of an int array (R, L): the first-zero cut and the word lookup vectorised."""
+        seqs = np.asarray(seqs)
+        if seqs.size == 0:
+            return [""] * seqs.shape[0]
+        words = getattr(self, "_word_array", None)
+        if words is None or len(words) <= int(seqs.max()):
+            i2w = self.vocab["ix_to_word"]
+            words = np.array([""] + [i2w[str(i)] for i in range(1, int(seqs.max()) + 1)], dtype=object)
+            self._word_array = words
+        zero = seqs == 0
+        lens = np.where(zero.any(1), zero.argmax(1), seqs.shape[1])
+        toks = words[seqs]
+        return [" ".join(row[:n]) + "." if n else "" for row, n in zip(toks.tolist(), lens.tolist())]
+
     def rtranslate(self, sent_ids):
         """Ids up to the first 0 -> 'w1 w2 ... wn.' ('' when the caption is empty)."""
         ids = list(sent_ids)

@@ -439,7 +439,11 @@ class PostProcess(nn.Module):
             tr = loader.dataset.translator
             host_scores = cap_scores.double().cpu().numpy()
             host_seq = seq_ranked.cpu().numpy().astype("int")
-            caps = [[tr.rtranslate(s) for s in vid] for vid in host_seq]
+            if hasattr(tr, "rtranslate_batch"):  # data.video_dataset.Translator: one vectorised pass
+                flat = tr.rtranslate_batch(host_seq.reshape(N * Q, -1))
+                caps = [flat[b * Q:(b + 1) * Q] for b in range(N)]
+            else:
+                caps = [[tr.rtranslate(s) for s in vid] for vid in host_seq]
             cap_scores = [list(row) for row in host_scores]
         else:  # no caption decoded (every query finished at once)
             cap_scores = [[-1e5] * Q for _ in range(N)]

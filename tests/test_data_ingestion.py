@@ -118,3 +118,13 @@ def test_pickled_feature_files_are_refused(tmp_path):
     p.write_bytes(b"not read")
     with pytest.raises(ValueError):
         VD.read_file(str(p), 4)
+
+
+def test_rtranslate_batch_equals_rtranslate(tmp_path):
+    tr = translator(tmp_path)
+    rng = np.random.RandomState(3)
+    seqs = rng.randint(0, len(WORDS) + 1, size=(300, 9))
+    seqs[::4, 0] = 0
+    seqs[1::5, 4] = 0
+    assert tr.rtranslate_batch(seqs) == [tr.rtranslate(s) for s in seqs]
+    assert tr.rtranslate_batch(np.zeros((2, 0), np.int64)) == ["", ""]
