@@ -13,8 +13,10 @@ Weak scaling: B videos per GPU at every N; value = all ranks' videos / max-over-
 
 --workload yc2_tsp_bf16 measures BASELINE.json configs[1] instead: cfgs/yc2_tsp_pdvc.yml, T=256, C=768, Q=100,
 E=8 events of 9 words, with every GEMM on bf16 operands and fp32 accumulation (pdvc/precision.py); its line
-carries dtype "bf16" and the GEMM roofline against the bf16 MFMA peak.  The default (no flags) is the
-headline fp32 line.
+carries dtype "bf16" and the GEMM roofline against the bf16 MFMA peak.  --workload yc2_newmodel measures
+BASELINE.json configs[3]: cfgs/yc2_newModel_sound.yml, NewModel = the dual-modality MHA front-end (T=512 clip
+and sound features, 768-d, 32 heads; csrc/seqattn.hip) in front of a 3+3-layer PDVC, E=8 events of 9 words,
+fp32.  The default (no flags) is the headline fp32 line.
 """
 import argparse
 import glob
@@ -44,6 +46,10 @@ WORKLOADS = {
                      metric="videos/sec fwd+bwd (PDVC, T=512 C=768 L=4 Q=100) at 1/2/4/8 MI355X"),
     "yc2_tsp_bf16": dict(cfg="cfgs/yc2_tsp_pdvc.yml", T=256, C=768, Q=100, events=8, words=9, precision="bf16",
                          metric="videos/sec fwd+bwd (PDVC yc2_tsp_pdvc, T=256 C=768 L=4 Q=100, bf16) on 1 MI355X"),
+    "yc2_newmodel": dict(cfg="cfgs/yc2_newModel_sound.yml", T=512, C=768, Q=100, events=8, words=9,
+                         precision="fp32", frontend=True, videos_per_gpu=512,
+                         metric="videos/sec fwd+bwd (NewModel yc2_newModel_sound: MHA front-end + PDVC, T=512 "
+                                "C=768 3+3 layers Q=100) on 1 MI355X"),
 }
 
 
@@ -52,10 +58,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--videos-per-gpu", type=int, default=1024)
+    p.add_argument("--videos-per-gpu", type=int, default=None, help="default: 1024 (512 for yc2_newmodel)")
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="anet_tsp",
                    help="anet_tsp: the metric's config (fp32, the reference's precision); yc2_tsp_bf16: "
-                        "BASELINE.json configs[1] (T=256, bf16 GEMMs, pdvc/precision.py)")
+                        "BASELINE.json configs[1] (T=256, bf16 GEMMs, pdvc/precision.py); yc2_newmodel: configs[3] "
+                        "(MHA front-end + 3+3-layer PDVC, T=512)")
     for k in ("T", "C", "Q", "events", "words"):
         p.add_argument(f"--{k}", type=int, default=None, help="override the workload's value")
     p.add_argument("--cfg", default=None)
@@ -79,19 +86,37 @@ def parse():
     p.add_argument("--gemm-table", choices=["auto", "off"], default="auto",
                    help="auto: library GEMMs use the pre-tuned solution table (pdvc/gemm_tuning.py) when present")
     a = p.parse_args()
+    a.frontend = None
     for k, v in WORKLOADS[a.workload].items():
         if getattr(a, k, None) is None:
             setattr(a, k, v)
+    a.frontend = bool(a.frontend)
+    if a.videos_per_gpu is None:
+        a.videos_per_gpu = 1024
     return a
 
 
 def build_model(a, device):
+    """(args, model, criterion); with the front-end (yc2_newmodel) the model is NewModel behind PDVC's calling
+    convention (pdvc/newmodel.py NewModelStep)."""
     import opts
     from pdvc.pdvc import build
     args = opts.parse_opts(["--cfg_path", a.cfg, "--device", "cuda"], cfg_root=PKG, feature_dim=a.C,
                            num_queries=a.Q, frame_embedding_num=a.T)
+    if a.frontend:
+        from pdvc.newmodel import NewModelStep, build_newmodel
+        nm, criterion, _ = build_newmodel(args)
+        return args, NewModelStep(nm).to(device), criterion
     model, criterion, _ = build(args)
     return args, model.to(device), criterion
+
+
+def add_sound(a, dt, device, seed):
+    """The front-end's second input (per-clip sound features, HuBERT-sized 768-d), synthetic like the clips."""
+    if a.frontend:
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        dt["sound_tensor"] = torch.randn(dt["video_tensor"].shape[0], a.T, 768, generator=g).to(device)
+    return dt
 
 
 def msda_alg_bytes(meta, kind):
@@ -173,14 +198,14 @@ def gemm_roofline(flop_step, timed_step, precision, graphed):
     return r
 
 
-def cpu_baseline(a):
+def cpu_baseline(a, enc_layers=2, dec_layers=2):
     """The reference's CPU deformable-attention path timed on this host: a torch restatement of
     ms_deform_attn_core_pytorch (pdvc/ops/functions/ms_deform_attn_func.py:41-68, grid_sample border; pinned to
     the reference's fixtures by tests/test_oracle.py) over one video's call set -- enc_layers x Lq=S + dec_layers
     x Lq=Q, forward + backward, M=8 D=64 L=4 P=4 fp32 -- with every CPU this process may use; 3 warm-ups, median
     of 20 runs."""
     from oracle.torch_core import time_call_set
-    med, info = time_call_set(T=a.T, Q=a.Q, runs=20, warmup=3)
+    med, info = time_call_set(T=a.T, Q=a.Q, enc_layers=enc_layers, dec_layers=dec_layers, runs=20, warmup=3)
     return {"value": 1.0 / med, "unit": "videos/s", "cores": info["threads"], "kind": "port",
             "cpu_model": info["cpu_model"], "physical_cores": info["physical_cores"],
             "usable_cpus": info["usable_cpus"], "ms_per_video": 1e3 * med,
@@ -189,7 +214,7 @@ def cpu_baseline(a):
                       f"torch.set_num_threads({info['threads']}): oracle/torch_core.py (grid_sample, border)"}
 
 
-def cpu_baseline_c(a, budget_s):
+def cpu_baseline_c(a, budget_s, enc_layers=2, dec_layers=2):
     """Secondary CPU figure: the single-threaded C restatement of the CUDA op (oracle/msda_oracle.c, zero
     padding), whole videos of the same call set until budget_s is spent."""
     from oracle import oracle as O
@@ -201,7 +226,7 @@ def cpu_baseline_c(a, budget_s):
     shapes = np.stack([np.ones(4, np.int64), np.asarray(T_l, np.int64)], -1)
     lsi = np.concatenate([[0], np.cumsum(T_l)[:-1]]).astype(np.int64)
     value = rng.randn(1, S, M, D).astype(np.float32)
-    calls = [S, S, a.Q, a.Q]
+    calls = [S] * enc_layers + [a.Q] * dec_layers
     inputs = []
     for Lq in calls:
         at = rng.uniform(size=(1, Lq, M, L, P)).astype(np.float32)
@@ -218,7 +243,7 @@ def cpu_baseline_c(a, budget_s):
         if el >= budget_s:
             break
     return {"value": videos / el, "unit": "videos/s", "cores": 1, "kind": "port",
-            "sample": f"{videos} video(s) x MSDA fwd+bwd call set (2 x Lq={S} + 2 x Lq={a.Q}), T={a.T}, fp32, "
+            "sample": f"{videos} video(s) x MSDA fwd+bwd call set ({enc_layers} x Lq={S} + {dec_layers} x Lq={a.Q}), T={a.T}, fp32, "
                       f"oracle/msda_oracle.c (zeros), single thread, {el:.1f} s"}
 
 
@@ -242,7 +267,8 @@ def eval_main(a):
     post = __import__("pdvc.pdvc", fromlist=["PostProcess"]).PostProcess(args)
     B = a.videos_per_gpu
     vocab = args.vocab_size + 1
-    dt = to_device(collate(synthetic_videos(B, a.T, a.C, a.events, a.words, vocab, seed=1000)), device)
+    dt = add_sound(a, to_device(collate(synthetic_videos(B, a.T, a.C, a.events, a.words, vocab, seed=1000)), device),
+                   device, 2000)
     tr = Translator.from_vocab({str(i): f"w{i}" for i in range(1, vocab)})
     loader = types.SimpleNamespace(dataset=types.SimpleNamespace(translator=tr))
     steps_seen = []
@@ -305,7 +331,8 @@ def main():
     opt = torch.optim.AdamW(params, lr=args.lr, weight_decay=args.weight_decay, fused=True)
     B = a.videos_per_gpu
     vocab = args.vocab_size + 1
-    dt = to_device(collate(synthetic_videos(B, a.T, a.C, a.events, a.words, vocab, seed=1000 + rank)), device)
+    dt = add_sound(a, to_device(collate(synthetic_videos(B, a.T, a.C, a.events, a.words, vocab, seed=1000 + rank)),
+                                device), device, 2000 + rank)
     wd = criterion.weight_dict
     from pdvc.precision import bf16_matmul
     bf16 = a.precision == "bf16"
@@ -355,7 +382,7 @@ def main():
         step()
     log("timed steps")
     names = ["pdvc_msda1d_forward_f32", "pdvc_msda1d_backward_f32", "pdvc_cap_gather_forward_f32",
-             "pdvc_cap_gather_backward_f32"]
+             "pdvc_cap_gather_backward_f32", "pdvc_seq_attention_forward_f32", "pdvc_seq_attention_backward_f32"]
     graphed = a.graph != "none"
     timer = _native.KernelTimer(names)
     if world > 1:
@@ -395,7 +422,9 @@ def main():
         "value": videos / el, "unit": "videos/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": 1000.0 * el / a.steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "bf16" if bf16 else "f32", "data": "synthetic",
-        "config": {"workload": f"{os.path.basename(a.cfg)[:-4]} training step (fwd+loss+bwd+allreduce+AdamW): "
+        "config": {"workload": f"{os.path.basename(a.cfg)[:-4]} training step (fwd+loss+bwd+allreduce+AdamW): " +
+                               ("dual-modality MHA front-end (clips + sound, 768-d, 32 heads) + " if a.frontend
+                                else "") +
                                f"T={a.T} C={a.C} L=4 Q={a.Q} {args.enc_layers} enc/{args.dec_layers} dec layers, "
                                f"E={a.events} events x {a.words} words, vocab {vocab}, dropout on" +
                                (", GEMMs on bf16 operands with fp32 accumulation, fp32 storage elsewhere" if bf16
@@ -427,6 +456,21 @@ def main():
                               "traffic": traffic, "traffic_source": tsrc, "avg_launch_us": avg_ms * 1e3,
                               "timing": timing_note,
                               "alg_bytes_per_launch": avg_bytes}
+    if a.frontend and ks.get("pdvc_seq_attention_forward_f32", {}).get("launches"):
+        # front-end attention core (csrc/seqattn.hip): 4*T*T*E flops per video forward (scores + P.V over all
+        # heads), 10*T*T*E backward (scores recomputed, dP, dQ, dK, dV), against the fp32 MFMA peak
+        E = 768
+        fl = 4.0 * B * a.T * a.T * E
+        r = {"kernel": "seqattn_fwd_kernel / seqattn_bwd_dq+dkv kernels (front-end MHA core, fp32 MFMA)",
+             "bound": "mfma", "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s", "timing": timing_note}
+        for n, key, f in (("pdvc_seq_attention_forward_f32", "forward", fl),
+                          ("pdvc_seq_attention_backward_f32", "backward", 2.5 * fl)):
+            k = ks.get(n)
+            if k and k["launches"]:
+                avg_ms = k["ms"] / k["launches"]
+                r[key] = {"avg_launch_us": 1e3 * avg_ms, "achieved": f / (avg_ms * 1e-3) / 1e12,
+                          "frac": f / (avg_ms * 1e-3) / 1e12 / F32_MFMA_PEAK_TFS, "gflop_per_launch": f / 1e9}
+        result["roofline_frontend_attention"] = r
     if groof is not None:  # the dominant kernels (~70% of the step's device time): `roofline` proper
         groof["share_of_step"] = groof["gemm_device_ms_per_step"] / (1e3 * el / a.steps)
         result["roofline"] = groof
@@ -444,9 +488,9 @@ def main():
                                       "layer, HIP events, per step of B videos per GPU"}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         log("CPU baseline (reference core, torch)")
-        result["cpu_baseline"] = cpu_baseline(a)
+        result["cpu_baseline"] = cpu_baseline(a, args.enc_layers, args.dec_layers)
         log("CPU baseline (C oracle)")
-        result["cpu_baseline_c_oracle"] = cpu_baseline_c(a, a.cpu_seconds)
+        result["cpu_baseline_c_oracle"] = cpu_baseline_c(a, a.cpu_seconds, args.enc_layers, args.dec_layers)
         if "msda_gpu" in result:
             result["msda_gpu"]["vs_cpu_baseline"] = result["msda_gpu"]["videos_per_s"] / result["cpu_baseline"]["value"]
     if rank == 0:

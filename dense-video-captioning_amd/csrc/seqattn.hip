@@ -2,13 +2,30 @@
 // (reference: NewModel.visual_self_attention / visual_sound_attention, NewModel.py:41-65: nn.MultiheadAttention(768,
 // 32 heads, batch_first) over the T clip features, queries = clips or sound features).  T = 512 queries and keys,
 // head_dim 24: outside the decoder kernel's range (mha.hip: Q <= 300), and a (T x T) score matrix per head is
-// 1 MB, so nothing of size T^2 is ever written: flash-style, one lane per query (forward, dq) or per key (dk, dv),
-// the other side streamed through LDS in 128-row tiles that every lane of the workgroup reads as a broadcast.
-//   forward:  out_i = sum_j softmax_j(scale q_i.k_j) v_j, lse_i saved (running max / sum, rescaled on a new max)
+// 1 MB, so nothing of size T^2 is ever written (flash-style: running max / sum, P recomputed in the backward).
+//
+//   forward:  out_i = sum_j softmax_j(scale q_i.k_j) v_j, lse_i saved
 //   backward: delta_i = dout_i.out_i;  p_ij = exp(scale q_i.k_j - lse_i);  ds_ij = p_ij (dout_i.v_j - delta_i)
-//             dq_i = scale sum_j ds_ij k_j  (query lanes);  dk_j = scale sum_i ds_ij q_i, dv_j = sum_i p_ij dout_i
-//             (key lanes) -- every gradient row has exactly one writer, no atomics.
-// Exponentials on the hardware exp2 (__expf: ~1 ulp of expf, well inside the 1e-4 parity bound).
+//             dq_i = scale sum_j ds_ij k_j  (query-owner kernel);  dk_j = scale sum_i ds_ij q_i,
+//             dv_j = sum_i p_ij dout_i (key-owner kernel) -- every gradient row has exactly one writer, no atomics.
+//
+// Every product runs on v_mfma_f32_32x32x2_f32 (exact fp32 products, fp32 accumulation).  A wave owns 32 rows of
+// its side (queries, or keys in the dk/dv kernel) and walks the other side in 32-row sub-blocks staged through
+// LDS, 64 rows per tile, double-buffered (the next tile's global loads are issued before the current tile's
+// MFMAs).  MFMA operand layout of one k-step: lane l supplies A[l%32][slot l/32] and B[slot l/32][l%32], the
+// accumulator register r of lane l holds C[crow(r, l/32)][l%32].  Two choices make the whole step run out of
+// registers with no LDS round trip of the probabilities:
+//   * scores are computed TRANSPOSED, C = K . Q^T (forward, dq) or Q . K^T (dk/dv), so the owned side indexes the
+//     lanes and the other side the accumulator registers.  The row statistics of the owned side (running max,
+//     lse, delta) are then one value per lane, and the softmax reduction runs over a lane's own 16 registers plus
+//     one exchange between the two 32-lane halves;
+//   * the reduction index of the second product is the other side, which the score tile holds in its registers:
+//     register r of P^T is directly the B operand of k-step r when the logical reduction slot (r, l/32) is mapped
+//     to the physical row crow(r, l/32) -- the matching A operand is that LDS row, read column-wise.
+// The head-dim reduction of the score products maps slot (kk, l/32) to channel (l/32) * D/2 + kk, so each lane
+// reads a contiguous D/2-channel chunk of its row (ds_read_b128).  Outputs with head_dim below a multiple of 32
+// (24 -> 32) carry zero channel rows: the LDS tiles keep columns D..32*NT zero.
+// Scores are kept in log2 units (q pre-multiplied by scale * log2(e)): exp2 is the hardware v_exp_f32.
 // No dropout and no key padding: the front-end uses neither (nn.MultiheadAttention defaults, all clips valid).
 #include <math.h>
 
@@ -16,233 +33,436 @@
 
 namespace pdvc {
 
-constexpr int kSqT = 128;   // lanes (queries or keys) per workgroup
-constexpr int kSqTile = 128;  // rows of the other side per LDS tile
+typedef float sq_f32x16 __attribute__((ext_vector_type(16)));
 
-// rows [r0, r0 + n) of a (T, ld) head slice -> LDS [n][D]; missing rows zero
+constexpr int kSqWaves = 8;            // waves per workgroup, each owning 32 rows
+constexpr int kSqThreads = 64 * kSqWaves;
+constexpr int kSqOwn = 32 * kSqWaves;  // owned rows per workgroup
+constexpr int kSqKT = 64;              // rows of the streamed side per LDS tile
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+__device__ __forceinline__ sq_f32x16 sq_mfma(float a, float b, sq_f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int sq_crow(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
+__device__ __forceinline__ float sq_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float sq_swap32(float x) { return __shfl_xor(x, 32, PDVC_WAVE); }
+
 template <int D>
-__device__ __forceinline__ void sq_stage(float* lds, const float* src, long ld, int r0, int n, int T) {
-    for (int e = threadIdx.x; e < n * D; e += kSqT) {
-        const int r = e / D, c = e - r * D;
-        lds[e] = (r0 + r < T) ? src[(long)(r0 + r) * ld + c] : 0.f;
+struct SqCfg {
+    static constexpr int DH = D / 2;               // score k-steps over the head dim
+    static constexpr int NT = (D + 31) / 32;       // 32-channel output tiles
+    // LDS row stride D + 4 (= 4 x odd): the 16 rows of a ds_read_b128 lane group land on distinct bank quads.
+    // Column walks (A operands of the second products) read lanes l%32 = 0..31 of a row; lanes past D read
+    // the next row's first channels -- garbage that only reaches output channel rows >= D, never written.
+    static constexpr int LD = D + 4;
+    static constexpr int TILE = kSqKT * LD;        // floats per staged matrix tile
+    static constexpr int SMEM = 4 * TILE + 64;     // [buf][2 matrices] + slack for the last row's column walk
+    static constexpr int EPT = kSqKT * D / kSqThreads;  // staged elements per thread per matrix
+    // accumulator registers holding real channels of output tile t (channel rows >= D are padding)
+    static constexpr int valid(int t) { return (D - 32 * t) >= 32 ? 16 : (D - 32 * t) / 2; }
+    // forward: a spare output channel row D (head_dim not a multiple of 32) carries the softmax denominator,
+    // V's column D being held at 1 (accumulator register 12 of the lanes l/32 = 0 for D = 24)
+    static constexpr bool ONES = (D % 32) != 0;
+    static_assert(D % 8 == 0 && D <= 64, "head_dim must be a multiple of 8, at most 64");
+    static_assert((kSqKT * D) % kSqThreads == 0, "tile elements must split evenly over the threads");
+};
+
+// Row chunk [hi*D/2, hi*D/2 + D/2) of LDS row `row` -> registers (ds_read_b128)
+template <int D>
+__device__ __forceinline__ void sq_chunk(const float* tile, int row, int hi, float (&x)[D / 2]) {
+    const float4* p = reinterpret_cast<const float4*>(tile + row * SqCfg<D>::LD + hi * (D / 2));
+#pragma unroll
+    for (int i = 0; i < D / 8; ++i) {
+        const float4 f = p[i];
+        x[4 * i] = f.x;
+        x[4 * i + 1] = f.y;
+        x[4 * i + 2] = f.z;
+        x[4 * i + 3] = f.w;
     }
 }
 
-template <int D, int R>
-__global__ __launch_bounds__(kSqT) void seqattn_fwd_kernel(const float* __restrict__ q, const float* __restrict__ k,
-                                                           const float* __restrict__ v, int H, int Tq, int Tk,
-                                                           long ldq, long ldk, long ldv, float scale,
-                                                           float* __restrict__ out, float* __restrict__ lse) {
-    __shared__ float ks[kSqTile * D], vs[kSqTile * D];
-    const int nh = blockIdx.y, n = nh / H, h = nh - n * H;
-    const float* qh = q + (long)n * Tq * ldq + h * D;
-    const float* kh = k + (long)n * Tk * ldk + h * D;
-    const float* vh = v + (long)n * Tk * ldv + h * D;
-    float qi[R][D], acc[R][D], m[R], l[R];
+// Global -> register -> LDS staging of kSqKT-row tiles of two (rows, D) head slices; rows past `nrows` are zero.
+template <int D>
+struct SqStager {
+    static constexpr int EPT = SqCfg<D>::EPT;
+    int goff[EPT], soff[EPT];
+    float a[EPT], b[EPT];
+    __device__ __forceinline__ SqStager(int tid) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int i = blockIdx.x * kSqT * R + r * kSqT + threadIdx.x;
-#pragma unroll
-        for (int c = 0; c < D; ++c) {
-            qi[r][c] = i < Tq ? qh[(long)i * ldq + c] * scale : 0.f;
-            acc[r][c] = 0.f;
+        for (int i = 0; i < EPT; ++i) {
+            const int e = tid + kSqThreads * i, r = e / D, c = e - r * D;
+            goff[i] = (r << 8) | c;  // row (< 256) and column, unpacked per tile
+            soff[i] = r * SqCfg<D>::LD + c;
         }
-        m[r] = -INFINITY;
-        l[r] = 0.f;
     }
-    for (int t0 = 0; t0 < Tk; t0 += kSqTile) {
-        const int nt = min(kSqTile, Tk - t0);
-        __syncthreads();
-        sq_stage<D>(ks, kh, ldk, t0, nt, Tk);
-        sq_stage<D>(vs, vh, ldv, t0, nt, Tk);
-        __syncthreads();
-        for (int j = 0; j < nt; ++j) {
-            float kv[D];
+    __device__ __forceinline__ void load(const float* __restrict__ A, long lda, const float* __restrict__ B, long ldb,
+                                         int r0, int nrows) {
+        const float* Ar = A + (long)r0 * lda;
+        const float* Br = B + (long)r0 * ldb;
+        if (r0 + kSqKT <= nrows) {  // full tile: no row predicate
 #pragma unroll
-            for (int c = 0; c < D; ++c) kv[c] = ks[j * D + c];
+            for (int i = 0; i < EPT; ++i) {
+                const int r = goff[i] >> 8, c = goff[i] & 255;
+                a[i] = Ar[r * lda + c];
+                b[i] = Br[r * ldb + c];
+            }
+        } else {
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                float s = 0.f;
-#pragma unroll
-                for (int c = 0; c < D; ++c) s += qi[r][c] * kv[c];
-                if (s > m[r]) {
-                    const float corr = __expf(m[r] - s);
-                    l[r] *= corr;
-#pragma unroll
-                    for (int c = 0; c < D; ++c) acc[r][c] *= corr;
-                    m[r] = s;
-                }
-                const float p = __expf(s - m[r]);
-                l[r] += p;
-#pragma unroll
-                for (int c = 0; c < D; ++c) acc[r][c] += p * vs[j * D + c];
+            for (int i = 0; i < EPT; ++i) {
+                const int r = goff[i] >> 8, c = goff[i] & 255;
+                const bool ok = r0 + r < nrows;
+                a[i] = ok ? Ar[r * lda + c] : 0.f;
+                b[i] = ok ? Br[r * ldb + c] : 0.f;
             }
         }
     }
+    __device__ __forceinline__ void store(float* ta, float* tb) const {
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int i = blockIdx.x * kSqT * R + r * kSqT + threadIdx.x;
-        if (i < Tq) {
-            const float inv = 1.f / l[r];
-            float* o = out + ((long)n * Tq + i) * H * D + h * D;
-#pragma unroll
-            for (int c = 0; c < D; ++c) o[c] = acc[r][c] * inv;
-            lse[(long)nh * Tq + i] = m[r] + logf(l[r]);
+        for (int i = 0; i < EPT; ++i) {
+            ta[soff[i]] = a[i];
+            tb[soff[i]] = b[i];
         }
+    }
+};
+
+// Workgroup -> (video*head, owned block): consecutive owned blocks of one head on one XCD (shared K/V in its L2)
+__device__ __forceinline__ void sq_block(int nblocks_own, int& nh, int& ob) {
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    nh = lb / nblocks_own;
+    ob = lb - nh * nblocks_own;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// forward: wave = 32 queries; per 64-key tile S^T = K . Q^T (two independent 32-key MFMA chains), one online
+// softmax update over the key registers, O^T += V^T . P^T.  Measured alternatives (tools/seqattn_bench.py, T=512,
+// 32 heads of 24, 64 videos; this kernel 0.62 ms = 83 TFLOP/s): two 32-query blocks per wave sharing the K / V
+// operand reads 75-85; a one-tile software pipeline (next tile's score MFMAs before this tile's softmax, two named
+// score states, 240 VGPRs) 69; 128-key tiles 65; s_setprio around the MFMA runs and sched_group_barrier
+// interleaves within noise.  The workgroup is 8 waves (256 queries, 2 per (video, head) at T = 512) held to 4
+// waves per SIMD (<= 128 VGPRs).
+template <int D>
+__global__ __launch_bounds__(kSqThreads) __attribute__((amdgpu_waves_per_eu(4))) void seqattn_fwd_kernel(
+    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v, int H, int Tq, int Tk,
+    long ldq, long ldk, long ldv, float qmul, int qblocks, float* __restrict__ out, float* __restrict__ lse) {
+    using C = SqCfg<D>;
+    constexpr int SB = kSqKT / 32;          // 32-key score blocks per tile
+    constexpr int TL = C::NT - 1;           // output tile holding channel row D (ONES)
+    constexpr int RL = (D - 32 * TL) / 2;   // its accumulator register in the lanes l/32 = 0
+    __shared__ __attribute__((aligned(16))) float smem[C::SMEM];  // [buf][K, V]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, hi = lane >> 5;
+    int nh, qb;
+    sq_block(qblocks, nh, qb);
+    const int n = nh / H, h = nh - n * H;
+    const int qi = qb * kSqOwn + w * 32 + l32;
+    const bool qok = qi < Tq;
+    float qr[C::DH];
+    {
+        const float* qp = q + ((long)n * Tq + (qok ? qi : 0)) * ldq + h * D + hi * C::DH;
+#pragma unroll
+        for (int kk = 0; kk < C::DH; ++kk) qr[kk] = qok ? qp[kk] * qmul : 0.f;
+    }
+    const float* kh = k + (long)n * Tk * ldk + h * D;
+    const float* vh = v + (long)n * Tk * ldv + h * D;
+    if (C::ONES)
+        for (int r = tid; r < 2 * kSqKT; r += kSqThreads)
+            smem[(r / kSqKT) * 2 * C::TILE + C::TILE + (r % kSqKT) * C::LD + D] = 1.f;
+    SqStager<D> st(tid);
+    st.load(kh, ldk, vh, ldv, 0, Tk);
+    st.store(smem, smem + C::TILE);
+    __syncthreads();
+    sq_f32x16 o[C::NT];
+#pragma unroll
+    for (int t = 0; t < C::NT; ++t) o[t] = sq_f32x16{};
+    float m = -INFINITY, l = 0.f;
+    const int ntiles = (Tk + kSqKT - 1) / kSqKT;
+    for (int it = 0; it < ntiles; ++it) {
+        const int t0 = it * kSqKT;
+        const float* Ks = smem + (it & 1) * 2 * C::TILE;
+        const float* Vs = Ks + C::TILE;
+        if (it + 1 < ntiles) st.load(kh, ldk, vh, ldv, t0 + kSqKT, Tk);
+        // the tile's 32-key score blocks (independent MFMA chains), one softmax update over the whole tile
+        sq_f32x16 s[SB];
+        {
+            float kc[SB][C::DH];
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) sq_chunk<D>(Ks, sb * 32 + l32, hi, kc[sb]);
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) s[sb] = sq_mfma(kc[sb][0], qr[0], sq_f32x16{});
+#pragma unroll
+            for (int kk = 1; kk < C::DH; ++kk)
+#pragma unroll
+                for (int sb = 0; sb < SB; ++sb) s[sb] = sq_mfma(kc[sb][kk], qr[kk], s[sb]);
+        }
+        if (t0 + kSqKT > Tk) {
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (t0 + sb * 32 + sq_crow(r, hi) >= Tk) s[sb][r] = -INFINITY;
+        }
+        float mx = s[0][0];
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[sb][r]);
+        mx = fmaxf(mx, sq_swap32(mx));
+        const float mn = fmaxf(m, mx);  // finite: the tile holds at least one valid key
+        const float corr = sq_exp2(m - mn);
+        m = mn;
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[sb][r] = sq_exp2(s[sb][r] - mn);
+        if (!C::ONES) {
+            l *= corr;
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) l += s[sb][r];
+        }
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+            for (int r = 0; r < C::valid(t) + (C::ONES && t == TL ? 1 : 0); ++r) o[t][r] *= corr;
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float* vc = Vs + (sb * 32 + sq_crow(r, hi)) * C::LD + l32;
+#pragma unroll
+                for (int t = 0; t < C::NT; ++t) o[t] = sq_mfma(vc[32 * t], s[sb][r], o[t]);
+            }
+        if (it + 1 < ntiles) st.store(smem + ((it + 1) & 1) * 2 * C::TILE, smem + ((it + 1) & 1) * 2 * C::TILE + C::TILE);
+        __syncthreads();
+    }
+    if (C::ONES) {  // channel row D = sum_j p_j, held by the lanes l/32 = 0
+        const float own = o[TL][RL], other = sq_swap32(own);
+        l = hi ? other : own;
+    } else {
+        l += sq_swap32(l);
+    }
+    if (qok) {
+        const float inv = 1.f / l;
+        float* orow = out + ((long)n * Tq + qi) * (long)(H * D) + h * D;
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+            for (int g = 0; g < C::valid(t) / 4; ++g)
+                *reinterpret_cast<float4*>(orow + 32 * t + 8 * g + 4 * hi) =
+                    make_float4(o[t][4 * g] * inv, o[t][4 * g + 1] * inv, o[t][4 * g + 2] * inv, o[t][4 * g + 3] * inv);
+        if (hi == 0) lse[(long)nh * Tq + qi] = (m + log2f(l)) * kLn2;
     }
 }
 
-template <int D, int R>
-__global__ __launch_bounds__(kSqT) void seqattn_bwd_dq_kernel(const float* __restrict__ q, const float* __restrict__ k,
+// ---------------------------------------------------------------------------------------------------------------
+// backward, query owner: S^T = K . Q^T, dP^T = V . dO^T, dS^T = P^T (dP^T - delta), dQ^T += K^T . dS^T.
+// Publishes delta_i = dout_i . out_i for the key-owner kernel.
+template <int D>
+__global__ __launch_bounds__(kSqThreads) void seqattn_bwd_dq_kernel(const float* __restrict__ q, const float* __restrict__ k,
+                                                             const float* __restrict__ v, const float* __restrict__ dout,
+                                                             const float* __restrict__ lse,
+                                                             const float* __restrict__ out, float* __restrict__ delta,
+                                                             int H, int Tq, int Tk, long ldq, long ldk, long ldv,
+                                                             float qmul, float scale, int qblocks,
+                                                             float* __restrict__ dq, long lddq) {
+    using C = SqCfg<D>;
+    __shared__ __attribute__((aligned(16))) float smem[C::SMEM];  // [buf][K, V]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, hi = lane >> 5;
+    int nh, qb;
+    sq_block(qblocks, nh, qb);
+    const int n = nh / H, h = nh - n * H;
+    const int E = H * D;
+    const int qi = qb * kSqOwn + w * 32 + l32;
+    const bool qok = qi < Tq;
+    float qr[C::DH], gr[C::DH];
+    float dl = 0.f, l2 = 0.f;
+    {
+        const long qrow = (long)n * Tq + (qok ? qi : 0);
+        const float* qp = q + qrow * ldq + h * D + hi * C::DH;
+        const float* gp = dout + qrow * E + h * D + hi * C::DH;
+        const float* op = out + qrow * E + h * D + hi * C::DH;
+#pragma unroll
+        for (int kk = 0; kk < C::DH; ++kk) {
+            qr[kk] = qok ? qp[kk] * qmul : 0.f;
+            gr[kk] = qok ? gp[kk] : 0.f;
+            dl += qok ? gr[kk] * op[kk] : 0.f;
+        }
+        dl += sq_swap32(dl);
+        if (qok) {
+            l2 = lse[(long)nh * Tq + qi] * kLog2e;
+            if (hi == 0) delta[(long)nh * Tq + qi] = dl;
+        }
+    }
+    const float* kh = k + (long)n * Tk * ldk + h * D;
+    const float* vh = v + (long)n * Tk * ldv + h * D;
+    SqStager<D> st(tid);
+    st.load(kh, ldk, vh, ldv, 0, Tk);
+    st.store(smem, smem + C::TILE);
+    __syncthreads();
+    sq_f32x16 acc[C::NT];
+#pragma unroll
+    for (int t = 0; t < C::NT; ++t) acc[t] = sq_f32x16{};
+    const int ntiles = (Tk + kSqKT - 1) / kSqKT;
+    for (int it = 0; it < ntiles; ++it) {
+        const int t0 = it * kSqKT;
+        const float* Ks = smem + (it & 1) * 2 * C::TILE;
+        const float* Vs = Ks + C::TILE;
+        if (it + 1 < ntiles) st.load(kh, ldk, vh, ldv, t0 + kSqKT, Tk);
+#pragma unroll
+        for (int sb = 0; sb < kSqKT / 32; ++sb) {
+            if (t0 + sb * 32 >= Tk) break;  // keys past Tk inside a sub-block are zero rows: ds * 0 adds nothing
+            float kc[C::DH], vc[C::DH];
+            sq_chunk<D>(Ks, sb * 32 + l32, hi, kc);
+            sq_chunk<D>(Vs, sb * 32 + l32, hi, vc);
+            sq_f32x16 s = sq_f32x16{}, dp = sq_f32x16{};
+#pragma unroll
+            for (int kk = 0; kk < C::DH; ++kk) {
+                s = sq_mfma(kc[kk], qr[kk], s);
+                dp = sq_mfma(vc[kk], gr[kk], dp);
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[r] = sq_exp2(s[r] - l2) * (dp[r] - dl);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float* kcol = Ks + (sb * 32 + sq_crow(r, hi)) * C::LD + l32;
+#pragma unroll
+                for (int t = 0; t < C::NT; ++t) acc[t] = sq_mfma(kcol[32 * t], s[r], acc[t]);
+            }
+        }
+        if (it + 1 < ntiles) st.store(smem + ((it + 1) & 1) * 2 * C::TILE, smem + ((it + 1) & 1) * 2 * C::TILE + C::TILE);
+        __syncthreads();
+    }
+    if (qok) {
+        float* row = dq + ((long)n * Tq + qi) * lddq + h * D;
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+            for (int r = 0; r < C::valid(t); ++r) row[32 * t + sq_crow(r, hi)] = acc[t][r] * scale;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// backward, key owner: S = Q . K^T, dP = dO . V^T (key index on the lanes), dV^T += dO^T . P, dK^T += Q^T . dS.
+template <int D>
+__global__ __launch_bounds__(kSqThreads) void seqattn_bwd_dkv_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                               const float* __restrict__ v,
                                                               const float* __restrict__ dout,
                                                               const float* __restrict__ lse,
-                                                              const float* __restrict__ out,
-                                                              float* __restrict__ delta, int H, int Tq, int Tk,
-                                                              long ldq, long ldk, long ldv, float scale,
-                                                              float* __restrict__ dq, long lddq) {
-    __shared__ float ks[kSqTile * D], vs[kSqTile * D];
-    const int nh = blockIdx.y, n = nh / H, h = nh - n * H;
+                                                              const float* __restrict__ delta, int H, int Tq, int Tk,
+                                                              long ldq, long ldk, long ldv, float kmul, float scale,
+                                                              int kblocks, float* __restrict__ dk, long lddk,
+                                                              float* __restrict__ dv, long lddv) {
+    using C = SqCfg<D>;
+    __shared__ __attribute__((aligned(16))) float smem[C::SMEM];  // [buf][Q, dO]
+    __shared__ __attribute__((aligned(16))) float rowst[2][2][kSqKT];   // [buf][lse2, delta]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, hi = lane >> 5;
+    int nh, kb;
+    sq_block(kblocks, nh, kb);
+    const int n = nh / H, h = nh - n * H;
+    const int E = H * D;
+    const int kj = kb * kSqOwn + w * 32 + l32;
+    const bool kok = kj < Tk;
+    float kr[C::DH], vr[C::DH];
+    {
+        const long krow = (long)n * Tk + (kok ? kj : 0);
+        const float* kp = k + krow * ldk + h * D + hi * C::DH;
+        const float* vp = v + krow * ldv + h * D + hi * C::DH;
+#pragma unroll
+        for (int kk = 0; kk < C::DH; ++kk) {
+            kr[kk] = kok ? kp[kk] * kmul : 0.f;
+            vr[kk] = kok ? vp[kk] : 0.f;
+        }
+    }
     const float* qh = q + (long)n * Tq * ldq + h * D;
-    const float* kh = k + (long)n * Tk * ldk + h * D;
-    const float* vh = v + (long)n * Tk * ldv + h * D;
-    const float* gh = dout + (long)n * Tq * H * D + h * D;
-    float qi[R][D], gi[R][D], acc[R][D], li[R], di[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int i = blockIdx.x * kSqT * R + r * kSqT + threadIdx.x;
-        const bool act = i < Tq;
-#pragma unroll
-        for (int c = 0; c < D; ++c) {
-            qi[r][c] = act ? qh[(long)i * ldq + c] * scale : 0.f;
-            gi[r][c] = act ? gh[(long)i * H * D + c] : 0.f;
-            acc[r][c] = 0.f;
+    const float* gh = dout + (long)n * Tq * E + h * D;
+    const float* lh = lse + (long)nh * Tq;
+    const float* dh = delta + (long)nh * Tq;
+    SqStager<D> st(tid);
+    float rl = 0.f, rd = 0.f;  // this thread's row statistic (threads < 64)
+    auto load_rows = [&](int r0) {
+        if (tid < kSqKT) {
+            const int i = r0 + tid;
+            rl = i < Tq ? lh[i] * kLog2e : INFINITY;  // padded queries: p = exp2(s - inf) = 0
+            rd = i < Tq ? dh[i] : 0.f;
         }
-        li[r] = act ? lse[(long)nh * Tq + i] : 0.f;
-        // delta_i = dout_i . out_i, from the lane's own rows; published for the dk/dv kernel launched after this
-        float dsum = 0.f;
-        if (act) {
-            const float* oh = out + ((long)n * Tq + i) * H * D + h * D;
-#pragma unroll
-            for (int c = 0; c < D; ++c) dsum += gi[r][c] * oh[c];
-            delta[(long)nh * Tq + i] = dsum;
+    };
+    auto store_rows = [&](int buf) {
+        if (tid < kSqKT) {
+            rowst[buf][0][tid] = rl;
+            rowst[buf][1][tid] = rd;
         }
-        di[r] = dsum;
-    }
-    for (int t0 = 0; t0 < Tk; t0 += kSqTile) {
-        const int nt = min(kSqTile, Tk - t0);
-        __syncthreads();
-        sq_stage<D>(ks, kh, ldk, t0, nt, Tk);
-        sq_stage<D>(vs, vh, ldv, t0, nt, Tk);
-        __syncthreads();
-        for (int j = 0; j < nt; ++j) {
-            float kv[D], vv[D];
+    };
+    st.load(qh, ldq, gh, E, 0, Tq);
+    load_rows(0);
+    st.store(smem, smem + C::TILE);
+    store_rows(0);
+    __syncthreads();
+    sq_f32x16 ak[C::NT], av[C::NT];
 #pragma unroll
-            for (int c = 0; c < D; ++c) {
-                kv[c] = ks[j * D + c];
-                vv[c] = vs[j * D + c];
+    for (int t = 0; t < C::NT; ++t) ak[t] = av[t] = sq_f32x16{};
+    const int ntiles = (Tq + kSqKT - 1) / kSqKT;
+    for (int it = 0; it < ntiles; ++it) {
+        const int t0 = it * kSqKT, buf = it & 1;
+        const float* Qs = smem + buf * 2 * C::TILE;
+        const float* Gs = Qs + C::TILE;
+        if (it + 1 < ntiles) {
+            st.load(qh, ldq, gh, E, t0 + kSqKT, Tq);
+            load_rows(t0 + kSqKT);
+        }
+#pragma unroll
+        for (int sb = 0; sb < kSqKT / 32; ++sb) {
+            if (t0 + sb * 32 >= Tq) break;
+            float qc[C::DH], gc[C::DH];
+            sq_chunk<D>(Qs, sb * 32 + l32, hi, qc);
+            sq_chunk<D>(Gs, sb * 32 + l32, hi, gc);
+            sq_f32x16 s = sq_f32x16{}, dp = sq_f32x16{};
+#pragma unroll
+            for (int kk = 0; kk < C::DH; ++kk) {
+                s = sq_mfma(qc[kk], kr[kk], s);
+                dp = sq_mfma(gc[kk], vr[kk], dp);
             }
+            // query rows of the registers: sb*32 + crow(r, hi) -> 4 float4 reads of each statistic
+            const float4* L4 = reinterpret_cast<const float4*>(&rowst[buf][0][sb * 32 + 4 * hi]);
+            const float4* D4 = reinterpret_cast<const float4*>(&rowst[buf][1][sb * 32 + 4 * hi]);
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                float s = 0.f, dp = 0.f;
+            for (int g = 0; g < 4; ++g) {
+                const float4 lv = L4[2 * g], dv4 = D4[2 * g];
+                const float lr[4] = {lv.x, lv.y, lv.z, lv.w}, dr[4] = {dv4.x, dv4.y, dv4.z, dv4.w};
 #pragma unroll
-                for (int c = 0; c < D; ++c) {
-                    s += qi[r][c] * kv[c];
-                    dp += gi[r][c] * vv[c];
+                for (int j = 0; j < 4; ++j) {
+                    const int r = 4 * g + j;
+                    s[r] = sq_exp2(s[r] - lr[j]);
+                    dp[r] = s[r] * (dp[r] - dr[j]);
                 }
-                const float ds = __expf(s - li[r]) * (dp - di[r]);
-#pragma unroll
-                for (int c = 0; c < D; ++c) acc[r][c] += ds * kv[c];
             }
-        }
-    }
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int i = blockIdx.x * kSqT * R + r * kSqT + threadIdx.x;
-        if (i < Tq) {
-            float* o = dq + ((long)n * Tq + i) * lddq + h * D;
+            for (int r = 0; r < 16; ++r) {
+                const int row = (sb * 32 + sq_crow(r, hi)) * C::LD + l32;
 #pragma unroll
-            for (int c = 0; c < D; ++c) o[c] = acc[r][c] * scale;
-        }
-    }
-}
-
-template <int D, int R>
-__global__ __launch_bounds__(kSqT) void seqattn_bwd_dkv_kernel(const float* __restrict__ q, const float* __restrict__ k,
-                                                               const float* __restrict__ v,
-                                                               const float* __restrict__ dout,
-                                                               const float* __restrict__ lse,
-                                                               const float* __restrict__ delta, int H, int Tq, int Tk,
-                                                               long ldq, long ldk, long ldv, float scale,
-                                                               float* __restrict__ dk, long lddk,
-                                                               float* __restrict__ dv, long lddv) {
-    __shared__ float qs[kSqTile * D], gs[kSqTile * D], ls[kSqTile], dls[kSqTile];
-    const int nh = blockIdx.y, n = nh / H, h = nh - n * H;
-    const float* qh = q + (long)n * Tq * ldq + h * D;
-    const float* kh = k + (long)n * Tk * ldk + h * D;
-    const float* vh = v + (long)n * Tk * ldv + h * D;
-    const float* gh = dout + (long)n * Tq * H * D + h * D;
-    float kj[R][D], vj[R][D], ak[R][D], av[R][D];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int j = blockIdx.x * kSqT * R + r * kSqT + threadIdx.x;
-        const bool act = j < Tk;
-#pragma unroll
-        for (int c = 0; c < D; ++c) {
-            kj[r][c] = act ? kh[(long)j * ldk + c] * scale : 0.f;
-            vj[r][c] = act ? vh[(long)j * ldv + c] : 0.f;
-            ak[r][c] = 0.f;
-            av[r][c] = 0.f;
-        }
-    }
-    for (int t0 = 0; t0 < Tq; t0 += kSqTile) {
-        const int nt = min(kSqTile, Tq - t0);
-        __syncthreads();
-        sq_stage<D>(qs, qh, ldq, t0, nt, Tq);
-        sq_stage<D>(gs, gh, (long)H * D, t0, nt, Tq);
-        for (int e = threadIdx.x; e < nt; e += kSqT) {
-            ls[e] = lse[(long)nh * Tq + t0 + e];
-            dls[e] = delta[(long)nh * Tq + t0 + e];
-        }
-        __syncthreads();
-        for (int i = 0; i < nt; ++i) {
-            float qv[D], gv[D];
-#pragma unroll
-            for (int c = 0; c < D; ++c) {
-                qv[c] = qs[i * D + c];
-                gv[c] = gs[i * D + c];
-            }
-            const float li = ls[i], di = dls[i];
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                float s = 0.f, dp = 0.f;
-#pragma unroll
-                for (int c = 0; c < D; ++c) {
-                    s += kj[r][c] * qv[c];
-                    dp += vj[r][c] * gv[c];
-                }
-                const float p = __expf(s - li);
-                const float ds = p * (dp - di);
-#pragma unroll
-                for (int c = 0; c < D; ++c) {
-                    av[r][c] += p * gv[c];
-                    ak[r][c] += ds * qv[c];
+                for (int t = 0; t < C::NT; ++t) {
+                    av[t] = sq_mfma(Gs[row + 32 * t], s[r], av[t]);
+                    ak[t] = sq_mfma(Qs[row + 32 * t], dp[r], ak[t]);
                 }
             }
         }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int j = blockIdx.x * kSqT * R + r * kSqT + threadIdx.x;
-        if (j < Tk) {
-            float* ok = dk + ((long)n * Tk + j) * lddk + h * D;
-            float* ov = dv + ((long)n * Tk + j) * lddv + h * D;
-#pragma unroll
-            for (int c = 0; c < D; ++c) {
-                ok[c] = ak[r][c] * scale;
-                ov[c] = av[r][c];
-            }
+        if (it + 1 < ntiles) {
+            st.store(smem + (buf ^ 1) * 2 * C::TILE, smem + (buf ^ 1) * 2 * C::TILE + C::TILE);
+            store_rows(buf ^ 1);
         }
+        __syncthreads();
+    }
+    if (kok) {
+        float* rk = dk + ((long)n * Tk + kj) * lddk + h * D;
+        float* rv = dv + ((long)n * Tk + kj) * lddv + h * D;
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+            for (int r = 0; r < C::valid(t); ++r) {
+                rk[32 * t + sq_crow(r, hi)] = ak[t][r] * scale;
+                rv[32 * t + sq_crow(r, hi)] = av[t][r];
+            }
     }
 }
 
@@ -255,13 +475,6 @@ __global__ __launch_bounds__(kSqT) void seqattn_bwd_dkv_kernel(const float* __re
         case 64: CALL(64); break;  \
         default: break;            \
     }
-
-// query rows per lane in the forward and dq kernels: 2 for head_dim <= 32 (each key row read from LDS serves two
-// queries), 1 above (register budget)
-static constexpr int sq_rows_per_lane(int D) { return D <= 32 ? 2 : 1; }
-
-// key rows per lane in the dk/dv kernel: 2 for head_dim <= 24 (four D-vectors per key row live in registers)
-static constexpr int sq_keys_per_lane(int D) { return D <= 24 ? 2 : 1; }
 
 static bool sq_head_dim_ok(int D) { return D == 16 || D == 24 || D == 32 || D == 48 || D == 64; }
 
@@ -276,19 +489,17 @@ extern "C" int pdvc_seq_attention_forward_f32(const float* q, long ldq, const fl
     PDVC_CHECK_ARG(sq_head_dim_ok(head_dim), "head_dim must be 16, 24, 32, 48 or 64, got %d", head_dim);
     const long E = (long)num_heads * head_dim;
     PDVC_CHECK_ARG(ldq >= E && ldk >= E && ldv >= E, "row strides must be >= num_heads * head_dim");
-    PDVC_CHECK_ARG((long)batch * num_heads < 65536, "batch * num_heads must be < 65536");
     if (batch == 0 || num_query == 0) return PDVC_OK;
+    const long blocks = (long)((num_query + kSqOwn - 1) / kSqOwn) * batch * num_heads;
+    PDVC_CHECK_ARG(blocks < (1L << 31), "too many (video, head, query block) workgroups");
+    PDVC_CHECK_ARG((long)num_key * ldk < (1L << 31) && (long)num_key * ldv < (1L << 31),
+                   "one video's keys must span < 2^31 floats");
     const float scale = 1.f / sqrtf((float)head_dim);
-    const int R = sq_rows_per_lane(head_dim);
-    dim3 grid((unsigned)((num_query + kSqT * R - 1) / (kSqT * R)), (unsigned)(batch * num_heads));
+    const int qblocks = (num_query + kSqOwn - 1) / kSqOwn;
     hipStream_t s = (hipStream_t)stream;
-#define PDVC_SQ_FWD(DD)                                                                                              \
-    if (sq_rows_per_lane(DD) == 2)                                                                                   \
-        hipLaunchKernelGGL((seqattn_fwd_kernel<DD, 2>), grid, dim3(kSqT), 0, s, q, k, v, num_heads, num_query,       \
-                           num_key, ldq, ldk, ldv, scale, out, lse);                                                \
-    else                                                                                                             \
-        hipLaunchKernelGGL((seqattn_fwd_kernel<DD, 1>), grid, dim3(kSqT), 0, s, q, k, v, num_heads, num_query,       \
-                           num_key, ldq, ldk, ldv, scale, out, lse)
+#define PDVC_SQ_FWD(DD)                                                                                          \
+    hipLaunchKernelGGL((seqattn_fwd_kernel<DD>), dim3((unsigned)blocks), dim3(kSqThreads), 0, s, q, k, v, num_heads,    \
+                       num_query, num_key, ldq, ldk, ldv, scale * kLog2e, qblocks, out, lse)
     PDVC_SQ_DISPATCH(head_dim, PDVC_SQ_FWD)
 #undef PDVC_SQ_FWD
     PDVC_CHECK_LAUNCH("seqattn_fwd_kernel");
@@ -305,7 +516,6 @@ extern "C" int pdvc_seq_attention_backward_f32(const float* q, long ldq, const f
     const long E = (long)num_heads * head_dim;
     PDVC_CHECK_ARG(ldq >= E && ldk >= E && ldv >= E && ld_grad_q >= E && ld_grad_k >= E && ld_grad_v >= E,
                    "row strides must be >= num_heads * head_dim");
-    PDVC_CHECK_ARG((long)batch * num_heads < 65536, "batch * num_heads must be < 65536");
     if (batch == 0) return PDVC_OK;
     hipStream_t s = (hipStream_t)stream;
     const float scale = 1.f / sqrtf((float)head_dim);
@@ -317,26 +527,21 @@ extern "C" int pdvc_seq_attention_backward_f32(const float* q, long ldq, const f
         if (e1 != hipSuccess || e2 != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_k/grad_v");
         return PDVC_OK;
     }
+    const int qblocks = (num_query + kSqOwn - 1) / kSqOwn, kblocks = (num_key + kSqOwn - 1) / kSqOwn;
+    const long gq = (long)qblocks * batch * num_heads, gk = (long)kblocks * batch * num_heads;
+    PDVC_CHECK_ARG(gq < (1L << 31) && gk < (1L << 31), "too many (video, head, block) workgroups");
+    PDVC_CHECK_ARG((long)num_query * ldq < (1L << 31) && (long)num_query * E < (1L << 31) &&
+                       (long)num_key * ldk < (1L << 31) && (long)num_key * ldv < (1L << 31),
+                   "one video's rows must span < 2^31 floats");
     float* delta = workspace;  // (N, H, Tq): written by the dq kernel, read by the dk/dv kernel
-    const int R = sq_rows_per_lane(head_dim);
-    dim3 gq((unsigned)((num_query + kSqT * R - 1) / (kSqT * R)), (unsigned)(batch * num_heads));
-    const int RK = sq_keys_per_lane(head_dim);
-    dim3 gk((unsigned)((num_key + kSqT * RK - 1) / (kSqT * RK)), (unsigned)(batch * num_heads));
-#define PDVC_SQ_DQ(DD)                                                                                               \
-    if (sq_rows_per_lane(DD) == 2)                                                                                   \
-        hipLaunchKernelGGL((seqattn_bwd_dq_kernel<DD, 2>), gq, dim3(kSqT), 0, s, q, k, v, grad_out, lse, out, delta, \
-                           num_heads, num_query, num_key, ldq, ldk, ldv, scale, grad_q, ld_grad_q);                 \
-    else                                                                                                             \
-        hipLaunchKernelGGL((seqattn_bwd_dq_kernel<DD, 1>), gq, dim3(kSqT), 0, s, q, k, v, grad_out, lse, out, delta, \
-                           num_heads, num_query, num_key, ldq, ldk, ldv, scale, grad_q, ld_grad_q)
-#define PDVC_SQ_DKV(DD)                                                                                              \
-    if (sq_keys_per_lane(DD) == 2)                                                                                   \
-        hipLaunchKernelGGL((seqattn_bwd_dkv_kernel<DD, 2>), gk, dim3(kSqT), 0, s, q, k, v, grad_out, lse, delta,     \
-                           num_heads, num_query, num_key, ldq, ldk, ldv, scale, grad_k, ld_grad_k, grad_v,          \
-                           ld_grad_v);                                                                              \
-    else                                                                                                             \
-        hipLaunchKernelGGL((seqattn_bwd_dkv_kernel<DD, 1>), gk, dim3(kSqT), 0, s, q, k, v, grad_out, lse, delta,     \
-                           num_heads, num_query, num_key, ldq, ldk, ldv, scale, grad_k, ld_grad_k, grad_v, ld_grad_v)
+#define PDVC_SQ_DQ(DD)                                                                                             \
+    hipLaunchKernelGGL((seqattn_bwd_dq_kernel<DD>), dim3((unsigned)gq), dim3(kSqThreads), 0, s, q, k, v, grad_out, lse, \
+                       out, delta, num_heads, num_query, num_key, ldq, ldk, ldv, scale * kLog2e, scale, qblocks,    \
+                       grad_q, ld_grad_q)
+#define PDVC_SQ_DKV(DD)                                                                                             \
+    hipLaunchKernelGGL((seqattn_bwd_dkv_kernel<DD>), dim3((unsigned)gk), dim3(kSqThreads), 0, s, q, k, v, grad_out, lse, \
+                       delta, num_heads, num_query, num_key, ldq, ldk, ldv, scale * kLog2e, scale, kblocks, grad_k, \
+                       ld_grad_k, grad_v, ld_grad_v)
     PDVC_SQ_DISPATCH(head_dim, PDVC_SQ_DQ)
     PDVC_CHECK_LAUNCH("seqattn_bwd_dq_kernel");
     PDVC_SQ_DISPATCH(head_dim, PDVC_SQ_DKV)

@@ -27,6 +27,28 @@ class NewModel(DualModalityFrontEnd):
         return output, loss, 0
 
 
+class NewModelStep(nn.Module):
+    """A NewModel behind PDVC's calling convention, model(dt, criterion, transformer_input_type, eval_mode) ->
+    (output, loss) (pdvc.py:124), so the training-step machinery (StepGraph, bench.py) drives it like PDVC:
+    the front-end runs on dt['video_tensor'] / dt['sound_tensor'], then PDVC on its output."""
+
+    def __init__(self, newmodel):
+        super().__init__()
+        self.newmodel = newmodel
+
+    def forward(self, dt, criterion=None, transformer_input_type="queries", eval_mode=False):
+        m = self.newmodel
+        clips = dt["video_tensor"]
+        # the front-end output replaces the clips for PDVC only while it runs: dt stays the caller's object (PDVC
+        # caches its host-side facts in it, which a hipGraph capture of the step relies on) and keeps the clips
+        dt["video_tensor"] = DualModalityFrontEnd.forward(m, clips, dt["sound_tensor"])
+        try:
+            return m.pdvcModel(dt, criterion if criterion is not None else m.pdvcCriterion, transformer_input_type,
+                               eval_mode=eval_mode)
+        finally:
+            dt["video_tensor"] = clips
+
+
 def build_newmodel(args):
     """(model, criterion, postprocessors) like pdvc.build, with the front-end in front (NewModel.py:15)."""
     m = NewModel(args)

@@ -73,7 +73,8 @@ def test_frontend_matches_multiheadattention_reference(T, dim, heads):
         close(p.grad, refp[n].grad, TOL, "grad " + n)
 
 
-@pytest.mark.parametrize("Tq,Tk,H,D", [(1, 1, 2, 16), (200, 300, 4, 64), (129, 257, 3, 48), (64, 5, 2, 32)])
+@pytest.mark.parametrize("Tq,Tk,H,D", [(1, 1, 2, 16), (200, 300, 4, 64), (129, 257, 3, 48), (64, 5, 2, 32),
+                                       (512, 512, 32, 24), (33, 70, 4, 24), (300, 1, 2, 24), (130, 97, 5, 16)])
 def test_seq_attention_core_vs_float64(Tq, Tk, H, D):
     """The attention core alone, queries and keys of different lengths, packed (strided) q/k/v views."""
     from pdvc.ops.functions.seq_attention import seq_attention
