@@ -139,8 +139,8 @@ __device__ __forceinline__ void sq_block(int nblocks_own, int& nh, int& ob) {
 // softmax update over the key registers, O^T += V^T . P^T.  Measured alternatives (tools/seqattn_bench.py, T=512,
 // 32 heads of 24, 64 videos; this kernel 0.62 ms = 83 TFLOP/s): two 32-query blocks per wave sharing the K / V
 // operand reads 75-85; a one-tile software pipeline (next tile's score MFMAs before this tile's softmax, two named
-// score states, 240 VGPRs) 69; 128-key tiles 65; s_setprio around the MFMA runs and sched_group_barrier
-// interleaves within noise.  The workgroup is 8 waves (256 queries, 2 per (video, head) at T = 512) held to 4
+// score states, 240 VGPRs) 69; 128-key tiles 65; s_setprio around the MFMA runs, sched_group_barrier
+// interleaves and skipping the identity rescale when no row max moved: within noise.  The workgroup is 8 waves (256 queries, 2 per (video, head) at T = 512) held to 4
 // waves per SIMD (<= 128 VGPRs).
 template <int D>
 __global__ __launch_bounds__(kSqThreads) __attribute__((amdgpu_waves_per_eu(4))) void seqattn_fwd_kernel(

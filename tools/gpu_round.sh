@@ -8,6 +8,7 @@
 #   gemm    bench.py --gemm hip + tools/gemmbench.py
 #   prof    rocprofv3 --kernel-trace --stats of bench.py, summarised by tools/profsum.py
 #   pmc     FETCH_SIZE and WRITE_SIZE passes over the roofline kernel -> tools/pmc_traffic.py
+# BENCH_ARGS (environment) is appended to the bench.py command lines of bench / prof (e.g. --workload ...).
 set -o pipefail
 TAG=${1:-r01}
 shift
@@ -47,7 +48,7 @@ if has tests; then
 fi
 if has bench; then
   echo "[$(date +%T)] bench"
-  timeout -k 10 400 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" \
+  timeout -k 10 400 python -u bench.py $BENCH_ARGS > "$OUT/bench.json" 2> "$OUT/bench.err" \
       || { echo "bench failed"; tail -30 "$OUT/bench.err"; exit 1; }
   cat "$OUT/bench.json"
 fi
@@ -63,7 +64,7 @@ fi
 if has prof; then
   echo "[$(date +%T)] rocprofv3 kernel stats"
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
-      -- python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err" \
+      -- python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline $BENCH_ARGS > "$OUT/prof_bench.json" 2> "$OUT/prof.err" \
       || { echo "rocprof failed"; tail -30 "$OUT/prof.err"; exit 1; }
   ks=$(find "$OUT/prof" -name "*kernel_stats.csv" | head -1)
   if [ -n "$ks" ]; then python tools/profsum.py "$ks" 0 45 > "$OUT/prof_summary.txt"; cat "$OUT/prof_summary.txt"; fi
