@@ -293,7 +293,7 @@ class DeformableTransformerDecoder(nn.Module):
                 query_pos=None, src_padding_mask=None, query_padding_mask=None, disable_iterative_refine=False):
         level_T = _level_T(src_temporal_shapes)
         output = tgt
-        intermediate, intermediate_refs = [], []
+        intermediate, intermediate_refs, box_out = [], [], []
         for lid, layer in enumerate(self.layers):
             if reference_points.shape[-1] == 2:
                 ref_in = reference_points[:, :, None] * torch.stack([src_valid_ratios, src_valid_ratios], -1)[:, None]
@@ -303,6 +303,7 @@ class DeformableTransformerDecoder(nn.Module):
                            query_padding_mask)
             if not disable_iterative_refine and self.bbox_head is not None:
                 tmp = self.bbox_head[lid](output)
+                box_out.append(tmp)
                 if reference_points.shape[-1] == 2:
                     new_ref = (tmp + inverse_sigmoid(reference_points)).sigmoid()
                 else:
@@ -314,6 +315,11 @@ class DeformableTransformerDecoder(nn.Module):
                 intermediate.append(output)
                 intermediate_refs.append(reference_points)
         if self.return_intermediate:
+            # side results for PDVC's per-layer heads (pdvc.py _layer_heads): every layer's output as its own
+            # tensor (the heads read them directly, so no select of the stacked hs reaches the backward) and the
+            # refinement's bbox_head outputs -- the heads' bbox_head call on the same rows and weights (the
+            # reference evaluates it twice, deformable_transformer.py:305 and pdvc.py:192 / 253), reused instead
+            self.__dict__["_side"] = (intermediate, box_out if len(box_out) == len(self.layers) else None)
             return torch.stack(intermediate), torch.stack(intermediate_refs)
         return output, reference_points
 

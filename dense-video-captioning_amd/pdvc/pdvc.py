@@ -153,7 +153,10 @@ class PDVC(nn.Module):
         init_reference, tgt, reference_points, query_embed = tr.prepare_decoder_input_query(memory, query_embed)
         hs, inter_references = tr.forward_decoder(tgt, reference_points, memory, level_T, lsi, valid_ratios,
                                                   query_embed, kmask, proposals_mask, False)
-        classes, counts, coords = self._layer_heads(hs, init_reference, inter_references, False)
+        side = tr.decoder.__dict__.pop("_side", None)
+        if os.environ.get("PDVC_HEAD_SIDE", "1") == "0":  # A/B switch: heads on hs[l], box MLP evaluated again
+            side = None
+        classes, counts, coords = self._layer_heads(hs, init_reference, inter_references, False, side)
         return (memory, mask_flatten, temporal_shapes, lsi, valid_ratios, proposals_mask, hs, init_reference,
                 inter_references, torch.stack(classes), torch.stack(counts), torch.stack(coords))
 
@@ -213,15 +216,19 @@ class PDVC(nn.Module):
     def predict_event_num(self, counter, hs_lid):
         return counter(torch.max(hs_lid, dim=1, keepdim=False)[0])
 
-    def _layer_heads(self, hs, init_reference, inter_references, disable_refine):
+    def _layer_heads(self, hs, init_reference, inter_references, disable_refine, side=None):
+        """Class / count / box heads of every decoder layer (pdvc.py:184-192, 245-253).  side = (per-layer outputs, the
+        decoder's refinement bbox_head outputs or None) from DeformableTransformerDecoder.forward: the same values
+        as hs[l] and bbox_head[l](hs[l]), without the select's backward and the repeated box MLP."""
+        outs, boxes = side if side is not None else (None, None)
         classes, counts, coords = [], [], []
         for l_id in range(hs.shape[0]):
-            hs_l = hs[l_id]
+            hs_l = outs[l_id] if outs is not None else hs[l_id]
             reference = init_reference if l_id == 0 else inter_references[l_id - 1]
             ch = self.class_head[l_id]
             classes.append(dense(hs_l, ch.weight, ch.bias))  # 1-wide head: weight gradient as a column sum
             counts.append(self.predict_event_num(self.count_head[l_id], hs_l))
-            tmp = self.bbox_head[l_id](hs_l)
+            tmp = boxes[l_id] if (boxes is not None and not disable_refine) else self.bbox_head[l_id](hs_l)
             if disable_refine:
                 coords.append(reference)
             else:
