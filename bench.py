@@ -16,7 +16,9 @@ E=8 events of 9 words, with every GEMM on bf16 operands and fp32 accumulation (p
 carries dtype "bf16" and the GEMM roofline against the bf16 MFMA peak.  --workload yc2_newmodel measures
 BASELINE.json configs[3]: cfgs/yc2_newModel_sound.yml, NewModel = the dual-modality MHA front-end (T=512 clip
 and sound features, 768-d, 32 heads; csrc/seqattn.hip) in front of a 3+3-layer PDVC, E=8 events of 9 words,
-fp32.  The default (no flags) is the headline fp32 line.
+fp32.  --workload anet_c3d measures configs[4], the long-video stress config (cfgs/anet_c3d_pdvc.yml: T=1024,
+C=500 C3D features, Q=300 queries, 2+2 layers, 512 videos per GPU).  The default (no flags) is the headline fp32
+line.
 """
 import argparse
 import glob
@@ -46,6 +48,10 @@ WORKLOADS = {
                      metric="videos/sec fwd+bwd (PDVC, T=512 C=768 L=4 Q=100) at 1/2/4/8 MI355X"),
     "yc2_tsp_bf16": dict(cfg="cfgs/yc2_tsp_pdvc.yml", T=256, C=768, Q=100, events=8, words=9, precision="bf16",
                          metric="videos/sec fwd+bwd (PDVC yc2_tsp_pdvc, T=256 C=768 L=4 Q=100, bf16) on 1 MI355X"),
+    "anet_c3d": dict(cfg="cfgs/anet_c3d_pdvc.yml", T=1024, C=500, Q=300, events=4, words=13, precision="fp32",
+                     videos_per_gpu=512,
+                     metric="videos/sec fwd+bwd (PDVC anet_c3d_pdvc long-video stress, T=1024 C=500 L=4 Q=300) per "
+                            "MI355X, DDP"),
     "yc2_newmodel": dict(cfg="cfgs/yc2_newModel_sound.yml", T=512, C=768, Q=100, events=8, words=9,
                          precision="fp32", frontend=True, videos_per_gpu=512,
                          metric="videos/sec fwd+bwd (NewModel yc2_newModel_sound: MHA front-end + PDVC, T=512 "
@@ -58,11 +64,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--videos-per-gpu", type=int, default=None, help="default: 1024 (512 for yc2_newmodel)")
+    p.add_argument("--videos-per-gpu", type=int, default=None,
+                   help="default: 1024 (512 for yc2_newmodel and anet_c3d)")
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="anet_tsp",
                    help="anet_tsp: the metric's config (fp32, the reference's precision); yc2_tsp_bf16: "
                         "BASELINE.json configs[1] (T=256, bf16 GEMMs, pdvc/precision.py); yc2_newmodel: configs[3] "
-                        "(MHA front-end + 3+3-layer PDVC, T=512)")
+                        "(MHA front-end + 3+3-layer PDVC, T=512); anet_c3d: configs[4] (T=1024, C=500, Q=300)")
     for k in ("T", "C", "Q", "events", "words"):
         p.add_argument(f"--{k}", type=int, default=None, help="override the workload's value")
     p.add_argument("--cfg", default=None)

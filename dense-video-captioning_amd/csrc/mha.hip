@@ -14,6 +14,7 @@
 // dK = dS^T q_scaled and dV = P_d^T dO.
 // Dropout keeps a counter-hash mask of (seed, video, head, query, key) -- regenerated in the backward.
 #include "pdvc_common.h"
+#include "seqattn.h"
 
 #include <cstdlib>
 
@@ -21,18 +22,6 @@ namespace pdvc {
 
 constexpr int kHD = 64;      // max head dim (PDVC: 512 / 8 = 64); lanes >= D idle in channel phases
 constexpr int kMaxQ = 300;   // LDS budget: 2 * Q * (D+1) floats + row buffers <= 160 KiB
-
-__device__ __forceinline__ uint32_t mix32(uint32_t x) {
-    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
-    return x;
-}
-
-__device__ __forceinline__ bool keep_elem(uint64_t seed, uint32_t head_idx, uint32_t q, uint32_t k, uint32_t Q,
-                                          uint32_t thresh) {
-    const uint32_t idx = (head_idx * Q + q) * Q + k;
-    const uint32_t h = mix32(mix32(idx ^ (uint32_t)seed) + (uint32_t)(seed >> 32) * 0x9e3779b9U);
-    return (h >> 8) >= thresh;  // keep with probability 1 - p (24-bit uniform)
-}
 
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
@@ -48,10 +37,6 @@ __device__ __forceinline__ float wave_add(float v) {
 constexpr int kKPL = (kMaxQ + 63) / 64;  // keys per lane
 
 constexpr int kQB = 16;  // queries (forward / backward phase A) or keys (phase B) per workgroup
-
-__device__ __forceinline__ uint64_t load_seed(uint64_t seed, const uint64_t* seed_dev) {
-    return seed_dev ? *seed_dev : seed;
-}
 
 __global__ __launch_bounds__(256) void mha_fwd_kernel(const float* __restrict__ qk, const float* __restrict__ v,
                                                       const uint8_t* __restrict__ kpm, int Q, int M, int D, float scaling,
@@ -558,12 +543,6 @@ __global__ __launch_bounds__(256) void mha_bwd_mfma_kernel(const float* __restri
     }
 }
 
-static uint32_t drop_threshold(float p) {
-    double t = (double)p * 16777216.0;
-    if (t < 0) t = 0;
-    if (t > 16777216.0) t = 16777216.0;
-    return (uint32_t)t;
-}
 
 }  // namespace pdvc
 
@@ -580,6 +559,14 @@ static_assert(kBwdMfmaLds <= 160 * 1024, "backward LDS budget");
 // matrix-core kernels for D == 64, Q <= 128 (PDVC_MHA_MFMA=0 selects the scalar kernels, for tests)
 static bool use_mfma(int Q, int D) {
     if (D != 64 || Q > kMQ) return false;
+    const char* e = getenv("PDVC_MHA_MFMA");
+    return !(e && e[0] == '0');
+}
+
+// longer query sets (anet_c3d: Q = 300): the flash-style MFMA kernels of seqattn.hip with this op's key padding
+// mask, dropout mask and scaling (PDVC_MHA_MFMA=0 selects the scalar kernels here too)
+static bool use_flash(int Q, int D) {
+    if (Q <= kMQ || !sq_head_dim_ok(D)) return false;
     const char* e = getenv("PDVC_MHA_MFMA");
     return !(e && e[0] == '0');
 }
@@ -613,6 +600,11 @@ extern "C" int pdvc_mha_forward_f32(const float* qk, const float* v, const uint8
     int rc = mha_attrs();
     if (rc) return rc;
     const float scaling = sqrtf(1.0f / (float)head_dim);
+    if (use_flash(num_query, head_dim)) {
+        const long E = (long)num_heads * head_dim;
+        return sq_forward(qk, 2 * E, qk + E, 2 * E, v, E, batch, num_query, num_query, num_heads, head_dim, scaling,
+                          key_padding_mask, dropout_p, seed, seed_dev, out, lse, (hipStream_t)stream);
+    }
     if (use_mfma(num_query, head_dim)) {
         hipLaunchKernelGGL(mha_fwd_mfma_kernel, dim3((unsigned)((long)batch * num_heads)), dim3(256), kFwdMfmaLds,
                            (hipStream_t)stream, qk, v, key_padding_mask, num_query, num_heads, scaling, dropout_p,
@@ -635,13 +627,19 @@ extern "C" int pdvc_mha_backward_f32(const float* qk, const float* v, const uint
     PDVC_CHECK_ARG(head_dim > 0 && head_dim <= kHD, "query self-attention kernel needs head_dim <= %d, got %d", kHD,
                    head_dim);
     PDVC_CHECK_ARG(num_query > 0 && num_query <= kMaxQ, "num_query must be in [1,%d], got %d", kMaxQ, num_query);
-    PDVC_CHECK_ARG(workspace != nullptr, "workspace (2*N*M*Q*Q floats) is required");
+    PDVC_CHECK_ARG(workspace != nullptr, "workspace (pdvc_mha_workspace_floats) is required");
     const int chunks = (num_query + kQB - 1) / kQB;
     const long nm = (long)batch * num_heads;
     if (nm == 0) return PDVC_OK;
     int rc = mha_attrs();
     if (rc) return rc;
     const float scaling = sqrtf(1.0f / (float)head_dim);
+    if (use_flash(num_query, head_dim)) {
+        const long E = (long)num_heads * head_dim;
+        return sq_backward(qk, 2 * E, qk + E, 2 * E, v, E, out, grad_out, lse, batch, num_query, num_query, num_heads,
+                           head_dim, scaling, key_padding_mask, dropout_p, seed, seed_dev, workspace, grad_qk, 2 * E,
+                           grad_qk + E, 2 * E, grad_v, E, (hipStream_t)stream);
+    }
     float* ws_p = workspace;
     float* ws_ds = workspace + (size_t)nm * num_query * num_query;
     hipStream_t s = (hipStream_t)stream;
@@ -660,4 +658,10 @@ extern "C" int pdvc_mha_backward_f32(const float* qk, const float* v, const uint
                        qk, grad_out, num_query, num_heads, head_dim, scaling, chunks, ws_p, ws_ds, grad_qk, grad_v);
     PDVC_CHECK_LAUNCH("mha_bwd_k_kernel");
     return PDVC_OK;
+}
+
+extern "C" long pdvc_mha_workspace_floats(int batch, int num_query, int num_heads, int head_dim) {
+    const long nmq = (long)batch * num_heads * num_query;
+    if (use_flash(num_query, head_dim)) return nmq;  // delta rows only
+    return 2 * nmq * num_query;                      // P_d and dS tiles of the scalar / single-workgroup kernels
 }

@@ -141,6 +141,32 @@ struct Levels {
     int start[PDVC_MAX_LEVELS];
 };
 
+// Attention dropout mask (mha.hip, seqattn.hip): a counter hash of (seed, video*head, query, key), regenerated in
+// the backward; keep with probability 1 - p (24-bit uniform against thresh = p * 2^24).
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+
+__device__ __forceinline__ bool keep_elem(uint64_t seed, uint32_t head_idx, uint32_t q, uint32_t k, uint32_t Q,
+                                          uint32_t thresh) {
+    const uint32_t idx = (head_idx * Q + q) * Q + k;
+    const uint32_t h = mix32(mix32(idx ^ (uint32_t)seed) + (uint32_t)(seed >> 32) * 0x9e3779b9U);
+    return (h >> 8) >= thresh;
+}
+
+// the dropout seed from device memory (drawn inside a captured graph) or the host value
+__device__ __forceinline__ uint64_t load_seed(uint64_t seed, const uint64_t* seed_dev) {
+    return seed_dev ? *seed_dev : seed;
+}
+
+static inline uint32_t drop_threshold(float p) {
+    double t = (double)p * 16777216.0;
+    if (t < 0) t = 0;
+    if (t > 16777216.0) t = 16777216.0;
+    return (uint32_t)t;
+}
+
 // Zero-fill as a kernel (vector stores).  hipMemsetAsync captured into a hipGraph did not re-zero its buffer
 // on replays after the first (tools/diag_refgrad.py: the decoder's atomically accumulated grad_ref kept the
 // previous replay's contents); a kernel node replays like every other launch.

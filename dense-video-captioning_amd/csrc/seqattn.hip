@@ -30,6 +30,7 @@
 #include <math.h>
 
 #include "pdvc_common.h"
+#include "seqattn.h"
 
 namespace pdvc {
 
@@ -134,29 +135,72 @@ __device__ __forceinline__ void sq_block(int nblocks_own, int& nh, int& ob) {
     ob = lb - nh * nblocks_own;
 }
 
+// Options of the decoder self-attention route (mha.hip, Q > 128): a key padding mask and dropout on the
+// probabilities with mha.hip's counter-hash mask, keep_elem(seed, video*head, query, key, Q), so every route of
+// pdvc_mha_* drops the same elements.  The front-end instantiates neither.
+struct SqOpts {
+    const uint8_t* kpm;  // (N, Tk) nonzero = padded key (KPM)
+    uint64_t seed0;
+    const uint64_t* seed_dev;
+    uint32_t thresh;     // drop_threshold(p) (DROP)
+    float keep_scale;    // 1 / (1 - p)
+};
+
+// per-tile additive key bias (0, or -inf at padded keys and keys >= Tk), staged with the K / V tile (KPM)
+struct SqKeyBias {
+    float b = 0.f;
+    __device__ __forceinline__ void load(const uint8_t* kpm_row, int r0, int nrows, int tid) {
+        if (tid < kSqKT) {
+            const int j = r0 + tid;
+            b = (j < nrows && !kpm_row[j]) ? 0.f : -INFINITY;
+        }
+    }
+    __device__ __forceinline__ void store(float* dst, int tid) const {
+        if (tid < kSqKT) dst[tid] = b;
+    }
+};
+
+// bias of the 16 keys a lane's score registers hold in 32-key block sb of a tile: rows sb*32 + crow(r, hi)
+__device__ __forceinline__ void sq_add_bias(sq_f32x16& s, const float* bias, int sb, int hi) {
+    const float4* B4 = reinterpret_cast<const float4*>(bias + sb * 32 + 4 * hi);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const float4 b = B4[2 * g];
+        s[4 * g] += b.x;
+        s[4 * g + 1] += b.y;
+        s[4 * g + 2] += b.z;
+        s[4 * g + 3] += b.w;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // forward: wave = 32 queries; per 64-key tile S^T = K . Q^T (two independent 32-key MFMA chains), one online
 // softmax update over the key registers, O^T += V^T . P^T.  Measured alternatives (tools/seqattn_bench.py, T=512,
 // 32 heads of 24, 64 videos; this kernel 0.62 ms = 83 TFLOP/s): two 32-query blocks per wave sharing the K / V
 // operand reads 75-85; a one-tile software pipeline (next tile's score MFMAs before this tile's softmax, two named
 // score states, 240 VGPRs) 69; 128-key tiles 65; s_setprio around the MFMA runs, sched_group_barrier
-// interleaves and skipping the identity rescale when no row max moved: within noise.  The workgroup is 8 waves (256 queries, 2 per (video, head) at T = 512) held to 4
-// waves per SIMD (<= 128 VGPRs).
-template <int D>
+// interleaves and skipping the identity rescale when no row max moved: within noise.  The workgroup is 8 waves
+// (256 queries, 2 per (video, head) at T = 512) held to 4 waves per SIMD (<= 128 VGPRs).
+// DROP: the denominator sums the undropped p (so no ones-column trick), P.V takes the dropped, rescaled p.
+template <int D, bool DROP, bool KPM>
 __global__ __launch_bounds__(kSqThreads) __attribute__((amdgpu_waves_per_eu(4))) void seqattn_fwd_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v, int H, int Tq, int Tk,
-    long ldq, long ldk, long ldv, float qmul, int qblocks, float* __restrict__ out, float* __restrict__ lse) {
+    long ldq, long ldk, long ldv, float qmul, int qblocks, SqOpts opt, float* __restrict__ out,
+    float* __restrict__ lse) {
     using C = SqCfg<D>;
+    constexpr bool ONES = C::ONES && !DROP;
     constexpr int SB = kSqKT / 32;          // 32-key score blocks per tile
     constexpr int TL = C::NT - 1;           // output tile holding channel row D (ONES)
     constexpr int RL = (D - 32 * TL) / 2;   // its accumulator register in the lanes l/32 = 0
     __shared__ __attribute__((aligned(16))) float smem[C::SMEM];  // [buf][K, V]
+    __shared__ __attribute__((aligned(16))) float kbias[KPM ? 2 : 1][KPM ? kSqKT : 4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, hi = lane >> 5;
     int nh, qb;
     sq_block(qblocks, nh, qb);
     const int n = nh / H, h = nh - n * H;
     const int qi = qb * kSqOwn + w * 32 + l32;
     const bool qok = qi < Tq;
+    const uint64_t seed = DROP ? load_seed(opt.seed0, opt.seed_dev) : 0;
     float qr[C::DH];
     {
         const float* qp = q + ((long)n * Tq + (qok ? qi : 0)) * ldq + h * D + hi * C::DH;
@@ -165,12 +209,16 @@ __global__ __launch_bounds__(kSqThreads) __attribute__((amdgpu_waves_per_eu(4)))
     }
     const float* kh = k + (long)n * Tk * ldk + h * D;
     const float* vh = v + (long)n * Tk * ldv + h * D;
-    if (C::ONES)
+    const uint8_t* kpm_row = KPM ? opt.kpm + (long)n * Tk : nullptr;
+    if (ONES)
         for (int r = tid; r < 2 * kSqKT; r += kSqThreads)
             smem[(r / kSqKT) * 2 * C::TILE + C::TILE + (r % kSqKT) * C::LD + D] = 1.f;
     SqStager<D> st(tid);
+    SqKeyBias kb;
     st.load(kh, ldk, vh, ldv, 0, Tk);
+    if (KPM) kb.load(kpm_row, 0, Tk, tid);
     st.store(smem, smem + C::TILE);
+    if (KPM) kb.store(kbias[0], tid);
     __syncthreads();
     sq_f32x16 o[C::NT];
 #pragma unroll
@@ -178,10 +226,13 @@ __global__ __launch_bounds__(kSqThreads) __attribute__((amdgpu_waves_per_eu(4)))
     float m = -INFINITY, l = 0.f;
     const int ntiles = (Tk + kSqKT - 1) / kSqKT;
     for (int it = 0; it < ntiles; ++it) {
-        const int t0 = it * kSqKT;
-        const float* Ks = smem + (it & 1) * 2 * C::TILE;
+        const int t0 = it * kSqKT, buf = it & 1;
+        const float* Ks = smem + buf * 2 * C::TILE;
         const float* Vs = Ks + C::TILE;
-        if (it + 1 < ntiles) st.load(kh, ldk, vh, ldv, t0 + kSqKT, Tk);
+        if (it + 1 < ntiles) {
+            st.load(kh, ldk, vh, ldv, t0 + kSqKT, Tk);
+            if (KPM) kb.load(kpm_row, t0 + kSqKT, Tk, tid);
+        }
         // the tile's 32-key score blocks (independent MFMA chains), one softmax update over the whole tile
         sq_f32x16 s[SB];
         {
@@ -195,7 +246,10 @@ __global__ __launch_bounds__(kSqThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
                 for (int sb = 0; sb < SB; ++sb) s[sb] = sq_mfma(kc[sb][kk], qr[kk], s[sb]);
         }
-        if (t0 + kSqKT > Tk) {
+        if (KPM) {
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) sq_add_bias(s[sb], kbias[buf], sb, hi);
+        } else if (t0 + kSqKT > Tk) {
 #pragma unroll
             for (int sb = 0; sb < SB; ++sb)
 #pragma unroll
@@ -215,17 +269,27 @@ __global__ __launch_bounds__(kSqThreads) __attribute__((amdgpu_waves_per_eu(4)))
         for (int sb = 0; sb < SB; ++sb)
 #pragma unroll
             for (int r = 0; r < 16; ++r) s[sb][r] = sq_exp2(s[sb][r] - mn);
-        if (!C::ONES) {
+        if (!ONES) {
             l *= corr;
 #pragma unroll
             for (int sb = 0; sb < SB; ++sb)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) l += s[sb][r];
         }
+        if (DROP) {
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const uint32_t key = (uint32_t)(t0 + sb * 32 + sq_crow(r, hi));
+                    s[sb][r] = keep_elem(seed, (uint32_t)nh, (uint32_t)qi, key, (uint32_t)Tq, opt.thresh)
+                                   ? s[sb][r] * opt.keep_scale : 0.f;
+                }
+        }
 #pragma unroll
         for (int t = 0; t < C::NT; ++t)
 #pragma unroll
-            for (int r = 0; r < C::valid(t) + (C::ONES && t == TL ? 1 : 0); ++r) o[t][r] *= corr;
+            for (int r = 0; r < C::valid(t) + (ONES && t == TL ? 1 : 0); ++r) o[t][r] *= corr;
 #pragma unroll
         for (int sb = 0; sb < SB; ++sb)
 #pragma unroll
@@ -234,10 +298,13 @@ __global__ __launch_bounds__(kSqThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
                 for (int t = 0; t < C::NT; ++t) o[t] = sq_mfma(vc[32 * t], s[sb][r], o[t]);
             }
-        if (it + 1 < ntiles) st.store(smem + ((it + 1) & 1) * 2 * C::TILE, smem + ((it + 1) & 1) * 2 * C::TILE + C::TILE);
+        if (it + 1 < ntiles) {
+            st.store(smem + (buf ^ 1) * 2 * C::TILE, smem + (buf ^ 1) * 2 * C::TILE + C::TILE);
+            if (KPM) kb.store(kbias[buf ^ 1], tid);
+        }
         __syncthreads();
     }
-    if (C::ONES) {  // channel row D = sum_j p_j, held by the lanes l/32 = 0
+    if (ONES) {  // channel row D = sum_j p_j, held by the lanes l/32 = 0
         const float own = o[TL][RL], other = sq_swap32(own);
         l = hi ? other : own;
     } else {
@@ -258,17 +325,17 @@ __global__ __launch_bounds__(kSqThreads) __attribute__((amdgpu_waves_per_eu(4)))
 
 // ---------------------------------------------------------------------------------------------------------------
 // backward, query owner: S^T = K . Q^T, dP^T = V . dO^T, dS^T = P^T (dP^T - delta), dQ^T += K^T . dS^T.
-// Publishes delta_i = dout_i . out_i for the key-owner kernel.
-template <int D>
-__global__ __launch_bounds__(kSqThreads) void seqattn_bwd_dq_kernel(const float* __restrict__ q, const float* __restrict__ k,
-                                                             const float* __restrict__ v, const float* __restrict__ dout,
-                                                             const float* __restrict__ lse,
-                                                             const float* __restrict__ out, float* __restrict__ delta,
-                                                             int H, int Tq, int Tk, long ldq, long ldk, long ldv,
-                                                             float qmul, float scale, int qblocks,
-                                                             float* __restrict__ dq, long lddq) {
+// Publishes delta_i = dout_i . out_i for the key-owner kernel.  DROP: dP = dP_d * keep / (1 - p) (delta is
+// unchanged: sum_j p_ij dP_ij = dout_i . out_i with out the dropped product).
+template <int D, bool DROP, bool KPM>
+__global__ __launch_bounds__(kSqThreads) void seqattn_bwd_dq_kernel(
+    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
+    const float* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ out,
+    float* __restrict__ delta, int H, int Tq, int Tk, long ldq, long ldk, long ldv, float qmul, float scale,
+    int qblocks, SqOpts opt, float* __restrict__ dq, long lddq) {
     using C = SqCfg<D>;
     __shared__ __attribute__((aligned(16))) float smem[C::SMEM];  // [buf][K, V]
+    __shared__ __attribute__((aligned(16))) float kbias[KPM ? 2 : 1][KPM ? kSqKT : 4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, hi = lane >> 5;
     int nh, qb;
     sq_block(qblocks, nh, qb);
@@ -276,6 +343,7 @@ __global__ __launch_bounds__(kSqThreads) void seqattn_bwd_dq_kernel(const float*
     const int E = H * D;
     const int qi = qb * kSqOwn + w * 32 + l32;
     const bool qok = qi < Tq;
+    const uint64_t seed = DROP ? load_seed(opt.seed0, opt.seed_dev) : 0;
     float qr[C::DH], gr[C::DH];
     float dl = 0.f, l2 = 0.f;
     {
@@ -297,19 +365,26 @@ __global__ __launch_bounds__(kSqThreads) void seqattn_bwd_dq_kernel(const float*
     }
     const float* kh = k + (long)n * Tk * ldk + h * D;
     const float* vh = v + (long)n * Tk * ldv + h * D;
+    const uint8_t* kpm_row = KPM ? opt.kpm + (long)n * Tk : nullptr;
     SqStager<D> st(tid);
+    SqKeyBias kb;
     st.load(kh, ldk, vh, ldv, 0, Tk);
+    if (KPM) kb.load(kpm_row, 0, Tk, tid);
     st.store(smem, smem + C::TILE);
+    if (KPM) kb.store(kbias[0], tid);
     __syncthreads();
     sq_f32x16 acc[C::NT];
 #pragma unroll
     for (int t = 0; t < C::NT; ++t) acc[t] = sq_f32x16{};
     const int ntiles = (Tk + kSqKT - 1) / kSqKT;
     for (int it = 0; it < ntiles; ++it) {
-        const int t0 = it * kSqKT;
-        const float* Ks = smem + (it & 1) * 2 * C::TILE;
+        const int t0 = it * kSqKT, buf = it & 1;
+        const float* Ks = smem + buf * 2 * C::TILE;
         const float* Vs = Ks + C::TILE;
-        if (it + 1 < ntiles) st.load(kh, ldk, vh, ldv, t0 + kSqKT, Tk);
+        if (it + 1 < ntiles) {
+            st.load(kh, ldk, vh, ldv, t0 + kSqKT, Tk);
+            if (KPM) kb.load(kpm_row, t0 + kSqKT, Tk, tid);
+        }
 #pragma unroll
         for (int sb = 0; sb < kSqKT / 32; ++sb) {
             if (t0 + sb * 32 >= Tk) break;  // keys past Tk inside a sub-block are zero rows: ds * 0 adds nothing
@@ -322,8 +397,17 @@ __global__ __launch_bounds__(kSqThreads) void seqattn_bwd_dq_kernel(const float*
                 s = sq_mfma(kc[kk], qr[kk], s);
                 dp = sq_mfma(vc[kk], gr[kk], dp);
             }
+            if (KPM) sq_add_bias(s, kbias[buf], sb, hi);
 #pragma unroll
-            for (int r = 0; r < 16; ++r) s[r] = sq_exp2(s[r] - l2) * (dp[r] - dl);
+            for (int r = 0; r < 16; ++r) {
+                float d = dp[r];
+                if (DROP) {
+                    const uint32_t key = (uint32_t)(t0 + sb * 32 + sq_crow(r, hi));
+                    d = keep_elem(seed, (uint32_t)nh, (uint32_t)qi, key, (uint32_t)Tq, opt.thresh) ? d * opt.keep_scale
+                                                                                                 : 0.f;
+                }
+                s[r] = sq_exp2(s[r] - l2) * (d - dl);
+            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const float* kcol = Ks + (sb * 32 + sq_crow(r, hi)) * C::LD + l32;
@@ -331,7 +415,10 @@ __global__ __launch_bounds__(kSqThreads) void seqattn_bwd_dq_kernel(const float*
                 for (int t = 0; t < C::NT; ++t) acc[t] = sq_mfma(kcol[32 * t], s[r], acc[t]);
             }
         }
-        if (it + 1 < ntiles) st.store(smem + ((it + 1) & 1) * 2 * C::TILE, smem + ((it + 1) & 1) * 2 * C::TILE + C::TILE);
+        if (it + 1 < ntiles) {
+            st.store(smem + (buf ^ 1) * 2 * C::TILE, smem + (buf ^ 1) * 2 * C::TILE + C::TILE);
+            if (KPM) kb.store(kbias[buf ^ 1], tid);
+        }
         __syncthreads();
     }
     if (qok) {
@@ -344,16 +431,13 @@ __global__ __launch_bounds__(kSqThreads) void seqattn_bwd_dq_kernel(const float*
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// backward, key owner: S = Q . K^T, dP = dO . V^T (key index on the lanes), dV^T += dO^T . P, dK^T += Q^T . dS.
-template <int D>
-__global__ __launch_bounds__(kSqThreads) void seqattn_bwd_dkv_kernel(const float* __restrict__ q, const float* __restrict__ k,
-                                                              const float* __restrict__ v,
-                                                              const float* __restrict__ dout,
-                                                              const float* __restrict__ lse,
-                                                              const float* __restrict__ delta, int H, int Tq, int Tk,
-                                                              long ldq, long ldk, long ldv, float kmul, float scale,
-                                                              int kblocks, float* __restrict__ dk, long lddk,
-                                                              float* __restrict__ dv, long lddv) {
+// backward, key owner: S = Q . K^T, dP = dO . V^T (key index on the lanes), dV^T += dO^T . P_d, dK^T += Q^T . dS.
+template <int D, bool DROP, bool KPM>
+__global__ __launch_bounds__(kSqThreads) void seqattn_bwd_dkv_kernel(
+    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
+    const float* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta, int H, int Tq,
+    int Tk, long ldq, long ldk, long ldv, float kmul, float scale, int kblocks, SqOpts opt, float* __restrict__ dk,
+    long lddk, float* __restrict__ dv, long lddv) {
     using C = SqCfg<D>;
     __shared__ __attribute__((aligned(16))) float smem[C::SMEM];  // [buf][Q, dO]
     __shared__ __attribute__((aligned(16))) float rowst[2][2][kSqKT];   // [buf][lse2, delta]
@@ -364,6 +448,9 @@ __global__ __launch_bounds__(kSqThreads) void seqattn_bwd_dkv_kernel(const float
     const int E = H * D;
     const int kj = kb * kSqOwn + w * 32 + l32;
     const bool kok = kj < Tk;
+    const uint64_t seed = DROP ? load_seed(opt.seed0, opt.seed_dev) : 0;
+    // this lane's key: padded -> every p of it is 0
+    const float kbias = (KPM && kok && opt.kpm[(long)n * Tk + kj]) ? -INFINITY : 0.f;
     float kr[C::DH], vr[C::DH];
     {
         const long krow = (long)n * Tk + (kok ? kj : 0);
@@ -433,8 +520,16 @@ __global__ __launch_bounds__(kSqThreads) void seqattn_bwd_dkv_kernel(const float
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int r = 4 * g + j;
-                    s[r] = sq_exp2(s[r] - lr[j]);
-                    dp[r] = s[r] * (dp[r] - dr[j]);
+                    const float p = sq_exp2(s[r] - lr[j] + kbias);
+                    float d = dp[r], pd = p;
+                    if (DROP) {
+                        const uint32_t qq = (uint32_t)(t0 + sb * 32 + sq_crow(r, hi));
+                        const bool keep = keep_elem(seed, (uint32_t)nh, qq, (uint32_t)kj, (uint32_t)Tq, opt.thresh);
+                        d = keep ? d * opt.keep_scale : 0.f;
+                        pd = keep ? p * opt.keep_scale : 0.f;
+                    }
+                    s[r] = pd;
+                    dp[r] = p * (d - dr[j]);
                 }
             }
 #pragma unroll
@@ -476,49 +571,75 @@ __global__ __launch_bounds__(kSqThreads) void seqattn_bwd_dkv_kernel(const float
         default: break;            \
     }
 
-static bool sq_head_dim_ok(int D) { return D == 16 || D == 24 || D == 32 || D == 48 || D == 64; }
+bool sq_head_dim_ok(int D) { return D == 16 || D == 24 || D == 32 || D == 48 || D == 64; }
 
-}  // namespace pdvc
+template <bool DROP, bool KPM>
+static void sq_launch_fwd(dim3 grid, hipStream_t s, const float* q, long ldq, const float* k, long ldk,
+                          const float* v, long ldv, int batch, int num_query, int num_key, int num_heads,
+                          int head_dim, float qmul, int qblocks, const SqOpts& o, float* out, float* lse) {
+#define PDVC_SQ_FWD(DD)                                                                                          \
+    hipLaunchKernelGGL((seqattn_fwd_kernel<DD, DROP, KPM>), grid, dim3(kSqThreads), 0, s, q, k, v, num_heads,    \
+                       num_query, num_key, ldq, ldk, ldv, qmul, qblocks, o, out, lse)
+    PDVC_SQ_DISPATCH(head_dim, PDVC_SQ_FWD)
+#undef PDVC_SQ_FWD
+}
 
-using namespace pdvc;
+template <bool DROP, bool KPM>
+static void sq_launch_bwd(dim3 gq, dim3 gk, hipStream_t s, const float* q, long ldq, const float* k, long ldk,
+                          const float* v, long ldv, const float* out, const float* grad_out, const float* lse,
+                          int num_query, int num_key, int num_heads, int head_dim, float qmul, float scale,
+                          int qblocks, int kblocks, const SqOpts& o, float* delta, float* grad_q, long ld_grad_q,
+                          float* grad_k, long ld_grad_k, float* grad_v, long ld_grad_v) {
+#define PDVC_SQ_DQ(DD)                                                                                               \
+    hipLaunchKernelGGL((seqattn_bwd_dq_kernel<DD, DROP, KPM>), gq, dim3(kSqThreads), 0, s, q, k, v, grad_out, lse,  \
+                       out, delta, num_heads, num_query, num_key, ldq, ldk, ldv, qmul, scale, qblocks, o, grad_q,    \
+                       ld_grad_q)
+#define PDVC_SQ_DKV(DD)                                                                                              \
+    hipLaunchKernelGGL((seqattn_bwd_dkv_kernel<DD, DROP, KPM>), gk, dim3(kSqThreads), 0, s, q, k, v, grad_out, lse, \
+                       delta, num_heads, num_query, num_key, ldq, ldk, ldv, qmul, scale, kblocks, o, grad_k,         \
+                       ld_grad_k, grad_v, ld_grad_v)
+    PDVC_SQ_DISPATCH(head_dim, PDVC_SQ_DQ)
+    PDVC_SQ_DISPATCH(head_dim, PDVC_SQ_DKV)
+#undef PDVC_SQ_DQ
+#undef PDVC_SQ_DKV
+}
 
-extern "C" int pdvc_seq_attention_forward_f32(const float* q, long ldq, const float* k, long ldk, const float* v,
-                                              long ldv, int batch, int num_query, int num_key, int num_heads,
-                                              int head_dim, float* out, float* lse, void* stream) {
-    PDVC_CHECK_ARG(batch >= 0 && num_query >= 0 && num_key > 0 && num_heads > 0, "invalid sizes");
-    PDVC_CHECK_ARG(sq_head_dim_ok(head_dim), "head_dim must be 16, 24, 32, 48 or 64, got %d", head_dim);
-    const long E = (long)num_heads * head_dim;
-    PDVC_CHECK_ARG(ldq >= E && ldk >= E && ldv >= E, "row strides must be >= num_heads * head_dim");
-    if (batch == 0 || num_query == 0) return PDVC_OK;
-    const long blocks = (long)((num_query + kSqOwn - 1) / kSqOwn) * batch * num_heads;
+// Shared by the C ABI below and mha.hip's route for long query sets: scale multiplies q . k (the caller's
+// convention: 1/sqrt(D) here, sqrt(1/D) there); kpm / dropout as SqOpts.  Arguments validated by the callers.
+int sq_forward(const float* q, long ldq, const float* k, long ldk, const float* v, long ldv, int batch,
+               int num_query, int num_key, int num_heads, int head_dim, float scale, const uint8_t* kpm,
+               float dropout_p, uint64_t seed, const uint64_t* seed_dev, float* out, float* lse, hipStream_t s) {
+    const int qblocks = (num_query + kSqOwn - 1) / kSqOwn;
+    const long blocks = (long)qblocks * batch * num_heads;
     PDVC_CHECK_ARG(blocks < (1L << 31), "too many (video, head, query block) workgroups");
     PDVC_CHECK_ARG((long)num_key * ldk < (1L << 31) && (long)num_key * ldv < (1L << 31),
                    "one video's keys must span < 2^31 floats");
-    const float scale = 1.f / sqrtf((float)head_dim);
-    const int qblocks = (num_query + kSqOwn - 1) / kSqOwn;
-    hipStream_t s = (hipStream_t)stream;
-#define PDVC_SQ_FWD(DD)                                                                                          \
-    hipLaunchKernelGGL((seqattn_fwd_kernel<DD>), dim3((unsigned)blocks), dim3(kSqThreads), 0, s, q, k, v, num_heads,    \
-                       num_query, num_key, ldq, ldk, ldv, scale * kLog2e, qblocks, out, lse)
-    PDVC_SQ_DISPATCH(head_dim, PDVC_SQ_FWD)
-#undef PDVC_SQ_FWD
+    const SqOpts o{kpm, seed, seed_dev, drop_threshold(dropout_p), dropout_p > 0.f ? 1.f / (1.f - dropout_p) : 1.f};
+    const dim3 grid((unsigned)blocks);
+    const float qmul = scale * kLog2e;
+    const bool drop = dropout_p > 0.f;
+    if (drop && kpm)
+        sq_launch_fwd<true, true>(grid, s, q, ldq, k, ldk, v, ldv, batch, num_query, num_key, num_heads, head_dim,
+                                  qmul, qblocks, o, out, lse);
+    else if (drop)
+        sq_launch_fwd<true, false>(grid, s, q, ldq, k, ldk, v, ldv, batch, num_query, num_key, num_heads, head_dim,
+                                   qmul, qblocks, o, out, lse);
+    else if (kpm)
+        sq_launch_fwd<false, true>(grid, s, q, ldq, k, ldk, v, ldv, batch, num_query, num_key, num_heads, head_dim,
+                                   qmul, qblocks, o, out, lse);
+    else
+        sq_launch_fwd<false, false>(grid, s, q, ldq, k, ldk, v, ldv, batch, num_query, num_key, num_heads, head_dim,
+                                    qmul, qblocks, o, out, lse);
     PDVC_CHECK_LAUNCH("seqattn_fwd_kernel");
     return PDVC_OK;
 }
 
-extern "C" int pdvc_seq_attention_backward_f32(const float* q, long ldq, const float* k, long ldk, const float* v,
-                                               long ldv, const float* out, const float* grad_out, const float* lse,
-                                               int batch, int num_query, int num_key, int num_heads, int head_dim,
-                                               float* workspace, float* grad_q, long ld_grad_q, float* grad_k,
-                                               long ld_grad_k, float* grad_v, long ld_grad_v, void* stream) {
-    PDVC_CHECK_ARG(batch >= 0 && num_query >= 0 && num_key > 0 && num_heads > 0, "invalid sizes");
-    PDVC_CHECK_ARG(sq_head_dim_ok(head_dim), "head_dim must be 16, 24, 32, 48 or 64, got %d", head_dim);
+int sq_backward(const float* q, long ldq, const float* k, long ldk, const float* v, long ldv, const float* out,
+                const float* grad_out, const float* lse, int batch, int num_query, int num_key, int num_heads,
+                int head_dim, float scale, const uint8_t* kpm, float dropout_p, uint64_t seed,
+                const uint64_t* seed_dev, float* workspace, float* grad_q, long ld_grad_q, float* grad_k,
+                long ld_grad_k, float* grad_v, long ld_grad_v, hipStream_t s) {
     const long E = (long)num_heads * head_dim;
-    PDVC_CHECK_ARG(ldq >= E && ldk >= E && ldv >= E && ld_grad_q >= E && ld_grad_k >= E && ld_grad_v >= E,
-                   "row strides must be >= num_heads * head_dim");
-    if (batch == 0) return PDVC_OK;
-    hipStream_t s = (hipStream_t)stream;
-    const float scale = 1.f / sqrtf((float)head_dim);
     if (num_query == 0) {  // no query: the key and value gradients are zero
         hipError_t e1 = hipMemset2DAsync(grad_k, sizeof(float) * ld_grad_k, 0, sizeof(float) * E,
                                          (size_t)batch * num_key, s);
@@ -533,20 +654,51 @@ extern "C" int pdvc_seq_attention_backward_f32(const float* q, long ldq, const f
     PDVC_CHECK_ARG((long)num_query * ldq < (1L << 31) && (long)num_query * E < (1L << 31) &&
                        (long)num_key * ldk < (1L << 31) && (long)num_key * ldv < (1L << 31),
                    "one video's rows must span < 2^31 floats");
+    const SqOpts o{kpm, seed, seed_dev, drop_threshold(dropout_p), dropout_p > 0.f ? 1.f / (1.f - dropout_p) : 1.f};
     float* delta = workspace;  // (N, H, Tq): written by the dq kernel, read by the dk/dv kernel
-#define PDVC_SQ_DQ(DD)                                                                                             \
-    hipLaunchKernelGGL((seqattn_bwd_dq_kernel<DD>), dim3((unsigned)gq), dim3(kSqThreads), 0, s, q, k, v, grad_out, lse, \
-                       out, delta, num_heads, num_query, num_key, ldq, ldk, ldv, scale * kLog2e, scale, qblocks,    \
-                       grad_q, ld_grad_q)
-#define PDVC_SQ_DKV(DD)                                                                                             \
-    hipLaunchKernelGGL((seqattn_bwd_dkv_kernel<DD>), dim3((unsigned)gk), dim3(kSqThreads), 0, s, q, k, v, grad_out, lse, \
-                       delta, num_heads, num_query, num_key, ldq, ldk, ldv, scale * kLog2e, scale, kblocks, grad_k, \
-                       ld_grad_k, grad_v, ld_grad_v)
-    PDVC_SQ_DISPATCH(head_dim, PDVC_SQ_DQ)
-    PDVC_CHECK_LAUNCH("seqattn_bwd_dq_kernel");
-    PDVC_SQ_DISPATCH(head_dim, PDVC_SQ_DKV)
-    PDVC_CHECK_LAUNCH("seqattn_bwd_dkv_kernel");
-#undef PDVC_SQ_DQ
-#undef PDVC_SQ_DKV
+    const float qmul = scale * kLog2e;
+    const bool drop = dropout_p > 0.f;
+#define PDVC_SQ_BWD(DR, KP)                                                                                      \
+    sq_launch_bwd<DR, KP>(dim3((unsigned)gq), dim3((unsigned)gk), s, q, ldq, k, ldk, v, ldv, out, grad_out, lse, \
+                          num_query, num_key, num_heads, head_dim, qmul, scale, qblocks, kblocks, o, delta, grad_q,   \
+                          ld_grad_q, grad_k, ld_grad_k, grad_v, ld_grad_v)
+    if (drop && kpm) PDVC_SQ_BWD(true, true);
+    else if (drop) PDVC_SQ_BWD(true, false);
+    else if (kpm) PDVC_SQ_BWD(false, true);
+    else PDVC_SQ_BWD(false, false);
+#undef PDVC_SQ_BWD
+    PDVC_CHECK_LAUNCH("seqattn_bwd_dq_kernel / seqattn_bwd_dkv_kernel");
     return PDVC_OK;
+}
+
+}  // namespace pdvc
+
+using namespace pdvc;
+
+extern "C" int pdvc_seq_attention_forward_f32(const float* q, long ldq, const float* k, long ldk, const float* v,
+                                              long ldv, int batch, int num_query, int num_key, int num_heads,
+                                              int head_dim, float* out, float* lse, void* stream) {
+    PDVC_CHECK_ARG(batch >= 0 && num_query >= 0 && num_key > 0 && num_heads > 0, "invalid sizes");
+    PDVC_CHECK_ARG(sq_head_dim_ok(head_dim), "head_dim must be 16, 24, 32, 48 or 64, got %d", head_dim);
+    const long E = (long)num_heads * head_dim;
+    PDVC_CHECK_ARG(ldq >= E && ldk >= E && ldv >= E, "row strides must be >= num_heads * head_dim");
+    if (batch == 0 || num_query == 0) return PDVC_OK;
+    return sq_forward(q, ldq, k, ldk, v, ldv, batch, num_query, num_key, num_heads, head_dim,
+                      1.f / sqrtf((float)head_dim), nullptr, 0.f, 0, nullptr, out, lse, (hipStream_t)stream);
+}
+
+extern "C" int pdvc_seq_attention_backward_f32(const float* q, long ldq, const float* k, long ldk, const float* v,
+                                               long ldv, const float* out, const float* grad_out, const float* lse,
+                                               int batch, int num_query, int num_key, int num_heads, int head_dim,
+                                               float* workspace, float* grad_q, long ld_grad_q, float* grad_k,
+                                               long ld_grad_k, float* grad_v, long ld_grad_v, void* stream) {
+    PDVC_CHECK_ARG(batch >= 0 && num_query >= 0 && num_key > 0 && num_heads > 0, "invalid sizes");
+    PDVC_CHECK_ARG(sq_head_dim_ok(head_dim), "head_dim must be 16, 24, 32, 48 or 64, got %d", head_dim);
+    const long E = (long)num_heads * head_dim;
+    PDVC_CHECK_ARG(ldq >= E && ldk >= E && ldv >= E && ld_grad_q >= E && ld_grad_k >= E && ld_grad_v >= E,
+                   "row strides must be >= num_heads * head_dim");
+    if (batch == 0) return PDVC_OK;
+    return sq_backward(q, ldq, k, ldk, v, ldv, out, grad_out, lse, batch, num_query, num_key, num_heads, head_dim,
+                       1.f / sqrtf((float)head_dim), nullptr, 0.f, 0, nullptr, workspace, grad_q, ld_grad_q, grad_k,
+                       ld_grad_k, grad_v, ld_grad_v, (hipStream_t)stream);
 }

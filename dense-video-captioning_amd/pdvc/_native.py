@@ -72,6 +72,8 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = argtypes
             fn.restype = ctypes.c_int
+        L.pdvc_mha_workspace_floats.argtypes = [ctypes.c_int] * 4
+        L.pdvc_mha_workspace_floats.restype = ctypes.c_long
         L.pdvc_last_error.restype = ctypes.c_char_p
         L.pdvc_abi_version.restype = ctypes.c_int
         _lib = L

@@ -36,11 +36,12 @@ class QuerySelfAttentionFunction(Function):
         num_heads, p, seed = ctx.meta
         grad_out = grad_out.contiguous()
         N, Q, E2 = qk.shape
-        ws = torch.empty(2 * N * num_heads * Q * Q, dtype=qk.dtype, device=qk.device)
+        D = E2 // 2 // num_heads
+        ws = torch.empty(_n.lib().pdvc_mha_workspace_floats(N, Q, num_heads, D), dtype=qk.dtype, device=qk.device)
         gqk = torch.empty_like(qk)
         gv = torch.empty_like(v)
         _n.call("pdvc_mha_backward_f32", _n.ptr(qk), _n.ptr(v), _n.ptr(kpm_u8), _n.ptr(out), _n.ptr(grad_out),
-                _n.ptr(lse), N, Q, num_heads, E2 // 2 // num_heads, p, seed, _n.ptr(seed_dev), _n.ptr(ws),
+                _n.ptr(lse), N, Q, num_heads, D, p, seed, _n.ptr(seed_dev), _n.ptr(ws),
                 _n.ptr(gqk), _n.ptr(gv),
                 _n.stream(), meta=(N, Q, num_heads))
         return gqk, gv, None, None, None, None

@@ -175,12 +175,15 @@ int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* value_pad_ma
 int pdvc_mha_forward_f32(const float* qk, const float* v, const uint8_t* key_padding_mask, int batch, int num_query,
                          int num_heads, int head_dim, float dropout_p, uint64_t seed, const uint64_t* seed_dev,
                          float* out, float* lse, void* stream);
-/* workspace: 2*N*M*Q*Q floats (P_d and dS); grad_qk (N,Q,2E) and grad_v (N,Q,E) fully written.  seed_dev
- * (device, may be NULL) overrides seed -- pass the forward's. */
+/* workspace: pdvc_mha_workspace_floats(N, Q, M, D) floats; grad_qk (N,Q,2E) and grad_v (N,Q,E) fully
+ * written.  seed_dev (device, may be NULL) overrides seed -- pass the forward's.  Q > 128 with head_dim in
+ * {16,24,32,48,64} runs the flash-style MFMA kernels of pdvc_seq_attention_* (same dropout mask). */
 int pdvc_mha_backward_f32(const float* qk, const float* v, const uint8_t* key_padding_mask, const float* out,
                           const float* grad_out, const float* lse, int batch, int num_query, int num_heads,
                           int head_dim, float dropout_p, uint64_t seed, const uint64_t* seed_dev, float* workspace,
                           float* grad_qk, float* grad_v, void* stream);
+/* floats of workspace pdvc_mha_backward_f32 needs: 2*N*M*Q*Q (P_d and dS tiles), or N*M*Q on the flash route */
+long pdvc_mha_workspace_floats(int batch, int num_query, int num_heads, int head_dim);
 
 /* ---- caption decoder step pieces (ShowAttendTellCore) ------------------------------------------------
  * softattn: att (R,M,16,A) = ctx2att(samples); att_h (R, ld_att_h) = h2att(h) (A values per row);

@@ -57,7 +57,8 @@ def torch_mha_core(qk, v, kpm, M):
     return (p @ vv).transpose(1, 2).reshape(N, Q, E), p
 
 
-@pytest.mark.parametrize("Q,masked", [(100, False), (100, True), (37, True), (128, True), (129, False), (300, False)])
+@pytest.mark.parametrize("Q,masked", [(100, False), (100, True), (37, True), (128, True), (129, False), (300, False),
+                                      (129, True), (300, True), (257, True)])
 def test_query_self_attention_vs_float64(Q, masked):
     from pdvc.ops.functions.attention import query_self_attention
     torch.manual_seed(Q)
@@ -112,10 +113,11 @@ def test_query_self_attention_dropout_consistent():
     close(b.grad, b64.grad, 1e-4, "grad_v")
 
 
-@pytest.mark.parametrize("Q,p", [(100, 0.1), (61, 0.0), (128, 0.3)])
+@pytest.mark.parametrize("Q,p", [(100, 0.1), (61, 0.0), (128, 0.3), (300, 0.1), (129, 0.3), (200, 0.0)])
 def test_query_self_attention_matrix_core_matches_scalar(Q, p, monkeypatch):
-    """The MFMA kernels (D = 64, Q <= 128) and the scalar kernels (PDVC_MHA_MFMA=0) draw the same dropout mask
-    from the same seed: outputs and gradients agree to fp32 rounding."""
+    """The MFMA kernels (D = 64: one workgroup per (video, head) at Q <= 128, the flash-style seqattn kernels
+    above) and the scalar kernels (PDVC_MHA_MFMA=0) draw the same dropout mask from the same seed: outputs and
+    gradients agree to fp32 rounding."""
     from pdvc.ops.functions.attention import QuerySelfAttentionFunction
     torch.manual_seed(Q)
     N, M, E = 3, 8, 512
