@@ -9,11 +9,13 @@
 // (seed, row, column) instead of stored.  One wave per row (d <= 512: <= 8 columns per lane, float4 loads);
 // workgroups walk rows with a grid stride so each lane keeps its columns' gamma/beta-gradient partials in
 // registers, summed over the workgroup in LDS and over workgroups by a second small kernel.
+// The same kernels serve NewModel's front-end (NewModel.py:41-65, `ln(h) + residual`, d = 768): no s term, the
+// residual added after the affine (pdvc_layernorm_residual_*).
 #include "pdvc_common.h"
 
 namespace pdvc {
 
-constexpr int kAND = 512;              // max row width
+constexpr int kAND = 768;              // max row width
 constexpr int kANW = 4;                // waves per workgroup
 
 __device__ __forceinline__ uint32_t an_mix(uint32_t x) {
@@ -34,12 +36,14 @@ __device__ __forceinline__ float an_wave_sum(float v) {
 }
 
 // lane's columns: c = lane*4 + 256*k + {0..3}  (float4 chunks, k < kAPL/4)
+// s == NULL: no second input (z = x); r != NULL: y = LN(z) * gamma + beta + r
 template <int CH>  // float4 chunks per lane
 __global__ __launch_bounds__(kANW * 64) void addnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ s,
                                                                 const float* __restrict__ gamma,
                                                                 const float* __restrict__ beta, int rows, int d,
                                                                 float p, uint32_t thresh, uint64_t seed0,
                                                                 const uint64_t* __restrict__ seed_dev, float eps,
+                                                                const float* __restrict__ r,
                                                                 float* __restrict__ y, float* __restrict__ mean_out,
                                                                 float* __restrict__ rstd_out) {
     const int lane = threadIdx.x & 63;
@@ -54,7 +58,8 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_fwd_kernel(const float* __r
             const int c = lane * 4 + 256 * k;
             if (c < d) {
                 const float4 xv = *reinterpret_cast<const float4*>(x + (size_t)row * d + c);
-                const float4 sv = *reinterpret_cast<const float4*>(s + (size_t)row * d + c);
+                const float4 sv = s ? *reinterpret_cast<const float4*>(s + (size_t)row * d + c)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
                 const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, ss[4] = {sv.x, sv.y, sv.z, sv.w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -93,6 +98,13 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_fwd_kernel(const float* __r
                 o.y = (z[k][1] - mean) * rstd * g.y + b.y;
                 o.z = (z[k][2] - mean) * rstd * g.z + b.z;
                 o.w = (z[k][3] - mean) * rstd * g.w + b.w;
+                if (r) {
+                    const float4 rv = *reinterpret_cast<const float4*>(r + (size_t)row * d + c);
+                    o.x += rv.x;
+                    o.y += rv.y;
+                    o.z += rv.z;
+                    o.w += rv.w;
+                }
                 *reinterpret_cast<float4*>(y + (size_t)row * d + c) = o;
             }
         }
@@ -136,7 +148,8 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_bwd_kernel(const float* __r
             keep_bits[k] = 0xF;
             if (c < d) {
                 const float4 xv = *reinterpret_cast<const float4*>(x + (size_t)row * d + c);
-                const float4 sv = *reinterpret_cast<const float4*>(s + (size_t)row * d + c);
+                const float4 sv = s ? *reinterpret_cast<const float4*>(s + (size_t)row * d + c)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
                 const float4 dv = *reinterpret_cast<const float4*>(dy + (size_t)row * d + c);
                 const float4 gv = *reinterpret_cast<const float4*>(gamma + c);
                 const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, ss[4] = {sv.x, sv.y, sv.z, sv.w};
@@ -174,7 +187,7 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_bwd_kernel(const float* __r
                     pd[k][e] += q[e];
                 }
                 *reinterpret_cast<float4*>(dx + (size_t)row * d + c) = make_float4(o[0], o[1], o[2], o[3]);
-                *reinterpret_cast<float4*>(ds + (size_t)row * d + c) = make_float4(q[0], q[1], q[2], q[3]);
+                if (ds) *reinterpret_cast<float4*>(ds + (size_t)row * d + c) = make_float4(q[0], q[1], q[2], q[3]);
             }
         }
     }
@@ -267,6 +280,46 @@ static int an_grid(int rows, int cap) {
 constexpr int kAnFwdBlocks = 1024;  // 4 per CU
 constexpr int kAnBwdBlocks = 1024;  // 4 per CU (16 waves): enough loads in flight to stream at HBM rate
 
+static int an_forward(const float* x, const float* s, const float* r, const float* gamma, const float* beta, int rows,
+                      int d, float p, uint64_t seed, const uint64_t* seed_dev, float eps, float* y, float* mean,
+                      float* rstd, void* stream) {
+    const dim3 grid((unsigned)an_grid(rows, kAnFwdBlocks)), block(kANW * 64);
+    hipStream_t st = (hipStream_t)stream;
+    const uint32_t th = an_threshold(p);
+#define AN_FWD(CH) \
+    hipLaunchKernelGGL(addnorm_fwd_kernel<CH>, grid, block, 0, st, x, s, gamma, beta, rows, d, p, th, seed, seed_dev, \
+                       eps, r, y, mean, rstd)
+    if (d <= 256) AN_FWD(1);
+    else if (d <= 512) AN_FWD(2);
+    else AN_FWD(3);
+#undef AN_FWD
+    PDVC_CHECK_LAUNCH("addnorm_fwd_kernel");
+    return PDVC_OK;
+}
+
+static int an_backward(const float* x, const float* s, const float* gamma, const float* mean, const float* rstd,
+                       const float* dy, int rows, int d, float p, uint64_t seed, const uint64_t* seed_dev, float* dx,
+                       float* ds, float* dgamma, float* dbeta, float* ds_colsum, float* workspace, hipStream_t st) {
+    const int parts = an_grid(rows, kAnBwdBlocks);
+    float* gpart = workspace;
+    float* bpart = workspace + (size_t)parts * d;
+    float* spart = ds_colsum ? workspace + 2 * (size_t)parts * d : nullptr;
+    const dim3 grid((unsigned)parts), block(kANW * 64);
+    const uint32_t th = an_threshold(p);
+#define AN_BWD(CH) \
+    hipLaunchKernelGGL(addnorm_bwd_kernel<CH>, grid, block, 0, st, x, s, gamma, mean, rstd, dy, rows, d, p, th, seed, \
+                       seed_dev, dx, ds, gpart, bpart, spart)
+    if (d <= 256) AN_BWD(1);
+    else if (d <= 512) AN_BWD(2);
+    else AN_BWD(3);
+#undef AN_BWD
+    PDVC_CHECK_LAUNCH("addnorm_bwd_kernel");
+    hipLaunchKernelGGL(addnorm_colsum_kernel, dim3((unsigned)((d / 4 + 15) / 16)), dim3(256), 0, st, gpart, bpart, spart,
+                       parts, d, dgamma, dbeta, ds_colsum);
+    PDVC_CHECK_LAUNCH("addnorm_colsum_kernel");
+    return PDVC_OK;
+}
+
 }  // namespace pdvc
 
 using namespace pdvc;
@@ -282,16 +335,7 @@ extern "C" int pdvc_add_dropout_layernorm_forward_f32(const float* x, const floa
                                                       float* rstd, void* stream) {
     AN_CHECK();
     if (rows == 0) return PDVC_OK;
-    const dim3 grid((unsigned)an_grid(rows, kAnFwdBlocks)), block(kANW * 64);
-    hipStream_t st = (hipStream_t)stream;
-    if (d <= 256)
-        hipLaunchKernelGGL(addnorm_fwd_kernel<1>, grid, block, 0, st, x, s, gamma, beta, rows, d, p, an_threshold(p),
-                           seed, seed_dev, eps, y, mean, rstd);
-    else
-        hipLaunchKernelGGL(addnorm_fwd_kernel<2>, grid, block, 0, st, x, s, gamma, beta, rows, d, p, an_threshold(p),
-                           seed, seed_dev, eps, y, mean, rstd);
-    PDVC_CHECK_LAUNCH("addnorm_fwd_kernel");
-    return PDVC_OK;
+    return an_forward(x, s, nullptr, gamma, beta, rows, d, p, seed, seed_dev, eps, y, mean, rstd, stream);
 }
 
 extern "C" int pdvc_add_dropout_layernorm_backward_f32(const float* x, const float* s, const float* gamma,
@@ -310,20 +354,32 @@ extern "C" int pdvc_add_dropout_layernorm_backward_f32(const float* x, const flo
             return pdvc_set_error(PDVC_ERR_LAUNCH, "memset failed");
         return PDVC_OK;
     }
-    const int parts = an_grid(rows, kAnBwdBlocks);
-    float* gpart = workspace;
-    float* bpart = workspace + (size_t)parts * d;
-    float* spart = ds_colsum ? workspace + 2 * (size_t)parts * d : nullptr;
-    const dim3 grid((unsigned)parts), block(kANW * 64);
-    if (d <= 256)
-        hipLaunchKernelGGL(addnorm_bwd_kernel<1>, grid, block, 0, st, x, s, gamma, mean, rstd, dy, rows, d, p,
-                           an_threshold(p), seed, seed_dev, dx, ds, gpart, bpart, spart);
-    else
-        hipLaunchKernelGGL(addnorm_bwd_kernel<2>, grid, block, 0, st, x, s, gamma, mean, rstd, dy, rows, d, p,
-                           an_threshold(p), seed, seed_dev, dx, ds, gpart, bpart, spart);
-    PDVC_CHECK_LAUNCH("addnorm_bwd_kernel");
-    hipLaunchKernelGGL(addnorm_colsum_kernel, dim3((unsigned)((d / 4 + 15) / 16)), dim3(256), 0, st, gpart, bpart, spart,
-                       parts, d, dgamma, dbeta, ds_colsum);
-    PDVC_CHECK_LAUNCH("addnorm_colsum_kernel");
-    return PDVC_OK;
+    return an_backward(x, s, gamma, mean, rstd, dy, rows, d, p, seed, seed_dev, dx, ds, dgamma, dbeta, ds_colsum,
+                       workspace, st);
+}
+
+extern "C" int pdvc_layernorm_residual_forward_f32(const float* x, const float* r, const float* gamma,
+                                                   const float* beta, int rows, int d, float eps, float* y, float* mean,
+                                                   float* rstd, void* stream) {
+    const float p = 0.f;
+    AN_CHECK();
+    if (rows == 0) return PDVC_OK;
+    return an_forward(x, nullptr, r, gamma, beta, rows, d, 0.f, 0, nullptr, eps, y, mean, rstd, stream);
+}
+
+extern "C" int pdvc_layernorm_backward_f32(const float* x, const float* gamma, const float* mean, const float* rstd,
+                                           const float* dy, int rows, int d, float* dx, float* dgamma, float* dbeta,
+                                           float* workspace, void* stream) {
+    const float p = 0.f;
+    AN_CHECK();
+    PDVC_CHECK_ARG(workspace != nullptr, "workspace (2 * 1024 * d floats) is required");
+    hipStream_t st = (hipStream_t)stream;
+    if (rows == 0) {
+        hipError_t e1 = zero_async(dgamma, d, st);
+        hipError_t e2 = zero_async(dbeta, d, st);
+        if (e1 != hipSuccess || e2 != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset failed");
+        return PDVC_OK;
+    }
+    return an_backward(x, nullptr, gamma, mean, rstd, dy, rows, d, 0.f, 0, nullptr, dx, nullptr, dgamma, dbeta,
+                       nullptr, workspace, st);
 }

@@ -34,6 +34,8 @@ SIGNATURES = {
     "pdvc_lstm_cell_backward_f32": [_vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _i, _vp, _vp],
     "pdvc_add_dropout_layernorm_forward_f32": [_vp] * 4 + [_i, _i, _f, _u64, _vp, _f] + [_vp] * 4,
     "pdvc_add_dropout_layernorm_backward_f32": [_vp] * 6 + [_i, _i, _f, _u64] + [_vp] * 8,
+    "pdvc_layernorm_residual_forward_f32": [_vp] * 4 + [_i, _i, _f] + [_vp] * 4,
+    "pdvc_layernorm_backward_f32": [_vp] * 5 + [_i, _i] + [_vp] * 5,
     "pdvc_lsap_f32": [_vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp],
     "pdvc_colsum_f32": [_vp, _i, _i, _i, _vp, _vp, _vp],
     "pdvc_relu_dropout_forward_f32": [_vp, ctypes.c_long, _i, _f, _u64, _vp, _vp],

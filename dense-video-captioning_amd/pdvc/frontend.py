@@ -15,6 +15,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from pdvc.ops.functions.addnorm import layernorm_residual
 from pdvc.ops.functions.seq_attention import seq_attention
 
 
@@ -54,13 +55,14 @@ class DualModalityFrontEnd(nn.Module):
         self.mha2 = FrontEndAttention(dim, num_heads)
         self.mlp_seq2 = nn.Sequential(nn.Linear(dim, dim), nn.LayerNorm(dim))
 
+    # every `ln(h) + residual` is one HIP pass each way (pdvc_layernorm_residual_*); mlp_seq = Linear, LayerNorm
     def visual_self_attention(self, clips):  # NewModel.py:41-52
-        f = self.ln1(self.mha1(clips, clips)) + clips
-        return self.mlp_seq1(f) + f
+        f = layernorm_residual(self.mha1(clips, clips), clips, self.ln1)
+        return layernorm_residual(self.mlp_seq1[0](f), f, self.mlp_seq1[1])
 
     def visual_sound_attention(self, clips, sound):  # NewModel.py:54-65
-        g = self.ln2(self.mha2(sound, clips)) + clips
-        return self.mlp_seq2(g) + g
+        g = layernorm_residual(self.mha2(sound, clips), clips, self.ln2)
+        return layernorm_residual(self.mlp_seq2[0](g), g, self.mlp_seq2[1])
 
     def forward(self, clips, sound):
         """clips, sound (N, T, dim) -> (N, T, dim), the video_tensor PDVC consumes (NewModel.py:82-87)."""

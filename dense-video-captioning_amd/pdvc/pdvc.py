@@ -322,8 +322,12 @@ class PDVC(nn.Module):
         for v in range(N):
             steps_v.append(caption_steps(cap_cpu[cap_off[v]:cap_off[v + 1]]))
         video_csr = (vr_start_d.to(torch.int32), vr_rows_d.to(torch.int32), max_rows)
+        # the last layer's rows are one contiguous block (rows are layer-major): its outputs are views, not copies
+        last_range = (last_sel[0], len(last_sel)) if last_sel and last_sel[-1] - last_sel[0] + 1 == len(last_sel) \
+            else None
         return dict(rows=rows, hs_rows=hs_rows, ref_rows=ref_rows.contiguous(), rd1=rd1, row_video=row_video,
-                    cap_rows=cap_rows, lay=lay, vid=vid, last_sel=last_sel_d, steps_v=steps_v, video_csr=video_csr)
+                    cap_rows=cap_rows, lay=lay, vid=vid, last_sel=last_sel_d, last_range=last_range, steps_v=steps_v,
+                    video_csr=video_csr)
 
     def parallel_prediction_matched(self, dt, criterion, hs, init_reference, inter_references, others,
                                     disable_refine, heads=None):
@@ -369,7 +373,11 @@ class PDVC(nn.Module):
         last_sel = R["last_sel"]
         last_v = [r[1] for r in rows if r[0] == Ld - 1]
         n_last = max([R["steps_v"][v] for v in last_v], default=0)
-        out.update({"caption_probs": {"cap_prob_train": logprobs.index_select(0, last_sel)[:, :n_last]},
+        if R["last_range"] is not None:
+            last_lp = logprobs.narrow(0, R["last_range"][0], R["last_range"][1])
+        else:
+            last_lp = logprobs.index_select(0, last_sel)
+        out.update({"caption_probs": {"cap_prob_train": last_lp[:, :n_last]},
                     "seq": seq_rows.index_select(0, last_sel)})
         return out, loss
 

@@ -33,6 +33,8 @@
  *                                      (LSTM_DSA.py:245-258: tanh, alpha_net, softmax, weighted sum)
  *   pdvc_add_dropout_layernorm_*    <- the residual epilogue norm(x + dropout(s)) of every transformer sub-layer
  *                                      (deformable_transformer.py:150-156, 253-271)
+ *   pdvc_layernorm_residual_* /
+ *   pdvc_layernorm_backward_f32     <- NewModel front-end's ln(h) + residual (NewModel.py:41-65)
  *   pdvc_lsap_f32                   <- HungarianMatcher's scipy.optimize.linear_sum_assignment per video
  *                                      (pdvc/matcher.py:119-121), same algorithm and tie rule, on the GPU
  *   pdvc_groupnorm_rows_*           <- nn.GroupNorm(32, d) of the base encoder's pyramid levels
@@ -212,7 +214,7 @@ int pdvc_lstm_cell_backward_f32(const float* grad_h, int ld_grad_h, const float*
                                 void* stream);
 
 /* ---- fused residual epilogue: y = LayerNorm(x + dropout(s)) -----------------------------------------
- * x, s, y (rows, d) contiguous, d % 4 == 0, d <= 512; gamma, beta (d); mean, rstd (rows) saved for the backward.
+ * x, s, y (rows, d) contiguous, d % 4 == 0, d <= 768; gamma, beta (d); mean, rstd (rows) saved for the backward.
  * Dropout keeps each element with probability 1-p from a counter hash of (seed, row, column), scaled by
  * 1/(1-p); seed_dev (device, may be NULL) overrides seed.  The backward regenerates the mask:
  * dx = dL/dx, ds = dL/ds, dgamma/dbeta fully written; ds_colsum (may be NULL) = column sums of ds (the bias
@@ -225,6 +227,14 @@ int pdvc_add_dropout_layernorm_backward_f32(const float* x, const float* s, cons
                                             uint64_t seed, const uint64_t* seed_dev, float* dx, float* ds,
                                             float* dgamma, float* dbeta, float* ds_colsum, float* workspace,
                                             void* stream);
+/* NewModel's front-end epilogue (NewModel.py:41-65, `ln(h) + residual`): y = LayerNorm(x) * gamma + beta + r.
+ * Same layout and limits; the backward writes dx and dgamma/dbeta (the residual's gradient is dy itself);
+ * workspace 2*1024*d floats. */
+int pdvc_layernorm_residual_forward_f32(const float* x, const float* r, const float* gamma, const float* beta, int rows,
+                                        int d, float eps, float* y, float* mean, float* rstd, void* stream);
+int pdvc_layernorm_backward_f32(const float* x, const float* gamma, const float* mean, const float* rstd,
+                                const float* dy, int rows, int d, float* dx, float* dgamma, float* dbeta,
+                                float* workspace, void* stream);
 
 /* ---- linear sum assignment (the set matcher) --------------------------------------------------------
  * costs (P, Q, max_targets) float32: problem p matches its first sizes[p] targets (rows of scipy's transposed
