@@ -15,7 +15,8 @@ HIPBLAS_COMPUTE_32F_FAST_16BF -- fp32 operands rounded inside the kernel -- ran 
 gfx950, so the rounding is an explicit cast here.)
 
 Mechanism: a TorchDispatchMode that reroutes aten mm / addmm / addmm_ / bmm / baddbmm / _addmm_activation
-(and their out= forms) on fp32 GPU tensors.  The mode is thread-local state that autograd carries into its
+(and their out= forms) on fp32 GPU tensors; each operand's base tensor is rounded once and the rounding reused
+by every GEMM that reads it (_bf).  The mode is thread-local state that autograd carries into its
 backward threads, so the gradient GEMMs are rerouted too; inside a captured step graph the rerouting happens
 once, at capture.  GEMMs below MIN_FLOPS (tiny heads, 1-wide projections) stay fp32: no time to win there.
 
@@ -33,12 +34,28 @@ aten = torch.ops.aten
 MIN_FLOPS = 1 << 22
 # GEMMs the mode saw: (op, M, N, K) -> [calls on the bf16 path, calls kept in fp32 (below MIN_FLOPS)]
 STATS = {}
+STATS_CAST = [0, 0]  # [bf16 roundings made, reused from the cache]
 _F32 = torch.float32
 _BF = torch.bfloat16
 
 
 def _bf(t):
-    return t.to(_BF)
+    """t rounded to bf16, the rounding cached on t's base tensor: a GEMM operand is usually a view (reshape,
+    transpose, split-K chunks) of a tensor that several GEMMs read -- x in the forward product and again in the
+    weight gradient, dy in the input- and weight-gradient products, a weight forward and backward -- so each
+    base is rounded once.  The cache lives as long as the base (an attribute of it) and is dropped when the
+    base's version counter moves (in-place updates, e.g. the optimizer's)."""
+    base = t._base if t._base is not None else t
+    if not base.is_contiguous() or base.is_leaf and base.requires_grad:  # parameters: small, updated in place
+        return t.to(_BF)
+    ent = base.__dict__.get("_pdvc_bf16")
+    if ent is None or ent[0] != base._version:
+        ent = (base._version, base.to(_BF))
+        base.__dict__["_pdvc_bf16"] = ent
+        STATS_CAST[0] += 1
+    else:
+        STATS_CAST[1] += 1
+    return ent[1].as_strided(t.shape, t.stride(), t.storage_offset() - base.storage_offset())
 
 
 def _f32_cuda(*ts):
@@ -128,3 +145,10 @@ def fp32_gemms():
 def routed_summary():
     """(GEMM calls on the bf16 path, calls kept fp32) over everything the mode saw."""
     return sum(v[0] for v in STATS.values()), sum(v[1] for v in STATS.values())
+
+
+def drop_cast_cache(tensors):
+    """Forget the cached bf16 roundings of these tensors (their bases)."""
+    for t in tensors:
+        base = t._base if t._base is not None else t
+        base.__dict__.pop("_pdvc_bf16", None)
