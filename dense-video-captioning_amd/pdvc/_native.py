@@ -74,6 +74,8 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = argtypes
             fn.restype = ctypes.c_int
+        L.pdvc_detokenize.argtypes = [_vp, _i, _i, _vp, _vp, _i, _vp, ctypes.c_int64, _vp]
+        L.pdvc_detokenize.restype = ctypes.c_int
         L.pdvc_mha_workspace_floats.argtypes = [ctypes.c_int] * 4
         L.pdvc_mha_workspace_floats.restype = ctypes.c_long
         L.pdvc_last_error.restype = ctypes.c_char_p
@@ -164,3 +166,29 @@ def int_array(values):
         hit = (arr, ctypes.cast(arr, ctypes.c_void_p))
         _INT_ARRAYS[key] = hit
     return hit[1]
+
+
+def detokenize(seqs, words, word_off):
+    """pdvc_detokenize over an int64 host array (rows, len): the captions as Python strings.  words: the
+    vocabulary bytes concatenated (numpy uint8), word_off: (num_words + 1,) int64 offsets (word 0 unused)."""
+    import numpy as np
+    seqs = np.ascontiguousarray(seqs, dtype=np.int64)
+    rows, length = seqs.shape
+    if rows == 0:
+        return []
+    longest = int(np.diff(word_off).max(initial=0))
+    cap = rows * (length * (longest + 1) + 2) + 1
+    out = np.empty(cap, dtype=np.uint8)
+    ends = np.empty(rows, dtype=np.int64)
+    rc = lib().pdvc_detokenize(seqs.ctypes.data, rows, length, words.ctypes.data, word_off.ctypes.data,
+                               len(word_off) - 1, out.ctypes.data, cap, ends.ctypes.data)
+    if rc != 0:
+        raise NativeError(f"pdvc_detokenize failed ({rc}): {lib().pdvc_last_error().decode(errors='replace')}")
+    total = int(ends[-1])
+    buf = out[:total].tobytes()
+    starts = np.concatenate([[0], ends[:-1]]).tolist()
+    stops = ends.tolist()
+    if buf.isascii():  # one decode, str slices (byte offsets are character offsets)
+        text = buf.decode("ascii")
+        return [text[a:b] for a, b in zip(starts, stops)]
+    return [buf[a:b].decode("utf-8") for a, b in zip(starts, stops)]

@@ -184,6 +184,15 @@ int pdvc_mha_backward_f32(const float* qk, const float* v, const uint8_t* key_pa
                           const float* grad_out, const float* lse, int batch, int num_query, int num_heads,
                           int head_dim, float dropout_p, uint64_t seed, const uint64_t* seed_dev, float* workspace,
                           float* grad_qk, float* grad_v, void* stream);
+/* ---- caption detokenisation (host code; no GPU) ------------------------------------------------------
+ * Replaces Translator.rtranslate (data/video_dataset.py:172-180) over a batch of rows for PostProcess
+ * (pdvc/pdvc.py:493-546): seqs (rows, len) int64 host array; words = the concatenated vocabulary bytes,
+ * word w at [word_off[w], word_off[w+1]) for 1 <= w < num_words (word_off has num_words + 1 entries).
+ * Row r: ids up to the first 0, joined by ' ' plus '.', or empty when the row starts with 0; written to out
+ * (out_cap bytes) back to back, row r ending at row_end[r].  Ids outside [1, num_words) are an error. */
+int pdvc_detokenize(const int64_t* seqs, int rows, int len, const char* words, const int64_t* word_off,
+                    int num_words, char* out, int64_t out_cap, int64_t* row_end);
+
 /* floats of workspace pdvc_mha_backward_f32 needs: 2*N*M*Q*Q (P_d and dS tiles), or N*M*Q on the flash route */
 long pdvc_mha_workspace_floats(int batch, int num_query, int num_heads, int head_dim);
 

@@ -128,3 +128,13 @@ def test_rtranslate_batch_equals_rtranslate(tmp_path):
     seqs[1::5, 4] = 0
     assert tr.rtranslate_batch(seqs) == [tr.rtranslate(s) for s in seqs]
     assert tr.rtranslate_batch(np.zeros((2, 0), np.int64)) == ["", ""]
+
+
+def test_rtranslate_batch_native_edge_cases():
+    """pdvc_detokenize (the native batch path): non-ASCII words, rows starting with 0, full-length rows, and an
+    id without a word raising as rtranslate does."""
+    tr = VD.Translator.from_vocab({"1": "café", "2": "naïve", "3": "x"})
+    seqs = np.array([[1, 2, 3, 0], [0, 1, 2, 3], [3, 3, 3, 3]])
+    assert tr.rtranslate_batch(seqs) == [tr.rtranslate(s) for s in seqs] == ["café naïve x.", "", "x x x x."]
+    with pytest.raises(KeyError):
+        tr.rtranslate_batch(np.array([[1, 9, 0]]))
