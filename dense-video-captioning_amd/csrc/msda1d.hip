@@ -501,6 +501,152 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
 }
 
 // -------------------------------------------------------------------------------------------------
+// backward, query side, dot-product form (D = 64: 16 lanes x float4 per query, 4 queries per wave).
+// Every quantity the query side needs from a sample's two corner rows is linear in the two dot products
+//     d1 = <dL/dout, value[x0]>,   d2 = <dL/dout, value[x0 + 1]>    (this head's 64 channels)
+// (.cuh:140-170: grad_attn = hw*d1 + lw*d2 and grad_loc = T * attn * (d2 - d1), each corner counted only where the
+// reference samples it).  So the lanes form only the raw per-channel products (8 FMAs per sample and lane),
+// reduce the level's 8 partials over the 16-lane group, and the lane that owns the sample (lane j = l*P + p,
+// the one that read its location and weight) applies the corner weights and the masks once, after the
+// reduction -- msda1d_bwd_query_kernel applies them per channel and lane (4x the VALU work) and recomputed the
+// sample parameters on every lane through shuffles.  Corner rows are read with buffer loads: one 32-bit offset
+// per sample (the second corner one row further), and a sample's clamping replaced by the
+// descriptor's range check (the video's S rows; a corner outside the level reads a neighbouring level's row
+// or zeros, and the mask removes it after the reduction).  The measured profile of msda1d_bwd_query_kernel was
+// VALU issue (1 900 VALU instructions per wave, 44 per VMEM read); this form issues ~400.
+// Reduction order per level: reduce-scatter over lane bits 8, 2, 1 (DPP), then an all-reduce over bit 4
+// (ds_swizzle): lane sub holds value (sub & 8 ? 4 : 0) + (sub & 3) of [d1_0..d1_3, d2_0..d2_3], and one xor-8
+// DPP exchange gives every lane the (d1, d2) pair of point sub & 3 -- so lane 4l + p, the owner of sample
+// (l, p), ends each level holding exactly its own pair.
+// -------------------------------------------------------------------------------------------------
+template <int RD>
+__global__ __launch_bounds__(256) void msda1d_bwd_query_dot_kernel(
+    const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
+    int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
+    int total_waves, const float* __restrict__ gout, const float* __restrict__ save_attn,
+    const float* __restrict__ save_loc, float* __restrict__ grad_proj, float* __restrict__ grad_ref) {
+    constexpr int D = 64;
+    const int lane = threadIdx.x & 63;
+    // wave-uniform by construction; readfirstlane tells the compiler, so the video / head / buffer descriptor
+    // live in scalar registers (a per-lane descriptor costs a waterfall loop around every buffer load)
+    const int wave = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
+    if (wave >= total_waves) return;
+    const WaveQuery w = wave_query<16>(wave, lane, Lq, M);
+    const int MD = M * D;
+    const size_t sbase = ((size_t)w.row * M + w.m) * kNS;
+    const int c0 = w.sub * 4;
+
+    // this lane's sample j = sub: level l_own, its corner row, weights and masks (ms_deform_attn.py:168-177 math
+    // as in the forward; the location and softmaxed weight come from the forward's save_loc / save_attn)
+    const int j = w.sub, l_own = j >> 2;
+    int T_own = lv.T[0], st_own = lv.start[0];  // branch-free per-lane level select
+#pragma unroll
+    for (int l = 1; l < kL; ++l) {
+        T_own = l_own >= l ? lv.T[l] : T_own;
+        st_own = l_own >= l ? lv.start[l] : st_own;
+    }
+    const float Tf = (float)T_own;
+    const float x = save_loc[sbase + j] * Tf - 0.5f;
+    const float a = save_attn[sbase + j];
+    const bool inside = x > -1.f && x < Tf;
+    const float xf = floorf(inside ? x : 0.f);
+    const int i0 = (int)xf;
+    const float lw = inside ? x - xf : 0.f;
+    bool ok1 = inside && i0 >= 0, ok2 = inside && i0 + 1 <= T_own - 1;
+    if (vmask) {
+        const uint8_t* mb = vmask + (size_t)w.b * S + st_own;
+        ok1 = ok1 && !mb[min(max(i0, 0), T_own - 1)];
+        ok2 = ok2 && !mb[min(max(i0 + 1, 0), T_own - 1)];
+    }
+    // byte offset of this sample's corner-1 row inside the video's value slice (broadcast to the group), and of
+    // this lane's channels of head m inside a row
+    const int roff = (st_own + i0) * (MD * 4);
+    const int coff = (w.m * D + c0) * 4;
+
+    float4 g = *reinterpret_cast<const float4*>(gout + (size_t)w.row * MD + (size_t)w.m * D + c0);
+    const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(value + (size_t)w.b * S * MD), (short)0, S * MD * 4, 0x00020000);
+    float d1 = 0.f, d2 = 0.f;  // this lane's sample's full dot products
+#pragma unroll
+    for (int l = 0; l < kL; ++l) {
+        float part[8];  // [d1_0..d1_3, d2_0..d2_3], this lane's 4 channels
+#pragma unroll
+        for (int p = 0; p < kP; ++p) {
+            const int off = grp_bcast<16>(roff, l * kP + p) + coff;
+            const auto u1 = __builtin_amdgcn_raw_buffer_load_b128(vr, off, 0, 0);
+            const auto u2 = __builtin_amdgcn_raw_buffer_load_b128(vr, off + MD * 4, 0, 0);
+            part[p] = g.x * __uint_as_float(u1[0]) + g.y * __uint_as_float(u1[1]) + g.z * __uint_as_float(u1[2]) +
+                      g.w * __uint_as_float(u1[3]);
+            part[4 + p] = g.x * __uint_as_float(u2[0]) + g.y * __uint_as_float(u2[1]) +
+                          g.z * __uint_as_float(u2[2]) + g.w * __uint_as_float(u2[3]);
+        }
+        // reduce-scatter over lane bits 8, 2, 1: lane keeps value (sub & 8 ? 4 : 0) + (sub & 3)
+        {
+            const bool u8 = (lane & 8) != 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float send = u8 ? part[i] : part[i + 4];
+                const float mine = u8 ? part[i + 4] : part[i];
+                part[i] = mine + grp_swap(send, 8);
+            }
+            const bool u2b = (lane & 2) != 0;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const float send = u2b ? part[i] : part[i + 2];
+                const float mine = u2b ? part[i + 2] : part[i];
+                part[i] = mine + grp_swap(send, 2);
+            }
+            const bool u1b = (lane & 1) != 0;
+            const float send = u1b ? part[0] : part[1];
+            const float mine = u1b ? part[1] : part[0];
+            part[0] = mine + grp_swap(send, 1);
+            part[0] += grp_swap(part[0], 4);
+        }
+        // lanes 0..7 hold d1 of point sub & 3, lanes 8..15 its d2; one xor-8 exchange pairs them
+        const float other = grp_swap(part[0], 8);
+        if (l_own == l) {
+            d1 = (l < 2) ? part[0] : other;
+            d2 = (l < 2) ? other : part[0];
+        }
+    }
+
+    // owner math (.cuh:140-170): corner weights and masks after the reduction
+    const float x1 = ok1 ? d1 : 0.f, x2 = ok2 ? d2 : 0.f;
+    const float ga = (1.f - lw) * x1 + lw * x2;  // dL/da_j
+    const float gloc = Tf * ((x2 - x1) * a);     // dL/dloc_j
+    const float* prow = proj + (size_t)w.row * proj_stride;
+    float* gprow = grad_proj + (size_t)w.row * proj_stride;
+    float g0 = gloc, g1 = 0.f, goff;
+    if (RD == 1) {
+        goff = gloc / Tf;
+    } else {
+        const float rr1 = ref[((size_t)w.row * kL + l_own) * 2 + 1];
+        const float t2 = gloc * 0.5f;
+        goff = (t2 * rr1) / (float)kP;
+        g1 = t2 * (prow[off_base + w.m * kNS + j] / (float)kP);
+    }
+    // softmax backward: delta = sum_j a_j dL/da_j over the (query, head)'s 16 samples
+    const float delta = group_allreduce<16>(a * ga);
+    if (w.active) {
+        gprow[off_base + w.m * kNS + j] = goff;
+        gprow[logit_base + w.m * kNS + j] = a * (ga - delta);
+    }
+    if (grad_ref) {  // per (query, level): sum over the level's 4 points = the lane quad; heads differ by wave
+        g0 += grp_swap(g0, 1);
+        g0 += grp_swap(g0, 2);
+        if (RD == 2) {
+            g1 += grp_swap(g1, 1);
+            g1 += grp_swap(g1, 2);
+        }
+        if ((j & 3) == 0 && w.active) {
+            float* dst = grad_ref + ((size_t)w.row * kL + l_own) * RD;
+            atomicAdd(dst, g0);
+            if (RD == 2) atomicAdd(dst + 1, g1);
+        }
+    }
+}
+
+// -------------------------------------------------------------------------------------------------
 // backward, value side: destination-centric sum over an inverted index, no float atomics.
 // One workgroup per (video, head, level) and chunk of queries.  Row t of the level receives
 //     grad_value[t] = sum_{x0(s) = t} hw_s a_s g_q(s)  +  sum_{x0(s) = t-1} lw_s a_s g_q(s)
@@ -786,6 +932,15 @@ static bool value_g4() {
     return on;
 }
 
+// dot-product backward-query kernel at D = 64 (PDVC_MSDA_BWDQ=0 selects msda1d_bwd_query_kernel: A/B)
+static bool bwdq_dot() {
+    static const bool on = [] {
+        const char* e = getenv("PDVC_MSDA_BWDQ");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 static int pyr_attrs() {
     static int rc = -1;
     if (rc < 0) {
@@ -902,7 +1057,18 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
         hipError_t e = zero_async(grad_ref, (size_t)rows * kL * ref_dim, s);
         if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_ref: %s", hipGetErrorString(e));
     }
-    if (tw > 0) {
+    if (tw > 0 && head_dim == 64 && bwdq_dot() && (long)S * num_heads * head_dim * 4 < (1L << 31)) {
+        dim3 grid((unsigned)((tw + 3) / 4));
+        if (ref_dim == 1)
+            hipLaunchKernelGGL((msda1d_bwd_query_dot_kernel<1>), grid, dim3(256), 0, s, value, value_pad_mask, proj,
+                               proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, (int)tw,
+                               grad_output, save_attn, save_loc, grad_proj, grad_ref);
+        else
+            hipLaunchKernelGGL((msda1d_bwd_query_dot_kernel<2>), grid, dim3(256), 0, s, value, value_pad_mask, proj,
+                               proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, (int)tw,
+                               grad_output, save_attn, save_loc, grad_proj, grad_ref);
+        PDVC_CHECK_LAUNCH("msda1d_bwd_query_dot_kernel");
+    } else if (tw > 0) {
         dim3 grid((unsigned)((tw + 3) / 4));
         if (ref_dim == 1)
             launch_bwdq1d<1>(g, grid, s, value, value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv,
