@@ -336,9 +336,10 @@ static bool sa_vec4(const void* const* ptrs, int n, int A, int D, int ld1, int l
     return true;
 }
 
-// gates = a + b + c (each (R,4H) with its own row stride; b or c may be NULL); acts <- (i,f,g,o) activations
+// gates = a + b + c + d (each (R,4H) with its own row stride; b, c or d may be NULL); acts <- (i,f,g,o) activations
 __global__ __launch_bounds__(256) void lstm_fwd_kernel(const float* __restrict__ ga, int lda, const float* __restrict__ gb,
                                                        int ldb, const float* __restrict__ gc, int ldc,
+                                                       const float* __restrict__ gd, int ldd,
                                                        const float* __restrict__ c_prev, int R, int H,
                                                        float* __restrict__ h_out, int ldho, float* __restrict__ c_out,
                                                        float* __restrict__ acts) {
@@ -352,6 +353,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(const float* __restrict__
         float v = ga[(size_t)r * lda + col];
         if (gb) v += gb[(size_t)r * ldb + col];
         if (gc) v += gc[(size_t)r * ldc + col];
+        if (gd) v += gd[(size_t)r * ldd + col];
         z[q] = v;
     }
     const float i = sigm(z[0]), f = sigm(z[1]), g = tanhf(z[2]), o = sigm(z[3]);
@@ -443,13 +445,15 @@ extern "C" int pdvc_softattn_backward_f32(const float* att, const float* att_h, 
 }
 
 extern "C" int pdvc_lstm_cell_forward_f32(const float* gates_a, int lda, const float* gates_b, int ldb,
-                                          const float* gates_c, int ldc, const float* c_prev, int rows, int hidden,
+                                          const float* gates_c, int ldc, const float* gates_d, int ldd,
+                                          const float* c_prev, int rows, int hidden,
                                           float* h_out, int ld_h_out, float* c_out, float* acts, void* stream) {
     PDVC_CHECK_ARG(rows >= 0 && hidden > 0 && lda >= 4 * hidden, "invalid sizes");
     const long n = (long)rows * hidden;
     if (n == 0) return PDVC_OK;
     hipLaunchKernelGGL(lstm_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, gates_a,
-                       lda, gates_b, ldb, gates_c, ldc, c_prev, rows, hidden, h_out, ld_h_out, c_out, acts);
+                       lda, gates_b, ldb, gates_c, ldc, gates_d, ldd, c_prev, rows, hidden, h_out, ld_h_out, c_out,
+                       acts);
     PDVC_CHECK_LAUNCH("lstm_fwd_kernel");
     return PDVC_OK;
 }

@@ -35,6 +35,13 @@ struct Levels1d {
     int start[kL];
 };
 
+// save_attn / save_loc (written by the forward, read by both backward kernels): level-major (N, M, L, Lq, P), so
+// the value-gradient workgroup of one (video, head, level) reads its samples as one contiguous slab, and the
+// query side reads a wave's 4 consecutive queries of a level as one 64-B piece.
+__device__ __forceinline__ size_t save_index(int b, int m, int l, int q, int p, int Lq, int M) {
+    return ((((size_t)b * M + m) * kL + l) * Lq + q) * kP + p;
+}
+
 template <int CPL>
 __device__ __forceinline__ void load_row(VecF<CPL>& v, const float* __restrict__ p, bool ok) {
     if (ok) v.load(p);
@@ -129,7 +136,7 @@ __global__ __launch_bounds__(256) void msda1d_fwd_kernel(
         const float r1 = (RD == 2) ? ref[((size_t)w.row * kL + l) * RD + 1] : 0.f;
         const float loc = (RD == 1) ? r0 + off / Tf : r0 + ((off / (float)kP) * r1) * 0.5f;
         if (save_loc && w.active) {
-            const size_t si = ((size_t)w.row * M + w.m) * kNS + j;
+            const size_t si = save_index(w.b, w.m, l, w.q, j % kP, Lq, M);
             save_loc[si] = loc;
             save_attn[si] = aw;
         }
@@ -174,6 +181,98 @@ __global__ __launch_bounds__(256) void msda1d_fwd_kernel(
         __builtin_amdgcn_sched_barrier(0);
     }
     if (w.active) acc.store(out + (size_t)w.row * MD + (size_t)w.m * D + w.sub * CPL);
+}
+
+// -------------------------------------------------------------------------------------------------
+// Forward at D = 64 with buffer loads (the query-side mapping of msda1d_bwd_query_dot_kernel): a lane owns one
+// sample of its query (j = lane % 16) for the parameter phase, and the group gathers the sample's two corner rows
+// through the broadcast row offset and corner weights.  The per-lane clamping and 64-bit address arithmetic of
+// msda1d_fwd_kernel are replaced by one 32-bit offset per sample and the descriptor's range check (a corner outside
+// its level reads a finite neighbouring row or zeros, and its weight is 0, as in the reference's skipped corner).
+// Same parameter math, same accumulation order as msda1d_fwd_kernel: the same bits.
+// -------------------------------------------------------------------------------------------------
+template <int RD>
+__global__ __launch_bounds__(256) void msda1d_fwd_buf_kernel(
+    const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
+    int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
+    int total_waves, float* __restrict__ out, float* __restrict__ save_attn, float* __restrict__ save_loc) {
+    constexpr int D = 64;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
+    if (wave >= total_waves) return;
+    const WaveQuery w = wave_query<16>(wave, lane, Lq, M);
+    const int MD = M * D;
+    const int j = w.sub, l_own = j >> 2;
+    int T_own = lv.T[0], st_own = lv.start[0];
+#pragma unroll
+    for (int l = 1; l < kL; ++l) {
+        T_own = l_own >= l ? lv.T[l] : T_own;
+        st_own = l_own >= l ? lv.start[l] : st_own;
+    }
+    const float Tf = (float)T_own;
+    const float* prow = proj + (size_t)w.row * proj_stride;
+    const float lg = prow[logit_base + w.m * kNS + j];
+    const float off = prow[off_base + w.m * kNS + j];
+    const float r0 = ref[((size_t)w.row * kL + l_own) * RD];
+    const float r1 = (RD == 2) ? ref[((size_t)w.row * kL + l_own) * RD + 1] : 0.f;
+    const float mx = group_max<16>(lg);
+    const float sum = group_allreduce<16>(expf(lg - mx));
+    const float aw = expf(lg - mx) / sum;
+    const float loc = (RD == 1) ? r0 + off / Tf : r0 + ((off / (float)kP) * r1) * 0.5f;
+    if (save_loc && w.active) {
+        const size_t si = save_index(w.b, w.m, l_own, w.q, j & 3, Lq, M);
+        save_loc[si] = loc;
+        save_attn[si] = aw;
+    }
+    const float x = loc * Tf - 0.5f;
+    const bool inside = x > -1.f && x < Tf;
+    const float xf = floorf(inside ? x : 0.f);
+    const int i0 = (int)xf;
+    const float lw = inside ? x - xf : 0.f;
+    bool ok1 = inside && i0 >= 0, ok2 = inside && i0 + 1 <= T_own - 1;
+    if (vmask) {
+        const uint8_t* mb = vmask + (size_t)w.b * S + st_own;
+        ok1 = ok1 && !mb[min(max(i0, 0), T_own - 1)];
+        ok2 = ok2 && !mb[min(max(i0 + 1, 0), T_own - 1)];
+    }
+    const float w1 = ok1 ? (1.f - lw) * aw : 0.f, w2 = ok2 ? lw * aw : 0.f;
+    const int roff = (st_own + i0) * (MD * 4);
+    const int coff = (w.m * D + w.sub * 4) * 4;
+    const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(  // scalar: one video per wave
+        (void*)(value + (size_t)__builtin_amdgcn_readfirstlane(w.b) * S * MD), (short)0, S * MD * 4, 0x00020000);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int l = 0; l < kL; ++l) {
+        // the level's broadcasts and loads depend (opaquely) on all four of the previous level's sums, so the compiler
+        // can neither hoist them nor defer the previous level's FMAs: one level's 8 corner loads live at a time
+        // (hoisting all 32 took 200 VGPRs; a dependency on acc.x alone, 127)
+        int rl = roff;
+        float wl1 = w1, wl2 = w2;
+        __asm__ volatile("" : "+v"(rl), "+v"(wl1), "+v"(wl2) : "v"(acc.x), "v"(acc.y), "v"(acc.z), "v"(acc.w));
+        float4 v1[kP], v2[kP];
+        float c1[kP], c2[kP];
+#pragma unroll
+        for (int p = 0; p < kP; ++p) {
+            const int o = grp_bcast<16>(rl, l * kP + p) + coff;
+            c1[p] = grp_bcast<16>(wl1, l * kP + p);
+            c2[p] = grp_bcast<16>(wl2, l * kP + p);
+            const auto u1 = __builtin_amdgcn_raw_buffer_load_b128(vr, o, 0, 0);
+            const auto u2 = __builtin_amdgcn_raw_buffer_load_b128(vr, o + MD * 4, 0, 0);
+            v1[p] = make_float4(__uint_as_float(u1[0]), __uint_as_float(u1[1]), __uint_as_float(u1[2]),
+                                __uint_as_float(u1[3]));
+            v2[p] = make_float4(__uint_as_float(u2[0]), __uint_as_float(u2[1]), __uint_as_float(u2[2]),
+                                __uint_as_float(u2[3]));
+        }
+#pragma unroll
+        for (int p = 0; p < kP; ++p) {
+            acc.x += c1[p] * v1[p].x + c2[p] * v2[p].x;
+            acc.y += c1[p] * v1[p].y + c2[p] * v2[p].y;
+            acc.z += c1[p] * v1[p].z + c2[p] * v2[p].z;
+            acc.w += c1[p] * v1[p].w + c2[p] * v2[p].w;
+        }
+    }
+    if (w.active)
+        *reinterpret_cast<float4*>(out + (size_t)w.row * MD + (size_t)w.m * D + w.sub * 4) = acc;
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -268,7 +367,7 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
         const float r1 = r1v[i];
         const float loc = (RD == 1) ? r0 + off / Tf_own : r0 + ((off / (float)kP) * r1) * 0.5f;
         if (save_loc && act) {
-            const size_t si = (row * M + m) * kNS + sub;
+            const size_t si = save_index(b, m, l_own, q, sub & 3, Lq, M);
             save_loc[si] = loc;
             save_attn[si] = aw;
         }
@@ -355,7 +454,6 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
     const WaveQuery w = wave_query<LPH>(wave, lane, Lq, M);
     const size_t MD = (size_t)M * D;
     const uint8_t* mbase = vmask ? vmask + (size_t)w.b * S : nullptr;
-    const size_t sbase = ((size_t)w.row * M + w.m) * kNS;
     const int c0 = w.sub * CPL;
 
     VecF<CPL> g;
@@ -382,7 +480,7 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
         const int l = j / kP;
         const int T = lvl_sel(lv.T, l), st = lvl_sel(lv.start, l);
         const float Tf = (float)T;
-        const float x = save_loc[sbase + j] * Tf - 0.5f;
+        const float x = save_loc[save_index(w.b, w.m, l, w.q, j % kP, Lq, M)] * Tf - 0.5f;
         const bool inside = x > -1.f && x < Tf;
         const float xf = floorf(inside ? x : 0.f);
         const int i0 = (int)xf;
@@ -453,7 +551,7 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
         }
         const bool owner = w.active && w.sub < G && (VPL == 2 || (r & 1) == 0);
         const int j = l * kP + p;
-        const float a = save_attn[sbase + j];
+        const float a = save_attn[save_index(w.b, w.m, l, w.q, p, Lq, M)];
         // CUDA: grad_loc_w = W * grad_w_weight * (top_grad * attn), summed over channels (.cuh:158)
         const float gloc = owner ? Tf * (gs * a) : 0.f;
         float g0 = gloc, g1 = 0.f;
@@ -493,7 +591,7 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_kernel(
 #pragma unroll
             for (int l = 0; l < kL; ++l) {
                 const int j = l * kP + p;
-                const float a = save_attn[sbase + j];  // re-read (cached) rather than held across the levels
+                const float a = save_attn[save_index(w.b, w.m, l, w.q, p, Lq, M)];  // re-read (cached) rather than held across the levels
                 gprow[logit_base + w.m * kNS + j] = a * (keep_ga[l] - delta);
             }
         }
@@ -533,7 +631,6 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_dot_kernel(
     if (wave >= total_waves) return;
     const WaveQuery w = wave_query<16>(wave, lane, Lq, M);
     const int MD = M * D;
-    const size_t sbase = ((size_t)w.row * M + w.m) * kNS;
     const int c0 = w.sub * 4;
 
     // this lane's sample j = sub: level l_own, its corner row, weights and masks (ms_deform_attn.py:168-177 math
@@ -546,8 +643,9 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_dot_kernel(
         st_own = l_own >= l ? lv.start[l] : st_own;
     }
     const float Tf = (float)T_own;
-    const float x = save_loc[sbase + j] * Tf - 0.5f;
-    const float a = save_attn[sbase + j];
+    const size_t si = save_index(w.b, w.m, l_own, w.q, j & 3, Lq, M);
+    const float x = save_loc[si] * Tf - 0.5f;
+    const float a = save_attn[si];
     const bool inside = x > -1.f && x < Tf;
     const float xf = floorf(inside ? x : 0.f);
     const int i0 = (int)xf;
@@ -564,8 +662,8 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_dot_kernel(
     const int coff = (w.m * D + c0) * 4;
 
     float4 g = *reinterpret_cast<const float4*>(gout + (size_t)w.row * MD + (size_t)w.m * D + c0);
-    const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(value + (size_t)w.b * S * MD), (short)0, S * MD * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(  // scalar: one video per wave
+        (void*)(value + (size_t)__builtin_amdgcn_readfirstlane(w.b) * S * MD), (short)0, S * MD * 4, 0x00020000);
     float d1 = 0.f, d2 = 0.f;  // this lane's sample's full dot products
 #pragma unroll
     for (int l = 0; l < kL; ++l) {
@@ -659,7 +757,8 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_dot_kernel(
 // no memset.  (The first version accumulated with ds_add_f32 and ran ~7x slower: LDS float atomics
 // were the kernel's whole cost, measured by replacing them with plain stores -- tools/kbench.py.)
 // -------------------------------------------------------------------------------------------------
-constexpr int kVW = 8;  // waves per value-gradient workgroup
+constexpr int kVW = 8;     // waves per value-gradient workgroup
+constexpr int kVQPT = 4;  // queries per thread in its sort passes: a launch chunk holds <= kVQPT * kVW * 64 queries
 
 // CW: channels per lane (D <= 64 -> 1, D = 128 -> 2).  G4 (D == 64): the gather phase runs on 16-lane groups
 // with a float4 per lane instead of whole waves with one float per lane -- 32 row ranges per workgroup, and one
@@ -687,16 +786,40 @@ __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_
     int* sq = lds_i + 2 * (T + 2);          // [n] query of each sorted sample
     float* clo = (float*)(sq + n);          // [n] hw * a  -> row x0
     float* chi = clo + n;                   // [n] lw * a  -> row x0 + 1
+    // G4: one 16-B entry per sorted sample instead (query, hw * a, lw * a, key), one ds_read_b128 in the walk
+    int4* ent = reinterpret_cast<int4*>(lds_i + ((2 * (T + 2) + 3) & ~3));
     __shared__ int wsum[kVW];
 
     for (int i = threadIdx.x; i < T + 2; i += blockDim.x) off[i] = 0;
     __syncthreads();
-    const size_t sbase = ((size_t)b * Lq * M + m) * kNS + l * kP;
-    // 1) histogram of key = x0 + 1 in [0, T] (samples outside (-1, T) touch no row, as in the reference)
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const int q = q0 + i / kP, p = i % kP;
-        const float x = save_loc[sbase + (size_t)q * M * kNS + p] * Tf - 0.5f;
-        if (x > -1.f && x < Tf) atomicAdd(&off[(int)floorf(x) + 1], 1);
+    // 1) histogram of key = x0 + 1 in [0, T] (samples outside (-1, T) touch no row, as in the reference).  A thread
+    // takes whole queries (one float4 = the level's 4 points, from the level-major slab) and keeps each sample's key
+    // and fraction in registers for the scatter pass, so save_loc is read once.
+    const size_t sbase = save_index(b, m, l, q0, 0, Lq, M);
+    int key[kVQPT][kP];
+    float lwv[kVQPT][kP];
+#pragma unroll
+    for (int k = 0; k < kVQPT; ++k) {
+        const int qi = threadIdx.x + k * blockDim.x;
+#pragma unroll
+        for (int p = 0; p < kP; ++p) {
+            key[k][p] = -1;
+            lwv[k][p] = 0.f;
+        }
+        if (qi < nq) {
+            const float4 lc = *reinterpret_cast<const float4*>(save_loc + sbase + (size_t)qi * kP);
+            const float xs[kP] = {lc.x, lc.y, lc.z, lc.w};
+#pragma unroll
+            for (int p = 0; p < kP; ++p) {
+                const float x = xs[p] * Tf - 0.5f;
+                if (x > -1.f && x < Tf) {
+                    const float xf = floorf(x);
+                    key[k][p] = (int)xf + 1;
+                    lwv[k][p] = x - xf;
+                    atomicAdd(&off[key[k][p]], 1);
+                }
+            }
+        }
     }
     __syncthreads();
     // 2) exclusive scan of off[0 .. T+1] (off[T+1] = 0 before, total after): per-thread chunks + wave scan
@@ -726,17 +849,26 @@ __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_
     }
     __syncthreads();
     // 3) scatter the samples into bucket order with their two corner coefficients
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const int q = q0 + i / kP, p = i % kP;
-        const size_t si = sbase + (size_t)q * M * kNS + p;
-        const float x = save_loc[si] * Tf - 0.5f;
-        if (x > -1.f && x < Tf) {
-            const float xf = floorf(x);
-            const float lw = x - xf, a = save_attn[si];
-            const int pos = atomicAdd(&cur[(int)xf + 1], 1);
-            sq[pos] = q;
-            clo[pos] = (1.f - lw) * a;
-            chi[pos] = lw * a;
+#pragma unroll
+    for (int k = 0; k < kVQPT; ++k) {
+        const int qi = threadIdx.x + k * blockDim.x;
+        if (qi < nq) {
+            const float4 at = *reinterpret_cast<const float4*>(save_attn + sbase + (size_t)qi * kP);
+            const float as[kP] = {at.x, at.y, at.z, at.w};
+#pragma unroll
+            for (int p = 0; p < kP; ++p) {
+                if (key[k][p] >= 0) {
+                    const int pos = atomicAdd(&cur[key[k][p]], 1);
+                    const float lo = (1.f - lwv[k][p]) * as[p], hi = lwv[k][p] * as[p];
+                    if constexpr (G4) {
+                        ent[pos] = make_int4(q0 + qi, __float_as_int(lo), __float_as_int(hi), key[k][p]);
+                    } else {
+                        sq[pos] = q0 + qi;
+                        clo[pos] = lo;
+                        chi[pos] = hi;
+                    }
+                }
+            }
         }
     }
     __syncthreads();
@@ -759,19 +891,27 @@ __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_
     const uint8_t* mrow = vmask ? vmask + (size_t)b * S + st : nullptr;
     constexpr int U = 8;
     if constexpr (G4) {
-        const int grp = lane >> 4, gl = lane & 15;
-        const int vg = wid * 4 + grp;
+        // rows whose two buckets (t: high corner, t + 1: low corner) are both empty get no sample: zeros (first
+        // query chunk only; later chunks add into what the first wrote).  Every other row is written by the walk.
+        const int gl = lane & 15;
+        float* ob = grad_value + ((size_t)b * S + st) * MD + (size_t)m * D + gl * 4;
+        if (!accumulate)
+            for (int t = threadIdx.x >> 4; t < T; t += blockDim.x >> 4)
+                if (off[t] == off[t + 2]) *reinterpret_cast<float4*>(ob + (size_t)t * MD) = make_float4(0.f, 0.f, 0.f, 0.f);
+        // walk: 16-lane group vg owns rows [r0, r1) and reads buckets r0 .. r1; one sorted entry and one gathered
+        // gradient row per sample, two running rows (key - 1 and key), each row written once when its last bucket
+        // has passed -- no per-row search, at most two row writes per change of key
+        const int vg = wid * 4 + (lane >> 4);
         const int r0 = split(vg), r1 = split(vg + 1);
-        if (r0 < r1) {  // per-group control flow below: no cross-lane operations
-            const float* gb = gout + (size_t)b * Lq * MD + (size_t)m * D + gl * 4;
-            float* ob = grad_value + ((size_t)b * S + st) * MD + (size_t)m * D + gl * 4;
-            float4 accp = make_float4(0.f, 0.f, 0.f, 0.f), acch = accp;  // rows k-1 and k
-            int k = r0;
-            auto close_bucket = [&]() {
-                const int r = k - 1;
-                if (r >= r0) {
+        const int jb = off[r0], je = off[r1 + 1];
+        if (r0 < r1 && jb < je) {  // per-group control flow below: no cross-lane operations
+            const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(gout + (size_t)b * Lq * MD), (short)0, (int)((size_t)Lq * MD * 4), 0x00020000);
+            const int coff = (m * D + gl * 4) * 4, rowb = (int)MD * 4;
+            auto put = [&](int r, float4 v) {
+                if (r >= r0 && r < r1) {
                     float4* orow = reinterpret_cast<float4*>(ob + (size_t)r * MD);
-                    float4 v = (mrow && mrow[r]) ? make_float4(0.f, 0.f, 0.f, 0.f) : accp;
+                    if (mrow && mrow[r]) v = make_float4(0.f, 0.f, 0.f, 0.f);
                     if (accumulate) {
                         const float4 o = *orow;
                         v.x += o.x;
@@ -781,35 +921,48 @@ __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_
                     }
                     *orow = v;
                 }
-                accp = acch;
-                acch = make_float4(0.f, 0.f, 0.f, 0.f);
-                ++k;
             };
-            const int jb = off[r0], je = off[r1 + 1];
+            int k = ent[jb].w;
+            float4 alo = make_float4(0.f, 0.f, 0.f, 0.f), ahi = alo;  // rows k - 1 and k
             for (int j0 = jb; j0 < je; j0 += U) {
+                int4 e[U];
                 float4 gv[U];
 #pragma unroll
+                for (int u = 0; u < U; ++u) e[u] = ent[(j0 + u < je) ? j0 + u : je - 1];
+#pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    const int j = (j0 + u < je) ? j0 + u : je - 1;
-                    gv[u] = *reinterpret_cast<const float4*>(gb + (size_t)sq[j] * MD);
+                    const auto t = __builtin_amdgcn_raw_buffer_load_b128(gr, e[u].x * rowb + coff, 0, 0);
+                    gv[u] = make_float4(__uint_as_float(t[0]), __uint_as_float(t[1]), __uint_as_float(t[2]),
+                                        __uint_as_float(t[3]));
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    const int j = j0 + u;
-                    if (j >= je) break;
-                    while (j >= off[k + 1]) close_bucket();
-                    const float cl = clo[j], chh = chi[j];
-                    accp.x = fmaf(cl, gv[u].x, accp.x);
-                    accp.y = fmaf(cl, gv[u].y, accp.y);
-                    accp.z = fmaf(cl, gv[u].z, accp.z);
-                    accp.w = fmaf(cl, gv[u].w, accp.w);
-                    acch.x = fmaf(chh, gv[u].x, acch.x);
-                    acch.y = fmaf(chh, gv[u].y, acch.y);
-                    acch.z = fmaf(chh, gv[u].z, acch.z);
-                    acch.w = fmaf(chh, gv[u].w, acch.w);
+                    if (j0 + u >= je) break;
+                    const int kj = e[u].w;
+                    if (kj != k) {  // bucket k complete: row k - 1 final; row k too unless bucket k + 1 follows
+                        put(k - 1, alo);
+                        if (kj == k + 1) {
+                            alo = ahi;
+                        } else {
+                            put(k, ahi);
+                            alo = make_float4(0.f, 0.f, 0.f, 0.f);
+                        }
+                        ahi = make_float4(0.f, 0.f, 0.f, 0.f);
+                        k = kj;
+                    }
+                    const float cl = __int_as_float(e[u].y), chh = __int_as_float(e[u].z);
+                    alo.x = fmaf(cl, gv[u].x, alo.x);
+                    alo.y = fmaf(cl, gv[u].y, alo.y);
+                    alo.z = fmaf(cl, gv[u].z, alo.z);
+                    alo.w = fmaf(cl, gv[u].w, alo.w);
+                    ahi.x = fmaf(chh, gv[u].x, ahi.x);
+                    ahi.y = fmaf(chh, gv[u].y, ahi.y);
+                    ahi.z = fmaf(chh, gv[u].z, ahi.z);
+                    ahi.w = fmaf(chh, gv[u].w, ahi.w);
                 }
             }
-            while (k <= r1) close_bucket();
+            put(k - 1, alo);
+            put(k, ahi);
         }
         return;
     }
@@ -941,6 +1094,15 @@ static bool bwdq_dot() {
     return on;
 }
 
+// buffer-load forward at D = 64 (PDVC_MSDA_FWDBUF=0 selects the whole-pyramid / per-query kernels: A/B)
+static bool fwd_buf() {
+    static const bool on = [] {
+        const char* e = getenv("PDVC_MSDA_FWDBUF");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 static int pyr_attrs() {
     static int rc = -1;
     if (rc < 0) {
@@ -1007,6 +1169,18 @@ extern "C" int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_
     PDVC_CHECK_ARG(tw < (1L << 31) / 4, "too many rows");
     dim3 grid((unsigned)((tw + 3) / 4));
     hipStream_t s = (hipStream_t)stream;
+    if (head_dim == 64 && fwd_buf() && (long)S * num_heads * head_dim * 4 < (1L << 31)) {
+        if (ref_dim == 1)
+            hipLaunchKernelGGL((msda1d_fwd_buf_kernel<1>), grid, dim3(256), 0, s, value, value_pad_mask, proj,
+                               proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, (int)tw, output,
+                               save_attn, save_loc);
+        else
+            hipLaunchKernelGGL((msda1d_fwd_buf_kernel<2>), grid, dim3(256), 0, s, value, value_pad_mask, proj,
+                               proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, (int)tw, output,
+                               save_attn, save_loc);
+        PDVC_CHECK_LAUNCH("msda1d_fwd_buf_kernel");
+        return PDVC_OK;
+    }
     if (const int qb = pick_pyr(lv, S, num_query, head_dim, kPyrQ)) {
         if ((rc = pyr_attrs())) return rc;
         PDVC_CHECK_ARG((long)batch * num_heads * qb < (1L << 31), "too many query blocks");
@@ -1092,9 +1266,12 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
         }
         int Tmax = 0;
         for (int l = 0; l < kL; ++l) Tmax = lv.T[l] > Tmax ? lv.T[l] : Tmax;
-        const long budget = 96 * 1024 - 8L * (Tmax + 2);
-        if (budget < 12L * kP) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "level length %d too long", Tmax);
-        int qchunk = (int)(budget / (12L * kP));
+        const bool g4 = head_dim == 64 && value_g4() && (long)num_query * num_heads * head_dim * 4 < (1L << 31);
+        const long per_sample = g4 ? 16 : 12;  // LDS bytes per sorted sample
+        const long budget = 96 * 1024 - 8L * (Tmax + 2) - 16;
+        if (budget < per_sample * kP) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "level length %d too long", Tmax);
+        int qchunk = (int)(budget / (per_sample * kP));
+        if (qchunk > kVQPT * kVW * 64) qchunk = kVQPT * kVW * 64;
         if (qchunk > num_query) qchunk = num_query;
         static bool attr = false;
         if (!attr) {  // dynamic LDS <= 96 KiB by construction of qchunk (plus 32 B static)
@@ -1112,9 +1289,10 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
         }
         for (int q0 = 0; q0 < num_query; q0 += qchunk) {
             const int nq = (num_query - q0) < qchunk ? (num_query - q0) : qchunk;
-            const size_t lds = sizeof(int) * (2 * (size_t)(Tmax + 2) + 3 * (size_t)nq * kP);
+            const size_t lds = g4 ? sizeof(int) * (((2 * (size_t)(Tmax + 2) + 3) & ~(size_t)3) + 4 * (size_t)nq * kP)
+                                  : sizeof(int) * (2 * (size_t)(Tmax + 2) + 3 * (size_t)nq * kP);
             const int acc = q0 > 0;
-            if (head_dim == 64 && value_g4())
+            if (g4)
                 hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
                                    value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
                                    save_attn, save_loc, grad_value);

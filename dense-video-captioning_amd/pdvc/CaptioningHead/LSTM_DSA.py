@@ -231,13 +231,14 @@ class LSTMDSACaptioner(Captioner):
         if n_steps == 0:
             empty = hs_rows.new_zeros(hs_rows.shape[0], 0, self.vocab_size + 1)
             return empty if pick_target is None else (empty, hs_rows.new_zeros(hs_rows.shape[0], 0))
-        xt = embed_rows(self.embed, seq[:, :n_steps])  # (R, n, E)
-        xg = F.linear(xt, w["W_x"]) + F.linear(hs_rows, w["W_hs"])[:, None]  # loop-invariant gate parts
+        xt = embed_rows(self.embed, seq[:, :n_steps].t())  # (n, R, E): step-major, the recurrence's layout
+        xe = F.linear(xt, w["W_x"])  # loop-invariant gate parts: word part per step, event part per row
+        hs_g = F.linear(hs_rows, w["W_hs"])
         off_hs = F.linear(hs_rows, w["W_off_hs"], w["b_off"])
         Nv, S, _ = value.shape
         M = core.deformable_att.n_heads
         Hs = CaptionDecodeFunction.apply(
-            value.view(Nv, S, M, -1), xg, off_hs, ref_rows, w["W_h"], w["b_h"], core.ctx2att.weight,
+            value.view(Nv, S, M, -1), xe, hs_g, off_hs, ref_rows, w["W_h"], w["b_h"], core.ctx2att.weight,
             core.ctx2att.bias, core.alpha_net.weight.view(-1), core.alpha_net.bias, w["W_att"], mask_u8, row_video,
             tuple(level_T), rd1_rows, video_csr)
         logits = self.logit(self.dropout(Hs))

@@ -6,10 +6,12 @@ Captioner.forward (LSTM_DSA.py:55-109).  Per step and row (h, c start at zero):
     clip    = border samples of value at  ref (+) (hp[:, :16] + off_hs)          (cap-gather kernel)
     att     = ctx2att(clip)                                                      (one GEMM, R*16 rows)
     res     = sum_j softmax_j(alpha_net(tanh(att_j + hp[:, h2att]))) clip_j      (soft-attention kernel)
-    gates   = xg_t + W_att res + hp[:, W_hh]                                     (one GEMM + LSTM kernel)
+    gates   = xe_t + W_att res + hp[:, W_hh] + W_hs hs                           (one GEMM + LSTM kernel)
     h, c    = LSTM cell(gates, c)
-xg_t = W_x embed(token_t) + W_hs hs and off_hs = W_off_hs hs + b_off are loop invariants computed by the
-caller (with autograd).  Autograd of the stock modules issues ~25 kernels per step forward and ~50
+xe_t = W_x embed(token_t) (step-major, (n, R, 4H)), hs_g = W_hs hs and off_hs = W_off_hs hs + b_off are loop
+invariants computed by the caller (with autograd); hs_g is the LSTM kernel's fourth addend, so the (R, n, 4H)
+sum xe + hs_g is never formed, and xe's gradient is returned as a view of the step-major
+gate gradients (no transposing copy).  Autograd of the stock modules issues ~25 kernels per step forward and ~50
 backward; here it is 6 launches per step each way, and every weight gradient is ONE GEMM over all steps
 after the backward loop (the per-step activations are kept: ~0.5 MB per row per step at PDVC's shape).
 """
@@ -24,24 +26,26 @@ from .ms_deform_attn_func import NUM_SAMPLES, _levels
 
 
 class CaptionDecodeFunction(Function):
-    """value (Nv,S,M,D) = value_proj(memory); xg (R,n,4H); off_hs (R, M*16); ref (R,L,1|2) (first rd1_rows rows
+    """value (Nv,S,M,D) = value_proj(memory); xe (n,R,4H); hs_g (R,4H); off_hs (R, M*16); ref (R,L,1|2) (first rd1_rows rows
     1-d when 2-wide); W_h (M*16 + A + 4H, H), b_h; W_ctx (A, D), b_ctx (A); alpha_w (A,), alpha_b (1,);
     W_att (4H, M*D).  Returns the hidden states (R, n, H)."""
 
     @staticmethod
-    def forward(ctx, value, xg, off_hs, ref, W_h, b_h, W_ctx, b_ctx, alpha_w, alpha_b, W_att, pad_mask, row_video,
-                level_T, rd1_rows, video_csr=None):
-        value, xg, off_hs, ref = value.contiguous(), xg.contiguous(), off_hs.contiguous(), ref.contiguous()
+    def forward(ctx, value, xe, hs_g, off_hs, ref, W_h, b_h, W_ctx, b_ctx, alpha_w, alpha_b, W_att, pad_mask,
+                row_video, level_T, rd1_rows, video_csr=None):
+        value, xe, off_hs, ref = value.contiguous(), xe.contiguous(), off_hs.contiguous(), ref.contiguous()
+        hs_g = hs_g.contiguous()
         W_h, W_ctx, W_att = W_h.contiguous(), W_ctx.contiguous(), W_att.contiguous()
         alpha_w, alpha_b = alpha_w.contiguous(), alpha_b.contiguous()
         Nv, S, M, D = value.shape
-        R, n, G = xg.shape
+        n, R, G = xe.shape
         H = G // 4
         A = W_ctx.shape[0]
         NS = NUM_SAMPLES
         n_off = M * NS
         Ph = W_h.shape[0]
-        if Ph != n_off + A + G or W_att.shape != (G, M * D) or off_hs.shape != (R, n_off):
+        if (Ph != n_off + A + G or W_att.shape != (G, M * D) or off_hs.shape != (R, n_off)
+                or hs_g.shape != (R, G)):
             raise ValueError("caption decode: inconsistent weight shapes")
         RD = ref.shape[2]
         lvl, nl = _levels(level_T)
@@ -72,10 +76,10 @@ class CaptionDecodeFunction(Function):
                 _n.call("pdvc_softattn_forward_f32", _n.ptr(ATT[i]), ah, ldh, _n.ptr(alpha_w), _n.ptr(alpha_b),
                         _n.ptr(CLIP[i]), R, M, A, D, _n.ptr(RES[i]), _n.ptr(PROBS[i]), st)
                 torch.mm(RES[i], W_att.t(), out=GATT)
-                xa, ldx = _n.rows(xg[:, i])
+                xa, ldx = _n.rows(xe[i])
                 gh, ldg = _n.rows(HP[i][:, n_off + A:])
                 ho, ldo = _n.rows(HS[:, i])
-                _n.call("pdvc_lstm_cell_forward_f32", xa, ldx, _n.ptr(GATT), G, gh, ldg,
+                _n.call("pdvc_lstm_cell_forward_f32", xa, ldx, _n.ptr(GATT), G, gh, ldg, _n.ptr(hs_g), G,
                         _n.ptr(CS[i - 1] if i > 0 else zero), R, H, ho, ldo, _n.ptr(CS[i]), _n.ptr(ACTS[i]), st)
         ctx.save_for_backward(value, off_hs, ref, W_h, W_ctx, alpha_w, W_att, pad_mask, row_video, HP, CLIP, LOC,
                               ATT, PROBS, RES, ACTS, CS, HS)
@@ -140,8 +144,8 @@ class CaptionDecodeFunction(Function):
             _n.call("pdvc_cap_value_grad_f32", _n.ptr(pad_mask), lvl, nl, Nv, M, D, NS // nl, R, n, int(max_rows),
                     _n.ptr(vr_start), _n.ptr(vr_rows), _n.ptr(LOC), _n.ptr(dCLIP_all), _n.ptr(gv), st)
         # weight gradients: one GEMM each over every (step, row)
-        d_gates = dHP[..., n_off + A:]                       # (n, R, 4H), row stride Ph
-        d_xg = d_gates.permute(1, 0, 2).contiguous()
+        d_gates = dHP[..., n_off + A:]                       # (n, R, 4H), row stride Ph: xe's gradient as is
+        d_hs_g = d_gates.sum(0)
         d_off_hs = dHP[..., :n_off].sum(0)
         if n > 1:
             dW_h = wgrad_mm(dHP[1:].reshape(-1, Ph), HS[:, :-1].transpose(0, 1).reshape(-1, H))
@@ -154,5 +158,5 @@ class CaptionDecodeFunction(Function):
         dalpha_w = colsum(GAW.view(-1, A))
         dalpha_b = GAB.sum().reshape(1)
         dW_att = wgrad_mm(d_gates.reshape(-1, G), RES.view(-1, M * D))
-        return (gv, d_xg, d_off_hs, gr, dW_h, db_h, dW_ctx, db_ctx, dalpha_w, dalpha_b, dW_att, None, None, None,
-                None, None)
+        return (gv, d_gates, d_hs_g, d_off_hs, gr, dW_h, db_h, dW_ctx, db_ctx, dalpha_w, dalpha_b, dW_att, None, None,
+                None, None, None)

@@ -106,7 +106,8 @@ def msda1d_forward(value, pad_mask, proj, ref, level_T, off_base, logit_base, sa
     out = torch.empty((N, Lq, M * D), dtype=value.dtype, device=value.device)
     save_attn = save_loc = None
     if save:
-        save_attn = torch.empty((N, Lq, M, NUM_SAMPLES), dtype=value.dtype, device=value.device)
+        # level-major (N, M, L, Lq, P): the kernels' layout (include/pdvc_msda.h)
+        save_attn = torch.empty((N, M, nl, Lq, NUM_SAMPLES // nl), dtype=value.dtype, device=value.device)
         save_loc = torch.empty_like(save_attn)
     _n.call("pdvc_msda1d_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(proj), C, off_base, logit_base,
             _n.ptr(ref), RD, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(out), _n.ptr(save_attn),

@@ -126,8 +126,8 @@ int pdvc_ms_deform_sample_backward_f32(const float* value, const int64_t* spatia
  * may be NULL; proj (N,Lq,proj_stride) holds the sampling_offsets logits at [off_base + m*L*P + l*P + p]
  * and the attention_weights logits at [logit_base + ...]; ref (N,Lq,L,ref_dim), ref_dim 1 (centre) or
  * 2 (centre, length) -- ms_deform_attn.py:171-177; level_T host (L,) temporal lengths, S = sum(level_T).
- * output (N,Lq,M*D).  save_attn / save_loc (N,Lq,M,L*P): softmaxed weights and sampling locations for
- * the backward (may be NULL in inference).  Supported: L*P == 16, D in {16,32,64,128}. */
+ * output (N,Lq,M*D).  save_attn / save_loc (N,M,L,Lq,P), level-major: softmaxed weights and sampling
+ * locations for the backward (may be NULL in inference).  Supported: L*P == 16, D in {16,32,64,128}. */
 int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_pad_mask, const float* proj,
                             int proj_stride, int off_base, int logit_base, const float* ref, int ref_dim,
                             const int32_t* level_T, int num_levels, int batch, int num_query,
@@ -210,10 +210,11 @@ int pdvc_softattn_backward_f32(const float* att, const float* att_h, int ld_att_
                                int num_heads, int att_hid, int head_dim, float* grad_att, float* grad_att_h,
                                int ld_grad_att_h, float* grad_clip, float* grad_alpha_w_part,
                                float* grad_alpha_b_part, void* stream);
-/* lstm cell: gates = gates_a + gates_b + gates_c (rows x 4*hidden, each with its own row stride; b/c may be
- * NULL), order (i,f,g,o); c_out = f*c_prev + i*g; h_out = o*tanh(c_out) (row stride ld_h_out); acts (R,4H). */
+/* lstm cell: gates = gates_a + gates_b + gates_c + gates_d (rows x 4*hidden, each with its own row stride;
+ * b/c/d may be NULL), order (i,f,g,o); c_out = f*c_prev + i*g; h_out = o*tanh(c_out) (row stride ld_h_out);
+ * acts (R,4H). */
 int pdvc_lstm_cell_forward_f32(const float* gates_a, int lda, const float* gates_b, int ldb, const float* gates_c,
-                               int ldc, const float* c_prev, int rows, int hidden, float* h_out, int ld_h_out,
+                               int ldc, const float* gates_d, int ldd, const float* c_prev, int rows, int hidden, float* h_out, int ld_h_out,
                                float* c_out, float* acts, void* stream);
 /* grad_gates (R, ld_grad_gates >= 4H; the first 4H columns written), grad_c_prev (R,H) from grad_h (+ grad_h2
  * if not NULL) and grad_c_next (or NULL). */

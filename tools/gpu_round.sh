@@ -34,7 +34,7 @@ if has tests; then
       > "$OUT/pytest_gpu.log" 2>&1
   rc=$?
   if [ $rc -eq 0 ]; then  # the per-query MSDA kernels (whole-pyramid ones off) against the oracle too
-    PDVC_MSDA_PYR=0 PDVC_MSDA_G4=0 PDVC_MSDA_BWDQ=0 timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -m gpu -x -q --timeout 120 \
+    PDVC_MSDA_PYR=0 PDVC_MSDA_G4=0 PDVC_MSDA_BWDQ=0 PDVC_MSDA_FWDBUF=0 timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -m gpu -x -q --timeout 120 \
         --timeout-method thread -k msda1d > "$OUT/pytest_gpu_perquery.log" 2>&1
     rc=$?
     tail -1 "$OUT/pytest_gpu_perquery.log"
