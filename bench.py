@@ -458,11 +458,21 @@ def main():
             with open(tfile) as f:
                 traffic = json.load(f).get("avg_bytes_per_launch")
             tsrc = os.path.relpath(tfile, ROOT)
-        result["roofline_gather"] = {"kernel": "msda1d_fwd_kernel (fused MSDeformAttn forward)", "bound": "hbm",
+        result["roofline_gather"] = {"kernel": "msda1d_fwd_buf_kernel (fused MSDeformAttn forward)", "bound": "hbm",
                               "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                               "traffic": traffic, "traffic_source": tsrc, "avg_launch_us": avg_ms * 1e3,
                               "timing": timing_note,
                               "alg_bytes_per_launch": avg_bytes}
+    kname = "pdvc_msda1d_backward_f32"  # the same for the backward (query-side + value-side kernels per launch)
+    if kname in ks and ks[kname]["launches"]:
+        k = ks[kname]
+        avg_ms = k["ms"] / k["launches"]
+        avg_bytes = sum(msda_alg_bytes(m, "bwd") for m in k["metas"]) / k["launches"]
+        ach = avg_bytes / (avg_ms * 1e-3) / 1e9
+        result["roofline_gather_bwd"] = {
+            "kernel": "msda1d_bwd_query_dot_kernel + msda1d_bwd_value_kernel (fused MSDeformAttn backward)",
+            "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "traffic": None, "avg_launch_us": avg_ms * 1e3, "timing": timing_note, "alg_bytes_per_launch": avg_bytes}
     if a.frontend and ks.get("pdvc_seq_attention_forward_f32", {}).get("launches"):
         # front-end attention core (csrc/seqattn.hip): 4*T*T*E flops per video forward (scores + P.V over all
         # heads), 10*T*T*E backward (scores recomputed, dP, dQ, dK, dV), against the fp32 MFMA peak
