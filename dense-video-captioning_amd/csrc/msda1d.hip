@@ -21,6 +21,7 @@
 //     exactly one writer.
 //   * blocks are XCD-remapped so that all blocks of one video run on one XCD and share its L2.
 #include <cstdlib>
+#include <type_traits>
 
 #include "pdvc_common.h"
 
@@ -389,26 +390,27 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
     VecF<4> acc[kPyrQPS];
 #pragma unroll
     for (int i = 0; i < kPyrQPS; ++i) acc[i].zero();
-#pragma unroll 1
-    for (int l = 0; l < kL; ++l) {  // rolled: keeps each level's address math out of the others' registers
-        if (l == 0) {  // level 0 was staged before the parameter math
-            __syncthreads();
-        } else if (l == 1) {  // levels 1..3 in one round trip
-            __syncthreads();
-            pyr_stage(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3], 0);
-            __syncthreads();
-        }
-        const int T = lvl_sel(lv.T, l), base = pyr_base(lv, l);
+    // one level of every query of the lane group: the sample parameters come from their owner lanes by DPP
+    // row_newbcast (a VALU modifier, so the LDS pipe serves only the corner-row reads); the level is a compile-time
+    // constant, which the DPP pattern needs
+    float4 tok = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto level = [&](auto Lc) {
+        constexpr int L = decltype(Lc)::value;
+        const int T = lv.T[L], base = pyr_base(lv, L);
 #pragma unroll
         for (int i = 0; i < kPyrQPS; ++i) {
             VecF<4> v1[kP], v2[kP];
             float c1[kP], c2[kP];
+            // this query's broadcasts depend (opaquely) on the previous query's sums: without it the compiler hoists
+            // every broadcast and LDS read of the level and spills (1 563 spilled VGPRs)
+            int iv = i0v[i];
+            float wa = w1v[i], wb = w2v[i];
+            __asm__ volatile("" : "+v"(iv), "+v"(wa), "+v"(wb) : "v"(tok.x), "v"(tok.y), "v"(tok.z), "v"(tok.w));
 #pragma unroll
             for (int p = 0; p < kP; ++p) {
-                const int src = gbase + l * kP + p;  // l is a runtime level index here: ds_bpermute
-                const int i0 = __shfl(i0v[i], src, PDVC_WAVE);
-                c1[p] = __shfl(w1v[i], src, PDVC_WAVE);
-                c2[p] = __shfl(w2v[i], src, PDVC_WAVE);
+                const int i0 = grp_bcast<16>(iv, L * kP + p);
+                c1[p] = grp_bcast<16>(wa, L * kP + p);
+                c2[p] = grp_bcast<16>(wb, L * kP + p);
                 const int a1 = min(max(i0, 0), T - 1), a2 = min(max(i0 + 1, 0), T - 1);
                 const float4 t1 = lds4[(base + a1) * 16 + sub], t2 = lds4[(base + a2) * 16 + sub];
                 v1[p].v[0] = t1.x; v1[p].v[1] = t1.y; v1[p].v[2] = t1.z; v1[p].v[3] = t1.w;
@@ -419,9 +421,17 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
 #pragma unroll
                 for (int c = 0; c < 4; ++c) acc[i].v[c] += c1[p] * v1[p].v[c] + c2[p] * v2[p].v[c];
             }
-            __builtin_amdgcn_sched_barrier(0);  // one query's 8 LDS reads in flight at a time: no spills
+            tok = make_float4(acc[i].v[0], acc[i].v[1], acc[i].v[2], acc[i].v[3]);
         }
-    }
+    };
+    __syncthreads();  // level 0 was staged before the parameter math
+    level(std::integral_constant<int, 0>{});
+    __syncthreads();  // levels 1..3 in one round trip
+    pyr_stage(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3], 0);
+    __syncthreads();
+    level(std::integral_constant<int, 1>{});
+    level(std::integral_constant<int, 2>{});
+    level(std::integral_constant<int, 3>{});
 #pragma unroll
     for (int i = 0; i < kPyrQPS; ++i) {
         const int q = qb * kPyrQ + slot + 64 * i;
@@ -742,6 +752,155 @@ __global__ __launch_bounds__(256) void msda1d_bwd_query_dot_kernel(
             if (RD == 2) atomicAdd(dst + 1, g1);
         }
     }
+}
+
+// -------------------------------------------------------------------------------------------------
+// Whole-pyramid twin of msda1d_bwd_query_dot_kernel for the encoder (Lq ~ S, D = 64): one 1024-thread workgroup per
+// (video, head, block of up to 960 queries), the head's value rows staged in LDS level by level as in
+// msda1d_fwd_pyr_kernel (level 0, then levels 1..3), every corner row read from LDS (ds_read_b128, 256 B/clk/CU)
+// instead of through L1.  A 16-lane group takes 15 queries in turn; per query the dot-product form, its reduction
+// and the owner-lane math of msda1d_bwd_query_dot_kernel, the sample's row index broadcast by DPP row_newbcast
+// (VALU: the LDS pipe serves only the row reads).  Level 0's owners (lanes 0..3) finish their offset gradient in the
+// first phase and carry dL/da to the second through LDS (15 KiB beside the 128 KiB of rows), where the softmax
+// term of all 16 samples is formed.
+// -------------------------------------------------------------------------------------------------
+constexpr int kBqQPS = 15;                                   // queries per 16-lane group
+constexpr int kBqQ = (kPyrThreads / 16) * kBqQPS;            // 960 queries per workgroup
+constexpr size_t kBqLds = kPyrLds + (size_t)kBqQ * 4 * sizeof(float);
+
+template <int RD>
+__global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
+    const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
+    int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
+    int qblocks, const float* __restrict__ gout, const float* __restrict__ save_attn,
+    const float* __restrict__ save_loc, float* __restrict__ grad_proj, float* __restrict__ grad_ref) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds4[];
+    float* carry = reinterpret_cast<float*>(lds4 + kPyrRows * 16);  // [kBqQ][4]: dL/da of level 0's samples
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int qb = blk % qblocks, bm = blk / qblocks;
+    const int b = bm / M, m = bm - b * M;
+    const int slot = threadIdx.x >> 4, sub = threadIdx.x & 15, lane = threadIdx.x & 63;
+    const int MD = M * 64;
+    const float* vsrc = value + (size_t)b * S * MD + (size_t)m * 64;
+    const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
+    const int l_own = sub >> 2, p_own = sub & 3;
+    int T_own = lv.T[0], st_own = lv.start[0];
+#pragma unroll
+    for (int l = 1; l < kL; ++l) {
+        T_own = l_own >= l ? lv.T[l] : T_own;
+        st_own = l_own >= l ? lv.start[l] : st_own;
+    }
+    const float Tf = (float)T_own;
+
+    // one query of this lane group through the levels [L0, L1): the lane's own sample parameters, the dot products
+    // of every sample of those levels from LDS, reduced onto their owner lanes; then the owner math of the lanes
+    // whose level is in range (offset gradient, grad_ref, dL/da)
+    auto run_query = [&](int i, auto L0c, auto L1c) {
+        constexpr int L0 = decltype(L0c)::value, L1 = decltype(L1c)::value;
+        const int q0 = qb * kBqQ + slot + 64 * i;
+        const bool act = q0 < Lq;
+        const int q = act ? q0 : Lq - 1;
+        const size_t row = (size_t)b * Lq + q;
+        const float4 g = *reinterpret_cast<const float4*>(gout + row * MD + (size_t)m * 64 + sub * 4);
+        const size_t si = save_index(b, m, l_own, q, p_own, Lq, M);
+        const float x = save_loc[si] * Tf - 0.5f;
+        const float a = save_attn[si];
+        const bool inside = x > -1.f && x < Tf;
+        const float xf = floorf(inside ? x : 0.f);
+        const int i0 = (int)xf;
+        const float lw = inside ? x - xf : 0.f;
+        float d1 = 0.f, d2 = 0.f;
+#pragma unroll
+        for (int L = L0; L < L1; ++L) {
+            const int T = lv.T[L], base = pyr_base(lv, L);
+            float part[8];
+#pragma unroll
+            for (int p = 0; p < kP; ++p) {
+                const int ib = grp_bcast<16>(i0, L * kP + p);
+                const int a1 = min(max(ib, 0), T - 1), a2 = min(max(ib + 1, 0), T - 1);
+                const float4 u1 = lds4[(base + a1) * 16 + sub], u2 = lds4[(base + a2) * 16 + sub];
+                part[p] = g.x * u1.x + g.y * u1.y + g.z * u1.z + g.w * u1.w;
+                part[4 + p] = g.x * u2.x + g.y * u2.y + g.z * u2.z + g.w * u2.w;
+            }
+            const bool u8 = (lane & 8) != 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float send = u8 ? part[k] : part[k + 4];
+                const float mine = u8 ? part[k + 4] : part[k];
+                part[k] = mine + grp_swap(send, 8);
+            }
+            const bool u2b = (lane & 2) != 0;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const float send = u2b ? part[k] : part[k + 2];
+                const float mine = u2b ? part[k + 2] : part[k];
+                part[k] = mine + grp_swap(send, 2);
+            }
+            const bool u1b = (lane & 1) != 0;
+            const float send = u1b ? part[0] : part[1];
+            const float mine = u1b ? part[1] : part[0];
+            part[0] = mine + grp_swap(send, 1);
+            part[0] += grp_swap(part[0], 4);
+            const float other = grp_swap(part[0], 8);
+            if (l_own == L) {
+                d1 = (L < 2) ? part[0] : other;
+                d2 = (L < 2) ? other : part[0];
+            }
+        }
+        // owner math of the lanes whose sample is in this phase (.cuh:140-170), as msda1d_bwd_query_dot_kernel
+        const bool mine_phase = l_own >= L0 && l_own < L1;
+        bool ok1 = inside && i0 >= 0, ok2 = inside && i0 + 1 <= T_own - 1;
+        if (mbase) {
+            ok1 = ok1 && !mbase[st_own + min(max(i0, 0), T_own - 1)];
+            ok2 = ok2 && !mbase[st_own + min(max(i0 + 1, 0), T_own - 1)];
+        }
+        const float x1 = ok1 ? d1 : 0.f, x2 = ok2 ? d2 : 0.f;
+        float ga = (1.f - lw) * x1 + lw * x2;
+        const float gloc = Tf * ((x2 - x1) * a);
+        const float* prow = proj + row * proj_stride;
+        float* gprow = grad_proj + row * proj_stride;
+        float g0 = mine_phase ? gloc : 0.f, g1 = 0.f, goff;
+        if (RD == 1) {
+            goff = gloc / Tf;
+        } else {
+            const float rr1 = ref[(row * kL + l_own) * 2 + 1];
+            const float t2 = gloc * 0.5f;
+            goff = (t2 * rr1) / (float)kP;
+            g1 = mine_phase ? t2 * (prow[off_base + m * kNS + sub] / (float)kP) : 0.f;
+        }
+        if (act && mine_phase) gprow[off_base + m * kNS + sub] = goff;
+        if (grad_ref) {  // per (query, level): the lane quad of the level; heads differ by workgroup: atomics
+            g0 += grp_swap(g0, 1);
+            g0 += grp_swap(g0, 2);
+            if (RD == 2) {
+                g1 += grp_swap(g1, 1);
+                g1 += grp_swap(g1, 2);
+            }
+            if (p_own == 0 && act && mine_phase) {
+                float* dst = grad_ref + (row * kL + l_own) * RD;
+                atomicAdd(dst, g0);
+                if (RD == 2) atomicAdd(dst + 1, g1);
+            }
+        }
+        const int ci = (slot + 64 * i) * 4 + p_own;
+        if (L0 == 0) {  // first phase: level 0's owners carry dL/da to the second
+            if (l_own == 0) carry[ci] = ga;
+        } else {  // second phase: the softmax term over all 16 samples, then every logit gradient
+            if (l_own == 0) ga = carry[ci];
+            const float delta = group_allreduce<16>(a * ga);
+            if (act) gprow[logit_base + m * kNS + sub] = a * (ga - delta);
+        }
+    };
+
+    pyr_stage(lds4, vsrc, MD, lv.start[0], lv.T[0], 0);
+    __syncthreads();
+#pragma unroll 1
+    for (int i = 0; i < kBqQPS; ++i) run_query(i, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+    __syncthreads();
+    pyr_stage(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3], 0);
+    __syncthreads();
+#pragma unroll 1
+    for (int i = 0; i < kBqQPS; ++i) run_query(i, std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{});
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -1085,13 +1244,29 @@ static bool value_g4() {
     return on;
 }
 
-// dot-product backward-query kernel at D = 64 (PDVC_MSDA_BWDQ=0 selects msda1d_bwd_query_kernel: A/B)
-static bool bwdq_dot() {
-    static const bool on = [] {
+// backward-query kernel at D = 64: PDVC_MSDA_BWDQ=0 msda1d_bwd_query_kernel, 2 msda1d_bwd_query_dot_kernel
+// everywhere, anything else (default) the whole-pyramid twin where it applies (encoder: 630 vs 680 us at 256
+// videos, tools/msda_ab.sh) and the dot kernel elsewhere.  PDVC_MSDA_PYR=0 turns both pyramid kernels off.
+static int bwdq_mode() {
+    static const int mode = [] {
         const char* e = getenv("PDVC_MSDA_BWDQ");
-        return !(e && e[0] == '0');
+        return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
     }();
-    return on;
+    return mode;
+}
+
+static int bwdq_pyr_attrs() {
+    static int rc = -1;
+    if (rc < 0) {
+        const void* ks[2] = {(const void*)msda1d_bwd_query_pyr_kernel<1>, (const void*)msda1d_bwd_query_pyr_kernel<2>};
+        rc = PDVC_OK;
+        for (const void* k : ks)
+            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBqLds) != hipSuccess) {
+                (void)hipGetLastError();
+                rc = pdvc_set_error(PDVC_ERR_LAUNCH, "msda1d_bwd_query_pyr_kernel: cannot raise the LDS limit");
+            }
+    }
+    return rc;
 }
 
 // buffer-load forward at D = 64 (PDVC_MSDA_FWDBUF=0 selects the whole-pyramid / per-query kernels: A/B)
@@ -1169,18 +1344,6 @@ extern "C" int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_
     PDVC_CHECK_ARG(tw < (1L << 31) / 4, "too many rows");
     dim3 grid((unsigned)((tw + 3) / 4));
     hipStream_t s = (hipStream_t)stream;
-    if (head_dim == 64 && fwd_buf() && (long)S * num_heads * head_dim * 4 < (1L << 31)) {
-        if (ref_dim == 1)
-            hipLaunchKernelGGL((msda1d_fwd_buf_kernel<1>), grid, dim3(256), 0, s, value, value_pad_mask, proj,
-                               proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, (int)tw, output,
-                               save_attn, save_loc);
-        else
-            hipLaunchKernelGGL((msda1d_fwd_buf_kernel<2>), grid, dim3(256), 0, s, value, value_pad_mask, proj,
-                               proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, (int)tw, output,
-                               save_attn, save_loc);
-        PDVC_CHECK_LAUNCH("msda1d_fwd_buf_kernel");
-        return PDVC_OK;
-    }
     if (const int qb = pick_pyr(lv, S, num_query, head_dim, kPyrQ)) {
         if ((rc = pyr_attrs())) return rc;
         PDVC_CHECK_ARG((long)batch * num_heads * qb < (1L << 31), "too many query blocks");
@@ -1194,6 +1357,18 @@ extern "C" int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_
                                proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, qb, output,
                                save_attn, save_loc);
         PDVC_CHECK_LAUNCH("msda1d_fwd_pyr_kernel");
+        return PDVC_OK;
+    }
+    if (head_dim == 64 && fwd_buf() && (long)S * num_heads * head_dim * 4 < (1L << 31)) {
+        if (ref_dim == 1)
+            hipLaunchKernelGGL((msda1d_fwd_buf_kernel<1>), grid, dim3(256), 0, s, value, value_pad_mask, proj,
+                               proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, (int)tw, output,
+                               save_attn, save_loc);
+        else
+            hipLaunchKernelGGL((msda1d_fwd_buf_kernel<2>), grid, dim3(256), 0, s, value, value_pad_mask, proj,
+                               proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, (int)tw, output,
+                               save_attn, save_loc);
+        PDVC_CHECK_LAUNCH("msda1d_fwd_buf_kernel");
         return PDVC_OK;
     }
     if (ref_dim == 1)
@@ -1231,7 +1406,21 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
         hipError_t e = zero_async(grad_ref, (size_t)rows * kL * ref_dim, s);
         if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_ref: %s", hipGetErrorString(e));
     }
-    if (tw > 0 && head_dim == 64 && bwdq_dot() && (long)S * num_heads * head_dim * 4 < (1L << 31)) {
+    const int bq_blocks = (tw > 0 && bwdq_mode() == 1) ? pick_pyr(lv, S, num_query, head_dim, kBqQ) : 0;
+    if (bq_blocks > 0) {
+        if ((rc = bwdq_pyr_attrs())) return rc;
+        PDVC_CHECK_ARG((long)batch * num_heads * bq_blocks < (1L << 31), "too many query blocks");
+        dim3 pg((unsigned)(batch * num_heads * bq_blocks));
+        if (ref_dim == 1)
+            hipLaunchKernelGGL((msda1d_bwd_query_pyr_kernel<1>), pg, dim3(kPyrThreads), kBqLds, s, value,
+                               value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv, num_query, S,
+                               num_heads, bq_blocks, grad_output, save_attn, save_loc, grad_proj, grad_ref);
+        else
+            hipLaunchKernelGGL((msda1d_bwd_query_pyr_kernel<2>), pg, dim3(kPyrThreads), kBqLds, s, value,
+                               value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv, num_query, S,
+                               num_heads, bq_blocks, grad_output, save_attn, save_loc, grad_proj, grad_ref);
+        PDVC_CHECK_LAUNCH("msda1d_bwd_query_pyr_kernel");
+    } else if (tw > 0 && head_dim == 64 && bwdq_mode() != 0 && (long)S * num_heads * head_dim * 4 < (1L << 31)) {
         dim3 grid((unsigned)((tw + 3) / 4));
         if (ref_dim == 1)
             hipLaunchKernelGGL((msda1d_bwd_query_dot_kernel<1>), grid, dim3(256), 0, s, value, value_pad_mask, proj,

@@ -49,6 +49,17 @@ __device__ __forceinline__ float lane_swap(float v, int d) {
 template <int G>
 __device__ __forceinline__ int grp_bcast(int v, int k) {
     static_assert(G == 4 || G == 8 || G == 16 || G == 32, "group of 4..32 lanes");
+    if constexpr (G == 16) {
+        // DPP row_newbcast:k (dpp_ctrl 0x150 + k): lane k of each 16-lane row to the whole row, a VALU operand
+        // modifier -- no LDS instruction (tools/probes/dpp_newbcast_probe.hip checks it on gfx950 for every k)
+#define PDVC_NB(K) case K: return __builtin_amdgcn_update_dpp(0, v, 0x150 + (K), 0xF, 0xF, false);
+        switch (k) {
+            PDVC_NB(0) PDVC_NB(1) PDVC_NB(2) PDVC_NB(3) PDVC_NB(4) PDVC_NB(5) PDVC_NB(6) PDVC_NB(7)
+            PDVC_NB(8) PDVC_NB(9) PDVC_NB(10) PDVC_NB(11) PDVC_NB(12) PDVC_NB(13) PDVC_NB(14) PDVC_NB(15)
+            default: return v;
+        }
+#undef PDVC_NB
+    }
     constexpr int and_mask = 0x1F & ~(G - 1);
 #define PDVC_SWZ(K) case K: return __builtin_amdgcn_ds_swizzle(v, and_mask | ((K) << 5));
     switch (k) {

@@ -39,6 +39,12 @@ if has tests; then
     rc=$?
     tail -1 "$OUT/pytest_gpu_perquery.log"
   fi
+  if [ $rc -eq 0 ]; then  # the buffer-load forward / dot backward-query kernels at the encoder shapes too
+    PDVC_MSDA_PYR=0 timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_batch.py -m gpu -x -q \
+        --timeout 120 --timeout-method thread > "$OUT/pytest_gpu_nopyr.log" 2>&1
+    rc=$?
+    tail -1 "$OUT/pytest_gpu_nopyr.log"
+  fi
   tail -3 "$OUT/pytest_gpu.log"
   if [ $rc -ne 0 ]; then echo "pytest failed rc=$rc"; grep -E "FAILED|Error" "$OUT/pytest_gpu.log" | head -30; exit $rc; fi
   echo "[$(date +%T)] smoke"
