@@ -687,11 +687,40 @@ def state_dict_keys_full():
          weight_dict_vals=np.asarray(list(criterion.weight_dict.values()), dtype=np.float64))
 
 
+def posembed():
+    """The encoder's positional input as the reference builds it: PositionEmbeddingSine(256, normalize=True) per
+    level on the nearest-interpolated masks (base_encoder.py:54-80, position_encoding.py:20-63), transposed, plus
+    the level embedding, concatenated over levels (deformable_transformer.py:84-112).  Three videos, two padded,
+    T = 64 -> levels 64/32/16/8; the reference's own duration layer (seeded) and a random level embedding."""
+    from misc.detr_utils.misc import NestedTensor
+    from pdvc.position_encoding import PositionEmbeddingSine
+    torch.manual_seed(11)
+    N, T, F_ = 3, 64, 256
+    pe = PositionEmbeddingSine(F_, normalize=True)
+    d = F_ + pe.max_duration
+    mask = torch.zeros(N, T, dtype=torch.bool)
+    mask[1, 40:] = True
+    mask[2, 21:] = True
+    dur = torch.tensor([100.0, 37.0, 12.5])
+    level_embed = torch.randn(4, d)
+    out = []
+    Tl = T
+    for lvl in range(4):
+        m = mask if lvl == 0 else F.interpolate(mask[None].float(), size=(Tl,)).to(torch.bool)[0]
+        src = torch.zeros(N, 8, Tl)
+        pos = pe(NestedTensor(src, m, dur))  # (N, d, Tl)
+        out.append(pos.transpose(1, 2) + level_embed[lvl].view(1, 1, -1))
+        Tl = (Tl + 1) // 2  # kernel-3 / stride-2 / pad-1 conv output length
+    save("posembed_levels", mask=mask.numpy(), duration=dur.numpy(), level_embed=level_embed,
+         dur_w=pe.duration_embed_layer.weight, dur_b=pe.duration_embed_layer.bias,
+         level_T=np.array([64, 32, 16, 8]), lvl_pos=torch.cat(out, 1))
+
+
 if __name__ == "__main__":
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     which = sys.argv[1:] or ["op_reftest", "op_1d", "op_sample", "module_msdeformattn", "module_layers",
                              "module_captioner", "whole_model", "whole_model_batch", "data_ingestion",
-                             "state_dict_keys_full"]
+                             "state_dict_keys_full", "posembed"]
     for w in which:
         globals()[w]()
     for k, v in OUT.items():

@@ -40,3 +40,31 @@ def test_level_pos_rows_matches_per_level_torch(N, T, F_):
     for a, b, name in zip(ga, gb, ("level_embed", "dur.weight", "dur.bias")):
         e = (a - b).abs().max().item()
         assert e <= 1e-4 * (1 + b.abs().max().item()), f"{name}: {e}"
+
+
+def _golden_pyramid(dev):
+    """The reference-generated positional input (tests/golden/make_golden.py::posembed) and our modules loaded
+    with its parameters: PositionEmbeddingSine(256, normalize=True), the nearest-interpolated level masks."""
+    import os
+    import numpy as np
+    import torch.nn.functional as F
+    from pdvc.position_encoding import PositionEmbeddingSine, PyramidPosEmbed
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "posembed_levels.npz"))
+    pe = PositionEmbeddingSine(256, normalize=True).to(dev)
+    with torch.no_grad():
+        pe.duration_embed_layer.weight.copy_(torch.from_numpy(z["dur_w"]))
+        pe.duration_embed_layer.bias.copy_(torch.from_numpy(z["dur_b"]))
+    mask = torch.from_numpy(z["mask"]).to(dev)
+    masks = [mask] + [F.interpolate(mask[None].float(), size=(int(t),)).to(torch.bool)[0] for t in z["level_T"][1:]]
+    pyr = PyramidPosEmbed(pe, masks, torch.from_numpy(z["duration"]).to(dev))
+    return pyr, torch.from_numpy(z["level_embed"]).to(dev), torch.from_numpy(z["lvl_pos"]).to(dev)
+
+
+def test_level_pos_rows_matches_reference_fixture():
+    """The fused kernel against the reference's own PositionEmbeddingSine + level_embed + cat (pinned)."""
+    from pdvc.ops.functions.posembed import level_pos_rows
+    pyr, level_embed, want = _golden_pyramid(DEV)
+    got = level_pos_rows(pyr, level_embed)
+    assert got.shape == want.shape
+    err = (got - want).abs().max().item()
+    assert err <= 1e-5, err
