@@ -566,7 +566,11 @@ static bool use_mfma(int Q, int D) {
 // longer query sets (anet_c3d: Q = 300): the flash-style MFMA kernels of seqattn.hip with this op's key padding
 // mask, dropout mask and scaling (PDVC_MHA_MFMA=0 selects the scalar kernels here too)
 static bool use_flash(int Q, int D) {
-    if (Q <= kMQ || !sq_head_dim_ok(D)) return false;
+    static const int force = [] {  // PDVC_MHA_FLASH=1: the flash route for every Q (A/B against the single-workgroup kernels)
+        const char* e = getenv("PDVC_MHA_FLASH");
+        return (e && e[0] == '1') ? 1 : 0;
+    }();
+    if ((Q <= kMQ && !force) || !sq_head_dim_ok(D)) return false;
     const char* e = getenv("PDVC_MHA_MFMA");
     return !(e && e[0] == '0');
 }

@@ -363,6 +363,61 @@ def test_fused_msda1d_windowed_full_size_vs_oracle(offset_scale, ref_dim):
     close(p.grad, egp, 1e-4, "grad_proj")
 
 
+def _away_from_cell_edges(proj, ref, T_l, M, margin=2e-3):
+    """Nudge the sampling offsets so that no sample's x = loc * T - 0.5 lies within `margin` of an integer: the
+    location gradient T * a * (v[x0 + 1] - v[x0]) . g is a step function of x, so at T = 1024 an fp32 location a few
+    ulps from a cell edge can take the neighbouring cell where the float64 expectation does not (the reference's
+    fp32 CUDA op has the same step) -- a property of the comparison, not of the kernels."""
+    P = 4
+    N, Lq = proj.shape[:2]
+    off = proj[..., :M * 16].reshape(N, Lq, M, len(T_l), P)
+    Tn = np.asarray(T_l, np.float64)[None, None, None, :, None]
+    r0 = ref[:, :, None, :, None, 0]
+    if ref.shape[-1] == 1:
+        x = (r0 + off / Tn) * Tn - 0.5
+        dxdoff = np.ones_like(x)
+    else:
+        r1 = ref[:, :, None, :, None, 1]
+        x = (r0 + off / P * r1 * 0.5) * Tn - 0.5
+        dxdoff = r1 * 0.5 / P * Tn * np.ones_like(x)
+    frac = x - np.floor(x)
+    near = np.minimum(frac, 1.0 - frac) < margin
+    off = off + near * (4 * margin) / dxdoff
+    out = proj.copy()
+    out[..., :M * 16] = off.reshape(N, Lq, M * 16)
+    return out
+
+
+@pytest.mark.parametrize("T_l,ref_dim", [((1024, 512, 256, 128), 1), ((1024, 512, 256, 128), 2),
+                                         ((512, 300, 150, 60), 1), ((512, 300, 150, 60), 2)])
+def test_fused_msda1d_long_pyramids_vs_oracle(T_l, ref_dim):
+    """Long pyramids: anet_c3d's T = 1024 (S = 1920: level 0 too long for the LDS pyramids, so the buffer-load
+    forward and the dot-product backward-query run at Lq = S; the value gradient takes two query chunks, the
+    second accumulating into the rows the first wrote), and S = 1022 (both pyramid kernels with two query blocks)."""
+    from pdvc.ops.functions import MSDA1dFunction
+    rng = np.random.RandomState(sum(T_l) + ref_dim)
+    S = sum(T_l)
+    M, D, N, Lq = 2, 64, 1, S
+    value = rng.randn(N, S, M, D)
+    proj = np.concatenate([rng.randn(N, Lq, M * 16) * 4.0, rng.randn(N, Lq, M * 16)], -1)
+    centre = np.concatenate([(np.arange(t) + 0.5) / t for t in T_l])[None, :, None, None].repeat(4, 2)
+    ref = centre if ref_dim == 1 else np.concatenate([centre, rng.uniform(0.05, 0.5, size=(N, Lq, 4, 1))], -1)
+    proj = _away_from_cell_edges(proj, ref, T_l, M)
+    mask = np.zeros((N, S), bool)
+    mask[0, T_l[0] - 40:T_l[0]] = True
+    gout = rng.randn(N, Lq, M * D)
+    eo, egv, egp, egr = expected_msda1d(value, mask, proj, ref, list(T_l), M, gout)
+    v = cu(value, torch.float32).requires_grad_()
+    p = cu(proj, torch.float32).requires_grad_()
+    r = cu(ref, torch.float32).requires_grad_()
+    out = MSDA1dFunction.apply(v, cu(mask).view(torch.uint8), p, r, tuple(T_l), 0, M * 16)
+    close(out, eo, 1e-4, "out")
+    out.backward(cu(gout, torch.float32))
+    close(v.grad, egv, 1e-4, "grad_value")
+    close(p.grad, egp, 1e-4, "grad_proj")
+    close(r.grad, egr, 1e-4, "grad_ref")
+
+
 def test_fused_msda1d_pyramid_equals_per_query():
     """The whole-pyramid and the per-query forward share their arithmetic (4 * Lq < S sends a query subset to
     the per-query kernel): equal up to FMA contraction."""
