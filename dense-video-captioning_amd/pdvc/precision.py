@@ -26,6 +26,7 @@ once, at capture.  GEMMs below MIN_FLOPS (tiny heads, 1-wide projections) stay f
 Tolerances against the fp32 path: tests/test_gpu_bf16.py and DESIGN.md.
 """
 import contextlib
+import threading
 
 import torch
 from torch.utils._python_dispatch import TorchDispatchMode
@@ -77,7 +78,7 @@ class BF16Matmul(TorchDispatchMode):
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
-        r = self._route(func, args, kwargs)
+        r = NotImplemented if getattr(_FP32, "depth", 0) else self._route(func, args, kwargs)
         return func(*args, **kwargs) if r is NotImplemented else r
 
     @staticmethod
@@ -132,14 +133,20 @@ def bf16_matmul(enabled=True):
         yield
 
 
+_FP32 = threading.local()  # depth > 0 inside fp32_gemms() on this thread: BF16Matmul passes every op through
+
+
 @contextlib.contextmanager
 def fp32_gemms():
     """GEMMs issued inside stay fp32 even under bf16_matmul: for the caption recurrence, whose per-step GEMMs
     feed the next step (bf16 rounding there compounds over the steps) and are small, latency-bound launches
-    with little to win."""
-    from torch.utils._python_dispatch import _disable_current_modes
-    with _disable_current_modes():
+    with little to win.  Only this module's routing is switched off: other dispatch modes (bench.py's GEMM flop
+    count) keep seeing the ops (disabling every mode hid the recurrence's GEMMs from the count)."""
+    _FP32.depth = getattr(_FP32, "depth", 0) + 1
+    try:
         yield
+    finally:
+        _FP32.depth -= 1
 
 
 def routed_summary():
