@@ -215,9 +215,67 @@ __global__ __launch_bounds__(kLpThreads) void logprob_pick_bwd_reg_kernel(const 
     }
 }
 
+// Greedy decoding's word choice (LSTM_DSA.py:149-151: sampleLogprobs, it = torch.max(logprobs, 1) over
+// logprobs = log_softmax(logits)): per row the first index of the largest logit and its log-probability
+// (x_max - max) - log(sum exp(x - max)) = -log(sum exp(x - max)), from ONE read of the logits -- the (rows, V)
+// log_softmax is never written.  One workgroup per row; per lane a running (max, first index) and (max, sum exp)
+// pair, merged over the workgroup (ties to the smaller index, as torch.max).
+__global__ __launch_bounds__(kLpThreads) void logprob_argmax_kernel(const float* __restrict__ x, int V,
+                                                                   int64_t* __restrict__ idx,
+                                                                   float* __restrict__ lp) {
+    __shared__ float red_m[kLpThreads / PDVC_WAVE], red_s[kLpThreads / PDVC_WAVE];
+    __shared__ int red_i[kLpThreads / PDVC_WAVE];
+    const long row = blockIdx.x;
+    const float* xr = x + row * (long)V;
+    float m = -INFINITY, s = 0.f;
+    int bi = 0x7fffffff;
+    for (int i = threadIdx.x; i < V; i += kLpThreads) {
+        const float v = xr[i];
+        if (v > m || bi == 0x7fffffff) bi = i;  // a lane's indices ascend: ties keep the first
+        lse_add(m, s, v);
+    }
+#pragma unroll
+    for (int d = 1; d < PDVC_WAVE; d <<= 1) {
+        const float m2 = lane_swap(m, d), s2 = lane_swap(s, d);
+        const int i2 = __shfl_xor(bi, d, PDVC_WAVE);
+        if (m2 > m || (m2 == m && i2 < bi)) bi = i2;
+        lse_merge(m, s, m2, s2);
+    }
+    const int wave = threadIdx.x / PDVC_WAVE, lane = threadIdx.x % PDVC_WAVE;
+    if (lane == 0) {
+        red_m[wave] = m;
+        red_s[wave] = s;
+        red_i[wave] = bi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = red_m[0];
+        s = red_s[0];
+        bi = red_i[0];
+#pragma unroll
+        for (int w = 1; w < kLpThreads / PDVC_WAVE; ++w) {
+            if (red_m[w] > m || (red_m[w] == m && red_i[w] < bi)) bi = red_i[w];
+            lse_merge(m, s, red_m[w], red_s[w]);
+        }
+        idx[row] = bi;
+        lp[row] = (xr[bi] - m) - logf(s);
+    }
+}
+
 }  // namespace pdvc
 
 using namespace pdvc;
+
+extern "C" int pdvc_logprob_argmax_f32(const float* logits, int rows, int V, int64_t* index, float* logp_max,
+                                       void* stream) {
+    PDVC_CHECK_ARG(rows >= 0 && V > 0, "invalid sizes (rows >= 0, V > 0)");
+    PDVC_CHECK_ARG(rows == 0 || (logits && index && logp_max), "null pointer");
+    if (rows == 0) return PDVC_OK;
+    hipLaunchKernelGGL(logprob_argmax_kernel, dim3((unsigned)rows), dim3(kLpThreads), 0, (hipStream_t)stream, logits,
+                       V, index, logp_max);
+    PDVC_CHECK_LAUNCH("logprob_argmax_kernel");
+    return PDVC_OK;
+}
 
 extern "C" int pdvc_logprob_pick_forward_f32(const float* logits, const int64_t* target, int rows, int V,
                                              float* logp, float* picked, void* stream) {

@@ -26,6 +26,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from pdvc import _native as _n
 from pdvc.ops.functions import CaptionDecodeFunction
 from pdvc.ops.functions.logprob import logprob_pick
 from pdvc.ops.modules import MSDeformAttnCap
@@ -212,6 +213,66 @@ class LSTMDSACaptioner(Captioner):
         gates = x_gates + hs_part + F.linear(att_res, w["W_att"]) + g_hh
         return lstm_cell(gates, c)
 
+    def _fused_step_ok(self, hs_rows, value, w):
+        """The greedy step can run on the teacher-forced recurrence's kernels (the same six launches per step as
+        CaptionDecodeFunction.forward): fp32 GPU rows, float4-aligned widths, a soft-attention hidden layer."""
+        core = self.core
+        M = core.deformable_att.n_heads
+        D = value.shape[-1] // M
+        return (hs_rows.is_cuda and hs_rows.dtype == torch.float32 and value.dtype == torch.float32
+                and w["A"] > 0 and w["A"] % 4 == 0 and D % 4 == 0 and (4 * w["H"]) % 4 == 0
+                and core.deformable_att.fused)
+
+    def _greedy_buffers(self, R, value, w):
+        core = self.core
+        M = core.deformable_att.n_heads
+        D = value.shape[-1] // M
+        Ph = w["W_h"].shape[0]
+        kw = dict(dtype=value.dtype, device=value.device)
+        return dict(HP=torch.empty((R, Ph), **kw), CLIP=torch.empty((R, M, 16, D), **kw),
+                    LOC=torch.empty((R, M, 16), **kw), ATT=torch.empty((R * M * 16, w["A"]), **kw),
+                    PROBS=torch.empty((R, M, 16), **kw), RES=torch.empty((R, M * D), **kw),
+                    GATT=torch.empty((R, 4 * w["H"]), **kw), ACTS=torch.empty((R, 4 * w["H"]), **kw),
+                    H=[torch.empty((R, w["H"]), **kw) for _ in range(2)],
+                    C=[torch.empty((R, w["H"]), **kw) for _ in range(2)])
+
+    def _step_fused(self, w, b, t, h, c, x_gates, hs_part, off_hs, value, mask_u8, row_video, ref_rows, rd1_rows,
+                    level_T):
+        """One decoder step for all rows on the fused kernels of the teacher-forced recurrence
+        (ops/functions/caption_decode.py): h-projection GEMM, border sampling at ref (+) (hp offsets + off_hs),
+        ctx2att GEMM, soft attention (tanh, alpha_net, softmax over the 16 samples, weighted sum), the attention
+        gate GEMM and the LSTM cell with the four gate addends -- LSTM_DSA.py:231-263, as _step."""
+        from pdvc import _native as _n
+        from pdvc.ops.functions.ms_deform_attn_func import NUM_SAMPLES, _levels
+        core = self.core
+        Nv, S, E = value.shape
+        M = core.deformable_att.n_heads
+        D = E // M
+        R, H = h.shape
+        G = 4 * H
+        n_off, A = w["n_off"], w["A"]
+        Ph = w["W_h"].shape[0]
+        lvl, nl = _levels(level_T)
+        st = _n.stream()
+        HP = b["HP"]
+        torch.addmm(w["b_h"], h, w["W_h"].t(), out=HP)
+        ref = ref_rows.contiguous()
+        _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(mask_u8), _n.ptr(row_video), _n.ptr(HP), Ph, 0,
+                _n.ptr(off_hs.contiguous()), _n.ptr(ref), ref.shape[2], int(rd1_rows), lvl, nl, Nv, R, M, D,
+                NUM_SAMPLES // nl, _n.ptr(b["CLIP"]), _n.ptr(b["LOC"]), st)
+        torch.addmm(core.ctx2att.bias, b["CLIP"].view(-1, D), core.ctx2att.weight.t(), out=b["ATT"])
+        ah, ldh = _n.rows(HP[:, n_off:n_off + A])
+        _n.call("pdvc_softattn_forward_f32", _n.ptr(b["ATT"]), ah, ldh, _n.ptr(core.alpha_net.weight.view(-1)),
+                _n.ptr(core.alpha_net.bias), _n.ptr(b["CLIP"]), R, M, A, D, _n.ptr(b["RES"]), _n.ptr(b["PROBS"]), st)
+        torch.mm(b["RES"], w["W_att"].t(), out=b["GATT"])
+        xg = x_gates.contiguous()
+        gh, ldg = _n.rows(HP[:, n_off + A:])
+        h_out, c_out = b["H"][t % 2], b["C"][t % 2]
+        _n.call("pdvc_lstm_cell_forward_f32", _n.ptr(xg), G, _n.ptr(b["GATT"]), G, gh, ldg,
+                _n.ptr(hs_part.contiguous()), G, _n.ptr(c.contiguous()), R, H, _n.ptr(h_out), H, _n.ptr(c_out),
+                _n.ptr(b["ACTS"]), st)
+        return h_out, c_out
+
     def decode_teacher_forced(self, hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten, level_T, seq,
                               n_steps, video_csr=None, pick_target=None):
         """hs_rows (R, d) event features; ref_rows (R, L, 2) references (rows < rd1_rows are 1-d: centre in
@@ -262,12 +323,21 @@ class LSTMDSACaptioner(Captioner):
         off_hs = F.linear(hs_rows, w["W_off_hs"], w["b_off"])
         h = hs_rows.new_zeros(R, w["H"])
         c = hs_rows.new_zeros(R, w["H"])
+        fused = self._fused_step_ok(hs_rows, value, w)
+        if fused:
+            value = value.contiguous()
+            step_bufs = self._greedy_buffers(R, value, w)
         it = torch.zeros(R, dtype=torch.long, device=hs_rows.device)
         seq, seqlp = [], []
         unfinished = None
         for t in range(max_len + 1):
             if t > 0:
-                if sample_max:
+                if sample_max and logprobs is None:  # fused: argmax and its log-probability from the logits
+                    sample_lp = torch.empty(R, dtype=logits.dtype, device=logits.device)
+                    it = torch.empty(R, dtype=torch.long, device=logits.device)
+                    _n.call("pdvc_logprob_argmax_f32", _n.ptr(logits), R, logits.shape[1], _n.ptr(it),
+                            _n.ptr(sample_lp), _n.stream())
+                elif sample_max:
                     sample_lp, it = torch.max(logprobs, 1)
                 else:
                     prob = torch.exp(logprobs if temperature == 1.0 else torch.div(logprobs, temperature))
@@ -275,9 +345,15 @@ class LSTMDSACaptioner(Captioner):
                     sample_lp = logprobs.gather(1, it)
                     it = it.view(-1)
             x_gates = F.linear(self.embed(it), w["W_x"])
-            h, c = self._step(w, h, c, x_gates, hs_part, off_hs, value, mask_u8, row_video, ref_rows, rd1_rows,
-                              level_T)
-            logprobs = F.log_softmax(self.logit(self.dropout(h)), dim=1)
+            if fused:
+                h, c = self._step_fused(w, step_bufs, t, h, c, x_gates, hs_part, off_hs, value, mask_u8, row_video,
+                                        ref_rows, rd1_rows, level_T)
+            else:
+                h, c = self._step(w, h, c, x_gates, hs_part, off_hs, value, mask_u8, row_video, ref_rows, rd1_rows,
+                                  level_T)
+            logits = self.logit(self.dropout(h))
+            # greedy on the fused path needs only each row's argmax and its log-probability (pdvc_logprob_argmax_f32)
+            logprobs = None if (fused and sample_max) else F.log_softmax(logits, dim=1)
             if t >= 1:
                 unfinished = (it > 0) if t == 1 else (unfinished & (it > 0))
                 if int(unfinished.sum()) == 0:

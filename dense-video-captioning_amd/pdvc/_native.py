@@ -42,6 +42,7 @@ SIGNATURES = {
     "pdvc_relu_dropout_backward_f32": [_vp, _vp, _i, _i, _f, _i, _vp, _vp, _vp],
     "pdvc_logprob_pick_forward_f32": [_vp, _vp, _i, _i, _vp, _vp, _vp],
     "pdvc_logprob_pick_backward_f32": [_vp, _vp, _vp, _i, _i, _vp, _vp],
+    "pdvc_logprob_argmax_f32": [_vp, _i, _i, _vp, _vp, _vp],
     "pdvc_seq_attention_forward_f32": [_vp, ctypes.c_long, _vp, ctypes.c_long, _vp, ctypes.c_long] + [_i] * 5
     + [_vp, _vp, _vp],
     "pdvc_seq_attention_backward_f32": [_vp, ctypes.c_long, _vp, ctypes.c_long, _vp, ctypes.c_long, _vp, _vp, _vp]

@@ -316,6 +316,10 @@ int pdvc_logprob_pick_forward_f32(const float* logits, const int64_t* target, in
                                   float* picked, void* stream);
 int pdvc_logprob_pick_backward_f32(const float* logp, const int64_t* target, const float* grad_picked, int rows,
                                    int V, float* grad_logits, void* stream);
+/* greedy decoding's word choice (LSTM_DSA.py:149-151, torch.max over log_softmax(logits)): index[r] = the first index
+ * of the largest logit of row r, logp_max[r] = its log-probability (x_max - max) - log(sum exp(x - max)); one read
+ * of the logits, the (rows, V) log-probabilities are not written. */
+int pdvc_logprob_argmax_f32(const float* logits, int rows, int V, int64_t* index, float* logp_max, void* stream);
 
 /* ---- long-sequence attention core (dual-modality front-end, cfgs/yc2_newModel_sound) --------------------
  * Replaces the core of the two nn.MultiheadAttention(768, 32, batch_first=True) calls of NewModel
