@@ -33,6 +33,11 @@ from pdvc.ops.modules import MSDeformAttnCap
 from pdvc.ops.modules.linear import Linear
 
 
+# greedy decoding: ctx2att of the samples as a gather of the once-projected memory rows (LSTMDSACaptioner.
+# _ctx2att_rows) instead of a GEMM per step; False keeps the GEMM (tests compare the two)
+GREEDY_CTX2ATT_GATHER = True
+
+
 class _EmbeddingRows(torch.autograd.Function):
     """nn.Embedding's lookup with an atomic scatter-add backward (index_add_).  torch's embedding backward
     sorts the indices and runs rocprim unique-by-key/partition passes; replayed inside a captured hipGraph
@@ -236,12 +241,30 @@ class LSTMDSACaptioner(Captioner):
                     H=[torch.empty((R, w["H"]), **kw) for _ in range(2)],
                     C=[torch.empty((R, w["H"]), **kw) for _ in range(2)])
 
+    def _ctx2att_rows(self, value, mask_u8):
+        """ctx2att of every memory position, once per decode: U = ctx2att(value masked to 0 at padding), (Nv, S, M, A).
+        A sample is a border-clamped bilinear blend of value rows whose weights sum to 1, so ctx2att(sample) =
+        W (sum_k w_k v_k) + b = sum_k w_k (W v_k + b): the same blend of U rows -- one gather per step instead of
+        a (rows x 16) x D x A GEMM per step (LSTM_DSA.py:245: att = self.ctx2att(clip)).  Padded rows are zeroed
+        before the projection (their U row is the bias), which reproduces the kernel's zero contribution of a
+        padded corner to the sample while the blend weights keep summing to 1."""
+        core = self.core
+        Nv, S, E = value.shape
+        M = core.deformable_att.n_heads
+        D = E // M
+        v = value.view(Nv, S, M, D)
+        if mask_u8 is not None:
+            v = v.masked_fill(mask_u8.view(Nv, S, 1, 1).bool(), 0.0)
+        U = torch.addmm(core.ctx2att.bias, v.reshape(-1, D), core.ctx2att.weight.t())
+        return U.view(Nv, S, M, -1)
+
     def _step_fused(self, w, b, t, h, c, x_gates, hs_part, off_hs, value, mask_u8, row_video, ref_rows, rd1_rows,
                     level_T):
         """One decoder step for all rows on the fused kernels of the teacher-forced recurrence
         (ops/functions/caption_decode.py): h-projection GEMM, border sampling at ref (+) (hp offsets + off_hs),
-        ctx2att GEMM, soft attention (tanh, alpha_net, softmax over the 16 samples, weighted sum), the attention
-        gate GEMM and the LSTM cell with the four gate addends -- LSTM_DSA.py:231-263, as _step."""
+        ctx2att as a second gather of the pre-projected rows U, soft attention (tanh, alpha_net, softmax over the
+        16 samples, weighted sum), the attention gate GEMM and the LSTM cell with the four gate addends --
+        LSTM_DSA.py:231-263, as _step."""
         from pdvc import _native as _n
         from pdvc.ops.functions.ms_deform_attn_func import NUM_SAMPLES, _levels
         core = self.core
@@ -260,7 +283,12 @@ class LSTMDSACaptioner(Captioner):
         _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(mask_u8), _n.ptr(row_video), _n.ptr(HP), Ph, 0,
                 _n.ptr(off_hs.contiguous()), _n.ptr(ref), ref.shape[2], int(rd1_rows), lvl, nl, Nv, R, M, D,
                 NUM_SAMPLES // nl, _n.ptr(b["CLIP"]), _n.ptr(b["LOC"]), st)
-        torch.addmm(core.ctx2att.bias, b["CLIP"].view(-1, D), core.ctx2att.weight.t(), out=b["ATT"])
+        if b["U"] is not None:  # att = ctx2att(clip) as the same sample blend of the projected rows U, no mask
+            _n.call("pdvc_cap_gather_forward_f32", _n.ptr(b["U"]), None, _n.ptr(row_video), _n.ptr(HP), Ph, 0,
+                    _n.ptr(off_hs.contiguous()), _n.ptr(ref), ref.shape[2], int(rd1_rows), lvl, nl, Nv, R, M, A,
+                    NUM_SAMPLES // nl, _n.ptr(b["ATT"]), None, st)
+        else:
+            torch.addmm(core.ctx2att.bias, b["CLIP"].view(-1, D), core.ctx2att.weight.t(), out=b["ATT"])
         ah, ldh = _n.rows(HP[:, n_off:n_off + A])
         _n.call("pdvc_softattn_forward_f32", _n.ptr(b["ATT"]), ah, ldh, _n.ptr(core.alpha_net.weight.view(-1)),
                 _n.ptr(core.alpha_net.bias), _n.ptr(b["CLIP"]), R, M, A, D, _n.ptr(b["RES"]), _n.ptr(b["PROBS"]), st)
@@ -327,6 +355,9 @@ class LSTMDSACaptioner(Captioner):
         if fused:
             value = value.contiguous()
             step_bufs = self._greedy_buffers(R, value, w)
+            A = w["A"]  # the gather kernel's widths: powers of two in [32, 512] (else ctx2att stays a GEMM)
+            gather = GREEDY_CTX2ATT_GATHER and 32 <= A <= 512 and A & (A - 1) == 0
+            step_bufs["U"] = self._ctx2att_rows(value, mask_u8) if gather else None
         it = torch.zeros(R, dtype=torch.long, device=hs_rows.device)
         seq, seqlp = [], []
         unfinished = None
