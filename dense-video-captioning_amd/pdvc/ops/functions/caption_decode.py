@@ -25,6 +25,10 @@ from .linear import colsum, wgrad_mm
 from .ms_deform_attn_func import NUM_SAMPLES, _levels
 
 
+# ctx2att of the samples as a gather of the once-projected value rows (see forward); False keeps the per-step GEMM
+CTX2ATT_GATHER = True
+
+
 class CaptionDecodeFunction(Function):
     """value (Nv,S,M,D) = value_proj(memory); xe (n,R,4H); hs_g (R,4H); off_hs (R, M*16); ref (R,L,1|2) (first rd1_rows rows
     1-d when 2-wide); W_h (M*16 + A + 4H, H), b_h; W_ctx (A, D), b_ctx (A); alpha_w (A,), alpha_b (1,);
@@ -63,6 +67,14 @@ class CaptionDecodeFunction(Function):
         zero = torch.zeros((R, H), **kw)
         st = _n.stream()
         with fp32_gemms():  # the recurrence stays fp32 in the bf16 mode (pdvc/precision.py)
+            # att = ctx2att(clip) is linear in the sample, and a sample is a blend of value rows with weights summing
+            # to 1: project the value rows once (padded rows zeroed: their projection is the bias) and blend the
+            # projections with the same gather -- U rows N*S instead of a (R*16) x D x A GEMM for each of n steps.
+            # The backward is unchanged (dW_ctx, db_ctx and dclip come from CLIP and dATT).
+            U = None
+            if CTX2ATT_GATHER and 32 <= A <= 512 and A & (A - 1) == 0 and n * R * M * NS > Nv * S * M:
+                vm = value if pad_mask is None else value.masked_fill(pad_mask.view(Nv, S, 1, 1).bool(), 0.0)
+                U = torch.addmm(b_ctx, vm.view(-1, D), W_ctx.t()).view(Nv, S, M, A)
             for i in range(n):
                 if i == 0:
                     HP[0].copy_(b_h.expand(R, Ph))  # h_{-1} = 0
@@ -71,7 +83,12 @@ class CaptionDecodeFunction(Function):
                 _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video), _n.ptr(HP[i]),
                         Ph, 0, _n.ptr(off_hs), _n.ptr(ref), RD, int(rd1_rows), lvl, nl, Nv, R, M, D, NS // nl,
                         _n.ptr(CLIP[i]), _n.ptr(LOC[i]), st)
-                torch.addmm(b_ctx, CLIP[i].view(-1, D), W_ctx.t(), out=ATT[i])
+                if U is not None:
+                    _n.call("pdvc_cap_gather_forward_f32", _n.ptr(U), None, _n.ptr(row_video), _n.ptr(HP[i]), Ph, 0,
+                            _n.ptr(off_hs), _n.ptr(ref), RD, int(rd1_rows), lvl, nl, Nv, R, M, A, NS // nl,
+                            _n.ptr(ATT[i]), None, st)
+                else:
+                    torch.addmm(b_ctx, CLIP[i].view(-1, D), W_ctx.t(), out=ATT[i])
                 ah, ldh = _n.rows(HP[i][:, n_off:n_off + A])
                 _n.call("pdvc_softattn_forward_f32", _n.ptr(ATT[i]), ah, ldh, _n.ptr(alpha_w), _n.ptr(alpha_b),
                         _n.ptr(CLIP[i]), R, M, A, D, _n.ptr(RES[i]), _n.ptr(PROBS[i]), st)

@@ -426,3 +426,52 @@ def test_greedy_ctx2att_gather_equals_gemm(masked):
     # state (random weights at this scale amplify it), so they get a looser bound
     assert (lp_u[:, 0] - lp_g[:, 0]).abs().max().item() <= 1e-5
     assert (lp_u - lp_g).abs().max().item() <= 1e-3
+
+
+@pytest.mark.parametrize("masked", [False, True])
+def test_teacher_forced_ctx2att_gather_equals_gemm(masked):
+    """The training recurrence's ctx2att as a gather of the once-projected value rows (CaptionDecodeFunction,
+    CTX2ATT_GATHER) against the per-step GEMM: log-probabilities, and every gradient (the backward is shared),
+    within 1e-4."""
+    import pdvc.ops.functions.caption_decode as CD
+    from pdvc.CaptioningHead.LSTM_DSA import LSTMDSACaptioner
+    opt = small_opt()
+    opt.att_hid_size = 64
+    torch.manual_seed(6)
+    cap = LSTMDSACaptioner(opt).to(DEV).train()
+    with torch.no_grad():
+        for p in cap.parameters():
+            p.copy_(torch.randn_like(p) * 0.1)
+    T_l = (32, 16, 8, 4)
+    S = sum(T_l)
+    Nv, E = 2, 4
+    mask = torch.zeros(Nv, S, dtype=torch.bool, device=DEV)
+    if masked:
+        mask[0, 20:32] = True
+        mask[0, 44:48] = True
+    hs0 = torch.randn(Nv, E, 64, device=DEV)
+    ref0 = torch.rand(Nv, E, 2, device=DEV)
+    mem0 = torch.randn(Nv, S, 64, device=DEV)
+    cap_tensor = torch.randint(1, 23, (Nv * E, 7), device=DEV)
+    cap_tensor[:, 0] = 0
+
+    def run(gather):
+        CD.CTX2ATT_GATHER = gather
+        try:
+            cap.zero_grad(set_to_none=True)
+            hs, ref, mem = (t.clone().requires_grad_() for t in (hs0, ref0, mem0))
+            others = {"memory": mem, "mask_flatten": mask, "level_T": T_l,
+                      "spatial_shapes": torch.tensor(T_l, device=DEV), "valid_ratios": torch.ones(Nv, 4, device=DEV)}
+            lp = cap(hs, ref, others, cap_tensor)
+            lp.sum().backward()
+            return lp.detach(), [hs.grad, ref.grad, mem.grad] + [p.grad for p in cap.parameters()]
+        finally:
+            CD.CTX2ATT_GATHER = True
+
+    lp_g, g_g = run(False)
+    lp_u, g_u = run(True)
+    close(lp_u, lp_g.cpu().numpy(), 1e-4, "logprobs")
+    for a, b in zip(g_u, g_g):
+        assert (a is None) == (b is None)
+        if a is not None:
+            close(a, b.cpu().numpy(), 1e-4, "grad")
