@@ -3,7 +3,9 @@
 For one video every number equals the reference's.  A batch of N videos returns, for every loss key, the
 mean over videos of the per-video values (each video normalised by its own event count, exactly as the
 reference's batch-size-1 training does); gradients are therefore the average of N batch-1 gradients.
-All decoder layers' matchings are solved after ONE device->host copy (the reference syncs once per layer).
+The decoder layers are stacked and matched together: one cost pass, and the assignments are solved on the GPU
+(pdvc_lsap_f32, scipy's algorithm and tie rule) with no host round trip -- the reference copies the costs to the
+host and runs scipy once per layer.  solve_padded keeps the host route (one copy for every layer).
 """
 import numpy as np
 import torch
