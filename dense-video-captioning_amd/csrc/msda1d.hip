@@ -922,7 +922,9 @@ constexpr int kVQPT = 4;  // queries per thread in its sort passes: a launch chu
 // CW: channels per lane (D <= 64 -> 1, D = 128 -> 2).  G4 (D == 64): the gather phase runs on 16-lane groups
 // with a float4 per lane instead of whole waves with one float per lane -- 32 row ranges per workgroup, and one
 // wave-instruction loads the gradient rows of 4 samples (4x fewer loads, LDS index reads and loop iterations).
-template <int CW, bool G4>
+// UG: samples in flight per 16-lane group in the G4 walk (8: 96 VGPRs; 4: 66, more workgroups per CU where the LDS
+// allows -- the decoder's short sample lists)
+template <int CW, bool G4, int UG = 8>
 __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
                                                                      int Lq, int q0, int nq, int S, int M, int D,
                                                                      int accumulate,
@@ -1083,19 +1085,19 @@ __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_
             };
             int k = ent[jb].w;
             float4 alo = make_float4(0.f, 0.f, 0.f, 0.f), ahi = alo;  // rows k - 1 and k
-            for (int j0 = jb; j0 < je; j0 += U) {
-                int4 e[U];
-                float4 gv[U];
+            for (int j0 = jb; j0 < je; j0 += UG) {
+                int4 e[UG];
+                float4 gv[UG];
 #pragma unroll
-                for (int u = 0; u < U; ++u) e[u] = ent[(j0 + u < je) ? j0 + u : je - 1];
+                for (int u = 0; u < UG; ++u) e[u] = ent[(j0 + u < je) ? j0 + u : je - 1];
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
+                for (int u = 0; u < UG; ++u) {
                     const auto t = __builtin_amdgcn_raw_buffer_load_b128(gr, e[u].x * rowb + coff, 0, 0);
                     gv[u] = make_float4(__uint_as_float(t[0]), __uint_as_float(t[1]), __uint_as_float(t[2]),
                                         __uint_as_float(t[3]));
                 }
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
+                for (int u = 0; u < UG; ++u) {
                     if (j0 + u >= je) break;
                     const int kj = e[u].w;
                     if (kj != k) {  // bucket k complete: row k - 1 final; row k too unless bucket k + 1 follows
@@ -1233,6 +1235,18 @@ static int pick_pyr(const Levels1d& lv, int S, int num_query, int head_dim, int 
     if (!enabled || head_dim != 64 || num_query <= 0 || 4L * num_query < S) return 0;
     if (lv.T[0] > kPyrRows || lv.T[1] + lv.T[2] + lv.T[3] > kPyrRows) return 0;
     return (num_query + per_block - 1) / per_block;
+}
+
+// value-gradient walk depth (PDVC_VALUE_UG=4 / 8 forces it): 4 where a level holds few samples per row (the
+// decoder, 4 * Lq < S: its workgroups' LDS is small, so the 66-VGPR form fits more of them per CU -- 206 -> 177 us at
+// 256 videos), 8 for the encoder (LDS-limited to two workgroups per CU anyway; 8 in flight: 770 -> 700 us)
+static int value_ug(int num_query, int S) {
+    static const int forced = [] {
+        const char* e = getenv("PDVC_VALUE_UG");
+        return e ? atoi(e) : 0;
+    }();
+    if (forced == 4 || forced == 8) return forced;
+    return 4L * num_query < S ? 4 : 8;
 }
 
 // 16-lane-group gather for the value gradient at D = 64 (PDVC_MSDA_G4=0 selects the wave-per-range form)
@@ -1470,7 +1484,9 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
             hipError_t e3 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1, true>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-            if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+            hipError_t e4 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1, true, 4>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+            if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess) {
                 (void)hipGetLastError();
                 return pdvc_set_error(PDVC_ERR_LAUNCH, "msda1d_bwd_value_kernel: cannot raise the LDS limit");
             }
@@ -1481,7 +1497,11 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
             const size_t lds = g4 ? sizeof(int) * (((2 * (size_t)(Tmax + 2) + 3) & ~(size_t)3) + 4 * (size_t)nq * kP)
                                   : sizeof(int) * (2 * (size_t)(Tmax + 2) + 3 * (size_t)nq * kP);
             const int acc = q0 > 0;
-            if (g4)
+            if (g4 && value_ug(num_query, S) == 4)
+                hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, 4>), dim3((unsigned)nblk), dim3(kVW * 64), lds,
+                                   s, value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
+                                   save_attn, save_loc, grad_value);
+            else if (g4)
                 hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
                                    value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
                                    save_attn, save_loc, grad_value);
