@@ -386,6 +386,129 @@ __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(const float* __restri
     }
 }
 
+// The same forward in 66 KiB of LDS (two workgroups per CU instead of one: mha_fwd_mfma_kernel's K, Q and V images
+// take 99 KiB).  A wave's query rows are its own MFMA A operand, so they are loaded straight into registers:
+// k-step kk of lane half hi takes channel 32*hi + kk (a permutation of the contraction index, applied to the K
+// image reads as well), i.e. each lane reads 32 contiguous channels of its query row.  P_d is written in two
+// 64-key halves into the K image (no longer needed once every wave has its scores), each half consumed by the
+// P.V MFMAs before the next is written.  Same softmax, dropout mask and log-sum-exp as mha_fwd_mfma_kernel.
+static constexpr int kPHLD = 65;  // P half-tile row stride (64 keys + 1)
+
+__global__ __launch_bounds__(256) void mha_fwd_mfma2_kernel(const float* __restrict__ qk, const float* __restrict__ v,
+                                                            const uint8_t* __restrict__ kpm, int Q, int M,
+                                                            float scaling, float p_drop, uint32_t thresh,
+                                                            uint64_t seed0, const uint64_t* __restrict__ seed_dev,
+                                                            float* __restrict__ out, float* __restrict__ lse) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int D = 64;
+    float* Ks = smem;                // [128][65]
+    float* Vs = Ks + kMQ * kMLD;     // [128][64]
+    const int E = M * D;
+    const int nm = xcd_remap(blockIdx.x, gridDim.x);
+    const int n = nm / M, m = nm - n * M;
+    const uint64_t seed = load_seed(seed0, seed_dev);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, hi = lane >> 5;
+    const float* qbase = qk + (size_t)n * Q * 2 * E + m * D;
+    const int row0 = w * 32;
+    float qa[32];  // q[row0 + l32][32*hi + kk] * scaling (zeros past Q)
+    {
+        const int q = row0 + l32;
+        const float4* src = reinterpret_cast<const float4*>(qbase + (size_t)q * 2 * E + 32 * hi);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float4 x = q < Q ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            qa[4 * i] = x.x * scaling;
+            qa[4 * i + 1] = x.y * scaling;
+            qa[4 * i + 2] = x.z * scaling;
+            qa[4 * i + 3] = x.w * scaling;
+        }
+    }
+    mha_stage(qbase + E, 2 * (size_t)E, Q, 1.f, Ks, kMLD, tid);
+    mha_stage(v + (size_t)n * Q * E + m * D, (size_t)E, Q, 1.f, Vs, D, tid);
+    __syncthreads();
+    mha_f32x16 s[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) s[kb] = mha_f32x16{};
+    {
+        const float* kbp = Ks + l32 * kMLD + 32 * hi;
+#pragma unroll
+        for (int kk = 0; kk < D / 2; ++kk) {
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb) s[kb] = mfma32(qa[kk], kbp[kb * 32 * kMLD + kk], s[kb]);
+        }
+    }
+    bool kval[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+        const int k = kb * 32 + l32;
+        kval[kb] = k < Q && !(kpm && kpm[(size_t)n * Q + k]);
+    }
+    // softmax rows in registers: s[kb][r] becomes P_d
+    const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int rl = crow(r, hi), q = row0 + rl;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) mx = fmaxf(mx, kval[kb] ? s[kb][r] : -INFINITY);
+#pragma unroll
+        for (int d = 16; d > 0; d >>= 1) mx = fmaxf(mx, lane_swap(mx, d));
+        float e[4], sum = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+            e[kb] = kval[kb] ? expf(s[kb][r] - mx) : 0.f;
+            sum += e[kb];
+        }
+#pragma unroll
+        for (int d = 16; d > 0; d >>= 1) sum += lane_swap(sum, d);
+        const float inv = 1.f / sum;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+            const int k = kb * 32 + l32;
+            float p = e[kb] * inv;
+            if (p_drop > 0.f && q < Q && k < Q)
+                p = keep_elem(seed, (uint32_t)nm, (uint32_t)q, (uint32_t)k, (uint32_t)Q, thresh) ? p * keep_scale : 0.f;
+            s[kb][r] = p;
+        }
+        if (l32 == 0 && q < Q) lse[(size_t)nm * Q + q] = mx + logf(sum);
+    }
+    __syncthreads();  // every wave is done with the K image: the P halves reuse it
+    float* Pw = smem + w * 32 * kPHLD;  // [32][65] this wave's P_d rows, one 64-key half at a time
+    mha_f32x16 o[2] = {mha_f32x16{}, mha_f32x16{}};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int rl = crow(r, hi);
+            Pw[rl * kPHLD + l32] = s[2 * h][r];
+            Pw[rl * kPHLD + 32 + l32] = s[2 * h + 1][r];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const float* pa = Pw + l32 * kPHLD + hi;
+        const float* vb = Vs + (64 * h + hi) * D + l32;
+#pragma unroll 8
+        for (int kk = 0; kk < 32; ++kk) {
+            const float a = pa[2 * kk];
+            o[0] = mfma32(a, vb[2 * kk * D], o[0]);
+            o[1] = mfma32(a, vb[2 * kk * D + 32], o[1]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int q = row0 + crow(r, hi);
+        if (q < Q) {
+            float* orow = out + ((size_t)n * Q + q) * E + m * D + l32;
+            orow[0] = o[0][r];
+            orow[32] = o[1][r];
+        }
+    }
+}
+
 // Backward, one workgroup per (video, head).  Phase A (wave w = query rows 32w..): recompute P from the saved
 // log-sum-exp, dP_d = dO . V^T, dS = P (dP_d z - delta), dq = dS . K; P_d and dS go to the global workspace
 // (stays in L2: this workgroup reads it back).  Phase B (wave w = key rows 32w..): dk = dS^T . q_scaled,
@@ -552,6 +675,8 @@ static size_t fwd_lds(int Q, int D) { return sizeof(float) * ((size_t)Q * (D + 1
 static size_t bwdq_lds(int Q, int D) { return sizeof(float) * (2 * (size_t)Q * (D + 1) + 4 * Q + 8 * kHD); }
 static size_t bwdk_lds(int Q, int D) { return sizeof(float) * (2 * (size_t)kQB * Q + 2 * (size_t)kQS * D); }
 static constexpr size_t kFwdMfmaLds = sizeof(float) * (2 * kMQ * kMLD + kMQ * 64);
+static constexpr size_t kFwdMfma2Lds = sizeof(float) * (kMQ * kMLD + kMQ * 64);
+static_assert(sizeof(float) * 4 * 32 * kPHLD <= sizeof(float) * kMQ * kMLD, "P half tiles must fit in the K image");
 static constexpr size_t kBwdMfmaLds = sizeof(float) * (4 * kMQ * kMLD + 4 * 32 * 33 + 2 * kMQ);
 static_assert(sizeof(float) * 4 * 32 * (kMQ + 1) <= sizeof(float) * 2 * kMQ * kMLD, "P tiles must fit in K/Q images");
 static_assert(kBwdMfmaLds <= 160 * 1024, "backward LDS budget");
@@ -561,6 +686,15 @@ static bool use_mfma(int Q, int D) {
     if (D != 64 || Q > kMQ) return false;
     const char* e = getenv("PDVC_MHA_MFMA");
     return !(e && e[0] == '0');
+}
+
+// the 66-KiB forward (two workgroups per CU); PDVC_MHA_FWD2=0 keeps the 99-KiB one (A/B)
+static bool fwd_lean() {
+    static const bool on = [] {
+        const char* e = getenv("PDVC_MHA_FWD2");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 // longer query sets (anet_c3d: Q = 300): the flash-style MFMA kernels of seqattn.hip with this op's key padding
@@ -578,8 +712,9 @@ static bool use_flash(int Q, int D) {
 static int mha_attrs() {
     static bool attr = false;
     if (!attr) {
-        const void* ks[5] = {(const void*)mha_fwd_kernel, (const void*)mha_bwd_q_kernel, (const void*)mha_bwd_k_kernel,
-                             (const void*)mha_fwd_mfma_kernel, (const void*)mha_bwd_mfma_kernel};
+        const void* ks[6] = {(const void*)mha_fwd_kernel, (const void*)mha_bwd_q_kernel, (const void*)mha_bwd_k_kernel,
+                             (const void*)mha_fwd_mfma_kernel, (const void*)mha_bwd_mfma_kernel,
+                             (const void*)mha_fwd_mfma2_kernel};
         for (const void* k : ks)
             if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) {
                 (void)hipGetLastError();
@@ -608,6 +743,13 @@ extern "C" int pdvc_mha_forward_f32(const float* qk, const float* v, const uint8
         const long E = (long)num_heads * head_dim;
         return sq_forward(qk, 2 * E, qk + E, 2 * E, v, E, batch, num_query, num_query, num_heads, head_dim, scaling,
                           key_padding_mask, dropout_p, seed, seed_dev, out, lse, (hipStream_t)stream);
+    }
+    if (use_mfma(num_query, head_dim) && fwd_lean()) {
+        hipLaunchKernelGGL(mha_fwd_mfma2_kernel, dim3((unsigned)((long)batch * num_heads)), dim3(256), kFwdMfma2Lds,
+                           (hipStream_t)stream, qk, v, key_padding_mask, num_query, num_heads, scaling, dropout_p,
+                           drop_threshold(dropout_p), seed, seed_dev, out, lse);
+        PDVC_CHECK_LAUNCH("mha_fwd_mfma2_kernel");
+        return PDVC_OK;
     }
     if (use_mfma(num_query, head_dim)) {
         hipLaunchKernelGGL(mha_fwd_mfma_kernel, dim3((unsigned)((long)batch * num_heads)), dim3(256), kFwdMfmaLds,
