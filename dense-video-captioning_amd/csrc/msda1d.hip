@@ -947,8 +947,10 @@ __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_
     int* sq = lds_i + 2 * (T + 2);          // [n] query of each sorted sample
     float* clo = (float*)(sq + n);          // [n] hw * a  -> row x0
     float* chi = clo + n;                   // [n] lw * a  -> row x0 + 1
-    // G4: one 16-B entry per sorted sample instead (query, hw * a, lw * a, key), one ds_read_b128 in the walk
-    int4* ent = reinterpret_cast<int4*>(lds_i + ((2 * (T + 2) + 3) & ~3));
+    // G4: 12 B per sorted sample instead -- (key << 16 | query) and (hw * a, lw * a) -- one ds_read_b32 and one
+    // ds_read_b64 in the walk (16-B entries held the encoder at two workgroups per CU)
+    uint32_t* eqk = reinterpret_cast<uint32_t*>(lds_i + 2 * (T + 2));
+    float2* ew = reinterpret_cast<float2*>(lds_i + ((2 * (T + 2) + n + 1) & ~1));
     __shared__ int wsum[kVW];
 
     for (int i = threadIdx.x; i < T + 2; i += blockDim.x) off[i] = 0;
@@ -1022,7 +1024,8 @@ __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_
                     const int pos = atomicAdd(&cur[key[k][p]], 1);
                     const float lo = (1.f - lwv[k][p]) * as[p], hi = lwv[k][p] * as[p];
                     if constexpr (G4) {
-                        ent[pos] = make_int4(q0 + qi, __float_as_int(lo), __float_as_int(hi), key[k][p]);
+                        eqk[pos] = ((uint32_t)key[k][p] << 16) | (uint32_t)(q0 + qi);
+                        ew[pos] = make_float2(lo, hi);
                     } else {
                         sq[pos] = q0 + qi;
                         clo[pos] = lo;
@@ -1083,23 +1086,23 @@ __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_
                     *orow = v;
                 }
             };
-            int k = ent[jb].w;
+            int k = (int)(eqk[jb] >> 16);
             float4 alo = make_float4(0.f, 0.f, 0.f, 0.f), ahi = alo;  // rows k - 1 and k
             for (int j0 = jb; j0 < je; j0 += UG) {
-                int4 e[UG];
+                uint32_t e[UG];
                 float4 gv[UG];
 #pragma unroll
-                for (int u = 0; u < UG; ++u) e[u] = ent[(j0 + u < je) ? j0 + u : je - 1];
+                for (int u = 0; u < UG; ++u) e[u] = eqk[(j0 + u < je) ? j0 + u : je - 1];
 #pragma unroll
                 for (int u = 0; u < UG; ++u) {
-                    const auto t = __builtin_amdgcn_raw_buffer_load_b128(gr, e[u].x * rowb + coff, 0, 0);
+                    const auto t = __builtin_amdgcn_raw_buffer_load_b128(gr, (int)(e[u] & 0xffffu) * rowb + coff, 0, 0);
                     gv[u] = make_float4(__uint_as_float(t[0]), __uint_as_float(t[1]), __uint_as_float(t[2]),
                                         __uint_as_float(t[3]));
                 }
 #pragma unroll
                 for (int u = 0; u < UG; ++u) {
                     if (j0 + u >= je) break;
-                    const int kj = e[u].w;
+                    const int kj = (int)(e[u] >> 16);
                     if (kj != k) {  // bucket k complete: row k - 1 final; row k too unless bucket k + 1 follows
                         put(k - 1, alo);
                         if (kj == k + 1) {
@@ -1111,7 +1114,8 @@ __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_
                         ahi = make_float4(0.f, 0.f, 0.f, 0.f);
                         k = kj;
                     }
-                    const float cl = __int_as_float(e[u].y), chh = __int_as_float(e[u].z);
+                    const float2 wgt = ew[j0 + u];
+                    const float cl = wgt.x, chh = wgt.y;
                     alo.x = fmaf(cl, gv[u].x, alo.x);
                     alo.y = fmaf(cl, gv[u].y, alo.y);
                     alo.z = fmaf(cl, gv[u].z, alo.z);
@@ -1469,8 +1473,10 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
         }
         int Tmax = 0;
         for (int l = 0; l < kL; ++l) Tmax = lv.T[l] > Tmax ? lv.T[l] : Tmax;
-        const bool g4 = head_dim == 64 && value_g4() && (long)num_query * num_heads * head_dim * 4 < (1L << 31);
-        const long per_sample = g4 ? 16 : 12;  // LDS bytes per sorted sample
+        // G4 packs (key, query) into 16 bits each
+        const bool g4 = head_dim == 64 && value_g4() && (long)num_query * num_heads * head_dim * 4 < (1L << 31) &&
+                        num_query < 65536 && Tmax < 65535;
+        const long per_sample = 12;  // LDS bytes per sorted sample (both forms)
         const long budget = 96 * 1024 - 8L * (Tmax + 2) - 16;
         if (budget < per_sample * kP) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "level length %d too long", Tmax);
         int qchunk = (int)(budget / (per_sample * kP));
@@ -1494,8 +1500,7 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
         }
         for (int q0 = 0; q0 < num_query; q0 += qchunk) {
             const int nq = (num_query - q0) < qchunk ? (num_query - q0) : qchunk;
-            const size_t lds = g4 ? sizeof(int) * (((2 * (size_t)(Tmax + 2) + 3) & ~(size_t)3) + 4 * (size_t)nq * kP)
-                                  : sizeof(int) * (2 * (size_t)(Tmax + 2) + 3 * (size_t)nq * kP);
+            const size_t lds = sizeof(int) * (2 * (size_t)(Tmax + 2) + 3 * (size_t)nq * kP + 2);
             const int acc = q0 > 0;
             if (g4 && value_ug(num_query, S) == 4)
                 hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, 4>), dim3((unsigned)nblk), dim3(kVW * 64), lds,
