@@ -94,7 +94,7 @@ __global__ void gn_finalize_kernel(const float* __restrict__ part, int N, int G,
 __global__ __launch_bounds__(256) void gn_apply_kernel(const float* __restrict__ x, const float* __restrict__ mean,
                                                        const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, int T, int C, int G, int total4,
-                                                       float* __restrict__ y) {
+                                                       float* __restrict__ y, long ys, float* __restrict__ y2) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total4) return;
     const int c4 = C / 4;
@@ -111,7 +111,8 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const float* __restrict__
     o.y = (v.y - mu) * rs * ga.y + be.y;
     o.z = (v.z - mu) * rs * ga.z + be.z;
     o.w = (v.w - mu) * rs * ga.w + be.w;
-    reinterpret_cast<float4*>(y)[i] = o;
+    reinterpret_cast<float4*>(y + (size_t)n * ys + (size_t)(row - n * T) * C)[cg] = o;
+    if (y2) reinterpret_cast<float4*>(y2)[i] = o;
 }
 
 // backward pass 1: per (video, chunk) group sums s1 = sum dy*gamma, s2 = sum dy*gamma*xhat, and per-column
@@ -119,7 +120,8 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const float* __restrict__
 __global__ __launch_bounds__(256) void gn_bwd_sums_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                                                           const float* __restrict__ mean, const float* __restrict__ rstd,
                                                           const float* __restrict__ gamma, int T, int C, int G,
-                                                          int chunks, float* __restrict__ gpart,
+                                                          int chunks, long dys, const float* __restrict__ dy2,
+                                                          float* __restrict__ gpart,
                                                           float* __restrict__ cpart) {
     __shared__ float4 red_s[256];
     __shared__ float4 red_c[2][256];
@@ -131,11 +133,17 @@ __global__ __launch_bounds__(256) void gn_bwd_sums_kernel(const float* __restric
     const float mu = mean[n * G + g], rs = rstd[n * G + g];
     const float4 ga = reinterpret_cast<const float4*>(gamma)[cg];
     const float4* xs = reinterpret_cast<const float4*>(x + (size_t)n * T * C) + cg;
-    const float4* ds = reinterpret_cast<const float4*>(dy + (size_t)n * T * C) + cg;
+    const float4* ds = reinterpret_cast<const float4*>(dy + (size_t)n * dys) + cg;
+    const float4* ds2 = dy2 ? reinterpret_cast<const float4*>(dy2 + (size_t)n * T * C) + cg : nullptr;
     float s1 = 0.f, s2 = 0.f;
     float4 dg = make_float4(0.f, 0.f, 0.f, 0.f), db = dg;
     for (int r = r0 + rr; r < r1; r += rpi) {
-        const float4 v = xs[(size_t)r * c4], d = ds[(size_t)r * c4];
+        const float4 v = xs[(size_t)r * c4];
+        float4 d = ds[(size_t)r * c4];
+        if (ds2) {
+            const float4 e = ds2[(size_t)r * c4];
+            d.x += e.x; d.y += e.y; d.z += e.z; d.w += e.w;
+        }
         const float h0 = (v.x - mu) * rs, h1 = (v.y - mu) * rs, h2 = (v.z - mu) * rs, h3 = (v.w - mu) * rs;
         s1 += d.x * ga.x + d.y * ga.y + d.z * ga.z + d.w * ga.w;
         s2 += d.x * ga.x * h0 + d.y * ga.y * h1 + d.z * ga.z * h2 + d.w * ga.w * h3;
@@ -193,7 +201,8 @@ __global__ __launch_bounds__(256) void gn_bwd_dx_kernel(const float* __restrict_
                                                         const float* __restrict__ mean, const float* __restrict__ rstd,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ gsum, int T, int C, int G,
-                                                        int total4, float* __restrict__ dx) {
+                                                        int total4, long dys, const float* __restrict__ dy2,
+                                                        float* __restrict__ dx) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total4) return;
     const int c4 = C / 4;
@@ -204,7 +213,12 @@ __global__ __launch_bounds__(256) void gn_bwd_dx_kernel(const float* __restrict_
     const float s1 = gsum[2 * (n * G + g)], s2 = gsum[2 * (n * G + g) + 1];
     const float inv_n = 1.f / ((float)T * (float)(C / G));
     const float mu = mean[n * G + g], rs = rstd[n * G + g];
-    const float4 v = reinterpret_cast<const float4*>(x)[i], d = reinterpret_cast<const float4*>(dy)[i];
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    float4 d = reinterpret_cast<const float4*>(dy + (size_t)n * dys + (size_t)(row - n * T) * C)[cg];
+    if (dy2) {
+        const float4 e = reinterpret_cast<const float4*>(dy2)[i];
+        d.x += e.x; d.y += e.y; d.z += e.z; d.w += e.w;
+    }
     const float4 ga = reinterpret_cast<const float4*>(gamma)[cg];
     float4 o;
     o.x = rs * (d.x * ga.x - (s1 + (v.x - mu) * rs * s2) * inv_n);
@@ -230,11 +244,14 @@ using namespace pdvc;
 
 static int gn_chunks(int T) { return (T + kGnRows - 1) / kGnRows; }
 
-extern "C" int pdvc_groupnorm_rows_forward_f32(const float* x, int N, int T, int C, int G, float eps,
-                                               const float* gamma, const float* beta, float* workspace, float* y,
-                                               float* mean, float* rstd, void* stream) {
+extern "C" int pdvc_groupnorm_rows_forward_out_f32(const float* x, int N, int T, int C, int G, float eps,
+                                                   const float* gamma, const float* beta, float* workspace, float* y,
+                                                   long y_video_stride, float* y_copy, float* mean, float* rstd,
+                                                   void* stream) {
     int rc = gn_check(N, T, C, G);
     if (rc) return rc;
+    PDVC_CHECK_ARG(y_video_stride >= (long)T * C && y_video_stride % 4 == 0, "invalid output video stride %ld",
+                   y_video_stride);
     if (N == 0) return PDVC_OK;
     hipStream_t s = (hipStream_t)stream;
     const int chunks = gn_chunks(T);
@@ -246,21 +263,32 @@ extern "C" int pdvc_groupnorm_rows_forward_f32(const float* x, int N, int T, int
     PDVC_CHECK_LAUNCH("gn_finalize_kernel");
     const int total4 = (int)((long)N * T * C / 4);
     hipLaunchKernelGGL(gn_apply_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, s, x, mean, rstd, gamma,
-                       beta, T, C, G, total4, y);
+                       beta, T, C, G, total4, y, y_video_stride, y_copy);
     PDVC_CHECK_LAUNCH("gn_apply_kernel");
     return PDVC_OK;
 }
 
-extern "C" int pdvc_groupnorm_rows_backward_f32(const float* x, const float* dy, const float* mean, const float* rstd,
-                                                const float* gamma, int N, int T, int C, int G, float* group_ws,
-                                                float* col_partials, float* dx, void* stream) {
+extern "C" int pdvc_groupnorm_rows_forward_f32(const float* x, int N, int T, int C, int G, float eps,
+                                               const float* gamma, const float* beta, float* workspace, float* y,
+                                               float* mean, float* rstd, void* stream) {
+    return pdvc_groupnorm_rows_forward_out_f32(x, N, T, C, G, eps, gamma, beta, workspace, y, (long)T * C, nullptr,
+                                               mean, rstd, stream);
+}
+
+extern "C" int pdvc_groupnorm_rows_backward_strided_f32(const float* x, const float* dy, long dy_video_stride,
+                                                        const float* dy_add, const float* mean, const float* rstd,
+                                                        const float* gamma, int N, int T, int C, int G,
+                                                        float* group_ws, float* col_partials, float* dx,
+                                                        void* stream) {
     int rc = gn_check(N, T, C, G);
     if (rc) return rc;
+    PDVC_CHECK_ARG(dy_video_stride >= (long)T * C && dy_video_stride % 4 == 0, "invalid gradient video stride %ld",
+                   dy_video_stride);
     if (N == 0) return PDVC_OK;
     hipStream_t s = (hipStream_t)stream;
     const int chunks = gn_chunks(T);
     hipLaunchKernelGGL(gn_bwd_sums_kernel, dim3((unsigned)N, (unsigned)chunks), dim3(256), 0, s, x, dy, mean, rstd,
-                       gamma, T, C, G, chunks, group_ws, col_partials);
+                       gamma, T, C, G, chunks, dy_video_stride, dy_add, group_ws, col_partials);
     PDVC_CHECK_LAUNCH("gn_bwd_sums_kernel");
     float* gsum = group_ws + (size_t)N * chunks * G * 2;
     hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3((unsigned)((N * G + 255) / 256)), dim3(256), 0, s, group_ws, N, G,
@@ -268,7 +296,14 @@ extern "C" int pdvc_groupnorm_rows_backward_f32(const float* x, const float* dy,
     PDVC_CHECK_LAUNCH("gn_bwd_finalize_kernel");
     const int total4 = (int)((long)N * T * C / 4);
     hipLaunchKernelGGL(gn_bwd_dx_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, s, x, dy, mean, rstd,
-                       gamma, gsum, T, C, G, total4, dx);
+                       gamma, gsum, T, C, G, total4, dy_video_stride, dy_add, dx);
     PDVC_CHECK_LAUNCH("gn_bwd_dx_kernel");
     return PDVC_OK;
+}
+
+extern "C" int pdvc_groupnorm_rows_backward_f32(const float* x, const float* dy, const float* mean, const float* rstd,
+                                                const float* gamma, int N, int T, int C, int G, float* group_ws,
+                                                float* col_partials, float* dx, void* stream) {
+    return pdvc_groupnorm_rows_backward_strided_f32(x, dy, (long)T * C, nullptr, mean, rstd, gamma, N, T, C, G,
+                                                    group_ws, col_partials, dx, stream);
 }

@@ -51,6 +51,9 @@ SIGNATURES = {
     "pdvc_level_pos_rows_backward_f32": [_vp, _vp] + [_i] * 4 + [_vp, _vp],
     "pdvc_groupnorm_rows_forward_f32": [_vp, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "pdvc_groupnorm_rows_backward_f32": [_vp] * 5 + [_i] * 4 + [_vp] * 4,
+    "pdvc_groupnorm_rows_forward_out_f32": [_vp, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp, ctypes.c_long, _vp, _vp,
+                                            _vp, _vp],
+    "pdvc_groupnorm_rows_backward_strided_f32": [_vp, _vp, ctypes.c_long] + [_vp] * 4 + [_i] * 4 + [_vp] * 4,
     "pdvc_gemm_f32": [_i, _i, _i, _vp, _i, _i, _vp, _i, _i, _vp, _i, _vp, _i, _i, _vp],
     "pdvc_mha_forward_f32": [_vp, _vp, _u8p] + [_i] * 4 + [_f, _u64] + [_vp] * 4,
     "pdvc_mha_backward_f32": [_vp, _vp, _u8p, _vp, _vp, _vp] + [_i] * 4 + [_f, _u64] + [_vp] * 5,

@@ -11,7 +11,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from .ops.functions.conv_rows import conv1d_rows, group_norm_rows
+from .ops.functions.conv_rows import conv1d_rows, group_norm_rows, group_norm_rows_into, group_norm_rows_ok
 from .position_encoding import PositionEmbeddingSine, PyramidPosEmbed
 
 
@@ -50,6 +50,8 @@ class BaseEncoder(nn.Module):
         (N, L_l, d) storage, so the transformer's flattening (src.transpose(1, 2)) costs no copy; the position
         embeddings come as a PyramidPosEmbed (indexable like the reference's list)."""
         x = vf.contiguous()
+        if self._flat_ok(x):
+            return self._forward_flat(x, mask, duration)
         rows = [self._proj(0, x)]
         masks = [mask]
         for lvl in range(1, self.num_feature_levels):
@@ -58,6 +60,39 @@ class BaseEncoder(nn.Module):
             rows.append(src)
             masks.append(m)
         return [r.transpose(1, 2) for r in rows], masks, PyramidPosEmbed(self.pos_embed, masks, duration)
+
+
+    def _flat_ok(self, x):
+        return (self.num_feature_levels > 1 and all(isinstance(p[0], nn.Conv1d) for p in self.input_proj)
+                and group_norm_rows_ok(self.input_proj[0][1], x.new_empty(0, self.hidden_dim)))
+
+    def _forward_flat(self, x, mask, duration):
+        """forward() with every level's GroupNorm writing into its rows of one (N, sum T_l, d) buffer: the
+        returned level tensors are views of it, tagged `_pdvc_flat`, so the transformer's flattening
+        (deformable_transformer.py:84-106, a torch.cat) takes the buffer as it is."""
+        N, T, _ = x.shape
+        Ts = [T]
+        for _ in range(1, self.num_feature_levels):
+            Ts.append((Ts[-1] + 1) // 2)  # Conv1d(k=3, s=2, p=1)
+        flat = x.new_empty(N, sum(Ts), self.hidden_dim)
+        start, prev, masks = 0, None, [mask]
+        for lvl in range(self.num_feature_levels):
+            conv, gn = self.input_proj[lvl][0], self.input_proj[lvl][1]
+            c = conv1d_rows(conv, x if lvl <= 1 else prev)
+            assert c.shape[1] == Ts[lvl]
+            want = 0 < lvl < self.num_feature_levels - 1  # the next level's conv input
+            out = group_norm_rows_into(gn, c, flat, start, want)
+            flat, prev = out if want else (out, None)
+            start += Ts[lvl]
+            if lvl:
+                masks.append(F.interpolate(mask[None].float(), size=Ts[lvl]).to(torch.bool)[0])
+        levels, start = [], 0
+        for t in Ts:
+            v = flat[:, start:start + t].transpose(1, 2)
+            v._pdvc_flat = (flat, start)
+            levels.append(v)
+            start += t
+        return levels, masks, PyramidPosEmbed(self.pos_embed, masks, duration)
 
 
 def build_base_encoder(args):

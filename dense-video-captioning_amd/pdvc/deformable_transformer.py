@@ -86,7 +86,13 @@ class DeformableTransformer(nn.Module):
             if not fused_pos:
                 lvl_pos.append(add_row_bias(pos_embeds[lvl].transpose(1, 2), self.level_embed[lvl]))
             mask_flatten.append(mask)
-        src_flatten = torch.cat(src_flatten, 1)
+        flat = getattr(srcs[0], "_pdvc_flat", (None, 0))[0]
+        tags = [getattr(s, "_pdvc_flat", (None, 0)) for s in srcs]
+        if flat is not None and flat.shape[1] == sum(level_T) and all(
+                t[0] is flat and t[1] == sum(level_T[:i]) for i, t in enumerate(tags)):
+            src_flatten = flat  # the base encoder wrote every level into its rows of one buffer (base_encoder.py)
+        else:
+            src_flatten = torch.cat(src_flatten, 1)
         mask_flatten = torch.cat(mask_flatten, 1)
         # all levels' sine + duration rows + level embeddings in one HIP pass (ops/functions/posembed.py); when every
         # encoder layer runs the fused attention block, their position gradients come back as per-(video, level)

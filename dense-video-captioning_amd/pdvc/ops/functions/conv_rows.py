@@ -102,6 +102,67 @@ class GroupNormRowsFunction(Function):
         return dx, gsum[:C].contiguous(), gsum[C:].contiguous(), None, None
 
 
+class GroupNormFlatFunction(Function):
+    """GroupNormRowsFunction writing its result straight into rows [start, start + T) of every video of the
+    flattened pyramid `flat` (N, S, C) -- in place, so the levels need no torch.cat (reference:
+    deformable_transformer.py:84-106 flattens and concatenates the level outputs).  With `want_copy` it also
+    returns the contiguous (N, T, C) result, the input of the next level's convolution; its gradient is added to
+    the slice's inside the backward kernels instead of by autograd."""
+
+    @staticmethod
+    def forward(ctx, flat, x, weight, bias, groups, eps, start, want_copy):
+        x = x.contiguous()
+        N, T, C = x.shape
+        S = flat.shape[1]
+        chunks = (T + GN_ROWS - 1) // GN_ROWS
+        kw = dict(dtype=x.dtype, device=x.device)
+        ws = torch.empty(N * chunks * groups * 3, **kw)
+        y2 = torch.empty_like(x) if want_copy else None
+        mean = torch.empty(N * groups, **kw)
+        rstd = torch.empty(N * groups, **kw)
+        _n.call("pdvc_groupnorm_rows_forward_out_f32", _n.ptr(x), N, T, C, groups, float(eps), _n.ptr(weight),
+                _n.ptr(bias), _n.ptr(ws), _n.ptr_any(flat[:, start:start + T]), S * C, _n.ptr(y2), _n.ptr(mean),
+                _n.ptr(rstd), _n.stream())
+        ctx.mark_dirty(flat)
+        ctx.save_for_backward(x, weight, mean, rstd)
+        ctx.meta = (groups, start, S, want_copy)
+        return (flat, y2) if want_copy else flat
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, d_flat, d_copy=None):
+        x, weight, mean, rstd = ctx.saved_tensors
+        G, start, S, want_copy = ctx.meta
+        N, T, C = x.shape
+        d_flat = d_flat.contiguous() if d_flat is not None else x.new_zeros(N, S, C)
+        d_copy = d_copy.contiguous() if d_copy is not None else None
+        chunks = (T + GN_ROWS - 1) // GN_ROWS
+        kw = dict(dtype=x.dtype, device=x.device)
+        gws = torch.empty(N * chunks * G * 2 + N * G * 2, **kw)
+        cpart = torch.empty(N * chunks, 2 * C, **kw)
+        dx = torch.empty_like(x)
+        _n.call("pdvc_groupnorm_rows_backward_strided_f32", _n.ptr(x), _n.ptr_any(d_flat[:, start:start + T]), S * C,
+                _n.ptr(d_copy), _n.ptr(mean), _n.ptr(rstd), _n.ptr(weight), N, T, C, G, _n.ptr(gws), _n.ptr(cpart),
+                _n.ptr(dx), _n.stream())
+        gsum = colsum(cpart)
+        # the slice [start, start + T) of the incoming flat was overwritten: only the earlier levels' functions
+        # (which read their own slices) consume this gradient, so it passes through unmasked
+        return d_flat, dx, gsum[:C].contiguous(), gsum[C:].contiguous(), None, None, None, None
+
+
+def group_norm_rows_ok(gn, x):
+    C = x.shape[-1]
+    cpg = C // gn.num_groups
+    return (x.is_cuda and x.dtype == torch.float32 and gn.affine and C % 4 == 0 and 256 % (C // 4) == 0
+            and cpg % 4 == 0 and (cpg // 4) & (cpg // 4 - 1) == 0)
+
+
+def group_norm_rows_into(gn, x, flat, start, want_copy):
+    """group_norm_rows(gn, x) written into flat[:, start:start + T] (see GroupNormFlatFunction).  Returns the new
+    flat (and the contiguous result when want_copy)."""
+    return GroupNormFlatFunction.apply(flat, x, gn.weight, gn.bias, gn.num_groups, gn.eps, start, want_copy)
+
+
 def conv1d_rows(conv, x):
     """nn.Conv1d (kernel 1, or kernel 3 / stride 2 / padding 1) applied to x (N, T, C) rows."""
     k = conv.weight.shape[2]
@@ -114,10 +175,6 @@ def conv1d_rows(conv, x):
 
 def group_norm_rows(gn, x):
     """nn.GroupNorm applied to x (N, T, C) rows (falls back to torch off the GPU / for other group shapes)."""
-    C = x.shape[-1]
-    cpg = C // gn.num_groups
-    ok = (x.is_cuda and x.dtype == torch.float32 and gn.affine and C % 4 == 0 and 256 % (C // 4) == 0
-          and cpg % 4 == 0 and (cpg // 4) & (cpg // 4 - 1) == 0)
-    if not ok:
+    if not group_norm_rows_ok(gn, x):
         return F.group_norm(x.transpose(1, 2), gn.num_groups, gn.weight, gn.bias, gn.eps).transpose(1, 2)
     return GroupNormRowsFunction.apply(x, gn.weight, gn.bias, gn.num_groups, gn.eps)

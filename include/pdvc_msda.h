@@ -266,6 +266,18 @@ int pdvc_groupnorm_rows_forward_f32(const float* x, int N, int T, int C, int G, 
 int pdvc_groupnorm_rows_backward_f32(const float* x, const float* dy, const float* mean, const float* rstd,
                                      const float* gamma, int N, int T, int C, int G, float* group_ws,
                                      float* col_partials, float* dx, void* stream);
+/* The pyramid-flattening forms (replace the torch.cat of the levels in deformable_transformer.py:84-106):
+ * y is level l's slice of the flattened (N, S, C) encoder input, y_video_stride = S*C elements between videos
+ * (>= T*C, a multiple of 4); y_copy (NULL for none) also receives the contiguous (N, T, C) result for the next
+ * level's convolution.  The backward reads dy with the same video stride and adds dy_add (contiguous (N, T, C),
+ * NULL for none) -- the gradient from the next level's convolution -- to it. */
+int pdvc_groupnorm_rows_forward_out_f32(const float* x, int N, int T, int C, int G, float eps, const float* gamma,
+                                        const float* beta, float* workspace, float* y, long y_video_stride,
+                                        float* y_copy, float* mean, float* rstd, void* stream);
+int pdvc_groupnorm_rows_backward_strided_f32(const float* x, const float* dy, long dy_video_stride,
+                                             const float* dy_add, const float* mean, const float* rstd,
+                                             const float* gamma, int N, int T, int C, int G, float* group_ws,
+                                             float* col_partials, float* dx, void* stream);
 
 /* ---- column sums (bias gradients) ---------------------------------------------------------------------
  * out[c] = sum_r x[r*cols + c] for a row-major (rows, cols) fp32 matrix, cols % 4 == 0, 16-byte aligned;

@@ -46,3 +46,42 @@ def test_base_encoder_rows_gpu_matches_reference_layout():
         ref.append(encd.input_proj[lvl](x if lvl == 1 else ref[-1]))
     for s, r in zip(srcs, ref):
         assert (s.double() - r).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("T", [512, 37])
+def test_base_encoder_flat_buffer_matches_per_level(T, monkeypatch):
+    """The levels written straight into one flattened buffer (GroupNormFlatFunction) against the per-level path
+    plus torch.cat: values and every gradient (x, conv and GroupNorm parameters), ragged T included."""
+    from pdvc.base_encoder import BaseEncoder
+    torch.manual_seed(T)
+    enc = BaseEncoder(4, 768, 512).to(DEV)
+    for p in enc.parameters():  # non-trivial GroupNorm affine parameters
+        if p.dim() == 1:
+            p.data.normal_()
+    N = 3
+    vf = torch.randn(N, T, 768, device=DEV)
+    mask = torch.zeros(N, T, dtype=torch.bool, device=DEV)
+    dur = torch.tensor([100.0, 37.0, 12.0], device=DEV)
+
+    def run(flat_path):
+        monkeypatch.setattr(BaseEncoder, "_flat_ok", lambda self, x: flat_path)
+        enc.zero_grad(set_to_none=True)
+        x = vf.clone().requires_grad_()
+        srcs, _, _ = enc(x, mask, dur)
+        if flat_path:
+            assert all(hasattr(s, "_pdvc_flat") for s in srcs)
+            flat = srcs[0]._pdvc_flat[0]
+        else:
+            flat = torch.cat([s.transpose(1, 2) for s in srcs], 1)
+        g = torch.randn(flat.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(1))
+        (flat * g).sum().backward()
+        return flat.detach(), x.grad, {k: p.grad.clone() for k, p in enc.input_proj.named_parameters()}
+
+    f1, dx1, gp1 = run(True)
+    f0, dx0, gp0 = run(False)
+    assert f1.shape == f0.shape
+    assert (f1 - f0).abs().max().item() == 0.0
+    assert (dx1 - dx0).abs().max().item() <= 1e-5 * (dx0.abs().max().item() + 1.0)
+    for k in gp0:
+        err = (gp1[k] - gp0[k]).abs().max().item()
+        assert err <= 1e-5 * (gp0[k].abs().max().item() + 1.0), (k, err)
