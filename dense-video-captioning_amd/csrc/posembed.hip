@@ -33,7 +33,8 @@ __global__ __launch_bounds__(256) void level_pos_fwd_kernel(const float* __restr
                                                             const float* __restrict__ dim_t,
                                                             const float* __restrict__ dur,
                                                             const float* __restrict__ lemb, PosLevels lv, int N,
-                                                            int S, int F, int Dd, float* __restrict__ pos) {
+                                                            int S, int F, int Dd, const float* __restrict__ add,
+                                                            float* __restrict__ pos) {
     const int C = F + Dd, c4n = C / 4;
     const long total = (long)N * S * c4n;
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -57,7 +58,12 @@ __global__ __launch_bounds__(256) void level_pos_fwd_kernel(const float* __restr
             v[2] = d.z;
             v[3] = d.w;
         }
-        reinterpret_cast<float4*>(pos)[i] = make_float4(v[0] + le.x, v[1] + le.y, v[2] + le.z, v[3] + le.w);
+        float4 o = make_float4(v[0] + le.x, v[1] + le.y, v[2] + le.z, v[3] + le.w);
+        if (add) {  // q = src + lvl_pos, in that order (deformable_transformer.py:146 with_pos_embed)
+            const float4 a = reinterpret_cast<const float4*>(add)[i];
+            o = make_float4(a.x + o.x, a.y + o.y, a.z + o.z, a.w + o.w);
+        }
+        reinterpret_cast<float4*>(pos)[i] = o;
     }
 }
 
@@ -114,10 +120,12 @@ static int fill_pos_levels(const int32_t* level_T, int L, int S, PosLevels& lv) 
 
 using namespace pdvc;
 
-extern "C" int pdvc_level_pos_rows_forward_f32(const float* xe, const float* dim_t, const float* dur,
-                                               const float* level_embed, const int32_t* level_T, int num_levels,
-                                               int N, int S, int F, int Dd, float* pos, void* stream) {
+extern "C" int pdvc_level_pos_rows_add_f32(const float* xe, const float* dim_t, const float* dur,
+                                           const float* level_embed, const int32_t* level_T, int num_levels, int N,
+                                           int S, int F, int Dd, const float* add, float* out, void* stream) {
+    float* pos = out;
     PDVC_CHECK_ARG(N >= 0 && S > 0 && F > 0 && Dd >= 0 && F % 4 == 0 && Dd % 4 == 0, "invalid sizes");
+    PDVC_CHECK_ARG(((uintptr_t)add % 16) == 0, "add must be 16-byte aligned");
     PDVC_CHECK_ARG(((uintptr_t)pos % 16) == 0 && ((uintptr_t)level_embed % 16) == 0 &&
                        (Dd == 0 || ((uintptr_t)dur % 16) == 0),
                    "pos, level_embed and dur must be 16-byte aligned");
@@ -129,9 +137,16 @@ extern "C" int pdvc_level_pos_rows_forward_f32(const float* xe, const float* dim
     const long want = (total + 255) / 256;
     const unsigned blocks = (unsigned)(want < 16384 ? want : 16384);
     hipLaunchKernelGGL(level_pos_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, xe, dim_t, dur,
-                       level_embed, lv, N, S, F, Dd, pos);
+                       level_embed, lv, N, S, F, Dd, add, pos);
     PDVC_CHECK_LAUNCH("level_pos_fwd_kernel");
     return PDVC_OK;
+}
+
+extern "C" int pdvc_level_pos_rows_forward_f32(const float* xe, const float* dim_t, const float* dur,
+                                               const float* level_embed, const int32_t* level_T, int num_levels,
+                                               int N, int S, int F, int Dd, float* pos, void* stream) {
+    return pdvc_level_pos_rows_add_f32(xe, dim_t, dur, level_embed, level_T, num_levels, N, S, F, Dd, nullptr, pos,
+                                       stream);
 }
 
 extern "C" int pdvc_level_pos_rows_backward_f32(const float* dpos, const int32_t* level_T, int num_levels, int N,

@@ -49,6 +49,7 @@ SIGNATURES = {
     + [_i] * 5 + [_vp, _vp, ctypes.c_long, _vp, ctypes.c_long, _vp, ctypes.c_long, _vp],
     "pdvc_level_pos_rows_forward_f32": [_vp] * 5 + [_i] * 5 + [_vp, _vp],
     "pdvc_level_pos_rows_backward_f32": [_vp, _vp] + [_i] * 4 + [_vp, _vp],
+    "pdvc_level_pos_rows_add_f32": [_vp] * 5 + [_i] * 5 + [_vp, _vp, _vp],
     "pdvc_groupnorm_rows_forward_f32": [_vp, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "pdvc_groupnorm_rows_backward_f32": [_vp] * 5 + [_i] * 4 + [_vp] * 4,
     "pdvc_groupnorm_rows_forward_out_f32": [_vp, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp, ctypes.c_long, _vp, _vp,

@@ -98,8 +98,7 @@ class DeformableTransformer(nn.Module):
         # encoder layer runs the fused attention block, their position gradients come back as per-(video, level)
         # sums through a small handle instead of a (N, S, d) gradient
         if fused_pos and not self.no_encoder and all(layer.block_ok(src_flatten) for layer in self.encoder.layers):
-            lvl_pos, handle = level_pos_rows_split(pos_embeds, self.level_embed)
-            lvl_pos._pdvc_level_grad = handle
+            lvl_pos, _ = level_pos_rows_split(pos_embeds, self.level_embed)  # a LevelPos, with the handle
         elif fused_pos:
             lvl_pos = level_pos_rows(pos_embeds, self.level_embed)
         else:

@@ -18,7 +18,7 @@ from pdvc import _native as _n
 from .addnorm import BWD_PARTS
 from .linear import colsum, wgrad_mm
 from .ms_deform_attn_func import NUM_SAMPLES, msda1d_backward, msda1d_forward
-from .posembed import level_row_sums
+from .posembed import LevelPos, level_row_sums
 
 
 class EncoderAttnBlockFunction(Function):
@@ -28,7 +28,7 @@ class EncoderAttnBlockFunction(Function):
         R = N * S
         D = d // M
         src2 = src.reshape(R, d).contiguous()
-        q = src2 + pos.reshape(R, d)
+        q = pos.add_to(src2) if isinstance(pos, LevelPos) else src2 + pos.reshape(R, d)
         value = torch.addmm(bv, src2, Wv.t())
         proj = torch.addmm(bq, q, Wq.t())
         nq = M * NUM_SAMPLES

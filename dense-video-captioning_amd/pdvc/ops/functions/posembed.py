@@ -69,17 +69,44 @@ class LevelPosGradFunction(Function):
         return d_dur, d_le, None, None
 
 
+class LevelPos:
+    """lvl_pos (N, S, d) kept as the inputs of its kernel: consumers that only add it to a tensor (the encoder's
+    query input src + pos, deformable_transformer.py:146) get the sum from one pass that generates the position
+    rows in registers (pdvc_level_pos_rows_add_f32) -- the (N, S, d) rows are never written or read.  Carries
+    no autograd history; `_pdvc_level_grad` is the gradient handle (LevelPosGradFunction)."""
+
+    def __init__(self, xe, dim_t, dur, level_embed, level_T, handle):
+        self.xe, self.dim_t, self.dur, self.level_embed, self.level_T = xe, dim_t, dur, level_embed, level_T
+        self._pdvc_level_grad = handle
+        self.shape = (xe.shape[0], xe.shape[1], dim_t.numel() + dur.shape[1])
+
+    def _call(self, add):
+        N, S = self.xe.shape
+        out = torch.empty(self.shape, dtype=torch.float32, device=self.xe.device)
+        _n.call("pdvc_level_pos_rows_add_f32", _n.ptr(self.xe), _n.ptr(self.dim_t), _n.ptr(self.dur),
+                _n.ptr(self.level_embed), _n.int_array(self.level_T), len(self.level_T), N, S, self.dim_t.numel(),
+                self.dur.shape[1], _n.ptr(add), _n.ptr(out), _n.stream())
+        return out
+
+    def add_to(self, x):
+        """x + lvl_pos for x (N*S, d) or (N, S, d) rows, shaped like x."""
+        return self._call(x.contiguous()).view(x.shape)
+
+    def materialize(self):
+        return self._call(None)
+
+
 def level_pos_rows_split(pyr, level_embed):
-    """(lvl_pos without autograd history, grad handle): lvl_pos as level_pos_rows computes it, and the (N, L, d)
-    handle through which consumers that can sum their own position gradients per (video, level) return them."""
+    """(lvl_pos as a LevelPos, grad handle): the position rows as level_pos_rows computes them, generated where
+    they are added, and the (N, L, d) handle through which consumers that can sum their own position gradients
+    per (video, level) return them."""
     pe = pyr.pe
     xe = torch.cat([pe.positions(m) for m in pyr.masks], 1).contiguous()
     dim_t = pe.freqs(xe.device)
     dur = pe.duration_embedding(pyr.duration).float().contiguous()
     level_T = tuple(int(m.shape[1]) for m in pyr.masks)
-    with torch.no_grad():
-        pos = LevelPosRowsFunction.apply(xe, dim_t, dur.detach(), level_embed.detach().contiguous(), level_T)
     handle = LevelPosGradFunction.apply(dur, level_embed, xe.shape[0], dim_t.numel())
+    pos = LevelPos(xe, dim_t, dur.detach(), level_embed.detach().contiguous(), level_T, handle)
     return pos, handle
 
 

@@ -306,6 +306,11 @@ int pdvc_level_pos_rows_forward_f32(const float* xe, const float* dim_t, const f
                                     void* stream);
 int pdvc_level_pos_rows_backward_f32(const float* dpos, const int32_t* level_T, int num_levels, int N, int S, int C,
                                      float* partials, void* stream);
+/* out = add + pos (add: (N, S, F + Dd), NULL for none, 16-byte aligned): the encoder's query input
+ * src + lvl_pos (deformable_transformer.py:146) with the position rows generated in registers, never stored. */
+int pdvc_level_pos_rows_add_f32(const float* xe, const float* dim_t, const float* dur, const float* level_embed,
+                                const int32_t* level_T, int num_levels, int N, int S, int F, int Dd, const float* add,
+                                float* out, void* stream);
 
 /* ---- FFN relu + dropout --------------------------------------------------------------------------------
  * forward, in place on h (rows x cols, cols % 4 == 0, 16-byte aligned): h = relu(h) * keep / (1 - p), keep a

@@ -68,3 +68,18 @@ def test_level_pos_rows_matches_reference_fixture():
     assert got.shape == want.shape
     err = (got - want).abs().max().item()
     assert err <= 1e-5, err
+
+
+def test_level_pos_add_matches_materialised_sum():
+    """LevelPos.add_to (the position rows generated inside the add, pdvc_level_pos_rows_add_f32) is bit-exact
+    against src + the materialised lvl_pos, and materialize() against level_pos_rows; on the reference fixture."""
+    from pdvc.ops.functions.posembed import level_pos_rows, level_pos_rows_split
+    pyr, level_embed, _ = _golden_pyramid(DEV)
+    full = level_pos_rows(pyr, level_embed)
+    lazy, handle = level_pos_rows_split(pyr, level_embed)
+    assert lazy._pdvc_level_grad is handle and tuple(lazy.shape) == tuple(full.shape)
+    assert torch.equal(lazy.materialize(), full)
+    src = torch.randn(full.shape, device=DEV)
+    assert torch.equal(lazy.add_to(src), src + full)
+    rows = src.view(-1, full.shape[-1])
+    assert torch.equal(lazy.add_to(rows), (src + full).view(-1, full.shape[-1]))
