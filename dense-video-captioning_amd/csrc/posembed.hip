@@ -67,6 +67,62 @@ __global__ __launch_bounds__(256) void level_pos_fwd_kernel(const float* __restr
     }
 }
 
+// The same values with the row arithmetic hoisted (the grid-stride form above divides 64-bit indices per float4):
+// block = rpi rows x c4n float4 lanes (c4n = C/4 divides 256), kPosRows consecutive flattened rows per block,
+// (video, row) advanced incrementally.  With C = 512, F = 256 a wave is all-sine or all-duration lanes.
+constexpr int kPosRows = 64;
+__global__ __launch_bounds__(256) void level_pos_rows_kernel(const float* __restrict__ xe,
+                                                             const float* __restrict__ dim_t,
+                                                             const float* __restrict__ dur,
+                                                             const float* __restrict__ lemb, PosLevels lv, int N,
+                                                             int S, int F, int Dd, const float* __restrict__ add,
+                                                             float* __restrict__ pos) {
+    const int C = F + Dd, c4n = C / 4, rpi = 256 / c4n;
+    const int cg = threadIdx.x % c4n, rr = threadIdx.x / c4n;
+    const int c = cg * 4;
+    const long rows = (long)N * S;
+    long r = (long)blockIdx.x * kPosRows + rr;
+    const long rend = min(rows, (long)(blockIdx.x + 1) * kPosRows);
+    if (r >= rend) return;
+    int n = (int)(r / S), s = (int)(r - (long)n * S);
+    float dt[4] = {1.f, 1.f, 1.f, 1.f};
+    if (c < F) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dt[k] = dim_t[c + k];
+    }
+    for (; r < rend; r += rpi) {
+        const int l = pos_level(lv, s);
+        const float4 le = *reinterpret_cast<const float4*>(lemb + (size_t)l * C + c);
+        float v[4];
+        if (c < F) {
+            const float x = xe[r];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float a = x / dt[k];
+                v[k] = ((c + k) & 1) ? cosf(a) : sinf(a);
+            }
+        } else {
+            const float4 d = *reinterpret_cast<const float4*>(dur + (size_t)n * Dd + (c - F));
+            v[0] = d.x;
+            v[1] = d.y;
+            v[2] = d.z;
+            v[3] = d.w;
+        }
+        float4 o = make_float4(v[0] + le.x, v[1] + le.y, v[2] + le.z, v[3] + le.w);
+        const size_t i = (size_t)r * c4n + cg;
+        if (add) {
+            const float4 a = reinterpret_cast<const float4*>(add)[i];
+            o = make_float4(a.x + o.x, a.y + o.y, a.z + o.z, a.w + o.w);
+        }
+        reinterpret_cast<float4*>(pos)[i] = o;
+        s += rpi;
+        while (s >= S) {
+            s -= S;
+            ++n;
+        }
+    }
+}
+
 // grid (C / 64, levels, N): 16 float4 column groups x 16 row lanes over the level's rows of one video
 __global__ __launch_bounds__(256) void level_pos_bwd_kernel(const float* __restrict__ dpos, PosLevels lv, int S,
                                                             int C, float* __restrict__ part) {
@@ -134,6 +190,14 @@ extern "C" int pdvc_level_pos_rows_add_f32(const float* xe, const float* dim_t, 
     if (rc) return rc;
     const long total = (long)N * S * ((F + Dd) / 4);
     if (total == 0) return PDVC_OK;
+    const int c4n = (F + Dd) / 4;
+    if (c4n <= 256 && 256 % c4n == 0) {
+        const long blocks = ((long)N * S + kPosRows - 1) / kPosRows;
+        hipLaunchKernelGGL(level_pos_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, xe, dim_t,
+                           dur, level_embed, lv, N, S, F, Dd, add, pos);
+        PDVC_CHECK_LAUNCH("level_pos_rows_kernel");
+        return PDVC_OK;
+    }
     const long want = (total + 255) / 256;
     const unsigned blocks = (unsigned)(want < 16384 ? want : 16384);
     hipLaunchKernelGGL(level_pos_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, xe, dim_t, dur,
