@@ -388,7 +388,7 @@ def main():
     for _ in range(a.warmup):
         step()
     log("timed steps")
-    names = ["pdvc_msda1d_forward_f32", "pdvc_msda1d_backward_f32", "pdvc_cap_gather_forward_f32",
+    names = ["pdvc_msda1d_forward_f32", "pdvc_msda1d_backward_ex_f32", "pdvc_cap_gather_forward_f32",
              "pdvc_cap_gather_backward_f32", "pdvc_seq_attention_forward_f32", "pdvc_seq_attention_backward_f32"]
     graphed = a.graph != "none"
     timer = _native.KernelTimer(names)
@@ -463,7 +463,7 @@ def main():
                               "traffic": traffic, "traffic_source": tsrc, "avg_launch_us": avg_ms * 1e3,
                               "timing": timing_note,
                               "alg_bytes_per_launch": avg_bytes}
-    kname = "pdvc_msda1d_backward_f32"  # the same for the backward (query-side + value-side kernels per launch)
+    kname = "pdvc_msda1d_backward_ex_f32"  # the same for the backward (query-side + value-side kernels per launch)
     if kname in ks and ks[kname]["launches"]:
         k = ks[kname]
         avg_ms = k["ms"] / k["launches"]
@@ -498,7 +498,7 @@ def main():
                              "share_of_step": v["ms"] / ksteps / (1e3 * el / a.steps)} for n, v in ks.items()}
     # the north-star comparison, like for like: MSDeformAttn fwd+bwd (the fused 1-D kernels, encoder + decoder
     # calls) per step on the GPU, from the HIP-event timings above, as videos/s against the CPU figure
-    msda_ms = sum(ks[n]["ms"] for n in ("pdvc_msda1d_forward_f32", "pdvc_msda1d_backward_f32") if n in ks) / ksteps
+    msda_ms = sum(ks[n]["ms"] for n in ("pdvc_msda1d_forward_f32", "pdvc_msda1d_backward_ex_f32") if n in ks) / ksteps
     if msda_ms > 0:
         result["msda_gpu"] = {"ms_per_step": msda_ms, "videos_per_s": B / (msda_ms * 1e-3) * world,
                               "what": "fused MSDeformAttn forward + backward kernels of every encoder and decoder "

@@ -925,13 +925,14 @@ constexpr int kVQPT = 4;  // queries per thread in its sort passes: a launch chu
 // UG: samples in flight per 16-lane group in the G4 walk (8: 96 VGPRs; 4: 66, more workgroups per CU where the LDS
 // allows -- the decoder's short sample lists)
 template <int CW, bool G4, int UG = 8>
-__global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
+__global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
                                                                      int Lq, int q0, int nq, int S, int M, int D,
                                                                      int accumulate,
                                                                      const float* __restrict__ gout,
                                                                      const float* __restrict__ save_attn,
                                                                      const float* __restrict__ save_loc,
-                                                                     float* __restrict__ grad_value) {
+                                                                     float* __restrict__ grad_value,
+                                                                     float* __restrict__ level_sums) {
     extern __shared__ __attribute__((aligned(16))) int lds_i[];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
@@ -1068,6 +1069,7 @@ __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_
         const int vg = wid * 4 + (lane >> 4);
         const int r0 = split(vg), r1 = split(vg + 1);
         const int jb = off[r0], je = off[r1 + 1];
+        float4 psum = make_float4(0.f, 0.f, 0.f, 0.f);  // this chunk's contributions to the group's rows
         if (r0 < r1 && jb < je) {  // per-group control flow below: no cross-lane operations
             const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)(gout + (size_t)b * Lq * MD), (short)0, (int)((size_t)Lq * MD * 4), 0x00020000);
@@ -1076,6 +1078,10 @@ __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_
                 if (r >= r0 && r < r1) {
                     float4* orow = reinterpret_cast<float4*>(ob + (size_t)r * MD);
                     if (mrow && mrow[r]) v = make_float4(0.f, 0.f, 0.f, 0.f);
+                    psum.x += v.x;
+                    psum.y += v.y;
+                    psum.z += v.z;
+                    psum.w += v.w;
                     if (accumulate) {
                         const float4 o = *orow;
                         v.x += o.x;
@@ -1128,6 +1134,40 @@ __global__ __launch_bounds__(kVW * 64) void msda1d_bwd_value_kernel(const uint8_
             }
             put(k - 1, alo);
             put(k, ahi);
+        }
+        if (level_sums) {  // the bias gradient's partial: column sums of the rows this workgroup wrote
+#pragma unroll
+            for (int d = 16; d < 64; d <<= 1) {
+                psum.x += __shfl_xor(psum.x, d, 64);
+                psum.y += __shfl_xor(psum.y, d, 64);
+                psum.z += __shfl_xor(psum.z, d, 64);
+                psum.w += __shfl_xor(psum.w, d, 64);
+            }
+            __syncthreads();  // every group's walk is done with the sorted entries: reuse their LDS
+            float4* red = reinterpret_cast<float4*>(lds_i);
+            if (lane < 16) red[wid * 16 + lane] = psum;
+            __syncthreads();
+            if (threadIdx.x < 16) {
+                float4 t = red[threadIdx.x];
+#pragma unroll
+                for (int w = 1; w < kVW; ++w) {
+                    const float4 u = red[w * 16 + threadIdx.x];
+                    t.x += u.x;
+                    t.y += u.y;
+                    t.z += u.z;
+                    t.w += u.w;
+                }
+                float4* o = reinterpret_cast<float4*>(level_sums + ((size_t)b * kL + l) * MD + (size_t)m * D) +
+                            threadIdx.x;
+                if (accumulate) {
+                    const float4 u = *o;
+                    t.x += u.x;
+                    t.y += u.y;
+                    t.z += u.z;
+                    t.w += u.w;
+                }
+                *o = t;
+            }
         }
         return;
     }
@@ -1399,13 +1439,21 @@ extern "C" int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_
     return PDVC_OK;
 }
 
-extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value_pad_mask, const float* ref,
-                                        int ref_dim, const float* proj, int proj_stride, int off_base, int logit_base,
-                                        const int32_t* level_T, int num_levels, int batch, int num_query,
-                                        int num_heads, int head_dim, int num_point, const float* grad_output,
-                                        const float* output, const float* save_attn, const float* save_loc,
-                                        float* grad_value,
-                                        float* grad_proj, float* grad_ref, void* stream) {
+extern "C" int pdvc_level_pos_rows_backward_f32(const float* dpos, const int32_t* level_T, int num_levels, int N,
+                                                int S, int C, float* partials, void* stream);
+
+extern "C" int pdvc_msda1d_backward_ex_f32(const float* value, const uint8_t* value_pad_mask, const float* ref,
+                                           int ref_dim, const float* proj, int proj_stride, int off_base,
+                                           int logit_base, const int32_t* level_T, int num_levels, int batch,
+                                           int num_query, int num_heads, int head_dim, int num_point,
+                                           const float* grad_output, const float* output, const float* save_attn,
+                                           const float* save_loc, float* grad_value, float* grad_proj,
+                                           float* grad_ref, float* grad_value_level_sums, void* stream) {
+    float* level_sums = grad_value_level_sums;
+    if (level_sums)
+        PDVC_CHECK_ARG(((long)num_heads * head_dim) % 4 == 0 && ((uintptr_t)level_sums % 16) == 0 &&
+                           ((uintptr_t)grad_value % 16) == 0,
+                       "level sums need num_heads * head_dim %% 4 == 0 and 16-byte aligned buffers");
     Levels1d lv;
     int S = 0;
     int rc = fill_levels(level_T, num_levels, num_point, lv, S);
@@ -1468,6 +1516,8 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
     if (nblk > 0) {
         if (num_query == 0) {
             hipError_t e = zero_async(grad_value, (size_t)batch * S * num_heads * head_dim, s);
+            if (e == hipSuccess && level_sums)
+                e = zero_async(level_sums, (size_t)batch * kL * num_heads * head_dim, s);
             if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_value: %s", hipGetErrorString(e));
             return PDVC_OK;
         }
@@ -1500,26 +1550,46 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
         }
         for (int q0 = 0; q0 < num_query; q0 += qchunk) {
             const int nq = (num_query - q0) < qchunk ? (num_query - q0) : qchunk;
-            const size_t lds = sizeof(int) * (2 * (size_t)(Tmax + 2) + 3 * (size_t)nq * kP + 2);
+            size_t lds = sizeof(int) * (2 * (size_t)(Tmax + 2) + 3 * (size_t)nq * kP + 2);
+            if (g4 && level_sums && lds < kVW * 16 * 16) lds = kVW * 16 * 16;  // the level-sum reduction
+            float* gsums = g4 ? level_sums : nullptr;
             const int acc = q0 > 0;
             if (g4 && value_ug(num_query, S) == 4)
                 hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, 4>), dim3((unsigned)nblk), dim3(kVW * 64), lds,
                                    s, value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
-                                   save_attn, save_loc, grad_value);
+                                   save_attn, save_loc, grad_value, gsums);
             else if (g4)
                 hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
                                    value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
-                                   save_attn, save_loc, grad_value);
+                                   save_attn, save_loc, grad_value, gsums);
             else if (head_dim <= 64)
                 hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, false>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
                                    value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
-                                   save_attn, save_loc, grad_value);
+                                   save_attn, save_loc, grad_value, gsums);
             else
                 hipLaunchKernelGGL((msda1d_bwd_value_kernel<2, false>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
                                    value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
-                                   save_attn, save_loc, grad_value);
+                                   save_attn, save_loc, grad_value, gsums);
             PDVC_CHECK_LAUNCH("msda1d_bwd_value_kernel");
+        }
+        if (level_sums && !g4) {  // the other value-gradient forms: one read of grad_value
+            int32_t lt[kL];
+            for (int l = 0; l < kL; ++l) lt[l] = lv.T[l];
+            rc = pdvc_level_pos_rows_backward_f32(grad_value, lt, kL, batch, S, num_heads * head_dim, level_sums, s);
+            if (rc) return rc;
         }
     }
     return PDVC_OK;
+}
+
+extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value_pad_mask, const float* ref,
+                                        int ref_dim, const float* proj, int proj_stride, int off_base, int logit_base,
+                                        const int32_t* level_T, int num_levels, int batch, int num_query,
+                                        int num_heads, int head_dim, int num_point, const float* grad_output,
+                                        const float* output, const float* save_attn, const float* save_loc,
+                                        float* grad_value, float* grad_proj, float* grad_ref, void* stream) {
+    return pdvc_msda1d_backward_ex_f32(value, value_pad_mask, ref, ref_dim, proj, proj_stride, off_base, logit_base,
+                                       level_T, num_levels, batch, num_query, num_heads, head_dim, num_point,
+                                       grad_output, output, save_attn, save_loc, grad_value, grad_proj, grad_ref,
+                                       nullptr, stream);
 }

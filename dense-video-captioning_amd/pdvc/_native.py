@@ -25,6 +25,7 @@ SIGNATURES = {
     "pdvc_ms_deform_sample_backward_f32": [_vp] * 5 + [_i] * 8 + [_vp] * 3,
     "pdvc_msda1d_forward_f32": [_vp, _u8p, _vp, _i, _i, _i, _vp, _i, _vp] + [_i] * 6 + [_vp] * 4,
     "pdvc_msda1d_backward_f32": [_vp, _u8p, _vp, _i, _vp, _i, _i, _i, _vp] + [_i] * 6 + [_vp] * 8,
+    "pdvc_msda1d_backward_ex_f32": [_vp, _u8p, _vp, _i, _vp, _i, _i, _i, _vp] + [_i] * 6 + [_vp] * 9,
     "pdvc_cap_gather_forward_f32": [_vp, _u8p, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _vp] + [_i] * 6 + [_vp] * 3,
     "pdvc_cap_gather_backward_f32": [_vp, _u8p, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _vp] + [_i] * 6 + [_vp] * 6,
     "pdvc_cap_value_grad_f32": [_u8p, _vp] + [_i] * 8 + [_vp] * 6,

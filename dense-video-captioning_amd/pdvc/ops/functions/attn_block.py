@@ -70,11 +70,13 @@ class EncoderAttnBlockFunction(Function):
         dWo = wgrad_mm(d_s2, out.view(R, d))
         d_out = torch.mm(d_s2, Wo)
         nq = M * NUM_SAMPLES
-        gv, gp, _ = msda1d_backward(value.view(N, S, M, D), pad_mask, proj.view(N, S, -1), ref, save_attn, save_loc,
-                                    out, d_out.view(N, S, d), level_T, 0, nq)
+        gv, gp, _, vsums = msda1d_backward(value.view(N, S, M, D), pad_mask, proj.view(N, S, -1), ref, save_attn,
+                                           save_loc, out, d_out.view(N, S, d), level_T, 0, nq,
+                                           level_sums=d % 4 == 0)
         gv2 = gv.view(R, d)
         gp2 = gp.view(R, -1)
-        dbv = colsum(gv2)
+        # the value bias gradient from the value-gradient kernel's per-(video, level) row sums
+        dbv = vsums.view(-1, d).sum(0) if vsums is not None else colsum(gv2)
         dWv = wgrad_mm(gv2, src2)
         dbq = colsum(gp2)
         dWq = wgrad_mm(gp2, q)

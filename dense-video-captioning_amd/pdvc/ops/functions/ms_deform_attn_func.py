@@ -121,9 +121,10 @@ _DELTA_FROM_OUT = os.environ.get("PDVC_MSDA_DELTA_OUT", "0") == "1"
 
 
 def msda1d_backward(value, pad_mask, proj, ref, save_attn, save_loc, out, grad_out, level_T, off_base, logit_base,
-                    need_ref=False):
-    """pdvc_msda1d_backward_f32: returns (grad_value, grad_proj, grad_ref or None).  `out` (the forward output)
-    is passed to the kernel only under PDVC_MSDA_DELTA_OUT=1."""
+                    need_ref=False, level_sums=False):
+    """pdvc_msda1d_backward_ex_f32: returns (grad_value, grad_proj, grad_ref or None), plus with `level_sums` the
+    (N, L, M*D) per-(video, level) column sums of grad_value (the value projection's bias gradient is their
+    sum).  `out` (the forward output) is passed to the kernel only under PDVC_MSDA_DELTA_OUT=1."""
     N, S, M, D = value.shape
     Lq, C = proj.shape[1], proj.shape[2]
     RD = ref.shape[3]
@@ -131,11 +132,12 @@ def msda1d_backward(value, pad_mask, proj, ref, save_attn, save_loc, out, grad_o
     gv = torch.empty_like(value)
     gp = torch.zeros_like(proj) if C != 2 * M * NUM_SAMPLES else torch.empty_like(proj)
     gr = torch.empty_like(ref) if need_ref else None
-    _n.call("pdvc_msda1d_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(ref), RD, _n.ptr(proj), C,
+    ls = torch.empty(N, nl, M * D, dtype=value.dtype, device=value.device) if level_sums else None
+    _n.call("pdvc_msda1d_backward_ex_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(ref), RD, _n.ptr(proj), C,
             off_base, logit_base, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(grad_out),
-            _n.ptr(out) if _DELTA_FROM_OUT else None, _n.ptr(save_attn), _n.ptr(save_loc), _n.ptr(gv), _n.ptr(gp), _n.ptr(gr), _n.stream(),
-            meta=(N, Lq, S, M, D, NUM_SAMPLES))
-    return gv, gp, gr
+            _n.ptr(out) if _DELTA_FROM_OUT else None, _n.ptr(save_attn), _n.ptr(save_loc), _n.ptr(gv), _n.ptr(gp), _n.ptr(gr), _n.ptr(ls),
+            _n.stream(), meta=(N, Lq, S, M, D, NUM_SAMPLES))
+    return (gv, gp, gr, ls) if level_sums else (gv, gp, gr)
 
 
 class MSDA1dFunction(Function):

@@ -143,6 +143,16 @@ int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value_pad_mask, 
                              int head_dim, int num_point, const float* grad_output, const float* output,
                              const float* save_attn, const float* save_loc, float* grad_value, float* grad_proj,
                              float* grad_ref, void* stream);
+/* The same, plus grad_value_level_sums (N, L, M*D) (NULL for none; M*D % 4 == 0, 16-byte aligned):
+ * sums[(n*L + l)*M*D + c] = sum over the rows s of level l of grad_value[n, s, c] -- the value projection's bias
+ * gradient is their sum over n and l.  At D = 64 the value-gradient kernel forms them from the rows it writes;
+ * the other forms read grad_value once more. */
+int pdvc_msda1d_backward_ex_f32(const float* value, const uint8_t* value_pad_mask, const float* ref,
+                                int ref_dim, const float* proj, int proj_stride, int off_base, int logit_base,
+                                const int32_t* level_T, int num_levels, int batch, int num_query, int num_heads,
+                                int head_dim, int num_point, const float* grad_output, const float* output,
+                                const float* save_attn, const float* save_loc, float* grad_value, float* grad_proj,
+                                float* grad_ref, float* grad_value_level_sums, void* stream);
 
 /* ---- caption-head border gather (MSDeformAttnCap) ----------------------------------------------------
  * value (N,S,M,D); value_pad_mask (N,S) or NULL; row_video (R,) int32 DEVICE: video of each query row;

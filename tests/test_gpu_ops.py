@@ -520,3 +520,36 @@ def test_module_msdeformattn_vs_golden(ref_dim):
     close(x.grad, d["grad_x"], 1e-4, "grad_x")
     for n, p in m.named_parameters():
         close(p.grad, d["grad." + n], 1e-4, n)
+
+
+@pytest.mark.parametrize("D,T_l,Lq,masked", [(64, (40, 20, 10, 5), 37, True), (64, (128, 64, 32, 16), 240, False),
+                                             (64, (1024, 512, 256, 128), 1920, True), (32, (40, 20, 10, 5), 37, True)])
+def test_msda1d_value_level_sums(D, T_l, Lq, masked):
+    """pdvc_msda1d_backward_ex_f32's per-(video, level) column sums of grad_value (the value bias gradient's
+    partials) against the sums of the grad_value it returns: formed inside the D = 64 value-gradient kernel
+    (one query chunk; two chunks at S = 1920, the second accumulating), by a second pass otherwise (D = 32)."""
+    from pdvc.ops.functions.ms_deform_attn_func import msda1d_backward, msda1d_forward
+    rng = np.random.RandomState(D + Lq)
+    M, N = 8 if D == 64 else 4, 2
+    S = sum(T_l)
+    value = cu(rng.randn(N, S, M, D), torch.float32)
+    proj = cu(np.concatenate([rng.randn(N, Lq, M * 16) * 3.0, rng.randn(N, Lq, M * 16)], -1), torch.float32)
+    ref = cu(rng.uniform(-0.05, 1.05, size=(N, Lq, 4, 1)), torch.float32)
+    mask = None
+    if masked:
+        mk = np.zeros((N, S), bool)
+        mk[1, 3:9] = True
+        mk[0, T_l[0]:T_l[0] + 4] = True
+        mask = cu(mk).view(torch.uint8)
+    gout = cu(rng.randn(N, Lq, M * D), torch.float32)
+    out, sa, sl = msda1d_forward(value, mask, proj, ref, T_l, 0, M * 16)
+    gv, gp, gr, ls = msda1d_backward(value, mask, proj, ref, sa, sl, out, gout, T_l, 0, M * 16, level_sums=True)
+    gv0, gp0, _ = msda1d_backward(value, mask, proj, ref, sa, sl, out, gout, T_l, 0, M * 16)
+    # the counting sort's LDS cursors order samples within a bucket arbitrarily: run-to-run ulp differences
+    assert torch.equal(gp, gp0) and (gv - gv0).abs().max().item() <= 1e-5
+    g = gv.double().view(N, S, M * D)
+    starts = np.cumsum((0,) + tuple(T_l))
+    exp = torch.stack([g[:, starts[i]:starts[i + 1]].sum(1) for i in range(4)], 1)
+    assert ls.shape == exp.shape
+    err = (ls.double() - exp).abs().max().item()
+    assert err <= 1e-5 * (g.abs().sum(1).max().item() + 1.0), err
