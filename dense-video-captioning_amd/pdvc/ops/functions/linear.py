@@ -200,6 +200,9 @@ def dense(x, weight, bias=None, relu=False):
     return F.relu(y) if relu else y
 
 
+LEVEL_SUM_USES = [0]  # bias gradients taken from a consumer's row sums (tests check the hand-over happens)
+
+
 class MultiLinearFunction(Function):
     """Several nn.Linear layers applied to the same input x: (x W_0^T + b_0, x W_1^T + b_1, ...).  Forward is
     one GEMM per layer; the backward accumulates the input gradient of all of them in the epilogues of their
@@ -231,7 +234,12 @@ class MultiLinearFunction(Function):
                 gx = torch.mm(g2, w)
             else:
                 gx.addmm_(g2, w)
-            gwb += [wgrad_mm(g2, x2), colsum(g2)]
+            # a fused deformable-attention consumer hands its value gradient over with per-(video, level) row sums
+            # (MSDA1dFunction): the bias gradient from those instead of another pass over g
+            ls = getattr(g, "_pdvc_level_sums", None)
+            LEVEL_SUM_USES[0] += ls is not None
+            gb = ls.view(-1, ls.shape[-1]).sum(0) if ls is not None and ls.shape[-1] == w.shape[0] else colsum(g2)
+            gwb += [wgrad_mm(g2, x2), gb]
         if gx is None:
             gx = torch.zeros_like(x2)
         return (gx.view(ctx.shape), *gwb)

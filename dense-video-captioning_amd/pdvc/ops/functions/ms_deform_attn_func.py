@@ -143,27 +143,40 @@ def msda1d_backward(value, pad_mask, proj, ref, save_attn, save_loc, out, grad_o
 class MSDA1dFunction(Function):
     """Fused MSDeformAttn core for a 1-D temporal pyramid (GPU semantics: zero padding).
 
-    value (N,S,M,D); pad_mask (N,S) uint8 or None; proj (N,Lq,C) holding offsets at [off_base, +M*16)
-    and attention logits at [logit_base, +M*16); ref (N,Lq,L,1|2).  Returns (N,Lq,M*D)."""
+    value (N,S,M,D), or (N,S,M*D) with `heads` = M; pad_mask (N,S) uint8 or None; proj (N,Lq,C) holding offsets
+    at [off_base, +M*16) and attention logits at [logit_base, +M*16); ref (N,Lq,L,1|2).  Returns (N,Lq,M*D).
+
+    With a (N,S,M*D) value (a projection's output, as the decoder passes it) the value gradient comes back in that
+    shape carrying `_pdvc_level_sums`, its per-(video, level) column sums from the value-gradient kernel: the
+    projection's backward (MultiLinearFunction) takes its bias gradient from them instead of re-reading it."""
 
     @staticmethod
-    def forward(ctx, value, pad_mask, proj, ref, level_T, off_base, logit_base):
+    def forward(ctx, value, pad_mask, proj, ref, level_T, off_base, logit_base, heads=None):
         value, proj, ref = value.contiguous(), proj.contiguous(), ref.contiguous()
+        flat = value.dim() == 3
+        v4 = value.view(value.shape[0], value.shape[1], heads, -1) if flat else value
         need = ctx.needs_input_grad[0] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
-        out, save_attn, save_loc = msda1d_forward(value, pad_mask, proj, ref, level_T, off_base, logit_base, need)
+        out, save_attn, save_loc = msda1d_forward(v4, pad_mask, proj, ref, level_T, off_base, logit_base, need)
         if need:
-            ctx.save_for_backward(value, pad_mask, proj, ref, save_attn, save_loc, out)
-        ctx.meta = (tuple(level_T), off_base, logit_base)
+            ctx.save_for_backward(v4, pad_mask, proj, ref, save_attn, save_loc, out)
+        ctx.meta = (tuple(level_T), off_base, logit_base, flat)
         return out
 
     @staticmethod
     @once_differentiable
     def backward(ctx, grad_out):
         value, pad_mask, proj, ref, save_attn, save_loc, out = ctx.saved_tensors
-        level_T, off_base, logit_base = ctx.meta
-        gv, gp, gr = msda1d_backward(value, pad_mask, proj, ref, save_attn, save_loc, out, grad_out.contiguous(),
-                                     level_T, off_base, logit_base, need_ref=ctx.needs_input_grad[3])
-        return gv, None, gp, gr, None, None, None
+        level_T, off_base, logit_base, flat = ctx.meta
+        N, S, M, D = value.shape
+        sums = flat and (M * D) % 4 == 0 and ctx.needs_input_grad[0]
+        res = msda1d_backward(value, pad_mask, proj, ref, save_attn, save_loc, out, grad_out.contiguous(), level_T,
+                              off_base, logit_base, need_ref=ctx.needs_input_grad[3], level_sums=sums)
+        gv, gp, gr = res[:3]
+        if flat:
+            gv = gv.view(N, S, M * D)
+            if sums:
+                gv._pdvc_level_sums = res[3]
+        return gv, None, gp, gr, None, None, None, None
 
 
 class CapGatherFunction(Function):

@@ -108,8 +108,9 @@ class MSDeformAttn(nn.Module):
             if input_padding_mask is not None:
                 mask = input_padding_mask.contiguous().view(torch.uint8)
             proj = self.project_query(query)
-            out = MSDA1dFunction.apply(value.reshape(N, Len_in, M, D), mask, proj, reference_points, T, 0,
-                                       M * NUM_SAMPLES_FUSED)
+            if value.shape != (N, Len_in, M * D):  # no reshape node otherwise: the value gradient keeps its sums
+                value = value.reshape(N, Len_in, M * D)
+            out = MSDA1dFunction.apply(value, mask, proj, reference_points, T, 0, M * NUM_SAMPLES_FUSED, M)
             return self.output_proj(out)
         return self.output_proj(self._lifted_general(query, reference_points, value, T, input_padding_mask))
 

@@ -105,3 +105,54 @@ def test_encoder_with_level_position_handle_matches_per_level_path(monkeypatch):
     close(m1, m2, 1e-5, "memory")
     for n in g2:
         close(g1[n], g2[n], 1e-4, n)
+
+
+def test_decoder_value_bias_from_level_sums(monkeypatch):
+    """The decoder's value projections (MultiLinearFunction over the encoder memory) take their bias gradients
+    from the row sums the fused deformable attention returns with the value gradient: the hand-over happens,
+    and the bias gradients equal colsum over the value gradient."""
+    from pdvc.ops.functions import linear as L
+    from pdvc.ops.functions.linear import multi_dense
+    from pdvc.ops.modules.ms_deform_attn import MSDeformAttn
+    torch.manual_seed(3)
+    N, T_l, Lq = 2, (64, 32, 16, 8), 50
+    S = sum(T_l)
+    layers = [MSDeformAttn(512, 4, 8, 4).to(DEV) for _ in range(2)]
+    mem = torch.randn(N, S, 512, device=DEV, requires_grad=True)
+    q = torch.randn(N, Lq, 512, device=DEV)
+    ref = torch.rand(N, Lq, 4, 2, device=DEV)
+    shapes, lsi = T_l, None
+    g = torch.randn(N, Lq, 512, device=DEV)
+
+    def run(handover):
+        for m in layers:
+            m.zero_grad(set_to_none=True)
+        if not handover:
+            monkeypatch.setattr(MSDA1dFunction_cls(), "backward", _strip_sums(MSDA1dFunction_cls().backward))
+        vals = multi_dense(mem, [m.value_proj for m in layers])
+        out = sum(m(q, ref, mem, shapes, lsi, None, value=v) for m, v in zip(layers, vals))
+        before = L.LEVEL_SUM_USES[0]
+        (out * g).sum().backward()
+        return L.LEVEL_SUM_USES[0] - before, [m.value_proj.bias.grad.clone() for m in layers]
+
+    used, gb1 = run(True)
+    assert used == 2
+    used0, gb0 = run(False)
+    assert used0 == 0
+    for a, b in zip(gb1, gb0):
+        assert (a - b).abs().max().item() <= 1e-4 * (b.abs().max().item() + 1.0)
+
+
+def MSDA1dFunction_cls():
+    from pdvc.ops.functions.ms_deform_attn_func import MSDA1dFunction
+    return MSDA1dFunction
+
+
+def _strip_sums(bwd):
+    def backward(ctx, grad_out):
+        res = bwd(ctx, grad_out)
+        gv = res[0]
+        if gv is not None and hasattr(gv, "_pdvc_level_sums"):
+            gv = gv.clone()
+        return (gv,) + tuple(res[1:])
+    return staticmethod(backward)
