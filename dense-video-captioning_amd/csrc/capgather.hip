@@ -248,7 +248,7 @@ template <int CW>  // channels per lane: D <= 64 * CW, channel = lane + 64 c
 __global__ __launch_bounds__(kCVW * 64) void cap_value_grad_kernel(
     const uint8_t* __restrict__ vmask, CapLevels lv, int S, int M, int D, int R, int s0, int ns, int accumulate,
     const int32_t* __restrict__ vr_start, const int32_t* __restrict__ vr_rows, const float* __restrict__ save_loc,
-    const float* __restrict__ gsamp, float* __restrict__ grad_value) {
+    const float* __restrict__ gsamp, float* __restrict__ grad_value, float* __restrict__ level_sums) {
     extern __shared__ __attribute__((aligned(16))) int lds_c[];
     __shared__ int wsum[kCVW];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -335,8 +335,11 @@ __global__ __launch_bounds__(kCVW * 64) void cap_value_grad_kernel(
         return lo;
     };
     const int r0 = split(wid), r1 = split(wid + 1);
-    if (r0 >= r1) return;
     const size_t MD = (size_t)M * D;
+    float psum[CW];  // this chunk's contributions to the wave's rows (the level sums)
+#pragma unroll
+    for (int c = 0; c < CW; ++c) psum[c] = 0.f;
+    if (r0 < r1) {
     float* ob = grad_value + ((size_t)b * S + st) * MD + (size_t)m * D;
     float accp[CW], acch[CW];
 #pragma unroll
@@ -351,6 +354,7 @@ __global__ __launch_bounds__(kCVW * 64) void cap_value_grad_kernel(
                 const int ch = lane + 64 * c;
                 if (ch < D) {
                     float v = accp[c];
+                    psum[c] += v;
                     if (accumulate) v += orow[ch];
                     orow[ch] = v;
                 }
@@ -391,6 +395,24 @@ __global__ __launch_bounds__(kCVW * 64) void cap_value_grad_kernel(
         }
     }
     while (k <= r1) close_bucket();
+    }
+    if (level_sums) {  // the bias gradient's partial: column sums of the rows this workgroup wrote
+        __syncthreads();  // every wave is done with the sorted samples: reuse their LDS
+        float* red = reinterpret_cast<float*>(lds_c);
+#pragma unroll
+        for (int c = 0; c < CW; ++c) red[(wid * CW + c) * 64 + lane] = psum[c];
+        __syncthreads();
+        for (int i = threadIdx.x; i < 64 * CW; i += blockDim.x) {
+            const int c = i >> 6, ln = i & 63, ch = ln + 64 * c;
+            if (ch < D) {
+                float t = red[c * 64 + ln];
+                for (int w = 1; w < kCVW; ++w) t += red[(w * CW + c) * 64 + ln];
+                float* o = level_sums + ((size_t)b * cL + l) * MD + (size_t)m * D + ch;
+                if (accumulate) t += *o;
+                *o = t;
+            }
+        }
+    }
 }
 
 static int cap_setup(const int32_t* level_T, int num_levels, int num_point, int head_dim, int num_heads, int ref_dim,
@@ -487,11 +509,12 @@ extern "C" int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* v
     return PDVC_OK;
 }
 
-extern "C" int pdvc_cap_value_grad_f32(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels,
-                                       int batch, int num_heads, int head_dim, int num_point, int rows, int steps,
-                                       int max_rows_per_video, const int32_t* video_row_start,
-                                       const int32_t* video_rows, const float* save_loc, const float* grad_samples,
-                                       float* grad_value, void* stream) {
+extern "C" int pdvc_cap_value_grad_ex_f32(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels,
+                                          int batch, int num_heads, int head_dim, int num_point, int rows, int steps,
+                                          int max_rows_per_video, const int32_t* video_row_start,
+                                          const int32_t* video_rows, const float* save_loc, const float* grad_samples,
+                                          float* grad_value, float* grad_value_level_sums, void* stream) {
+    float* level_sums = grad_value_level_sums;
     CapLevels lv;
     int S = 0;
     PDVC_CHECK_ARG(level_T != nullptr && num_levels == cL && num_point == cP, "caption value gradient needs %d x %d",
@@ -509,6 +532,7 @@ extern "C" int pdvc_cap_value_grad_f32(const uint8_t* value_pad_mask, const int3
     if (nblk == 0) return PDVC_OK;
     if (steps == 0 || max_rows_per_video == 0) {
         hipError_t e = zero_async(grad_value, (size_t)batch * S * num_heads * head_dim, s);
+        if (e == hipSuccess && level_sums) e = zero_async(level_sums, (size_t)batch * cL * num_heads * head_dim, s);
         return e == hipSuccess ? PDVC_OK : pdvc_set_error(PDVC_ERR_LAUNCH, "memset: %s", hipGetErrorString(e));
     }
     int Tmax = 0;
@@ -531,12 +555,14 @@ extern "C" int pdvc_cap_value_grad_f32(const uint8_t* value_pad_mask, const int3
     const int cw = head_dim <= 64 ? 1 : head_dim <= 128 ? 2 : head_dim <= 256 ? 4 : 8;
     for (int s0 = 0; s0 < steps; s0 += chunk) {
         const int ns = steps - s0 < chunk ? steps - s0 : chunk;
-        const size_t lds = sizeof(int) * (2 * (size_t)(Tmax + 2) + 3 * (size_t)ns * max_rows_per_video * cP);
+        size_t lds = sizeof(int) * (2 * (size_t)(Tmax + 2) + 3 * (size_t)ns * max_rows_per_video * cP);
+        const size_t red = sizeof(float) * kCVW * 64 * cw;  // the level-sum reduction
+        if (level_sums && lds < red) lds = red;
         const int acc = s0 > 0;
         const dim3 grid((unsigned)nblk), block(kCVW * 64);
 #define CVG(CW) hipLaunchKernelGGL((cap_value_grad_kernel<CW>), grid, block, lds, s, value_pad_mask, lv, S, num_heads, \
                                    head_dim, rows, s0, ns, acc, video_row_start, video_rows, save_loc, grad_samples,     \
-                                   grad_value)
+                                   grad_value, level_sums)
         if (cw == 1) CVG(1);
         else if (cw == 2) CVG(2);
         else if (cw == 4) CVG(4);
@@ -545,4 +571,14 @@ extern "C" int pdvc_cap_value_grad_f32(const uint8_t* value_pad_mask, const int3
         PDVC_CHECK_LAUNCH("cap_value_grad_kernel");
     }
     return PDVC_OK;
+}
+
+extern "C" int pdvc_cap_value_grad_f32(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels,
+                                       int batch, int num_heads, int head_dim, int num_point, int rows, int steps,
+                                       int max_rows_per_video, const int32_t* video_row_start,
+                                       const int32_t* video_rows, const float* save_loc, const float* grad_samples,
+                                       float* grad_value, void* stream) {
+    return pdvc_cap_value_grad_ex_f32(value_pad_mask, level_T, num_levels, batch, num_heads, head_dim, num_point, rows,
+                                      steps, max_rows_per_video, video_row_start, video_rows, save_loc, grad_samples,
+                                      grad_value, nullptr, stream);
 }

@@ -326,10 +326,11 @@ class LSTMDSACaptioner(Captioner):
         off_hs = F.linear(hs_rows, w["W_off_hs"], w["b_off"])
         Nv, S, _ = value.shape
         M = core.deformable_att.n_heads
+        # the projection output itself (no view node): its gradient comes back with the bias gradient's row sums
         Hs = CaptionDecodeFunction.apply(
-            value.view(Nv, S, M, -1), xe, hs_g, off_hs, ref_rows, w["W_h"], w["b_h"], core.ctx2att.weight,
+            value, xe, hs_g, off_hs, ref_rows, w["W_h"], w["b_h"], core.ctx2att.weight,
             core.ctx2att.bias, core.alpha_net.weight.view(-1), core.alpha_net.bias, w["W_att"], mask_u8, row_video,
-            tuple(level_T), rd1_rows, video_csr)
+            tuple(level_T), rd1_rows, video_csr, M)
         logits = self.logit(self.dropout(Hs))
         if pick_target is not None:
             return logprob_pick(logits, pick_target[:, :n_steps])

@@ -36,7 +36,12 @@ class CaptionDecodeFunction(Function):
 
     @staticmethod
     def forward(ctx, value, xe, hs_g, off_hs, ref, W_h, b_h, W_ctx, b_ctx, alpha_w, alpha_b, W_att, pad_mask,
-                row_video, level_T, rd1_rows, video_csr=None):
+                row_video, level_T, rd1_rows, video_csr=None, heads=None):
+        # value (Nv, S, M, D), or the projection's (Nv, S, M*D) output with `heads` = M: then the value gradient
+        # goes back in that shape carrying its per-(video, level) row sums (`_pdvc_level_sums`, as MSDA1dFunction)
+        ctx.flat_value = value.dim() == 3
+        if ctx.flat_value:
+            value = value.view(value.shape[0], value.shape[1], heads, -1)
         value, xe, off_hs, ref = value.contiguous(), xe.contiguous(), off_hs.contiguous(), ref.contiguous()
         hs_g = hs_g.contiguous()
         W_h, W_ctx, W_att = W_h.contiguous(), W_ctx.contiguous(), W_att.contiguous()
@@ -158,8 +163,9 @@ class CaptionDecodeFunction(Function):
                     torch.mm(dHP[i], W_h, out=dh)
         if deferred:
             vr_start, vr_rows, max_rows = video_csr
-            _n.call("pdvc_cap_value_grad_f32", _n.ptr(pad_mask), lvl, nl, Nv, M, D, NS // nl, R, n, int(max_rows),
-                    _n.ptr(vr_start), _n.ptr(vr_rows), _n.ptr(LOC), _n.ptr(dCLIP_all), _n.ptr(gv), st)
+            lsums = torch.empty(Nv, nl, M * D, dtype=gv.dtype, device=gv.device) if ctx.flat_value else None
+            _n.call("pdvc_cap_value_grad_ex_f32", _n.ptr(pad_mask), lvl, nl, Nv, M, D, NS // nl, R, n, int(max_rows),
+                    _n.ptr(vr_start), _n.ptr(vr_rows), _n.ptr(LOC), _n.ptr(dCLIP_all), _n.ptr(gv), _n.ptr(lsums), st)
         # weight gradients: one GEMM each over every (step, row)
         d_gates = dHP[..., n_off + A:]                       # (n, R, 4H), row stride Ph: xe's gradient as is
         d_hs_g = d_gates.sum(0)
@@ -175,5 +181,9 @@ class CaptionDecodeFunction(Function):
         dalpha_w = colsum(GAW.view(-1, A))
         dalpha_b = GAB.sum().reshape(1)
         dW_att = wgrad_mm(d_gates.reshape(-1, G), RES.view(-1, M * D))
+        if ctx.flat_value:
+            gv = gv.view(Nv, -1, M * D)
+            if deferred:
+                gv._pdvc_level_sums = lsums
         return (gv, d_gates, d_hs_g, d_off_hs, gr, dW_h, db_h, dW_ctx, db_ctx, dalpha_w, dalpha_b, dW_att, None, None,
-                None, None, None)
+                None, None, None, None)

@@ -305,6 +305,13 @@ int pdvc_cap_value_grad_f32(const uint8_t* value_pad_mask, const int32_t* level_
                             int num_heads, int head_dim, int num_point, int rows, int steps, int max_rows_per_video,
                             const int32_t* video_row_start, const int32_t* video_rows, const float* save_loc,
                             const float* grad_samples, float* grad_value, void* stream);
+/* The same, plus grad_value_level_sums (N, L, M*D) or NULL: per-(video, level) column sums of grad_value, formed
+ * from the rows the kernel writes (the caption value projection's bias gradient is their sum over n and l). */
+int pdvc_cap_value_grad_ex_f32(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels, int batch,
+                               int num_heads, int head_dim, int num_point, int rows, int steps, int max_rows_per_video,
+                               const int32_t* video_row_start, const int32_t* video_rows, const float* save_loc,
+                               const float* grad_samples, float* grad_value, float* grad_value_level_sums,
+                               void* stream);
 
 /* ---- encoder positional input ------------------------------------------------------------------------
  * pos[n, s, c] = (c < F ? (c even ? sin : cos)(xe[n*S + s] / dim_t[c]) : dur[n*Dd + c - F])

@@ -132,7 +132,11 @@ def test_training_step_matches_reference(case, no_padding):
     close(out["pred_count"], d["pred_count"], 1e-4, 1e-4, "pred_count")
     # captioning logits (log-probabilities of every teacher-forced step): north-star bar 1e-4
     close(out["caption_probs"]["cap_prob_train"], d["cap_prob_train"], 1e-4, 1e-4, "cap_prob_train")
+    from pdvc.ops.functions import linear as L
+    before = L.LEVEL_SUM_USES[0]
     total.backward()
+    # the memory projections took bias gradients from their consumers' row sums (decoder MSDA, caption gather)
+    assert L.LEVEL_SUM_USES[0] > before
     for n, p in model.named_parameters():
         if "gradnone." + n in d.files:
             assert p.grad is None, f"{n} must receive no gradient (as in the reference)"
