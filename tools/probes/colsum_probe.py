@@ -20,5 +20,5 @@ for rows, cols in ((983040, 256), (983040, 512), (524288, 512), (262144, 512), (
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 20
     err = (y.double() - ref).abs().max().item()
-    print(f"{rows}x{cols}: {ms * 1e3:7.1f} us  {rows * cols * 4 / ms / 1e9:6.0f} GB/s  err {err:.2e}", flush=True)
+    print(f"{rows}x{cols}: {ms * 1e3:7.1f} us  {rows * cols * 4 / ms / 1e6:6.0f} GB/s  err {err:.2e}", flush=True)
     del x
