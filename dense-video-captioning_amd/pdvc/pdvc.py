@@ -183,7 +183,12 @@ class PDVC(nn.Module):
         replay (graph-safe RNG; the HIP kernels draw their seeds on the device)."""
         sample = (dt["video_tensor"], dt["video_mask"], dt["video_length"][:, 1].contiguous())
         mod = _TrunkModule(self)
-        key = tuple((tuple(t.shape), t.dtype) for t in sample)
+        # the padding decision is captured with the graph: take it from THIS batch, and key the replay on it
+        no_padding = bool(dt.get("video_mask_all_valid", False))
+        object.__setattr__(self, "_no_padding", no_padding)
+        key = (tuple((tuple(t.shape), t.dtype) for t in sample), no_padding)
+        from .precision import begin_capture
+        begin_capture()
         graphed = torch.cuda.make_graphed_callables(mod, sample, allow_unused_input=True)
         # kept outside the module registry: state_dict keys stay the reference's
         object.__setattr__(self, "_graph_key", key)
@@ -192,8 +197,9 @@ class PDVC(nn.Module):
     def _run_trunk(self, dt):
         args = (dt["video_tensor"], dt["video_mask"], dt["video_length"][:, 1].contiguous())
         g = self.__dict__.get("_graphed_trunk")
-        if g is not None and self.training and tuple((tuple(t.shape), t.dtype) for t in args) == self._graph_key:
-            return g(*args)
+        key = (tuple((tuple(t.shape), t.dtype) for t in args), bool(self.__dict__.get("_no_padding", False)))
+        if g is not None and self.training and key == self._graph_key:
+            return g(*args)  # same shapes and padding decision as the capture
         return self.trunk(*args)
 
     def forward(self, dt, criterion, transformer_input_type, eval_mode=False):

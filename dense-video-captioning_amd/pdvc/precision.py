@@ -40,18 +40,37 @@ _F32 = torch.float32
 _BF = torch.bfloat16
 
 
+_CAPTURE = [0]  # capture epoch: bumped by begin_capture() before every graph capture of the step
+
+
+def begin_capture():
+    """Start a new capture epoch: no rounding made before this point is reused inside the capture that follows.
+
+    A rounding cached eagerly (StepGraph's warm-up steps run on the very `dt` tensors the capture then reads)
+    would otherwise be a cache hit at capture time, so no cast kernel would be recorded, and every replay after
+    `StepGraph.load(next batch)` would multiply the warm-up batch's bf16 features."""
+    _CAPTURE[0] += 1
+
+
+def _epoch():
+    return _CAPTURE[0] if torch.cuda.is_current_stream_capturing() else 0
+
+
 def _bf(t):
     """t rounded to bf16, the rounding cached on t's base tensor: a GEMM operand is usually a view (reshape,
     transpose, split-K chunks) of a tensor that several GEMMs read -- x in the forward product and again in the
     weight gradient, dy in the input- and weight-gradient products, a weight forward and backward -- so each
     base is rounded once.  The cache lives as long as the base (an attribute of it) and is dropped when the
-    base's version counter moves (in-place updates, e.g. the optimizer's)."""
+    base's version counter moves (in-place updates, e.g. the optimizer's).  An entry is reused only in the
+    epoch that made it: never across the boundary of a graph capture (eager entries inside a capture, or one
+    capture's entries in another), so every captured GEMM operand's cast is itself a node of the graph."""
     base = t._base if t._base is not None else t
     if not base.is_contiguous() or base.is_leaf and base.requires_grad:  # parameters: small, updated in place
         return t.to(_BF)
     ent = base.__dict__.get("_pdvc_bf16")
-    if ent is None or ent[0] != base._version:
-        ent = (base._version, base.to(_BF))
+    epoch = _epoch()
+    if ent is None or ent[0] != base._version or ent[2] != epoch:
+        ent = (base._version, base.to(_BF), epoch)
         base.__dict__["_pdvc_bf16"] = ent
         STATS_CAST[0] += 1
     else:

@@ -29,6 +29,7 @@ class StepGraph:
             dt["video_target_padded"] = padded_targets(dt["video_target"], dt["video_tensor"].device)
         if "cap_tensor_cpu" not in dt:
             dt["cap_tensor_cpu"] = dt["cap_tensor"].detach().cpu()
+        self.signature = self._signature(dt)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):  # warm-up: lazy init, allocator pools, cached host->device bookkeeping
@@ -40,6 +41,8 @@ class StepGraph:
         torch.cuda.current_stream().wait_stream(side)
         model.zero_grad(set_to_none=True)
         self.graph = torch.cuda.CUDAGraph()
+        from .precision import begin_capture
+        begin_capture()  # bf16 mode: every operand rounding of the step becomes a node of the graph
         if reducer is not None:
             reducer.suspended = True
         try:
@@ -55,11 +58,43 @@ class StepGraph:
         total.backward()
         return total, loss
 
+    @staticmethod
+    def _signature(dt):
+        """The host facts the captured step depends on: events per video and each video's caption step count
+        (the reference's loop stops at the video's first all-zero token column, LSTM_DSA.py:88-104)."""
+        from .CaptioningHead.LSTM_DSA import caption_steps
+        counts = [len(t["labels"]) for t in dt["video_target"]]
+        cap = dt.get("cap_tensor_cpu")
+        cap = dt["cap_tensor"].detach().cpu() if cap is None else cap
+        off = [0]
+        for c in counts:
+            off.append(off[-1] + c)
+        steps = [caption_steps(cap[off[v]:off[v + 1]]) for v in range(len(counts))]
+        return tuple(counts), tuple(steps)
+
     def load(self, dt):
-        """Copy a batch of the captured shapes (same event and caption counts) into the graph's inputs."""
+        """Copy a batch of the captured shapes (same event and caption counts) into the graph's inputs: the
+        features, masks, token rows and the padded targets the device matching reads."""
         if bool(dt.get("video_mask_all_valid", False)) != bool(self.dt.get("video_mask_all_valid", False)):
             raise ValueError("StepGraph.load: the batch's padding (video_mask_all_valid) differs from the captured "
                              "batch's; capture a graph for it")
+        if "video_target" in dt:
+            sig = self._signature(dt)
+            if sig != self.signature:
+                raise ValueError("StepGraph.load: the batch's event / caption-step counts differ from the captured "
+                                 "batch's; capture a graph for it")
+            from .matcher import padded_targets
+            new = padded_targets(dt["video_target"], self.dt["video_tensor"].device)
+            old = self.dt["video_target_padded"]
+            for k, v in new.items():
+                if isinstance(v, torch.Tensor):
+                    old[k].copy_(v, non_blocking=True)
+            for k, rep in old.items():  # the per-layer repeats the criterion cached on the dict (repeat_targets)
+                if isinstance(k, tuple) and k[0] == "repeat":
+                    for kk, v in rep.items():
+                        if isinstance(v, torch.Tensor):
+                            v.copy_(new[kk].repeat(k[1], *([1] * (v.dim() - 1))), non_blocking=True)
+            self.dt["cap_tensor_cpu"] = dt.get("cap_tensor_cpu", dt["cap_tensor"].detach().cpu())
         for k, v in dt.items():
             dst = self.dt.get(k)
             if isinstance(v, torch.Tensor) and isinstance(dst, torch.Tensor) and dst.device.type == "cuda":

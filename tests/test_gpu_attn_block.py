@@ -4,17 +4,15 @@ off: layer output and the gradients of src, pos and every parameter; and of the 
 level-position gradient handle (ops/functions/posembed.py) against the per-level position path."""
 import pytest
 import torch
+from parity import assert_close
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
 def close(a, b, tol, what):
-    a, b = a.detach().double(), b.detach().double()
-    assert a.shape == b.shape, f"{what}: {tuple(a.shape)} vs {tuple(b.shape)}"
-    err = (a - b).abs().max().item()
-    scale = max(1.0, b.abs().max().item())
-    assert err <= tol * scale, f"{what}: max|diff| {err:.3e} > {tol:.0e} * {scale:.3g}"
+    """Per-tensor relative bound: max|a - b| <= tol * max|b| + 1e-7 (tests/parity.py)."""
+    assert_close(a, b, what, tol)
 
 
 def _layer(d, heads):

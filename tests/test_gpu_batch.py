@@ -7,8 +7,9 @@ key is the mean over videos of the reference's batch-1 value, so the gradient of
 of the N batch-1 gradients.  The fixture has 3 videos with 2, 3 and 5 events, ragged caption lengths,
 different durations and one padded (masked) video; it holds each video's losses, matched indices of every
 decoder layer, heads, captioning log-probabilities, eval outputs and PostProcess results, and the mean
-gradient of every parameter as a full tensor.  Tolerance: 1e-4 * max(1, max|ref|) per tensor (fp32);
-matched indices, ranked query ids, labels, counts and greedy tokens bit-exact."""
+gradient of every parameter as a full tensor.  Tolerance (tests/parity.py): max|got - ref| <= 1e-4 * max|ref|
++ 1e-7 per tensor (fp32), plus the fixture's stored SVD packing error for packed gradients; matched indices,
+ranked query ids, labels, counts and greedy tokens bit-exact."""
 import os
 import sys
 import types
@@ -21,21 +22,15 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import test_gpu_model as TM  # noqa: E402
+from parity import assert_close, assert_scalar, bound  # noqa: E402
 
 DEV = "cuda"
 TOL = 1e-4
 NAME = "pdvc_batch3_anet"
 
 
-def close(got, ref, what, tol=TOL):
-    got = got.detach().double().cpu().numpy() if isinstance(got, torch.Tensor) else np.asarray(got, np.float64)
-    ref = np.asarray(ref, np.float64)
-    assert got.shape == ref.shape, f"{what}: shape {got.shape} vs {ref.shape}"
-    if ref.size == 0:
-        return
-    err = float(np.abs(got - ref).max())
-    scale = max(1.0, float(np.abs(ref).max()))
-    assert err <= tol * scale, f"{what}: max|diff| {err:.3e} > {tol:.0e} * {scale:.3g}"
+def close(got, ref, what, tol=TOL, extra=0.0):
+    assert_close(got, ref, what, tol, extra=extra)
 
 
 def batch_dt(d):
@@ -72,7 +67,7 @@ def _check_forward(d, out, loss, cap, nv):
     for k in wd_keys:
         ref = np.mean([float(d[f"v{v}.loss.{k}"]) for v in range(nv)])
         got = loss[k].item() if isinstance(loss[k], torch.Tensor) else float(loss[k])
-        assert abs(got - ref) <= TOL * max(1.0, abs(ref)), f"loss {k}: {got} vs mean of batch-1 {ref}"
+        assert_scalar(got, ref, f"loss {k} vs the mean of the batch-1 values")
     for v in range(nv):
         close(out["pred_logits"][v:v + 1], d[f"v{v}.pred_logits"], f"video {v} pred_logits")
         close(out["pred_boxes"][v:v + 1], d[f"v{v}.pred_boxes"], f"video {v} pred_boxes")
@@ -99,9 +94,33 @@ def _check_grads(d, named_params, what):
             assert p.grad is None, f"{what}: {n} must receive no gradient (as in the reference)"
             continue
         assert p.grad is not None, f"{what}: {n} has no gradient"
-        close(p.grad, TM.full_grad(d, n), f"{what}: grad {n}")
+        close(p.grad, TM.full_grad(d, n), f"{what}: grad {n}", extra=TM.grad_err(d, n))
         n_checked += 1
     assert n_checked > 100
+
+
+# the smallest reference gradients of the batch fixture sit in the caption head (LSTM_DSA.py:218-220, 245-258)
+MUTANTS = ("caption_head.0.core.h2att.weight", "caption_head.0.core.h2att.bias", "caption_head.0.core.ctx2att.bias",
+           "caption_head.0.core.alpha_net.weight")
+
+
+def _check_mutants(d, named_params):
+    """The bound must reject a zeroed or sign-flipped gradient of every checked tensor, the smallest included:
+    a bound that lets those through does not constrain the tensor."""
+    params = dict(named_params)
+    for n, p in params.items():
+        if p.grad is None:
+            continue
+        ref = TM.full_grad(d, n)
+        peak = float(np.abs(ref).max())
+        if peak > 1e-6:
+            assert bound(ref, extra=TM.grad_err(d, n)) < 0.5 * peak, f"{n}: the bound does not constrain the tensor"
+    for n in MUTANTS:
+        g = params[n].grad
+        ref = TM.full_grad(d, n)
+        for bad in (torch.zeros_like(g), -g, g * 1.01):
+            with pytest.raises(AssertionError):
+                close(bad, ref, f"mutant {n}", extra=TM.grad_err(d, n))
 
 
 def test_batched_step_equals_mean_of_reference_batch1_steps(fixture):
@@ -117,9 +136,10 @@ def test_batched_step_equals_mean_of_reference_batch1_steps(fixture):
     wd = criterion.weight_dict
     total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
     ref_total = np.mean([float(d[f"v{v}.total_loss"]) for v in range(nv)])
-    assert abs(total.item() - ref_total) <= TOL * max(1.0, abs(ref_total))
+    assert_scalar(total, ref_total, "total loss")
     total.backward()
     _check_grads(d, model.named_parameters(), "eager batch")
+    _check_mutants(d, model.named_parameters())
 
 
 def test_batched_step_graph_equals_reference(fixture):
@@ -134,7 +154,7 @@ def test_batched_step_graph_equals_reference(fixture):
     for _ in range(2):
         total = sg.replay().item()
         ref_total = np.mean([float(d[f"v{v}.total_loss"]) for v in range(nv)])
-        assert abs(total - ref_total) <= TOL * max(1.0, abs(ref_total))
+        assert_scalar(total, ref_total, "total loss (graph replay)")
         _check_grads(d, model.named_parameters(), "step graph")
 
 

@@ -228,3 +228,30 @@ def test_cfg2_training_step_bf16_vs_fp32():
                 continue
             err = (p.grad - g16_own[n]).norm().item()
             assert err <= 1e-2 * g16_own[n].norm().item() + 1e-7, f"replayed grad {n}: {err:.3e}"
+
+
+def test_cfg2_bf16_step_graph_follows_loaded_batch():
+    """The bf16 StepGraph fed a SECOND batch through load() equals the eager bf16 step on that batch: every
+    operand rounding of the step is a node of the graph, none is a cast cached from the warm-up batch (ADVICE
+    round 2: the warm-up's rounding of dt['video_tensor'] was a cache hit at capture, and every replay after a
+    load multiplied the first batch's features)."""
+    from pdvc.data import collate, synthetic_videos, to_device
+    from pdvc.precision import bf16_matmul
+    from pdvc.step_graph import StepGraph
+    model, criterion, dt = _cfg2_model_and_batch()
+    with bf16_matmul():
+        sg = StepGraph(model, criterion, dt)
+    dt2 = to_device(collate(synthetic_videos(2, 256, 768, 8, 9, model.opt.vocab_size + 1, seed=8)), DEV)
+    assert not torch.equal(dt2["video_tensor"], dt["video_tensor"])
+    sg.load(dt2)
+    sg.replay()
+    torch.cuda.synchronize()
+    got = {n: (None if p.grad is None else p.grad.detach().clone()) for n, p in model.named_parameters()}
+    dt2 = to_device(collate(synthetic_videos(2, 256, 768, 8, 9, model.opt.vocab_size + 1, seed=8)), DEV)
+    with bf16_matmul():
+        _, ref = _step(model, criterion, dt2)
+    for n, r in ref.items():
+        assert (r is None) == (got[n] is None), n
+        if r is not None:
+            err = (got[n] - r).norm().item()
+            assert err <= 1e-2 * r.norm().item() + 1e-7, f"replay after load(): grad {n} {err:.3e} vs |ref| {r.norm().item():.3e}"

@@ -1,6 +1,6 @@
 """Data-parallel equivalence on the real model: two ranks, each running 2 videos
 through the training step and GradAllReducer, end with the gradients one process computes for the 4-video
-union batch -- within 1e-4 * max(1, max|ref|) per tensor, with the same parameters left at grad None (the
+union batch -- within 1e-4 * max|ref| + 1e-7 per tensor, with the same parameters left at grad None (the
 reference's never-used ones).  Ranks are fresh processes (tests/dp_worker.py) on cuda:0 over gloo (a 1-GPU
 box; the bench's N-GPU runs use RCCL with the same reducer); both the eager step and the StepGraph replay
 (forward + losses + backward as one hipGraph, the path bench.py times) are covered.  The union gradient is
@@ -19,6 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.join(HERE, "golden"))
 import test_gpu_model as TM  # noqa: E402
+from parity import assert_close  # noqa: E402
 
 
 def _free_port():
@@ -74,6 +75,4 @@ def test_two_ranks_equal_union_batch(tmp_path, union, mode):
                 assert "none." + n in g.files, f"rank {r}: {n} must stay None"
                 continue
             got = g["grad." + n].astype(np.float64)
-            err = float(np.abs(got - ref).max())
-            scale = max(1.0, float(np.abs(ref).max()))
-            assert err <= 1e-4 * scale, f"rank {r} {mode}: grad {n} max|diff| {err:.3e}"
+            assert_close(got, ref, f"rank {r} {mode}: grad {n}")

@@ -4,17 +4,15 @@ deformable_transformer.py:140-145.  The in-kernel dropout mask is recovered by r
 on a tensor of ones with the same seed (the mask depends on (seed, row, column) only)."""
 import pytest
 import torch
+from parity import assert_close
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
 def close(a, b, tol, what):
-    a, b = a.detach().double(), b.detach().double()
-    assert a.shape == b.shape, f"{what}: {tuple(a.shape)} vs {tuple(b.shape)}"
-    err = (a - b).abs().max().item() if a.numel() else 0.0
-    scale = max(1.0, b.abs().max().item() if b.numel() else 1.0)
-    assert err <= tol * scale, f"{what}: max|diff| {err:.3e} > {tol:.0e} * {scale:.3g}"
+    """Per-tensor relative bound: max|a - b| <= tol * max|b| + 1e-7 (tests/parity.py)."""
+    assert_close(a, b, what, tol)
 
 
 def act_mask(seed_tensor, rows, cols, p):

@@ -6,19 +6,17 @@ HuBERT is not rebuilt (its weights are a network download): synthetic sound feat
 pinned against torch's MultiheadAttention arithmetic, not against a reference run."""
 import pytest
 import torch
+from parity import assert_close
 from torch import nn
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-TOL = 1e-4  # fp32 vs float64, relative to max(1, |reference|)
+TOL = 1e-4  # fp32 vs float64: max|diff| <= TOL * max|reference| + 1e-7 per tensor
 
 
 def close(a, b, tol, what):
-    a, b = a.detach().double(), b.detach().double()
-    assert a.shape == b.shape, f"{what}: {tuple(a.shape)} vs {tuple(b.shape)}"
-    err = (a - b).abs().max().item() if a.numel() else 0.0
-    scale = max(1.0, b.abs().max().item() if b.numel() else 1.0)
-    assert err <= tol * scale, f"{what}: max|diff| {err:.3e} > {tol:.0e} * {scale:.3g}"
+    """Per-tensor relative bound: max|a - b| <= tol * max|b| + 1e-7 (tests/parity.py)."""
+    assert_close(a, b, what, tol)
 
 
 class RefFrontEnd(nn.Module):
@@ -94,7 +92,11 @@ def test_seq_attention_core_vs_float64(Tq, Tk, H, D):
     ref = (p @ vh).transpose(1, 2).reshape(N, Tq, E)
     (ref * g.double()).sum().backward()
     close(out, ref, TOL, "out")
-    close(q1.grad, q0.grad, TOL, "grad q")
+    if Tk == 1:  # one key: the softmax is constant, the query gradient is zero in exact arithmetic -- its fp32
+        # rounding noise is bounded against the scale of the value gradient instead of its own (zero) scale
+        assert_close(q1.grad, q0.grad, "grad q (zero)", TOL, scale=kv0.grad.abs().max().item())
+    else:
+        close(q1.grad, q0.grad, TOL, "grad q")
     close(kv1.grad, kv0.grad, TOL, "grad kv")
 
 

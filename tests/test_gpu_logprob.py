@@ -5,18 +5,16 @@ itself.  All kernel forms: register-resident (V % 4 == 0, V <= 8192: ActivityNet
 (V % 4 == 0, V > 8192) and scalar (V % 4 != 0: YouCook2's 1609)."""
 import pytest
 import torch
+from parity import assert_close
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-TOL = 1e-5  # fp32 vs float64 reference, relative to max(1, |reference|)
+TOL = 1e-5  # fp32 vs float64 reference: max|diff| <= TOL * max|reference| + 1e-7 per tensor
 
 
 def close(a, b, tol, what):
-    a, b = a.detach().double(), b.detach().double()
-    assert a.shape == b.shape, f"{what}: {tuple(a.shape)} vs {tuple(b.shape)}"
-    err = (a - b).abs().max().item() if a.numel() else 0.0
-    scale = max(1.0, b.abs().max().item() if b.numel() else 1.0)
-    assert err <= tol * scale, f"{what}: max|diff| {err:.3e} > {tol:.0e} * {scale:.3g}"
+    """Per-tensor relative bound: max|a - b| <= tol * max|b| + 1e-7 (tests/parity.py)."""
+    assert_close(a, b, what, tol)
 
 
 @pytest.mark.parametrize("V", [5748, 1609, 7, 300, 8200])  # 8200: the streaming float4 form (> 8192)

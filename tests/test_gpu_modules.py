@@ -14,6 +14,8 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 G = os.path.join(HERE, "golden")
 sys.path.insert(0, G)
+sys.path.insert(0, HERE)
+from parity import assert_close  # noqa: E402
 DEV = "cuda"
 
 
@@ -27,12 +29,8 @@ def cu(a, dtype=None):
 
 
 def close(a, b, tol, what):
-    a = a.detach().double().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a, np.float64)
-    b = b.detach().double().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b, np.float64)
-    assert a.shape == b.shape, f"{what}: {a.shape} vs {b.shape}"
-    err = np.abs(a - b).max() if a.size else 0.0
-    scale = max(1.0, np.abs(b).max() if b.size else 1.0)
-    assert err <= tol * scale, f"{what}: max|diff| {err:.3e} > {tol:.0e} * {scale:.3g}"
+    """Per-tensor relative bound: max|a - b| <= tol * max|b| + 1e-7 (tests/parity.py)."""
+    assert_close(a, b, what, tol)
 
 
 def fill(module):

@@ -6,6 +6,7 @@ import os
 import numpy as np
 import pytest
 import torch
+from parity import assert_close
 
 from oracle import oracle as O
 
@@ -26,11 +27,8 @@ def cu(a, dtype=None):
 
 
 def close(a, b, tol, what=""):
-    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else a
-    b = b.detach().cpu().numpy() if isinstance(b, torch.Tensor) else b
-    err = np.abs(a - b).max() if a.size else 0.0
-    scale = max(1.0, np.abs(b).max() if b.size else 1.0)
-    assert err <= tol * scale, f"{what}: max|diff|={err:.3e} > {tol:.1e}*{scale:.2f}"
+    """Per-tensor relative bound: max|a - b| <= tol * max|b| + 1e-7 (tests/parity.py)."""
+    assert_close(a, b, what, tol)
 
 
 # ------------------------------------------------------------------------------------------------
