@@ -254,6 +254,51 @@ def cpu_baseline_c(a, budget_s, enc_layers=2, dec_layers=2):
                       f"oracle/msda_oracle.c (zeros), single thread, {el:.1f} s"}
 
 
+def dropin_msda(T, videos=256, reps=10):
+    """The drop-in operator MultiScaleDeformableAttention (what a stock MSDeformAttn module calls, vision.cpp:13-16)
+    at PDVC's lifted pyramid (spatial_shapes [[1, T_l]], y = 0.5), encoder (Lq = S) and decoder (Lq = 100) shapes,
+    M = 8, D = 64, fp32: per-launch forward / backward time (HIP events on the launching stream, median of `reps`
+    after 3 warm-ups) and the section 8(d) algorithmic bytes per launch over it."""
+    import MultiScaleDeformableAttention as MSDA
+    dev = torch.device("cuda")
+    T_l = [T // (2 ** i) for i in range(4)]
+    S, M, D, L, P = sum(T_l), 8, 64, 4, 4
+    shapes = torch.tensor([[1, t] for t in T_l], dtype=torch.int64, device=dev)
+    lsi = torch.tensor([0] + list(np.cumsum(T_l)[:-1]), dtype=torch.int64, device=dev)
+    g = torch.Generator(device=dev).manual_seed(0)
+    value = torch.randn(videos, S, M, D, device=dev, generator=g)
+    res = {"op": "MultiScaleDeformableAttention.ms_deform_attn_forward / _backward (1-D fast path)",
+           "videos": videos, "timing": f"HIP events, median of {reps} launches after 3 warm-ups"}
+    for name, Lq in (("encoder", S), ("decoder", 100)):
+        x = torch.rand(videos, Lq, M, L, P, device=dev, generator=g)
+        loc = torch.stack([x, torch.full_like(x, 0.5)], -1).contiguous()
+        attn = torch.rand(videos, Lq, M, L, P, device=dev, generator=g)
+        attn = (attn / attn.sum((-1, -2), keepdim=True)).contiguous()
+        gout = torch.randn(videos, Lq, M * D, device=dev, generator=g)
+        t = {}
+        for kind, fn in (("fwd", lambda: MSDA.ms_deform_attn_forward(value, shapes, lsi, loc, attn, 64)),
+                         ("bwd", lambda: MSDA.ms_deform_attn_backward(value, shapes, lsi, loc, attn, gout, 64))):
+            for _ in range(3):
+                fn()
+            ms = []
+            for _ in range(reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn()
+                e1.record()
+                e1.synchronize()
+                ms.append(e0.elapsed_time(e1))
+            med = float(np.median(ms))
+            nbytes = msda_alg_bytes((videos, Lq, S, M, D, L * P), kind)
+            t[kind] = {"avg_launch_us": 1e3 * med, "alg_bytes_per_launch": nbytes,
+                       "achieved_gbs": nbytes / (med * 1e-3) / 1e9, "frac_hbm": nbytes / (med * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        res[name] = t
+        del x, loc, attn, gout
+    del value
+    torch.cuda.empty_cache()
+    return res
+
+
 def log(msg):
     """Progress on stderr (a long GPU run that prints nothing for minutes is taken to be hung)."""
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
@@ -423,6 +468,10 @@ def main():
     ks = timer.summary()
     log("GEMM roofline step")
     groof = None if a.no_gemm_roofline else gemm_roofline(fwd_bwd, step, a.precision, graphed)
+    dropin = None
+    if rank == 0 and not a.frontend:
+        log("drop-in operator timing")
+        dropin = dropin_msda(a.T)
     videos = a.steps * B * world
     result = {
         "metric": WORKLOADS[a.workload]["metric"],
@@ -493,6 +542,8 @@ def main():
         result["roofline"] = groof
     elif "roofline_gather" in result:
         result["roofline"] = result["roofline_gather"]
+    if dropin is not None:
+        result["dropin_msda"] = dropin
     ksteps = 2 if graphed else a.steps
     result["kernels"] = {n: {"launches": v["launches"], "avg_us": 1e3 * v["ms"] / max(v["launches"], 1),
                              "share_of_step": v["ms"] / ksteps / (1e3 * el / a.steps)} for n, v in ks.items()}

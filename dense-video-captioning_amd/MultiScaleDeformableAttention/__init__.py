@@ -77,6 +77,15 @@ def ms_deform_attn_backward(value, spatial_shapes, level_start_index, sampling_l
     gv = torch.empty_like(value)
     gl = torch.empty_like(sampling_loc)
     ga = torch.empty_like(attn_weight)
+    if value.dtype == torch.float32:
+        # workspace of the 1-D fast path (the level-major location / weight slab its value gradient sorts); the
+        # library decides on the device whether the table is a lifted 1-D pyramid
+        nws = int(_n.lib().pdvc_ms_deform_attn_workspace_floats(N, M, L, Lq, P))
+        ws = torch.empty(max(nws, 1), dtype=torch.float32, device=value.device)
+        _n.call("pdvc_ms_deform_attn_backward_ws_f32", _n.ptr(value), _n.ptr(spatial_shapes),
+                _n.ptr(level_start_index), _n.ptr(sampling_loc), _n.ptr(attn_weight), _n.ptr(grad_output), N, S, M,
+                D, L, Lq, P, int(im2col_step), _n.ptr(gv), _n.ptr(gl), _n.ptr(ga), _n.ptr(ws), nws, _n.stream())
+        return [gv, gl, ga]
     _n.call("pdvc_ms_deform_attn_backward_" + _sfx(value), _n.ptr(value), _n.ptr(spatial_shapes),
             _n.ptr(level_start_index), _n.ptr(sampling_loc), _n.ptr(attn_weight), _n.ptr(grad_output), N, S, M,
             D, L, Lq, P, int(im2col_step), _n.ptr(gv), _n.ptr(gl), _n.ptr(ga), _n.stream())

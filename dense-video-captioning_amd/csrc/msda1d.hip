@@ -29,12 +29,7 @@ namespace pdvc {
 
 constexpr int kNS = 16;  // samples per (query, head) = L * P; PDVC: 4 levels x 4 points
 constexpr int kP = 4;     // points per level
-constexpr int kL = 4;     // levels
-
-struct Levels1d {
-    int T[kL];
-    int start[kL];
-};
+constexpr int kL = kL1d;  // levels (Levels1d, pdvc_common.h)
 
 // save_attn / save_loc (written by the forward, read by both backward kernels): level-major (N, M, L, Lq, P), so
 // the value-gradient workgroup of one (video, head, level) reads its samples as one contiguous slab, and the
@@ -290,35 +285,55 @@ __global__ __launch_bounds__(256) void msda1d_fwd_buf_kernel(
 constexpr int kPyrThreads = 1024;
 constexpr int kPyrQPS = 8;                                  // queries per 16-lane group
 constexpr int kPyrQ = (kPyrThreads / 16) * kPyrQPS;        // 512 queries per workgroup
-constexpr int kPyrRows = 512;                               // LDS rows (256 B each): 128 KiB
-constexpr size_t kPyrLds = (size_t)kPyrRows * 64 * sizeof(float);
+constexpr int kPyrRows = 512;                               // data rows per staging phase (256 B each): 128 KiB
+constexpr int kPyrRowsG = kPyrRows + 2;                     // + a guard row at each end
+constexpr size_t kPyrLds = (size_t)kPyrRowsG * 64 * sizeof(float);
 
-// stage rows [r0, r0 + n) of one head (vsrc = value + b*S*MD + m*64) into LDS rows [dst, dst + n)
-__device__ __forceinline__ void pyr_stage(float4* __restrict__ lds, const float* __restrict__ vsrc, size_t MD, int r0,
-                                          int n, int dst) {
+// Guarded LDS layout of the whole-pyramid kernels: row 0 is a zero guard, a phase's data rows follow from row 1
+// (level 0 alone; then levels 1..3 packed back to back), and one zero guard row closes them.  A sample's corner
+// rows x0 and x0 + 1 with x0 in [-1, T - 1] (every sample inside the level's open interval) are then always rows
+// of the buffer -- a guard, or a neighbouring level's row -- so the kernels read them without clamping: a corner
+// outside its level carries weight 0 and the row it reads is finite.  (The clamps were 536 of the forward's
+// ~3 800 VALU instructions per wave.)
+
+// stage rows [r0, r0 + n) of one head (vsrc = value + b*S*MD + m*64) into LDS rows [1, n + 1), zero rows 0 and n + 1
+__device__ __forceinline__ void pyr_stage_g(float4* __restrict__ lds, const float* __restrict__ vsrc, size_t MD,
+                                            int r0, int n) {
     const float4* src = reinterpret_cast<const float4*>(vsrc);
     const size_t rs = MD / 4;
     const int total = n * 16;
 #pragma unroll 4
-    for (int i = threadIdx.x; i < total; i += kPyrThreads) lds[(size_t)(dst + (i >> 4)) * 16 + (i & 15)] =
+    for (int i = threadIdx.x; i < total; i += kPyrThreads) lds[(size_t)(1 + (i >> 4)) * 16 + (i & 15)] =
         src[(size_t)(r0 + (i >> 4)) * rs + (i & 15)];
+    if (threadIdx.x < 32) {
+        const int row = threadIdx.x < 16 ? 0 : n + 1;
+        lds[row * 16 + (threadIdx.x & 15)] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 }
 
-// pyr_stage with 2 loads in flight per thread (used while the parameter loads hold registers)
-__device__ __forceinline__ void pyr_stage_lean(float4* __restrict__ lds, const float* __restrict__ vsrc, size_t MD,
-                                               int r0, int n, int dst) {
+// pyr_stage_g with 2 loads in flight per thread (used while the parameter loads hold registers)
+__device__ __forceinline__ void pyr_stage_g_lean(float4* __restrict__ lds, const float* __restrict__ vsrc, size_t MD,
+                                                 int r0, int n) {
     const float4* src = reinterpret_cast<const float4*>(vsrc);
     const size_t rs = MD / 4;
     const int total = n * 16;
 #pragma unroll 2
-    for (int i = threadIdx.x; i < total; i += kPyrThreads) lds[(size_t)(dst + (i >> 4)) * 16 + (i & 15)] =
+    for (int i = threadIdx.x; i < total; i += kPyrThreads) lds[(size_t)(1 + (i >> 4)) * 16 + (i & 15)] =
         src[(size_t)(r0 + (i >> 4)) * rs + (i & 15)];
+    if (threadIdx.x < 32) {
+        const int row = threadIdx.x < 16 ? 0 : n + 1;
+        lds[row * 16 + (threadIdx.x & 15)] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 }
 
-// LDS row base of level l: level 0 alone, then levels 1..3 packed
+// LDS row of level l's first position in its phase (guarded layout): level 0 alone, then levels 1..3 packed
 __device__ __forceinline__ int pyr_base(const Levels1d& lv, int l) {
-    return l <= 1 ? 0 : (l == 2 ? lv.T[1] : lv.T[1] + lv.T[2]);
+    return l <= 1 ? 1 : (l == 2 ? 1 + lv.T[1] : 1 + lv.T[1] + lv.T[2]);
 }
+
+// Per-sample LDS byte offset of corner row x0 (x0 in [-1, T-1] for a sample inside its level, 0 otherwise) in the
+// guarded layout; the corner x0 + 1 is the next row (+256 B, a ds_read immediate)
+__device__ __forceinline__ int pyr_corner(int base, int i0) { return (base + i0) * 256; }
 
 template <int RD>
 __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
@@ -329,14 +344,17 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
     const int blk = xcd_remap(blockIdx.x, gridDim.x);  // the query blocks and heads of a video share an XCD
     const int qb = blk % qblocks, bm = blk / qblocks;
     const int b = bm / M, m = bm - b * M;
-    const int slot = threadIdx.x >> 4, sub = threadIdx.x & 15, lane = threadIdx.x & 63, gbase = lane - sub;
+    const int slot = threadIdx.x >> 4, sub = threadIdx.x & 15;
     const size_t MD = (size_t)M * 64;
     const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
     const float* vsrc = value + (size_t)b * S * MD + (size_t)m * 64;
+    // this lane's 16 B of every LDS row
+    const char* lrow = reinterpret_cast<const char*>(lds4) + sub * 16;
 
     // parameters of this lane's sample j = sub for its 8 queries (msda1d_fwd_kernel's arithmetic)
     const int l_own = sub >> 2;
     const int T_own = lvl_sel(lv.T, l_own), st_own = lvl_sel(lv.start, l_own);
+    const int base_own = pyr_base(lv, l_own);
     const float Tf_own = (float)T_own;
     // issue every parameter load first, then stage level 0 while they are in flight (neither depends on the
     // other), then do the parameter math: the loads' latency hides under the staging
@@ -351,14 +369,14 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
         r0v[i] = ref[(row * kL + l_own) * RD];
         r1v[i] = (RD == 2) ? ref[(row * kL + l_own) * RD + 1] : 0.f;
     }
-    pyr_stage_lean(lds4, vsrc, MD, lv.start[0], lv.T[0], 0);
-    int i0v[kPyrQPS];
+    pyr_stage_g_lean(lds4, vsrc, MD, lv.start[0], lv.T[0]);
+    // per query: the owner lane's corner-row byte offset and its two corner weights, the attention weight folded in
+    int adv[kPyrQPS];
     float w1v[kPyrQPS], w2v[kPyrQPS];
 #pragma unroll
     for (int i = 0; i < kPyrQPS; ++i) {
         const int q = qb * kPyrQ + slot + 64 * i;
         const bool act = q < Lq;
-        const size_t row = (size_t)b * Lq + (act ? q : 0);
         const float lg = lgv[i];
         const float mx = group_max<16>(lg);
         const float sum = group_allreduce<16>(expf(lg - mx));
@@ -375,59 +393,63 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
         const float x = loc * Tf_own - 0.5f;
         const bool inside = x > -1.f && x < Tf_own;
         const float xf = floorf(inside ? x : 0.f);
-        const int i0 = (int)xf;
+        const int i0 = (int)xf;  // in [-1, T - 1] inside, 0 outside
         const float lw = inside ? x - xf : 0.f;
         bool ok1 = inside && i0 >= 0, ok2 = inside && i0 + 1 <= T_own - 1;
         if (mbase) {
             ok1 = ok1 && !mbase[st_own + min(max(i0, 0), T_own - 1)];
             ok2 = ok2 && !mbase[st_own + min(max(i0 + 1, 0), T_own - 1)];
         }
-        i0v[i] = i0;
+        adv[i] = pyr_corner(base_own, i0);
         w1v[i] = ok1 ? (1.f - lw) * aw : 0.f;
         w2v[i] = ok2 ? lw * aw : 0.f;
     }
 
-    VecF<4> acc[kPyrQPS];
+    float4 acc[kPyrQPS];
 #pragma unroll
-    for (int i = 0; i < kPyrQPS; ++i) acc[i].zero();
-    // one level of every query of the lane group: the sample parameters come from their owner lanes by DPP
-    // row_newbcast (a VALU modifier, so the LDS pipe serves only the corner-row reads); the level is a compile-time
-    // constant, which the DPP pattern needs
+    for (int i = 0; i < kPyrQPS; ++i) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // one level of every query of the lane group: the sample's corner offset and weights come from their owner lane
+    // by DPP row_newbcast (a VALU modifier, so the LDS pipe serves only the corner-row reads); the level is a
+    // compile-time constant, which the DPP pattern needs.  Per sample and lane: 3 broadcasts, 1 address add, 2 LDS
+    // reads (the second at +256 B), 4 packed FMAs (acc = w1 * v[x0] + acc, then w2 * v[x0 + 1] + acc).
     float4 tok = make_float4(0.f, 0.f, 0.f, 0.f);
     auto level = [&](auto Lc) {
         constexpr int L = decltype(Lc)::value;
-        const int T = lv.T[L], base = pyr_base(lv, L);
 #pragma unroll
         for (int i = 0; i < kPyrQPS; ++i) {
-            VecF<4> v1[kP], v2[kP];
+            float4 v1[kP], v2[kP];
             float c1[kP], c2[kP];
             // this query's broadcasts depend (opaquely) on the previous query's sums: without it the compiler hoists
             // every broadcast and LDS read of the level and spills (1 563 spilled VGPRs)
-            int iv = i0v[i];
+            int ad = adv[i];
             float wa = w1v[i], wb = w2v[i];
-            __asm__ volatile("" : "+v"(iv), "+v"(wa), "+v"(wb) : "v"(tok.x), "v"(tok.y), "v"(tok.z), "v"(tok.w));
+            __asm__ volatile("" : "+v"(ad), "+v"(wa), "+v"(wb) : "v"(tok.x), "v"(tok.y), "v"(tok.z), "v"(tok.w));
 #pragma unroll
             for (int p = 0; p < kP; ++p) {
-                const int i0 = grp_bcast<16>(iv, L * kP + p);
+                const char* r = lrow + grp_bcast<16>(ad, L * kP + p);
                 c1[p] = grp_bcast<16>(wa, L * kP + p);
                 c2[p] = grp_bcast<16>(wb, L * kP + p);
-                const int a1 = min(max(i0, 0), T - 1), a2 = min(max(i0 + 1, 0), T - 1);
-                const float4 t1 = lds4[(base + a1) * 16 + sub], t2 = lds4[(base + a2) * 16 + sub];
-                v1[p].v[0] = t1.x; v1[p].v[1] = t1.y; v1[p].v[2] = t1.z; v1[p].v[3] = t1.w;
-                v2[p].v[0] = t2.x; v2[p].v[1] = t2.y; v2[p].v[2] = t2.z; v2[p].v[3] = t2.w;
+                v1[p] = *reinterpret_cast<const float4*>(r);
+                v2[p] = *reinterpret_cast<const float4*>(r + 256);
             }
 #pragma unroll
             for (int p = 0; p < kP; ++p) {
-#pragma unroll
-                for (int c = 0; c < 4; ++c) acc[i].v[c] += c1[p] * v1[p].v[c] + c2[p] * v2[p].v[c];
+                acc[i].x = fmaf(c1[p], v1[p].x, acc[i].x);
+                acc[i].y = fmaf(c1[p], v1[p].y, acc[i].y);
+                acc[i].z = fmaf(c1[p], v1[p].z, acc[i].z);
+                acc[i].w = fmaf(c1[p], v1[p].w, acc[i].w);
+                acc[i].x = fmaf(c2[p], v2[p].x, acc[i].x);
+                acc[i].y = fmaf(c2[p], v2[p].y, acc[i].y);
+                acc[i].z = fmaf(c2[p], v2[p].z, acc[i].z);
+                acc[i].w = fmaf(c2[p], v2[p].w, acc[i].w);
             }
-            tok = make_float4(acc[i].v[0], acc[i].v[1], acc[i].v[2], acc[i].v[3]);
+            tok = acc[i];
         }
     };
     __syncthreads();  // level 0 was staged before the parameter math
     level(std::integral_constant<int, 0>{});
     __syncthreads();  // levels 1..3 in one round trip
-    pyr_stage(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3], 0);
+    pyr_stage_g(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3]);
     __syncthreads();
     level(std::integral_constant<int, 1>{});
     level(std::integral_constant<int, 2>{});
@@ -435,7 +457,8 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
 #pragma unroll
     for (int i = 0; i < kPyrQPS; ++i) {
         const int q = qb * kPyrQ + slot + 64 * i;
-        if (q < Lq) acc[i].store(out + ((size_t)b * Lq + q) * MD + (size_t)m * 64 + sub * 4);
+        if (q < Lq)
+            *reinterpret_cast<float4*>(out + ((size_t)b * Lq + q) * MD + (size_t)m * 64 + sub * 4) = acc[i];
     }
 }
 
@@ -775,7 +798,7 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
     int qblocks, const float* __restrict__ gout, const float* __restrict__ save_attn,
     const float* __restrict__ save_loc, float* __restrict__ grad_proj, float* __restrict__ grad_ref) {
     extern __shared__ __attribute__((aligned(16))) float4 lds4[];
-    float* carry = reinterpret_cast<float*>(lds4 + kPyrRows * 16);  // [kBqQ][4]: dL/da of level 0's samples
+    float* carry = reinterpret_cast<float*>(lds4 + kPyrRowsG * 16);  // [kBqQ][4]: dL/da of level 0's samples
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int qb = blk % qblocks, bm = blk / qblocks;
     const int b = bm / M, m = bm - b * M;
@@ -791,6 +814,8 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
         st_own = l_own >= l ? lv.start[l] : st_own;
     }
     const float Tf = (float)T_own;
+    const int base_own = pyr_base(lv, l_own);
+    const char* lrow = reinterpret_cast<const char*>(lds4) + sub * 16;  // this lane's 16 B of every LDS row
 
     // one query of this lane group through the levels [L0, L1): the lane's own sample parameters, the dot products
     // of every sample of those levels from LDS, reduced onto their owner lanes; then the owner math of the lanes
@@ -809,16 +834,16 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
         const float xf = floorf(inside ? x : 0.f);
         const int i0 = (int)xf;
         const float lw = inside ? x - xf : 0.f;
+        const int ad = pyr_corner(base_own, i0);  // guarded layout: no clamps (msda1d_fwd_pyr_kernel)
         float d1 = 0.f, d2 = 0.f;
 #pragma unroll
         for (int L = L0; L < L1; ++L) {
-            const int T = lv.T[L], base = pyr_base(lv, L);
             float part[8];
 #pragma unroll
             for (int p = 0; p < kP; ++p) {
-                const int ib = grp_bcast<16>(i0, L * kP + p);
-                const int a1 = min(max(ib, 0), T - 1), a2 = min(max(ib + 1, 0), T - 1);
-                const float4 u1 = lds4[(base + a1) * 16 + sub], u2 = lds4[(base + a2) * 16 + sub];
+                const char* r = lrow + grp_bcast<16>(ad, L * kP + p);
+                const float4 u1 = *reinterpret_cast<const float4*>(r);
+                const float4 u2 = *reinterpret_cast<const float4*>(r + 256);
                 part[p] = g.x * u1.x + g.y * u1.y + g.z * u1.z + g.w * u1.w;
                 part[4 + p] = g.x * u2.x + g.y * u2.y + g.z * u2.z + g.w * u2.w;
             }
@@ -892,12 +917,12 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
         }
     };
 
-    pyr_stage(lds4, vsrc, MD, lv.start[0], lv.T[0], 0);
+    pyr_stage_g(lds4, vsrc, MD, lv.start[0], lv.T[0]);
     __syncthreads();
 #pragma unroll 1
     for (int i = 0; i < kBqQPS; ++i) run_query(i, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
     __syncthreads();
-    pyr_stage(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3], 0);
+    pyr_stage_g(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3]);
     __syncthreads();
 #pragma unroll 1
     for (int i = 0; i < kBqQPS; ++i) run_query(i, std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{});
@@ -932,8 +957,12 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
                                                                      const float* __restrict__ save_attn,
                                                                      const float* __restrict__ save_loc,
                                                                      float* __restrict__ grad_value,
-                                                                     float* __restrict__ level_sums) {
+                                                                     float* __restrict__ level_sums,
+                                                                     const int64_t* __restrict__ dshapes = nullptr,
+                                                                     const int64_t* __restrict__ dlsi = nullptr) {
     extern __shared__ __attribute__((aligned(16))) int lds_i[];
+    // the drop-in fast path passes its device level table: the kernel runs only for a 1-D pyramid (dropin_levels)
+    if (dshapes != nullptr && !dropin_levels(dshapes, dlsi, S, lv)) return;
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -1228,6 +1257,183 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
         }
     }
     while (k <= r1) close_bucket();
+}
+
+// -------------------------------------------------------------------------------------------------
+// The drop-in operator's 1-D fast path.  A reference user who keeps the stock MSDeformAttn module calls
+// MultiScaleDeformableAttention.ms_deform_attn_forward/backward (pdvc/ops/src/vision.cpp:13-16) with PDVC's lifted
+// pyramid: spatial_shapes [[1, T_l]] for every level (pdvc/ops/modules/ms_deform_attn.py:114-117), sampling
+// locations (N, Lq, M, L, P, 2) and softmaxed weights (N, Lq, M, L, P).  The level table lives in device memory, so
+// these kernels read it themselves (a few scalar loads) and run only when it is such a pyramid -- 4 levels, every
+// H == 1, W > 0, the start index the prefix sum of W, sum W == S; the general 2-D kernels (msda_op.hip) take
+// every other table.  No host read of spatial_shapes: the dispatch is a device-side branch on both paths.
+// At H = 1 the y coordinate still matters (.cuh:34-85 with height 1): h = y - 0.5 must lie in (-1, 1), and exactly
+// one row corner is in range -- row 0 as h_low (weight 1 - h, d/dh = -1) for h >= 0, as h_high (weight 1 + h,
+// d/dh = +1) below -- so a sample is the 1-D sample scaled by fy = 1 - |h|.  PDVC passes y = 0.5: fy = 1.
+// -------------------------------------------------------------------------------------------------
+struct DropinSample {
+    int roff;         // byte offset of corner row x0 inside the video's value rows
+    float lw, fy, sy; // fraction of x, the row-corner factor, d(fy)/dh
+    float a;          // attention weight
+    bool ok1, ok2;    // corners x0, x0 + 1 in range (the sample inside its level in x and y)
+};
+
+__device__ __forceinline__ DropinSample dropin_sample(float lx, float ly, float a, int T, int st, int MD) {
+    DropinSample s;
+    const float Tf = (float)T;
+    const float x = lx * Tf - 0.5f;  // w_im (.cuh:283-284)
+    const float h = ly - 0.5f;       // h_im at height 1
+    const bool inside = x > -1.f && x < Tf && h > -1.f && h < 1.f;
+    const float xf = floorf(inside ? x : 0.f);
+    const int i0 = (int)xf;
+    s.lw = inside ? x - xf : 0.f;
+    s.fy = inside ? (h >= 0.f ? 1.f - h : 1.f + h) : 0.f;
+    s.sy = inside ? (h >= 0.f ? -1.f : 1.f) : 0.f;
+    s.ok1 = inside && i0 >= 0;
+    s.ok2 = inside && i0 + 1 <= T - 1;
+    s.roff = (st + i0) * (MD * 4);  // a corner below the video's rows reads 0 through the buffer range check
+    s.a = a;
+    return s;
+}
+
+// forward: msda1d_fwd_buf_kernel's mapping (one wave per 4 queries of one (video, head), 16 lanes x float4 per query,
+// lane j owns sample j for the parameter phase), reading the drop-in layout's locations and weights
+__global__ __launch_bounds__(256) void msda_dropin_fwd_kernel(const float* __restrict__ value,
+                                                              const int64_t* __restrict__ shapes,
+                                                              const int64_t* __restrict__ lsi,
+                                                              const float* __restrict__ loc,
+                                                              const float* __restrict__ attn, int Lq, int S, int M,
+                                                              int total_waves, float* __restrict__ out) {
+    constexpr int D = 64;
+    Levels1d lv;
+    if (!dropin_levels(shapes, lsi, S, lv)) return;  // a 2-D table: msda2d_fwd_kernel's
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
+    if (wave >= total_waves) return;
+    const WaveQuery w = wave_query<16>(wave, lane, Lq, M);
+    const int MD = M * D;
+    const int j = w.sub, l_own = j >> 2;
+    const size_t si = ((size_t)w.row * M + w.m) * kNS + j;  // (N, Lq, M, L, P) index of this lane's sample
+    const float2 lc = *reinterpret_cast<const float2*>(loc + 2 * si);
+    const DropinSample sm = dropin_sample(lc.x, lc.y, attn[si], lvl_sel(lv.T, l_own), lvl_sel(lv.start, l_own), MD);
+    const float w1 = sm.ok1 ? ((1.f - sm.lw) * sm.fy) * sm.a : 0.f, w2 = sm.ok2 ? (sm.lw * sm.fy) * sm.a : 0.f;
+    const int coff = (w.m * D + w.sub * 4) * 4;
+    const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(value + (size_t)__builtin_amdgcn_readfirstlane(w.b) * S * MD), (short)0, S * MD * 4, 0x00020000);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int l = 0; l < kL; ++l) {
+        int rl = sm.roff;
+        float wl1 = w1, wl2 = w2;
+        __asm__ volatile("" : "+v"(rl), "+v"(wl1), "+v"(wl2) : "v"(acc.x), "v"(acc.y), "v"(acc.z), "v"(acc.w));
+        float4 v1[kP], v2[kP];
+        float c1[kP], c2[kP];
+#pragma unroll
+        for (int p = 0; p < kP; ++p) {
+            const int o = grp_bcast<16>(rl, l * kP + p) + coff;
+            c1[p] = grp_bcast<16>(wl1, l * kP + p);
+            c2[p] = grp_bcast<16>(wl2, l * kP + p);
+            const auto u1 = __builtin_amdgcn_raw_buffer_load_b128(vr, o, 0, 0);
+            const auto u2 = __builtin_amdgcn_raw_buffer_load_b128(vr, o + MD * 4, 0, 0);
+            v1[p] = make_float4(__uint_as_float(u1[0]), __uint_as_float(u1[1]), __uint_as_float(u1[2]),
+                                __uint_as_float(u1[3]));
+            v2[p] = make_float4(__uint_as_float(u2[0]), __uint_as_float(u2[1]), __uint_as_float(u2[2]),
+                                __uint_as_float(u2[3]));
+        }
+#pragma unroll
+        for (int p = 0; p < kP; ++p) {
+            acc.x = fmaf(c1[p], v1[p].x, acc.x);
+            acc.y = fmaf(c1[p], v1[p].y, acc.y);
+            acc.z = fmaf(c1[p], v1[p].z, acc.z);
+            acc.w = fmaf(c1[p], v1[p].w, acc.w);
+            acc.x = fmaf(c2[p], v2[p].x, acc.x);
+            acc.y = fmaf(c2[p], v2[p].y, acc.y);
+            acc.z = fmaf(c2[p], v2[p].z, acc.z);
+            acc.w = fmaf(c2[p], v2[p].w, acc.w);
+        }
+    }
+    if (w.active)
+        *reinterpret_cast<float4*>(out + (size_t)w.row * MD + (size_t)w.m * D + w.sub * 4) = acc;
+}
+
+// backward, query side: msda1d_bwd_query_dot_kernel's dot-product form and reduction; the owner lane writes
+// grad_sampling_loc (x, y) and grad_attn_weight in the drop-in layout (.cuh:88-160 at height 1: dL/da = fy * dot,
+// dL/dx = W * a * fy * (d2 - d1), dL/dy = a * sy * dot with dot = hw * d1 + lw * d2 over the corners in range), and
+// the level-major (location x, a * fy) slab the value-gradient kernel sorts
+__global__ __launch_bounds__(256) void msda_dropin_bwd_query_kernel(
+    const float* __restrict__ value, const int64_t* __restrict__ shapes, const int64_t* __restrict__ lsi,
+    const float* __restrict__ loc, const float* __restrict__ attn, int Lq, int S, int M, int total_waves,
+    const float* __restrict__ gout, float* __restrict__ grad_loc, float* __restrict__ grad_attn,
+    float* __restrict__ save_attn, float* __restrict__ save_loc) {
+    constexpr int D = 64;
+    Levels1d lv;
+    if (!dropin_levels(shapes, lsi, S, lv)) return;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
+    if (wave >= total_waves) return;
+    const WaveQuery w = wave_query<16>(wave, lane, Lq, M);
+    const int MD = M * D;
+    const int c0 = w.sub * 4;
+    const int j = w.sub, l_own = j >> 2;
+    const int T_own = lvl_sel(lv.T, l_own);
+    const size_t si = ((size_t)w.row * M + w.m) * kNS + j;
+    const float2 lc = *reinterpret_cast<const float2*>(loc + 2 * si);
+    const DropinSample sm = dropin_sample(lc.x, lc.y, attn[si], T_own, lvl_sel(lv.start, l_own), MD);
+    if (w.active) {
+        const size_t vi = save_index(w.b, w.m, l_own, w.q, j & 3, Lq, M);
+        save_loc[vi] = lc.x;
+        save_attn[vi] = sm.a * sm.fy;
+    }
+    const int coff = (w.m * D + c0) * 4;
+    const float4 g = *reinterpret_cast<const float4*>(gout + (size_t)w.row * MD + (size_t)w.m * D + c0);
+    const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(value + (size_t)__builtin_amdgcn_readfirstlane(w.b) * S * MD), (short)0, S * MD * 4, 0x00020000);
+    float d1 = 0.f, d2 = 0.f;
+#pragma unroll
+    for (int l = 0; l < kL; ++l) {
+        float part[8];
+#pragma unroll
+        for (int p = 0; p < kP; ++p) {
+            const int off = grp_bcast<16>(sm.roff, l * kP + p) + coff;
+            const auto u1 = __builtin_amdgcn_raw_buffer_load_b128(vr, off, 0, 0);
+            const auto u2 = __builtin_amdgcn_raw_buffer_load_b128(vr, off + MD * 4, 0, 0);
+            part[p] = g.x * __uint_as_float(u1[0]) + g.y * __uint_as_float(u1[1]) + g.z * __uint_as_float(u1[2]) +
+                      g.w * __uint_as_float(u1[3]);
+            part[4 + p] = g.x * __uint_as_float(u2[0]) + g.y * __uint_as_float(u2[1]) +
+                          g.z * __uint_as_float(u2[2]) + g.w * __uint_as_float(u2[3]);
+        }
+        const bool u8 = (lane & 8) != 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float send = u8 ? part[i] : part[i + 4];
+            const float mine = u8 ? part[i + 4] : part[i];
+            part[i] = mine + grp_swap(send, 8);
+        }
+        const bool u2b = (lane & 2) != 0;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const float send = u2b ? part[i] : part[i + 2];
+            const float mine = u2b ? part[i + 2] : part[i];
+            part[i] = mine + grp_swap(send, 2);
+        }
+        const bool u1b = (lane & 1) != 0;
+        const float send = u1b ? part[0] : part[1];
+        const float mine = u1b ? part[1] : part[0];
+        part[0] = mine + grp_swap(send, 1);
+        part[0] += grp_swap(part[0], 4);
+        const float other = grp_swap(part[0], 8);
+        if (l_own == l) {
+            d1 = (l < 2) ? part[0] : other;
+            d2 = (l < 2) ? other : part[0];
+        }
+    }
+    const float x1 = sm.ok1 ? d1 : 0.f, x2 = sm.ok2 ? d2 : 0.f;
+    const float dot = (1.f - sm.lw) * x1 + sm.lw * x2;
+    if (w.active) {
+        grad_attn[si] = sm.fy * dot;
+        *reinterpret_cast<float2*>(grad_loc + 2 * si) =
+            make_float2((float)T_own * ((sm.a * sm.fy) * (x2 - x1)), sm.a * (sm.sy * dot));
+    }
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -1593,3 +1799,80 @@ extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value
                                        grad_output, output, save_attn, save_loc, grad_value, grad_proj, grad_ref,
                                        nullptr, stream);
 }
+
+// ---- the drop-in operator's 1-D fast path (msda_op.hip dispatches here; the level table is checked on the device) ----
+namespace pdvc {
+
+// host-side conditions: D = 64, 4 levels x 4 points, offsets within the kernels' 32-bit arithmetic; PDVC_DROPIN_1D=0
+// turns the path off (A/B)
+bool dropin1d_applies(int S, int M, int D, int L, int Lq, int P) {
+    static const bool on = [] {
+        const char* e = getenv("PDVC_DROPIN_1D");
+        return !(e && e[0] == '0');
+    }();
+    return on && D == 64 && L == kL && P == kP && Lq > 0 && Lq < 65536 && S < 65535 &&
+           (long)S * M * D * 4 < (1L << 31) && (long)Lq * M * D * 4 < (1L << 31);
+}
+
+int dropin1d_forward(const float* value, const int64_t* shapes, const int64_t* lsi, const float* loc,
+                     const float* attn, int N, int S, int M, int Lq, float* out, hipStream_t s) {
+    const long tw = (long)N * M * ((Lq + 3) / 4);
+    if (tw == 0) return PDVC_OK;
+    PDVC_CHECK_ARG(tw < (1L << 31) / 4, "too many rows");
+    hipLaunchKernelGGL(msda_dropin_fwd_kernel, dim3((unsigned)((tw + 3) / 4)), dim3(256), 0, s, value, shapes, lsi, loc,
+                       attn, Lq, S, M, (int)tw, out);
+    PDVC_CHECK_LAUNCH("msda_dropin_fwd_kernel");
+    return PDVC_OK;
+}
+
+// workspace: 2 * N * Lq * M * 16 floats (the level-major location / weight slab of the value gradient)
+int dropin1d_backward(const float* value, const int64_t* shapes, const int64_t* lsi, const float* loc,
+                      const float* attn, const float* gout, int N, int S, int M, int Lq, float* grad_value,
+                      float* grad_loc, float* grad_attn, float* workspace, hipStream_t s) {
+    const long tw = (long)N * M * ((Lq + 3) / 4);
+    if (tw == 0) return PDVC_OK;
+    PDVC_CHECK_ARG(tw < (1L << 31) / 4, "too many rows");
+    float* save_attn = workspace;
+    float* save_loc = workspace + (size_t)N * Lq * M * kNS;
+    hipLaunchKernelGGL(msda_dropin_bwd_query_kernel, dim3((unsigned)((tw + 3) / 4)), dim3(256), 0, s, value, shapes,
+                       lsi, loc, attn, Lq, S, M, (int)tw, gout, grad_loc, grad_attn, save_attn, save_loc);
+    PDVC_CHECK_LAUNCH("msda_dropin_bwd_query_kernel");
+    // value gradient: msda1d_bwd_value_kernel on the slab, its LDS sized for the longest possible level (S)
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e3 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1, true>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        hipError_t e4 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1, true, 4>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        if (e3 != hipSuccess || e4 != hipSuccess) {
+            (void)hipGetLastError();
+            return pdvc_set_error(PDVC_ERR_LAUNCH, "msda1d_bwd_value_kernel: cannot raise the LDS limit");
+        }
+        attr = true;
+    }
+    const long per_sample = 12;
+    const long budget = 96 * 1024 - 8L * (S + 2) - 16;
+    if (budget < per_sample * kP) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "spatial size %d too long", S);
+    int qchunk = (int)(budget / (per_sample * kP));
+    if (qchunk > kVQPT * kVW * 64) qchunk = kVQPT * kVW * 64;
+    if (qchunk > Lq) qchunk = Lq;
+    const long nblk = (long)N * M * kL;
+    Levels1d lv{};  // read on the device
+    for (int q0 = 0; q0 < Lq; q0 += qchunk) {
+        const int nq = (Lq - q0) < qchunk ? (Lq - q0) : qchunk;
+        const size_t lds = sizeof(int) * (2 * (size_t)(S + 2) + 3 * (size_t)nq * kP + 2);
+        const int acc = q0 > 0;
+        if (value_ug(Lq, S) == 4)
+            hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, 4>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
+                               nullptr, lv, Lq, q0, nq, S, M, 64, acc, gout, save_attn, save_loc, grad_value, nullptr,
+                               shapes, lsi);
+        else
+            hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
+                               nullptr, lv, Lq, q0, nq, S, M, 64, acc, gout, save_attn, save_loc, grad_value, nullptr,
+                               shapes, lsi);
+        PDVC_CHECK_LAUNCH("msda1d_bwd_value_kernel (drop-in)");
+    }
+    return PDVC_OK;
+}
+
+}  // namespace pdvc

@@ -11,9 +11,19 @@
 // reference's N*Lq*M*D/1024 blocks (480 blocks of 1024 threads at PDVC's encoder shape).  The whole batch
 // is one launch (no im2col_step chunk loop: 288 GB of HBM makes chunking pointless).  This general path
 // keeps atomics for grad_value; PDVC's modules use the fused 1-D kernels in msda1d.hip instead.
+#include <algorithm>
+
 #include "pdvc_common.h"
 
 namespace pdvc {
+
+// the drop-in operator's 1-D fast path (msda1d.hip)
+bool dropin1d_applies(int S, int M, int D, int L, int Lq, int P);
+int dropin1d_forward(const float* value, const int64_t* shapes, const int64_t* lsi, const float* loc,
+                     const float* attn, int N, int S, int M, int Lq, float* out, hipStream_t s);
+int dropin1d_backward(const float* value, const int64_t* shapes, const int64_t* lsi, const float* loc,
+                      const float* attn, const float* gout, int N, int S, int M, int Lq, float* grad_value,
+                      float* grad_loc, float* grad_attn, float* workspace, hipStream_t s);
 
 constexpr int kMaxLevels2d = 64;
 
@@ -105,12 +115,17 @@ template <typename T, int PAD, int MODE>
 __global__ __launch_bounds__(256) void msda2d_fwd_kernel(const T* __restrict__ value, const int64_t* __restrict__ shapes,
                                                           const int64_t* __restrict__ lsi, const T* __restrict__ loc,
                                                           const T* __restrict__ attn, int N, int S, int M, int D, int L,
-                                                          int Lq, int P, T* __restrict__ out) {
+                                                          int Lq, int P, int gate_1d, T* __restrict__ out) {
+    if (gate_1d) {  // a lifted 1-D pyramid is the drop-in fast path's (msda_dropin_fwd_kernel)
+        Levels1d lv;
+        if (dropin_levels(shapes, lsi, S, lv)) return;
+    }
     __shared__ int sH[kMaxLevels2d], sW[kMaxLevels2d], sStart[kMaxLevels2d];
     load_levels(shapes, lsi, L, S, sH, sW, sStart);
     const int lane = threadIdx.x & 63;
-    const long wave = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (wave >= (long)N * Lq * M) return;
+    const long nwaves = (long)gridDim.x * (blockDim.x >> 6);
+    for (long wave = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); wave < (long)N * Lq * M;
+         wave += nwaves) {
     const int m = (int)(wave % M);
     const int q = (int)((wave / M) % Lq);
     const int n = (int)(wave / ((long)M * Lq));
@@ -130,6 +145,7 @@ __global__ __launch_bounds__(256) void msda2d_fwd_kernel(const T* __restrict__ v
         }
         if (MODE == 0) out[(size_t)wave * D + c] = col;
     }
+    }
 }
 
 // MODE 0: backward of the weighted op;  MODE 1: backward of the raw-sample mode (no attn)
@@ -137,14 +153,19 @@ template <typename T, int PAD, int MODE>
 __global__ __launch_bounds__(256) void msda2d_bwd_kernel(const T* __restrict__ value, const int64_t* __restrict__ shapes,
                                                           const int64_t* __restrict__ lsi, const T* __restrict__ loc,
                                                           const T* __restrict__ attn, const T* __restrict__ gout,
-                                                          int N, int S, int M, int D, int L, int Lq, int P,
+                                                          int N, int S, int M, int D, int L, int Lq, int P, int gate_1d,
                                                           T* __restrict__ grad_value, T* __restrict__ grad_loc,
                                                           T* __restrict__ grad_attn) {
+    if (gate_1d) {  // a lifted 1-D pyramid is the drop-in fast path's (msda_dropin_bwd_query_kernel + value kernel)
+        Levels1d lv;
+        if (dropin_levels(shapes, lsi, S, lv)) return;
+    }
     __shared__ int sH[kMaxLevels2d], sW[kMaxLevels2d], sStart[kMaxLevels2d];
     load_levels(shapes, lsi, L, S, sH, sW, sStart);
     const int lane = threadIdx.x & 63;
-    const long wave = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (wave >= (long)N * Lq * M) return;
+    const long nwaves = (long)gridDim.x * (blockDim.x >> 6);
+    for (long wave = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); wave < (long)N * Lq * M;
+         wave += nwaves) {
     const int m = (int)(wave % M);
     const int q = (int)((wave / M) % Lq);
     const int n = (int)(wave / ((long)M * Lq));
@@ -181,16 +202,36 @@ __global__ __launch_bounds__(256) void msda2d_bwd_kernel(const T* __restrict__ v
             }
         }
     }
+    }
 }
+
+// grad_value's zero fill for the atomics of msda2d_bwd_kernel; skipped (gate_1d) when the table is a lifted 1-D
+// pyramid: the fast path's value-gradient kernel writes every row itself
+__global__ __launch_bounds__(256) void msda2d_zero_kernel(float* __restrict__ p, size_t n4,
+                                                           const int64_t* __restrict__ shapes,
+                                                           const int64_t* __restrict__ lsi, int S, int gate_1d) {
+    if (gate_1d) {
+        Levels1d lv;
+        if (dropin_levels(shapes, lsi, S, lv)) return;
+    }
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    float4* q = reinterpret_cast<float4*>(p);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
+        q[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// grid-stride launches, at most kMaxBlocks2d workgroups: enough to fill the chip, and cheap to retire when the
+// 1-D gate sends the work to the fast path
+constexpr long kMaxBlocks2d = 8192;
 
 template <typename T, int PAD, int MODE>
 static int launch_fwd(const T* value, const int64_t* shapes, const int64_t* lsi, const T* loc, const T* attn, int N,
-                      int S, int M, int D, int L, int Lq, int P, T* out, hipStream_t stream) {
+                      int S, int M, int D, int L, int Lq, int P, T* out, hipStream_t stream, int gate_1d = 0) {
     const long waves = (long)N * Lq * M;
     if (waves == 0) return PDVC_OK;
-    const int blocks = (int)((waves + 3) / 4);
+    const int blocks = (int)std::min((waves + 3) / 4, kMaxBlocks2d);
     hipLaunchKernelGGL((msda2d_fwd_kernel<T, PAD, MODE>), dim3(blocks), dim3(256), 0, stream, value, shapes, lsi, loc,
-                       attn, N, S, M, D, L, Lq, P, out);
+                       attn, N, S, M, D, L, Lq, P, gate_1d, out);
     PDVC_CHECK_LAUNCH("msda2d_fwd_kernel");
     return PDVC_OK;
 }
@@ -198,16 +239,24 @@ static int launch_fwd(const T* value, const int64_t* shapes, const int64_t* lsi,
 template <typename T, int PAD, int MODE>
 static int launch_bwd(const T* value, const int64_t* shapes, const int64_t* lsi, const T* loc, const T* attn,
                       const T* gout, int N, int S, int M, int D, int L, int Lq, int P, T* gv, T* gl, T* ga,
-                      hipStream_t stream) {
-    if ((long)N * S * M * D > 0) {
-        hipError_t e = zero_async(reinterpret_cast<float*>(gv), sizeof(T) / sizeof(float) * (size_t)N * S * M * D, stream);
-        if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_value: %s", hipGetErrorString(e));
+                      hipStream_t stream, int gate_1d = 0) {
+    const size_t nf = sizeof(T) / sizeof(float) * (size_t)N * S * M * D;
+    if (nf > 0) {
+        if (gate_1d) {  // D = 64 on this path: float4 stores, aligned (a torch allocation)
+            const unsigned zb = (unsigned)std::min<size_t>(nf / 4 / 256 + 1, 8192);
+            hipLaunchKernelGGL(msda2d_zero_kernel, dim3(zb), dim3(256), 0, stream, reinterpret_cast<float*>(gv), nf / 4,
+                               shapes, lsi, S, gate_1d);
+            PDVC_CHECK_LAUNCH("msda2d_zero_kernel");
+        } else {
+            hipError_t e = zero_async(reinterpret_cast<float*>(gv), nf, stream);
+            if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_value: %s", hipGetErrorString(e));
+        }
     }
     const long waves = (long)N * Lq * M;
     if (waves == 0) return PDVC_OK;
-    const int blocks = (int)((waves + 3) / 4);
+    const int blocks = (int)std::min((waves + 3) / 4, kMaxBlocks2d);
     hipLaunchKernelGGL((msda2d_bwd_kernel<T, PAD, MODE>), dim3(blocks), dim3(256), 0, stream, value, shapes, lsi, loc,
-                       attn, gout, N, S, M, D, L, Lq, P, gv, gl, ga);
+                       attn, gout, N, S, M, D, L, Lq, P, gate_1d, gv, gl, ga);
     PDVC_CHECK_LAUNCH("msda2d_bwd_kernel");
     return PDVC_OK;
 }
@@ -263,8 +312,71 @@ using namespace pdvc;
                                                 grad_attn_weight, (hipStream_t)stream);                             \
     }
 
-PDVC_DEFINE_OP(float, f32)
 PDVC_DEFINE_OP(double, f64)
+
+// f32: the same entry points, plus the 1-D fast path for a lifted pyramid (device-side dispatch, dropin_levels)
+extern "C" int pdvc_ms_deform_attn_forward_f32(const float* value, const int64_t* spatial_shapes,
+                                               const int64_t* level_start_index, const float* sampling_loc,
+                                               const float* attn_weight, int batch, int spatial_size, int num_heads,
+                                               int channels, int num_levels, int num_query, int num_point,
+                                               int im2col_step, float* output, void* stream) {
+    int rc = check_common(batch, spatial_size, num_heads, channels, num_levels, num_query, num_point);
+    if (rc) return rc;
+    if ((rc = check_step(batch, im2col_step))) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const int fast = dropin1d_applies(spatial_size, num_heads, channels, num_levels, num_query, num_point);
+    if (fast && (rc = dropin1d_forward(value, spatial_shapes, level_start_index, sampling_loc, attn_weight, batch,
+                                       spatial_size, num_heads, num_query, output, s)))
+        return rc;
+    return launch_fwd<float, PDVC_PAD_ZEROS, 0>(value, spatial_shapes, level_start_index, sampling_loc, attn_weight,
+                                                batch, spatial_size, num_heads, channels, num_levels, num_query,
+                                                num_point, output, s, fast);
+}
+
+extern "C" size_t pdvc_ms_deform_attn_workspace_floats(int batch, int num_heads, int num_levels, int num_query,
+                                                       int num_point) {
+    return 2 * (size_t)batch * num_query * num_heads * num_levels * num_point;
+}
+
+extern "C" int pdvc_ms_deform_attn_backward_ws_f32(const float* value, const int64_t* spatial_shapes,
+                                                   const int64_t* level_start_index, const float* sampling_loc,
+                                                   const float* attn_weight, const float* grad_output, int batch,
+                                                   int spatial_size, int num_heads, int channels, int num_levels,
+                                                   int num_query, int num_point, int im2col_step, float* grad_value,
+                                                   float* grad_sampling_loc, float* grad_attn_weight, float* workspace,
+                                                   size_t workspace_floats, void* stream) {
+    int rc = check_common(batch, spatial_size, num_heads, channels, num_levels, num_query, num_point);
+    if (rc) return rc;
+    if ((rc = check_step(batch, im2col_step))) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const int fast = workspace != nullptr &&
+                     workspace_floats >= pdvc_ms_deform_attn_workspace_floats(batch, num_heads, num_levels, num_query,
+                                                                              num_point) &&
+                     dropin1d_applies(spatial_size, num_heads, channels, num_levels, num_query, num_point);
+    // the general path first: with the gate its zero fill and kernel retire at once for a 1-D pyramid
+    if ((rc = launch_bwd<float, PDVC_PAD_ZEROS, 0>(value, spatial_shapes, level_start_index, sampling_loc, attn_weight,
+                                                   grad_output, batch, spatial_size, num_heads, channels, num_levels,
+                                                   num_query, num_point, grad_value, grad_sampling_loc,
+                                                   grad_attn_weight, s, fast)))
+        return rc;
+    if (fast)
+        return dropin1d_backward(value, spatial_shapes, level_start_index, sampling_loc, attn_weight, grad_output,
+                                 batch, spatial_size, num_heads, num_query, grad_value, grad_sampling_loc,
+                                 grad_attn_weight, workspace, s);
+    return PDVC_OK;
+}
+
+extern "C" int pdvc_ms_deform_attn_backward_f32(const float* value, const int64_t* spatial_shapes,
+                                                const int64_t* level_start_index, const float* sampling_loc,
+                                                const float* attn_weight, const float* grad_output, int batch,
+                                                int spatial_size, int num_heads, int channels, int num_levels,
+                                                int num_query, int num_point, int im2col_step, float* grad_value,
+                                                float* grad_sampling_loc, float* grad_attn_weight, void* stream) {
+    return pdvc_ms_deform_attn_backward_ws_f32(value, spatial_shapes, level_start_index, sampling_loc, attn_weight,
+                                               grad_output, batch, spatial_size, num_heads, channels, num_levels,
+                                               num_query, num_point, im2col_step, grad_value, grad_sampling_loc,
+                                               grad_attn_weight, nullptr, 0, stream);
+}
 
 extern "C" int pdvc_ms_deform_sample_f32(const float* value, const int64_t* spatial_shapes,
                                          const int64_t* level_start_index, const float* sampling_loc, int batch,

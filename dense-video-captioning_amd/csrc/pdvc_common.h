@@ -152,6 +152,30 @@ struct Levels {
     int start[PDVC_MAX_LEVELS];
 };
 
+// PDVC's temporal pyramid for the fused 1-D kernels (msda1d.hip): 4 levels, lengths and start rows, by value.
+constexpr int kL1d = 4;
+struct Levels1d {
+    int T[kL1d];
+    int start[kL1d];
+};
+
+// The drop-in operator's level table, read from device memory: true when it is PDVC's lifted 1-D pyramid (see the
+// drop-in kernels below).
+__device__ __forceinline__ bool dropin_levels(const int64_t* __restrict__ shapes, const int64_t* __restrict__ lsi, int S,
+                                              Levels1d& lv) {
+    bool ok = true;
+    int64_t st = 0;
+#pragma unroll
+    for (int l = 0; l < kL1d; ++l) {
+        const int64_t h = shapes[2 * l], w = shapes[2 * l + 1];
+        ok = ok && h == 1 && w > 0 && lsi[l] == st;
+        lv.T[l] = (int)w;
+        lv.start[l] = (int)st;
+        st += w;
+    }
+    return ok && st == (int64_t)S;
+}
+
 // Attention dropout mask (mha.hip, seqattn.hip): a counter hash of (seed, video*head, query, key), regenerated in
 // the backward; keep with probability 1 - p (24-bit uniform against thresh = p * 2^24).
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {

@@ -21,6 +21,7 @@ SIGNATURES = {
     "pdvc_ms_deform_attn_forward_f64": [_vp] * 5 + [_i] * 8 + [_vp, _vp],
     "pdvc_ms_deform_attn_backward_f32": [_vp] * 6 + [_i] * 8 + [_vp] * 4,
     "pdvc_ms_deform_attn_backward_f64": [_vp] * 6 + [_i] * 8 + [_vp] * 4,
+    "pdvc_ms_deform_attn_backward_ws_f32": [_vp] * 6 + [_i] * 8 + [_vp] * 4 + [ctypes.c_size_t, _vp],
     "pdvc_ms_deform_sample_f32": [_vp] * 4 + [_i] * 8 + [_vp, _vp],
     "pdvc_ms_deform_sample_backward_f32": [_vp] * 5 + [_i] * 8 + [_vp] * 3,
     "pdvc_msda1d_forward_f32": [_vp, _u8p, _vp, _i, _i, _i, _vp, _i, _vp] + [_i] * 6 + [_vp] * 4,
@@ -85,6 +86,8 @@ def lib():
         L.pdvc_detokenize.restype = ctypes.c_int
         L.pdvc_mha_workspace_floats.argtypes = [ctypes.c_int] * 4
         L.pdvc_mha_workspace_floats.restype = ctypes.c_long
+        L.pdvc_ms_deform_attn_workspace_floats.argtypes = [ctypes.c_int] * 5
+        L.pdvc_ms_deform_attn_workspace_floats.restype = ctypes.c_size_t
         L.pdvc_last_error.restype = ctypes.c_char_p
         L.pdvc_abi_version.restype = ctypes.c_int
         _lib = L

@@ -59,6 +59,7 @@
 #ifndef PDVC_MSDA_H
 #define PDVC_MSDA_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -107,6 +108,22 @@ int pdvc_ms_deform_attn_backward_f64(const double* value, const int64_t* spatial
                                      int spatial_size, int num_heads, int channels, int num_levels,
                                      int num_query, int num_point, int im2col_step, double* grad_value,
                                      double* grad_sampling_loc, double* grad_attn_weight, void* stream);
+
+/* The f32 entry points take a 1-D fast path when the level table (read on the device, never by the host) is
+ * PDVC's lifted pyramid -- 4 levels, every H == 1, starts the prefix sums of W, sum W == S -- with D == 64 and
+ * P == 4 (pdvc/ops/modules/ms_deform_attn.py:114-117 calls the op exactly so): the fused 1-D gather kernels,
+ * and a value gradient without float atomics.  Any other table takes the general 2-D kernels.  The backward's
+ * fast path needs a workspace of pdvc_ms_deform_attn_workspace_floats(...) floats (16-byte aligned): the
+ * ws entry point below; pdvc_ms_deform_attn_backward_f32 (no workspace) is the general path.
+ * PDVC_DROPIN_1D=0 in the environment disables the fast path (A/B). */
+size_t pdvc_ms_deform_attn_workspace_floats(int batch, int num_heads, int num_levels, int num_query, int num_point);
+int pdvc_ms_deform_attn_backward_ws_f32(const float* value, const int64_t* spatial_shapes,
+                                        const int64_t* level_start_index, const float* sampling_loc,
+                                        const float* attn_weight, const float* grad_output, int batch,
+                                        int spatial_size, int num_heads, int channels, int num_levels, int num_query,
+                                        int num_point, int im2col_step, float* grad_value, float* grad_sampling_loc,
+                                        float* grad_attn_weight, float* workspace, size_t workspace_floats,
+                                        void* stream);
 
 /* ---- raw samples (return_value=True), general 2-D, padding PDVC_PAD_* --------------------------------
  * samples (N*M, D, Lq, L, P) exactly as the reference core returns them. */

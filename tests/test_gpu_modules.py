@@ -341,7 +341,11 @@ def test_caption_decode_function_matches_step_loop(heads, rd1, deferred):
         close(a, b, 1e-4, "grad_" + name)
     assert set(gp1) == set(gp0)
     for k in gp0:
-        close(gp1[k], gp0[k], 1e-4, k)
+        if k.endswith("alpha_net.bias"):  # zero in exact arithmetic (softmax shift invariance): both sides are
+            # rounding noise, bounded against the scale of the alpha_net weight gradient
+            assert_close(gp1[k], gp0[k], k, 1e-4, scale=gp0[k[:-4] + "weight"].abs().max().item())
+        else:
+            close(gp1[k], gp0[k], 1e-4, k)
 
 
 def test_caption_value_grad_chunked_steps():

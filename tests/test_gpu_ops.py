@@ -88,6 +88,86 @@ def test_dropin_gradient_channels_vs_oracle(channels):
     close(ga, ega, 1e-11, "grad_attn")
 
 
+def _lifted_inputs(rng, N, M, T_l, Lq, D=64, P=4, y_mode="half"):
+    """Drop-in op inputs on PDVC's lifted pyramid (spatial_shapes [[1, T_l]], ms_deform_attn.py:114-117): x over the
+    levels and past both ends, kept off cell edges (the location gradient steps there); y = 0.5 as PDVC passes it,
+    or (y_mode "mixed") a quarter of the samples at other heights -- inside (-0.5, 1.5), off the kinks at y = 0.5
+    and at the ends, and a few outside."""
+    L = len(T_l)
+    S = sum(T_l)
+    shapes = np.array([(1, t) for t in T_l], np.int64)
+    lsi = np.concatenate([[0], np.cumsum(T_l)[:-1]]).astype(np.int64)
+    value = rng.randn(N, S, M, D)
+    Tn = np.asarray(T_l, np.float64)[None, None, None, :, None]
+    x = rng.uniform(-0.05, 1.05, size=(N, Lq, M, L, P))
+    u = x * Tn - 0.5
+    frac = u - np.floor(u)
+    u = np.where(np.minimum(frac, 1 - frac) < 2e-3, u + 5e-3, u)
+    x = (u + 0.5) / Tn
+    y = np.full_like(x, 0.5)
+    if y_mode == "mixed":
+        pick = rng.rand(*x.shape) < 0.25
+        h = rng.uniform(-0.97, 0.97, size=x.shape)
+        h = np.where(np.abs(h) < 2e-3, 0.1, h)
+        out = rng.rand(*x.shape) < 0.05
+        h = np.where(out, rng.choice([-1.3, 1.2], size=x.shape), h)
+        y = np.where(pick, h + 0.5, y)
+    loc = np.stack([x, y], -1)
+    attn = rng.rand(N, Lq, M, L, P) + 1e-3
+    attn /= attn.sum((-1, -2), keepdims=True)
+    gout = rng.randn(N, Lq, M * D)
+    return value, shapes, lsi, loc, attn, gout
+
+
+@pytest.mark.parametrize("Lq,y_mode", [(960, "half"), (100, "half"), (960, "mixed"), (100, "mixed")])
+def test_dropin_fast_path_full_size_vs_oracle(Lq, y_mode):
+    """The drop-in operator on PDVC's full lifted pyramid (T = 512: S = 960; the encoder's Lq = S and the decoder's
+    Lq = 100, M = 8, D = 64, fp32) -- the shapes a stock MSDeformAttn module hands the extension.  The library takes
+    its 1-D fast path (device-side check of the level table, atomic-free value gradient) and must equal the oracle's
+    zero-padding CUDA semantics, y at 0.5 and at other heights in the cell."""
+    import MultiScaleDeformableAttention as MSDA
+    rng = np.random.RandomState(Lq + len(y_mode))
+    T_l = [512, 256, 128, 64]
+    N, M = 2, 8
+    value, shapes, lsi, loc, attn, gout = _lifted_inputs(rng, N, M, T_l, Lq, y_mode=y_mode)
+    ev = O.msda_forward(value, shapes, lsi, loc, attn, "zeros")
+    egv, egl, ega = O.msda_backward(value, shapes, lsi, loc, attn, gout, "zeros")
+    f32 = torch.float32
+    v, lo, a = cu(value, f32), cu(loc, f32), cu(attn, f32)
+    out = MSDA.ms_deform_attn_forward(v, cu(shapes), cu(lsi), lo, a, 64)
+    close(out, ev, 1e-4, "fwd")
+    gv, gl, ga = MSDA.ms_deform_attn_backward(v, cu(shapes), cu(lsi), lo, a, cu(gout, f32), 64)
+    close(gv, egv, 1e-4, "grad_value")
+    close(gl[..., 0], egl[..., 0], 1e-4, "grad_loc x")
+    close(gl[..., 1], egl[..., 1], 1e-4, "grad_loc y")
+    close(ga, ega, 1e-4, "grad_attn")
+
+
+def test_dropin_fast_path_leaves_2d_tables_to_the_general_kernels():
+    """A 2-D table of the same sizes (4 levels x 4 points, D = 64) and a 1-D table whose start index is not the prefix
+    sum of its lengths: both must take the general kernels (the fast path's device check refuses them) and still
+    equal the oracle."""
+    import MultiScaleDeformableAttention as MSDA
+    rng = np.random.RandomState(5)
+    N, M, Lq, D = 2, 2, 37, 64
+    for shapes, lsi in ((np.array([(2, 16), (2, 8), (1, 8), (2, 2)], np.int64), np.array([0, 32, 48, 56], np.int64)),
+                        (np.array([(1, 16), (1, 8), (1, 8), (1, 4)], np.int64), np.array([0, 16, 20, 28], np.int64))):
+        S = 60
+        value = rng.randn(N, S, M, D)
+        loc = rng.uniform(-0.1, 1.1, size=(N, Lq, M, 4, 4, 2))
+        attn = rng.rand(N, Lq, M, 4, 4)
+        gout = rng.randn(N, Lq, M * D)
+        ev = O.msda_forward(value, shapes, lsi, loc, attn, "zeros")
+        egv, egl, ega = O.msda_backward(value, shapes, lsi, loc, attn, gout, "zeros")
+        f32 = torch.float32
+        v, lo, a = cu(value, f32), cu(loc, f32), cu(attn, f32)
+        out = MSDA.ms_deform_attn_forward(v, cu(shapes), cu(lsi), lo, a, 64)
+        close(out, ev, 1e-4, "fwd")
+        gv, gl, ga = MSDA.ms_deform_attn_backward(v, cu(shapes), cu(lsi), lo, a, cu(gout, f32), 64)
+        close(gv, egv, 1e-4, "grad_value")
+        close(ga, ega, 1e-4, "grad_attn")
+
+
 def test_dropin_autograd_gradcheck():
     """torch.autograd.gradcheck through MSDeformAttnFunction (test.py:63-78), fp64."""
     from pdvc.ops.functions import MSDeformAttnFunction
