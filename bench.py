@@ -92,6 +92,12 @@ def parse():
                    help="skip the profiled eager step that prices the projection GEMMs against the MFMA peak")
     p.add_argument("--gemm-table", choices=["auto", "off"], default="auto",
                    help="auto: library GEMMs use the pre-tuned solution table (pdvc/gemm_tuning.py) when present")
+    p.add_argument("--stream", choices=["fixed", "ragged"], default="fixed",
+                   help="fixed: one synthetic batch, E events x W words per video, replayed every step (the metric's "
+                        "config); ragged: a seeded stream of distinct batches -- events per video drawn from the "
+                        "ActivityNet count distribution, caption lengths from 2 to 28 words -- one per step, padded to "
+                        "fixed capacities (pdvc/batch_layout.py) so one captured step graph serves them all")
+    p.add_argument("--stream-batches", type=int, default=4, help="distinct batches of the ragged stream")
     a = p.parse_args()
     a.frontend = None
     for k, v in WORKLOADS[a.workload].items():
@@ -254,6 +260,44 @@ def cpu_baseline_c(a, budget_s, enc_layers=2, dec_layers=2):
                       f"oracle/msda_oracle.c (zeros), single thread, {el:.1f} s"}
 
 
+def ragged_items(n_videos, T, C, vocab, seed, duration=120.0):
+    """One batch of a ragged stream in the collate tuple format: per video the event count drawn from the
+    ActivityNet train distribution (criterion.COUNTER_CLASS_RATE, 2..27 events, mean 3.7), each caption's word count
+    from a gamma law of mean 13.5 clipped to [2, 28] (the reference's translate() keeps at most max_caption_len - 2
+    = 28 words, data/video_dataset.py:161-168)."""
+    from pdvc.criterion import COUNTER_CLASS_RATE
+    rng = np.random.RandomState(seed)
+    rate = np.asarray(COUNTER_CLASS_RATE, np.float64)
+    rate = rate / rate.sum()
+    out = []
+    for v in range(n_videos):
+        ne = int(rng.choice(len(rate), p=rate))
+        feat = rng.standard_normal((T, C)).astype(np.float32)
+        ts = np.sort(rng.uniform(0, duration, size=(ne, 2)), axis=1)
+        ts[:, 1] = np.minimum(np.maximum(ts[:, 1], ts[:, 0] + 1.0), duration)
+        words = np.clip(np.round(rng.gamma(5.0, 13.5 / 5.0, size=ne)), 2, 28).astype(int)
+        caps = [np.array([0] + list(rng.randint(1, vocab, size=w)) + [0], dtype=np.int64) for w in words]
+        stamps = [[t[0] / duration * T, t[1] / duration * T] for t in ts]
+        out.append((feat, stamps, [0] * ne, caps, [list(t) for t in ts], duration, ["w"] * ne, f"rag_{seed}_{v}"))
+    return out
+
+
+def ragged_stream(a, B, vocab, device, rank, padded):
+    """`a.stream_batches` distinct ragged batches resident in HBM, capacity-padded when `padded` (the graph path):
+    capacities = 27 events per video, the stream's largest caption-row count rounded up to 128, 30 tokens."""
+    from pdvc.batch_layout import pad_to_capacity
+    from pdvc.data import collate, to_device
+    raw = [collate(ragged_items(B, a.T, a.C, vocab, seed=5000 + 97 * rank + i)) for i in range(a.stream_batches)]
+    rows = max(int(d["cap_tensor"].shape[0]) for d in raw)
+    caps = dict(events=27, rows=(rows + 127) // 128 * 128, words=30)
+    stats = {"events_per_video_mean": float(np.mean([len(t["labels"]) for d in raw for t in d["video_target"]])),
+             "caption_rows_per_batch": [int(d["cap_tensor"].shape[0]) for d in raw],
+             "words_per_caption_mean": float(np.mean([float(m.sum()) - 2 for d in raw for m in d["cap_mask"]])),
+             "capacity": caps if padded else None}
+    out = [to_device(pad_to_capacity(d, **caps) if padded else d, device) for d in raw]
+    return out, stats
+
+
 def dropin_msda(T, videos=256, reps=10):
     """The drop-in operator MultiScaleDeformableAttention (what a stock MSDeformAttn module calls, vision.cpp:13-16)
     at PDVC's lifted pyramid (spatial_shapes [[1, T_l]], y = 0.5), encoder (Lq = S) and decoder (Lq = 100) shapes,
@@ -383,20 +427,36 @@ def main():
     opt = torch.optim.AdamW(params, lr=args.lr, weight_decay=args.weight_decay, fused=True)
     B = a.videos_per_gpu
     vocab = args.vocab_size + 1
-    dt = add_sound(a, to_device(collate(synthetic_videos(B, a.T, a.C, a.events, a.words, vocab, seed=1000 + rank)),
-                                device), device, 2000 + rank)
+    stream, stream_stats = None, None
+    if a.stream == "ragged":
+        if a.frontend:
+            raise SystemExit("--stream ragged: PDVC workloads only")
+        stream, stream_stats = ragged_stream(a, B, vocab, device, rank, padded=a.graph == "step")
+        dt = stream[0]
+    else:
+        dt = add_sound(a, to_device(collate(synthetic_videos(B, a.T, a.C, a.events, a.words, vocab,
+                                                             seed=1000 + rank)), device), device, 2000 + rank)
+    cur = [dt]  # the batch the eager step runs on (the ragged stream advances it)
     wd = criterion.weight_dict
     from pdvc.precision import bf16_matmul
     bf16 = a.precision == "bf16"
+    step_no = [0]
+
+    def next_batch():
+        if stream is not None:
+            cur[0] = stream[step_no[0] % len(stream)]
+            step_no[0] += 1
+        return cur[0]
 
     def fwd_bwd():
-        out, loss = model(dt, criterion, "queries")
+        out, loss = model(cur[0], criterion, "queries")
         total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
         opt.zero_grad(set_to_none=True)
         total.backward()
         return total
 
     def eager_step():
+        next_batch()
         with bf16_matmul(bf16):
             total = fwd_bwd()
         if reducer is not None:
@@ -416,6 +476,8 @@ def main():
         dbg = os.environ.get("PDVC_DEBUG_SYNC") == "1"
 
         def step():  # the graph leaves the gradients in place (and averaged over ranks by its reducer)
+            if stream is not None:  # the stream's next batch into the captured inputs (same capacities)
+                sg.load(next_batch())
             total = sg.replay()
             if dbg:
                 torch.cuda.synchronize()
@@ -465,11 +527,13 @@ def main():
         _native.TIMER = None
         timing_note = ("HIP events around every launch in 2 eager steps right after the timed (hipGraph) steps, "
                        "same shapes; step wall time excludes them")
+        if stream is not None:
+            timing_note += " (eager steps on the capacity-padded batches)"
     ks = timer.summary()
     log("GEMM roofline step")
     groof = None if a.no_gemm_roofline else gemm_roofline(fwd_bwd, step, a.precision, graphed)
     dropin = None
-    if rank == 0 and not a.frontend:
+    if rank == 0 and not a.frontend and stream is None:
         log("drop-in operator timing")
         dropin = dropin_msda(a.T)
     videos = a.steps * B * world
@@ -481,8 +545,12 @@ def main():
         "config": {"workload": f"{os.path.basename(a.cfg)[:-4]} training step (fwd+loss+bwd+allreduce+AdamW): " +
                                ("dual-modality MHA front-end (clips + sound, 768-d, 32 heads) + " if a.frontend
                                 else "") +
-                               f"T={a.T} C={a.C} L=4 Q={a.Q} {args.enc_layers} enc/{args.dec_layers} dec layers, "
-                               f"E={a.events} events x {a.words} words, vocab {vocab}, dropout on" +
+                               f"T={a.T} C={a.C} L=4 Q={a.Q} {args.enc_layers} enc/{args.dec_layers} dec layers, " +
+                               (f"E={a.events} events x {a.words} words" if stream is None else
+                                f"ragged stream of {len(stream)} distinct batches (events per video from the "
+                                f"ActivityNet count distribution, 2-28 words per caption), a new batch every step" +
+                                (" loaded into the captured graph" if a.graph == "step" else "")) +
+                               f", vocab {vocab}, dropout on" +
                                (", GEMMs on bf16 operands with fp32 accumulation, fp32 storage elsewhere" if bf16
                                 else ", fp32 throughout"),
                    "videos_per_gpu": B, "global_batch": B * world, "seq_len": a.T,
@@ -544,6 +612,8 @@ def main():
         result["roofline"] = result["roofline_gather"]
     if dropin is not None:
         result["dropin_msda"] = dropin
+    if stream_stats is not None:
+        result["config"]["stream"] = stream_stats
     ksteps = 2 if graphed else a.steps
     result["kernels"] = {n: {"launches": v["launches"], "avg_us": 1e3 * v["ms"] / max(v["launches"], 1),
                              "share_of_step": v["ms"] / ksteps / (1e3 * el / a.steps)} for n, v in ks.items()}

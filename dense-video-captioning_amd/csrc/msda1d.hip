@@ -335,7 +335,8 @@ __device__ __forceinline__ int pyr_base(const Levels1d& lv, int l) {
 // guarded layout; the corner x0 + 1 is the next row (+256 B, a ds_read immediate)
 __device__ __forceinline__ int pyr_corner(int base, int i0) { return (base + i0) * 256; }
 
-template <int RD>
+// ABL (measurement only, PDVC_PYR_ABLATE): 1 = no HBM staging (LDS holds whatever it held), 2 = no gather phase
+template <int RD, int ABL = 0>
 __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
     int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
@@ -369,7 +370,7 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
         r0v[i] = ref[(row * kL + l_own) * RD];
         r1v[i] = (RD == 2) ? ref[(row * kL + l_own) * RD + 1] : 0.f;
     }
-    pyr_stage_g_lean(lds4, vsrc, MD, lv.start[0], lv.T[0]);
+    if (ABL != 1) pyr_stage_g_lean(lds4, vsrc, MD, lv.start[0], lv.T[0]);
     // per query: the owner lane's corner-row byte offset and its two corner weights, the attention weight folded in
     int adv[kPyrQPS];
     float w1v[kPyrQPS], w2v[kPyrQPS];
@@ -447,13 +448,15 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
         }
     };
     __syncthreads();  // level 0 was staged before the parameter math
-    level(std::integral_constant<int, 0>{});
+    if (ABL != 2) level(std::integral_constant<int, 0>{});
     __syncthreads();  // levels 1..3 in one round trip
-    pyr_stage_g(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3]);
+    if (ABL != 1) pyr_stage_g(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3]);
     __syncthreads();
-    level(std::integral_constant<int, 1>{});
-    level(std::integral_constant<int, 2>{});
-    level(std::integral_constant<int, 3>{});
+    if (ABL != 2) {
+        level(std::integral_constant<int, 1>{});
+        level(std::integral_constant<int, 2>{});
+        level(std::integral_constant<int, 3>{});
+    }
 #pragma unroll
     for (int i = 0; i < kPyrQPS; ++i) {
         const int q = qb * kPyrQ + slot + 64 * i;
@@ -1612,7 +1615,22 @@ extern "C" int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_
         if ((rc = pyr_attrs())) return rc;
         PDVC_CHECK_ARG((long)batch * num_heads * qb < (1L << 31), "too many query blocks");
         dim3 pg((unsigned)(batch * num_heads * qb));
-        if (ref_dim == 1)
+        static const int ablate = [] {
+            const char* e = getenv("PDVC_PYR_ABLATE");
+            return e ? atoi(e) : 0;
+        }();
+        if (ablate == 1 || ablate == 2) {  // measurement only (tools/kbench.py)
+            const void* k = ablate == 1 ? (const void*)msda1d_fwd_pyr_kernel<1, 1> : (const void*)msda1d_fwd_pyr_kernel<1, 2>;
+            (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPyrLds);
+            if (ablate == 1)
+                hipLaunchKernelGGL((msda1d_fwd_pyr_kernel<1, 1>), pg, dim3(kPyrThreads), kPyrLds, s, value,
+                                   value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv, num_query, S,
+                                   num_heads, qb, output, save_attn, save_loc);
+            else
+                hipLaunchKernelGGL((msda1d_fwd_pyr_kernel<1, 2>), pg, dim3(kPyrThreads), kPyrLds, s, value,
+                                   value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv, num_query, S,
+                                   num_heads, qb, output, save_attn, save_loc);
+        } else if (ref_dim == 1)
             hipLaunchKernelGGL((msda1d_fwd_pyr_kernel<1>), pg, dim3(kPyrThreads), kPyrLds, s, value, value_pad_mask,
                                proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, qb, output,
                                save_attn, save_loc);

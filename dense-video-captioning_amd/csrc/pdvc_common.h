@@ -27,10 +27,12 @@ __device__ __forceinline__ float grp_swap(float v, int d) {
     const int x = __float_as_int(v);
     int r;
     switch (d) {
-        case 1: r = __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false); break;   // quad_perm(1,0,3,2)
-        case 2: r = __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false); break;   // quad_perm(2,3,0,1)
-        case 4: r = __builtin_amdgcn_ds_swizzle(x, 0x1F | (0x04 << 10)); break;         // lane ^ 4
-        default: r = __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false); break;  // row_ror:8 = lane ^ 8
+        // every lane has a valid source in these patterns: mov_dpp (no `old` operand) saves the v_mov that would
+        // initialise one
+        case 1: r = __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true); break;   // quad_perm(1,0,3,2)
+        case 2: r = __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, true); break;   // quad_perm(2,3,0,1)
+        case 4: r = __builtin_amdgcn_ds_swizzle(x, 0x1F | (0x04 << 10)); break;  // lane ^ 4
+        default: r = __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, true); break;  // row_ror:8 = lane ^ 8
     }
     return __int_as_float(r);
 }
@@ -52,7 +54,7 @@ __device__ __forceinline__ int grp_bcast(int v, int k) {
     if constexpr (G == 16) {
         // DPP row_newbcast:k (dpp_ctrl 0x150 + k): lane k of each 16-lane row to the whole row, a VALU operand
         // modifier -- no LDS instruction (tools/probes/dpp_newbcast_probe.hip checks it on gfx950 for every k)
-#define PDVC_NB(K) case K: return __builtin_amdgcn_update_dpp(0, v, 0x150 + (K), 0xF, 0xF, false);
+#define PDVC_NB(K) case K: return __builtin_amdgcn_mov_dpp(v, 0x150 + (K), 0xF, 0xF, true);
         switch (k) {
             PDVC_NB(0) PDVC_NB(1) PDVC_NB(2) PDVC_NB(3) PDVC_NB(4) PDVC_NB(5) PDVC_NB(6) PDVC_NB(7)
             PDVC_NB(8) PDVC_NB(9) PDVC_NB(10) PDVC_NB(11) PDVC_NB(12) PDVC_NB(13) PDVC_NB(14) PDVC_NB(15)

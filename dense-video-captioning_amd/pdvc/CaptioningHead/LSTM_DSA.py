@@ -311,10 +311,11 @@ class LSTMDSACaptioner(Captioner):
         and the loss's gather in one pass, the backward in one pass -- the input of build_loss_picked)."""
         core = self.core
         if self.training and self.ss_prob > 0:
-            # LSTM_DSA.py:89-99 feeds sampled words back when ss_prob > 0; the whole-sequence decode here takes
-            # every input word up front.  (train.py:156 sets ss_prob on the caption_head ModuleList, which no
-            # captioner reads, so the reference's schedule never reaches this point either.)
-            raise NotImplementedError("scheduled sampling (ss_prob > 0) is not supported by the batched decode")
+            out = self.decode_scheduled_sampling(hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten,
+                                                 level_T, seq, n_steps)
+            if pick_target is None:
+                return out
+            return out, out.gather(2, pick_target[:, :n_steps, None]).squeeze(2)
         w = self._step_weights()
         value, mask_u8 = self._prepare(memory, mask_flatten)
         if n_steps == 0:
@@ -335,6 +336,43 @@ class LSTMDSACaptioner(Captioner):
         if pick_target is not None:
             return logprob_pick(logits, pick_target[:, :n_steps])
         return F.log_softmax(logits, dim=-1)
+
+    def decode_scheduled_sampling(self, hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten, level_T, seq,
+                                  n_steps, generator=None, record=None):
+        """The teacher-forced loop with scheduled sampling (LSTM_DSA.py:88-107, training with ss_prob > 0): from
+        step 1 on, each row's input word is, with probability ss_prob, drawn from the previous step's distribution
+        exp(logprobs) (torch.multinomial over every row, the drawn words substituted where a uniform draw falls
+        below ss_prob) instead of the ground-truth word; the drawn words carry no gradient.  Every step's input
+        then depends on the previous step's output, so the word gates are formed per step and the steps run
+        through autograd (the same per-step math as _step) instead of the whole-sequence CaptionDecodeFunction.
+        Rows whose video's loop has already stopped (the reference breaks at the video's first all-zero token
+        column) keep stepping with their masked targets, which the loss ignores.  record: a list that receives
+        each step's input words (R,) -- tests replay them through the teacher-forced path.  Returns logprobs
+        (R, n_steps, V).  (train.py:152-156 assigns the schedule to the caption_head ModuleList, which no
+        captioner reads: set Captioner.ss_prob itself to enable it.)"""
+        R = hs_rows.shape[0]
+        w = self._step_weights()
+        value, mask_u8 = self._prepare(memory, mask_flatten)
+        hs_part = F.linear(hs_rows, w["W_hs"])
+        off_hs = F.linear(hs_rows, w["W_off_hs"], w["b_off"])
+        h = hs_rows.new_zeros(R, w["H"])
+        c = hs_rows.new_zeros(R, w["H"])
+        outs = []
+        for i in range(n_steps):
+            it = seq[:, i].clone()
+            if i >= 1:
+                u = torch.rand(R, device=hs_rows.device, generator=generator)
+                drawn = torch.multinomial(torch.exp(outs[-1].detach()), 1, generator=generator).view(-1)
+                it = torch.where(u < self.ss_prob, drawn, it)
+            if record is not None:
+                record.append(it)
+            x_gates = F.linear(embed_rows(self.embed, it), w["W_x"])
+            h, c = self._step(w, h, c, x_gates, hs_part, off_hs, value, mask_u8, row_video, ref_rows, rd1_rows,
+                              level_T)
+            outs.append(F.log_softmax(self.logit(self.dropout(h)), dim=-1))
+        if not outs:
+            return hs_rows.new_zeros(R, 0, self.vocab_size + 1)
+        return torch.stack(outs, 1)
 
     @torch.no_grad()
     def decode_greedy(self, hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten, level_T, max_len=None,

@@ -77,6 +77,7 @@ class SetCriterion(nn.Module):
         nb = pt["num_boxes"]  # (N,) float, clamp(min=1)
         # matched pairs of every video, flattened: (video, query, target slot, rank) and the per-video match
         # counts -- one asynchronous host->device copy
+        pvalid = None  # capacity-padded batch: the pairs of phantom targets are masked out (pdvc/batch_layout.py)
         if pairs is None:
             vid = np.concatenate([np.full(len(i), v, np.int64) for v, (i, _) in enumerate(indices)])
             qid = np.concatenate([i.numpy() for i, _ in indices])
@@ -85,11 +86,18 @@ class SetCriterion(nn.Module):
             nmatch = np.asarray([len(i) for i, _ in indices], np.int64)
             pv, pq, pt_, pr, n_dev = hostio.pack_to_device([vid, qid, tid, rank, nmatch], dev)
             emax = max(len(i) for i, _ in indices) if indices else 0
+        elif len(pairs) == 7:
+            pv, pq, pt_, pr, n_dev, emax, pvalid = pairs
         else:
             pv, pq, pt_, pr, n_dev, emax = pairs
         # labels: focal loss over every query and class (criterion.py:46-65)
-        tclass = torch.full((N, Q), self.num_classes, dtype=torch.int64, device=dev)
-        tclass[pv, pq] = pt["labels"][pv, pt_]
+        if pvalid is None:
+            tclass = torch.full((N, Q), self.num_classes, dtype=torch.int64, device=dev)
+            tclass[pv, pq] = pt["labels"][pv, pt_]
+        else:  # a phantom pair writes into a spare column
+            tclass = torch.full((N, Q + 1), self.num_classes, dtype=torch.int64, device=dev)
+            tclass[pv, torch.where(pvalid, pq, Q)] = pt["labels"][pv, pt_]
+            tclass = tclass[:, :Q]
         onehot = torch.zeros((N, Q, C + 1), dtype=logits.dtype, device=dev)
         onehot.scatter_(2, tclass.unsqueeze(-1), 1)
         onehot = onehot[:, :, :-1]
@@ -112,13 +120,18 @@ class SetCriterion(nn.Module):
         l1 = F.l1_loss(src, tgt, reduction="none").sum(1)
         sxy, txy = box_ops.box_cl_to_xy(src), box_ops.box_cl_to_xy(tgt)
         giou = box_ops.generalized_box_iou(sxy[:, None], txy[:, None])[:, 0, 0]
+        gterm = 1 - giou
+        if pvalid is not None:
+            w = pvalid.to(l1.dtype)
+            l1, gterm = l1 * w, gterm * w
         loss_bbox = torch.zeros(N, device=dev, dtype=l1.dtype).index_add_(0, pv, l1) / nb
-        loss_giou = torch.zeros(N, device=dev, dtype=l1.dtype).index_add_(0, pv, 1 - giou) / nb
+        loss_giou = torch.zeros(N, device=dev, dtype=l1.dtype).index_add_(0, pv, gterm) / nb
         # self-IoU among each video's matched predictions, upper triangle, / (n(n-1)/2)
         padded = torch.zeros(N, max(emax, 1), 2, device=dev, dtype=sxy.dtype)
         padded[pv, pr] = sxy
         valid = torch.zeros(N, max(emax, 1), dtype=torch.bool, device=dev)
-        valid.index_put_((pv, pr), torch.ones(pv.shape, dtype=torch.bool, device=dev))  # no host scalar
+        valid.index_put_((pv, pr), torch.ones(pv.shape, dtype=torch.bool, device=dev) if pvalid is None
+                         else pvalid)  # no host scalar
         iou = box_ops.box_iou(padded, padded)[0]
         iou = torch.triu(iou, diagonal=1) * (valid[:, :, None] & valid[:, None, :])
         n = n_dev.to(l1.dtype)
@@ -141,11 +154,18 @@ class SetCriterion(nn.Module):
         count = torch.cat([o["pred_count"] for o in layers], 0)
         costs = self.matcher.cost_padded(logits, boxes, ptL)  # (Ld*N, Q, Emax)
         on_device = self.device_matching if self.device_matching is not None else costs.is_cuda
+        cap = pt.get("capacity")
+        if cap is not None and not (on_device and costs.dtype == torch.float32 and cap <= costs.shape[1]):
+            raise ValueError("a capacity-padded batch needs the device matching with capacity <= queries")
         if on_device and costs.dtype == torch.float32 and max(pt["sizes"], default=0) <= costs.shape[1]:
-            # matching on the GPU (scipy's algorithm): no host round trip anywhere in the training step
-            m = self.matcher.solve_device(costs, ptL["sizes"], ptL["sizes_i32"])
+            # matching on the GPU (scipy's algorithm): no host round trip anywhere in the training step; a
+            # capacity-padded batch passes the capacity as every problem's host bound, the counts on the device
+            m = self.matcher.solve_device(costs, ptL["sizes"] if cap is None else [cap] * costs.shape[0],
+                                          ptL["sizes_i32"])
             pp, pk, nm, emax = static_pairs(ptL)
             pairs = (pp, m.queries[pp, pk], m.targets[pp, pk], pk, nm, emax)
+            if cap is not None:
+                pairs = pairs + (pk < nm[pp],)
             per = self.video_losses(logits, boxes, count, ptL, None, pairs)
             idx = [(LazyIndices(m, b, N), None) for b in range(Ld)]
         else:
@@ -169,7 +189,8 @@ def static_pairs(pt):
     matched -- plus the per-problem match counts and the largest; device tensors, cached on the dict."""
     key = ("pairs",)
     if key not in pt:
-        sizes = pt["sizes"]
+        # a capacity-padded batch: every (problem, rank < capacity) pair, the phantom ones masked by the caller
+        sizes = pt["sizes"] if pt.get("capacity") is None else [pt["capacity"]] * len(pt["sizes"])
         pp = np.concatenate([np.full(e, p, np.int64) for p, e in enumerate(sizes)] or [np.zeros(0, np.int64)])
         pk = np.concatenate([np.arange(e) for e in sizes] or [np.zeros(0, np.int64)])
         dev = pt["sizes_long"].device

@@ -83,5 +83,7 @@ def to_device(dt, device):
             out[k] = v
     out["cap_tensor_cpu"] = dt["cap_tensor"].clone()
     from .matcher import padded_targets
-    out["video_target_padded"] = padded_targets(dt["video_target"], device)  # from the host copies
+    cap = dt.get("capacity")  # a capacity-padded batch (pdvc/batch_layout.py): targets padded to its event capacity
+    out["video_target_padded"] = padded_targets(dt["video_target"], device,
+                                                None if cap is None else cap["events"])  # from the host copies
     return out

@@ -63,7 +63,7 @@ class HungarianMatcher(nn.Module):
         to = torch.zeros_like(qo)
         _n.call("pdvc_lsap_f32", _n.ptr(costs.contiguous()), P, Q, E, _n.int_array(tuple(sizes)),
                 _n.ptr(sizes_dev), _n.ptr(qo), _n.ptr(to), _n.stream())
-        return DeviceMatching(qo, to, list(sizes))
+        return DeviceMatching(qo, to, list(sizes), sizes_dev)
 
     @staticmethod
     def solve_padded(costs, sizes):
@@ -96,14 +96,16 @@ class HungarianMatcher(nn.Module):
 class DeviceMatching:
     """Matchings of P problems held on the device: queries (P, Emax) ascending, targets (P, Emax)."""
 
-    def __init__(self, queries, targets, sizes):
+    def __init__(self, queries, targets, sizes, sizes_dev=None):
         self.queries, self.targets, self.sizes = queries, targets, sizes
+        self.sizes_dev = sizes_dev  # the true per-problem counts (sizes may be a capacity bound)
         self._host = None
 
     def host(self):
-        if self._host is None:  # one device->host copy, only when a caller asks for Python lists
+        if self._host is None:  # device->host copies, only when a caller asks for Python lists
             q, t = self.queries.cpu(), self.targets.cpu()
-            self._host = [(q[p, :e].clone(), t[p, :e].clone()) for p, e in enumerate(self.sizes)]
+            sizes = self.sizes_dev.cpu().tolist() if self.sizes_dev is not None else self.sizes
+            self._host = [(q[p, :e].clone(), t[p, :e].clone()) for p, e in enumerate(sizes)]
         return self._host
 
 
@@ -127,11 +129,17 @@ class LazyIndices:
         return iter(self._list())
 
 
-def padded_targets(targets, device):
+def padded_targets(targets, device, capacity=None):
     """Targets of a batch padded to the largest event count: labels (N, Emax) long, boxes (N, Emax, 2)
-    (padding boxes are a harmless (0.5, 0.5) segment), valid (N, Emax) bool, sizes [E_v]."""
+    (padding boxes are a harmless (0.5, 0.5) segment), valid (N, Emax) bool, sizes [E_v].  capacity: pad to
+    that many events per video instead (a shape-stable batch, pdvc/batch_layout.py), recorded as
+    "capacity": the host-side code then sizes everything by it and reads the true counts on the device."""
     sizes = [len(t["labels"]) for t in targets]
     emax = max(max(sizes), 1)
+    if capacity is not None:
+        if emax > capacity:
+            raise ValueError(f"padded_targets: a video has {emax} events, capacity {capacity}")
+        emax = capacity
     N = len(targets)
     labels = torch.zeros(N, emax, dtype=torch.long)
     boxes = torch.full((N, emax, 2), 0.5)
@@ -146,7 +154,7 @@ def padded_targets(targets, device):
     return {"labels": hostio.to_device(labels, device), "boxes": hostio.to_device(boxes, device),
             "valid": hostio.to_device(valid, device), "sizes": sizes,
             "sizes_long": hostio.to_device(sizes_t, device), "sizes_i32": hostio.to_device(sizes_t.int(), device),
-            "num_boxes": hostio.to_device(sizes_t.float().clamp(min=1.0), device)}
+            "num_boxes": hostio.to_device(sizes_t.float().clamp(min=1.0), device), "capacity": capacity}
 
 
 def build_matcher(args):

@@ -23,6 +23,7 @@ from .CaptioningHead import build_captioner
 from .CaptioningHead.LSTM_DSA import caption_steps
 from .criterion import SetCriterion
 from .deformable_transformer import build_deforamble_transformer
+from .batch_layout import caption_layout, caption_layout_to_device
 from .matcher import LazyIndices, build_matcher
 
 
@@ -271,32 +272,33 @@ class PDVC(nn.Module):
         for g in gt_counts:
             cap_off.append(cap_off[-1] + g)
         Ld_last = Ld - 1
+        cap = dt.get("capacity")
         if all(isinstance(ix, LazyIndices) for ix in layer_indices):
             # matching on the device: which rows exist is known from the target counts alone (every target is
-            # matched); only the matched query and target of each row come from the device matching
+            # matched); only the matched query and target of each row come from the device matching.  The row
+            # bookkeeping is host numpy over the counts (batch_layout.caption_layout), copied to the device once per
+            # batch and cached on dt -- a captured step graph re-uses the device tensors, and StepGraph.load
+            # refreshes them for a new batch of a capacity-padded stream
             m = layer_indices[0].matching
-            rows, r_p, r_k, r_base, r_cap = [], [], [], [], []
-            for l_id, ix in enumerate(layer_indices):  # layer-major: layer 0 (1-d references) first
-                for v in range(N):
-                    for k in range(gt_counts[v]):
-                        rows.append((l_id, v))
-                        r_p.append(ix.block * N + v)
-                        r_k.append(k)
-                        r_base.append((l_id * N + v) * Q)
-                        r_cap.append(cap_off[v])
-            last_sel = [i for i, r in enumerate(rows) if r[0] == Ld_last]
-            # the row bookkeeping depends on the batch's event counts only: one host->device copy per batch
-            # (cached on dt, so a captured step graph re-uses device tensors and copies nothing)
-            key = ("_caption_rows", Ld, N, Q, tuple(ix.block for ix in layer_indices))
+            blocks = tuple(ix.block for ix in layer_indices)
+            key = ("_caption_rows", Ld, N, Q, blocks)
             if key not in dt:
-                vr_start, vr_rows, max_rows = _video_csr(rows, N)
-                dt[key] = hostio.pack_to_device(
-                    [r_p, r_k, r_base, r_cap, [r[1] for r in rows], [r[0] for r in rows], [r[1] for r in rows],
-                     last_sel, vr_start, vr_rows], dev) + [max_rows]
-            rp, rk, rb, rc, row_video, lay, vid, last_sel_d, vr_start_d, vr_rows_d, max_rows = dt[key]
+                lay = caption_layout(gt_counts, Ld, N, Q, blocks, None if cap is None else cap["rows"],
+                                     None if cap is None else cap["events"])
+                dt[key] = caption_layout_to_device(lay, dev)
+            Lc = dt[key]
+            rp, rk, rb, rc, row_video = Lc["p"], Lc["k"], Lc["base"], Lc["cap"], Lc["vid"]
+            lay_t, vid, last_sel_d, vr_start_d, vr_rows_d = Lc["lay"], Lc["vid"], Lc["last_sel"], Lc["vr_start"], \
+                Lc["vr_rows"]
+            max_rows, Rl = Lc["max_rows"], Lc["rows_per_layer"]
             flat_idx = rb + m.queries[rp, rk]
-            cap_rows = rc + m.targets[rp, rk]
+            cap_rows = rc + m.targets[rp, rk] * Lc["valid"]
+            rows = Lc["rows_host"]  # (layer, video) per row, phantom rows (layer, 0): rd1 and n_last below
+            last_sel = list(range((Ld - 1) * Rl, Ld * Rl))
+            row_valid = Lc["valid"] if cap is not None else None
+            lay = lay_t
         else:
+            row_valid = None
             rows = []  # (layer, video, flat_hs_index, cap_row)
             for l_id, indices in enumerate(layer_indices):
                 for v, (qi, gi) in enumerate(indices):
@@ -324,16 +326,17 @@ class PDVC(nn.Module):
             refs.append(ref)
         ref_all = torch.stack(refs).reshape(Ld * N * Q, L, 2)
         ref_rows = ref_all.index_select(0, flat_idx)
-        steps_v = []
-        for v in range(N):
-            steps_v.append(caption_steps(cap_cpu[cap_off[v]:cap_off[v + 1]]))
+        if cap is not None:  # every video's loop runs the capacity's steps (the steps past a video's end are masked)
+            steps_v = [cap["words"] - 1] * N
+        else:
+            steps_v = [caption_steps(cap_cpu[cap_off[v]:cap_off[v + 1]]) for v in range(N)]
         video_csr = (vr_start_d.to(torch.int32), vr_rows_d.to(torch.int32), max_rows)
         # the last layer's rows are one contiguous block (rows are layer-major): its outputs are views, not copies
         last_range = (last_sel[0], len(last_sel)) if last_sel and last_sel[-1] - last_sel[0] + 1 == len(last_sel) \
             else None
         return dict(rows=rows, hs_rows=hs_rows, ref_rows=ref_rows.contiguous(), rd1=rd1, row_video=row_video,
                     cap_rows=cap_rows, lay=lay, vid=vid, last_sel=last_sel_d, last_range=last_range, steps_v=steps_v,
-                    video_csr=video_csr)
+                    video_csr=video_csr, row_valid=row_valid)
 
     def parallel_prediction_matched(self, dt, criterion, hs, init_reference, inter_references, others,
                                     disable_refine, heads=None):
@@ -369,9 +372,12 @@ class PDVC(nn.Module):
         # per (layer, video) mean over events, then mean over videos (= the reference's batch-1 losses)
         rows = R["rows"]
         key = R["lay"] * N + R["vid"]
+        ones = torch.ones_like(cap_loss)
+        if R["row_valid"] is not None:  # phantom rows of a capacity-padded batch count for no video
+            ones = R["row_valid"].to(cap_loss.dtype)
+            cap_loss = cap_loss * ones
         sums = torch.zeros(Ld * N, device=hs.device, dtype=cap_loss.dtype).index_add_(0, key, cap_loss)
-        cnts = torch.zeros(Ld * N, device=hs.device, dtype=cap_loss.dtype).index_add_(
-            0, key, torch.ones_like(cap_loss))
+        cnts = torch.zeros(Ld * N, device=hs.device, dtype=cap_loss.dtype).index_add_(0, key, ones)
         per = (sums / cnts.clamp(min=1)).view(Ld, N).mean(1)
         for l_id in range(Ld):
             k = "loss_caption" if l_id == Ld - 1 else f"loss_caption_{l_id}"
@@ -379,6 +385,8 @@ class PDVC(nn.Module):
         last_sel = R["last_sel"]
         last_v = [r[1] for r in rows if r[0] == Ld - 1]
         n_last = max([R["steps_v"][v] for v in last_v], default=0)
+        if dt.get("capacity") is not None:
+            n_last = n_steps
         if R["last_range"] is not None:
             last_lp = logprobs.narrow(0, R["last_range"][0], R["last_range"][1])
         else:

@@ -8,6 +8,10 @@ kernel needs a host read-back, so the step is captured once per batch shape and 
 
     sg = StepGraph(model, criterion, dt)   # warm-up + capture (dt tensors become the graph's inputs)
     sg.load(dt_next)                       # copy a same-shape batch into the captured inputs (optional)
+
+A batch padded to fixed capacities (pdvc/batch_layout.py pad_to_capacity: events per video, caption rows,
+caption width) makes every later batch of the stream a same-shape batch, whatever its event counts and caption
+lengths: load() then also recomputes the caption rows' bookkeeping on the host and copies it in.
     total = sg.replay()                    # forward + losses + backward; param.grad hold the new gradients
 
 Dropout stays random per replay (torch's graph-safe Philox offsets; the HIP kernels draw their seeds on the
@@ -61,8 +65,12 @@ class StepGraph:
     @staticmethod
     def _signature(dt):
         """The host facts the captured step depends on: events per video and each video's caption step count
-        (the reference's loop stops at the video's first all-zero token column, LSTM_DSA.py:88-104)."""
+        (the reference's loop stops at the video's first all-zero token column, LSTM_DSA.py:88-104) -- or, for a
+        capacity-padded batch (pdvc/batch_layout.py), only the capacities and the batch size."""
         from .CaptioningHead.LSTM_DSA import caption_steps
+        if dt.get("capacity") is not None:
+            c = dt["capacity"]
+            return ("capacity", len(dt["video_target"]), c["events"], c["rows"], c["words"])
         counts = [len(t["labels"]) for t in dt["video_target"]]
         cap = dt.get("cap_tensor_cpu")
         cap = dt["cap_tensor"].detach().cpu() if cap is None else cap
@@ -84,7 +92,8 @@ class StepGraph:
                 raise ValueError("StepGraph.load: the batch's event / caption-step counts differ from the captured "
                                  "batch's; capture a graph for it")
             from .matcher import padded_targets
-            new = padded_targets(dt["video_target"], self.dt["video_tensor"].device)
+            new = padded_targets(dt["video_target"], self.dt["video_tensor"].device,
+                                 (dt.get("capacity") or {}).get("events"))
             old = self.dt["video_target_padded"]
             for k, v in new.items():
                 if isinstance(v, torch.Tensor):
@@ -95,6 +104,15 @@ class StepGraph:
                         if isinstance(v, torch.Tensor):
                             v.copy_(new[kk].repeat(k[1], *([1] * (v.dim() - 1))), non_blocking=True)
             self.dt["cap_tensor_cpu"] = dt.get("cap_tensor_cpu", dt["cap_tensor"].detach().cpu())
+            if dt.get("capacity") is not None:  # the caption rows' bookkeeping of the new counts
+                from .batch_layout import caption_layout, refresh_caption_layout
+                counts = [len(t["labels"]) for t in dt["video_target"]]
+                cap = dt["capacity"]
+                for k, cached in self.dt.items():
+                    if isinstance(k, tuple) and k and k[0] == "_caption_rows":
+                        _, Ld, N, Q, blocks = k
+                        refresh_caption_layout(cached, caption_layout(counts, Ld, N, Q, blocks, cap["rows"],
+                                                                      cap["events"]))
         for k, v in dt.items():
             dst = self.dt.get(k)
             if isinstance(v, torch.Tensor) and isinstance(dst, torch.Tensor) and dst.device.type == "cuda":

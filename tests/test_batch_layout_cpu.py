@@ -1,0 +1,98 @@
+"""Host logic of capacity-padded batches (pdvc/batch_layout.py), CPU only: the caption-row layout against the
+per-row loop it replaced (pdvc.py `_caption_rows` up to round 2), phantom rows, pad_to_capacity, and the
+criterion's static pairs at a capacity."""
+import numpy as np
+import pytest
+import torch
+
+from pdvc.batch_layout import caption_layout, pad_to_capacity
+
+
+def legacy_rows(counts, Ld, N, Q, blocks):
+    """The round-2 loop: for every layer, video and event: (problem, rank, hs base, caption base, video, layer)."""
+    cap_off = [0]
+    for g in counts:
+        cap_off.append(cap_off[-1] + g)
+    rows, r_p, r_k, r_base, r_cap = [], [], [], [], []
+    for l_id in range(Ld):
+        for v in range(N):
+            for k in range(counts[v]):
+                rows.append((l_id, v))
+                r_p.append(blocks[l_id] * N + v)
+                r_k.append(k)
+                r_base.append((l_id * N + v) * Q)
+                r_cap.append(cap_off[v])
+    by_video = [[] for _ in range(N)]
+    for i, r in enumerate(rows):
+        by_video[r[1]].append(i)
+    start = [0]
+    for v in range(N):
+        start.append(start[-1] + len(by_video[v]))
+    flat = [i for v in range(N) for i in by_video[v]]
+    return rows, r_p, r_k, r_base, r_cap, start, flat, max((len(b) for b in by_video), default=0)
+
+
+@pytest.mark.parametrize("counts", [[2, 3, 5], [1], [4, 0, 7, 1], [3] * 9])
+@pytest.mark.parametrize("Ld", [1, 2, 3])
+def test_exact_layout_equals_the_row_loop(counts, Ld):
+    N, Q = len(counts), 10
+    blocks = [(l + 1) % Ld for l in range(Ld)]  # aux layers 1.., the last layer block 0 (criterion.forward)
+    rows, r_p, r_k, r_base, r_cap, start, flat, mx = legacy_rows(counts, Ld, N, Q, blocks)
+    lay = caption_layout(counts, Ld, N, Q, blocks)
+    assert lay["p"].tolist() == r_p and lay["k"].tolist() == r_k
+    assert lay["base"].tolist() == r_base and lay["cap"].tolist() == r_cap
+    assert list(zip(lay["lay"].tolist(), lay["vid"].tolist())) == rows
+    assert lay["vr_start"].tolist() == start and lay["vr_rows"].tolist() == flat and lay["max_rows"] == mx
+    assert lay["valid"].tolist() == [1] * len(rows)
+    assert lay["last_sel"].tolist() == [i for i, r in enumerate(rows) if r[0] == Ld - 1]
+
+
+@pytest.mark.parametrize("counts,cap", [([2, 3, 5], 12), ([1, 1], 5), ([4, 0, 7, 1], 16)])
+def test_capacity_layout_keeps_the_real_rows_and_adds_phantoms(counts, cap):
+    N, Q, Ld = len(counts), 10, 2
+    blocks = [1, 0]
+    ex = caption_layout(counts, Ld, N, Q, blocks)
+    lay = caption_layout(counts, Ld, N, Q, blocks, rows_cap=cap, events_cap=max(counts) + 2)
+    tot = sum(counts)
+    for l_id in range(Ld):
+        real = slice(l_id * cap, l_id * cap + tot)
+        phantom = slice(l_id * cap + tot, (l_id + 1) * cap)
+        for k in ("p", "k", "base", "cap", "vid", "lay"):
+            assert lay[k][real].tolist() == ex[k][l_id * tot:(l_id + 1) * tot].tolist(), k
+        assert (lay["valid"][real] == 1).all() and (lay["valid"][phantom] == 0).all()
+        assert (lay["cap"][phantom] == tot).all(), "phantom rows read the all-zero caption row"
+        assert (lay["lay"][phantom] == l_id).all()
+    assert lay["last_sel"].tolist() == list(range((Ld - 1) * cap, Ld * cap))
+    # the CSR lists exactly the real rows, video by video, at their capacity positions
+    n_real = int(lay["vr_start"][-1])
+    assert n_real == Ld * tot and len(lay["vr_rows"]) == Ld * cap
+    real_rows = sorted(lay["vr_rows"][:n_real].tolist())
+    assert real_rows == sorted(i for i in range(Ld * cap) if lay["valid"][i])
+    assert lay["max_rows"] == Ld * (max(counts) + 2)
+    with pytest.raises(ValueError):
+        caption_layout(counts, Ld, N, Q, blocks, rows_cap=tot - 1)
+
+
+def test_pad_to_capacity():
+    from pdvc.data import collate, synthetic_videos
+    dt = collate(synthetic_videos(3, 16, 8, 4, 5, 30, seed=1))
+    p = pad_to_capacity(dt, events=6, rows=20, words=11)
+    assert p["cap_tensor"].shape == (21, 11) and p["cap_mask"].shape == (21, 11)
+    tot, K = dt["cap_tensor"].shape
+    assert torch.equal(p["cap_tensor"][:tot, :K], dt["cap_tensor"]) and not p["cap_tensor"][tot:].any()
+    assert not p["cap_tensor"][:, K:].any() and not p["cap_mask"][tot:].any()
+    assert p["gt_boxes"].shape == (3, 6, 2) and p["capacity"] == {"events": 6, "rows": 20, "words": 11}
+    for bad in (dict(events=3, rows=20, words=11), dict(events=6, rows=11, words=11),
+                dict(events=6, rows=20, words=K - 1)):
+        with pytest.raises(ValueError):
+            pad_to_capacity(dt, **bad)
+
+
+def test_static_pairs_at_capacity():
+    from pdvc.criterion import static_pairs
+    sizes = [2, 0, 3]
+    pt = {"sizes": sizes, "sizes_long": torch.tensor(sizes), "capacity": 4}
+    pp, pk, nm, emax = static_pairs(pt)
+    assert emax == 4 and pp.tolist() == [0] * 4 + [1] * 4 + [2] * 4 and pk.tolist() == list(range(4)) * 3
+    valid = (pk < nm[pp]).tolist()
+    assert valid == [True, True, False, False] + [False] * 4 + [True, True, True, False]

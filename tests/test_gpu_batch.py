@@ -194,3 +194,87 @@ def test_batched_eval_and_postprocess_match_reference(fixture):
         assert int(r["pred_seq_len"]) == int(d[f"v{v}.post.pred_seq_len"])
         close(np.asarray(r["caption_scores"]), d[f"v{v}.post.caption_scores"], f"video {v} caption scores")
         assert list(r["captions"]) == [str(s) for s in d[f"v{v}.post.captions"]], f"video {v} captions"
+
+
+# ------------------------------------------------------------------------------------------------
+# capacity-padded batches (pdvc/batch_layout.py): one captured step for a stream of ragged batches
+# ------------------------------------------------------------------------------------------------
+CAPS = dict(events=7, rows=16, words=12)
+
+
+def padded_dt(items):
+    import weights as W  # noqa: F401
+    from pdvc.batch_layout import pad_to_capacity
+    from pdvc.data import collate, to_device
+    return to_device(pad_to_capacity(collate(items), **CAPS), DEV)
+
+
+def _check_padded_forward(d, out, loss, nv, cap):
+    wd_keys = [f[len("v0.loss."):] for f in d.files if f.startswith("v0.loss.")]
+    for k in wd_keys:
+        ref = np.mean([float(d[f"v{v}.loss.{k}"]) for v in range(nv)])
+        assert_scalar(loss[k], ref, f"loss {k} (capacity-padded) vs the mean of the batch-1 values")
+    for v in range(nv):
+        close(out["pred_logits"][v:v + 1], d[f"v{v}.pred_logits"], f"video {v} pred_logits")
+        close(out["pred_boxes"][v:v + 1], d[f"v{v}.pred_boxes"], f"video {v} pred_boxes")
+    probs = out["caption_probs"]["cap_prob_train"]
+    assert probs.shape[0] == cap["rows"] and probs.shape[1] == cap["words"] - 1
+    row = 0
+    for v in range(nv):
+        ref = d[f"v{v}.cap_prob_train"]
+        e, steps = ref.shape[0], ref.shape[1]
+        close(probs[row:row + e, :steps], ref, f"video {v} cap_prob_train (capacity-padded)")
+        row += e
+
+
+def test_capacity_padded_batch_equals_reference(fixture):
+    """The fixture's 3 videos padded to fixed capacities (7 events per video, 16 caption rows per layer, 12-token
+    captions): phantom targets and caption rows change no loss and no gradient -- the same bound against the
+    reference's batch-1 steps as the unpadded batch."""
+    d = fixture
+    nv = int(d["n_videos"])
+    model, criterion = TM.build_filled(d)
+    model.train()
+    import weights as W
+    dt = padded_dt(W.batch_items(vocab=29))
+    out, loss = model(dt, criterion, "queries")
+    _check_padded_forward(d, out, loss, nv, dt["capacity"])
+    wd = criterion.weight_dict
+    total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
+    assert_scalar(total, np.mean([float(d[f"v{v}.total_loss"]) for v in range(nv)]), "total loss (capacity-padded)")
+    total.backward()
+    _check_grads(d, model.named_parameters(), "capacity-padded batch")
+
+
+def test_capacity_step_graph_follows_a_ragged_stream(fixture):
+    """ONE StepGraph captured on a capacity-padded batch serves batches of other event counts and caption lengths:
+    load() a batch of the same videos in another order (per-position counts 5, 2, 3 instead of 2, 3, 5) and the
+    replay equals the eager unpadded step on it; load the first batch back and the replay equals the reference."""
+    from pdvc.data import collate, to_device
+    from pdvc.step_graph import StepGraph
+    import weights as W
+    d = fixture
+    nv = int(d["n_videos"])
+    model, criterion = TM.build_filled(d)
+    model.train()
+    items = W.batch_items(vocab=29)
+    perm = [items[2], items[0], items[1]]
+    # eager reference on the permuted batch, unpadded
+    wd = criterion.weight_dict
+    model.zero_grad(set_to_none=True)
+    _, loss_b = model(to_device(collate(perm), DEV), criterion, "queries")
+    total_b = sum(loss_b[k] * wd[k] for k in loss_b.keys() if k in wd)
+    total_b.backward()
+    grads_b = {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
+    model.zero_grad(set_to_none=True)
+    sg = StepGraph(model, criterion, padded_dt(items))
+    assert_scalar(sg.replay(), np.mean([float(d[f"v{v}.total_loss"]) for v in range(nv)]), "replay, batch A")
+    _check_grads(d, model.named_parameters(), "capacity step graph, batch A")
+    sg.load(padded_dt(perm))
+    assert_scalar(sg.replay(), total_b.item(), "replay after load(batch B)")
+    for n, p in model.named_parameters():
+        if n in grads_b:
+            close(p.grad, grads_b[n], f"capacity step graph, batch B: grad {n}")
+    sg.load(padded_dt(items))
+    sg.replay()
+    _check_grads(d, model.named_parameters(), "capacity step graph, batch A again")

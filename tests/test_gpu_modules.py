@@ -477,3 +477,116 @@ def test_teacher_forced_ctx2att_gather_equals_gemm(masked):
         assert (a is None) == (b is None)
         if a is not None:
             close(a, b.cpu().numpy(), 1e-4, "grad")
+
+
+# ------------------------------------------------------------------------------------------------
+# scheduled sampling (LSTM_DSA.py:88-99): parity unpinned for the draws themselves (torch's device RNG is
+# not the reference's CPU RNG); pinned through the realised input words and the law of the draws
+# ------------------------------------------------------------------------------------------------
+def _ss_setup(R_copies=None):
+    from pdvc.CaptioningHead.LSTM_DSA import LSTMDSACaptioner, caption_steps
+    d = load("module_captioner_ref1")
+    cap = LSTMDSACaptioner(small_opt()).to(DEV)
+    fill(cap)
+    cap.train()
+    T_l = tuple(int(t) for t in d["T_l"])
+    hs, ref = cu(d["hs"]), cu(d["ref"])
+    cap_tensor = cu(d["cap_tensor"])
+    if R_copies:
+        hs = hs[:, :1].expand(1, R_copies, -1).contiguous()
+        ref = ref[:, :1].expand(1, R_copies, -1).contiguous()
+        cap_tensor = cap_tensor[:1].expand(R_copies, -1).contiguous()
+    others = {"memory": cu(d["memory"]), "mask_flatten": cu(d["mask"]), "level_T": T_l,
+              "spatial_shapes": torch.tensor(T_l, device=DEV), "valid_ratios": torch.ones(1, 4, device=DEV)}
+    rows = cap._rows_from_reference(hs, ref, others)
+    n = caption_steps(cap_tensor.cpu())
+    return cap, rows, others, cap_tensor, n
+
+
+def test_scheduled_sampling_equals_teacher_forcing_on_the_realised_words():
+    """With ss_prob = 0.5 the loop feeds drawn words back; replaying the realised input words through the teacher-forced
+    path (CaptionDecodeFunction, pinned to the reference by test_captioner_vs_golden) must give the same log-probabilities
+    and every gradient, within 1e-4."""
+    cap, (hs_rows, ref, rd1, rv, T), others, cap_tensor, n = _ss_setup()
+    gen = torch.Generator(device=DEV).manual_seed(11)
+    g = torch.randn(hs_rows.shape[0], n, cap.vocab_size + 1, device=DEV)
+
+    def run(ss, seq, record=None):
+        cap.zero_grad(set_to_none=True)
+        cap.ss_prob = ss
+        h, r, mem = hs_rows.clone().requires_grad_(), ref.clone().requires_grad_(), others["memory"].clone().requires_grad_()
+        if ss > 0:
+            lp = cap.decode_scheduled_sampling(h, r, rd1, rv, mem, others["mask_flatten"], T, seq, n, generator=gen,
+                                               record=record)
+        else:
+            lp = cap.decode_teacher_forced(h, r, rd1, rv, mem, others["mask_flatten"], T, seq, n)
+        (lp * g).sum().backward()
+        return lp.detach(), [h.grad, r.grad, mem.grad], {k: p.grad for k, p in cap.named_parameters() if p.grad is not None}
+
+    record = []
+    lp_ss, gi_ss, gp_ss = run(0.5, cap_tensor, record)
+    assert len(record) == n
+    realised = cap_tensor.clone()
+    for i, it in enumerate(record):
+        realised[:, i] = it
+    assert not torch.equal(realised[:, :n], cap_tensor[:, :n]), "no word was drawn at ss_prob 0.5"
+    lp_tf, gi_tf, gp_tf = run(0.0, realised)
+    close(lp_ss, lp_tf, 1e-4, "logprobs")
+    for name, a, b in zip(("hs", "ref", "memory"), gi_ss, gi_tf):
+        close(a, b, 1e-4, "grad_" + name)
+    assert set(gp_ss) == set(gp_tf)
+    for k in gp_tf:
+        if k.endswith("alpha_net.bias"):
+            assert_close(gp_ss[k], gp_tf[k], k, 1e-4, scale=gp_tf[k[:-4] + "weight"].abs().max().item())
+        else:
+            close(gp_ss[k], gp_tf[k], 1e-4, k)
+
+
+def test_scheduled_sampling_draws_follow_the_previous_step():
+    """ss_prob = 1: every input word from step 1 on is drawn from exp(previous step's log-probabilities).  4096 copies of
+    one row share step 0's distribution: the frequency ratio of the two most drawn step-1 words matches
+    exp(lp_a - lp_b) within 5 standard errors; at ss_prob = 0 the words are the ground truth."""
+    cap, (hs_rows, ref, rd1, rv, T), others, cap_tensor, n = _ss_setup(R_copies=4096)
+    cap.ss_prob = 1.0
+    rec = []
+    with torch.no_grad():
+        lp = cap.decode_scheduled_sampling(hs_rows, ref, rd1, rv, others["memory"], others["mask_flatten"], T,
+                                           cap_tensor, n, generator=torch.Generator(device=DEV).manual_seed(3),
+                                           record=rec)
+    words = rec[1].cpu().numpy()
+    lp0 = lp[0, 0].double().cpu().numpy()
+    assert np.allclose(lp[:, 0].cpu().numpy(), lp[0:1, 0].cpu().numpy(), atol=1e-6), "copies must share step 0"
+    vals, counts = np.unique(words, return_counts=True)
+    assert len(vals) >= 2
+    a, b = vals[np.argsort(-counts)[:2]]
+    ca, cb = counts[vals == a][0], counts[vals == b][0]
+    expect = np.exp(lp0[a] - lp0[b])
+    se = (ca / cb) * np.sqrt(1.0 / ca + 1.0 / cb)
+    assert abs(ca / cb - expect) <= 5 * se, f"ratio {ca / cb:.3f} vs exp(lp_a - lp_b) {expect:.3f}"
+    assert torch.equal(rec[0], cap_tensor[:, 0]), "step 0 always takes the ground-truth word"
+    cap.ss_prob = 0.0
+    rec0 = []
+    with torch.no_grad():
+        cap.decode_scheduled_sampling(hs_rows[:8], ref[:8], min(rd1, 8), rv[:8], others["memory"],
+                                      others["mask_flatten"], T, cap_tensor[:8], n, record=rec0)
+    for i, it in enumerate(rec0):
+        assert torch.equal(it, cap_tensor[:8, i])
+
+
+def test_model_step_with_scheduled_sampling():
+    """A whole batched training step with Captioner.ss_prob = 0.25 (the decode's per-step path): finite losses and
+    gradients for every parameter the teacher-forced step trains."""
+    sys.path.insert(0, HERE)
+    import test_gpu_model as TM
+    d = TM.load("pdvc_small_anet")
+    model, criterion = TM.build_filled(d)
+    model.train()
+    model.caption_head[0].ss_prob = 0.25
+    out, loss = model(TM.fixture_dt(d), criterion, "queries")
+    total = sum(loss[k] * criterion.weight_dict[k] for k in loss.keys() if k in criterion.weight_dict)
+    assert torch.isfinite(total)
+    total.backward()
+    for n_, p in model.named_parameters():
+        assert (p.grad is None) == ("gradnone." + n_ in d.files), n_
+        if p.grad is not None:
+            assert torch.isfinite(p.grad).all(), n_

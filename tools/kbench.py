@@ -56,7 +56,7 @@ def main():
         fb = N * S * M * D * e + N * Lq * M * 16 * 12 + N * Lq * M * D * e
         bb = 3 * N * S * M * D * e + N * Lq * M * D * e + 2 * N * Lq * M * 16 * 12
         print(f"{name:8s} N={N} Lq={Lq}: fwd {tf:8.1f} us ({fb / tf / 1e3:7.1f} GB/s alg)  "
-              f"bwd {tb:8.1f} us ({bb / tb / 1e3:7.1f} GB/s alg)  [ablate={os.environ.get('PDVC_ABLATE_VALUE', '0')}]",
+              f"bwd {tb:8.1f} us ({bb / tb / 1e3:7.1f} GB/s alg)  [ablate={os.environ.get('PDVC_PYR_ABLATE', '0')}]",
               flush=True)
 
 
