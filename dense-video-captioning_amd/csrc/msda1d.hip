@@ -370,7 +370,13 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
         r0v[i] = ref[(row * kL + l_own) * RD];
         r1v[i] = (RD == 2) ? ref[(row * kL + l_own) * RD + 1] : 0.f;
     }
-    if (ABL != 1) pyr_stage_g_lean(lds4, vsrc, MD, lv.start[0], lv.T[0]);
+    // ABL == 3 (measurement only): workgroups of odd slot pairs run the levels in the other order (levels 1..3 staged
+    // and gathered first), so that neighbouring CUs stage at different times
+    const bool rev = ABL == 3 && ((blockIdx.x >> 3) & 1);
+    if (ABL != 1) {
+        if (rev) pyr_stage_g_lean(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3]);
+        else pyr_stage_g_lean(lds4, vsrc, MD, lv.start[0], lv.T[0]);
+    }
     // per query: the owner lane's corner-row byte offset and its two corner weights, the attention weight folded in
     int adv[kPyrQPS];
     float w1v[kPyrQPS], w2v[kPyrQPS];
@@ -447,15 +453,25 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
             tok = acc[i];
         }
     };
-    __syncthreads();  // level 0 was staged before the parameter math
-    if (ABL != 2) level(std::integral_constant<int, 0>{});
-    __syncthreads();  // levels 1..3 in one round trip
-    if (ABL != 1) pyr_stage_g(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3]);
-    __syncthreads();
-    if (ABL != 2) {
+    __syncthreads();  // the first phase's rows were staged before the parameter math
+    if (rev) {
         level(std::integral_constant<int, 1>{});
         level(std::integral_constant<int, 2>{});
         level(std::integral_constant<int, 3>{});
+        __syncthreads();
+        pyr_stage_g(lds4, vsrc, MD, lv.start[0], lv.T[0]);
+        __syncthreads();
+        level(std::integral_constant<int, 0>{});
+    } else {
+        if (ABL != 2) level(std::integral_constant<int, 0>{});
+        __syncthreads();  // levels 1..3 in one round trip
+        if (ABL != 1) pyr_stage_g(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3]);
+        __syncthreads();
+        if (ABL != 2) {
+            level(std::integral_constant<int, 1>{});
+            level(std::integral_constant<int, 2>{});
+            level(std::integral_constant<int, 3>{});
+        }
     }
 #pragma unroll
     for (int i = 0; i < kPyrQPS; ++i) {
@@ -1619,11 +1635,17 @@ extern "C" int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_
             const char* e = getenv("PDVC_PYR_ABLATE");
             return e ? atoi(e) : 0;
         }();
-        if (ablate == 1 || ablate == 2) {  // measurement only (tools/kbench.py)
-            const void* k = ablate == 1 ? (const void*)msda1d_fwd_pyr_kernel<1, 1> : (const void*)msda1d_fwd_pyr_kernel<1, 2>;
+        if (ablate >= 1 && ablate <= 3 && ref_dim == 1) {  // measurement only (tools/kbench.py)
+            const void* k = ablate == 1 ? (const void*)msda1d_fwd_pyr_kernel<1, 1>
+                            : ablate == 2 ? (const void*)msda1d_fwd_pyr_kernel<1, 2>
+                                          : (const void*)msda1d_fwd_pyr_kernel<1, 3>;
             (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPyrLds);
             if (ablate == 1)
                 hipLaunchKernelGGL((msda1d_fwd_pyr_kernel<1, 1>), pg, dim3(kPyrThreads), kPyrLds, s, value,
+                                   value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv, num_query, S,
+                                   num_heads, qb, output, save_attn, save_loc);
+            else if (ablate == 3)
+                hipLaunchKernelGGL((msda1d_fwd_pyr_kernel<1, 3>), pg, dim3(kPyrThreads), kPyrLds, s, value,
                                    value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv, num_query, S,
                                    num_heads, qb, output, save_attn, save_loc);
             else

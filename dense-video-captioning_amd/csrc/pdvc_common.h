@@ -1,6 +1,7 @@
 // pdvc_common.h -- shared device helpers for the PDVC HIP kernels (gfx950 / CDNA4, wave64).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 
 #include "pdvc_msda.h"
@@ -221,6 +222,11 @@ __global__ __launch_bounds__(256) void zero_fill_kernel(float* __restrict__ p, s
 
 static inline hipError_t zero_async(float* p, size_t n, hipStream_t s) {
     if (n == 0) return hipSuccess;
+    static const bool use_memset = [] {  // diagnosis only (tools/diag_memset_graph.py): the hipMemsetAsync form
+        const char* e = getenv("PDVC_ZERO_MEMSET");
+        return e && e[0] == '1';
+    }();
+    if (use_memset) return hipMemsetAsync(p, 0, n * sizeof(float), s);
     const bool vec = ((uintptr_t)p % 16 == 0) && (n % 4 == 0);
     const size_t work = vec ? n / 4 : n;
     const unsigned blocks = (unsigned)(work / 256 + 1 < 8192 ? work / 256 + 1 : 8192);

@@ -225,7 +225,7 @@ class LSTMDSACaptioner(Captioner):
         M = core.deformable_att.n_heads
         D = value.shape[-1] // M
         return (hs_rows.is_cuda and hs_rows.dtype == torch.float32 and value.dtype == torch.float32
-                and w["A"] > 0 and w["A"] % 4 == 0 and D % 4 == 0 and (4 * w["H"]) % 4 == 0
+                and w["A"] > 0 and w["A"] % 4 == 0 and D % 4 == 0 and w["H"] % 4 == 0
                 and core.deformable_att.fused)
 
     def _greedy_buffers(self, R, value, w):

@@ -66,7 +66,7 @@ class SetCriterion(nn.Module):
         v = self.video_losses(outputs["pred_logits"], outputs["pred_boxes"], outputs["pred_count"], pt, indices)
         return {k: t.mean() for k, t in v.items()}
 
-    def video_losses(self, logits, boxes, count, pt, indices, pairs=None):
+    def video_losses(self, logits, boxes, count, pt, indices, pairs=None, query_mask=None):
         """Per-video loss vectors (N,) for a batch of N videos -- or of N = layers x videos when the decoder
         layers are stacked -- computed for all at once.  logits (N,Q,C), boxes (N,Q,2), count (N,K+1); pt:
         padded targets; indices: list of (query ids, target ids) per video, or None with `pairs` = device
@@ -102,7 +102,10 @@ class SetCriterion(nn.Module):
         onehot.scatter_(2, tclass.unsqueeze(-1), 1)
         onehot = onehot[:, :, :-1]
         focal = sigmoid_focal_terms(logits, onehot, self.focal_alpha, self.focal_gamma)  # (N,Q,C)
-        loss_ce = focal.mean(1).sum(1) / nb * Q
+        if query_mask is None:
+            loss_ce = focal.mean(1).sum(1) / nb * Q
+        else:  # 'gt_proposals' batch: the sum over each video's real proposals (= its batch-1 mean x its Q)
+            loss_ce = (focal * query_mask[:, :, None].to(focal.dtype)).sum((1, 2)) / nb
         # counter (criterion.py:67-76)
         max_length = count.shape[1] - 1
         ctgt = pt["sizes_long"].clamp(max=max_length)
@@ -112,7 +115,10 @@ class SetCriterion(nn.Module):
                               dev)
         loss_counter = counter_loss_terms(count, ctgt_onehot, self.opt.lloss_gau_mask, self.opt.lloss_beta, weight)
         # cardinality (logging only, criterion.py:80-92)
-        card_pred = (logits.argmax(-1) != C - 1).sum(1).float()
+        card_hit = logits.argmax(-1) != C - 1
+        if query_mask is not None:
+            card_hit = card_hit & query_mask
+        card_pred = card_hit.sum(1).float()
         card_err = (card_pred - pt["sizes_long"].float()).abs()
         # boxes (criterion.py:94-123): L1 and GIoU of matched pairs, per-video sums via index_add
         src = boxes[pv, pq]
@@ -153,6 +159,10 @@ class SetCriterion(nn.Module):
         boxes = torch.cat([o["pred_boxes"] for o in layers], 0)
         count = torch.cat([o["pred_count"] for o in layers], 0)
         costs = self.matcher.cost_padded(logits, boxes, ptL)  # (Ld*N, Q, Emax)
+        qm = outputs.get("query_mask")  # 'gt_proposals': padded proposal slots never match, nor enter a loss
+        if qm is not None:
+            qm = qm.repeat(Ld, 1)
+            costs = costs.masked_fill(~qm[:, :, None], 1.0e6)
         on_device = self.device_matching if self.device_matching is not None else costs.is_cuda
         cap = pt.get("capacity")
         if cap is not None and not (on_device and costs.dtype == torch.float32 and cap <= costs.shape[1]):
@@ -166,12 +176,12 @@ class SetCriterion(nn.Module):
             pairs = (pp, m.queries[pp, pk], m.targets[pp, pk], pk, nm, emax)
             if cap is not None:
                 pairs = pairs + (pk < nm[pp],)
-            per = self.video_losses(logits, boxes, count, ptL, None, pairs)
+            per = self.video_losses(logits, boxes, count, ptL, None, pairs, qm)
             idx = [(LazyIndices(m, b, N), None) for b in range(Ld)]
         else:
             solved = self.matcher.solve_padded(list(costs.view(Ld, N, *costs.shape[1:])), pt["sizes"])
             idx = [(s_, None) for s_ in solved]
-            per = self.video_losses(logits, boxes, count, ptL, [m_ for s_ in solved for m_ in s_])
+            per = self.video_losses(logits, boxes, count, ptL, [m_ for s_ in solved for m_ in s_], query_mask=qm)
         last_indices = idx[0]
         outputs["matched_indices"] = last_indices
         per = {k: v.view(Ld, N).mean(1) for k, v in per.items()}

@@ -21,12 +21,13 @@ from torch.autograd.function import once_differentiable
 
 from pdvc import _native as _n
 from pdvc.precision import fp32_gemms
-from .linear import colsum, wgrad_mm
+from .linear import colsum, tag_level_sums, wgrad_mm
 from .ms_deform_attn_func import NUM_SAMPLES, _levels
 
 
 # ctx2att of the samples as a gather of the once-projected value rows (see forward); False keeps the per-step GEMM
 CTX2ATT_GATHER = True
+U_MAX_BYTES = 16 << 30  # largest projected-rows buffer of the gather form (bound its memory)
 
 
 class CaptionDecodeFunction(Function):
@@ -77,7 +78,11 @@ class CaptionDecodeFunction(Function):
             # projections with the same gather -- U rows N*S instead of a (R*16) x D x A GEMM for each of n steps.
             # The backward is unchanged (dW_ctx, db_ctx and dclip come from CLIP and dATT).
             U = None
-            if CTX2ATT_GATHER and 32 <= A <= 512 and A & (A - 1) == 0 and n * R * M * NS > Nv * S * M:
+            # the projected rows take Nv*S*M*A floats, A/D times the value's (8x at cap_nheads 8): the gather form only
+            # while that stays within U_MAX_BYTES (the per-step GEMM needs no such buffer)
+            u_bytes = 4 * Nv * S * M * A
+            if (CTX2ATT_GATHER and 32 <= A <= 512 and A & (A - 1) == 0 and n * R * M * NS > Nv * S * M
+                    and u_bytes <= U_MAX_BYTES):
                 vm = value if pad_mask is None else value.masked_fill(pad_mask.view(Nv, S, 1, 1).bool(), 0.0)
                 U = torch.addmm(b_ctx, vm.view(-1, D), W_ctx.t()).view(Nv, S, M, A)
             for i in range(n):
@@ -184,6 +189,6 @@ class CaptionDecodeFunction(Function):
         if ctx.flat_value:
             gv = gv.view(Nv, -1, M * D)
             if deferred:
-                gv._pdvc_level_sums = lsums
+                tag_level_sums(gv, lsums)
         return (gv, d_gates, d_hs_g, d_off_hs, gr, dW_h, db_h, dW_ctx, db_ctx, dalpha_w, dalpha_b, dW_att, None, None,
                 None, None, None, None)

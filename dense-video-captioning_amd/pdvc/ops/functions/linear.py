@@ -236,13 +236,29 @@ class MultiLinearFunction(Function):
                 gx.addmm_(g2, w)
             # a fused deformable-attention consumer hands its value gradient over with per-(video, level) row sums
             # (MSDA1dFunction): the bias gradient from those instead of another pass over g
-            ls = getattr(g, "_pdvc_level_sums", None)
+            ls = level_sums_of(g)
             LEVEL_SUM_USES[0] += ls is not None
             gb = ls.view(-1, ls.shape[-1]).sum(0) if ls is not None and ls.shape[-1] == w.shape[0] else colsum(g2)
             gwb += [wgrad_mm(g2, x2), gb]
         if gx is None:
             gx = torch.zeros_like(x2)
         return (gx.view(ctx.shape), *gwb)
+
+
+def tag_level_sums(g, sums):
+    """Hand a value gradient over to its projection's backward with its per-(video, level) row sums, tagged with
+    the gradient's version counter: if autograd later accumulates a second consumer's gradient into g in place,
+    the version moves and the sums are ignored."""
+    g._pdvc_level_sums = (sums, g._version)
+    return g
+
+
+def level_sums_of(g):
+    """The row sums tag_level_sums attached to g, or None when absent or stale (g modified since tagging)."""
+    ent = getattr(g, "_pdvc_level_sums", None)
+    if ent is None or ent[1] != g._version:
+        return None
+    return ent[0]
 
 
 def multi_dense(x, layers):

@@ -175,7 +175,8 @@ class MSDA1dFunction(Function):
         if flat:
             gv = gv.view(N, S, M * D)
             if sums:
-                gv._pdvc_level_sums = res[3]
+                from .linear import tag_level_sums
+                tag_level_sums(gv, res[3])
         return gv, None, gp, gr, None, None, None, None
 
 

@@ -32,11 +32,21 @@ def _get_clones(module, N):
 
 
 def decide_two_stage(transformer_input_type, dt, criterion):
-    """misc/utils.py:31-49 ('queries' mode; the '*_gt' proposal-input variants are out of scope)."""
+    """misc/utils.py:31-49.  'gt_proposals' (the cfgs/*_gt.yml runs): the ground-truth segments dt['gt_boxes']
+    (N, Emax, 2) become the decoder's queries and reference points, their mask dt['gt_boxes_mask'] the query mask;
+    the caption cost leaves the matcher and the length / class / box / GIoU losses get weight 0 -- on the
+    criterion object itself, as the reference does (a later 'queries' call keeps those weights) -- and the
+    decoder's iterative refinement is off."""
+    if transformer_input_type == "gt_proposals":
+        criterion.matcher.cost_caption = 0
+        for q_k in ("loss_length", "loss_ce", "loss_bbox", "loss_giou"):
+            for key in criterion.weight_dict.keys():
+                if q_k in key:
+                    criterion.weight_dict[key] = 0
+        return True, True, dt["gt_boxes"], dt["gt_boxes_mask"]
     if transformer_input_type == "queries":
         return False, False, None, None
-    raise NotImplementedError(f"transformer_input_type '{transformer_input_type}' is not supported on the "
-                              f"MI355X path (BASELINE configs use 'queries')")
+    raise ValueError(f"Wrong value of transformer_input_type, got {transformer_input_type}")
 
 
 # PDVC_CAP_DEFERRED=0: per-step float atomics for the caption value gradient (A/B switch)
@@ -90,6 +100,14 @@ class _TrunkModule(nn.Module):
         return self._pdvc.trunk(vf, video_mask, duration)
 
 
+def _masked_query_max(hs_l, query_mask):
+    """The count head's max over queries (pdvc.py:169-172) over the valid queries only: a batch of videos with
+    different proposal counts pads the shorter ones (the reference runs one video, every query valid)."""
+    if query_mask is None:
+        return hs_l
+    return hs_l.masked_fill(~query_mask[..., None], float("-inf"))
+
+
 class PDVC(nn.Module):
     def __init__(self, base_encoder, transformer, captioner, num_classes, num_queries, num_feature_levels,
                  aux_loss=True, with_box_refine=False, opt=None, translator=None):
@@ -132,11 +150,13 @@ class PDVC(nn.Module):
         self.disable_mid_caption_heads = opt.disable_mid_caption_heads
 
     # ------------------------------------------------------------------------------------------------
-    def trunk(self, vf, video_mask, duration):
+    def trunk(self, vf, video_mask, duration, proposals=None, proposals_mask=None):
         """The static-shape part of PDVC.forward (pdvc/pdvc.py:123-150 in the reference): base encoder,
         deformable encoder, decoder with iterative refinement and the per-layer class/count/box heads.
         Tensors in, tensors out, no host synchronisation: it can be captured as one hipGraph forward and
-        one backward (enable_graph)."""
+        one backward (enable_graph).  With proposals (the 'gt_proposals' input, pdvc.py:141-143): the decoder's
+        queries come from the proposals (prepare_decoder_input_proposal), the refinement is off and the boxes
+        are the proposals."""
         mask = ~video_mask
         N = vf.shape[0]
         srcs, masks, pos = self.base_encoder(vf, mask, duration)
@@ -149,15 +169,20 @@ class PDVC(nn.Module):
         kmask = None if self.__dict__.get("_no_padding", False) else mask_flatten
         memory = tr.forward_encoder(src_flatten, level_T, lsi, valid_ratios, lvl_pos, kmask)
         self._project_memory(memory)
-        query_embed = self.query_embed.weight
-        proposals_mask = torch.ones(N, query_embed.shape[0], device=query_embed.device).bool()
-        init_reference, tgt, reference_points, query_embed = tr.prepare_decoder_input_query(memory, query_embed)
+        two_stage = proposals is not None
+        if two_stage:
+            init_reference, tgt, reference_points, query_embed = tr.prepare_decoder_input_proposal(proposals)
+        else:
+            query_embed = self.query_embed.weight
+            proposals_mask = torch.ones(N, query_embed.shape[0], device=query_embed.device).bool()
+            init_reference, tgt, reference_points, query_embed = tr.prepare_decoder_input_query(memory, query_embed)
         hs, inter_references = tr.forward_decoder(tgt, reference_points, memory, level_T, lsi, valid_ratios,
-                                                  query_embed, kmask, proposals_mask, False)
+                                                  query_embed, kmask, proposals_mask, two_stage)
         side = tr.decoder.__dict__.pop("_side", None)
         if os.environ.get("PDVC_HEAD_SIDE", "1") == "0":  # A/B switch: heads on hs[l], box MLP evaluated again
             side = None
-        classes, counts, coords = self._layer_heads(hs, init_reference, inter_references, False, side)
+        classes, counts, coords = self._layer_heads(hs, init_reference, inter_references, two_stage, side,
+                                                    proposals_mask if two_stage else None)
         return (memory, mask_flatten, temporal_shapes, lsi, valid_ratios, proposals_mask, hs, init_reference,
                 inter_references, torch.stack(classes), torch.stack(counts), torch.stack(coords))
 
@@ -195,8 +220,10 @@ class PDVC(nn.Module):
         object.__setattr__(self, "_graph_key", key)
         object.__setattr__(self, "_graphed_trunk", graphed)
 
-    def _run_trunk(self, dt):
+    def _run_trunk(self, dt, proposals=None, proposals_mask=None):
         args = (dt["video_tensor"], dt["video_mask"], dt["video_length"][:, 1].contiguous())
+        if proposals is not None:  # the proposal-input trunk is not graphed on its own (StepGraph captures it whole)
+            return self.trunk(*args, proposals=proposals, proposals_mask=proposals_mask)
         g = self.__dict__.get("_graphed_trunk")
         key = (tuple((tuple(t.shape), t.dtype) for t in args), bool(self.__dict__.get("_no_padding", False)))
         if g is not None and self.training and key == self._graph_key:
@@ -208,7 +235,8 @@ class PDVC(nn.Module):
                                                                                  criterion)
         object.__setattr__(self, "_no_padding", bool(dt.get("video_mask_all_valid", False)))
         (memory, mask_flatten, temporal_shapes, lsi, valid_ratios, proposals_mask, hs, init_reference,
-         inter_references, classes, counts, coords) = self._run_trunk(dt)
+         inter_references, classes, counts, coords) = self._run_trunk(dt, proposals if two_stage else None,
+                                                                      proposals_mask if two_stage else None)
         others = {"memory": memory, "mask_flatten": None if self._no_padding else mask_flatten,
                   "spatial_shapes": temporal_shapes,
                   "level_T": self.transformer.last_level_T, "level_start_index": lsi, "valid_ratios": valid_ratios,
@@ -220,10 +248,10 @@ class PDVC(nn.Module):
         return self.parallel_prediction_matched(dt, criterion, hs, init_reference, inter_references, others,
                                                 disable_refine, heads)
 
-    def predict_event_num(self, counter, hs_lid):
-        return counter(torch.max(hs_lid, dim=1, keepdim=False)[0])
+    def predict_event_num(self, counter, hs_lid, query_mask=None):
+        return counter(torch.max(_masked_query_max(hs_lid, query_mask), dim=1, keepdim=False)[0])
 
-    def _layer_heads(self, hs, init_reference, inter_references, disable_refine, side=None):
+    def _layer_heads(self, hs, init_reference, inter_references, disable_refine, side=None, query_mask=None):
         """Class / count / box heads of every decoder layer (pdvc.py:184-192, 245-253).  side = (per-layer outputs, the
         decoder's refinement bbox_head outputs or None) from DeformableTransformerDecoder.forward: the same values
         as hs[l] and bbox_head[l](hs[l]), without the select's backward and the repeated box MLP."""
@@ -234,11 +262,11 @@ class PDVC(nn.Module):
             reference = init_reference if l_id == 0 else inter_references[l_id - 1]
             ch = self.class_head[l_id]
             classes.append(dense(hs_l, ch.weight, ch.bias))  # 1-wide head: weight gradient as a column sum
-            counts.append(self.predict_event_num(self.count_head[l_id], hs_l))
-            tmp = boxes[l_id] if (boxes is not None and not disable_refine) else self.bbox_head[l_id](hs_l)
-            if disable_refine:
+            counts.append(self.predict_event_num(self.count_head[l_id], hs_l, query_mask))
+            if disable_refine:  # the boxes are the references (pdvc.py:257-258); the box MLP's output is unused
                 coords.append(reference)
             else:
+                tmp = boxes[l_id] if boxes is not None else self.bbox_head[l_id](hs_l)
                 r = inverse_sigmoid(reference)
                 if r.shape[-1] == 2:
                     tmp = tmp + r
@@ -247,9 +275,11 @@ class PDVC(nn.Module):
                 coords.append(tmp.sigmoid())
         return classes, counts, coords
 
-    def _pack(self, classes, counts, coords, cap_probs, seqs):
+    def _pack(self, classes, counts, coords, cap_probs, seqs, query_mask=None):
         all_out = {"pred_logits": torch.stack(classes), "pred_count": torch.stack(counts),
                    "pred_boxes": torch.stack(coords), "caption_probs": cap_probs, "seq": seqs}
+        if query_mask is not None:  # 'gt_proposals': which proposal slots are real (the criterion masks the rest)
+            all_out["query_mask"] = [query_mask] * len(classes)
         out = {k: v[-1] for k, v in all_out.items()}
         if self.aux_loss:
             ks, vs = list(zip(*all_out.items()))
@@ -346,7 +376,8 @@ class PDVC(nn.Module):
         zero_probs = {"cap_prob_train": torch.zeros(1, device=hs.device),
                       "cap_prob_eval": torch.zeros(N, Q, 3, device=hs.device)}
         zero_seq = torch.zeros(N, Q, 3, device=hs.device)
-        out = self._pack(classes, counts, coords, [zero_probs] * len(classes), [zero_seq] * len(classes))
+        qmask = others["proposals_mask"] if disable_refine else None
+        out = self._pack(classes, counts, coords, [zero_probs] * len(classes), [zero_seq] * len(classes), qmask)
         if not self.aux_loss:
             raise NotImplementedError("aux_loss=False is not supported")
         loss, last_indices, aux_indices = criterion(out, dt["video_target"], dt.get("video_target_padded"))
@@ -427,7 +458,7 @@ class PDVC(nn.Module):
             else:
                 probs.append({"cap_prob_eval": lp.reshape(N, Q, -1)})
                 seqs.append(seq.reshape(N, Q, -1))
-        out = self._pack(classes, counts, coords, probs, seqs)
+        out = self._pack(classes, counts, coords, probs, seqs, others["proposals_mask"] if disable_refine else None)
         loss, last_indices, aux_indices = criterion(out, dt["video_target"], dt.get("video_target_padded"))
         return out, loss
 

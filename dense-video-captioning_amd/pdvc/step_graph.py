@@ -23,7 +23,7 @@ import torch
 
 
 class StepGraph:
-    def __init__(self, model, criterion, dt, transformer_input_type="queries", warmup=2, reducer=None):
+    def __init__(self, model, criterion, dt, transformer_input_type="queries", warmup=2, reducer=None, debug_dot=None):
         self.model, self.criterion, self.dt, self.tit = model, criterion, dt, transformer_input_type
         self.wd = criterion.weight_dict
         self.reducer = reducer
@@ -45,6 +45,8 @@ class StepGraph:
         torch.cuda.current_stream().wait_stream(side)
         model.zero_grad(set_to_none=True)
         self.graph = torch.cuda.CUDAGraph()
+        if debug_dot:  # keep the captured graph for hipGraphDebugDotPrint (tools/diag_memset_graph.py)
+            self.graph.enable_debug_mode()
         from .precision import begin_capture
         begin_capture()  # bf16 mode: every operand rounding of the step becomes a node of the graph
         if reducer is not None:
@@ -55,6 +57,8 @@ class StepGraph:
         finally:
             if reducer is not None:
                 reducer.suspended = False
+        if debug_dot:
+            self.graph.debug_dump(debug_dot)
 
     def _forward_backward(self):
         out, loss = self.model(self.dt, self.criterion, self.tit)

@@ -480,7 +480,14 @@ def synthetic_translator(vocab):
     return tr
 
 
-def whole_model_batch():
+def whole_model_batch_gt():
+    """whole_model_batch with transformer_input_type 'gt_proposals' (cfgs/*_gt.yml; pdvc/pdvc.py:138-143,
+    misc/utils.py:31-49): the ground-truth segments are the decoder's queries, the refinement is off and the
+    class / box / GIoU / length losses weigh 0 (decide_two_stage mutates the criterion)."""
+    whole_model_batch("gt_proposals", "pdvc_batch3_anet_gt")
+
+
+def whole_model_batch(tit="queries", fixture_name="pdvc_batch3_anet"):
     """Reference batch-1 training steps on three different videos (batch_items): per-video losses, matched
     indices of every decoder layer, captioning log-probabilities and heads; the MEAN of the three per-video
     gradients as full tensors (what one 3-video batch of the MI355X path must produce: every loss is the mean
@@ -522,7 +529,7 @@ def whole_model_batch():
             dt["video_mask"] = torch.cat([dt["video_mask"], dt["video_mask"].new_zeros(1, T - Tv)], 1)
         model.train()
         model.zero_grad(set_to_none=True)
-        out, loss = model(dt, criterion, "queries")
+        out, loss = model(dt, criterion, tit)
         total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
         total.backward()
         for n, p in model.named_parameters():
@@ -546,7 +553,7 @@ def whole_model_batch():
         # eval forward + PostProcess on this video
         model.eval()
         with torch.no_grad():
-            out_e, _ = model(dt, criterion, "queries", eval_mode=True)
+            out_e, _ = model(dt, criterion, tit, eval_mode=True)
             pp = post["bbox"](out_e, dt["video_length"][:, 1], loader)[0]
         res[f"v{v}.eval.pred_logits"] = out_e["pred_logits"]
         res[f"v{v}.eval.pred_boxes"] = out_e["pred_boxes"]
@@ -565,7 +572,10 @@ def whole_model_batch():
     res["param_names"] = np.asarray([n for n, _ in model.named_parameters()])
     res["args"] = np.asarray([f"{k}={v!r}" for k, v in sorted(over.items())] + [f"cfg={cfg!r}"])
     res["n_videos"] = np.asarray(nv)
-    save("pdvc_batch3_anet", **res)
+    res["transformer_input_type"] = np.asarray(tit)
+    res["weight_dict_keys"] = np.asarray(list(wd.keys()))
+    res["weight_dict_vals"] = np.asarray(list(wd.values()), np.float64)
+    save(fixture_name, **res)
 
 
 INGEST_WORDS = ["a", "man", "is", "cutting", "the", "onion", "with", "knife", "woman", "pours", "water", "into",
@@ -719,7 +729,7 @@ def posembed():
 if __name__ == "__main__":
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     which = sys.argv[1:] or ["op_reftest", "op_1d", "op_sample", "module_msdeformattn", "module_layers",
-                             "module_captioner", "whole_model", "whole_model_batch", "data_ingestion",
+                             "module_captioner", "whole_model", "whole_model_batch", "whole_model_batch_gt", "data_ingestion",
                              "state_dict_keys_full", "posembed"]
     for w in which:
         globals()[w]()
