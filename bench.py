@@ -78,6 +78,7 @@ def parse():
                    help="eval: the reference's evaluation pass instead (eval_utils.py:178 -> PDVC.forward(eval_mode="
                         "True): greedy captions of every query, then PostProcess) -- videos/s, not the headline")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-dropin", action="store_true", help="skip the drop-in operator's timing (profiling runs)")
     p.add_argument("--dist-backend", default=None, help="torch.distributed backend (default: nccl = RCCL on GPUs)")
     p.add_argument("--same-device", action="store_true",
                    help="rehearsal on a 1-GPU box: every rank on cuda:0 (use with --dist-backend gloo)")
@@ -343,6 +344,21 @@ def dropin_msda(T, videos=256, reps=10):
     return res
 
 
+def latest_profile(suffix):
+    """The newest profiles/r*_<suffix> file, or None."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_" + suffix)))
+    return files[-1] if files else None
+
+
+def pmc_bytes(kernel, workload):
+    """avg HBM bytes per launch of a kernel from the workload's PMC file (tools/pmc_traffic.py), and its path."""
+    f = latest_profile(f"{kernel}_traffic_{workload}.json")
+    if not f:
+        return None, None
+    with open(f) as fh:
+        return json.load(fh).get("avg_bytes_per_launch"), os.path.relpath(f, ROOT)
+
+
 def log(msg):
     """Progress on stderr (a long GPU run that prints nothing for minutes is taken to be hung)."""
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
@@ -533,7 +549,7 @@ def main():
     log("GEMM roofline step")
     groof = None if a.no_gemm_roofline else gemm_roofline(fwd_bwd, step, a.precision, graphed)
     dropin = None
-    if rank == 0 and not a.frontend and stream is None:
+    if rank == 0 and not a.frontend and stream is None and not a.no_dropin:
         log("drop-in operator timing")
         dropin = dropin_msda(a.T)
     videos = a.steps * B * world
@@ -568,13 +584,8 @@ def main():
         avg_ms = k["ms"] / k["launches"]
         avg_bytes = sum(msda_alg_bytes(m, "fwd") for m in k["metas"]) / k["launches"]
         ach = avg_bytes / (avg_ms * 1e-3) / 1e9
-        traffic, tsrc = None, None
-        tfiles = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_msda1d_fwd_traffic.json")))
-        tfile = tfiles[-1] if tfiles else ""
-        if tfile and os.path.exists(tfile):  # PMC pass of the same command (tools/pmc_traffic.py): HBM bytes per launch
-            with open(tfile) as f:
-                traffic = json.load(f).get("avg_bytes_per_launch")
-            tsrc = os.path.relpath(tfile, ROOT)
+        # PMC passes of the same workload (tools/r03g.sh -> tools/pmc_traffic.py): HBM bytes per launch
+        traffic, tsrc = pmc_bytes("msda1d_fwd", a.workload)
         result["roofline_gather"] = {"kernel": "msda1d_fwd_buf_kernel (fused MSDeformAttn forward)", "bound": "hbm",
                               "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                               "traffic": traffic, "traffic_source": tsrc, "avg_launch_us": avg_ms * 1e3,
@@ -586,10 +597,14 @@ def main():
         avg_ms = k["ms"] / k["launches"]
         avg_bytes = sum(msda_alg_bytes(m, "bwd") for m in k["metas"]) / k["launches"]
         ach = avg_bytes / (avg_ms * 1e-3) / 1e9
+        tq, sq = pmc_bytes("msda1d_bwd_query", a.workload)
+        tv, sv = pmc_bytes("msda1d_bwd_value", a.workload)
         result["roofline_gather_bwd"] = {
-            "kernel": "msda1d_bwd_query_dot_kernel + msda1d_bwd_value_kernel (fused MSDeformAttn backward)",
+            "kernel": "msda1d_bwd_query_{pyr,dot}_kernel + msda1d_bwd_value_kernel (fused MSDeformAttn backward)",
             "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-            "traffic": None, "avg_launch_us": avg_ms * 1e3, "timing": timing_note, "alg_bytes_per_launch": avg_bytes}
+            "traffic": (tq + tv) if (tq is not None and tv is not None) else None,
+            "traffic_source": [sq, sv] if sq else None,
+            "avg_launch_us": avg_ms * 1e3, "timing": timing_note, "alg_bytes_per_launch": avg_bytes}
     if a.frontend and ks.get("pdvc_seq_attention_forward_f32", {}).get("launches"):
         # front-end attention core (csrc/seqattn.hip): 4*T*T*E flops per video forward (scores + P.V over all
         # heads), 10*T*T*E backward (scores recomputed, dP, dQ, dK, dV), against the fp32 MFMA peak
@@ -607,6 +622,13 @@ def main():
         result["roofline_frontend_attention"] = r
     if groof is not None:  # the dominant kernels (~70% of the step's device time): `roofline` proper
         groof["share_of_step"] = groof["gemm_device_ms_per_step"] / (1e3 * el / a.steps)
+        gfile = latest_profile(f"gemm_traffic_{a.workload}.json")
+        if gfile and B == 1024:  # PMC passes of an eager step at 1024 videos (tools/r03g.sh -> tools/pmc_gemm.py)
+            with open(gfile) as f:
+                g = json.load(f)
+            groof["traffic"] = g.get("bytes_per_step")
+            groof["traffic_unit"] = "HBM bytes per step, every library GEMM launch (eager step)"
+            groof["traffic_source"] = os.path.relpath(gfile, ROOT)
         result["roofline"] = groof
     elif "roofline_gather" in result:
         result["roofline"] = result["roofline_gather"]

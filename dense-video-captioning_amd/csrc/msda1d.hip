@@ -1010,9 +1010,11 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
     const size_t sbase = save_index(b, m, l, q0, 0, Lq, M);
     int key[kVQPT][kP];
     float lwv[kVQPT][kP];
+    // a thread takes kVQPT consecutive queries: neighbouring lanes are kVQPT queries apart, so on the coarse levels
+    // (where neighbouring queries sample the same rows) fewer lanes of one atomic hit the same counter
 #pragma unroll
     for (int k = 0; k < kVQPT; ++k) {
-        const int qi = threadIdx.x + k * blockDim.x;
+        const int qi = threadIdx.x * kVQPT + k;
 #pragma unroll
         for (int p = 0; p < kP; ++p) {
             key[k][p] = -1;
@@ -1063,7 +1065,7 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
     // 3) scatter the samples into bucket order with their two corner coefficients
 #pragma unroll
     for (int k = 0; k < kVQPT; ++k) {
-        const int qi = threadIdx.x + k * blockDim.x;
+        const int qi = threadIdx.x * kVQPT + k;
         if (qi < nq) {
             const float4 at = *reinterpret_cast<const float4*>(save_attn + sbase + (size_t)qi * kP);
             const float as[kP] = {at.x, at.y, at.z, at.w};

@@ -70,7 +70,7 @@ fi
 if has prof; then
   echo "[$(date +%T)] rocprofv3 kernel stats"
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
-      -- python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline $BENCH_ARGS > "$OUT/prof_bench.json" 2> "$OUT/prof.err" \
+      -- python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-dropin $BENCH_ARGS > "$OUT/prof_bench.json" 2> "$OUT/prof.err" \
       || { echo "rocprof failed"; tail -30 "$OUT/prof.err"; exit 1; }
   ks=$(find "$OUT/prof" -name "*kernel_stats.csv" | head -1)
   if [ -n "$ks" ]; then python tools/profsum.py "$ks" 0 45 > "$OUT/prof_summary.txt"; cat "$OUT/prof_summary.txt"; fi
