@@ -45,7 +45,8 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_fwd_kernel(const float* __r
                                                                 const uint64_t* __restrict__ seed_dev, float eps,
                                                                 const float* __restrict__ r,
                                                                 float* __restrict__ y, float* __restrict__ mean_out,
-                                                                float* __restrict__ rstd_out) {
+                                                                float* __restrict__ rstd_out,
+                                                                uint16_t* __restrict__ y16) {
     const int lane = threadIdx.x & 63;
     const uint64_t seed = seed_dev ? *seed_dev : seed0;
     const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
@@ -106,6 +107,7 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_fwd_kernel(const float* __r
                     o.w += rv.w;
                 }
                 *reinterpret_cast<float4*>(y + (size_t)row * d + c) = o;
+                if (y16) store_bf16x4(y16 + (size_t)row * d + c, o.x, o.y, o.z, o.w);
             }
         }
         if (lane == 0) {
@@ -126,7 +128,8 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_bwd_kernel(const float* __r
                                                                 float* __restrict__ dx, float* __restrict__ ds,
                                                                 float* __restrict__ dgamma_part,
                                                                 float* __restrict__ dbeta_part,
-                                                                float* __restrict__ dsum_part) {
+                                                                float* __restrict__ dsum_part,
+                                                                uint16_t* __restrict__ ds16) {
     __shared__ float red[3][kANW][kAND];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t seed = seed_dev ? *seed_dev : seed0;
@@ -188,6 +191,7 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_bwd_kernel(const float* __r
                 }
                 *reinterpret_cast<float4*>(dx + (size_t)row * d + c) = make_float4(o[0], o[1], o[2], o[3]);
                 if (ds) *reinterpret_cast<float4*>(ds + (size_t)row * d + c) = make_float4(q[0], q[1], q[2], q[3]);
+                if (ds16) store_bf16x4(ds16 + (size_t)row * d + c, q[0], q[1], q[2], q[3]);
             }
         }
     }
@@ -282,13 +286,13 @@ constexpr int kAnBwdBlocks = 1024;  // 4 per CU (16 waves): enough loads in flig
 
 static int an_forward(const float* x, const float* s, const float* r, const float* gamma, const float* beta, int rows,
                       int d, float p, uint64_t seed, const uint64_t* seed_dev, float eps, float* y, float* mean,
-                      float* rstd, void* stream) {
+                      float* rstd, void* stream, uint16_t* y16 = nullptr) {
     const dim3 grid((unsigned)an_grid(rows, kAnFwdBlocks)), block(kANW * 64);
     hipStream_t st = (hipStream_t)stream;
     const uint32_t th = an_threshold(p);
 #define AN_FWD(CH) \
     hipLaunchKernelGGL(addnorm_fwd_kernel<CH>, grid, block, 0, st, x, s, gamma, beta, rows, d, p, th, seed, seed_dev, \
-                       eps, r, y, mean, rstd)
+                       eps, r, y, mean, rstd, y16)
     if (d <= 256) AN_FWD(1);
     else if (d <= 512) AN_FWD(2);
     else AN_FWD(3);
@@ -299,7 +303,8 @@ static int an_forward(const float* x, const float* s, const float* r, const floa
 
 static int an_backward(const float* x, const float* s, const float* gamma, const float* mean, const float* rstd,
                        const float* dy, int rows, int d, float p, uint64_t seed, const uint64_t* seed_dev, float* dx,
-                       float* ds, float* dgamma, float* dbeta, float* ds_colsum, float* workspace, hipStream_t st) {
+                       float* ds, float* dgamma, float* dbeta, float* ds_colsum, float* workspace, hipStream_t st,
+                       uint16_t* ds16 = nullptr) {
     const int parts = an_grid(rows, kAnBwdBlocks);
     float* gpart = workspace;
     float* bpart = workspace + (size_t)parts * d;
@@ -308,7 +313,7 @@ static int an_backward(const float* x, const float* s, const float* gamma, const
     const uint32_t th = an_threshold(p);
 #define AN_BWD(CH) \
     hipLaunchKernelGGL(addnorm_bwd_kernel<CH>, grid, block, 0, st, x, s, gamma, mean, rstd, dy, rows, d, p, th, seed, \
-                       seed_dev, dx, ds, gpart, bpart, spart)
+                       seed_dev, dx, ds, gpart, bpart, spart, ds16)
     if (d <= 256) AN_BWD(1);
     else if (d <= 512) AN_BWD(2);
     else AN_BWD(3);
@@ -356,6 +361,36 @@ extern "C" int pdvc_add_dropout_layernorm_backward_f32(const float* x, const flo
     }
     return an_backward(x, s, gamma, mean, rstd, dy, rows, d, p, seed, seed_dev, dx, ds, dgamma, dbeta, ds_colsum,
                        workspace, st);
+}
+
+// The bf16 mode's forms (pdvc/precision.py): the same passes, also writing the bf16 rounding (RNE, torch's cast)
+// of y / ds into y16 / ds16 -- the operand the next GEMM reads -- so no separate cast pass reads y / ds again.
+extern "C" int pdvc_add_dropout_layernorm_forward_f32_bf16out(const float* x, const float* s, const float* gamma,
+                                                              const float* beta, int rows, int d, float p,
+                                                              uint64_t seed, const uint64_t* seed_dev, float eps,
+                                                              float* y, float* mean, float* rstd, uint16_t* y16,
+                                                              void* stream) {
+    AN_CHECK();
+    PDVC_CHECK_ARG(y16 != nullptr && ((uintptr_t)y16 % 8) == 0, "y16 must be an 8-byte aligned bf16 buffer");
+    if (rows == 0) return PDVC_OK;
+    return an_forward(x, s, nullptr, gamma, beta, rows, d, p, seed, seed_dev, eps, y, mean, rstd, stream, y16);
+}
+
+extern "C" int pdvc_add_dropout_layernorm_backward_f32_bf16out(const float* x, const float* s, const float* gamma,
+                                                               const float* mean, const float* rstd, const float* dy,
+                                                               int rows, int d, float p, uint64_t seed,
+                                                               const uint64_t* seed_dev, float* dx, float* ds,
+                                                               float* dgamma, float* dbeta, float* ds_colsum,
+                                                               float* workspace, uint16_t* ds16, void* stream) {
+    AN_CHECK();
+    PDVC_CHECK_ARG(workspace != nullptr, "workspace (3 * 1024 * d floats) is required");
+    PDVC_CHECK_ARG(ds != nullptr && ds16 != nullptr && ((uintptr_t)ds16 % 8) == 0,
+                   "ds16 must be an 8-byte aligned bf16 buffer beside ds");
+    if (rows == 0)
+        return pdvc_add_dropout_layernorm_backward_f32(x, s, gamma, mean, rstd, dy, rows, d, p, seed, seed_dev, dx, ds,
+                                                       dgamma, dbeta, ds_colsum, workspace, stream);
+    return an_backward(x, s, gamma, mean, rstd, dy, rows, d, p, seed, seed_dev, dx, ds, dgamma, dbeta, ds_colsum,
+                       workspace, (hipStream_t)stream, ds16);
 }
 
 extern "C" int pdvc_layernorm_residual_forward_f32(const float* x, const float* r, const float* gamma,

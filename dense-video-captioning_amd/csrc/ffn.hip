@@ -26,7 +26,8 @@ __device__ __forceinline__ bool ffn_keep(uint64_t seed, uint32_t row, uint32_t c
 
 __global__ __launch_bounds__(256) void relu_dropout_fwd_kernel(float* __restrict__ h, long rows, int cols, float p,
                                                                uint32_t thresh, float scale, uint64_t seed0,
-                                                               const uint64_t* __restrict__ seed_dev) {
+                                                               const uint64_t* __restrict__ seed_dev,
+                                                               uint16_t* __restrict__ h16) {
     const uint64_t seed = seed_dev ? *seed_dev : seed0;
     const int c4 = cols / 4;
     const long n4 = rows * c4;
@@ -42,13 +43,15 @@ __global__ __launch_bounds__(256) void relu_dropout_fwd_kernel(float* __restrict
             e[k] = x;
         }
         h4[i] = make_float4(e[0], e[1], e[2], e[3]);
+        if (h16) store_bf16x4(h16 + (size_t)i * 4, e[0], e[1], e[2], e[3]);
     }
 }
 
 // grid (ceil(cols/64), parts): 16 float4 column groups x 16 row lanes over one row slab
 __global__ __launch_bounds__(256) void relu_dropout_bwd_kernel(const float* __restrict__ hd, float* __restrict__ g,
                                                                int rows, int cols, int parts, float scale,
-                                                               float* __restrict__ part) {
+                                                               float* __restrict__ part,
+                                                               uint16_t* __restrict__ g16) {
     __shared__ float4 red[16][16];
     const int cg = threadIdx.x & 15, rl = threadIdx.x >> 4;
     const int c4 = blockIdx.x * 16 + cg;
@@ -69,6 +72,7 @@ __global__ __launch_bounds__(256) void relu_dropout_bwd_kernel(const float* __re
             d.z = x.z > 0.f ? d.z * scale : 0.f;
             d.w = x.w > 0.f ? d.w * scale : 0.f;
             g4[o] = d;
+            if (g16) store_bf16x4(g16 + ((size_t)r * cs + c4) * 4, d.x, d.y, d.z, d.w);
             a.x += d.x;
             a.y += d.y;
             a.z += d.z;
@@ -134,8 +138,8 @@ static uint32_t ffn_threshold(float p) {
 
 using namespace pdvc;
 
-extern "C" int pdvc_relu_dropout_forward_f32(float* h, long rows, int cols, float p, uint64_t seed,
-                                             const uint64_t* seed_dev, void* stream) {
+static int relu_dropout_forward(float* h, long rows, int cols, float p, uint64_t seed, const uint64_t* seed_dev,
+                                uint16_t* h16, void* stream) {
     PDVC_CHECK_ARG(rows >= 0 && cols > 0 && cols % 4 == 0 && ((uintptr_t)h % 16) == 0,
                    "relu_dropout needs 16-byte aligned rows (cols %% 4 == 0)");
     PDVC_CHECK_ARG(rows <= 0xffffffffL, "too many rows");
@@ -146,13 +150,13 @@ extern "C" int pdvc_relu_dropout_forward_f32(float* h, long rows, int cols, floa
     const long want = (n4 + 255) / 256;
     const unsigned blocks = (unsigned)(want < 8192 ? want : 8192);
     hipLaunchKernelGGL(relu_dropout_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, h, rows, cols, p,
-                       ffn_threshold(p), scale, seed, seed_dev);
+                       ffn_threshold(p), scale, seed, seed_dev, h16);
     PDVC_CHECK_LAUNCH("relu_dropout_fwd_kernel");
     return PDVC_OK;
 }
 
-extern "C" int pdvc_relu_dropout_backward_f32(const float* hd, float* grad, int rows, int cols, float p, int parts,
-                                              float* workspace, float* dbias, void* stream) {
+static int relu_dropout_backward(const float* hd, float* grad, int rows, int cols, float p, int parts,
+                                 float* workspace, float* dbias, uint16_t* g16, void* stream) {
     PDVC_CHECK_ARG(rows >= 0 && cols > 0 && cols % 4 == 0 && parts >= 1, "invalid sizes");
     PDVC_CHECK_ARG(((uintptr_t)hd % 16) == 0 && ((uintptr_t)grad % 16) == 0, "16-byte aligned rows required");
     PDVC_CHECK_ARG((dbias == nullptr) == (workspace == nullptr), "dbias needs a workspace of parts*cols floats");
@@ -163,7 +167,7 @@ extern "C" int pdvc_relu_dropout_backward_f32(const float* hd, float* grad, int 
     const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
     const unsigned cb = (unsigned)((cols / 4 + 15) / 16);
     hipLaunchKernelGGL(relu_dropout_bwd_kernel, dim3(cb, (unsigned)parts), dim3(256), 0, s, hd, grad, rows, cols,
-                       parts, scale, workspace);
+                       parts, scale, workspace, g16);
     PDVC_CHECK_LAUNCH("relu_dropout_bwd_kernel");
     if (dbias) {
         hipLaunchKernelGGL(ffn_colsum_final_kernel, dim3((unsigned)((cols / 4 + 15) / 16)), dim3(256), 0, s, workspace,
@@ -171,4 +175,29 @@ extern "C" int pdvc_relu_dropout_backward_f32(const float* hd, float* grad, int 
         PDVC_CHECK_LAUNCH("ffn_colsum_final_kernel");
     }
     return PDVC_OK;
+}
+
+extern "C" int pdvc_relu_dropout_forward_f32(float* h, long rows, int cols, float p, uint64_t seed,
+                                             const uint64_t* seed_dev, void* stream) {
+    return relu_dropout_forward(h, rows, cols, p, seed, seed_dev, nullptr, stream);
+}
+
+extern "C" int pdvc_relu_dropout_backward_f32(const float* hd, float* grad, int rows, int cols, float p, int parts,
+                                              float* workspace, float* dbias, void* stream) {
+    return relu_dropout_backward(hd, grad, rows, cols, p, parts, workspace, dbias, nullptr, stream);
+}
+
+// The bf16 mode's forms (pdvc/precision.py): the same passes, also writing the bf16 rounding of the result (h / dh,
+// the next GEMM's operand) into h16 / g16.
+extern "C" int pdvc_relu_dropout_forward_f32_bf16out(float* h, long rows, int cols, float p, uint64_t seed,
+                                                     const uint64_t* seed_dev, uint16_t* h16, void* stream) {
+    PDVC_CHECK_ARG(h16 != nullptr && ((uintptr_t)h16 % 8) == 0, "h16 must be an 8-byte aligned bf16 buffer");
+    return relu_dropout_forward(h, rows, cols, p, seed, seed_dev, h16, stream);
+}
+
+extern "C" int pdvc_relu_dropout_backward_f32_bf16out(const float* hd, float* grad, int rows, int cols, float p,
+                                                      int parts, float* workspace, float* dbias, uint16_t* g16,
+                                                      void* stream) {
+    PDVC_CHECK_ARG(g16 != nullptr && ((uintptr_t)g16 % 8) == 0, "g16 must be an 8-byte aligned bf16 buffer");
+    return relu_dropout_backward(hd, grad, rows, cols, p, parts, workspace, dbias, g16, stream);
 }

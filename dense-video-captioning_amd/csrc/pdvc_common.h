@@ -179,6 +179,18 @@ __device__ __forceinline__ bool dropin_levels(const int64_t* __restrict__ shapes
     return ok && st == (int64_t)S;
 }
 
+// fp32 -> bf16 bits, round to nearest even -- the conversion of torch's Tensor.to(torch.bfloat16) (c10::BFloat16:
+// NaN -> 0x7FC0): a producing kernel that also writes the bf16 rounding of its output (the bf16 mode's GEMM operand,
+// pdvc/precision.py attach_bf16) writes exactly the bits the cast pass would have
+__device__ __forceinline__ uint32_t bf16_bits(float f) {
+    const uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0u;
+    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ void store_bf16x4(uint16_t* p, float a, float b, float c, float d) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(bf16_bits(a) | (bf16_bits(b) << 16), bf16_bits(c) | (bf16_bits(d) << 16));
+}
+
 // Attention dropout mask (mha.hip, seqattn.hip): a counter hash of (seed, video*head, query, key), regenerated in
 // the backward; keep with probability 1 - p (24-bit uniform against thresh = p * 2^24).
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {

@@ -43,6 +43,10 @@ SIGNATURES = {
     "pdvc_colsum_f32": [_vp, _i, _i, _i, _vp, _vp, _vp],
     "pdvc_relu_dropout_forward_f32": [_vp, ctypes.c_long, _i, _f, _u64, _vp, _vp],
     "pdvc_relu_dropout_backward_f32": [_vp, _vp, _i, _i, _f, _i, _vp, _vp, _vp],
+    "pdvc_add_dropout_layernorm_forward_f32_bf16out": [_vp] * 4 + [_i, _i, _f, _u64, _vp, _f] + [_vp] * 5,
+    "pdvc_add_dropout_layernorm_backward_f32_bf16out": [_vp] * 6 + [_i, _i, _f, _u64] + [_vp] * 9,
+    "pdvc_relu_dropout_forward_f32_bf16out": [_vp, ctypes.c_long, _i, _f, _u64, _vp, _vp, _vp],
+    "pdvc_relu_dropout_backward_f32_bf16out": [_vp, _vp, _i, _i, _f, _i, _vp, _vp, _vp, _vp],
     "pdvc_logprob_pick_forward_f32": [_vp, _vp, _i, _i, _vp, _vp, _vp],
     "pdvc_logprob_pick_backward_f32": [_vp, _vp, _vp, _i, _i, _vp, _vp],
     "pdvc_logprob_argmax_f32": [_vp, _i, _i, _vp, _vp, _vp],

@@ -15,7 +15,7 @@ from torch.autograd import Function
 from torch.autograd.function import once_differentiable
 
 from pdvc import _native as _n
-from .addnorm import BWD_PARTS
+from .addnorm import BWD_PARTS, an_backward, an_forward
 from .linear import colsum, wgrad_mm
 from .ms_deform_attn_func import NUM_SAMPLES, msda1d_backward, msda1d_forward
 from .posembed import LevelPos, level_row_sums
@@ -41,9 +41,7 @@ class EncoderAttnBlockFunction(Function):
         rstd = torch.empty_like(mean)
         seed_dev = seed if isinstance(seed, torch.Tensor) else None
         seed_int = 0 if seed_dev is not None else int(seed)
-        _n.call("pdvc_add_dropout_layernorm_forward_f32", _n.ptr(src2), _n.ptr(s2), _n.ptr(gamma), _n.ptr(beta), R,
-                d, float(p), seed_int, _n.ptr(seed_dev), float(eps), _n.ptr(y), _n.ptr(mean), _n.ptr(rstd),
-                _n.stream())
+        an_forward(src2, s2, gamma, beta, p, seed_int, seed_dev, eps, y, mean, rstd)
         ctx.save_for_backward(src2, q, value, proj, ref, pad_mask, save_attn, save_loc, out, s2, Wv, Wq, Wo, gamma,
                               mean, rstd, seed_dev)
         ctx.meta = (N, S, d, M, float(p), seed_int, tuple(level_T), handle is not None)
@@ -64,9 +62,7 @@ class EncoderAttnBlockFunction(Function):
         dbeta = torch.empty_like(gamma)
         dbo = torch.empty_like(gamma)
         ws = torch.empty(3 * BWD_PARTS * d, dtype=src2.dtype, device=src2.device)
-        _n.call("pdvc_add_dropout_layernorm_backward_f32", _n.ptr(src2), _n.ptr(s2), _n.ptr(gamma), _n.ptr(mean),
-                _n.ptr(rstd), _n.ptr(dy2), R, d, p, seed_int, _n.ptr(seed_dev), _n.ptr(d_src), _n.ptr(d_s2),
-                _n.ptr(dgamma), _n.ptr(dbeta), _n.ptr(dbo), _n.ptr(ws), _n.stream())
+        an_backward(src2, s2, gamma, mean, rstd, dy2, p, seed_int, seed_dev, d_src, d_s2, dgamma, dbeta, dbo, ws)
         dWo = wgrad_mm(d_s2, out.view(R, d))
         d_out = torch.mm(d_s2, Wo)
         nq = M * NUM_SAMPLES

@@ -18,7 +18,8 @@ from torch.autograd import Function
 from torch.autograd.function import once_differentiable
 
 from pdvc import _native as _n
-from .addnorm import BWD_PARTS
+from pdvc.precision import attach_bf16, shadow_for
+from .addnorm import BWD_PARTS, an_backward, an_forward
 from . import linear as _lin
 from .linear import CU, wgrad_mm
 
@@ -45,13 +46,19 @@ class FFNBlockFunction(Function):
         rows = x2.shape[0]
         seed_act, seed_out = _seed_ptrs(seeds)
         h = torch.addmm(b1, x2, w1.t())
-        _n.call("pdvc_relu_dropout_forward_f32", _n.ptr(h), rows, h.shape[1], float(p_act), 0, seed_act, _n.stream())
+        h16 = shadow_for(h)  # bf16 mode: linear2's operand written by the same pass
+        if h16 is None:
+            _n.call("pdvc_relu_dropout_forward_f32", _n.ptr(h), rows, h.shape[1], float(p_act), 0, seed_act,
+                    _n.stream())
+        else:
+            _n.call("pdvc_relu_dropout_forward_f32_bf16out", _n.ptr(h), rows, h.shape[1], float(p_act), 0, seed_act,
+                    _n.ptr(h16), _n.stream())
+            attach_bf16(h, h16)
         y = torch.addmm(b2, h, w2.t())
         out = torch.empty_like(x2)
         mean = torch.empty(rows, dtype=x.dtype, device=x.device)
         rstd = torch.empty_like(mean)
-        _n.call("pdvc_add_dropout_layernorm_forward_f32", _n.ptr(x2), _n.ptr(y), _n.ptr(gamma), _n.ptr(beta), rows,
-                d, float(p_out), 0, seed_out, float(eps), _n.ptr(out), _n.ptr(mean), _n.ptr(rstd), _n.stream())
+        an_forward(x2, y, gamma, beta, p_out, 0, seed_out, eps, out, mean, rstd)
         ctx.save_for_backward(x2, h, y, w1, w2, gamma, mean, rstd, seeds)
         ctx.meta = (shape, float(p_act), float(p_out))
         return out.view(shape)
@@ -71,16 +78,20 @@ class FFNBlockFunction(Function):
         dbeta = torch.empty_like(gamma)
         ws = torch.empty(3 * BWD_PARTS * d, dtype=x2.dtype, device=x2.device)
         db2 = torch.empty_like(gamma)  # linear2's bias gradient = column sums of dy, summed by the same pass
-        _n.call("pdvc_add_dropout_layernorm_backward_f32", _n.ptr(x2), _n.ptr(y), _n.ptr(gamma), _n.ptr(mean),
-                _n.ptr(rstd), _n.ptr(dout2), rows, d, p_out, 0, seed_out, _n.ptr(dx), _n.ptr(dy), _n.ptr(dgamma),
-                _n.ptr(dbeta), _n.ptr(db2), _n.ptr(ws), _n.stream())
+        an_backward(x2, y, gamma, mean, rstd, dout2, p_out, 0, seed_out, dx, dy, dgamma, dbeta, db2, ws)
         dw2 = wgrad_mm(dy, h)
         dh = torch.mm(dy, w2)
         parts = _parts(rows, fdim)
         ws1 = torch.empty(parts * fdim, dtype=h.dtype, device=h.device)
         db1 = torch.empty(fdim, dtype=h.dtype, device=h.device)
-        _n.call("pdvc_relu_dropout_backward_f32", _n.ptr(h), _n.ptr(dh), rows, fdim, p_act, parts, _n.ptr(ws1),
-                _n.ptr(db1), _n.stream())
+        dh16 = shadow_for(dh)  # bf16 mode: the operand of linear1's two gradient GEMMs, written by the same pass
+        if dh16 is None:
+            _n.call("pdvc_relu_dropout_backward_f32", _n.ptr(h), _n.ptr(dh), rows, fdim, p_act, parts, _n.ptr(ws1),
+                    _n.ptr(db1), _n.stream())
+        else:
+            _n.call("pdvc_relu_dropout_backward_f32_bf16out", _n.ptr(h), _n.ptr(dh), rows, fdim, p_act, parts,
+                    _n.ptr(ws1), _n.ptr(db1), _n.ptr(dh16), _n.stream())
+            attach_bf16(dh, dh16)
         dw1 = wgrad_mm(dh, x2)
         dx.addmm_(dh, w1)  # residual gradient + linear1's input gradient in one GEMM (beta = 1)
         return dx.view(shape), dw1, db1, dw2, db2, dgamma, dbeta, None, None, None, None

@@ -26,6 +26,8 @@ once, at capture.  GEMMs below MIN_FLOPS (tiny heads, 1-wide projections) stay f
 Tolerances against the fp32 path: tests/test_gpu_bf16.py and DESIGN.md.
 """
 import contextlib
+import os
+import sys
 import threading
 
 import torch
@@ -35,7 +37,9 @@ aten = torch.ops.aten
 MIN_FLOPS = 1 << 22
 # GEMMs the mode saw: (op, M, N, K) -> [calls on the bf16 path, calls kept in fp32 (below MIN_FLOPS)]
 STATS = {}
-STATS_CAST = [0, 0]  # [bf16 roundings made, reused from the cache]
+STATS_CAST = [0, 0, 0]  # [bf16 roundings made, reused from the cache, written by the producing kernel]
+# PDVC_CAST_LOG=1 (diagnosis, tools/diag_bf16_casts.py): every rounding pass made, as (shape, where it was asked for)
+CAST_LOG = [] if os.environ.get("PDVC_CAST_LOG") else None
 _F32 = torch.float32
 _BF = torch.bfloat16
 
@@ -73,9 +77,23 @@ def _bf(t):
         ent = (base._version, base.to(_BF), epoch)
         base.__dict__["_pdvc_bf16"] = ent
         STATS_CAST[0] += 1
+        if CAST_LOG is not None:
+            CAST_LOG.append((tuple(base.shape), _origin()))
     else:
         STATS_CAST[1] += 1
     return ent[1].as_strided(t.shape, t.stride(), t.storage_offset() - base.storage_offset())
+
+
+def _origin():
+    """The innermost caller outside this module and torch (file:line function), or "autograd" for a GEMM issued by
+    a built-in backward formula (no Python frame of ours on the stack)."""
+    f = sys._getframe(2)
+    while f is not None:
+        fn = f.f_code.co_filename
+        if fn != __file__ and "/torch/" not in fn:
+            return f"{os.path.basename(fn)}:{f.f_lineno} {f.f_code.co_name}"
+        f = f.f_back
+    return "autograd"
 
 
 def _f32_cuda(*ts):
@@ -171,6 +189,38 @@ def fp32_gemms():
 def routed_summary():
     """(GEMM calls on the bf16 path, calls kept fp32) over everything the mode saw."""
     return sum(v[0] for v in STATS.values()), sum(v[1] for v in STATS.values())
+
+
+def bf16_active():
+    """True inside bf16_matmul (on this thread or an autograd thread it carried the mode into): producing kernels
+    then also write the bf16 rounding of their output (attach_bf16), so the GEMM that reads it needs no cast."""
+    if getattr(_FP32, "depth", 0):
+        return False
+    from torch.utils._python_dispatch import _get_current_dispatch_mode_stack
+    return any(isinstance(m, BF16Matmul) for m in _get_current_dispatch_mode_stack())
+
+
+SHADOWS = [True]  # the producing kernels write the bf16 operands (False: every operand is a cast pass; tests)
+
+
+def shadow_for(t):
+    """A bf16 buffer of t's shape for the kernel producing t to write t's rounding into (then attach_bf16(t, it)),
+    or None outside the bf16 mode."""
+    if not (SHADOWS[0] and t.is_cuda and bf16_active()):
+        return None
+    return torch.empty(t.shape, dtype=_BF, device=t.device)
+
+
+def attach_bf16(t, t16):
+    """Register t16 (t rounded to bf16, written by the kernel that produced t) as t's cached rounding: _bf finds it
+    exactly as if it had cast t itself (same version, same capture epoch), so no cast kernel runs."""
+    if t16 is None:
+        return t
+    base = t._base if t._base is not None else t
+    if base is t and t.is_contiguous() and t16.shape == t.shape:
+        t.__dict__["_pdvc_bf16"] = (t._version, t16, _epoch())
+        STATS_CAST[2] += 1
+    return t
 
 
 def drop_cast_cache(tensors):

@@ -264,6 +264,18 @@ int pdvc_add_dropout_layernorm_backward_f32(const float* x, const float* s, cons
                                             uint64_t seed, const uint64_t* seed_dev, float* dx, float* ds,
                                             float* dgamma, float* dbeta, float* ds_colsum, float* workspace,
                                             void* stream);
+/* The bf16 mode's forms (pdvc/precision.py): the same passes, also writing y16 (forward) / ds16 (backward) =
+ * the bf16 rounding (round to nearest even, NaN -> 0x7FC0: torch's cast) of y / ds, the operand of the GEMM
+ * that reads it; y16 / ds16 rows x d uint16 (bf16 bits), 8-byte aligned. */
+int pdvc_add_dropout_layernorm_forward_f32_bf16out(const float* x, const float* s, const float* gamma,
+                                                   const float* beta, int rows, int d, float p, uint64_t seed,
+                                                   const uint64_t* seed_dev, float eps, float* y, float* mean,
+                                                   float* rstd, uint16_t* y16, void* stream);
+int pdvc_add_dropout_layernorm_backward_f32_bf16out(const float* x, const float* s, const float* gamma,
+                                                    const float* mean, const float* rstd, const float* dy, int rows,
+                                                    int d, float p, uint64_t seed, const uint64_t* seed_dev, float* dx,
+                                                    float* ds, float* dgamma, float* dbeta, float* ds_colsum,
+                                                    float* workspace, uint16_t* ds16, void* stream);
 /* NewModel's front-end epilogue (NewModel.py:41-65, `ln(h) + residual`): y = LayerNorm(x) * gamma + beta + r.
  * Same layout and limits; the backward writes dx and dgamma/dbeta (the residual's gradient is dy itself);
  * workspace 2*1024*d floats. */
@@ -355,6 +367,11 @@ int pdvc_relu_dropout_forward_f32(float* h, long rows, int cols, float p, uint64
                                   void* stream);
 int pdvc_relu_dropout_backward_f32(const float* hd, float* grad, int rows, int cols, float p, int parts,
                                    float* workspace, float* dbias, void* stream);
+/* bf16 mode: the same passes, also writing the bf16 rounding of h / grad into h16 / g16 (rows x cols uint16). */
+int pdvc_relu_dropout_forward_f32_bf16out(float* h, long rows, int cols, float p, uint64_t seed,
+                                          const uint64_t* seed_dev, uint16_t* h16, void* stream);
+int pdvc_relu_dropout_backward_f32_bf16out(const float* hd, float* grad, int rows, int cols, float p, int parts,
+                                           float* workspace, float* dbias, uint16_t* g16, void* stream);
 
 /* ---- caption word log-probabilities + target pick ----------------------------------------------------
  * Replaces log_softmax(logit(.)) (LSTM_DSA.py:112-116) and the target gather of the caption loss

@@ -266,12 +266,14 @@ def test_capacity_step_graph_follows_a_ragged_stream(fixture):
     total_b = sum(loss_b[k] * wd[k] for k in loss_b.keys() if k in wd)
     total_b.backward()
     grads_b = {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
+    total_b = total_b.item()
+    del loss_b  # the eager step's autograd graph (and its default-stream AccumulateGrad nodes) must not outlive it
     model.zero_grad(set_to_none=True)
     sg = StepGraph(model, criterion, padded_dt(items))
     assert_scalar(sg.replay(), np.mean([float(d[f"v{v}.total_loss"]) for v in range(nv)]), "replay, batch A")
     _check_grads(d, model.named_parameters(), "capacity step graph, batch A")
     sg.load(padded_dt(perm))
-    assert_scalar(sg.replay(), total_b.item(), "replay after load(batch B)")
+    assert_scalar(sg.replay(), total_b, "replay after load(batch B)")
     for n, p in model.named_parameters():
         if n in grads_b:
             close(p.grad, grads_b[n], f"capacity step graph, batch B: grad {n}")

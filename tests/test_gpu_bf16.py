@@ -255,3 +255,121 @@ def test_cfg2_bf16_step_graph_follows_loaded_batch():
         if r is not None:
             err = (got[n] - r).norm().item()
             assert err <= 1e-2 * r.norm().item() + 1e-7, f"replay after load(): grad {n} {err:.3e} vs |ref| {r.norm().item():.3e}"
+
+
+def _bits(t):
+    return t.contiguous().view(torch.int16)
+
+
+def test_bf16out_entry_points_round_like_torch():
+    """The *_bf16out forms of the add-norm and relu-dropout passes write the same fp32 results as the plain
+    forms and, beside them, bit for bit torch's bf16 cast of those results (round to nearest even, ties, NaN,
+    +-inf, overflow to inf, subnormals)."""
+    from pdvc import _native as _n
+    from pdvc.ops.functions.ffn import _parts
+    g = torch.Generator(device=DEV).manual_seed(3)
+    rows, cols = 777, 512
+    # relu-dropout forward, p = 0.1 with a device seed
+    h = torch.randn(rows, cols, device=DEV, generator=g) * 3
+    h.view(-1)[:6] = torch.tensor([1 + 2 ** -8, 1 + 3 * 2 ** -8, 3.3895e38, 1e-40, float("inf"), 2 ** -130],
+                                  device=DEV)
+    seed = torch.tensor([12345], device=DEV, dtype=torch.int64)
+    h_ref, h_got = h.clone(), h.clone()
+    h16 = torch.empty(rows, cols, device=DEV, dtype=torch.bfloat16)
+    _n.call("pdvc_relu_dropout_forward_f32", _n.ptr(h_ref), rows, cols, 0.1, 0, _n.ptr(seed), _n.stream())
+    _n.call("pdvc_relu_dropout_forward_f32_bf16out", _n.ptr(h_got), rows, cols, 0.1, 0, _n.ptr(seed), _n.ptr(h16),
+            _n.stream())
+    assert torch.equal(h_got, h_ref)
+    assert torch.equal(_bits(h16), _bits(h_ref.to(torch.bfloat16))), "relu-dropout forward bf16 rounding"
+    # relu-dropout backward with special gradient values where the forward kept the element
+    gr = torch.randn(rows, cols, device=DEV, generator=g)
+    keep = (h_ref > 0).nonzero()[:8]
+    specials = torch.tensor([float("nan"), float("inf"), -float("inf"), 1 + 2 ** -8, -(1 + 3 * 2 ** -8), 3.39e38,
+                             -1e-40, 0.0], device=DEV)
+    gr[keep[:, 0], keep[:, 1]] = specials / 0.9  # the pass scales by 1 / (1 - p)
+    parts = _parts(rows, cols)
+    out = []
+    for bf in (False, True):
+        gg = gr.clone()
+        ws = torch.empty(parts * cols, device=DEV)
+        db = torch.empty(cols, device=DEV)
+        if bf:
+            g16 = torch.empty(rows, cols, device=DEV, dtype=torch.bfloat16)
+            _n.call("pdvc_relu_dropout_backward_f32_bf16out", _n.ptr(h_ref), _n.ptr(gg), rows, cols, 0.1, parts,
+                    _n.ptr(ws), _n.ptr(db), _n.ptr(g16), _n.stream())
+        else:
+            _n.call("pdvc_relu_dropout_backward_f32", _n.ptr(h_ref), _n.ptr(gg), rows, cols, 0.1, parts, _n.ptr(ws),
+                    _n.ptr(db), _n.stream())
+        out.append((gg, db))
+    assert torch.equal(out[0][0].nan_to_num(7.0), out[1][0].nan_to_num(7.0))
+    assert torch.equal(_bits(g16), _bits(out[1][0].to(torch.bfloat16))), "relu-dropout backward bf16 rounding"
+    assert (_bits(g16) == 0x7FC0).sum() >= 1  # the NaN made it through as torch's canonical bf16 NaN
+    # add-norm forward and backward (dropout p = 0.1 on s)
+    d = 512
+    x = torch.randn(rows, d, device=DEV, generator=g)
+    s = torch.randn(rows, d, device=DEV, generator=g)
+    gam = torch.randn(d, device=DEV, generator=g)
+    bet = torch.randn(d, device=DEV, generator=g)
+    res = []
+    for bf in (False, True):
+        y = torch.empty(rows, d, device=DEV)
+        mean = torch.empty(rows, device=DEV)
+        rstd = torch.empty(rows, device=DEV)
+        a = (_n.ptr(x), _n.ptr(s), _n.ptr(gam), _n.ptr(bet), rows, d, 0.1, 0, _n.ptr(seed), 1e-5, _n.ptr(y),
+             _n.ptr(mean), _n.ptr(rstd))
+        if bf:
+            y16 = torch.empty(rows, d, device=DEV, dtype=torch.bfloat16)
+            _n.call("pdvc_add_dropout_layernorm_forward_f32_bf16out", *a, _n.ptr(y16), _n.stream())
+        else:
+            _n.call("pdvc_add_dropout_layernorm_forward_f32", *a, _n.stream())
+        res.append((y, mean, rstd))
+    for u, v in zip(*res):
+        assert torch.equal(u, v)
+    assert torch.equal(_bits(y16), _bits(res[1][0].to(torch.bfloat16))), "add-norm forward bf16 rounding"
+    y, mean, rstd = res[0]
+    dy = torch.randn(rows, d, device=DEV, generator=g)
+    grads = []
+    for bf in (False, True):
+        dx, ds = torch.empty_like(x), torch.empty_like(s)
+        dgam, dbet, dcol = (torch.empty(d, device=DEV) for _ in range(3))
+        ws = torch.empty(3 * 1024 * d, device=DEV)
+        a = (_n.ptr(x), _n.ptr(s), _n.ptr(gam), _n.ptr(mean), _n.ptr(rstd), _n.ptr(dy), rows, d, 0.1, 0, _n.ptr(seed),
+             _n.ptr(dx), _n.ptr(ds), _n.ptr(dgam), _n.ptr(dbet), _n.ptr(dcol), _n.ptr(ws))
+        if bf:
+            ds16 = torch.empty(rows, d, device=DEV, dtype=torch.bfloat16)
+            _n.call("pdvc_add_dropout_layernorm_backward_f32_bf16out", *a, _n.ptr(ds16), _n.stream())
+        else:
+            _n.call("pdvc_add_dropout_layernorm_backward_f32", *a, _n.stream())
+        grads.append((dx, ds, dgam, dbet, dcol))
+    for u, v in zip(*grads):
+        assert torch.equal(u, v)
+    assert torch.equal(_bits(ds16), _bits(grads[1][1].to(torch.bfloat16))), "add-norm backward bf16 rounding"
+
+
+def test_cfg2_bf16_step_with_producer_shadows_equals_cast_passes():
+    """The bf16 step with the producing kernels writing the bf16 operands (add-norm, relu-dropout) equals the step
+    whose every operand is a cast pass: the same bf16 bits reach the same GEMMs (the entry-point test above pins
+    the rounding bit for bit), so losses and gradients agree within 1e-3 * max|ref| per tensor -- the only
+    difference is the summation order of atomic kernels, whose last-ulp fp32 noise can flip the bf16 rounding of a
+    later GEMM operand -- and fewer cast passes ran."""
+    from parity import assert_close, assert_scalar
+    from pdvc import precision as P
+    model, criterion, dt = _cfg2_model_and_batch()
+    runs = []
+    for shadows in (False, True):
+        P.SHADOWS[0] = shadows
+        P.STATS_CAST[:] = [0, 0, 0]
+        try:
+            with P.bf16_matmul():
+                losses, grads = _step(model, criterion, dt)
+        finally:
+            P.SHADOWS[0] = True
+        runs.append((losses, grads, list(P.STATS_CAST)))
+    (l0, g0, c0), (l1, g1, c1) = runs
+    assert c0[2] == 0 and c1[2] >= 10 and c1[0] <= c0[0] - 10, (c0, c1)
+    for k in l0:
+        assert_scalar(l1[k], l0[k], f"loss {k}", tol=1e-3)
+    for n, r in g0.items():
+        assert (r is None) == (g1[n] is None), n
+        if r is not None:
+            assert_close(g1[n], r, f"grad {n} (shadows vs casts)", tol=1e-3)
