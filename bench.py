@@ -578,33 +578,51 @@ def main():
     }
     # roofline_gather: the fused MSDA forward (the north star's gather kernel; algorithmic bytes per launch / avg
     # launch time).  `roofline` is the dominant work, the GEMMs against the MFMA peak of the precision in use
-    kname = "pdvc_msda1d_forward_f32"
-    if kname in ks and ks[kname]["launches"]:
-        k = ks[kname]
-        avg_ms = k["ms"] / k["launches"]
-        avg_bytes = sum(msda_alg_bytes(m, "fwd") for m in k["metas"]) / k["launches"]
-        ach = avg_bytes / (avg_ms * 1e-3) / 1e9
+    def msda_split(kname, kind):
+        """(encoder, decoder) launch groups of one MSDA entry point: (launches, avg us, avg algorithmic bytes);
+        an encoder launch has Lq == S (self-attention over the pyramid), a decoder launch Lq = Q queries."""
+        k = ks.get(kname)
+        if not k or not k["launches"] or len(k.get("launch_ms", [])) != len(k["metas"]):
+            return None, None
+        out = []
+        for enc in (True, False):
+            sel = [(ms, m) for ms, m in zip(k["launch_ms"], k["metas"]) if (m[1] == m[2]) == enc]
+            if not sel:
+                out.append(None)
+                continue
+            ms = sum(x for x, _ in sel) / len(sel)
+            by = sum(msda_alg_bytes(m, kind) for _, m in sel) / len(sel)
+            out.append({"launches": len(sel), "avg_launch_us": ms * 1e3, "alg_bytes_per_launch": by,
+                        "achieved": by / (ms * 1e-3) / 1e9, "frac": by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS})
+        return out[0], out[1]
+
+    # roofline_gather: the fused MSDA forward of the encoder's self-attention (the north star's gather kernel, the
+    # pyramid kernel): algorithmic bytes per launch / avg launch time; the decoder's launches (Q = 100 queries,
+    # msda1d_fwd_buf_kernel) beside it.  `roofline` is the dominant work, the GEMMs against the MFMA peak
+    enc, dec = msda_split("pdvc_msda1d_forward_f32", "fwd")
+    if enc is not None:
         # PMC passes of the same workload (tools/r03g.sh -> tools/pmc_traffic.py): HBM bytes per launch
-        traffic, tsrc = pmc_bytes("msda1d_fwd", a.workload)
-        result["roofline_gather"] = {"kernel": "msda1d_fwd_buf_kernel (fused MSDeformAttn forward)", "bound": "hbm",
-                              "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                              "traffic": traffic, "traffic_source": tsrc, "avg_launch_us": avg_ms * 1e3,
-                              "timing": timing_note,
-                              "alg_bytes_per_launch": avg_bytes}
-    kname = "pdvc_msda1d_backward_ex_f32"  # the same for the backward (query-side + value-side kernels per launch)
-    if kname in ks and ks[kname]["launches"]:
-        k = ks[kname]
-        avg_ms = k["ms"] / k["launches"]
-        avg_bytes = sum(msda_alg_bytes(m, "bwd") for m in k["metas"]) / k["launches"]
-        ach = avg_bytes / (avg_ms * 1e-3) / 1e9
-        tq, sq = pmc_bytes("msda1d_bwd_query", a.workload)
-        tv, sv = pmc_bytes("msda1d_bwd_value", a.workload)
-        result["roofline_gather_bwd"] = {
-            "kernel": "msda1d_bwd_query_{pyr,dot}_kernel + msda1d_bwd_value_kernel (fused MSDeformAttn backward)",
-            "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-            "traffic": (tq + tv) if (tq is not None and tv is not None) else None,
-            "traffic_source": [sq, sv] if sq else None,
-            "avg_launch_us": avg_ms * 1e3, "timing": timing_note, "alg_bytes_per_launch": avg_bytes}
+        traffic, tsrc = pmc_bytes("msda1d_fwd_pyr", a.workload)
+        result["roofline_gather"] = dict(
+            {"kernel": "msda1d_fwd_pyr_kernel (fused MSDeformAttn forward, encoder self-attention, Lq = S)",
+             "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": traffic, "traffic_source": tsrc,
+             "timing": timing_note}, **enc)
+        if dec is not None:
+            dt_, ds_ = pmc_bytes("msda1d_fwd_buf", a.workload)
+            result["roofline_gather"]["decoder"] = dict({"kernel": "msda1d_fwd_buf_kernel (decoder cross-attention, "
+                                                         "Lq = Q)", "traffic": dt_, "traffic_source": ds_}, **dec)
+    enc, dec = msda_split("pdvc_msda1d_backward_ex_f32", "bwd")  # query-side + value-side kernels per launch
+    if enc is not None:
+        tq, sq = pmc_bytes("msda1d_bwd_query_pyr", a.workload)
+        tv, sv = pmc_bytes("msda1d_bwd_value_enc", a.workload)
+        result["roofline_gather_bwd"] = dict(
+            {"kernel": "msda1d_bwd_query_pyr_kernel + msda1d_bwd_value_kernel (fused MSDeformAttn backward, encoder "
+                       "self-attention)", "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "traffic": (tq + tv) if (tq is not None and tv is not None) else None,
+             "traffic_source": [sq, sv] if sq else None, "timing": timing_note}, **enc)
+        if dec is not None:
+            result["roofline_gather_bwd"]["decoder"] = dict(
+                {"kernel": "msda1d_bwd_query_dot_kernel + msda1d_bwd_value_kernel (decoder cross-attention)"}, **dec)
     if a.frontend and ks.get("pdvc_seq_attention_forward_f32", {}).get("launches"):
         # front-end attention core (csrc/seqattn.hip): 4*T*T*E flops per video forward (scores + P.V over all
         # heads), 10*T*T*E backward (scores recomputed, dP, dQ, dK, dV), against the fp32 MFMA peak

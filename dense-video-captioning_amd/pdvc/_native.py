@@ -110,10 +110,12 @@ class KernelTimer:
         torch.cuda.synchronize()
         out = {}
         for name, e0, e1, meta in self.records:
-            d = out.setdefault(name, {"launches": 0, "ms": 0.0, "metas": []})
+            d = out.setdefault(name, {"launches": 0, "ms": 0.0, "metas": [], "launch_ms": []})
+            ms = e0.elapsed_time(e1)
             d["launches"] += 1
-            d["ms"] += e0.elapsed_time(e1)
+            d["ms"] += ms
             d["metas"].append(meta)
+            d["launch_ms"].append(ms)
         return out
 
 

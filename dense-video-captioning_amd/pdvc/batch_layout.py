@@ -130,6 +130,8 @@ def refresh_caption_layout(cached, lay):
         dst = cached[k]
         if tuple(src.shape) != tuple(dst.shape):
             raise ValueError(f"caption layout {k}: {tuple(src.shape)} vs captured {tuple(dst.shape)}")
-        dst.copy_(src.to(dst.dtype), non_blocking=False)
+        # pinned and asynchronous: queued behind the previous replay, which still reads dst (the caching host
+        # allocator keeps the pinned block until the copy has run)
+        dst.copy_(src.to(dst.dtype).pin_memory(), non_blocking=True)
     cached["real_rows"] = lay["real_rows"]
     cached["rows_host"] = list(zip(lay["lay"].tolist(), lay["vid"].tolist()))

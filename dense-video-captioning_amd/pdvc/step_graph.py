@@ -18,6 +18,11 @@ Dropout stays random per replay (torch's graph-safe Philox offsets; the HIP kern
 device).  Gradients live in the graph's memory pool: do not set them to None between replays (the optimizer
 step and grad clipping run eagerly on them).  A GradAllReducer (data parallel) is suspended while capturing;
 call its finish() after each replay to average the gradients over ranks.
+
+Release the autograd graphs of earlier eager steps (their loss tensors) before constructing a StepGraph: they keep
+the parameters' AccumulateGrad nodes alive, created on the stream of that eager step, and a capture whose
+gradient accumulation then joins the default stream ended in a crash at capture end on ROCm 7
+(tests/test_gpu_batch.py test_capacity_step_graph_follows_a_ragged_stream, tools/diag_capacity_capture.py).
 """
 import torch
 
@@ -86,7 +91,10 @@ class StepGraph:
 
     def load(self, dt):
         """Copy a batch of the captured shapes (same event and caption counts) into the graph's inputs: the
-        features, masks, token rows and the padded targets the device matching reads."""
+        features, masks, token rows and the padded targets the device matching reads.  Every copy is queued on
+        the current stream behind the previous replay (device-to-device, or from pinned host memory), and the
+        host facts come from the batch's host copies (data.to_device keeps them), so load() never waits for the
+        GPU: the host prepares batch k + 1 while replay k runs."""
         if bool(dt.get("video_mask_all_valid", False)) != bool(self.dt.get("video_mask_all_valid", False)):
             raise ValueError("StepGraph.load: the batch's padding (video_mask_all_valid) differs from the captured "
                              "batch's; capture a graph for it")
@@ -96,8 +104,10 @@ class StepGraph:
                 raise ValueError("StepGraph.load: the batch's event / caption-step counts differ from the captured "
                                  "batch's; capture a graph for it")
             from .matcher import padded_targets
-            new = padded_targets(dt["video_target"], self.dt["video_tensor"].device,
-                                 (dt.get("capacity") or {}).get("events"))
+            cap_events = (dt.get("capacity") or {}).get("events")
+            new = dt.get("video_target_padded")  # made by data.to_device from the host copies of the targets
+            if new is None or new.get("capacity") != cap_events:  # (from device targets: one sync per video)
+                new = padded_targets(dt["video_target"], self.dt["video_tensor"].device, cap_events)
             old = self.dt["video_target_padded"]
             for k, v in new.items():
                 if isinstance(v, torch.Tensor):
@@ -107,7 +117,8 @@ class StepGraph:
                     for kk, v in rep.items():
                         if isinstance(v, torch.Tensor):
                             v.copy_(new[kk].repeat(k[1], *([1] * (v.dim() - 1))), non_blocking=True)
-            self.dt["cap_tensor_cpu"] = dt.get("cap_tensor_cpu", dt["cap_tensor"].detach().cpu())
+            cpu = dt.get("cap_tensor_cpu")
+            self.dt["cap_tensor_cpu"] = dt["cap_tensor"].detach().cpu() if cpu is None else cpu
             if dt.get("capacity") is not None:  # the caption rows' bookkeeping of the new counts
                 from .batch_layout import caption_layout, refresh_caption_layout
                 counts = [len(t["labels"]) for t in dt["video_target"]]

@@ -262,12 +262,12 @@ def test_capacity_step_graph_follows_a_ragged_stream(fixture):
     # eager reference on the permuted batch, unpadded
     wd = criterion.weight_dict
     model.zero_grad(set_to_none=True)
-    _, loss_b = model(to_device(collate(perm), DEV), criterion, "queries")
+    out_b, loss_b = model(to_device(collate(perm), DEV), criterion, "queries")
     total_b = sum(loss_b[k] * wd[k] for k in loss_b.keys() if k in wd)
     total_b.backward()
     grads_b = {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
     total_b = total_b.item()
-    del loss_b  # the eager step's autograd graph (and its default-stream AccumulateGrad nodes) must not outlive it
+    del out_b, loss_b  # the eager step's autograd graph (its default-stream AccumulateGrad nodes) must not outlive it
     model.zero_grad(set_to_none=True)
     sg = StepGraph(model, criterion, padded_dt(items))
     assert_scalar(sg.replay(), np.mean([float(d[f"v{v}.total_loss"]) for v in range(nv)]), "replay, batch A")

@@ -348,15 +348,15 @@ def test_bf16out_entry_points_round_like_torch():
 
 def test_cfg2_bf16_step_with_producer_shadows_equals_cast_passes():
     """The bf16 step with the producing kernels writing the bf16 operands (add-norm, relu-dropout) equals the step
-    whose every operand is a cast pass: the same bf16 bits reach the same GEMMs (the entry-point test above pins
-    the rounding bit for bit), so losses and gradients agree within 1e-3 * max|ref| per tensor -- the only
-    difference is the summation order of atomic kernels, whose last-ulp fp32 noise can flip the bf16 rounding of a
-    later GEMM operand -- and fewer cast passes ran."""
-    from parity import assert_close, assert_scalar
+    whose every operand is a cast pass as closely as two runs of the cast-pass step equal each other: the same
+    bf16 bits reach the same GEMMs (the entry-point test above pins the rounding bit for bit); what differs run to
+    run is the summation order of atomic kernels, whose last-ulp fp32 noise can flip the bf16 rounding of a later
+    GEMM operand.  Per tensor, max|shadows - casts| <= 4 * (the largest run-to-run difference of any tensor,
+    relative to its max|ref|) * max|ref| + 1e-6 * max|ref|; fewer cast passes ran."""
     from pdvc import precision as P
     model, criterion, dt = _cfg2_model_and_batch()
     runs = []
-    for shadows in (False, True):
+    for shadows in (False, False, True):
         P.SHADOWS[0] = shadows
         P.STATS_CAST[:] = [0, 0, 0]
         try:
@@ -365,11 +365,17 @@ def test_cfg2_bf16_step_with_producer_shadows_equals_cast_passes():
         finally:
             P.SHADOWS[0] = True
         runs.append((losses, grads, list(P.STATS_CAST)))
-    (l0, g0, c0), (l1, g1, c1) = runs
+    (l0, g0, c0), (la, ga, _), (l1, g1, c1) = runs
     assert c0[2] == 0 and c1[2] >= 10 and c1[0] <= c0[0] - 10, (c0, c1)
+
+    def rel(a, b):
+        return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
+    noise = max([rel(ga[n], r) for n, r in g0.items() if r is not None]
+                + [abs(la[k] - l0[k]) / max(abs(l0[k]), 1e-30) for k in l0])
+    bound = 4 * noise + 1e-6
     for k in l0:
-        assert_scalar(l1[k], l0[k], f"loss {k}", tol=1e-3)
+        assert abs(l1[k] - l0[k]) <= bound * max(abs(l0[k]), 1e-30), f"loss {k}: {l1[k]} vs {l0[k]} (noise {noise:.2e})"
     for n, r in g0.items():
         assert (r is None) == (g1[n] is None), n
         if r is not None:
-            assert_close(g1[n], r, f"grad {n} (shadows vs casts)", tol=1e-3)
+            assert rel(g1[n], r) <= bound, f"grad {n}: {rel(g1[n], r):.2e} relative, run-to-run noise {noise:.2e}"

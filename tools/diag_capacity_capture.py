@@ -1,7 +1,7 @@
 """Diagnosis: capture the StepGraph of a capacity-padded batch (pdvc/batch_layout.py) in isolation, with torch's
 sync debug mode on (every synchronising call during warm-up or capture is reported with its stack), then replay.
 
-    python tools/diag_capacity_capture.py [--eager-first [--release]]
+    python tools/diag_capacity_capture.py [--eager-first [--release]] [--no-sync-debug]
 
 --eager-first runs an eager unpadded step on the default stream before the capture and keeps its loss tensors
 (hence its autograd graph, whose AccumulateGrad nodes were created on the default stream) alive; --release drops
@@ -26,6 +26,12 @@ from pdvc.step_graph import StepGraph  # noqa: E402
 
 
 def main():
+    import ctypes
+    import faulthandler
+    faulthandler.enable(all_threads=True)
+    lib = os.path.join(ROOT, "tools", "native", "libsegv_trace.so")
+    if os.path.exists(lib):  # native backtrace on SIGSEGV, chained to faulthandler's Python stacks
+        ctypes.CDLL(lib).segv_trace_install()
     d = TM.load("pdvc_batch3_anet")
     model, criterion = TM.build_filled(d)
     model.train()
@@ -34,14 +40,19 @@ def main():
     dt = to_device(pad_to_capacity(collate(items), **caps), "cuda")
     if "--eager-first" in sys.argv:
         wd = criterion.weight_dict
-        _, loss = model(to_device(collate([items[2], items[0], items[1]]), "cuda"), criterion, "queries")
-        sum(loss[k] * wd[k] for k in loss.keys() if k in wd).backward()
+        out, loss = model(to_device(collate([items[2], items[0], items[1]]), "cuda"), criterion, "queries")
+        total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
+        total.backward()
+        grads = {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
+        total = total.item()
         torch.cuda.synchronize()
+        print("eager total", total, len(grads), "grads", flush=True)
         if "--release" in sys.argv:
-            del loss
+            del out, loss
         model.zero_grad(set_to_none=True)
         print("eager unpadded step done", flush=True)
-    torch.cuda.set_sync_debug_mode("warn")
+    if "--no-sync-debug" not in sys.argv:
+        torch.cuda.set_sync_debug_mode("warn")
     warnings.simplefilter("always")
     orig = warnings.showwarning
 

@@ -45,9 +45,10 @@ def main():
     model.train()
     wd = criterion.weight_dict
     mk = lambda: D.to_device(D.collate(D.W.batch_items(vocab=29)[1:2]), "cuda")
-    _, loss = model(mk(), criterion, "queries")
+    out, loss = model(mk(), criterion, "queries")
     sum(loss[k] * wd[k] for k in loss.keys() if k in wd).backward()
     torch.cuda.synchronize()
+    del out, loss  # a live eager graph keeps default-stream AccumulateGrad nodes: capture then crashes (step_graph.py)
     eager = {k: v.clone() for k, v in D.BUFS.items()}
     model.zero_grad(set_to_none=True)
     D.BUFS.clear()

@@ -1,10 +1,11 @@
 """HBM traffic per launch of one kernel from two rocprofv3 --pmc passes (MI355X_MICROARCH.md section HBM):
     rocprofv3 --pmc FETCH_SIZE --kernel-include-regex K --output-format csv -d DIR/fetch -- python bench.py ...
     rocprofv3 --pmc WRITE_SIZE --kernel-include-regex K --output-format csv -d DIR/write -- python bench.py ...
-    python tools/pmc_traffic.py DIR KERNEL_SUBSTRING OUT.json
+    python tools/pmc_traffic.py DIR KERNEL_SUBSTRING OUT.json [--largest-grid]
 FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide (16 B/lane)
 stream, so traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 -- the kernels priced here read their value rows
-with 16-B loads.  Launches are grouped by grid size (encoder vs decoder calls) and averaged."""
+with 16-B loads.  Launches are grouped by grid size (encoder vs decoder calls) and averaged; --largest-grid prices
+only the group of the largest grid (the encoder's launches of a kernel both call sites use)."""
 import collections
 import csv
 import glob
@@ -45,6 +46,10 @@ def main():
         total += b * len(v["fetch_kib"])
         n += len(v["fetch_kib"])
     res["avg_bytes_per_launch"] = total / max(n, 1)
+    if "--largest-grid" in sys.argv and res["by_grid"]:
+        g = max(res["by_grid"], key=lambda k: int(k) if str(k).isdigit() else -1)
+        res["avg_bytes_per_launch"] = res["by_grid"][g]["bytes"]
+        res["priced_grid"] = g
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
