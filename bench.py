@@ -512,7 +512,10 @@ def main():
         step()
     log("timed steps")
     names = ["pdvc_msda1d_forward_f32", "pdvc_msda1d_backward_ex_f32", "pdvc_cap_gather_forward_f32",
-             "pdvc_cap_gather_backward_f32", "pdvc_seq_attention_forward_f32", "pdvc_seq_attention_backward_f32"]
+             "pdvc_cap_gather_backward_f32", "pdvc_cap_gather_backward2_f32", "pdvc_seq_attention_forward_f32",
+             "pdvc_seq_attention_backward_f32",
+             # the bf16 mode's forms of the encoder's MSDA launches (also writing the bf16 GEMM operands)
+             "pdvc_msda1d_forward_f32_bf16out", "pdvc_msda1d_backward_ex_f32_bf16out"]
     graphed = a.graph != "none"
     timer = _native.KernelTimer(names)
     if world > 1:
@@ -546,6 +549,14 @@ def main():
         if stream is not None:
             timing_note += " (eager steps on the capacity-padded batches)"
     ks = timer.summary()
+    for base in ("pdvc_msda1d_forward_f32", "pdvc_msda1d_backward_ex_f32"):  # one entry per MSDA pass, either form
+        extra = ks.pop(base + "_bf16out", None)
+        if extra:
+            d = ks.setdefault(base, {"launches": 0, "ms": 0.0, "metas": [], "launch_ms": []})
+            for k in ("launches", "ms"):
+                d[k] += extra[k]
+            d["metas"] += extra["metas"]
+            d["launch_ms"] += extra["launch_ms"]
     log("GEMM roofline step")
     groof = None if a.no_gemm_roofline else gemm_roofline(fwd_bwd, step, a.precision, graphed)
     dropin = None

@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
     const float* __restrict__ ref, int rd1_rows, CapLevels lv, int S, int M, int D, int waves_per_row,
     int total_waves, const float* __restrict__ save_loc,
     const float* __restrict__ gsamp, float* __restrict__ grad_value, float* __restrict__ grad_off,
-    float* __restrict__ grad_ref) {
+    float* __restrict__ grad_ref, const float* __restrict__ value2, const float* __restrict__ gsamp2) {
     constexpr int HPW = 64 / LPH;
     const int lane = threadIdx.x & 63;
     const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -186,6 +186,24 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
             s += gv * ((ok1[u] ? v1[u][c] : 0.f) - (ok0[u] ? v0[u][c] : 0.f));  // gix = -vnw + vne
         }
         part[u] = s;
+    }
+    if (value2) {  // a second sampled tensor at the same locations (no padding mask): its location gradient adds in
+        const float* v2base = value2 + (size_t)b * S * MD + (size_t)m * D + c0;
+#pragma unroll
+        for (int u = 0; u < kSPW; ++u) {
+            const int a1 = min(x0[u] + 1, T - 1);
+            const float* gp = gsamp2 + (((size_t)r * M + m) * cNS + j0 + u) * D + c0;
+            const float* p0 = v2base + (size_t)(st + x0[u]) * MD;
+            const float* p1 = v2base + (size_t)(st + a1) * MD;
+            const bool hi = x0[u] + 1 < T;
+            float s2 = 0.f;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const float gv = active ? gp[LPH * c] : 0.f;
+                s2 += gv * ((hi ? p1[LPH * c] : 0.f) - p0[LPH * c]);
+            }
+            part[u] += s2;
+        }
     }
     // sum over the LPH lanes of the head (all lanes end with the head's totals)
 #pragma unroll
@@ -478,14 +496,14 @@ extern "C" int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* va
     return PDVC_OK;
 }
 
-extern "C" int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* value_pad_mask,
-                                            const int32_t* row_video, const float* offsets, int off_stride,
-                                            int off_col0, const float* off_add, const float* ref, int ref_dim,
-                                            int rd1_rows,
-                                            const int32_t* level_T,
-                                            int num_levels, int batch, int rows, int num_heads, int head_dim,
-                                            int num_point, const float* save_loc, const float* grad_samples,
-                                            float* grad_value, float* grad_offsets, float* grad_ref, void* stream) {
+extern "C" int pdvc_cap_gather_backward2_f32(const float* value, const uint8_t* value_pad_mask,
+                                             const int32_t* row_video, const float* offsets, int off_stride,
+                                             int off_col0, const float* off_add, const float* ref, int ref_dim,
+                                             int rd1_rows, const int32_t* level_T, int num_levels, int batch, int rows,
+                                             int num_heads, int head_dim, int num_point, const float* save_loc,
+                                             const float* grad_samples, float* grad_value, float* grad_offsets,
+                                             float* grad_ref, const float* value2, const float* grad_samples2,
+                                             void* stream) {
     CapLevels lv;
     int S, lph, wpr;
     int rc = cap_setup(level_T, num_levels, num_point, head_dim, num_heads, ref_dim, lv, S, lph, wpr);
@@ -499,14 +517,28 @@ extern "C" int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* v
     if (ref_dim == 1) {
         CAP_DISPATCH(cap_gather_bwd_kernel, 1, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
                      off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples,
-                     grad_value, grad_offsets, grad_ref)
+                     grad_value, grad_offsets, grad_ref, value2, grad_samples2)
     } else {
         CAP_DISPATCH(cap_gather_bwd_kernel, 2, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
                      off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples,
-                     grad_value, grad_offsets, grad_ref)
+                     grad_value, grad_offsets, grad_ref, value2, grad_samples2)
     }
     PDVC_CHECK_LAUNCH("cap_gather_bwd_kernel");
     return PDVC_OK;
+}
+
+extern "C" int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* value_pad_mask,
+                                            const int32_t* row_video, const float* offsets, int off_stride,
+                                            int off_col0, const float* off_add, const float* ref, int ref_dim,
+                                            int rd1_rows,
+                                            const int32_t* level_T,
+                                            int num_levels, int batch, int rows, int num_heads, int head_dim,
+                                            int num_point, const float* save_loc, const float* grad_samples,
+                                            float* grad_value, float* grad_offsets, float* grad_ref, void* stream) {
+    return pdvc_cap_gather_backward2_f32(value, value_pad_mask, row_video, offsets, off_stride, off_col0, off_add, ref,
+                                         ref_dim, rd1_rows, level_T, num_levels, batch, rows, num_heads, head_dim,
+                                         num_point, save_loc, grad_samples, grad_value, grad_offsets, grad_ref, nullptr,
+                                         nullptr, stream);
 }
 
 extern "C" int pdvc_cap_value_grad_ex_f32(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels,

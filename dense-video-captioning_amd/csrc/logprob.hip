@@ -190,7 +190,8 @@ __global__ __launch_bounds__(kLpThreads) void logprob_pick_fwd_reg_kernel(const 
 __global__ __launch_bounds__(kLpThreads) void logprob_pick_bwd_reg_kernel(const float* __restrict__ logp,
                                                                          const int64_t* __restrict__ target,
                                                                          const float* __restrict__ gpick, int V,
-                                                                         float* __restrict__ dx) {
+                                                                         float* __restrict__ dx,
+                                                                         uint16_t* __restrict__ dx16) {
     const long row = blockIdx.x;
     const int v4 = V / 4;
     const float g = gpick[row];
@@ -208,9 +209,12 @@ __global__ __launch_bounds__(kLpThreads) void logprob_pick_bwd_reg_kernel(const 
         const int i = threadIdx.x + k * kLpThreads;
         if (i < v4) {
             const int j = 4 * i;
-            d4[i] = make_float4(g * ((j == t ? 1.f : 0.f) - expf(r[k].x)), g * ((j + 1 == t ? 1.f : 0.f) - expf(r[k].y)),
-                                g * ((j + 2 == t ? 1.f : 0.f) - expf(r[k].z)),
-                                g * ((j + 3 == t ? 1.f : 0.f) - expf(r[k].w)));
+            const float4 o = make_float4(g * ((j == t ? 1.f : 0.f) - expf(r[k].x)),
+                                         g * ((j + 1 == t ? 1.f : 0.f) - expf(r[k].y)),
+                                         g * ((j + 2 == t ? 1.f : 0.f) - expf(r[k].z)),
+                                         g * ((j + 3 == t ? 1.f : 0.f) - expf(r[k].w)));
+            d4[i] = o;
+            if (dx16) store_bf16x4(dx16 + row * (long)V + j, o.x, o.y, o.z, o.w);
         }
     }
 }
@@ -306,7 +310,7 @@ extern "C" int pdvc_logprob_pick_backward_f32(const float* logp, const int64_t* 
     hipStream_t s = (hipStream_t)stream;
     if (vec4 && V / 4 <= kLpThreads * kLpKR)
         hipLaunchKernelGGL(logprob_pick_bwd_reg_kernel, dim3((unsigned)rows), dim3(kLpThreads), 0, s, logp, target,
-                           grad_picked, V, grad_logits);
+                           grad_picked, V, grad_logits, (uint16_t*)nullptr);
     else if (vec4)
         hipLaunchKernelGGL(logprob_pick_bwd_kernel<true>, dim3((unsigned)rows), dim3(kLpThreads), 0, s, logp,
                            target, grad_picked, V, grad_logits);
@@ -314,5 +318,23 @@ extern "C" int pdvc_logprob_pick_backward_f32(const float* logp, const int64_t* 
         hipLaunchKernelGGL(logprob_pick_bwd_kernel<false>, dim3((unsigned)rows), dim3(kLpThreads), 0, s, logp,
                            target, grad_picked, V, grad_logits);
     PDVC_CHECK_LAUNCH("logprob_pick_bwd_kernel");
+    return PDVC_OK;
+}
+
+// The bf16 mode's form (pdvc/precision.py): also writes grad_logits' bf16 rounding into grad16 -- the operand of
+// the logit layer's two gradient GEMMs.  Only the register-resident form (V % 4 == 0, V / 4 <= 2048 float4s per
+// row, 16-byte aligned rows): otherwise PDVC_ERR_UNSUPPORTED and nothing is launched (the caller casts instead).
+extern "C" int pdvc_logprob_pick_backward_f32_bf16out(const float* logp, const int64_t* target,
+                                                      const float* grad_picked, int rows, int V, float* grad_logits,
+                                                      uint16_t* grad16, void* stream) {
+    PDVC_CHECK_ARG(rows >= 0 && V > 0, "invalid sizes (rows >= 0, V > 0)");
+    PDVC_CHECK_ARG(rows == 0 || (logp && target && grad_picked && grad_logits && grad16), "null pointer");
+    const bool reg = (V % 4) == 0 && ((uintptr_t)logp % 16) == 0 && ((uintptr_t)grad_logits % 16) == 0 &&
+                     ((uintptr_t)grad16 % 8) == 0 && V / 4 <= kLpThreads * kLpKR;
+    if (!reg) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "bf16 shadow needs the register-resident row form");
+    if (rows == 0) return PDVC_OK;
+    hipLaunchKernelGGL(logprob_pick_bwd_reg_kernel, dim3((unsigned)rows), dim3(kLpThreads), 0, (hipStream_t)stream,
+                       logp, target, grad_picked, V, grad_logits, grad16);
+    PDVC_CHECK_LAUNCH("logprob_pick_bwd_reg_kernel");
     return PDVC_OK;
 }

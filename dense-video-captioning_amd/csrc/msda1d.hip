@@ -482,6 +482,216 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr_kernel(
 }
 
 // -------------------------------------------------------------------------------------------------
+// msda1d_fwd_pyr2_kernel: msda1d_fwd_pyr_kernel's arithmetic (same bits) with the staging moved onto LDS-DMA
+// (global_load_lds_dwordx4: HBM -> LDS with no VGPR round trip, 1 KiB = 4 rows per wave-instruction) and laid out
+// in the whole 160 KiB so that it overlaps compute:
+//   * the parameter loads are waited for first, then the first phase's rows are issued as DMAs and the parameter
+//     math (softmax, locations, corner weights) runs while they land;
+//   * a pyramid of S + 2 <= 640 rows (T <= 318: yc2's T = 256, S = 480) is staged whole, one phase, one barrier;
+//   * otherwise (anet's T = 512, S = 960) level 0 takes rows [0, T0 + 2) and levels 1..3 are placed at the END of
+//     the LDS (rows [640 - 1 - n1, 640)), so the part of them above level 0's rows is prefetched during level 0's
+//     gather and only the rest is staged between the two gathers.
+// Guarded layout as in msda1d_fwd_pyr_kernel: a zero row before level 0 and after the last staged level, levels
+// 1..3 back to back (a corner outside its level reads a neighbour's finite row with weight 0).
+// -------------------------------------------------------------------------------------------------
+constexpr int kLdsRows = 640;                                     // 160 KiB of 256-B rows
+constexpr size_t kPyr2LdsMax = (size_t)kLdsRows * 256;
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+// LDS-DMA copy of n head rows (256 B: the head's 64 channels) from global rows [g0, g0 + n) of vsrc to LDS rows
+// [r0, r0 + n): chunk c (4 rows, one wave-instruction) goes to wave c % 16; lanes past the end are masked off
+__device__ __forceinline__ void pyr_dma_rows(float4* __restrict__ lds, const float* __restrict__ vsrc, size_t MD,
+                                             int g0, int r0, int n) {
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    const int nch = (n + 3) >> 2;
+    for (int c = wave; c < nch; c += kPyrThreads / 64) {
+        const int row = c * 4 + (lane >> 4);
+        char* dst = reinterpret_cast<char*>(lds) + (size_t)(r0 + c * 4) * 256;
+        if (row < n)
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)(vsrc + (size_t)(g0 + row) * MD + (lane & 15) * 4),
+                                             (lds_void_t*)dst, 16, 0, 0);
+    }
+}
+
+// the same copy issued by inline assembly: the compiler does not see these LDS writes, so it does not order the
+// LDS reads that follow after them (it waits vmcnt(0) before the first ds_read after a builtin DMA, which would
+// serialise a prefetch with the gather it is meant to hide under).  The caller keeps the reads off these rows
+// and retires the DMAs itself (pyr_dma_wait, then a barrier) before the rows are read.
+__device__ __forceinline__ void pyr_dma_rows_async(float4* __restrict__ lds, const float* __restrict__ vsrc,
+                                                   size_t MD, int g0, int r0, int n) {
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    const int nch = (n + 3) >> 2;
+    for (int c = wave; c < nch; c += kPyrThreads / 64) {
+        const int row = c * 4 + (lane >> 4);
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(uintptr_t)(lds_void_t*)(reinterpret_cast<char*>(lds) + (size_t)(r0 + c * 4) * 256));
+        if (row < n) {
+            const float* src = vsrc + (size_t)(g0 + row) * MD + (lane & 15) * 4;
+            int keep;
+            __asm__ volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(src), "s"(dst)
+                : "memory");
+        }
+    }
+}
+
+__device__ __forceinline__ void pyr_dma_wait() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0) only
+
+__device__ __forceinline__ void pyr_zero_row(float4* __restrict__ lds, int row, int tid0) {
+    const int t = (int)threadIdx.x - tid0;
+    if (t >= 0 && t < 16) lds[(size_t)row * 16 + t] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+template <int RD>
+__global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr2_kernel(
+    const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
+    int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
+    int qblocks, float* __restrict__ out, float* __restrict__ save_attn, float* __restrict__ save_loc,
+    uint16_t* __restrict__ out16) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds4[];
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);  // the query blocks and heads of a video share an XCD
+    const int qb = blk % qblocks, bm = blk / qblocks;
+    const int b = bm / M, m = bm - b * M;
+    const int slot = threadIdx.x >> 4, sub = threadIdx.x & 15;
+    const size_t MD = (size_t)M * 64;
+    const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
+    const float* vsrc = value + (size_t)b * S * MD + (size_t)m * 64;
+    const char* lrow = reinterpret_cast<const char*>(lds4) + sub * 16;
+    const int n0 = lv.T[0], n1 = lv.T[1] + lv.T[2] + lv.T[3];
+    const bool single = n0 + n1 + 2 <= kLdsRows;
+    const int p2 = single ? 1 + n0 : kLdsRows - 1 - n1;  // LDS row of level 1's first position
+
+    // the guard rows first: a ds_write issued while DMAs are in flight waits for them (the compiler orders LDS
+    // writes after pending LDS-DMA writes)
+    pyr_zero_row(lds4, 0, 0);
+    pyr_zero_row(lds4, single ? n0 + n1 + 1 : n0 + 1, 64);
+    if (!single) pyr_zero_row(lds4, kLdsRows - 1, 128);
+    const int l_own = sub >> 2;
+    const int T_own = lvl_sel(lv.T, l_own), st_own = lvl_sel(lv.start, l_own);
+    const int base_own = l_own == 0 ? 1 : p2 + (st_own - lv.start[1]);
+    const float Tf_own = (float)T_own;
+    float lgv[kPyrQPS], offv[kPyrQPS], r0v[kPyrQPS], r1v[kPyrQPS];
+#pragma unroll
+    for (int i = 0; i < kPyrQPS; ++i) {
+        const int q = qb * kPyrQ + slot + 64 * i;
+        const size_t row = (size_t)b * Lq + (q < Lq ? q : 0);
+        const float* prow = proj + row * proj_stride;
+        lgv[i] = prow[logit_base + m * kNS + sub];
+        offv[i] = prow[off_base + m * kNS + sub];
+        r0v[i] = ref[(row * kL + l_own) * RD];
+        r1v[i] = (RD == 2) ? ref[(row * kL + l_own) * RD + 1] : 0.f;
+    }
+    // the parameters first (a use of them while DMAs are in flight would wait for the DMAs too), then the first
+    // phase's rows as DMAs, landing while the parameter math runs
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): gfx9 encoding, lgkm/exp counts left at their maximum
+    pyr_dma_rows(lds4, vsrc, MD, lv.start[0], 1, single ? n0 + n1 : n0);
+    int adv[kPyrQPS];
+    float w1v[kPyrQPS], w2v[kPyrQPS];
+#pragma unroll
+    for (int i = 0; i < kPyrQPS; ++i) {
+        const int q = qb * kPyrQ + slot + 64 * i;
+        const bool act = q < Lq;
+        const float lg = lgv[i];
+        const float mx = group_max<16>(lg);
+        const float sum = group_allreduce<16>(expf(lg - mx));
+        const float aw = expf(lg - mx) / sum;
+        const float off = offv[i];
+        const float r0 = r0v[i];
+        const float r1 = r1v[i];
+        const float loc = (RD == 1) ? r0 + off / Tf_own : r0 + ((off / (float)kP) * r1) * 0.5f;
+        if (save_loc && act) {
+            const size_t si = save_index(b, m, l_own, q, sub & 3, Lq, M);
+            save_loc[si] = loc;
+            save_attn[si] = aw;
+        }
+        const float x = loc * Tf_own - 0.5f;
+        const bool inside = x > -1.f && x < Tf_own;
+        const float xf = floorf(inside ? x : 0.f);
+        const int i0 = (int)xf;
+        const float lw = inside ? x - xf : 0.f;
+        bool ok1 = inside && i0 >= 0, ok2 = inside && i0 + 1 <= T_own - 1;
+        if (mbase) {
+            ok1 = ok1 && !mbase[st_own + min(max(i0, 0), T_own - 1)];
+            ok2 = ok2 && !mbase[st_own + min(max(i0 + 1, 0), T_own - 1)];
+        }
+        adv[i] = pyr_corner(base_own, i0);
+        w1v[i] = ok1 ? (1.f - lw) * aw : 0.f;
+        w2v[i] = ok2 ? lw * aw : 0.f;
+    }
+
+    float4 acc[kPyrQPS];
+#pragma unroll
+    for (int i = 0; i < kPyrQPS; ++i) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 tok = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto level = [&](auto Lc) {
+        constexpr int L = decltype(Lc)::value;
+#pragma unroll
+        for (int i = 0; i < kPyrQPS; ++i) {
+            float4 v1[kP], v2[kP];
+            float c1[kP], c2[kP];
+            int ad = adv[i];
+            float wa = w1v[i], wb = w2v[i];
+            __asm__ volatile("" : "+v"(ad), "+v"(wa), "+v"(wb) : "v"(tok.x), "v"(tok.y), "v"(tok.z), "v"(tok.w));
+#pragma unroll
+            for (int p = 0; p < kP; ++p) {
+                const char* r = lrow + grp_bcast<16>(ad, L * kP + p);
+                c1[p] = grp_bcast<16>(wa, L * kP + p);
+                c2[p] = grp_bcast<16>(wb, L * kP + p);
+                v1[p] = *reinterpret_cast<const float4*>(r);
+                v2[p] = *reinterpret_cast<const float4*>(r + 256);
+            }
+#pragma unroll
+            for (int p = 0; p < kP; ++p) {
+                acc[i].x = fmaf(c1[p], v1[p].x, acc[i].x);
+                acc[i].y = fmaf(c1[p], v1[p].y, acc[i].y);
+                acc[i].z = fmaf(c1[p], v1[p].z, acc[i].z);
+                acc[i].w = fmaf(c1[p], v1[p].w, acc[i].w);
+                acc[i].x = fmaf(c2[p], v2[p].x, acc[i].x);
+                acc[i].y = fmaf(c2[p], v2[p].y, acc[i].y);
+                acc[i].z = fmaf(c2[p], v2[p].z, acc[i].z);
+                acc[i].w = fmaf(c2[p], v2[p].w, acc[i].w);
+            }
+            tok = acc[i];
+        }
+    };
+    __syncthreads();  // the first phase's DMAs have landed (every wave waited for its own before the barrier)
+    if (single) {
+        level(std::integral_constant<int, 0>{});
+        level(std::integral_constant<int, 1>{});
+        level(std::integral_constant<int, 2>{});
+        level(std::integral_constant<int, 3>{});
+    } else {
+        // levels 1..3's rows above level 0's region land during level 0's gather
+        const int pre = n0 + 2 > p2 ? n0 + 2 - p2 : 0;  // phase-2 rows [0, pre) overlap level 0's rows
+        pyr_dma_rows_async(lds4, vsrc, MD, lv.start[1] + pre, p2 + pre, n1 - pre);
+        level(std::integral_constant<int, 0>{});
+        pyr_dma_wait();   // this wave's prefetch landed ...
+        __syncthreads();  // ... and every wave's; level 0 read by every wave
+        pyr_zero_row(lds4, p2 - 1, 0);
+        pyr_dma_rows(lds4, vsrc, MD, lv.start[1], p2, pre);
+        __syncthreads();
+        level(std::integral_constant<int, 1>{});
+        level(std::integral_constant<int, 2>{});
+        level(std::integral_constant<int, 3>{});
+    }
+#pragma unroll
+    for (int i = 0; i < kPyrQPS; ++i) {
+        const int q = qb * kPyrQ + slot + 64 * i;
+        if (q < Lq) {
+            const size_t o = ((size_t)b * Lq + q) * MD + (size_t)m * 64 + sub * 4;
+            *reinterpret_cast<float4*>(out + o) = acc[i];
+            if (out16) store_bf16x4(out16 + o, acc[i].x, acc[i].y, acc[i].z, acc[i].w);
+        }
+    }
+}
+
+// -------------------------------------------------------------------------------------------------
 // backward, query side: grad of the offset and attention logits (+ reference points)
 // softmax backward needs delta = sum_j a_j dL/da_j over the 16 samples of a (query, head).  Default (fout NULL):
 // each level's owner lanes keep their (a_j, dL/da_j) pair in registers -- one pair per lane per level -- and the
@@ -815,7 +1025,8 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
     int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
     int qblocks, const float* __restrict__ gout, const float* __restrict__ save_attn,
-    const float* __restrict__ save_loc, float* __restrict__ grad_proj, float* __restrict__ grad_ref) {
+    const float* __restrict__ save_loc, float* __restrict__ grad_proj, float* __restrict__ grad_ref,
+    uint16_t* __restrict__ gp16) {
     extern __shared__ __attribute__((aligned(16))) float4 lds4[];
     float* carry = reinterpret_cast<float*>(lds4 + kPyrRowsG * 16);  // [kBqQ][4]: dL/da of level 0's samples
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
@@ -912,7 +1123,10 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
             goff = (t2 * rr1) / (float)kP;
             g1 = mine_phase ? t2 * (prow[off_base + m * kNS + sub] / (float)kP) : 0.f;
         }
-        if (act && mine_phase) gprow[off_base + m * kNS + sub] = goff;
+        if (act && mine_phase) {
+            gprow[off_base + m * kNS + sub] = goff;
+            if (gp16) gp16[row * proj_stride + off_base + m * kNS + sub] = (uint16_t)bf16_bits(goff);
+        }
         if (grad_ref) {  // per (query, level): the lane quad of the level; heads differ by workgroup: atomics
             g0 += grp_swap(g0, 1);
             g0 += grp_swap(g0, 2);
@@ -932,7 +1146,11 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
         } else {  // second phase: the softmax term over all 16 samples, then every logit gradient
             if (l_own == 0) ga = carry[ci];
             const float delta = group_allreduce<16>(a * ga);
-            if (act) gprow[logit_base + m * kNS + sub] = a * (ga - delta);
+            if (act) {
+                const float gl = a * (ga - delta);
+                gprow[logit_base + m * kNS + sub] = gl;
+                if (gp16) gp16[row * proj_stride + logit_base + m * kNS + sub] = (uint16_t)bf16_bits(gl);
+            }
         }
     };
 
@@ -978,7 +1196,8 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
                                                                      float* __restrict__ grad_value,
                                                                      float* __restrict__ level_sums,
                                                                      const int64_t* __restrict__ dshapes = nullptr,
-                                                                     const int64_t* __restrict__ dlsi = nullptr) {
+                                                                     const int64_t* __restrict__ dlsi = nullptr,
+                                                                     uint16_t* __restrict__ gv16 = nullptr) {
     extern __shared__ __attribute__((aligned(16))) int lds_i[];
     // the drop-in fast path passes its device level table: the kernel runs only for a 1-D pyramid (dropin_levels)
     if (dshapes != nullptr && !dropin_levels(dshapes, dlsi, S, lv)) return;
@@ -1110,9 +1329,14 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
         // query chunk only; later chunks add into what the first wrote).  Every other row is written by the walk.
         const int gl = lane & 15;
         float* ob = grad_value + ((size_t)b * S + st) * MD + (size_t)m * D + gl * 4;
+        // bf16 mode: the rounding of every row written, at the same offsets (the value projection's operand)
+        uint16_t* ob16 = gv16 ? gv16 + ((size_t)b * S + st) * MD + (size_t)m * D + gl * 4 : nullptr;
         if (!accumulate)
             for (int t = threadIdx.x >> 4; t < T; t += blockDim.x >> 4)
-                if (off[t] == off[t + 2]) *reinterpret_cast<float4*>(ob + (size_t)t * MD) = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (off[t] == off[t + 2]) {
+                    *reinterpret_cast<float4*>(ob + (size_t)t * MD) = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (ob16) *reinterpret_cast<uint2*>(ob16 + (size_t)t * MD) = make_uint2(0u, 0u);
+                }
         // walk: 16-lane group vg owns rows [r0, r1) and reads buckets r0 .. r1; one sorted entry and one gathered
         // gradient row per sample, two running rows (key - 1 and key), each row written once when its last bucket
         // has passed -- no per-row search, at most two row writes per change of key
@@ -1140,6 +1364,7 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
                         v.w += o.w;
                     }
                     *orow = v;
+                    if (ob16) store_bf16x4(ob16 + (size_t)r * MD, v.x, v.y, v.z, v.w);
                 }
             };
             int k = (int)(eqk[jb] >> 16);
@@ -1566,15 +1791,26 @@ static bool fwd_buf() {
 static int pyr_attrs() {
     static int rc = -1;
     if (rc < 0) {
-        const void* ks[2] = {(const void*)msda1d_fwd_pyr_kernel<1>, (const void*)msda1d_fwd_pyr_kernel<2>};
+        const void* ks[4] = {(const void*)msda1d_fwd_pyr_kernel<1>, (const void*)msda1d_fwd_pyr_kernel<2>,
+                             (const void*)msda1d_fwd_pyr2_kernel<1>, (const void*)msda1d_fwd_pyr2_kernel<2>};
+        const size_t lds[4] = {kPyrLds, kPyrLds, kPyr2LdsMax, kPyr2LdsMax};
         rc = PDVC_OK;
-        for (const void* k : ks)
-            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPyrLds) != hipSuccess) {
+        for (int i = 0; i < 4; ++i)
+            if (hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds[i]) != hipSuccess) {
                 (void)hipGetLastError();
                 rc = pdvc_set_error(PDVC_ERR_LAUNCH, "msda1d pyramid kernels: cannot raise the LDS limit");
             }
     }
     return rc;
+}
+
+// LDS-DMA pyramid forward (msda1d_fwd_pyr2_kernel; PDVC_PYR_DMA=0 selects msda1d_fwd_pyr_kernel: A/B)
+static bool pyr_dma() {
+    static const bool on = [] {
+        const char* e = getenv("PDVC_PYR_DMA");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 }  // namespace pdvc
@@ -1606,11 +1842,12 @@ static void launch_bwdq1d(const Geometry& g, dim3 grid, hipStream_t s, const flo
 #undef ARGS
 }
 
-extern "C" int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_pad_mask, const float* proj,
-                                       int proj_stride, int off_base, int logit_base, const float* ref, int ref_dim,
-                                       const int32_t* level_T, int num_levels, int batch, int num_query,
-                                       int num_heads, int head_dim, int num_point, float* output, float* save_attn,
-                                       float* save_loc, void* stream) {
+// out16 (bf16 mode): the output's bf16 rounding beside it -- only on the LDS-DMA pyramid path (the encoder's
+// self-attention); any other path returns PDVC_ERR_UNSUPPORTED before launching anything
+static int msda1d_forward_impl(const float* value, const uint8_t* value_pad_mask, const float* proj, int proj_stride,
+                               int off_base, int logit_base, const float* ref, int ref_dim, const int32_t* level_T,
+                               int num_levels, int batch, int num_query, int num_heads, int head_dim, int num_point,
+                               float* output, float* save_attn, float* save_loc, uint16_t* out16, void* stream) {
     Levels1d lv;
     int S = 0;
     int rc = fill_levels(level_T, num_levels, num_point, lv, S);
@@ -1633,11 +1870,13 @@ extern "C" int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_
         if ((rc = pyr_attrs())) return rc;
         PDVC_CHECK_ARG((long)batch * num_heads * qb < (1L << 31), "too many query blocks");
         dim3 pg((unsigned)(batch * num_heads * qb));
+        if (out16 && !pyr_dma())
+            return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "bf16 output only on the LDS-DMA pyramid path");
         static const int ablate = [] {
             const char* e = getenv("PDVC_PYR_ABLATE");
             return e ? atoi(e) : 0;
         }();
-        if (ablate >= 1 && ablate <= 3 && ref_dim == 1) {  // measurement only (tools/kbench.py)
+        if (ablate >= 1 && ablate <= 3 && ref_dim == 1 && !out16) {  // measurement only (tools/kbench.py)
             const void* k = ablate == 1 ? (const void*)msda1d_fwd_pyr_kernel<1, 1>
                             : ablate == 2 ? (const void*)msda1d_fwd_pyr_kernel<1, 2>
                                           : (const void*)msda1d_fwd_pyr_kernel<1, 3>;
@@ -1654,6 +1893,17 @@ extern "C" int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_
                 hipLaunchKernelGGL((msda1d_fwd_pyr_kernel<1, 2>), pg, dim3(kPyrThreads), kPyrLds, s, value,
                                    value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv, num_query, S,
                                    num_heads, qb, output, save_attn, save_loc);
+        } else if (pyr_dma()) {
+            const int n_all = lv.T[0] + lv.T[1] + lv.T[2] + lv.T[3] + 2;
+            const size_t lds = n_all <= kLdsRows ? (size_t)n_all * 256 : kPyr2LdsMax;
+            if (ref_dim == 1)
+                hipLaunchKernelGGL((msda1d_fwd_pyr2_kernel<1>), pg, dim3(kPyrThreads), lds, s, value, value_pad_mask,
+                                   proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, qb,
+                                   output, save_attn, save_loc, out16);
+            else
+                hipLaunchKernelGGL((msda1d_fwd_pyr2_kernel<2>), pg, dim3(kPyrThreads), lds, s, value, value_pad_mask,
+                                   proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, qb,
+                                   output, save_attn, save_loc, out16);
         } else if (ref_dim == 1)
             hipLaunchKernelGGL((msda1d_fwd_pyr_kernel<1>), pg, dim3(kPyrThreads), kPyrLds, s, value, value_pad_mask,
                                proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, qb, output,
@@ -1665,6 +1915,7 @@ extern "C" int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_
         PDVC_CHECK_LAUNCH("msda1d_fwd_pyr_kernel");
         return PDVC_OK;
     }
+    if (out16) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "bf16 output only on the LDS-DMA pyramid path");
     if (head_dim == 64 && fwd_buf() && (long)S * num_heads * head_dim * 4 < (1L << 31)) {
         if (ref_dim == 1)
             hipLaunchKernelGGL((msda1d_fwd_buf_kernel<1>), grid, dim3(256), 0, s, value, value_pad_mask, proj,
@@ -1690,13 +1941,38 @@ extern "C" int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_
 extern "C" int pdvc_level_pos_rows_backward_f32(const float* dpos, const int32_t* level_T, int num_levels, int N,
                                                 int S, int C, float* partials, void* stream);
 
-extern "C" int pdvc_msda1d_backward_ex_f32(const float* value, const uint8_t* value_pad_mask, const float* ref,
-                                           int ref_dim, const float* proj, int proj_stride, int off_base,
-                                           int logit_base, const int32_t* level_T, int num_levels, int batch,
-                                           int num_query, int num_heads, int head_dim, int num_point,
-                                           const float* grad_output, const float* output, const float* save_attn,
-                                           const float* save_loc, float* grad_value, float* grad_proj,
-                                           float* grad_ref, float* grad_value_level_sums, void* stream) {
+extern "C" int pdvc_msda1d_forward_f32(const float* value, const uint8_t* value_pad_mask, const float* proj,
+                                       int proj_stride, int off_base, int logit_base, const float* ref, int ref_dim,
+                                       const int32_t* level_T, int num_levels, int batch, int num_query,
+                                       int num_heads, int head_dim, int num_point, float* output, float* save_attn,
+                                       float* save_loc, void* stream) {
+    return msda1d_forward_impl(value, value_pad_mask, proj, proj_stride, off_base, logit_base, ref, ref_dim, level_T,
+                               num_levels, batch, num_query, num_heads, head_dim, num_point, output, save_attn,
+                               save_loc, nullptr, stream);
+}
+
+extern "C" int pdvc_msda1d_forward_f32_bf16out(const float* value, const uint8_t* value_pad_mask, const float* proj,
+                                               int proj_stride, int off_base, int logit_base, const float* ref,
+                                               int ref_dim, const int32_t* level_T, int num_levels, int batch,
+                                               int num_query, int num_heads, int head_dim, int num_point,
+                                               float* output, float* save_attn, float* save_loc, uint16_t* out16,
+                                               void* stream) {
+    PDVC_CHECK_ARG(out16 != nullptr && ((uintptr_t)out16 % 8) == 0, "out16 must be an 8-byte aligned bf16 buffer");
+    return msda1d_forward_impl(value, value_pad_mask, proj, proj_stride, off_base, logit_base, ref, ref_dim, level_T,
+                               num_levels, batch, num_query, num_heads, head_dim, num_point, output, save_attn,
+                               save_loc, out16, stream);
+}
+
+// gv16 / gp16 (bf16 mode): the bf16 roundings of grad_value / grad_proj beside them -- only where the encoder's
+// pyramid backward-query kernel and the 16-lane value-gradient walk run and grad_proj is all offset and logit
+// columns (proj_stride = 2 * num_heads * 16); otherwise PDVC_ERR_UNSUPPORTED before launching anything
+static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mask, const float* ref, int ref_dim,
+                                const float* proj, int proj_stride, int off_base, int logit_base,
+                                const int32_t* level_T, int num_levels, int batch, int num_query, int num_heads,
+                                int head_dim, int num_point, const float* grad_output, const float* output,
+                                const float* save_attn, const float* save_loc, float* grad_value, float* grad_proj,
+                                float* grad_ref, float* grad_value_level_sums, uint16_t* gv16, uint16_t* gp16,
+                                void* stream) {
     float* level_sums = grad_value_level_sums;
     if (level_sums)
         PDVC_CHECK_ARG(((long)num_heads * head_dim) % 4 == 0 && ((uintptr_t)level_sums % 16) == 0 &&
@@ -1721,6 +1997,14 @@ extern "C" int pdvc_msda1d_backward_ex_f32(const float* value, const uint8_t* va
         if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "memset grad_ref: %s", hipGetErrorString(e));
     }
     const int bq_blocks = (tw > 0 && bwdq_mode() == 1) ? pick_pyr(lv, S, num_query, head_dim, kBqQ) : 0;
+    if (gv16 || gp16) {
+        int Tm = 0;
+        for (int l = 0; l < kL; ++l) Tm = lv.T[l] > Tm ? lv.T[l] : Tm;
+        const bool g4ok = head_dim == 64 && value_g4() && (long)num_query * num_heads * head_dim * 4 < (1L << 31) &&
+                          num_query < 65536 && Tm < 65535;
+        if (bq_blocks <= 0 || !g4ok || proj_stride != 2 * NSM || (uintptr_t)gv16 % 8 || (uintptr_t)gp16 % 2)
+            return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "bf16 gradients only on the encoder's pyramid path");
+    }
     if (bq_blocks > 0) {
         if ((rc = bwdq_pyr_attrs())) return rc;
         PDVC_CHECK_ARG((long)batch * num_heads * bq_blocks < (1L << 31), "too many query blocks");
@@ -1728,11 +2012,11 @@ extern "C" int pdvc_msda1d_backward_ex_f32(const float* value, const uint8_t* va
         if (ref_dim == 1)
             hipLaunchKernelGGL((msda1d_bwd_query_pyr_kernel<1>), pg, dim3(kPyrThreads), kBqLds, s, value,
                                value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv, num_query, S,
-                               num_heads, bq_blocks, grad_output, save_attn, save_loc, grad_proj, grad_ref);
+                               num_heads, bq_blocks, grad_output, save_attn, save_loc, grad_proj, grad_ref, gp16);
         else
             hipLaunchKernelGGL((msda1d_bwd_query_pyr_kernel<2>), pg, dim3(kPyrThreads), kBqLds, s, value,
                                value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv, num_query, S,
-                               num_heads, bq_blocks, grad_output, save_attn, save_loc, grad_proj, grad_ref);
+                               num_heads, bq_blocks, grad_output, save_attn, save_loc, grad_proj, grad_ref, gp16);
         PDVC_CHECK_LAUNCH("msda1d_bwd_query_pyr_kernel");
     } else if (tw > 0 && head_dim == 64 && bwdq_mode() != 0 && (long)S * num_heads * head_dim * 4 < (1L << 31)) {
         dim3 grid((unsigned)((tw + 3) / 4));
@@ -1805,11 +2089,13 @@ extern "C" int pdvc_msda1d_backward_ex_f32(const float* value, const uint8_t* va
             if (g4 && value_ug(num_query, S) == 4)
                 hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, 4>), dim3((unsigned)nblk), dim3(kVW * 64), lds,
                                    s, value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
-                                   save_attn, save_loc, grad_value, gsums);
+                                   save_attn, save_loc, grad_value, gsums, (const int64_t*)nullptr,
+                                   (const int64_t*)nullptr, gv16);
             else if (g4)
                 hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
                                    value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
-                                   save_attn, save_loc, grad_value, gsums);
+                                   save_attn, save_loc, grad_value, gsums, (const int64_t*)nullptr,
+                                   (const int64_t*)nullptr, gv16);
             else if (head_dim <= 64)
                 hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, false>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
                                    value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
@@ -1828,6 +2114,35 @@ extern "C" int pdvc_msda1d_backward_ex_f32(const float* value, const uint8_t* va
         }
     }
     return PDVC_OK;
+}
+
+extern "C" int pdvc_msda1d_backward_ex_f32(const float* value, const uint8_t* value_pad_mask, const float* ref,
+                                           int ref_dim, const float* proj, int proj_stride, int off_base,
+                                           int logit_base, const int32_t* level_T, int num_levels, int batch,
+                                           int num_query, int num_heads, int head_dim, int num_point,
+                                           const float* grad_output, const float* output, const float* save_attn,
+                                           const float* save_loc, float* grad_value, float* grad_proj,
+                                           float* grad_ref, float* grad_value_level_sums, void* stream) {
+    return msda1d_backward_impl(value, value_pad_mask, ref, ref_dim, proj, proj_stride, off_base, logit_base, level_T,
+                                num_levels, batch, num_query, num_heads, head_dim, num_point, grad_output, output,
+                                save_attn, save_loc, grad_value, grad_proj, grad_ref, grad_value_level_sums, nullptr,
+                                nullptr, stream);
+}
+
+extern "C" int pdvc_msda1d_backward_ex_f32_bf16out(const float* value, const uint8_t* value_pad_mask,
+                                                   const float* ref, int ref_dim, const float* proj, int proj_stride,
+                                                   int off_base, int logit_base, const int32_t* level_T,
+                                                   int num_levels, int batch, int num_query, int num_heads,
+                                                   int head_dim, int num_point, const float* grad_output,
+                                                   const float* output, const float* save_attn, const float* save_loc,
+                                                   float* grad_value, float* grad_proj, float* grad_ref,
+                                                   float* grad_value_level_sums, uint16_t* grad_value16,
+                                                   uint16_t* grad_proj16, void* stream) {
+    PDVC_CHECK_ARG(grad_value16 != nullptr && grad_proj16 != nullptr, "both bf16 buffers are required");
+    return msda1d_backward_impl(value, value_pad_mask, ref, ref_dim, proj, proj_stride, off_base, logit_base, level_T,
+                                num_levels, batch, num_query, num_heads, head_dim, num_point, grad_output, output,
+                                save_attn, save_loc, grad_value, grad_proj, grad_ref, grad_value_level_sums,
+                                grad_value16, grad_proj16, stream);
 }
 
 extern "C" int pdvc_msda1d_backward_f32(const float* value, const uint8_t* value_pad_mask, const float* ref,

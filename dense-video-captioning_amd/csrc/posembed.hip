@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void level_pos_fwd_kernel(const float* __restr
                                                             const float* __restrict__ dur,
                                                             const float* __restrict__ lemb, PosLevels lv, int N,
                                                             int S, int F, int Dd, const float* __restrict__ add,
-                                                            float* __restrict__ pos) {
+                                                            float* __restrict__ pos, uint16_t* __restrict__ pos16) {
     const int C = F + Dd, c4n = C / 4;
     const long total = (long)N * S * c4n;
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -64,6 +64,7 @@ __global__ __launch_bounds__(256) void level_pos_fwd_kernel(const float* __restr
             o = make_float4(a.x + o.x, a.y + o.y, a.z + o.z, a.w + o.w);
         }
         reinterpret_cast<float4*>(pos)[i] = o;
+        if (pos16) store_bf16x4(pos16 + i * 4, o.x, o.y, o.z, o.w);
     }
 }
 
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(256) void level_pos_rows_kernel(const float* __rest
                                                              const float* __restrict__ dur,
                                                              const float* __restrict__ lemb, PosLevels lv, int N,
                                                              int S, int F, int Dd, const float* __restrict__ add,
-                                                             float* __restrict__ pos) {
+                                                             float* __restrict__ pos, uint16_t* __restrict__ pos16) {
     const int C = F + Dd, c4n = C / 4, rpi = 256 / c4n;
     const int cg = threadIdx.x % c4n, rr = threadIdx.x / c4n;
     const int c = cg * 4;
@@ -115,6 +116,7 @@ __global__ __launch_bounds__(256) void level_pos_rows_kernel(const float* __rest
             o = make_float4(a.x + o.x, a.y + o.y, a.z + o.z, a.w + o.w);
         }
         reinterpret_cast<float4*>(pos)[i] = o;
+        if (pos16) store_bf16x4(pos16 + i * 4, o.x, o.y, o.z, o.w);
         s += rpi;
         while (s >= S) {
             s -= S;
@@ -176,10 +178,12 @@ static int fill_pos_levels(const int32_t* level_T, int L, int S, PosLevels& lv) 
 
 using namespace pdvc;
 
-extern "C" int pdvc_level_pos_rows_add_f32(const float* xe, const float* dim_t, const float* dur,
-                                           const float* level_embed, const int32_t* level_T, int num_levels, int N,
-                                           int S, int F, int Dd, const float* add, float* out, void* stream) {
+extern "C" int pdvc_level_pos_rows_add_f32_bf16out(const float* xe, const float* dim_t, const float* dur,
+                                                   const float* level_embed, const int32_t* level_T, int num_levels,
+                                                   int N, int S, int F, int Dd, const float* add, float* out,
+                                                   uint16_t* out16, void* stream) {
     float* pos = out;
+    PDVC_CHECK_ARG(((uintptr_t)out16 % 8) == 0, "out16 must be 8-byte aligned");
     PDVC_CHECK_ARG(N >= 0 && S > 0 && F > 0 && Dd >= 0 && F % 4 == 0 && Dd % 4 == 0, "invalid sizes");
     PDVC_CHECK_ARG(((uintptr_t)add % 16) == 0, "add must be 16-byte aligned");
     PDVC_CHECK_ARG(((uintptr_t)pos % 16) == 0 && ((uintptr_t)level_embed % 16) == 0 &&
@@ -194,16 +198,23 @@ extern "C" int pdvc_level_pos_rows_add_f32(const float* xe, const float* dim_t, 
     if (c4n <= 256 && 256 % c4n == 0) {
         const long blocks = ((long)N * S + kPosRows - 1) / kPosRows;
         hipLaunchKernelGGL(level_pos_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, xe, dim_t,
-                           dur, level_embed, lv, N, S, F, Dd, add, pos);
+                           dur, level_embed, lv, N, S, F, Dd, add, pos, out16);
         PDVC_CHECK_LAUNCH("level_pos_rows_kernel");
         return PDVC_OK;
     }
     const long want = (total + 255) / 256;
     const unsigned blocks = (unsigned)(want < 16384 ? want : 16384);
     hipLaunchKernelGGL(level_pos_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, xe, dim_t, dur,
-                       level_embed, lv, N, S, F, Dd, add, pos);
+                       level_embed, lv, N, S, F, Dd, add, pos, out16);
     PDVC_CHECK_LAUNCH("level_pos_fwd_kernel");
     return PDVC_OK;
+}
+
+extern "C" int pdvc_level_pos_rows_add_f32(const float* xe, const float* dim_t, const float* dur,
+                                           const float* level_embed, const int32_t* level_T, int num_levels, int N,
+                                           int S, int F, int Dd, const float* add, float* out, void* stream) {
+    return pdvc_level_pos_rows_add_f32_bf16out(xe, dim_t, dur, level_embed, level_T, num_levels, N, S, F, Dd, add, out,
+                                               nullptr, stream);
 }
 
 extern "C" int pdvc_level_pos_rows_forward_f32(const float* xe, const float* dim_t, const float* dur,

@@ -27,8 +27,11 @@ SIGNATURES = {
     "pdvc_msda1d_forward_f32": [_vp, _u8p, _vp, _i, _i, _i, _vp, _i, _vp] + [_i] * 6 + [_vp] * 4,
     "pdvc_msda1d_backward_f32": [_vp, _u8p, _vp, _i, _vp, _i, _i, _i, _vp] + [_i] * 6 + [_vp] * 8,
     "pdvc_msda1d_backward_ex_f32": [_vp, _u8p, _vp, _i, _vp, _i, _i, _i, _vp] + [_i] * 6 + [_vp] * 9,
+    "pdvc_msda1d_forward_f32_bf16out": [_vp, _u8p, _vp, _i, _i, _i, _vp, _i, _vp] + [_i] * 6 + [_vp] * 5,
+    "pdvc_msda1d_backward_ex_f32_bf16out": [_vp, _u8p, _vp, _i, _vp, _i, _i, _i, _vp] + [_i] * 6 + [_vp] * 11,
     "pdvc_cap_gather_forward_f32": [_vp, _u8p, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _vp] + [_i] * 6 + [_vp] * 3,
     "pdvc_cap_gather_backward_f32": [_vp, _u8p, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _vp] + [_i] * 6 + [_vp] * 6,
+    "pdvc_cap_gather_backward2_f32": [_vp, _u8p, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _vp] + [_i] * 6 + [_vp] * 8,
     "pdvc_cap_value_grad_f32": [_u8p, _vp] + [_i] * 8 + [_vp] * 6,
     "pdvc_cap_value_grad_ex_f32": [_u8p, _vp] + [_i] * 8 + [_vp] * 7,
     "pdvc_softattn_forward_f32": [_vp, _vp, _i, _vp, _vp, _vp] + [_i] * 4 + [_vp] * 3,
@@ -47,6 +50,8 @@ SIGNATURES = {
     "pdvc_add_dropout_layernorm_backward_f32_bf16out": [_vp] * 6 + [_i, _i, _f, _u64] + [_vp] * 9,
     "pdvc_relu_dropout_forward_f32_bf16out": [_vp, ctypes.c_long, _i, _f, _u64, _vp, _vp, _vp],
     "pdvc_relu_dropout_backward_f32_bf16out": [_vp, _vp, _i, _i, _f, _i, _vp, _vp, _vp, _vp],
+    "pdvc_logprob_pick_backward_f32_bf16out": [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp],
+    "pdvc_level_pos_rows_add_f32_bf16out": [_vp] * 5 + [_i] * 5 + [_vp] * 4,
     "pdvc_logprob_pick_forward_f32": [_vp, _vp, _i, _i, _vp, _vp, _vp],
     "pdvc_logprob_pick_backward_f32": [_vp, _vp, _vp, _i, _i, _vp, _vp],
     "pdvc_logprob_argmax_f32": [_vp, _i, _i, _vp, _vp, _vp],

@@ -27,6 +27,7 @@ from .ms_deform_attn_func import NUM_SAMPLES, _levels
 
 # ctx2att of the samples as a gather of the once-projected value rows (see forward); False keeps the per-step GEMM
 CTX2ATT_GATHER = True
+U_GRAD = True  # the backward in the same form (see forward); False: dW_ctx and dclip from CLIP and dATT per sample
 U_MAX_BYTES = 16 << 30  # largest projected-rows buffer of the gather form (bound its memory)
 
 
@@ -72,19 +73,23 @@ class CaptionDecodeFunction(Function):
         GATT = torch.empty((R, G), **kw)
         zero = torch.zeros((R, H), **kw)
         st = _n.stream()
+        # att = ctx2att(clip) is linear in the sample, and a sample is a blend of value rows with weights summing to
+        # 1: project the value rows once (padded rows zeroed: their projection is the bias) and blend the projections
+        # with the same gather -- U rows N*S instead of a (R*16) x D x A GEMM for each of n steps.  A loop invariant,
+        # not part of the recurrence: in the bf16 mode it is a bf16 GEMM like the other projections.
+        U = vm = None
+        # the projected rows take Nv*S*M*A floats, A/D times the value's (8x at cap_nheads 8): the gather form only
+        # while that stays within U_MAX_BYTES (the per-step GEMM needs no such buffer)
+        u_bytes = 4 * Nv * S * M * A
+        if (CTX2ATT_GATHER and 32 <= A <= 512 and A & (A - 1) == 0 and n * R * M * NS > Nv * S * M
+                and u_bytes <= U_MAX_BYTES):
+            vm = value if pad_mask is None else value.masked_fill(pad_mask.view(Nv, S, 1, 1).bool(), 0.0)
+            U = torch.addmm(b_ctx, vm.view(-1, D), W_ctx.t()).view(Nv, S, M, A)
+        # the backward in the same form (U_GRAD): dATT is scattered onto the value rows once (dU), so dW_ctx = dU^T vm
+        # and the value gradient's ctx2att part dU W_ctx are GEMMs over N*S rows instead of n*R*16, and the
+        # location gradient of att is read off U at the sample corners (pdvc_cap_gather_backward2_f32)
+        ctx.u_grad = U is not None and U_GRAD and A == D and video_csr is not None
         with fp32_gemms():  # the recurrence stays fp32 in the bf16 mode (pdvc/precision.py)
-            # att = ctx2att(clip) is linear in the sample, and a sample is a blend of value rows with weights summing
-            # to 1: project the value rows once (padded rows zeroed: their projection is the bias) and blend the
-            # projections with the same gather -- U rows N*S instead of a (R*16) x D x A GEMM for each of n steps.
-            # The backward is unchanged (dW_ctx, db_ctx and dclip come from CLIP and dATT).
-            U = None
-            # the projected rows take Nv*S*M*A floats, A/D times the value's (8x at cap_nheads 8): the gather form only
-            # while that stays within U_MAX_BYTES (the per-step GEMM needs no such buffer)
-            u_bytes = 4 * Nv * S * M * A
-            if (CTX2ATT_GATHER and 32 <= A <= 512 and A & (A - 1) == 0 and n * R * M * NS > Nv * S * M
-                    and u_bytes <= U_MAX_BYTES):
-                vm = value if pad_mask is None else value.masked_fill(pad_mask.view(Nv, S, 1, 1).bool(), 0.0)
-                U = torch.addmm(b_ctx, vm.view(-1, D), W_ctx.t()).view(Nv, S, M, A)
             for i in range(n):
                 if i == 0:
                     HP[0].copy_(b_h.expand(R, Ph))  # h_{-1} = 0
@@ -109,7 +114,7 @@ class CaptionDecodeFunction(Function):
                 _n.call("pdvc_lstm_cell_forward_f32", xa, ldx, _n.ptr(GATT), G, gh, ldg, _n.ptr(hs_g), G,
                         _n.ptr(CS[i - 1] if i > 0 else zero), R, H, ho, ldo, _n.ptr(CS[i]), _n.ptr(ACTS[i]), st)
         ctx.save_for_backward(value, off_hs, ref, W_h, W_ctx, alpha_w, W_att, pad_mask, row_video, HP, CLIP, LOC,
-                              ATT, PROBS, RES, ACTS, CS, HS)
+                              ATT, PROBS, RES, ACTS, CS, HS, U if ctx.u_grad else None, vm if ctx.u_grad else None)
         ctx.meta = (tuple(level_T), int(rd1_rows), video_csr)
         return HS
 
@@ -117,7 +122,8 @@ class CaptionDecodeFunction(Function):
     @once_differentiable
     def backward(ctx, dHS):
         (value, off_hs, ref, W_h, W_ctx, alpha_w, W_att, pad_mask, row_video, HP, CLIP, LOC, ATT, PROBS, RES, ACTS,
-         CS, HS) = ctx.saved_tensors
+         CS, HS, U, vm) = ctx.saved_tensors
+        u_grad = ctx.u_grad
         level_T, rd1_rows, video_csr = ctx.meta
         dHS = dHS.contiguous()
         Nv, S, M, D = value.shape
@@ -160,12 +166,20 @@ class CaptionDecodeFunction(Function):
                 _n.call("pdvc_softattn_backward_f32", _n.ptr(ATT[i]), ah, ldh, _n.ptr(alpha_w), _n.ptr(CLIP[i]),
                         _n.ptr(PROBS[i]), _n.ptr(dRES), R, M, A, D, _n.ptr(dATT[i]), gah, ldgah, _n.ptr(dCLIP),
                         _n.ptr(GAW[i]), _n.ptr(GAB[i]), st)
-                dCLIP.view(-1, D).addmm_(dATT[i], W_ctx)
-                _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video),
-                        _n.ptr(HP[i]), Ph, 0, _n.ptr(off_hs), _n.ptr(ref), RD, rd1_rows, lvl, nl, Nv, R, M, D, NS // nl,
-                        _n.ptr(LOC[i]), _n.ptr(dCLIP), None if deferred else _n.ptr(gv), _n.ptr(dHP[i]), _n.ptr(gr), st)
+                if u_grad:  # dCLIP keeps the soft-attention part only; att's location gradient read off U
+                    _n.call("pdvc_cap_gather_backward2_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video),
+                            _n.ptr(HP[i]), Ph, 0, _n.ptr(off_hs), _n.ptr(ref), RD, rd1_rows, lvl, nl, Nv, R, M, D,
+                            NS // nl, _n.ptr(LOC[i]), _n.ptr(dCLIP), None, _n.ptr(dHP[i]), _n.ptr(gr), _n.ptr(U),
+                            _n.ptr(dATT[i]), st)
+                else:
+                    dCLIP.view(-1, D).addmm_(dATT[i], W_ctx)
+                    _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video),
+                            _n.ptr(HP[i]), Ph, 0, _n.ptr(off_hs), _n.ptr(ref), RD, rd1_rows, lvl, nl, Nv, R, M, D,
+                            NS // nl, _n.ptr(LOC[i]), _n.ptr(dCLIP), None if deferred else _n.ptr(gv), _n.ptr(dHP[i]),
+                            _n.ptr(gr), st)
                 if i > 0:
                     torch.mm(dHP[i], W_h, out=dh)
+        lsums = None
         if deferred:
             vr_start, vr_rows, max_rows = video_csr
             lsums = torch.empty(Nv, nl, M * D, dtype=gv.dtype, device=gv.device) if ctx.flat_value else None
@@ -180,15 +194,34 @@ class CaptionDecodeFunction(Function):
         else:
             dW_h = torch.zeros_like(W_h)
         db_h = colsum(dHP.view(-1, Ph))
-        dA2 = dATT.view(-1, A)
-        dW_ctx = wgrad_mm(dA2, CLIP.view(-1, D))
-        db_ctx = colsum(dA2)
+        if u_grad:
+            # dU = dATT scattered onto the value rows with the sampling weights (no padding mask: U's padded rows are
+            # the bias), with its per-(video, level) row sums
+            dU = torch.empty((Nv, S, M, A), **kw)
+            lsU = torch.empty((Nv, nl, M * A), **kw)
+            _n.call("pdvc_cap_value_grad_ex_f32", None, lvl, nl, Nv, M, A, NS // nl, R, n, int(max_rows),
+                    _n.ptr(vr_start), _n.ptr(vr_rows), _n.ptr(LOC), _n.ptr(dATT), _n.ptr(dU), _n.ptr(lsU), st)
+            dU2 = dU.view(-1, A)
+            dW_ctx = wgrad_mm(dU2, vm.reshape(-1, D))
+            db_ctx = lsU.view(-1, A).sum(0)  # the weights of a sample sum to 1: sum dU = sum dATT
+            if pad_mask is None:
+                gv.view(-1, D).addmm_(dU2, W_ctx)
+                if lsums is not None:  # the level sums of gv gain those of dU W_ctx
+                    lsums.view(-1, D).addmm_(lsU.view(-1, A), W_ctx)
+            else:  # vm = value with its padded rows zeroed: no gradient reaches them
+                t = torch.mm(dU2, W_ctx).view(Nv, S, M, D)
+                gv.add_(t.masked_fill_(pad_mask.view(Nv, S, 1, 1).bool(), 0.0))
+                lsums = None  # (the consumer falls back to a column sum)
+        else:
+            dA2 = dATT.view(-1, A)
+            dW_ctx = wgrad_mm(dA2, CLIP.view(-1, D))
+            db_ctx = colsum(dA2)
         dalpha_w = colsum(GAW.view(-1, A))
         dalpha_b = GAB.sum().reshape(1)
         dW_att = wgrad_mm(d_gates.reshape(-1, G), RES.view(-1, M * D))
         if ctx.flat_value:
             gv = gv.view(Nv, -1, M * D)
-            if deferred:
+            if deferred and lsums is not None:
                 tag_level_sums(gv, lsums)
         return (gv, d_gates, d_hs_g, d_off_hs, gr, dW_h, db_h, dW_ctx, db_ctx, dalpha_w, dalpha_b, dW_att, None, None,
                 None, None, None, None)

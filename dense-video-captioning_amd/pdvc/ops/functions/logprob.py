@@ -10,6 +10,7 @@ import torch
 from torch.autograd import Function
 
 from pdvc import _native as _n
+from pdvc.precision import attach_bf16, shadow_for
 
 
 class LogProbPickFunction(Function):
@@ -39,8 +40,19 @@ class LogProbPickFunction(Function):
             g_picked = logp.new_zeros(tgt.shape)
         g_picked = g_picked.contiguous()
         grad = torch.empty_like(logp)
-        _n.call("pdvc_logprob_pick_backward_f32", _n.ptr(logp), _n.ptr(tgt), _n.ptr(g_picked), tgt.numel(), V,
-                _n.ptr(grad), _n.stream())
+        g16 = shadow_for(grad) if g_logp is None else None  # bf16 mode: the logit GEMMs' operand, same pass
+        done = False
+        if g16 is not None:
+            try:
+                _n.call("pdvc_logprob_pick_backward_f32_bf16out", _n.ptr(logp), _n.ptr(tgt), _n.ptr(g_picked),
+                        tgt.numel(), V, _n.ptr(grad), _n.ptr(g16), _n.stream())
+                attach_bf16(grad, g16)
+                done = True
+            except _n.NativeError:  # not the register-resident row form: the GEMMs cast grad themselves
+                pass
+        if not done:
+            _n.call("pdvc_logprob_pick_backward_f32", _n.ptr(logp), _n.ptr(tgt), _n.ptr(g_picked), tgt.numel(), V,
+                    _n.ptr(grad), _n.stream())
         if g_logp is not None:
             grad.add_(g_logp - logp.exp() * g_logp.sum(-1, keepdim=True))
         return grad, None

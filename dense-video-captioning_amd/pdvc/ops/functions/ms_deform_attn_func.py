@@ -16,6 +16,7 @@ from torch.autograd.function import once_differentiable
 
 import MultiScaleDeformableAttention as MSDA
 from pdvc import _native as _n
+from pdvc.precision import attach_bf16, shadow_for
 
 NUM_SAMPLES = 16  # levels x points on the fused paths
 NUM_SAMPLES_FUSED = NUM_SAMPLES
@@ -109,9 +110,18 @@ def msda1d_forward(value, pad_mask, proj, ref, level_T, off_base, logit_base, sa
         # level-major (N, M, L, Lq, P): the kernels' layout (include/pdvc_msda.h)
         save_attn = torch.empty((N, M, nl, Lq, NUM_SAMPLES // nl), dtype=value.dtype, device=value.device)
         save_loc = torch.empty_like(save_attn)
-    _n.call("pdvc_msda1d_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(proj), C, off_base, logit_base,
-            _n.ptr(ref), RD, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(out), _n.ptr(save_attn),
-            _n.ptr(save_loc), _n.stream(), meta=(N, Lq, S, M, D, NUM_SAMPLES))
+    args = (_n.ptr(value), _n.ptr(pad_mask), _n.ptr(proj), C, off_base, logit_base, _n.ptr(ref), RD, lvl, nl, N, Lq,
+            M, D, NUM_SAMPLES // nl, _n.ptr(out), _n.ptr(save_attn), _n.ptr(save_loc))
+    meta = (N, Lq, S, M, D, NUM_SAMPLES)
+    out16 = shadow_for(out) if Lq == S else None  # bf16 mode, encoder: the output projection's operand
+    if out16 is not None:
+        try:
+            _n.call("pdvc_msda1d_forward_f32_bf16out", *args, _n.ptr(out16), _n.stream(), meta=meta)
+            attach_bf16(out, out16)
+            return out, save_attn, save_loc
+        except _n.NativeError:  # not the pyramid path: the GEMM casts the output itself
+            pass
+    _n.call("pdvc_msda1d_forward_f32", *args, _n.stream(), meta=meta)
     return out, save_attn, save_loc
 
 
@@ -133,10 +143,23 @@ def msda1d_backward(value, pad_mask, proj, ref, save_attn, save_loc, out, grad_o
     gp = torch.zeros_like(proj) if C != 2 * M * NUM_SAMPLES else torch.empty_like(proj)
     gr = torch.empty_like(ref) if need_ref else None
     ls = torch.empty(N, nl, M * D, dtype=value.dtype, device=value.device) if level_sums else None
-    _n.call("pdvc_msda1d_backward_ex_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(ref), RD, _n.ptr(proj), C,
-            off_base, logit_base, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl, _n.ptr(grad_out),
-            _n.ptr(out) if _DELTA_FROM_OUT else None, _n.ptr(save_attn), _n.ptr(save_loc), _n.ptr(gv), _n.ptr(gp), _n.ptr(gr), _n.ptr(ls),
-            _n.stream(), meta=(N, Lq, S, M, D, NUM_SAMPLES))
+    args = (_n.ptr(value), _n.ptr(pad_mask), _n.ptr(ref), RD, _n.ptr(proj), C, off_base, logit_base, lvl, nl, N, Lq, M,
+            D, NUM_SAMPLES // nl, _n.ptr(grad_out), _n.ptr(out) if _DELTA_FROM_OUT else None, _n.ptr(save_attn),
+            _n.ptr(save_loc), _n.ptr(gv), _n.ptr(gp), _n.ptr(gr), _n.ptr(ls))
+    meta = (N, Lq, S, M, D, NUM_SAMPLES)
+    done = False
+    gv16 = shadow_for(gv) if Lq == S else None  # bf16 mode, encoder: the projections' gradient-GEMM operands
+    if gv16 is not None:
+        gp16 = shadow_for(gp)
+        try:
+            _n.call("pdvc_msda1d_backward_ex_f32_bf16out", *args, _n.ptr(gv16), _n.ptr(gp16), _n.stream(), meta=meta)
+            attach_bf16(gv, gv16)
+            attach_bf16(gp, gp16)
+            done = True
+        except _n.NativeError:  # not the pyramid path: the GEMMs cast the gradients themselves
+            pass
+    if not done:
+        _n.call("pdvc_msda1d_backward_ex_f32", *args, _n.stream(), meta=meta)
     return (gv, gp, gr, ls) if level_sums else (gv, gp, gr)
 
 

@@ -9,6 +9,7 @@ from torch.autograd import Function
 from torch.autograd.function import once_differentiable
 
 from pdvc import _native as _n
+from pdvc.precision import attach_bf16, shadow_for
 
 
 class LevelPosRowsFunction(Function):
@@ -83,9 +84,15 @@ class LevelPos:
     def _call(self, add):
         N, S = self.xe.shape
         out = torch.empty(self.shape, dtype=torch.float32, device=self.xe.device)
-        _n.call("pdvc_level_pos_rows_add_f32", _n.ptr(self.xe), _n.ptr(self.dim_t), _n.ptr(self.dur),
-                _n.ptr(self.level_embed), _n.int_array(self.level_T), len(self.level_T), N, S, self.dim_t.numel(),
-                self.dur.shape[1], _n.ptr(add), _n.ptr(out), _n.stream())
+        args = (_n.ptr(self.xe), _n.ptr(self.dim_t), _n.ptr(self.dur), _n.ptr(self.level_embed),
+                _n.int_array(self.level_T), len(self.level_T), N, S, self.dim_t.numel(), self.dur.shape[1],
+                _n.ptr(add), _n.ptr(out))
+        out16 = shadow_for(out) if add is not None else None  # bf16 mode: the query projection's operand
+        if out16 is None:
+            _n.call("pdvc_level_pos_rows_add_f32", *args, _n.stream())
+        else:
+            _n.call("pdvc_level_pos_rows_add_f32_bf16out", *args, _n.ptr(out16), _n.stream())
+            attach_bf16(out, out16)
         return out
 
     def add_to(self, x):

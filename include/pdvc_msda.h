@@ -170,6 +170,23 @@ int pdvc_msda1d_backward_ex_f32(const float* value, const uint8_t* value_pad_mas
                                 int head_dim, int num_point, const float* grad_output, const float* output,
                                 const float* save_attn, const float* save_loc, float* grad_value, float* grad_proj,
                                 float* grad_ref, float* grad_value_level_sums, void* stream);
+/* bf16 mode (pdvc/precision.py): the same passes, also writing the bf16 roundings (torch's RNE cast) of output /
+ * grad_value / grad_proj, the operands of the projections' GEMMs -- only on the encoder's pyramid path (Lq = S,
+ * head_dim 64, level 0 <= 512 positions; the backward also needs proj_stride = 2 * num_heads * 16); any other
+ * call returns PDVC_ERR_UNSUPPORTED before launching anything. */
+int pdvc_msda1d_forward_f32_bf16out(const float* value, const uint8_t* value_pad_mask, const float* proj,
+                                    int proj_stride, int off_base, int logit_base, const float* ref, int ref_dim,
+                                    const int32_t* level_T, int num_levels, int batch, int num_query, int num_heads,
+                                    int head_dim, int num_point, float* output, float* save_attn, float* save_loc,
+                                    uint16_t* output16, void* stream);
+int pdvc_msda1d_backward_ex_f32_bf16out(const float* value, const uint8_t* value_pad_mask, const float* ref,
+                                        int ref_dim, const float* proj, int proj_stride, int off_base, int logit_base,
+                                        const int32_t* level_T, int num_levels, int batch, int num_query,
+                                        int num_heads, int head_dim, int num_point, const float* grad_output,
+                                        const float* output, const float* save_attn, const float* save_loc,
+                                        float* grad_value, float* grad_proj, float* grad_ref,
+                                        float* grad_value_level_sums, uint16_t* grad_value16,
+                                        uint16_t* grad_proj16, void* stream);
 
 /* ---- caption-head border gather (MSDeformAttnCap) ----------------------------------------------------
  * value (N,S,M,D); value_pad_mask (N,S) or NULL; row_video (R,) int32 DEVICE: video of each query row;
@@ -194,6 +211,16 @@ int pdvc_cap_gather_backward_f32(const float* value, const uint8_t* value_pad_ma
                                  int batch, int rows, int num_heads, int head_dim, int num_point,
                                  const float* save_loc, const float* grad_samples, float* grad_value,
                                  float* grad_offsets, float* grad_ref, void* stream);
+/* The same with a second tensor sampled at the same locations (value2, same shape as value, no padding mask;
+ * grad_samples2 its sample gradients, same shape as grad_samples): its location gradient is added to the offset and
+ * reference gradients -- the caption head's ctx2att rows projected once (pdvc/ops/functions/caption_decode.py). */
+int pdvc_cap_gather_backward2_f32(const float* value, const uint8_t* value_pad_mask, const int32_t* row_video,
+                                  const float* offsets, int off_stride, int off_col0, const float* off_add,
+                                  const float* ref, int ref_dim, int rd1_rows, const int32_t* level_T, int num_levels,
+                                  int batch, int rows, int num_heads, int head_dim, int num_point,
+                                  const float* save_loc, const float* grad_samples, float* grad_value,
+                                  float* grad_offsets, float* grad_ref, const float* value2,
+                                  const float* grad_samples2, void* stream);
 
 /* ---- decoder query self-attention core (nn.MultiheadAttention, batch-first) -------------------------
  * qk (N,Q,2E) = [q | k] in-projections (E = num_heads*head_dim), v (N,Q,E); key_padding_mask (N,Q) uint8,
@@ -357,6 +384,10 @@ int pdvc_level_pos_rows_backward_f32(const float* dpos, const int32_t* level_T, 
 int pdvc_level_pos_rows_add_f32(const float* xe, const float* dim_t, const float* dur, const float* level_embed,
                                 const int32_t* level_T, int num_levels, int N, int S, int F, int Dd, const float* add,
                                 float* out, void* stream);
+/* bf16 mode (pdvc/precision.py): the same, also writing out16 = out rounded to bf16 (torch's RNE cast). */
+int pdvc_level_pos_rows_add_f32_bf16out(const float* xe, const float* dim_t, const float* dur,
+                                        const float* level_embed, const int32_t* level_T, int num_levels, int N, int S,
+                                        int F, int Dd, const float* add, float* out, uint16_t* out16, void* stream);
 
 /* ---- FFN relu + dropout --------------------------------------------------------------------------------
  * forward, in place on h (rows x cols, cols % 4 == 0, 16-byte aligned): h = relu(h) * keep / (1 - p), keep a
@@ -384,6 +415,11 @@ int pdvc_logprob_pick_forward_f32(const float* logits, const int64_t* target, in
                                   float* picked, void* stream);
 int pdvc_logprob_pick_backward_f32(const float* logp, const int64_t* target, const float* grad_picked, int rows,
                                    int V, float* grad_logits, void* stream);
+/* bf16 mode (pdvc/precision.py): the same, also writing grad16 = grad_logits rounded to bf16 (torch's RNE cast) --
+ * only in the register-resident row form (V % 4 == 0, V <= 8192, 16-byte aligned rows; else PDVC_ERR_UNSUPPORTED
+ * and nothing is launched). */
+int pdvc_logprob_pick_backward_f32_bf16out(const float* logp, const int64_t* target, const float* grad_picked,
+                                           int rows, int V, float* grad_logits, uint16_t* grad16, void* stream);
 /* greedy decoding's word choice (LSTM_DSA.py:149-151, torch.max over log_softmax(logits)): index[r] = the first index
  * of the largest logit of row r, logp_max[r] = its log-probability (x_max - max) - log(sum exp(x - max)); one read
  * of the logits, the (rows, V) log-probabilities are not written. */

@@ -346,6 +346,92 @@ def test_bf16out_entry_points_round_like_torch():
     assert torch.equal(_bits(ds16), _bits(grads[1][1].to(torch.bfloat16))), "add-norm backward bf16 rounding"
 
 
+def test_logprob_backward_bf16out_rounds_like_torch():
+    """pdvc_logprob_pick_backward_f32_bf16out: the same fp32 logit gradient as the plain form and, beside it, torch's
+    bf16 cast of it bit for bit (vocabulary 5748, the cfg-2 size); a row form it cannot serve (V % 4 != 0) is refused
+    with nothing written."""
+    from pdvc import _native as _n
+    g = torch.Generator(device=DEV).manual_seed(9)
+    rows, V = 333, 5748
+    logits = torch.randn(rows, V, device=DEV, generator=g) * 4
+    logp = torch.log_softmax(logits, -1).contiguous()
+    tgt = torch.randint(0, V, (rows,), device=DEV, generator=g)
+    gp = torch.randn(rows, device=DEV, generator=g)
+    ref = torch.empty_like(logp)
+    got = torch.empty_like(logp)
+    g16 = torch.empty(rows, V, device=DEV, dtype=torch.bfloat16)
+    _n.call("pdvc_logprob_pick_backward_f32", _n.ptr(logp), _n.ptr(tgt), _n.ptr(gp), rows, V, _n.ptr(ref), _n.stream())
+    _n.call("pdvc_logprob_pick_backward_f32_bf16out", _n.ptr(logp), _n.ptr(tgt), _n.ptr(gp), rows, V, _n.ptr(got),
+            _n.ptr(g16), _n.stream())
+    assert torch.equal(got, ref)
+    assert torch.equal(_bits(g16), _bits(ref.to(torch.bfloat16)))
+    odd = torch.empty(rows, V - 1, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(_n.NativeError):
+        _n.call("pdvc_logprob_pick_backward_f32_bf16out", _n.ptr(logp[:, :-1].contiguous()), _n.ptr(tgt), _n.ptr(gp),
+                rows, V - 1, _n.ptr(torch.empty(rows, V - 1, device=DEV)), _n.ptr(odd), _n.stream())
+
+
+def test_msda_bf16out_rounds_like_torch():
+    """The encoder MSDA's bf16 forms (pdvc_msda1d_forward_f32_bf16out / pdvc_msda1d_backward_ex_f32_bf16out, the
+    pyramid path at the cfg-2 shape T = 256): the same fp32 output and gradients as the plain forms, and beside them
+    torch's bf16 casts of output, grad_value and grad_proj bit for bit; a decoder-shaped call (Lq != S) is refused."""
+    from pdvc import _native as _n
+    from pdvc.ops.functions.ms_deform_attn_func import NUM_SAMPLES, _levels
+    g = torch.Generator(device=DEV).manual_seed(4)
+    T_l = (256, 128, 64, 32)
+    N, S, M, D = 3, sum(T_l), 8, 64
+    lvl, nl = _levels(T_l)
+    value = torch.randn(N, S, M, D, device=DEV, generator=g)
+    proj = torch.cat([torch.randn(N, S, M * 16, device=DEV, generator=g) * 2,
+                      torch.randn(N, S, M * 16, device=DEV, generator=g)], -1).contiguous()
+    ref = torch.cat([(torch.arange(t, device=DEV) + 0.5) / t for t in T_l])[None, :, None, None]
+    ref = ref.expand(N, S, 4, 1).contiguous()
+    C = proj.shape[2]
+
+    def fwd(bf):
+        out = torch.empty(N, S, M * D, device=DEV)
+        sa = torch.empty(N, M, nl, S, NUM_SAMPLES // nl, device=DEV)
+        sl = torch.empty_like(sa)
+        a = (_n.ptr(value), None, _n.ptr(proj), C, 0, M * 16, _n.ptr(ref), 1, lvl, nl, N, S, M, D, NUM_SAMPLES // nl,
+             _n.ptr(out), _n.ptr(sa), _n.ptr(sl))
+        o16 = torch.empty(N, S, M * D, device=DEV, dtype=torch.bfloat16)
+        if bf:
+            _n.call("pdvc_msda1d_forward_f32_bf16out", *a, _n.ptr(o16), _n.stream())
+        else:
+            _n.call("pdvc_msda1d_forward_f32", *a, _n.stream())
+        return out, sa, sl, o16
+
+    o0, sa, sl, _ = fwd(False)
+    o1, sa1, sl1, o16 = fwd(True)
+    assert torch.equal(o0, o1) and torch.equal(sa, sa1) and torch.equal(sl, sl1)
+    assert torch.equal(_bits(o16), _bits(o0.to(torch.bfloat16)))
+    gout = torch.randn(N, S, M * D, device=DEV, generator=g)
+
+    def bwd(bf):
+        gv = torch.empty_like(value)
+        gp = torch.empty_like(proj)
+        a = (_n.ptr(value), None, _n.ptr(ref), 1, _n.ptr(proj), C, 0, M * 16, lvl, nl, N, S, M, D, NUM_SAMPLES // nl,
+             _n.ptr(gout), None, _n.ptr(sa), _n.ptr(sl), _n.ptr(gv), _n.ptr(gp), None, None)
+        gv16 = torch.empty(gv.shape, device=DEV, dtype=torch.bfloat16)
+        gp16 = torch.empty(gp.shape, device=DEV, dtype=torch.bfloat16)
+        if bf:
+            _n.call("pdvc_msda1d_backward_ex_f32_bf16out", *a, _n.ptr(gv16), _n.ptr(gp16), _n.stream())
+        else:
+            _n.call("pdvc_msda1d_backward_ex_f32", *a, _n.stream())
+        return gv, gp, gv16, gp16
+
+    gv0, gp0, _, _ = bwd(False)
+    gv1, gp1, gv16, gp16 = bwd(True)
+    assert torch.equal(gp0, gp1) and (gv1 - gv0).abs().max().item() <= 1e-6 * gv0.abs().max().item()
+    assert torch.equal(_bits(gv16), _bits(gv1.to(torch.bfloat16)))
+    assert torch.equal(_bits(gp16), _bits(gp1.to(torch.bfloat16)))
+    out = torch.empty(N, 100, M * D, device=DEV)
+    with pytest.raises(_n.NativeError):
+        _n.call("pdvc_msda1d_forward_f32_bf16out", _n.ptr(value), None, _n.ptr(proj[:, :100].contiguous()), C, 0,
+                M * 16, _n.ptr(ref[:, :100].contiguous()), 1, lvl, nl, N, 100, M, D, NUM_SAMPLES // nl, _n.ptr(out),
+                None, None, _n.ptr(torch.empty(N, 100, M * D, device=DEV, dtype=torch.bfloat16)), _n.stream())
+
+
 def test_cfg2_bf16_step_with_producer_shadows_equals_cast_passes():
     """The bf16 step with the producing kernels writing the bf16 operands (add-norm, relu-dropout) equals the step
     whose every operand is a cast pass as closely as two runs of the cast-pass step equal each other: the same

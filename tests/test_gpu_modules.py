@@ -390,6 +390,70 @@ def test_caption_value_grad_chunked_steps():
     close(run(video_csr), run(None), 1e-4, "grad_memory")
 
 
+@pytest.mark.parametrize("masked,heads", [(False, 1), (True, 1), (False, 2)])
+def test_caption_decode_projected_row_backward_equals_per_sample(masked, heads):
+    """The caption recurrence's backward in the projected-row form (caption_decode.U_GRAD: dATT scattered onto the
+    value rows once, dW_ctx = dU^T value, the value gradient's ctx2att part dU W_ctx, the location gradient of
+    att read off U at the sample corners) against the per-sample form (dclip += dATT W_ctx each step, dW_ctx over
+    every sample): every input and parameter gradient within 1e-4 * max|ref|, with and without padded frames."""
+    import types
+    import pdvc.ops.functions.caption_decode as CD
+    from pdvc.CaptioningHead.LSTM_DSA import LSTMDSACaptioner
+    opt = types.SimpleNamespace(
+        vocab_size=40, input_encoding_size=512, rnn_size=512, num_layers=1, drop_prob=0.0, max_caption_len=10,
+        clip_context_dim=512, cap_nheads=heads, att_hid_size=512, wordRNN_input_feats_type="C", hidden_dim=512,
+        cap_num_feature_levels=4, cap_dec_n_points=4, num_feature_levels=4, event_context_dim=None)
+    torch.manual_seed(3)
+    cap = LSTMDSACaptioner(opt).to(DEV)
+    with torch.no_grad():
+        for p in cap.parameters():
+            p.normal_(0, 0.03)
+    T_l = (64, 32, 16, 8)
+    S = sum(T_l)
+    Nv, R, n = 3, 24, 8
+    memory = torch.randn(Nv, S, 512, device=DEV)
+    mask = torch.zeros(Nv, S, dtype=torch.bool, device=DEV)
+    if masked:
+        mask[1, 50:64] = True
+        mask[1, 90:96] = True
+    hs = torch.randn(R, 512, device=DEV)
+    ref = torch.rand(R, 4, 2, device=DEV) * 0.9 + 0.05
+    rv = [i % 3 if i % 7 else 1 for i in range(R)]
+    row_video = torch.tensor(rv, dtype=torch.int32, device=DEV)
+    starts, flat = [0], []
+    for v in range(Nv):
+        flat += [i for i in range(R) if rv[i] == v]
+        starts.append(len(flat))
+    video_csr = (torch.tensor(starts, dtype=torch.int32, device=DEV),
+                 torch.tensor(flat, dtype=torch.int32, device=DEV), max(rv.count(v) for v in range(Nv)))
+    seq = torch.randint(1, 41, (R, n + 1), device=DEV)
+    g = torch.randn(R, n, 41, device=DEV)
+
+    def run(u_grad):
+        CD.U_GRAD = u_grad
+        try:
+            cap.zero_grad(set_to_none=True)
+            ins = [t.clone().requires_grad_() for t in (hs, ref, memory)]
+            out = cap.decode_teacher_forced(ins[0], ins[1], 5, row_video, ins[2], mask, T_l, seq, n,
+                                            video_csr=video_csr)
+            (out * g).sum().backward()
+            return [t.grad.clone() for t in ins], {k: p.grad.clone() for k, p in cap.named_parameters()
+                                                   if p.grad is not None}
+        finally:
+            CD.U_GRAD = True
+
+    gi0, gp0 = run(False)
+    gi1, gp1 = run(True)
+    for name, a, b in zip(("hs", "ref", "memory"), gi1, gi0):
+        close(a, b, 1e-4, "grad_" + name)
+    assert set(gp1) == set(gp0)
+    for k in gp0:
+        if k.endswith("alpha_net.bias"):
+            assert_close(gp1[k], gp0[k], k, 1e-4, scale=gp0[k[:-4] + "weight"].abs().max().item())
+        else:
+            close(gp1[k], gp0[k], 1e-4, k)
+
+
 @pytest.mark.parametrize("masked", [False, True])
 def test_greedy_ctx2att_gather_equals_gemm(masked):
     """Greedy decoding's ctx2att as a gather of the once-projected memory rows (U = ctx2att(value), blended with

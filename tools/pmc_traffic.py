@@ -1,11 +1,13 @@
 """HBM traffic per launch of one kernel from two rocprofv3 --pmc passes (MI355X_MICROARCH.md section HBM):
     rocprofv3 --pmc FETCH_SIZE --kernel-include-regex K --output-format csv -d DIR/fetch -- python bench.py ...
     rocprofv3 --pmc WRITE_SIZE --kernel-include-regex K --output-format csv -d DIR/write -- python bench.py ...
-    python tools/pmc_traffic.py DIR KERNEL_SUBSTRING OUT.json [--largest-grid]
+    python tools/pmc_traffic.py DIR KERNEL_SUBSTRING OUT.json [--largest-grid | --large-launches]
 FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide (16 B/lane)
 stream, so traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 -- the kernels priced here read their value rows
 with 16-B loads.  Launches are grouped by grid size (encoder vs decoder calls) and averaged; --largest-grid prices
-only the group of the largest grid (the encoder's launches of a kernel both call sites use)."""
+only the group of the largest grid; --large-launches only the launches whose FETCH_SIZE is at least half the
+largest (the encoder's launches of a kernel both call sites launch on the same grid, e.g. the value-gradient
+kernel, one workgroup per (video, head, level) for the encoder and the decoder alike)."""
 import collections
 import csv
 import glob
@@ -46,6 +48,12 @@ def main():
         total += b * len(v["fetch_kib"])
         n += len(v["fetch_kib"])
     res["avg_bytes_per_launch"] = total / max(n, 1)
+    if "--large-launches" in sys.argv and fetch:
+        top = max(fetch.values())
+        sel = [d for d, v in fetch.items() if v >= 0.5 * top and d in write]
+        b = sum((2 * fetch[d] + write[d]) * 1024 for d in sel) / max(len(sel), 1)
+        res["large_launches"] = {"launches": len(sel), "bytes": b}
+        res["avg_bytes_per_launch"] = b
     if "--largest-grid" in sys.argv and res["by_grid"]:
         g = max(res["by_grid"], key=lambda k: int(k) if str(k).isdigit() else -1)
         res["avg_bytes_per_launch"] = res["by_grid"][g]["bytes"]
