@@ -1020,7 +1020,9 @@ constexpr int kBqQPS = 15;                                   // queries per 16-l
 constexpr int kBqQ = (kPyrThreads / 16) * kBqQPS;            // 960 queries per workgroup
 constexpr size_t kBqLds = kPyrLds + (size_t)kBqQ * 4 * sizeof(float);
 
-template <int RD>
+// QU: queries of a lane group run back to back per loop trip (interleavable by the scheduler: each query is a
+// dependent chain of LDS reads, a 16-lane reduction and the owner math, and the LDS caps the CU at 4 waves/SIMD)
+template <int RD, int QU = 1>
 __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
     int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
@@ -1047,122 +1049,140 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
     const int base_own = pyr_base(lv, l_own);
     const char* lrow = reinterpret_cast<const char*>(lds4) + sub * 16;  // this lane's 16 B of every LDS row
 
-    // one query of this lane group through the levels [L0, L1): the lane's own sample parameters, the dot products
-    // of every sample of those levels from LDS, reduced onto their owner lanes; then the owner math of the lanes
-    // whose level is in range (offset gradient, grad_ref, dL/da)
-    auto run_query = [&](int i, auto L0c, auto L1c) {
+    // QU queries of this lane group (queries i0, i0 + 1, ..) through the levels [L0, L1): the lanes' own sample
+    // parameters, the dot products of every sample of those levels from LDS reduced onto their owner lanes, then the
+    // owner math of the lanes whose level is in range (offset gradient, grad_ref, dL/da).  The QU queries' loads, LDS
+    // reads and reductions are independent chains written side by side, so they overlap (the carry / gradient
+    // stores come last: they would otherwise order the next query's LDS reads behind them)
+    auto run_queries = [&](int i0q, auto L0c, auto L1c) {
         constexpr int L0 = decltype(L0c)::value, L1 = decltype(L1c)::value;
-        const int q0 = qb * kBqQ + slot + 64 * i;
-        const bool act = q0 < Lq;
-        const int q = act ? q0 : Lq - 1;
-        const size_t row = (size_t)b * Lq + q;
-        const float4 g = *reinterpret_cast<const float4*>(gout + row * MD + (size_t)m * 64 + sub * 4);
-        const size_t si = save_index(b, m, l_own, q, p_own, Lq, M);
-        const float x = save_loc[si] * Tf - 0.5f;
-        const float a = save_attn[si];
-        const bool inside = x > -1.f && x < Tf;
-        const float xf = floorf(inside ? x : 0.f);
-        const int i0 = (int)xf;
-        const float lw = inside ? x - xf : 0.f;
-        const int ad = pyr_corner(base_own, i0);  // guarded layout: no clamps (msda1d_fwd_pyr_kernel)
-        float d1 = 0.f, d2 = 0.f;
+        bool act[QU], inside[QU];
+        size_t row[QU];
+        float4 g[QU];
+        float a[QU], lw[QU], d1[QU], d2[QU];
+        int i0[QU], ad[QU];
+#pragma unroll
+        for (int u = 0; u < QU; ++u) {
+            const int q0 = qb * kBqQ + slot + 64 * (i0q + u);
+            act[u] = q0 < Lq;
+            const int q = act[u] ? q0 : Lq - 1;
+            row[u] = (size_t)b * Lq + q;
+            g[u] = *reinterpret_cast<const float4*>(gout + row[u] * MD + (size_t)m * 64 + sub * 4);
+            const size_t si = save_index(b, m, l_own, q, p_own, Lq, M);
+            const float x = save_loc[si] * Tf - 0.5f;
+            a[u] = save_attn[si];
+            inside[u] = x > -1.f && x < Tf;
+            const float xf = floorf(inside[u] ? x : 0.f);
+            i0[u] = (int)xf;
+            lw[u] = inside[u] ? x - xf : 0.f;
+            ad[u] = pyr_corner(base_own, i0[u]);  // guarded layout: no clamps (msda1d_fwd_pyr_kernel)
+            d1[u] = 0.f;
+            d2[u] = 0.f;
+        }
 #pragma unroll
         for (int L = L0; L < L1; ++L) {
-            float part[8];
 #pragma unroll
-            for (int p = 0; p < kP; ++p) {
-                const char* r = lrow + grp_bcast<16>(ad, L * kP + p);
-                const float4 u1 = *reinterpret_cast<const float4*>(r);
-                const float4 u2 = *reinterpret_cast<const float4*>(r + 256);
-                part[p] = g.x * u1.x + g.y * u1.y + g.z * u1.z + g.w * u1.w;
-                part[4 + p] = g.x * u2.x + g.y * u2.y + g.z * u2.z + g.w * u2.w;
-            }
-            const bool u8 = (lane & 8) != 0;
+            for (int u = 0; u < QU; ++u) {
+                float part[8];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float send = u8 ? part[k] : part[k + 4];
-                const float mine = u8 ? part[k + 4] : part[k];
-                part[k] = mine + grp_swap(send, 8);
-            }
-            const bool u2b = (lane & 2) != 0;
+                for (int p = 0; p < kP; ++p) {
+                    const char* r = lrow + grp_bcast<16>(ad[u], L * kP + p);
+                    const float4 u1 = *reinterpret_cast<const float4*>(r);
+                    const float4 u2 = *reinterpret_cast<const float4*>(r + 256);
+                    part[p] = g[u].x * u1.x + g[u].y * u1.y + g[u].z * u1.z + g[u].w * u1.w;
+                    part[4 + p] = g[u].x * u2.x + g[u].y * u2.y + g[u].z * u2.z + g[u].w * u2.w;
+                }
+                const bool u8 = (lane & 8) != 0;
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const float send = u2b ? part[k] : part[k + 2];
-                const float mine = u2b ? part[k + 2] : part[k];
-                part[k] = mine + grp_swap(send, 2);
-            }
-            const bool u1b = (lane & 1) != 0;
-            const float send = u1b ? part[0] : part[1];
-            const float mine = u1b ? part[1] : part[0];
-            part[0] = mine + grp_swap(send, 1);
-            part[0] += grp_swap(part[0], 4);
-            const float other = grp_swap(part[0], 8);
-            if (l_own == L) {
-                d1 = (L < 2) ? part[0] : other;
-                d2 = (L < 2) ? other : part[0];
+                for (int k = 0; k < 4; ++k) {
+                    const float send = u8 ? part[k] : part[k + 4];
+                    const float mine = u8 ? part[k + 4] : part[k];
+                    part[k] = mine + grp_swap(send, 8);
+                }
+                const bool u2b = (lane & 2) != 0;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const float send = u2b ? part[k] : part[k + 2];
+                    const float mine = u2b ? part[k + 2] : part[k];
+                    part[k] = mine + grp_swap(send, 2);
+                }
+                const bool u1b = (lane & 1) != 0;
+                const float send = u1b ? part[0] : part[1];
+                const float mine = u1b ? part[1] : part[0];
+                part[0] = mine + grp_swap(send, 1);
+                part[0] += grp_swap(part[0], 4);
+                const float other = grp_swap(part[0], 8);
+                if (l_own == L) {
+                    d1[u] = (L < 2) ? part[0] : other;
+                    d2[u] = (L < 2) ? other : part[0];
+                }
             }
         }
         // owner math of the lanes whose sample is in this phase (.cuh:140-170), as msda1d_bwd_query_dot_kernel
         const bool mine_phase = l_own >= L0 && l_own < L1;
-        bool ok1 = inside && i0 >= 0, ok2 = inside && i0 + 1 <= T_own - 1;
-        if (mbase) {
-            ok1 = ok1 && !mbase[st_own + min(max(i0, 0), T_own - 1)];
-            ok2 = ok2 && !mbase[st_own + min(max(i0 + 1, 0), T_own - 1)];
-        }
-        const float x1 = ok1 ? d1 : 0.f, x2 = ok2 ? d2 : 0.f;
-        float ga = (1.f - lw) * x1 + lw * x2;
-        const float gloc = Tf * ((x2 - x1) * a);
-        const float* prow = proj + row * proj_stride;
-        float* gprow = grad_proj + row * proj_stride;
-        float g0 = mine_phase ? gloc : 0.f, g1 = 0.f, goff;
-        if (RD == 1) {
-            goff = gloc / Tf;
-        } else {
-            const float rr1 = ref[(row * kL + l_own) * 2 + 1];
-            const float t2 = gloc * 0.5f;
-            goff = (t2 * rr1) / (float)kP;
-            g1 = mine_phase ? t2 * (prow[off_base + m * kNS + sub] / (float)kP) : 0.f;
-        }
-        if (act && mine_phase) {
-            gprow[off_base + m * kNS + sub] = goff;
-            if (gp16) gp16[row * proj_stride + off_base + m * kNS + sub] = (uint16_t)bf16_bits(goff);
-        }
-        if (grad_ref) {  // per (query, level): the lane quad of the level; heads differ by workgroup: atomics
-            g0 += grp_swap(g0, 1);
-            g0 += grp_swap(g0, 2);
-            if (RD == 2) {
-                g1 += grp_swap(g1, 1);
-                g1 += grp_swap(g1, 2);
+#pragma unroll
+        for (int u = 0; u < QU; ++u) {
+            bool ok1 = inside[u] && i0[u] >= 0, ok2 = inside[u] && i0[u] + 1 <= T_own - 1;
+            if (mbase) {
+                ok1 = ok1 && !mbase[st_own + min(max(i0[u], 0), T_own - 1)];
+                ok2 = ok2 && !mbase[st_own + min(max(i0[u] + 1, 0), T_own - 1)];
             }
-            if (p_own == 0 && act && mine_phase) {
-                float* dst = grad_ref + (row * kL + l_own) * RD;
-                atomicAdd(dst, g0);
-                if (RD == 2) atomicAdd(dst + 1, g1);
+            const float x1 = ok1 ? d1[u] : 0.f, x2 = ok2 ? d2[u] : 0.f;
+            float ga = (1.f - lw[u]) * x1 + lw[u] * x2;
+            const float gloc = Tf * ((x2 - x1) * a[u]);
+            const float* prow = proj + row[u] * proj_stride;
+            float* gprow = grad_proj + row[u] * proj_stride;
+            float g0 = mine_phase ? gloc : 0.f, g1 = 0.f, goff;
+            if (RD == 1) {
+                goff = gloc / Tf;
+            } else {
+                const float rr1 = ref[(row[u] * kL + l_own) * 2 + 1];
+                const float t2 = gloc * 0.5f;
+                goff = (t2 * rr1) / (float)kP;
+                g1 = mine_phase ? t2 * (prow[off_base + m * kNS + sub] / (float)kP) : 0.f;
             }
-        }
-        const int ci = (slot + 64 * i) * 4 + p_own;
-        if (L0 == 0) {  // first phase: level 0's owners carry dL/da to the second
-            if (l_own == 0) carry[ci] = ga;
-        } else {  // second phase: the softmax term over all 16 samples, then every logit gradient
-            if (l_own == 0) ga = carry[ci];
-            const float delta = group_allreduce<16>(a * ga);
-            if (act) {
-                const float gl = a * (ga - delta);
-                gprow[logit_base + m * kNS + sub] = gl;
-                if (gp16) gp16[row * proj_stride + logit_base + m * kNS + sub] = (uint16_t)bf16_bits(gl);
+            if (act[u] && mine_phase) {
+                gprow[off_base + m * kNS + sub] = goff;
+                if (gp16) gp16[row[u] * proj_stride + off_base + m * kNS + sub] = (uint16_t)bf16_bits(goff);
+            }
+            if (grad_ref) {  // per (query, level): the lane quad of the level; heads differ by workgroup: atomics
+                g0 += grp_swap(g0, 1);
+                g0 += grp_swap(g0, 2);
+                if (RD == 2) {
+                    g1 += grp_swap(g1, 1);
+                    g1 += grp_swap(g1, 2);
+                }
+                if (p_own == 0 && act[u] && mine_phase) {
+                    float* dst = grad_ref + (row[u] * kL + l_own) * RD;
+                    atomicAdd(dst, g0);
+                    if (RD == 2) atomicAdd(dst + 1, g1);
+                }
+            }
+            const int ci = (slot + 64 * (i0q + u)) * 4 + p_own;
+            if (L0 == 0) {  // first phase: level 0's owners carry dL/da to the second
+                if (l_own == 0) carry[ci] = ga;
+            } else {  // second phase: the softmax term over all 16 samples, then every logit gradient
+                if (l_own == 0) ga = carry[ci];
+                const float delta = group_allreduce<16>(a[u] * ga);
+                if (act[u]) {
+                    const float gl = a[u] * (ga - delta);
+                    gprow[logit_base + m * kNS + sub] = gl;
+                    if (gp16) gp16[row[u] * proj_stride + logit_base + m * kNS + sub] = (uint16_t)bf16_bits(gl);
+                }
             }
         }
     };
 
     pyr_stage_g(lds4, vsrc, MD, lv.start[0], lv.T[0]);
     __syncthreads();
+    static_assert(kBqQPS % QU == 0, "QU must divide the queries per lane group");
 #pragma unroll 1
-    for (int i = 0; i < kBqQPS; ++i) run_query(i, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+    for (int i = 0; i < kBqQPS; i += QU) run_queries(i, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
     __syncthreads();
     pyr_stage_g(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3]);
     __syncthreads();
 #pragma unroll 1
-    for (int i = 0; i < kBqQPS; ++i) run_query(i, std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{});
+    for (int i = 0; i < kBqQPS; i += QU) run_queries(i, std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{});
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -1186,7 +1206,9 @@ constexpr int kVQPT = 4;  // queries per thread in its sort passes: a launch chu
 // wave-instruction loads the gradient rows of 4 samples (4x fewer loads, LDS index reads and loop iterations).
 // UG: samples in flight per 16-lane group in the G4 walk (8: 96 VGPRs; 4: 66, more workgroups per CU where the LDS
 // allows -- the decoder's short sample lists)
-template <int CW, bool G4, int UG = 8>
+// B16: also writes the bf16 rounding of every row into gv16 (the bf16 mode; a separate instantiation, so the
+// fp32 path keeps its registers: the pointer and its stores cost the depth-8 walk 9 spilled VGPRs)
+template <int CW, bool G4, int UG = 8, bool B16 = false>
 __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
                                                                      int Lq, int q0, int nq, int S, int M, int D,
                                                                      int accumulate,
@@ -1330,12 +1352,12 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
         const int gl = lane & 15;
         float* ob = grad_value + ((size_t)b * S + st) * MD + (size_t)m * D + gl * 4;
         // bf16 mode: the rounding of every row written, at the same offsets (the value projection's operand)
-        uint16_t* ob16 = gv16 ? gv16 + ((size_t)b * S + st) * MD + (size_t)m * D + gl * 4 : nullptr;
+        uint16_t* ob16 = B16 ? gv16 + ((size_t)b * S + st) * MD + (size_t)m * D + gl * 4 : nullptr;
         if (!accumulate)
             for (int t = threadIdx.x >> 4; t < T; t += blockDim.x >> 4)
                 if (off[t] == off[t + 2]) {
                     *reinterpret_cast<float4*>(ob + (size_t)t * MD) = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (ob16) *reinterpret_cast<uint2*>(ob16 + (size_t)t * MD) = make_uint2(0u, 0u);
+                    if (B16) *reinterpret_cast<uint2*>(ob16 + (size_t)t * MD) = make_uint2(0u, 0u);
                 }
         // walk: 16-lane group vg owns rows [r0, r1) and reads buckets r0 .. r1; one sorted entry and one gathered
         // gradient row per sample, two running rows (key - 1 and key), each row written once when its last bucket
@@ -1364,7 +1386,7 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
                         v.w += o.w;
                     }
                     *orow = v;
-                    if (ob16) store_bf16x4(ob16 + (size_t)r * MD, v.x, v.y, v.z, v.w);
+                    if (B16) store_bf16x4(ob16 + (size_t)r * MD, v.x, v.y, v.z, v.w);
                 }
             };
             int k = (int)(eqk[jb] >> 16);
@@ -1768,7 +1790,11 @@ static int bwdq_mode() {
 static int bwdq_pyr_attrs() {
     static int rc = -1;
     if (rc < 0) {
-        const void* ks[2] = {(const void*)msda1d_bwd_query_pyr_kernel<1>, (const void*)msda1d_bwd_query_pyr_kernel<2>};
+        const void* ks[6] = {(const void*)msda1d_bwd_query_pyr_kernel<1>, (const void*)msda1d_bwd_query_pyr_kernel<2>,
+                             (const void*)msda1d_bwd_query_pyr_kernel<1, 3>,
+                             (const void*)msda1d_bwd_query_pyr_kernel<2, 3>,
+                             (const void*)msda1d_bwd_query_pyr_kernel<1, 5>,
+                             (const void*)msda1d_bwd_query_pyr_kernel<2, 5>};
         rc = PDVC_OK;
         for (const void* k : ks)
             if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBqLds) != hipSuccess) {
@@ -2009,14 +2035,25 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
         if ((rc = bwdq_pyr_attrs())) return rc;
         PDVC_CHECK_ARG((long)batch * num_heads * bq_blocks < (1L << 31), "too many query blocks");
         dim3 pg((unsigned)(batch * num_heads * bq_blocks));
-        if (ref_dim == 1)
-            hipLaunchKernelGGL((msda1d_bwd_query_pyr_kernel<1>), pg, dim3(kPyrThreads), kBqLds, s, value,
-                               value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv, num_query, S,
-                               num_heads, bq_blocks, grad_output, save_attn, save_loc, grad_proj, grad_ref, gp16);
-        else
-            hipLaunchKernelGGL((msda1d_bwd_query_pyr_kernel<2>), pg, dim3(kPyrThreads), kBqLds, s, value,
-                               value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv, num_query, S,
-                               num_heads, bq_blocks, grad_output, save_attn, save_loc, grad_proj, grad_ref, gp16);
+        static const int qu = [] {  // queries per loop trip (PDVC_BQ_QU = 1 | 3 | 5: A/B)
+            const char* e = getenv("PDVC_BQ_QU");
+            const int v = e ? atoi(e) : 1;
+            return (v == 3 || v == 5) ? v : 1;
+        }();
+#define BQ_LAUNCH(R, Q)                                                                                           \
+    hipLaunchKernelGGL((msda1d_bwd_query_pyr_kernel<R, Q>), pg, dim3(kPyrThreads), kBqLds, s, value, value_pad_mask, \
+                       proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, bq_blocks,        \
+                       grad_output, save_attn, save_loc, grad_proj, grad_ref, gp16)
+        if (ref_dim == 1) {
+            if (qu == 3) BQ_LAUNCH(1, 3);
+            else if (qu == 5) BQ_LAUNCH(1, 5);
+            else BQ_LAUNCH(1, 1);
+        } else {
+            if (qu == 3) BQ_LAUNCH(2, 3);
+            else if (qu == 5) BQ_LAUNCH(2, 5);
+            else BQ_LAUNCH(2, 1);
+        }
+#undef BQ_LAUNCH
         PDVC_CHECK_LAUNCH("msda1d_bwd_query_pyr_kernel");
     } else if (tw > 0 && head_dim == 64 && bwdq_mode() != 0 && (long)S * num_heads * head_dim * 4 < (1L << 31)) {
         dim3 grid((unsigned)((tw + 3) / 4));
@@ -2074,7 +2111,9 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
             hipError_t e4 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1, true, 4>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-            if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess) {
+            hipError_t e5 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1, true, 4, true>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+            if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess) {
                 (void)hipGetLastError();
                 return pdvc_set_error(PDVC_ERR_LAUNCH, "msda1d_bwd_value_kernel: cannot raise the LDS limit");
             }
@@ -2086,16 +2125,14 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
             if (g4 && level_sums && lds < kVW * 16 * 16) lds = kVW * 16 * 16;  // the level-sum reduction
             float* gsums = g4 ? level_sums : nullptr;
             const int acc = q0 > 0;
-            if (g4 && value_ug(num_query, S) == 4)
-                hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, 4>), dim3((unsigned)nblk), dim3(kVW * 64), lds,
-                                   s, value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
-                                   save_attn, save_loc, grad_value, gsums, (const int64_t*)nullptr,
-                                   (const int64_t*)nullptr, gv16);
-            else if (g4)
-                hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
-                                   value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
-                                   save_attn, save_loc, grad_value, gsums, (const int64_t*)nullptr,
-                                   (const int64_t*)nullptr, gv16);
+#define VAL_LAUNCH(UGV, B16V)                                                                                       \
+    hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, UGV, B16V>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s, \
+                       value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output, save_attn,  \
+                       save_loc, grad_value, gsums, (const int64_t*)nullptr, (const int64_t*)nullptr, gv16)
+            if (g4 && gv16) VAL_LAUNCH(4, true);  // the bf16 stores spill the depth-8 walk (7 VGPRs): depth 4
+            else if (g4 && value_ug(num_query, S) == 4) VAL_LAUNCH(4, false);
+            else if (g4) VAL_LAUNCH(8, false);
+#undef VAL_LAUNCH
             else if (head_dim <= 64)
                 hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, false>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
                                    value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,

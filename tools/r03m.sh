@@ -7,6 +7,12 @@ ok() { local rc=$1; if [ $rc -gt 1 ]; then echo "step rc=$rc: stop"; exit $rc; f
 echo "[$(date +%T)] tests"
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf > $O/tests.log 2>&1; rc=$?
 tail -8 $O/tests.log; ok $rc
+for qu in 1 3 5; do
+  PDVC_BQ_QU=$qu timeout -k 10 120 python -u tools/kbench.py --videos 1024 --reps 10 > $O/kb_qu$qu.txt 2>&1; rc=$?
+  echo "QU=$qu: $(grep encoder $O/kb_qu$qu.txt)"; ok $rc
+done
+PDVC_BQ_QU=5 timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -m gpu -q --timeout 120 --timeout-method thread -rf > $O/ops_qu5.log 2>&1; rc=$?
+tail -3 $O/ops_qu5.log; ok $rc
 echo "[$(date +%T)] bf16 casts"
 PDVC_CAST_LOG=1 timeout -k 10 200 python -u tools/diag_bf16_casts.py --videos 128 > $O/casts.txt 2>&1; rc=$?
 head -30 $O/casts.txt; ok $rc
