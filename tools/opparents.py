@@ -76,6 +76,17 @@ def main():
     print(f"non-GEMM aten device time {tot:.2f} ms/step over {sum(v[1] for v in rows.values())} ops")
     for (name, shp, owner), (ms, n) in sorted(rows.items(), key=lambda x: -x[1][0])[:a.top]:
         print(f"{ms:7.3f} ms n={n:4d} {name:22s} {shp:70s} <- {owner[:70]}")
+    # launches per owner (autograd node or forward op): where the op count comes from
+    by_owner = collections.defaultdict(lambda: [0.0, 0, collections.Counter()])
+    for (name, shp, owner), (ms, n) in rows.items():
+        r = by_owner[owner]
+        r[0] += ms
+        r[1] += n
+        r[2][name] += n
+    print("\nops per owner (count-sorted)")
+    for owner, (ms, n, names) in sorted(by_owner.items(), key=lambda x: -x[1][1])[:a.top]:
+        top = ", ".join(f"{k.replace('aten::', '')}x{c}" for k, c in names.most_common(6))
+        print(f"n={n:4d} {ms:7.3f} ms  {owner[:60]:60s} {top}")
 
 
 if __name__ == "__main__":
