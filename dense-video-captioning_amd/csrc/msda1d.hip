@@ -625,37 +625,32 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr2_kernel(
         w2v[i] = ok2 ? lw * aw : 0.f;
     }
 
-    float4 acc[kPyrQPS];
+    PAcc4 acc[kPyrQPS];
 #pragma unroll
-    for (int i = 0; i < kPyrQPS; ++i) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 tok = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < kPyrQPS; ++i) acc[i] = pacc_zero();
+    PAcc4 tok = pacc_zero();
+    // per sample and lane: 3 DPP broadcasts, 1 address add, 2 LDS reads, 4 v_pk_fma_f32 on the loaded registers
     auto level = [&](auto Lc) {
         constexpr int L = decltype(Lc)::value;
 #pragma unroll
         for (int i = 0; i < kPyrQPS; ++i) {
-            float4 v1[kP], v2[kP];
+            pf4 v1[kP], v2[kP];
             float c1[kP], c2[kP];
             int ad = adv[i];
             float wa = w1v[i], wb = w2v[i];
-            __asm__ volatile("" : "+v"(ad), "+v"(wa), "+v"(wb) : "v"(tok.x), "v"(tok.y), "v"(tok.z), "v"(tok.w));
+            __asm__ volatile("" : "+v"(ad), "+v"(wa), "+v"(wb) : "v"(tok.lo), "v"(tok.hi));
 #pragma unroll
             for (int p = 0; p < kP; ++p) {
                 const char* r = lrow + grp_bcast<16>(ad, L * kP + p);
                 c1[p] = grp_bcast<16>(wa, L * kP + p);
                 c2[p] = grp_bcast<16>(wb, L * kP + p);
-                v1[p] = *reinterpret_cast<const float4*>(r);
-                v2[p] = *reinterpret_cast<const float4*>(r + 256);
+                v1[p] = *reinterpret_cast<const pf4*>(r);
+                v2[p] = *reinterpret_cast<const pf4*>(r + 256);
             }
 #pragma unroll
             for (int p = 0; p < kP; ++p) {
-                acc[i].x = fmaf(c1[p], v1[p].x, acc[i].x);
-                acc[i].y = fmaf(c1[p], v1[p].y, acc[i].y);
-                acc[i].z = fmaf(c1[p], v1[p].z, acc[i].z);
-                acc[i].w = fmaf(c1[p], v1[p].w, acc[i].w);
-                acc[i].x = fmaf(c2[p], v2[p].x, acc[i].x);
-                acc[i].y = fmaf(c2[p], v2[p].y, acc[i].y);
-                acc[i].z = fmaf(c2[p], v2[p].z, acc[i].z);
-                acc[i].w = fmaf(c2[p], v2[p].w, acc[i].w);
+                pacc_fma(acc[i], c1[p], v1[p]);
+                pacc_fma(acc[i], c2[p], v2[p]);
             }
             tok = acc[i];
         }
@@ -685,8 +680,9 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr2_kernel(
         const int q = qb * kPyrQ + slot + 64 * i;
         if (q < Lq) {
             const size_t o = ((size_t)b * Lq + q) * MD + (size_t)m * 64 + sub * 4;
-            *reinterpret_cast<float4*>(out + o) = acc[i];
-            if (out16) store_bf16x4(out16 + o, acc[i].x, acc[i].y, acc[i].z, acc[i].w);
+            const float4 r = pacc_f4(acc[i]);
+            *reinterpret_cast<float4*>(out + o) = r;
+            if (out16) store_bf16x4(out16 + o, r.x, r.y, r.z, r.w);
         }
     }
 }
@@ -1208,7 +1204,8 @@ constexpr int kVQPT = 4;  // queries per thread in its sort passes: a launch chu
 // allows -- the decoder's short sample lists)
 // B16: also writes the bf16 rounding of every row into gv16 (the bf16 mode; a separate instantiation, so the
 // fp32 path keeps its registers: the pointer and its stores cost the depth-8 walk 9 spilled VGPRs)
-template <int CW, bool G4, int UG = 8, bool B16 = false>
+// ABL (measurement only, PDVC_VAL_ABLATE): 1 = stop after the sort, 2 = walk without the gradient-row gathers
+template <int CW, bool G4, int UG = 8, bool B16 = false, int ABL = 0>
 __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
                                                                      int Lq, int q0, int nq, int S, int M, int D,
                                                                      int accumulate,
@@ -1328,6 +1325,10 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
         }
     }
     __syncthreads();
+    if constexpr (ABL == 1) {  // keep the sort live: one word of it leaves the workgroup
+        if (threadIdx.x == 0) grad_value[(size_t)blockIdx.x] = (float)off[T + 1] + __uint_as_float(eqk[0]);
+        return;
+    }
     // 4) row ranges: split points balance the sorted samples over the waves (or 16-lane groups)
     const int total = off[T + 1];
     constexpr int kParts = G4 ? kVW * 4 : kVW;
@@ -1390,47 +1391,44 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
                 }
             };
             int k = (int)(eqk[jb] >> 16);
-            float4 alo = make_float4(0.f, 0.f, 0.f, 0.f), ahi = alo;  // rows k - 1 and k
+            PAcc4 alo = pacc_zero(), ahi = pacc_zero();  // rows k - 1 and k
             for (int j0 = jb; j0 < je; j0 += UG) {
                 uint32_t e[UG];
-                float4 gv[UG];
+                pf4 gv[UG];
 #pragma unroll
                 for (int u = 0; u < UG; ++u) e[u] = eqk[(j0 + u < je) ? j0 + u : je - 1];
 #pragma unroll
                 for (int u = 0; u < UG; ++u) {
-                    const auto t = __builtin_amdgcn_raw_buffer_load_b128(gr, (int)(e[u] & 0xffffu) * rowb + coff, 0, 0);
-                    gv[u] = make_float4(__uint_as_float(t[0]), __uint_as_float(t[1]), __uint_as_float(t[2]),
-                                        __uint_as_float(t[3]));
+                    if constexpr (ABL == 2) {
+                        gv[u] = pf4{__uint_as_float(e[u]), 0.f, 0.f, 0.f};
+                    } else {
+                        const auto t =
+                            __builtin_amdgcn_raw_buffer_load_b128(gr, (int)__umul24(e[u] & 0xffffu, (unsigned)rowb) + coff, 0, 0);
+                        gv[u] = __builtin_bit_cast(pf4, t);
+                    }
                 }
 #pragma unroll
                 for (int u = 0; u < UG; ++u) {
                     if (j0 + u >= je) break;
                     const int kj = (int)(e[u] >> 16);
                     if (kj != k) {  // bucket k complete: row k - 1 final; row k too unless bucket k + 1 follows
-                        put(k - 1, alo);
+                        put(k - 1, pacc_f4(alo));
                         if (kj == k + 1) {
                             alo = ahi;
                         } else {
-                            put(k, ahi);
-                            alo = make_float4(0.f, 0.f, 0.f, 0.f);
+                            put(k, pacc_f4(ahi));
+                            alo = pacc_zero();
                         }
-                        ahi = make_float4(0.f, 0.f, 0.f, 0.f);
+                        ahi = pacc_zero();
                         k = kj;
                     }
                     const float2 wgt = ew[j0 + u];
-                    const float cl = wgt.x, chh = wgt.y;
-                    alo.x = fmaf(cl, gv[u].x, alo.x);
-                    alo.y = fmaf(cl, gv[u].y, alo.y);
-                    alo.z = fmaf(cl, gv[u].z, alo.z);
-                    alo.w = fmaf(cl, gv[u].w, alo.w);
-                    ahi.x = fmaf(chh, gv[u].x, ahi.x);
-                    ahi.y = fmaf(chh, gv[u].y, ahi.y);
-                    ahi.z = fmaf(chh, gv[u].z, ahi.z);
-                    ahi.w = fmaf(chh, gv[u].w, ahi.w);
+                    pacc_fma(alo, wgt.x, gv[u]);
+                    pacc_fma(ahi, wgt.y, gv[u]);
                 }
             }
-            put(k - 1, alo);
-            put(k, ahi);
+            put(k - 1, pacc_f4(alo));
+            put(k, pacc_f4(ahi));
         }
         if (level_sums) {  // the bias gradient's partial: column sums of the rows this workgroup wrote
 #pragma unroll
@@ -2129,7 +2127,25 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
     hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, UGV, B16V>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s, \
                        value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output, save_attn,  \
                        save_loc, grad_value, gsums, (const int64_t*)nullptr, (const int64_t*)nullptr, gv16)
-            if (g4 && gv16) VAL_LAUNCH(4, true);  // the bf16 stores spill the depth-8 walk (7 VGPRs): depth 4
+            static const int vabl = [] {
+                const char* e = getenv("PDVC_VAL_ABLATE");
+                return e ? atoi(e) : 0;
+            }();
+            if (g4 && !gv16 && (vabl == 1 || vabl == 2) && value_ug(num_query, S) == 8) {  // measurement only
+                const void* k = vabl == 1 ? (const void*)msda1d_bwd_value_kernel<1, true, 8, false, 1>
+                                          : (const void*)msda1d_bwd_value_kernel<1, true, 8, false, 2>;
+                (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+                if (vabl == 1)
+                    hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, 8, false, 1>), dim3((unsigned)nblk),
+                                       dim3(kVW * 64), lds, s, value_pad_mask, lv, num_query, q0, nq, S, num_heads,
+                                       head_dim, acc, grad_output, save_attn, save_loc, grad_value, gsums,
+                                       (const int64_t*)nullptr, (const int64_t*)nullptr, gv16);
+                else
+                    hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, 8, false, 2>), dim3((unsigned)nblk),
+                                       dim3(kVW * 64), lds, s, value_pad_mask, lv, num_query, q0, nq, S, num_heads,
+                                       head_dim, acc, grad_output, save_attn, save_loc, grad_value, gsums,
+                                       (const int64_t*)nullptr, (const int64_t*)nullptr, gv16);
+            } else if (g4 && gv16) VAL_LAUNCH(4, true);  // the bf16 stores spill the depth-8 walk (7 VGPRs): depth 4
             else if (g4 && value_ug(num_query, S) == 4) VAL_LAUNCH(4, false);
             else if (g4) VAL_LAUNCH(8, false);
 #undef VAL_LAUNCH

@@ -20,6 +20,29 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
     return base + slot;
 }
 
+// Packed fp32 lanes: a float4 held as two register pairs (.xy, .zw), each updated by one v_pk_fma_f32 with the
+// scalar weight broadcast (op_sel_hi).  Written per component with fmaf on a float4, the compiler pairs (x, z) and
+// (y, w) for v_pk_fma_f32 and re-packs every loaded row with three v_mov_b32 (1 798 movs against 1 024 packed FMAs in
+// the pyramid forward); on (.xy, .zw) the loaded registers are the operands as they stand.  Same products, same
+// order per component as the fmaf form: the same bits.
+typedef float pf2 __attribute__((ext_vector_type(2)));
+typedef float pf4 __attribute__((ext_vector_type(4)));
+
+struct PAcc4 {
+    pf2 lo, hi;  // (x, y), (z, w)
+};
+
+__device__ __forceinline__ PAcc4 pacc_zero() { return PAcc4{pf2{0.f, 0.f}, pf2{0.f, 0.f}}; }
+
+// acc += c * v (4 channels)
+__device__ __forceinline__ void pacc_fma(PAcc4& a, float c, const pf4 v) {
+    const pf2 cc = {c, c};
+    a.lo = __builtin_elementwise_fma(cc, v.xy, a.lo);
+    a.hi = __builtin_elementwise_fma(cc, v.zw, a.hi);
+}
+
+__device__ __forceinline__ float4 pacc_f4(const PAcc4& a) { return make_float4(a.lo.x, a.lo.y, a.hi.x, a.hi.y); }
+
 // Exact xor-partner exchange for butterfly step d (1, 2, 4, 8) inside aligned 16-lane groups without
 // ds_bpermute's lane-index arithmetic: d = 1, 2 on DPP quad_perm, d = 8 on DPP row_ror:8 (VALU operand
 // modifiers, no LDS traffic), d = 4 on ds_swizzle's bit mode (gfx9 DPP has no xor-4 pattern; row_half_mirror

@@ -49,8 +49,10 @@ class StepGraph:
                     reducer.finish()
         torch.cuda.current_stream().wait_stream(side)
         model.zero_grad(set_to_none=True)
-        self.graph = torch.cuda.CUDAGraph()
-        if debug_dot:  # keep the captured graph for hipGraphDebugDotPrint (tools/diag_memset_graph.py)
+        # debug_dot: keep the captured hipGraph_t for hipGraphDebugDotPrint and the node walk of
+        # tools/diag_memset_graph.py (raw_cuda_graph() needs keep_graph)
+        self.graph = torch.cuda.CUDAGraph(keep_graph=True) if debug_dot else torch.cuda.CUDAGraph()
+        if debug_dot:
             self.graph.enable_debug_mode()
         from .precision import begin_capture
         begin_capture()  # bf16 mode: every operand rounding of the step becomes a node of the graph
