@@ -667,6 +667,244 @@ __global__ __launch_bounds__(256) void mha_bwd_mfma_kernel(const float* __restri
 }
 
 
+// Backward in 51 KiB of LDS (mha_bwd_mfma_kernel's four 33-KiB row images held one workgroup per CU; this one is held
+// at two by its 248 registers -- the own-row A operands take 64): the K / V rows (phase A) and the q / dO rows
+// (phase B) stream through two 32-row block buffers, the next block staged after the current one's MFMAs (a register
+// prefetch under them took the kernel to 264 registers, one workgroup per CU).  Phase A (wave w = query rows 32w..32w+31) takes its
+// own q (scaled) and dO rows as register A operands with mha_fwd_mfma2_kernel's permuted contraction index (k-step kk
+// of lane half hi = channel 32*hi + kk, the same for the B reads of the K / V block), so no q / dO image is staged
+// for it.  Per key block: S, dP_d, P = exp(S - lse), dS = P (dP_d z - delta), P_d and dS to the workspace, dq += dS.K
+// through the wave's 32x33 dS block.  Phase B (wave w = keys 32w..32w+31): dk = dS^T.q_scaled, dv = P_d^T.dO, A
+// operands from the workspace, B operands from the q / dO block.  Same arithmetic as mha_bwd_mfma_kernel per element
+// and the same summation order over keys (dq) and queries (dk, dv).
+static constexpr int kBlkLd = 65;                       // block row stride (conflict-free column walks)
+static constexpr int kBlkF = 32 * kBlkLd;               // floats per 32-row block image
+static constexpr size_t kBwdMfma2Lds = sizeof(float) * (4 * kBlkF + 4 * 32 * 33 + 2 * kMQ);
+
+// rows [r0, r0 + 32) of one head's 64 channels (row stride ld, x mul; rows >= Q zero) into two float4 registers per
+// thread, then into a 32-row block image
+struct BlkRegs {
+    float4 x[2];
+};
+__device__ __forceinline__ BlkRegs blk_load(const float* __restrict__ src, size_t ld, int r0, int Q, float mul,
+                                            int tid) {
+    BlkRegs b;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int idx = tid + 256 * i, r = idx >> 4, c = (idx & 15) * 4;
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r0 + r < Q) x = *reinterpret_cast<const float4*>(src + (size_t)(r0 + r) * ld + c);
+        b.x[i] = make_float4(x.x * mul, x.y * mul, x.z * mul, x.w * mul);
+    }
+    return b;
+}
+__device__ __forceinline__ void blk_store(const BlkRegs& b, float* dst, int tid) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int idx = tid + 256 * i, r = idx >> 4, c = (idx & 15) * 4;
+        float* d = dst + r * kBlkLd + c;
+        d[0] = b.x[i].x;
+        d[1] = b.x[i].y;
+        d[2] = b.x[i].z;
+        d[3] = b.x[i].w;
+    }
+}
+
+__global__ __launch_bounds__(256) void mha_bwd_mfma2_kernel(const float* __restrict__ qk, const float* __restrict__ v,
+                                                            const uint8_t* __restrict__ kpm,
+                                                            const float* __restrict__ out,
+                                                            const float* __restrict__ gout,
+                                                            const float* __restrict__ lse, int Q, int M, float scaling,
+                                                            float p_drop, uint32_t thresh, uint64_t seed0,
+                                                            const uint64_t* __restrict__ seed_dev,
+                                                            float* __restrict__ ws_p, float* __restrict__ ws_ds,
+                                                            float* __restrict__ dqk, float* __restrict__ dv) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int D = 64;
+    constexpr int kDLD = 33;
+    float* blk = smem;                    // [2 buffers][2 images][32][65]
+    float* Ds = blk + 4 * kBlkF;          // [4][32][33] per-wave dS block
+    float* rowl = Ds + 4 * 32 * kDLD;     // [128] lse
+    float* rowd = rowl + kMQ;             // [128] delta = dO . O
+    const int E = M * D;
+    const int nm = xcd_remap(blockIdx.x, gridDim.x);
+    const int n = nm / M, m = nm - n * M;
+    const uint64_t seed = load_seed(seed0, seed_dev);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, hi = lane >> 5;
+    const float* qbase = qk + (size_t)n * Q * 2 * E + m * D;
+    const size_t hbase = (size_t)n * Q * E + m * D;
+    const int nblk = (Q + 31) >> 5;
+    // block 0 of K and V first (their loads in flight while the own rows and the row statistics load)
+    BlkRegs pk = blk_load(qbase + E, 2 * (size_t)E, 0, Q, 1.f, tid);
+    BlkRegs pv = blk_load(v + hbase, (size_t)E, 0, Q, 1.f, tid);
+    const int row0 = w * 32;
+    float qa[32], oa[32];  // q[row0 + l32][32*hi + kk] * scaling and dO[row0 + l32][32*hi + kk] (zeros past Q)
+    {
+        const int q = row0 + l32;
+        const float4* qs = reinterpret_cast<const float4*>(qbase + (size_t)q * 2 * E + 32 * hi);
+        const float4* os = reinterpret_cast<const float4*>(gout + hbase + (size_t)q * E + 32 * hi);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float4 x = q < Q ? qs[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 y = q < Q ? os[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            qa[4 * i] = x.x * scaling;
+            qa[4 * i + 1] = x.y * scaling;
+            qa[4 * i + 2] = x.z * scaling;
+            qa[4 * i + 3] = x.w * scaling;
+            oa[4 * i] = y.x;
+            oa[4 * i + 1] = y.y;
+            oa[4 * i + 2] = y.z;
+            oa[4 * i + 3] = y.w;
+        }
+    }
+    if (tid < kMQ) {
+        float dl = 0.f, l = 0.f;
+        if (tid < Q) {
+            const float4* orow = reinterpret_cast<const float4*>(out + hbase + (size_t)tid * E);
+            const float4* grow = reinterpret_cast<const float4*>(gout + hbase + (size_t)tid * E);
+#pragma unroll 4
+            for (int c = 0; c < D / 4; ++c) {
+                const float4 a = orow[c], b = grow[c];
+                dl += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+            }
+            l = lse[(size_t)nm * Q + tid];
+        }
+        rowd[tid] = dl;
+        rowl[tid] = l;
+    }
+    blk_store(pk, blk, tid);
+    blk_store(pv, blk + kBlkF, tid);
+    __syncthreads();
+    const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    float* wsp = ws_p + (size_t)nm * Q * Q;
+    float* wsd = ws_ds + (size_t)nm * Q * Q;
+    float* Dw = Ds + w * 32 * kDLD;
+    mha_f32x16 dq[2] = {mha_f32x16{}, mha_f32x16{}};
+    // phase A: key blocks
+#pragma unroll 1
+    for (int kb = 0; kb < nblk; ++kb) {
+        const float* Kb = blk + (kb & 1) * 2 * kBlkF;
+        const float* Vb = Kb + kBlkF;
+        const bool more = kb + 1 < nblk;
+        const int k = kb * 32 + l32;
+        const bool kv = k < Q && !(kpm && kpm[(size_t)n * Q + k]);
+        mha_f32x16 s = mha_f32x16{}, dp = mha_f32x16{};
+        {
+            const float* kbp = Kb + l32 * kBlkLd + 32 * hi;
+            const float* vbp = Vb + l32 * kBlkLd + 32 * hi;
+            // in chunks of 8 k-steps: the compiler would otherwise hoist all 64 operand reads of the block (64 VGPRs)
+#pragma unroll
+            for (int c = 0; c < D / 2; c += 8) {
+#pragma unroll
+                for (int kk = c; kk < c + 8; ++kk) {
+                    s = mfma32(qa[kk], kbp[kk], s);
+                    dp = mfma32(oa[kk], vbp[kk], dp);
+                }
+                __asm__ volatile("" ::: "memory");
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int rl = crow(r, hi), q = row0 + rl;
+            float ds = 0.f;
+            if (q < Q) {
+                const float p = kv ? expf(s[r] - rowl[q]) : 0.f;
+                float z = 1.f;
+                if (p_drop > 0.f && k < Q)
+                    z = keep_elem(seed, (uint32_t)nm, (uint32_t)q, (uint32_t)k, (uint32_t)Q, thresh) ? keep_scale : 0.f;
+                ds = p * (dp[r] * z - rowd[q]);
+                if (k < Q) {
+                    wsp[(size_t)q * Q + k] = p * z;
+                    wsd[(size_t)q * Q + k] = ds;
+                }
+            }
+            Dw[rl * kDLD + l32] = ds;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        {
+            const float* da = Dw + l32 * kDLD + hi;
+            const float* kb0 = Kb + hi * kBlkLd + l32;
+#pragma unroll 8
+            for (int kk = 0; kk < 16; ++kk) {
+                const float a = da[2 * kk];
+                dq[0] = mfma32(a, kb0[2 * kk * kBlkLd], dq[0]);
+                dq[1] = mfma32(a, kb0[2 * kk * kBlkLd + 32], dq[1]);
+            }
+        }
+        if (more) {  // the next block into the other buffer (every wave finished reading it before the last barrier)
+            pk = blk_load(qbase + E, 2 * (size_t)E, (kb + 1) * 32, Q, 1.f, tid);
+            pv = blk_load(v + hbase, (size_t)E, (kb + 1) * 32, Q, 1.f, tid);
+            float* nb = blk + ((kb + 1) & 1) * 2 * kBlkF;
+            blk_store(pk, nb, tid);
+            blk_store(pv, nb + kBlkF, tid);
+        }
+        __syncthreads();  // the next block is staged; this wave's dS block may be rewritten
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int q = row0 + crow(r, hi);
+        if (q < Q) {
+            float* drow = dqk + ((size_t)n * Q + q) * 2 * E + m * D + l32;
+            drow[0] = dq[0][r] * scaling;
+            drow[32] = dq[1][r] * scaling;
+        }
+    }
+    // phase B: wave w owns keys key0..key0+31; query blocks of q (scaled) and dO stream through the block buffers.
+    // The workspace rows of every wave were written before the last barrier of phase A (visible to the workgroup).
+    const int key0 = w * 32, kl = key0 + l32;
+    const bool kin = kl < Q;
+    mha_f32x16 gk[2] = {mha_f32x16{}, mha_f32x16{}}, gv[2] = {mha_f32x16{}, mha_f32x16{}};
+    pk = blk_load(qbase, 2 * (size_t)E, 0, Q, scaling, tid);
+    pv = blk_load(gout + hbase, (size_t)E, 0, Q, 1.f, tid);
+    blk_store(pk, blk, tid);
+    blk_store(pv, blk + kBlkF, tid);
+    __syncthreads();
+#pragma unroll 1
+    for (int qb = 0; qb < nblk; ++qb) {
+        const float* Qb = blk + (qb & 1) * 2 * kBlkF;
+        const float* Ob = Qb + kBlkF;
+        const bool more = qb + 1 < nblk;
+        if (key0 < Q) {
+#pragma unroll 4
+            for (int kk = 0; kk < 16; ++kk) {
+                const int ql = 2 * kk + hi, q = qb * 32 + ql;
+                const bool in = kin && q < Q;
+                const float ad = in ? wsd[(size_t)q * Q + kl] : 0.f;
+                const float ap = in ? wsp[(size_t)q * Q + kl] : 0.f;
+                const float* qr = Qb + ql * kBlkLd + l32;
+                const float* orr = Ob + ql * kBlkLd + l32;
+                gk[0] = mfma32(ad, qr[0], gk[0]);
+                gk[1] = mfma32(ad, qr[32], gk[1]);
+                gv[0] = mfma32(ap, orr[0], gv[0]);
+                gv[1] = mfma32(ap, orr[32], gv[1]);
+            }
+        }
+        if (more) {
+            pk = blk_load(qbase, 2 * (size_t)E, (qb + 1) * 32, Q, scaling, tid);
+            pv = blk_load(gout + hbase, (size_t)E, (qb + 1) * 32, Q, 1.f, tid);
+            float* nb = blk + ((qb + 1) & 1) * 2 * kBlkF;
+            blk_store(pk, nb, tid);
+            blk_store(pv, nb + kBlkF, tid);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int k = key0 + crow(r, hi);
+        if (k < Q) {
+            float* krow = dqk + ((size_t)n * Q + k) * 2 * E + E + m * D + l32;
+            float* vrow = dv + ((size_t)n * Q + k) * E + m * D + l32;
+            krow[0] = gk[0][r];
+            krow[32] = gk[1][r];
+            vrow[0] = gv[0][r];
+            vrow[32] = gv[1][r];
+        }
+    }
+}
+
+
 }  // namespace pdvc
 
 using namespace pdvc;
@@ -697,6 +935,12 @@ static bool fwd_lean() {
     return on;
 }
 
+// the 51-KiB backward (three workgroups per CU); PDVC_MHA_BWD2=0 keeps the 133-KiB one (A/B, tests)
+static bool bwd_lean() {
+    const char* e = getenv("PDVC_MHA_BWD2");
+    return !(e && e[0] == '0');
+}
+
 // longer query sets (anet_c3d: Q = 300): the flash-style MFMA kernels of seqattn.hip with this op's key padding
 // mask, dropout mask and scaling (PDVC_MHA_MFMA=0 selects the scalar kernels here too)
 static bool use_flash(int Q, int D) {
@@ -712,9 +956,9 @@ static bool use_flash(int Q, int D) {
 static int mha_attrs() {
     static bool attr = false;
     if (!attr) {
-        const void* ks[6] = {(const void*)mha_fwd_kernel, (const void*)mha_bwd_q_kernel, (const void*)mha_bwd_k_kernel,
+        const void* ks[7] = {(const void*)mha_fwd_kernel, (const void*)mha_bwd_q_kernel, (const void*)mha_bwd_k_kernel,
                              (const void*)mha_fwd_mfma_kernel, (const void*)mha_bwd_mfma_kernel,
-                             (const void*)mha_fwd_mfma2_kernel};
+                             (const void*)mha_fwd_mfma2_kernel, (const void*)mha_bwd_mfma2_kernel};
         for (const void* k : ks)
             if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) {
                 (void)hipGetLastError();
@@ -789,6 +1033,13 @@ extern "C" int pdvc_mha_backward_f32(const float* qk, const float* v, const uint
     float* ws_p = workspace;
     float* ws_ds = workspace + (size_t)nm * num_query * num_query;
     hipStream_t s = (hipStream_t)stream;
+    if (use_mfma(num_query, head_dim) && bwd_lean()) {
+        hipLaunchKernelGGL(mha_bwd_mfma2_kernel, dim3((unsigned)nm), dim3(256), kBwdMfma2Lds, s, qk, v,
+                           key_padding_mask, out, grad_out, lse, num_query, num_heads, scaling, dropout_p,
+                           drop_threshold(dropout_p), seed, seed_dev, ws_p, ws_ds, grad_qk, grad_v);
+        PDVC_CHECK_LAUNCH("mha_bwd_mfma2_kernel");
+        return PDVC_OK;
+    }
     if (use_mfma(num_query, head_dim)) {
         hipLaunchKernelGGL(mha_bwd_mfma_kernel, dim3((unsigned)nm), dim3(256), kBwdMfmaLds, s, qk, v,
                            key_padding_mask, out, grad_out, lse, num_query, num_heads, scaling, dropout_p,

@@ -136,6 +136,30 @@ def test_query_self_attention_matrix_core_matches_scalar(Q, p, monkeypatch):
         close(x, y, 2e-5, name)
 
 
+@pytest.mark.parametrize("Q,p", [(100, 0.1), (61, 0.0), (128, 0.3), (33, 0.1)])
+def test_query_self_attention_streaming_backward_matches(Q, p, monkeypatch):
+    """The 51-KiB streaming backward (mha_bwd_mfma2_kernel: K / V and q / dO rows in 32-row blocks, own rows as
+    register A operands) against the 133-KiB one (PDVC_MHA_BWD2=0): the same dropout mask, products and summation
+    order, so the gradients agree to fp32 rounding; both against float64 in the tests above."""
+    from pdvc.ops.functions.attention import QuerySelfAttentionFunction
+    torch.manual_seed(Q + 7)
+    N, M, E = 3, 8, 512
+    qk = torch.randn(N, Q, 2 * E, device=DEV)
+    v = torch.randn(N, Q, E, device=DEV)
+    kpm = torch.zeros(N, Q, dtype=torch.bool, device=DEV)
+    kpm[1, -4:] = True
+    g = torch.randn(N, Q, E, device=DEV)
+    res = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PDVC_MHA_BWD2", mode)
+        a, b = qk.clone().requires_grad_(), v.clone().requires_grad_()
+        out = QuerySelfAttentionFunction.apply(a, b, kpm, M, p, 99)
+        out.backward(g)
+        res.append((a.grad, b.grad))
+    for name, x, y in zip(("grad_qk", "grad_v"), res[0], res[1]):
+        close(x, y, 2e-5, name)
+
+
 # ------------------------------------------------------------------------------------------------
 # transformer layers vs the reference layers (tests/golden/make_golden.py::module_layers)
 # ------------------------------------------------------------------------------------------------
