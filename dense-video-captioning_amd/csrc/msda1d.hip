@@ -1371,9 +1371,10 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
             const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)(gout + (size_t)b * Lq * MD), (short)0, (int)((size_t)Lq * MD * 4), 0x00020000);
             const int coff = (m * D + gl * 4) * 4, rowb = (int)MD * 4;
+            const unsigned MDu = (unsigned)MD;  // < 2^24: the row offset is one v_mul_u32_u24 (a 64-bit one cost ~6 VALU)
             auto put = [&](int r, float4 v) {
                 if (r >= r0 && r < r1) {
-                    float4* orow = reinterpret_cast<float4*>(ob + (size_t)r * MD);
+                    float4* orow = reinterpret_cast<float4*>(ob + __umul24((unsigned)r, MDu));
                     if (mrow && mrow[r]) v = make_float4(0.f, 0.f, 0.f, 0.f);
                     psum.x += v.x;
                     psum.y += v.y;

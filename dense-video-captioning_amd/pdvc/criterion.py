@@ -7,6 +7,8 @@ The decoder layers are stacked and matched together: one cost pass, and the assi
 (pdvc_lsap_f32, scipy's algorithm and tie rule) with no host round trip -- the reference copies the costs to the
 host and runs scipy once per layer.  solve_padded keeps the host route (one copy for every layer).
 """
+import os
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -14,6 +16,7 @@ from torch import nn
 
 from . import box_ops, hostio
 from .matcher import LazyIndices, padded_targets
+from .ops.functions import setcrit
 
 COUNTER_CLASS_RATE = [0.00000000e+00, 0.00000000e+00, 1.93425917e-01, 4.12129084e-01, 1.88929963e-01,
                       7.81296833e-02, 5.09541413e-02, 3.12718553e-02, 1.84833650e-02, 8.39244680e-03,
@@ -21,6 +24,12 @@ COUNTER_CLASS_RATE = [0.00000000e+00, 0.00000000e+00, 1.93425917e-01, 4.12129084
                       4.99550405e-04, 4.99550405e-04, 1.99820162e-04, 2.99730243e-04, 3.99640324e-04,
                       2.99730243e-04, 0.00000000e+00, 1.99820162e-04, 0.00000000e+00, 0.00000000e+00,
                       0.00000000e+00, 9.99100809e-05, 9.99100809e-05]
+
+
+def fused_enabled(t):
+    """The native set criterion (ops/functions/setcrit.py) for float32 GPU tensors; PDVC_FUSED_CRITERION=0 keeps
+    the torch form (A/B and tests)."""
+    return t.is_cuda and t.dtype == torch.float32 and os.environ.get("PDVC_FUSED_CRITERION", "1") != "0"
 
 
 def sigmoid_focal_terms(inputs, targets, alpha=0.25, gamma=2):
@@ -172,24 +181,39 @@ class SetCriterion(nn.Module):
             # capacity-padded batch passes the capacity as every problem's host bound, the counts on the device
             m = self.matcher.solve_device(costs, ptL["sizes"] if cap is None else [cap] * costs.shape[0],
                                           ptL["sizes_i32"])
+            idx = [(LazyIndices(m, b, N), None) for b in range(Ld)]
+            if fused_enabled(logits) and costs.shape[2] <= setcrit.MAX_TARGETS:
+                # every loss term of every (layer, video) problem in one launch, its backward in one more
+                max_length = count.shape[1] - 1
+                rate = hostio.const(("counter_class_rate", max_length),
+                                    lambda: self.counter_class_rate[:max_length + 1], logits.device)
+                lv = setcrit.set_losses(logits, boxes, count, ptL, m, qm, rate, self.opt, self.focal_alpha,
+                                        self.focal_gamma)  # (Ld * N, 6)
+                per_layer = lv.view(Ld, N, 6).mean(1).reshape(-1).unbind(0)
+                per_layer = [dict(zip(setcrit.LOSS_KEYS, per_layer[6 * i:6 * i + 6])) for i in range(Ld)]
+                return self._layer_dicts(outputs, idx, per_layer)
             pp, pk, nm, emax = static_pairs(ptL)
             pairs = (pp, m.queries[pp, pk], m.targets[pp, pk], pk, nm, emax)
             if cap is not None:
                 pairs = pairs + (pk < nm[pp],)
             per = self.video_losses(logits, boxes, count, ptL, None, pairs, qm)
-            idx = [(LazyIndices(m, b, N), None) for b in range(Ld)]
         else:
             solved = self.matcher.solve_padded(list(costs.view(Ld, N, *costs.shape[1:])), pt["sizes"])
             idx = [(s_, None) for s_ in solved]
             per = self.video_losses(logits, boxes, count, ptL, [m_ for s_ in solved for m_ in s_], query_mask=qm)
+        per = {k: v.view(Ld, N).mean(1) for k, v in per.items()}
+        return self._layer_dicts(outputs, idx, [{k: v[i] for k, v in per.items()} for i in range(Ld)])
+
+    @staticmethod
+    def _layer_dicts(outputs, idx, per_layer):
+        """The reference's return value: the last layer's losses, then each aux layer's under key + f"_{i}"."""
         last_indices = idx[0]
         outputs["matched_indices"] = last_indices
-        per = {k: v.view(Ld, N).mean(1) for k, v in per.items()}
-        losses = {k: v[0] for k, v in per.items()}
+        losses = dict(per_layer[0])
         if "aux_outputs" in outputs:
             aux_indices = idx[1:]
-            for i in range(Ld - 1):
-                losses.update({k + f"_{i}": v[i + 1] for k, v in per.items()})
+            for i in range(len(per_layer) - 1):
+                losses.update({k + f"_{i}": v for k, v in per_layer[i + 1].items()})
             return losses, last_indices, aux_indices
         return losses, last_indices
 

@@ -6,6 +6,8 @@ algorithm and tie rule of scipy's linear_sum_assignment, so matched indices are 
 host round trip; `solve_padded` keeps the host/scipy route (ONE device->host copy for every block).
 The reference also solves a 4x-replicated "many-to-one" problem whose result no loss uses; it is skipped.
 """
+import os
+
 import numpy as np
 import torch
 from scipy.optimize import linear_sum_assignment
@@ -36,6 +38,12 @@ class HungarianMatcher(nn.Module):
     def cost_padded(self, pred_logits, pred_boxes, pt):
         """All videos at once: (N, Q, Emax) cost with targets padded to Emax (padding columns are junk and
         are sliced away by the caller).  Elementwise the same operations as the reference's flat cost."""
+        if (pred_logits.is_cuda and pred_logits.dtype == torch.float32
+                and os.environ.get("PDVC_FUSED_CRITERION", "1") != "0"):
+            # one launch: the same fp32 operations in the same order as below (csrc/setcrit.hip; a few ulp apart)
+            from .ops.functions.setcrit import match_cost
+            return match_cost(pred_logits, pred_boxes, pt["labels"], pt["boxes"], self.cost_alpha, self.cost_gamma,
+                              self.cost_bbox, self.cost_class, self.cost_giou)
         out_prob = pred_logits.sigmoid()  # (N, Q, C)
         alpha, gamma = self.cost_alpha, self.cost_gamma
         neg = (1 - alpha) * (out_prob ** gamma) * (-(1 - out_prob + 1e-8).log())

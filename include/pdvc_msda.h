@@ -37,6 +37,10 @@
  *   pdvc_layernorm_backward_f32     <- NewModel front-end's ln(h) + residual (NewModel.py:41-65)
  *   pdvc_lsap_f32                   <- HungarianMatcher's scipy.optimize.linear_sum_assignment per video
  *                                      (pdvc/matcher.py:119-121), same algorithm and tie rule, on the GPU
+ *   pdvc_match_cost_f32             <- HungarianMatcher's cost matrix (pdvc/matcher.py:87-117), torch's op order
+ *   pdvc_set_losses_*               <- SetCriterion's loss terms of every (layer, video) problem and their
+ *                                      gradients (pdvc/criterion.py:46-123 loss_labels / loss_boxes,
+ *                                      :200-248 cross_entropy_with_gaussian_mask / sigmoid_focal_loss)
  *   pdvc_groupnorm_rows_*           <- nn.GroupNorm(32, d) of the base encoder's pyramid levels
  *                                      (pdvc/base_encoder.py:32-41), on channels-last rows
  *   pdvc_colsum_f32                 <- the bias gradients (sum over rows of dY) of those nn.Linear layers
@@ -319,6 +323,30 @@ int pdvc_layernorm_backward_f32(const float* x, const float* gamma, const float*
  * (row_ind, col_ind) of the (Q, sizes[p]) matrix; entries past sizes[p] are not written. */
 int pdvc_lsap_f32(const float* costs, int num_problems, int num_query, int max_targets, const int32_t* sizes_host,
                   const int32_t* sizes_dev, int64_t* query_out, int64_t* target_out, void* stream);
+
+/* ---- set criterion: matching cost and loss terms (pdvc/matcher.py:87-117, pdvc/criterion.py:46-123,200-248) ----
+ * P problems (decoder layer x video) of Q queries, C classes, E target slots.  cost (P, Q, E) =
+ * w_bbox * L1 + w_class * (focal pos - neg at the target's label) + w_giou * (-GIoU), every operation rounded to
+ * fp32 in the order torch evaluates HungarianMatcher.cost_padded (alpha and 1 - alpha passed as the host rounds
+ * them); exp / log / division as the device library rounds them. */
+int pdvc_match_cost_f32(const float* logits, const float* boxes, const int64_t* labels, const float* tboxes, int P,
+                        int Q, int C, int E, float alpha, float one_minus_alpha, float gamma, float w_bbox,
+                        float w_class, float w_giou, float* cost, void* stream);
+/* losses (P, 6) = focal ce / num_boxes, counter BCE (Gaussian-masked), L1 / num_boxes, (1 - GIoU) / num_boxes,
+ * self-IoU of the matched predictions, cardinality error; logits (P, Q, C), boxes (P, Q, 2) (centre, length),
+ * count (P, K1); labels (P, E) int64, tboxes (P, E, 2); nmatch (P) int64 = the true target count (ranks used);
+ * num_boxes (P) float; match_query / match_target (P, E) int64 from pdvc_lsap_f32; query_mask (P, Q) u8 or NULL;
+ * counter_rate (K1).  Local gradients written: dlogit (P, Q, C), dcount (P, K1), dbox (3, P, Q, 2) (L1, GIoU,
+ * self-IoU planes).  E <= 64. */
+int pdvc_set_losses_f32(const float* logits, const float* boxes, const float* count, const int64_t* labels,
+                        const float* tboxes, const int64_t* nmatch, const float* num_boxes, const int64_t* match_query,
+                        const int64_t* match_target, const uint8_t* query_mask, const float* counter_rate, int P,
+                        int Q, int C, int E, int K1, float focal_alpha, float focal_gamma, int gau_mask, float beta,
+                        float* losses, float* dlogit, float* dcount, float* dbox, void* stream);
+/* grad_logits = g[:, 0] dlogit, grad_count = g[:, 1] dcount, grad_boxes = g[:, 2..4] . dbox planes; g (P, 6). */
+int pdvc_set_losses_backward_f32(const float* grad_losses, const float* dlogit, const float* dcount, const float* dbox,
+                                 int P, int Q, int C, int K1, float* grad_logits, float* grad_count, float* grad_boxes,
+                                 void* stream);
 
 /* ---- GroupNorm on channels-last rows (the base encoder's nn.GroupNorm(G, C) after each Conv1d) -------------
  * x, y, dy, dx (N, T, C) row-major; group g = channels [g*C/G, (g+1)*C/G) of every row of a video; mean, rstd
