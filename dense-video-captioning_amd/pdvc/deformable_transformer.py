@@ -19,12 +19,14 @@ from . import hostio
 from .ops.functions import add_dropout_layernorm
 
 from .box_ops import inverse_sigmoid
-from .ops.functions.linear import add_row_bias, dense
+from .ops.functions import linear as _lin
+from .ops.functions.linear import PackedLinearFunction, add_row_bias, dense
 from .ops.modules import MSDeformAttn
 from .ops.modules.linear import Linear
 from .ops.functions.attention import query_self_attention
 from .ops.functions.ffn import ffn_block, use_ffn_block
 from .ops.functions.attn_block import encoder_attn_block, use_attn_block
+from .ops.functions.boxref import box_refine
 from .ops.functions.posembed import level_pos_rows, level_pos_rows_split
 from .position_encoding import PyramidPosEmbed
 
@@ -237,8 +239,12 @@ class QuerySelfAttention(nn.Module):
         key_padding_mask (N, Q) True = ignore.  Returns (N, Q, E)."""
         E = self.embed_dim
         w, b = self.in_proj_weight, self.in_proj_bias
-        qk = dense(qk_in, w[:2 * E], b[:2 * E])
-        v = dense(v_in, w[2 * E:], b[2 * E:])
+        if qk_in.is_cuda and qk_in.dtype == torch.float32 and _lin.BACKEND != "hip":
+            # both row blocks of in_proj with one packed weight gradient (no per-slice zero fill, copy and add)
+            qk, v = PackedLinearFunction.apply(w, b, (2 * E, E), qk_in, v_in)
+        else:
+            qk = dense(qk_in, w[:2 * E], b[:2 * E])
+            v = dense(v_in, w[2 * E:], b[2 * E:])
         p = self.dropout if self.training else 0.0
         out = query_self_attention(qk, v, key_padding_mask, self.num_heads, p)
         return self.out_proj(out)
@@ -309,13 +315,10 @@ class DeformableTransformerDecoder(nn.Module):
             if not disable_iterative_refine and self.bbox_head is not None:
                 tmp = self.bbox_head[lid](output)
                 box_out.append(tmp)
-                if reference_points.shape[-1] == 2:
-                    new_ref = (tmp + inverse_sigmoid(reference_points)).sigmoid()
-                else:
-                    # deformable_transformer.py:311-313: only the centre is refined from a 1-d reference
-                    new_ref = torch.cat([tmp[..., :1] + inverse_sigmoid(reference_points), tmp[..., 1:]], -1)
-                    new_ref = new_ref.sigmoid()
-                reference_points = new_ref.detach()
+                # (tmp + inverse_sigmoid(ref)).sigmoid(); a 1-d reference refines only the centre
+                # (deformable_transformer.py:311-313); detached, so computed outside autograd in one launch
+                with torch.no_grad():
+                    reference_points = box_refine(tmp.detach(), reference_points.detach())
             if self.return_intermediate:
                 intermediate.append(output)
                 intermediate_refs.append(reference_points)

@@ -110,17 +110,18 @@ def wgrad_splits(rows):
     return 1
 
 
-def colsum(x):
+def colsum(x, out=None):
     """x.sum(0) for a 2-D fp32 GPU tensor: pdvc_colsum_f32 (csrc/colsum.hip) when the rows are long and
-    16-byte aligned, else torch.  The bias gradient of every projection."""
+    16-byte aligned, else torch.  The bias gradient of every projection.  out: a contiguous (cols,) destination."""
     rows, cols = x.shape
     if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and cols % 4 == 0 and rows >= 512
             and x.data_ptr() % 16 == 0):
-        return x.sum(0)
+        return x.sum(0) if out is None else torch.sum(x, 0, out=out)
     cblocks = (cols // 4 + 15) // 16
     parts = max(1, min(256, (8 * CU) // cblocks, rows // 64))  # >= 8 workgroups per CU on wide gradients
     ws = torch.empty(parts * cols, dtype=x.dtype, device=x.device)
-    out = torch.empty(cols, dtype=x.dtype, device=x.device)
+    if out is None:
+        out = torch.empty(cols, dtype=x.dtype, device=x.device)
     _n.call("pdvc_colsum_f32", _n.ptr(x), rows, cols, parts, _n.ptr(ws), _n.ptr(out), _n.stream())
     return out
 
@@ -145,15 +146,60 @@ def add_row_bias(x, bias):
     return AddRowBias.apply(x, bias)
 
 
-def wgrad_mm(gy, x):
-    """gy^T x for row-major gy (rows, O) and x (rows, I): the weight-gradient product, split over K."""
+def wgrad_mm(gy, x, out=None):
+    """gy^T x for row-major gy (rows, O) and x (rows, I): the weight-gradient product, split over K.  out: a
+    contiguous (O, I) destination (a row block of a packed weight's gradient)."""
     rows = gy.shape[0]
     if gy.shape[1] == 1:  # a 1-wide layer: a weighted column sum, not an (M = 1) GEMM (~1 TB/s on hipBLASLt)
-        return colsum((x * gy).contiguous()).view(1, -1)
+        r = colsum((x * gy).contiguous()).view(1, -1)
+        return r if out is None else out.copy_(r)
     s = wgrad_splits(rows)
     if s == 1:
-        return torch.mm(gy.t(), x)
-    return torch.bmm(gy.reshape(s, rows // s, gy.shape[1]).transpose(1, 2), x.reshape(s, rows // s, x.shape[1])).sum(0)
+        return torch.mm(gy.t(), x) if out is None else torch.mm(gy.t(), x, out=out)
+    p = torch.bmm(gy.reshape(s, rows // s, gy.shape[1]).transpose(1, 2), x.reshape(s, rows // s, x.shape[1]))
+    return p.sum(0) if out is None else torch.sum(p, 0, out=out)
+
+
+class PackedLinearFunction(Function):
+    """Row blocks of ONE packed nn.Linear weight applied to different inputs, y_i = x_i W[r_i:r_i+1]^T + b[...]:
+    nn.MultiheadAttention's in_proj over the (query | key) input and the value input (torch's MHA slices
+    in_proj_weight the same way).  The blocks' weight and bias gradients are written into one packed gradient
+    (GEMM / column-sum out= views), where per-slice autograd built a zero-filled full-size gradient, copied the
+    block in and added the others (SliceBackward: a fill, a copy and an add per slice and step)."""
+
+    @staticmethod
+    def forward(ctx, weight, bias, rows, *xs):
+        outs = []
+        r0 = 0
+        for x, r in zip(xs, rows):
+            x2 = x.reshape(-1, x.shape[-1])
+            y = torch.addmm(bias[r0:r0 + r], x2, weight[r0:r0 + r].t())
+            outs.append(y.view(*x.shape[:-1], r))
+            r0 += r
+        ctx.rows = rows
+        ctx.shapes = [x.shape for x in xs]
+        ctx.save_for_backward(weight, *[x.reshape(-1, x.shape[-1]) for x in xs])
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gys):
+        weight, *x2s = ctx.saved_tensors
+        gw = torch.zeros_like(weight) if any(g is None for g in gys) else torch.empty_like(weight)
+        gb = weight.new_zeros(weight.shape[0]) if any(g is None for g in gys) else weight.new_empty(weight.shape[0])
+        gxs = []
+        r0 = 0
+        for g, x2, r, shp in zip(gys, x2s, ctx.rows, ctx.shapes):
+            if g is None:
+                gxs.append(None)
+                r0 += r
+                continue
+            g2 = g.reshape(-1, r).contiguous()
+            w = weight[r0:r0 + r]
+            gxs.append(torch.mm(g2, w).view(shp) if ctx.needs_input_grad[3 + len(gxs)] else None)
+            wgrad_mm(g2, x2, out=gw[r0:r0 + r])
+            colsum(g2, out=gb[r0:r0 + r])
+            r0 += r
+        return (gw, gb, None) + tuple(gxs)
 
 
 class TorchLinearFunction(Function):

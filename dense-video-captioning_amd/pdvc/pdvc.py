@@ -18,7 +18,7 @@ from . import box_ops, hostio
 from .base_encoder import build_base_encoder
 from .ops.functions import linear as _lin
 from .ops.functions.linear import dense, multi_dense
-from .box_ops import inverse_sigmoid
+from .ops.functions.boxref import box_refine
 from .CaptioningHead import build_captioner
 from .CaptioningHead.LSTM_DSA import caption_steps
 from .criterion import SetCriterion
@@ -267,12 +267,7 @@ class PDVC(nn.Module):
                 coords.append(reference)
             else:
                 tmp = boxes[l_id] if boxes is not None else self.bbox_head[l_id](hs_l)
-                r = inverse_sigmoid(reference)
-                if r.shape[-1] == 2:
-                    tmp = tmp + r
-                else:
-                    tmp = torch.cat([tmp[..., :1] + r, tmp[..., 1:]], -1)
-                coords.append(tmp.sigmoid())
+                coords.append(box_refine(tmp, reference))  # sigmoid(tmp + inverse_sigmoid(reference)), one pass
         return classes, counts, coords
 
     def _pack(self, classes, counts, coords, cap_probs, seqs, query_mask=None):

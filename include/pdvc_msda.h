@@ -38,6 +38,9 @@
  *   pdvc_lsap_f32                   <- HungarianMatcher's scipy.optimize.linear_sum_assignment per video
  *                                      (pdvc/matcher.py:119-121), same algorithm and tie rule, on the GPU
  *   pdvc_match_cost_f32             <- HungarianMatcher's cost matrix (pdvc/matcher.py:87-117), torch's op order
+ *   pdvc_box_refine_*               <- iterative box refinement sigmoid(tmp + inverse_sigmoid(ref)) of the
+ *                                      decoder (deformable_transformer.py:303-313) and PDVC's box heads
+ *                                      (pdvc/pdvc.py:245-253, misc/detr_utils/misc.py:540-544)
  *   pdvc_set_losses_*               <- SetCriterion's loss terms of every (layer, video) problem and their
  *                                      gradients (pdvc/criterion.py:46-123 loss_labels / loss_boxes,
  *                                      :200-248 cross_entropy_with_gaussian_mask / sigmoid_focal_loss)
@@ -347,6 +350,15 @@ int pdvc_set_losses_f32(const float* logits, const float* boxes, const float* co
 int pdvc_set_losses_backward_f32(const float* grad_losses, const float* dlogit, const float* dcount, const float* dbox,
                                  int P, int Q, int C, int K1, float* grad_logits, float* grad_count, float* grad_boxes,
                                  void* stream);
+
+/* ---- box refinement: out = sigmoid(tmp + inverse_sigmoid(ref)) (deformable_transformer.py:303-313) ----------
+ * tmp, out (rows, 2) (centre, length); ref (rows, rd), rd = 2, or 1 (only the centre refined); inverse_sigmoid clamps
+ * to [0, 1] then log(max(x, eps) / max(1 - x, eps)).  Backward: grad_tmp = g s (1 - s), grad_ref (optional, NULL to
+ * skip) through inverse_sigmoid with torch's clamp convention. */
+int pdvc_box_refine_forward_f32(const float* tmp, const float* ref, long rows, int rd, float eps, float* out,
+                                void* stream);
+int pdvc_box_refine_backward_f32(const float* grad_out, const float* out, const float* ref, long rows, int rd,
+                                 float eps, float* grad_tmp, float* grad_ref, void* stream);
 
 /* ---- GroupNorm on channels-last rows (the base encoder's nn.GroupNorm(G, C) after each Conv1d) -------------
  * x, y, dy, dx (N, T, C) row-major; group g = channels [g*C/G, (g+1)*C/G) of every row of a video; mean, rstd

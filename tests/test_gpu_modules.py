@@ -160,6 +160,55 @@ def test_query_self_attention_streaming_backward_matches(Q, p, monkeypatch):
         close(x, y, 2e-5, name)
 
 
+def test_packed_in_proj_matches_per_slice_linears():
+    """PackedLinearFunction (the decoder self-attention's in_proj over the (query | key) and value inputs, one
+    packed weight gradient) against the per-slice F.linear form torch's nn.MultiheadAttention uses, in float64."""
+    from pdvc.ops.functions.linear import PackedLinearFunction
+    torch.manual_seed(3)
+    E = 512
+    w = torch.randn(3 * E, E, device=DEV) * 0.05
+    b = torch.randn(3 * E, device=DEV) * 0.1
+    a_in = torch.randn(4, 100, E, device=DEV)
+    v_in = torch.randn(4, 100, E, device=DEV)
+    ga, gv = torch.randn(4, 100, 2 * E, device=DEV), torch.randn(4, 100, E, device=DEV)
+    leaves = [t.clone().requires_grad_() for t in (w, b, a_in, v_in)]
+    qk, v = PackedLinearFunction.apply(leaves[0], leaves[1], (2 * E, E), leaves[2], leaves[3])
+    torch.autograd.backward((qk, v), (ga, gv))
+    ref = [t.double().requires_grad_() for t in (w, b, a_in, v_in)]
+    rqk = torch.nn.functional.linear(ref[2], ref[0][:2 * E], ref[1][:2 * E])
+    rv = torch.nn.functional.linear(ref[3], ref[0][2 * E:], ref[1][2 * E:])
+    torch.autograd.backward((rqk, rv), (ga.double(), gv.double()))
+    close(qk, rqk, 1e-5, "qk")
+    close(v, rv, 1e-5, "v")
+    for name, x, r in zip(("weight", "bias", "qk_in", "v_in"), leaves, ref):
+        close(x.grad, r.grad, 1e-4, "grad " + name)
+
+
+@pytest.mark.parametrize("rd", [1, 2])
+def test_box_refine_matches_inverse_sigmoid_chain(rd):
+    """box_refine (csrc/boxref.hip) against the reference's chain sigmoid(tmp + inverse_sigmoid(ref))
+    (misc/detr_utils/misc.py:540-544; a 1-d reference refines only the centre) in float64, forward and both
+    gradients, with references at and beyond the clamp edges (0, 1, eps, outside [0, 1])."""
+    from pdvc.box_ops import inverse_sigmoid
+    from pdvc.ops.functions.boxref import box_refine
+    torch.manual_seed(rd)
+    tmp = torch.randn(7, 100, 2, device=DEV)
+    ref = torch.rand(7, 100, rd, device=DEV)
+    edge = torch.tensor([0.0, 1.0, 1e-6, 1 - 1e-6, -0.2, 1.3], device=DEV)
+    ref.view(-1)[:edge.numel()] = edge
+    g = torch.randn(7, 100, 2, device=DEV)
+    t1, r1 = tmp.clone().requires_grad_(), ref.clone().requires_grad_()
+    out = box_refine(t1, r1)
+    out.backward(g)
+    t2, r2 = tmp.double().requires_grad_(), ref.double().requires_grad_()
+    r = inverse_sigmoid(r2)
+    ref_out = (t2 + r).sigmoid() if rd == 2 else torch.cat([t2[..., :1] + r, t2[..., 1:]], -1).sigmoid()
+    ref_out.backward(g.double())
+    close(out, ref_out, 1e-5, "out")
+    close(t1.grad, t2.grad, 1e-4, "grad tmp")
+    close(r1.grad, r2.grad, 1e-4, "grad ref")
+
+
 # ------------------------------------------------------------------------------------------------
 # transformer layers vs the reference layers (tests/golden/make_golden.py::module_layers)
 # ------------------------------------------------------------------------------------------------
