@@ -1,0 +1,79 @@
+// graphfix.hip -- rewrites the memset nodes of a captured hipGraph as kernel nodes, before instantiation.
+//
+// A small captured memset node does not re-apply on every replay on this ROCm stack: tools/memset_torch_probe.py
+// captures fill(5) -> hipMemsetAsync(160 B) -> add(1) on torch-allocated memory and finds the first element at 3073
+// instead of 1 from the second replay on, after eager work between replays (larger memsets, and hipMalloc'd buffers
+// in plain HIP, re-apply: tools/memset_graph_probe2/3.hip).  torch's multi-block reductions zero their semaphores with
+// such tiny memsets (4-32 B), and the 1024-video training step graph holds 11 of them: replays after the first
+// produced garbage in the gradients those reductions form (tools/check_graph_replays.py).  Every library zero-fill
+// of ours is a kernel already (zero_async, pdvc_common.h); this pass gives torch's memsets the same treatment in the
+// captured graph: each 1-D memset node becomes a kernel node that writes the same value over the same bytes, with the
+// same dependencies.
+#include <vector>
+
+#include "pdvc_common.h"
+
+namespace pdvc {
+
+__global__ __launch_bounds__(256) void memset_node_kernel(void* dst, size_t count, uint32_t value, int esize) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x) {
+        if (esize == 4)
+            reinterpret_cast<uint32_t*>(dst)[i] = value;
+        else if (esize == 2)
+            reinterpret_cast<uint16_t*>(dst)[i] = (uint16_t)value;
+        else
+            reinterpret_cast<uint8_t*>(dst)[i] = (uint8_t)value;
+    }
+}
+
+}  // namespace pdvc
+
+using namespace pdvc;
+
+extern "C" int pdvc_graph_replace_memsets(void* graph, int* replaced) {
+    PDVC_CHECK_ARG(graph != nullptr, "graph is NULL");
+    hipGraph_t g = (hipGraph_t)graph;
+    size_t n = 0;
+    if (hipGraphGetNodes(g, nullptr, &n) != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "hipGraphGetNodes");
+    std::vector<hipGraphNode_t> nodes(n);
+    if (n && hipGraphGetNodes(g, nodes.data(), &n) != hipSuccess)
+        return pdvc_set_error(PDVC_ERR_LAUNCH, "hipGraphGetNodes");
+    int done = 0;
+    for (hipGraphNode_t node : nodes) {
+        hipGraphNodeType t;
+        if (hipGraphNodeGetType(node, &t) != hipSuccess || t != hipGraphNodeTypeMemset) continue;
+        hipMemsetParams p;
+        if (hipGraphMemsetNodeGetParams(node, &p) != hipSuccess)
+            return pdvc_set_error(PDVC_ERR_LAUNCH, "hipGraphMemsetNodeGetParams");
+        if (p.height > 1 || (p.elementSize != 1 && p.elementSize != 2 && p.elementSize != 4)) continue;  // 2-D: kept
+        size_t nd = 0, no = 0;
+        hipGraphNodeGetDependencies(node, nullptr, &nd);
+        hipGraphNodeGetDependentNodes(node, nullptr, &no);
+        std::vector<hipGraphNode_t> deps(nd), outs(no);
+        if (nd) hipGraphNodeGetDependencies(node, deps.data(), &nd);
+        if (no) hipGraphNodeGetDependentNodes(node, outs.data(), &no);
+        void* dst = p.dst;
+        size_t count = p.width;
+        uint32_t value = p.value;
+        int esize = (int)p.elementSize;
+        void* args[] = {&dst, &count, &value, &esize};
+        hipKernelNodeParams kp{};
+        kp.func = reinterpret_cast<void*>(memset_node_kernel);
+        const size_t blocks = (count + 255) / 256;
+        kp.gridDim = dim3((unsigned)(blocks < 4096 ? (blocks ? blocks : 1) : 4096));
+        kp.blockDim = dim3(256);
+        kp.sharedMemBytes = 0;
+        kp.kernelParams = args;
+        kp.extra = nullptr;
+        hipGraphNode_t kn;
+        if (hipGraphAddKernelNode(&kn, g, nd ? deps.data() : nullptr, nd, &kp) != hipSuccess)
+            return pdvc_set_error(PDVC_ERR_LAUNCH, "hipGraphAddKernelNode");
+        for (hipGraphNode_t o : outs)
+            if (hipGraphAddDependencies(g, &kn, &o, 1) != hipSuccess)
+                return pdvc_set_error(PDVC_ERR_LAUNCH, "hipGraphAddDependencies");
+        if (hipGraphDestroyNode(node) != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "hipGraphDestroyNode");
+        ++done;
+    }
+    if (replaced) *replaced = done;
+    return PDVC_OK;
+}

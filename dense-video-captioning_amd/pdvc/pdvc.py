@@ -214,8 +214,10 @@ class PDVC(nn.Module):
         object.__setattr__(self, "_no_padding", no_padding)
         key = (tuple((tuple(t.shape), t.dtype) for t in sample), no_padding)
         from .precision import begin_capture
+        from .step_graph import rewriting_graphs
         begin_capture()
-        graphed = torch.cuda.make_graphed_callables(mod, sample, allow_unused_input=True)
+        with rewriting_graphs():  # the captured memset nodes become kernel nodes (step_graph.replace_memsets)
+            graphed = torch.cuda.make_graphed_callables(mod, sample, allow_unused_input=True)
         # kept outside the module registry: state_dict keys stay the reference's
         object.__setattr__(self, "_graph_key", key)
         object.__setattr__(self, "_graphed_trunk", graphed)

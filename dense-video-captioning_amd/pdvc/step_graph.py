@@ -24,7 +24,55 @@ the parameters' AccumulateGrad nodes alive, created on the stream of that eager 
 gradient accumulation then joins the default stream ended in a crash at capture end on ROCm 7
 (tests/test_gpu_batch.py test_capacity_step_graph_follows_a_ragged_stream, tools/diag_capacity_capture.py).
 """
+import ctypes
+import os
+
 import torch
+
+
+def replace_memsets(graph):
+    """Rewrite the memset nodes of a captured, not yet instantiated torch.cuda.CUDAGraph(keep_graph=True) as kernel
+    nodes (pdvc_graph_replace_memsets, csrc/graphfix.hip): torch's multi-block reductions zero their semaphores with
+    4-32 B memsets, and small captured memset nodes did not re-apply on replays after the first (DESIGN.md section 1;
+    tools/memset_torch_probe.py, tools/check_graph_replays.py).  PDVC_GRAPH_MEMSETS=keep skips it (diagnosis).
+    Returns the number of nodes rewritten."""
+    if os.environ.get("PDVC_GRAPH_MEMSETS") == "keep":
+        return 0
+    from . import _native as _n
+    count = ctypes.c_int(0)
+    _n.call("pdvc_graph_replace_memsets", ctypes.c_void_p(graph.raw_cuda_graph()), ctypes.byref(count))
+    return count.value
+
+
+class _RewritingGraph(torch.cuda.CUDAGraph):
+    """A CUDAGraph that keeps its hipGraph_t, rewrites its memset nodes and instantiates at capture end."""
+
+    def __new__(cls, keep_graph=False):
+        return super().__new__(cls, True)
+
+    def __init__(self, keep_graph=False):  # the native object is built by __init__: keep the hipGraph_t
+        super().__init__(True)
+
+    def capture_end(self):
+        super().capture_end()
+        replace_memsets(self)
+        self.instantiate()
+
+
+class rewriting_graphs:
+    """Within this context, graphs torch creates itself (torch.cuda.make_graphed_callables: the trunk graph,
+    PDVC.enable_graph) rewrite their memset nodes as StepGraph does."""
+
+    def __enter__(self):
+        import torch.cuda.graphs as tg
+        self._saved = (torch.cuda.CUDAGraph, tg.CUDAGraph)
+        torch.cuda.CUDAGraph = tg.CUDAGraph = _RewritingGraph  # make_graphed_callables looks up torch.cuda.CUDAGraph
+        return self
+
+    def __exit__(self, *exc):
+        import torch.cuda.graphs as tg
+        torch.cuda.CUDAGraph, tg.CUDAGraph = self._saved
+        return False
 
 
 class StepGraph:
@@ -49,9 +97,10 @@ class StepGraph:
                     reducer.finish()
         torch.cuda.current_stream().wait_stream(side)
         model.zero_grad(set_to_none=True)
-        # debug_dot: keep the captured hipGraph_t for hipGraphDebugDotPrint and the node walk of
-        # tools/diag_memset_graph.py (raw_cuda_graph() needs keep_graph)
-        self.graph = torch.cuda.CUDAGraph(keep_graph=True) if debug_dot else torch.cuda.CUDAGraph()
+        # the captured hipGraph_t is kept (keep_graph) so that its memset nodes are rewritten as kernel nodes before
+        # instantiation (replace_memsets: small captured memsets did not re-apply on replays);
+        # debug_dot: also dumped by hipGraphDebugDotPrint for tools/diag_memset_graph.py
+        self.graph = torch.cuda.CUDAGraph(keep_graph=True)
         if debug_dot:
             self.graph.enable_debug_mode()
         from .precision import begin_capture
@@ -66,6 +115,8 @@ class StepGraph:
                 reducer.suspended = False
         if debug_dot:
             self.graph.debug_dump(debug_dot)
+        self.memsets_replaced = replace_memsets(self.graph)
+        self.graph.instantiate()
 
     def _forward_backward(self):
         out, loss = self.model(self.dt, self.criterion, self.tit)

@@ -38,6 +38,8 @@
  *   pdvc_lsap_f32                   <- HungarianMatcher's scipy.optimize.linear_sum_assignment per video
  *                                      (pdvc/matcher.py:119-121), same algorithm and tie rule, on the GPU
  *   pdvc_match_cost_f32             <- HungarianMatcher's cost matrix (pdvc/matcher.py:87-117), torch's op order
+ *   pdvc_graph_replace_memsets      <- (no reference counterpart) the captured training-step graph's memset nodes
+ *                                      rewritten as kernel nodes before instantiation (csrc/graphfix.hip)
  *   pdvc_box_refine_*               <- iterative box refinement sigmoid(tmp + inverse_sigmoid(ref)) of the
  *                                      decoder (deformable_transformer.py:303-313) and PDVC's box heads
  *                                      (pdvc/pdvc.py:245-253, misc/detr_utils/misc.py:540-544)
@@ -350,6 +352,13 @@ int pdvc_set_losses_f32(const float* logits, const float* boxes, const float* co
 int pdvc_set_losses_backward_f32(const float* grad_losses, const float* dlogit, const float* dcount, const float* dbox,
                                  int P, int Q, int C, int K1, float* grad_logits, float* grad_count, float* grad_boxes,
                                  void* stream);
+
+/* ---- captured graphs: memset nodes as kernel nodes (csrc/graphfix.hip) -----------------------------------------
+ * graph: a hipGraph_t not yet instantiated (torch.cuda.CUDAGraph(keep_graph=True).raw_cuda_graph()).  Every 1-D
+ * memset node (element size 1, 2 or 4) is replaced by a kernel node writing the same value over the same elements,
+ * with the same dependencies; *replaced receives the count.  Small memset nodes did not re-apply on replays on this
+ * ROCm stack. */
+int pdvc_graph_replace_memsets(void* graph, int* replaced);
 
 /* ---- box refinement: out = sigmoid(tmp + inverse_sigmoid(ref)) (deformable_transformer.py:303-313) ----------
  * tmp, out (rows, 2) (centre, length); ref (rows, rd), rd = 2, or 1 (only the centre refined); inverse_sigmoid clamps

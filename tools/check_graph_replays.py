@@ -43,23 +43,28 @@ def main():
     torch.cuda.synchronize()
     ref = {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
     ref_total = total.item()
+    ref_losses = {k: float(v) for k, v in loss.items()}
     del out, loss, total
     model.zero_grad(set_to_none=True)
     sg = StepGraph(model, criterion, dt)
     print(f"videos {a.videos}: eager total loss {ref_total:.6f}, {len(ref)} gradients", flush=True)
+    gmax = max(v.abs().max().item() for v in ref.values())
     for r in range(3):
         t = sg.replay().item()
         torch.cuda.synchronize()
-        worst, wname = 0.0, ""
+        errs = []
         for n, p in model.named_parameters():
             if n not in ref:
                 continue
-            g = p.grad
-            e = ((g - ref[n]).abs().max() / ref[n].abs().max().clamp_min(1e-30)).item()
-            if e > worst:
-                worst, wname = e, n
-        print(f"replay {r}: total loss {t:.6f} (eager {ref_total:.6f}), worst relative gradient difference "
-              f"{worst:.3e} ({wname})", flush=True)
+            m = ref[n].abs().max().item()
+            if m < 1e-4 * gmax:  # near-zero in exact arithmetic (e.g. a softmax logit bias): no relative scale
+                continue
+            errs.append(((p.grad - ref[n]).abs().max().item() / m, n))
+        errs.sort(reverse=True)
+        dl = {k: float(v) - ref_losses[k] for k, v in sg.losses.items() if abs(float(v) - ref_losses[k]) >
+              1e-4 * max(abs(ref_losses[k]), 1e-3)}
+        print(f"replay {r}: total loss {t:.6f} (eager {ref_total:.6f}); worst relative gradient differences "
+              + ", ".join(f"{e:.2e} {n}" for e, n in errs[:4]) + f"; losses off by > 1e-4: {dl}", flush=True)
         junk = [torch.randn(4096 + 17 * i, device="cuda").sum() for i in range(64)]  # eager work between replays
         del junk
 
