@@ -45,6 +45,20 @@ def main():
     ref_total = total.item()
     ref_losses = {k: float(v) for k, v in loss.items()}
     del out, loss, total
+    # a second eager step: how far two eager steps on the same batch differ (atomics in the backward, split-K GEMMs,
+    # and through them near-tied set matchings of a random-init model) -- the scale the replays are judged on
+    model.zero_grad(set_to_none=True)
+    out, loss = model(dt, criterion, "queries")
+    total2 = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
+    total2.backward()
+    torch.cuda.synchronize()
+    gmax0 = max(v.abs().max().item() for v in ref.values())
+    e2 = sorted((((p.grad - ref[n]).abs().max().item() / ref[n].abs().max().item(), n)
+                 for n, p in model.named_parameters() if n in ref and ref[n].abs().max().item() >= 1e-4 * gmax0),
+                reverse=True)
+    print(f"second eager step: total loss {total2.item():.6f}; worst relative gradient differences "
+          + ", ".join(f"{e:.2e} {n}" for e, n in e2[:4]), flush=True)
+    del out, loss, total2
     model.zero_grad(set_to_none=True)
     sg = StepGraph(model, criterion, dt)
     print(f"videos {a.videos}: eager total loss {ref_total:.6f}, {len(ref)} gradients", flush=True)

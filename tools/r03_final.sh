@@ -10,6 +10,9 @@ echo "[$(date +%T)] tests"
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf > $O/tests.log 2>&1; rc=$?
 tail -3 $O/tests.log; ok $rc
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; rc=$?; tail -1 $O/smoke.log; ok $rc
+echo "[$(date +%T)] replays vs eager at 1024 videos"
+timeout -k 10 400 python -u tools/check_graph_replays.py --videos 1024 > $O/replays_1024.txt 2>&1; rc=$?
+grep -E "^videos|^second|^replay" $O/replays_1024.txt | cut -c1-200; ok $rc
 run() {  # name, then bench.py arguments
   local n=$1; shift
   echo "[$(date +%T)] $n"
