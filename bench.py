@@ -482,6 +482,7 @@ def main():
         return total
 
     step = eager_step
+    sg = None
     if a.graph == "trunk":
         model.enable_graph(dt)  # capture base encoder -> encoder -> decoder -> heads, fwd and bwd
     elif a.graph == "step":
@@ -665,6 +666,9 @@ def main():
         result["dropin_msda"] = dropin
     if stream_stats is not None:
         result["config"]["stream"] = stream_stats
+    if sg is not None:  # the replayed step's launches (graph nodes by type, after the memset-node rewrite)
+        result["config"]["graph_nodes_per_replay"] = dict(getattr(sg, "node_counts", {}),
+                                                          memsets_rewritten=getattr(sg, "memsets_replaced", None))
     ksteps = 2 if graphed else a.steps
     result["kernels"] = {n: {"launches": v["launches"], "avg_us": 1e3 * v["ms"] / max(v["launches"], 1),
                              "share_of_step": v["ms"] / ksteps / (1e3 * el / a.steps)} for n, v in ks.items()}

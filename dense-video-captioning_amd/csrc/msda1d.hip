@@ -1080,13 +1080,17 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
 #pragma unroll
             for (int u = 0; u < QU; ++u) {
                 float part[8];
+                // the 4-channel dot products on packed fp32 pairs: v_pk_mul + v_pk_fma + one add per corner row
+                const pf2 gxy = {g[u].x, g[u].y}, gzw = {g[u].z, g[u].w};
 #pragma unroll
                 for (int p = 0; p < kP; ++p) {
                     const char* r = lrow + grp_bcast<16>(ad[u], L * kP + p);
-                    const float4 u1 = *reinterpret_cast<const float4*>(r);
-                    const float4 u2 = *reinterpret_cast<const float4*>(r + 256);
-                    part[p] = g[u].x * u1.x + g[u].y * u1.y + g[u].z * u1.z + g[u].w * u1.w;
-                    part[4 + p] = g[u].x * u2.x + g[u].y * u2.y + g[u].z * u2.z + g[u].w * u2.w;
+                    const pf4 u1 = *reinterpret_cast<const pf4*>(r);
+                    const pf4 u2 = *reinterpret_cast<const pf4*>(r + 256);
+                    const pf2 t1 = __builtin_elementwise_fma(gzw, u1.zw, gxy * u1.xy);
+                    const pf2 t2 = __builtin_elementwise_fma(gzw, u2.zw, gxy * u2.xy);
+                    part[p] = t1.x + t1.y;
+                    part[4 + p] = t2.x + t2.y;
                 }
                 const bool u8 = (lane & 8) != 0;
 #pragma unroll
@@ -1205,6 +1209,7 @@ constexpr int kVQPT = 4;  // queries per thread in its sort passes: a launch chu
 // B16: also writes the bf16 rounding of every row into gv16 (the bf16 mode; a separate instantiation, so the
 // fp32 path keeps its registers: the pointer and its stores cost the depth-8 walk 9 spilled VGPRs)
 // ABL (measurement only, PDVC_VAL_ABLATE): 1 = stop after the sort, 2 = walk without the gradient-row gathers
+// (PDVC_VAL_ABLATE=1/2 select them for the depth-8 encoder walk, 3/4 for the depth-4 decoder walk)
 template <int CW, bool G4, int UG = 8, bool B16 = false, int ABL = 0>
 __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
                                                                      int Lq, int q0, int nq, int S, int M, int D,
@@ -1249,10 +1254,12 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
     int key[kVQPT][kP];
     float lwv[kVQPT][kP];
     // a thread takes kVQPT consecutive queries: neighbouring lanes are kVQPT queries apart, so on the coarse levels
-    // (where neighbouring queries sample the same rows) fewer lanes of one atomic hit the same counter
+    // (where neighbouring queries sample the same rows) fewer lanes of one atomic hit the same counter.  A chunk of
+    // at most one query per thread (the decoder: 100) spreads them one per thread instead (25 threads did all)
+    const bool spread = nq <= (int)blockDim.x;
 #pragma unroll
     for (int k = 0; k < kVQPT; ++k) {
-        const int qi = threadIdx.x * kVQPT + k;
+        const int qi = spread ? (k == 0 ? (int)threadIdx.x : nq) : (int)threadIdx.x * kVQPT + k;
 #pragma unroll
         for (int p = 0; p < kP; ++p) {
             key[k][p] = -1;
@@ -1274,6 +1281,22 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
         }
     }
     __syncthreads();
+    // G4: rows whose two buckets (t: high corner, t + 1: low corner) are both empty get no sample: zeros, written
+    // here from the bucket counts so that the stores drain while the scan and the scatter run (written after the
+    // scatter they were the decoder's longest phase: PDVC_VAL_ABLATE=3/4, sort 234 and walk-without-gathers 690 of
+    // 799 us).  First query chunk only; later chunks add into what the first wrote.  Every other row is written by
+    // the walk.
+    if constexpr (G4 && ABL != 1) {
+        if (!accumulate) {
+            float* obz = grad_value + ((size_t)b * S + st) * M * D + (size_t)m * D + (lane & 15) * 4;
+            uint16_t* obz16 = B16 ? gv16 + ((size_t)b * S + st) * M * D + (size_t)m * D + (lane & 15) * 4 : nullptr;
+            for (int t = threadIdx.x >> 4; t < T; t += blockDim.x >> 4)
+                if (off[t] == 0 && off[t + 1] == 0) {
+                    *reinterpret_cast<float4*>(obz + (size_t)t * M * D) = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (B16) *reinterpret_cast<uint2*>(obz16 + (size_t)t * M * D) = make_uint2(0u, 0u);
+                }
+        }
+    }
     // 2) exclusive scan of off[0 .. T+1] (off[T+1] = 0 before, total after): per-thread chunks + wave scan
     {
         const int len = T + 2;
@@ -1303,7 +1326,7 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
     // 3) scatter the samples into bucket order with their two corner coefficients
 #pragma unroll
     for (int k = 0; k < kVQPT; ++k) {
-        const int qi = threadIdx.x * kVQPT + k;
+        const int qi = spread ? (k == 0 ? (int)threadIdx.x : nq) : (int)threadIdx.x * kVQPT + k;
         if (qi < nq) {
             const float4 at = *reinterpret_cast<const float4*>(save_attn + sbase + (size_t)qi * kP);
             const float as[kP] = {at.x, at.y, at.z, at.w};
@@ -1348,18 +1371,11 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
     const uint8_t* mrow = vmask ? vmask + (size_t)b * S + st : nullptr;
     constexpr int U = 8;
     if constexpr (G4) {
-        // rows whose two buckets (t: high corner, t + 1: low corner) are both empty get no sample: zeros (first
-        // query chunk only; later chunks add into what the first wrote).  Every other row is written by the walk.
+        // (rows no sample touches were zeroed right after the histogram, above)
         const int gl = lane & 15;
         float* ob = grad_value + ((size_t)b * S + st) * MD + (size_t)m * D + gl * 4;
         // bf16 mode: the rounding of every row written, at the same offsets (the value projection's operand)
         uint16_t* ob16 = B16 ? gv16 + ((size_t)b * S + st) * MD + (size_t)m * D + gl * 4 : nullptr;
-        if (!accumulate)
-            for (int t = threadIdx.x >> 4; t < T; t += blockDim.x >> 4)
-                if (off[t] == off[t + 2]) {
-                    *reinterpret_cast<float4*>(ob + (size_t)t * MD) = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (B16) *reinterpret_cast<uint2*>(ob16 + (size_t)t * MD) = make_uint2(0u, 0u);
-                }
         // walk: 16-lane group vg owns rows [r0, r1) and reads buckets r0 .. r1; one sorted entry and one gathered
         // gradient row per sample, two running rows (key - 1 and key), each row written once when its last bucket
         // has passed -- no per-row search, at most two row writes per change of key
@@ -2132,7 +2148,21 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
                 const char* e = getenv("PDVC_VAL_ABLATE");
                 return e ? atoi(e) : 0;
             }();
-            if (g4 && !gv16 && (vabl == 1 || vabl == 2) && value_ug(num_query, S) == 8) {  // measurement only
+            if (g4 && !gv16 && (vabl == 3 || vabl == 4) && value_ug(num_query, S) == 4) {  // measurement only
+                const void* k = vabl == 3 ? (const void*)msda1d_bwd_value_kernel<1, true, 4, false, 1>
+                                          : (const void*)msda1d_bwd_value_kernel<1, true, 4, false, 2>;
+                (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+                if (vabl == 3)
+                    hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, 4, false, 1>), dim3((unsigned)nblk),
+                                       dim3(kVW * 64), lds, s, value_pad_mask, lv, num_query, q0, nq, S, num_heads,
+                                       head_dim, acc, grad_output, save_attn, save_loc, grad_value, gsums,
+                                       (const int64_t*)nullptr, (const int64_t*)nullptr, gv16);
+                else
+                    hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, 4, false, 2>), dim3((unsigned)nblk),
+                                       dim3(kVW * 64), lds, s, value_pad_mask, lv, num_query, q0, nq, S, num_heads,
+                                       head_dim, acc, grad_output, save_attn, save_loc, grad_value, gsums,
+                                       (const int64_t*)nullptr, (const int64_t*)nullptr, gv16);
+            } else if (g4 && !gv16 && (vabl == 1 || vabl == 2) && value_ug(num_query, S) == 8) {  // measurement only
                 const void* k = vabl == 1 ? (const void*)msda1d_bwd_value_kernel<1, true, 8, false, 1>
                                           : (const void*)msda1d_bwd_value_kernel<1, true, 8, false, 2>;
                 (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);

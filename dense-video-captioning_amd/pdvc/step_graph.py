@@ -44,6 +44,27 @@ def replace_memsets(graph):
     return count.value
 
 
+def graph_node_counts(graph):
+    """Nodes of a kept captured graph by type ({"kernel": k, "memcpy": c, ...}): the launches of one replay."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    raw = ctypes.c_void_p(graph.raw_cuda_graph())
+    n = ctypes.c_size_t(0)
+    if hip.hipGraphGetNodes(raw, None, ctypes.byref(n)) != 0:
+        return {}
+    nodes = (ctypes.c_void_p * n.value)()
+    hip.hipGraphGetNodes(raw, nodes, ctypes.byref(n))
+    names = {0: "kernel", 1: "memcpy", 2: "memset", 3: "host", 4: "graph", 5: "empty", 6: "wait_event",
+             7: "event_record"}
+    out = {}
+    for nd in nodes:
+        t = ctypes.c_int(-1)
+        hip.hipGraphNodeGetType(ctypes.c_void_p(nd), ctypes.byref(t))
+        k = names.get(t.value, str(t.value))
+        out[k] = out.get(k, 0) + 1
+    out["total"] = int(n.value)
+    return out
+
+
 class _RewritingGraph(torch.cuda.CUDAGraph):
     """A CUDAGraph that keeps its hipGraph_t, rewrites its memset nodes and instantiates at capture end."""
 
@@ -116,6 +137,7 @@ class StepGraph:
         if debug_dot:
             self.graph.debug_dump(debug_dot)
         self.memsets_replaced = replace_memsets(self.graph)
+        self.node_counts = graph_node_counts(self.graph)  # the launches of one replay, by node type
         self.graph.instantiate()
 
     def _forward_backward(self):
