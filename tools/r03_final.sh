@@ -29,5 +29,7 @@ echo "[$(date +%T)] rocprof"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-dropin > $O/prof_bench.json 2> $O/prof.err; rc=$?
 ks=$(find $O/prof -name "*kernel_stats.csv" | head -1)
 if [ -n "$ks" ]; then python tools/profsum.py "$ks" 0 45 > $O/prof_summary.txt; head -8 $O/prof_summary.txt; fi
+kt=$(find $O/prof -name "*kernel_trace.csv" | head -1)
+if [ -n "$kt" ]; then python tools/profsteps.py "$kt" 45 > $O/prof_steps.txt; head -4 $O/prof_steps.txt; fi
 ok $rc
 echo "[$(date +%T)] done"
