@@ -312,7 +312,8 @@ def dropin_msda(T, videos=256, reps=10):
     lsi = torch.tensor([0] + list(np.cumsum(T_l)[:-1]), dtype=torch.int64, device=dev)
     g = torch.Generator(device=dev).manual_seed(0)
     value = torch.randn(videos, S, M, D, device=dev, generator=g)
-    res = {"op": "MultiScaleDeformableAttention.ms_deform_attn_forward / _backward (1-D fast path)",
+    res = {"op": "MultiScaleDeformableAttention.ms_deform_attn_forward / _backward (1-D fast path: whole-pyramid "
+                 "kernels at the encoder shape, L2-gather kernels at the decoder shape)",
            "videos": videos, "timing": f"HIP events, median of {reps} launches after 3 warm-ups"}
     for name, Lq in (("encoder", S), ("decoder", 100)):
         x = torch.rand(videos, Lq, M, L, P, device=dev, generator=g)

@@ -47,11 +47,11 @@ extern "C" int pdvc_graph_replace_memsets(void* graph, int* replaced) {
             return pdvc_set_error(PDVC_ERR_LAUNCH, "hipGraphMemsetNodeGetParams");
         if (p.height > 1 || (p.elementSize != 1 && p.elementSize != 2 && p.elementSize != 4)) continue;  // 2-D: kept
         size_t nd = 0, no = 0;
-        hipGraphNodeGetDependencies(node, nullptr, &nd);
-        hipGraphNodeGetDependentNodes(node, nullptr, &no);
+        (void)hipGraphNodeGetDependencies(node, nullptr, &nd);
+        (void)hipGraphNodeGetDependentNodes(node, nullptr, &no);
         std::vector<hipGraphNode_t> deps(nd), outs(no);
-        if (nd) hipGraphNodeGetDependencies(node, deps.data(), &nd);
-        if (no) hipGraphNodeGetDependentNodes(node, outs.data(), &no);
+        if (nd) (void)hipGraphNodeGetDependencies(node, deps.data(), &nd);
+        if (no) (void)hipGraphNodeGetDependentNodes(node, outs.data(), &no);
         void* dst = p.dst;
         size_t count = p.width;
         uint32_t value = p.value;

@@ -1554,8 +1554,14 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
 // one row corner is in range -- row 0 as h_low (weight 1 - h, d/dh = -1) for h >= 0, as h_high (weight 1 + h,
 // d/dh = +1) below -- so a sample is the 1-D sample scaled by fy = 1 - |h|.  PDVC passes y = 0.5: fy = 1.
 // -------------------------------------------------------------------------------------------------
+// the whole-pyramid drop-in kernels' condition: each staging phase fits the guarded 512-row layout (pick_pyr's)
+__device__ __forceinline__ bool dropin_pyr_fits(const Levels1d& lv) {
+    return lv.T[0] <= kPyrRows && lv.T[1] + lv.T[2] + lv.T[3] <= kPyrRows;
+}
+
 struct DropinSample {
     int roff;         // byte offset of corner row x0 inside the video's value rows
+    int i0;           // corner row x0 within the level (in [-1, T - 1] inside, 0 outside)
     float lw, fy, sy; // fraction of x, the row-corner factor, d(fy)/dh
     float a;          // attention weight
     bool ok1, ok2;    // corners x0, x0 + 1 in range (the sample inside its level in x and y)
@@ -1575,6 +1581,7 @@ __device__ __forceinline__ DropinSample dropin_sample(float lx, float ly, float 
     s.ok1 = inside && i0 >= 0;
     s.ok2 = inside && i0 + 1 <= T - 1;
     s.roff = (st + i0) * (MD * 4);  // a corner below the video's rows reads 0 through the buffer range check
+    s.i0 = i0;
     s.a = a;
     return s;
 }
@@ -1586,57 +1593,62 @@ __global__ __launch_bounds__(256) void msda_dropin_fwd_kernel(const float* __res
                                                               const int64_t* __restrict__ lsi,
                                                               const float* __restrict__ loc,
                                                               const float* __restrict__ attn, int Lq, int S, int M,
-                                                              int total_waves, float* __restrict__ out) {
+                                                              int total_waves, int pyr_first,
+                                                              float* __restrict__ out) {
     constexpr int D = 64;
     Levels1d lv;
     if (!dropin_levels(shapes, lsi, S, lv)) return;  // a 2-D table: msda2d_fwd_kernel's
+    if (pyr_first && dropin_pyr_fits(lv)) return;    // msda_dropin_fwd_pyr_kernel's
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
-    if (wave >= total_waves) return;
-    const WaveQuery w = wave_query<16>(wave, lane, Lq, M);
-    const int MD = M * D;
-    const int j = w.sub, l_own = j >> 2;
-    const size_t si = ((size_t)w.row * M + w.m) * kNS + j;  // (N, Lq, M, L, P) index of this lane's sample
-    const float2 lc = *reinterpret_cast<const float2*>(loc + 2 * si);
-    const DropinSample sm = dropin_sample(lc.x, lc.y, attn[si], lvl_sel(lv.T, l_own), lvl_sel(lv.start, l_own), MD);
-    const float w1 = sm.ok1 ? ((1.f - sm.lw) * sm.fy) * sm.a : 0.f, w2 = sm.ok2 ? (sm.lw * sm.fy) * sm.a : 0.f;
-    const int coff = (w.m * D + w.sub * 4) * 4;
-    const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(value + (size_t)__builtin_amdgcn_readfirstlane(w.b) * S * MD), (short)0, S * MD * 4, 0x00020000);
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int l = 0; l < kL; ++l) {
-        int rl = sm.roff;
-        float wl1 = w1, wl2 = w2;
-        __asm__ volatile("" : "+v"(rl), "+v"(wl1), "+v"(wl2) : "v"(acc.x), "v"(acc.y), "v"(acc.z), "v"(acc.w));
-        float4 v1[kP], v2[kP];
-        float c1[kP], c2[kP];
-#pragma unroll
-        for (int p = 0; p < kP; ++p) {
-            const int o = grp_bcast<16>(rl, l * kP + p) + coff;
-            c1[p] = grp_bcast<16>(wl1, l * kP + p);
-            c2[p] = grp_bcast<16>(wl2, l * kP + p);
-            const auto u1 = __builtin_amdgcn_raw_buffer_load_b128(vr, o, 0, 0);
-            const auto u2 = __builtin_amdgcn_raw_buffer_load_b128(vr, o + MD * 4, 0, 0);
-            v1[p] = make_float4(__uint_as_float(u1[0]), __uint_as_float(u1[1]), __uint_as_float(u1[2]),
-                                __uint_as_float(u1[3]));
-            v2[p] = make_float4(__uint_as_float(u2[0]), __uint_as_float(u2[1]), __uint_as_float(u2[2]),
-                                __uint_as_float(u2[3]));
+    const int wave0 = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
+    // one wave per 4 queries of one (video, head); grid-strided, so that after a pyramid launch (pyr_first) a small
+    // grid retires at once when the pyramid took the call
+    for (int wave = wave0; wave < total_waves; wave += 4 * (int)gridDim.x) {
+        const WaveQuery w = wave_query<16>(wave, lane, Lq, M);
+        const int MD = M * D;
+        const int j = w.sub, l_own = j >> 2;
+        const size_t si = ((size_t)w.row * M + w.m) * kNS + j;  // (N, Lq, M, L, P) index of this lane's sample
+        const float2 lc = *reinterpret_cast<const float2*>(loc + 2 * si);
+        const DropinSample sm = dropin_sample(lc.x, lc.y, attn[si], lvl_sel(lv.T, l_own), lvl_sel(lv.start, l_own), MD);
+        const float w1 = sm.ok1 ? ((1.f - sm.lw) * sm.fy) * sm.a : 0.f, w2 = sm.ok2 ? (sm.lw * sm.fy) * sm.a : 0.f;
+        const int coff = (w.m * D + w.sub * 4) * 4;
+        const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(value + (size_t)__builtin_amdgcn_readfirstlane(w.b) * S * MD), (short)0, S * MD * 4, 0x00020000);
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    #pragma unroll
+        for (int l = 0; l < kL; ++l) {
+            int rl = sm.roff;
+            float wl1 = w1, wl2 = w2;
+            __asm__ volatile("" : "+v"(rl), "+v"(wl1), "+v"(wl2) : "v"(acc.x), "v"(acc.y), "v"(acc.z), "v"(acc.w));
+            float4 v1[kP], v2[kP];
+            float c1[kP], c2[kP];
+    #pragma unroll
+            for (int p = 0; p < kP; ++p) {
+                const int o = grp_bcast<16>(rl, l * kP + p) + coff;
+                c1[p] = grp_bcast<16>(wl1, l * kP + p);
+                c2[p] = grp_bcast<16>(wl2, l * kP + p);
+                const auto u1 = __builtin_amdgcn_raw_buffer_load_b128(vr, o, 0, 0);
+                const auto u2 = __builtin_amdgcn_raw_buffer_load_b128(vr, o + MD * 4, 0, 0);
+                v1[p] = make_float4(__uint_as_float(u1[0]), __uint_as_float(u1[1]), __uint_as_float(u1[2]),
+                                    __uint_as_float(u1[3]));
+                v2[p] = make_float4(__uint_as_float(u2[0]), __uint_as_float(u2[1]), __uint_as_float(u2[2]),
+                                    __uint_as_float(u2[3]));
+            }
+    #pragma unroll
+            for (int p = 0; p < kP; ++p) {
+                acc.x = fmaf(c1[p], v1[p].x, acc.x);
+                acc.y = fmaf(c1[p], v1[p].y, acc.y);
+                acc.z = fmaf(c1[p], v1[p].z, acc.z);
+                acc.w = fmaf(c1[p], v1[p].w, acc.w);
+                acc.x = fmaf(c2[p], v2[p].x, acc.x);
+                acc.y = fmaf(c2[p], v2[p].y, acc.y);
+                acc.z = fmaf(c2[p], v2[p].z, acc.z);
+                acc.w = fmaf(c2[p], v2[p].w, acc.w);
+            }
         }
-#pragma unroll
-        for (int p = 0; p < kP; ++p) {
-            acc.x = fmaf(c1[p], v1[p].x, acc.x);
-            acc.y = fmaf(c1[p], v1[p].y, acc.y);
-            acc.z = fmaf(c1[p], v1[p].z, acc.z);
-            acc.w = fmaf(c1[p], v1[p].w, acc.w);
-            acc.x = fmaf(c2[p], v2[p].x, acc.x);
-            acc.y = fmaf(c2[p], v2[p].y, acc.y);
-            acc.z = fmaf(c2[p], v2[p].z, acc.z);
-            acc.w = fmaf(c2[p], v2[p].w, acc.w);
-        }
+        if (w.active)
+            *reinterpret_cast<float4*>(out + (size_t)w.row * MD + (size_t)w.m * D + w.sub * 4) = acc;
     }
-    if (w.active)
-        *reinterpret_cast<float4*>(out + (size_t)w.row * MD + (size_t)w.m * D + w.sub * 4) = acc;
 }
 
 // backward, query side: msda1d_bwd_query_dot_kernel's dot-product form and reduction; the owner lane writes
@@ -1646,77 +1658,288 @@ __global__ __launch_bounds__(256) void msda_dropin_fwd_kernel(const float* __res
 __global__ __launch_bounds__(256) void msda_dropin_bwd_query_kernel(
     const float* __restrict__ value, const int64_t* __restrict__ shapes, const int64_t* __restrict__ lsi,
     const float* __restrict__ loc, const float* __restrict__ attn, int Lq, int S, int M, int total_waves,
-    const float* __restrict__ gout, float* __restrict__ grad_loc, float* __restrict__ grad_attn,
+    int pyr_first, const float* __restrict__ gout, float* __restrict__ grad_loc, float* __restrict__ grad_attn,
     float* __restrict__ save_attn, float* __restrict__ save_loc) {
     constexpr int D = 64;
     Levels1d lv;
     if (!dropin_levels(shapes, lsi, S, lv)) return;
+    if (pyr_first && dropin_pyr_fits(lv)) return;  // msda_dropin_bwd_query_pyr_kernel's
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
-    if (wave >= total_waves) return;
-    const WaveQuery w = wave_query<16>(wave, lane, Lq, M);
-    const int MD = M * D;
-    const int c0 = w.sub * 4;
-    const int j = w.sub, l_own = j >> 2;
+    const int wave0 = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
+    // one wave per 4 queries of one (video, head); grid-strided, so that after a pyramid launch (pyr_first) a small
+    // grid retires at once when the pyramid took the call
+    for (int wave = wave0; wave < total_waves; wave += 4 * (int)gridDim.x) {
+        const WaveQuery w = wave_query<16>(wave, lane, Lq, M);
+        const int MD = M * D;
+        const int c0 = w.sub * 4;
+        const int j = w.sub, l_own = j >> 2;
+        const int T_own = lvl_sel(lv.T, l_own);
+        const size_t si = ((size_t)w.row * M + w.m) * kNS + j;
+        const float2 lc = *reinterpret_cast<const float2*>(loc + 2 * si);
+        const DropinSample sm = dropin_sample(lc.x, lc.y, attn[si], T_own, lvl_sel(lv.start, l_own), MD);
+        if (w.active) {
+            const size_t vi = save_index(w.b, w.m, l_own, w.q, j & 3, Lq, M);
+            save_loc[vi] = lc.x;
+            save_attn[vi] = sm.a * sm.fy;
+        }
+        const int coff = (w.m * D + c0) * 4;
+        const float4 g = *reinterpret_cast<const float4*>(gout + (size_t)w.row * MD + (size_t)w.m * D + c0);
+        const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(value + (size_t)__builtin_amdgcn_readfirstlane(w.b) * S * MD), (short)0, S * MD * 4, 0x00020000);
+        float d1 = 0.f, d2 = 0.f;
+    #pragma unroll
+        for (int l = 0; l < kL; ++l) {
+            float part[8];
+    #pragma unroll
+            for (int p = 0; p < kP; ++p) {
+                const int off = grp_bcast<16>(sm.roff, l * kP + p) + coff;
+                const auto u1 = __builtin_amdgcn_raw_buffer_load_b128(vr, off, 0, 0);
+                const auto u2 = __builtin_amdgcn_raw_buffer_load_b128(vr, off + MD * 4, 0, 0);
+                part[p] = g.x * __uint_as_float(u1[0]) + g.y * __uint_as_float(u1[1]) + g.z * __uint_as_float(u1[2]) +
+                          g.w * __uint_as_float(u1[3]);
+                part[4 + p] = g.x * __uint_as_float(u2[0]) + g.y * __uint_as_float(u2[1]) +
+                              g.z * __uint_as_float(u2[2]) + g.w * __uint_as_float(u2[3]);
+            }
+            const bool u8 = (lane & 8) != 0;
+    #pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float send = u8 ? part[i] : part[i + 4];
+                const float mine = u8 ? part[i + 4] : part[i];
+                part[i] = mine + grp_swap(send, 8);
+            }
+            const bool u2b = (lane & 2) != 0;
+    #pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const float send = u2b ? part[i] : part[i + 2];
+                const float mine = u2b ? part[i + 2] : part[i];
+                part[i] = mine + grp_swap(send, 2);
+            }
+            const bool u1b = (lane & 1) != 0;
+            const float send = u1b ? part[0] : part[1];
+            const float mine = u1b ? part[1] : part[0];
+            part[0] = mine + grp_swap(send, 1);
+            part[0] += grp_swap(part[0], 4);
+            const float other = grp_swap(part[0], 8);
+            if (l_own == l) {
+                d1 = (l < 2) ? part[0] : other;
+                d2 = (l < 2) ? other : part[0];
+            }
+        }
+        const float x1 = sm.ok1 ? d1 : 0.f, x2 = sm.ok2 ? d2 : 0.f;
+        const float dot = (1.f - sm.lw) * x1 + sm.lw * x2;
+        if (w.active) {
+            grad_attn[si] = sm.fy * dot;
+            *reinterpret_cast<float2*>(grad_loc + 2 * si) =
+                make_float2((float)T_own * ((sm.a * sm.fy) * (x2 - x1)), sm.a * (sm.sy * dot));
+        }
+    }
+}
+
+// -------------------------------------------------------------------------------------------------
+// The drop-in operator's encoder-shaped calls (4 Lq >= S: each position is sampled many times) on the whole-pyramid
+// kernels, as the product path's encoder runs: the head's value rows staged in LDS and every corner row read from
+// there (msda1d_fwd_pyr2_kernel's LDS-DMA staging; msda1d_bwd_query_pyr_kernel's two phases), the parameter phase
+// reading the drop-in layout (locations (N, Lq, M, L, P, 2), softmaxed weights) and the level table read on the
+// device.  They return without work when the table is not a lifted 1-D pyramid or a staging phase would not fit
+// (dropin_pyr_fits); the L2-gather kernels above, launched after them with pyr_first = 1, take exactly those calls.
+// -------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kPyrThreads) void msda_dropin_fwd_pyr_kernel(
+    const float* __restrict__ value, const int64_t* __restrict__ shapes, const int64_t* __restrict__ lsi,
+    const float* __restrict__ loc, const float* __restrict__ attn, int Lq, int S, int M, int qblocks,
+    float* __restrict__ out) {
+    Levels1d lv;
+    if (!dropin_levels(shapes, lsi, S, lv) || !dropin_pyr_fits(lv)) return;
+    extern __shared__ __attribute__((aligned(16))) float4 lds4[];
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);  // the query blocks and heads of a video share an XCD
+    const int qb = blk % qblocks, bm = blk / qblocks;
+    const int b = bm / M, m = bm - b * M;
+    const int slot = threadIdx.x >> 4, sub = threadIdx.x & 15;
+    const size_t MD = (size_t)M * 64;
+    const float* vsrc = value + (size_t)b * S * MD + (size_t)m * 64;
+    const char* lrow = reinterpret_cast<const char*>(lds4) + sub * 16;
+    const int n0 = lv.T[0], n1 = lv.T[1] + lv.T[2] + lv.T[3];
+    const bool single = n0 + n1 + 2 <= kLdsRows;
+    const int p2 = single ? 1 + n0 : kLdsRows - 1 - n1;  // LDS row of level 1's first position
+    pyr_zero_row(lds4, 0, 0);
+    pyr_zero_row(lds4, single ? n0 + n1 + 1 : n0 + 1, 64);
+    if (!single) pyr_zero_row(lds4, kLdsRows - 1, 128);
+    const int l_own = sub >> 2;
+    const int T_own = lvl_sel(lv.T, l_own), st_own = lvl_sel(lv.start, l_own);
+    const int base_own = l_own == 0 ? 1 : p2 + (st_own - lv.start[1]);
+    float2 lcv[kPyrQPS];
+    float av[kPyrQPS];
+#pragma unroll
+    for (int i = 0; i < kPyrQPS; ++i) {
+        const int q = qb * kPyrQ + slot + 64 * i;
+        const size_t si = (((size_t)b * Lq + (q < Lq ? q : 0)) * M + m) * kNS + sub;
+        lcv[i] = *reinterpret_cast<const float2*>(loc + 2 * si);
+        av[i] = attn[si];
+    }
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): the parameters before the DMAs (msda1d_fwd_pyr2_kernel)
+    pyr_dma_rows(lds4, vsrc, MD, lv.start[0], 1, single ? n0 + n1 : n0);
+    int adv[kPyrQPS];
+    float w1v[kPyrQPS], w2v[kPyrQPS];
+#pragma unroll
+    for (int i = 0; i < kPyrQPS; ++i) {  // msda_dropin_fwd_kernel's corner weights, bit for bit
+        const DropinSample sm = dropin_sample(lcv[i].x, lcv[i].y, av[i], T_own, 0, 0);
+        adv[i] = pyr_corner(base_own, sm.i0);
+        w1v[i] = sm.ok1 ? ((1.f - sm.lw) * sm.fy) * sm.a : 0.f;
+        w2v[i] = sm.ok2 ? (sm.lw * sm.fy) * sm.a : 0.f;
+    }
+    PAcc4 acc[kPyrQPS];
+#pragma unroll
+    for (int i = 0; i < kPyrQPS; ++i) acc[i] = pacc_zero();
+    PAcc4 tok = pacc_zero();
+    auto level = [&](auto Lc) {
+        constexpr int L = decltype(Lc)::value;
+#pragma unroll
+        for (int i = 0; i < kPyrQPS; ++i) {
+            pf4 v1[kP], v2[kP];
+            float c1[kP], c2[kP];
+            int ad = adv[i];
+            float wa = w1v[i], wb = w2v[i];
+            __asm__ volatile("" : "+v"(ad), "+v"(wa), "+v"(wb) : "v"(tok.lo), "v"(tok.hi));
+#pragma unroll
+            for (int p = 0; p < kP; ++p) {
+                const char* r = lrow + grp_bcast<16>(ad, L * kP + p);
+                c1[p] = grp_bcast<16>(wa, L * kP + p);
+                c2[p] = grp_bcast<16>(wb, L * kP + p);
+                v1[p] = *reinterpret_cast<const pf4*>(r);
+                v2[p] = *reinterpret_cast<const pf4*>(r + 256);
+            }
+#pragma unroll
+            for (int p = 0; p < kP; ++p) {
+                pacc_fma(acc[i], c1[p], v1[p]);
+                pacc_fma(acc[i], c2[p], v2[p]);
+            }
+            tok = acc[i];
+        }
+    };
+    __syncthreads();
+    if (single) {
+        level(std::integral_constant<int, 0>{});
+        level(std::integral_constant<int, 1>{});
+        level(std::integral_constant<int, 2>{});
+        level(std::integral_constant<int, 3>{});
+    } else {
+        const int pre = n0 + 2 > p2 ? n0 + 2 - p2 : 0;
+        pyr_dma_rows_async(lds4, vsrc, MD, lv.start[1] + pre, p2 + pre, n1 - pre);
+        level(std::integral_constant<int, 0>{});
+        pyr_dma_wait();
+        __syncthreads();
+        pyr_zero_row(lds4, p2 - 1, 0);
+        pyr_dma_rows(lds4, vsrc, MD, lv.start[1], p2, pre);
+        __syncthreads();
+        level(std::integral_constant<int, 1>{});
+        level(std::integral_constant<int, 2>{});
+        level(std::integral_constant<int, 3>{});
+    }
+#pragma unroll
+    for (int i = 0; i < kPyrQPS; ++i) {
+        const int q = qb * kPyrQ + slot + 64 * i;
+        if (q < Lq)
+            *reinterpret_cast<float4*>(out + ((size_t)b * Lq + q) * MD + (size_t)m * 64 + sub * 4) = pacc_f4(acc[i]);
+    }
+}
+
+// backward, query side: msda1d_bwd_query_pyr_kernel's staging (level 0, then levels 1..3) and dot-product reduction;
+// each phase's owner lanes write grad_attn and grad_loc of their samples in the drop-in layout (msda_dropin_bwd_query_
+// kernel's owner math: no softmax here, so nothing is carried between the phases), and the first phase writes the
+// level-major (location x, a * fy) slab of every sample for the value-gradient kernel
+__global__ __launch_bounds__(kPyrThreads) void msda_dropin_bwd_query_pyr_kernel(
+    const float* __restrict__ value, const int64_t* __restrict__ shapes, const int64_t* __restrict__ lsi,
+    const float* __restrict__ loc, const float* __restrict__ attn, int Lq, int S, int M, int qblocks,
+    const float* __restrict__ gout, float* __restrict__ grad_loc, float* __restrict__ grad_attn,
+    float* __restrict__ save_attn, float* __restrict__ save_loc) {
+    Levels1d lv;
+    if (!dropin_levels(shapes, lsi, S, lv) || !dropin_pyr_fits(lv)) return;
+    extern __shared__ __attribute__((aligned(16))) float4 lds4[];
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int qb = blk % qblocks, bm = blk / qblocks;
+    const int b = bm / M, m = bm - b * M;
+    const int slot = threadIdx.x >> 4, sub = threadIdx.x & 15, lane = threadIdx.x & 63;
+    const int MD = M * 64;
+    const float* vsrc = value + (size_t)b * S * MD + (size_t)m * 64;
+    const int l_own = sub >> 2, p_own = sub & 3;
     const int T_own = lvl_sel(lv.T, l_own);
-    const size_t si = ((size_t)w.row * M + w.m) * kNS + j;
-    const float2 lc = *reinterpret_cast<const float2*>(loc + 2 * si);
-    const DropinSample sm = dropin_sample(lc.x, lc.y, attn[si], T_own, lvl_sel(lv.start, l_own), MD);
-    if (w.active) {
-        const size_t vi = save_index(w.b, w.m, l_own, w.q, j & 3, Lq, M);
-        save_loc[vi] = lc.x;
-        save_attn[vi] = sm.a * sm.fy;
-    }
-    const int coff = (w.m * D + c0) * 4;
-    const float4 g = *reinterpret_cast<const float4*>(gout + (size_t)w.row * MD + (size_t)w.m * D + c0);
-    const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(value + (size_t)__builtin_amdgcn_readfirstlane(w.b) * S * MD), (short)0, S * MD * 4, 0x00020000);
-    float d1 = 0.f, d2 = 0.f;
+    const float Tf = (float)T_own;
+    const int base_own = pyr_base(lv, l_own);
+    const char* lrow = reinterpret_cast<const char*>(lds4) + sub * 16;
+
+    auto run_query = [&](int iq, auto L0c, auto L1c) {
+        constexpr int L0 = decltype(L0c)::value, L1 = decltype(L1c)::value;
+        const int q0 = qb * kBqQ + slot + 64 * iq;
+        const bool act = q0 < Lq;
+        const int q = act ? q0 : Lq - 1;
+        const size_t row = (size_t)b * Lq + q;
+        const float4 g = *reinterpret_cast<const float4*>(gout + row * MD + (size_t)m * 64 + sub * 4);
+        const size_t si = (row * M + m) * kNS + sub;
+        const float2 lc = *reinterpret_cast<const float2*>(loc + 2 * si);
+        const DropinSample sm = dropin_sample(lc.x, lc.y, attn[si], T_own, 0, 0);
+        const int ad = pyr_corner(base_own, sm.i0);
+        float d1 = 0.f, d2 = 0.f;
+        const pf2 gxy = {g.x, g.y}, gzw = {g.z, g.w};
 #pragma unroll
-    for (int l = 0; l < kL; ++l) {
-        float part[8];
+        for (int L = L0; L < L1; ++L) {
+            float part[8];
 #pragma unroll
-        for (int p = 0; p < kP; ++p) {
-            const int off = grp_bcast<16>(sm.roff, l * kP + p) + coff;
-            const auto u1 = __builtin_amdgcn_raw_buffer_load_b128(vr, off, 0, 0);
-            const auto u2 = __builtin_amdgcn_raw_buffer_load_b128(vr, off + MD * 4, 0, 0);
-            part[p] = g.x * __uint_as_float(u1[0]) + g.y * __uint_as_float(u1[1]) + g.z * __uint_as_float(u1[2]) +
-                      g.w * __uint_as_float(u1[3]);
-            part[4 + p] = g.x * __uint_as_float(u2[0]) + g.y * __uint_as_float(u2[1]) +
-                          g.z * __uint_as_float(u2[2]) + g.w * __uint_as_float(u2[3]);
-        }
-        const bool u8 = (lane & 8) != 0;
+            for (int p = 0; p < kP; ++p) {
+                const char* r = lrow + grp_bcast<16>(ad, L * kP + p);
+                const pf4 u1 = *reinterpret_cast<const pf4*>(r);
+                const pf4 u2 = *reinterpret_cast<const pf4*>(r + 256);
+                const pf2 t1 = __builtin_elementwise_fma(gzw, u1.zw, gxy * u1.xy);
+                const pf2 t2 = __builtin_elementwise_fma(gzw, u2.zw, gxy * u2.xy);
+                part[p] = t1.x + t1.y;
+                part[4 + p] = t2.x + t2.y;
+            }
+            const bool u8 = (lane & 8) != 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float send = u8 ? part[i] : part[i + 4];
-            const float mine = u8 ? part[i + 4] : part[i];
-            part[i] = mine + grp_swap(send, 8);
-        }
-        const bool u2b = (lane & 2) != 0;
+            for (int k = 0; k < 4; ++k) {
+                const float send = u8 ? part[k] : part[k + 4];
+                const float mine = u8 ? part[k + 4] : part[k];
+                part[k] = mine + grp_swap(send, 8);
+            }
+            const bool u2b = (lane & 2) != 0;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const float send = u2b ? part[i] : part[i + 2];
-            const float mine = u2b ? part[i + 2] : part[i];
-            part[i] = mine + grp_swap(send, 2);
+            for (int k = 0; k < 2; ++k) {
+                const float send = u2b ? part[k] : part[k + 2];
+                const float mine = u2b ? part[k + 2] : part[k];
+                part[k] = mine + grp_swap(send, 2);
+            }
+            const bool u1b = (lane & 1) != 0;
+            const float send = u1b ? part[0] : part[1];
+            const float mine = u1b ? part[1] : part[0];
+            part[0] = mine + grp_swap(send, 1);
+            part[0] += grp_swap(part[0], 4);
+            const float other = grp_swap(part[0], 8);
+            if (l_own == L) {
+                d1 = (L < 2) ? part[0] : other;
+                d2 = (L < 2) ? other : part[0];
+            }
         }
-        const bool u1b = (lane & 1) != 0;
-        const float send = u1b ? part[0] : part[1];
-        const float mine = u1b ? part[1] : part[0];
-        part[0] = mine + grp_swap(send, 1);
-        part[0] += grp_swap(part[0], 4);
-        const float other = grp_swap(part[0], 8);
-        if (l_own == l) {
-            d1 = (l < 2) ? part[0] : other;
-            d2 = (l < 2) ? other : part[0];
+        if (act && L0 == 0) {
+            const size_t vi = save_index(b, m, l_own, q, p_own, Lq, M);
+            save_loc[vi] = lc.x;
+            save_attn[vi] = sm.a * sm.fy;
         }
-    }
-    const float x1 = sm.ok1 ? d1 : 0.f, x2 = sm.ok2 ? d2 : 0.f;
-    const float dot = (1.f - sm.lw) * x1 + sm.lw * x2;
-    if (w.active) {
-        grad_attn[si] = sm.fy * dot;
-        *reinterpret_cast<float2*>(grad_loc + 2 * si) =
-            make_float2((float)T_own * ((sm.a * sm.fy) * (x2 - x1)), sm.a * (sm.sy * dot));
-    }
+        if (act && l_own >= L0 && l_own < L1) {
+            const float x1 = sm.ok1 ? d1 : 0.f, x2 = sm.ok2 ? d2 : 0.f;
+            const float dot = (1.f - sm.lw) * x1 + sm.lw * x2;
+            grad_attn[si] = sm.fy * dot;
+            *reinterpret_cast<float2*>(grad_loc + 2 * si) =
+                make_float2(Tf * ((sm.a * sm.fy) * (x2 - x1)), sm.a * (sm.sy * dot));
+        }
+    };
+
+    pyr_stage_g(lds4, vsrc, MD, lv.start[0], lv.T[0]);
+    __syncthreads();
+#pragma unroll 1
+    for (int i = 0; i < kBqQPS; ++i) run_query(i, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+    __syncthreads();
+    pyr_stage_g(lds4, vsrc, MD, lv.start[1], lv.T[1] + lv.T[2] + lv.T[3]);
+    __syncthreads();
+#pragma unroll 1
+    for (int i = 0; i < kBqQPS; ++i) run_query(i, std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{});
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -2255,13 +2478,53 @@ bool dropin1d_applies(int S, int M, int D, int L, int Lq, int P) {
            (long)S * M * D * 4 < (1L << 31) && (long)Lq * M * D * 4 < (1L << 31);
 }
 
+// whole-pyramid drop-in kernels for encoder-shaped calls (4 Lq >= S, pick_pyr's rule); PDVC_DROPIN_PYR=0 keeps every
+// call on the L2-gather kernels (A/B).  Returns the query blocks per (video, head), 0 when the pyramid form is off.
+static int dropin_pyr_blocks(int S, int Lq, int per_block) {
+    static const bool on = [] {
+        const char* e = getenv("PDVC_DROPIN_PYR");
+        return !(e && e[0] == '0');
+    }();
+    if (!on || 4L * Lq < S) return 0;
+    static int attr = -1;
+    if (attr < 0) {
+        const hipError_t e1 = hipFuncSetAttribute((const void*)msda_dropin_fwd_pyr_kernel,
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPyr2LdsMax);
+        const hipError_t e2 = hipFuncSetAttribute((const void*)msda_dropin_bwd_query_pyr_kernel,
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPyrLds);
+        attr = (e1 == hipSuccess && e2 == hipSuccess) ? 1 : 0;
+        if (!attr) (void)hipGetLastError();
+    }
+    return attr ? (Lq + per_block - 1) / per_block : 0;
+}
+
+// the gather-form launch after a pyramid launch is needed only when a staging phase might not fit: with S <= 512
+// every level table summing to S fits (dropin_pyr_fits), and the fallback is skipped
+static bool dropin_may_not_fit(int S) { return S > kPyrRows; }
+
+// grid of the gather kernels: one workgroup per 4 waves, or -- behind a pyramid launch, where it usually retires at
+// once -- one chip's worth (8 workgroups of 4 waves on each of the 256 CUs), grid-strided over the waves
+static unsigned dropin_gather_grid(long tw, int pyr_first) {
+    const long full = (tw + 3) / 4;
+    return (unsigned)(pyr_first && full > 2048 ? 2048 : full);
+}
+
 int dropin1d_forward(const float* value, const int64_t* shapes, const int64_t* lsi, const float* loc,
                      const float* attn, int N, int S, int M, int Lq, float* out, hipStream_t s) {
     const long tw = (long)N * M * ((Lq + 3) / 4);
     if (tw == 0) return PDVC_OK;
     PDVC_CHECK_ARG(tw < (1L << 31) / 4, "too many rows");
-    hipLaunchKernelGGL(msda_dropin_fwd_kernel, dim3((unsigned)((tw + 3) / 4)), dim3(256), 0, s, value, shapes, lsi, loc,
-                       attn, Lq, S, M, (int)tw, out);
+    int pyr_first = 0;
+    if (const int qb = dropin_pyr_blocks(S, Lq, kPyrQ)) {
+        PDVC_CHECK_ARG((long)N * M * qb < (1L << 31), "too many query blocks");
+        hipLaunchKernelGGL(msda_dropin_fwd_pyr_kernel, dim3((unsigned)(N * M * qb)), dim3(kPyrThreads), kPyr2LdsMax, s,
+                           value, shapes, lsi, loc, attn, Lq, S, M, qb, out);
+        PDVC_CHECK_LAUNCH("msda_dropin_fwd_pyr_kernel");
+        pyr_first = 1;
+        if (!dropin_may_not_fit(S)) return PDVC_OK;
+    }
+    hipLaunchKernelGGL(msda_dropin_fwd_kernel, dim3(dropin_gather_grid(tw, pyr_first)), dim3(256), 0, s, value, shapes,
+                       lsi, loc, attn, Lq, S, M, (int)tw, pyr_first, out);
     PDVC_CHECK_LAUNCH("msda_dropin_fwd_kernel");
     return PDVC_OK;
 }
@@ -2275,9 +2538,21 @@ int dropin1d_backward(const float* value, const int64_t* shapes, const int64_t* 
     PDVC_CHECK_ARG(tw < (1L << 31) / 4, "too many rows");
     float* save_attn = workspace;
     float* save_loc = workspace + (size_t)N * Lq * M * kNS;
-    hipLaunchKernelGGL(msda_dropin_bwd_query_kernel, dim3((unsigned)((tw + 3) / 4)), dim3(256), 0, s, value, shapes,
-                       lsi, loc, attn, Lq, S, M, (int)tw, gout, grad_loc, grad_attn, save_attn, save_loc);
-    PDVC_CHECK_LAUNCH("msda_dropin_bwd_query_kernel");
+    int pyr_first = 0;
+    if (const int qb = dropin_pyr_blocks(S, Lq, kBqQ)) {
+        PDVC_CHECK_ARG((long)N * M * qb < (1L << 31), "too many query blocks");
+        hipLaunchKernelGGL(msda_dropin_bwd_query_pyr_kernel, dim3((unsigned)(N * M * qb)), dim3(kPyrThreads), kPyrLds,
+                           s, value, shapes, lsi, loc, attn, Lq, S, M, qb, gout, grad_loc, grad_attn, save_attn,
+                           save_loc);
+        PDVC_CHECK_LAUNCH("msda_dropin_bwd_query_pyr_kernel");
+        pyr_first = 1;
+    }
+    if (!pyr_first || dropin_may_not_fit(S)) {
+        hipLaunchKernelGGL(msda_dropin_bwd_query_kernel, dim3(dropin_gather_grid(tw, pyr_first)), dim3(256), 0, s, value,
+                           shapes, lsi, loc, attn, Lq, S, M, (int)tw, pyr_first, gout, grad_loc, grad_attn, save_attn,
+                           save_loc);
+        PDVC_CHECK_LAUNCH("msda_dropin_bwd_query_kernel");
+    }
     // value gradient: msda1d_bwd_value_kernel on the slab, its LDS sized for the longest possible level (S)
     static bool attr = false;
     if (!attr) {

@@ -143,6 +143,36 @@ def test_dropin_fast_path_full_size_vs_oracle(Lq, y_mode):
     close(ga, ega, 1e-4, "grad_attn")
 
 
+@pytest.mark.parametrize("T_l,Lq,y_mode,N", [
+    ([256, 128, 64, 32], 480, "half", 2),     # yc2's encoder: whole-pyramid kernels, one staging phase, no fallback
+    ([256, 128, 64, 32], 480, "mixed", 2),
+    ([512, 256, 128, 64], 1200, "mixed", 2),  # more queries than positions: 3 forward / 2 backward query blocks
+    ([512, 256, 128, 64], 240, "half", 2),    # 4 Lq == S: the smallest call the pyramid form takes, a partial block
+    ([600, 300, 150, 75], 1125, "half", 4),   # level 0 longer than a staging phase: the gather kernels take the call,
+                                              # grid-strided (9 024 waves over 2 048 workgroups)
+    ([400, 300, 200, 100], 1000, "mixed", 2),  # levels 1..3 longer than a staging phase: likewise, one pass
+])
+def test_dropin_pyramid_form_vs_oracle(T_l, Lq, y_mode, N):
+    """Encoder-shaped drop-in calls (4 Lq >= S) run on the whole-pyramid kernels (msda_dropin_fwd_pyr_kernel,
+    msda_dropin_bwd_query_pyr_kernel) when both staging phases fit 512 rows -- decided on the device from the level
+    table -- and on the L2-gather kernels launched after them otherwise; every case must equal the oracle."""
+    import MultiScaleDeformableAttention as MSDA
+    rng = np.random.RandomState(Lq + sum(T_l) + len(y_mode))
+    M = 8
+    value, shapes, lsi, loc, attn, gout = _lifted_inputs(rng, N, M, T_l, Lq, y_mode=y_mode)
+    ev = O.msda_forward(value, shapes, lsi, loc, attn, "zeros")
+    egv, egl, ega = O.msda_backward(value, shapes, lsi, loc, attn, gout, "zeros")
+    f32 = torch.float32
+    v, lo, a = cu(value, f32), cu(loc, f32), cu(attn, f32)
+    out = MSDA.ms_deform_attn_forward(v, cu(shapes), cu(lsi), lo, a, 64)
+    close(out, ev, 1e-4, "fwd")
+    gv, gl, ga = MSDA.ms_deform_attn_backward(v, cu(shapes), cu(lsi), lo, a, cu(gout, f32), 64)
+    close(gv, egv, 1e-4, "grad_value")
+    close(gl[..., 0], egl[..., 0], 1e-4, "grad_loc x")
+    close(gl[..., 1], egl[..., 1], 1e-4, "grad_loc y")
+    close(ga, ega, 1e-4, "grad_attn")
+
+
 def test_dropin_fast_path_leaves_2d_tables_to_the_general_kernels():
     """A 2-D table of the same sizes (4 levels x 4 points, D = 64) and a 1-D table whose start index is not the prefix
     sum of its lengths: both must take the general kernels (the fast path's device check refuses them) and still
