@@ -4,6 +4,9 @@
     python bench.py [--gpus N --steps K --warmup W --videos-per-gpu B]
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N rank processes itself (launch_ranks:
+one per GPU, RCCL); under torchrun it is one of them.  Either way the world size must equal --gpus.
+
 Workload (BASELINE.json metric config): cfgs/anet_tsp_pdvc.yml with C=768 features, T=512 frames
 (4 levels: 512/256/128/64 -> S=960), Q=100 queries, 2 encoder + 2 decoder layers, vocab 5748, E=4 events of
 13 words per video; synthetic inputs already resident in HBM; random-init weights.
@@ -414,8 +417,65 @@ def eval_main(a):
     print(json.dumps(result), flush=True)
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a, script=None, argv=None):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this same command line, one per GPU, with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (torchrun's contract; RCCL unless --dist-backend),
+    and return the exit status.  Runs before anything touches the GPU (the children are started, not exec'd).  Rank 0
+    prints the one JSON line; if any rank fails the others are stopped (by PID) and the status is non-zero."""
+    import subprocess
+    if not a.same_device:
+        have = torch.cuda.device_count()  # does not initialise the GPU on this image
+        if have < a.gpus:
+            print(f"bench.py: --gpus {a.gpus} but {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    port = free_port()
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL between processes)
+        cmd = [sys.executable, script or os.path.abspath(__file__)] + list(sys.argv[1:] if argv is None else argv)
+        procs.append(subprocess.Popen(cmd, env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    log(f"launched {a.gpus} rank processes (pids {[p.pid for p in procs]}), master port {port}")
+    status = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.5)
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 1
+                log(f"rank pid {p.pid} exited with {rc}: stopping the other ranks")
+                for q in live:
+                    q.terminate()
+                deadline = time.time() + 20
+                for q in live:
+                    try:
+                        q.wait(timeout=max(1.0, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+    return status
+
+
 def main():
     a = parse()
+    if a.mode == "eval" and a.gpus > 1:
+        raise SystemExit("bench.py --mode eval measures one GPU")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
     if a.mode == "eval":
         return eval_main(a)
     from pdvc.distributed import GradAllReducer, broadcast_parameters, init_distributed
@@ -426,8 +486,8 @@ def main():
     if a.gemm:
         _lin.BACKEND = a.gemm
     rank, world, local = init_distributed(a.dist_backend)
-    if world != a.gpus and rank == 0:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the initialised world size is {world}")
     device = torch.device("cuda:0" if a.same_device else f"cuda:{local}")
     torch.cuda.set_device(device)
     from pdvc import gemm_tuning
@@ -468,7 +528,10 @@ def main():
     def fwd_bwd():
         out, loss = model(cur[0], criterion, "queries")
         total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
-        opt.zero_grad(set_to_none=True)
+        if reducer is not None:
+            reducer.zero_grad()  # bucket-resident gradients (pdvc/distributed.py): one fill per bucket
+        else:
+            opt.zero_grad(set_to_none=True)
         total.backward()
         return total
 

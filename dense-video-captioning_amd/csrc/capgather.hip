@@ -573,17 +573,13 @@ extern "C" int pdvc_cap_value_grad_ex_f32(const uint8_t* value_pad_mask, const i
     const long per_step = 12L * max_rows_per_video * cP;  // LDS bytes per step of samples
     PDVC_CHECK_ARG(budget >= per_step, "too many caption rows per video (%d) for one step in LDS", max_rows_per_video);
     const int chunk = (int)(budget / per_step);
-    static bool attr = false;
-    if (!attr) {
-        const void* ks[4] = {(const void*)cap_value_grad_kernel<1>, (const void*)cap_value_grad_kernel<2>,
-                             (const void*)cap_value_grad_kernel<4>, (const void*)cap_value_grad_kernel<8>};
-        for (const void* k : ks)
-            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) != hipSuccess) {
-                (void)hipGetLastError();
-                return pdvc_set_error(PDVC_ERR_LAUNCH, "cap_value_grad_kernel: cannot raise the LDS limit");
-            }
-        attr = true;
-    }
+    static std::atomic<int> done[kMaxDevices];
+    if (const int rc = lds_optin(done, {{(const void*)cap_value_grad_kernel<1>, 96 * 1024},
+                                        {(const void*)cap_value_grad_kernel<2>, 96 * 1024},
+                                        {(const void*)cap_value_grad_kernel<4>, 96 * 1024},
+                                        {(const void*)cap_value_grad_kernel<8>, 96 * 1024}},
+                                 "cap_value_grad_kernel"))
+        return rc;
     const int cw = head_dim <= 64 ? 1 : head_dim <= 128 ? 2 : head_dim <= 256 ? 4 : 8;
     for (int s0 = 0; s0 < steps; s0 += chunk) {
         const int ns = steps - s0 < chunk ? steps - s0 : chunk;

@@ -8,21 +8,27 @@
 // produced garbage in the gradients those reductions form (tools/check_graph_replays.py).  Every library zero-fill
 // of ours is a kernel already (zero_async, pdvc_common.h); this pass gives torch's memsets the same treatment in the
 // captured graph: each 1-D memset node becomes a kernel node that writes the same value over the same bytes, with the
-// same dependencies.
+// same dependencies.  Pitched (2-D) memsets are rewritten the same way; a node this pass cannot rewrite is an error,
+// never a silently kept memset.
 #include <vector>
 
 #include "pdvc_common.h"
 
 namespace pdvc {
 
-__global__ __launch_bounds__(256) void memset_node_kernel(void* dst, size_t count, uint32_t value, int esize) {
+// width elements of esize bytes per row, `height` rows `pitch` bytes apart (a 1-D memset: height 1)
+__global__ __launch_bounds__(256) void memset_node_kernel(char* dst, size_t width, size_t height, size_t pitch,
+                                                          uint32_t value, int esize) {
+    const size_t count = width * height;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / width, c = i - r * width;
+        char* at = dst + r * pitch + c * (size_t)esize;
         if (esize == 4)
-            reinterpret_cast<uint32_t*>(dst)[i] = value;
+            *reinterpret_cast<uint32_t*>(at) = value;
         else if (esize == 2)
-            reinterpret_cast<uint16_t*>(dst)[i] = (uint16_t)value;
+            *reinterpret_cast<uint16_t*>(at) = (uint16_t)value;
         else
-            reinterpret_cast<uint8_t*>(dst)[i] = (uint8_t)value;
+            *reinterpret_cast<uint8_t*>(at) = (uint8_t)value;
     }
 }
 
@@ -45,18 +51,22 @@ extern "C" int pdvc_graph_replace_memsets(void* graph, int* replaced) {
         hipMemsetParams p;
         if (hipGraphMemsetNodeGetParams(node, &p) != hipSuccess)
             return pdvc_set_error(PDVC_ERR_LAUNCH, "hipGraphMemsetNodeGetParams");
-        if (p.height > 1 || (p.elementSize != 1 && p.elementSize != 2 && p.elementSize != 4)) continue;  // 2-D: kept
+        if (p.elementSize != 1 && p.elementSize != 2 && p.elementSize != 4)
+            return pdvc_set_error(PDVC_ERR_INVALID_ARG, "memset node with element size %u: not rewritable",
+                                  (unsigned)p.elementSize);
         size_t nd = 0, no = 0;
         (void)hipGraphNodeGetDependencies(node, nullptr, &nd);
         (void)hipGraphNodeGetDependentNodes(node, nullptr, &no);
         std::vector<hipGraphNode_t> deps(nd), outs(no);
         if (nd) (void)hipGraphNodeGetDependencies(node, deps.data(), &nd);
         if (no) (void)hipGraphNodeGetDependentNodes(node, outs.data(), &no);
-        void* dst = p.dst;
-        size_t count = p.width;
+        char* dst = static_cast<char*>(p.dst);
+        size_t width = p.width, height = p.height ? p.height : 1;
+        size_t pitch = height > 1 ? p.pitch : width * p.elementSize;
         uint32_t value = p.value;
         int esize = (int)p.elementSize;
-        void* args[] = {&dst, &count, &value, &esize};
+        const size_t count = width * height;
+        void* args[] = {&dst, &width, &height, &pitch, &value, &esize};
         hipKernelNodeParams kp{};
         kp.func = reinterpret_cast<void*>(memset_node_kernel);
         const size_t blocks = (count + 255) / 256;

@@ -182,15 +182,8 @@ extern "C" int pdvc_lsap_f32(const float* costs, int num_problems, int num_query
     const size_t lds = lsap_lds(num_query, max_targets);
     PDVC_CHECK_ARG(lds <= 160 * 1024, "matching problem too large for LDS (%d queries x %d targets)", num_query,
                    max_targets);
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute((const void*)lsap_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
-            hipSuccess) {
-            (void)hipGetLastError();
-            return pdvc_set_error(PDVC_ERR_LAUNCH, "lsap: cannot raise the LDS limit");
-        }
-        attr = true;
-    }
+    static std::atomic<int> done[kMaxDevices];
+    if (const int rc = lds_optin(done, {{(const void*)lsap_kernel, 160 * 1024}}, "lsap")) return rc;
     hipLaunchKernelGGL(lsap_kernel, dim3((unsigned)num_problems), dim3(64), lds, (hipStream_t)stream, costs, num_query,
                        max_targets, sizes_dev, query_out, target_out);
     PDVC_CHECK_LAUNCH("lsap_kernel");

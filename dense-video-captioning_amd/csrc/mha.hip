@@ -954,19 +954,13 @@ static bool use_flash(int Q, int D) {
 }
 
 static int mha_attrs() {
-    static bool attr = false;
-    if (!attr) {
-        const void* ks[7] = {(const void*)mha_fwd_kernel, (const void*)mha_bwd_q_kernel, (const void*)mha_bwd_k_kernel,
-                             (const void*)mha_fwd_mfma_kernel, (const void*)mha_bwd_mfma_kernel,
-                             (const void*)mha_fwd_mfma2_kernel, (const void*)mha_bwd_mfma2_kernel};
-        for (const void* k : ks)
-            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) {
-                (void)hipGetLastError();
-                return pdvc_set_error(PDVC_ERR_LAUNCH, "mha: cannot raise the LDS limit");
-            }
-        attr = true;
-    }
-    return PDVC_OK;
+    static std::atomic<int> done[kMaxDevices];
+    const int b = 160 * 1024;
+    return lds_optin(done, {{(const void*)mha_fwd_kernel, b}, {(const void*)mha_bwd_q_kernel, b},
+                            {(const void*)mha_bwd_k_kernel, b}, {(const void*)mha_fwd_mfma_kernel, b},
+                            {(const void*)mha_bwd_mfma_kernel, b}, {(const void*)mha_fwd_mfma2_kernel, b},
+                            {(const void*)mha_bwd_mfma2_kernel, b}},
+                     "mha");
 }
 
 extern "C" int pdvc_mha_forward_f32(const float* qk, const float* v, const uint8_t* key_padding_mask, int batch,

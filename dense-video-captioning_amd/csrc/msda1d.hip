@@ -2026,21 +2026,15 @@ static int bwdq_mode() {
 }
 
 static int bwdq_pyr_attrs() {
-    static int rc = -1;
-    if (rc < 0) {
-        const void* ks[6] = {(const void*)msda1d_bwd_query_pyr_kernel<1>, (const void*)msda1d_bwd_query_pyr_kernel<2>,
-                             (const void*)msda1d_bwd_query_pyr_kernel<1, 3>,
-                             (const void*)msda1d_bwd_query_pyr_kernel<2, 3>,
-                             (const void*)msda1d_bwd_query_pyr_kernel<1, 5>,
-                             (const void*)msda1d_bwd_query_pyr_kernel<2, 5>};
-        rc = PDVC_OK;
-        for (const void* k : ks)
-            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBqLds) != hipSuccess) {
-                (void)hipGetLastError();
-                rc = pdvc_set_error(PDVC_ERR_LAUNCH, "msda1d_bwd_query_pyr_kernel: cannot raise the LDS limit");
-            }
-    }
-    return rc;
+    static std::atomic<int> done[kMaxDevices];
+    const int b = (int)kBqLds;
+    return lds_optin(done, {{(const void*)msda1d_bwd_query_pyr_kernel<1>, b},
+                            {(const void*)msda1d_bwd_query_pyr_kernel<2>, b},
+                            {(const void*)msda1d_bwd_query_pyr_kernel<1, 3>, b},
+                            {(const void*)msda1d_bwd_query_pyr_kernel<2, 3>, b},
+                            {(const void*)msda1d_bwd_query_pyr_kernel<1, 5>, b},
+                            {(const void*)msda1d_bwd_query_pyr_kernel<2, 5>, b}},
+                     "msda1d_bwd_query_pyr_kernel");
 }
 
 // buffer-load forward at D = 64 (PDVC_MSDA_FWDBUF=0 selects the whole-pyramid / per-query kernels: A/B)
@@ -2053,19 +2047,12 @@ static bool fwd_buf() {
 }
 
 static int pyr_attrs() {
-    static int rc = -1;
-    if (rc < 0) {
-        const void* ks[4] = {(const void*)msda1d_fwd_pyr_kernel<1>, (const void*)msda1d_fwd_pyr_kernel<2>,
-                             (const void*)msda1d_fwd_pyr2_kernel<1>, (const void*)msda1d_fwd_pyr2_kernel<2>};
-        const size_t lds[4] = {kPyrLds, kPyrLds, kPyr2LdsMax, kPyr2LdsMax};
-        rc = PDVC_OK;
-        for (int i = 0; i < 4; ++i)
-            if (hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds[i]) != hipSuccess) {
-                (void)hipGetLastError();
-                rc = pdvc_set_error(PDVC_ERR_LAUNCH, "msda1d pyramid kernels: cannot raise the LDS limit");
-            }
-    }
-    return rc;
+    static std::atomic<int> done[kMaxDevices];
+    return lds_optin(done, {{(const void*)msda1d_fwd_pyr_kernel<1>, (int)kPyrLds},
+                            {(const void*)msda1d_fwd_pyr_kernel<2>, (int)kPyrLds},
+                            {(const void*)msda1d_fwd_pyr2_kernel<1>, (int)kPyr2LdsMax},
+                            {(const void*)msda1d_fwd_pyr2_kernel<2>, (int)kPyr2LdsMax}},
+                     "msda1d pyramid kernels");
 }
 
 // LDS-DMA pyramid forward (msda1d_fwd_pyr2_kernel; PDVC_PYR_DMA=0 selects msda1d_fwd_pyr_kernel: A/B)
@@ -2339,24 +2326,14 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
         int qchunk = (int)(budget / (per_sample * kP));
         if (qchunk > kVQPT * kVW * 64) qchunk = kVQPT * kVW * 64;
         if (qchunk > num_query) qchunk = num_query;
-        static bool attr = false;
-        if (!attr) {  // dynamic LDS <= 96 KiB by construction of qchunk (plus 32 B static)
-            hipError_t e1 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1, false>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-            hipError_t e2 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<2, false>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-            hipError_t e3 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1, true>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-            hipError_t e4 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1, true, 4>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-            hipError_t e5 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1, true, 4, true>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-            if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess) {
-                (void)hipGetLastError();
-                return pdvc_set_error(PDVC_ERR_LAUNCH, "msda1d_bwd_value_kernel: cannot raise the LDS limit");
-            }
-            attr = true;
-        }
+        static std::atomic<int> done[kMaxDevices];  // dynamic LDS <= 96 KiB by construction of qchunk (+32 B static)
+        if ((rc = lds_optin(done, {{(const void*)msda1d_bwd_value_kernel<1, false>, 96 * 1024},
+                                   {(const void*)msda1d_bwd_value_kernel<2, false>, 96 * 1024},
+                                   {(const void*)msda1d_bwd_value_kernel<1, true>, 96 * 1024},
+                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4>, 96 * 1024},
+                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, true>, 96 * 1024}},
+                            "msda1d_bwd_value_kernel")))
+            return rc;
         for (int q0 = 0; q0 < num_query; q0 += qchunk) {
             const int nq = (num_query - q0) < qchunk ? (num_query - q0) : qchunk;
             size_t lds = sizeof(int) * (2 * (size_t)(Tmax + 2) + 3 * (size_t)nq * kP + 2);
@@ -2486,15 +2463,10 @@ static int dropin_pyr_blocks(int S, int Lq, int per_block) {
         return !(e && e[0] == '0');
     }();
     if (!on || 4L * Lq < S) return 0;
-    static int attr = -1;
-    if (attr < 0) {
-        const hipError_t e1 = hipFuncSetAttribute((const void*)msda_dropin_fwd_pyr_kernel,
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPyr2LdsMax);
-        const hipError_t e2 = hipFuncSetAttribute((const void*)msda_dropin_bwd_query_pyr_kernel,
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPyrLds);
-        attr = (e1 == hipSuccess && e2 == hipSuccess) ? 1 : 0;
-        if (!attr) (void)hipGetLastError();
-    }
+    static std::atomic<int> done[kMaxDevices];
+    const bool attr = lds_optin(done, {{(const void*)msda_dropin_fwd_pyr_kernel, (int)kPyr2LdsMax},
+                                       {(const void*)msda_dropin_bwd_query_pyr_kernel, (int)kPyrLds}},
+                                "msda_dropin pyramid kernels") == PDVC_OK;
     return attr ? (Lq + per_block - 1) / per_block : 0;
 }
 
@@ -2554,18 +2526,11 @@ int dropin1d_backward(const float* value, const int64_t* shapes, const int64_t* 
         PDVC_CHECK_LAUNCH("msda_dropin_bwd_query_kernel");
     }
     // value gradient: msda1d_bwd_value_kernel on the slab, its LDS sized for the longest possible level (S)
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e3 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1, true>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-        hipError_t e4 = hipFuncSetAttribute((const void*)msda1d_bwd_value_kernel<1, true, 4>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-        if (e3 != hipSuccess || e4 != hipSuccess) {
-            (void)hipGetLastError();
-            return pdvc_set_error(PDVC_ERR_LAUNCH, "msda1d_bwd_value_kernel: cannot raise the LDS limit");
-        }
-        attr = true;
-    }
+    static std::atomic<int> done[kMaxDevices];
+    if (const int rc = lds_optin(done, {{(const void*)msda1d_bwd_value_kernel<1, true>, 96 * 1024},
+                                        {(const void*)msda1d_bwd_value_kernel<1, true, 4>, 96 * 1024}},
+                                 "msda1d_bwd_value_kernel"))
+        return rc;
     const long per_sample = 12;
     const long budget = 96 * 1024 - 8L * (S + 2) - 16;
     if (budget < per_sample * kP) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "spatial size %d too long", S);

@@ -1,7 +1,10 @@
 // pdvc_common.h -- shared device helpers for the PDVC HIP kernels (gfx950 / CDNA4, wave64).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <cstdlib>
+#include <initializer_list>
+#include <utility>
 #include <stdint.h>
 
 #include "pdvc_msda.h"
@@ -286,3 +289,23 @@ extern "C" int pdvc_set_error(int code, const char* fmt, ...);
         if (_e != hipSuccess)                                                                     \
             return pdvc_set_error(PDVC_ERR_LAUNCH, "%s: launch failed: %s", name, hipGetErrorString(_e)); \
     } while (0)
+
+namespace pdvc {
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) applies to the CURRENT device: the opt-in of a kernel set is made
+// once per device and remembered per device (`done`: a zero-initialised static array of kMaxDevices flags).  Two
+// threads that race on the first call both set the attribute, which is idempotent; a failure is not remembered.
+constexpr int kMaxDevices = 64;
+inline int lds_optin(std::atomic<int>* done, std::initializer_list<std::pair<const void*, int>> kernels,
+                     const char* what) {
+    int dev = -1;
+    const bool cacheable = hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kMaxDevices;
+    if (cacheable && done[dev].load(std::memory_order_acquire)) return PDVC_OK;
+    for (const auto& k : kernels)
+        if (hipFuncSetAttribute(k.first, hipFuncAttributeMaxDynamicSharedMemorySize, k.second) != hipSuccess) {
+            (void)hipGetLastError();
+            return pdvc_set_error(PDVC_ERR_LAUNCH, "%s: cannot raise the LDS limit", what);
+        }
+    if (cacheable) done[dev].store(1, std::memory_order_release);
+    return PDVC_OK;
+}
+}  // namespace pdvc

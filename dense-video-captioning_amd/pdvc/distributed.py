@@ -11,6 +11,13 @@ SURVEY.md section 8(e)) are detected on the first step and excluded, keeping `gr
 reference.  A parameter found active on the first step whose gradient is None on a later step (a branch
 not taken on this rank) contributes zeros, so every rank still issues the same collectives, and receives the
 rank mean like every other.  Semantics: after finish(), every active gradient is the mean over ranks.
+
+Bucket-resident gradients (torch DDP's gradient_as_bucket_view): after the first finish() every active
+parameter's `.grad` IS a view into its bucket's flat buffer.  A step that zeroes through `zero_grad()` (one fill
+per bucket, no set-to-None) keeps the views: backward's AccumulateGrad adds into them in place, and finish() is one
+all-reduce and one scale per bucket -- no concatenation, no copy back.  A caller that sets the gradients to None
+instead still gets the right result: a gradient that is not the bucket's view is copied into its slot at launch
+and the view is re-bound after the reduce (`copies` counts those copies; 0 on the resident path).
 """
 import os
 
@@ -53,6 +60,8 @@ class GradAllReducer:
         self.bucket_bytes = int(bucket_mb * 1024 * 1024)
         self.active = None  # params known to receive gradients (set after the first step)
         self.suspended = False  # True while a step graph is captured: finish() then reduces every bucket
+        self.flats = None  # one flat buffer per bucket once the active set is known
+        self.copies = 0  # gradients copied into a bucket (not resident); stays 0 when zero_grad() is used
         self._hooks = []
         self._build(self.params)
 
@@ -79,10 +88,39 @@ class GradAllReducer:
             self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
         self._reset()
 
+    def _make_flats(self):
+        """One flat buffer per bucket (dtype and device of its parameters) and each parameter's view into it."""
+        self.flats, self.views = [], {}
+        for b in self.buckets:
+            flat = torch.zeros(sum(p.numel() for p in b), dtype=b[0].dtype, device=b[0].device)
+            off = 0
+            for p in b:
+                n = p.numel()
+                self.views[id(p)] = flat[off:off + n].view_as(p)
+                off += n
+            self.flats.append(flat)
+
+    def _resident(self, p):
+        v = self.views[id(p)]
+        return p.grad is not None and p.grad.data_ptr() == v.data_ptr() and p.grad.shape == v.shape
+
     def _reset(self):
         self.pending = [len(b) for b in self.buckets]
         self.next_launch = 0
         self.works = []  # (bucket index, flat, work)
+
+    def zero_grad(self):
+        """Zero every bucket (one fill each) and bind the active parameters' gradients to their views; the next
+        backward accumulates into the buckets in place.  Before the first finish() this is zero_grad(set_to_none)."""
+        if self.flats is None:
+            for p in self.params:
+                p.grad = None
+            return
+        for f in self.flats:
+            f.zero_()
+        for p in self.active:
+            if not self._resident(p):
+                p.grad = self.views[id(p)]
 
     def _on_grad(self, p):
         bi = self.bucket_of.get(id(p))
@@ -95,18 +133,26 @@ class GradAllReducer:
                 self.next_launch += 1
 
     def _launch(self, bi):
-        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.buckets[bi]]
-        flat = torch.cat([g.reshape(-1) for g in grads])
+        flat = self.flats[bi]
+        for p in self.buckets[bi]:  # gradients that are not the bucket's views (set to None, or missing)
+            if not self._resident(p):
+                v = self.views[id(p)]
+                if p.grad is None:
+                    v.zero_()
+                else:
+                    v.copy_(p.grad)
+                    self.copies += 1
         work = dist.all_reduce(flat, group=self.group, async_op=True)
         self.works.append((bi, flat, work))
 
     def finish(self):
-        """Wait for (and, on the first step, issue) every bucket's all-reduce; average into .grad."""
+        """Wait for (and, on the first step, issue) every bucket's all-reduce; the rank mean is left in the
+        buckets, which every active .grad views afterwards."""
         if self.active is None:
             # first step: learn which params get gradients (identical on every rank), rebuild, reduce now
             self.active = [p for p in self.params if p.grad is not None]
             self._build(self.active)
-            self.active = list(self.active)
+            self._make_flats()
             for bi in range(len(self.buckets)):
                 self._launch(bi)
         else:
@@ -117,12 +163,7 @@ class GradAllReducer:
         for bi, flat, work in self.works:
             work.wait()
             flat.mul_(inv)
-            off = 0
             for p in self.buckets[bi]:
-                n = p.numel()
-                if p.grad is None:
-                    p.grad = flat[off:off + n].view_as(p).clone()
-                else:
-                    p.grad.copy_(flat[off:off + n].view_as(p.grad))
-                off += n
+                if not self._resident(p):
+                    p.grad = self.views[id(p)]
         self._reset()

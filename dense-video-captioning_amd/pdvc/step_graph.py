@@ -17,7 +17,9 @@ lengths: load() then also recomputes the caption rows' bookkeeping on the host a
 Dropout stays random per replay (torch's graph-safe Philox offsets; the HIP kernels draw their seeds on the
 device).  Gradients live in the graph's memory pool: do not set them to None between replays (the optimizer
 step and grad clipping run eagerly on them).  A GradAllReducer (data parallel) is suspended while capturing;
-call its finish() after each replay to average the gradients over ranks.
+replay() calls its finish() to average the gradients over ranks.  With a reducer the gradients are views into its
+flat buckets (bucket-resident, pdvc/distributed.py): the captured step begins with the buckets' zero fill and the
+backward accumulates into them, so finish() is one all-reduce and one scale per bucket.
 
 Release the autograd graphs of earlier eager steps (their loss tensors) before constructing a StepGraph: they keep
 the parameters' AccumulateGrad nodes alive, created on the stream of that eager step, and a capture whose
@@ -41,6 +43,9 @@ def replace_memsets(graph):
     from . import _native as _n
     count = ctypes.c_int(0)
     _n.call("pdvc_graph_replace_memsets", ctypes.c_void_p(graph.raw_cuda_graph()), ctypes.byref(count))
+    left = graph_node_counts(graph).get("memset", 0)
+    if left:  # never instantiate a graph whose memsets may not re-apply
+        raise RuntimeError(f"replace_memsets: {left} memset node(s) left in the captured graph")
     return count.value
 
 
@@ -112,12 +117,12 @@ class StepGraph:
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):  # warm-up: lazy init, allocator pools, cached host->device bookkeeping
             for _ in range(warmup):
-                model.zero_grad(set_to_none=True)
+                self._zero_grad()
                 self._forward_backward()
                 if reducer is not None:
                     reducer.finish()
         torch.cuda.current_stream().wait_stream(side)
-        model.zero_grad(set_to_none=True)
+        self._zero_grad()
         # the captured hipGraph_t is kept (keep_graph) so that its memset nodes are rewritten as kernel nodes before
         # instantiation (replace_memsets: small captured memsets did not re-apply on replays);
         # debug_dot: also dumped by hipGraphDebugDotPrint for tools/diag_memset_graph.py
@@ -130,15 +135,28 @@ class StepGraph:
             reducer.suspended = True
         try:
             with torch.cuda.graph(self.graph):
+                if reducer is not None and reducer.flats is not None:
+                    reducer.zero_grad()  # every replay starts from zeroed buckets (a fill node per bucket)
                 self.total, self.losses = self._forward_backward()
         finally:
             if reducer is not None:
                 reducer.suspended = False
         if debug_dot:
             self.graph.debug_dump(debug_dot)
+        # the captured outputs, detached: the storage is the graph's, but the autograd graph of the capture (and
+        # through it the parameters' AccumulateGrad nodes, made on the capture stream) is released, so eager steps
+        # after the capture build their own nodes on their own stream
+        self.total = self.total.detach()
+        self.losses = {k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in self.losses.items()}
         self.memsets_replaced = replace_memsets(self.graph)
         self.node_counts = graph_node_counts(self.graph)  # the launches of one replay, by node type
         self.graph.instantiate()
+
+    def _zero_grad(self):
+        if self.reducer is not None:
+            self.reducer.zero_grad()  # bucket views once the reducer knows its active set, else set to None
+        else:
+            self.model.zero_grad(set_to_none=True)
 
     def _forward_backward(self):
         out, loss = self.model(self.dt, self.criterion, self.tit)

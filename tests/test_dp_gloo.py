@@ -1,7 +1,8 @@
 """CPU, world_size 2 over gloo: the data-parallel gradient all-reducer (pdvc/distributed.py) gives every rank
 the mean of the per-rank gradients, keeps never-used parameters at grad None (as the reference's 8 unused
 PDVC parameters), overlaps buckets with backward (several buckets in flight), survives repeated steps, builds
-the same bucket order on every rank, and treats a gradient missing on one rank in a later step (a branch not
+the same bucket order on every rank, keeps the gradients resident in the buckets when steps zero through
+GradAllReducer.zero_grad() (nothing copied; a set-to-None step still reduces correctly), and treats a gradient missing on one rank in a later step (a branch not
 taken there) as zeros -- both ranks still issue identical collectives and receive the mean."""
 import os
 import socket
@@ -64,14 +65,20 @@ def _worker(rank, world, port, data, q):
     m = Toy()
     broadcast_parameters(m)
     red = GradAllReducer(list(m.parameters()), bucket_mb=0.002)  # tiny buckets: several in flight
-    res = []
+    res, copies, resident = [], [], []
     for step, x in enumerate(data[rank]):
-        m.zero_grad(set_to_none=True)
+        if step == 0 or step == len(data[rank]) - 1:
+            m.zero_grad(set_to_none=True)  # gradients not in the buckets: copied in at launch, views re-bound
+        else:
+            red.zero_grad()  # bucket-resident: backward accumulates into the flat buffers, nothing copied
+        c0 = red.copies
         m(x, _branch(rank, step)).backward()
         red.finish()
+        copies.append(red.copies - c0)
+        resident.append(all(red._resident(p) for p in red.active))
         res.append({n: (p.grad.numpy().copy() if p.grad is not None else None) for n, p in m.named_parameters()})
     names = {id(p): n for n, p in m.named_parameters()}
-    q.put((rank, res, [[names[id(p)] for p in b] for b in red.buckets]))
+    q.put((rank, res, [[names[id(p)] for p in b] for b in red.buckets], copies, resident))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -88,10 +95,13 @@ def test_grad_allreduce_is_mean_of_ranks():
         p.start()
     results, orders = dict(), dict()
     for _ in range(world):
-        r, res, buckets = q.get(timeout=120)
+        r, res, buckets, copies, resident = q.get(timeout=120)
         results[r] = res
         orders[r] = buckets
         assert len(buckets) >= 2
+        assert all(resident), "after finish() every active gradient views its bucket"
+        # the resident step copies nothing; a set-to-None step copies every gradient it produced
+        assert copies[1] == 0 and copies[2] > 0, copies
     assert orders[0] == orders[1], "bucket order differs between ranks"
     assert not any(n.startswith("unused") for b in orders[0] for n in b)
     for p in procs:
