@@ -28,6 +28,7 @@ from torch import nn
 
 from pdvc import _native as _n
 from pdvc.ops.functions import CaptionDecodeFunction
+from pdvc.caption_tokens import DeferredLogprobs
 from pdvc.ops.functions.logprob import logprob_pick
 from pdvc.ops.modules import MSDeformAttnCap
 from pdvc.ops.modules.linear import Linear
@@ -302,13 +303,15 @@ class LSTMDSACaptioner(Captioner):
         return h_out, c_out
 
     def decode_teacher_forced(self, hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten, level_T, seq,
-                              n_steps, video_csr=None, pick_target=None):
+                              n_steps, video_csr=None, pick_target=None, tokens=None):
         """hs_rows (R, d) event features; ref_rows (R, L, 2) references (rows < rd1_rows are 1-d: centre in
         [..., 0]); row_video (R,) int32; memory (N, S, d); seq (R, K) long; returns logprobs (R, n_steps, V).
         video_csr (start, rows, max rows per video) of row_video lets the backward sum the value gradient of all
         steps in one destination-sorted pass (no float atomics).  With pick_target (R, >= n_steps) long, returns
         (logprobs, picked) where picked (R, n_steps) = logprobs at the target words (csrc/logprob.hip: log_softmax
-        and the loss's gather in one pass, the backward in one pass -- the input of build_loss_picked)."""
+        and the loss's gather in one pass, the backward in one pass -- the input of build_loss_picked).  With tokens
+        (index, scatter) of pdvc/caption_tokens.py pack_tokens as well, the logit GEMM and that pass run over the packed
+        valid tokens only, picked is zero at the other positions, and the logprobs come back as a DeferredLogprobs."""
         core = self.core
         if self.training and self.ss_prob > 0:
             out = self.decode_scheduled_sampling(hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten,
@@ -332,7 +335,17 @@ class LSTMDSACaptioner(Captioner):
             value, xe, hs_g, off_hs, ref_rows, w["W_h"], w["b_h"], core.ctx2att.weight,
             core.ctx2att.bias, core.alpha_net.weight.view(-1), core.alpha_net.bias, w["W_att"], mask_u8, row_video,
             tuple(level_T), rd1_rows, video_csr, M)
-        logits = self.logit(self.dropout(Hs))
+        Hd = self.dropout(Hs)
+        if pick_target is not None and tokens is not None:
+            index, scatter = tokens
+            R, n, H = Hd.shape
+            Hp = Hd.reshape(R * n, H).index_select(0, index)
+            tgt = pick_target[:, :n_steps].reshape(-1).index_select(0, index)
+            _, picked_p = logprob_pick(self.logit(Hp), tgt)
+            picked = Hp.new_zeros(R * n + 1).index_copy(0, scatter, picked_p)[:R * n].view(R, n)
+            return DeferredLogprobs(Hd.detach(), self.logit.weight.detach().clone(),
+                                    self.logit.bias.detach().clone()), picked
+        logits = self.logit(Hd)
         if pick_target is not None:
             return logprob_pick(logits, pick_target[:, :n_steps])
         return F.log_softmax(logits, dim=-1)

@@ -76,10 +76,13 @@ def caption_layout(counts, Ld, N, Q, blocks, rows_cap=None, events_cap=None):
     return out
 
 
-def pad_to_capacity(dt, events, rows, words):
+def pad_to_capacity(dt, events, rows, words, tokens=None):
     """A collated batch (host tensors) padded to fixed shapes: every caption token row `words` wide, `rows + 1`
     caption rows (the real ones first, then all-zero rows; `rows` >= the batch's sum of events), `events` targets
-    per video in the padded targets (to_device builds them), and dt["capacity"] recording the three."""
+    per video in the padded targets (to_device builds them), and dt["capacity"] recording them.  tokens: the
+    loss-carrying caption tokens per decoder layer the stream's batches may hold (>= this batch's sum of
+    cap_mask[:, 1:], pdvc/caption_tokens.py); the logit projection runs over that many token rows.  None: no
+    packing (every (row, step) position)."""
     cap = dt["cap_tensor"]
     tot, K = cap.shape
     counts = [len(t["labels"]) for t in dt["video_target"]]
@@ -91,6 +94,11 @@ def pad_to_capacity(dt, events, rows, words):
         raise ValueError(f"pad_to_capacity: a video has {max(counts)} events, capacity {events}")
     if tot > rows:
         raise ValueError(f"pad_to_capacity: {tot} caption rows, capacity {rows}")
+    if tokens is None:
+        tokens = rows * (words - 1)
+    have = int(dt["cap_mask"][:, 1:words].sum())
+    if have > tokens:
+        raise ValueError(f"pad_to_capacity: {have} caption tokens, capacity {tokens}")
     out = dict(dt)
     c = torch.zeros(rows + 1, words, dtype=cap.dtype)
     c[:tot, :K] = cap
@@ -107,7 +115,7 @@ def pad_to_capacity(dt, events, rows, words):
         gb[:, :dt["gt_boxes"].shape[1]] = dt["gt_boxes"]
         out["gt_boxes"] = gb
         out["gt_boxes_mask"] = (gb != 0).sum(2) > 0
-    out["capacity"] = {"events": int(events), "rows": int(rows), "words": int(words)}
+    out["capacity"] = {"events": int(events), "rows": int(rows), "words": int(words), "tokens": int(tokens)}
     return out
 
 

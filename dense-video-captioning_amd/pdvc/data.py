@@ -82,6 +82,7 @@ def to_device(dt, device):
         else:
             out[k] = v
     out["cap_tensor_cpu"] = dt["cap_tensor"].clone()
+    out["cap_mask_cpu"] = dt["cap_mask"].clone()  # the caption token count (pdvc/caption_tokens.py)
     from .matcher import padded_targets
     cap = dt.get("capacity")  # a capacity-padded batch (pdvc/batch_layout.py): targets padded to its event capacity
     out["video_target_padded"] = padded_targets(dt["video_target"], device,

@@ -24,6 +24,7 @@ from .CaptioningHead.LSTM_DSA import caption_steps
 from .criterion import SetCriterion
 from .deformable_transformer import build_deforamble_transformer
 from .batch_layout import caption_layout, caption_layout_to_device
+from .caption_tokens import DeferredLogprobs, LazyProbs, pack_tokens, token_count
 from .matcher import LazyIndices, build_matcher
 
 
@@ -52,6 +53,19 @@ def decide_two_stage(transformer_input_type, dt, criterion):
 # PDVC_CAP_DEFERRED=0: per-step float atomics for the caption value gradient (A/B switch)
 _CAP_DEFERRED = os.environ.get("PDVC_CAP_DEFERRED", "1") != "0"
 # caption log-probabilities and the loss's target gather in one HIP pass each way (csrc/logprob.hip);
+# PDVC_TOKENS_PACKED=0: the logit GEMM and log-softmax over every (row, step) position, not the packed valid tokens
+_TOKENS_PACKED = os.environ.get("PDVC_TOKENS_PACKED", "1") != "0"
+
+
+def _cap_mask_cpu(dt):
+    """The host copy of cap_mask (data.to_device keeps one; else one device->host copy)."""
+    m = dt.get("cap_mask_cpu")
+    if m is None:
+        m = dt["cap_mask"].detach().cpu()
+        dt["cap_mask_cpu"] = m
+    return m
+
+
 # PDVC_LOGPROB_FUSED=0 keeps torch's log_softmax + gather (same-box A/B)
 _LOGPROB_FUSED = os.environ.get("PDVC_LOGPROB_FUSED", "1") != "0"
 
@@ -384,12 +398,22 @@ class PDVC(nn.Module):
         n_steps = max(R["steps_v"]) if R["steps_v"] else 0
         seq_rows = dt["cap_tensor"].index_select(0, R["cap_rows"])
         cap_mask_rows = dt["cap_mask"].index_select(0, R["cap_rows"])
+        tokens = None
+        if _LOGPROB_FUSED and _TOKENS_PACKED and n_steps > 0:
+            # the logit GEMM and log-softmax over the loss-carrying tokens only (pdvc/caption_tokens.py): capacity =
+            # the batch's token count (a capacity-padded stream: its fixed token capacity); no packing when every
+            # (row, step) position carries the loss
+            cap_tok = (dt.get("capacity") or {}).get("tokens")
+            per_layer = cap_tok if cap_tok is not None else token_count(_cap_mask_cpu(dt), n_steps)
+            capacity = Ld * int(per_layer)
+            if capacity < seq_rows.shape[0] * n_steps:
+                tokens = pack_tokens(cap_mask_rows[:, 1:n_steps + 1] > 0, capacity)
         if self.share_caption_head:
             logprobs = self.caption_head[0].decode_teacher_forced(
                 R["hs_rows"], R["ref_rows"], R["rd1"], R["row_video"], others["memory"], others["mask_flatten"],
                 others["level_T"], seq_rows, n_steps,
                 video_csr=R["video_csr"] if _CAP_DEFERRED else None,
-                pick_target=seq_rows[:, 1:] if _LOGPROB_FUSED else None)
+                pick_target=seq_rows[:, 1:] if _LOGPROB_FUSED else None, tokens=tokens)
         else:
             raise NotImplementedError("share_caption_head=0 is not supported on the batched caption path")
         if _LOGPROB_FUSED:
@@ -415,12 +439,16 @@ class PDVC(nn.Module):
         n_last = max([R["steps_v"][v] for v in last_v], default=0)
         if dt.get("capacity") is not None:
             n_last = n_steps
-        if R["last_range"] is not None:
-            last_lp = logprobs.narrow(0, R["last_range"][0], R["last_range"][1])
+        if isinstance(logprobs, DeferredLogprobs):  # packed tokens: materialised on first read
+            probs = LazyProbs(cap_prob_train=logprobs.select(
+                tuple(R["last_range"]) if R["last_range"] is not None else last_sel, n_last))
         else:
-            last_lp = logprobs.index_select(0, last_sel)
-        out.update({"caption_probs": {"cap_prob_train": last_lp[:, :n_last]},
-                    "seq": seq_rows.index_select(0, last_sel)})
+            if R["last_range"] is not None:
+                last_lp = logprobs.narrow(0, R["last_range"][0], R["last_range"][1])
+            else:
+                last_lp = logprobs.index_select(0, last_sel)
+            probs = {"cap_prob_train": last_lp[:, :n_last]}
+        out.update({"caption_probs": probs, "seq": seq_rows.index_select(0, last_sel)})
         return out, loss
 
     def parallel_prediction_full(self, dt, criterion, hs, init_reference, inter_references, others,

@@ -170,9 +170,10 @@ class StepGraph:
         (the reference's loop stops at the video's first all-zero token column, LSTM_DSA.py:88-104) -- or, for a
         capacity-padded batch (pdvc/batch_layout.py), only the capacities and the batch size."""
         from .CaptioningHead.LSTM_DSA import caption_steps
+        from .caption_tokens import token_count
         if dt.get("capacity") is not None:
             c = dt["capacity"]
-            return ("capacity", len(dt["video_target"]), c["events"], c["rows"], c["words"])
+            return ("capacity", len(dt["video_target"]), c["events"], c["rows"], c["words"], c.get("tokens"))
         counts = [len(t["labels"]) for t in dt["video_target"]]
         cap = dt.get("cap_tensor_cpu")
         cap = dt["cap_tensor"].detach().cpu() if cap is None else cap
@@ -180,7 +181,10 @@ class StepGraph:
         for c in counts:
             off.append(off[-1] + c)
         steps = [caption_steps(cap[off[v]:off[v + 1]]) for v in range(len(counts))]
-        return tuple(counts), tuple(steps)
+        # the caption token count sizes the packed logit projection (pdvc/caption_tokens.py)
+        mask = dt.get("cap_mask_cpu")
+        mask = dt["cap_mask"].detach().cpu() if mask is None else mask
+        return tuple(counts), tuple(steps), token_count(mask, max(steps, default=0))
 
     def load(self, dt):
         """Copy a batch of the captured shapes (same event and caption counts) into the graph's inputs: the
@@ -212,6 +216,13 @@ class StepGraph:
                             v.copy_(new[kk].repeat(k[1], *([1] * (v.dim() - 1))), non_blocking=True)
             cpu = dt.get("cap_tensor_cpu")
             self.dt["cap_tensor_cpu"] = dt["cap_tensor"].detach().cpu() if cpu is None else cpu
+            mcpu = dt.get("cap_mask_cpu")
+            self.dt["cap_mask_cpu"] = dt["cap_mask"].detach().cpu() if mcpu is None else mcpu
+            cap_tok = (dt.get("capacity") or {}).get("tokens")
+            if cap_tok is not None:
+                have = int(self.dt["cap_mask_cpu"][:, 1:dt["capacity"]["words"]].sum())
+                if have > cap_tok:
+                    raise ValueError(f"StepGraph.load: {have} caption tokens, capacity {cap_tok}")
             if dt.get("capacity") is not None:  # the caption rows' bookkeeping of the new counts
                 from .batch_layout import caption_layout, refresh_caption_layout
                 counts = [len(t["labels"]) for t in dt["video_target"]]

@@ -81,7 +81,7 @@ def test_pad_to_capacity():
     tot, K = dt["cap_tensor"].shape
     assert torch.equal(p["cap_tensor"][:tot, :K], dt["cap_tensor"]) and not p["cap_tensor"][tot:].any()
     assert not p["cap_tensor"][:, K:].any() and not p["cap_mask"][tot:].any()
-    assert p["gt_boxes"].shape == (3, 6, 2) and p["capacity"] == {"events": 6, "rows": 20, "words": 11}
+    assert p["gt_boxes"].shape == (3, 6, 2) and p["capacity"] == {"events": 6, "rows": 20, "words": 11, "tokens": 200}
     for bad in (dict(events=3, rows=20, words=11), dict(events=6, rows=11, words=11),
                 dict(events=6, rows=20, words=K - 1)):
         with pytest.raises(ValueError):

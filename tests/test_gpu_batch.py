@@ -202,11 +202,15 @@ def test_batched_eval_and_postprocess_match_reference(fixture):
 CAPS = dict(events=7, rows=16, words=12)
 
 
-def padded_dt(items):
+def padded_dt(items, packed=False):
+    """packed: a token capacity 8 above the batch's caption-token count, so the logit projection runs over the
+    packed valid tokens (pdvc/caption_tokens.py); else every (row, step) position."""
     import weights as W  # noqa: F401
     from pdvc.batch_layout import pad_to_capacity
     from pdvc.data import collate, to_device
-    return to_device(pad_to_capacity(collate(items), **CAPS), DEV)
+    c = collate(items)
+    tokens = int(c["cap_mask"][:, 1:CAPS["words"]].sum()) + 8 if packed else None
+    return to_device(pad_to_capacity(c, tokens=tokens, **CAPS), DEV)
 
 
 def _check_padded_forward(d, out, loss, nv, cap):
@@ -227,16 +231,17 @@ def _check_padded_forward(d, out, loss, nv, cap):
         row += e
 
 
-def test_capacity_padded_batch_equals_reference(fixture):
+@pytest.mark.parametrize("packed", [False, True], ids=["all_positions", "packed_tokens"])
+def test_capacity_padded_batch_equals_reference(fixture, packed):
     """The fixture's 3 videos padded to fixed capacities (7 events per video, 16 caption rows per layer, 12-token
     captions): phantom targets and caption rows change no loss and no gradient -- the same bound against the
-    reference's batch-1 steps as the unpadded batch."""
+    reference's batch-1 steps as the unpadded batch.  packed: the logits over the packed caption tokens only."""
     d = fixture
     nv = int(d["n_videos"])
     model, criterion = TM.build_filled(d)
     model.train()
     import weights as W
-    dt = padded_dt(W.batch_items(vocab=29))
+    dt = padded_dt(W.batch_items(vocab=29), packed)
     out, loss = model(dt, criterion, "queries")
     _check_padded_forward(d, out, loss, nv, dt["capacity"])
     wd = criterion.weight_dict
@@ -246,7 +251,8 @@ def test_capacity_padded_batch_equals_reference(fixture):
     _check_grads(d, model.named_parameters(), "capacity-padded batch")
 
 
-def test_capacity_step_graph_follows_a_ragged_stream(fixture):
+@pytest.mark.parametrize("packed", [False, True], ids=["all_positions", "packed_tokens"])
+def test_capacity_step_graph_follows_a_ragged_stream(fixture, packed):
     """ONE StepGraph captured on a capacity-padded batch serves batches of other event counts and caption lengths:
     load() a batch of the same videos in another order (per-position counts 5, 2, 3 instead of 2, 3, 5) and the
     replay equals the eager unpadded step on it; load the first batch back and the replay equals the reference."""
@@ -269,14 +275,14 @@ def test_capacity_step_graph_follows_a_ragged_stream(fixture):
     total_b = total_b.item()
     del out_b, loss_b  # the eager step's autograd graph (its default-stream AccumulateGrad nodes) must not outlive it
     model.zero_grad(set_to_none=True)
-    sg = StepGraph(model, criterion, padded_dt(items))
+    sg = StepGraph(model, criterion, padded_dt(items, packed))
     assert_scalar(sg.replay(), np.mean([float(d[f"v{v}.total_loss"]) for v in range(nv)]), "replay, batch A")
     _check_grads(d, model.named_parameters(), "capacity step graph, batch A")
-    sg.load(padded_dt(perm))
+    sg.load(padded_dt(perm, packed))
     assert_scalar(sg.replay(), total_b, "replay after load(batch B)")
     for n, p in model.named_parameters():
         if n in grads_b:
             close(p.grad, grads_b[n], f"capacity step graph, batch B: grad {n}")
-    sg.load(padded_dt(items))
+    sg.load(padded_dt(items, packed))
     sg.replay()
     _check_grads(d, model.named_parameters(), "capacity step graph, batch A again")

@@ -6,7 +6,7 @@ mkdir -p $O
 export TMPDIR=/tmp
 echo "[$(date +%T)] tests"
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_bench_launcher.py \
-    tests/test_gpu_dp.py tests/test_gpu_graph_memset.py tests/test_gpu_ops.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+    tests/test_gpu_dp.py tests/test_gpu_graph_memset.py tests/test_gpu_ops.py tests/test_gpu_batch.py tests/test_gpu_model.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -3 $O/tests.log
 for pf in 0 4 0 4; do
   echo "[$(date +%T)] kbench PDVC_VAL_PF=$pf"
