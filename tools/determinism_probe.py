@@ -40,14 +40,18 @@ def main():
     if not a.no_table:
         gemm_tuning.enable()
     torch.manual_seed(0)
-    args = opts.parse_opts(["--cfg_path", "cfgs/anet_tsp_pdvc.yml", "--device", "cuda",
-                            "--transformer_dropout_prob", "0", "--hidden_dropout_prob", "0", "--drop_prob", "0"],
-                           cfg_root=PKG, feature_dim=768, num_queries=100, frame_embedding_num=512)
+    # every dropout off: as keyword overrides -- the cfg chain (anet_c3d_pdvcl.yml: transformer_dropout_prob 0.1)
+    # overrides command-line flags, and that probability also drives the decoder self-attention kernel's dropout
+    args = opts.parse_opts(["--cfg_path", "cfgs/anet_tsp_pdvc.yml", "--device", "cuda"], cfg_root=PKG,
+                           feature_dim=768, num_queries=100, frame_embedding_num=512, transformer_dropout_prob=0.0,
+                           hidden_dropout_prob=0.0, drop_prob=0.0)
     model, criterion, _ = build(args)
     model = model.cuda().train()
     for mod in model.modules():
         if isinstance(mod, torch.nn.Dropout):
             mod.p = 0.0
+        elif isinstance(getattr(mod, "dropout", None), float):  # QuerySelfAttention: the MHA kernel's own dropout
+            mod.dropout = 0.0
     wd = criterion.weight_dict
     dt = to_device(collate(synthetic_videos(a.videos, 512, 768, 4, 13, args.vocab_size + 1, seed=1000)), "cuda")
     names = {m: n for n, m in list(model.named_modules()) + [("criterion." + n, m) for n, m in criterion.named_modules()]}
