@@ -16,6 +16,8 @@ for pf in 0 4; do
     python -c "import csv,sys; [print(f\"pf$pf {float(r['AverageNs'])/1e3:9.1f} us x{r['Calls']:>4} {r['Name'][:110]}\") for r in csv.DictReader(open(sys.argv[1])) if 'msda1d' in r['Name']]" $f
   done
 done | tee $O/kb_ab.txt
+echo "[$(date +%T)] scale test"
+timeout -k 10 600 python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_gpu_step_graph_scale.py > $O/scale_test.log 2>&1; tail -15 $O/scale_test.log
 echo "[$(date +%T)] graph replays vs eager, 256 videos"
 timeout -k 10 400 python -u tools/check_graph_replays.py --videos 256 > $O/replays256.log 2>&1 || { tail -20 $O/replays256.log; exit 1; }
 grep -v Warning $O/replays256.log | tail -6
