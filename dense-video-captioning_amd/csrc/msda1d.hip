@@ -1210,10 +1210,7 @@ constexpr int kVQPT = 4;  // queries per thread in its sort passes: a launch chu
 // fp32 path keeps its registers: the pointer and its stores cost the depth-8 walk 9 spilled VGPRs)
 // ABL (measurement only, PDVC_VAL_ABLATE): 1 = stop after the sort, 2 = walk without the gradient-row gathers
 // (PDVC_VAL_ABLATE=1/2 select them for the depth-8 encoder walk, 3/4 for the depth-4 decoder walk)
-// PF (G4): software-pipelined walk -- the next UG sorted entries and their gradient rows are requested before the
-// current UG are summed, so a 16-lane group always has a block of gathers in flight (without it every block waited for
-// its LDS reads and then its gathers: the kernel was latency-bound, ~17% of issue slots used, r02 PMC counters)
-template <int CW, bool G4, int UG = 8, bool B16 = false, int ABL = 0, bool PF = false>
+template <int CW, bool G4, int UG = 8, bool B16 = false, int ABL = 0>
 __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
                                                                      int Lq, int q0, int nq, int S, int M, int D,
                                                                      int accumulate,
@@ -1412,48 +1409,6 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
             };
             int k = (int)(eqk[jb] >> 16);
             PAcc4 alo = pacc_zero(), ahi = pacc_zero();  // rows k - 1 and k
-            if constexpr (PF) {
-                // two register blocks: A holds entries j0 .. j0 + UG - 1 and their rows, B the next UG
-                uint32_t eA[UG], eB[UG];
-                pf4 gA[UG], gB[UG];
-                auto fetch = [&](int j0, uint32_t(&e)[UG], pf4(&g)[UG]) {
-#pragma unroll
-                    for (int u = 0; u < UG; ++u) e[u] = eqk[(j0 + u < je) ? j0 + u : je - 1];
-#pragma unroll
-                    for (int u = 0; u < UG; ++u)
-                        g[u] = __builtin_bit_cast(pf4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                           gr, (int)__umul24(e[u] & 0xffffu, (unsigned)rowb) + coff, 0, 0));
-                };
-                auto consume = [&](int j0, const uint32_t(&e)[UG], const pf4(&g)[UG]) {
-#pragma unroll
-                    for (int u = 0; u < UG; ++u) {
-                        if (j0 + u >= je) break;
-                        const int kj = (int)(e[u] >> 16);
-                        if (kj != k) {
-                            put(k - 1, pacc_f4(alo));
-                            if (kj == k + 1) {
-                                alo = ahi;
-                            } else {
-                                put(k, pacc_f4(ahi));
-                                alo = pacc_zero();
-                            }
-                            ahi = pacc_zero();
-                            k = kj;
-                        }
-                        const float2 wgt = ew[j0 + u];
-                        pacc_fma(alo, wgt.x, g[u]);
-                        pacc_fma(ahi, wgt.y, g[u]);
-                    }
-                };
-                fetch(jb, eA, gA);
-                for (int j0 = jb; j0 < je; j0 += 2 * UG) {
-                    if (j0 + UG < je) fetch(j0 + UG, eB, gB);
-                    consume(j0, eA, gA);
-                    if (j0 + UG >= je) break;
-                    if (j0 + 2 * UG < je) fetch(j0 + 2 * UG, eA, gA);
-                    consume(j0 + UG, eB, gB);
-                }
-            } else
             for (int j0 = jb; j0 < je; j0 += UG) {
                 uint32_t e[UG];
                 pf4 gv[UG];
@@ -2041,16 +1996,6 @@ static int pick_pyr(const Levels1d& lv, int S, int num_query, int head_dim, int 
 // value-gradient walk depth (PDVC_VALUE_UG=4 / 8 forces it): 4 where a level holds few samples per row (the
 // decoder, 4 * Lq < S: its workgroups' LDS is small, so the 66-VGPR form fits more of them per CU -- 206 -> 177 us at
 // 256 videos), 8 for the encoder (LDS-limited to two workgroups per CU anyway; 8 in flight: 770 -> 700 us)
-// the software-pipelined value walk (PF, blocks of 4 entries: the depth-8 form spills under the 6-wave bound):
-// PDVC_VAL_PF=0 selects the unpipelined walks (A/B)
-static int value_pf() {
-    static const int v = [] {
-        const char* e = getenv("PDVC_VAL_PF");
-        return e ? atoi(e) : 4;
-    }();
-    return v;
-}
-
 static int value_ug(int num_query, int S) {
     static const int forced = [] {
         const char* e = getenv("PDVC_VALUE_UG");
@@ -2386,8 +2331,7 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
                                    {(const void*)msda1d_bwd_value_kernel<2, false>, 96 * 1024},
                                    {(const void*)msda1d_bwd_value_kernel<1, true>, 96 * 1024},
                                    {(const void*)msda1d_bwd_value_kernel<1, true, 4>, 96 * 1024},
-                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, true>, 96 * 1024},
-                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, false, 0, true>, 96 * 1024}},
+                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, true>, 96 * 1024}},
                             "msda1d_bwd_value_kernel")))
             return rc;
         for (int q0 = 0; q0 < num_query; q0 += qchunk) {
@@ -2433,11 +2377,6 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
                                        head_dim, acc, grad_output, save_attn, save_loc, grad_value, gsums,
                                        (const int64_t*)nullptr, (const int64_t*)nullptr, gv16);
             } else if (g4 && gv16) VAL_LAUNCH(4, true);  // the bf16 stores spill the depth-8 walk (7 VGPRs): depth 4
-            else if (g4 && value_pf() == 4)
-                hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, 4, false, 0, true>), dim3((unsigned)nblk),
-                                   dim3(kVW * 64), lds, s, value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim,
-                                   acc, grad_output, save_attn, save_loc, grad_value, gsums, (const int64_t*)nullptr,
-                                   (const int64_t*)nullptr, gv16);
             else if (g4 && value_ug(num_query, S) == 4) VAL_LAUNCH(4, false);
             else if (g4) VAL_LAUNCH(8, false);
 #undef VAL_LAUNCH
