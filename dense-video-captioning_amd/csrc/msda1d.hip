@@ -1543,280 +1543,6 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
 }
 
 // -------------------------------------------------------------------------------------------------
-// msda1d_bwd_value_q4_kernel: the value gradient with a WAVE-UNIFORM walk (D = 64).  msda1d_bwd_value_kernel's G4 walk
-// gives each 16-lane group its own row range, so the four groups of a wave change key (and flush rows) at different
-// entries: every flush and its branches run under exec masks for the whole wave, and the walk without its gathers
-// alone took 1.3 of the kernel's 2.6 ms at 1024 videos (r03 ablation) with ~17% of the issue slots used.  Here the
-// counting sort pads every bucket to a multiple of 4 entries (padding: weight 0 and a query index past the gradient's
-// buffer range, whose load returns 0 without a memory access), so the 4 entries of a QUAD share one key; lane
-// (slot s = lane / 16, channel group c = lane % 16) sums entry 4i + s of quad i, a wave owns a row range, and the key
-// of each quad is wave-uniform (readfirstlane): key changes are scalar branches, never divergent.  A finished row is
-// the sum of the 4 slots' partials: two exchange-adds (v_permlane16_swap, v_permlane32_swap: gfx950's half-row and
-// half-wave swaps, VALU, no LDS), then slot 0 writes it.  LDS: 10 B per (padded) entry + 2 B per quad + 8 B per
-// bucket -- 61 KiB at the encoder's level 0 (two workgroups per CU, 128 VGPRs).
-// -------------------------------------------------------------------------------------------------
-__device__ __forceinline__ float slot_sum4(float x) {  // sum over lanes l, l ^ 16, l ^ 32, l ^ 48
-    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    x = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-    auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    return __uint_as_float(t[0]) + __uint_as_float(t[1]);
-}
-
-// largest padded entry count of a chunk of n samples over a level of T rows (buckets 0 .. T, each padded by <= 3)
-__host__ __device__ inline long q4_entries(long n, int T) {
-    const long pad = 3L * ((long)T + 1 < n ? (long)T + 1 : n);
-    return (n + pad + 3) & ~3L;
-}
-
-// LDS bytes of one q4 workgroup: off, cur [T + 2] ints; ew [P] float2; eq [P] u16; qk [P / 4] u16
-__host__ __device__ inline size_t q4_lds_bytes(long n, int T) {
-    const long P = q4_entries(n, T);
-    return (size_t)8 * (T + 2) + (size_t)P * 8 + (size_t)P * 2 + (size_t)(P / 4) * 2 + 16;
-}
-
-template <int UG, bool B16>
-__global__ __launch_bounds__(kVW * 64, 4) void msda1d_bwd_value_q4_kernel(
-    const uint8_t* __restrict__ vmask, Levels1d lv, int Lq, int q0, int nq, int S, int M, int accumulate,
-    const float* __restrict__ gout, const float* __restrict__ save_attn, const float* __restrict__ save_loc,
-    float* __restrict__ grad_value, float* __restrict__ level_sums, const int64_t* __restrict__ dshapes,
-    const int64_t* __restrict__ dlsi, uint16_t* __restrict__ gv16) {
-    constexpr int D = 64;
-    extern __shared__ __attribute__((aligned(16))) int lds_i[];
-    if (dshapes != nullptr && !dropin_levels(dshapes, dlsi, S, lv)) return;
-    const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
-    const int lb = xcd_remap(blockIdx.x, gridDim.x);
-    const int l = lb % kL;
-    const int bm = lb / kL;
-    const int b = bm / M, m = bm - b * M;
-    const int T = lvl_sel(lv.T, l), st = lvl_sel(lv.start, l);
-    const float Tf = (float)T;
-    const int n = nq * kP;
-    const long P = q4_entries(n, T);
-    int* off = lds_i;                                                       // [T + 2]
-    int* cur = lds_i + (T + 2);                                             // [T + 2]
-    float2* ew = reinterpret_cast<float2*>(lds_i + ((2 * (T + 2) + 1) & ~1)); // [P]
-    uint16_t* eq = reinterpret_cast<uint16_t*>(ew + P);                      // [P]
-    uint16_t* qk = eq + P;                                                  // [P / 4]
-    __shared__ int wsum[kVW];
-
-    for (int i = threadIdx.x; i < T + 2; i += blockDim.x) off[i] = 0;
-    __syncthreads();
-    // 1) histogram of key = x0 + 1 in [0, T] (msda1d_bwd_value_kernel's pass: one float4 of save_loc per query)
-    const size_t sbase = save_index(b, m, l, q0, 0, Lq, M);
-    int key[kVQPT][kP];
-    float lwv[kVQPT][kP];
-    const bool spread = nq <= (int)blockDim.x;
-#pragma unroll
-    for (int k = 0; k < kVQPT; ++k) {
-        const int qi = spread ? (k == 0 ? (int)threadIdx.x : nq) : (int)threadIdx.x * kVQPT + k;
-#pragma unroll
-        for (int p = 0; p < kP; ++p) {
-            key[k][p] = -1;
-            lwv[k][p] = 0.f;
-        }
-        if (qi < nq) {
-            const float4 lc = *reinterpret_cast<const float4*>(save_loc + sbase + (size_t)qi * kP);
-            const float xs[kP] = {lc.x, lc.y, lc.z, lc.w};
-#pragma unroll
-            for (int p = 0; p < kP; ++p) {
-                const float x = xs[p] * Tf - 0.5f;
-                if (x > -1.f && x < Tf) {
-                    const float xf = floorf(x);
-                    key[k][p] = (int)xf + 1;
-                    lwv[k][p] = x - xf;
-                    atomicAdd(&off[key[k][p]], 1);
-                }
-            }
-        }
-    }
-    __syncthreads();
-    const size_t MD = (size_t)M * D;
-    // rows whose two buckets are empty get no sample: zeros now (first query chunk only)
-    if (!accumulate) {
-        float* obz = grad_value + ((size_t)b * S + st) * MD + (size_t)m * D + (lane & 15) * 4;
-        uint16_t* obz16 = B16 ? gv16 + ((size_t)b * S + st) * MD + (size_t)m * D + (lane & 15) * 4 : nullptr;
-        for (int t = threadIdx.x >> 4; t < T; t += blockDim.x >> 4)
-            if (off[t] == 0 && off[t + 1] == 0) {
-                *reinterpret_cast<float4*>(obz + (size_t)t * MD) = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (B16) *reinterpret_cast<uint2*>(obz16 + (size_t)t * MD) = make_uint2(0u, 0u);
-            }
-    }
-    // 2) exclusive scan of the PADDED counts (each bucket rounded up to a multiple of 4 entries)
-    {
-        const int len = T + 2;
-        const int per = (len + blockDim.x - 1) / blockDim.x;
-        const int i0 = threadIdx.x * per;
-        int tot = 0;
-        for (int i = i0; i < i0 + per && i < len; ++i) tot += (off[i] + 3) & ~3;
-        int inc = tot;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int y = __shfl_up(inc, d, 64);
-            if (lane >= d) inc += y;
-        }
-        if (lane == 63) wsum[wid] = inc;
-        __syncthreads();
-        int base = 0;
-        for (int w = 0; w < wid; ++w) base += wsum[w];
-        int run = base + inc - tot;
-        for (int i = i0; i < i0 + per && i < len; ++i) {
-            const int c = (off[i] + 3) & ~3;
-            off[i] = run;
-            cur[i] = run;
-            run += c;
-        }
-    }
-    __syncthreads();
-    // 3) scatter: (query, the two corner coefficients) per sample
-#pragma unroll
-    for (int k = 0; k < kVQPT; ++k) {
-        const int qi = spread ? (k == 0 ? (int)threadIdx.x : nq) : (int)threadIdx.x * kVQPT + k;
-        if (qi < nq) {
-            const float4 at = *reinterpret_cast<const float4*>(save_attn + sbase + (size_t)qi * kP);
-            const float as[kP] = {at.x, at.y, at.z, at.w};
-#pragma unroll
-            for (int p = 0; p < kP; ++p) {
-                if (key[k][p] >= 0) {
-                    const int pos = atomicAdd(&cur[key[k][p]], 1);
-                    eq[pos] = (uint16_t)(q0 + qi);
-                    ew[pos] = make_float2((1.f - lwv[k][p]) * as[p], lwv[k][p] * as[p]);
-                }
-            }
-        }
-    }
-    __syncthreads();
-    // 4) padding entries (weight 0, query 0xffff: past the buffer range) and the key of every quad
-    for (int bk = threadIdx.x; bk <= T; bk += blockDim.x) {
-        const int e1 = off[bk + 1];
-        for (int j = cur[bk]; j < e1; ++j) {
-            eq[j] = 0xffffu;
-            ew[j] = make_float2(0.f, 0.f);
-        }
-        for (int qd = off[bk] >> 2; qd < (e1 >> 2); ++qd) qk[qd] = (uint16_t)bk;
-    }
-    __syncthreads();
-    // 5) row ranges: wave w owns rows [r0, r1), split so that the waves see equal quad counts
-    const int total = off[T + 1];
-    auto split = [&](int w) -> int {
-        if (w <= 0) return 0;
-        if (w >= kVW) return T;
-        const int target = (int)(((long)total * w) / kVW);
-        int lo = 0, hi = T;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (off[mid] >= target) hi = mid;
-            else lo = mid + 1;
-        }
-        return lo;
-    };
-    // (wave-uniform values: in SGPRs, so that every branch on them below is a scalar branch)
-    const int r0 = __builtin_amdgcn_readfirstlane(split(wid)), r1 = __builtin_amdgcn_readfirstlane(split(wid + 1));
-    const int qb = __builtin_amdgcn_readfirstlane(off[r0] >> 2), qe = __builtin_amdgcn_readfirstlane(off[r1 + 1] >> 2);
-    const int sl = lane >> 4, gc = lane & 15;
-    float4 psum = make_float4(0.f, 0.f, 0.f, 0.f);  // slot 0: column sums of the rows this wave wrote
-    if (r0 < r1 && qb < qe) {  // wave-uniform
-        float* ob = grad_value + ((size_t)b * S + st) * MD + (size_t)m * D + gc * 4;
-        uint16_t* ob16 = B16 ? gv16 + ((size_t)b * S + st) * MD + (size_t)m * D + gc * 4 : nullptr;
-        const uint8_t* mrow = vmask ? vmask + (size_t)b * S + st : nullptr;
-        const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(gout + (size_t)b * Lq * MD), (short)0, (int)((size_t)Lq * MD * 4), 0x00020000);
-        const int coff = (m * D + gc * 4) * 4;
-        const unsigned rowb = (unsigned)MD * 4;
-        auto put = [&](int r, const PAcc4& a) {  // r is wave-uniform: every lane joins the slot reduction
-            if (r < r0 || r >= r1) return;
-            float4 v = pacc_f4(a);
-            v.x = slot_sum4(v.x);
-            v.y = slot_sum4(v.y);
-            v.z = slot_sum4(v.z);
-            v.w = slot_sum4(v.w);
-            if (mrow && __builtin_amdgcn_readfirstlane((int)mrow[r])) v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (sl == 0) {
-                float4* orow = reinterpret_cast<float4*>(ob + (size_t)r * MD);
-                psum.x += v.x;
-                psum.y += v.y;
-                psum.z += v.z;
-                psum.w += v.w;
-                if (accumulate) {
-                    const float4 o = *orow;
-                    v.x += o.x;
-                    v.y += o.y;
-                    v.z += o.z;
-                    v.w += o.w;
-                }
-                *orow = v;
-                if (B16) store_bf16x4(ob16 + (size_t)r * MD, v.x, v.y, v.z, v.w);
-            }
-        };
-        int k = __builtin_amdgcn_readfirstlane((int)qk[qb]);
-        PAcc4 alo = pacc_zero(), ahi = pacc_zero();  // this slot's partials of rows k - 1 and k
-        for (int i0 = qb; i0 < qe; i0 += UG) {
-            int eqv[UG], kk[UG];
-            float2 w[UG];
-            pf4 g[UG];
-#pragma unroll
-            for (int u = 0; u < UG; ++u) {
-                const int iu = (i0 + u < qe) ? i0 + u : qe - 1;
-                eqv[u] = eq[4 * iu + sl];
-                w[u] = ew[4 * iu + sl];
-                kk[u] = qk[iu];
-            }
-#pragma unroll
-            for (int u = 0; u < UG; ++u)
-                g[u] = __builtin_bit_cast(pf4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                   gr, (int)__umul24((unsigned)eqv[u], rowb) + coff, 0, 0));
-#pragma unroll
-            for (int u = 0; u < UG; ++u) {
-                if (i0 + u >= qe) break;
-                const int kj = __builtin_amdgcn_readfirstlane(kk[u]);
-                if (kj != k) {  // bucket k complete: row k - 1 final; row k too unless bucket k + 1 follows
-                    put(k - 1, alo);
-                    if (kj == k + 1) {
-                        alo = ahi;
-                    } else {
-                        put(k, ahi);
-                        alo = pacc_zero();
-                    }
-                    ahi = pacc_zero();
-                    k = kj;
-                }
-                pacc_fma(alo, w[u].x, g[u]);
-                pacc_fma(ahi, w[u].y, g[u]);
-            }
-        }
-        put(k - 1, alo);
-        put(k, ahi);
-    }
-    if (level_sums) {
-        __syncthreads();  // every wave is done with the sorted entries: reuse their LDS
-        float4* red = reinterpret_cast<float4*>(lds_i);
-        if (sl == 0) red[wid * 16 + gc] = psum;
-        __syncthreads();
-        if (threadIdx.x < 16) {
-            float4 t = red[threadIdx.x];
-#pragma unroll
-            for (int w = 1; w < kVW; ++w) {
-                const float4 u = red[w * 16 + threadIdx.x];
-                t.x += u.x;
-                t.y += u.y;
-                t.z += u.z;
-                t.w += u.w;
-            }
-            float4* o = reinterpret_cast<float4*>(level_sums + ((size_t)b * kL + l) * MD + (size_t)m * D) +
-                        threadIdx.x;
-            if (accumulate) {
-                const float4 u = *o;
-                t.x += u.x;
-                t.y += u.y;
-                t.z += u.z;
-                t.w += u.w;
-            }
-            *o = t;
-        }
-    }
-}
-
-// -------------------------------------------------------------------------------------------------
 // The drop-in operator's 1-D fast path.  A reference user who keeps the stock MSDeformAttn module calls
 // MultiScaleDeformableAttention.ms_deform_attn_forward/backward (pdvc/ops/src/vision.cpp:13-16) with PDVC's lifted
 // pyramid: spatial_shapes [[1, T_l]] for every level (pdvc/ops/modules/ms_deform_attn.py:114-117), sampling
@@ -2270,24 +1996,6 @@ static int pick_pyr(const Levels1d& lv, int S, int num_query, int head_dim, int 
 // value-gradient walk depth (PDVC_VALUE_UG=4 / 8 forces it): 4 where a level holds few samples per row (the
 // decoder, 4 * Lq < S: its workgroups' LDS is small, so the 66-VGPR form fits more of them per CU -- 206 -> 177 us at
 // 256 videos), 8 for the encoder (LDS-limited to two workgroups per CU anyway; 8 in flight: 770 -> 700 us)
-// the wave-uniform value walk (msda1d_bwd_value_q4_kernel) for D = 64; PDVC_VAL_Q4=0 selects the 16-lane-group walk (A/B)
-static bool value_q4() {
-    static const bool on = [] {
-        const char* e = getenv("PDVC_VAL_Q4");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-// a measurement-only ablation of the 16-lane-group walk is requested (PDVC_VAL_ABLATE): that kernel runs
-static bool vabl_any() {
-    static const bool on = [] {
-        const char* e = getenv("PDVC_VAL_ABLATE");
-        return e && atoi(e) != 0;
-    }();
-    return on;
-}
-
 static int value_ug(int num_query, int S) {
     static const int forced = [] {
         const char* e = getenv("PDVC_VALUE_UG");
@@ -2618,35 +2326,6 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
         int qchunk = (int)(budget / (per_sample * kP));
         if (qchunk > kVQPT * kVW * 64) qchunk = kVQPT * kVW * 64;
         if (qchunk > num_query) qchunk = num_query;
-        if (g4 && !vabl_any() && value_q4()) {  // the wave-uniform walk (msda1d_bwd_value_q4_kernel)
-            int qc = kVQPT * kVW * 64 < num_query ? kVQPT * kVW * 64 : num_query;
-            while (qc > 1 && q4_lds_bytes((long)qc * kP, Tmax) > 96 * 1024) qc = (qc + 1) / 2;
-            if (q4_lds_bytes((long)qc * kP, Tmax) > 96 * 1024)
-                return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "level length %d too long", Tmax);
-            static std::atomic<int> done4[kMaxDevices];
-            if ((rc = lds_optin(done4, {{(const void*)msda1d_bwd_value_q4_kernel<8, false>, 96 * 1024},
-                                        {(const void*)msda1d_bwd_value_q4_kernel<8, true>, 96 * 1024}},
-                                "msda1d_bwd_value_q4_kernel")))
-                return rc;
-            for (int q0 = 0; q0 < num_query; q0 += qc) {
-                const int nq = (num_query - q0) < qc ? (num_query - q0) : qc;
-                size_t lds = q4_lds_bytes((long)nq * kP, Tmax);
-                if (level_sums && lds < kVW * 16 * 16) lds = kVW * 16 * 16;
-                const int acc = q0 > 0;
-                if (gv16)
-                    hipLaunchKernelGGL((msda1d_bwd_value_q4_kernel<8, true>), dim3((unsigned)nblk), dim3(kVW * 64), lds,
-                                       s, value_pad_mask, lv, num_query, q0, nq, S, num_heads, acc, grad_output,
-                                       save_attn, save_loc, grad_value, level_sums, (const int64_t*)nullptr,
-                                       (const int64_t*)nullptr, gv16);
-                else
-                    hipLaunchKernelGGL((msda1d_bwd_value_q4_kernel<8, false>), dim3((unsigned)nblk), dim3(kVW * 64),
-                                       lds, s, value_pad_mask, lv, num_query, q0, nq, S, num_heads, acc, grad_output,
-                                       save_attn, save_loc, grad_value, level_sums, (const int64_t*)nullptr,
-                                       (const int64_t*)nullptr, gv16);
-                PDVC_CHECK_LAUNCH("msda1d_bwd_value_q4_kernel");
-            }
-            return PDVC_OK;
-        }
         static std::atomic<int> done[kMaxDevices];  // dynamic LDS <= 96 KiB by construction of qchunk (+32 B static)
         if ((rc = lds_optin(done, {{(const void*)msda1d_bwd_value_kernel<1, false>, 96 * 1024},
                                    {(const void*)msda1d_bwd_value_kernel<2, false>, 96 * 1024},
