@@ -289,14 +289,22 @@ def ragged_items(n_videos, T, C, vocab, seed, duration=120.0):
 def ragged_stream(a, B, vocab, device, rank, padded):
     """`a.stream_batches` distinct ragged batches resident in HBM, capacity-padded when `padded` (the graph path):
     capacities = 27 events per video, the stream's largest caption-row count rounded up to 128, 30 tokens per
-    caption, and the stream's largest count of loss-carrying caption words rounded up to 256 (the packed logit
-    projection, pdvc/caption_tokens.py)."""
+    caption, the stream's largest count of loss-carrying caption words rounded up to 256 (the packed logit
+    projection, pdvc/caption_tokens.py), and per step the stream's largest count of caption rows still in their
+    video's loop, rounded up to 64 (the recurrence's row ranges, pdvc.py `_caption_rows`)."""
     from pdvc.batch_layout import pad_to_capacity
     from pdvc.data import collate, to_device
     raw = [collate(ragged_items(B, a.T, a.C, vocab, seed=5000 + 97 * rank + i)) for i in range(a.stream_batches)]
+    from pdvc.batch_layout import live_rows
+    from pdvc.pdvc import video_steps
     rows = max(int(d["cap_tensor"].shape[0]) for d in raw)
     tokens = max(int(d["cap_mask"][:, 1:30].sum()) for d in raw)  # loss-carrying words (pdvc/caption_tokens.py)
-    caps = dict(events=27, rows=(rows + 127) // 128 * 128, words=30, tokens=(tokens + 255) // 256 * 256)
+    # caption rows per decoder layer still in their video's loop at each step (the recurrence's row ranges)
+    lives = [live_rows([len(t["labels"]) for t in d["video_target"]],
+                       video_steps(d["cap_tensor"], [len(t["labels"]) for t in d["video_target"]]), 29) for d in raw]
+    alive = [max(x[t] for x in lives) for t in range(29)]
+    alive = [min((a + 63) // 64 * 64, (rows + 127) // 128 * 128) for a in alive]
+    caps = dict(events=27, rows=(rows + 127) // 128 * 128, words=30, tokens=(tokens + 255) // 256 * 256, alive=alive)
     stats = {"events_per_video_mean": float(np.mean([len(t["labels"]) for d in raw for t in d["video_target"]])),
              "caption_rows_per_batch": [int(d["cap_tensor"].shape[0]) for d in raw],
              "words_per_caption_mean": float(np.mean([float(m.sum()) - 2 for d in raw for m in d["cap_mask"]])),

@@ -266,7 +266,8 @@ template <int CW>  // channels per lane: D <= 64 * CW, channel = lane + 64 c
 __global__ __launch_bounds__(kCVW * 64) void cap_value_grad_kernel(
     const uint8_t* __restrict__ vmask, CapLevels lv, int S, int M, int D, int R, int s0, int ns, int accumulate,
     const int32_t* __restrict__ vr_start, const int32_t* __restrict__ vr_rows, const float* __restrict__ save_loc,
-    const float* __restrict__ gsamp, float* __restrict__ grad_value, float* __restrict__ level_sums) {
+    const float* __restrict__ gsamp, float* __restrict__ grad_value, float* __restrict__ level_sums,
+    const int32_t* __restrict__ step_rows) {
     extern __shared__ __attribute__((aligned(16))) int lds_c[];
     __shared__ int wsum[kCVW];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -287,9 +288,12 @@ __global__ __launch_bounds__(kCVW * 64) void cap_value_grad_kernel(
     const uint8_t* mrow = vmask ? vmask + (size_t)b * S + st : nullptr;
     for (int i = threadIdx.x; i < T + 2; i += blockDim.x) off[i] = 0;
     __syncthreads();
-    auto sample = [&](int i, int& gidx) -> float {  // clipped pixel coordinate of sample i; gidx its gradient row
+    // step_rows (steps x [start, count]): the rows each step of the recurrence computed (a video's rows stop at its
+    // last step, caption_decode.py); samples of the other (step, row) pairs were never formed and are skipped
+    auto sample = [&](int i, int& gidx) -> float {  // clipped pixel coordinate of sample i (-1: skipped); gidx its row
         const int step = s0 + i / per_step, rem = i - (i / per_step) * per_step;
         const int r = vr_rows[rb0 + rem / cP], j = l * cP + rem % cP;
+        if (step_rows && (r < step_rows[2 * step] || r >= step_rows[2 * step] + step_rows[2 * step + 1])) return -1.f;
         const size_t si = (((size_t)step * R + r) * M + m) * cNS + j;
         gidx = (int)si;
         float gm;
@@ -298,7 +302,7 @@ __global__ __launch_bounds__(kCVW * 64) void cap_value_grad_kernel(
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         int gidx;
         const float ix = sample(i, gidx);
-        atomicAdd(&off[(int)floorf(ix) + 1], 1);
+        if (ix >= 0.f) atomicAdd(&off[(int)floorf(ix) + 1], 1);
     }
     __syncthreads();
     {  // exclusive scan of off[0 .. T+1]
@@ -329,6 +333,7 @@ __global__ __launch_bounds__(kCVW * 64) void cap_value_grad_kernel(
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         int gidx;
         const float ix = sample(i, gidx);
+        if (ix < 0.f) continue;
         const float xf = floorf(ix);
         const int x0 = (int)xf;
         const bool ok0 = !(mrow && mrow[x0]);
@@ -546,6 +551,17 @@ extern "C" int pdvc_cap_value_grad_ex_f32(const uint8_t* value_pad_mask, const i
                                           int max_rows_per_video, const int32_t* video_row_start,
                                           const int32_t* video_rows, const float* save_loc, const float* grad_samples,
                                           float* grad_value, float* grad_value_level_sums, void* stream) {
+    return pdvc_cap_value_grad_ranged_f32(value_pad_mask, level_T, num_levels, batch, num_heads, head_dim, num_point,
+                                          rows, steps, max_rows_per_video, video_row_start, video_rows, nullptr,
+                                          save_loc, grad_samples, grad_value, grad_value_level_sums, stream);
+}
+
+extern "C" int pdvc_cap_value_grad_ranged_f32(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels,
+                                              int batch, int num_heads, int head_dim, int num_point, int rows,
+                                              int steps, int max_rows_per_video, const int32_t* video_row_start,
+                                              const int32_t* video_rows, const int32_t* step_rows,
+                                              const float* save_loc, const float* grad_samples, float* grad_value,
+                                              float* grad_value_level_sums, void* stream) {
     float* level_sums = grad_value_level_sums;
     CapLevels lv;
     int S = 0;
@@ -590,7 +606,7 @@ extern "C" int pdvc_cap_value_grad_ex_f32(const uint8_t* value_pad_mask, const i
         const dim3 grid((unsigned)nblk), block(kCVW * 64);
 #define CVG(CW) hipLaunchKernelGGL((cap_value_grad_kernel<CW>), grid, block, lds, s, value_pad_mask, lv, S, num_heads, \
                                    head_dim, rows, s0, ns, acc, video_row_start, video_rows, save_loc, grad_samples,     \
-                                   grad_value, level_sums)
+                                   grad_value, level_sums, step_rows)
         if (cw == 1) CVG(1);
         else if (cw == 2) CVG(2);
         else if (cw == 4) CVG(4);

@@ -303,7 +303,7 @@ class LSTMDSACaptioner(Captioner):
         return h_out, c_out
 
     def decode_teacher_forced(self, hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten, level_T, seq,
-                              n_steps, video_csr=None, pick_target=None, tokens=None):
+                              n_steps, video_csr=None, pick_target=None, tokens=None, step_ranges=None):
         """hs_rows (R, d) event features; ref_rows (R, L, 2) references (rows < rd1_rows are 1-d: centre in
         [..., 0]); row_video (R,) int32; memory (N, S, d); seq (R, K) long; returns logprobs (R, n_steps, V).
         video_csr (start, rows, max rows per video) of row_video lets the backward sum the value gradient of all
@@ -311,7 +311,9 @@ class LSTMDSACaptioner(Captioner):
         (logprobs, picked) where picked (R, n_steps) = logprobs at the target words (csrc/logprob.hip: log_softmax
         and the loss's gather in one pass, the backward in one pass -- the input of build_loss_picked).  With tokens
         (index, scatter) of pdvc/caption_tokens.py pack_tokens as well, the logit GEMM and that pass run over the packed
-        valid tokens only, picked is zero at the other positions, and the logprobs come back as a DeferredLogprobs."""
+        valid tokens only, picked is zero at the other positions, and the logprobs come back as a DeferredLogprobs.
+        step_ranges: (host per-step (start, count), device copy) -- the rows of each step when the rows are ordered by
+        their video's step count (pdvc.py `_caption_rows`); the other (row, step) hidden states are zeros."""
         core = self.core
         if self.training and self.ss_prob > 0:
             out = self.decode_scheduled_sampling(hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten,
@@ -334,7 +336,7 @@ class LSTMDSACaptioner(Captioner):
         Hs = CaptionDecodeFunction.apply(
             value, xe, hs_g, off_hs, ref_rows, w["W_h"], w["b_h"], core.ctx2att.weight,
             core.ctx2att.bias, core.alpha_net.weight.view(-1), core.alpha_net.bias, w["W_att"], mask_u8, row_video,
-            tuple(level_T), rd1_rows, video_csr, M)
+            tuple(level_T), rd1_rows, video_csr, M, step_ranges)
         Hd = self.dropout(Hs)
         if pick_target is not None and tokens is not None:
             index, scatter = tokens

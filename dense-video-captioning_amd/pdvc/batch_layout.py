@@ -36,35 +36,60 @@ def _rows_per_layer(counts, rows_cap):
     return tot, int(rows_cap)
 
 
-def caption_layout(counts, Ld, N, Q, blocks, rows_cap=None, events_cap=None):
-    """Host bookkeeping of the caption rows of every (decoder layer, video, event), layer-major then
-    video-major (pdvc.py `_caption_rows`).  counts: events per video; blocks: the matching block of each layer
-    (LazyIndices.block); rows_cap: rows per layer block (None: exactly sum(counts), no phantom rows).
+def caption_layout(counts, Ld, N, Q, blocks, rows_cap=None, events_cap=None, steps=None):
+    """Host bookkeeping of the caption rows of every (decoder layer, video, event), layer-major (pdvc.py
+    `_caption_rows`).  counts: events per video; blocks: the matching block of each layer (LazyIndices.block);
+    rows_cap: rows per layer block (None: exactly sum(counts), no phantom rows).
+    steps: each video's caption step count (its teacher-forced loop length, LSTM_DSA.py:103-104), or None.  Without
+    it the rows of a layer are video-major.  With it (and Ld <= 2) the rows of each layer are ordered by their video's
+    steps so that the rows still running at any step form ONE contiguous range (step_ranges): layer 0 by ascending
+    steps with its phantom rows first, layer 1 by descending steps with its phantom rows last -- the live rows of step
+    t are the last a_t of layer 0 and the first a_t of layer 1.
     Returns numpy arrays of length Ld * rows: problem p, rank k, hs base row, caption row base, video, layer,
-    valid (0 for phantom rows); the last layer's row indices; the per-video CSR of the real rows (start,
-    rows) and its largest per-video row count (a bound from events_cap for a capacity-padded batch)."""
+    valid (0 for phantom rows); last_sel: the last layer's rows in video-major order (phantom rows after); the
+    per-video CSR of the real rows (start, rows) and its largest per-video row count (a bound from events_cap for a
+    capacity-padded batch)."""
     counts = [int(c) for c in counts]
     tot, R = _rows_per_layer(counts, rows_cap)
     cap_off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
     vid_real = np.repeat(np.arange(N, dtype=np.int64), counts)
     rank_real = np.arange(tot, dtype=np.int64) - cap_off[vid_real]
     pad = R - tot
+    ordered = steps is not None and Ld <= 2
+    if ordered:
+        st = np.asarray(steps, np.int64)[vid_real]
     parts = {k: [] for k in ("p", "k", "base", "cap", "vid", "lay", "valid")}
+    pos_real = []  # per layer: global position of the real rows, in video-major order
     for l_id in range(Ld):
         b = int(blocks[l_id])
-        parts["p"] += [b * N + vid_real, np.full(pad, b * N, np.int64)]
-        parts["k"] += [rank_real, np.zeros(pad, np.int64)]
-        parts["base"] += [(l_id * N + vid_real) * Q, np.full(pad, l_id * N * Q, np.int64)]
+        asc = ordered and Ld == 2 and l_id == 0
+        if ordered:
+            perm = np.argsort(st if asc else -st, kind="stable")
+        else:
+            perm = np.arange(tot, dtype=np.int64)
+        vr, rk = vid_real[perm], rank_real[perm]
+        real = {"p": b * N + vr, "k": rk, "base": (l_id * N + vr) * Q, "cap": cap_off[vr], "vid": vr,
+                "lay": np.full(tot, l_id, np.int64), "valid": np.ones(tot, np.int64)}
         # a phantom row reads caption row `tot` (an all-zero row of the padded cap_tensor) and rank 0 of the
         # layer's first problem; its target offset is multiplied by valid = 0
-        parts["cap"] += [cap_off[vid_real], np.full(pad, tot, np.int64)]
-        parts["vid"] += [vid_real, np.zeros(pad, np.int64)]
-        parts["lay"] += [np.full(tot, l_id, np.int64), np.full(pad, l_id, np.int64)]
-        parts["valid"] += [np.ones(tot, np.int64), np.zeros(pad, np.int64)]
+        phantom = {"p": np.full(pad, b * N, np.int64), "k": np.zeros(pad, np.int64),
+                   "base": np.full(pad, l_id * N * Q, np.int64), "cap": np.full(pad, tot, np.int64),
+                   "vid": np.zeros(pad, np.int64), "lay": np.full(pad, l_id, np.int64),
+                   "valid": np.zeros(pad, np.int64)}
+        first, second = (phantom, real) if asc else (real, phantom)
+        for k in parts:
+            parts[k] += [first[k], second[k]]
+        where = np.empty(tot, np.int64)
+        where[perm] = l_id * R + (pad if asc else 0) + np.arange(tot, dtype=np.int64)
+        pos_real.append(where)
     out = {k: np.concatenate(v) if v else np.zeros(0, np.int64) for k, v in parts.items()}
-    out["last_sel"] = np.arange((Ld - 1) * R, Ld * R, dtype=np.int64) if Ld else np.zeros(0, np.int64)
+    if Ld:
+        lp = (Ld - 1) * R + tot + np.arange(pad, dtype=np.int64)  # the last layer's phantom rows come last
+        out["last_sel"] = np.concatenate([pos_real[-1], lp])
+    else:
+        out["last_sel"] = np.zeros(0, np.int64)
     # per-video CSR of the real rows (the caption value gradient sums each video's rows in one pass)
-    rows_of_video = [np.concatenate([l_id * R + cap_off[v] + np.arange(counts[v]) for l_id in range(Ld)])
+    rows_of_video = [np.concatenate([pos_real[l_id][cap_off[v]:cap_off[v + 1]] for l_id in range(Ld)])
                      if counts[v] else np.zeros(0, np.int64) for v in range(N)]
     start = np.concatenate([[0], np.cumsum([len(r) for r in rows_of_video])]).astype(np.int64)
     flat = np.concatenate(rows_of_video) if rows_of_video else np.zeros(0, np.int64)
@@ -73,16 +98,37 @@ def caption_layout(counts, Ld, N, Q, blocks, rows_cap=None, events_cap=None):
     out["vr_start"], out["vr_rows"] = start, flat
     out["max_rows"] = Ld * (int(events_cap) if events_cap is not None else max(counts, default=0))
     out["rows_per_layer"], out["real_rows"] = R, tot
+    out["ordered"] = ordered
     return out
 
 
-def pad_to_capacity(dt, events, rows, words, tokens=None):
+def live_rows(counts, steps, n_steps):
+    """Real caption rows per decoder layer still running at each step t < n_steps: sum of counts[v] over the
+    videos with steps[v] > t."""
+    c = np.asarray(counts, np.int64)
+    s = np.asarray(steps, np.int64)
+    return [int(c[s > t].sum()) for t in range(n_steps)]
+
+
+def step_ranges(live, Ld, R):
+    """(start, count) of the rows of each step for a caption_layout(..., steps=...) ordering: the live rows of
+    Ld = 2 are [R - a_t, R + a_t), of Ld = 1 [0, a_t)."""
+    if Ld == 2:
+        return tuple((R - a, 2 * a) for a in live)
+    if Ld == 1:
+        return tuple((0, a) for a in live)
+    raise ValueError("step ranges need 1 or 2 decoder layers")
+
+
+def pad_to_capacity(dt, events, rows, words, tokens=None, alive=None):
     """A collated batch (host tensors) padded to fixed shapes: every caption token row `words` wide, `rows + 1`
     caption rows (the real ones first, then all-zero rows; `rows` >= the batch's sum of events), `events` targets
     per video in the padded targets (to_device builds them), and dt["capacity"] recording them.  tokens: the
     loss-carrying caption tokens per decoder layer the stream's batches may hold (>= this batch's sum of
     cap_mask[:, 1:], pdvc/caption_tokens.py); the logit projection runs over that many token rows.  None: no
-    packing (every (row, step) position)."""
+    packing (every (row, step) position).  alive: per step t < words - 1, the caption rows per decoder layer the
+    stream's batches may still run at step t (>= live_rows of this batch); the recurrence then runs each step over
+    that many rows per layer (pdvc.py `_caption_rows`).  None: every row runs every step."""
     cap = dt["cap_tensor"]
     tot, K = cap.shape
     counts = [len(t["labels"]) for t in dt["video_target"]]
@@ -115,7 +161,20 @@ def pad_to_capacity(dt, events, rows, words, tokens=None):
         gb[:, :dt["gt_boxes"].shape[1]] = dt["gt_boxes"]
         out["gt_boxes"] = gb
         out["gt_boxes_mask"] = (gb != 0).sum(2) > 0
-    out["capacity"] = {"events": int(events), "rows": int(rows), "words": int(words), "tokens": int(tokens)}
+    if alive is not None:
+        alive = tuple(int(a) for a in alive)
+        if len(alive) != words - 1:
+            raise ValueError(f"pad_to_capacity: alive needs {words - 1} steps, got {len(alive)}")
+        from .CaptioningHead.LSTM_DSA import caption_steps
+        o, steps = 0, []
+        for c_ in counts:
+            steps.append(caption_steps(cap[o:o + c_]) if c_ else 0)
+            o += c_
+        have = live_rows(counts, steps, words - 1)
+        if any(h > a for h, a in zip(have, alive)) or max(alive, default=0) > rows:
+            raise ValueError("pad_to_capacity: live caption rows exceed the alive capacity")
+    out["capacity"] = {"events": int(events), "rows": int(rows), "words": int(words), "tokens": int(tokens),
+                       "alive": alive}
     return out
 
 
@@ -128,6 +187,8 @@ def caption_layout_to_device(lay, device):
     out = dict(zip(_DEVICE_KEYS, ts))
     out["max_rows"], out["rows_per_layer"], out["real_rows"] = lay["max_rows"], lay["rows_per_layer"], lay["real_rows"]
     out["rows_host"] = list(zip(lay["lay"].tolist(), lay["vid"].tolist()))
+    out["last_sel_host"] = lay["last_sel"].tolist()
+    out["ordered"] = lay.get("ordered", False)
     return out
 
 
@@ -143,3 +204,4 @@ def refresh_caption_layout(cached, lay):
         dst.copy_(src.to(dst.dtype).pin_memory(), non_blocking=True)
     cached["real_rows"] = lay["real_rows"]
     cached["rows_host"] = list(zip(lay["lay"].tolist(), lay["vid"].tolist()))
+    cached["last_sel_host"] = lay["last_sel"].tolist()

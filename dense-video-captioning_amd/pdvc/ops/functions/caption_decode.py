@@ -34,13 +34,18 @@ U_MAX_BYTES = 16 << 30  # largest projected-rows buffer of the gather form (ADVI
 class CaptionDecodeFunction(Function):
     """value (Nv,S,M,D) = value_proj(memory); xe (n,R,4H); hs_g (R,4H); off_hs (R, M*16); ref (R,L,1|2) (first rd1_rows rows
     1-d when 2-wide); W_h (M*16 + A + 4H, H), b_h; W_ctx (A, D), b_ctx (A); alpha_w (A,), alpha_b (1,);
-    W_att (4H, M*D).  Returns the hidden states (R, n, H)."""
+    W_att (4H, M*D); step_ranges (host per-step (start, count), device (n, 2) int32) or None.  Returns the hidden
+    states (R, n, H) (zeros at the (row, step) pairs a range leaves out)."""
 
     @staticmethod
     def forward(ctx, value, xe, hs_g, off_hs, ref, W_h, b_h, W_ctx, b_ctx, alpha_w, alpha_b, W_att, pad_mask,
-                row_video, level_T, rd1_rows, video_csr=None, heads=None):
+                row_video, level_T, rd1_rows, video_csr=None, heads=None, step_ranges=None):
         # value (Nv, S, M, D), or the projection's (Nv, S, M*D) output with `heads` = M: then the value gradient
         # goes back in that shape carrying its per-(video, level) row sums (`_pdvc_level_sums`, as MSDA1dFunction)
+        # step_ranges: per step (start, count) -- the rows that step computes (rows ordered by their video's step
+        # count, batch_layout.caption_layout(steps=...)); a row stops with its video's loop (LSTM_DSA.py:103-104).
+        # The other (step, row) entries of HS, RES, dHP, GAW are zeros, so the all-step weight-gradient GEMMs and
+        # sums below are exact; the other per-step buffers are never read there.
         ctx.flat_value = value.dim() == 3
         if ctx.flat_value:
             value = value.view(value.shape[0], value.shape[1], heads, -1)
@@ -51,6 +56,12 @@ class CaptionDecodeFunction(Function):
         Nv, S, M, D = value.shape
         n, R, G = xe.shape
         H = G // 4
+        ranged = step_ranges is not None
+        # step_ranges = (host tuple of (start, count) per step, the same as a (n, 2) int32 device tensor): the device
+        # copy is made once per batch by the caller, outside any captured graph
+        ranges = tuple(tuple(r) for r in step_ranges[0]) if ranged else ((0, R),) * n
+        if len(ranges) != n or any(s0 < 0 or c < 0 or s0 + c > R for s0, c in ranges):
+            raise ValueError("caption decode: step_ranges must give one in-bounds (start, count) per step")
         A = W_ctx.shape[0]
         NS = NUM_SAMPLES
         n_off = M * NS
@@ -66,10 +77,10 @@ class CaptionDecodeFunction(Function):
         LOC = torch.empty((n, R, M, NS), **kw)
         ATT = torch.empty((n, R * M * NS, A), **kw)
         PROBS = torch.empty((n, R, M, NS), **kw)
-        RES = torch.empty((n, R, M * D), **kw)
+        RES = (torch.zeros if ranged else torch.empty)((n, R, M * D), **kw)
         ACTS = torch.empty((n, R, G), **kw)
         CS = torch.empty((n, R, H), **kw)
-        HS = torch.empty((R, n, H), **kw)
+        HS = (torch.zeros if ranged else torch.empty)((R, n, H), **kw)
         GATT = torch.empty((R, G), **kw)
         zero = torch.zeros((R, H), **kw)
         st = _n.stream()
@@ -89,33 +100,45 @@ class CaptionDecodeFunction(Function):
         # and the value gradient's ctx2att part dU W_ctx are GEMMs over N*S rows instead of n*R*16, and the
         # location gradient of att is read off U at the sample corners (pdvc_cap_gather_backward2_f32)
         ctx.u_grad = U is not None and U_GRAD and A == D and video_csr is not None
+        if ranged and not ctx.u_grad:  # dW_ctx reads CLIP and dATT over every (step, row): no stale entries
+            CLIP.zero_()
+        ns_ = M * NS
         with fp32_gemms():  # the recurrence stays fp32 in the bf16 mode (pdvc/precision.py)
             for i in range(n):
+                s0, c = ranges[i]
+                if c == 0:
+                    continue
+                rs = slice(s0, s0 + c)
+                rd1 = min(max(int(rd1_rows) - s0, 0), c)  # the range's rows with a 1-d reference
+                hp = HP[i][rs]
                 if i == 0:
-                    HP[0].copy_(b_h.expand(R, Ph))  # h_{-1} = 0
+                    hp.copy_(b_h.expand(c, Ph))  # h_{-1} = 0
                 else:
-                    torch.addmm(b_h, HS[:, i - 1], W_h.t(), out=HP[i])
-                _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video), _n.ptr(HP[i]),
-                        Ph, 0, _n.ptr(off_hs), _n.ptr(ref), RD, int(rd1_rows), lvl, nl, Nv, R, M, D, NS // nl,
-                        _n.ptr(CLIP[i]), _n.ptr(LOC[i]), st)
+                    torch.addmm(b_h, HS[rs, i - 1], W_h.t(), out=hp)
+                _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video[rs]),
+                        _n.ptr(hp), Ph, 0, _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, D,
+                        NS // nl, _n.ptr(CLIP[i][rs]), _n.ptr(LOC[i][rs]), st)
+                att = ATT[i][s0 * ns_:(s0 + c) * ns_]
                 if U is not None:
-                    _n.call("pdvc_cap_gather_forward_f32", _n.ptr(U), None, _n.ptr(row_video), _n.ptr(HP[i]), Ph, 0,
-                            _n.ptr(off_hs), _n.ptr(ref), RD, int(rd1_rows), lvl, nl, Nv, R, M, A, NS // nl,
-                            _n.ptr(ATT[i]), None, st)
+                    _n.call("pdvc_cap_gather_forward_f32", _n.ptr(U), None, _n.ptr(row_video[rs]), _n.ptr(hp), Ph, 0,
+                            _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, A, NS // nl,
+                            _n.ptr(att), None, st)
                 else:
-                    torch.addmm(b_ctx, CLIP[i].view(-1, D), W_ctx.t(), out=ATT[i])
-                ah, ldh = _n.rows(HP[i][:, n_off:n_off + A])
-                _n.call("pdvc_softattn_forward_f32", _n.ptr(ATT[i]), ah, ldh, _n.ptr(alpha_w), _n.ptr(alpha_b),
-                        _n.ptr(CLIP[i]), R, M, A, D, _n.ptr(RES[i]), _n.ptr(PROBS[i]), st)
-                torch.mm(RES[i], W_att.t(), out=GATT)
-                xa, ldx = _n.rows(xe[i])
-                gh, ldg = _n.rows(HP[i][:, n_off + A:])
-                ho, ldo = _n.rows(HS[:, i])
-                _n.call("pdvc_lstm_cell_forward_f32", xa, ldx, _n.ptr(GATT), G, gh, ldg, _n.ptr(hs_g), G,
-                        _n.ptr(CS[i - 1] if i > 0 else zero), R, H, ho, ldo, _n.ptr(CS[i]), _n.ptr(ACTS[i]), st)
+                    torch.addmm(b_ctx, CLIP[i][rs].reshape(-1, D), W_ctx.t(), out=att)
+                ah, ldh = _n.rows(hp[:, n_off:n_off + A])
+                _n.call("pdvc_softattn_forward_f32", _n.ptr(att), ah, ldh, _n.ptr(alpha_w), _n.ptr(alpha_b),
+                        _n.ptr(CLIP[i][rs]), c, M, A, D, _n.ptr(RES[i][rs]), _n.ptr(PROBS[i][rs]), st)
+                torch.mm(RES[i][rs], W_att.t(), out=GATT[:c])
+                xa, ldx = _n.rows(xe[i][rs])
+                gh, ldg = _n.rows(hp[:, n_off + A:])
+                ho, ldo = _n.rows(HS[rs, i])
+                _n.call("pdvc_lstm_cell_forward_f32", xa, ldx, _n.ptr(GATT), G, gh, ldg, _n.ptr(hs_g[rs]), G,
+                        _n.ptr(CS[i - 1][rs] if i > 0 else zero), c, H, ho, ldo, _n.ptr(CS[i][rs]),
+                        _n.ptr(ACTS[i][rs]), st)
         ctx.save_for_backward(value, off_hs, ref, W_h, W_ctx, alpha_w, W_att, pad_mask, row_video, HP, CLIP, LOC,
                               ATT, PROBS, RES, ACTS, CS, HS, U if ctx.u_grad else None, vm if ctx.u_grad else None)
-        ctx.meta = (tuple(level_T), int(rd1_rows), video_csr)
+        ctx.meta = (tuple(level_T), int(rd1_rows), video_csr, ranges if ranged else None,
+                    step_ranges[1] if ranged else None)
         return HS
 
     @staticmethod
@@ -124,7 +147,8 @@ class CaptionDecodeFunction(Function):
         (value, off_hs, ref, W_h, W_ctx, alpha_w, W_att, pad_mask, row_video, HP, CLIP, LOC, ATT, PROBS, RES, ACTS,
          CS, HS, U, vm) = ctx.saved_tensors
         u_grad = ctx.u_grad
-        level_T, rd1_rows, video_csr = ctx.meta
+        level_T, rd1_rows, video_csr, ranged, sr_dev = ctx.meta
+        ranges = ranged if ranged is not None else ((0, HP.shape[1]),) * HP.shape[0]
         dHS = dHS.contiguous()
         Nv, S, M, D = value.shape
         n, R, Ph = HP.shape
@@ -136,55 +160,69 @@ class CaptionDecodeFunction(Function):
         RD = ref.shape[2]
         lvl, nl = _levels(level_T)
         kw = dict(dtype=value.dtype, device=value.device)
-        dHP = torch.empty((n, R, Ph), **kw)
-        dATT = torch.empty((n, R * M * NS, A), **kw)
-        GAW = torch.empty((n, R * M, A), **kw)
-        GAB = torch.empty((n, R * M), **kw)
+        alloc = torch.zeros if ranged is not None else torch.empty  # ranged: the skipped entries stay zero
+        dHP = alloc((n, R, Ph), **kw)
+        dATT = (alloc if not u_grad else torch.empty)((n, R * M * NS, A), **kw)
+        GAW = alloc((n, R * M, A), **kw)
+        GAB = alloc((n, R * M), **kw)
         # with the rows' per-video CSR, every step's sample gradient is kept and the value gradient is one
         # destination-sorted pass after the loop (pdvc_cap_value_grad_f32) instead of per-step atomics
         deferred = video_csr is not None
         dCLIP_all = torch.empty((n if deferred else 1, R, M, NS, D), **kw)
         dRES = torch.empty((R, M * D), **kw)
         dh = torch.empty((R, H), **kw)
-        dc = [torch.empty((R, H), **kw), torch.empty((R, H), **kw)]
+        dc = [alloc((R, H), **kw), alloc((R, H), **kw)]
         zero = torch.zeros((R, H), **kw)
         gv = torch.empty_like(value) if deferred else torch.zeros_like(value)
         gr = torch.zeros_like(ref) if ctx.needs_input_grad[3] else None
         st = _n.stream()
+        ns_ = M * NS
         with fp32_gemms():  # the recurrence stays fp32 in the bf16 mode
             for i in reversed(range(n)):
-                last = i == n - 1
-                dCLIP = dCLIP_all[i if deferred else 0]
-                gh_, ldgh = _n.rows(dHS[:, i])
-                dg, lddg = _n.rows(dHP[i][:, n_off + A:])
-                _n.call("pdvc_lstm_cell_backward_f32", gh_, ldgh, None if last else _n.ptr(dh), H,
-                        None if last else _n.ptr(dc[(i + 1) % 2]), _n.ptr(ACTS[i]),
-                        _n.ptr(CS[i - 1] if i > 0 else zero), _n.ptr(CS[i]), R, H, dg, lddg, _n.ptr(dc[i % 2]), st)
-                torch.mm(dHP[i][:, n_off + A:], W_att, out=dRES)
-                ah, ldh = _n.rows(HP[i][:, n_off:n_off + A])
-                gah, ldgah = _n.rows(dHP[i][:, n_off:n_off + A])
-                _n.call("pdvc_softattn_backward_f32", _n.ptr(ATT[i]), ah, ldh, _n.ptr(alpha_w), _n.ptr(CLIP[i]),
-                        _n.ptr(PROBS[i]), _n.ptr(dRES), R, M, A, D, _n.ptr(dATT[i]), gah, ldgah, _n.ptr(dCLIP),
-                        _n.ptr(GAW[i]), _n.ptr(GAB[i]), st)
-                if u_grad:  # dCLIP keeps the soft-attention part only; att's location gradient read off U
-                    _n.call("pdvc_cap_gather_backward2_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video),
-                            _n.ptr(HP[i]), Ph, 0, _n.ptr(off_hs), _n.ptr(ref), RD, rd1_rows, lvl, nl, Nv, R, M, D,
-                            NS // nl, _n.ptr(LOC[i]), _n.ptr(dCLIP), None, _n.ptr(dHP[i]), _n.ptr(gr), _n.ptr(U),
-                            _n.ptr(dATT[i]), st)
-                else:
-                    dCLIP.view(-1, D).addmm_(dATT[i], W_ctx)
-                    _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video),
-                            _n.ptr(HP[i]), Ph, 0, _n.ptr(off_hs), _n.ptr(ref), RD, rd1_rows, lvl, nl, Nv, R, M, D,
-                            NS // nl, _n.ptr(LOC[i]), _n.ptr(dCLIP), None if deferred else _n.ptr(gv), _n.ptr(dHP[i]),
-                            _n.ptr(gr), st)
-                if i > 0:
-                    torch.mm(dHP[i], W_h, out=dh)
+                s0, c = ranges[i]
+                rs = slice(s0, s0 + c)
+                rd1 = min(max(int(rd1_rows) - s0, 0), c)
+                dCLIP = dCLIP_all[i if deferred else 0][rs]
+                if c > 0:
+                    last = i == n - 1
+                    dhp = dHP[i][rs]
+                    gh_, ldgh = _n.rows(dHS[rs, i])
+                    dg, lddg = _n.rows(dhp[:, n_off + A:])
+                    _n.call("pdvc_lstm_cell_backward_f32", gh_, ldgh, None if last else _n.ptr(dh[rs]), H,
+                            None if last else _n.ptr(dc[(i + 1) % 2][rs]), _n.ptr(ACTS[i][rs]),
+                            _n.ptr(CS[i - 1][rs] if i > 0 else zero), _n.ptr(CS[i][rs]), c, H, dg, lddg,
+                            _n.ptr(dc[i % 2][rs]), st)
+                    torch.mm(dhp[:, n_off + A:], W_att, out=dRES[:c])
+                    ah, ldh = _n.rows(HP[i][rs][:, n_off:n_off + A])
+                    gah, ldgah = _n.rows(dhp[:, n_off:n_off + A])
+                    att = ATT[i][s0 * ns_:(s0 + c) * ns_]
+                    datt = dATT[i][s0 * ns_:(s0 + c) * ns_]
+                    _n.call("pdvc_softattn_backward_f32", _n.ptr(att), ah, ldh, _n.ptr(alpha_w), _n.ptr(CLIP[i][rs]),
+                            _n.ptr(PROBS[i][rs]), _n.ptr(dRES), c, M, A, D, _n.ptr(datt), gah, ldgah, _n.ptr(dCLIP),
+                            _n.ptr(GAW[i][s0 * M:(s0 + c) * M]), _n.ptr(GAB[i][s0 * M:(s0 + c) * M]), st)
+                    gr_ = gr[rs] if gr is not None else None
+                    if u_grad:  # dCLIP keeps the soft-attention part only; att's location gradient read off U
+                        _n.call("pdvc_cap_gather_backward2_f32", _n.ptr(value), _n.ptr(pad_mask),
+                                _n.ptr(row_video[rs]), _n.ptr(HP[i][rs]), Ph, 0, _n.ptr(off_hs[rs]), _n.ptr(ref[rs]),
+                                RD, rd1, lvl, nl, Nv, c, M, D, NS // nl, _n.ptr(LOC[i][rs]), _n.ptr(dCLIP), None,
+                                _n.ptr(dhp), _n.ptr(gr_), _n.ptr(U), _n.ptr(datt), st)
+                    else:
+                        dCLIP.reshape(-1, D).addmm_(datt, W_ctx)
+                        _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(pad_mask),
+                                _n.ptr(row_video[rs]), _n.ptr(HP[i][rs]), Ph, 0, _n.ptr(off_hs[rs]),
+                                _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, D, NS // nl, _n.ptr(LOC[i][rs]),
+                                _n.ptr(dCLIP), None if deferred else _n.ptr(gv), _n.ptr(dhp), _n.ptr(gr_), st)
+                if i > 0:  # dh of step i - 1's rows (rows that stopped at step i have dHP[i] = 0 there)
+                    p0, pc = ranges[i - 1]
+                    if pc > 0:
+                        torch.mm(dHP[i][p0:p0 + pc], W_h, out=dh[p0:p0 + pc])
         lsums = None
         if deferred:
             vr_start, vr_rows, max_rows = video_csr
             lsums = torch.empty(Nv, nl, M * D, dtype=gv.dtype, device=gv.device) if ctx.flat_value else None
-            _n.call("pdvc_cap_value_grad_ex_f32", _n.ptr(pad_mask), lvl, nl, Nv, M, D, NS // nl, R, n, int(max_rows),
-                    _n.ptr(vr_start), _n.ptr(vr_rows), _n.ptr(LOC), _n.ptr(dCLIP_all), _n.ptr(gv), _n.ptr(lsums), st)
+            _n.call("pdvc_cap_value_grad_ranged_f32", _n.ptr(pad_mask), lvl, nl, Nv, M, D, NS // nl, R, n,
+                    int(max_rows), _n.ptr(vr_start), _n.ptr(vr_rows), _n.ptr(sr_dev), _n.ptr(LOC), _n.ptr(dCLIP_all),
+                    _n.ptr(gv), _n.ptr(lsums), st)
         # weight gradients: one GEMM each over every (step, row)
         d_gates = dHP[..., n_off + A:]                       # (n, R, 4H), row stride Ph: xe's gradient as is
         d_hs_g = d_gates.sum(0)
@@ -199,8 +237,9 @@ class CaptionDecodeFunction(Function):
             # the bias), with its per-(video, level) row sums
             dU = torch.empty((Nv, S, M, A), **kw)
             lsU = torch.empty((Nv, nl, M * A), **kw)
-            _n.call("pdvc_cap_value_grad_ex_f32", None, lvl, nl, Nv, M, A, NS // nl, R, n, int(max_rows),
-                    _n.ptr(vr_start), _n.ptr(vr_rows), _n.ptr(LOC), _n.ptr(dATT), _n.ptr(dU), _n.ptr(lsU), st)
+            _n.call("pdvc_cap_value_grad_ranged_f32", None, lvl, nl, Nv, M, A, NS // nl, R, n, int(max_rows),
+                    _n.ptr(vr_start), _n.ptr(vr_rows), _n.ptr(sr_dev), _n.ptr(LOC), _n.ptr(dATT), _n.ptr(dU),
+                    _n.ptr(lsU), st)
             dU2 = dU.view(-1, A)
             dW_ctx = wgrad_mm(dU2, vm.reshape(-1, D))
             db_ctx = lsU.view(-1, A).sum(0)  # the weights of a sample sum to 1: sum dU = sum dATT
@@ -224,4 +263,4 @@ class CaptionDecodeFunction(Function):
             if deferred and lsums is not None:
                 tag_level_sums(gv, lsums)
         return (gv, d_gates, d_hs_g, d_off_hs, gr, dW_h, db_h, dW_ctx, db_ctx, dalpha_w, dalpha_b, dW_att, None, None,
-                None, None, None, None)
+                None, None, None, None, None)

@@ -23,7 +23,7 @@ from .CaptioningHead import build_captioner
 from .CaptioningHead.LSTM_DSA import caption_steps
 from .criterion import SetCriterion
 from .deformable_transformer import build_deforamble_transformer
-from .batch_layout import caption_layout, caption_layout_to_device
+from .batch_layout import caption_layout, caption_layout_to_device, live_rows, step_ranges
 from .caption_tokens import DeferredLogprobs, LazyProbs, pack_tokens, token_count
 from .matcher import LazyIndices, build_matcher
 
@@ -53,6 +53,20 @@ def decide_two_stage(transformer_input_type, dt, criterion):
 # PDVC_CAP_DEFERRED=0: per-step float atomics for the caption value gradient (A/B switch)
 _CAP_DEFERRED = os.environ.get("PDVC_CAP_DEFERRED", "1") != "0"
 # caption log-probabilities and the loss's target gather in one HIP pass each way (csrc/logprob.hip);
+# PDVC_STEP_RANGES=0: every caption row runs every step of the recurrence (no per-video stop, no row ordering)
+_STEP_RANGES = os.environ.get("PDVC_STEP_RANGES", "1") != "0"
+
+
+def video_steps(cap_cpu, counts):
+    """Each video's caption step count (LSTM_DSA.py:103-104: its loop stops at the first all-zero token column of its
+    captions), from the host copy of cap_tensor; 0 for a video without captions."""
+    out, o = [], 0
+    for c in counts:
+        out.append(caption_steps(cap_cpu[o:o + c]) if c else 0)
+        o += c
+    return out
+
+
 # PDVC_TOKENS_PACKED=0: the logit GEMM and log-softmax over every (row, step) position, not the packed valid tokens
 _TOKENS_PACKED = os.environ.get("PDVC_TOKENS_PACKED", "1") != "0"
 
@@ -324,9 +338,21 @@ class PDVC(nn.Module):
             blocks = tuple(ix.block for ix in layer_indices)
             key = ("_caption_rows", Ld, N, Q, blocks)
             if key not in dt:
+                # rows ordered by their video's step count, so that every step of the recurrence runs over one
+                # contiguous range of the rows still in their video's loop (ranged_steps); a capacity-padded batch
+                # needs the stream's live-row capacities for that (pad_to_capacity(alive=...))
+                ranged = _STEP_RANGES and Ld <= 2 and (cap is None or cap.get("alive") is not None)
+                vsteps = video_steps(cap_cpu, gt_counts) if ranged else None
                 lay = caption_layout(gt_counts, Ld, N, Q, blocks, None if cap is None else cap["rows"],
-                                     None if cap is None else cap["events"])
-                dt[key] = caption_layout_to_device(lay, dev)
+                                     None if cap is None else cap["events"], steps=vsteps)
+                Lc = caption_layout_to_device(lay, dev)
+                if ranged:
+                    n_dec = cap["words"] - 1 if cap is not None else max(vsteps, default=0)
+                    live = tuple(cap["alive"]) if cap is not None else live_rows(gt_counts, vsteps, n_dec)
+                    host = step_ranges(live, Ld, Lc["rows_per_layer"])
+                    Lc["step_ranges"] = (host, hostio.pack_to_device([[v for r in host for v in r]], dev)[0]
+                                         .to(torch.int32))
+                dt[key] = Lc
             Lc = dt[key]
             rp, rk, rb, rc, row_video = Lc["p"], Lc["k"], Lc["base"], Lc["cap"], Lc["vid"]
             lay_t, vid, last_sel_d, vr_start_d, vr_rows_d = Lc["lay"], Lc["vid"], Lc["last_sel"], Lc["vr_start"], \
@@ -335,11 +361,13 @@ class PDVC(nn.Module):
             flat_idx = rb + m.queries[rp, rk]
             cap_rows = rc + m.targets[rp, rk] * Lc["valid"]
             rows = Lc["rows_host"]  # (layer, video) per row, phantom rows (layer, 0): rd1 and n_last below
-            last_sel = list(range((Ld - 1) * Rl, Ld * Rl))
+            last_sel = Lc["last_sel_host"]
+            ranges = Lc.get("step_ranges")
             row_valid = Lc["valid"] if cap is not None else None
             lay = lay_t
         else:
             row_valid = None
+            ranges = None
             rows = []  # (layer, video, flat_hs_index, cap_row)
             for l_id, indices in enumerate(layer_indices):
                 for v, (qi, gi) in enumerate(indices):
@@ -377,7 +405,7 @@ class PDVC(nn.Module):
             else None
         return dict(rows=rows, hs_rows=hs_rows, ref_rows=ref_rows.contiguous(), rd1=rd1, row_video=row_video,
                     cap_rows=cap_rows, lay=lay, vid=vid, last_sel=last_sel_d, last_range=last_range, steps_v=steps_v,
-                    video_csr=video_csr, row_valid=row_valid)
+                    video_csr=video_csr, row_valid=row_valid, step_ranges=ranges)
 
     def parallel_prediction_matched(self, dt, criterion, hs, init_reference, inter_references, others,
                                     disable_refine, heads=None):
@@ -413,7 +441,8 @@ class PDVC(nn.Module):
                 R["hs_rows"], R["ref_rows"], R["rd1"], R["row_video"], others["memory"], others["mask_flatten"],
                 others["level_T"], seq_rows, n_steps,
                 video_csr=R["video_csr"] if _CAP_DEFERRED else None,
-                pick_target=seq_rows[:, 1:] if _LOGPROB_FUSED else None, tokens=tokens)
+                pick_target=seq_rows[:, 1:] if _LOGPROB_FUSED else None, tokens=tokens,
+                step_ranges=R["step_ranges"])
         else:
             raise NotImplementedError("share_caption_head=0 is not supported on the batched caption path")
         if _LOGPROB_FUSED:

@@ -173,7 +173,8 @@ class StepGraph:
         from .caption_tokens import token_count
         if dt.get("capacity") is not None:
             c = dt["capacity"]
-            return ("capacity", len(dt["video_target"]), c["events"], c["rows"], c["words"], c.get("tokens"))
+            return ("capacity", len(dt["video_target"]), c["events"], c["rows"], c["words"], c.get("tokens"),
+                    tuple(c["alive"]) if c.get("alive") is not None else None)
         counts = [len(t["labels"]) for t in dt["video_target"]]
         cap = dt.get("cap_tensor_cpu")
         cap = dt["cap_tensor"].detach().cpu() if cap is None else cap
@@ -224,14 +225,21 @@ class StepGraph:
                 if have > cap_tok:
                     raise ValueError(f"StepGraph.load: {have} caption tokens, capacity {cap_tok}")
             if dt.get("capacity") is not None:  # the caption rows' bookkeeping of the new counts
-                from .batch_layout import caption_layout, refresh_caption_layout
+                from .batch_layout import caption_layout, live_rows, refresh_caption_layout
+                from .pdvc import video_steps
                 counts = [len(t["labels"]) for t in dt["video_target"]]
                 cap = dt["capacity"]
                 for k, cached in self.dt.items():
                     if isinstance(k, tuple) and k and k[0] == "_caption_rows":
                         _, Ld, N, Q, blocks = k
+                        vsteps = None
+                        if cached.get("ordered"):  # rows ordered by step count, within the captured live ranges
+                            vsteps = video_steps(self.dt["cap_tensor_cpu"], counts)
+                            live = live_rows(counts, vsteps, cap["words"] - 1)
+                            if any(a > b for a, b in zip(live, cap["alive"])):
+                                raise ValueError("StepGraph.load: the batch's live caption rows exceed the capacity")
                         refresh_caption_layout(cached, caption_layout(counts, Ld, N, Q, blocks, cap["rows"],
-                                                                      cap["events"]))
+                                                                      cap["events"], steps=vsteps))
         for k, v in dt.items():
             dst = self.dt.get(k)
             if isinstance(v, torch.Tensor) and isinstance(dst, torch.Tensor) and dst.device.type == "cuda":

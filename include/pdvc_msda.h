@@ -417,6 +417,15 @@ int pdvc_cap_value_grad_ex_f32(const uint8_t* value_pad_mask, const int32_t* lev
                                const int32_t* video_row_start, const int32_t* video_rows, const float* save_loc,
                                const float* grad_samples, float* grad_value, float* grad_value_level_sums,
                                void* stream);
+/* The same with step_rows (steps, 2) DEVICE int32 or NULL: step t of the recurrence computed only the rows
+ * [step_rows[2t], step_rows[2t] + step_rows[2t + 1]) (each video's rows stop at its own last step,
+ * LSTM_DSA.py:103-104); the samples of the other (step, row) pairs are skipped -- their save_loc / grad_samples
+ * entries are never read. */
+int pdvc_cap_value_grad_ranged_f32(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels, int batch,
+                                   int num_heads, int head_dim, int num_point, int rows, int steps,
+                                   int max_rows_per_video, const int32_t* video_row_start, const int32_t* video_rows,
+                                   const int32_t* step_rows, const float* save_loc, const float* grad_samples,
+                                   float* grad_value, float* grad_value_level_sums, void* stream);
 
 /* ---- encoder positional input ------------------------------------------------------------------------
  * pos[n, s, c] = (c < F ? (c even ? sin : cos)(xe[n*S + s] / dim_t[c]) : dur[n*Dd + c - F])

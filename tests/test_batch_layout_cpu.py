@@ -81,7 +81,7 @@ def test_pad_to_capacity():
     tot, K = dt["cap_tensor"].shape
     assert torch.equal(p["cap_tensor"][:tot, :K], dt["cap_tensor"]) and not p["cap_tensor"][tot:].any()
     assert not p["cap_tensor"][:, K:].any() and not p["cap_mask"][tot:].any()
-    assert p["gt_boxes"].shape == (3, 6, 2) and p["capacity"] == {"events": 6, "rows": 20, "words": 11, "tokens": 200}
+    assert p["gt_boxes"].shape == (3, 6, 2) and p["capacity"] == {"events": 6, "rows": 20, "words": 11, "tokens": 200, "alive": None}
     for bad in (dict(events=3, rows=20, words=11), dict(events=6, rows=11, words=11),
                 dict(events=6, rows=20, words=K - 1)):
         with pytest.raises(ValueError):
@@ -96,3 +96,33 @@ def test_static_pairs_at_capacity():
     assert emax == 4 and pp.tolist() == [0] * 4 + [1] * 4 + [2] * 4 and pk.tolist() == list(range(4)) * 3
     valid = (pk < nm[pp]).tolist()
     assert valid == [True, True, False, False] + [False] * 4 + [True, True, True, False]
+
+
+@pytest.mark.parametrize("Ld,rows_cap", [(2, None), (2, 40), (1, None), (1, 33)])
+def test_step_ordered_layout_keeps_live_rows_contiguous(Ld, rows_cap):
+    """caption_layout(..., steps=...): the same rows as the video-major layout, reordered so that the rows of the
+    videos still running at each step are exactly step_ranges' range; last_sel lists the last layer video-major and
+    the CSR still names each video's rows."""
+    from pdvc.batch_layout import caption_layout, live_rows, step_ranges
+    rng = np.random.RandomState(3)
+    N, Q = 7, 20
+    counts = [int(c) for c in rng.randint(0, 6, N)]
+    steps = [int(s) for s in rng.randint(1, 12, N)]
+    steps[2] = 0 if counts[2] else steps[2]
+    blocks = list(range(Ld))
+    plain = caption_layout(counts, Ld, N, Q, blocks, rows_cap=rows_cap)
+    lay = caption_layout(counts, Ld, N, Q, blocks, rows_cap=rows_cap, steps=steps)
+    R = lay["rows_per_layer"]
+    key = lambda L, i: tuple(int(L[k][i]) for k in ("p", "k", "base", "cap", "vid", "lay", "valid"))
+    assert sorted(key(lay, i) for i in range(Ld * R)) == sorted(key(plain, i) for i in range(Ld * R))
+    n = max(steps)
+    live = live_rows(counts, steps, n)
+    for t, (s0, c) in enumerate(step_ranges(live, Ld, R)):
+        running = {i for i in range(Ld * R) if lay["valid"][i] and steps[lay["vid"][i]] > t}
+        assert running == set(range(s0, s0 + c)), f"step {t}"
+    # the last layer's rows, video-major, as the unordered layout lists them
+    assert [key(lay, i) for i in lay["last_sel"]] == [key(plain, i) for i in plain["last_sel"]]
+    for v in range(N):
+        rows = lay["vr_rows"][lay["vr_start"][v]:lay["vr_start"][v + 1]]
+        assert sorted(int(lay["vid"][r]) for r in rows) == [v] * (Ld * counts[v])
+        assert all(lay["valid"][r] for r in rows)

@@ -204,13 +204,21 @@ CAPS = dict(events=7, rows=16, words=12)
 
 def padded_dt(items, packed=False):
     """packed: a token capacity 8 above the batch's caption-token count, so the logit projection runs over the
-    packed valid tokens (pdvc/caption_tokens.py); else every (row, step) position."""
+    packed valid tokens (pdvc/caption_tokens.py), and live-row capacities per step, so the recurrence runs each step
+    over the rows still in their video's loop; else every (row, step) position."""
     import weights as W  # noqa: F401
     from pdvc.batch_layout import pad_to_capacity
     from pdvc.data import collate, to_device
     c = collate(items)
-    tokens = int(c["cap_mask"][:, 1:CAPS["words"]].sum()) + 8 if packed else None
-    return to_device(pad_to_capacity(c, tokens=tokens, **CAPS), DEV)
+    tokens = alive = None
+    if packed:  # and the recurrence over the live rows of each step (with 2 rows of slack)
+        from pdvc.batch_layout import live_rows
+        from pdvc.pdvc import video_steps
+        tokens = int(c["cap_mask"][:, 1:CAPS["words"]].sum()) + 8
+        counts = [len(t["labels"]) for t in c["video_target"]]
+        alive = [min(a + 2, CAPS["rows"]) for a in live_rows(counts, video_steps(c["cap_tensor"], counts),
+                                                             CAPS["words"] - 1)]
+    return to_device(pad_to_capacity(c, tokens=tokens, alive=alive, **CAPS), DEV)
 
 
 def _check_padded_forward(d, out, loss, nv, cap):
