@@ -1,0 +1,15 @@
+#!/bin/bash
+# round-4 GPU pass E: caption recurrence over live row ranges -- model tests, then the ragged bench A/B
+set -o pipefail
+O=gpurun_out/r04e
+mkdir -p $O
+export TMPDIR=/tmp
+echo "[$(date +%T)] tests"
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_batch.py tests/test_gpu_batch_gt.py \
+    tests/test_gpu_model.py tests/test_gpu_modules.py tests/test_gpu_bf16.py tests/test_gpu_dp.py tests/test_gpu_configs.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+for sr in 1 0; do
+  echo "[$(date +%T)] ragged bench PDVC_STEP_RANGES=$sr"
+  PDVC_STEP_RANGES=$sr timeout -k 10 500 python -u bench.py --stream ragged --no-cpu-baseline --no-gemm-roofline --no-dropin > $O/bench_ragged_sr$sr.json 2> $O/bench_ragged_sr$sr.err || { tail -20 $O/bench_ragged_sr$sr.err; exit 1; }
+  python -c "import json; d=json.load(open('$O/bench_ragged_sr$sr.json')); print(d['value'], d['ms_per_step'])"
+done
