@@ -688,6 +688,170 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_pyr2_kernel(
 }
 
 // -------------------------------------------------------------------------------------------------
+// msda1d_fwd_win_kernel: the whole-pyramid forward for pyramids whose level 0 does not fit one staging phase --
+// 512 < T0 <= 1024 with T1 <= 512 and T2 + T3 <= 512 (anet_c3d's T = 1024: 1024 / 512 / 256 / 128, BASELINE.json
+// configs[4]; at T0 = 1024 one head's level 0 is 256 KiB, past the 160 KiB of LDS).  Level 0 is staged in two
+// WINDOWS of rows, [0, 513) and [512, T0), overlapping by one row: a sample's corner rows x0, x0 + 1 with
+// x0 <= 511 lie in the first, with x0 >= 512 in the second (x0 + 1 = T0 reads the guard row after it).  The owner
+// lane of a level-0 sample computes its LDS offset for both windows -- in the window that does not hold the sample it
+// points at two zero rows kept past the staged rows, so the weights need no second copy -- and the gather phase of
+// each window broadcasts its own offset
+// (msda1d_fwd_pyr2_kernel's DPP row_newbcast).  Then level 1 alone, then levels 2 and 3 packed: four staging phases,
+// every corner row read from LDS, the same arithmetic and accumulation order as msda1d_fwd_pyr2_kernel (per query:
+// levels in order, points in order, corner x0 then x0 + 1 -- a level-0 sample contributes in exactly one window).
+// -------------------------------------------------------------------------------------------------
+constexpr int kWinSplit = 512;                                   // first level-0 row of the second window
+constexpr int kWinRows = kWinSplit + 1;                          // data rows of the first window
+constexpr int kWinZero = kWinRows + 2;                           // two zero rows: the out-of-window corners
+constexpr size_t kWinLds = (size_t)(kWinZero + 2) * 256;          // guard, 513 rows, guard, the two zero rows
+
+__host__ __device__ inline bool win_fits(const Levels1d& lv) {
+    return lv.T[0] > kWinSplit && lv.T[0] <= 2 * kWinSplit && lv.T[1] <= kWinSplit &&
+           lv.T[2] + lv.T[3] <= kWinSplit;
+}
+
+template <int RD>
+__global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_win_kernel(
+    const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
+    int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
+    int qblocks, float* __restrict__ out, float* __restrict__ save_attn, float* __restrict__ save_loc,
+    uint16_t* __restrict__ out16) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds4[];
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);  // the query blocks and heads of a video share an XCD
+    const int qb = blk % qblocks, bm = blk / qblocks;
+    const int b = bm / M, m = bm - b * M;
+    const int slot = threadIdx.x >> 4, sub = threadIdx.x & 15;
+    const size_t MD = (size_t)M * 64;
+    const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
+    const float* vsrc = value + (size_t)b * S * MD + (size_t)m * 64;
+    const char* lrow = reinterpret_cast<const char*>(lds4) + sub * 16;
+    pyr_zero_row(lds4, 0, 0);  // the leading guard row of every phase
+    pyr_zero_row(lds4, kWinZero, 64);
+    pyr_zero_row(lds4, kWinZero + 1, 128);
+    const int l_own = sub >> 2;
+    const int T_own = lvl_sel(lv.T, l_own), st_own = lvl_sel(lv.start, l_own);
+    const int base_own = l_own == 3 ? 1 + lv.T[2] : 1;  // LDS row of the owner level's row 0 in its phase
+    const float Tf_own = (float)T_own;
+    float lgv[kPyrQPS], offv[kPyrQPS], r0v[kPyrQPS], r1v[kPyrQPS];
+#pragma unroll
+    for (int i = 0; i < kPyrQPS; ++i) {
+        const int q = qb * kPyrQ + slot + 64 * i;
+        const size_t row = (size_t)b * Lq + (q < Lq ? q : 0);
+        const float* prow = proj + row * proj_stride;
+        lgv[i] = prow[logit_base + m * kNS + sub];
+        offv[i] = prow[off_base + m * kNS + sub];
+        r0v[i] = ref[(row * kL + l_own) * RD];
+        r1v[i] = (RD == 2) ? ref[(row * kL + l_own) * RD + 1] : 0.f;
+    }
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): the parameters, before the first phase's DMAs are issued
+    pyr_dma_rows(lds4, vsrc, MD, lv.start[0], 1, kWinRows);
+    // per query: the owner's corner weights and its LDS offset for window A (level 0 rows [0, 513); every other
+    // level's phase) and for window B (level 0 rows [512, T0))
+    int adA[kPyrQPS], adB[kPyrQPS];
+    float w1v[kPyrQPS], w2v[kPyrQPS];
+#pragma unroll
+    for (int i = 0; i < kPyrQPS; ++i) {
+        const int q = qb * kPyrQ + slot + 64 * i;
+        const bool act = q < Lq;
+        const float lg = lgv[i];
+        const float mx = group_max<16>(lg);
+        const float sum = group_allreduce<16>(expf(lg - mx));
+        const float aw = expf(lg - mx) / sum;
+        const float off = offv[i];
+        const float r0 = r0v[i];
+        const float r1 = r1v[i];
+        const float loc = (RD == 1) ? r0 + off / Tf_own : r0 + ((off / (float)kP) * r1) * 0.5f;
+        if (save_loc && act) {
+            const size_t si = save_index(b, m, l_own, q, sub & 3, Lq, M);
+            save_loc[si] = loc;
+            save_attn[si] = aw;
+        }
+        const float x = loc * Tf_own - 0.5f;
+        const bool inside = x > -1.f && x < Tf_own;
+        const float xf = floorf(inside ? x : 0.f);
+        const int i0 = (int)xf;
+        const float lw = inside ? x - xf : 0.f;
+        bool ok1 = inside && i0 >= 0, ok2 = inside && i0 + 1 <= T_own - 1;
+        if (mbase) {
+            ok1 = ok1 && !mbase[st_own + min(max(i0, 0), T_own - 1)];
+            ok2 = ok2 && !mbase[st_own + min(max(i0 + 1, 0), T_own - 1)];
+        }
+        w1v[i] = ok1 ? (1.f - lw) * aw : 0.f;
+        w2v[i] = ok2 ? lw * aw : 0.f;
+        const int ad = pyr_corner(base_own, i0);
+        const bool inB = l_own == 0 && i0 >= kWinSplit;
+        adA[i] = inB ? kWinZero * 256 : ad;
+        adB[i] = inB ? ad - kWinSplit * 256 : kWinZero * 256;
+    }
+    PAcc4 acc[kPyrQPS];
+#pragma unroll
+    for (int i = 0; i < kPyrQPS; ++i) acc[i] = pacc_zero();
+    PAcc4 tok = pacc_zero();
+    auto level = [&](auto Lc, auto Bc) {
+        constexpr int L = decltype(Lc)::value;
+        constexpr bool B = decltype(Bc)::value;
+#pragma unroll
+        for (int i = 0; i < kPyrQPS; ++i) {
+            pf4 v1[kP], v2[kP];
+            float c1[kP], c2[kP];
+            int ad = B ? adB[i] : adA[i];
+            float wa = w1v[i], wb = w2v[i];
+            __asm__ volatile("" : "+v"(ad), "+v"(wa), "+v"(wb) : "v"(tok.lo), "v"(tok.hi));
+#pragma unroll
+            for (int p = 0; p < kP; ++p) {
+                const char* r = lrow + grp_bcast<16>(ad, L * kP + p);
+                c1[p] = grp_bcast<16>(wa, L * kP + p);
+                c2[p] = grp_bcast<16>(wb, L * kP + p);
+                v1[p] = *reinterpret_cast<const pf4*>(r);
+                v2[p] = *reinterpret_cast<const pf4*>(r + 256);
+            }
+#pragma unroll
+            for (int p = 0; p < kP; ++p) {
+                pacc_fma(acc[i], c1[p], v1[p]);
+                pacc_fma(acc[i], c2[p], v2[p]);
+            }
+            tok = acc[i];
+        }
+    };
+    using F = std::false_type;
+    using Tt = std::true_type;
+    pyr_dma_wait();
+    __syncthreads();  // window A landed
+    level(std::integral_constant<int, 0>{}, F{});
+    __syncthreads();  // every wave is done with window A
+    const int nB = lv.T[0] - kWinSplit;
+    pyr_dma_rows(lds4, vsrc, MD, lv.start[0] + kWinSplit, 1, nB);
+    pyr_zero_row(lds4, 1 + nB, 0);
+    pyr_dma_wait();
+    __syncthreads();
+    level(std::integral_constant<int, 0>{}, Tt{});
+    __syncthreads();
+    pyr_dma_rows(lds4, vsrc, MD, lv.start[1], 1, lv.T[1]);
+    pyr_zero_row(lds4, 1 + lv.T[1], 0);
+    pyr_dma_wait();
+    __syncthreads();
+    level(std::integral_constant<int, 1>{}, F{});
+    __syncthreads();
+    const int n23 = lv.T[2] + lv.T[3];
+    pyr_dma_rows(lds4, vsrc, MD, lv.start[2], 1, n23);
+    pyr_zero_row(lds4, 1 + n23, 0);
+    pyr_dma_wait();
+    __syncthreads();
+    level(std::integral_constant<int, 2>{}, F{});
+    level(std::integral_constant<int, 3>{}, F{});
+#pragma unroll
+    for (int i = 0; i < kPyrQPS; ++i) {
+        const int q = qb * kPyrQ + slot + 64 * i;
+        if (q < Lq) {
+            const size_t o = ((size_t)b * Lq + q) * MD + (size_t)m * 64 + sub * 4;
+            const float4 r = pacc_f4(acc[i]);
+            *reinterpret_cast<float4*>(out + o) = r;
+            if (out16) store_bf16x4(out16 + o, r.x, r.y, r.z, r.w);
+        }
+    }
+}
+
+// -------------------------------------------------------------------------------------------------
 // backward, query side: grad of the offset and attention logits (+ reference points)
 // softmax backward needs delta = sum_j a_j dL/da_j over the 16 samples of a (query, head).  Default (fout NULL):
 // each level's owner lanes keep their (a_j, dL/da_j) pair in registers -- one pair per lane per level -- and the
@@ -1996,6 +2160,16 @@ static int pick_pyr(const Levels1d& lv, int S, int num_query, int head_dim, int 
 // value-gradient walk depth (PDVC_VALUE_UG=4 / 8 forces it): 4 where a level holds few samples per row (the
 // decoder, 4 * Lq < S: its workgroups' LDS is small, so the 66-VGPR form fits more of them per CU -- 206 -> 177 us at
 // 256 videos), 8 for the encoder (LDS-limited to two workgroups per CU anyway; 8 in flight: 770 -> 700 us)
+// the windowed whole-pyramid kernels (msda1d_fwd_win_kernel) where pick_pyr's staging does not fit: encoder-shaped
+// calls (4 Lq >= S) at D = 64 on a pyramid with win_fits; PDVC_MSDA_WIN=0 keeps the L2-gather kernels (A/B)
+static bool win_ok(const Levels1d& lv, int num_query, int S, int head_dim) {
+    static const bool on = [] {
+        const char* e = getenv("PDVC_MSDA_WIN");
+        return !(e && e[0] == '0');
+    }();
+    return on && head_dim == 64 && num_query > 0 && 4L * num_query >= S && win_fits(lv);
+}
+
 static int value_ug(int num_query, int S) {
     static const int forced = [] {
         const char* e = getenv("PDVC_VALUE_UG");
@@ -2164,6 +2338,26 @@ static int msda1d_forward_impl(const float* value, const uint8_t* value_pad_mask
                                proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, qb, output,
                                save_attn, save_loc);
         PDVC_CHECK_LAUNCH("msda1d_fwd_pyr_kernel");
+        return PDVC_OK;
+    }
+    if (win_ok(lv, num_query, S, head_dim)) {  // level 0 past one staging phase: two row windows
+        static std::atomic<int> done[kMaxDevices];
+        if ((rc = lds_optin(done, {{(const void*)msda1d_fwd_win_kernel<1>, (int)kWinLds},
+                                   {(const void*)msda1d_fwd_win_kernel<2>, (int)kWinLds}},
+                            "msda1d_fwd_win_kernel")))
+            return rc;
+        const int qb = (num_query + kPyrQ - 1) / kPyrQ;
+        PDVC_CHECK_ARG((long)batch * num_heads * qb < (1L << 31), "too many query blocks");
+        dim3 pg((unsigned)(batch * num_heads * qb));
+        if (ref_dim == 1)
+            hipLaunchKernelGGL((msda1d_fwd_win_kernel<1>), pg, dim3(kPyrThreads), kWinLds, s, value, value_pad_mask,
+                               proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, qb, output,
+                               save_attn, save_loc, out16);
+        else
+            hipLaunchKernelGGL((msda1d_fwd_win_kernel<2>), pg, dim3(kPyrThreads), kWinLds, s, value, value_pad_mask,
+                               proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, qb, output,
+                               save_attn, save_loc, out16);
+        PDVC_CHECK_LAUNCH("msda1d_fwd_win_kernel");
         return PDVC_OK;
     }
     if (out16) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "bf16 output only on the LDS-DMA pyramid path");

@@ -496,16 +496,20 @@ def _away_from_cell_edges(proj, ref, T_l, M, margin=2e-3):
     return out
 
 
-@pytest.mark.parametrize("T_l,ref_dim", [((1024, 512, 256, 128), 1), ((1024, 512, 256, 128), 2),
-                                         ((512, 300, 150, 60), 1), ((512, 300, 150, 60), 2)])
-def test_fused_msda1d_long_pyramids_vs_oracle(T_l, ref_dim):
-    """Long pyramids: anet_c3d's T = 1024 (S = 1920: level 0 too long for the LDS pyramids, so the buffer-load
-    forward and the dot-product backward-query run at Lq = S; the value gradient takes two query chunks, the
-    second accumulating into the rows the first wrote), and S = 1022 (both pyramid kernels with two query blocks)."""
+@pytest.mark.parametrize("T_l,ref_dim,M", [((1024, 512, 256, 128), 1, 2), ((1024, 512, 256, 128), 2, 2),
+                                           ((1024, 512, 256, 128), 1, 8), ((1024, 512, 256, 128), 2, 8),
+                                           ((700, 512, 256, 200), 1, 8),
+                                           ((512, 300, 150, 60), 1, 2), ((512, 300, 150, 60), 2, 2)])
+def test_fused_msda1d_long_pyramids_vs_oracle(T_l, ref_dim, M):
+    """Long pyramids: anet_c3d's T = 1024 (S = 1920: level 0 past one LDS staging phase, so the forward runs the
+    windowed pyramid kernel -- level 0 in two row windows, msda1d_fwd_win_kernel -- and the backward-query the
+    dot-product kernel at Lq = S; the value gradient takes two query chunks, the second accumulating into the rows the
+    first wrote), a level 0 of 700 rows (second window shorter than the first), and S = 1022 (both pyramid kernels with
+    two query blocks).  M = 8 is the headline's head count."""
     from pdvc.ops.functions import MSDA1dFunction
-    rng = np.random.RandomState(sum(T_l) + ref_dim)
+    rng = np.random.RandomState(sum(T_l) + ref_dim + M)
     S = sum(T_l)
-    M, D, N, Lq = 2, 64, 1, S
+    D, N, Lq = 64, 1, S
     value = rng.randn(N, S, M, D)
     proj = np.concatenate([rng.randn(N, Lq, M * 16) * 4.0, rng.randn(N, Lq, M * 16)], -1)
     centre = np.concatenate([(np.arange(t) + 0.5) / t for t in T_l])[None, :, None, None].repeat(4, 2)
