@@ -13,3 +13,10 @@ for sr in 1 0; do
   PDVC_STEP_RANGES=$sr timeout -k 10 500 python -u bench.py --stream ragged --no-cpu-baseline --no-gemm-roofline --no-dropin > $O/bench_ragged_sr$sr.json 2> $O/bench_ragged_sr$sr.err || { tail -20 $O/bench_ragged_sr$sr.err; exit 1; }
   python -c "import json; d=json.load(open('$O/bench_ragged_sr$sr.json')); print(d['value'], d['ms_per_step'])"
 done
+echo "[$(date +%T)] long-pyramid ops tests"
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_ops.py -k "long_pyramids" > $O/ops_long.log 2>&1 || { tail -30 $O/ops_long.log; exit 1; }
+tail -2 $O/ops_long.log
+for w in 0 1; do
+  echo "[$(date +%T)] kbench T=1024 PDVC_MSDA_WIN=$w"
+  PDVC_MSDA_WIN=$w timeout -k 10 120 python -u tools/kbench.py --videos 512 --reps 4 --T 1024 2>&1 | grep -E "^(encoder|decoder)" | tee -a $O/kbench_T1024_win$w.log || exit 1
+done
