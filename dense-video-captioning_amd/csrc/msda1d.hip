@@ -1350,183 +1350,6 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
 }
 
 // -------------------------------------------------------------------------------------------------
-// msda1d_bwd_query_win_kernel: msda1d_bwd_query_pyr_kernel's dot-product backward on msda1d_fwd_win_kernel's four
-// staging phases (level 0 in the row windows [0, 513) and [512, T0), level 1, levels 2 + 3).  A level-0 sample is
-// reduced in both windows (its out-of-window offset points at two zero rows) but its owner math -- the offset
-// gradient, grad_ref, dL/da -- runs only in the window that holds it; grad_ref's per-(query, level) quad sum is issued
-// in both windows (the other window's part is 0).  dL/da of levels 0 and 1 reaches the last phase, where the softmax
-// term over all 16 samples is formed, through two LDS carries (2 x 15 KiB beside the 517 rows: 159.3 KiB).
-// -------------------------------------------------------------------------------------------------
-constexpr size_t kBqWinLds = kWinLds + 2 * (size_t)kBqQ * 4 * sizeof(float);
-
-template <int RD>
-__global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_win_kernel(
-    const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
-    int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
-    int qblocks, const float* __restrict__ gout, const float* __restrict__ save_attn,
-    const float* __restrict__ save_loc, float* __restrict__ grad_proj, float* __restrict__ grad_ref,
-    uint16_t* __restrict__ gp16) {
-    extern __shared__ __attribute__((aligned(16))) float4 lds4[];
-    float* carry0 = reinterpret_cast<float*>(lds4 + (kWinZero + 2) * 16);  // [kBqQ][4]: dL/da of level 0's samples
-    float* carry1 = carry0 + kBqQ * 4;                                      // [kBqQ][4]: level 1's
-    const int blk = xcd_remap(blockIdx.x, gridDim.x);
-    const int qb = blk % qblocks, bm = blk / qblocks;
-    const int b = bm / M, m = bm - b * M;
-    const int slot = threadIdx.x >> 4, sub = threadIdx.x & 15, lane = threadIdx.x & 63;
-    const int MD = M * 64;
-    const float* vsrc = value + (size_t)b * S * MD + (size_t)m * 64;
-    const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
-    const int l_own = sub >> 2, p_own = sub & 3;
-    const int T_own = lvl_sel(lv.T, l_own), st_own = lvl_sel(lv.start, l_own);
-    const float Tf = (float)T_own;
-    const int base_own = l_own == 3 ? 1 + lv.T[2] : 1;
-    const char* lrow = reinterpret_cast<const char*>(lds4) + sub * 16;
-    if (threadIdx.x < 16) lds4[(size_t)kWinZero * 16 + threadIdx.x] = make_float4(0.f, 0.f, 0.f, 0.f);
-    else if (threadIdx.x < 32) lds4[(size_t)(kWinZero + 1) * 16 + (threadIdx.x & 15)] = make_float4(0.f, 0.f, 0.f, 0.f);
-
-    // one query of this lane group through the levels [L0, L1) of phase PH (0, 1: level 0's windows; 2: level 1;
-    // 3: levels 2 + 3)
-    auto run_query = [&](int iq, auto L0c, auto L1c, auto PHc) {
-        constexpr int L0 = decltype(L0c)::value, L1 = decltype(L1c)::value, PH = decltype(PHc)::value;
-        const int q0 = qb * kBqQ + slot + 64 * iq;
-        const bool act = q0 < Lq;
-        const int q = act ? q0 : Lq - 1;
-        const size_t row = (size_t)b * Lq + q;
-        const float4 g = *reinterpret_cast<const float4*>(gout + row * MD + (size_t)m * 64 + sub * 4);
-        const size_t si = save_index(b, m, l_own, q, p_own, Lq, M);
-        const float x = save_loc[si] * Tf - 0.5f;
-        const float a = save_attn[si];
-        const bool inside = x > -1.f && x < Tf;
-        const float xf = floorf(inside ? x : 0.f);
-        const int i0 = (int)xf;
-        const float lw = inside ? x - xf : 0.f;
-        const bool inB = l_own == 0 && i0 >= kWinSplit;
-        const int adn = pyr_corner(base_own, i0);
-        const int ad = PH == 0 ? (inB ? kWinZero * 256 : adn) : PH == 1 ? (inB ? adn - kWinSplit * 256 : kWinZero * 256)
-                                                                        : adn;
-        float d1 = 0.f, d2 = 0.f;
-#pragma unroll
-        for (int L = L0; L < L1; ++L) {
-            float part[8];
-            const pf2 gxy = {g.x, g.y}, gzw = {g.z, g.w};
-#pragma unroll
-            for (int p = 0; p < kP; ++p) {
-                const char* r = lrow + grp_bcast<16>(ad, L * kP + p);
-                const pf4 u1 = *reinterpret_cast<const pf4*>(r);
-                const pf4 u2 = *reinterpret_cast<const pf4*>(r + 256);
-                const pf2 t1 = __builtin_elementwise_fma(gzw, u1.zw, gxy * u1.xy);
-                const pf2 t2 = __builtin_elementwise_fma(gzw, u2.zw, gxy * u2.xy);
-                part[p] = t1.x + t1.y;
-                part[4 + p] = t2.x + t2.y;
-            }
-            const bool u8 = (lane & 8) != 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float send = u8 ? part[k] : part[k + 4];
-                const float mine = u8 ? part[k + 4] : part[k];
-                part[k] = mine + grp_swap(send, 8);
-            }
-            const bool u2b = (lane & 2) != 0;
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const float send = u2b ? part[k] : part[k + 2];
-                const float mine = u2b ? part[k + 2] : part[k];
-                part[k] = mine + grp_swap(send, 2);
-            }
-            const bool u1b = (lane & 1) != 0;
-            const float send = u1b ? part[0] : part[1];
-            const float mine = u1b ? part[1] : part[0];
-            part[0] = mine + grp_swap(send, 1);
-            part[0] += grp_swap(part[0], 4);
-            const float other = grp_swap(part[0], 8);
-            if (l_own == L) {
-                d1 = (L < 2) ? part[0] : other;
-                d2 = (L < 2) ? other : part[0];
-            }
-        }
-        // owner math of the lanes whose sample this phase holds (.cuh:140-170)
-        const bool level_phase = l_own >= L0 && l_own < L1;
-        const bool mine_phase = level_phase && (PH > 1 || inB == (PH == 1));
-        bool ok1 = inside && i0 >= 0, ok2 = inside && i0 + 1 <= T_own - 1;
-        if (mbase) {
-            ok1 = ok1 && !mbase[st_own + min(max(i0, 0), T_own - 1)];
-            ok2 = ok2 && !mbase[st_own + min(max(i0 + 1, 0), T_own - 1)];
-        }
-        const float x1 = ok1 ? d1 : 0.f, x2 = ok2 ? d2 : 0.f;
-        float ga = (1.f - lw) * x1 + lw * x2;
-        const float gloc = Tf * ((x2 - x1) * a);
-        const float* prow = proj + row * proj_stride;
-        float* gprow = grad_proj + row * proj_stride;
-        float g0 = mine_phase ? gloc : 0.f, g1 = 0.f, goff;
-        if (RD == 1) {
-            goff = gloc / Tf;
-        } else {
-            const float rr1 = ref[(row * kL + l_own) * 2 + 1];
-            const float t2 = gloc * 0.5f;
-            goff = (t2 * rr1) / (float)kP;
-            g1 = mine_phase ? t2 * (prow[off_base + m * kNS + sub] / (float)kP) : 0.f;
-        }
-        if (act && mine_phase) {
-            gprow[off_base + m * kNS + sub] = goff;
-            if (gp16) gp16[row * proj_stride + off_base + m * kNS + sub] = (uint16_t)bf16_bits(goff);
-        }
-        if (grad_ref) {  // per (query, level): the lane quad of the level (a level-0 quad may span both windows)
-            g0 += grp_swap(g0, 1);
-            g0 += grp_swap(g0, 2);
-            if (RD == 2) {
-                g1 += grp_swap(g1, 1);
-                g1 += grp_swap(g1, 2);
-            }
-            if (p_own == 0 && act && level_phase) {
-                float* dst = grad_ref + (row * kL + l_own) * RD;
-                atomicAdd(dst, g0);
-                if (RD == 2) atomicAdd(dst + 1, g1);
-            }
-        }
-        const int ci = (slot + 64 * iq) * 4 + p_own;
-        if (PH < 2) {
-            if (mine_phase) carry0[ci] = ga;
-        } else if (PH == 2) {
-            if (l_own == 1) carry1[ci] = ga;
-        } else {  // last phase: the softmax term over all 16 samples, then every logit gradient
-            if (l_own == 0) ga = carry0[ci];
-            else if (l_own == 1) ga = carry1[ci];
-            const float delta = group_allreduce<16>(a * ga);
-            if (act) {
-                const float gl = a * (ga - delta);
-                gprow[logit_base + m * kNS + sub] = gl;
-                if (gp16) gp16[row * proj_stride + logit_base + m * kNS + sub] = (uint16_t)bf16_bits(gl);
-            }
-        }
-    };
-
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    using I3 = std::integral_constant<int, 3>;
-    using I4 = std::integral_constant<int, 4>;
-    pyr_stage_g(lds4, vsrc, MD, lv.start[0], kWinRows);  // window A (+ zero rows 0 and 514)
-    __syncthreads();
-#pragma unroll 1
-    for (int i = 0; i < kBqQPS; ++i) run_query(i, I0{}, I1{}, I0{});
-    __syncthreads();
-    pyr_stage_g(lds4, vsrc, MD, lv.start[0] + kWinSplit, lv.T[0] - kWinSplit);  // window B
-    __syncthreads();
-#pragma unroll 1
-    for (int i = 0; i < kBqQPS; ++i) run_query(i, I0{}, I1{}, I1{});
-    __syncthreads();
-    pyr_stage_g(lds4, vsrc, MD, lv.start[1], lv.T[1]);
-    __syncthreads();
-#pragma unroll 1
-    for (int i = 0; i < kBqQPS; ++i) run_query(i, I1{}, I2{}, I2{});
-    __syncthreads();
-    pyr_stage_g(lds4, vsrc, MD, lv.start[2], lv.T[2] + lv.T[3]);
-    __syncthreads();
-#pragma unroll 1
-    for (int i = 0; i < kBqQPS; ++i) run_query(i, I2{}, I4{}, I3{});
-}
-
-// -------------------------------------------------------------------------------------------------
 // backward, value side: destination-centric sum over an inverted index, no float atomics.
 // One workgroup per (video, head, level) and chunk of queries.  Row t of the level receives
 //     grad_value[t] = sum_{x0(s) = t} hw_s a_s g_q(s)  +  sum_{x0(s) = t-1} lw_s a_s g_q(s)
@@ -2651,24 +2474,6 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
         }
 #undef BQ_LAUNCH
         PDVC_CHECK_LAUNCH("msda1d_bwd_query_pyr_kernel");
-    } else if (tw > 0 && bwdq_mode() == 1 && win_ok(lv, num_query, S, head_dim)) {  // level 0 in two row windows
-        static std::atomic<int> done[kMaxDevices];
-        if ((rc = lds_optin(done, {{(const void*)msda1d_bwd_query_win_kernel<1>, (int)kBqWinLds},
-                                   {(const void*)msda1d_bwd_query_win_kernel<2>, (int)kBqWinLds}},
-                            "msda1d_bwd_query_win_kernel")))
-            return rc;
-        const int qb = (num_query + kBqQ - 1) / kBqQ;
-        PDVC_CHECK_ARG((long)batch * num_heads * qb < (1L << 31), "too many query blocks");
-        dim3 pg((unsigned)(batch * num_heads * qb));
-        if (ref_dim == 1)
-            hipLaunchKernelGGL((msda1d_bwd_query_win_kernel<1>), pg, dim3(kPyrThreads), kBqWinLds, s, value,
-                               value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv, num_query, S,
-                               num_heads, qb, grad_output, save_attn, save_loc, grad_proj, grad_ref, gp16);
-        else
-            hipLaunchKernelGGL((msda1d_bwd_query_win_kernel<2>), pg, dim3(kPyrThreads), kBqWinLds, s, value,
-                               value_pad_mask, proj, proj_stride, off_base, logit_base, ref, lv, num_query, S,
-                               num_heads, qb, grad_output, save_attn, save_loc, grad_proj, grad_ref, gp16);
-        PDVC_CHECK_LAUNCH("msda1d_bwd_query_win_kernel");
     } else if (tw > 0 && head_dim == 64 && bwdq_mode() != 0 && (long)S * num_heads * head_dim * 4 < (1L << 31)) {
         dim3 grid((unsigned)((tw + 3) / 4));
         if (ref_dim == 1)

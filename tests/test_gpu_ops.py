@@ -501,10 +501,10 @@ def _away_from_cell_edges(proj, ref, T_l, M, margin=2e-3):
                                            ((700, 512, 256, 200), 1, 8),
                                            ((512, 300, 150, 60), 1, 2), ((512, 300, 150, 60), 2, 2)])
 def test_fused_msda1d_long_pyramids_vs_oracle(T_l, ref_dim, M):
-    """Long pyramids: anet_c3d's T = 1024 (S = 1920: level 0 past one LDS staging phase, so the forward and the
-    backward-query run the windowed pyramid kernels -- level 0 in two row windows, msda1d_fwd_win_kernel and
-    msda1d_bwd_query_win_kernel, two query blocks; the value gradient takes two query chunks, the second accumulating
-    into the rows the first wrote), a level 0 of 700 rows (second window shorter than the first), and S = 1022 (both pyramid kernels with
+    """Long pyramids: anet_c3d's T = 1024 (S = 1920: level 0 past one LDS staging phase, so the forward runs the
+    windowed pyramid kernel -- level 0 in two row windows, msda1d_fwd_win_kernel -- and the backward-query the
+    dot-product kernel at Lq = S; the value gradient takes two query chunks, the second accumulating into the rows the
+    first wrote), a level 0 of 700 rows (second window shorter than the first), and S = 1022 (both pyramid kernels with
     two query blocks).  M = 8 is the headline's head count."""
     from pdvc.ops.functions import MSDA1dFunction
     rng = np.random.RandomState(sum(T_l) + ref_dim + M)
