@@ -687,11 +687,16 @@ def main():
     # pyramid kernel): algorithmic bytes per launch / avg launch time; the decoder's launches (Q = 100 queries,
     # msda1d_fwd_buf_kernel) beside it.  `roofline` is the dominant work, the GEMMs against the MFMA peak
     enc, dec = msda_split("pdvc_msda1d_forward_f32", "fwd")
+    # the encoder's kernels at this pyramid (msda1d.hip's dispatch: whole-pyramid staging while level 0 fits one
+    # 512-row phase, two row windows of level 0 up to 1024 rows)
+    T0 = a.T
+    fwd_k, bwdq_k = (("msda1d_fwd_pyr2", "msda1d_bwd_query_pyr") if T0 <= 512 else
+                     ("msda1d_fwd_win", "msda1d_bwd_query_dot"))
     if enc is not None:
-        # PMC passes of the same workload (tools/r03g.sh -> tools/pmc_traffic.py): HBM bytes per launch
-        traffic, tsrc = pmc_bytes("msda1d_fwd_pyr", a.workload)
+        # PMC passes of the same workload (tools/pmc_workload.sh -> tools/pmc_traffic.py): HBM bytes per launch
+        traffic, tsrc = pmc_bytes(fwd_k if T0 > 512 else "msda1d_fwd_pyr", a.workload)
         result["roofline_gather"] = dict(
-            {"kernel": "msda1d_fwd_pyr_kernel (fused MSDeformAttn forward, encoder self-attention, Lq = S)",
+            {"kernel": f"{fwd_k}_kernel (fused MSDeformAttn forward, encoder self-attention, Lq = S)",
              "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": traffic, "traffic_source": tsrc,
              "timing": timing_note}, **enc)
         if dec is not None:
@@ -700,10 +705,10 @@ def main():
                                                          "Lq = Q)", "traffic": dt_, "traffic_source": ds_}, **dec)
     enc, dec = msda_split("pdvc_msda1d_backward_ex_f32", "bwd")  # query-side + value-side kernels per launch
     if enc is not None:
-        tq, sq = pmc_bytes("msda1d_bwd_query_pyr", a.workload)
+        tq, sq = pmc_bytes(bwdq_k, a.workload)
         tv, sv = pmc_bytes("msda1d_bwd_value_enc", a.workload)
         result["roofline_gather_bwd"] = dict(
-            {"kernel": "msda1d_bwd_query_pyr_kernel + msda1d_bwd_value_kernel (fused MSDeformAttn backward, encoder "
+            {"kernel": f"{bwdq_k}_kernel + msda1d_bwd_value_kernel (fused MSDeformAttn backward, encoder "
                        "self-attention)", "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "traffic": (tq + tv) if (tq is not None and tv is not None) else None,
              "traffic_source": [sq, sv] if sq else None, "timing": timing_note}, **enc)

@@ -16,7 +16,9 @@ for k in msda1d_fwd msda1d_bwd Cijk_; do
 done
 python tools/pmc_traffic.py "$O/msda1d_fwd" msda1d_fwd_pyr "$O/msda1d_fwd_pyr_traffic_$WL.json" | tail -2
 python tools/pmc_traffic.py "$O/msda1d_fwd" msda1d_fwd_buf "$O/msda1d_fwd_buf_traffic_$WL.json" | tail -2
+python tools/pmc_traffic.py "$O/msda1d_fwd" msda1d_fwd_win "$O/msda1d_fwd_win_traffic_$WL.json" | tail -2
 python tools/pmc_traffic.py "$O/msda1d_bwd" msda1d_bwd_query_pyr "$O/msda1d_bwd_query_pyr_traffic_$WL.json" | tail -2
+python tools/pmc_traffic.py "$O/msda1d_bwd" msda1d_bwd_query_dot "$O/msda1d_bwd_query_dot_traffic_$WL.json" --largest-grid | tail -2
 python tools/pmc_traffic.py "$O/msda1d_bwd" msda1d_bwd_value "$O/msda1d_bwd_value_enc_traffic_$WL.json" --large-launches | tail -2
 python tools/pmc_gemm.py "$O/Cijk_" 3 "$O/gemm_traffic_$WL.json" | tail -3
 echo "[$(date +%T)] done"
