@@ -12,3 +12,6 @@ python -c "import json; d=json.load(open('$O/bench_anet_c3d.json')); print(d['va
 echo "[$(date +%T)] anet_c3d bench under rocprofv3"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o c3d -- python -u bench.py --workload anet_c3d --steps 5 --warmup 2 --no-cpu-baseline --no-dropin > $O/prof_bench.json 2> $O/prof_bench.err || { tail -20 $O/prof_bench.err; exit 1; }
 f=$(find $O/prof -name "*kernel_stats.csv" | head -1); python tools/profsum.py $f 0 30 > $O/prof_summary.txt; head -40 $O/prof_summary.txt
+echo "[$(date +%T)] ragged stream under rocprofv3"
+timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d $O/prof_rag -o rag -- python -u bench.py --stream ragged --steps 6 --warmup 2 --no-cpu-baseline --no-dropin --no-gemm-roofline > $O/prof_rag.json 2> $O/prof_rag.err || { tail -20 $O/prof_rag.err; exit 1; }
+kt=$(find $O/prof_rag -name "*kernel_trace.csv" | head -1); python tools/profsteps.py "$kt" 45 > $O/prof_rag_steps.txt; head -30 $O/prof_rag_steps.txt
