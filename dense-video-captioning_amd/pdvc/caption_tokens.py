@@ -46,6 +46,29 @@ def pack_tokens(valid, capacity):
     return index, scatter
 
 
+class _PackRows(torch.autograd.Function):
+    """x (N, H) -> x[index] (capacity, H); backward: the rows written back with index_copy through `scatter` (every
+    live position once, the padding into a dump row) -- no float atomics (index_select's backward is an atomic
+    index_add_)."""
+
+    @staticmethod
+    def forward(ctx, x, index, scatter):
+        ctx.save_for_backward(scatter)
+        ctx.n = x.shape[0]
+        return x.index_select(0, index)
+
+    @staticmethod
+    def backward(ctx, g):
+        (scatter,) = ctx.saved_tensors
+        gx = g.new_zeros((ctx.n + 1, g.shape[1])).index_copy_(0, scatter, g)[:ctx.n]
+        return gx, None, None
+
+
+def pack_rows(x, tokens):
+    """The packed token rows of x (N, H), N = rows * steps flattened row-major (pack_tokens' positions)."""
+    return _PackRows.apply(x, tokens[0], tokens[1])
+
+
 class DeferredLogprobs:
     """log_softmax(logit(Hd)) of a (rows, steps) selection, formed when first read.  Hd (R, n, H) are the hidden
     states after the caption dropout of the forward that made them; weight / bias a copy of the logit layer's
