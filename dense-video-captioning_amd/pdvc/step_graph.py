@@ -28,6 +28,7 @@ gradient accumulation then joins the default stream ended in a crash at capture 
 """
 import ctypes
 import os
+import threading
 
 import torch
 
@@ -71,33 +72,53 @@ def graph_node_counts(graph):
 
 
 class _RewritingGraph(torch.cuda.CUDAGraph):
-    """A CUDAGraph that keeps its hipGraph_t, rewrites its memset nodes and instantiates at capture end."""
+    """A CUDAGraph that keeps its hipGraph_t, rewrites its memset nodes and instantiates at capture end (unless the
+    caller asked for keep_graph itself, in which case it instantiates when it chooses, as torch's class does)."""
 
     def __new__(cls, keep_graph=False):
         return super().__new__(cls, True)
 
     def __init__(self, keep_graph=False):  # the native object is built by __init__: keep the hipGraph_t
         super().__init__(True)
+        self._caller_keeps = bool(keep_graph)
 
     def capture_end(self):
         super().capture_end()
         replace_memsets(self)
-        self.instantiate()
+        if not self._caller_keeps:
+            self.instantiate()
+
+
+_REWRITE_LOCK = threading.RLock()
+_REWRITE_DEPTH = [0]
+_REWRITE_SAVED = [None]
 
 
 class rewriting_graphs:
     """Within this context, graphs torch creates itself (torch.cuda.make_graphed_callables: the trunk graph,
-    PDVC.enable_graph) rewrite their memset nodes as StepGraph does."""
+    PDVC.enable_graph) rewrite their memset nodes as StepGraph does.  The patch is process-wide (make_graphed_callables
+    looks up torch.cuda.CUDAGraph), so the context holds a lock: another thread that enters it waits, and a thread that
+    builds a CUDAGraph outside it while it is active would also get the rewriting class -- do not capture graphs from
+    other threads meanwhile.  Re-entrant: a nested use keeps the patch and the outermost exit restores torch's class."""
 
     def __enter__(self):
         import torch.cuda.graphs as tg
-        self._saved = (torch.cuda.CUDAGraph, tg.CUDAGraph)
-        torch.cuda.CUDAGraph = tg.CUDAGraph = _RewritingGraph  # make_graphed_callables looks up torch.cuda.CUDAGraph
+        _REWRITE_LOCK.acquire()
+        if _REWRITE_DEPTH[0] == 0:
+            _REWRITE_SAVED[0] = (torch.cuda.CUDAGraph, tg.CUDAGraph)
+            torch.cuda.CUDAGraph = tg.CUDAGraph = _RewritingGraph
+        _REWRITE_DEPTH[0] += 1
         return self
 
     def __exit__(self, *exc):
         import torch.cuda.graphs as tg
-        torch.cuda.CUDAGraph, tg.CUDAGraph = self._saved
+        try:
+            _REWRITE_DEPTH[0] -= 1
+            if _REWRITE_DEPTH[0] == 0:
+                torch.cuda.CUDAGraph, tg.CUDAGraph = _REWRITE_SAVED[0]
+                _REWRITE_SAVED[0] = None
+        finally:
+            _REWRITE_LOCK.release()
         return False
 
 
