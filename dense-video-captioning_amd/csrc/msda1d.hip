@@ -2532,6 +2532,11 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
             const int nq = (num_query - q0) < qchunk ? (num_query - q0) : qchunk;
             size_t lds = sizeof(int) * (2 * (size_t)(Tmax + 2) + 3 * (size_t)nq * kP + 2);
             if (g4 && level_sums && lds < kVW * 16 * 16) lds = kVW * 16 * 16;  // the level-sum reduction
+            static const size_t lds_floor = [] {  // measurement only: PDVC_VAL_LDS_KIB caps the workgroups per CU
+                const char* e = getenv("PDVC_VAL_LDS_KIB");
+                return e ? (size_t)atoi(e) * 1024 : (size_t)0;
+            }();
+            if (lds < lds_floor && lds_floor <= 96 * 1024) lds = lds_floor;
             float* gsums = g4 ? level_sums : nullptr;
             const int acc = q0 > 0;
 #define VAL_LAUNCH(UGV, B16V)                                                                                       \
