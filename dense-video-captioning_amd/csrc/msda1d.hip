@@ -2454,10 +2454,10 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
         if ((rc = bwdq_pyr_attrs())) return rc;
         PDVC_CHECK_ARG((long)batch * num_heads * bq_blocks < (1L << 31), "too many query blocks");
         dim3 pg((unsigned)(batch * num_heads * bq_blocks));
-        static const int qu = [] {  // queries per loop trip (PDVC_BQ_QU = 1 | 3 | 5: A/B)
-            const char* e = getenv("PDVC_BQ_QU");
-            const int v = e ? atoi(e) : 1;
-            return (v == 3 || v == 5) ? v : 1;
+        static const int qu = [] {  // queries per loop trip (PDVC_BQ_QU = 1 | 3 | 5: A/B); 3: encoder backward
+            const char* e = getenv("PDVC_BQ_QU");  // 4 605 -> 4 500 us at 1024 videos (profiles/r04_bwdq_qu_ab.txt)
+            const int v = e ? atoi(e) : 3;
+            return (v == 1 || v == 5) ? v : 3;
         }();
 #define BQ_LAUNCH(R, Q)                                                                                           \
     hipLaunchKernelGGL((msda1d_bwd_query_pyr_kernel<R, Q>), pg, dim3(kPyrThreads), kBqLds, s, value, value_pad_mask, \
@@ -2532,11 +2532,6 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
             const int nq = (num_query - q0) < qchunk ? (num_query - q0) : qchunk;
             size_t lds = sizeof(int) * (2 * (size_t)(Tmax + 2) + 3 * (size_t)nq * kP + 2);
             if (g4 && level_sums && lds < kVW * 16 * 16) lds = kVW * 16 * 16;  // the level-sum reduction
-            static const size_t lds_floor = [] {  // measurement only: PDVC_VAL_LDS_KIB caps the workgroups per CU
-                const char* e = getenv("PDVC_VAL_LDS_KIB");
-                return e ? (size_t)atoi(e) * 1024 : (size_t)0;
-            }();
-            if (lds < lds_floor && lds_floor <= 96 * 1024) lds = lds_floor;
             float* gsums = g4 ? level_sums : nullptr;
             const int acc = q0 > 0;
 #define VAL_LAUNCH(UGV, B16V)                                                                                       \
