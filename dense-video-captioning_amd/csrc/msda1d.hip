@@ -1375,7 +1375,7 @@ constexpr int kVQPT = 4;  // queries per thread in its sort passes: a launch chu
 // ABL (measurement only, PDVC_VAL_ABLATE): 1 = stop after the sort, 2 = walk without the gradient-row gathers
 // (PDVC_VAL_ABLATE=1/2 select them for the depth-8 encoder walk, 3/4 for the depth-4 decoder walk)
 template <int CW, bool G4, int UG = 8, bool B16 = false, int ABL = 0>
-__global__ __launch_bounds__(kVW * 64, UG >= 16 ? 4 : 6) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
+__global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
                                                                      int Lq, int q0, int nq, int S, int M, int D,
                                                                      int accumulate,
                                                                      const float* __restrict__ gout,
@@ -2175,7 +2175,7 @@ static int value_ug(int num_query, int S) {
         const char* e = getenv("PDVC_VALUE_UG");
         return e ? atoi(e) : 0;
     }();
-    if (forced == 4 || forced == 8 || forced == 16) return forced;
+    if (forced == 4 || forced == 8) return forced;
     return 4L * num_query < S ? 4 : 8;
 }
 
@@ -2525,8 +2525,7 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
                                    {(const void*)msda1d_bwd_value_kernel<2, false>, 96 * 1024},
                                    {(const void*)msda1d_bwd_value_kernel<1, true>, 96 * 1024},
                                    {(const void*)msda1d_bwd_value_kernel<1, true, 4>, 96 * 1024},
-                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, true>, 96 * 1024},
-                                   {(const void*)msda1d_bwd_value_kernel<1, true, 16>, 96 * 1024}},
+                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, true>, 96 * 1024}},
                             "msda1d_bwd_value_kernel")))
             return rc;
         for (int q0 = 0; q0 < num_query; q0 += qchunk) {
@@ -2573,7 +2572,6 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
                                        (const int64_t*)nullptr, (const int64_t*)nullptr, gv16);
             } else if (g4 && gv16) VAL_LAUNCH(4, true);  // the bf16 stores spill the depth-8 walk (7 VGPRs): depth 4
             else if (g4 && value_ug(num_query, S) == 4) VAL_LAUNCH(4, false);
-            else if (g4 && value_ug(num_query, S) == 16) VAL_LAUNCH(16, false);  // measurement: PDVC_VALUE_UG=16
             else if (g4) VAL_LAUNCH(8, false);
 #undef VAL_LAUNCH
             else if (head_dim <= 64)
