@@ -733,7 +733,8 @@ def main():
     if groof is not None:  # the dominant kernels (~70% of the step's device time): `roofline` proper
         groof["share_of_step"] = groof["gemm_device_ms_per_step"] / (1e3 * el / a.steps)
         gfile = latest_profile(f"gemm_traffic_{a.workload}.json")
-        if gfile and B == 1024:  # PMC passes of an eager step at 1024 videos (tools/r03g.sh -> tools/pmc_gemm.py)
+        if gfile and B == WORKLOADS[a.workload].get("videos_per_gpu", 1024):  # PMC passes of an eager step at the
+            # workload's default batch (tools/pmc_workload.sh -> tools/pmc_gemm.py)
             with open(gfile) as f:
                 g = json.load(f)
             groof["traffic"] = g.get("bytes_per_step")
