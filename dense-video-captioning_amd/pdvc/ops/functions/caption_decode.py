@@ -15,12 +15,14 @@ gate gradients (no transposing copy).  Autograd of the stock modules issues ~25 
 backward; here it is 6 launches per step each way, and every weight gradient is ONE GEMM over all steps
 after the backward loop (the per-step activations are kept: ~0.5 MB per row per step at PDVC's shape).
 """
+import os
+
 import torch
 from torch.autograd import Function
 from torch.autograd.function import once_differentiable
 
 from pdvc import _native as _n
-from pdvc.precision import fp32_gemms
+from pdvc.precision import bf16_active, fp32_gemms
 from .linear import colsum, tag_level_sums, wgrad_mm
 from .ms_deform_attn_func import NUM_SAMPLES, _levels
 
@@ -29,6 +31,25 @@ from .ms_deform_attn_func import NUM_SAMPLES, _levels
 CTX2ATT_GATHER = True
 U_GRAD = True  # the backward in the same form (see forward); False: dW_ctx and dclip from CLIP and dATT per sample
 U_MAX_BYTES = 16 << 30  # largest projected-rows buffer of the gather form (bound its memory)
+# In the bf16 mode (pdvc/precision.py) the recurrence's per-step GEMMs also run on bf16 operands with fp32 accumulation
+# and fp32 results (round 4; PDVC_BF16_RECURRENCE=0 keeps them fp32, the earlier policy).  The step's inputs are
+# rounded freshly each step (they are written by the HIP kernels, which the mode's per-tensor rounding cache cannot
+# see) and the weights once per pass.
+BF16_RECURRENCE = os.environ.get("PDVC_BF16_RECURRENCE", "1") != "0"
+_BF16 = torch.bfloat16
+
+
+def _gemm(inp, a, b, out, b16):
+    """out = inp + a @ b (inp None: a @ b), fp32 out; b16: a rounded to bf16 here, b already bf16."""
+    if b16 is None:
+        if inp is None:
+            torch.mm(a, b, out=out)
+        else:
+            torch.addmm(inp, a, b, out=out)
+    elif inp is None:
+        torch.ops.aten.mm.dtype_out(a.to(_BF16), b16, torch.float32, out=out)
+    else:
+        torch.ops.aten.addmm.dtype_out(inp, a.to(_BF16), b16, torch.float32, out=out)
 
 
 class CaptionDecodeFunction(Function):
@@ -103,7 +124,12 @@ class CaptionDecodeFunction(Function):
         if ranged and not ctx.u_grad:  # dW_ctx reads CLIP and dATT over every (step, row): no stale entries
             CLIP.zero_()
         ns_ = M * NS
-        with fp32_gemms():  # the recurrence stays fp32 in the bf16 mode (pdvc/precision.py)
+        b16 = BF16_RECURRENCE and bf16_active()
+        ctx.b16 = b16
+        Wh16 = W_h.t().to(_BF16) if b16 else None
+        Wctx16 = W_ctx.t().to(_BF16) if b16 else None
+        Watt16 = W_att.t().to(_BF16) if b16 else None
+        with fp32_gemms():  # the per-step GEMMs are routed here (_gemm), not by the mode
             for i in range(n):
                 s0, c = ranges[i]
                 if c == 0:
@@ -114,7 +140,7 @@ class CaptionDecodeFunction(Function):
                 if i == 0:
                     hp.copy_(b_h.expand(c, Ph))  # h_{-1} = 0
                 else:
-                    torch.addmm(b_h, HS[rs, i - 1], W_h.t(), out=hp)
+                    _gemm(b_h, HS[rs, i - 1], W_h.t(), hp, Wh16)
                 _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video[rs]),
                         _n.ptr(hp), Ph, 0, _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, D,
                         NS // nl, _n.ptr(CLIP[i][rs]), _n.ptr(LOC[i][rs]), st)
@@ -124,11 +150,11 @@ class CaptionDecodeFunction(Function):
                             _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, A, NS // nl,
                             _n.ptr(att), None, st)
                 else:
-                    torch.addmm(b_ctx, CLIP[i][rs].reshape(-1, D), W_ctx.t(), out=att)
+                    _gemm(b_ctx, CLIP[i][rs].reshape(-1, D), W_ctx.t(), att, Wctx16)
                 ah, ldh = _n.rows(hp[:, n_off:n_off + A])
                 _n.call("pdvc_softattn_forward_f32", _n.ptr(att), ah, ldh, _n.ptr(alpha_w), _n.ptr(alpha_b),
                         _n.ptr(CLIP[i][rs]), c, M, A, D, _n.ptr(RES[i][rs]), _n.ptr(PROBS[i][rs]), st)
-                torch.mm(RES[i][rs], W_att.t(), out=GATT[:c])
+                _gemm(None, RES[i][rs], W_att.t(), GATT[:c], Watt16)
                 xa, ldx = _n.rows(xe[i][rs])
                 gh, ldg = _n.rows(hp[:, n_off + A:])
                 ho, ldo = _n.rows(HS[rs, i])
@@ -177,7 +203,11 @@ class CaptionDecodeFunction(Function):
         gr = torch.zeros_like(ref) if ctx.needs_input_grad[3] else None
         st = _n.stream()
         ns_ = M * NS
-        with fp32_gemms():  # the recurrence stays fp32 in the bf16 mode
+        b16 = getattr(ctx, "b16", False)
+        Watt16 = W_att.to(_BF16) if b16 else None
+        Wh16 = W_h.to(_BF16) if b16 else None
+        Wctx16 = W_ctx.to(_BF16) if b16 else None
+        with fp32_gemms():  # the per-step GEMMs are routed here (_gemm), not by the mode
             for i in reversed(range(n)):
                 s0, c = ranges[i]
                 rs = slice(s0, s0 + c)
@@ -192,7 +222,7 @@ class CaptionDecodeFunction(Function):
                             None if last else _n.ptr(dc[(i + 1) % 2][rs]), _n.ptr(ACTS[i][rs]),
                             _n.ptr(CS[i - 1][rs] if i > 0 else zero), _n.ptr(CS[i][rs]), c, H, dg, lddg,
                             _n.ptr(dc[i % 2][rs]), st)
-                    torch.mm(dhp[:, n_off + A:], W_att, out=dRES[:c])
+                    _gemm(None, dhp[:, n_off + A:], W_att, dRES[:c], Watt16)
                     ah, ldh = _n.rows(HP[i][rs][:, n_off:n_off + A])
                     gah, ldgah = _n.rows(dhp[:, n_off:n_off + A])
                     att = ATT[i][s0 * ns_:(s0 + c) * ns_]
@@ -207,7 +237,11 @@ class CaptionDecodeFunction(Function):
                                 RD, rd1, lvl, nl, Nv, c, M, D, NS // nl, _n.ptr(LOC[i][rs]), _n.ptr(dCLIP), None,
                                 _n.ptr(dhp), _n.ptr(gr_), _n.ptr(U), _n.ptr(datt), st)
                     else:
-                        dCLIP.reshape(-1, D).addmm_(datt, W_ctx)
+                        if b16:
+                            dc_ = dCLIP.reshape(-1, D)
+                            _gemm(dc_, datt, W_ctx, dc_, Wctx16)
+                        else:
+                            dCLIP.reshape(-1, D).addmm_(datt, W_ctx)
                         _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(pad_mask),
                                 _n.ptr(row_video[rs]), _n.ptr(HP[i][rs]), Ph, 0, _n.ptr(off_hs[rs]),
                                 _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, D, NS // nl, _n.ptr(LOC[i][rs]),
@@ -215,7 +249,7 @@ class CaptionDecodeFunction(Function):
                 if i > 0:  # dh of step i - 1's rows (rows that stopped at step i have dHP[i] = 0 there)
                     p0, pc = ranges[i - 1]
                     if pc > 0:
-                        torch.mm(dHP[i][p0:p0 + pc], W_h, out=dh[p0:p0 + pc])
+                        _gemm(None, dHP[i][p0:p0 + pc], W_h, dh[p0:p0 + pc], Wh16)
         lsums = None
         if deferred:
             vr_start, vr_rows, max_rows = video_csr
