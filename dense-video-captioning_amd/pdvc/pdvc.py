@@ -350,8 +350,9 @@ class PDVC(nn.Module):
                     n_dec = cap["words"] - 1 if cap is not None else max(vsteps, default=0)
                     live = tuple(cap["alive"]) if cap is not None else live_rows(gt_counts, vsteps, n_dec)
                     host = step_ranges(live, Ld, Lc["rows_per_layer"])
-                    Lc["step_ranges"] = (host, hostio.pack_to_device([[v for r in host for v in r]], dev)[0]
-                                         .to(torch.int32))
+                    if any(c < Ld * Lc["rows_per_layer"] for _, c in host):  # (every row at every step: no ranges)
+                        Lc["step_ranges"] = (host, hostio.pack_to_device([[v for r in host for v in r]], dev)[0]
+                                             .to(torch.int32))
                 dt[key] = Lc
             Lc = dt[key]
             rp, rk, rb, rc, row_video = Lc["p"], Lc["k"], Lc["base"], Lc["cap"], Lc["vid"]
