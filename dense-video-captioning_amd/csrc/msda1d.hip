@@ -2520,6 +2520,11 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
         int qchunk = (int)(budget / (per_sample * kP));
         if (qchunk > kVQPT * kVW * 64) qchunk = kVQPT * kVW * 64;
         if (qchunk > num_query) qchunk = num_query;
+        static const int forced_chunk = [] {  // measurement: PDVC_VAL_QCHUNK forces the query chunk
+            const char* e = getenv("PDVC_VAL_QCHUNK");
+            return e ? atoi(e) : 0;
+        }();
+        if (forced_chunk > 0 && forced_chunk < qchunk) qchunk = forced_chunk;
         static std::atomic<int> done[kMaxDevices];  // dynamic LDS <= 96 KiB by construction of qchunk (+32 B static)
         if ((rc = lds_optin(done, {{(const void*)msda1d_bwd_value_kernel<1, false>, 96 * 1024},
                                    {(const void*)msda1d_bwd_value_kernel<2, false>, 96 * 1024},
