@@ -715,7 +715,7 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_win_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
     int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
     int qblocks, float* __restrict__ out, float* __restrict__ save_attn, float* __restrict__ save_loc,
-    uint16_t* __restrict__ out16) {
+    uint16_t* __restrict__ out16, int abl = 0) {
     extern __shared__ __attribute__((aligned(16))) float4 lds4[];
     const int blk = xcd_remap(blockIdx.x, gridDim.x);  // the query blocks and heads of a video share an XCD
     const int qb = blk % qblocks, bm = blk / qblocks;
@@ -725,6 +725,7 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_win_kernel(
     const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
     const float* vsrc = value + (size_t)b * S * MD + (size_t)m * 64;
     const char* lrow = reinterpret_cast<const char*>(lds4) + sub * 16;
+    // abl (measurement only, PDVC_WIN_ABLATE): 1 = no staging after window A (the gathers read stale rows)
     pyr_zero_row(lds4, 0, 0);  // the leading guard row of every phase
     pyr_zero_row(lds4, kWinZero, 64);
     pyr_zero_row(lds4, kWinZero + 1, 128);
@@ -820,12 +821,14 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_win_kernel(
     level(std::integral_constant<int, 0>{}, F{});
     __syncthreads();  // every wave is done with window A
     const int nB = lv.T[0] - kWinSplit;
+    if (!abl)
     pyr_dma_rows(lds4, vsrc, MD, lv.start[0] + kWinSplit, 1, nB);
     pyr_zero_row(lds4, 1 + nB, 0);
     pyr_dma_wait();
     __syncthreads();
     level(std::integral_constant<int, 0>{}, Tt{});
     __syncthreads();
+    if (!abl)
     pyr_dma_rows(lds4, vsrc, MD, lv.start[1], 1, lv.T[1]);
     pyr_zero_row(lds4, 1 + lv.T[1], 0);
     pyr_dma_wait();
@@ -833,6 +836,7 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_win_kernel(
     level(std::integral_constant<int, 1>{}, F{});
     __syncthreads();
     const int n23 = lv.T[2] + lv.T[3];
+    if (!abl)
     pyr_dma_rows(lds4, vsrc, MD, lv.start[2], 1, n23);
     pyr_zero_row(lds4, 1 + n23, 0);
     pyr_dma_wait();
@@ -2349,14 +2353,18 @@ static int msda1d_forward_impl(const float* value, const uint8_t* value_pad_mask
         const int qb = (num_query + kPyrQ - 1) / kPyrQ;
         PDVC_CHECK_ARG((long)batch * num_heads * qb < (1L << 31), "too many query blocks");
         dim3 pg((unsigned)(batch * num_heads * qb));
+        static const int wabl = [] {
+            const char* e = getenv("PDVC_WIN_ABLATE");
+            return e ? atoi(e) : 0;
+        }();
         if (ref_dim == 1)
             hipLaunchKernelGGL((msda1d_fwd_win_kernel<1>), pg, dim3(kPyrThreads), kWinLds, s, value, value_pad_mask,
                                proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, qb, output,
-                               save_attn, save_loc, out16);
+                               save_attn, save_loc, out16, wabl);
         else
             hipLaunchKernelGGL((msda1d_fwd_win_kernel<2>), pg, dim3(kPyrThreads), kWinLds, s, value, value_pad_mask,
                                proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, qb, output,
-                               save_attn, save_loc, out16);
+                               save_attn, save_loc, out16, wabl);
         PDVC_CHECK_LAUNCH("msda1d_fwd_win_kernel");
         return PDVC_OK;
     }
