@@ -1186,7 +1186,13 @@ constexpr size_t kBqLds = kPyrLds + (size_t)kBqQ * 4 * sizeof(float);
 
 // QU: queries of a lane group run back to back per loop trip (interleavable by the scheduler: each query is a
 // dependent chain of LDS reads, a 16-lane reduction and the owner math, and the LDS caps the CU at 4 waves/SIMD)
-template <int RD, int QU = 1>
+// PF: each trip's global inputs (dOut row, sampling location, attention weight) are loaded during the previous trip,
+// before that trip's gradient stores, and the stores are unconditional buffer stores (inactive lanes get an
+// out-of-range offset, which the buffer range check drops).  vmcnt counts loads and stores together in issue order,
+// so inputs loaded after a trip's stores wait for those stores' write acknowledgements (hundreds to thousands of
+// cycles); loaded before them, the wait is an exact vmcnt(#stores) -- exact only while the stores are not under
+// branches, whose store-less path would make hipcc wait for everything.
+template <int RD, int QU = 1, bool PF = false>
 __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
     int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
@@ -1218,6 +1224,25 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
     // owner math of the lanes whose level is in range (offset gradient, grad_ref, dL/da).  The QU queries' loads, LDS
     // reads and reductions are independent chains written side by side, so they overlap (the carry / gradient
     // stores come last: they would otherwise order the next query's LDS reads behind them)
+    // PF: the inputs of queries i0q .. i0q + QU - 1 into pg / ploc / pat
+    float4 pg[QU];
+    float ploc[QU], pat[QU];
+    auto fetch = [&](int i0q) {
+#pragma unroll
+        for (int u = 0; u < QU; ++u) {
+            const int q0 = qb * kBqQ + slot + 64 * (i0q + u);
+            const int q = q0 < Lq ? q0 : Lq - 1;
+            pg[u] = *reinterpret_cast<const float4*>(gout + ((size_t)b * Lq + q) * MD + (size_t)m * 64 + sub * 4);
+            const size_t si = save_index(b, m, l_own, q, p_own, Lq, M);
+            ploc[u] = save_loc[si];
+            pat[u] = save_attn[si];
+        }
+    };
+    const int gp_bytes = Lq * proj_stride * 4;  // PF stores: one video's rows of grad_proj (gp16) per descriptor
+    const __amdgpu_buffer_rsrc_t gpr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(grad_proj + (size_t)b * Lq * proj_stride), (short)0, gp_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t gpr16 = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(gp16 ? gp16 + (size_t)b * Lq * proj_stride : nullptr), (short)0, gp16 ? gp_bytes / 2 : 0, 0x00020000);
     auto run_queries = [&](int i0q, auto L0c, auto L1c) {
         constexpr int L0 = decltype(L0c)::value, L1 = decltype(L1c)::value;
         bool act[QU], inside[QU];
@@ -1231,10 +1256,17 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
             act[u] = q0 < Lq;
             const int q = act[u] ? q0 : Lq - 1;
             row[u] = (size_t)b * Lq + q;
-            g[u] = *reinterpret_cast<const float4*>(gout + row[u] * MD + (size_t)m * 64 + sub * 4);
-            const size_t si = save_index(b, m, l_own, q, p_own, Lq, M);
-            const float x = save_loc[si] * Tf - 0.5f;
-            a[u] = save_attn[si];
+            float x;
+            if constexpr (PF) {
+                g[u] = pg[u];
+                x = ploc[u] * Tf - 0.5f;
+                a[u] = pat[u];
+            } else {
+                g[u] = *reinterpret_cast<const float4*>(gout + row[u] * MD + (size_t)m * 64 + sub * 4);
+                const size_t si = save_index(b, m, l_own, q, p_own, Lq, M);
+                x = save_loc[si] * Tf - 0.5f;
+                a[u] = save_attn[si];
+            }
             inside[u] = x > -1.f && x < Tf;
             const float xf = floorf(inside[u] ? x : 0.f);
             i0[u] = (int)xf;
@@ -1286,6 +1318,9 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
                 }
             }
         }
+        // PF: the next trip's inputs (the phase's first trip after its last: the second phase starts there, and its
+        // own last trip loads a spare copy) -- issued here, after every use of g and before this trip's stores
+        if constexpr (PF) fetch(i0q + QU < kBqQPS ? i0q + QU : 0);
         // owner math of the lanes whose sample is in this phase (.cuh:140-170), as msda1d_bwd_query_dot_kernel
         const bool mine_phase = l_own >= L0 && l_own < L1;
 #pragma unroll
@@ -1309,7 +1344,15 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
                 goff = (t2 * rr1) / (float)kP;
                 g1 = mine_phase ? t2 * (prow[off_base + m * kNS + sub] / (float)kP) : 0.f;
             }
-            if (act[u] && mine_phase) {
+            const int qrow = (int)(row[u] - (size_t)b * Lq);
+            if constexpr (PF) {
+                const int col = qrow * proj_stride + off_base + m * kNS + sub;
+                const bool st = act[u] && mine_phase;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(goff), gpr, st ? col * 4 : gp_bytes, 0, 0);
+                if (gp16)
+                    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bf16_bits(goff), gpr16,
+                                                          st ? col * 2 : gp_bytes, 0, 0);
+            } else if (act[u] && mine_phase) {
                 gprow[off_base + m * kNS + sub] = goff;
                 if (gp16) gp16[row[u] * proj_stride + off_base + m * kNS + sub] = (uint16_t)bf16_bits(goff);
             }
@@ -1332,8 +1375,14 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
             } else {  // second phase: the softmax term over all 16 samples, then every logit gradient
                 if (l_own == 0) ga = carry[ci];
                 const float delta = group_allreduce<16>(a[u] * ga);
-                if (act[u]) {
-                    const float gl = a[u] * (ga - delta);
+                const float gl = a[u] * (ga - delta);
+                if constexpr (PF) {
+                    const int col = qrow * proj_stride + logit_base + m * kNS + sub;
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gl), gpr, act[u] ? col * 4 : gp_bytes, 0, 0);
+                    if (gp16)
+                        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bf16_bits(gl), gpr16,
+                                                              act[u] ? col * 2 : gp_bytes, 0, 0);
+                } else if (act[u]) {
                     gprow[logit_base + m * kNS + sub] = gl;
                     if (gp16) gp16[row[u] * proj_stride + logit_base + m * kNS + sub] = (uint16_t)bf16_bits(gl);
                 }
@@ -1341,6 +1390,7 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
         }
     };
 
+    if constexpr (PF) fetch(0);
     pyr_stage_g(lds4, vsrc, MD, lv.start[0], lv.T[0]);
     __syncthreads();
     static_assert(kBqQPS % QU == 0, "QU must divide the queries per lane group");
@@ -1378,7 +1428,9 @@ constexpr int kVQPT = 4;  // queries per thread in its sort passes: a launch chu
 // fp32 path keeps its registers: the pointer and its stores cost the depth-8 walk 9 spilled VGPRs)
 // ABL (measurement only, PDVC_VAL_ABLATE): 1 = stop after the sort, 2 = walk without the gradient-row gathers
 // (PDVC_VAL_ABLATE=1/2 select them for the depth-8 encoder walk, 3/4 for the depth-4 decoder walk)
-template <int CW, bool G4, int UG = 8, bool B16 = false, int ABL = 0>
+// DEF: finished rows held back in registers (up to DEF of them) and stored at the top of the walk's next trip, ahead of
+// that trip's gathers (see the walk)
+template <int CW, bool G4, int UG = 8, bool B16 = false, int ABL = 0, int DEF = 0>
 __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
                                                                      int Lq, int q0, int nq, int S, int M, int D,
                                                                      int accumulate,
@@ -1520,6 +1572,15 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
         if (threadIdx.x == 0) grad_value[(size_t)blockIdx.x] = (float)off[T + 1] + __uint_as_float(eqk[0]);
         return;
     }
+    // G4: the level's pad mask as ints in the scatter cursors' place (dead now), so that the walk reads it from LDS --
+    // a global byte load there waits for every gather and store the wave has outstanding (vmcnt(0))
+    const int* mk = cur;
+    if constexpr (G4) {
+        if (vmask) {
+            for (int t = threadIdx.x; t < T; t += blockDim.x) cur[t] = vmask[(size_t)b * S + st + t];
+            __syncthreads();
+        }
+    }
     // 4) row ranges: split points balance the sorted samples over the waves (or 16-lane groups)
     const int total = off[T + 1];
     constexpr int kParts = G4 ? kVW * 4 : kVW;
@@ -1556,28 +1617,67 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
                 (void*)(gout + (size_t)b * Lq * MD), (short)0, (int)((size_t)Lq * MD * 4), 0x00020000);
             const int coff = (m * D + gl * 4) * 4, rowb = (int)MD * 4;
             const unsigned MDu = (unsigned)MD;  // < 2^24: the row offset is one v_mul_u32_u24 (a 64-bit one cost ~6 VALU)
+            auto emit = [&](int r, float4 v) {
+                *reinterpret_cast<float4*>(ob + __umul24((unsigned)r, MDu)) = v;
+                if (B16) store_bf16x4(ob16 + (size_t)r * MD, v.x, v.y, v.z, v.w);
+            };
+            // DEF > 0: vmcnt counts loads and stores together, in issue order, and a store holds its address and data
+            // VGPRs until it completes (hipcc waits vmcnt before reusing them), so a row stored among a trip's gathers
+            // makes the trip wait for that store's write acknowledgement (MI355X_MICROARCH.md: ~600-3000 cycles with
+            // every CU writing).  Up to DEF finished rows wait in loop-carried registers instead -- data and buffer
+            // offset both, rewritten only by a later put, well after the store -- and are stored at the top of the next
+            // trip, before its gathers, whose latency then covers the acknowledgement.  (A third row finished in one
+            // trip is stored at once.)
+            const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(grad_value + ((size_t)b * S + st) * MD), (short)0, (int)((size_t)T * MD * 4), 0x00020000);
+            using u4 = unsigned int __attribute__((ext_vector_type(4)));
+            u4 dw0 = u4{0u, 0u, 0u, 0u}, dw1 = dw0;
+            int do0 = 0, do1 = 0;        // buffer offsets of the held rows
+            bool ok0 = false, ok1 = false;  // rows held
+            auto flush = [&]() {
+                if constexpr (DEF > 0) {
+                    if (ok0) __builtin_amdgcn_raw_buffer_store_b128(dw0, orsrc, do0, 0, 0);
+                    if (DEF > 1 && ok1) __builtin_amdgcn_raw_buffer_store_b128(dw1, orsrc, do1, 0, 0);
+                    ok0 = false;
+                    ok1 = false;
+                }
+            };
             auto put = [&](int r, float4 v) {
                 if (r >= r0 && r < r1) {
-                    float4* orow = reinterpret_cast<float4*>(ob + __umul24((unsigned)r, MDu));
-                    if (mrow && mrow[r]) v = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (mrow && mk[r]) v = make_float4(0.f, 0.f, 0.f, 0.f);
                     psum.x += v.x;
                     psum.y += v.y;
                     psum.z += v.z;
                     psum.w += v.w;
                     if (accumulate) {
-                        const float4 o = *orow;
+                        const float4 o = *reinterpret_cast<const float4*>(ob + __umul24((unsigned)r, MDu));
                         v.x += o.x;
                         v.y += o.y;
                         v.z += o.z;
                         v.w += o.w;
                     }
-                    *orow = v;
-                    if (B16) store_bf16x4(ob16 + (size_t)r * MD, v.x, v.y, v.z, v.w);
+                    if constexpr (DEF == 0) {
+                        emit(r, v);
+                    } else {  // vector selects (a branch assigning float4 structs put them on the stack)
+                        const bool to0 = !ok0, to1 = DEF > 1 && ok0 && !ok1;
+                        const u4 vb = __builtin_bit_cast(u4, v);
+                        const int o = (int)__umul24((unsigned)r, (unsigned)rowb) + coff;
+                        dw0 = to0 ? vb : dw0;
+                        do0 = to0 ? o : do0;
+                        ok0 = true;
+                        if (DEF > 1) {
+                            dw1 = to1 ? vb : dw1;
+                            do1 = to1 ? o : do1;
+                            ok1 = ok1 || to1;
+                        }
+                        if (!to0 && !to1) emit(r, v);
+                    }
                 }
             };
             int k = (int)(eqk[jb] >> 16);
             PAcc4 alo = pacc_zero(), ahi = pacc_zero();  // rows k - 1 and k
             for (int j0 = jb; j0 < je; j0 += UG) {
+                flush();
                 uint32_t e[UG];
                 pf4 gv[UG];
 #pragma unroll
@@ -1611,9 +1711,14 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
                     pacc_fma(alo, wgt.x, gv[u]);
                     pacc_fma(ahi, wgt.y, gv[u]);
                 }
+                // DEF: drain here, where every gather of the trip has been waited for anyway (a last trip's unused
+                // gathers aside) -- otherwise hipcc waits at the next trip's first register reuse, right after that
+                // trip's held-row stores, for those stores too.  s_waitcnt vmcnt(0): gfx9 simm16, expcnt/lgkmcnt max
+                if constexpr (DEF > 0) __builtin_amdgcn_s_waitcnt(0x0F70);
             }
             put(k - 1, pacc_f4(alo));
             put(k, pacc_f4(ahi));
+            flush();
         }
         if (level_sums) {  // the bias gradient's partial: column sums of the rows this workgroup wrote
 #pragma unroll
@@ -2179,8 +2284,17 @@ static int value_ug(int num_query, int S) {
         const char* e = getenv("PDVC_VALUE_UG");
         return e ? atoi(e) : 0;
     }();
-    if (forced == 4 || forced == 8) return forced;
+    if (forced == 4 || forced == 6 || forced == 8) return forced;
     return 4L * num_query < S ? 4 : 8;
+}
+
+// rows the value walk holds back before storing them (msda1d_bwd_value_kernel's DEF; PDVC_VAL_DEFER=0/1/2)
+static int value_defer() {
+    static const int d = [] {
+        const char* e = getenv("PDVC_VAL_DEFER");
+        return e ? atoi(e) : 0;
+    }();
+    return d;
 }
 
 // 16-lane-group gather for the value gradient at D = 64 (PDVC_MSDA_G4=0 selects the wave-per-range form)
@@ -2211,7 +2325,9 @@ static int bwdq_pyr_attrs() {
                             {(const void*)msda1d_bwd_query_pyr_kernel<1, 3>, b},
                             {(const void*)msda1d_bwd_query_pyr_kernel<2, 3>, b},
                             {(const void*)msda1d_bwd_query_pyr_kernel<1, 5>, b},
-                            {(const void*)msda1d_bwd_query_pyr_kernel<2, 5>, b}},
+                            {(const void*)msda1d_bwd_query_pyr_kernel<2, 5>, b},
+                            {(const void*)msda1d_bwd_query_pyr_kernel<1, 3, true>, b},
+                            {(const void*)msda1d_bwd_query_pyr_kernel<2, 3, true>, b}},
                      "msda1d_bwd_query_pyr_kernel");
 }
 
@@ -2467,11 +2583,18 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
             const int v = e ? atoi(e) : 3;
             return (v == 1 || v == 5) ? v : 3;
         }();
-#define BQ_LAUNCH(R, Q)                                                                                           \
-    hipLaunchKernelGGL((msda1d_bwd_query_pyr_kernel<R, Q>), pg, dim3(kPyrThreads), kBqLds, s, value, value_pad_mask, \
+#define BQ_LAUNCH(R, Q, ...)                                                                                      \
+    hipLaunchKernelGGL((msda1d_bwd_query_pyr_kernel<R, Q, ##__VA_ARGS__>), pg, dim3(kPyrThreads), kBqLds, s, value, value_pad_mask, \
                        proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, bq_blocks,        \
                        grad_output, save_attn, save_loc, grad_proj, grad_ref, gp16)
-        if (ref_dim == 1) {
+        static const bool pf = [] {  // PDVC_BQ_PF=1: inputs prefetched a trip ahead, unconditional stores (A/B)
+            const char* e = getenv("PDVC_BQ_PF");
+            return e && e[0] == '1';
+        }();
+        if (pf && qu == 3) {
+            if (ref_dim == 1) BQ_LAUNCH(1, 3, true);
+            else BQ_LAUNCH(2, 3, true);
+        } else if (ref_dim == 1) {
             if (qu == 3) BQ_LAUNCH(1, 3);
             else if (qu == 5) BQ_LAUNCH(1, 5);
             else BQ_LAUNCH(1, 1);
@@ -2538,7 +2661,16 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
                                    {(const void*)msda1d_bwd_value_kernel<2, false>, 96 * 1024},
                                    {(const void*)msda1d_bwd_value_kernel<1, true>, 96 * 1024},
                                    {(const void*)msda1d_bwd_value_kernel<1, true, 4>, 96 * 1024},
-                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, true>, 96 * 1024}},
+                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, true>, 96 * 1024},
+                                   {(const void*)msda1d_bwd_value_kernel<1, true, 8, false, 0, 1>, 96 * 1024},
+                                   {(const void*)msda1d_bwd_value_kernel<1, true, 8, false, 0, 2>, 96 * 1024},
+                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, false, 0, 1>, 96 * 1024},
+                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, false, 0, 2>, 96 * 1024},
+                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, true, 0, 1>, 96 * 1024},
+                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, true, 0, 2>, 96 * 1024},
+                                   {(const void*)msda1d_bwd_value_kernel<1, true, 6, false, 0, 0>, 96 * 1024},
+                                   {(const void*)msda1d_bwd_value_kernel<1, true, 6, false, 0, 1>, 96 * 1024},
+                                   {(const void*)msda1d_bwd_value_kernel<1, true, 6, false, 0, 2>, 96 * 1024}},
                             "msda1d_bwd_value_kernel")))
             return rc;
         for (int q0 = 0; q0 < num_query; q0 += qchunk) {
@@ -2547,10 +2679,17 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
             if (g4 && level_sums && lds < kVW * 16 * 16) lds = kVW * 16 * 16;  // the level-sum reduction
             float* gsums = g4 ? level_sums : nullptr;
             const int acc = q0 > 0;
-#define VAL_LAUNCH(UGV, B16V)                                                                                       \
-    hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, UGV, B16V>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s, \
-                       value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output, save_attn,  \
-                       save_loc, grad_value, gsums, (const int64_t*)nullptr, (const int64_t*)nullptr, gv16)
+#define VAL_LAUNCH1(UGV, B16V, DEFV)                                                                                \
+    hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, UGV, B16V, 0, DEFV>), dim3((unsigned)nblk), dim3(kVW * 64), \
+                       lds, s, value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,     \
+                       save_attn, save_loc, grad_value, gsums, (const int64_t*)nullptr, (const int64_t*)nullptr, gv16)
+#define VAL_LAUNCH(UGV, B16V)                                               \
+    do {                                                                    \
+        if (vdef >= 2) VAL_LAUNCH1(UGV, B16V, 2);                           \
+        else if (vdef == 1) VAL_LAUNCH1(UGV, B16V, 1);                      \
+        else VAL_LAUNCH1(UGV, B16V, 0);                                     \
+    } while (0)
+            const int vdef = value_defer();
             static const int vabl = [] {
                 const char* e = getenv("PDVC_VAL_ABLATE");
                 return e ? atoi(e) : 0;
@@ -2585,8 +2724,10 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
                                        (const int64_t*)nullptr, (const int64_t*)nullptr, gv16);
             } else if (g4 && gv16) VAL_LAUNCH(4, true);  // the bf16 stores spill the depth-8 walk (7 VGPRs): depth 4
             else if (g4 && value_ug(num_query, S) == 4) VAL_LAUNCH(4, false);
+            else if (g4 && value_ug(num_query, S) == 6) VAL_LAUNCH(6, false);
             else if (g4) VAL_LAUNCH(8, false);
 #undef VAL_LAUNCH
+#undef VAL_LAUNCH1
             else if (head_dim <= 64)
                 hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, false>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
                                    value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
