@@ -2119,6 +2119,9 @@ __global__ __launch_bounds__(kPyrThreads) void msda_dropin_fwd_pyr_kernel(
 // each phase's owner lanes write grad_attn and grad_loc of their samples in the drop-in layout (msda_dropin_bwd_query_
 // kernel's owner math: no softmax here, so nothing is carried between the phases), and the first phase writes the
 // level-major (location x, a * fy) slab of every sample for the value-gradient kernel
+// PF: msda1d_bwd_query_pyr_kernel's PF (the next query's inputs loaded before this query's stores, which are
+// unconditional buffer stores)
+template <bool PF = false>
 __global__ __launch_bounds__(kPyrThreads) void msda_dropin_bwd_query_pyr_kernel(
     const float* __restrict__ value, const int64_t* __restrict__ shapes, const int64_t* __restrict__ lsi,
     const float* __restrict__ loc, const float* __restrict__ attn, int Lq, int S, int M, int qblocks,
@@ -2139,16 +2142,47 @@ __global__ __launch_bounds__(kPyrThreads) void msda_dropin_bwd_query_pyr_kernel(
     const int base_own = pyr_base(lv, l_own);
     const char* lrow = reinterpret_cast<const char*>(lds4) + sub * 16;
 
+    float4 pg;  // PF: the next query's inputs
+    float2 plc;
+    float pat;
+    auto fetch = [&](int iq) {
+        const int q0 = qb * kBqQ + slot + 64 * iq;
+        const size_t row = (size_t)b * Lq + (q0 < Lq ? q0 : Lq - 1);
+        pg = *reinterpret_cast<const float4*>(gout + row * MD + (size_t)m * 64 + sub * 4);
+        const size_t si = (row * M + m) * kNS + sub;
+        plc = *reinterpret_cast<const float2*>(loc + 2 * si);
+        pat = attn[si];
+    };
+    // PF stores: one video's rows per descriptor; an inactive lane's offset is the descriptor's size (dropped)
+    const int ga_bytes = Lq * M * kNS * 4, sv_bytes = kL * Lq * kP * 4;
+    const __amdgpu_buffer_rsrc_t gar = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(grad_attn + (size_t)b * Lq * M * kNS), (short)0, ga_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t glr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(grad_loc + 2 * (size_t)b * Lq * M * kNS), (short)0, 2 * ga_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t slr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(save_loc + save_index(b, m, 0, 0, 0, Lq, M)), (short)0, sv_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t sar = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(save_attn + save_index(b, m, 0, 0, 0, Lq, M)), (short)0, sv_bytes, 0x00020000);
     auto run_query = [&](int iq, auto L0c, auto L1c) {
         constexpr int L0 = decltype(L0c)::value, L1 = decltype(L1c)::value;
         const int q0 = qb * kBqQ + slot + 64 * iq;
         const bool act = q0 < Lq;
         const int q = act ? q0 : Lq - 1;
         const size_t row = (size_t)b * Lq + q;
-        const float4 g = *reinterpret_cast<const float4*>(gout + row * MD + (size_t)m * 64 + sub * 4);
+        float4 g;
+        float2 lc;
+        float av;
         const size_t si = (row * M + m) * kNS + sub;
-        const float2 lc = *reinterpret_cast<const float2*>(loc + 2 * si);
-        const DropinSample sm = dropin_sample(lc.x, lc.y, attn[si], T_own, 0, 0);
+        if constexpr (PF) {
+            g = pg;
+            lc = plc;
+            av = pat;
+        } else {
+            g = *reinterpret_cast<const float4*>(gout + row * MD + (size_t)m * 64 + sub * 4);
+            lc = *reinterpret_cast<const float2*>(loc + 2 * si);
+            av = attn[si];
+        }
+        const DropinSample sm = dropin_sample(lc.x, lc.y, av, T_own, 0, 0);
         const int ad = pyr_corner(base_own, sm.i0);
         float d1 = 0.f, d2 = 0.f;
         const pf2 gxy = {g.x, g.y}, gzw = {g.z, g.w};
@@ -2190,19 +2224,38 @@ __global__ __launch_bounds__(kPyrThreads) void msda_dropin_bwd_query_pyr_kernel(
                 d2 = (L < 2) ? other : part[0];
             }
         }
-        if (act && L0 == 0) {
-            const size_t vi = save_index(b, m, l_own, q, p_own, Lq, M);
-            save_loc[vi] = lc.x;
-            save_attn[vi] = sm.a * sm.fy;
-        }
-        if (act && l_own >= L0 && l_own < L1) {
+        if constexpr (PF) {
+            fetch(iq + 1 < kBqQPS ? iq + 1 : 0);  // after every use of g, before the stores
+            const int ls = ((size_t)l_own * Lq + q) * kP + p_own;  // save slab offset inside (b, m)
+            if (L0 == 0) {
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lc.x), slr, act ? ls * 4 : sv_bytes, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sm.a * sm.fy), sar, act ? ls * 4 : sv_bytes, 0,
+                                                      0);
+            }
+            const bool st = act && l_own >= L0 && l_own < L1;
             const float x1 = sm.ok1 ? d1 : 0.f, x2 = sm.ok2 ? d2 : 0.f;
             const float dot = (1.f - sm.lw) * x1 + sm.lw * x2;
-            grad_attn[si] = sm.fy * dot;
-            *reinterpret_cast<float2*>(grad_loc + 2 * si) =
-                make_float2(Tf * ((sm.a * sm.fy) * (x2 - x1)), sm.a * (sm.sy * dot));
+            const int li = (q * M + m) * kNS + sub;  // sample index inside the video
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sm.fy * dot), gar, st ? li * 4 : ga_bytes, 0, 0);
+            using u2 = unsigned int __attribute__((ext_vector_type(2)));
+            const u2 glv = u2{__float_as_uint(Tf * ((sm.a * sm.fy) * (x2 - x1))), __float_as_uint(sm.a * (sm.sy * dot))};
+            __builtin_amdgcn_raw_buffer_store_b64(glv, glr, st ? li * 8 : 2 * ga_bytes, 0, 0);
+        } else {
+            if (act && L0 == 0) {
+                const size_t vi = save_index(b, m, l_own, q, p_own, Lq, M);
+                save_loc[vi] = lc.x;
+                save_attn[vi] = sm.a * sm.fy;
+            }
+            if (act && l_own >= L0 && l_own < L1) {
+                const float x1 = sm.ok1 ? d1 : 0.f, x2 = sm.ok2 ? d2 : 0.f;
+                const float dot = (1.f - sm.lw) * x1 + sm.lw * x2;
+                grad_attn[si] = sm.fy * dot;
+                *reinterpret_cast<float2*>(grad_loc + 2 * si) =
+                    make_float2(Tf * ((sm.a * sm.fy) * (x2 - x1)), sm.a * (sm.sy * dot));
+            }
         }
     };
+    if constexpr (PF) fetch(0);
 
     pyr_stage_g(lds4, vsrc, MD, lv.start[0], lv.T[0]);
     __syncthreads();
@@ -2295,6 +2348,15 @@ static int value_defer() {
         return e ? atoi(e) : 0;
     }();
     return d;
+}
+
+// the backward-query pyramid kernels' PF form (PDVC_BQ_PF=1)
+static bool bq_pf() {
+    static const bool on = [] {
+        const char* e = getenv("PDVC_BQ_PF");
+        return e && e[0] == '1';
+    }();
+    return on;
 }
 
 // 16-lane-group gather for the value gradient at D = 64 (PDVC_MSDA_G4=0 selects the wave-per-range form)
@@ -2587,11 +2649,7 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
     hipLaunchKernelGGL((msda1d_bwd_query_pyr_kernel<R, Q, ##__VA_ARGS__>), pg, dim3(kPyrThreads), kBqLds, s, value, value_pad_mask, \
                        proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, bq_blocks,        \
                        grad_output, save_attn, save_loc, grad_proj, grad_ref, gp16)
-        static const bool pf = [] {  // PDVC_BQ_PF=1: inputs prefetched a trip ahead, unconditional stores (A/B)
-            const char* e = getenv("PDVC_BQ_PF");
-            return e && e[0] == '1';
-        }();
-        if (pf && qu == 3) {
+        if (bq_pf() && qu == 3) {
             if (ref_dim == 1) BQ_LAUNCH(1, 3, true);
             else BQ_LAUNCH(2, 3, true);
         } else if (ref_dim == 1) {
@@ -2813,7 +2871,8 @@ static int dropin_pyr_blocks(int S, int Lq, int per_block) {
     if (!on || 4L * Lq < S) return 0;
     static std::atomic<int> done[kMaxDevices];
     const bool attr = lds_optin(done, {{(const void*)msda_dropin_fwd_pyr_kernel, (int)kPyr2LdsMax},
-                                       {(const void*)msda_dropin_bwd_query_pyr_kernel, (int)kPyrLds}},
+                                       {(const void*)msda_dropin_bwd_query_pyr_kernel<false>, (int)kPyrLds},
+                                       {(const void*)msda_dropin_bwd_query_pyr_kernel<true>, (int)kPyrLds}},
                                 "msda_dropin pyramid kernels") == PDVC_OK;
     return attr ? (Lq + per_block - 1) / per_block : 0;
 }
@@ -2861,9 +2920,14 @@ int dropin1d_backward(const float* value, const int64_t* shapes, const int64_t* 
     int pyr_first = 0;
     if (const int qb = dropin_pyr_blocks(S, Lq, kBqQ)) {
         PDVC_CHECK_ARG((long)N * M * qb < (1L << 31), "too many query blocks");
-        hipLaunchKernelGGL(msda_dropin_bwd_query_pyr_kernel, dim3((unsigned)(N * M * qb)), dim3(kPyrThreads), kPyrLds,
-                           s, value, shapes, lsi, loc, attn, Lq, S, M, qb, gout, grad_loc, grad_attn, save_attn,
-                           save_loc);
+        if (bq_pf())
+            hipLaunchKernelGGL(msda_dropin_bwd_query_pyr_kernel<true>, dim3((unsigned)(N * M * qb)), dim3(kPyrThreads),
+                               kPyrLds, s, value, shapes, lsi, loc, attn, Lq, S, M, qb, gout, grad_loc, grad_attn,
+                               save_attn, save_loc);
+        else
+            hipLaunchKernelGGL(msda_dropin_bwd_query_pyr_kernel<false>, dim3((unsigned)(N * M * qb)), dim3(kPyrThreads),
+                               kPyrLds, s, value, shapes, lsi, loc, attn, Lq, S, M, qb, gout, grad_loc, grad_attn,
+                               save_attn, save_loc);
         PDVC_CHECK_LAUNCH("msda_dropin_bwd_query_pyr_kernel");
         pyr_first = 1;
     }
@@ -2876,8 +2940,10 @@ int dropin1d_backward(const float* value, const int64_t* shapes, const int64_t* 
     // value gradient: msda1d_bwd_value_kernel on the slab, its LDS sized for the longest possible level (S)
     static std::atomic<int> done[kMaxDevices];
     if (const int rc = lds_optin(done, {{(const void*)msda1d_bwd_value_kernel<1, true>, 96 * 1024},
-                                        {(const void*)msda1d_bwd_value_kernel<1, true, 4>, 96 * 1024}},
-                                 "msda1d_bwd_value_kernel"))
+                                        {(const void*)msda1d_bwd_value_kernel<1, true, 4>, 96 * 1024},
+                                        {(const void*)msda1d_bwd_value_kernel<1, true, 4, false, 0, 2>, 96 * 1024},
+                                        {(const void*)msda1d_bwd_value_kernel<1, true, 6, false, 0, 2>, 96 * 1024}},
+                                 "msda1d_bwd_value_kernel (drop-in)"))
         return rc;
     const long per_sample = 12;
     const long budget = 96 * 1024 - 8L * (S + 2) - 16;
@@ -2891,7 +2957,15 @@ int dropin1d_backward(const float* value, const int64_t* shapes, const int64_t* 
         const int nq = (Lq - q0) < qchunk ? (Lq - q0) : qchunk;
         const size_t lds = sizeof(int) * (2 * (size_t)(S + 2) + 3 * (size_t)nq * kP + 2);
         const int acc = q0 > 0;
-        if (value_ug(Lq, S) == 4)
+#define DROPIN_VAL(UGV, DEFV)                                                                                     \
+    hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, UGV, false, 0, DEFV>), dim3((unsigned)nblk), dim3(kVW * 64), \
+                       lds, s, nullptr, lv, Lq, q0, nq, S, M, 64, acc, gout, save_attn, save_loc, grad_value, nullptr, \
+                       shapes, lsi)
+        const int ug = value_ug(Lq, S);
+        if (value_defer() == 2 && ug == 4) DROPIN_VAL(4, 2);
+        else if (value_defer() == 2 && ug == 6) DROPIN_VAL(6, 2);
+#undef DROPIN_VAL
+        else if (ug == 4)
             hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, 4>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
                                nullptr, lv, Lq, q0, nq, S, M, 64, acc, gout, save_attn, save_loc, grad_value, nullptr,
                                shapes, lsi);

@@ -37,3 +37,14 @@ for ab in 0 1 0 1; do
   echo "[$(date +%T)] PDVC_WIN_ABLATE=$ab (forward, T=1024)"
   PDVC_WIN_ABLATE=$ab timeout -k 10 120 python -u tools/kbench.py --videos 512 --reps 4 --T 1024 2>&1 | grep -E "^encoder" || exit 1
 done
+for v in "0 0 0" "2 6 1" "0 0 0" "2 6 1"; do
+  set -- $v
+  echo "[$(date +%T)] drop-in PDVC_VAL_DEFER=$1 PDVC_VALUE_UG=$2 PDVC_BQ_PF=$3"
+  PDVC_VAL_DEFER=$1 PDVC_VALUE_UG=$2 PDVC_BQ_PF=$3 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv \
+    -d $O/dropin_d$1u$2p$3 -o dp_$RANDOM -- python -u tools/dropin_prof.py 2>&1 | tail -3 || exit 1
+done
+for d in $O/dropin_*; do
+  for f in $(find $d -name "*kernel_stats.csv"); do
+    python -c "import csv,sys; [print(f\"$(basename $d) {float(r['AverageNs'])/1e3:9.1f} us x{r['Calls']:>4} {r['Name'][:96]}\") for r in csv.DictReader(open(sys.argv[1])) if 'bwd' in r['Name']]" $f
+  done
+done
