@@ -1630,14 +1630,26 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
             // trip is stored at once.)
             const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)(grad_value + ((size_t)b * S + st) * MD), (short)0, (int)((size_t)T * MD * 4), 0x00020000);
+            // B16: the held rows' bf16 roundings too, at half the fp32 offsets
+            const __amdgpu_buffer_rsrc_t orsrc16 = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(B16 ? gv16 + ((size_t)b * S + st) * MD : nullptr), (short)0, B16 ? (int)((size_t)T * MD * 2) : 0,
+                0x00020000);
             using u4 = unsigned int __attribute__((ext_vector_type(4)));
+            using u2 = unsigned int __attribute__((ext_vector_type(2)));
             u4 dw0 = u4{0u, 0u, 0u, 0u}, dw1 = dw0;
+            u2 dh0 = u2{0u, 0u}, dh1 = dh0;
             int do0 = 0, do1 = 0;        // buffer offsets of the held rows
             bool ok0 = false, ok1 = false;  // rows held
             auto flush = [&]() {
                 if constexpr (DEF > 0) {
-                    if (ok0) __builtin_amdgcn_raw_buffer_store_b128(dw0, orsrc, do0, 0, 0);
-                    if (DEF > 1 && ok1) __builtin_amdgcn_raw_buffer_store_b128(dw1, orsrc, do1, 0, 0);
+                    if (ok0) {
+                        __builtin_amdgcn_raw_buffer_store_b128(dw0, orsrc, do0, 0, 0);
+                        if (B16) __builtin_amdgcn_raw_buffer_store_b64(dh0, orsrc16, do0 >> 1, 0, 0);
+                    }
+                    if (DEF > 1 && ok1) {
+                        __builtin_amdgcn_raw_buffer_store_b128(dw1, orsrc, do1, 0, 0);
+                        if (B16) __builtin_amdgcn_raw_buffer_store_b64(dh1, orsrc16, do1 >> 1, 0, 0);
+                    }
                     ok0 = false;
                     ok1 = false;
                 }
@@ -1665,10 +1677,16 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
                         dw0 = to0 ? vb : dw0;
                         do0 = to0 ? o : do0;
                         ok0 = true;
+                        u2 hb = u2{0u, 0u};
+                        if (B16) {
+                            hb = u2{bf16_bits(v.x) | (bf16_bits(v.y) << 16), bf16_bits(v.z) | (bf16_bits(v.w) << 16)};
+                            dh0 = to0 ? hb : dh0;
+                        }
                         if (DEF > 1) {
                             dw1 = to1 ? vb : dw1;
                             do1 = to1 ? o : do1;
                             ok1 = ok1 || to1;
+                            if (B16) dh1 = to1 ? hb : dh1;
                         }
                         if (!to0 && !to1) emit(r, v);
                     }
