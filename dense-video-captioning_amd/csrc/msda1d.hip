@@ -715,7 +715,7 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_win_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
     int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
     int qblocks, float* __restrict__ out, float* __restrict__ save_attn, float* __restrict__ save_loc,
-    uint16_t* __restrict__ out16, int abl = 0) {
+    uint16_t* __restrict__ out16) {
     extern __shared__ __attribute__((aligned(16))) float4 lds4[];
     const int blk = xcd_remap(blockIdx.x, gridDim.x);  // the query blocks and heads of a video share an XCD
     const int qb = blk % qblocks, bm = blk / qblocks;
@@ -725,7 +725,6 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_win_kernel(
     const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
     const float* vsrc = value + (size_t)b * S * MD + (size_t)m * 64;
     const char* lrow = reinterpret_cast<const char*>(lds4) + sub * 16;
-    // abl (measurement only, PDVC_WIN_ABLATE): 1 = no staging after window A (the gathers read stale rows)
     pyr_zero_row(lds4, 0, 0);  // the leading guard row of every phase
     pyr_zero_row(lds4, kWinZero, 64);
     pyr_zero_row(lds4, kWinZero + 1, 128);
@@ -750,6 +749,10 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_win_kernel(
     // level's phase) and for window B (level 0 rows [512, T0))
     int adA[kPyrQPS], adB[kPyrQPS];
     float w1v[kPyrQPS], w2v[kPyrQPS];
+    // per query: does any level-0 sample of the wave's 4 queries lie in window A / B (wave-uniform ballots)?  A wave's
+    // queries are 4 neighbouring positions, so their level-0 samples nearly always share one window: the other
+    // window's pass over them -- all 16 lanes reading the two zero rows -- is skipped
+    uint32_t inA_any = 0u, inB_any = 0u;  // bit i: query i
 #pragma unroll
     for (int i = 0; i < kPyrQPS; ++i) {
         const int q = qb * kPyrQ + slot + 64 * i;
@@ -783,6 +786,8 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_win_kernel(
         const bool inB = l_own == 0 && i0 >= kWinSplit;
         adA[i] = inB ? kWinZero * 256 : ad;
         adB[i] = inB ? ad - kWinSplit * 256 : kWinZero * 256;
+        inA_any |= (uint32_t)(__builtin_amdgcn_ballot_w64(l_own == 0 && !inB) != 0) << i;
+        inB_any |= (uint32_t)(__builtin_amdgcn_ballot_w64(inB) != 0) << i;
     }
     PAcc4 acc[kPyrQPS];
 #pragma unroll
@@ -793,6 +798,7 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_win_kernel(
         constexpr bool B = decltype(Bc)::value;
 #pragma unroll
         for (int i = 0; i < kPyrQPS; ++i) {
+            if (L == 0 && !(((B ? inB_any : inA_any) >> i) & 1u)) continue;  // uniform: none of the wave's in this window
             pf4 v1[kP], v2[kP];
             float c1[kP], c2[kP];
             int ad = B ? adB[i] : adA[i];
@@ -821,14 +827,12 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_win_kernel(
     level(std::integral_constant<int, 0>{}, F{});
     __syncthreads();  // every wave is done with window A
     const int nB = lv.T[0] - kWinSplit;
-    if (!abl)
     pyr_dma_rows(lds4, vsrc, MD, lv.start[0] + kWinSplit, 1, nB);
     pyr_zero_row(lds4, 1 + nB, 0);
     pyr_dma_wait();
     __syncthreads();
     level(std::integral_constant<int, 0>{}, Tt{});
     __syncthreads();
-    if (!abl)
     pyr_dma_rows(lds4, vsrc, MD, lv.start[1], 1, lv.T[1]);
     pyr_zero_row(lds4, 1 + lv.T[1], 0);
     pyr_dma_wait();
@@ -836,7 +840,6 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_win_kernel(
     level(std::integral_constant<int, 1>{}, F{});
     __syncthreads();
     const int n23 = lv.T[2] + lv.T[3];
-    if (!abl)
     pyr_dma_rows(lds4, vsrc, MD, lv.start[2], 1, n23);
     pyr_zero_row(lds4, 1 + n23, 0);
     pyr_dma_wait();
@@ -1186,13 +1189,7 @@ constexpr size_t kBqLds = kPyrLds + (size_t)kBqQ * 4 * sizeof(float);
 
 // QU: queries of a lane group run back to back per loop trip (interleavable by the scheduler: each query is a
 // dependent chain of LDS reads, a 16-lane reduction and the owner math, and the LDS caps the CU at 4 waves/SIMD)
-// PF: each trip's global inputs (dOut row, sampling location, attention weight) are loaded during the previous trip,
-// before that trip's gradient stores, and the stores are unconditional buffer stores (inactive lanes get an
-// out-of-range offset, which the buffer range check drops).  vmcnt counts loads and stores together in issue order,
-// so inputs loaded after a trip's stores wait for those stores' write acknowledgements (hundreds to thousands of
-// cycles); loaded before them, the wait is an exact vmcnt(#stores) -- exact only while the stores are not under
-// branches, whose store-less path would make hipcc wait for everything.
-template <int RD, int QU = 1, bool PF = false>
+template <int RD, int QU = 1>
 __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ proj,
     int proj_stride, int off_base, int logit_base, const float* __restrict__ ref, Levels1d lv, int Lq, int S, int M,
@@ -1224,25 +1221,6 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
     // owner math of the lanes whose level is in range (offset gradient, grad_ref, dL/da).  The QU queries' loads, LDS
     // reads and reductions are independent chains written side by side, so they overlap (the carry / gradient
     // stores come last: they would otherwise order the next query's LDS reads behind them)
-    // PF: the inputs of queries i0q .. i0q + QU - 1 into pg / ploc / pat
-    float4 pg[QU];
-    float ploc[QU], pat[QU];
-    auto fetch = [&](int i0q) {
-#pragma unroll
-        for (int u = 0; u < QU; ++u) {
-            const int q0 = qb * kBqQ + slot + 64 * (i0q + u);
-            const int q = q0 < Lq ? q0 : Lq - 1;
-            pg[u] = *reinterpret_cast<const float4*>(gout + ((size_t)b * Lq + q) * MD + (size_t)m * 64 + sub * 4);
-            const size_t si = save_index(b, m, l_own, q, p_own, Lq, M);
-            ploc[u] = save_loc[si];
-            pat[u] = save_attn[si];
-        }
-    };
-    const int gp_bytes = Lq * proj_stride * 4;  // PF stores: one video's rows of grad_proj (gp16) per descriptor
-    const __amdgpu_buffer_rsrc_t gpr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(grad_proj + (size_t)b * Lq * proj_stride), (short)0, gp_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t gpr16 = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(gp16 ? gp16 + (size_t)b * Lq * proj_stride : nullptr), (short)0, gp16 ? gp_bytes / 2 : 0, 0x00020000);
     auto run_queries = [&](int i0q, auto L0c, auto L1c) {
         constexpr int L0 = decltype(L0c)::value, L1 = decltype(L1c)::value;
         bool act[QU], inside[QU];
@@ -1256,17 +1234,10 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
             act[u] = q0 < Lq;
             const int q = act[u] ? q0 : Lq - 1;
             row[u] = (size_t)b * Lq + q;
-            float x;
-            if constexpr (PF) {
-                g[u] = pg[u];
-                x = ploc[u] * Tf - 0.5f;
-                a[u] = pat[u];
-            } else {
-                g[u] = *reinterpret_cast<const float4*>(gout + row[u] * MD + (size_t)m * 64 + sub * 4);
-                const size_t si = save_index(b, m, l_own, q, p_own, Lq, M);
-                x = save_loc[si] * Tf - 0.5f;
-                a[u] = save_attn[si];
-            }
+            g[u] = *reinterpret_cast<const float4*>(gout + row[u] * MD + (size_t)m * 64 + sub * 4);
+            const size_t si = save_index(b, m, l_own, q, p_own, Lq, M);
+            const float x = save_loc[si] * Tf - 0.5f;
+            a[u] = save_attn[si];
             inside[u] = x > -1.f && x < Tf;
             const float xf = floorf(inside[u] ? x : 0.f);
             i0[u] = (int)xf;
@@ -1318,9 +1289,6 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
                 }
             }
         }
-        // PF: the next trip's inputs (the phase's first trip after its last: the second phase starts there, and its
-        // own last trip loads a spare copy) -- issued here, after every use of g and before this trip's stores
-        if constexpr (PF) fetch(i0q + QU < kBqQPS ? i0q + QU : 0);
         // owner math of the lanes whose sample is in this phase (.cuh:140-170), as msda1d_bwd_query_dot_kernel
         const bool mine_phase = l_own >= L0 && l_own < L1;
 #pragma unroll
@@ -1344,15 +1312,7 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
                 goff = (t2 * rr1) / (float)kP;
                 g1 = mine_phase ? t2 * (prow[off_base + m * kNS + sub] / (float)kP) : 0.f;
             }
-            const int qrow = (int)(row[u] - (size_t)b * Lq);
-            if constexpr (PF) {
-                const int col = qrow * proj_stride + off_base + m * kNS + sub;
-                const bool st = act[u] && mine_phase;
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(goff), gpr, st ? col * 4 : gp_bytes, 0, 0);
-                if (gp16)
-                    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bf16_bits(goff), gpr16,
-                                                          st ? col * 2 : gp_bytes, 0, 0);
-            } else if (act[u] && mine_phase) {
+            if (act[u] && mine_phase) {
                 gprow[off_base + m * kNS + sub] = goff;
                 if (gp16) gp16[row[u] * proj_stride + off_base + m * kNS + sub] = (uint16_t)bf16_bits(goff);
             }
@@ -1375,14 +1335,8 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
             } else {  // second phase: the softmax term over all 16 samples, then every logit gradient
                 if (l_own == 0) ga = carry[ci];
                 const float delta = group_allreduce<16>(a[u] * ga);
-                const float gl = a[u] * (ga - delta);
-                if constexpr (PF) {
-                    const int col = qrow * proj_stride + logit_base + m * kNS + sub;
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gl), gpr, act[u] ? col * 4 : gp_bytes, 0, 0);
-                    if (gp16)
-                        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bf16_bits(gl), gpr16,
-                                                              act[u] ? col * 2 : gp_bytes, 0, 0);
-                } else if (act[u]) {
+                if (act[u]) {
+                    const float gl = a[u] * (ga - delta);
                     gprow[logit_base + m * kNS + sub] = gl;
                     if (gp16) gp16[row[u] * proj_stride + logit_base + m * kNS + sub] = (uint16_t)bf16_bits(gl);
                 }
@@ -1390,7 +1344,6 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_bwd_query_pyr_kernel(
         }
     };
 
-    if constexpr (PF) fetch(0);
     pyr_stage_g(lds4, vsrc, MD, lv.start[0], lv.T[0]);
     __syncthreads();
     static_assert(kBqQPS % QU == 0, "QU must divide the queries per lane group");
@@ -1428,9 +1381,7 @@ constexpr int kVQPT = 4;  // queries per thread in its sort passes: a launch chu
 // fp32 path keeps its registers: the pointer and its stores cost the depth-8 walk 9 spilled VGPRs)
 // ABL (measurement only, PDVC_VAL_ABLATE): 1 = stop after the sort, 2 = walk without the gradient-row gathers
 // (PDVC_VAL_ABLATE=1/2 select them for the depth-8 encoder walk, 3/4 for the depth-4 decoder walk)
-// DEF: finished rows held back in registers (up to DEF of them) and stored at the top of the walk's next trip, ahead of
-// that trip's gathers (see the walk)
-template <int CW, bool G4, int UG = 8, bool B16 = false, int ABL = 0, int DEF = 0>
+template <int CW, bool G4, int UG = 8, bool B16 = false, int ABL = 0>
 __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uint8_t* __restrict__ vmask, Levels1d lv,
                                                                      int Lq, int q0, int nq, int S, int M, int D,
                                                                      int accumulate,
@@ -1617,85 +1568,28 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
                 (void*)(gout + (size_t)b * Lq * MD), (short)0, (int)((size_t)Lq * MD * 4), 0x00020000);
             const int coff = (m * D + gl * 4) * 4, rowb = (int)MD * 4;
             const unsigned MDu = (unsigned)MD;  // < 2^24: the row offset is one v_mul_u32_u24 (a 64-bit one cost ~6 VALU)
-            auto emit = [&](int r, float4 v) {
-                *reinterpret_cast<float4*>(ob + __umul24((unsigned)r, MDu)) = v;
-                if (B16) store_bf16x4(ob16 + (size_t)r * MD, v.x, v.y, v.z, v.w);
-            };
-            // DEF > 0: vmcnt counts loads and stores together, in issue order, and a store holds its address and data
-            // VGPRs until it completes (hipcc waits vmcnt before reusing them), so a row stored among a trip's gathers
-            // makes the trip wait for that store's write acknowledgement (MI355X_MICROARCH.md: ~600-3000 cycles with
-            // every CU writing).  Up to DEF finished rows wait in loop-carried registers instead -- data and buffer
-            // offset both, rewritten only by a later put, well after the store -- and are stored at the top of the next
-            // trip, before its gathers, whose latency then covers the acknowledgement.  (A third row finished in one
-            // trip is stored at once.)
-            const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(grad_value + ((size_t)b * S + st) * MD), (short)0, (int)((size_t)T * MD * 4), 0x00020000);
-            // B16: the held rows' bf16 roundings too, at half the fp32 offsets
-            const __amdgpu_buffer_rsrc_t orsrc16 = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(B16 ? gv16 + ((size_t)b * S + st) * MD : nullptr), (short)0, B16 ? (int)((size_t)T * MD * 2) : 0,
-                0x00020000);
-            using u4 = unsigned int __attribute__((ext_vector_type(4)));
-            using u2 = unsigned int __attribute__((ext_vector_type(2)));
-            u4 dw0 = u4{0u, 0u, 0u, 0u}, dw1 = dw0;
-            u2 dh0 = u2{0u, 0u}, dh1 = dh0;
-            int do0 = 0, do1 = 0;        // buffer offsets of the held rows
-            bool ok0 = false, ok1 = false;  // rows held
-            auto flush = [&]() {
-                if constexpr (DEF > 0) {
-                    if (ok0) {
-                        __builtin_amdgcn_raw_buffer_store_b128(dw0, orsrc, do0, 0, 0);
-                        if (B16) __builtin_amdgcn_raw_buffer_store_b64(dh0, orsrc16, do0 >> 1, 0, 0);
-                    }
-                    if (DEF > 1 && ok1) {
-                        __builtin_amdgcn_raw_buffer_store_b128(dw1, orsrc, do1, 0, 0);
-                        if (B16) __builtin_amdgcn_raw_buffer_store_b64(dh1, orsrc16, do1 >> 1, 0, 0);
-                    }
-                    ok0 = false;
-                    ok1 = false;
-                }
-            };
             auto put = [&](int r, float4 v) {
                 if (r >= r0 && r < r1) {
+                    float4* orow = reinterpret_cast<float4*>(ob + __umul24((unsigned)r, MDu));
                     if (mrow && mk[r]) v = make_float4(0.f, 0.f, 0.f, 0.f);
                     psum.x += v.x;
                     psum.y += v.y;
                     psum.z += v.z;
                     psum.w += v.w;
                     if (accumulate) {
-                        const float4 o = *reinterpret_cast<const float4*>(ob + __umul24((unsigned)r, MDu));
+                        const float4 o = *orow;
                         v.x += o.x;
                         v.y += o.y;
                         v.z += o.z;
                         v.w += o.w;
                     }
-                    if constexpr (DEF == 0) {
-                        emit(r, v);
-                    } else {  // vector selects (a branch assigning float4 structs put them on the stack)
-                        const bool to0 = !ok0, to1 = DEF > 1 && ok0 && !ok1;
-                        const u4 vb = __builtin_bit_cast(u4, v);
-                        const int o = (int)__umul24((unsigned)r, (unsigned)rowb) + coff;
-                        dw0 = to0 ? vb : dw0;
-                        do0 = to0 ? o : do0;
-                        ok0 = true;
-                        u2 hb = u2{0u, 0u};
-                        if (B16) {
-                            hb = u2{bf16_bits(v.x) | (bf16_bits(v.y) << 16), bf16_bits(v.z) | (bf16_bits(v.w) << 16)};
-                            dh0 = to0 ? hb : dh0;
-                        }
-                        if (DEF > 1) {
-                            dw1 = to1 ? vb : dw1;
-                            do1 = to1 ? o : do1;
-                            ok1 = ok1 || to1;
-                            if (B16) dh1 = to1 ? hb : dh1;
-                        }
-                        if (!to0 && !to1) emit(r, v);
-                    }
+                    *orow = v;
+                    if (B16) store_bf16x4(ob16 + (size_t)r * MD, v.x, v.y, v.z, v.w);
                 }
             };
             int k = (int)(eqk[jb] >> 16);
             PAcc4 alo = pacc_zero(), ahi = pacc_zero();  // rows k - 1 and k
             for (int j0 = jb; j0 < je; j0 += UG) {
-                flush();
                 uint32_t e[UG];
                 pf4 gv[UG];
 #pragma unroll
@@ -1729,14 +1623,9 @@ __global__ __launch_bounds__(kVW * 64, 6) void msda1d_bwd_value_kernel(const uin
                     pacc_fma(alo, wgt.x, gv[u]);
                     pacc_fma(ahi, wgt.y, gv[u]);
                 }
-                // DEF: drain here, where every gather of the trip has been waited for anyway (a last trip's unused
-                // gathers aside) -- otherwise hipcc waits at the next trip's first register reuse, right after that
-                // trip's held-row stores, for those stores too.  s_waitcnt vmcnt(0): gfx9 simm16, expcnt/lgkmcnt max
-                if constexpr (DEF > 0) __builtin_amdgcn_s_waitcnt(0x0F70);
             }
             put(k - 1, pacc_f4(alo));
             put(k, pacc_f4(ahi));
-            flush();
         }
         if (level_sums) {  // the bias gradient's partial: column sums of the rows this workgroup wrote
 #pragma unroll
@@ -2137,9 +2026,11 @@ __global__ __launch_bounds__(kPyrThreads) void msda_dropin_fwd_pyr_kernel(
 // each phase's owner lanes write grad_attn and grad_loc of their samples in the drop-in layout (msda_dropin_bwd_query_
 // kernel's owner math: no softmax here, so nothing is carried between the phases), and the first phase writes the
 // level-major (location x, a * fy) slab of every sample for the value-gradient kernel
-// PF: msda1d_bwd_query_pyr_kernel's PF (the next query's inputs loaded before this query's stores, which are
-// unconditional buffer stores)
-template <bool PF = false>
+// Each query's global inputs (dOut row, location pair, weight) are loaded during the previous query, before its stores,
+// and the stores are unconditional buffer stores (an inactive lane's offset is past the descriptor's range, which drops
+// it): vmcnt counts loads and stores together in issue order, so inputs loaded after a query's stores would wait for
+// their write acknowledgements, and a store under a branch leaves hipcc a store-less path to count by, so it waits for
+// everything.  740 -> 719 us per launch at 256 videos (profiles/r04_vmcnt_store_coupling.txt).
 __global__ __launch_bounds__(kPyrThreads) void msda_dropin_bwd_query_pyr_kernel(
     const float* __restrict__ value, const int64_t* __restrict__ shapes, const int64_t* __restrict__ lsi,
     const float* __restrict__ loc, const float* __restrict__ attn, int Lq, int S, int M, int qblocks,
@@ -2160,7 +2051,7 @@ __global__ __launch_bounds__(kPyrThreads) void msda_dropin_bwd_query_pyr_kernel(
     const int base_own = pyr_base(lv, l_own);
     const char* lrow = reinterpret_cast<const char*>(lds4) + sub * 16;
 
-    float4 pg;  // PF: the next query's inputs
+    float4 pg;  // the next query's inputs
     float2 plc;
     float pat;
     auto fetch = [&](int iq) {
@@ -2171,7 +2062,7 @@ __global__ __launch_bounds__(kPyrThreads) void msda_dropin_bwd_query_pyr_kernel(
         plc = *reinterpret_cast<const float2*>(loc + 2 * si);
         pat = attn[si];
     };
-    // PF stores: one video's rows per descriptor; an inactive lane's offset is the descriptor's size (dropped)
+    // stores: one video's rows per descriptor; an inactive lane's offset is the descriptor's size (dropped)
     const int ga_bytes = Lq * M * kNS * 4, sv_bytes = kL * Lq * kP * 4;
     const __amdgpu_buffer_rsrc_t gar = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(grad_attn + (size_t)b * Lq * M * kNS), (short)0, ga_bytes, 0x00020000);
@@ -2186,21 +2077,9 @@ __global__ __launch_bounds__(kPyrThreads) void msda_dropin_bwd_query_pyr_kernel(
         const int q0 = qb * kBqQ + slot + 64 * iq;
         const bool act = q0 < Lq;
         const int q = act ? q0 : Lq - 1;
-        const size_t row = (size_t)b * Lq + q;
-        float4 g;
-        float2 lc;
-        float av;
-        const size_t si = (row * M + m) * kNS + sub;
-        if constexpr (PF) {
-            g = pg;
-            lc = plc;
-            av = pat;
-        } else {
-            g = *reinterpret_cast<const float4*>(gout + row * MD + (size_t)m * 64 + sub * 4);
-            lc = *reinterpret_cast<const float2*>(loc + 2 * si);
-            av = attn[si];
-        }
-        const DropinSample sm = dropin_sample(lc.x, lc.y, av, T_own, 0, 0);
+        const float4 g = pg;
+        const float2 lc = plc;
+        const DropinSample sm = dropin_sample(lc.x, lc.y, pat, T_own, 0, 0);
         const int ad = pyr_corner(base_own, sm.i0);
         float d1 = 0.f, d2 = 0.f;
         const pf2 gxy = {g.x, g.y}, gzw = {g.z, g.w};
@@ -2242,38 +2121,22 @@ __global__ __launch_bounds__(kPyrThreads) void msda_dropin_bwd_query_pyr_kernel(
                 d2 = (L < 2) ? other : part[0];
             }
         }
-        if constexpr (PF) {
-            fetch(iq + 1 < kBqQPS ? iq + 1 : 0);  // after every use of g, before the stores
-            const int ls = ((size_t)l_own * Lq + q) * kP + p_own;  // save slab offset inside (b, m)
-            if (L0 == 0) {
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lc.x), slr, act ? ls * 4 : sv_bytes, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sm.a * sm.fy), sar, act ? ls * 4 : sv_bytes, 0,
-                                                      0);
-            }
-            const bool st = act && l_own >= L0 && l_own < L1;
-            const float x1 = sm.ok1 ? d1 : 0.f, x2 = sm.ok2 ? d2 : 0.f;
-            const float dot = (1.f - sm.lw) * x1 + sm.lw * x2;
-            const int li = (q * M + m) * kNS + sub;  // sample index inside the video
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sm.fy * dot), gar, st ? li * 4 : ga_bytes, 0, 0);
-            using u2 = unsigned int __attribute__((ext_vector_type(2)));
-            const u2 glv = u2{__float_as_uint(Tf * ((sm.a * sm.fy) * (x2 - x1))), __float_as_uint(sm.a * (sm.sy * dot))};
-            __builtin_amdgcn_raw_buffer_store_b64(glv, glr, st ? li * 8 : 2 * ga_bytes, 0, 0);
-        } else {
-            if (act && L0 == 0) {
-                const size_t vi = save_index(b, m, l_own, q, p_own, Lq, M);
-                save_loc[vi] = lc.x;
-                save_attn[vi] = sm.a * sm.fy;
-            }
-            if (act && l_own >= L0 && l_own < L1) {
-                const float x1 = sm.ok1 ? d1 : 0.f, x2 = sm.ok2 ? d2 : 0.f;
-                const float dot = (1.f - sm.lw) * x1 + sm.lw * x2;
-                grad_attn[si] = sm.fy * dot;
-                *reinterpret_cast<float2*>(grad_loc + 2 * si) =
-                    make_float2(Tf * ((sm.a * sm.fy) * (x2 - x1)), sm.a * (sm.sy * dot));
-            }
+        fetch(iq + 1 < kBqQPS ? iq + 1 : 0);  // after every use of g, before the stores
+        const int ls = (l_own * Lq + q) * kP + p_own;  // save slab offset inside (b, m)
+        if (L0 == 0) {
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lc.x), slr, act ? ls * 4 : sv_bytes, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sm.a * sm.fy), sar, act ? ls * 4 : sv_bytes, 0, 0);
         }
+        const bool st = act && l_own >= L0 && l_own < L1;
+        const float x1 = sm.ok1 ? d1 : 0.f, x2 = sm.ok2 ? d2 : 0.f;
+        const float dot = (1.f - sm.lw) * x1 + sm.lw * x2;
+        const int li = (q * M + m) * kNS + sub;  // sample index inside the video
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sm.fy * dot), gar, st ? li * 4 : ga_bytes, 0, 0);
+        using u2 = unsigned int __attribute__((ext_vector_type(2)));
+        const u2 glv = u2{__float_as_uint(Tf * ((sm.a * sm.fy) * (x2 - x1))), __float_as_uint(sm.a * (sm.sy * dot))};
+        __builtin_amdgcn_raw_buffer_store_b64(glv, glr, st ? li * 8 : 2 * ga_bytes, 0, 0);
     };
-    if constexpr (PF) fetch(0);
+    fetch(0);
 
     pyr_stage_g(lds4, vsrc, MD, lv.start[0], lv.T[0]);
     __syncthreads();
@@ -2355,26 +2218,8 @@ static int value_ug(int num_query, int S) {
         const char* e = getenv("PDVC_VALUE_UG");
         return e ? atoi(e) : 0;
     }();
-    if (forced == 4 || forced == 6 || forced == 8) return forced;
+    if (forced == 4 || forced == 8) return forced;
     return 4L * num_query < S ? 4 : 8;
-}
-
-// rows the value walk holds back before storing them (msda1d_bwd_value_kernel's DEF; PDVC_VAL_DEFER=0/1/2)
-static int value_defer() {
-    static const int d = [] {
-        const char* e = getenv("PDVC_VAL_DEFER");
-        return e ? atoi(e) : 0;
-    }();
-    return d;
-}
-
-// the backward-query pyramid kernels' PF form (PDVC_BQ_PF=1)
-static bool bq_pf() {
-    static const bool on = [] {
-        const char* e = getenv("PDVC_BQ_PF");
-        return e && e[0] == '1';
-    }();
-    return on;
 }
 
 // 16-lane-group gather for the value gradient at D = 64 (PDVC_MSDA_G4=0 selects the wave-per-range form)
@@ -2405,9 +2250,7 @@ static int bwdq_pyr_attrs() {
                             {(const void*)msda1d_bwd_query_pyr_kernel<1, 3>, b},
                             {(const void*)msda1d_bwd_query_pyr_kernel<2, 3>, b},
                             {(const void*)msda1d_bwd_query_pyr_kernel<1, 5>, b},
-                            {(const void*)msda1d_bwd_query_pyr_kernel<2, 5>, b},
-                            {(const void*)msda1d_bwd_query_pyr_kernel<1, 3, true>, b},
-                            {(const void*)msda1d_bwd_query_pyr_kernel<2, 3, true>, b}},
+                            {(const void*)msda1d_bwd_query_pyr_kernel<2, 5>, b}},
                      "msda1d_bwd_query_pyr_kernel");
 }
 
@@ -2549,18 +2392,14 @@ static int msda1d_forward_impl(const float* value, const uint8_t* value_pad_mask
         const int qb = (num_query + kPyrQ - 1) / kPyrQ;
         PDVC_CHECK_ARG((long)batch * num_heads * qb < (1L << 31), "too many query blocks");
         dim3 pg((unsigned)(batch * num_heads * qb));
-        static const int wabl = [] {
-            const char* e = getenv("PDVC_WIN_ABLATE");
-            return e ? atoi(e) : 0;
-        }();
         if (ref_dim == 1)
             hipLaunchKernelGGL((msda1d_fwd_win_kernel<1>), pg, dim3(kPyrThreads), kWinLds, s, value, value_pad_mask,
                                proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, qb, output,
-                               save_attn, save_loc, out16, wabl);
+                               save_attn, save_loc, out16);
         else
             hipLaunchKernelGGL((msda1d_fwd_win_kernel<2>), pg, dim3(kPyrThreads), kWinLds, s, value, value_pad_mask,
                                proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, qb, output,
-                               save_attn, save_loc, out16, wabl);
+                               save_attn, save_loc, out16);
         PDVC_CHECK_LAUNCH("msda1d_fwd_win_kernel");
         return PDVC_OK;
     }
@@ -2663,14 +2502,11 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
             const int v = e ? atoi(e) : 3;
             return (v == 1 || v == 5) ? v : 3;
         }();
-#define BQ_LAUNCH(R, Q, ...)                                                                                      \
-    hipLaunchKernelGGL((msda1d_bwd_query_pyr_kernel<R, Q, ##__VA_ARGS__>), pg, dim3(kPyrThreads), kBqLds, s, value, value_pad_mask, \
+#define BQ_LAUNCH(R, Q)                                                                                           \
+    hipLaunchKernelGGL((msda1d_bwd_query_pyr_kernel<R, Q>), pg, dim3(kPyrThreads), kBqLds, s, value, value_pad_mask, \
                        proj, proj_stride, off_base, logit_base, ref, lv, num_query, S, num_heads, bq_blocks,        \
                        grad_output, save_attn, save_loc, grad_proj, grad_ref, gp16)
-        if (bq_pf() && qu == 3) {
-            if (ref_dim == 1) BQ_LAUNCH(1, 3, true);
-            else BQ_LAUNCH(2, 3, true);
-        } else if (ref_dim == 1) {
+        if (ref_dim == 1) {
             if (qu == 3) BQ_LAUNCH(1, 3);
             else if (qu == 5) BQ_LAUNCH(1, 5);
             else BQ_LAUNCH(1, 1);
@@ -2727,26 +2563,12 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
         int qchunk = (int)(budget / (per_sample * kP));
         if (qchunk > kVQPT * kVW * 64) qchunk = kVQPT * kVW * 64;
         if (qchunk > num_query) qchunk = num_query;
-        static const int forced_chunk = [] {  // measurement: PDVC_VAL_QCHUNK forces the query chunk
-            const char* e = getenv("PDVC_VAL_QCHUNK");
-            return e ? atoi(e) : 0;
-        }();
-        if (forced_chunk > 0 && forced_chunk < qchunk) qchunk = forced_chunk;
         static std::atomic<int> done[kMaxDevices];  // dynamic LDS <= 96 KiB by construction of qchunk (+32 B static)
         if ((rc = lds_optin(done, {{(const void*)msda1d_bwd_value_kernel<1, false>, 96 * 1024},
                                    {(const void*)msda1d_bwd_value_kernel<2, false>, 96 * 1024},
                                    {(const void*)msda1d_bwd_value_kernel<1, true>, 96 * 1024},
                                    {(const void*)msda1d_bwd_value_kernel<1, true, 4>, 96 * 1024},
-                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, true>, 96 * 1024},
-                                   {(const void*)msda1d_bwd_value_kernel<1, true, 8, false, 0, 1>, 96 * 1024},
-                                   {(const void*)msda1d_bwd_value_kernel<1, true, 8, false, 0, 2>, 96 * 1024},
-                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, false, 0, 1>, 96 * 1024},
-                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, false, 0, 2>, 96 * 1024},
-                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, true, 0, 1>, 96 * 1024},
-                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, true, 0, 2>, 96 * 1024},
-                                   {(const void*)msda1d_bwd_value_kernel<1, true, 6, false, 0, 0>, 96 * 1024},
-                                   {(const void*)msda1d_bwd_value_kernel<1, true, 6, false, 0, 1>, 96 * 1024},
-                                   {(const void*)msda1d_bwd_value_kernel<1, true, 6, false, 0, 2>, 96 * 1024}},
+                                   {(const void*)msda1d_bwd_value_kernel<1, true, 4, true>, 96 * 1024}},
                             "msda1d_bwd_value_kernel")))
             return rc;
         for (int q0 = 0; q0 < num_query; q0 += qchunk) {
@@ -2755,17 +2577,10 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
             if (g4 && level_sums && lds < kVW * 16 * 16) lds = kVW * 16 * 16;  // the level-sum reduction
             float* gsums = g4 ? level_sums : nullptr;
             const int acc = q0 > 0;
-#define VAL_LAUNCH1(UGV, B16V, DEFV)                                                                                \
-    hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, UGV, B16V, 0, DEFV>), dim3((unsigned)nblk), dim3(kVW * 64), \
-                       lds, s, value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,     \
-                       save_attn, save_loc, grad_value, gsums, (const int64_t*)nullptr, (const int64_t*)nullptr, gv16)
-#define VAL_LAUNCH(UGV, B16V)                                               \
-    do {                                                                    \
-        if (vdef >= 2) VAL_LAUNCH1(UGV, B16V, 2);                           \
-        else if (vdef == 1) VAL_LAUNCH1(UGV, B16V, 1);                      \
-        else VAL_LAUNCH1(UGV, B16V, 0);                                     \
-    } while (0)
-            const int vdef = value_defer();
+#define VAL_LAUNCH(UGV, B16V)                                                                                       \
+    hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, UGV, B16V>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s, \
+                       value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output, save_attn,  \
+                       save_loc, grad_value, gsums, (const int64_t*)nullptr, (const int64_t*)nullptr, gv16)
             static const int vabl = [] {
                 const char* e = getenv("PDVC_VAL_ABLATE");
                 return e ? atoi(e) : 0;
@@ -2800,10 +2615,8 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
                                        (const int64_t*)nullptr, (const int64_t*)nullptr, gv16);
             } else if (g4 && gv16) VAL_LAUNCH(4, true);  // the bf16 stores spill the depth-8 walk (7 VGPRs): depth 4
             else if (g4 && value_ug(num_query, S) == 4) VAL_LAUNCH(4, false);
-            else if (g4 && value_ug(num_query, S) == 6) VAL_LAUNCH(6, false);
             else if (g4) VAL_LAUNCH(8, false);
 #undef VAL_LAUNCH
-#undef VAL_LAUNCH1
             else if (head_dim <= 64)
                 hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, false>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
                                    value_pad_mask, lv, num_query, q0, nq, S, num_heads, head_dim, acc, grad_output,
@@ -2889,8 +2702,7 @@ static int dropin_pyr_blocks(int S, int Lq, int per_block) {
     if (!on || 4L * Lq < S) return 0;
     static std::atomic<int> done[kMaxDevices];
     const bool attr = lds_optin(done, {{(const void*)msda_dropin_fwd_pyr_kernel, (int)kPyr2LdsMax},
-                                       {(const void*)msda_dropin_bwd_query_pyr_kernel<false>, (int)kPyrLds},
-                                       {(const void*)msda_dropin_bwd_query_pyr_kernel<true>, (int)kPyrLds}},
+                                       {(const void*)msda_dropin_bwd_query_pyr_kernel, (int)kPyrLds}},
                                 "msda_dropin pyramid kernels") == PDVC_OK;
     return attr ? (Lq + per_block - 1) / per_block : 0;
 }
@@ -2938,14 +2750,9 @@ int dropin1d_backward(const float* value, const int64_t* shapes, const int64_t* 
     int pyr_first = 0;
     if (const int qb = dropin_pyr_blocks(S, Lq, kBqQ)) {
         PDVC_CHECK_ARG((long)N * M * qb < (1L << 31), "too many query blocks");
-        if (bq_pf())
-            hipLaunchKernelGGL(msda_dropin_bwd_query_pyr_kernel<true>, dim3((unsigned)(N * M * qb)), dim3(kPyrThreads),
-                               kPyrLds, s, value, shapes, lsi, loc, attn, Lq, S, M, qb, gout, grad_loc, grad_attn,
-                               save_attn, save_loc);
-        else
-            hipLaunchKernelGGL(msda_dropin_bwd_query_pyr_kernel<false>, dim3((unsigned)(N * M * qb)), dim3(kPyrThreads),
-                               kPyrLds, s, value, shapes, lsi, loc, attn, Lq, S, M, qb, gout, grad_loc, grad_attn,
-                               save_attn, save_loc);
+        hipLaunchKernelGGL(msda_dropin_bwd_query_pyr_kernel, dim3((unsigned)(N * M * qb)), dim3(kPyrThreads), kPyrLds,
+                           s, value, shapes, lsi, loc, attn, Lq, S, M, qb, gout, grad_loc, grad_attn, save_attn,
+                           save_loc);
         PDVC_CHECK_LAUNCH("msda_dropin_bwd_query_pyr_kernel");
         pyr_first = 1;
     }
@@ -2958,10 +2765,8 @@ int dropin1d_backward(const float* value, const int64_t* shapes, const int64_t* 
     // value gradient: msda1d_bwd_value_kernel on the slab, its LDS sized for the longest possible level (S)
     static std::atomic<int> done[kMaxDevices];
     if (const int rc = lds_optin(done, {{(const void*)msda1d_bwd_value_kernel<1, true>, 96 * 1024},
-                                        {(const void*)msda1d_bwd_value_kernel<1, true, 4>, 96 * 1024},
-                                        {(const void*)msda1d_bwd_value_kernel<1, true, 4, false, 0, 2>, 96 * 1024},
-                                        {(const void*)msda1d_bwd_value_kernel<1, true, 6, false, 0, 2>, 96 * 1024}},
-                                 "msda1d_bwd_value_kernel (drop-in)"))
+                                        {(const void*)msda1d_bwd_value_kernel<1, true, 4>, 96 * 1024}},
+                                 "msda1d_bwd_value_kernel"))
         return rc;
     const long per_sample = 12;
     const long budget = 96 * 1024 - 8L * (S + 2) - 16;
@@ -2975,15 +2780,7 @@ int dropin1d_backward(const float* value, const int64_t* shapes, const int64_t* 
         const int nq = (Lq - q0) < qchunk ? (Lq - q0) : qchunk;
         const size_t lds = sizeof(int) * (2 * (size_t)(S + 2) + 3 * (size_t)nq * kP + 2);
         const int acc = q0 > 0;
-#define DROPIN_VAL(UGV, DEFV)                                                                                     \
-    hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, UGV, false, 0, DEFV>), dim3((unsigned)nblk), dim3(kVW * 64), \
-                       lds, s, nullptr, lv, Lq, q0, nq, S, M, 64, acc, gout, save_attn, save_loc, grad_value, nullptr, \
-                       shapes, lsi)
-        const int ug = value_ug(Lq, S);
-        if (value_defer() == 2 && ug == 4) DROPIN_VAL(4, 2);
-        else if (value_defer() == 2 && ug == 6) DROPIN_VAL(6, 2);
-#undef DROPIN_VAL
-        else if (ug == 4)
+        if (value_ug(Lq, S) == 4)
             hipLaunchKernelGGL((msda1d_bwd_value_kernel<1, true, 4>), dim3((unsigned)nblk), dim3(kVW * 64), lds, s,
                                nullptr, lv, Lq, q0, nq, S, M, 64, acc, gout, save_attn, save_loc, grad_value, nullptr,
                                shapes, lsi);
