@@ -749,10 +749,6 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_win_kernel(
     // level's phase) and for window B (level 0 rows [512, T0))
     int adA[kPyrQPS], adB[kPyrQPS];
     float w1v[kPyrQPS], w2v[kPyrQPS];
-    // per query: does any level-0 sample of the wave's 4 queries lie in window A / B (wave-uniform ballots)?  A wave's
-    // queries are 4 neighbouring positions, so their level-0 samples nearly always share one window: the other
-    // window's pass over them -- all 16 lanes reading the two zero rows -- is skipped
-    uint32_t inA_any = 0u, inB_any = 0u;  // bit i: query i
 #pragma unroll
     for (int i = 0; i < kPyrQPS; ++i) {
         const int q = qb * kPyrQ + slot + 64 * i;
@@ -786,8 +782,6 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_win_kernel(
         const bool inB = l_own == 0 && i0 >= kWinSplit;
         adA[i] = inB ? kWinZero * 256 : ad;
         adB[i] = inB ? ad - kWinSplit * 256 : kWinZero * 256;
-        inA_any |= (uint32_t)(__builtin_amdgcn_ballot_w64(l_own == 0 && !inB) != 0) << i;
-        inB_any |= (uint32_t)(__builtin_amdgcn_ballot_w64(inB) != 0) << i;
     }
     PAcc4 acc[kPyrQPS];
 #pragma unroll
@@ -798,7 +792,6 @@ __global__ __launch_bounds__(kPyrThreads) void msda1d_fwd_win_kernel(
         constexpr bool B = decltype(Bc)::value;
 #pragma unroll
         for (int i = 0; i < kPyrQPS; ++i) {
-            if (L == 0 && !(((B ? inB_any : inA_any) >> i) & 1u)) continue;  // uniform: none of the wave's in this window
             pf4 v1[kP], v2[kP];
             float c1[kP], c2[kP];
             int ad = B ? adB[i] : adA[i];
