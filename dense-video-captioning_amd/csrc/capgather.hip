@@ -52,10 +52,10 @@ __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __rest
                                                               const float* __restrict__ ref, int rd1_rows,
                                                               CapLevels lv, int S, int M, int D, int waves_per_row,
                                                               int total_waves, float* __restrict__ samples,
-                                                              float* __restrict__ save_loc) {
+                                                              float* __restrict__ save_loc, int remap) {
     constexpr int HPW = 64 / LPH;
     const int lane = threadIdx.x & 63;
-    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int wave = (remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x) * 4 + (threadIdx.x >> 6);
     if (wave >= total_waves) return;
     const int r = wave / waves_per_row;
     const int wr = wave - r * waves_per_row;
@@ -119,10 +119,10 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
     const float* __restrict__ ref, int rd1_rows, CapLevels lv, int S, int M, int D, int waves_per_row,
     int total_waves, const float* __restrict__ save_loc,
     const float* __restrict__ gsamp, float* __restrict__ grad_value, float* __restrict__ grad_off,
-    float* __restrict__ grad_ref, const float* __restrict__ value2, const float* __restrict__ gsamp2) {
+    float* __restrict__ grad_ref, const float* __restrict__ value2, const float* __restrict__ gsamp2, int remap) {
     constexpr int HPW = 64 / LPH;
     const int lane = threadIdx.x & 63;
-    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int wave = (remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x) * 4 + (threadIdx.x >> 6);
     if (wave >= total_waves) return;
     const int r = wave / waves_per_row;
     const int wr = wave - r * waves_per_row;
@@ -438,6 +438,17 @@ __global__ __launch_bounds__(kCVW * 64) void cap_value_grad_kernel(
     }
 }
 
+// XCD-aware wave order (PDVC_CAP_XCD=0: the dispatch order, A/B): a video's caption rows are consecutive in every
+// layout (pdvc/batch_layout.py), so with xcd_remap its waves run on one XCD, together, and the corner rows its events
+// and points share (the coarse levels above all) come from that XCD's L2
+static int cap_remap() {
+    static const int on = [] {
+        const char* e = getenv("PDVC_CAP_XCD");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return on;
+}
+
 static int cap_setup(const int32_t* level_T, int num_levels, int num_point, int head_dim, int num_heads, int ref_dim,
                      CapLevels& lv, int& S, int& lph, int& wpr) {
     PDVC_CHECK_ARG(level_T != nullptr, "level_T must not be NULL");
@@ -492,10 +503,10 @@ extern "C" int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* va
     hipStream_t s = (hipStream_t)stream;
     if (ref_dim == 1) {
         CAP_DISPATCH(cap_gather_fwd_kernel, 1, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
-                     off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc)
+                     off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc, cap_remap())
     } else {
         CAP_DISPATCH(cap_gather_fwd_kernel, 2, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
-                     off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc)
+                     off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc, cap_remap())
     }
     PDVC_CHECK_LAUNCH("cap_gather_fwd_kernel");
     return PDVC_OK;
@@ -522,11 +533,11 @@ extern "C" int pdvc_cap_gather_backward2_f32(const float* value, const uint8_t* 
     if (ref_dim == 1) {
         CAP_DISPATCH(cap_gather_bwd_kernel, 1, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
                      off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples,
-                     grad_value, grad_offsets, grad_ref, value2, grad_samples2)
+                     grad_value, grad_offsets, grad_ref, value2, grad_samples2, cap_remap())
     } else {
         CAP_DISPATCH(cap_gather_bwd_kernel, 2, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
                      off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples,
-                     grad_value, grad_offsets, grad_ref, value2, grad_samples2)
+                     grad_value, grad_offsets, grad_ref, value2, grad_samples2, cap_remap())
     }
     PDVC_CHECK_LAUNCH("cap_gather_bwd_kernel");
     return PDVC_OK;
