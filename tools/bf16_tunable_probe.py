@@ -44,6 +44,15 @@ def main():
         cases.append((name, A, B, 2.0 * sa[0] * sa[1] * sb[1]))
     op = torch.ops.aten.mm.dtype
     res = {}
+    # the split-K form the step uses for weight gradients (pdvc/ops/functions/linear.py wgrad_mm), bf16 operands
+    sys.path[:0] = [os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dense-video-captioning_amd")]
+    from pdvc.ops.functions.linear import wgrad_splits
+    s_ = wgrad_splits(R)
+    gy = torch.randn(R, 512, device=dev).to(torch.bfloat16)
+    x = torch.randn(R, 512, device=dev).to(torch.bfloat16)
+    bop = torch.ops.aten.bmm.dtype
+    t = timeit(lambda: bop(gy.reshape(s_, R // s_, 512).transpose(1, 2), x.reshape(s_, R // s_, 512), torch.float32).sum(0))
+    print(f"split-K wgrad 512x512 over {s_} chunks: {t * 1e3:8.3f} ms  {2.0 * R * 512 * 512 / t / 1e12:7.1f} TF/s", flush=True)
     for name, A, B, fl in cases:
         t = timeit(lambda: op(A, B, torch.float32))
         res[name] = [t]
@@ -58,7 +67,6 @@ def main():
     for name, A, B, fl in cases:
         op(A, B, torch.float32)
         torch.cuda.synchronize()
-    tun.write_file()
     tun.tuning_enable(False)
     for name, A, B, fl in cases:
         t = timeit(lambda: op(A, B, torch.float32))
