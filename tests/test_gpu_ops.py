@@ -602,6 +602,66 @@ def test_cap_gather_vs_oracle(D, M, ref_dim):
     close(rf.grad, exp_gr, 1e-4, "grad_ref")
 
 
+@pytest.mark.parametrize("D,M", [(64, 8), (32, 2), (128, 3)])
+@pytest.mark.parametrize("ref_dim", [1, 2])
+@pytest.mark.parametrize("masked", [False, True])
+def test_cap_gather_diff_matches_gathering_backward(D, M, ref_dim, masked):
+    """pdvc_cap_gather_forward2_f32 / pdvc_cap_gather_backward_diff_f32 (the caption decoder's default with the value
+    gradient deferred) against pdvc_cap_gather_forward_f32 / pdvc_cap_gather_backward_f32 with grad_value NULL: the
+    same samples and save_loc, and the same offset and reference gradients, bit for bit (same operations, same order;
+    grad_ref by atomics is compared to 1e-6)."""
+    from pdvc import _native as _n
+    rng = np.random.RandomState(D + M + 10 * ref_dim + 100 * masked)
+    T_l = [24, 12, 6, 3]
+    S, N, R = sum(T_l), 3, 13
+    value = cu(rng.randn(N, S, M, D), torch.float32)
+    mask = None
+    if masked:
+        mk = np.zeros((N, S), np.uint8)
+        mk[1, 5:9] = 1
+        mk[2, 30:33] = 1
+        mask = cu(mk)
+    row_video = cu(rng.randint(0, N, size=R).astype(np.int32))
+    off_stride = M * 16 + 5
+    offsets = cu(rng.randn(R, off_stride) * 3.0, torch.float32)
+    off_add = cu(rng.randn(R, M * 16) * 0.5, torch.float32)
+    if ref_dim == 1:
+        ref = cu(rng.uniform(-0.1, 1.1, size=(R, 4, 1)), torch.float32)
+    else:
+        ref = cu(np.concatenate([rng.uniform(0, 1, size=(R, 4, 1)), rng.uniform(0.05, 0.9, size=(R, 4, 1))], -1),
+                 torch.float32)
+    rd1 = 4 if ref_dim == 2 else 0
+    lvl = _n.int_array(T_l)
+    gs = cu(rng.randn(R, M, 16, D), torch.float32)
+    outs = []
+    for diff in (False, True):
+        samples = torch.empty(R, M, 16, D, device=DEV)
+        loc = torch.empty(R, M, 16, device=DEV)
+        sd = torch.empty(R, M, 16, D, device=DEV) if diff else None
+        head = (_n.ptr(value), _n.ptr(mask), _n.ptr(row_video), _n.ptr(offsets), off_stride, 5, _n.ptr(off_add),
+                _n.ptr(ref), ref_dim, rd1, lvl, 4, N, R, M, D, 4)
+        if diff:
+            _n.call("pdvc_cap_gather_forward2_f32", *head, _n.ptr(samples), _n.ptr(loc), _n.ptr(sd), _n.stream())
+        else:
+            _n.call("pdvc_cap_gather_forward_f32", *head, _n.ptr(samples), _n.ptr(loc), _n.stream())
+        go = torch.zeros(R, off_stride, device=DEV)
+        gr = torch.zeros(R, 4, ref_dim, device=DEV)
+        if diff:
+            _n.call("pdvc_cap_gather_backward_diff_f32", _n.ptr(sd), _n.ptr(offsets), off_stride, 5, _n.ptr(off_add),
+                    _n.ptr(ref), ref_dim, rd1, lvl, 4, N, R, M, D, 4, _n.ptr(loc), _n.ptr(gs), _n.ptr(go), _n.ptr(gr),
+                    _n.stream())
+        else:
+            _n.call("pdvc_cap_gather_backward_f32", *head, _n.ptr(loc), _n.ptr(gs), None, _n.ptr(go), _n.ptr(gr),
+                    _n.stream())
+        torch.cuda.synchronize()
+        outs.append((samples, loc, go, gr))
+    (s0, l0, go0, gr0), (s1, l1, go1, gr1) = outs
+    assert torch.equal(s0, s1) and torch.equal(l0, l1)
+    assert torch.equal(go0, go1), (go0 - go1).abs().max().item()
+    assert (gr0 - gr1).abs().max().item() <= 1e-6 * (gr0.abs().max().item() + 1.0)
+    assert go0[:, 5:].abs().sum().item() > 0 and gr0.abs().sum().item() > 0
+
+
 # ------------------------------------------------------------------------------------------------
 # modules vs golden vectors generated from the reference modules
 # ------------------------------------------------------------------------------------------------
