@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
     int total_waves, const float* __restrict__ save_loc,
     const float* __restrict__ gsamp, float* __restrict__ grad_value, float* __restrict__ grad_off,
     float* __restrict__ grad_ref, const float* __restrict__ value2, const float* __restrict__ gsamp2, int remap,
-    const float* __restrict__ sdiff) {
+    const float* __restrict__ sdiff, const float* __restrict__ sdiff2) {
     constexpr int HPW = 64 / LPH;
     const int lane = threadIdx.x & 63;
     const int wave = (remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x) * 4 + (threadIdx.x >> 6);
@@ -208,6 +208,19 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
             else s += gv * ((ok1[u] ? v1[u][c] : 0.f) - (ok0[u] ? v0[u][c] : 0.f));  // gix = -vnw + vne
         }
         part[u] = s;
+    }
+    if (DIFF && gsamp2) {  // the second tensor's saved differences: (x0 + 1 row, 0 past the level) - (x0 row)
+#pragma unroll
+        for (int u = 0; u < kSPW; ++u) {
+            const size_t si = (((size_t)r * M + m) * cNS + j0 + u) * D + c0;
+            float s2 = 0.f;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const float gv = active ? gsamp2[si + LPH * c] : 0.f;
+                s2 += gv * sdiff2[si + LPH * c];
+            }
+            part[u] += s2;
+        }
     }
     if (!DIFF && value2) {  // a second sampled tensor at the same locations (no padding mask): its location gradient adds in
         const float* v2base = value2 + (size_t)b * S * MD + (size_t)m * D + c0;
@@ -567,11 +580,11 @@ extern "C" int pdvc_cap_gather_backward2_f32(const float* value, const uint8_t* 
     if (ref_dim == 1) {
         CAP_DISPATCH(cap_gather_bwd_kernel, 1, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
                      off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples,
-                     grad_value, grad_offsets, grad_ref, value2, grad_samples2, cap_remap(), (const float*)nullptr)
+                     grad_value, grad_offsets, grad_ref, value2, grad_samples2, cap_remap(), (const float*)nullptr, (const float*)nullptr)
     } else {
         CAP_DISPATCH(cap_gather_bwd_kernel, 2, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
                      off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples,
-                     grad_value, grad_offsets, grad_ref, value2, grad_samples2, cap_remap(), (const float*)nullptr)
+                     grad_value, grad_offsets, grad_ref, value2, grad_samples2, cap_remap(), (const float*)nullptr, (const float*)nullptr)
     }
     PDVC_CHECK_LAUNCH("cap_gather_bwd_kernel");
     return PDVC_OK;
@@ -593,7 +606,8 @@ extern "C" int pdvc_cap_gather_backward_diff_f32(const float* sample_diff, const
                                                  int rd1_rows, const int32_t* level_T, int num_levels, int batch,
                                                  int rows, int num_heads, int head_dim, int num_point,
                                                  const float* save_loc, const float* grad_samples, float* grad_offsets,
-                                                 float* grad_ref, void* stream) {
+                                                 float* grad_ref, const float* sample_diff2,
+                                                 const float* grad_samples2, void* stream) {
     CapLevels lv;
     int S, lph, wpr;
     int rc = cap_setup(level_T, num_levels, num_point, head_dim, num_heads, ref_dim, lv, S, lph, wpr);
@@ -602,6 +616,8 @@ extern "C" int pdvc_cap_gather_backward_diff_f32(const float* sample_diff, const
                    "the diff backward needs sample_diff, save_loc and grad_samples");
     PDVC_CHECK_ARG(off_col0 >= 0 && off_col0 + num_heads * cNS <= off_stride, "offset columns out of range");
     PDVC_CHECK_ARG(batch >= 0 && rows >= 0, "negative sizes");
+    PDVC_CHECK_ARG((sample_diff2 == nullptr) == (grad_samples2 == nullptr),
+                   "sample_diff2 and grad_samples2 go together");
     hipStream_t s = (hipStream_t)stream;
     const long tw = (long)rows * wpr;
     if (tw == 0) return PDVC_OK;
@@ -613,11 +629,11 @@ extern "C" int pdvc_cap_gather_backward_diff_f32(const float* sample_diff, const
     if (ref_dim == 1) {
         CAP_DISPATCH_DIFF(1, grid, s, nf, nm, nr, offsets, off_stride, off_col0, off_add, ref, rd1_rows, lv, S,
                           num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples, ng, grad_offsets, grad_ref, nf,
-                          nf, cap_remap(), sample_diff)
+                          grad_samples2, cap_remap(), sample_diff, sample_diff2)
     } else {
         CAP_DISPATCH_DIFF(2, grid, s, nf, nm, nr, offsets, off_stride, off_col0, off_add, ref, rd1_rows, lv, S,
                           num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples, ng, grad_offsets, grad_ref, nf,
-                          nf, cap_remap(), sample_diff)
+                          grad_samples2, cap_remap(), sample_diff, sample_diff2)
     }
     PDVC_CHECK_LAUNCH("cap_gather_bwd_kernel (diff)");
     return PDVC_OK;

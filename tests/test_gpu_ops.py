@@ -605,16 +605,19 @@ def test_cap_gather_vs_oracle(D, M, ref_dim):
 @pytest.mark.parametrize("D,M", [(64, 8), (32, 2), (128, 3)])
 @pytest.mark.parametrize("ref_dim", [1, 2])
 @pytest.mark.parametrize("masked", [False, True])
-def test_cap_gather_diff_matches_gathering_backward(D, M, ref_dim, masked):
+@pytest.mark.parametrize("second", [False, True])
+def test_cap_gather_diff_matches_gathering_backward(D, M, ref_dim, masked, second):
     """pdvc_cap_gather_forward2_f32 / pdvc_cap_gather_backward_diff_f32 (the caption decoder's default with the value
-    gradient deferred) against pdvc_cap_gather_forward_f32 / pdvc_cap_gather_backward_f32 with grad_value NULL: the
-    same samples and save_loc, and the same offset and reference gradients, bit for bit (same operations, same order;
-    grad_ref by atomics is compared to 1e-6)."""
+    gradient deferred) against pdvc_cap_gather_forward_f32 / pdvc_cap_gather_backward_f32 with grad_value NULL -- or,
+    with `second`, pdvc_cap_gather_backward2_f32 with a second tensor sampled at the same locations (the ctx2att rows
+    U, gathered without a mask): the same samples and save_loc, and the same offset gradients bit for bit (same
+    operations, same order); grad_ref, summed by atomics, to 1e-6."""
     from pdvc import _native as _n
-    rng = np.random.RandomState(D + M + 10 * ref_dim + 100 * masked)
+    rng = np.random.RandomState(D + M + 10 * ref_dim + 100 * masked + 1000 * second)
     T_l = [24, 12, 6, 3]
     S, N, R = sum(T_l), 3, 13
     value = cu(rng.randn(N, S, M, D), torch.float32)
+    U = cu(rng.randn(N, S, M, D), torch.float32) if second else None
     mask = None
     if masked:
         mk = np.zeros((N, S), np.uint8)
@@ -633,30 +636,45 @@ def test_cap_gather_diff_matches_gathering_backward(D, M, ref_dim, masked):
     rd1 = 4 if ref_dim == 2 else 0
     lvl = _n.int_array(T_l)
     gs = cu(rng.randn(R, M, 16, D), torch.float32)
+    gs2 = cu(rng.randn(R, M, 16, D), torch.float32) if second else None
     outs = []
     for diff in (False, True):
         samples = torch.empty(R, M, 16, D, device=DEV)
+        samples2 = torch.empty(R, M, 16, D, device=DEV)
         loc = torch.empty(R, M, 16, device=DEV)
         sd = torch.empty(R, M, 16, D, device=DEV) if diff else None
-        head = (_n.ptr(value), _n.ptr(mask), _n.ptr(row_video), _n.ptr(offsets), off_stride, 5, _n.ptr(off_add),
-                _n.ptr(ref), ref_dim, rd1, lvl, 4, N, R, M, D, 4)
+        sd2 = torch.empty(R, M, 16, D, device=DEV) if (diff and second) else None
+        geo = (_n.ptr(row_video), _n.ptr(offsets), off_stride, 5, _n.ptr(off_add), _n.ptr(ref), ref_dim, rd1, lvl, 4,
+               N, R, M, D, 4)
         if diff:
-            _n.call("pdvc_cap_gather_forward2_f32", *head, _n.ptr(samples), _n.ptr(loc), _n.ptr(sd), _n.stream())
+            _n.call("pdvc_cap_gather_forward2_f32", _n.ptr(value), _n.ptr(mask), *geo, _n.ptr(samples), _n.ptr(loc),
+                    _n.ptr(sd), _n.stream())
+            if second:
+                _n.call("pdvc_cap_gather_forward2_f32", _n.ptr(U), None, *geo, _n.ptr(samples2), None, _n.ptr(sd2),
+                        _n.stream())
         else:
-            _n.call("pdvc_cap_gather_forward_f32", *head, _n.ptr(samples), _n.ptr(loc), _n.stream())
+            _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(mask), *geo, _n.ptr(samples), _n.ptr(loc),
+                    _n.stream())
+            if second:
+                _n.call("pdvc_cap_gather_forward_f32", _n.ptr(U), None, *geo, _n.ptr(samples2), None, _n.stream())
         go = torch.zeros(R, off_stride, device=DEV)
         gr = torch.zeros(R, 4, ref_dim, device=DEV)
         if diff:
             _n.call("pdvc_cap_gather_backward_diff_f32", _n.ptr(sd), _n.ptr(offsets), off_stride, 5, _n.ptr(off_add),
                     _n.ptr(ref), ref_dim, rd1, lvl, 4, N, R, M, D, 4, _n.ptr(loc), _n.ptr(gs), _n.ptr(go), _n.ptr(gr),
-                    _n.stream())
+                    _n.ptr(sd2), _n.ptr(gs2), _n.stream())
+        elif second:
+            _n.call("pdvc_cap_gather_backward2_f32", _n.ptr(value), _n.ptr(mask), *geo, _n.ptr(loc), _n.ptr(gs), None,
+                    _n.ptr(go), _n.ptr(gr), _n.ptr(U), _n.ptr(gs2), _n.stream())
         else:
-            _n.call("pdvc_cap_gather_backward_f32", *head, _n.ptr(loc), _n.ptr(gs), None, _n.ptr(go), _n.ptr(gr),
-                    _n.stream())
+            _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(mask), *geo, _n.ptr(loc), _n.ptr(gs), None,
+                    _n.ptr(go), _n.ptr(gr), _n.stream())
         torch.cuda.synchronize()
-        outs.append((samples, loc, go, gr))
-    (s0, l0, go0, gr0), (s1, l1, go1, gr1) = outs
+        outs.append((samples, samples2 if second else None, loc, go, gr))
+    (s0, u0, l0, go0, gr0), (s1, u1, l1, go1, gr1) = outs
     assert torch.equal(s0, s1) and torch.equal(l0, l1)
+    if second:
+        assert torch.equal(u0, u1)
     assert torch.equal(go0, go1), (go0 - go1).abs().max().item()
     assert (gr0 - gr1).abs().max().item() <= 1e-6 * (gr0.abs().max().item() + 1.0)
     assert go0[:, 5:].abs().sum().item() > 0 and gr0.abs().sum().item() > 0
