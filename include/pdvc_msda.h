@@ -241,7 +241,7 @@ int pdvc_cap_gather_forward2_f32(const float* value, const uint8_t* value_pad_ma
 /* The offset and reference gradients of pdvc_cap_gather_backward_f32 (grad_value NULL) -- or, with sample_diff2 and
  * grad_samples2, of pdvc_cap_gather_backward2_f32 (the second tensor's differences from its own forward2 call, made
  * without a padding mask) -- from the forward's sample_diff: no value rows are read; grad_ref is ACCUMULATED as
- * there.  The same floating-point operations in the same order: the same bits. */
+ * there.  The same floating-point operations in the same order (results within an ulp of the gathering form). */
 int pdvc_cap_gather_backward_diff_f32(const float* sample_diff, const float* offsets, int off_stride, int off_col0,
                                       const float* off_add, const float* ref, int ref_dim, int rd1_rows,
                                       const int32_t* level_T, int num_levels, int batch, int rows, int num_heads,
