@@ -52,8 +52,7 @@ __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __rest
                                                               const float* __restrict__ ref, int rd1_rows,
                                                               CapLevels lv, int S, int M, int D, int waves_per_row,
                                                               int total_waves, float* __restrict__ samples,
-                                                              float* __restrict__ save_loc, int remap,
-                                                              float* __restrict__ sdiff) {
+                                                              float* __restrict__ save_loc, int remap) {
     constexpr int HPW = 64 / LPH;
     const int lane = threadIdx.x & 63;
     const int wave = (remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x) * 4 + (threadIdx.x >> 6);
@@ -110,26 +109,17 @@ __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __rest
         for (int c = 0; c < CPL; ++c)
             o.v[c] = (ok0[u] ? v0[u].v[c] : 0.f) * nw[u] + (ok1[u] ? v1[u].v[c] : 0.f) * ne[u];
         o.store(samples + (((size_t)r * M + m) * cNS + j0 + u) * D + c0);
-        if (sdiff) {  // the backward's location term: the masked corner difference, the same subtraction it would do
-            VecF<CPL> dd;
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) dd.v[c] = (ok1[u] ? v1[u].v[c] : 0.f) - (ok0[u] ? v0[u].v[c] : 0.f);
-            dd.store(sdiff + (((size_t)r * M + m) * cNS + j0 + u) * D + c0);
-        }
     }
 }
 
-// DIFF: the forward's saved corner differences (sdiff) replace the two corner-row gathers; no value gradient (the
-// caller defers it to cap_value_grad_kernel) and no second sampled tensor
-template <int CPL, int LPH, int RD, bool DIFF = false>
+template <int CPL, int LPH, int RD>
 __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const int32_t* __restrict__ row_video,
     const float* __restrict__ offsets, int off_stride, int off_col0, const float* __restrict__ off_add,
     const float* __restrict__ ref, int rd1_rows, CapLevels lv, int S, int M, int D, int waves_per_row,
     int total_waves, const float* __restrict__ save_loc,
     const float* __restrict__ gsamp, float* __restrict__ grad_value, float* __restrict__ grad_off,
-    float* __restrict__ grad_ref, const float* __restrict__ value2, const float* __restrict__ gsamp2, int remap,
-    const float* __restrict__ sdiff, const float* __restrict__ sdiff2) {
+    float* __restrict__ grad_ref, const float* __restrict__ value2, const float* __restrict__ gsamp2, int remap) {
     constexpr int HPW = 64 / LPH;
     const int lane = threadIdx.x & 63;
     const int wave = (remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x) * 4 + (threadIdx.x >> 6);
@@ -146,11 +136,11 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
     // lane-strided channels (sub + LPH*c): every atomic wave-instruction adds one contiguous LPH*4-byte
     // segment per head (256 B at D = 512), the shape global float atomics run at full rate with
     const int c0 = sub;
-    const int b = DIFF ? 0 : row_video[r];
+    const int b = row_video[r];
     const size_t MD = (size_t)M * D;
-    const float* vbase = DIFF ? nullptr : value + (size_t)b * S * MD + (size_t)m * D + c0;
-    float* gvbase = (DIFF || !grad_value) ? nullptr : grad_value + (size_t)b * S * MD + (size_t)m * D + c0;
-    const uint8_t* mbase = (!DIFF && vmask) ? vmask + (size_t)b * S : nullptr;
+    const float* vbase = value + (size_t)b * S * MD + (size_t)m * D + c0;
+    float* gvbase = grad_value + (size_t)b * S * MD + (size_t)m * D + c0;
+    const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
     const int T = lv.T[0] * (l == 0) + lv.T[1] * (l == 1) + lv.T[2] * (l == 2) + lv.T[3] * (l == 3);
     const int st = lv.start[0] * (l == 0) + lv.start[1] * (l == 1) + lv.start[2] * (l == 2) + lv.start[3] * (l == 3);
 
@@ -170,28 +160,17 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
 #pragma unroll
     for (int u = 0; u < kSPW; ++u) {
         const int a1 = min(x0[u] + 1, T - 1);
-        const size_t si = (((size_t)r * M + m) * cNS + j0 + u) * D + c0;
-        const float* gp = gsamp + si;
-        if constexpr (DIFF) {  // v1 holds the saved difference, v0 is unused
+        const float* gp = gsamp + (((size_t)r * M + m) * cNS + j0 + u) * D + c0;
+        const float* p0 = vbase + (size_t)(st + x0[u]) * MD;
+        const float* p1 = vbase + (size_t)(st + a1) * MD;
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                g[u][c] = gp[LPH * c];
-                v1[u][c] = sdiff[si + LPH * c];
-                v0[u][c] = 0.f;
-            }
-            ok0[u] = ok1[u] = active;
-        } else {
-            const float* p0 = vbase + (size_t)(st + x0[u]) * MD;
-            const float* p1 = vbase + (size_t)(st + a1) * MD;
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                g[u][c] = gp[LPH * c];
-                v0[u][c] = p0[LPH * c];
-                v1[u][c] = p1[LPH * c];
-            }
-            ok0[u] = active && !(mbase && mbase[st + x0[u]]);
-            ok1[u] = active && x0[u] + 1 < T && !(mbase && mbase[st + a1]);
+        for (int c = 0; c < CPL; ++c) {
+            g[u][c] = gp[LPH * c];
+            v0[u][c] = p0[LPH * c];
+            v1[u][c] = p1[LPH * c];
         }
+        ok0[u] = active && !(mbase && mbase[st + x0[u]]);
+        ok1[u] = active && x0[u] + 1 < T && !(mbase && mbase[st + a1]);
     }
     float part[kSPW];
 #pragma unroll
@@ -200,29 +179,15 @@ __global__ __launch_bounds__(256) void cap_gather_bwd_kernel(
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const float gv = active ? g[u][c] : 0.f;
-            if (!DIFF && gvbase) {  // NULL: the value gradient comes from cap_value_grad_kernel after all steps
+            if (grad_value) {  // NULL: the value gradient comes from cap_value_grad_kernel after all steps
                 if (ok0[u]) atomicAdd(gvbase + (size_t)(st + x0[u]) * MD + LPH * c, nw[u] * gv);
                 if (ok1[u]) atomicAdd(gvbase + (size_t)(st + x0[u] + 1) * MD + LPH * c, ne[u] * gv);
             }
-            if constexpr (DIFF) s += gv * v1[u][c];  // the forward's (ok1 ? v1 : 0) - (ok0 ? v0 : 0)
-            else s += gv * ((ok1[u] ? v1[u][c] : 0.f) - (ok0[u] ? v0[u][c] : 0.f));  // gix = -vnw + vne
+            s += gv * ((ok1[u] ? v1[u][c] : 0.f) - (ok0[u] ? v0[u][c] : 0.f));  // gix = -vnw + vne
         }
         part[u] = s;
     }
-    if (DIFF && gsamp2) {  // the second tensor's saved differences: (x0 + 1 row, 0 past the level) - (x0 row)
-#pragma unroll
-        for (int u = 0; u < kSPW; ++u) {
-            const size_t si = (((size_t)r * M + m) * cNS + j0 + u) * D + c0;
-            float s2 = 0.f;
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                const float gv = active ? gsamp2[si + LPH * c] : 0.f;
-                s2 += gv * sdiff2[si + LPH * c];
-            }
-            part[u] += s2;
-        }
-    }
-    if (!DIFF && value2) {  // a second sampled tensor at the same locations (no padding mask): its location gradient adds in
+    if (value2) {  // a second sampled tensor at the same locations (no padding mask): its location gradient adds in
         const float* v2base = value2 + (size_t)b * S * MD + (size_t)m * D + c0;
 #pragma unroll
         for (int u = 0; u < kSPW; ++u) {
@@ -520,12 +485,12 @@ using namespace pdvc;
         default: hipLaunchKernelGGL((KERNEL<8, 64, RD>), grid, dim3(256), 0, s, __VA_ARGS__); break;            \
     }
 
-extern "C" int pdvc_cap_gather_forward2_f32(const float* value, const uint8_t* value_pad_mask,
-                                            const int32_t* row_video, const float* offsets, int off_stride,
-                                            int off_col0, const float* off_add, const float* ref, int ref_dim,
-                                            int rd1_rows, const int32_t* level_T, int num_levels, int batch, int rows,
-                                            int num_heads, int head_dim, int num_point, float* samples,
-                                            float* save_loc, float* sample_diff, void* stream) {
+extern "C" int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* value_pad_mask, const int32_t* row_video,
+                                           const float* offsets, int off_stride, int off_col0, const float* off_add,
+                                           const float* ref,
+                                           int ref_dim, int rd1_rows, const int32_t* level_T, int num_levels, int batch, int rows,
+                                           int num_heads, int head_dim, int num_point, float* samples, float* save_loc,
+                                           void* stream) {
     CapLevels lv;
     int S, lph, wpr;
     int rc = cap_setup(level_T, num_levels, num_point, head_dim, num_heads, ref_dim, lv, S, lph, wpr);
@@ -538,25 +503,13 @@ extern "C" int pdvc_cap_gather_forward2_f32(const float* value, const uint8_t* v
     hipStream_t s = (hipStream_t)stream;
     if (ref_dim == 1) {
         CAP_DISPATCH(cap_gather_fwd_kernel, 1, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
-                     off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc, cap_remap(),
-                     sample_diff)
+                     off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc, cap_remap())
     } else {
         CAP_DISPATCH(cap_gather_fwd_kernel, 2, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
-                     off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc, cap_remap(),
-                     sample_diff)
+                     off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc, cap_remap())
     }
     PDVC_CHECK_LAUNCH("cap_gather_fwd_kernel");
     return PDVC_OK;
-}
-
-extern "C" int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* value_pad_mask, const int32_t* row_video,
-                                           const float* offsets, int off_stride, int off_col0, const float* off_add,
-                                           const float* ref, int ref_dim, int rd1_rows, const int32_t* level_T,
-                                           int num_levels, int batch, int rows, int num_heads, int head_dim,
-                                           int num_point, float* samples, float* save_loc, void* stream) {
-    return pdvc_cap_gather_forward2_f32(value, value_pad_mask, row_video, offsets, off_stride, off_col0, off_add, ref,
-                                        ref_dim, rd1_rows, level_T, num_levels, batch, rows, num_heads, head_dim,
-                                        num_point, samples, save_loc, nullptr, stream);
 }
 
 extern "C" int pdvc_cap_gather_backward2_f32(const float* value, const uint8_t* value_pad_mask,
@@ -580,62 +533,13 @@ extern "C" int pdvc_cap_gather_backward2_f32(const float* value, const uint8_t* 
     if (ref_dim == 1) {
         CAP_DISPATCH(cap_gather_bwd_kernel, 1, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
                      off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples,
-                     grad_value, grad_offsets, grad_ref, value2, grad_samples2, cap_remap(), (const float*)nullptr, (const float*)nullptr)
+                     grad_value, grad_offsets, grad_ref, value2, grad_samples2, cap_remap())
     } else {
         CAP_DISPATCH(cap_gather_bwd_kernel, 2, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
                      off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples,
-                     grad_value, grad_offsets, grad_ref, value2, grad_samples2, cap_remap(), (const float*)nullptr, (const float*)nullptr)
+                     grad_value, grad_offsets, grad_ref, value2, grad_samples2, cap_remap())
     }
     PDVC_CHECK_LAUNCH("cap_gather_bwd_kernel");
-    return PDVC_OK;
-}
-
-#define CAP_DISPATCH_DIFF(RD, grid, s, ...)                                                                        \
-    switch (lph) {                                                                                                 \
-        case 4: hipLaunchKernelGGL((cap_gather_bwd_kernel<8, 4, RD, true>), grid, dim3(256), 0, s, __VA_ARGS__); break;   \
-        case 8: hipLaunchKernelGGL((cap_gather_bwd_kernel<8, 8, RD, true>), grid, dim3(256), 0, s, __VA_ARGS__); break;   \
-        case 16: hipLaunchKernelGGL((cap_gather_bwd_kernel<8, 16, RD, true>), grid, dim3(256), 0, s, __VA_ARGS__); break; \
-        case 32: hipLaunchKernelGGL((cap_gather_bwd_kernel<8, 32, RD, true>), grid, dim3(256), 0, s, __VA_ARGS__); break; \
-        default: hipLaunchKernelGGL((cap_gather_bwd_kernel<8, 64, RD, true>), grid, dim3(256), 0, s, __VA_ARGS__); break; \
-    }
-
-// the backward from the forward's saved corner differences (pdvc_cap_gather_forward2_f32's sample_diff): offset and
-// reference gradients only -- the value gradient is the caller's cap_value_grad pass; no value rows are read
-extern "C" int pdvc_cap_gather_backward_diff_f32(const float* sample_diff, const float* offsets, int off_stride,
-                                                 int off_col0, const float* off_add, const float* ref, int ref_dim,
-                                                 int rd1_rows, const int32_t* level_T, int num_levels, int batch,
-                                                 int rows, int num_heads, int head_dim, int num_point,
-                                                 const float* save_loc, const float* grad_samples, float* grad_offsets,
-                                                 float* grad_ref, const float* sample_diff2,
-                                                 const float* grad_samples2, void* stream) {
-    CapLevels lv;
-    int S, lph, wpr;
-    int rc = cap_setup(level_T, num_levels, num_point, head_dim, num_heads, ref_dim, lv, S, lph, wpr);
-    if (rc) return rc;
-    PDVC_CHECK_ARG(sample_diff != nullptr && save_loc != nullptr && grad_samples != nullptr,
-                   "the diff backward needs sample_diff, save_loc and grad_samples");
-    PDVC_CHECK_ARG(off_col0 >= 0 && off_col0 + num_heads * cNS <= off_stride, "offset columns out of range");
-    PDVC_CHECK_ARG(batch >= 0 && rows >= 0, "negative sizes");
-    PDVC_CHECK_ARG((sample_diff2 == nullptr) == (grad_samples2 == nullptr),
-                   "sample_diff2 and grad_samples2 go together");
-    hipStream_t s = (hipStream_t)stream;
-    const long tw = (long)rows * wpr;
-    if (tw == 0) return PDVC_OK;
-    dim3 grid((unsigned)((tw + 3) / 4));
-    const float* nf = nullptr;
-    const uint8_t* nm = nullptr;
-    const int32_t* nr = nullptr;
-    float* ng = nullptr;
-    if (ref_dim == 1) {
-        CAP_DISPATCH_DIFF(1, grid, s, nf, nm, nr, offsets, off_stride, off_col0, off_add, ref, rd1_rows, lv, S,
-                          num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples, ng, grad_offsets, grad_ref, nf,
-                          grad_samples2, cap_remap(), sample_diff, sample_diff2)
-    } else {
-        CAP_DISPATCH_DIFF(2, grid, s, nf, nm, nr, offsets, off_stride, off_col0, off_add, ref, rd1_rows, lv, S,
-                          num_heads, head_dim, wpr, (int)tw, save_loc, grad_samples, ng, grad_offsets, grad_ref, nf,
-                          grad_samples2, cap_remap(), sample_diff, sample_diff2)
-    }
-    PDVC_CHECK_LAUNCH("cap_gather_bwd_kernel (diff)");
     return PDVC_OK;
 }
 

@@ -36,10 +36,6 @@ U_MAX_BYTES = 16 << 30  # largest projected-rows buffer of the gather form (ADVI
 # rounded freshly each step (they are written by the HIP kernels, which the mode's per-tensor rounding cache cannot
 # see) and the weights once per pass.
 BF16_RECURRENCE = os.environ.get("PDVC_BF16_RECURRENCE", "1") != "0"
-# the forward saves each sample's masked corner difference (pdvc_cap_gather_forward2_f32), and the backward's offset /
-# reference gradients read it (pdvc_cap_gather_backward_diff_f32) instead of gathering the two value rows again --
-# with the value gradient deferred to the destination-sorted pass (video_csr).  PDVC_CAP_DIFF=0: the gathering form.
-CAP_DIFF = os.environ.get("PDVC_CAP_DIFF", "1") != "0"
 _BF16 = torch.bfloat16
 
 
@@ -127,9 +123,6 @@ class CaptionDecodeFunction(Function):
         ctx.u_grad = U is not None and U_GRAD and A == D and video_csr is not None
         if ranged and not ctx.u_grad:  # dW_ctx reads CLIP and dATT over every (step, row): no stale entries
             CLIP.zero_()
-        # read by the backward over the computed (step, row) entries only: no zero fill
-        DIFF = torch.empty((n, R, M, NS, D), **kw) if (CAP_DIFF and video_csr is not None) else None
-        DIFF2 = torch.empty((n, R, M, NS, A), **kw) if (DIFF is not None and ctx.u_grad) else None  # of the U gather
         ns_ = M * NS
         b16 = BF16_RECURRENCE and bf16_active()
         ctx.b16 = b16
@@ -148,15 +141,14 @@ class CaptionDecodeFunction(Function):
                     hp.copy_(b_h.expand(c, Ph))  # h_{-1} = 0
                 else:
                     _gemm(b_h, HS[rs, i - 1], W_h.t(), hp, Wh16)
-                _n.call("pdvc_cap_gather_forward2_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video[rs]),
+                _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video[rs]),
                         _n.ptr(hp), Ph, 0, _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, D,
-                        NS // nl, _n.ptr(CLIP[i][rs]), _n.ptr(LOC[i][rs]),
-                        _n.ptr(DIFF[i][rs]) if DIFF is not None else None, st)
+                        NS // nl, _n.ptr(CLIP[i][rs]), _n.ptr(LOC[i][rs]), st)
                 att = ATT[i][s0 * ns_:(s0 + c) * ns_]
                 if U is not None:
-                    _n.call("pdvc_cap_gather_forward2_f32", _n.ptr(U), None, _n.ptr(row_video[rs]), _n.ptr(hp), Ph,
-                            0, _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, A, NS // nl,
-                            _n.ptr(att), None, _n.ptr(DIFF2[i][rs]) if DIFF2 is not None else None, st)
+                    _n.call("pdvc_cap_gather_forward_f32", _n.ptr(U), None, _n.ptr(row_video[rs]), _n.ptr(hp), Ph, 0,
+                            _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, A, NS // nl,
+                            _n.ptr(att), None, st)
                 else:
                     _gemm(b_ctx, CLIP[i][rs].reshape(-1, D), W_ctx.t(), att, Wctx16)
                 ah, ldh = _n.rows(hp[:, n_off:n_off + A])
@@ -170,8 +162,7 @@ class CaptionDecodeFunction(Function):
                         _n.ptr(CS[i - 1][rs] if i > 0 else zero), c, H, ho, ldo, _n.ptr(CS[i][rs]),
                         _n.ptr(ACTS[i][rs]), st)
         ctx.save_for_backward(value, off_hs, ref, W_h, W_ctx, alpha_w, W_att, pad_mask, row_video, HP, CLIP, LOC,
-                              ATT, PROBS, RES, ACTS, CS, HS, U if ctx.u_grad else None, vm if ctx.u_grad else None,
-                              DIFF, DIFF2)
+                              ATT, PROBS, RES, ACTS, CS, HS, U if ctx.u_grad else None, vm if ctx.u_grad else None)
         ctx.meta = (tuple(level_T), int(rd1_rows), video_csr, ranges if ranged else None,
                     step_ranges[1] if ranged else None)
         return HS
@@ -180,7 +171,7 @@ class CaptionDecodeFunction(Function):
     @once_differentiable
     def backward(ctx, dHS):
         (value, off_hs, ref, W_h, W_ctx, alpha_w, W_att, pad_mask, row_video, HP, CLIP, LOC, ATT, PROBS, RES, ACTS,
-         CS, HS, U, vm, DIFF, DIFF2) = ctx.saved_tensors
+         CS, HS, U, vm) = ctx.saved_tensors
         u_grad = ctx.u_grad
         level_T, rd1_rows, video_csr, ranged, sr_dev = ctx.meta
         ranges = ranged if ranged is not None else ((0, HP.shape[1]),) * HP.shape[0]
@@ -240,12 +231,7 @@ class CaptionDecodeFunction(Function):
                             _n.ptr(PROBS[i][rs]), _n.ptr(dRES), c, M, A, D, _n.ptr(datt), gah, ldgah, _n.ptr(dCLIP),
                             _n.ptr(GAW[i][s0 * M:(s0 + c) * M]), _n.ptr(GAB[i][s0 * M:(s0 + c) * M]), st)
                     gr_ = gr[rs] if gr is not None else None
-                    if u_grad and DIFF2 is not None:  # as below, from the forward's saved corner differences
-                        _n.call("pdvc_cap_gather_backward_diff_f32", _n.ptr(DIFF[i][rs]), _n.ptr(HP[i][rs]), Ph, 0,
-                                _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, D, NS // nl,
-                                _n.ptr(LOC[i][rs]), _n.ptr(dCLIP), _n.ptr(dhp), _n.ptr(gr_), _n.ptr(DIFF2[i][rs]),
-                                _n.ptr(datt), st)
-                    elif u_grad:  # dCLIP keeps the soft-attention part only; att's location gradient read off U
+                    if u_grad:  # dCLIP keeps the soft-attention part only; att's location gradient read off U
                         _n.call("pdvc_cap_gather_backward2_f32", _n.ptr(value), _n.ptr(pad_mask),
                                 _n.ptr(row_video[rs]), _n.ptr(HP[i][rs]), Ph, 0, _n.ptr(off_hs[rs]), _n.ptr(ref[rs]),
                                 RD, rd1, lvl, nl, Nv, c, M, D, NS // nl, _n.ptr(LOC[i][rs]), _n.ptr(dCLIP), None,
@@ -256,15 +242,10 @@ class CaptionDecodeFunction(Function):
                             _gemm(dc_, datt, W_ctx, dc_, Wctx16)
                         else:
                             dCLIP.reshape(-1, D).addmm_(datt, W_ctx)
-                        if DIFF is not None and deferred:
-                            _n.call("pdvc_cap_gather_backward_diff_f32", _n.ptr(DIFF[i][rs]), _n.ptr(HP[i][rs]), Ph,
-                                    0, _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, D, NS // nl,
-                                    _n.ptr(LOC[i][rs]), _n.ptr(dCLIP), _n.ptr(dhp), _n.ptr(gr_), None, None, st)
-                        else:
-                            _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(pad_mask),
-                                    _n.ptr(row_video[rs]), _n.ptr(HP[i][rs]), Ph, 0, _n.ptr(off_hs[rs]),
-                                    _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, D, NS // nl, _n.ptr(LOC[i][rs]),
-                                    _n.ptr(dCLIP), None if deferred else _n.ptr(gv), _n.ptr(dhp), _n.ptr(gr_), st)
+                        _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(pad_mask),
+                                _n.ptr(row_video[rs]), _n.ptr(HP[i][rs]), Ph, 0, _n.ptr(off_hs[rs]),
+                                _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, D, NS // nl, _n.ptr(LOC[i][rs]),
+                                _n.ptr(dCLIP), None if deferred else _n.ptr(gv), _n.ptr(dhp), _n.ptr(gr_), st)
                 if i > 0:  # dh of step i - 1's rows (rows that stopped at step i have dHP[i] = 0 there)
                     p0, pc = ranges[i - 1]
                     if pc > 0:

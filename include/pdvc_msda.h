@@ -230,24 +230,6 @@ int pdvc_cap_gather_backward2_f32(const float* value, const uint8_t* value_pad_m
                                   const float* save_loc, const float* grad_samples, float* grad_value,
                                   float* grad_offsets, float* grad_ref, const float* value2,
                                   const float* grad_samples2, void* stream);
-/* pdvc_cap_gather_forward_f32 plus, when sample_diff (R, M, L*P, D) is not NULL, each sample's masked corner
- * difference (x0 + 1 row, or 0 outside/masked) - (x0 row, or 0 if masked): the location term of the backward, so
- * that pdvc_cap_gather_backward_diff_f32 reads it sequentially instead of gathering the two corner rows again. */
-int pdvc_cap_gather_forward2_f32(const float* value, const uint8_t* value_pad_mask, const int32_t* row_video,
-                                 const float* offsets, int off_stride, int off_col0, const float* off_add,
-                                 const float* ref, int ref_dim, int rd1_rows, const int32_t* level_T, int num_levels,
-                                 int batch, int rows, int num_heads, int head_dim, int num_point, float* samples,
-                                 float* save_loc, float* sample_diff, void* stream);
-/* The offset and reference gradients of pdvc_cap_gather_backward_f32 (grad_value NULL) -- or, with sample_diff2 and
- * grad_samples2, of pdvc_cap_gather_backward2_f32 (the second tensor's differences from its own forward2 call, made
- * without a padding mask) -- from the forward's sample_diff: no value rows are read; grad_ref is ACCUMULATED as
- * there.  The same floating-point operations in the same order (results within an ulp of the gathering form). */
-int pdvc_cap_gather_backward_diff_f32(const float* sample_diff, const float* offsets, int off_stride, int off_col0,
-                                      const float* off_add, const float* ref, int ref_dim, int rd1_rows,
-                                      const int32_t* level_T, int num_levels, int batch, int rows, int num_heads,
-                                      int head_dim, int num_point, const float* save_loc, const float* grad_samples,
-                                      float* grad_offsets, float* grad_ref, const float* sample_diff2,
-                                      const float* grad_samples2, void* stream);
 
 /* ---- decoder query self-attention core (nn.MultiheadAttention, batch-first) -------------------------
  * qk (N,Q,2E) = [q | k] in-projections (E = num_heads*head_dim), v (N,Q,E); key_padding_mask (N,Q) uint8,

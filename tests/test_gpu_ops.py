@@ -602,85 +602,6 @@ def test_cap_gather_vs_oracle(D, M, ref_dim):
     close(rf.grad, exp_gr, 1e-4, "grad_ref")
 
 
-@pytest.mark.parametrize("D,M", [(64, 8), (32, 2), (128, 3)])
-@pytest.mark.parametrize("ref_dim", [1, 2])
-@pytest.mark.parametrize("masked", [False, True])
-@pytest.mark.parametrize("second", [False, True])
-def test_cap_gather_diff_matches_gathering_backward(D, M, ref_dim, masked, second):
-    """pdvc_cap_gather_forward2_f32 / pdvc_cap_gather_backward_diff_f32 (the caption decoder's default with the value
-    gradient deferred) against pdvc_cap_gather_forward_f32 / pdvc_cap_gather_backward_f32 with grad_value NULL -- or,
-    with `second`, pdvc_cap_gather_backward2_f32 with a second tensor sampled at the same locations (the ctx2att rows
-    U, gathered without a mask): the same samples and save_loc bit for bit, the same offset gradients to 1e-6 of
-    their largest magnitude (the same operations in the same order; the two kernels' code generation rounds the location
-    dot products differently by up to an ulp -- measured 5.7e-6 on values ~20), grad_ref (atomics) likewise."""
-    from pdvc import _native as _n
-    rng = np.random.RandomState(D + M + 10 * ref_dim + 100 * masked + 1000 * second)
-    T_l = [24, 12, 6, 3]
-    S, N, R = sum(T_l), 3, 13
-    value = cu(rng.randn(N, S, M, D), torch.float32)
-    U = cu(rng.randn(N, S, M, D), torch.float32) if second else None
-    mask = None
-    if masked:
-        mk = np.zeros((N, S), np.uint8)
-        mk[1, 5:9] = 1
-        mk[2, 30:33] = 1
-        mask = cu(mk)
-    row_video = cu(rng.randint(0, N, size=R).astype(np.int32))
-    off_stride = M * 16 + 5
-    offsets = cu(rng.randn(R, off_stride) * 3.0, torch.float32)
-    off_add = cu(rng.randn(R, M * 16) * 0.5, torch.float32)
-    if ref_dim == 1:
-        ref = cu(rng.uniform(-0.1, 1.1, size=(R, 4, 1)), torch.float32)
-    else:
-        ref = cu(np.concatenate([rng.uniform(0, 1, size=(R, 4, 1)), rng.uniform(0.05, 0.9, size=(R, 4, 1))], -1),
-                 torch.float32)
-    rd1 = 4 if ref_dim == 2 else 0
-    lvl = _n.int_array(T_l)
-    gs = cu(rng.randn(R, M, 16, D), torch.float32)
-    gs2 = cu(rng.randn(R, M, 16, D), torch.float32) if second else None
-    outs = []
-    for diff in (False, True):
-        samples = torch.empty(R, M, 16, D, device=DEV)
-        samples2 = torch.empty(R, M, 16, D, device=DEV)
-        loc = torch.empty(R, M, 16, device=DEV)
-        sd = torch.empty(R, M, 16, D, device=DEV) if diff else None
-        sd2 = torch.empty(R, M, 16, D, device=DEV) if (diff and second) else None
-        geo = (_n.ptr(row_video), _n.ptr(offsets), off_stride, 5, _n.ptr(off_add), _n.ptr(ref), ref_dim, rd1, lvl, 4,
-               N, R, M, D, 4)
-        if diff:
-            _n.call("pdvc_cap_gather_forward2_f32", _n.ptr(value), _n.ptr(mask), *geo, _n.ptr(samples), _n.ptr(loc),
-                    _n.ptr(sd), _n.stream())
-            if second:
-                _n.call("pdvc_cap_gather_forward2_f32", _n.ptr(U), None, *geo, _n.ptr(samples2), None, _n.ptr(sd2),
-                        _n.stream())
-        else:
-            _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(mask), *geo, _n.ptr(samples), _n.ptr(loc),
-                    _n.stream())
-            if second:
-                _n.call("pdvc_cap_gather_forward_f32", _n.ptr(U), None, *geo, _n.ptr(samples2), None, _n.stream())
-        go = torch.zeros(R, off_stride, device=DEV)
-        gr = torch.zeros(R, 4, ref_dim, device=DEV)
-        if diff:
-            _n.call("pdvc_cap_gather_backward_diff_f32", _n.ptr(sd), _n.ptr(offsets), off_stride, 5, _n.ptr(off_add),
-                    _n.ptr(ref), ref_dim, rd1, lvl, 4, N, R, M, D, 4, _n.ptr(loc), _n.ptr(gs), _n.ptr(go), _n.ptr(gr),
-                    _n.ptr(sd2), _n.ptr(gs2), _n.stream())
-        elif second:
-            _n.call("pdvc_cap_gather_backward2_f32", _n.ptr(value), _n.ptr(mask), *geo, _n.ptr(loc), _n.ptr(gs), None,
-                    _n.ptr(go), _n.ptr(gr), _n.ptr(U), _n.ptr(gs2), _n.stream())
-        else:
-            _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(mask), *geo, _n.ptr(loc), _n.ptr(gs), None,
-                    _n.ptr(go), _n.ptr(gr), _n.stream())
-        torch.cuda.synchronize()
-        outs.append((samples, samples2 if second else None, loc, go, gr))
-    (s0, u0, l0, go0, gr0), (s1, u1, l1, go1, gr1) = outs
-    assert torch.equal(s0, s1) and torch.equal(l0, l1)
-    if second:
-        assert torch.equal(u0, u1)
-    assert (go0 - go1).abs().max().item() <= 1e-6 * (go0.abs().max().item() + 1.0), (go0 - go1).abs().max().item()
-    assert (gr0 - gr1).abs().max().item() <= 1e-6 * (gr0.abs().max().item() + 1.0)
-    assert go0[:, 5:].abs().sum().item() > 0 and gr0.abs().sum().item() > 0
-
-
 # ------------------------------------------------------------------------------------------------
 # modules vs golden vectors generated from the reference modules
 # ------------------------------------------------------------------------------------------------
