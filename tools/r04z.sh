@@ -1,6 +1,6 @@
 #!/bin/bash
-# round-4 GPU pass Y: the caption gather backward from the forward's saved corner differences (PDVC_CAP_TWO, default
-# on): parity (bitwise ABI test + the model-level suites), then A/B of the headline and bf16 bench lines
+# round-4 GPU pass Z: the caption gather forward of the value rows and the projected ctx2att rows in one launch
+# (PDVC_CAP_TWO, default on): parity (ABI test + the model-level suites), then A/B of the headline and bf16 bench lines
 cd "${GRAFT_REPO_ROOT:-$(pwd)}" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r04z; mkdir -p $O
