@@ -43,10 +43,7 @@ __device__ __forceinline__ void ld(VecF<CPL>& v, const float* __restrict__ p, bo
 constexpr int kSPW = 2;              // samples per wave
 constexpr int kSplit = cNS / kSPW;   // waves per (row, head group)
 
-// TWO: a second tensor of the same shape (value2, no padding mask) sampled at the same locations into samples2 -- the
-// caption head's ctx2att rows U (pdvc/ops/functions/caption_decode.py) -- in the same wave: the location math once,
-// both tensors' corner rows in flight together
-template <int CPL, int LPH, int RD, bool TWO = false>
+template <int CPL, int LPH, int RD>
 __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __restrict__ value,
                                                               const uint8_t* __restrict__ vmask,
                                                               const int32_t* __restrict__ row_video,
@@ -55,9 +52,7 @@ __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __rest
                                                               const float* __restrict__ ref, int rd1_rows,
                                                               CapLevels lv, int S, int M, int D, int waves_per_row,
                                                               int total_waves, float* __restrict__ samples,
-                                                              float* __restrict__ save_loc, int remap,
-                                                              const float* __restrict__ value2,
-                                                              float* __restrict__ samples2) {
+                                                              float* __restrict__ save_loc, int remap) {
     constexpr int HPW = 64 / LPH;
     const int lane = threadIdx.x & 63;
     const int wave = (remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x) * 4 + (threadIdx.x >> 6);
@@ -98,35 +93,22 @@ __global__ __launch_bounds__(256) void cap_gather_fwd_kernel(const float* __rest
         ne[u] = (ix - xf);
     }
     VecF<CPL> v0[kSPW], v1[kSPW];
-    VecF<CPL> w0[TWO ? kSPW : 1], w1[TWO ? kSPW : 1];
     bool ok0[kSPW], ok1[kSPW];
-    const float* wbase = TWO ? value2 + (size_t)b * S * MD + (size_t)m * D + c0 : nullptr;
 #pragma unroll
     for (int u = 0; u < kSPW; ++u) {  // all corner rows in flight together (clamped, selected after)
         const int a1 = min(x0[u] + 1, T - 1);
         v0[u].load(vbase + (size_t)(st + x0[u]) * MD);
         v1[u].load(vbase + (size_t)(st + a1) * MD);
-        if constexpr (TWO) {
-            w0[u].load(wbase + (size_t)(st + x0[u]) * MD);
-            w1[u].load(wbase + (size_t)(st + a1) * MD);
-        }
         ok0[u] = !(mbase && mbase[st + x0[u]]);
         ok1[u] = x0[u] + 1 < T && !(mbase && mbase[st + a1]);
     }
 #pragma unroll
     for (int u = 0; u < kSPW; ++u) {
-        const size_t so = (((size_t)r * M + m) * cNS + j0 + u) * D + c0;
         VecF<CPL> o;
 #pragma unroll
         for (int c = 0; c < CPL; ++c)
             o.v[c] = (ok0[u] ? v0[u].v[c] : 0.f) * nw[u] + (ok1[u] ? v1[u].v[c] : 0.f) * ne[u];
-        o.store(samples + so);
-        if constexpr (TWO) {  // no mask: corner x0 always, x0 + 1 inside the level
-            const bool hi = x0[u] + 1 < T;
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) o.v[c] = w0[u].v[c] * nw[u] + (hi ? w1[u].v[c] : 0.f) * ne[u];
-            o.store(samples2 + so);
-        }
+        o.store(samples + (((size_t)r * M + m) * cNS + j0 + u) * D + c0);
     }
 }
 
@@ -503,66 +485,31 @@ using namespace pdvc;
         default: hipLaunchKernelGGL((KERNEL<8, 64, RD>), grid, dim3(256), 0, s, __VA_ARGS__); break;            \
     }
 
-#define CAP_DISPATCH_TWO(RD, grid, s, ...)                                                                       \
-    switch (lph) {                                                                                               \
-        case 4: hipLaunchKernelGGL((cap_gather_fwd_kernel<8, 4, RD, true>), grid, dim3(256), 0, s, __VA_ARGS__); break;   \
-        case 8: hipLaunchKernelGGL((cap_gather_fwd_kernel<8, 8, RD, true>), grid, dim3(256), 0, s, __VA_ARGS__); break;   \
-        case 16: hipLaunchKernelGGL((cap_gather_fwd_kernel<8, 16, RD, true>), grid, dim3(256), 0, s, __VA_ARGS__); break; \
-        case 32: hipLaunchKernelGGL((cap_gather_fwd_kernel<8, 32, RD, true>), grid, dim3(256), 0, s, __VA_ARGS__); break; \
-        default: hipLaunchKernelGGL((cap_gather_fwd_kernel<8, 64, RD, true>), grid, dim3(256), 0, s, __VA_ARGS__); break; \
-    }
-
-extern "C" int pdvc_cap_gather_forward2_f32(const float* value, const uint8_t* value_pad_mask,
-                                            const int32_t* row_video, const float* offsets, int off_stride,
-                                            int off_col0, const float* off_add, const float* ref, int ref_dim,
-                                            int rd1_rows, const int32_t* level_T, int num_levels, int batch, int rows,
-                                            int num_heads, int head_dim, int num_point, float* samples,
-                                            float* save_loc, const float* value2, float* samples2, void* stream) {
+extern "C" int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* value_pad_mask, const int32_t* row_video,
+                                           const float* offsets, int off_stride, int off_col0, const float* off_add,
+                                           const float* ref,
+                                           int ref_dim, int rd1_rows, const int32_t* level_T, int num_levels, int batch, int rows,
+                                           int num_heads, int head_dim, int num_point, float* samples, float* save_loc,
+                                           void* stream) {
     CapLevels lv;
     int S, lph, wpr;
     int rc = cap_setup(level_T, num_levels, num_point, head_dim, num_heads, ref_dim, lv, S, lph, wpr);
     if (rc) return rc;
     PDVC_CHECK_ARG(batch >= 0 && rows >= 0, "negative sizes");
     PDVC_CHECK_ARG(off_col0 >= 0 && off_col0 + num_heads * cNS <= off_stride, "offset columns out of range");
-    PDVC_CHECK_ARG((value2 == nullptr) == (samples2 == nullptr), "value2 and samples2 go together");
     const long tw = (long)rows * wpr;
     if (tw == 0) return PDVC_OK;
     dim3 grid((unsigned)((tw + 3) / 4));
     hipStream_t s = (hipStream_t)stream;
-    if (value2) {
-        if (ref_dim == 1) {
-            CAP_DISPATCH_TWO(1, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0, off_add, ref,
-                             rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc, cap_remap(), value2,
-                             samples2)
-        } else {
-            CAP_DISPATCH_TWO(2, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0, off_add, ref,
-                             rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc, cap_remap(), value2,
-                             samples2)
-        }
-        PDVC_CHECK_LAUNCH("cap_gather_fwd_kernel (two tensors)");
-        return PDVC_OK;
-    }
     if (ref_dim == 1) {
         CAP_DISPATCH(cap_gather_fwd_kernel, 1, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
-                     off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc, cap_remap(),
-                     (const float*)nullptr, (float*)nullptr)
+                     off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc, cap_remap())
     } else {
         CAP_DISPATCH(cap_gather_fwd_kernel, 2, grid, s, value, value_pad_mask, row_video, offsets, off_stride, off_col0,
-                     off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc, cap_remap(),
-                     (const float*)nullptr, (float*)nullptr)
+                     off_add, ref, rd1_rows, lv, S, num_heads, head_dim, wpr, (int)tw, samples, save_loc, cap_remap())
     }
     PDVC_CHECK_LAUNCH("cap_gather_fwd_kernel");
     return PDVC_OK;
-}
-
-extern "C" int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* value_pad_mask, const int32_t* row_video,
-                                           const float* offsets, int off_stride, int off_col0, const float* off_add,
-                                           const float* ref, int ref_dim, int rd1_rows, const int32_t* level_T,
-                                           int num_levels, int batch, int rows, int num_heads, int head_dim,
-                                           int num_point, float* samples, float* save_loc, void* stream) {
-    return pdvc_cap_gather_forward2_f32(value, value_pad_mask, row_video, offsets, off_stride, off_col0, off_add, ref,
-                                        ref_dim, rd1_rows, level_T, num_levels, batch, rows, num_heads, head_dim,
-                                        num_point, samples, save_loc, nullptr, nullptr, stream);
 }
 
 extern "C" int pdvc_cap_gather_backward2_f32(const float* value, const uint8_t* value_pad_mask,

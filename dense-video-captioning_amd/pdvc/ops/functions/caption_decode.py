@@ -36,8 +36,6 @@ U_MAX_BYTES = 16 << 30  # largest projected-rows buffer of the gather form (ADVI
 # rounded freshly each step (they are written by the HIP kernels, which the mode's per-tensor rounding cache cannot
 # see) and the weights once per pass.
 BF16_RECURRENCE = os.environ.get("PDVC_BF16_RECURRENCE", "1") != "0"
-# the value rows' and the projected rows' samples in one gather launch (pdvc_cap_gather_forward2_f32); 0: two launches
-CAP_TWO = os.environ.get("PDVC_CAP_TWO", "1") != "0"
 _BF16 = torch.bfloat16
 
 
@@ -143,17 +141,15 @@ class CaptionDecodeFunction(Function):
                     hp.copy_(b_h.expand(c, Ph))  # h_{-1} = 0
                 else:
                     _gemm(b_h, HS[rs, i - 1], W_h.t(), hp, Wh16)
-                att = ATT[i][s0 * ns_:(s0 + c) * ns_]
-                both = CAP_TWO and U is not None and A == D  # the samples and the projected rows' samples at once
-                _n.call("pdvc_cap_gather_forward2_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video[rs]),
+                _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video[rs]),
                         _n.ptr(hp), Ph, 0, _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, D,
-                        NS // nl, _n.ptr(CLIP[i][rs]), _n.ptr(LOC[i][rs]), _n.ptr(U) if both else None,
-                        _n.ptr(att) if both else None, st)
-                if U is not None and not both:  # projected rows of another width: their own gather
+                        NS // nl, _n.ptr(CLIP[i][rs]), _n.ptr(LOC[i][rs]), st)
+                att = ATT[i][s0 * ns_:(s0 + c) * ns_]
+                if U is not None:
                     _n.call("pdvc_cap_gather_forward_f32", _n.ptr(U), None, _n.ptr(row_video[rs]), _n.ptr(hp), Ph, 0,
                             _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, A, NS // nl,
                             _n.ptr(att), None, st)
-                elif U is None:
+                else:
                     _gemm(b_ctx, CLIP[i][rs].reshape(-1, D), W_ctx.t(), att, Wctx16)
                 ah, ldh = _n.rows(hp[:, n_off:n_off + A])
                 _n.call("pdvc_softattn_forward_f32", _n.ptr(att), ah, ldh, _n.ptr(alpha_w), _n.ptr(alpha_b),

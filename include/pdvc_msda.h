@@ -211,13 +211,6 @@ int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* value_pad_mas
                                 const float* ref, int ref_dim, int rd1_rows, const int32_t* level_T, int num_levels,
                                 int batch, int rows, int num_heads, int head_dim, int num_point, float* samples,
                                 float* save_loc, void* stream);
-/* pdvc_cap_gather_forward_f32 plus, when value2 is not NULL, a second tensor of value's shape (no padding mask) sampled
- * at the same locations into samples2 -- the caption head's ctx2att rows, gathered by the same waves. */
-int pdvc_cap_gather_forward2_f32(const float* value, const uint8_t* value_pad_mask, const int32_t* row_video,
-                                 const float* offsets, int off_stride, int off_col0, const float* off_add,
-                                 const float* ref, int ref_dim, int rd1_rows, const int32_t* level_T, int num_levels,
-                                 int batch, int rows, int num_heads, int head_dim, int num_point, float* samples,
-                                 float* save_loc, const float* value2, float* samples2, void* stream);
 /* grad_value and grad_ref (R,L,ref_dim, may be NULL) are ACCUMULATED (atomic adds; zero them before the first
  * call -- the caption decoder accumulates every step into one buffer); grad_offsets (R, off_stride): only the
  * offset columns are written (it is also the gradient of off_add). */

@@ -602,51 +602,6 @@ def test_cap_gather_vs_oracle(D, M, ref_dim):
     close(rf.grad, exp_gr, 1e-4, "grad_ref")
 
 
-@pytest.mark.parametrize("D,M", [(64, 8), (32, 2), (128, 3)])
-@pytest.mark.parametrize("ref_dim", [1, 2])
-@pytest.mark.parametrize("masked", [False, True])
-def test_cap_gather_two_tensors_matches_two_launches(D, M, ref_dim, masked):
-    """pdvc_cap_gather_forward2_f32 with value2 (the caption decoder's samples of the value rows and of the ctx2att rows
-    U in one launch) against two pdvc_cap_gather_forward_f32 calls (value with its mask, U without): the same samples
-    and save_loc to 1e-6 of their magnitude (the same blend; code generation may round a product differently)."""
-    from pdvc import _native as _n
-    rng = np.random.RandomState(D + M + 10 * ref_dim + 100 * masked)
-    T_l = [24, 12, 6, 3]
-    S, N, R = sum(T_l), 3, 13
-    value = cu(rng.randn(N, S, M, D), torch.float32)
-    U = cu(rng.randn(N, S, M, D), torch.float32)
-    mask = None
-    if masked:
-        mk = np.zeros((N, S), np.uint8)
-        mk[1, 5:9] = 1
-        mk[2, 30:33] = 1
-        mask = cu(mk)
-    row_video = cu(rng.randint(0, N, size=R).astype(np.int32))
-    off_stride = M * 16 + 5
-    offsets = cu(rng.randn(R, off_stride) * 3.0, torch.float32)
-    off_add = cu(rng.randn(R, M * 16) * 0.5, torch.float32)
-    if ref_dim == 1:
-        ref = cu(rng.uniform(-0.1, 1.1, size=(R, 4, 1)), torch.float32)
-    else:
-        ref = cu(np.concatenate([rng.uniform(0, 1, size=(R, 4, 1)), rng.uniform(0.05, 0.9, size=(R, 4, 1))], -1),
-                 torch.float32)
-    rd1 = 4 if ref_dim == 2 else 0
-    geo = (_n.ptr(row_video), _n.ptr(offsets), off_stride, 5, _n.ptr(off_add), _n.ptr(ref), ref_dim, rd1,
-           _n.int_array(T_l), 4, N, R, M, D, 4)
-    s1, u1, l1 = (torch.empty(R, M, 16, D, device=DEV), torch.empty(R, M, 16, D, device=DEV),
-                  torch.empty(R, M, 16, device=DEV))
-    _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(mask), *geo, _n.ptr(s1), _n.ptr(l1), _n.stream())
-    _n.call("pdvc_cap_gather_forward_f32", _n.ptr(U), None, *geo, _n.ptr(u1), None, _n.stream())
-    s2, u2, l2 = torch.empty_like(s1), torch.empty_like(u1), torch.empty_like(l1)
-    _n.call("pdvc_cap_gather_forward2_f32", _n.ptr(value), _n.ptr(mask), *geo, _n.ptr(s2), _n.ptr(l2), _n.ptr(U),
-            _n.ptr(u2), _n.stream())
-    torch.cuda.synchronize()
-    assert torch.equal(l1, l2)
-    for a, b in ((s1, s2), (u1, u2)):
-        assert (a - b).abs().max().item() <= 1e-6 * (a.abs().max().item() + 1.0)
-    assert u2.abs().sum().item() > 0
-
-
 # ------------------------------------------------------------------------------------------------
 # modules vs golden vectors generated from the reference modules
 # ------------------------------------------------------------------------------------------------
