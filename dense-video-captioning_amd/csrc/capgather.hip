@@ -472,94 +472,6 @@ static int cap_setup(const int32_t* level_T, int num_levels, int num_point, int 
     return PDVC_OK;
 }
 
-
-// -------------------------------------------------------------------------------------------------
-// One caption step's sampling and soft attention in one launch (the training recurrence with the ctx2att rows
-// projected once, pdvc/ops/functions/caption_decode.py; D = A = 64): for each (row, head) one wave, lane = channel.
-// Lanes 0..15 form sample j's location and corners (cap_gather_fwd_kernel's math), the wave reads the two corner rows
-// of the value and of U for all 16 samples (every read a coalesced 256-B row), forms the samples clip_j and att_j,
-// then the soft attention of softattn_fwd4_kernel (capstep.hip): dot_j = sum_a tanh(att_j[a] + att_h[a]) w_a + b by
-// a reduce-scatter over the lanes, softmax, res = sum_j p_j clip_j.  clip, att, save_loc and probs are written for
-// the backward as before; the separate soft-attention pass no longer reads clip and att back.
-// -------------------------------------------------------------------------------------------------
-template <int RD>
-__global__ __launch_bounds__(256) void cap_softattn_fwd_kernel(
-    const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ U,
-    const int32_t* __restrict__ row_video, const float* __restrict__ offsets, int off_stride, int off_col0,
-    const float* __restrict__ off_add, const float* __restrict__ ref, int rd1_rows, CapLevels lv, int S, int M,
-    const float* __restrict__ att_h, int ldh, const float* __restrict__ aw, const float* __restrict__ ab,
-    int total_waves, float* __restrict__ clip, float* __restrict__ save_loc, float* __restrict__ att,
-    float* __restrict__ probs, float* __restrict__ res) {
-    constexpr int D = 64;
-    const int lane = threadIdx.x & 63;
-    const int wave = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
-    if (wave >= total_waves) return;
-    const int r = wave / M, m = wave - r * M;
-    const int b = row_video[r];
-    const size_t MD = (size_t)M * D;
-    // lane j < 16: sample j's parameters (lanes 16..63 repeat them, unused)
-    const int j = lane & 15, l = j >> 2;
-    const int T = lv.T[0] * (l == 0) + lv.T[1] * (l == 1) + lv.T[2] * (l == 2) + lv.T[3] * (l == 3);
-    const int st = lv.start[0] * (l == 0) + lv.start[1] * (l == 1) + lv.start[2] * (l == 2) + lv.start[3] * (l == 3);
-    const float* orow = offsets + (size_t)r * off_stride + off_col0 + m * cNS;
-    const float off = off_add ? orow[j] + off_add[((size_t)r * M + m) * cNS + j] : orow[j];
-    const bool centre_only = (RD == 1) || (r < rd1_rows);
-    const float r0 = ref[((size_t)r * cL + l) * RD];
-    const float r1 = (RD == 2) ? ref[((size_t)r * cL + l) * RD + 1] : 0.f;
-    const float loc = centre_only ? r0 + off / (float)T : r0 + ((off / (float)cP) * r1) * 0.5f;
-    if (lane < cNS) save_loc[((size_t)r * M + m) * cNS + j] = loc;
-    float gm;
-    const float ix = border_ix(loc, T, gm);
-    const float xf = floorf(ix);
-    const int x0 = (int)xf;
-    const int a1 = min(x0 + 1, T - 1);
-    const float nw = ((float)(x0 + 1) - ix), ne = (ix - xf);
-    const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
-    const bool ok0 = !(mbase && mbase[st + x0]);
-    const bool ok1 = x0 + 1 < T && !(mbase && mbase[st + a1]);
-    const int flags = (ok0 ? 1 : 0) | (ok1 ? 2 : 0) | (x0 + 1 < T ? 4 : 0);
-    const float* vb = value + (size_t)b * S * MD + (size_t)m * D + lane;
-    const float* ub = U + (size_t)b * S * MD + (size_t)m * D + lane;
-    float v0[cNS], v1[cNS], u0[cNS], u1[cNS];
-#pragma unroll
-    for (int k = 0; k < cNS; ++k) {  // every corner row of the 16 samples in flight together
-        const int row0 = __builtin_amdgcn_readlane(st + x0, k), row1 = __builtin_amdgcn_readlane(st + a1, k);
-        v0[k] = vb[(size_t)row0 * MD];
-        v1[k] = vb[(size_t)row1 * MD];
-        u0[k] = ub[(size_t)row0 * MD];
-        u1[k] = ub[(size_t)row1 * MD];
-    }
-    const size_t so = ((size_t)r * M + m) * cNS;
-    const float hv = att_h[(size_t)r * ldh + lane], wv = aw[lane];
-    float cl[cNS], part[cNS];
-#pragma unroll
-    for (int k = 0; k < cNS; ++k) {
-        const float NW = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nw), k));
-        const float NE = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ne), k));
-        const int fl = __builtin_amdgcn_readlane(flags, k);
-        cl[k] = ((fl & 1) ? v0[k] : 0.f) * NW + ((fl & 2) ? v1[k] : 0.f) * NE;
-        const float at = u0[k] * NW + ((fl & 4) ? u1[k] : 0.f) * NE;  // U: no mask, the x0 corner always
-        clip[(so + k) * D + lane] = cl[k];
-        att[(so + k) * D + lane] = at;
-        part[k] = tanhf(at + hv) * wv;
-    }
-    group_reduce_scatter<cNS, 16>(part, lane);  // lane % 16 = k: the 16-lane partial of dot_k
-    float dsum = part[0];
-    dsum += lane_swap(dsum, 16);
-    dsum += __shfl_xor(dsum, 32, 64);
-    // softmax over the 16 dots, one per lane of each 16-lane group (every group holds all 16)
-    const float z = dsum + ab[0];
-    float mx = z;
-#pragma unroll
-    for (int d = 1; d < 16; d <<= 1) mx = fmaxf(mx, lane_swap(mx, d));
-    const float e = expf(z - mx);
-    const float pk = e / group_allreduce<16>(e);
-    if (lane < cNS) probs[so + lane] = pk;
-    float o = 0.f;
-#pragma unroll
-    for (int k = 0; k < cNS; ++k) o += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pk), k)) * cl[k];
-    res[(size_t)r * MD + (size_t)m * D + lane] = o;
-}
 }  // namespace pdvc
 
 using namespace pdvc;
@@ -724,42 +636,4 @@ extern "C" int pdvc_cap_value_grad_f32(const uint8_t* value_pad_mask, const int3
     return pdvc_cap_value_grad_ex_f32(value_pad_mask, level_T, num_levels, batch, num_heads, head_dim, num_point, rows,
                                       steps, max_rows_per_video, video_row_start, video_rows, save_loc, grad_samples,
                                       grad_value, nullptr, stream);
-}
-
-// One caption step's sampling of the value rows and of the projected ctx2att rows U (same shape, no mask) plus the
-// soft attention over the 16 samples (pdvc_cap_gather_forward_f32 twice and pdvc_softattn_forward_f32 in one launch);
-// head_dim 64 = the attention width.  Outputs as those calls': samples (R,M,16,64), save_loc (R,M,16), att
-// (R*M*16, 64), probs (R,M,16), res (R, M*64).
-extern "C" int pdvc_cap_softattn_forward_f32(const float* value, const uint8_t* value_pad_mask, const float* U,
-                                             const int32_t* row_video, const float* offsets, int off_stride,
-                                             int off_col0, const float* off_add, const float* ref, int ref_dim,
-                                             int rd1_rows, const int32_t* level_T, int num_levels, int batch,
-                                             int rows, int num_heads, int head_dim, int num_point,
-                                             const float* att_h, int ld_att_h, const float* alpha_w,
-                                             const float* alpha_b, float* samples, float* save_loc, float* att,
-                                             float* probs, float* res, void* stream) {
-    CapLevels lv;
-    int S, lph, wpr;
-    int rc = cap_setup(level_T, num_levels, num_point, head_dim, num_heads, ref_dim, lv, S, lph, wpr);
-    if (rc) return rc;
-    if (head_dim != 64) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "fused caption step needs head_dim 64, got %d", head_dim);
-    PDVC_CHECK_ARG(U && att_h && alpha_w && alpha_b && samples && save_loc && att && probs && res,
-                   "fused caption step: NULL argument");
-    PDVC_CHECK_ARG(off_col0 >= 0 && off_col0 + num_heads * cNS <= off_stride, "offset columns out of range");
-    PDVC_CHECK_ARG(batch >= 0 && rows >= 0 && ld_att_h >= 64, "invalid sizes");
-    const long tw = (long)rows * num_heads;
-    if (tw == 0) return PDVC_OK;
-    PDVC_CHECK_ARG(tw < (1L << 31) / 4, "too many rows");
-    dim3 grid((unsigned)((tw + 3) / 4));
-    hipStream_t s = (hipStream_t)stream;
-    if (ref_dim == 1)
-        hipLaunchKernelGGL(cap_softattn_fwd_kernel<1>, grid, dim3(256), 0, s, value, value_pad_mask, U, row_video,
-                           offsets, off_stride, off_col0, off_add, ref, rd1_rows, lv, S, num_heads, att_h, ld_att_h,
-                           alpha_w, alpha_b, (int)tw, samples, save_loc, att, probs, res);
-    else
-        hipLaunchKernelGGL(cap_softattn_fwd_kernel<2>, grid, dim3(256), 0, s, value, value_pad_mask, U, row_video,
-                           offsets, off_stride, off_col0, off_add, ref, rd1_rows, lv, S, num_heads, att_h, ld_att_h,
-                           alpha_w, alpha_b, (int)tw, samples, save_loc, att, probs, res);
-    PDVC_CHECK_LAUNCH("cap_softattn_fwd_kernel");
-    return PDVC_OK;
 }
