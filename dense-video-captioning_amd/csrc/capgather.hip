@@ -472,6 +472,140 @@ static int cap_setup(const int32_t* level_T, int num_levels, int num_point, int 
     return PDVC_OK;
 }
 
+
+// -------------------------------------------------------------------------------------------------
+// One caption step's sampling and soft attention in one launch, for the 512-wide head every cfg uses (cap_nheads 1;
+// D = A = 512; pdvc/ops/functions/caption_decode.py): one 128-thread workgroup per (row, head), a float4 of channels
+// per thread -- the mapping of softattn_fwd4_kernel (capstep.hip).  Threads 0..15 form sample j's location and
+// corners (cap_gather_fwd_kernel's math) into LDS; every thread then reads its 16 bytes of the two corner rows of the
+// value and of U for the 16 samples (2 KiB rows, coalesced), forms clip_k and att_k, and the soft attention follows
+// as softattn_fwd4_kernel computes it (the same per-thread sums, block reduction and softmax).  clip, att, save_loc
+// and probs are written for the backward; the separate soft-attention pass no longer reads clip and att back.
+// -------------------------------------------------------------------------------------------------
+constexpr int kCSA = 128;  // threads per fused caption-step workgroup (512 channels as float4s)
+
+template <int RD>
+__global__ __launch_bounds__(kCSA) void cap_softattn_fwd_kernel(
+    const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ U,
+    const int32_t* __restrict__ row_video, const float* __restrict__ offsets, int off_stride, int off_col0,
+    const float* __restrict__ off_add, const float* __restrict__ ref, int rd1_rows, CapLevels lv, int S, int M,
+    const float* __restrict__ att_h, int ldh, const float* __restrict__ aw, const float* __restrict__ ab,
+    float* __restrict__ clip, float* __restrict__ save_loc, float* __restrict__ att, float* __restrict__ probs,
+    float* __restrict__ res) {
+    constexpr int D = 512, D4 = D / 4;
+    __shared__ int srow0[cNS], srow1[cNS], sfl[cNS];
+    __shared__ float snw[cNS], sne[cNS], red[3 * cNS];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    const int r = wg / M, m = wg - r * M;
+    const int b = row_video[r];
+    const size_t MD = (size_t)M * D;
+    const size_t so = (size_t)wg * cNS;  // (r * M + m) * 16
+    if (tid < cNS) {
+        const int j = tid, l = j >> 2;
+        const int T = lv.T[0] * (l == 0) + lv.T[1] * (l == 1) + lv.T[2] * (l == 2) + lv.T[3] * (l == 3);
+        const int st = lv.start[0] * (l == 0) + lv.start[1] * (l == 1) + lv.start[2] * (l == 2) + lv.start[3] * (l == 3);
+        const float* orow = offsets + (size_t)r * off_stride + off_col0 + m * cNS;
+        const float off = off_add ? orow[j] + off_add[((size_t)r * M + m) * cNS + j] : orow[j];
+        const bool centre_only = (RD == 1) || (r < rd1_rows);
+        const float r0 = ref[((size_t)r * cL + l) * RD];
+        const float r1 = (RD == 2) ? ref[((size_t)r * cL + l) * RD + 1] : 0.f;
+        const float loc = centre_only ? r0 + off / (float)T : r0 + ((off / (float)cP) * r1) * 0.5f;
+        save_loc[so + j] = loc;
+        float gm;
+        const float ix = border_ix(loc, T, gm);
+        const float xf = floorf(ix);
+        const int x0 = (int)xf, a1 = min(x0 + 1, T - 1);
+        const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
+        const bool ok0 = !(mbase && mbase[st + x0]);
+        const bool ok1 = x0 + 1 < T && !(mbase && mbase[st + a1]);
+        srow0[j] = st + x0;
+        srow1[j] = st + a1;
+        sfl[j] = (ok0 ? 1 : 0) | (ok1 ? 2 : 0) | (x0 + 1 < T ? 4 : 0);
+        snw[j] = ((float)(x0 + 1) - ix);
+        sne[j] = (ix - xf);
+    }
+    __syncthreads();
+    const float4* vb = reinterpret_cast<const float4*>(value + (size_t)b * S * MD + (size_t)m * D) + tid;
+    const float4* ub = reinterpret_cast<const float4*>(U + (size_t)b * S * MD + (size_t)m * D) + tid;
+    const size_t MD4 = MD / 4;
+    const float4 hv = reinterpret_cast<const float4*>(att_h + (size_t)r * ldh)[tid];
+    const float4 wv = reinterpret_cast<const float4*>(aw)[tid];
+    float4* c4 = reinterpret_cast<float4*>(clip + so * D) + tid;
+    float4* a4 = reinterpret_cast<float4*>(att + so * D) + tid;
+    float4 cl[cNS];
+    float part[cNS];
+#pragma unroll
+    for (int k0 = 0; k0 < cNS; k0 += 4) {  // four samples' corner rows in flight at a time
+        float4 v0[4], v1[4], u0[4], u1[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const size_t o0 = (size_t)srow0[k0 + q] * MD4, o1 = (size_t)srow1[k0 + q] * MD4;
+            v0[q] = vb[o0];
+            v1[q] = vb[o1];
+            u0[q] = ub[o0];
+            u1[q] = ub[o1];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = k0 + q, fl = sfl[k];
+            const float nw = snw[k], ne = sne[k];
+            const bool k0ok = fl & 1, k1ok = fl & 2, hi = fl & 4;
+            cl[k] = make_float4((k0ok ? v0[q].x : 0.f) * nw + (k1ok ? v1[q].x : 0.f) * ne,
+                                (k0ok ? v0[q].y : 0.f) * nw + (k1ok ? v1[q].y : 0.f) * ne,
+                                (k0ok ? v0[q].z : 0.f) * nw + (k1ok ? v1[q].z : 0.f) * ne,
+                                (k0ok ? v0[q].w : 0.f) * nw + (k1ok ? v1[q].w : 0.f) * ne);
+            const float4 a = make_float4(u0[q].x * nw + (hi ? u1[q].x : 0.f) * ne, u0[q].y * nw + (hi ? u1[q].y : 0.f) * ne,
+                                         u0[q].z * nw + (hi ? u1[q].z : 0.f) * ne, u0[q].w * nw + (hi ? u1[q].w : 0.f) * ne);
+            c4[(size_t)k * D4] = cl[k];
+            a4[(size_t)k * D4] = a;
+            part[k] = 0.f + (tanhf(a.x + hv.x) * wv.x + tanhf(a.y + hv.y) * wv.y + tanhf(a.z + hv.z) * wv.z +
+                             tanhf(a.w + hv.w) * wv.w);
+        }
+    }
+    // softattn_fwd4_kernel's block sum, softmax and weighted sum
+    group_reduce_scatter<cNS, 16>(part, lane);
+    float v = part[0];
+    v += lane_swap(v, 16);
+    v += __shfl_xor(v, 32, 64);
+    if (lane < cNS) red[wid * cNS + lane] = v;
+    __syncthreads();
+    if (tid < cNS) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < kCSA / 64; ++w) t += red[w * cNS + tid];
+        red[2 * cNS + tid] = t;
+    }
+    __syncthreads();
+    const float* dots = red + 2 * cNS;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < cNS; ++k) mx = fmaxf(mx, dots[k] + ab[0]);
+    float p[cNS], sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < cNS; ++k) {
+        p[k] = expf(dots[k] + ab[0] - mx);
+        sum += p[k];
+    }
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int k = 0; k < cNS; ++k) p[k] = p[k] * inv;
+    if (tid < cNS) {
+        float pj = 0.f;
+#pragma unroll
+        for (int k = 0; k < cNS; ++k) pj = (k == tid) ? p[k] : pj;
+        probs[so + tid] = pj;
+    }
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < cNS; ++k) {
+        o.x += p[k] * cl[k].x;
+        o.y += p[k] * cl[k].y;
+        o.z += p[k] * cl[k].z;
+        o.w += p[k] * cl[k].w;
+    }
+    reinterpret_cast<float4*>(res + (size_t)r * MD + (size_t)m * D)[tid] = o;
+}
 }  // namespace pdvc
 
 using namespace pdvc;
@@ -636,4 +770,45 @@ extern "C" int pdvc_cap_value_grad_f32(const uint8_t* value_pad_mask, const int3
     return pdvc_cap_value_grad_ex_f32(value_pad_mask, level_T, num_levels, batch, num_heads, head_dim, num_point, rows,
                                       steps, max_rows_per_video, video_row_start, video_rows, save_loc, grad_samples,
                                       grad_value, nullptr, stream);
+}
+
+// One caption step's sampling of the value rows (with value_pad_mask) and of the projected ctx2att rows U (same shape,
+// no mask) plus the soft attention over the 16 samples: pdvc_cap_gather_forward_f32 twice and pdvc_softattn_forward_f32
+// in one launch, for head_dim = attention width = 512 (every cfg's cap_nheads 1).  Outputs as theirs.
+extern "C" int pdvc_cap_softattn_forward_f32(const float* value, const uint8_t* value_pad_mask, const float* U,
+                                             const int32_t* row_video, const float* offsets, int off_stride,
+                                             int off_col0, const float* off_add, const float* ref, int ref_dim,
+                                             int rd1_rows, const int32_t* level_T, int num_levels, int batch,
+                                             int rows, int num_heads, int head_dim, int num_point,
+                                             const float* att_h, int ld_att_h, const float* alpha_w,
+                                             const float* alpha_b, float* samples, float* save_loc, float* att,
+                                             float* probs, float* res, void* stream) {
+    CapLevels lv;
+    int S, lph, wpr;
+    int rc = cap_setup(level_T, num_levels, num_point, head_dim, num_heads, ref_dim, lv, S, lph, wpr);
+    if (rc) return rc;
+    if (head_dim != 512)
+        return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "fused caption step needs head_dim 512, got %d", head_dim);
+    PDVC_CHECK_ARG(U && att_h && alpha_w && alpha_b && samples && save_loc && att && probs && res,
+                   "fused caption step: NULL argument");
+    PDVC_CHECK_ARG(off_col0 >= 0 && off_col0 + num_heads * cNS <= off_stride, "offset columns out of range");
+    PDVC_CHECK_ARG(batch >= 0 && rows >= 0 && ld_att_h >= 512, "invalid sizes");
+    const void* al[] = {value, U, att_h, alpha_w, samples, att, res};
+    for (const void* q : al)
+        if ((uintptr_t)q % 16) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "fused caption step needs 16-B alignment");
+    if (ld_att_h % 4) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "fused caption step needs ld_att_h % 4 == 0");
+    const long nwg = (long)rows * num_heads;
+    if (nwg == 0) return PDVC_OK;
+    PDVC_CHECK_ARG(nwg < (1L << 31), "too many rows");
+    hipStream_t s = (hipStream_t)stream;
+    if (ref_dim == 1)
+        hipLaunchKernelGGL(cap_softattn_fwd_kernel<1>, dim3((unsigned)nwg), dim3(kCSA), 0, s, value, value_pad_mask, U,
+                           row_video, offsets, off_stride, off_col0, off_add, ref, rd1_rows, lv, S, num_heads, att_h,
+                           ld_att_h, alpha_w, alpha_b, samples, save_loc, att, probs, res);
+    else
+        hipLaunchKernelGGL(cap_softattn_fwd_kernel<2>, dim3((unsigned)nwg), dim3(kCSA), 0, s, value, value_pad_mask, U,
+                           row_video, offsets, off_stride, off_col0, off_add, ref, rd1_rows, lv, S, num_heads, att_h,
+                           ld_att_h, alpha_w, alpha_b, samples, save_loc, att, probs, res);
+    PDVC_CHECK_LAUNCH("cap_softattn_fwd_kernel");
+    return PDVC_OK;
 }

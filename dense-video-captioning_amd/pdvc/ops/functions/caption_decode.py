@@ -36,7 +36,15 @@ U_MAX_BYTES = 16 << 30  # largest projected-rows buffer of the gather form (ADVI
 # rounded freshly each step (they are written by the HIP kernels, which the mode's per-tensor rounding cache cannot
 # see) and the weights once per pass.
 BF16_RECURRENCE = os.environ.get("PDVC_BF16_RECURRENCE", "1") != "0"
+# a step's value and projected-row samples and its soft attention in one launch (pdvc_cap_softattn_forward_f32, the
+# 512-wide head of every cfg); PDVC_CAP_FUSED=0: the three launches (gather, gather, soft attention)
+CAP_FUSED = os.environ.get("PDVC_CAP_FUSED", "1") != "0"
 _BF16 = torch.bfloat16
+
+
+def _aligned16(*ptrs):
+    """every pointer 16-B aligned (the fused step reads and writes its rows as float4s)"""
+    return all(p % 16 == 0 for p in ptrs)
 
 
 def _gemm(inp, a, b, out, b16):
@@ -129,6 +137,10 @@ class CaptionDecodeFunction(Function):
         Wh16 = W_h.t().to(_BF16) if b16 else None
         Wctx16 = W_ctx.t().to(_BF16) if b16 else None
         Watt16 = W_att.t().to(_BF16) if b16 else None
+        # one launch per step for the value and projected-row samples and the soft attention (512-wide heads)
+        fused = (CAP_FUSED and U is not None and A == D == 512 and Ph % 4 == 0 and n_off % 4 == 0
+                 and _aligned16(_n.ptr(value), _n.ptr(U), _n.ptr(HP), _n.ptr(alpha_w), _n.ptr(CLIP), _n.ptr(ATT),
+                                _n.ptr(RES)))
         with fp32_gemms():  # the per-step GEMMs are routed here (_gemm), not by the mode
             for i in range(n):
                 s0, c = ranges[i]
@@ -141,19 +153,26 @@ class CaptionDecodeFunction(Function):
                     hp.copy_(b_h.expand(c, Ph))  # h_{-1} = 0
                 else:
                     _gemm(b_h, HS[rs, i - 1], W_h.t(), hp, Wh16)
-                _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video[rs]),
-                        _n.ptr(hp), Ph, 0, _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, D,
-                        NS // nl, _n.ptr(CLIP[i][rs]), _n.ptr(LOC[i][rs]), st)
                 att = ATT[i][s0 * ns_:(s0 + c) * ns_]
-                if U is not None:
-                    _n.call("pdvc_cap_gather_forward_f32", _n.ptr(U), None, _n.ptr(row_video[rs]), _n.ptr(hp), Ph, 0,
-                            _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, A, NS // nl,
-                            _n.ptr(att), None, st)
-                else:
-                    _gemm(b_ctx, CLIP[i][rs].reshape(-1, D), W_ctx.t(), att, Wctx16)
                 ah, ldh = _n.rows(hp[:, n_off:n_off + A])
-                _n.call("pdvc_softattn_forward_f32", _n.ptr(att), ah, ldh, _n.ptr(alpha_w), _n.ptr(alpha_b),
-                        _n.ptr(CLIP[i][rs]), c, M, A, D, _n.ptr(RES[i][rs]), _n.ptr(PROBS[i][rs]), st)
+                if fused:  # the two gathers and the soft attention in one launch
+                    _n.call("pdvc_cap_softattn_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(U),
+                            _n.ptr(row_video[rs]), _n.ptr(hp), Ph, 0, _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1,
+                            lvl, nl, Nv, c, M, D, NS // nl, ah, ldh, _n.ptr(alpha_w), _n.ptr(alpha_b),
+                            _n.ptr(CLIP[i][rs]), _n.ptr(LOC[i][rs]), _n.ptr(att), _n.ptr(PROBS[i][rs]),
+                            _n.ptr(RES[i][rs]), st)
+                else:
+                    _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video[rs]),
+                            _n.ptr(hp), Ph, 0, _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, D,
+                            NS // nl, _n.ptr(CLIP[i][rs]), _n.ptr(LOC[i][rs]), st)
+                    if U is not None:
+                        _n.call("pdvc_cap_gather_forward_f32", _n.ptr(U), None, _n.ptr(row_video[rs]), _n.ptr(hp), Ph,
+                                0, _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, A, NS // nl,
+                                _n.ptr(att), None, st)
+                    else:
+                        _gemm(b_ctx, CLIP[i][rs].reshape(-1, D), W_ctx.t(), att, Wctx16)
+                    _n.call("pdvc_softattn_forward_f32", _n.ptr(att), ah, ldh, _n.ptr(alpha_w), _n.ptr(alpha_b),
+                            _n.ptr(CLIP[i][rs]), c, M, A, D, _n.ptr(RES[i][rs]), _n.ptr(PROBS[i][rs]), st)
                 _gemm(None, RES[i][rs], W_att.t(), GATT[:c], Watt16)
                 xa, ldx = _n.rows(xe[i][rs])
                 gh, ldg = _n.rows(hp[:, n_off + A:])

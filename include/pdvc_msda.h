@@ -211,6 +211,19 @@ int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* value_pad_mas
                                 const float* ref, int ref_dim, int rd1_rows, const int32_t* level_T, int num_levels,
                                 int batch, int rows, int num_heads, int head_dim, int num_point, float* samples,
                                 float* save_loc, void* stream);
+/* One caption step's sampling of the value rows (with value_pad_mask) and of the projected ctx2att rows U (same
+ * shape, no mask) plus the soft attention over the 16 samples (pdvc_softattn_forward_f32 with att_h, alpha_w, alpha_b):
+ * pdvc_cap_gather_forward_f32 twice and pdvc_softattn_forward_f32 in one launch, for head_dim = the attention width
+ * = 512 (cap_nheads 1, every cfg).  value, U, att_h, alpha_w, samples, att and res 16-B aligned, ld_att_h % 4 == 0
+ * (else PDVC_ERR_UNSUPPORTED).  Outputs as theirs: samples (R,M,16,512), save_loc (R,M,16), att (R*M*16, 512),
+ * probs (R,M,16), res (R, M*512). */
+int pdvc_cap_softattn_forward_f32(const float* value, const uint8_t* value_pad_mask, const float* U,
+                                  const int32_t* row_video, const float* offsets, int off_stride, int off_col0,
+                                  const float* off_add, const float* ref, int ref_dim, int rd1_rows,
+                                  const int32_t* level_T, int num_levels, int batch, int rows, int num_heads,
+                                  int head_dim, int num_point, const float* att_h, int ld_att_h, const float* alpha_w,
+                                  const float* alpha_b, float* samples, float* save_loc, float* att, float* probs,
+                                  float* res, void* stream);
 /* grad_value and grad_ref (R,L,ref_dim, may be NULL) are ACCUMULATED (atomic adds; zero them before the first
  * call -- the caption decoder accumulates every step into one buffer); grad_offsets (R, off_stride): only the
  * offset columns are written (it is also the gradient of off_add). */

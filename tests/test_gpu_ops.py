@@ -602,6 +602,72 @@ def test_cap_gather_vs_oracle(D, M, ref_dim):
     close(rf.grad, exp_gr, 1e-4, "grad_ref")
 
 
+@pytest.mark.parametrize("M", [1, 2])
+@pytest.mark.parametrize("ref_dim", [1, 2])
+@pytest.mark.parametrize("masked", [False, True])
+def test_cap_softattn_forward_matches_three_launches(M, ref_dim, masked):
+    """pdvc_cap_softattn_forward_f32 (a caption step's value and projected-row samples and its soft attention in one
+    launch, 512-wide heads) against pdvc_cap_gather_forward_f32 on the value (with its mask), on U (without) and
+    pdvc_softattn_forward_f32: samples, save_loc and the U samples to 1e-6 of their magnitude (the same blends),
+    probabilities and the attended rows to 1e-5 (the same sums; the tolerance covers codegen contraction)."""
+    from pdvc import _native as _n
+    rng = np.random.RandomState(M + 10 * ref_dim + 100 * masked)
+    T_l = [24, 12, 6, 3]
+    S, N, R, D = sum(T_l), 3, 13, 512
+    value = cu(rng.randn(N, S, M, D), torch.float32)
+    U = cu(rng.randn(N, S, M, D) * 0.2, torch.float32)
+    mask = None
+    if masked:
+        mk = np.zeros((N, S), np.uint8)
+        mk[1, 5:9] = 1
+        mk[2, 30:33] = 1
+        mask = cu(mk)
+    row_video = cu(rng.randint(0, N, size=R).astype(np.int32))
+    off_stride = M * 16 + 4 + D  # the offsets at column 0, then the att_h block at a 16-B aligned column
+    hp = cu(rng.randn(R, off_stride) * 2.0, torch.float32)
+    off_add = cu(rng.randn(R, M * 16) * 0.5, torch.float32)
+    if ref_dim == 1:
+        ref = cu(rng.uniform(-0.1, 1.1, size=(R, 4, 1)), torch.float32)
+    else:
+        ref = cu(np.concatenate([rng.uniform(0, 1, size=(R, 4, 1)), rng.uniform(0.05, 0.9, size=(R, 4, 1))], -1),
+                 torch.float32)
+    rd1 = 4 if ref_dim == 2 else 0
+    aw = cu(rng.randn(D) * 0.1, torch.float32)
+    ab = cu(rng.randn(1), torch.float32)
+    ah, ldh = _n.rows(hp[:, M * 16 + 4:])
+    lvl = _n.int_array(T_l)
+    geo = (_n.ptr(row_video), _n.ptr(hp), off_stride, 0, _n.ptr(off_add), _n.ptr(ref), ref_dim, rd1, lvl, 4, N, R, M,
+           D, 4)
+    out = []
+    for fused in (False, True):
+        smp, loc = torch.empty(R, M, 16, D, device=DEV), torch.empty(R, M, 16, device=DEV)
+        att, probs, res = (torch.empty(R * M * 16, D, device=DEV), torch.empty(R, M, 16, device=DEV),
+                           torch.empty(R, M * D, device=DEV))
+        if fused:
+            _n.call("pdvc_cap_softattn_forward_f32", _n.ptr(value), _n.ptr(mask), _n.ptr(U), *geo, ah, ldh, _n.ptr(aw),
+                    _n.ptr(ab), _n.ptr(smp), _n.ptr(loc), _n.ptr(att), _n.ptr(probs), _n.ptr(res), _n.stream())
+        else:
+            _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(mask), *geo, _n.ptr(smp), _n.ptr(loc),
+                    _n.stream())
+            _n.call("pdvc_cap_gather_forward_f32", _n.ptr(U), None, *geo, _n.ptr(att), None, _n.stream())
+            _n.call("pdvc_softattn_forward_f32", _n.ptr(att), ah, ldh, _n.ptr(aw), _n.ptr(ab), _n.ptr(smp), R, M, D, D,
+                    _n.ptr(res), _n.ptr(probs), _n.stream())
+        torch.cuda.synchronize()
+        out.append((smp, loc, att, probs, res))
+    for name, a, b, tol in zip(("samples", "save_loc", "att", "probs", "res"), *out, (1e-6, 0.0, 1e-6, 1e-5, 1e-5)):
+        err = (a - b).abs().max().item()
+        assert err <= tol * (a.abs().max().item() + 1.0), (name, err)
+    assert out[1][3].max().item() < 0.99  # the soft attention is not degenerate
+
+
+def test_cap_softattn_forward_rejects_other_widths():
+    """the fused step is the 512-wide form only: any other head width is PDVC_ERR_UNSUPPORTED, not a wrong answer"""
+    from pdvc import _native as _n
+    with pytest.raises(Exception):
+        _n.call("pdvc_cap_softattn_forward_f32", *([None] * 5), 80, 0, None, None, 1, 0, _n.int_array([4, 2, 1, 1]),
+                4, 1, 1, 1, 64, 4, None, 64, *([None] * 7), _n.stream())
+
+
 # ------------------------------------------------------------------------------------------------
 # modules vs golden vectors generated from the reference modules
 # ------------------------------------------------------------------------------------------------
