@@ -44,7 +44,7 @@ _BF16 = torch.bfloat16
 
 def _aligned16(*ptrs):
     """every pointer 16-B aligned (the fused step reads and writes its rows as float4s)"""
-    return all(p % 16 == 0 for p in ptrs)
+    return all((p.value or 0) % 16 == 0 for p in ptrs)
 
 
 def _gemm(inp, a, b, out, b16):
