@@ -588,7 +588,7 @@ def main():
         step()
     log("timed steps")
     names = ["pdvc_msda1d_forward_f32", "pdvc_msda1d_backward_ex_f32", "pdvc_cap_gather_forward_f32",
-             "pdvc_cap_gather_backward_f32", "pdvc_cap_gather_backward2_f32", "pdvc_cap_softattn_forward_f32",
+             "pdvc_cap_gather_backward_f32", "pdvc_cap_gather_backward2_f32", "pdvc_cap_softattn_forward_f32", "pdvc_cap_softattn_backward_f32",
              "pdvc_softattn_forward_f32", "pdvc_seq_attention_forward_f32",
              "pdvc_seq_attention_backward_f32",
              # the bf16 mode's forms of the encoder's MSDA launches (also writing the bf16 GEMM operands)

@@ -557,8 +557,10 @@ __global__ __launch_bounds__(kCSA) void cap_softattn_fwd_kernel(
                                 (k0ok ? v0[q].w : 0.f) * nw + (k1ok ? v1[q].w : 0.f) * ne);
             const float4 a = make_float4(u0[q].x * nw + (hi ? u1[q].x : 0.f) * ne, u0[q].y * nw + (hi ? u1[q].y : 0.f) * ne,
                                          u0[q].z * nw + (hi ? u1[q].z : 0.f) * ne, u0[q].w * nw + (hi ? u1[q].w : 0.f) * ne);
-            c4[(size_t)k * D4] = cl[k];
-            a4[(size_t)k * D4] = a;
+            if (clip) {  // NULL: the fused backward re-forms the samples from their corners
+                c4[(size_t)k * D4] = cl[k];
+                a4[(size_t)k * D4] = a;
+            }
             part[k] = 0.f + (tanhf(a.x + hv.x) * wv.x + tanhf(a.y + hv.y) * wv.y + tanhf(a.z + hv.z) * wv.z +
                              tanhf(a.w + hv.w) * wv.w);
         }
@@ -605,6 +607,185 @@ __global__ __launch_bounds__(kCSA) void cap_softattn_fwd_kernel(
         o.w += p[k] * cl[k].w;
     }
     reinterpret_cast<float4*>(res + (size_t)r * MD + (size_t)m * D)[tid] = o;
+}
+
+// The backward of cap_softattn_fwd_kernel (512-wide head; the u_grad form of the caption decode): softattn_bwd4_kernel
+// (capstep.hip) and cap_gather_bwd_kernel with value2 = U in one launch.  The samples and att are re-formed from the
+// corner rows the location gradient reads anyway (the forward then writes neither); the sample gradients (p_k * dres)
+// and att gradients are written for the destination-sorted value / U passes after the loop.  A sample's location
+// gradient, dsample_k . (v1 - v0) + datt_k . (u1 - u0), factors as p_k (dres . (v1 - v0)) + dd_k (w (1 - t^2)) . (u1 - u0)
+// (dd_k the softmax backward's scalar): its two channel sums are reduced with the 16 dots in one block reduction,
+// and only the 16 tanh rows stay in registers for the att gradients.  One 128-thread workgroup per (row, head).
+constexpr int cRED = 3 * cNS;  // dots, value-difference sums, U-difference sums
+
+template <int RD>
+__global__ __launch_bounds__(kCSA) void cap_softattn_bwd_kernel(
+    const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ U,
+    const int32_t* __restrict__ row_video, const float* __restrict__ offsets, int off_stride, int off_col0,
+    const float* __restrict__ off_add, const float* __restrict__ ref, int rd1_rows, CapLevels lv, int S, int M,
+    const float* __restrict__ save_loc, const float* __restrict__ probs, const float* __restrict__ gres,
+    const float* __restrict__ att_h, int ldh, const float* __restrict__ aw, float* __restrict__ gatt,
+    float* __restrict__ gatt_h, int ldgh, float* __restrict__ gclip, float* __restrict__ gaw_part,
+    float* __restrict__ gab_part, float* __restrict__ grad_off, float* __restrict__ grad_ref) {
+    constexpr int D = 512, D4 = D / 4;
+    __shared__ int srow0[cNS], srow1[cNS], sfl[cNS];
+    __shared__ float snw[cNS], sne[cNS], red[(kCSA / 64 + 1) * cRED];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    const int r = wg / M, m = wg - r * M;
+    const int b = row_video[r];
+    const size_t MD = (size_t)M * D;
+    const size_t so = (size_t)wg * cNS;
+    float gm = 0.f;
+    int T = 1;
+    if (tid < cNS) {
+        const int j = tid, l = j >> 2;
+        T = lv.T[0] * (l == 0) + lv.T[1] * (l == 1) + lv.T[2] * (l == 2) + lv.T[3] * (l == 3);
+        const int st = lv.start[0] * (l == 0) + lv.start[1] * (l == 1) + lv.start[2] * (l == 2) + lv.start[3] * (l == 3);
+        const float ix = border_ix(save_loc[so + j], T, gm);
+        const float xf = floorf(ix);
+        const int x0 = (int)xf, a1 = min(x0 + 1, T - 1);
+        const uint8_t* mbase = vmask ? vmask + (size_t)b * S : nullptr;
+        const bool ok0 = !(mbase && mbase[st + x0]);
+        const bool ok1 = x0 + 1 < T && !(mbase && mbase[st + a1]);
+        srow0[j] = st + x0;
+        srow1[j] = st + a1;
+        sfl[j] = (ok0 ? 1 : 0) | (ok1 ? 2 : 0) | (x0 + 1 < T ? 4 : 0);
+        snw[j] = ((float)(x0 + 1) - ix);
+        sne[j] = (ix - xf);
+    }
+    __syncthreads();
+    const float4* vb = reinterpret_cast<const float4*>(value + (size_t)b * S * MD + (size_t)m * D) + tid;
+    const float4* ub = reinterpret_cast<const float4*>(U + (size_t)b * S * MD + (size_t)m * D) + tid;
+    const size_t MD4 = MD / 4;
+    const float4 g = reinterpret_cast<const float4*>(gres + (size_t)r * MD + (size_t)m * D)[tid];
+    const float4 hv = reinterpret_cast<const float4*>(att_h + (size_t)r * ldh)[tid];
+    const float4 wv = reinterpret_cast<const float4*>(aw)[tid];
+    float p[cNS];
+#pragma unroll
+    for (int k = 0; k < cNS; ++k) p[k] = probs[so + k];
+    float4* gc4 = reinterpret_cast<float4*>(gclip + so * D) + tid;
+    float4 th[cNS];    // tanh(att_k + att_h)
+    float part[cRED];  // [0,16): dres . sample_k   [16,32): dres . (v1 - v0)_k   [32,48): (w (1 - t^2)) . (u1 - u0)_k
+#pragma unroll
+    for (int k0 = 0; k0 < cNS; k0 += 4) {
+        float4 v0[4], v1[4], u0[4], u1[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const size_t o0 = (size_t)srow0[k0 + q] * MD4, o1 = (size_t)srow1[k0 + q] * MD4;
+            v0[q] = vb[o0];
+            v1[q] = vb[o1];
+            u0[q] = ub[o0];
+            u1[q] = ub[o1];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = k0 + q, fl = sfl[k];
+            const float nw = snw[k], ne = sne[k];
+            const bool k0ok = fl & 1, k1ok = fl & 2, hi = fl & 4;
+            const float4 a0 = make_float4(k0ok ? v0[q].x : 0.f, k0ok ? v0[q].y : 0.f, k0ok ? v0[q].z : 0.f,
+                                          k0ok ? v0[q].w : 0.f);
+            const float4 a1 = make_float4(k1ok ? v1[q].x : 0.f, k1ok ? v1[q].y : 0.f, k1ok ? v1[q].z : 0.f,
+                                          k1ok ? v1[q].w : 0.f);
+            const float4 cl = make_float4(a0.x * nw + a1.x * ne, a0.y * nw + a1.y * ne, a0.z * nw + a1.z * ne,
+                                          a0.w * nw + a1.w * ne);
+            const float4 h1 = make_float4(hi ? u1[q].x : 0.f, hi ? u1[q].y : 0.f, hi ? u1[q].z : 0.f,
+                                          hi ? u1[q].w : 0.f);
+            const float4 at = make_float4(u0[q].x * nw + h1.x * ne, u0[q].y * nw + h1.y * ne,
+                                          u0[q].z * nw + h1.z * ne, u0[q].w * nw + h1.w * ne);
+            th[k] = make_float4(tanhf(at.x + hv.x), tanhf(at.y + hv.y), tanhf(at.z + hv.z), tanhf(at.w + hv.w));
+            part[k] = 0.f + (g.x * cl.x + g.y * cl.y + g.z * cl.z + g.w * cl.w);
+            part[cNS + k] = g.x * (a1.x - a0.x) + g.y * (a1.y - a0.y) + g.z * (a1.z - a0.z) + g.w * (a1.w - a0.w);
+            part[2 * cNS + k] = wv.x * (1.f - th[k].x * th[k].x) * (h1.x - u0[q].x) +
+                                wv.y * (1.f - th[k].y * th[k].y) * (h1.y - u0[q].y) +
+                                wv.z * (1.f - th[k].z * th[k].z) * (h1.z - u0[q].z) +
+                                wv.w * (1.f - th[k].w * th[k].w) * (h1.w - u0[q].w);
+            gc4[(size_t)k * D4] = make_float4(p[k] * g.x, p[k] * g.y, p[k] * g.z, p[k] * g.w);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one chunk's 16 rows in flight at a time (registers: one wave per SIMD else)
+    }
+    // the 48 channel sums over the workgroup: lane r of each 16-lane group ends with values [3r, 3r + 3)
+    group_reduce_scatter<cRED, 16>(part, lane);
+#pragma unroll
+    for (int i = 0; i < cRED / 16; ++i) {
+        float v = part[i];
+        v += lane_swap(v, 16);
+        v += __shfl_xor(v, 32, 64);
+        if (lane < 16) red[wid * cRED + lane * (cRED / 16) + i] = v;
+    }
+    __syncthreads();
+    if (tid < cRED) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < kCSA / 64; ++w) t += red[w * cRED + tid];
+        red[(kCSA / 64) * cRED + tid] = t;
+    }
+    __syncthreads();
+    const float* dp = red + (kCSA / 64) * cRED;  // dots, then the two difference sums
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < cNS; ++k) t += p[k] * dp[k];
+    float dd[cNS], sb = 0.f;
+#pragma unroll
+    for (int k = 0; k < cNS; ++k) {
+        dd[k] = p[k] * (dp[k] - t);
+        sb += dd[k];
+    }
+    if (tid == 0) gab_part[wg] = sb;
+    float4* ga4 = reinterpret_cast<float4*>(gatt + so * D) + tid;
+    float4 gh = make_float4(0.f, 0.f, 0.f, 0.f), gw = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < cNS; ++k) {
+        const float tx = th[k].x, ty = th[k].y, tz = th[k].z, tw = th[k].w;
+        const float4 dpre = make_float4(dd[k] * wv.x * (1.f - tx * tx), dd[k] * wv.y * (1.f - ty * ty),
+                                        dd[k] * wv.z * (1.f - tz * tz), dd[k] * wv.w * (1.f - tw * tw));
+        ga4[(size_t)k * D4] = dpre;
+        gh.x += dpre.x; gh.y += dpre.y; gh.z += dpre.z; gh.w += dpre.w;
+        gw.x += dd[k] * tx; gw.y += dd[k] * ty; gw.z += dd[k] * tz; gw.w += dd[k] * tw;
+    }
+    if (M == 1) {
+        reinterpret_cast<float4*>(gatt_h + (size_t)r * ldgh)[tid] = gh;
+    } else {
+        float* gp = gatt_h + (size_t)r * ldgh + 4 * tid;
+        atomicAdd(gp, gh.x); atomicAdd(gp + 1, gh.y); atomicAdd(gp + 2, gh.z); atomicAdd(gp + 3, gh.w);
+    }
+    reinterpret_cast<float4*>(gaw_part + (size_t)wg * D)[tid] = gw;
+    if (tid < cNS) {  // offset and reference gradients of sample j (cap_gather_bwd_kernel's chain)
+        const int j = tid, l = j >> 2;
+        float pj = 0.f, dj = 0.f;
+#pragma unroll
+        for (int k = 0; k < cNS; ++k) {
+            pj = (k == j) ? p[k] : pj;
+            dj = (k == j) ? dd[k] : dj;
+        }
+        const float s = pj * dp[cNS + j] + dj * dp[2 * cNS + j];
+        const bool centre_only = (RD == 1) || (r < rd1_rows);
+        const float gloc = 2.f * (gm * s);  // grid = 2*loc - 1
+        float goff, gr0 = gloc, gr1 = 0.f;
+        if (centre_only) {
+            goff = gloc / (float)T;
+        } else {
+            const float r1 = ref[((size_t)r * cL + l) * 2 + 1];
+            const float t2 = gloc * 0.5f;
+            goff = (t2 * r1) / (float)cP;
+            float o = offsets[(size_t)r * off_stride + off_col0 + m * cNS + j];
+            if (off_add) o += off_add[((size_t)r * M + m) * cNS + j];
+            gr1 = t2 * (o / (float)cP);
+        }
+        grad_off[(size_t)r * off_stride + off_col0 + m * cNS + j] = goff;
+        if (grad_ref) {  // the level's four points summed, one atomic per (row, head, level)
+            gr0 += lane_swap(gr0, 1);
+            gr0 += lane_swap(gr0, 2);
+            if (RD == 2) {
+                gr1 += lane_swap(gr1, 1);
+                gr1 += lane_swap(gr1, 2);
+            }
+            if ((j & 3) == 0) {
+                atomicAdd(grad_ref + ((size_t)r * cL + l) * RD, gr0);
+                if (RD == 2) atomicAdd(grad_ref + ((size_t)r * cL + l) * RD + 1, gr1);
+            }
+        }
+    }
 }
 }  // namespace pdvc
 
@@ -789,7 +970,7 @@ extern "C" int pdvc_cap_softattn_forward_f32(const float* value, const uint8_t* 
     if (rc) return rc;
     if (head_dim != 512)
         return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "fused caption step needs head_dim 512, got %d", head_dim);
-    PDVC_CHECK_ARG(U && att_h && alpha_w && alpha_b && samples && save_loc && att && probs && res,
+    PDVC_CHECK_ARG(U && att_h && alpha_w && alpha_b && save_loc && probs && res && (!samples) == (!att),
                    "fused caption step: NULL argument");
     PDVC_CHECK_ARG(off_col0 >= 0 && off_col0 + num_heads * cNS <= off_stride, "offset columns out of range");
     PDVC_CHECK_ARG(batch >= 0 && rows >= 0 && ld_att_h >= 512, "invalid sizes");
@@ -810,5 +991,53 @@ extern "C" int pdvc_cap_softattn_forward_f32(const float* value, const uint8_t* 
                            row_video, offsets, off_stride, off_col0, off_add, ref, rd1_rows, lv, S, num_heads, att_h,
                            ld_att_h, alpha_w, alpha_b, samples, save_loc, att, probs, res);
     PDVC_CHECK_LAUNCH("cap_softattn_fwd_kernel");
+    return PDVC_OK;
+}
+
+// The backward of pdvc_cap_softattn_forward_f32 in the caption decoder's u_grad form (the value and U gradients come
+// from the destination-sorted passes after the loop): pdvc_softattn_backward_f32 and pdvc_cap_gather_backward2_f32 in
+// one launch, re-forming the samples and att from their corner rows (the forward may then skip writing them).
+extern "C" int pdvc_cap_softattn_backward_f32(const float* value, const uint8_t* value_pad_mask, const float* U,
+                                              const int32_t* row_video, const float* offsets, int off_stride,
+                                              int off_col0, const float* off_add, const float* ref, int ref_dim,
+                                              int rd1_rows, const int32_t* level_T, int num_levels, int batch,
+                                              int rows, int num_heads, int head_dim, int num_point,
+                                              const float* save_loc, const float* probs, const float* grad_res,
+                                              const float* att_h, int ld_att_h, const float* alpha_w,
+                                              float* grad_att, float* grad_att_h, int ld_grad_att_h,
+                                              float* grad_samples, float* grad_alpha_w_part,
+                                              float* grad_alpha_b_part, float* grad_offsets, float* grad_ref,
+                                              void* stream) {
+    CapLevels lv;
+    int S, lph, wpr;
+    int rc = cap_setup(level_T, num_levels, num_point, head_dim, num_heads, ref_dim, lv, S, lph, wpr);
+    if (rc) return rc;
+    if (head_dim != 512)
+        return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "fused caption step needs head_dim 512, got %d", head_dim);
+    PDVC_CHECK_ARG(value && U && row_video && offsets && ref && save_loc && probs && grad_res && att_h && alpha_w &&
+                       grad_att && grad_att_h && grad_samples && grad_alpha_w_part && grad_alpha_b_part &&
+                       grad_offsets, "fused caption step backward: NULL argument");
+    PDVC_CHECK_ARG(off_col0 >= 0 && off_col0 + num_heads * cNS <= off_stride, "offset columns out of range");
+    PDVC_CHECK_ARG(batch >= 0 && rows >= 0 && ld_att_h >= 512 && ld_grad_att_h >= 512, "invalid sizes");
+    const void* al[] = {value, U, grad_res, att_h, alpha_w, grad_att, grad_att_h, grad_samples, grad_alpha_w_part};
+    for (const void* q : al)
+        if ((uintptr_t)q % 16) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "fused caption step needs 16-B alignment");
+    if (ld_att_h % 4 || ld_grad_att_h % 4)
+        return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "fused caption step needs row strides % 4 == 0");
+    const long nwg = (long)rows * num_heads;
+    if (nwg == 0) return PDVC_OK;
+    PDVC_CHECK_ARG(nwg < (1L << 31), "too many rows");
+    hipStream_t s = (hipStream_t)stream;
+    if (ref_dim == 1)
+        hipLaunchKernelGGL(cap_softattn_bwd_kernel<1>, dim3((unsigned)nwg), dim3(kCSA), 0, s, value, value_pad_mask, U,
+                           row_video, offsets, off_stride, off_col0, off_add, ref, rd1_rows, lv, S, num_heads,
+                           save_loc, probs, grad_res, att_h, ld_att_h, alpha_w, grad_att, grad_att_h, ld_grad_att_h,
+                           grad_samples, grad_alpha_w_part, grad_alpha_b_part, grad_offsets, grad_ref);
+    else
+        hipLaunchKernelGGL(cap_softattn_bwd_kernel<2>, dim3((unsigned)nwg), dim3(kCSA), 0, s, value, value_pad_mask, U,
+                           row_video, offsets, off_stride, off_col0, off_add, ref, rd1_rows, lv, S, num_heads,
+                           save_loc, probs, grad_res, att_h, ld_att_h, alpha_w, grad_att, grad_att_h, ld_grad_att_h,
+                           grad_samples, grad_alpha_w_part, grad_alpha_b_part, grad_offsets, grad_ref);
+    PDVC_CHECK_LAUNCH("cap_softattn_bwd_kernel");
     return PDVC_OK;
 }

@@ -34,6 +34,8 @@ SIGNATURES = {
     "pdvc_cap_gather_backward2_f32": [_vp, _u8p, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _vp] + [_i] * 6 + [_vp] * 8,
     "pdvc_cap_softattn_forward_f32": [_vp, _u8p, _vp, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _vp] + [_i] * 6
     + [_vp, _i] + [_vp] * 8,
+    "pdvc_cap_softattn_backward_f32": [_vp, _u8p, _vp, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _vp] + [_i] * 6
+    + [_vp] * 4 + [_i] + [_vp] * 3 + [_i] + [_vp] * 6,
     "pdvc_cap_value_grad_f32": [_u8p, _vp] + [_i] * 8 + [_vp] * 6,
     "pdvc_cap_value_grad_ex_f32": [_u8p, _vp] + [_i] * 8 + [_vp] * 7,
     "pdvc_cap_value_grad_ranged_f32": [_u8p, _vp] + [_i] * 8 + [_vp] * 8,

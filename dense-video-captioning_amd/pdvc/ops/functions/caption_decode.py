@@ -39,6 +39,9 @@ BF16_RECURRENCE = os.environ.get("PDVC_BF16_RECURRENCE", "1") != "0"
 # a step's value and projected-row samples and its soft attention in one launch (pdvc_cap_softattn_forward_f32, the
 # 512-wide head of every cfg); PDVC_CAP_FUSED=0: the three launches (gather, gather, soft attention)
 CAP_FUSED = os.environ.get("PDVC_CAP_FUSED", "1") != "0"
+# ... and its backward in one launch (pdvc_cap_softattn_backward_f32, U-gradient form), re-forming the samples and att
+# from their corner rows: the forward then writes neither.  PDVC_CAP_FUSED_BWD=0: the two backward launches
+CAP_FUSED_BWD = os.environ.get("PDVC_CAP_FUSED_BWD", "1") != "0"
 _BF16 = torch.bfloat16
 
 
@@ -102,9 +105,7 @@ class CaptionDecodeFunction(Function):
         lvl, nl = _levels(level_T)
         kw = dict(dtype=value.dtype, device=value.device)
         HP = torch.empty((n, R, Ph), **kw)
-        CLIP = torch.empty((n, R, M, NS, D), **kw)
         LOC = torch.empty((n, R, M, NS), **kw)
-        ATT = torch.empty((n, R * M * NS, A), **kw)
         PROBS = torch.empty((n, R, M, NS), **kw)
         RES = (torch.zeros if ranged else torch.empty)((n, R, M * D), **kw)
         ACTS = torch.empty((n, R, G), **kw)
@@ -129,6 +130,14 @@ class CaptionDecodeFunction(Function):
         # and the value gradient's ctx2att part dU W_ctx are GEMMs over N*S rows instead of n*R*16, and the
         # location gradient of att is read off U at the sample corners (pdvc_cap_gather_backward2_f32)
         ctx.u_grad = U is not None and U_GRAD and A == D and video_csr is not None
+        # one launch per step for the value and projected-row samples and the soft attention (512-wide heads)
+        fused = (CAP_FUSED and U is not None and A == D == 512 and Ph % 4 == 0 and n_off % 4 == 0
+                 and _aligned16(_n.ptr(value), _n.ptr(U), _n.ptr(HP), _n.ptr(alpha_w)))
+        # ... and its backward: the samples and att are re-formed there, so they are neither written nor kept
+        ctx.fused_bwd = fused and ctx.u_grad and CAP_FUSED_BWD
+        keep = 0 if ctx.fused_bwd else n
+        CLIP = torch.empty((keep, R, M, NS, D), **kw)
+        ATT = torch.empty((keep, R * M * NS, A), **kw)
         if ranged and not ctx.u_grad:  # dW_ctx reads CLIP and dATT over every (step, row): no stale entries
             CLIP.zero_()
         ns_ = M * NS
@@ -137,10 +146,6 @@ class CaptionDecodeFunction(Function):
         Wh16 = W_h.t().to(_BF16) if b16 else None
         Wctx16 = W_ctx.t().to(_BF16) if b16 else None
         Watt16 = W_att.t().to(_BF16) if b16 else None
-        # one launch per step for the value and projected-row samples and the soft attention (512-wide heads)
-        fused = (CAP_FUSED and U is not None and A == D == 512 and Ph % 4 == 0 and n_off % 4 == 0
-                 and _aligned16(_n.ptr(value), _n.ptr(U), _n.ptr(HP), _n.ptr(alpha_w), _n.ptr(CLIP), _n.ptr(ATT),
-                                _n.ptr(RES)))
         with fp32_gemms():  # the per-step GEMMs are routed here (_gemm), not by the mode
             for i in range(n):
                 s0, c = ranges[i]
@@ -153,14 +158,14 @@ class CaptionDecodeFunction(Function):
                     hp.copy_(b_h.expand(c, Ph))  # h_{-1} = 0
                 else:
                     _gemm(b_h, HS[rs, i - 1], W_h.t(), hp, Wh16)
-                att = ATT[i][s0 * ns_:(s0 + c) * ns_]
+                att = None if ctx.fused_bwd else ATT[i][s0 * ns_:(s0 + c) * ns_]
                 ah, ldh = _n.rows(hp[:, n_off:n_off + A])
                 if fused:  # the two gathers and the soft attention in one launch
                     _n.call("pdvc_cap_softattn_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(U),
                             _n.ptr(row_video[rs]), _n.ptr(hp), Ph, 0, _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1,
                             lvl, nl, Nv, c, M, D, NS // nl, ah, ldh, _n.ptr(alpha_w), _n.ptr(alpha_b),
-                            _n.ptr(CLIP[i][rs]), _n.ptr(LOC[i][rs]), _n.ptr(att), _n.ptr(PROBS[i][rs]),
-                            _n.ptr(RES[i][rs]), st)
+                            None if ctx.fused_bwd else _n.ptr(CLIP[i][rs]), _n.ptr(LOC[i][rs]), _n.ptr(att),
+                            _n.ptr(PROBS[i][rs]), _n.ptr(RES[i][rs]), st)
                 else:
                     _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(row_video[rs]),
                             _n.ptr(hp), Ph, 0, _n.ptr(off_hs[rs]), _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, D,
@@ -244,27 +249,37 @@ class CaptionDecodeFunction(Function):
                     _gemm(None, dhp[:, n_off + A:], W_att, dRES[:c], Watt16)
                     ah, ldh = _n.rows(HP[i][rs][:, n_off:n_off + A])
                     gah, ldgah = _n.rows(dhp[:, n_off:n_off + A])
-                    att = ATT[i][s0 * ns_:(s0 + c) * ns_]
                     datt = dATT[i][s0 * ns_:(s0 + c) * ns_]
-                    _n.call("pdvc_softattn_backward_f32", _n.ptr(att), ah, ldh, _n.ptr(alpha_w), _n.ptr(CLIP[i][rs]),
-                            _n.ptr(PROBS[i][rs]), _n.ptr(dRES), c, M, A, D, _n.ptr(datt), gah, ldgah, _n.ptr(dCLIP),
-                            _n.ptr(GAW[i][s0 * M:(s0 + c) * M]), _n.ptr(GAB[i][s0 * M:(s0 + c) * M]), st)
                     gr_ = gr[rs] if gr is not None else None
-                    if u_grad:  # dCLIP keeps the soft-attention part only; att's location gradient read off U
-                        _n.call("pdvc_cap_gather_backward2_f32", _n.ptr(value), _n.ptr(pad_mask),
+                    if ctx.fused_bwd:  # the soft attention's and the sampling's backward in one launch
+                        _n.call("pdvc_cap_softattn_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(U),
                                 _n.ptr(row_video[rs]), _n.ptr(HP[i][rs]), Ph, 0, _n.ptr(off_hs[rs]), _n.ptr(ref[rs]),
-                                RD, rd1, lvl, nl, Nv, c, M, D, NS // nl, _n.ptr(LOC[i][rs]), _n.ptr(dCLIP), None,
-                                _n.ptr(dhp), _n.ptr(gr_), _n.ptr(U), _n.ptr(datt), st)
+                                RD, rd1, lvl, nl, Nv, c, M, D, NS // nl, _n.ptr(LOC[i][rs]), _n.ptr(PROBS[i][rs]),
+                                _n.ptr(dRES), ah, ldh, _n.ptr(alpha_w), _n.ptr(datt), gah, ldgah, _n.ptr(dCLIP),
+                                _n.ptr(GAW[i][s0 * M:(s0 + c) * M]), _n.ptr(GAB[i][s0 * M:(s0 + c) * M]), _n.ptr(dhp),
+                                _n.ptr(gr_), st)
                     else:
-                        if b16:
-                            dc_ = dCLIP.reshape(-1, D)
-                            _gemm(dc_, datt, W_ctx, dc_, Wctx16)
+                        att = ATT[i][s0 * ns_:(s0 + c) * ns_]
+                        _n.call("pdvc_softattn_backward_f32", _n.ptr(att), ah, ldh, _n.ptr(alpha_w),
+                                _n.ptr(CLIP[i][rs]), _n.ptr(PROBS[i][rs]), _n.ptr(dRES), c, M, A, D, _n.ptr(datt),
+                                gah, ldgah, _n.ptr(dCLIP), _n.ptr(GAW[i][s0 * M:(s0 + c) * M]),
+                                _n.ptr(GAB[i][s0 * M:(s0 + c) * M]), st)
+                        if u_grad:  # dCLIP keeps the soft-attention part only; att's location gradient read off U
+                            _n.call("pdvc_cap_gather_backward2_f32", _n.ptr(value), _n.ptr(pad_mask),
+                                    _n.ptr(row_video[rs]), _n.ptr(HP[i][rs]), Ph, 0, _n.ptr(off_hs[rs]),
+                                    _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, D, NS // nl, _n.ptr(LOC[i][rs]),
+                                    _n.ptr(dCLIP), None, _n.ptr(dhp), _n.ptr(gr_), _n.ptr(U), _n.ptr(datt), st)
                         else:
-                            dCLIP.reshape(-1, D).addmm_(datt, W_ctx)
-                        _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(pad_mask),
-                                _n.ptr(row_video[rs]), _n.ptr(HP[i][rs]), Ph, 0, _n.ptr(off_hs[rs]),
-                                _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, D, NS // nl, _n.ptr(LOC[i][rs]),
-                                _n.ptr(dCLIP), None if deferred else _n.ptr(gv), _n.ptr(dhp), _n.ptr(gr_), st)
+                            if b16:
+                                dc_ = dCLIP.reshape(-1, D)
+                                _gemm(dc_, datt, W_ctx, dc_, Wctx16)
+                            else:
+                                dCLIP.reshape(-1, D).addmm_(datt, W_ctx)
+                            _n.call("pdvc_cap_gather_backward_f32", _n.ptr(value), _n.ptr(pad_mask),
+                                    _n.ptr(row_video[rs]), _n.ptr(HP[i][rs]), Ph, 0, _n.ptr(off_hs[rs]),
+                                    _n.ptr(ref[rs]), RD, rd1, lvl, nl, Nv, c, M, D, NS // nl, _n.ptr(LOC[i][rs]),
+                                    _n.ptr(dCLIP), None if deferred else _n.ptr(gv), _n.ptr(dhp), _n.ptr(gr_),
+                                    st)
                 if i > 0:  # dh of step i - 1's rows (rows that stopped at step i have dHP[i] = 0 there)
                     p0, pc = ranges[i - 1]
                     if pc > 0:

@@ -216,7 +216,7 @@ int pdvc_cap_gather_forward_f32(const float* value, const uint8_t* value_pad_mas
  * pdvc_cap_gather_forward_f32 twice and pdvc_softattn_forward_f32 in one launch, for head_dim = the attention width
  * = 512 (cap_nheads 1, every cfg).  value, U, att_h, alpha_w, samples, att and res 16-B aligned, ld_att_h % 4 == 0
  * (else PDVC_ERR_UNSUPPORTED).  Outputs as theirs: samples (R,M,16,512), save_loc (R,M,16), att (R*M*16, 512),
- * probs (R,M,16), res (R, M*512). */
+ * probs (R,M,16), res (R, M*512); samples and att may both be NULL (pdvc_cap_softattn_backward_f32 re-forms them). */
 int pdvc_cap_softattn_forward_f32(const float* value, const uint8_t* value_pad_mask, const float* U,
                                   const int32_t* row_video, const float* offsets, int off_stride, int off_col0,
                                   const float* off_add, const float* ref, int ref_dim, int rd1_rows,
@@ -224,6 +224,21 @@ int pdvc_cap_softattn_forward_f32(const float* value, const uint8_t* value_pad_m
                                   int head_dim, int num_point, const float* att_h, int ld_att_h, const float* alpha_w,
                                   const float* alpha_b, float* samples, float* save_loc, float* att, float* probs,
                                   float* res, void* stream);
+/* The backward of pdvc_cap_softattn_forward_f32 in the caption decoder's U-gradient form (the value and U gradients
+ * come from pdvc_cap_value_grad_ranged_f32 after the loop): pdvc_softattn_backward_f32 and
+ * pdvc_cap_gather_backward2_f32 (value2 = U) in one launch, re-forming the samples and att from their corner rows.
+ * Writes grad_att (R*M*16, 512), grad_samples (R,M,16,512), grad_alpha_w_part (R*M, 512), grad_alpha_b_part (R*M),
+ * grad_att_h (written at M == 1, accumulated otherwise) and the offset columns of grad_offsets (row stride off_stride);
+ * grad_ref (may be NULL) is ACCUMULATED.  Alignment as pdvc_cap_softattn_forward_f32. */
+int pdvc_cap_softattn_backward_f32(const float* value, const uint8_t* value_pad_mask, const float* U,
+                                   const int32_t* row_video, const float* offsets, int off_stride, int off_col0,
+                                   const float* off_add, const float* ref, int ref_dim, int rd1_rows,
+                                   const int32_t* level_T, int num_levels, int batch, int rows, int num_heads,
+                                   int head_dim, int num_point, const float* save_loc, const float* probs,
+                                   const float* grad_res, const float* att_h, int ld_att_h, const float* alpha_w,
+                                   float* grad_att, float* grad_att_h, int ld_grad_att_h, float* grad_samples,
+                                   float* grad_alpha_w_part, float* grad_alpha_b_part, float* grad_offsets,
+                                   float* grad_ref, void* stream);
 /* grad_value and grad_ref (R,L,ref_dim, may be NULL) are ACCUMULATED (atomic adds; zero them before the first
  * call -- the caption decoder accumulates every step into one buffer); grad_offsets (R, off_stride): only the
  * offset columns are written (it is also the gradient of off_add). */

@@ -660,6 +660,75 @@ def test_cap_softattn_forward_matches_three_launches(M, ref_dim, masked):
     assert out[1][3].max().item() < 0.99  # the soft attention is not degenerate
 
 
+@pytest.mark.parametrize("M", [1, 2])
+@pytest.mark.parametrize("ref_dim", [1, 2])
+@pytest.mark.parametrize("masked", [False, True])
+def test_cap_softattn_backward_matches_two_launches(M, ref_dim, masked):
+    """pdvc_cap_softattn_backward_f32 (the soft attention's and the sampling's backward in one launch, the samples and
+    att re-formed from their corner rows) against pdvc_softattn_backward_f32 + pdvc_cap_gather_backward2_f32 (value2
+    = U) on the forward's saved tensors: the att and sample gradients, the att_h, alpha_w and alpha_b gradients to
+    1e-5 of their magnitude (the same expressions, the dots reduced in another order), the offset and reference
+    gradients to 1e-4 (the location gradient's channel sums taken as p_k (dres . dv) + dd_k (w (1 - t^2) . du))."""
+    from pdvc import _native as _n
+    rng = np.random.RandomState(7 + M + 10 * ref_dim + 100 * masked)
+    T_l = [24, 12, 6, 3]
+    S, N, R, D = sum(T_l), 3, 13, 512
+    value = cu(rng.randn(N, S, M, D), torch.float32)
+    U = cu(rng.randn(N, S, M, D) * 0.2, torch.float32)
+    mask = None
+    if masked:
+        mk = np.zeros((N, S), np.uint8)
+        mk[1, 5:9] = 1
+        mk[2, 30:33] = 1
+        mask = cu(mk)
+    row_video = cu(rng.randint(0, N, size=R).astype(np.int32))
+    off_stride = M * 16 + 4 + D
+    hp = cu(rng.randn(R, off_stride) * 2.0, torch.float32)
+    off_add = cu(rng.randn(R, M * 16) * 0.5, torch.float32)
+    if ref_dim == 1:
+        ref = cu(rng.uniform(-0.1, 1.1, size=(R, 4, 1)), torch.float32)
+    else:
+        ref = cu(np.concatenate([rng.uniform(0, 1, size=(R, 4, 1)), rng.uniform(0.05, 0.9, size=(R, 4, 1))], -1),
+                 torch.float32)
+    rd1 = 4 if ref_dim == 2 else 0
+    aw = cu(rng.randn(D) * 0.1, torch.float32)
+    ab = cu(rng.randn(1), torch.float32)
+    ah, ldh = _n.rows(hp[:, M * 16 + 4:])
+    lvl = _n.int_array(T_l)
+    geo = (_n.ptr(row_video), _n.ptr(hp), off_stride, 0, _n.ptr(off_add), _n.ptr(ref), ref_dim, rd1, lvl, 4, N, R, M,
+           D, 4)
+    smp, loc = torch.empty(R, M, 16, D, device=DEV), torch.empty(R, M, 16, device=DEV)
+    att, probs, res = (torch.empty(R * M * 16, D, device=DEV), torch.empty(R, M, 16, device=DEV),
+                       torch.empty(R, M * D, device=DEV))
+    _n.call("pdvc_cap_softattn_forward_f32", _n.ptr(value), _n.ptr(mask), _n.ptr(U), *geo, ah, ldh, _n.ptr(aw),
+            _n.ptr(ab), _n.ptr(smp), _n.ptr(loc), _n.ptr(att), _n.ptr(probs), _n.ptr(res), _n.stream())
+    dres = cu(rng.randn(R, M * D), torch.float32)
+    out = []
+    for fused in (False, True):
+        datt, dsmp = torch.empty(R * M * 16, D, device=DEV), torch.empty(R, M, 16, D, device=DEV)
+        gaw, gab = torch.empty(R * M, D, device=DEV), torch.empty(R * M, device=DEV)
+        dhp = torch.zeros(R, off_stride, device=DEV)
+        gr = torch.zeros_like(ref)
+        gah, ldgah = _n.rows(dhp[:, M * 16 + 4:])
+        if fused:
+            _n.call("pdvc_cap_softattn_backward_f32", _n.ptr(value), _n.ptr(mask), _n.ptr(U), *geo, _n.ptr(loc),
+                    _n.ptr(probs), _n.ptr(dres), ah, ldh, _n.ptr(aw), _n.ptr(datt), gah, ldgah, _n.ptr(dsmp),
+                    _n.ptr(gaw), _n.ptr(gab), _n.ptr(dhp), _n.ptr(gr), _n.stream())
+        else:
+            _n.call("pdvc_softattn_backward_f32", _n.ptr(att), ah, ldh, _n.ptr(aw), _n.ptr(smp), _n.ptr(probs),
+                    _n.ptr(dres), R, M, D, D, _n.ptr(datt), gah, ldgah, _n.ptr(dsmp), _n.ptr(gaw), _n.ptr(gab),
+                    _n.stream())
+            _n.call("pdvc_cap_gather_backward2_f32", _n.ptr(value), _n.ptr(mask), *geo, _n.ptr(loc), _n.ptr(dsmp),
+                    None, _n.ptr(dhp), _n.ptr(gr), _n.ptr(U), _n.ptr(datt), _n.stream())
+        torch.cuda.synchronize()
+        out.append((datt, dsmp, gaw, gab, dhp[:, M * 16 + 4:], dhp[:, :M * 16], gr))
+    names = ("grad_att", "grad_samples", "grad_alpha_w", "grad_alpha_b", "grad_att_h", "grad_offsets", "grad_ref")
+    for name, a, b, tol in zip(names, *out, (1e-5,) * 5 + (1e-4, 1e-4)):
+        err = (a - b).abs().max().item()
+        assert err <= tol * (a.abs().max().item() + 1.0), (name, err)
+    assert out[0][5].abs().max().item() > 0 and out[0][6].abs().max().item() > 0
+
+
 def test_cap_softattn_forward_rejects_other_widths():
     """the fused step is the 512-wide form only: any other head width is PDVC_ERR_UNSUPPORTED, not a wrong answer"""
     from pdvc import _native as _n
