@@ -27,6 +27,7 @@ gradient accumulation then joins the default stream ended in a crash at capture 
 (tests/test_gpu_batch.py test_capacity_step_graph_follows_a_ragged_stream, tools/diag_capacity_capture.py).
 """
 import ctypes
+import gc
 import os
 import threading
 
@@ -154,12 +155,20 @@ class StepGraph:
         begin_capture()  # bf16 mode: every operand rounding of the step becomes a node of the graph
         if reducer is not None:
             reducer.suspended = True
+        # no garbage collection inside the capture: a collection there runs the destructors of unrelated cyclic
+        # garbage (autograd graphs of earlier eager steps, their tensors) while the stream captures, which aborted the
+        # process with no HIP message (round 4: the step-graph test after the other model suites, only when the
+        # collector's thresholds happened to fall inside the capture); torch.cuda.graph collects once on entry
+        gc_enabled = gc.isenabled()
+        gc.disable()
         try:
             with torch.cuda.graph(self.graph):
                 if reducer is not None and reducer.flats is not None:
                     reducer.zero_grad()  # every replay starts from zeroed buckets (a fill node per bucket)
                 self.total, self.losses = self._forward_backward()
         finally:
+            if gc_enabled:
+                gc.enable()
             if reducer is not None:
                 reducer.suspended = False
         if debug_dot:
