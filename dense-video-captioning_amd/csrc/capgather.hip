@@ -484,7 +484,7 @@ static int cap_setup(const int32_t* level_T, int num_levels, int num_point, int 
 // -------------------------------------------------------------------------------------------------
 constexpr int kCSA = 128;  // threads per fused caption-step workgroup (512 channels as float4s)
 
-template <int RD>
+template <int RD, int CH>
 __global__ __launch_bounds__(kCSA) void cap_softattn_fwd_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ U,
     const int32_t* __restrict__ row_video, const float* __restrict__ offsets, int off_stride, int off_col0,
@@ -536,10 +536,10 @@ __global__ __launch_bounds__(kCSA) void cap_softattn_fwd_kernel(
     float4 cl[cNS];
     float part[cNS];
 #pragma unroll
-    for (int k0 = 0; k0 < cNS; k0 += 4) {  // four samples' corner rows in flight at a time
-        float4 v0[4], v1[4], u0[4], u1[4];
+    for (int k0 = 0; k0 < cNS; k0 += CH) {  // CH samples' corner rows per chunk (CH = 4: 228 registers, 1: 160)
+        float4 v0[CH], v1[CH], u0[CH], u1[CH];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < CH; ++q) {
             const size_t o0 = (size_t)srow0[k0 + q] * MD4, o1 = (size_t)srow1[k0 + q] * MD4;
             v0[q] = vb[o0];
             v1[q] = vb[o1];
@@ -547,7 +547,7 @@ __global__ __launch_bounds__(kCSA) void cap_softattn_fwd_kernel(
             u1[q] = ub[o1];
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < CH; ++q) {
             const int k = k0 + q, fl = sfl[k];
             const float nw = snw[k], ne = sne[k];
             const bool k0ok = fl & 1, k1ok = fl & 2, hi = fl & 4;
@@ -618,7 +618,7 @@ __global__ __launch_bounds__(kCSA) void cap_softattn_fwd_kernel(
 // and only the 16 tanh rows stay in registers for the att gradients.  One 128-thread workgroup per (row, head).
 constexpr int cRED = 3 * cNS;  // dots, value-difference sums, U-difference sums
 
-template <int RD>
+template <int RD, int CH>
 __global__ __launch_bounds__(kCSA) void cap_softattn_bwd_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ U,
     const int32_t* __restrict__ row_video, const float* __restrict__ offsets, int off_stride, int off_col0,
@@ -668,10 +668,10 @@ __global__ __launch_bounds__(kCSA) void cap_softattn_bwd_kernel(
     float4 th[cNS];    // tanh(att_k + att_h)
     float part[cRED];  // [0,16): dres . sample_k   [16,32): dres . (v1 - v0)_k   [32,48): (w (1 - t^2)) . (u1 - u0)_k
 #pragma unroll
-    for (int k0 = 0; k0 < cNS; k0 += 4) {
-        float4 v0[4], v1[4], u0[4], u1[4];
+    for (int k0 = 0; k0 < cNS; k0 += CH) {  // CH samples' corner rows per chunk
+        float4 v0[CH], v1[CH], u0[CH], u1[CH];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < CH; ++q) {
             const size_t o0 = (size_t)srow0[k0 + q] * MD4, o1 = (size_t)srow1[k0 + q] * MD4;
             v0[q] = vb[o0];
             v1[q] = vb[o1];
@@ -679,7 +679,7 @@ __global__ __launch_bounds__(kCSA) void cap_softattn_bwd_kernel(
             u1[q] = ub[o1];
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < CH; ++q) {
             const int k = k0 + q, fl = sfl[k];
             const float nw = snw[k], ne = sne[k];
             const bool k0ok = fl & 1, k1ok = fl & 2, hi = fl & 4;
@@ -702,7 +702,9 @@ __global__ __launch_bounds__(kCSA) void cap_softattn_bwd_kernel(
                                 wv.w * (1.f - th[k].w * th[k].w) * (h1.w - u0[q].w);
             gc4[(size_t)k * D4] = make_float4(p[k] * g.x, p[k] * g.y, p[k] * g.z, p[k] * g.w);
         }
-        __builtin_amdgcn_sched_barrier(0);  // one chunk's 16 rows in flight at a time (registers: one wave per SIMD else)
+        // CH = 4: one chunk's 16 rows in flight at a time (454 registers without the barrier, 449 with: one wave per
+        // SIMD); CH = 1: 252 registers, two waves per SIMD, the scheduler hoisting the next samples' loads itself
+        if constexpr (CH > 1) __builtin_amdgcn_sched_barrier(0);
     }
     // the 48 channel sums over the workgroup: lane r of each 16-lane group ends with values [3r, 3r + 3)
     group_reduce_scatter<cRED, 16>(part, lane);
@@ -982,14 +984,15 @@ extern "C" int pdvc_cap_softattn_forward_f32(const float* value, const uint8_t* 
     if (nwg == 0) return PDVC_OK;
     PDVC_CHECK_ARG(nwg < (1L << 31), "too many rows");
     hipStream_t s = (hipStream_t)stream;
-    if (ref_dim == 1)
-        hipLaunchKernelGGL(cap_softattn_fwd_kernel<1>, dim3((unsigned)nwg), dim3(kCSA), 0, s, value, value_pad_mask, U,
-                           row_video, offsets, off_stride, off_col0, off_add, ref, rd1_rows, lv, S, num_heads, att_h,
-                           ld_att_h, alpha_w, alpha_b, samples, save_loc, att, probs, res);
-    else
-        hipLaunchKernelGGL(cap_softattn_fwd_kernel<2>, dim3((unsigned)nwg), dim3(kCSA), 0, s, value, value_pad_mask, U,
-                           row_video, offsets, off_stride, off_col0, off_add, ref, rd1_rows, lv, S, num_heads, att_h,
-                           ld_att_h, alpha_w, alpha_b, samples, save_loc, att, probs, res);
+    static const int ch = [] {  // PDVC_CAP_FWD_CH=4: the 4-sample chunks (same-box A/B)
+        const char* e = getenv("PDVC_CAP_FWD_CH");
+        return e && e[0] == '4' ? 4 : 1;
+    }();
+    auto kern = ref_dim == 1 ? (ch == 4 ? cap_softattn_fwd_kernel<1, 4> : cap_softattn_fwd_kernel<1, 1>)
+                             : (ch == 4 ? cap_softattn_fwd_kernel<2, 4> : cap_softattn_fwd_kernel<2, 1>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kCSA), 0, s, value, value_pad_mask, U, row_video, offsets,
+                       off_stride, off_col0, off_add, ref, rd1_rows, lv, S, num_heads, att_h, ld_att_h, alpha_w,
+                       alpha_b, samples, save_loc, att, probs, res);
     PDVC_CHECK_LAUNCH("cap_softattn_fwd_kernel");
     return PDVC_OK;
 }
@@ -1028,16 +1031,16 @@ extern "C" int pdvc_cap_softattn_backward_f32(const float* value, const uint8_t*
     if (nwg == 0) return PDVC_OK;
     PDVC_CHECK_ARG(nwg < (1L << 31), "too many rows");
     hipStream_t s = (hipStream_t)stream;
-    if (ref_dim == 1)
-        hipLaunchKernelGGL(cap_softattn_bwd_kernel<1>, dim3((unsigned)nwg), dim3(kCSA), 0, s, value, value_pad_mask, U,
-                           row_video, offsets, off_stride, off_col0, off_add, ref, rd1_rows, lv, S, num_heads,
-                           save_loc, probs, grad_res, att_h, ld_att_h, alpha_w, grad_att, grad_att_h, ld_grad_att_h,
-                           grad_samples, grad_alpha_w_part, grad_alpha_b_part, grad_offsets, grad_ref);
-    else
-        hipLaunchKernelGGL(cap_softattn_bwd_kernel<2>, dim3((unsigned)nwg), dim3(kCSA), 0, s, value, value_pad_mask, U,
-                           row_video, offsets, off_stride, off_col0, off_add, ref, rd1_rows, lv, S, num_heads,
-                           save_loc, probs, grad_res, att_h, ld_att_h, alpha_w, grad_att, grad_att_h, ld_grad_att_h,
-                           grad_samples, grad_alpha_w_part, grad_alpha_b_part, grad_offsets, grad_ref);
+    static const int ch = [] {  // PDVC_CAP_BWD_CH=4: the 4-sample chunks (same-box A/B)
+        const char* e = getenv("PDVC_CAP_BWD_CH");
+        return e && e[0] == '4' ? 4 : 1;
+    }();
+    auto kern = ref_dim == 1 ? (ch == 4 ? cap_softattn_bwd_kernel<1, 4> : cap_softattn_bwd_kernel<1, 1>)
+                             : (ch == 4 ? cap_softattn_bwd_kernel<2, 4> : cap_softattn_bwd_kernel<2, 1>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kCSA), 0, s, value, value_pad_mask, U, row_video, offsets,
+                       off_stride, off_col0, off_add, ref, rd1_rows, lv, S, num_heads, save_loc, probs, grad_res, att_h,
+                       ld_att_h, alpha_w, grad_att, grad_att_h, ld_grad_att_h, grad_samples, grad_alpha_w_part,
+                       grad_alpha_b_part, grad_offsets, grad_ref);
     PDVC_CHECK_LAUNCH("cap_softattn_bwd_kernel");
     return PDVC_OK;
 }
