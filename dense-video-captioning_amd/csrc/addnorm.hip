@@ -37,7 +37,19 @@ __device__ __forceinline__ float an_wave_sum(float v) {
 
 // lane's columns: c = lane*4 + 256*k + {0..3}  (float4 chunks, k < kAPL/4)
 // s == NULL: no second input (z = x); r != NULL: y = LN(z) * gamma + beta + r
-template <int CH>  // float4 chunks per lane
+// Row loads of a wave: CH float4 chunks per lane, at clamped (always valid) addresses so that they are unconditional;
+// the values of columns >= d and rows >= rows are never used.
+template <int CH>
+__device__ __forceinline__ void an_load(float4 (&v)[CH], const float* __restrict__ t, int row, int rows, int d,
+                                        int lane) {
+    const size_t rw = (size_t)min(row, rows - 1);
+#pragma unroll
+    for (int k = 0; k < CH; ++k) v[k] = *reinterpret_cast<const float4*>(t + rw * d + min(lane * 4 + 256 * k, d - 4));
+}
+
+// PF: double-buffered rows -- the next row's loads are issued before this row's reductions, into the other register
+// set (two row bodies per loop trip, so that no register copy waits for the loads); gamma and beta held across rows
+template <int CH, bool PF>  // float4 chunks per lane
 __global__ __launch_bounds__(kANW * 64) void addnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ s,
                                                                 const float* __restrict__ gamma,
                                                                 const float* __restrict__ beta, int rows, int d,
@@ -51,16 +63,18 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_fwd_kernel(const float* __r
     const uint64_t seed = seed_dev ? *seed_dev : seed0;
     const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
     const float inv_d = 1.f / (float)d;
-    for (int row = blockIdx.x * kANW + (threadIdx.x >> 6); row < rows; row += gridDim.x * kANW) {
+    float4 gk[CH], bk[CH];
+    an_load<CH>(gk, gamma, 0, 1, d, lane);
+    an_load<CH>(bk, beta, 0, 1, d, lane);
+    auto body = [&](int row, const float4 (&xv4)[CH], const float4 (&sv4)[CH]) {
         float z[CH][4];
         float sum = 0.f;
 #pragma unroll
         for (int k = 0; k < CH; ++k) {
             const int c = lane * 4 + 256 * k;
             if (c < d) {
-                const float4 xv = *reinterpret_cast<const float4*>(x + (size_t)row * d + c);
-                const float4 sv = s ? *reinterpret_cast<const float4*>(s + (size_t)row * d + c)
-                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 xv = xv4[k];
+                const float4 sv = s ? sv4[k] : make_float4(0.f, 0.f, 0.f, 0.f);
                 const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, ss[4] = {sv.x, sv.y, sv.z, sv.w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -92,8 +106,7 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_fwd_kernel(const float* __r
         for (int k = 0; k < CH; ++k) {
             const int c = lane * 4 + 256 * k;
             if (c < d) {
-                const float4 g = *reinterpret_cast<const float4*>(gamma + c);
-                const float4 b = *reinterpret_cast<const float4*>(beta + c);
+                const float4 g = gk[k], b = bk[k];
                 float4 o;
                 o.x = (z[k][0] - mean) * rstd * g.x + b.x;
                 o.y = (z[k][1] - mean) * rstd * g.y + b.y;
@@ -114,10 +127,34 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_fwd_kernel(const float* __r
             mean_out[row] = mean;
             rstd_out[row] = rstd;
         }
+    };
+    const int stride = gridDim.x * kANW;
+    const float* sp = s ? s : x;  // s == NULL: the loads read x again (unused), the branch stays uniform
+    int row = blockIdx.x * kANW + (threadIdx.x >> 6);
+    if constexpr (!PF) {
+        for (; row < rows; row += stride) {
+            float4 xa[CH], sa[CH];
+            an_load<CH>(xa, x, row, rows, d, lane);
+            if (s) an_load<CH>(sa, sp, row, rows, d, lane);
+            body(row, xa, sa);
+        }
+    } else {
+        float4 xa[CH], sa[CH], xb[CH], sb[CH];
+        an_load<CH>(xa, x, row, rows, d, lane);
+        if (s) an_load<CH>(sa, sp, row, rows, d, lane);
+        for (; row < rows; row += 2 * stride) {
+            an_load<CH>(xb, x, row + stride, rows, d, lane);
+            if (s) an_load<CH>(sb, sp, row + stride, rows, d, lane);
+            body(row, xa, sa);
+            if (row + stride >= rows) break;
+            an_load<CH>(xa, x, row + 2 * stride, rows, d, lane);
+            if (s) an_load<CH>(sa, sp, row + 2 * stride, rows, d, lane);
+            body(row + stride, xb, sb);
+        }
     }
 }
 
-template <int CH>
+template <int CH, bool PF>
 __global__ __launch_bounds__(kANW * 64) void addnorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ s,
                                                                 const float* __restrict__ gamma,
                                                                 const float* __restrict__ mean_in,
@@ -140,8 +177,10 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_bwd_kernel(const float* __r
     for (int k = 0; k < CH; ++k)
 #pragma unroll
         for (int e = 0; e < 4; ++e) pg[k][e] = pb[k][e] = pd[k][e] = 0.f;
-    for (int row = blockIdx.x * kANW + wid; row < rows; row += gridDim.x * kANW) {
-        const float mean = mean_in[row], rstd = rstd_in[row];
+    float4 gk[CH];
+    an_load<CH>(gk, gamma, 0, 1, d, lane);
+    auto body = [&](int row, const float4 (&xv4)[CH], const float4 (&sv4)[CH], const float4 (&dv4)[CH], float mean,
+                    float rstd) {
         float xh[CH][4], gg[CH][4];
         unsigned keep_bits[CH];
         float s1 = 0.f, s2 = 0.f;
@@ -150,11 +189,10 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_bwd_kernel(const float* __r
             const int c = lane * 4 + 256 * k;
             keep_bits[k] = 0xF;
             if (c < d) {
-                const float4 xv = *reinterpret_cast<const float4*>(x + (size_t)row * d + c);
-                const float4 sv = s ? *reinterpret_cast<const float4*>(s + (size_t)row * d + c)
-                                    : make_float4(0.f, 0.f, 0.f, 0.f);
-                const float4 dv = *reinterpret_cast<const float4*>(dy + (size_t)row * d + c);
-                const float4 gv = *reinterpret_cast<const float4*>(gamma + c);
+                const float4 xv = xv4[k];
+                const float4 sv = s ? sv4[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 dv = dv4[k];
+                const float4 gv = gk[k];
                 const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, ss[4] = {sv.x, sv.y, sv.z, sv.w};
                 const float dd[4] = {dv.x, dv.y, dv.z, dv.w}, gm[4] = {gv.x, gv.y, gv.z, gv.w};
 #pragma unroll
@@ -193,6 +231,45 @@ __global__ __launch_bounds__(kANW * 64) void addnorm_bwd_kernel(const float* __r
                 if (ds) *reinterpret_cast<float4*>(ds + (size_t)row * d + c) = make_float4(q[0], q[1], q[2], q[3]);
                 if (ds16) store_bf16x4(ds16 + (size_t)row * d + c, q[0], q[1], q[2], q[3]);
             }
+        }
+    };
+    const int stride = gridDim.x * kANW;
+    const float* sp = s ? s : x;
+    int row = blockIdx.x * kANW + wid;
+    auto stats = [&](int rw, float& m, float& rs) {
+        const int rc = min(rw, rows - 1);
+        m = mean_in[rc];
+        rs = rstd_in[rc];
+    };
+    if constexpr (!PF) {
+        for (; row < rows; row += stride) {
+            float4 xa[CH], sa[CH], da[CH];
+            float ma, ra;
+            stats(row, ma, ra);
+            an_load<CH>(xa, x, row, rows, d, lane);
+            if (s) an_load<CH>(sa, sp, row, rows, d, lane);
+            an_load<CH>(da, dy, row, rows, d, lane);
+            body(row, xa, sa, da, ma, ra);
+        }
+    } else {
+        float4 xa[CH], sa[CH], da[CH], xb[CH], sb[CH], db[CH];
+        float ma, ra, mb, rb;
+        stats(row, ma, ra);
+        an_load<CH>(xa, x, row, rows, d, lane);
+        if (s) an_load<CH>(sa, sp, row, rows, d, lane);
+        an_load<CH>(da, dy, row, rows, d, lane);
+        for (; row < rows; row += 2 * stride) {
+            stats(row + stride, mb, rb);
+            an_load<CH>(xb, x, row + stride, rows, d, lane);
+            if (s) an_load<CH>(sb, sp, row + stride, rows, d, lane);
+            an_load<CH>(db, dy, row + stride, rows, d, lane);
+            body(row, xa, sa, da, ma, ra);
+            if (row + stride >= rows) break;
+            stats(row + 2 * stride, ma, ra);
+            an_load<CH>(xa, x, row + 2 * stride, rows, d, lane);
+            if (s) an_load<CH>(sa, sp, row + 2 * stride, rows, d, lane);
+            an_load<CH>(da, dy, row + 2 * stride, rows, d, lane);
+            body(row + stride, xb, sb, db, mb, rb);
         }
     }
     // workgroup sum of the column partials, one row of partials per workgroup
@@ -284,15 +361,26 @@ static int an_grid(int rows, int cap) {
 constexpr int kAnFwdBlocks = 1024;  // 4 per CU
 constexpr int kAnBwdBlocks = 1024;  // 4 per CU (16 waves): enough loads in flight to stream at HBM rate
 
+static bool an_pf() {  // PDVC_AN_PF=0: the kernels without the next-row prefetch (same-box A/B)
+    static const bool on = [] {
+        const char* e = getenv("PDVC_AN_PF");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 static int an_forward(const float* x, const float* s, const float* r, const float* gamma, const float* beta, int rows,
                       int d, float p, uint64_t seed, const uint64_t* seed_dev, float eps, float* y, float* mean,
                       float* rstd, void* stream, uint16_t* y16 = nullptr) {
     const dim3 grid((unsigned)an_grid(rows, kAnFwdBlocks)), block(kANW * 64);
     hipStream_t st = (hipStream_t)stream;
     const uint32_t th = an_threshold(p);
-#define AN_FWD(CH) \
-    hipLaunchKernelGGL(addnorm_fwd_kernel<CH>, grid, block, 0, st, x, s, gamma, beta, rows, d, p, th, seed, seed_dev, \
-                       eps, r, y, mean, rstd, y16)
+#define AN_FWD(CH)                                                                                                  \
+    do {                                                                                                            \
+        auto kern = an_pf() ? addnorm_fwd_kernel<CH, true> : addnorm_fwd_kernel<CH, false>;                         \
+        hipLaunchKernelGGL(kern, grid, block, 0, st, x, s, gamma, beta, rows, d, p, th, seed, seed_dev, eps, r, y,  \
+                           mean, rstd, y16);                                                                        \
+    } while (0)
     if (d <= 256) AN_FWD(1);
     else if (d <= 512) AN_FWD(2);
     else AN_FWD(3);
@@ -311,9 +399,12 @@ static int an_backward(const float* x, const float* s, const float* gamma, const
     float* spart = ds_colsum ? workspace + 2 * (size_t)parts * d : nullptr;
     const dim3 grid((unsigned)parts), block(kANW * 64);
     const uint32_t th = an_threshold(p);
-#define AN_BWD(CH) \
-    hipLaunchKernelGGL(addnorm_bwd_kernel<CH>, grid, block, 0, st, x, s, gamma, mean, rstd, dy, rows, d, p, th, seed, \
-                       seed_dev, dx, ds, gpart, bpart, spart, ds16)
+#define AN_BWD(CH)                                                                                                  \
+    do {                                                                                                            \
+        auto kern = an_pf() ? addnorm_bwd_kernel<CH, true> : addnorm_bwd_kernel<CH, false>;                         \
+        hipLaunchKernelGGL(kern, grid, block, 0, st, x, s, gamma, mean, rstd, dy, rows, d, p, th, seed, seed_dev,   \
+                           dx, ds, gpart, bpart, spart, ds16);                                                      \
+    } while (0)
     if (d <= 256) AN_BWD(1);
     else if (d <= 512) AN_BWD(2);
     else AN_BWD(3);
