@@ -24,9 +24,6 @@ __device__ __forceinline__ bool ffn_keep(uint64_t seed, uint32_t row, uint32_t c
     return (h >> 8) >= thresh;
 }
 
-// U float4s per thread per loop trip, all loaded before any is stored (U = 1: one load in flight per thread, and the
-// next trip's load waits for this trip's store -- the vmcnt store coupling); loads at clamped indices, unconditional
-template <int U>
 __global__ __launch_bounds__(256) void relu_dropout_fwd_kernel(float* __restrict__ h, long rows, int cols, float p,
                                                                uint32_t thresh, float scale, uint64_t seed0,
                                                                const uint64_t* __restrict__ seed_dev,
@@ -34,32 +31,23 @@ __global__ __launch_bounds__(256) void relu_dropout_fwd_kernel(float* __restrict
     const uint64_t seed = seed_dev ? *seed_dev : seed0;
     const int c4 = cols / 4;
     const long n4 = rows * c4;
-    const long G = (long)gridDim.x * 256;
     float4* h4 = reinterpret_cast<float4*>(h);
-    for (long i0 = (long)blockIdx.x * 256 + threadIdx.x; i0 < n4; i0 += U * G) {
-        float4 v[U];
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+        const uint32_t row = (uint32_t)(i / c4), col = (uint32_t)(i - (long)row * c4) * 4;
+        float4 v = h4[i];
+        float e[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = h4[min(i0 + u * G, n4 - 1)];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const long i = i0 + u * G;
-            if (i >= n4) break;
-            const uint32_t row = (uint32_t)(i / c4), col = (uint32_t)(i - (long)row * c4) * 4;
-            float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                float x = fmaxf(e[k], 0.f);
-                if (p > 0.f) x = ffn_keep(seed, row, col + k, thresh) ? x * scale : 0.f;
-                e[k] = x;
-            }
-            h4[i] = make_float4(e[0], e[1], e[2], e[3]);
-            if (h16) store_bf16x4(h16 + (size_t)i * 4, e[0], e[1], e[2], e[3]);
+        for (int k = 0; k < 4; ++k) {
+            float x = fmaxf(e[k], 0.f);
+            if (p > 0.f) x = ffn_keep(seed, row, col + k, thresh) ? x * scale : 0.f;
+            e[k] = x;
         }
+        h4[i] = make_float4(e[0], e[1], e[2], e[3]);
+        if (h16) store_bf16x4(h16 + (size_t)i * 4, e[0], e[1], e[2], e[3]);
     }
 }
 
 // grid (ceil(cols/64), parts): 16 float4 column groups x 16 row lanes over one row slab
-template <int U>  // U rows per lane per loop trip, loaded before any is stored
 __global__ __launch_bounds__(256) void relu_dropout_bwd_kernel(const float* __restrict__ hd, float* __restrict__ g,
                                                                int rows, int cols, int parts, float scale,
                                                                float* __restrict__ part,
@@ -74,32 +62,21 @@ __global__ __launch_bounds__(256) void relu_dropout_bwd_kernel(const float* __re
     if (c4 < cs) {
         const float4* h4 = reinterpret_cast<const float4*>(hd) + c4;
         float4* g4 = reinterpret_cast<float4*>(g) + c4;
-        for (int rb = r0 + rl; rb < r1; rb += 16 * U) {
-            float4 xs[U], ds[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const size_t o = (size_t)min(rb + 16 * u, r1 - 1) * cs;
-                xs[u] = h4[o];
-                ds[u] = g4[o];
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int r = rb + 16 * u;
-                if (r >= r1) break;
-                const size_t o = (size_t)r * cs;
-                const float4 x = xs[u];
-                float4 d = ds[u];
-                d.x = x.x > 0.f ? d.x * scale : 0.f;
-                d.y = x.y > 0.f ? d.y * scale : 0.f;
-                d.z = x.z > 0.f ? d.z * scale : 0.f;
-                d.w = x.w > 0.f ? d.w * scale : 0.f;
-                g4[o] = d;
-                if (g16) store_bf16x4(g16 + ((size_t)r * cs + c4) * 4, d.x, d.y, d.z, d.w);
-                a.x += d.x;
-                a.y += d.y;
-                a.z += d.z;
-                a.w += d.w;
-            }
+#pragma unroll 4
+        for (int r = r0 + rl; r < r1; r += 16) {
+            const size_t o = (size_t)r * cs;
+            const float4 x = h4[o];
+            float4 d = g4[o];
+            d.x = x.x > 0.f ? d.x * scale : 0.f;
+            d.y = x.y > 0.f ? d.y * scale : 0.f;
+            d.z = x.z > 0.f ? d.z * scale : 0.f;
+            d.w = x.w > 0.f ? d.w * scale : 0.f;
+            g4[o] = d;
+            if (g16) store_bf16x4(g16 + ((size_t)r * cs + c4) * 4, d.x, d.y, d.z, d.w);
+            a.x += d.x;
+            a.y += d.y;
+            a.z += d.z;
+            a.w += d.w;
         }
     }
     if (part == nullptr) return;  // block-uniform
@@ -161,14 +138,6 @@ static uint32_t ffn_threshold(float p) {
 
 using namespace pdvc;
 
-static bool ffn_unroll() {  // PDVC_FFN_U=1: one element group in flight per lane (same-box A/B)
-    static const bool on = [] {
-        const char* e = getenv("PDVC_FFN_U");
-        return !(e && e[0] == '1');
-    }();
-    return on;
-}
-
 static int relu_dropout_forward(float* h, long rows, int cols, float p, uint64_t seed, const uint64_t* seed_dev,
                                 uint16_t* h16, void* stream) {
     PDVC_CHECK_ARG(rows >= 0 && cols > 0 && cols % 4 == 0 && ((uintptr_t)h % 16) == 0,
@@ -180,8 +149,8 @@ static int relu_dropout_forward(float* h, long rows, int cols, float p, uint64_t
     const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
     const long want = (n4 + 255) / 256;
     const unsigned blocks = (unsigned)(want < 8192 ? want : 8192);
-    hipLaunchKernelGGL(ffn_unroll() ? relu_dropout_fwd_kernel<4> : relu_dropout_fwd_kernel<1>, dim3(blocks), dim3(256),
-                       0, (hipStream_t)stream, h, rows, cols, p, ffn_threshold(p), scale, seed, seed_dev, h16);
+    hipLaunchKernelGGL(relu_dropout_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, h, rows, cols, p,
+                       ffn_threshold(p), scale, seed, seed_dev, h16);
     PDVC_CHECK_LAUNCH("relu_dropout_fwd_kernel");
     return PDVC_OK;
 }
@@ -197,8 +166,8 @@ static int relu_dropout_backward(const float* hd, float* grad, int rows, int col
     hipStream_t s = (hipStream_t)stream;
     const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
     const unsigned cb = (unsigned)((cols / 4 + 15) / 16);
-    hipLaunchKernelGGL(ffn_unroll() ? relu_dropout_bwd_kernel<4> : relu_dropout_bwd_kernel<1>, dim3(cb, (unsigned)parts),
-                       dim3(256), 0, s, hd, grad, rows, cols, parts, scale, workspace, g16);
+    hipLaunchKernelGGL(relu_dropout_bwd_kernel, dim3(cb, (unsigned)parts), dim3(256), 0, s, hd, grad, rows, cols,
+                       parts, scale, workspace, g16);
     PDVC_CHECK_LAUNCH("relu_dropout_bwd_kernel");
     if (dbias) {
         hipLaunchKernelGGL(ffn_colsum_final_kernel, dim3((unsigned)((cols / 4 + 15) / 16)), dim3(256), 0, s, workspace,
