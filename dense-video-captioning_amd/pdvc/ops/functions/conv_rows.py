@@ -7,8 +7,6 @@
     the W0 tap of the previous odd row, added shifted by one output row (zero at t = 0: the padding);
   * GroupNorm(G, C) on rows: pdvc_groupnorm_rows_* (csrc/groupnorm.hip).
 Same parameters (nn.Conv1d / nn.GroupNorm), same math."""
-import os
-
 import torch
 import torch.nn.functional as F
 from torch.autograd import Function
@@ -18,10 +16,6 @@ from pdvc import _native as _n
 from .linear import colsum, dense, wgrad_mm
 
 GN_ROWS = 64  # rows per stats chunk (csrc/groupnorm.hip kGnRows)
-# the W0 tap accumulated in place by a strided batched GEMM (one batch per video, the output rows shifted by one),
-# and its weight gradient as one GEMM over the flat rows shifted by one minus the N - 1 pairs that cross a video
-# boundary; PDVC_CONV_BMM=0: the separate product, its shifted add and the zero-padded shifted gradient copy
-CONV_BMM = os.environ.get("PDVC_CONV_BMM", "1") != "0"
 
 
 class ConvS2RowsFunction(Function):
@@ -41,13 +35,9 @@ class ConvS2RowsFunction(Function):
         w12 = torch.cat([weight[:, :, 1], weight[:, :, 2]], 1)  # (O, 2C): taps on x[2t], x[2t+1]
         w0 = weight[:, :, 0].contiguous()                       # (O, C): tap on x[2t-1]
         y = torch.addmm(bias, X2, w12.t())
+        z = torch.mm(X2[:, C:], w0.t())                         # x[2t+1] W0^T feeds output row t+1
         yv = y.view(N, L, O)
-        if CONV_BMM:  # x[2t+1] W0^T accumulated straight into output row t+1 of the same video
-            if L > 1:
-                yv[:, 1:].baddbmm_(X2.view(N, L, 2 * C)[:, :-1, C:], w0.t().expand(N, C, O))
-        else:
-            z = torch.mm(X2[:, C:], w0.t())                     # x[2t+1] W0^T feeds output row t+1
-            yv[:, 1:] += z.view(N, L, O)[:, :-1]
+        yv[:, 1:] += z.view(N, L, O)[:, :-1]
         ctx.save_for_backward(X2, w12, w0)
         ctx.shape = (N, T, C, L, O, Tin)
         return yv
@@ -58,40 +48,18 @@ class ConvS2RowsFunction(Function):
         X2, w12, w0 = ctx.saved_tensors
         N, T, C, L, O, Tin = ctx.shape
         dy2 = dy.reshape(N * L, O).contiguous()
+        dz = torch.zeros_like(dy2).view(N, L, O)
+        dz[:, :-1] = dy2.view(N, L, O)[:, 1:]
+        dz2 = dz.view(N * L, O)
         gx = gw = gb = None
-        if CONV_BMM:
-            dyv = dy2.view(N, L, O)
-            if ctx.needs_input_grad[0]:
-                dX2 = torch.mm(dy2, w12)
-                if L > 1:  # dy[t+1] W0 accumulated straight into the odd half of input pair t
-                    dX2.view(N, L, 2 * C)[:, :-1, C:].baddbmm_(dyv[:, 1:], w0.expand(N, O, C))
-                gx = dX2.view(N, T, C)[:, :Tin]
-            if ctx.needs_input_grad[1]:
-                g12 = wgrad_mm(dy2, X2)
-                # sum over (video, t < L-1) of dy[t+1]^T x[2t+1]: the flat rows shifted by one, less the pairs
-                # (first row of video n+1, last odd row of video n) the shift adds across video boundaries
-                # (the shifted product over a multiple of 64 rows keeps wgrad_mm's split-K; the few rows left over
-                # are one small product)
-                R = N * L
-                R0 = (R - 1) // 64 * 64
-                g0 = wgrad_mm(dy2[1:R0 + 1], X2[:R0, C:]) if R0 > 0 else torch.zeros_like(w0)
-                if R0 < R - 1:
-                    g0 += torch.mm(dy2[R0 + 1:].t(), X2[R0:R - 1, C:])
-                if N > 1:
-                    g0 -= torch.mm(dyv[1:, 0].t(), X2.view(N, L, 2 * C)[:-1, L - 1, C:])
-                gw = torch.stack([g0, g12[:, :C], g12[:, C:]], 2)
-        else:
-            dz = torch.zeros_like(dy2).view(N, L, O)
-            dz[:, :-1] = dy2.view(N, L, O)[:, 1:]
-            dz2 = dz.view(N * L, O)
-            if ctx.needs_input_grad[0]:
-                dX2 = torch.mm(dy2, w12)
-                dX2[:, C:] += torch.mm(dz2, w0)
-                gx = dX2.view(N, T, C)[:, :Tin]
-            if ctx.needs_input_grad[1]:
-                g12 = wgrad_mm(dy2, X2)
-                g0 = wgrad_mm(dz2, X2[:, C:])
-                gw = torch.stack([g0, g12[:, :C], g12[:, C:]], 2)
+        if ctx.needs_input_grad[0]:
+            dX2 = torch.mm(dy2, w12)
+            dX2[:, C:] += torch.mm(dz2, w0)
+            gx = dX2.view(N, T, C)[:, :Tin]
+        if ctx.needs_input_grad[1]:
+            g12 = wgrad_mm(dy2, X2)
+            g0 = wgrad_mm(dz2, X2[:, C:])
+            gw = torch.stack([g0, g12[:, :C], g12[:, C:]], 2)
         if ctx.needs_input_grad[2]:
             gb = colsum(dy2)
         return gx, gw, gb
