@@ -618,9 +618,8 @@ __global__ __launch_bounds__(kCSA) void cap_softattn_fwd_kernel(
 // and only the 16 tanh rows stay in registers for the att gradients.  One 128-thread workgroup per (row, head).
 constexpr int cRED = 3 * cNS;  // dots, value-difference sums, U-difference sums
 
-// KEEP = false: 168 registers (three waves per SIMD) at the price of ~13 spilled values and the U corners read twice
-template <int RD, int CH, bool KEEP>
-__global__ __launch_bounds__(kCSA) __attribute__((amdgpu_waves_per_eu(KEEP ? 1 : 3))) void cap_softattn_bwd_kernel(
+template <int RD, int CH>
+__global__ __launch_bounds__(kCSA) void cap_softattn_bwd_kernel(
     const float* __restrict__ value, const uint8_t* __restrict__ vmask, const float* __restrict__ U,
     const int32_t* __restrict__ row_video, const float* __restrict__ offsets, int off_stride, int off_col0,
     const float* __restrict__ off_add, const float* __restrict__ ref, int rd1_rows, CapLevels lv, int S, int M,
@@ -666,7 +665,7 @@ __global__ __launch_bounds__(kCSA) __attribute__((amdgpu_waves_per_eu(KEEP ? 1 :
 #pragma unroll
     for (int k = 0; k < cNS; ++k) p[k] = probs[so + k];
     float4* gc4 = reinterpret_cast<float4*>(gclip + so * D) + tid;
-    float4 th[KEEP ? cNS : 1];  // tanh(att_k + att_h) (KEEP: held for the second pass, else re-formed there)
+    float4 th[cNS];    // tanh(att_k + att_h)
     float part[cRED];  // [0,16): dres . sample_k   [16,32): dres . (v1 - v0)_k   [32,48): (w (1 - t^2)) . (u1 - u0)_k
 #pragma unroll
     for (int k0 = 0; k0 < cNS; k0 += CH) {  // CH samples' corner rows per chunk
@@ -694,15 +693,13 @@ __global__ __launch_bounds__(kCSA) __attribute__((amdgpu_waves_per_eu(KEEP ? 1 :
                                           hi ? u1[q].w : 0.f);
             const float4 at = make_float4(u0[q].x * nw + h1.x * ne, u0[q].y * nw + h1.y * ne,
                                           u0[q].z * nw + h1.z * ne, u0[q].w * nw + h1.w * ne);
-            const float4 tk = make_float4(tanhf(at.x + hv.x), tanhf(at.y + hv.y), tanhf(at.z + hv.z),
-                                          tanhf(at.w + hv.w));
-            if constexpr (KEEP) th[k] = tk;
+            th[k] = make_float4(tanhf(at.x + hv.x), tanhf(at.y + hv.y), tanhf(at.z + hv.z), tanhf(at.w + hv.w));
             part[k] = 0.f + (g.x * cl.x + g.y * cl.y + g.z * cl.z + g.w * cl.w);
             part[cNS + k] = g.x * (a1.x - a0.x) + g.y * (a1.y - a0.y) + g.z * (a1.z - a0.z) + g.w * (a1.w - a0.w);
-            part[2 * cNS + k] = wv.x * (1.f - tk.x * tk.x) * (h1.x - u0[q].x) +
-                                wv.y * (1.f - tk.y * tk.y) * (h1.y - u0[q].y) +
-                                wv.z * (1.f - tk.z * tk.z) * (h1.z - u0[q].z) +
-                                wv.w * (1.f - tk.w * tk.w) * (h1.w - u0[q].w);
+            part[2 * cNS + k] = wv.x * (1.f - th[k].x * th[k].x) * (h1.x - u0[q].x) +
+                                wv.y * (1.f - th[k].y * th[k].y) * (h1.y - u0[q].y) +
+                                wv.z * (1.f - th[k].z * th[k].z) * (h1.z - u0[q].z) +
+                                wv.w * (1.f - th[k].w * th[k].w) * (h1.w - u0[q].w);
             gc4[(size_t)k * D4] = make_float4(p[k] * g.x, p[k] * g.y, p[k] * g.z, p[k] * g.w);
         }
         // CH = 4: one chunk's 16 rows in flight at a time (454 registers without the barrier, 449 with: one wave per
@@ -741,19 +738,7 @@ __global__ __launch_bounds__(kCSA) __attribute__((amdgpu_waves_per_eu(KEEP ? 1 :
     float4 gh = make_float4(0.f, 0.f, 0.f, 0.f), gw = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int k = 0; k < cNS; ++k) {
-        float4 tk;
-        if constexpr (KEEP) {
-            tk = th[k];
-        } else {  // re-formed from the U corners (L2-resident: this workgroup read them in the first pass)
-            const size_t o0 = (size_t)srow0[k] * MD4, o1 = (size_t)srow1[k] * MD4;
-            const float4 u0 = ub[o0], u1 = ub[o1];
-            const float nw = snw[k], ne = sne[k];
-            const bool hi = sfl[k] & 4;
-            const float4 at = make_float4(u0.x * nw + (hi ? u1.x : 0.f) * ne, u0.y * nw + (hi ? u1.y : 0.f) * ne,
-                                          u0.z * nw + (hi ? u1.z : 0.f) * ne, u0.w * nw + (hi ? u1.w : 0.f) * ne);
-            tk = make_float4(tanhf(at.x + hv.x), tanhf(at.y + hv.y), tanhf(at.z + hv.z), tanhf(at.w + hv.w));
-        }
-        const float tx = tk.x, ty = tk.y, tz = tk.z, tw = tk.w;
+        const float tx = th[k].x, ty = th[k].y, tz = th[k].z, tw = th[k].w;
         const float4 dpre = make_float4(dd[k] * wv.x * (1.f - tx * tx), dd[k] * wv.y * (1.f - ty * ty),
                                         dd[k] * wv.z * (1.f - tz * tz), dd[k] * wv.w * (1.f - tw * tw));
         ga4[(size_t)k * D4] = dpre;
@@ -1050,15 +1035,8 @@ extern "C" int pdvc_cap_softattn_backward_f32(const float* value, const uint8_t*
         const char* e = getenv("PDVC_CAP_BWD_CH");
         return e && e[0] == '4' ? 4 : 1;
     }();
-    static const bool keep = [] {  // PDVC_CAP_BWD_KEEP=0: the tanh rows re-formed from the U corners (same-box A/B)
-        const char* e = getenv("PDVC_CAP_BWD_KEEP");
-        return !(e && e[0] == '0');
-    }();
-    auto kern = ref_dim == 1
-                    ? (ch == 4 ? cap_softattn_bwd_kernel<1, 4, true>
-                               : (keep ? cap_softattn_bwd_kernel<1, 1, true> : cap_softattn_bwd_kernel<1, 1, false>))
-                    : (ch == 4 ? cap_softattn_bwd_kernel<2, 4, true>
-                               : (keep ? cap_softattn_bwd_kernel<2, 1, true> : cap_softattn_bwd_kernel<2, 1, false>));
+    auto kern = ref_dim == 1 ? (ch == 4 ? cap_softattn_bwd_kernel<1, 4> : cap_softattn_bwd_kernel<1, 1>)
+                             : (ch == 4 ? cap_softattn_bwd_kernel<2, 4> : cap_softattn_bwd_kernel<2, 1>);
     hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kCSA), 0, s, value, value_pad_mask, U, row_video, offsets,
                        off_stride, off_col0, off_add, ref, rd1_rows, lv, S, num_heads, save_loc, probs, grad_res, att_h,
                        ld_att_h, alpha_w, grad_att, grad_att_h, ld_grad_att_h, grad_samples, grad_alpha_w_part,
