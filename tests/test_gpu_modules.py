@@ -345,7 +345,7 @@ def test_captioner_multinomial_sampling(temperature):
 
 
 @pytest.mark.parametrize("heads,rd1,deferred", [(1, 3, False), (2, 0, False), (1, 3, True), (2, 0, True)])
-def test_caption_decode_function_matches_step_loop(heads, rd1, deferred):
+def test_caption_decode_function_matches_step_loop(heads, rd1, deferred, monkeypatch):
     """The fused teacher-forced recurrence (ops/functions/caption_decode.py) against the per-step autograd
     loop of the same math (LSTMDSACaptioner._step: cap-gather kernel + torch ops), at the PDVC caption shape
     (d=512, A=512, H=512, 16 samples) with a mix of 1-d and (c, len) reference rows. deferred: the value
@@ -407,7 +407,22 @@ def test_caption_decode_function_matches_step_loop(heads, rd1, deferred):
         grads = {k: p.grad.clone() for k, p in cap.named_parameters() if p.grad is not None}
         return out.detach(), [t.grad.clone() for t in ins], grads
 
+    from pdvc import _native as _nm
+    from pdvc.ops.functions import caption_decode as cd
+    called, real_call = set(), _nm.call
+
+    def spy(name, *a, **k):
+        called.add(name)
+        return real_call(name, *a, **k)
+
+    monkeypatch.setattr(_nm, "call", spy)
     o1, gi1, gp1 = run(True)
+    monkeypatch.setattr(_nm, "call", real_call)
+    # the one-launch caption step is the path taken at the 512-wide head (heads = 1: D = A = 512), its backward
+    # with the per-video row CSR (the U-gradient form); the 256-wide heads take the separate launches
+    assert ("pdvc_cap_softattn_forward_f32" in called) == (heads == 1 and cd.CAP_FUSED)
+    assert ("pdvc_cap_softattn_backward_f32" in called) == (heads == 1 and deferred and cd.CAP_FUSED
+                                                            and cd.CAP_FUSED_BWD)
     o0, gi0, gp0 = run(False)
     close(o1, o0, 1e-5, "logprobs")
     for name, a, b in zip(("hs", "ref", "memory"), gi1, gi0):
