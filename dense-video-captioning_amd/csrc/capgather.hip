@@ -267,7 +267,7 @@ __global__ __launch_bounds__(kCVW * 64) void cap_value_grad_kernel(
     const uint8_t* __restrict__ vmask, CapLevels lv, int S, int M, int D, int R, int s0, int ns, int accumulate,
     const int32_t* __restrict__ vr_start, const int32_t* __restrict__ vr_rows, const float* __restrict__ save_loc,
     const float* __restrict__ gsamp, float* __restrict__ grad_value, float* __restrict__ level_sums,
-    const int32_t* __restrict__ step_rows) {
+    const int32_t* __restrict__ step_rows, const float* __restrict__ grow, const float* __restrict__ gscale) {
     extern __shared__ __attribute__((aligned(16))) int lds_c[];
     __shared__ int wsum[kCVW];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -397,11 +397,23 @@ __global__ __launch_bounds__(kCVW * 64) void cap_value_grad_kernel(
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int j = (j0 + u < je) ? j0 + u : je - 1;
-            const float* gp = gsamp + (size_t)sq[j] * D;
+            const int si = sq[j];
+            if (grow) {  // rank-1 sample gradients: gscale[s] * grow[(step, row, head)] (the fused caption backward's
+                         // p_k * dres, formed here with the same product instead of stored 16 times per row)
+                const float sc = gscale[si];
+                const float* gp = grow + (size_t)(si / cNS) * D;
 #pragma unroll
-            for (int c = 0; c < CW; ++c) {
-                const int ch = lane + 64 * c;
-                gv[u][c] = gp[ch < D ? ch : 0];
+                for (int c = 0; c < CW; ++c) {
+                    const int ch = lane + 64 * c;
+                    gv[u][c] = sc * gp[ch < D ? ch : 0];
+                }
+            } else {
+                const float* gp = gsamp + (size_t)si * D;
+#pragma unroll
+                for (int c = 0; c < CW; ++c) {
+                    const int ch = lane + 64 * c;
+                    gv[u][c] = gp[ch < D ? ch : 0];
+                }
             }
         }
 #pragma unroll
@@ -700,7 +712,7 @@ __global__ __launch_bounds__(kCSA) void cap_softattn_bwd_kernel(
                                 wv.y * (1.f - th[k].y * th[k].y) * (h1.y - u0[q].y) +
                                 wv.z * (1.f - th[k].z * th[k].z) * (h1.z - u0[q].z) +
                                 wv.w * (1.f - th[k].w * th[k].w) * (h1.w - u0[q].w);
-            gc4[(size_t)k * D4] = make_float4(p[k] * g.x, p[k] * g.y, p[k] * g.z, p[k] * g.w);
+            if (gclip) gc4[(size_t)k * D4] = make_float4(p[k] * g.x, p[k] * g.y, p[k] * g.z, p[k] * g.w);
         }
         // CH = 4: one chunk's 16 rows in flight at a time (454 registers without the barrier, 449 with: one wave per
         // SIMD); CH = 1: 252 registers, two waves per SIMD, the scheduler hoisting the next samples' loads itself
@@ -884,12 +896,12 @@ extern "C" int pdvc_cap_value_grad_ex_f32(const uint8_t* value_pad_mask, const i
                                           save_loc, grad_samples, grad_value, grad_value_level_sums, stream);
 }
 
-extern "C" int pdvc_cap_value_grad_ranged_f32(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels,
-                                              int batch, int num_heads, int head_dim, int num_point, int rows,
-                                              int steps, int max_rows_per_video, const int32_t* video_row_start,
-                                              const int32_t* video_rows, const int32_t* step_rows,
-                                              const float* save_loc, const float* grad_samples, float* grad_value,
-                                              float* grad_value_level_sums, void* stream) {
+static int cap_value_grad_impl(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels, int batch,
+                               int num_heads, int head_dim, int num_point, int rows, int steps,
+                               int max_rows_per_video, const int32_t* video_row_start, const int32_t* video_rows,
+                               const int32_t* step_rows, const float* save_loc, const float* grad_samples,
+                               const float* grad_rows, const float* grad_scale, float* grad_value,
+                               float* grad_value_level_sums, void* stream) {
     float* level_sums = grad_value_level_sums;
     CapLevels lv;
     int S = 0;
@@ -934,7 +946,7 @@ extern "C" int pdvc_cap_value_grad_ranged_f32(const uint8_t* value_pad_mask, con
         const dim3 grid((unsigned)nblk), block(kCVW * 64);
 #define CVG(CW) hipLaunchKernelGGL((cap_value_grad_kernel<CW>), grid, block, lds, s, value_pad_mask, lv, S, num_heads, \
                                    head_dim, rows, s0, ns, acc, video_row_start, video_rows, save_loc, grad_samples,     \
-                                   grad_value, level_sums, step_rows)
+                                   grad_value, level_sums, step_rows, grad_rows, grad_scale)
         if (cw == 1) CVG(1);
         else if (cw == 2) CVG(2);
         else if (cw == 4) CVG(4);
@@ -943,6 +955,33 @@ extern "C" int pdvc_cap_value_grad_ranged_f32(const uint8_t* value_pad_mask, con
         PDVC_CHECK_LAUNCH("cap_value_grad_kernel");
     }
     return PDVC_OK;
+}
+
+extern "C" int pdvc_cap_value_grad_ranged_f32(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels,
+                                              int batch, int num_heads, int head_dim, int num_point, int rows,
+                                              int steps, int max_rows_per_video, const int32_t* video_row_start,
+                                              const int32_t* video_rows, const int32_t* step_rows,
+                                              const float* save_loc, const float* grad_samples, float* grad_value,
+                                              float* grad_value_level_sums, void* stream) {
+    PDVC_CHECK_ARG(grad_samples != nullptr, "grad_samples must not be NULL");
+    return cap_value_grad_impl(value_pad_mask, level_T, num_levels, batch, num_heads, head_dim, num_point, rows, steps,
+                               max_rows_per_video, video_row_start, video_rows, step_rows, save_loc, grad_samples,
+                               nullptr, nullptr, grad_value, grad_value_level_sums, stream);
+}
+
+// The same pass with rank-1 sample gradients: sample s = (step, row, head, k) has gradient grad_scale[s] *
+// grad_rows[(step, row, head)] (grad_rows (steps, rows, heads, head_dim), grad_scale (steps, rows, heads, 16)) -- the
+// caption step's p_k * dres, which pdvc_cap_softattn_backward_f32 then need not write 16 times per row.
+extern "C" int pdvc_cap_value_grad_rank1_f32(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels,
+                                             int batch, int num_heads, int head_dim, int num_point, int rows,
+                                             int steps, int max_rows_per_video, const int32_t* video_row_start,
+                                             const int32_t* video_rows, const int32_t* step_rows,
+                                             const float* save_loc, const float* grad_rows, const float* grad_scale,
+                                             float* grad_value, float* grad_value_level_sums, void* stream) {
+    PDVC_CHECK_ARG(grad_rows != nullptr && grad_scale != nullptr, "grad_rows and grad_scale must not be NULL");
+    return cap_value_grad_impl(value_pad_mask, level_T, num_levels, batch, num_heads, head_dim, num_point, rows, steps,
+                               max_rows_per_video, video_row_start, video_rows, step_rows, save_loc, nullptr,
+                               grad_rows, grad_scale, grad_value, grad_value_level_sums, stream);
 }
 
 extern "C" int pdvc_cap_value_grad_f32(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels,
@@ -1018,8 +1057,8 @@ extern "C" int pdvc_cap_softattn_backward_f32(const float* value, const uint8_t*
     if (head_dim != 512)
         return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "fused caption step needs head_dim 512, got %d", head_dim);
     PDVC_CHECK_ARG(value && U && row_video && offsets && ref && save_loc && probs && grad_res && att_h && alpha_w &&
-                       grad_att && grad_att_h && grad_samples && grad_alpha_w_part && grad_alpha_b_part &&
-                       grad_offsets, "fused caption step backward: NULL argument");
+                       grad_att && grad_att_h && grad_alpha_w_part && grad_alpha_b_part && grad_offsets,
+                   "fused caption step backward: NULL argument");
     PDVC_CHECK_ARG(off_col0 >= 0 && off_col0 + num_heads * cNS <= off_stride, "offset columns out of range");
     PDVC_CHECK_ARG(batch >= 0 && rows >= 0 && ld_att_h >= 512 && ld_grad_att_h >= 512, "invalid sizes");
     const void* al[] = {value, U, grad_res, att_h, alpha_w, grad_att, grad_att_h, grad_samples, grad_alpha_w_part};

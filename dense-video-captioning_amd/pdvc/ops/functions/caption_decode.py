@@ -42,6 +42,9 @@ CAP_FUSED = os.environ.get("PDVC_CAP_FUSED", "1") != "0"
 # ... and its backward in one launch (pdvc_cap_softattn_backward_f32, U-gradient form), re-forming the samples and att
 # from their corner rows: the forward then writes neither.  PDVC_CAP_FUSED_BWD=0: the two backward launches
 CAP_FUSED_BWD = os.environ.get("PDVC_CAP_FUSED_BWD", "1") != "0"
+# ... and the sample gradients it would write (p_k * dres, rank 1 per row) formed by the value-gradient pass from the
+# per-step dres rows and the probabilities (pdvc_cap_value_grad_rank1_f32); PDVC_CAP_RANK1=0: written and read back
+CAP_RANK1 = os.environ.get("PDVC_CAP_RANK1", "1") != "0"
 _BF16 = torch.bfloat16
 
 
@@ -218,8 +221,11 @@ class CaptionDecodeFunction(Function):
         # with the rows' per-video CSR, every step's sample gradient is kept and the value gradient is one
         # destination-sorted pass after the loop (pdvc_cap_value_grad_f32) instead of per-step atomics
         deferred = video_csr is not None
-        dCLIP_all = torch.empty((n if deferred else 1, R, M, NS, D), **kw)
+        # rank-1 sample gradients (fused backward, U-gradient form): the per-step dres rows are kept instead
+        rank1 = ctx.fused_bwd and deferred and CAP_RANK1
+        dCLIP_all = torch.empty((0 if rank1 else (n if deferred else 1), R, M, NS, D), **kw)
         dRES = torch.empty((R, M * D), **kw)
+        dRES_all = torch.empty((n, R, M * D), **kw) if rank1 else None
         dh = torch.empty((R, H), **kw)
         dc = [alloc((R, H), **kw), alloc((R, H), **kw)]
         zero = torch.zeros((R, H), **kw)
@@ -236,7 +242,7 @@ class CaptionDecodeFunction(Function):
                 s0, c = ranges[i]
                 rs = slice(s0, s0 + c)
                 rd1 = min(max(int(rd1_rows) - s0, 0), c)
-                dCLIP = dCLIP_all[i if deferred else 0][rs]
+                dCLIP = None if rank1 else dCLIP_all[i if deferred else 0][rs]
                 if c > 0:
                     last = i == n - 1
                     dhp = dHP[i][rs]
@@ -246,7 +252,8 @@ class CaptionDecodeFunction(Function):
                             None if last else _n.ptr(dc[(i + 1) % 2][rs]), _n.ptr(ACTS[i][rs]),
                             _n.ptr(CS[i - 1][rs] if i > 0 else zero), _n.ptr(CS[i][rs]), c, H, dg, lddg,
                             _n.ptr(dc[i % 2][rs]), st)
-                    _gemm(None, dhp[:, n_off + A:], W_att, dRES[:c], Watt16)
+                    dres = dRES_all[i][rs] if rank1 else dRES[:c]
+                    _gemm(None, dhp[:, n_off + A:], W_att, dres, Watt16)
                     ah, ldh = _n.rows(HP[i][rs][:, n_off:n_off + A])
                     gah, ldgah = _n.rows(dhp[:, n_off:n_off + A])
                     datt = dATT[i][s0 * ns_:(s0 + c) * ns_]
@@ -255,7 +262,7 @@ class CaptionDecodeFunction(Function):
                         _n.call("pdvc_cap_softattn_backward_f32", _n.ptr(value), _n.ptr(pad_mask), _n.ptr(U),
                                 _n.ptr(row_video[rs]), _n.ptr(HP[i][rs]), Ph, 0, _n.ptr(off_hs[rs]), _n.ptr(ref[rs]),
                                 RD, rd1, lvl, nl, Nv, c, M, D, NS // nl, _n.ptr(LOC[i][rs]), _n.ptr(PROBS[i][rs]),
-                                _n.ptr(dRES), ah, ldh, _n.ptr(alpha_w), _n.ptr(datt), gah, ldgah, _n.ptr(dCLIP),
+                                _n.ptr(dres), ah, ldh, _n.ptr(alpha_w), _n.ptr(datt), gah, ldgah, _n.ptr(dCLIP),
                                 _n.ptr(GAW[i][s0 * M:(s0 + c) * M]), _n.ptr(GAB[i][s0 * M:(s0 + c) * M]), _n.ptr(dhp),
                                 _n.ptr(gr_), st)
                     else:
@@ -288,9 +295,14 @@ class CaptionDecodeFunction(Function):
         if deferred:
             vr_start, vr_rows, max_rows = video_csr
             lsums = torch.empty(Nv, nl, M * D, dtype=gv.dtype, device=gv.device) if ctx.flat_value else None
-            _n.call("pdvc_cap_value_grad_ranged_f32", _n.ptr(pad_mask), lvl, nl, Nv, M, D, NS // nl, R, n,
-                    int(max_rows), _n.ptr(vr_start), _n.ptr(vr_rows), _n.ptr(sr_dev), _n.ptr(LOC), _n.ptr(dCLIP_all),
-                    _n.ptr(gv), _n.ptr(lsums), st)
+            if rank1:
+                _n.call("pdvc_cap_value_grad_rank1_f32", _n.ptr(pad_mask), lvl, nl, Nv, M, D, NS // nl, R, n,
+                        int(max_rows), _n.ptr(vr_start), _n.ptr(vr_rows), _n.ptr(sr_dev), _n.ptr(LOC),
+                        _n.ptr(dRES_all), _n.ptr(PROBS), _n.ptr(gv), _n.ptr(lsums), st)
+            else:
+                _n.call("pdvc_cap_value_grad_ranged_f32", _n.ptr(pad_mask), lvl, nl, Nv, M, D, NS // nl, R, n,
+                        int(max_rows), _n.ptr(vr_start), _n.ptr(vr_rows), _n.ptr(sr_dev), _n.ptr(LOC),
+                        _n.ptr(dCLIP_all), _n.ptr(gv), _n.ptr(lsums), st)
         # weight gradients: one GEMM each over every (step, row)
         d_gates = dHP[..., n_off + A:]                       # (n, R, 4H), row stride Ph: xe's gradient as is
         d_hs_g = d_gates.sum(0)

@@ -227,7 +227,8 @@ int pdvc_cap_softattn_forward_f32(const float* value, const uint8_t* value_pad_m
 /* The backward of pdvc_cap_softattn_forward_f32 in the caption decoder's U-gradient form (the value and U gradients
  * come from pdvc_cap_value_grad_ranged_f32 after the loop): pdvc_softattn_backward_f32 and
  * pdvc_cap_gather_backward2_f32 (value2 = U) in one launch, re-forming the samples and att from their corner rows.
- * Writes grad_att (R*M*16, 512), grad_samples (R,M,16,512), grad_alpha_w_part (R*M, 512), grad_alpha_b_part (R*M),
+ * Writes grad_att (R*M*16, 512), grad_samples (R,M,16,512; may be NULL: they are probs * grad_res, rank 1, which
+ * pdvc_cap_value_grad_rank1_f32 forms itself), grad_alpha_w_part (R*M, 512), grad_alpha_b_part (R*M),
  * grad_att_h (written at M == 1, accumulated otherwise) and the offset columns of grad_offsets (row stride off_stride);
  * grad_ref (may be NULL) is ACCUMULATED.  Alignment as pdvc_cap_softattn_forward_f32. */
 int pdvc_cap_softattn_backward_f32(const float* value, const uint8_t* value_pad_mask, const float* U,
@@ -454,6 +455,15 @@ int pdvc_cap_value_grad_ranged_f32(const uint8_t* value_pad_mask, const int32_t*
                                    int max_rows_per_video, const int32_t* video_row_start, const int32_t* video_rows,
                                    const int32_t* step_rows, const float* save_loc, const float* grad_samples,
                                    float* grad_value, float* grad_value_level_sums, void* stream);
+/* pdvc_cap_value_grad_ranged_f32 with rank-1 sample gradients: sample (step, row, head, k) has gradient
+ * grad_scale[step, row, head, k] * grad_rows[step, row, head, :] -- grad_rows (steps, rows, heads, head_dim),
+ * grad_scale (steps, rows, heads, 16) (the caption step's probabilities times its attended-row gradient). */
+int pdvc_cap_value_grad_rank1_f32(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels, int batch,
+                                  int num_heads, int head_dim, int num_point, int rows, int steps,
+                                  int max_rows_per_video, const int32_t* video_row_start, const int32_t* video_rows,
+                                  const int32_t* step_rows, const float* save_loc, const float* grad_rows,
+                                  const float* grad_scale, float* grad_value, float* grad_value_level_sums,
+                                  void* stream);
 
 /* ---- encoder positional input ------------------------------------------------------------------------
  * pos[n, s, c] = (c < F ? (c even ? sin : cos)(xe[n*S + s] / dim_t[c]) : dur[n*Dd + c - F])

@@ -729,6 +729,49 @@ def test_cap_softattn_backward_matches_two_launches(M, ref_dim, masked):
     assert out[0][5].abs().max().item() > 0 and out[0][6].abs().max().item() > 0
 
 
+@pytest.mark.parametrize("D,M", [(512, 1), (64, 2)])
+@pytest.mark.parametrize("masked", [False, True])
+def test_cap_value_grad_rank1_matches_materialised(D, M, masked):
+    """pdvc_cap_value_grad_rank1_f32 (sample gradients grad_scale[s] * grad_rows[step, row, head], formed in the
+    value-gradient pass) against pdvc_cap_value_grad_ranged_f32 on the materialised (steps, rows, heads, 16, D)
+    sample gradients: the same fp32 products summed in the same order, so bitwise equal (value gradient and level
+    sums)."""
+    from pdvc import _native as _n
+    rng = np.random.RandomState(D + M + masked)
+    T_l = [24, 12, 6, 3]
+    S, Nv, R, n = sum(T_l), 3, 10, 3
+    rv = rng.randint(0, Nv, size=R)
+    order = np.argsort(rv, kind="stable")
+    starts = np.concatenate([[0], np.cumsum(np.bincount(rv, minlength=Nv))]).astype(np.int32)
+    loc = cu(rng.uniform(-0.1, 1.1, size=(n, R, M, 16)), torch.float32)
+    grow = cu(rng.randn(n, R, M, D), torch.float32)
+    gsc = cu(rng.uniform(0, 1, size=(n, R, M, 16)), torch.float32)
+    gs = (gsc[..., None] * grow[:, :, :, None, :]).contiguous()
+    mask = None
+    if masked:
+        mk = np.zeros((Nv, S), np.uint8)
+        mk[1, 3:7] = 1
+        mk[2, 40:] = 1
+        mask = cu(mk)
+    vs, vr = cu(starts), cu(order.astype(np.int32))
+    max_rows = int(np.bincount(rv, minlength=Nv).max())
+    lvl = _n.int_array(T_l)
+    out = []
+    for rank1 in (False, True):
+        gv = torch.empty(Nv, S, M, D, device=DEV)
+        ls = torch.empty(Nv, 4, M * D, device=DEV)
+        if rank1:
+            _n.call("pdvc_cap_value_grad_rank1_f32", _n.ptr(mask), lvl, 4, Nv, M, D, 4, R, n, max_rows, _n.ptr(vs),
+                    _n.ptr(vr), None, _n.ptr(loc), _n.ptr(grow), _n.ptr(gsc), _n.ptr(gv), _n.ptr(ls), _n.stream())
+        else:
+            _n.call("pdvc_cap_value_grad_ranged_f32", _n.ptr(mask), lvl, 4, Nv, M, D, 4, R, n, max_rows, _n.ptr(vs),
+                    _n.ptr(vr), None, _n.ptr(loc), _n.ptr(gs), _n.ptr(gv), _n.ptr(ls), _n.stream())
+        torch.cuda.synchronize()
+        out.append((gv, ls))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    assert out[0][0].abs().max().item() > 0
+
+
 def test_cap_softattn_forward_rejects_other_widths():
     """the fused step is the 512-wide form only: any other head width is PDVC_ERR_UNSUPPORTED, not a wrong answer"""
     from pdvc import _native as _n
