@@ -734,8 +734,8 @@ def test_cap_softattn_backward_matches_two_launches(M, ref_dim, masked):
 def test_cap_value_grad_rank1_matches_materialised(D, M, masked):
     """pdvc_cap_value_grad_rank1_f32 (sample gradients grad_scale[s] * grad_rows[step, row, head], formed in the
     value-gradient pass) against pdvc_cap_value_grad_ranged_f32 on the materialised (steps, rows, heads, 16, D)
-    sample gradients: the same fp32 products summed in the same order, so bitwise equal (value gradient and level
-    sums)."""
+    sample gradients: the same fp32 products; the counting sort places a row's samples in atomic order, so the sums
+    agree to rounding (1e-6 of their magnitude), not bitwise, run to run as between the two forms."""
     from pdvc import _native as _n
     rng = np.random.RandomState(D + M + masked)
     T_l = [24, 12, 6, 3]
@@ -768,7 +768,8 @@ def test_cap_value_grad_rank1_matches_materialised(D, M, masked):
                     _n.ptr(vr), None, _n.ptr(loc), _n.ptr(gs), _n.ptr(gv), _n.ptr(ls), _n.stream())
         torch.cuda.synchronize()
         out.append((gv, ls))
-    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    for a, b in zip(out[0], out[1]):
+        assert (a - b).abs().max().item() <= 1e-6 * (a.abs().max().item() + 1.0)
     assert out[0][0].abs().max().item() > 0
 
 
