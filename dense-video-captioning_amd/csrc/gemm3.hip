@@ -1,0 +1,534 @@
+// gemm3.hip -- fp32 GEMM on the gfx950 bf16 matrix cores by exact three-term splitting.
+//
+// gfx950 has no xf32: the f32-input MFMA runs at 64 FLOP/clk/SIMD (157 TF/s), 1/16 of the bf16 MFMA rate.  Every
+// fp32 operand x is split on its way into LDS into three bf16 terms by round-to-nearest,
+//     x0 = bf16(x),  x1 = bf16(x - x0),  x2 = bf16(x - x0 - x1) = x - x0 - x1  (exactly),
+// with |x1| <= 2^-8 |x| and |x2| <= 2^-16 |x| -- the split is EXACT for normal fp32 values (24 significant bits in
+// three 8-bit pieces; the subtractions are exact in fp32).  The product keeps the six terms whose order is at most
+// 2^-16:  a.b = a0b0 + (a0b1 + a1b0) + (a0b2 + a2b0 + a1b1) + drop,  |drop| = |a1b2 + a2b1 + a2b2| <= 2^-23 |a||b|,
+// i.e. the same order as the rounding of one fp32 product (2^-24); every bf16 x bf16 product is exact in the fp32
+// accumulator of v_mfma_f32_32x32x16_bf16.  Six bf16 MFMAs per 32x32x16 step = 1024 * 16 / 6 / 64 = 2.67x the
+// f32-input MFMA's rate in exact arithmetic terms.  tests/test_gpu_gemm3.py measures the error against float64
+// next to hipBLASLt's fp32 GEMM on the same operands (GEMMs).
+//
+//   C[M,N] (op) = sum_k opA[m,k] * opB[n,k]
+//   A_KC: A[m*lda + k] (k contiguous) else A[k*lda + m];   B_KC: B[n*ldb + k] else B[k*ldb + n]
+//   nn.Linear: forward  y = x W^T       A = x (KC),  B = W (KC)
+//              dgrad    dx = dy W       A = dy (KC), B = W (MC: opB[n=in, k=out] = W[k*in + n])
+//              wgrad    dW = dy^T x     A = dy (MC), B = x (MC); the reduction (rows) split over gridDim.z
+//
+// Tiling: a 512-thread workgroup (8 waves) computes a BM x BN tile, each wave a 64 x 64 piece as 2 x 2 blocks of
+// 32 x 32; K advances in 32-deep stages.  A stage's fp32 slices are loaded into registers one stage ahead (full 128-B
+// lines for k-contiguous operands; 4 x 4 micro-blocks transposed in registers for mn-contiguous ones), split, and
+// written as three bf16 plane images [row][32 k] (64-B rows; the 16-B k-chunk index XOR-swizzled by (row >> 2) & 3,
+// so the 16-lane groups of a fragment read hit 16 distinct 16-B bank slots), double buffered: one barrier a stage.
+#include "pdvc_common.h"
+
+namespace pdvc {
+namespace g3 {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+#ifndef G3_ABLATE
+#define G3_ABLATE 0  // measurement-only builds (tools/variant_lib.sh): 1 no staging stores, 2 no staging loads, 4 no MFMA
+#endif
+
+constexpr int BK = 32;     // k per stage
+constexpr int ROWB = 64;   // bytes per LDS image row (BK bf16)
+constexpr int NT = 512;    // threads per workgroup
+
+enum { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_RELU = 2, EPI_ACCUM = 3, EPI_SLAB = 4 };
+
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+    const bf16x2 h = __builtin_convertvector((f32x2){a, b}, bf16x2);  // v_cvt_pk_bf16_f32, round to nearest even
+    return __builtin_bit_cast(unsigned, h);
+}
+
+// x -> (x0, x1, x2) for two values; packed pairs, element 0 in the low half (the lower k)
+__device__ __forceinline__ void split2(float a, float b, unsigned& p0, unsigned& p1, unsigned& p2) {
+    p0 = pk_bf16(a, b);
+    const float ra = a - __uint_as_float(p0 << 16);
+    const float rb = b - __uint_as_float(p0 & 0xffff0000u);
+    p1 = pk_bf16(ra, rb);
+    const float sa = ra - __uint_as_float(p1 << 16);
+    const float sb = rb - __uint_as_float(p1 & 0xffff0000u);
+    p2 = pk_bf16(sa, sb);
+}
+
+// byte offset of the 4 k values [4*k4, 4*k4 + 4) of image row `row`
+__device__ __forceinline__ int unit_off(int row, int k4) {
+    return row * ROWB + ((((k4 >> 1) ^ (row >> 2)) & 3) << 4) + ((k4 & 1) << 3);
+}
+// byte offset of the 8 k values [8*c, 8*c + 8) of image row `row` (a fragment's 16 bytes)
+__device__ __forceinline__ int frag_off(int row, int c) { return row * ROWB + (((c ^ (row >> 2)) & 3) << 4); }
+
+// One operand's stage: R rows (m or n) x BK k, staged through registers (NV float4 per thread) as NU pieces: a KC
+// piece is 4 k values of one row (threads 8 apart walk a row: full 128-B lines), an MC piece a 4 k x 4 mn block
+// transposed in registers (k group fastest across lanes: 8 lanes cover one 128-B line of each of 4 k rows, and the
+// 8 lanes of one mn group then write a whole 64-B image row -- conflict-free).
+template <int R, bool KC>
+struct Stage {
+    static constexpr int NP = KC ? R * BK / 4 : (R / 4) * (BK / 4);  // pieces per stage
+    static constexpr int NU = (NP + NT - 1) / NT;
+    static constexpr int NV = KC ? NU : 4 * NU;  // float4 registers
+    float4 v[NV];
+
+    __device__ __forceinline__ static bool has(int i) { return NP % NT == 0 || (int)threadIdx.x + NT * i < NP; }
+
+    // unconditional loads (no branch, no per-load wait): K is a multiple of BK, so a stage never leaves the k range;
+    // rows (KC) or column groups (MC) past the matrix are clamped to its last one -- they feed only outputs that are
+    // never stored
+    __device__ __forceinline__ void load(int i, const float* __restrict__ P, long ld, int mn0, int k0, int MN) {
+        const int u = has(i) ? threadIdx.x + NT * i : 0;
+        if constexpr (KC) {
+            const int row = min(mn0 + (u >> 3), MN - 1), k = k0 + ((u & 7) << 2);
+            v[i] = *reinterpret_cast<const float4*>(P + (long)row * ld + k);
+        } else {
+            const int kg = u & 7, mn = min(mn0 + 4 * (u >> 3), MN - 4);
+            const float* q = P + (long)(k0 + 4 * kg) * ld + mn;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[4 * i + j] = *reinterpret_cast<const float4*>(q + j * ld);
+        }
+    }
+
+    // split piece i and write its three planes (plane p at img + p * R * ROWB)
+    __device__ __forceinline__ void store(int i, char* __restrict__ img) const {
+        if (!has(i)) return;
+        const int u = threadIdx.x + NT * i;
+        if constexpr (KC) {
+            const int off = unit_off(u >> 3, u & 7);
+            uint2 p0, p1, p2;
+            split2(v[i].x, v[i].y, p0.x, p1.x, p2.x);
+            split2(v[i].z, v[i].w, p0.y, p1.y, p2.y);
+            *reinterpret_cast<uint2*>(img + off) = p0;
+            *reinterpret_cast<uint2*>(img + R * ROWB + off) = p1;
+            *reinterpret_cast<uint2*>(img + 2 * R * ROWB + off) = p2;
+        } else {
+            const int kg = u & 7, r0 = 4 * (u >> 3);
+            const float4* q = v + 4 * i;
+            // image row r0 + e takes (q[0].e, q[1].e, q[2].e, q[3].e): k = 4kg .. 4kg + 3
+#define G3_COL(E, F)                                                                        \
+    {                                                                                      \
+        const int off = unit_off(r0 + E, kg);                                              \
+        uint2 p0, p1, p2;                                                                  \
+        split2(q[0].F, q[1].F, p0.x, p1.x, p2.x);                                          \
+        split2(q[2].F, q[3].F, p0.y, p1.y, p2.y);                                          \
+        *reinterpret_cast<uint2*>(img + off) = p0;                                         \
+        *reinterpret_cast<uint2*>(img + R * ROWB + off) = p1;                              \
+        *reinterpret_cast<uint2*>(img + 2 * R * ROWB + off) = p2;                          \
+    }
+            G3_COL(0, x) G3_COL(1, y) G3_COL(2, z) G3_COL(3, w)
+#undef G3_COL
+        }
+    }
+    __device__ __forceinline__ void load_all(const float* P, long ld, int mn0, int k0, int MN) {
+#pragma unroll
+        for (int i = 0; i < NU; ++i) load(i, P, ld, mn0, k0, MN);
+    }
+    __device__ __forceinline__ void store_all(char* img) const {
+#pragma unroll
+        for (int i = 0; i < NU; ++i) store(i, img);
+    }
+};
+
+// the six products of one 32 x 32 x 16 step, smallest terms first
+__device__ __forceinline__ f32x16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 x) {
+    x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], x, 0, 0, 0);
+    x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], x, 0, 0, 0);
+    x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], x, 0, 0, 0);
+    x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], x, 0, 0, 0);
+    x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], x, 0, 0, 0);
+    x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], x, 0, 0, 0);
+    return x;
+}
+
+template <int EPI, bool FULL>
+__device__ __forceinline__ void store_tile(const f32x16 (&acc)[2][2], float* __restrict__ C, long ldc,
+                                           const float* __restrict__ bias, int r0, int c0, int M, int N, int l32,
+                                           int h) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int col = c0 + 32 * j + l32;
+        const bool colok = FULL || col < N;
+        const float bv = (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) ? bias[colok ? col : 0] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int rbase = r0 + 32 * i + 4 * h;
+            float* p0 = C + (long)rbase * ldc + col;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int dr = (r & 3) + 8 * (r >> 2);
+                if (FULL || (colok && rbase + dr < M)) {
+                    float v = acc[i][j][r] + bv;
+                    if (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+                    float* p = p0 + (long)dr * ldc;
+                    if (EPI == EPI_ACCUM) v += *p;
+                    *p = v;
+                }
+            }
+        }
+    }
+}
+
+template <int BM, int BN, bool AKC, bool BKC, int EPI>
+__global__ __launch_bounds__(NT, 1) void gemm3_kernel(int M, int N, int K, const float* __restrict__ A, long lda,
+                                                      const float* __restrict__ B, long ldb, float* __restrict__ C,
+                                                      long ldc, const float* __restrict__ bias, int k_per_split,
+                                                      int tiles_n, long slab) {
+    static_assert((BM / 64) * (BN / 64) == NT / 64, "one 64 x 64 piece per wave");
+    constexpr int AIMG = 3 * BM * ROWB, BIMG = 3 * BN * ROWB, STAGE = AIMG + BIMG;
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);  // the tiles of one row block run on one XCD (A from its L2)
+    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kb = blockIdx.z * k_per_split;
+    const int nst = (min(K, kb + k_per_split) - kb) / BK;
+    const int wm = (wid / (BN / 64)) * 64, wn = (wid % (BN / 64)) * 64;
+    const int l32 = lane & 31, h = lane >> 5;
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // register ring one stage deep: the registers hold stage s + 1 while stage s computes; they are split into
+    // the other LDS buffer during stage s's first k half and reloaded with stage s + 2 during its second
+    Stage<BM, AKC> sa;
+    Stage<BN, BKC> sb;
+    if (nst > 0) {
+        sa.load_all(A, lda, m0, kb, M);
+        sb.load_all(B, ldb, n0, kb, N);
+        sa.store_all(lds);
+        sb.store_all(lds + AIMG);
+        if (nst > 1) {
+            sa.load_all(A, lda, m0, kb + BK, M);
+            sb.load_all(B, ldb, n0, kb + BK, N);
+        }
+    }
+    __syncthreads();
+    for (int s = 0; s < nst; ++s) {
+        const char* cur = lds + (s & 1) * STAGE;
+        char* nxt = lds + ((s + 1) & 1) * STAGE;
+        const bool more = s + 1 < nst, more2 = s + 2 < nst;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 a[2][3], b[2][3];
+            const int c = 2 * ks + h;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int ra = wm + 32 * i + l32, rb = wn + 32 * i + l32;
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    a[i][p] = *reinterpret_cast<const bf16x8*>(cur + p * BM * ROWB + frag_off(ra, c));
+                    b[i][p] = *reinterpret_cast<const bf16x8*>(cur + AIMG + p * BN * ROWB + frag_off(rb, c));
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int i = q >> 1, j = q & 1;
+                if constexpr ((G3_ABLATE & 4) == 0) acc[i][j] = mfma6(a[i], b[j], acc[i][j]);
+                else {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) asm volatile("" ::"v"(a[i][p]), "v"(b[j][p]));
+                }
+                if (ks == 0 && more && (G3_ABLATE & 1) == 0) {
+                    // staging work between the MFMA groups: A pieces after groups 0..NU_A-1, then B
+#pragma unroll
+                    for (int u = 0; u < Stage<BM, AKC>::NU; ++u)
+                        if (u * 4 / Stage<BM, AKC>::NU == q) sa.store(u, nxt);
+#pragma unroll
+                    for (int u = 0; u < Stage<BN, BKC>::NU; ++u)
+                        if (u * 4 / Stage<BN, BKC>::NU == q) sb.store(u, nxt + AIMG);
+                }
+                if (ks == 1 && more2 && (G3_ABLATE & 2) == 0) {
+#pragma unroll
+                    for (int u = 0; u < Stage<BM, AKC>::NU; ++u)
+                        if (u * 4 / Stage<BM, AKC>::NU == q) sa.load(u, A, lda, m0, kb + (s + 2) * BK, M);
+#pragma unroll
+                    for (int u = 0; u < Stage<BN, BKC>::NU; ++u)
+                        if (u * 4 / Stage<BN, BKC>::NU == q) sb.load(u, B, ldb, n0, kb + (s + 2) * BK, N);
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // epilogue: acc[i][j] register r of lane l is C[row][col], col = l % 32, row = (r & 3) + 8 (r >> 2) + 4 (l / 32)
+    float* Cz = C + (EPI == EPI_SLAB ? (long)blockIdx.z * slab : 0);
+    const bool full = m0 + BM <= M && n0 + BN <= N;  // whole tile inside C: no per-element checks
+    if (full) {
+        store_tile<EPI, true>(acc, Cz, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h);
+    } else {
+        store_tile<EPI, false>(acc, Cz, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h);
+    }
+}
+
+// ---- opB pre-split: the weight operand's three planes made once per call (split_planes_kernel) and streamed into
+// LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, no VALU), so the in-loop split work is the A operand's
+// alone.  Tile BM = 128 (A, split in registers) x BN = 256 (B planes), 8 waves of 64 x 64.
+
+typedef __attribute__((address_space(3))) void g3_lds_t;
+
+// planes[p][n][k] (bf16 bits) of opB[n][k]; b_kc 1: B[n*ldb + k], 0: B[k*ldb + n].  One thread per 4 k of a row.
+__global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ B, long ldb, int b_kc, int N,
+                                                           int K, uint16_t* __restrict__ planes) {
+    const long n4 = (long)N * (K / 4);
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+        const int n = (int)(i / (K / 4)), k = (int)(i % (K / 4)) * 4;
+        float v[4];
+        if (b_kc) {
+            const float4 x = *reinterpret_cast<const float4*>(B + (long)n * ldb + k);
+            v[0] = x.x, v[1] = x.y, v[2] = x.z, v[3] = x.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = B[(long)(k + j) * ldb + n];
+        }
+        uint2 p0, p1, p2;
+        split2(v[0], v[1], p0.x, p1.x, p2.x);
+        split2(v[2], v[3], p0.y, p1.y, p2.y);
+        const long o = (long)n * K + k;
+        *reinterpret_cast<uint2*>(planes + o) = p0;
+        *reinterpret_cast<uint2*>(planes + (long)N * K + o) = p1;
+        *reinterpret_cast<uint2*>(planes + 2L * N * K + o) = p2;
+    }
+}
+
+// one LDS-DMA wave-instruction: 16 image rows x 64 B of one plane.  Lane l lands at dst + 16 l = row l / 4, slot
+// l % 4; the slot holds k chunk (l % 4) ^ ((row >> 2) & 3) (the image's swizzle, applied on the source address).
+// Issued by inline assembly: the compiler neither sees nor waits for it (its own waits only over-count, never
+// under-count, since these DMAs only add to vmcnt); the kernel retires them with an explicit vmcnt before the barrier.
+__device__ __forceinline__ void planes_dma(char* dst, const uint16_t* __restrict__ plane, int K, int row0, int N,
+                                           int k0, int lane) {
+    const int row = row0 + (lane >> 2);
+    const int c = (lane & 3) ^ ((row >> 2) & 3);
+    const uint16_t* src = plane + (long)min(row, N - 1) * K + k0 + 8 * c;
+    const uint32_t d = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(g3_lds_t*)dst);
+    int keep;
+    __asm__ volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(src), "s"(d)
+                     : "memory");
+}
+
+template <int EPI>
+__global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, const float* __restrict__ A, long lda,
+                                                       const uint16_t* __restrict__ planes, float* __restrict__ C,
+                                                       long ldc, const float* __restrict__ bias, int tiles_n) {
+    constexpr int BM = 128, BN = 256;
+    constexpr int AIMG = 3 * BM * ROWB, BIMG = 3 * BN * ROWB, STAGE = AIMG + BIMG;
+    constexpr int BDMA = 3 * BN / 16 / (NT / 64);  // LDS-DMA instructions per wave per stage (6)
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);  // the column tiles of one row block share an XCD's L2
+    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int nst = K / BK;
+    const int wm = (wid / (BN / 64)) * 64, wn = (wid % (BN / 64)) * 64;
+    const int l32 = lane & 31, h = lane >> 5;
+    const long pstride = (long)N * K;
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    auto b_dma = [&](char* img, int k0) {
+#pragma unroll
+        for (int q = 0; q < BDMA; ++q) {
+            const int g = wid * BDMA + q;  // 48 instructions: plane g / 16, rows 16 (g % 16) ..
+            const int p = g / (BN / 16), r0 = (g % (BN / 16)) * 16;
+            planes_dma(img + AIMG + p * BN * ROWB + r0 * ROWB, planes + p * pstride, K, n0 + r0, N, k0, lane);
+        }
+    };
+
+    Stage<BM, true> sa;
+    if (nst > 0) {
+        b_dma(lds, 0);
+        sa.load_all(A, lda, m0, 0, M);
+        sa.store_all(lds);
+        if (nst > 1) sa.load_all(A, lda, m0, BK, M);
+        __builtin_amdgcn_s_waitcnt(0x0F70 | (Stage<BM, true>::NU & 15));  // vmcnt(A loads): the DMAs have landed
+    }
+    __syncthreads();
+    for (int s = 0; s < nst; ++s) {
+        const char* cur = lds + (s & 1) * STAGE;
+        char* nxt = lds + ((s + 1) & 1) * STAGE;
+        const bool more = s + 1 < nst, more2 = s + 2 < nst;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 a[2][3], b[2][3];
+            const int c = 2 * ks + h;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int ra = wm + 32 * i + l32, rb = wn + 32 * i + l32;
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    a[i][p] = *reinterpret_cast<const bf16x8*>(cur + p * BM * ROWB + frag_off(ra, c));
+                    b[i][p] = *reinterpret_cast<const bf16x8*>(cur + AIMG + p * BN * ROWB + frag_off(rb, c));
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int i = q >> 1, j = q & 1;
+                acc[i][j] = mfma6(a[i], b[j], acc[i][j]);
+                if (ks == 0 && more && q < Stage<BM, true>::NU) sa.store(q, nxt);
+                // after the A registers are in LDS: stage s + 1's B planes (DMA), then stage s + 2's A rows.  In
+                // this order the compiler's own wait for the A rows (next stage) never covers fresh DMAs
+                if (ks == 0 && more && q == Stage<BM, true>::NU) b_dma(nxt, (s + 1) * BK);
+                if (ks == 0 && more2 && q == Stage<BM, true>::NU) sa.load_all(A, lda, m0, (s + 2) * BK, M);
+            }
+        }
+        // the B DMAs of stage s + 1 are older than this stage's A loads (at most NU of them): retire the DMAs
+        if (more2) __builtin_amdgcn_s_waitcnt(0x0F70 | (Stage<BM, true>::NU & 15));
+        else __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
+    }
+
+    float* Cz = C;
+    const bool full = m0 + BM <= M && n0 + BN <= N;
+    if (full) store_tile<EPI, true>(acc, Cz, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h);
+    else store_tile<EPI, false>(acc, Cz, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h);
+}
+
+// out[i] (=|+=) sum_z ws[z * n + i], float4 lanes (n % 4 == 0)
+template <bool ACC>
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ ws, int splits, long n4,
+                                                       float* __restrict__ out) {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+        float4 s = ACC ? reinterpret_cast<const float4*>(out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int z = 0; z < splits; ++z) {
+            const float4 v = reinterpret_cast<const float4*>(ws)[(long)z * n4 + i];
+            s.x += v.x;
+            s.y += v.y;
+            s.z += v.z;
+            s.w += v.w;
+        }
+        reinterpret_cast<float4*>(out)[i] = s;
+    }
+}
+
+}  // namespace g3
+}  // namespace pdvc
+
+using namespace pdvc;
+using namespace pdvc::g3;
+
+namespace {
+
+template <int BM, int BN, bool AKC, bool BKC>
+void launch_epi(int epi, dim3 grid, hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B,
+                long ldb, float* C, long ldc, const float* bias, int kps, int tiles_n, long slab) {
+#define G3_L(E) \
+    hipLaunchKernelGGL((gemm3_kernel<BM, BN, AKC, BKC, E>), grid, dim3(NT), 0, s, M, N, K, A, lda, B, ldb, C, ldc, bias, kps, tiles_n, slab)
+    switch (epi) {
+        case EPI_STORE: G3_L(EPI_STORE); break;
+        case EPI_BIAS: G3_L(EPI_BIAS); break;
+        case EPI_BIAS_RELU: G3_L(EPI_BIAS_RELU); break;
+        case EPI_ACCUM: G3_L(EPI_ACCUM); break;
+        default: G3_L(EPI_SLAB); break;
+    }
+#undef G3_L
+}
+
+}  // namespace
+
+// C-ABI: see include/pdvc_msda.h ("fp32 GEMM on the bf16 matrix cores")
+extern "C" int pdvc_gemm3_f32(int M, int N, int K, const float* A, long lda, int a_kc, const float* B, long ldb,
+                              int b_kc, float* C, long ldc, const float* bias, int epilogue, int splits,
+                              float* workspace, void* stream) {
+    PDVC_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "negative sizes");
+    PDVC_CHECK_ARG((a_kc == 0 || a_kc == 1) && (b_kc == 0 || b_kc == 1), "a_kc / b_kc must be 0 or 1");
+    PDVC_CHECK_ARG(epilogue >= 0 && epilogue <= 3, "epilogue must be 0..3");
+    PDVC_CHECK_ARG(epilogue != 1 && epilogue != 2 ? true : bias != nullptr, "bias epilogue needs a bias");
+    PDVC_CHECK_ARG(splits >= 1 && (splits == 1 || (epilogue == 0 || epilogue == 3)), "splits > 1: store or accumulate only");
+    PDVC_CHECK_ARG(splits == 1 || workspace != nullptr, "splits > 1 needs a workspace of splits * M * N floats");
+    PDVC_CHECK_ARG(lda >= (a_kc ? K : M) && ldb >= (b_kc ? K : N) && ldc >= N, "leading dimensions too small");
+    // float4 operand loads: 16-B aligned bases, leading dimensions and the contiguous extents multiples of 4
+    PDVC_CHECK_ARG((uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0,
+                   "operands must be 16-byte aligned with leading dimensions divisible by 4");
+    PDVC_CHECK_ARG(K % BK == 0, "K must be a multiple of 32");
+    PDVC_CHECK_ARG((a_kc ? 4 : M) % 4 == 0 && (b_kc ? 4 : N) % 4 == 0 && (a_kc || M >= 4) && (b_kc || N >= 4),
+                   "mn-contiguous operands need M (N) divisible by 4");
+    PDVC_CHECK_ARG(splits == 1 || (ldc == N && N % 4 == 0 && (uintptr_t)C % 16 == 0),
+                   "split reduction needs a dense, 16-byte aligned C with N divisible by 4");
+    if (M == 0 || N == 0) return PDVC_OK;
+    hipStream_t s = (hipStream_t)stream;
+    constexpr int BM = 256, BN = 128;
+    const long tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+    PDVC_CHECK_ARG(tiles_m * tiles_n < (1L << 31), "too many tiles");
+    int kps = (K + splits - 1) / splits;
+    kps = (kps + BK - 1) / BK * BK;
+    const int nz = K == 0 ? 1 : (K + kps - 1) / kps;
+    PDVC_CHECK_ARG(nz <= 65535, "too many splits");
+    const dim3 grid((unsigned)(tiles_m * tiles_n), 1, (unsigned)nz);
+    const bool slab = nz > 1;
+    float* dst = slab ? workspace : C;
+    const long ld = slab ? N : ldc;
+    const int epi = slab ? (int)EPI_SLAB : epilogue;
+    const long slab_n = (long)M * N;
+    if (a_kc && b_kc) launch_epi<BM, BN, true, true>(epi, grid, s, M, N, K, A, lda, B, ldb, dst, ld, bias, kps, (int)tiles_n, slab_n);
+    else if (a_kc) launch_epi<BM, BN, true, false>(epi, grid, s, M, N, K, A, lda, B, ldb, dst, ld, bias, kps, (int)tiles_n, slab_n);
+    else if (b_kc) launch_epi<BM, BN, false, true>(epi, grid, s, M, N, K, A, lda, B, ldb, dst, ld, bias, kps, (int)tiles_n, slab_n);
+    else launch_epi<BM, BN, false, false>(epi, grid, s, M, N, K, A, lda, B, ldb, dst, ld, bias, kps, (int)tiles_n, slab_n);
+    PDVC_CHECK_LAUNCH("gemm3_kernel");
+    if (slab) {
+        const long n4 = slab_n / 4;
+        const int blocks = (int)std::min<long>((n4 + 255) / 256, 2048);
+        if (epilogue == 3) hipLaunchKernelGGL(slab_sum_kernel<true>, dim3(blocks), dim3(256), 0, s, workspace, nz, n4, C);
+        else hipLaunchKernelGGL(slab_sum_kernel<false>, dim3(blocks), dim3(256), 0, s, workspace, nz, n4, C);
+        PDVC_CHECK_LAUNCH("slab_sum_kernel");
+    }
+    return PDVC_OK;
+}
+
+// C-ABI: see include/pdvc_msda.h
+extern "C" int pdvc_split3_planes_f32(const float* B, long ldb, int b_kc, int N, int K, uint16_t* planes,
+                                      void* stream) {
+    PDVC_CHECK_ARG(N > 0 && K > 0 && K % BK == 0, "N > 0 and K a positive multiple of 32");
+    PDVC_CHECK_ARG(ldb >= (b_kc ? K : N), "leading dimension too small");
+    PDVC_CHECK_ARG(!b_kc || ((uintptr_t)B % 16 == 0 && ldb % 4 == 0), "k-contiguous B: 16-byte aligned rows");
+    PDVC_CHECK_ARG((uintptr_t)planes % 16 == 0, "planes must be 16-byte aligned");
+    const long n4 = (long)N * (K / 4);
+    const int blocks = (int)std::min<long>((n4 + 255) / 256, 4096);
+    hipLaunchKernelGGL(split_planes_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, B, ldb, b_kc, N, K, planes);
+    PDVC_CHECK_LAUNCH("split_planes_kernel");
+    return PDVC_OK;
+}
+
+extern "C" int pdvc_gemm3p_f32(int M, int N, int K, const float* A, long lda, const uint16_t* planes, float* C,
+                               long ldc, const float* bias, int epilogue, void* stream) {
+    PDVC_CHECK_ARG(M >= 0 && N > 0 && K >= 0 && K % BK == 0, "sizes: N > 0, K a multiple of 32");
+    PDVC_CHECK_ARG(epilogue >= 0 && epilogue <= 3, "epilogue must be 0..3");
+    PDVC_CHECK_ARG(epilogue != 1 && epilogue != 2 ? true : bias != nullptr, "bias epilogue needs a bias");
+    PDVC_CHECK_ARG(lda >= K && ldc >= N, "leading dimensions too small");
+    PDVC_CHECK_ARG((uintptr_t)A % 16 == 0 && lda % 4 == 0 && (uintptr_t)planes % 16 == 0,
+                   "A rows and the planes must be 16-byte aligned");
+    if (M == 0) return PDVC_OK;
+    const long tiles_m = (M + 127) / 128, tiles_n = (N + 255) / 256;
+    PDVC_CHECK_ARG(tiles_m * tiles_n < (1L << 31), "too many tiles");
+    const dim3 grid((unsigned)(tiles_m * tiles_n));
+    hipStream_t s = (hipStream_t)stream;
+#define G3P_L(E) hipLaunchKernelGGL(gemm3p_kernel<E>, grid, dim3(NT), 0, s, M, N, K, A, lda, planes, C, ldc, bias, (int)tiles_n)
+    switch (epilogue) {
+        case 0: G3P_L(EPI_STORE); break;
+        case 1: G3P_L(EPI_BIAS); break;
+        case 2: G3P_L(EPI_BIAS_RELU); break;
+        default: G3P_L(EPI_ACCUM); break;
+    }
+#undef G3P_L
+    PDVC_CHECK_LAUNCH("gemm3p_kernel");
+    return PDVC_OK;
+}

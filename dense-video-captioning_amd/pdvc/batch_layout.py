@@ -113,6 +113,9 @@ def live_rows(counts, steps, n_steps):
 def step_ranges(live, Ld, R):
     """(start, count) of the rows of each step for a caption_layout(..., steps=...) ordering: the live rows of
     Ld = 2 are [R - a_t, R + a_t), of Ld = 1 [0, a_t)."""
+    live = [int(a) for a in live]
+    if any(b > a for a, b in zip(live, live[1:])) or any(a < 0 or a > R for a in live):
+        raise ValueError("step_ranges: live rows must be non-increasing and within the layer's rows")
     if Ld == 2:
         return tuple((R - a, 2 * a) for a in live)
     if Ld == 1:
@@ -165,6 +168,10 @@ def pad_to_capacity(dt, events, rows, words, tokens=None, alive=None):
         alive = tuple(int(a) for a in alive)
         if len(alive) != words - 1:
             raise ValueError(f"pad_to_capacity: alive needs {words - 1} steps, got {len(alive)}")
+        if any(b > a for a, b in zip(alive, alive[1:])) or min(alive, default=0) < 0:
+            # each step's rows must be nested in the previous step's (CaptionDecodeFunction reads step t - 1's
+            # state for every row of step t): a row entering a range late would read state never written
+            raise ValueError("pad_to_capacity: alive must be non-increasing and non-negative")
         from .CaptioningHead.LSTM_DSA import caption_steps
         o, steps = 0, []
         for c_ in counts:

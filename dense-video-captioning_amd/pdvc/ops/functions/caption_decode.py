@@ -97,6 +97,10 @@ class CaptionDecodeFunction(Function):
         ranges = tuple(tuple(r) for r in step_ranges[0]) if ranged else ((0, R),) * n
         if len(ranges) != n or any(s0 < 0 or c < 0 or s0 + c > R for s0, c in ranges):
             raise ValueError("caption decode: step_ranges must give one in-bounds (start, count) per step")
+        # step t reads step t - 1's state (CS, HS) of each of its rows: every range must lie inside the previous one,
+        # else a row entering late reads entries no step wrote
+        if any(s1 < s0 or s1 + c1 > s0 + c0 for (s0, c0), (s1, c1) in zip(ranges, ranges[1:])):
+            raise ValueError("caption decode: step_ranges must be nested (each step's rows inside the previous step's)")
         A = W_ctx.shape[0]
         NS = NUM_SAMPLES
         n_off = M * NS

@@ -136,6 +136,16 @@ def _masked_query_max(hs_l, query_mask):
     return hs_l.masked_fill(~query_mask[..., None], float("-inf"))
 
 
+
+def contiguous_range(sel):
+    """(start, length) when the row list `sel` is exactly start, start + 1, ..., start + length - 1, else None: the
+    last decoder layer's caption rows can then be a narrow view instead of a gather (a permutation
+    of a contiguous block is not such a range)."""
+    if not sel:
+        return None
+    s0 = int(sel[0])
+    return (s0, len(sel)) if list(sel) == list(range(s0, s0 + len(sel))) else None
+
 class PDVC(nn.Module):
     def __init__(self, base_encoder, transformer, captioner, num_classes, num_queries, num_feature_levels,
                  aux_loss=True, with_box_refine=False, opt=None, translator=None):
@@ -363,12 +373,16 @@ class PDVC(nn.Module):
             cap_rows = rc + m.targets[rp, rk] * Lc["valid"]
             rows = Lc["rows_host"]  # (layer, video) per row, phantom rows (layer, 0): rd1 and n_last below
             last_sel = Lc["last_sel_host"]
+            # a step-ordered layout permutes the last layer's rows per batch; a captured step graph keeps whatever
+            # view it was captured with, so such a layout always gathers (never a narrow view)
+            ordered_layout = bool(Lc.get("ordered"))
             ranges = Lc.get("step_ranges")
             row_valid = Lc["valid"] if cap is not None else None
             lay = lay_t
         else:
             row_valid = None
             ranges = None
+            ordered_layout = False
             rows = []  # (layer, video, flat_hs_index, cap_row)
             for l_id, indices in enumerate(layer_indices):
                 for v, (qi, gi) in enumerate(indices):
@@ -401,9 +415,10 @@ class PDVC(nn.Module):
         else:
             steps_v = [caption_steps(cap_cpu[cap_off[v]:cap_off[v + 1]]) for v in range(N)]
         video_csr = (vr_start_d.to(torch.int32), vr_rows_d.to(torch.int32), max_rows)
-        # the last layer's rows are one contiguous block (rows are layer-major): its outputs are views, not copies
-        last_range = (last_sel[0], len(last_sel)) if last_sel and last_sel[-1] - last_sel[0] + 1 == len(last_sel) \
-            else None
+        # the last layer's rows are one contiguous block in video-major order (rows are layer-major): its outputs
+        # are views, not copies.  With the step-ordered layout last_sel is a permutation of its block (layer 1 in
+        # descending step count), so the test is element by element, not first/last/length
+        last_range = contiguous_range(last_sel) if not ordered_layout else None
         return dict(rows=rows, hs_rows=hs_rows, ref_rows=ref_rows.contiguous(), rd1=rd1, row_video=row_video,
                     cap_rows=cap_rows, lay=lay, vid=vid, last_sel=last_sel_d, last_range=last_range, steps_v=steps_v,
                     video_csr=video_csr, row_valid=row_valid, step_ranges=ranges)

@@ -545,6 +545,19 @@ int pdvc_seq_attention_backward_f32(const float* q, long ldq, const float* k, lo
 int pdvc_gemm_f32(int M, int N, int K, const float* A, int lda, int trans_a, const float* B, int ldb, int trans_b,
                   float* C, int ldc, const float* bias, int epilogue, int split_k, void* stream);
 
+/* ---- fp32 GEMM on the bf16 matrix cores (three-term split) ----------------------------------------
+ * Replaces the nn.Linear products of the reference's projections (pdvc/ops/modules/ms_deform_attn.py:55-58,
+ * deformable_transformer.py:162-189 and their autograd backward; torch.addmm / mm in the reference).
+ * C[M,N] (=|+=) sum_k opA[m,k] opB[n,k] (+ bias[n]) (ReLU), fp32 in and out.  a_kc 1 -> A[m*lda + k], 0 ->
+ * A[k*lda + m]; b_kc 1 -> B[n*ldb + k], 0 -> B[k*ldb + n].  Each operand is split exactly into three bf16 terms
+ * (x = x0 + x1 + x2) and the six products of order >= 2^-16 run on v_mfma_f32_32x32x16_bf16 with fp32
+ * accumulation: the dropped terms are <= 2^-23 |a||b| per product (one fp32 product rounding is 2^-24).
+ * epilogue 0 store, 1 + bias, 2 + bias then ReLU, 3 accumulate into C.  splits > 1 splits K over workgroups
+ * into `workspace` (splits * M * N floats, epilogues 0/3 only) and sums the slabs deterministically.
+ * Operands 16-byte aligned, leading dimensions and contiguous extents divisible by 4. */
+int pdvc_gemm3_f32(int M, int N, int K, const float* A, long lda, int a_kc, const float* B, long ldb, int b_kc,
+                   float* C, long ldc, const float* bias, int epilogue, int splits, float* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -126,3 +126,35 @@ def test_step_ordered_layout_keeps_live_rows_contiguous(Ld, rows_cap):
         rows = lay["vr_rows"][lay["vr_start"][v]:lay["vr_start"][v + 1]]
         assert sorted(int(lay["vid"][r]) for r in rows) == [v] * (Ld * counts[v])
         assert all(lay["valid"][r] for r in rows)
+
+
+def test_step_ordered_last_layer_is_a_permutation_not_a_range():
+    """with steps [9, 5, 7] and phantom rows, layer 1 (descending steps) puts video 0 first, so
+    last_sel = [16, 18, 17, 19..31] -- first/last/length look contiguous but the order is not video-major.  The
+    row selection must then gather, and contiguous_range must say so."""
+    from pdvc.pdvc import contiguous_range
+    counts, Ld, N, Q = [1, 1, 1], 2, 3, 10
+    lay = caption_layout(counts, Ld, N, Q, [1, 0], rows_cap=16, events_cap=1, steps=[9, 5, 7])
+    sel = lay["last_sel"].tolist()
+    assert sel[:3] == [16, 18, 17] and sel[3:] == list(range(19, 32))
+    assert sel[-1] - sel[0] + 1 == len(sel)  # the old test's condition holds ...
+    assert contiguous_range(sel) is None  # ... but the rows are not in order
+    # the gathered rows are video-major: row sel[i] of the layout belongs to video i for the real rows
+    vids = lay["vid"][sel[:3]].tolist()
+    assert vids == [0, 1, 2]
+    assert contiguous_range(list(range(5, 9))) == (5, 4) and contiguous_range([]) is None
+
+
+def test_alive_capacity_must_be_non_increasing():
+    """CaptionDecodeFunction needs each step's rows nested in the previous step's."""
+    from pdvc.batch_layout import step_ranges
+    dt = {"cap_tensor": torch.tensor([[1, 5, 6, 0], [1, 7, 0, 0]]), "cap_mask": torch.tensor([[1, 1, 1, 0],
+                                                                                               [1, 1, 0, 0]]),
+          "video_target": [{"labels": torch.zeros(1)}, {"labels": torch.zeros(1)}]}
+    with pytest.raises(ValueError, match="non-increasing"):
+        pad_to_capacity(dt, events=2, rows=4, words=4, alive=(2, 3, 1))
+    out = pad_to_capacity(dt, events=2, rows=4, words=4, alive=(3, 2, 1))
+    assert out["capacity"]["alive"] == (3, 2, 1)
+    with pytest.raises(ValueError, match="non-increasing"):
+        step_ranges([2, 4, 1], 2, 8)
+    assert step_ranges([4, 2, 0], 2, 8) == ((4, 8), (6, 4), (8, 0))

@@ -1,0 +1,130 @@
+"""pdvc_gemm3_f32 (fp32 GEMM by exact three-term bf16 split, csrc/gemm3.hip) against hipBLASLt fp32 (torch) on the
+encoder's nn.Linear shapes: forward (x W^T + b), data gradient (dy W) and weight gradient (dy^T x over all rows).
+Prints TF/s (algorithmic fp32 flops) and the error of both against float64 (max |c - ref| / sum_k |a||b|, and
+relative to max |ref|).
+
+    python tools/gemm3_bench.py [--rows 983040] [--iters 10]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "dense-video-captioning_amd"))
+from pdvc import _native as _n  # noqa: E402
+
+
+def gemm3(M, N, K, A, lda, akc, B, ldb, bkc, C, ldc, bias=None, epi=0, splits=1, ws=None):
+    _n.call("pdvc_gemm3_f32", M, N, K, _n.ptr_any(A), lda, akc, _n.ptr_any(B), ldb, bkc, _n.ptr_any(C), ldc,
+            _n.ptr(bias), epi, splits, None if ws is None else _n.ptr_any(ws), _n.stream())
+
+
+def gemm3p(M, N, K, A, lda, B, ldb, bkc, planes, C, ldc, bias=None, epi=0):
+    _n.call("pdvc_split3_planes_f32", _n.ptr_any(B), ldb, bkc, N, K, _n.ptr_any(planes), _n.stream())
+    _n.call("pdvc_gemm3p_f32", M, N, K, _n.ptr_any(A), lda, _n.ptr_any(planes), _n.ptr_any(C), ldc, _n.ptr(bias), epi,
+            _n.stream())
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def err(c, ref, scale):
+    d = (c.double() - ref).abs()
+    return {"max_rel_sum": float((d / scale.clamp_min(1e-300)).max()), "max_rel_ref": float(d.max() / ref.abs().max())}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=983040)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--splits", type=int, default=64)
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--only", default="", help="comma list of ops (fwd,dgrad,wgrad); empty = all")
+    ap.add_argument("--shapes", default="512x512,256x512,512x256", help="OxI list")
+    ap.add_argument("--no-err", action="store_true")
+    a = ap.parse_args()
+    torch.manual_seed(0)
+    dev = "cuda"
+    M = a.rows
+    res = []
+    only = set(a.only.split(",")) if a.only else {"fwd", "dgrad", "wgrad", "fwdp", "dgradp"}
+    ref_lib = os.environ.get("PDVC_GEMM3_NO_BLASLT") is None
+
+    def run(op, Mo, No, Ko, ours, blaslt, check):
+        fl = 2.0 * Mo * No * Ko
+        r = {"op": op, "M": Mo, "N": No, "K": Ko}
+        r["ours_ms"] = timeit(ours, a.iters)
+        r["ours_tfs"] = fl / r["ours_ms"] / 1e9
+        if ref_lib:
+            r["blaslt_ms"] = timeit(blaslt, a.iters)
+            r["blaslt_tfs"] = fl / r["blaslt_ms"] / 1e9
+        if not a.no_err:
+            r["err_ours"], r["err_blaslt"] = check()
+        res.append(r)
+        print(json.dumps(r), flush=True)
+
+    for (O, I) in [tuple(int(v) for v in sh.split("x")) for sh in a.shapes.split(",")]:
+        x = torch.randn(M, I, device=dev)
+        W = torch.randn(O, I, device=dev) / I ** 0.5
+        b = torch.randn(O, device=dev)
+        dy = torch.randn(M, O, device=dev)
+        y = torch.empty(M, O, device=dev)
+        dx = torch.empty(M, I, device=dev)
+        dW = torch.empty(O, I, device=dev)
+        ws = torch.empty(a.splits * O * I, device=dev)
+        planes = torch.empty(3 * O * I, dtype=torch.int16, device=dev)
+        sub = 4096
+        s = 64
+
+        def chk_fwd():
+            ref = torch.addmm(b.double(), x[:sub].double(), W.double().t())
+            scale = x[:sub].double().abs() @ W.double().abs().t() + b.double().abs()
+            return err(y[:sub], ref, scale), err(torch.addmm(b, x[:sub], W.t()), ref, scale)
+
+        def chk_dgrad():
+            ref = dy[:sub].double() @ W.double()
+            scale = dy[:sub].double().abs() @ W.double().abs()
+            return err(dx[:sub], ref, scale), err(torch.mm(dy[:sub], W), ref, scale)
+
+        def chk_wgrad():
+            ref = dy.double().t() @ x.double()
+            scale = dy.double().abs().t() @ x.double().abs()
+            theirs = torch.bmm(dy.view(s, M // s, O).transpose(1, 2), x.view(s, M // s, I)).sum(0)
+            return err(dW, ref, scale), err(theirs, ref, scale)
+
+        if "fwd" in only:  # y = x W^T + b
+            run("fwd", M, O, I, lambda: gemm3(M, O, I, x, I, 1, W, I, 1, y, O, b, 1),
+                lambda: torch.addmm(b, x, W.t()), chk_fwd)
+        if "dgrad" in only:  # dx = dy W
+            run("dgrad", M, I, O, lambda: gemm3(M, I, O, dy, O, 1, W, I, 0, dx, I), lambda: torch.mm(dy, W), chk_dgrad)
+        if "fwdp" in only:  # the same with W split once into bf16 planes
+            run("fwdp", M, O, I, lambda: gemm3p(M, O, I, x, I, W, I, 1, planes, y, O, b, 1),
+                lambda: torch.addmm(b, x, W.t()), chk_fwd)
+        if "dgradp" in only:
+            run("dgradp", M, I, O, lambda: gemm3p(M, I, O, dy, O, W, I, 0, planes, dx, I), lambda: torch.mm(dy, W),
+                chk_dgrad)
+        if "wgrad" in only:  # dW = dy^T x over all rows, split
+            run("wgrad", O, I, M, lambda: gemm3(O, I, M, dy, O, 0, x, I, 0, dW, I, None, 0, a.splits, ws),
+                lambda: torch.bmm(dy.view(s, M // s, O).transpose(1, 2), x.view(s, M // s, I)).sum(0), chk_wgrad)
+        del x, W, b, dy, y, dx, dW, ws, planes
+        torch.cuda.empty_cache()
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
