@@ -459,25 +459,30 @@ def launch_ranks(a, script=None, argv=None):
                                       stdout=None if r == 0 else subprocess.DEVNULL))
     log(f"launched {a.gpus} rank processes (pids {[p.pid for p in procs]}), master port {port}")
     status = 0
-    live = list(procs)
+    live = {p.pid: p for p in procs}
+    deadline = None  # set once a rank failed: the others get 20 s after SIGTERM, then SIGKILL
     while live:
-        time.sleep(0.5)
-        for p in list(live):
-            rc = p.poll()
-            if rc is None:
-                continue
-            live.remove(p)
-            if rc != 0 and status == 0:
-                status = rc if rc > 0 else 1
-                log(f"rank pid {p.pid} exited with {rc}: stopping the other ranks")
-                for q in live:
-                    q.terminate()
-                deadline = time.time() + 20
-                for q in live:
-                    try:
-                        q.wait(timeout=max(1.0, deadline - time.time()))
-                    except subprocess.TimeoutExpired:
-                        q.kill()
+        # reap in exit order (os.waitpid on any child): the FIRST failing rank's status is the job's, not that of a
+        # peer that then lost its collective connection and exited in the same instant
+        pid, wst = os.waitpid(-1, 0 if deadline is None else os.WNOHANG)
+        if pid == 0:  # (WNOHANG) nobody exited yet
+            if time.time() > deadline:
+                for q in live.values():
+                    q.kill()
+                deadline = float("inf")
+            time.sleep(0.1)
+            continue
+        p = live.pop(pid, None)
+        if p is None:
+            continue
+        rc = os.waitstatus_to_exitcode(wst)
+        p.returncode = rc
+        if rc != 0 and status == 0:
+            status = rc if rc > 0 else 1
+            log(f"rank pid {pid} exited with {rc}: stopping the other ranks")
+            for q in live.values():
+                q.terminate()
+            deadline = time.time() + 20
     return status
 
 

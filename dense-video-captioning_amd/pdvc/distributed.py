@@ -70,16 +70,24 @@ class GradAllReducer:
         for h in self._hooks:
             h.remove()
         self._hooks = []
-        self.buckets, cur, size = [], [], 0
+        # buckets by (dtype, device) -- a bucket's flat buffer has one dtype -- each filled in reverse registration
+        # order up to bucket_bytes; the kinds in order of first appearance, so every rank builds the same sequence
+        self.buckets = []
+        open_ = {}  # (dtype, device) -> [params, bytes]
         for p in reversed(params):
+            key = (p.dtype, p.device)
             nbytes = p.numel() * p.element_size()
-            if cur and size + nbytes > self.bucket_bytes:
-                self.buckets.append(cur)
-                cur, size = [], 0
-            cur.append(p)
-            size += nbytes
-        if cur:
-            self.buckets.append(cur)
+            cur = open_.get(key)
+            if cur is not None and cur[0] and cur[1] + nbytes > self.bucket_bytes:
+                self.buckets.append(cur[0])
+                cur = None
+            if cur is None:
+                cur = open_[key] = [[], 0]
+            cur[0].append(p)
+            cur[1] += nbytes
+        for cur in open_.values():
+            if cur[0]:
+                self.buckets.append(cur[0])
         self.bucket_of = {}
         for bi, b in enumerate(self.buckets):
             for p in b:
@@ -121,6 +129,9 @@ class GradAllReducer:
         for p in self.active:
             if not self._resident(p):
                 p.grad = self.views[id(p)]
+        for p in self.params:  # outside the active set (no gradient on the first step): never reduced, so never
+            if id(p) not in self.bucket_of:  # left to accumulate across steps either
+                p.grad = None
 
     def _on_grad(self, p):
         bi = self.bucket_of.get(id(p))

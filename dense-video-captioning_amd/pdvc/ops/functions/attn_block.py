@@ -16,6 +16,7 @@ from torch.autograd.function import once_differentiable
 
 from pdvc import _native as _n
 from .addnorm import BWD_PARTS, an_backward, an_forward
+from .gemm3 import addmm_nt, mm_dgrad
 from .linear import colsum, wgrad_mm
 from .ms_deform_attn_func import NUM_SAMPLES, msda1d_backward, msda1d_forward
 from .posembed import LevelPos, level_row_sums
@@ -29,13 +30,13 @@ class EncoderAttnBlockFunction(Function):
         D = d // M
         src2 = src.reshape(R, d).contiguous()
         q = pos.add_to(src2) if isinstance(pos, LevelPos) else src2 + pos.reshape(R, d)
-        value = torch.addmm(bv, src2, Wv.t())
-        proj = torch.addmm(bq, q, Wq.t())
+        value = addmm_nt(bv, src2, Wv)
+        proj = addmm_nt(bq, q, Wq)
         nq = M * NUM_SAMPLES
         ref = ref.contiguous()
         out, save_attn, save_loc = msda1d_forward(value.view(N, S, M, D), pad_mask, proj.view(N, S, -1), ref,
                                                   level_T, 0, nq)
-        s2 = torch.addmm(bo, out.view(R, d), Wo.t())
+        s2 = addmm_nt(bo, out.view(R, d), Wo)
         y = torch.empty_like(src2)
         mean = torch.empty(R, dtype=src.dtype, device=src.device)
         rstd = torch.empty_like(mean)
@@ -64,7 +65,7 @@ class EncoderAttnBlockFunction(Function):
         ws = torch.empty(3 * BWD_PARTS * d, dtype=src2.dtype, device=src2.device)
         an_backward(src2, s2, gamma, mean, rstd, dy2, p, seed_int, seed_dev, d_src, d_s2, dgamma, dbeta, dbo, ws)
         dWo = wgrad_mm(d_s2, out.view(R, d))
-        d_out = torch.mm(d_s2, Wo)
+        d_out = mm_dgrad(d_s2, Wo)
         nq = M * NUM_SAMPLES
         gv, gp, _, vsums = msda1d_backward(value.view(N, S, M, D), pad_mask, proj.view(N, S, -1), ref, save_attn,
                                            save_loc, out, d_out.view(N, S, d), level_T, 0, nq,
@@ -79,14 +80,14 @@ class EncoderAttnBlockFunction(Function):
         d_pos = d_handle = None
         if has_handle:
             d_handle = torch.matmul(level_row_sums(gp.view(N, S, -1), level_T), Wq)
-            d_src.addmm_(gp2, Wq)
+            mm_dgrad(gp2, Wq, out=d_src)
         elif ctx.needs_input_grad[1]:
-            d_q = torch.mm(gp2, Wq)
+            d_q = mm_dgrad(gp2, Wq)
             d_pos = d_q.view(N, S, d)
             d_src.add_(d_q)
         else:
-            d_src.addmm_(gp2, Wq)
-        d_src.addmm_(gv2, Wv)  # residual + value path + query path, accumulated in the GEMM epilogues
+            mm_dgrad(gp2, Wq, out=d_src)
+        mm_dgrad(gv2, Wv, out=d_src)  # residual + value path + query path, accumulated in the GEMM epilogues
         return (d_src.view(N, S, d), d_pos, d_handle, None, None, dWv, dbv, dWq, dbq, dWo, dbo, dgamma, dbeta,
                 None, None, None, None, None)
 

@@ -13,6 +13,7 @@ from torch.autograd import Function
 from torch.autograd.function import once_differentiable
 
 from pdvc import _native as _n
+from .gemm3 import addmm_nt, mm_dgrad, mm_nt
 from .linear import colsum, dense, wgrad_mm
 
 GN_ROWS = 64  # rows per stats chunk (csrc/groupnorm.hip kGnRows)
@@ -34,8 +35,8 @@ class ConvS2RowsFunction(Function):
         X2 = x.view(N * L, 2 * C)
         w12 = torch.cat([weight[:, :, 1], weight[:, :, 2]], 1)  # (O, 2C): taps on x[2t], x[2t+1]
         w0 = weight[:, :, 0].contiguous()                       # (O, C): tap on x[2t-1]
-        y = torch.addmm(bias, X2, w12.t())
-        z = torch.mm(X2[:, C:], w0.t())                         # x[2t+1] W0^T feeds output row t+1
+        y = addmm_nt(bias, X2, w12)
+        z = mm_nt(X2[:, C:], w0)                         # x[2t+1] W0^T feeds output row t+1
         yv = y.view(N, L, O)
         yv[:, 1:] += z.view(N, L, O)[:, :-1]
         ctx.save_for_backward(X2, w12, w0)
@@ -53,8 +54,8 @@ class ConvS2RowsFunction(Function):
         dz2 = dz.view(N * L, O)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            dX2 = torch.mm(dy2, w12)
-            dX2[:, C:] += torch.mm(dz2, w0)
+            dX2 = mm_dgrad(dy2, w12)
+            mm_dgrad(dz2, w0, out=dX2[:, C:])
             gx = dX2.view(N, T, C)[:, :Tin]
         if ctx.needs_input_grad[1]:
             g12 = wgrad_mm(dy2, X2)

@@ -21,6 +21,7 @@ from pdvc import _native as _n
 from pdvc.precision import attach_bf16, shadow_for
 from .addnorm import BWD_PARTS, an_backward, an_forward
 from . import linear as _lin
+from .gemm3 import addmm_nt, mm_dgrad
 from .linear import CU, wgrad_mm
 
 
@@ -45,7 +46,7 @@ class FFNBlockFunction(Function):
         x2 = x.reshape(-1, d).contiguous()
         rows = x2.shape[0]
         seed_act, seed_out = _seed_ptrs(seeds)
-        h = torch.addmm(b1, x2, w1.t())
+        h = addmm_nt(b1, x2, w1)
         h16 = shadow_for(h)  # bf16 mode: linear2's operand written by the same pass
         if h16 is None:
             _n.call("pdvc_relu_dropout_forward_f32", _n.ptr(h), rows, h.shape[1], float(p_act), 0, seed_act,
@@ -54,7 +55,7 @@ class FFNBlockFunction(Function):
             _n.call("pdvc_relu_dropout_forward_f32_bf16out", _n.ptr(h), rows, h.shape[1], float(p_act), 0, seed_act,
                     _n.ptr(h16), _n.stream())
             attach_bf16(h, h16)
-        y = torch.addmm(b2, h, w2.t())
+        y = addmm_nt(b2, h, w2)
         out = torch.empty_like(x2)
         mean = torch.empty(rows, dtype=x.dtype, device=x.device)
         rstd = torch.empty_like(mean)
@@ -80,7 +81,7 @@ class FFNBlockFunction(Function):
         db2 = torch.empty_like(gamma)  # linear2's bias gradient = column sums of dy, summed by the same pass
         an_backward(x2, y, gamma, mean, rstd, dout2, p_out, 0, seed_out, dx, dy, dgamma, dbeta, db2, ws)
         dw2 = wgrad_mm(dy, h)
-        dh = torch.mm(dy, w2)
+        dh = mm_dgrad(dy, w2)
         parts = _parts(rows, fdim)
         ws1 = torch.empty(parts * fdim, dtype=h.dtype, device=h.device)
         db1 = torch.empty(fdim, dtype=h.dtype, device=h.device)
@@ -93,7 +94,7 @@ class FFNBlockFunction(Function):
                     _n.ptr(ws1), _n.ptr(db1), _n.ptr(dh16), _n.stream())
             attach_bf16(dh, dh16)
         dw1 = wgrad_mm(dh, x2)
-        dx.addmm_(dh, w1)  # residual gradient + linear1's input gradient in one GEMM (beta = 1)
+        mm_dgrad(dh, w1, out=dx)  # residual gradient + linear1's input gradient in one GEMM (beta = 1)
         return dx.view(shape), dw1, db1, dw2, db2, dgamma, dbeta, None, None, None, None
 
 

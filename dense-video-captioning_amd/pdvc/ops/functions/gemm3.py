@@ -1,0 +1,124 @@
+"""fp32 products of PDVC's large nn.Linear layers on the bf16 matrix cores (csrc/gemm3.hip, pdvc_gemm3*_f32).
+
+gfx950 has no xf32, and its f32-input MFMA runs at 1/16 of the bf16 rate.  pdvc_gemm3 splits each fp32 operand
+exactly into three bf16 terms and keeps the six products of order >= 2^-16 (the dropped ones are <= 2^-23 |a||b|,
+one fp32 product rounding is 2^-24), accumulating in fp32: an fp32 GEMM whose error against float64 is at or below
+hipBLASLt's fp32 GEMM on the same operands (tests/test_gpu_gemm3.py measures both), at up to ~1.8x its rate.
+
+These helpers are drop-in for the torch calls of the projections (pdvc/ops/modules/ms_deform_attn.py:55-58,
+deformable_transformer.py:162-189 in the reference -- torch.addmm / mm in the forward, and the input- and
+weight-gradient products of their backward), with the same argument meaning:
+
+    addmm_nt(bias, x, W, relu=False)  = torch.addmm(bias, x, W.t())  (+ ReLU)
+    mm_nt(x, W)                       = x @ W.t()
+    mm_dgrad(dy, W, out=None)         = dy @ W; out given: out += dy @ W  (out.addmm_(dy, W))
+    mm_wgrad(gy, x, out=None)         = gy.t() @ x, the reduction over all rows split over workgroups
+
+Shapes the kernels do not take (K not a multiple of 32, unaligned or strided operands, few rows) and the bf16 mode
+(pdvc/precision.py, which reroutes torch's GEMMs to bf16 operands) go to torch, i.e. hipBLASLt -- a GPU library
+path, never a CPU one.  PDVC_GEMM3=0 sends everything to torch (the A/B switch).
+"""
+import os
+
+import torch
+
+from pdvc import _native as _n
+
+ENABLED = os.environ.get("PDVC_GEMM3", "1") != "0"
+MIN_ROWS = int(os.environ.get("PDVC_GEMM3_MIN_ROWS", "8192"))  # below: launch-bound shapes stay on hipBLASLt
+CALLS = {"gemm3": 0, "torch": 0}  # how many products took each path (tests check the encoder takes gemm3)
+
+
+def _bf16_mode():
+    from pdvc.precision import bf16_active
+    return bf16_active()
+
+
+def _rows_ok(t):
+    """A 2-D fp32 GPU operand with unit column stride, 16-byte aligned rows."""
+    return (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 4 == 0
+            and t.data_ptr() % 16 == 0 and t.stride(0) >= t.shape[1])
+
+
+def _use(M, K, *ops):
+    if not ENABLED or M < MIN_ROWS or K % 32 != 0 or not all(_rows_ok(t) for t in ops) or _bf16_mode():
+        CALLS["torch"] += 1
+        return False
+    CALLS["gemm3"] += 1
+    return True
+
+
+def split_planes(B, b_kc, N, K):
+    """The three bf16 planes [3][N][K] of opB[n][k] (b_kc 1: B[n][k]; 0: B[k][n], i.e. opB = B^T)."""
+    planes = torch.empty((3, N, K), dtype=torch.int16, device=B.device)
+    _n.call("pdvc_split3_planes_f32", _n.ptr_any(B), B.stride(0), int(b_kc), N, K, _n.ptr(planes), _n.stream())
+    return planes
+
+
+def _gemm3p(a, planes, N, out, bias, epi):
+    M, K = a.shape
+    _n.call("pdvc_gemm3p_f32", M, N, K, _n.ptr_any(a), a.stride(0), _n.ptr(planes), _n.ptr_any(out), out.stride(0),
+            _n.ptr(bias), epi, _n.stream())
+    return out
+
+
+def addmm_nt(bias, x, W, relu=False):
+    """torch.addmm(bias, x, W.t()) (bias may be None), + ReLU when relu=True."""
+    M, K = x.shape
+    N = W.shape[0]
+    if not _use(M, K, x, W) or not W.is_contiguous() or (bias is not None and not bias.is_contiguous()):
+        if bias is None:
+            y = torch.mm(x, W.t())
+            return y.relu_() if relu else y
+        if relu:
+            return torch._addmm_activation(bias, x, W.t(), use_gelu=False)
+        return torch.addmm(bias, x, W.t())
+    out = torch.empty((M, N), dtype=torch.float32, device=x.device)
+    epi = 0 if bias is None else (2 if relu else 1)
+    if bias is None and relu:
+        _gemm3p(x, split_planes(W, 1, N, K), N, out, None, 0)
+        return out.relu_()
+    return _gemm3p(x, split_planes(W, 1, N, K), N, out, bias, epi)
+
+
+def mm_nt(x, W):
+    return addmm_nt(None, x, W)
+
+
+def mm_dgrad(dy, W, out=None):
+    """dy @ W for dy (M, O) and W (O, I): the input gradient of y = x W^T.  out given (M, I): out += dy @ W."""
+    M, K = dy.shape
+    N = W.shape[1]
+    ok = _use(M, K, dy, W) and W.is_contiguous() and (out is None or (_rows_ok(out) and out.shape == (M, N)))
+    if not ok:
+        return torch.mm(dy, W) if out is None else out.addmm_(dy, W)
+    planes = split_planes(W, 0, N, K)
+    if out is None:
+        return _gemm3p(dy, planes, N, torch.empty((M, N), dtype=torch.float32, device=dy.device), None, 0)
+    return _gemm3p(dy, planes, N, out, None, 3)
+
+
+def wgrad_splits(rows, tiles):
+    """Row chunks of a weight gradient's reduction: about two workgroups per CU over the output tiles, chunks of
+    at least 2048 rows (64 stages)."""
+    want = max(1, (512 + tiles - 1) // tiles)
+    return max(1, min(want, rows // 2048, 1024))
+
+
+def mm_wgrad(gy, x, out=None):
+    """gy^T x for gy (rows, O) and x (rows, I): the weight gradient of y = x W^T, deterministic (row chunks summed
+    in a fixed order).  out: a contiguous (O, I) destination (written, not accumulated)."""
+    rows, O = gy.shape
+    I = x.shape[1]
+    ok = (_use(rows, 32, gy, x) and O % 4 == 0 and I % 4 == 0 and rows % 32 == 0
+          and (out is None or (out.is_contiguous() and out.shape == (O, I))))
+    if not ok:
+        return None
+    if out is None:
+        out = torch.empty((O, I), dtype=torch.float32, device=gy.device)
+    tiles = ((O + 255) // 256) * ((I + 127) // 128)
+    splits = wgrad_splits(rows, tiles)
+    ws = torch.empty(splits * O * I if splits > 1 else 0, dtype=torch.float32, device=gy.device)
+    _n.call("pdvc_gemm3_f32", O, I, rows, _n.ptr_any(gy), gy.stride(0), 0, _n.ptr_any(x), x.stride(0), 0,
+            _n.ptr_any(out), I, None, 0, splits, _n.ptr(ws) if splits > 1 else None, _n.stream())
+    return out

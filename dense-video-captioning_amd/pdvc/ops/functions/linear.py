@@ -11,6 +11,7 @@ import torch.nn.functional as F
 from torch.autograd import Function
 
 from pdvc import _native as _n
+from .gemm3 import addmm_nt, mm_dgrad
 
 CU = 256  # MI355X compute units
 # "hip": the projections run on pdvc_gemm_f32; "torch": F.linear (hipBLASLt) -- an A/B switch for bench.py
@@ -153,6 +154,10 @@ def wgrad_mm(gy, x, out=None):
     if gy.shape[1] == 1:  # a 1-wide layer: a weighted column sum, not an (M = 1) GEMM (~1 TB/s on hipBLASLt)
         r = colsum((x * gy).contiguous()).view(1, -1)
         return r if out is None else out.copy_(r)
+    from .gemm3 import mm_wgrad
+    r = mm_wgrad(gy, x, out)  # fp32 on the bf16 matrix cores when the shape allows it
+    if r is not None:
+        return r
     s = wgrad_splits(rows)
     if s == 1:
         return torch.mm(gy.t(), x) if out is None else torch.mm(gy.t(), x, out=out)
@@ -210,9 +215,9 @@ class TorchLinearFunction(Function):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
         if relu and bias is not None and _RELU_EPILOGUE:
-            y = torch._addmm_activation(bias, x2, weight.t(), use_gelu=False)  # ReLU in the GEMM epilogue
+            y = addmm_nt(bias, x2, weight, relu=True)  # ReLU in the GEMM epilogue
         else:
-            y = torch.addmm(bias, x2, weight.t()) if bias is not None else torch.mm(x2, weight.t())
+            y = addmm_nt(bias, x2, weight)
             if relu:
                 y.relu_()
         ctx.save_for_backward(x2, weight, y if relu else None)
@@ -228,7 +233,7 @@ class TorchLinearFunction(Function):
             gy2 = torch.ops.aten.threshold_backward(gy2, y, 0.0)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = torch.mm(gy2, weight).view(*gy.shape[:-1], weight.shape[1])
+            gx = mm_dgrad(gy2, weight).view(*gy.shape[:-1], weight.shape[1])
         if ctx.needs_input_grad[1]:
             gw = wgrad_mm(gy2, x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
@@ -261,7 +266,7 @@ class MultiLinearFunction(Function):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
         ws, bs = wb[0::2], wb[1::2]
-        outs = tuple(torch.addmm(b, x2, w.t()).view(*shape[:-1], w.shape[0]) for w, b in zip(ws, bs))
+        outs = tuple(addmm_nt(b, x2, w).view(*shape[:-1], w.shape[0]) for w, b in zip(ws, bs))
         ctx.save_for_backward(x2, *ws)
         ctx.shape = shape
         return outs
@@ -277,9 +282,9 @@ class MultiLinearFunction(Function):
                 continue
             g2 = g.reshape(-1, w.shape[0]).contiguous()
             if gx is None:
-                gx = torch.mm(g2, w)
+                gx = mm_dgrad(g2, w)
             else:
-                gx.addmm_(g2, w)
+                mm_dgrad(g2, w, out=gx)
             # a fused deformable-attention consumer hands its value gradient over with per-(video, level) row sums
             # (MSDA1dFunction): the bias gradient from those instead of another pass over g
             ls = level_sums_of(g)

@@ -554,9 +554,18 @@ int pdvc_gemm_f32(int M, int N, int K, const float* A, int lda, int trans_a, con
  * accumulation: the dropped terms are <= 2^-23 |a||b| per product (one fp32 product rounding is 2^-24).
  * epilogue 0 store, 1 + bias, 2 + bias then ReLU, 3 accumulate into C.  splits > 1 splits K over workgroups
  * into `workspace` (splits * M * N floats, epilogues 0/3 only) and sums the slabs deterministically.
- * Operands 16-byte aligned, leading dimensions and contiguous extents divisible by 4. */
+ * K a multiple of 32; operands 16-byte aligned, leading dimensions divisible by 4, an mn-contiguous operand's
+ * extent (M or N) divisible by 4. */
 int pdvc_gemm3_f32(int M, int N, int K, const float* A, long lda, int a_kc, const float* B, long ldb, int b_kc,
                    float* C, long ldc, const float* bias, int epilogue, int splits, float* workspace, void* stream);
+
+/* The weight operand split once per call: planes[p][n][k] (bf16 bits, p = 0..2) of opB[n][k] (b_kc 1: B[n*ldb + k],
+ * 0: B[k*ldb + n]); K a multiple of 32.  pdvc_gemm3p_f32 then computes C[M,N] (=|+=) sum_k A[m*lda + k] opB[n,k]
+ * (+ bias) (ReLU) -- epilogues as pdvc_gemm3_f32 -- with the planes streamed into LDS by LDS-DMA, so that only A is
+ * split inside the kernel (the forward x W^T and the data gradient dy W of nn.Linear). */
+int pdvc_split3_planes_f32(const float* B, long ldb, int b_kc, int N, int K, uint16_t* planes, void* stream);
+int pdvc_gemm3p_f32(int M, int N, int K, const float* A, long lda, const uint16_t* planes, float* C, long ldc,
+                    const float* bias, int epilogue, void* stream);
 
 #ifdef __cplusplus
 }

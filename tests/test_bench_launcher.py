@@ -46,3 +46,23 @@ def test_bench_refuses_world_size_mismatch():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0
     assert "initialised world size is 1" in r.stderr
+
+
+def test_launcher_starts_world_of_eight_ranks(capfd):
+    """The 8-GPU node's world (the driver's SCALE run), rehearsed with 8 gloo rank processes on the CPU."""
+    b = _bench()
+    a = types.SimpleNamespace(gpus=8, same_device=True)
+    rc = b.launch_ranks(a, script=PROBE, argv=[])
+    out = capfd.readouterr().out.strip().splitlines()
+    assert rc == 0
+    line = json.loads(out[-1])
+    assert line == {"world": 8, "sum_of_ranks": 28.0, "local_rank": 0, "master_addr": "127.0.0.1"}
+    assert sum(l.startswith("{") for l in out) == 1
+
+
+def test_launcher_stops_seven_ranks_when_one_fails(capfd):
+    b = _bench()
+    a = types.SimpleNamespace(gpus=8, same_device=True)
+    rc = b.launch_ranks(a, script=PROBE, argv=["--fail-rank", "5"])
+    capfd.readouterr()
+    assert rc == 3

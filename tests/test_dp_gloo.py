@@ -1,9 +1,11 @@
-"""CPU, world_size 2 over gloo: the data-parallel gradient all-reducer (pdvc/distributed.py) gives every rank
+"""CPU, world_size 2 and 8 over gloo: the data-parallel gradient all-reducer (pdvc/distributed.py) gives every rank
 the mean of the per-rank gradients, keeps never-used parameters at grad None (as the reference's 8 unused
 PDVC parameters), overlaps buckets with backward (several buckets in flight), survives repeated steps, builds
 the same bucket order on every rank, keeps the gradients resident in the buckets when steps zero through
 GradAllReducer.zero_grad() (nothing copied; a set-to-None step still reduces correctly), and treats a gradient missing on one rank in a later step (a branch not
-taken there) as zeros -- both ranks still issue identical collectives and receive the mean."""
+taken there) as zeros -- every rank still issues identical collectives and receives the mean.  Round 5:
+a float64 parameter gets a bucket of its own dtype, and a parameter first used after the first step (outside the
+active set, never reduced) does not accumulate across zero_grad() steps."""
 import os
 import socket
 
@@ -29,12 +31,16 @@ class Toy(torch.nn.Module):
         self.unused = torch.nn.Linear(8, 8)  # never touched by forward
         self.shared = torch.nn.Linear(8, 8)
         self.branch = torch.nn.Linear(8, 8)  # used on every step except rank 1's second
+        self.scale = torch.nn.Parameter(torch.linspace(0.5, 1.5, 8, dtype=torch.float64))  # a float64 bucket
+        self.late = torch.nn.Linear(8, 8)  # first used on step 1: outside the active set, never reduced
 
-    def forward(self, x, branch=True):
+    def forward(self, x, branch=True, step=0):
         h = torch.relu(self.a(x))
-        y = self.b(h)
+        y = self.b(h) * self.scale.float()
         if branch:
             y = y + self.branch(y)
+        if step >= 1:
+            y = y + 0.1 * self.late(y)
         return (self.shared(y) + self.shared(y * 0.5)).pow(2).mean()
 
 
@@ -48,7 +54,7 @@ def _grads_single(seed_rank, steps_data):
     out = []
     for step, x in enumerate(steps_data[seed_rank]):
         m.zero_grad(set_to_none=True)
-        m(x, _branch(seed_rank, step)).backward()
+        m(x, _branch(seed_rank, step), step).backward()
         out.append({n: (p.grad.clone() if p.grad is not None else None) for n, p in m.named_parameters()})
     return out
 
@@ -72,7 +78,7 @@ def _worker(rank, world, port, data, q):
         else:
             red.zero_grad()  # bucket-resident: backward accumulates into the flat buffers, nothing copied
         c0 = red.copies
-        m(x, _branch(rank, step)).backward()
+        m(x, _branch(rank, step), step).backward()
         red.finish()
         copies.append(red.copies - c0)
         resident.append(all(red._resident(p) for p in red.active))
@@ -83,10 +89,11 @@ def _worker(rank, world, port, data, q):
     dist.destroy_process_group()
 
 
-def test_grad_allreduce_is_mean_of_ranks():
-    world = 2
+@pytest.mark.parametrize("world", [2, 8])
+def test_grad_allreduce_is_mean_of_ranks(world):
+    steps = 4
     g = torch.Generator().manual_seed(1)
-    data = [[torch.randn(5, 16, generator=g) for _ in range(3)] for _ in range(world)]
+    data = [[torch.randn(5, 16, generator=g) for _ in range(steps)] for _ in range(world)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -95,28 +102,41 @@ def test_grad_allreduce_is_mean_of_ranks():
         p.start()
     results, orders = dict(), dict()
     for _ in range(world):
-        r, res, buckets, copies, resident = q.get(timeout=120)
+        r, res, buckets, copies, resident = q.get(timeout=300)
         results[r] = res
         orders[r] = buckets
         assert len(buckets) >= 2
         assert all(resident), "after finish() every active gradient views its bucket"
-        # the resident step copies nothing; a set-to-None step copies every gradient it produced
-        assert copies[1] == 0 and copies[2] > 0, copies
-    assert orders[0] == orders[1], "bucket order differs between ranks"
-    assert not any(n.startswith("unused") for b in orders[0] for n in b)
+        # the resident steps copy nothing; a set-to-None step copies every gradient it produced
+        assert copies[1] == 0 and copies[2] == 0 and copies[3] > 0, copies
+    for r in range(1, world):
+        assert orders[r] == orders[0], f"bucket order differs between ranks 0 and {r}"
+    assert not any(n.startswith("unused") or n.startswith("late") for b in orders[0] for n in b)
+    assert any(b == ["scale"] for b in orders[0]), "the float64 parameter must have a bucket of its own dtype"
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     singles = [_grads_single(r, data) for r in range(world)]
-    for step in range(3):
+    for step in range(steps):
         for name in results[0][step]:
             if name.startswith("unused"):
-                assert results[0][step][name] is None and results[1][step][name] is None
+                assert all(results[r][step][name] is None for r in range(world))
                 continue
-            g0, g1 = singles[0][step][name], singles[1][step][name]
-            if g1 is None:  # rank 1 skipped the branch on this step: it contributes zeros
-                assert name.startswith("branch") and step == 1
-                g1 = torch.zeros_like(g0)
-            expect = (g0 + g1) / 2
+            if name.startswith("late"):  # never reduced: each rank's own gradient of this step, not accumulated
+                for r in range(world):
+                    if step == 0:
+                        assert results[r][step][name] is None
+                    else:
+                        torch.testing.assert_close(torch.from_numpy(results[r][step][name]), singles[r][step][name],
+                                                   rtol=1e-6, atol=1e-7)
+                continue
+            gs = []
+            for r in range(world):
+                gr = singles[r][step][name]
+                if gr is None:  # rank 1 skipped the branch on this step: it contributes zeros
+                    assert name.startswith("branch") and step == 1 and r == 1
+                    gr = torch.zeros_like(singles[0][step][name])
+                gs.append(gr)
+            expect = sum(gs) / world
             for r in range(world):
                 torch.testing.assert_close(torch.from_numpy(results[r][step][name]), expect, rtol=1e-6, atol=1e-7)

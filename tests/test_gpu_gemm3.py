@@ -1,0 +1,193 @@
+"""GPU: the fp32 GEMM on the bf16 matrix cores (csrc/gemm3.hip, pdvc/ops/functions/gemm3.py).
+
+Each fp32 operand is split exactly into three bf16 terms (x = x0 + x1 + x2) and the six products of order >= 2^-16
+are accumulated in fp32 (the dropped terms are <= 2^-23 |a||b| per product).  The tests check:
+  * the split is exact (the three planes sum to the fp32 value, bit for bit, over 80 binades);
+  * every entry point and layout against float64 -- the per-element error scaled by sum_k |a_k||b_k| below 1e-6 and
+    at most twice hipBLASLt's fp32 error on the same operands (tolerance stated here: the products' own rounding
+    is 2^-24 ~ 6e-8 of that scale; K-deep fp32 accumulation adds ~sqrt(K) of it);
+  * epilogues (bias, ReLU, accumulate), ragged M / N, strided rows, split-K determinism, argument errors;
+  * the encoder nodes and the whole batched training step with every eligible product on gemm3 (MIN_ROWS = 0)
+    against the same references as their hipBLASLt runs (tests/parity.py bound, the reference fixture).
+"""
+import os
+import sys
+
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _lib():
+    from pdvc import _native as _n
+    return _n
+
+
+def scaled_err(c, ref, scale):
+    return float(((c.double() - ref).abs() / scale.clamp_min(1e-300)).max())
+
+
+def gemm3(M, N, K, A, lda, akc, B, ldb, bkc, C, ldc, bias=None, epi=0, splits=1, ws=None):
+    _n = _lib()
+    _n.call("pdvc_gemm3_f32", M, N, K, _n.ptr_any(A), lda, akc, _n.ptr_any(B), ldb, bkc, _n.ptr_any(C), ldc,
+            _n.ptr(bias), epi, splits, None if ws is None else _n.ptr(ws), _n.stream())
+
+
+def op_mat(X, kc, rows, cols):
+    """The logical (rows, cols) operand of a stored matrix: kc -> X is (rows, ld); else X is (cols, ld) transposed."""
+    return X[:rows, :cols] if kc else X[:cols, :rows].t()
+
+
+def test_split_planes_are_exact():
+    from pdvc.ops.functions.gemm3 import split_planes
+    torch.manual_seed(0)
+    N, K = 96, 128
+    W = torch.randn(N, K, device=DEV) * torch.exp2(torch.randint(-40, 40, (N, K), device=DEV).float())
+    for kc in (1, 0):
+        src = W if kc else W.t().contiguous()
+        planes = split_planes(src, kc, N, K)
+        bits = planes.view(3, N, K).cpu().numpy().view("uint16").astype("uint32") << 16
+        vals = torch.from_numpy(bits.view("float32")).double()
+        recon = vals.sum(0)
+        assert torch.equal(recon, W.cpu().double()), "x0 + x1 + x2 must equal x exactly"
+        assert float((vals[1].abs() - vals[0].abs() * 2.0 ** -8).clamp_min(0).max()) == 0.0
+        assert float((vals[2].abs() - vals[0].abs() * 2.0 ** -16).clamp_min(0).max()) == 0.0
+
+
+CASES = [  # (M, N, K, a_kc, b_kc, epi)
+    (4096, 512, 512, 1, 1, 1),
+    (1000, 200, 96, 1, 1, 2),
+    (4100, 512, 256, 1, 0, 0),
+    (300, 64, 1536, 1, 0, 3),
+    (512, 256, 4096, 0, 0, 0),
+    (260, 132, 64, 0, 1, 3),
+]
+
+
+@pytest.mark.parametrize("M,N,K,akc,bkc,epi", CASES)
+def test_gemm3_matches_float64(M, N, K, akc, bkc, epi):
+    torch.manual_seed(M + N + K)
+    lda = (K if akc else M) + 8
+    ldb = (K if bkc else N) + 4
+    A = torch.randn((M if akc else K), lda, device=DEV)
+    B = torch.randn((N if bkc else K), ldb, device=DEV)
+    a, b = op_mat(A, akc, M, K), op_mat(B, bkc, N, K)
+    bias = torch.randn(N, device=DEV)
+    C0 = torch.randn(M, N + 12, device=DEV)
+    C = C0.clone()
+    gemm3(M, N, K, A, lda, akc, B, ldb, bkc, C, N + 12, bias if epi in (1, 2) else None, epi)
+    ref = a.double() @ b.double().t()
+    scale = a.double().abs() @ b.double().abs().t()
+    theirs = a @ b.t()
+    if epi in (1, 2):
+        ref, theirs, scale = ref + bias.double(), theirs + bias, scale + bias.double().abs()
+    if epi == 2:
+        ref, theirs = ref.clamp_min(0), theirs.clamp_min(0)
+    if epi == 3:
+        ref, theirs, scale = ref + C0[:, :N].double(), theirs + C0[:, :N], scale + C0[:, :N].double().abs()
+    ours_e = scaled_err(C[:, :N], ref, scale)
+    blas_e = scaled_err(theirs, ref, scale)
+    assert ours_e < 1e-6 and ours_e <= 2 * blas_e + 1e-8, (ours_e, blas_e)
+    assert torch.equal(C[:, N:], C0[:, N:]), "columns past N must be untouched"
+
+
+@pytest.mark.parametrize("M,N,K,bkc,epi", [(4096, 512, 512, 1, 1), (3000, 200, 96, 1, 2), (2500, 512, 256, 0, 3),
+                                           (700, 100, 64, 0, 0)])
+def test_gemm3p_matches_float64(M, N, K, bkc, epi):
+    from pdvc.ops.functions.gemm3 import split_planes
+    _n = _lib()
+    torch.manual_seed(M + K)
+    A = torch.randn(M, K + 4, device=DEV)
+    Bst = torch.randn((N, K) if bkc else (K, N), device=DEV)
+    b = Bst if bkc else Bst.t()
+    a = A[:, :K]
+    bias = torch.randn(N, device=DEV)
+    C0 = torch.randn(M, N, device=DEV)
+    C = C0.clone()
+    planes = split_planes(Bst, bkc, N, K)
+    _n.call("pdvc_gemm3p_f32", M, N, K, _n.ptr_any(A), K + 4, _n.ptr(planes), _n.ptr(C), N,
+            _n.ptr(bias) if epi in (1, 2) else None, epi, _n.stream())
+    ref = a.double() @ b.double().t()
+    scale = a.double().abs() @ b.double().abs().t()
+    theirs = a @ b.t()
+    if epi in (1, 2):
+        ref, theirs, scale = ref + bias.double(), theirs + bias, scale + bias.double().abs()
+    if epi == 2:
+        ref, theirs = ref.clamp_min(0), theirs.clamp_min(0)
+    if epi == 3:
+        ref, theirs, scale = ref + C0.double(), theirs + C0, scale + C0.double().abs()
+    ours_e = scaled_err(C, ref, scale)
+    blas_e = scaled_err(theirs, ref, scale)
+    assert ours_e < 1e-6 and ours_e <= 2 * blas_e + 1e-8, (ours_e, blas_e)
+
+
+def test_wgrad_split_is_deterministic_and_accurate():
+    from pdvc.ops.functions.gemm3 import mm_wgrad
+    torch.manual_seed(5)
+    rows, O, I = 65536, 256, 512
+    gy = torch.randn(rows, O, device=DEV)
+    x = torch.randn(rows, I + 8, device=DEV)[:, :I]  # strided rows (the base encoder's X2[:, C:] view)
+    import pdvc.ops.functions.gemm3 as G
+    old = G.MIN_ROWS
+    G.MIN_ROWS = 0
+    try:
+        w1 = mm_wgrad(gy, x)
+        w2 = mm_wgrad(gy, x)
+    finally:
+        G.MIN_ROWS = old
+    assert w1 is not None and torch.equal(w1, w2), "split-K weight gradient must be deterministic"
+    ref = gy.double().t() @ x.double()
+    scale = gy.double().abs().t() @ x.double().abs()
+    assert scaled_err(w1, ref, scale) < 1e-6
+
+
+def test_gemm3_argument_errors():
+    _n = _lib()
+    A = torch.randn(64, 48, device=DEV)
+    B = torch.randn(64, 48, device=DEV)
+    C = torch.empty(64, 64, device=DEV)
+    with pytest.raises(_n.NativeError, match="multiple of 32"):
+        gemm3(64, 64, 48, A, 48, 1, B, 48, 1, C, 64)
+    A2 = torch.randn(64 * 64 + 1, device=DEV)[1:].view(64, 64)  # 4-byte aligned, not 16
+    with pytest.raises(_n.NativeError, match="16-byte"):
+        gemm3(64, 64, 64, A2, 64, 1, A2, 64, 1, C, 64)
+    with pytest.raises(_n.NativeError, match="workspace"):
+        gemm3(64, 64, 64, C, 64, 1, C, 64, 1, torch.empty(64, 64, device=DEV), 64, None, 0, 2, None)
+
+
+def _on_gemm3(monkeypatch):
+    import pdvc.ops.functions.gemm3 as G
+    monkeypatch.setattr(G, "MIN_ROWS", 0)
+    monkeypatch.setattr(G, "ENABLED", True)
+    return G
+
+
+def test_ffn_block_on_gemm3(monkeypatch):
+    G = _on_gemm3(monkeypatch)
+    import test_gpu_ffn
+    before = G.CALLS["gemm3"]
+    test_gpu_ffn.test_ffn_block_matches_float64_chain(2048, 128, 512, 0.3)
+    assert G.CALLS["gemm3"] >= before + 6, "the FFN's six products must run on gemm3"
+
+
+def test_encoder_attn_block_on_gemm3(monkeypatch):
+    G = _on_gemm3(monkeypatch)
+    import test_gpu_attn_block
+    before = G.CALLS["gemm3"]
+    test_gpu_attn_block.test_encoder_attn_block_matches_module_chain(512, 8, False, monkeypatch)
+    assert G.CALLS["gemm3"] >= before + 9
+
+
+def test_batched_step_on_gemm3_equals_reference(monkeypatch):
+    """The batched training step of the reference fixture (tests/test_gpu_batch.py) with every eligible product of
+    the model on gemm3: the same per-tensor bound against the reference's batch-1 gradients."""
+    G = _on_gemm3(monkeypatch)
+    import test_gpu_batch as TB
+    before = G.CALLS["gemm3"]
+    TB.test_batched_step_equals_mean_of_reference_batch1_steps(TB.TM.load(TB.NAME))
+    assert G.CALLS["gemm3"] > before + 20
