@@ -8,6 +8,8 @@ import pytest
 
 from oracle import oracle as O
 
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
 G = os.path.join(os.path.dirname(__file__), "golden")
 
 
@@ -116,3 +118,44 @@ def test_cpu_baseline_timer_runs():
     from oracle.torch_core import time_call_set
     t, info = time_call_set(T=32, Q=10, runs=3, warmup=1, threads=2)
     assert t > 0 and info["threads"] == 2 and info["runs"] == 3
+
+
+# ---- the caption head's decode step (oracle/cap_step.py) against the reference captioner's fixtures ----------
+CAP_SHAPES = {  # the reference LSTMDSACaptioner(small_opt) parameters (tests/golden/make_golden.py::module_captioner)
+    "embed.weight": (24, 32), "logit.weight": (24, 64), "logit.bias": (24,),
+    "core.rnn.weight_ih_l0": (256, 160), "core.rnn.weight_hh_l0": (256, 64),
+    "core.deformable_att.sampling_offsets.weight": (16, 128), "core.deformable_att.sampling_offsets.bias": (16,),
+    "core.deformable_att.value_proj.weight": (64, 64), "core.deformable_att.value_proj.bias": (64,),
+    "core.ctx2att.weight": (48, 64), "core.ctx2att.bias": (48,), "core.h2att.weight": (48, 64),
+    "core.h2att.bias": (48,), "core.alpha_net.weight": (1, 48), "core.alpha_net.bias": (1,),
+}
+
+
+@pytest.mark.parametrize("ref_dim", [1, 2])
+def test_caption_step_oracle_matches_reference_captioner(ref_dim):
+    """oracle/cap_step.py's float64 restatement of the captioner (soft-attention step, LSTM cell, logits) against
+    the reference module's fixture: logprobs, loss and every gradient (the fixture is float32: 1e-5 relative)."""
+    import sys
+    import torch
+    sys.path.insert(0, GOLD)
+    import weights as W
+    from oracle import cap_step as C
+    d = np.load(os.path.join(GOLD, f"module_captioner_ref{ref_dim}.npz"))
+    P = {}
+    for name, shape in CAP_SHAPES.items():
+        scale = 0.5 if "sampling_offsets" in name else None
+        P[name] = C.to_f64(W.param_array(name, shape, scale), grad=True)
+    hs, ref, memory = C.to_f64(d["hs"], True), C.to_f64(d["ref"], True), C.to_f64(d["memory"], True)
+    mask = torch.as_tensor(d["mask"])
+    cap = torch.as_tensor(d["cap_tensor"])
+    lp = C.captioner_forward(P, hs, ref, memory, mask, [int(t) for t in d["T_l"]], cap)
+    np.testing.assert_allclose(lp.detach().numpy(), d["logprobs"], rtol=0, atol=1e-5 * np.abs(d["logprobs"]).max())
+    loss = C.build_loss(lp, cap[:, 1:], torch.as_tensor(d["cap_mask"][:, 1:]).double(), 23).mean()
+    assert abs(float(loss) - float(d["loss"])) <= 1e-5 * abs(float(d["loss"]))
+    loss.backward()
+    checks = [("grad_hs", hs.grad), ("grad_ref", ref.grad), ("grad_memory", memory.grad)]
+    checks += [(f"grad.{n}", p.grad) for n, p in P.items()]
+    for key, g in checks:
+        want = d[key]
+        err = np.abs(g.numpy() - want).max()
+        assert err <= 1e-5 * np.abs(want).max() + 1e-9, (key, err, np.abs(want).max())
