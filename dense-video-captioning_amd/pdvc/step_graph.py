@@ -106,8 +106,10 @@ class rewriting_graphs:
         import torch.cuda.graphs as tg
         _REWRITE_LOCK.acquire()
         if _REWRITE_DEPTH[0] == 0:
-            _REWRITE_SAVED[0] = (torch.cuda.CUDAGraph, tg.CUDAGraph)
+            _REWRITE_SAVED[0] = (torch.cuda.CUDAGraph, tg.CUDAGraph, gc.isenabled())
             torch.cuda.CUDAGraph = tg.CUDAGraph = _RewritingGraph
+            gc.collect()
+            gc.disable()  # no collection inside the captures made here (no_gc_capture: a graph destroyed mid-capture)
         _REWRITE_DEPTH[0] += 1
         return self
 
@@ -116,8 +118,10 @@ class rewriting_graphs:
         try:
             _REWRITE_DEPTH[0] -= 1
             if _REWRITE_DEPTH[0] == 0:
-                torch.cuda.CUDAGraph, tg.CUDAGraph = _REWRITE_SAVED[0]
+                torch.cuda.CUDAGraph, tg.CUDAGraph, enabled = _REWRITE_SAVED[0]
                 _REWRITE_SAVED[0] = None
+                if enabled:
+                    gc.enable()
         finally:
             _REWRITE_LOCK.release()
         return False
@@ -155,10 +159,14 @@ class StepGraph:
         begin_capture()  # bf16 mode: every operand rounding of the step becomes a node of the graph
         if reducer is not None:
             reducer.suspended = True
-        # no garbage collection inside the capture: a collection there runs the destructors of unrelated cyclic
-        # garbage (autograd graphs of earlier eager steps, their tensors) while the stream captures, which aborted the
-        # process with no HIP message (round 4: the step-graph test after the other model suites, only when the
-        # collector's thresholds happened to fall inside the capture); torch.cuda.graph collects once on entry
+        # no garbage collection inside the capture.  Round 5 pinned the mechanism (tools/gc_capture_probe.py,
+        # profiles/r05_gc_capture_probe.txt): a collection inside a capture that frees cyclic garbage holding
+        # CUDA tensors, an eager autograd graph or events is harmless, but one that frees an unreachable
+        # torch.cuda.CUDAGraph (an earlier test's StepGraph or trunk graph) runs ~CUDAGraph, whose hipGraph
+        # destruction is refused while a stream captures (hipErrorStreamCaptureUnsupported, HIPGraph.cpp:324) and
+        # throws from a destructor: std::terminate, SIGABRT -- round 4's pass-AC abort inside the step-graph capture
+        # test, which ran after the model suites that leave such graphs behind.  torch.cuda.graph collects once on
+        # entry; tests/test_gpu_capture_gc.py checks no collection starts inside the capture
         gc_enabled = gc.isenabled()
         gc.disable()
         try:

@@ -105,7 +105,7 @@ def test_cap_step_kernels_match_float64_oracle(ref_dim, masked):
     assert_close(sloc, loc.detach().reshape(R, M, 16).numpy(), "sampling locations", TOL)
     assert_close(probs, p.detach().numpy(), "probabilities", TOL)
     assert_close(resg, res.detach().numpy(), "attended rows", TOL)
-    assert float(p.max()) < 0.9, "the soft attention must not be degenerate"
+    assert float(p.detach().max()) < 0.9, "the soft attention must not be degenerate"
 
     dresg = cu(dres, torch.float32)
     datt = torch.empty(R * M * 16, D, device=DEV)
@@ -122,7 +122,10 @@ def test_cap_step_kernels_match_float64_oracle(ref_dim, masked):
     assert_close(datt.view(R, M, 16, D), dU_ref.numpy(), "grad att (dL/dU per sample)", TOL)
     assert_close(dhp[:, 20:], aht.grad.numpy(), "grad att_h", TOL)
     assert_close(gaw.sum(0), awt.grad.numpy(), "grad alpha_net.weight", TOL)
-    assert_close(gab.sum(0, keepdim=True), abt.grad.numpy(), "grad alpha_net.bias", TOL)
+    # the alpha_net bias gradient is zero in exact arithmetic (a softmax is shift-invariant: sum_k dL/de_k = 0 per
+    # row); bounded against the scale of its sibling, the alpha_net weight gradient
+    assert_close(gab.sum(0, keepdim=True), abt.grad.numpy(), "grad alpha_net.bias", TOL,
+                 scale=float(awt.grad.abs().max()))
     assert_close(dhp[:, :16], offt.grad.numpy(), "grad sampling offsets", TOL)
     assert_close(gr, reft.grad.numpy(), "grad reference points", TOL)
 
