@@ -33,7 +33,8 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 #ifndef G3_ABLATE
-#define G3_ABLATE 0  // measurement-only builds (tools/variant_lib.sh): 1 no staging stores, 2 no staging loads, 4 no MFMA
+#define G3_ABLATE 0  // measurement-only builds (tools/variant_lib.sh): 1 no staging stores, 2 no staging loads, 4 no MFMA,
+                     // 8 no B-plane DMA (gemm3p)
 #endif
 
 constexpr int BK = 32;     // k per stage
@@ -47,14 +48,22 @@ __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
     return __builtin_bit_cast(unsigned, h);
 }
 
+// a - b as one v_sub_f32: written plainly, the compiler pairs the two lanes' subtractions into v_pk_add_f32, a
+// packed fp32 op that costs more issue cycles beside MFMAs than two plain ones (MI355X_MICROARCH.md, constants)
+__device__ __forceinline__ float sub_f32(float a, float b) {
+    float r;
+    asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // x -> (x0, x1, x2) for two values; packed pairs, element 0 in the low half (the lower k)
 __device__ __forceinline__ void split2(float a, float b, unsigned& p0, unsigned& p1, unsigned& p2) {
     p0 = pk_bf16(a, b);
-    const float ra = a - __uint_as_float(p0 << 16);
-    const float rb = b - __uint_as_float(p0 & 0xffff0000u);
+    const float ra = sub_f32(a, __uint_as_float(p0 << 16));
+    const float rb = sub_f32(b, __uint_as_float(p0 & 0xffff0000u));
     p1 = pk_bf16(ra, rb);
-    const float sa = ra - __uint_as_float(p1 << 16);
-    const float sb = rb - __uint_as_float(p1 & 0xffff0000u);
+    const float sa = sub_f32(ra, __uint_as_float(p1 << 16));
+    const float sb = sub_f32(rb, __uint_as_float(p1 & 0xffff0000u));
     p2 = pk_bf16(sa, sb);
 }
 
@@ -109,19 +118,24 @@ struct Stage {
         } else {
             const int kg = u & 7, r0 = 4 * (u >> 3);
             const float4* q = v + 4 * i;
-            // image row r0 + e takes (q[0].e, q[1].e, q[2].e, q[3].e): k = 4kg .. 4kg + 3
-#define G3_COL(E, F)                                                                        \
+            // image row r0 + e takes (q[0].e, q[1].e, q[2].e, q[3].e): k = 4kg .. 4kg + 3.  A ds_write_b64 serves 16
+            // lanes (two mn groups) per LDS cycle in 128 B: rows 4m + e and 4m + 4 + e would share one 64-B half (a
+            // 2-way conflict), so the odd mn group writes its rows in the order e ^ 1 -- rows 3 or 5 apart
+            const bool odd = (u >> 3) & 1;
+#define G3_SEL(A, B) (odd ? (B) : (A))
+#define G3_COL(E, F, G)                                                                     \
     {                                                                                      \
-        const int off = unit_off(r0 + E, kg);                                              \
+        const int off = unit_off(r0 + ((E) ^ (int)odd), kg);                               \
         uint2 p0, p1, p2;                                                                  \
-        split2(q[0].F, q[1].F, p0.x, p1.x, p2.x);                                          \
-        split2(q[2].F, q[3].F, p0.y, p1.y, p2.y);                                          \
+        split2(G3_SEL(q[0].F, q[0].G), G3_SEL(q[1].F, q[1].G), p0.x, p1.x, p2.x);          \
+        split2(G3_SEL(q[2].F, q[2].G), G3_SEL(q[3].F, q[3].G), p0.y, p1.y, p2.y);          \
         *reinterpret_cast<uint2*>(img + off) = p0;                                         \
         *reinterpret_cast<uint2*>(img + R * ROWB + off) = p1;                              \
         *reinterpret_cast<uint2*>(img + 2 * R * ROWB + off) = p2;                          \
     }
-            G3_COL(0, x) G3_COL(1, y) G3_COL(2, z) G3_COL(3, w)
+            G3_COL(0, x, y) G3_COL(1, y, x) G3_COL(2, z, w) G3_COL(3, w, z)
 #undef G3_COL
+#undef G3_SEL
         }
     }
     __device__ __forceinline__ void load_all(const float* P, long ld, int mn0, int k0, int MN) {
@@ -145,17 +159,17 @@ __device__ __forceinline__ f32x16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[
     return x;
 }
 
-template <int EPI, bool FULL>
-__device__ __forceinline__ void store_tile(const f32x16 (&acc)[2][2], float* __restrict__ C, long ldc,
+template <int EPI, bool FULL, int BI = 2, int BJ = 2>
+__device__ __forceinline__ void store_tile(const f32x16 (&acc)[BI][BJ], float* __restrict__ C, long ldc,
                                            const float* __restrict__ bias, int r0, int c0, int M, int N, int l32,
                                            int h) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < BJ; ++j) {
         const int col = c0 + 32 * j + l32;
         const bool colok = FULL || col < N;
         const float bv = (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) ? bias[colok ? col : 0] : 0.f;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < BI; ++i) {
             const int rbase = r0 + 32 * i + 4 * h;
             float* p0 = C + (long)rbase * ldc + col;
 #pragma unroll
@@ -169,6 +183,26 @@ __device__ __forceinline__ void store_tile(const f32x16 (&acc)[2][2], float* __r
                     *p = v;
                 }
             }
+        }
+    }
+}
+
+// one k16 step's fragments of a wave's 64 x 64 piece: a[i][p] rows wm + 32 i, b[j][p] rows wn + 32 j, plane p
+struct Frags {
+    bf16x8 a[2][3], b[2][3];
+};
+
+template <int BM, int BN>
+__device__ __forceinline__ void read_frags(Frags& f, const char* img, int wm, int wn, int ks, int l32, int h) {
+    constexpr int AIMG = 3 * BM * ROWB;
+    const int c = 2 * ks + h;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int ra = wm + 32 * i + l32, rb = wn + 32 * i + l32;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            f.a[i][p] = *reinterpret_cast<const bf16x8*>(img + p * BM * ROWB + frag_off(ra, c));
+            f.b[i][p] = *reinterpret_cast<const bf16x8*>(img + AIMG + p * BN * ROWB + frag_off(rb, c));
         }
     }
 }
@@ -199,10 +233,12 @@ __global__ __launch_bounds__(NT, 1) void gemm3_kernel(int M, int N, int K, const
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    // register ring one stage deep: the registers hold stage s + 1 while stage s computes; they are split into
-    // the other LDS buffer during stage s's first k half and reloaded with stage s + 2 during its second
+    // register ring one stage deep: the registers hold stage s + 1 while stage s computes; they are split into the
+    // other LDS buffer among the first k16 step's MFMAs and reloaded with stage s + 2 after them.  The second k16
+    // step's fragments (f1) are consumed after the stage's barrier, covering the next stage's first reads (gemm3p).
     Stage<BM, AKC> sa;
     Stage<BN, BKC> sb;
+    Frags f0, f1;
     if (nst > 0) {
         sa.load_all(A, lda, m0, kb, M);
         sb.load_all(B, ldb, n0, kb, N);
@@ -214,51 +250,46 @@ __global__ __launch_bounds__(NT, 1) void gemm3_kernel(int M, int N, int K, const
         }
     }
     __syncthreads();
+    if (nst > 0) read_frags<BM, BN>(f0, lds, wm, wn, 0, l32, h);
     for (int s = 0; s < nst; ++s) {
         const char* cur = lds + (s & 1) * STAGE;
         char* nxt = lds + ((s + 1) & 1) * STAGE;
         const bool more = s + 1 < nst, more2 = s + 2 < nst;
+        read_frags<BM, BN>(f1, cur, wm, wn, 1, l32, h);
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            bf16x8 a[2][3], b[2][3];
-            const int c = 2 * ks + h;
+        for (int q = 0; q < 4; ++q) {
+            const int i = q >> 1, j = q & 1;
+            if constexpr ((G3_ABLATE & 4) == 0) acc[i][j] = mfma6(f0.a[i], f0.b[j], acc[i][j]);
+            else {
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int ra = wm + 32 * i + l32, rb = wn + 32 * i + l32;
-#pragma unroll
-                for (int p = 0; p < 3; ++p) {
-                    a[i][p] = *reinterpret_cast<const bf16x8*>(cur + p * BM * ROWB + frag_off(ra, c));
-                    b[i][p] = *reinterpret_cast<const bf16x8*>(cur + AIMG + p * BN * ROWB + frag_off(rb, c));
-                }
+                for (int p = 0; p < 3; ++p) asm volatile("" ::"v"(f0.a[i][p]), "v"(f0.b[j][p]));
             }
+            if (more && (G3_ABLATE & 1) == 0) {
+                // staging work between the MFMA groups: A pieces, then B pieces, spread over the four groups
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int i = q >> 1, j = q & 1;
-                if constexpr ((G3_ABLATE & 4) == 0) acc[i][j] = mfma6(a[i], b[j], acc[i][j]);
-                else {
+                for (int u = 0; u < Stage<BM, AKC>::NU; ++u)
+                    if (u * 4 / (Stage<BM, AKC>::NU + Stage<BN, BKC>::NU) == q) sa.store(u, nxt);
 #pragma unroll
-                    for (int p = 0; p < 3; ++p) asm volatile("" ::"v"(a[i][p]), "v"(b[j][p]));
-                }
-                if (ks == 0 && more && (G3_ABLATE & 1) == 0) {
-                    // staging work between the MFMA groups: A pieces after groups 0..NU_A-1, then B
-#pragma unroll
-                    for (int u = 0; u < Stage<BM, AKC>::NU; ++u)
-                        if (u * 4 / Stage<BM, AKC>::NU == q) sa.store(u, nxt);
-#pragma unroll
-                    for (int u = 0; u < Stage<BN, BKC>::NU; ++u)
-                        if (u * 4 / Stage<BN, BKC>::NU == q) sb.store(u, nxt + AIMG);
-                }
-                if (ks == 1 && more2 && (G3_ABLATE & 2) == 0) {
-#pragma unroll
-                    for (int u = 0; u < Stage<BM, AKC>::NU; ++u)
-                        if (u * 4 / Stage<BM, AKC>::NU == q) sa.load(u, A, lda, m0, kb + (s + 2) * BK, M);
-#pragma unroll
-                    for (int u = 0; u < Stage<BN, BKC>::NU; ++u)
-                        if (u * 4 / Stage<BN, BKC>::NU == q) sb.load(u, B, ldb, n0, kb + (s + 2) * BK, N);
-                }
+                for (int u = 0; u < Stage<BN, BKC>::NU; ++u)
+                    if ((Stage<BM, AKC>::NU + u) * 4 / (Stage<BM, AKC>::NU + Stage<BN, BKC>::NU) == q)
+                        sb.store(u, nxt + AIMG);
+            }
+            if (q == 3 && more2 && (G3_ABLATE & 2) == 0) {
+                sa.load_all(A, lda, m0, kb + (s + 2) * BK, M);
+                sb.load_all(B, ldb, n0, kb + (s + 2) * BK, N);
             }
         }
         __syncthreads();
+        if (more) read_frags<BM, BN>(f0, nxt, wm, wn, 0, l32, h);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if constexpr ((G3_ABLATE & 4) == 0)
+                acc[q >> 1][q & 1] = mfma6(f1.a[q >> 1], f1.b[q & 1], acc[q >> 1][q & 1]);
+            else {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) asm volatile("" ::"v"(f1.a[q >> 1][p]), "v"(f1.b[q & 1][p]));
+            }
+        }
     }
 
     // epilogue: acc[i][j] register r of lane l is C[row][col], col = l % 32, row = (r & 3) + 8 (r >> 2) + 4 (l / 32)
@@ -319,27 +350,80 @@ __device__ __forceinline__ void planes_dma(char* dst, const uint16_t* __restrict
                      : "memory");
 }
 
+// gemm3p geometry: a 256 x 256 tile, K in 16-deep stages through a ring of three LDS stages (3 x 48 KiB), 8 waves of
+// 128 x 64 (4 x 2 blocks of 32 x 32: 48 MFMAs a stage, 18 fragment reads).  Against a 128 x 256 tile of 32-deep
+// stages this halves the L2 -> LDS bytes and the fragment reads per MFMA, and the ring keeps the DMAs and row loads two
+// stages ahead of their use.  Image rows are 32 B (16 bf16); the 16-B half of row r holding k chunk c is
+// c ^ ((r >> 3) & 1), so the 16-lane groups of a fragment read and the DMA / A-row writes are conflict-free.
+namespace p3 {
+constexpr int BM = 256, BN = 256, KS = 16, RB = 32, NSTAGE = 3;
+constexpr int AIMG = 3 * BM * RB, BIMG = 3 * BN * RB, STAGE = AIMG + BIMG;  // 24 + 24 KiB
+constexpr int NUA = BM * KS / 4 / NT;                                    // A pieces (4 k of a row) per thread: 2
+constexpr int BDMA = 3 * BN * RB / 1024 / (NT / 64);                      // 1-KiB DMAs per wave per stage: 3
+
+__device__ __forceinline__ int unit_off16(int row, int k4) {
+    return row * RB + ((((k4 >> 1) ^ (row >> 3)) & 1) << 4) + ((k4 & 1) << 3);
+}
+__device__ __forceinline__ int frag_off16(int row, int h) { return row * RB + (((h ^ (row >> 3)) & 1) << 4); }
+
+struct ARegs {
+    float4 v[NUA];
+    __device__ __forceinline__ void load(const float* __restrict__ A, long lda, int m0, int k0, int M) {
+#pragma unroll
+        for (int i = 0; i < NUA; ++i) {
+            const int u = threadIdx.x + NT * i;
+            const int row = min(m0 + (u >> 2), M - 1);
+            v[i] = *reinterpret_cast<const float4*>(A + (long)row * lda + k0 + ((u & 3) << 2));
+        }
+    }
+    __device__ __forceinline__ void store(int i, char* __restrict__ img) const {
+        const int u = threadIdx.x + NT * i;
+        const int off = unit_off16(u >> 2, u & 3);
+        uint2 q0, q1, q2;
+        split2(v[i].x, v[i].y, q0.x, q1.x, q2.x);
+        split2(v[i].z, v[i].w, q0.y, q1.y, q2.y);
+        *reinterpret_cast<uint2*>(img + off) = q0;
+        *reinterpret_cast<uint2*>(img + BM * RB + off) = q1;
+        *reinterpret_cast<uint2*>(img + 2 * BM * RB + off) = q2;
+    }
+};
+
+// one 1-KiB LDS-DMA wave-instruction: 32 image rows x 32 B of one plane; lane l lands at dst + 16 l = row l / 2,
+// half l % 2, which holds k chunk (l % 2) ^ ((row >> 3) & 1)
+__device__ __forceinline__ void dma32(char* dst, const uint16_t* __restrict__ plane, int K, int row0, int N, int k0,
+                                      int lane) {
+    const int row = row0 + (lane >> 1);
+    const int c = (lane & 1) ^ ((row >> 3) & 1);
+    const uint16_t* src = plane + (long)min(row, N - 1) * K + k0 + 8 * c;
+    const uint32_t d = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(g3_lds_t*)dst);
+    int keep;
+    __asm__ volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(src), "s"(d)
+                     : "memory");
+}
+}  // namespace p3
+
 template <int EPI>
 __global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, const float* __restrict__ A, long lda,
                                                        const uint16_t* __restrict__ planes, float* __restrict__ C,
                                                        long ldc, const float* __restrict__ bias, int tiles_n) {
-    constexpr int BM = 128, BN = 256;
-    constexpr int AIMG = 3 * BM * ROWB, BIMG = 3 * BN * ROWB, STAGE = AIMG + BIMG;
-    constexpr int BDMA = 3 * BN / 16 / (NT / 64);  // LDS-DMA instructions per wave per stage (6)
-    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+    using namespace p3;
+    __shared__ __attribute__((aligned(16))) char lds[NSTAGE * STAGE];
 
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int tile = xcd_remap(blockIdx.x, gridDim.x);  // the column tiles of one row block share an XCD's L2
     const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
-    const int nst = K / BK;
-    const int wm = (wid / (BN / 64)) * 64, wn = (wid % (BN / 64)) * 64;
+    const int nst = K / KS;
+    const int wm = (wid >> 2) * 128, wn = (wid & 3) * 64;
     const int l32 = lane & 31, h = lane >> 5;
     const long pstride = (long)N * K;
 
-    f32x16 acc[2][2];
+    f32x16 acc[4][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -348,59 +432,65 @@ __global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, cons
     auto b_dma = [&](char* img, int k0) {
 #pragma unroll
         for (int q = 0; q < BDMA; ++q) {
-            const int g = wid * BDMA + q;  // 48 instructions: plane g / 16, rows 16 (g % 16) ..
-            const int p = g / (BN / 16), r0 = (g % (BN / 16)) * 16;
-            planes_dma(img + AIMG + p * BN * ROWB + r0 * ROWB, planes + p * pstride, K, n0 + r0, N, k0, lane);
+            const int g = wid * BDMA + q;  // 24 instructions: plane g / 8, rows 32 (g % 8) ..
+            const int p = g / (BN / 32), r0 = (g % (BN / 32)) * 32;
+            dma32(img + AIMG + p * BN * RB + r0 * RB, planes + p * pstride, K, n0 + r0, N, k0, lane);
         }
     };
 
-    Stage<BM, true> sa;
+    // prologue: stage 0 complete in LDS, stage 1's DMAs issued and its A rows in registers
+    ARegs ra;
     if (nst > 0) {
+        ra.load(A, lda, m0, 0, M);
+#pragma unroll
+        for (int i = 0; i < NUA; ++i) ra.store(i, lds);  // (waits for the rows; nothing else is in flight)
         b_dma(lds, 0);
-        sa.load_all(A, lda, m0, 0, M);
-        sa.store_all(lds);
-        if (nst > 1) sa.load_all(A, lda, m0, BK, M);
-        __builtin_amdgcn_s_waitcnt(0x0F70 | (Stage<BM, true>::NU & 15));  // vmcnt(A loads): the DMAs have landed
+        if (nst > 1) {
+            b_dma(lds + STAGE, KS);
+            ra.load(A, lda, m0, KS, M);
+        }
+        // stage 0's DMAs are older than stage 1's DMAs and rows: leave those in flight
+        if (nst > 1) __builtin_amdgcn_s_waitcnt(0x0F70 | ((BDMA + NUA) & 15));
+        else __builtin_amdgcn_s_waitcnt(0x0F70);
     }
     __syncthreads();
     for (int s = 0; s < nst; ++s) {
-        const char* cur = lds + (s & 1) * STAGE;
-        char* nxt = lds + ((s + 1) & 1) * STAGE;
+        const char* cur = lds + (s % NSTAGE) * STAGE;
+        char* nx1 = lds + ((s + 1) % NSTAGE) * STAGE;
+        char* nx2 = lds + ((s + 2) % NSTAGE) * STAGE;
         const bool more = s + 1 < nst, more2 = s + 2 < nst;
+        bf16x8 fa[4][3], fb[2][3];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            bf16x8 a[2][3], b[2][3];
-            const int c = 2 * ks + h;
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int ra = wm + 32 * i + l32, rb = wn + 32 * i + l32;
+            for (int p = 0; p < 3; ++p)
+                fb[j][p] = *reinterpret_cast<const bf16x8*>(cur + AIMG + p * BN * RB + frag_off16(wn + 32 * j + l32, h));
 #pragma unroll
-                for (int p = 0; p < 3; ++p) {
-                    a[i][p] = *reinterpret_cast<const bf16x8*>(cur + p * BM * ROWB + frag_off(ra, c));
-                    b[i][p] = *reinterpret_cast<const bf16x8*>(cur + AIMG + p * BN * ROWB + frag_off(rb, c));
-                }
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                fa[i][p] = *reinterpret_cast<const bf16x8*>(cur + p * BM * RB + frag_off16(wm + 32 * i + l32, h));
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int i = q >> 1, j = q & 1;
+            if constexpr ((G3_ABLATE & 4) == 0) acc[i][j] = mfma6(fa[i], fb[j], acc[i][j]);
+            else {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) asm volatile("" ::"v"(fa[i][p]), "v"(fb[j][p]));
             }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int i = q >> 1, j = q & 1;
-                acc[i][j] = mfma6(a[i], b[j], acc[i][j]);
-                if (ks == 0 && more && q < Stage<BM, true>::NU) sa.store(q, nxt);
-                // after the A registers are in LDS: stage s + 1's B planes (DMA), then stage s + 2's A rows.  In
-                // this order the compiler's own wait for the A rows (next stage) never covers fresh DMAs
-                if (ks == 0 && more && q == Stage<BM, true>::NU) b_dma(nxt, (s + 1) * BK);
-                if (ks == 0 && more2 && q == Stage<BM, true>::NU) sa.load_all(A, lda, m0, (s + 2) * BK, M);
-            }
+            // stage s + 1's A rows split into its buffer (the compiler waits for them: loaded a stage ago, and with
+            // them every older DMA -- stage s + 1's), then stage s + 2's DMAs and rows, two stages ahead
+            if (more && q >= 2 && q < 2 + NUA && (G3_ABLATE & 1) == 0) ra.store(q - 2, nx1);
+            if (more2 && q == 2 + NUA && (G3_ABLATE & 8) == 0) b_dma(nx2, (s + 2) * KS);
+            if (more2 && q == 2 + NUA && (G3_ABLATE & 2) == 0) ra.load(A, lda, m0, (s + 2) * KS, M);
         }
-        // the B DMAs of stage s + 1 are older than this stage's A loads (at most NU of them): retire the DMAs
-        if (more2) __builtin_amdgcn_s_waitcnt(0x0F70 | (Stage<BM, true>::NU & 15));
-        else __builtin_amdgcn_s_waitcnt(0x0F70);
+        if (more && !more2) __builtin_amdgcn_s_waitcnt(0x0F70);  // the last stage's DMAs (no later rows to wait on)
         __syncthreads();
     }
 
-    float* Cz = C;
     const bool full = m0 + BM <= M && n0 + BN <= N;
-    if (full) store_tile<EPI, true>(acc, Cz, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h);
-    else store_tile<EPI, false>(acc, Cz, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h);
+    if (full) store_tile<EPI, true, 4, 2>(acc, C, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h);
+    else store_tile<EPI, false, 4, 2>(acc, C, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h);
 }
 
 // out[i] (=|+=) sum_z ws[z * n + i], float4 lanes (n % 4 == 0)
@@ -517,7 +607,7 @@ extern "C" int pdvc_gemm3p_f32(int M, int N, int K, const float* A, long lda, co
     PDVC_CHECK_ARG((uintptr_t)A % 16 == 0 && lda % 4 == 0 && (uintptr_t)planes % 16 == 0,
                    "A rows and the planes must be 16-byte aligned");
     if (M == 0) return PDVC_OK;
-    const long tiles_m = (M + 127) / 128, tiles_n = (N + 255) / 256;
+    const long tiles_m = (M + p3::BM - 1) / p3::BM, tiles_n = (N + p3::BN - 1) / p3::BN;
     PDVC_CHECK_ARG(tiles_m * tiles_n < (1L << 31), "too many tiles");
     const dim3 grid((unsigned)(tiles_m * tiles_n));
     hipStream_t s = (hipStream_t)stream;

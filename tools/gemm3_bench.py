@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--only", default="", help="comma list of ops (fwd,dgrad,wgrad); empty = all")
     ap.add_argument("--shapes", default="512x512,256x512,512x256", help="OxI list")
     ap.add_argument("--no-err", action="store_true")
+    ap.add_argument("--mnk", default="", help="fwdp only at M,N,K (e.g. 245760,512,2048)")
     a = ap.parse_args()
     torch.manual_seed(0)
     dev = "cuda"
@@ -76,6 +77,16 @@ def main():
         res.append(r)
         print(json.dumps(r), flush=True)
 
+    if a.mnk:
+        Mx, Nx, Kx = (int(v) for v in a.mnk.split(","))
+        x = torch.randn(Mx, Kx, device=dev)
+        W = torch.randn(Nx, Kx, device=dev)
+        b = torch.randn(Nx, device=dev)
+        y = torch.empty(Mx, Nx, device=dev)
+        planes = torch.empty(3 * Nx * Kx, dtype=torch.int16, device=dev)
+        run("fwdp", Mx, Nx, Kx, lambda: gemm3p(Mx, Nx, Kx, x, Kx, W, Kx, 1, planes, y, Nx, b, 1),
+            lambda: torch.addmm(b, x, W.t()), lambda: ({}, {}))
+        return
     for (O, I) in [tuple(int(v) for v in sh.split("x")) for sh in a.shapes.split(",")]:
         x = torch.randn(M, I, device=dev)
         W = torch.randn(O, I, device=dev) / I ** 0.5
