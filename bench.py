@@ -44,7 +44,8 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 F32_MFMA_PEAK_TFS = 157.3  # MI355X dense FP32 matrix peak (MI355X_MICROARCH.md: no xf32 on gfx950)
 BF16_MFMA_PEAK_TFS = 2500.0  # MI355X dense BF16 matrix peak (MI355X_MICROARCH.md; the 5 PF figure is 2:1 sparse)
-GEMM_KERNEL = re.compile(r"^Cijk_|gemm|Gemm")  # hipBLASLt / rocBLAS (Tensile) kernels, pdvc_gemm_f32
+GEMM_KERNEL = re.compile(r"^Cijk_|gemm|Gemm")  # hipBLASLt / rocBLAS (Tensile) kernels, pdvc_gemm_f32, gemm3
+GEMM3_KERNEL = re.compile(r"gemm3|split_planes_kernel|slab_sum_kernel")  # the in-tree split-bf16 GEMM family
 # the two benchmarked workloads: the metric's headline config, and BASELINE.json configs[1] in bf16
 WORKLOADS = {
     "anet_tsp": dict(cfg="cfgs/anet_tsp_pdvc.yml", T=512, C=768, Q=100, events=4, words=13, precision="fp32",
@@ -169,10 +170,15 @@ class GemmFlops:
 
         self._mode = _Mode()
         self._mode.__enter__()
+        from pdvc.ops.functions import gemm3
+        self._g3 = gemm3.FLOPS[0]
         return self
 
     def __exit__(self, *exc):
         self._mode.__exit__(*exc)
+        from pdvc.ops.functions import gemm3
+        self.gemm3_flops = gemm3.FLOPS[0] - self._g3  # products on the in-tree kernels (not aten ops)
+        self.flops += self.gemm3_flops
         return False
 
 
@@ -187,14 +193,18 @@ def gemm_roofline(flop_step, timed_step, precision, graphed):
         flop_step()
     torch.cuda.synchronize()
     flops = fc.flops
+    g3_flops = getattr(fc, "gemm3_flops", 0)
     with profile(activities=[ProfilerActivity.CUDA]) as prof:
         timed_step()
         torch.cuda.synchronize()
-    gemm_us, cast_us, launches, total_us = 0.0, 0.0, 0, 0.0
+    gemm_us, cast_us, launches, total_us, g3_us, g3_launches = 0.0, 0.0, 0, 0.0, 0.0, 0
     for e in prof.key_averages():
         dt = e.device_time_total
         total_us += dt
-        if GEMM_KERNEL.search(e.key):
+        if GEMM3_KERNEL.search(e.key):
+            g3_us += dt
+            g3_launches += e.count
+        if GEMM_KERNEL.search(e.key) or GEMM3_KERNEL.search(e.key):
             gemm_us += dt
             launches += e.count
         elif precision == "bf16" and "copy" in e.key.lower() and "bfloat16" in e.key.lower():
@@ -212,6 +222,25 @@ def gemm_roofline(flop_step, timed_step, precision, graphed):
                     "kernel device time in 1 profiled eager step") + "; flops: 2mnk of every aten GEMM of 1 eager step (GemmFlops)"}
     if precision == "bf16":
         r["bf16_cast_ms_per_step"] = cast_us / 1e3
+    if g3_flops and g3_us > 0:
+        # the in-tree kernels (csrc/gemm3.hip): fp32 products as six bf16 MFMA terms each -- priced on the bf16 matrix
+        # peak with the EXECUTED flops (6 x 2mnk); the fp32-equivalent rate beside the fp32 matrix peak
+        from pdvc.ops.functions.gemm3 import EXECUTED_PER_ALGORITHMIC as X
+        alg = g3_flops / (g3_us * 1e-6) / 1e12
+        lib_us, lib_flops = gemm_us - g3_us, flops - g3_flops
+        r["gemm3"] = {"kernel": "gemm3p_kernel / gemm3_kernel (in-tree fp32 GEMM, exact 3-term bf16 split, six MFMA "
+                                "products, fp32 accumulation)", "bound": "mfma", "achieved": X * alg,
+                      "peak": BF16_MFMA_PEAK_TFS, "unit": "TFLOP/s (bf16 MFMA, executed)",
+                      "frac": X * alg / BF16_MFMA_PEAK_TFS, "fp32_equivalent_tfs": alg,
+                      "fp32_equivalent_vs_fp32_peak": alg / F32_MFMA_PEAK_TFS, "gflop_per_step": g3_flops / 1e9,
+                      "device_ms_per_step": g3_us / 1e3, "launches_per_step": g3_launches}
+        if lib_us > 0:
+            r["library"] = {"kernel": "hipBLASLt / rocBLAS (fp32, tuned table)", "achieved": lib_flops / (lib_us * 1e-6) / 1e12,
+                            "peak": F32_MFMA_PEAK_TFS, "frac": lib_flops / (lib_us * 1e-6) / 1e12 / F32_MFMA_PEAK_TFS,
+                            "gflop_per_step": lib_flops / 1e9, "device_ms_per_step": lib_us / 1e3,
+                            "launches_per_step": launches - g3_launches}
+        r["kernel"] = ("projection / FFN / LSTM / logit GEMMs: in-tree gemm3 (split-bf16 MFMA) for the encoder-scale "
+                       "products, hipBLASLt fp32 for the rest")
     return r
 
 
@@ -411,16 +440,33 @@ def eval_main(a):
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
+    # every step timed on its own: host wall time (the greedy loop checks for finished rows on the host once per
+    # decode step, LSTM_DSA.py:172-179) beside the device time between two events on the step's stream, so a slow
+    # step is attributed to the host (wall >> device) or to the device
+    walls, devs = [], []
     t0 = time.perf_counter()
     for _ in range(a.steps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        w0 = time.perf_counter()
+        e0.record()
         step()
-    torch.cuda.synchronize()
+        e1.record()
+        torch.cuda.synchronize()
+        walls.append(1e3 * (time.perf_counter() - w0))
+        devs.append(e0.elapsed_time(e1))
     el = time.perf_counter() - t0
+    ws, ds = sorted(walls), sorted(devs)
+    med = ws[len(ws) // 2] if len(ws) % 2 else 0.5 * (ws[len(ws) // 2 - 1] + ws[len(ws) // 2])
+    dmed = ds[len(ds) // 2] if len(ds) % 2 else 0.5 * (ds[len(ds) // 2 - 1] + ds[len(ds) // 2])
     result = {"metric": "videos/sec eval (PDVC forward + greedy captions of all queries + PostProcess, "
                         f"T={a.T} C={a.C} Q={a.Q}) on 1 MI355X",
               "value": a.steps * B / el, "unit": "videos/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
               "ms_per_step": 1e3 * el / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
               "dtype": "f32", "data": "synthetic",
+              "per_step": {"median_videos_per_s": 1e3 * B / med, "wall_ms": {"median": med, "min": ws[0], "max": ws[-1]},
+                           "device_ms": {"median": dmed, "min": ds[0], "max": ds[-1]},
+                           "host_ms_median": med - dmed, "wall_ms_all": [round(w, 2) for w in walls],
+                           "device_ms_all": [round(d, 2) for d in devs]},
               "config": {"workload": f"{os.path.basename(a.cfg)[:-4]} eval: {B} videos x {a.Q} queries, greedy "
                                      f"decoding up to max_caption_len {args.max_caption_len} + 1 steps, random-init "
                                      f"weights (decode length {steps_seen[-1]} steps)",

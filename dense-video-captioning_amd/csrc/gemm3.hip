@@ -493,6 +493,121 @@ __global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, cons
     else store_tile<EPI, false, 4, 2>(acc, C, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h);
 }
 
+// ---- both operands mn-contiguous (the weight gradient dW = dy^T x: the reduction runs over the rows of both) ----
+// gemm3w: a 256 x 256 tile, 16 reduction rows per stage, two LDS stages (2 x 48 KiB), 8 waves of 128 x 64.  The
+// images are k-major, [k][256 mn] per plane (512-B rows; the 8-B chunk holding mn 4c .. 4c + 3 of row k sits at chunk
+// (c + 8 (k & 3)) & 63): a thread's float4 of 4 consecutive mn is split and stored as it was loaded (16 lanes write
+// 128 contiguous bytes, no register transpose), and each 32 x 32 x 16 fragment is two ds_read_b64_tr_b16 (4 k x 16
+// mn blocks delivered transposed: lane i of a 16-lane group gets mn i of the block's 4 k rows) -- the row rotation
+// puts a half-wave's 4 rows x 8 chunks on 32 distinct 8-B slots.
+namespace w3 {
+constexpr int BM = 256, BN = 256, KS = 16, ROW = 512, PL = KS * ROW;  // a plane: 16 k rows of 256 mn (8 KiB)
+constexpr int AIMG = 3 * PL, STAGE = 6 * PL;                          // 24 + 24 KiB
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ int chunk_off(int k, int c) { return k * ROW + (((c + 8 * (k & 3)) & 63) << 3); }
+
+// the 32 x 32 x 16 fragment of plane image `img` at mn base mb: lanes hold mn = mb + (l & 31), k = 8 (l >> 5) + j
+__device__ __forceinline__ bf16x8 frag_tr(const char* img, int mb, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    const int c = ((mb + ((g & 1) << 4)) >> 2) + pp;
+    const int k = 8 * (g >> 1) + q;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + chunk_off(k, c)));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + chunk_off(k + 4, c)));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+struct Regs {  // one stage of both operands: float4 u = t + 512 i (i = 0, 1) is row k = u / 64, mn chunk u % 64
+    float4 a[2], b[2];
+    __device__ __forceinline__ void load(const float* __restrict__ A, long lda, int m0, int M,
+                                         const float* __restrict__ B, long ldb, int n0, int N, int k0) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int u = threadIdx.x + NT * i, k = k0 + (u >> 6), c = u & 63;
+            a[i] = *reinterpret_cast<const float4*>(A + (long)k * lda + min(m0 + 4 * c, M - 4));
+            b[i] = *reinterpret_cast<const float4*>(B + (long)k * ldb + min(n0 + 4 * c, N - 4));
+        }
+    }
+    __device__ __forceinline__ static void put(const float4& v, char* img, int u) {
+        const int off = chunk_off(u >> 6, u & 63);
+        uint2 q0, q1, q2;
+        split2(v.x, v.y, q0.x, q1.x, q2.x);
+        split2(v.z, v.w, q0.y, q1.y, q2.y);
+        *reinterpret_cast<uint2*>(img + off) = q0;
+        *reinterpret_cast<uint2*>(img + PL + off) = q1;
+        *reinterpret_cast<uint2*>(img + 2 * PL + off) = q2;
+    }
+    __device__ __forceinline__ void store(int piece, char* img) const {  // pieces 0, 1: A; 2, 3: B
+        const int i = piece & 1, u = threadIdx.x + NT * i;
+        if (piece < 2) put(a[i], img, u);
+        else put(b[i], img + AIMG, u);
+    }
+};
+}  // namespace w3
+
+template <int EPI>
+__global__ __launch_bounds__(NT, 1) void gemm3w_kernel(int M, int N, int K, const float* __restrict__ A, long lda,
+                                                       const float* __restrict__ B, long ldb, float* __restrict__ C,
+                                                       long ldc, int k_per_split, int tiles_n, long slab) {
+    using namespace w3;
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kb = blockIdx.z * k_per_split;
+    const int nst = (min(K, kb + k_per_split) - kb) / KS;
+    const int wm = (wid >> 2) * 128, wn = (wid & 3) * 64;
+    const int l32 = lane & 31, h = lane >> 5;
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    Regs rg;
+    if (nst > 0) {
+        rg.load(A, lda, m0, M, B, ldb, n0, N, kb);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rg.store(q, lds);
+        if (nst > 1) rg.load(A, lda, m0, M, B, ldb, n0, N, kb + KS);
+    }
+    __syncthreads();
+    for (int s = 0; s < nst; ++s) {
+        const char* cur = lds + (s & 1) * STAGE;
+        char* nxt = lds + ((s + 1) & 1) * STAGE;
+        const bool more = s + 1 < nst, more2 = s + 2 < nst;
+        bf16x8 fa[4][3], fb[2][3];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) fb[j][p] = frag_tr(cur + AIMG + p * PL, wn + 32 * j, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) fa[i][p] = frag_tr(cur + p * PL, wm + 32 * i, lane);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int i = q >> 1, j = q & 1;
+            acc[i][j] = mfma6(fa[i], fb[j], acc[i][j]);
+            if (more && q >= 1 && q <= 4) rg.store(q - 1, nxt);  // stage s + 1 into the other buffer
+            if (more2 && q == 5) rg.load(A, lda, m0, M, B, ldb, n0, N, kb + (s + 2) * KS);
+        }
+        __syncthreads();
+    }
+    (void)l32;
+    float* Cz = C + (EPI == EPI_SLAB ? (long)blockIdx.z * slab : 0);
+    const bool full = m0 + BM <= M && n0 + BN <= N;
+    if (full) store_tile<EPI, true, 4, 2>(acc, Cz, ldc, nullptr, m0 + wm, n0 + wn, M, N, l32, h);
+    else store_tile<EPI, false, 4, 2>(acc, Cz, ldc, nullptr, m0 + wm, n0 + wn, M, N, l32, h);
+}
+
 // out[i] (=|+=) sum_z ws[z * n + i], float4 lanes (n % 4 == 0)
 template <bool ACC>
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ ws, int splits, long n4,
@@ -569,6 +684,26 @@ extern "C" int pdvc_gemm3_f32(int M, int N, int K, const float* A, long lda, int
     const long ld = slab ? N : ldc;
     const int epi = slab ? (int)EPI_SLAB : epilogue;
     const long slab_n = (long)M * N;
+    if (!a_kc && !b_kc && (epi == EPI_STORE || epi == EPI_SLAB)) {  // the weight-gradient form: gemm3w's tile
+        const long wm_ = (M + w3::BM - 1) / w3::BM, wn_ = (N + w3::BN - 1) / w3::BN;
+        int kpw = (K + splits - 1) / splits;
+        kpw = (kpw + w3::KS - 1) / w3::KS * w3::KS;
+        const int nzw = K == 0 ? 1 : (K + kpw - 1) / kpw;
+        const dim3 gw((unsigned)(wm_ * wn_), 1, (unsigned)nzw);
+        float* dw = nzw > 1 ? workspace : C;
+        const long ldw = nzw > 1 ? N : ldc;
+        if (nzw > 1) hipLaunchKernelGGL(gemm3w_kernel<EPI_SLAB>, gw, dim3(NT), 0, s, M, N, K, A, lda, B, ldb, dw, ldw, kpw, (int)wn_, slab_n);
+        else hipLaunchKernelGGL(gemm3w_kernel<EPI_STORE>, gw, dim3(NT), 0, s, M, N, K, A, lda, B, ldb, dw, ldw, kpw, (int)wn_, slab_n);
+        PDVC_CHECK_LAUNCH("gemm3w_kernel");
+        if (nzw > 1) {
+            const long n4 = slab_n / 4;
+            const int blocks = (int)std::min<long>((n4 + 255) / 256, 2048);
+            if (epilogue == 3) hipLaunchKernelGGL(slab_sum_kernel<true>, dim3(blocks), dim3(256), 0, s, workspace, nzw, n4, C);
+            else hipLaunchKernelGGL(slab_sum_kernel<false>, dim3(blocks), dim3(256), 0, s, workspace, nzw, n4, C);
+            PDVC_CHECK_LAUNCH("slab_sum_kernel");
+        }
+        return PDVC_OK;
+    }
     if (a_kc && b_kc) launch_epi<BM, BN, true, true>(epi, grid, s, M, N, K, A, lda, B, ldb, dst, ld, bias, kps, (int)tiles_n, slab_n);
     else if (a_kc) launch_epi<BM, BN, true, false>(epi, grid, s, M, N, K, A, lda, B, ldb, dst, ld, bias, kps, (int)tiles_n, slab_n);
     else if (b_kc) launch_epi<BM, BN, false, true>(epi, grid, s, M, N, K, A, lda, B, ldb, dst, ld, bias, kps, (int)tiles_n, slab_n);

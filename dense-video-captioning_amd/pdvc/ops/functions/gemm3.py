@@ -27,6 +27,8 @@ from pdvc import _native as _n
 ENABLED = os.environ.get("PDVC_GEMM3", "1") != "0"
 MIN_ROWS = int(os.environ.get("PDVC_GEMM3_MIN_ROWS", "8192"))  # below: launch-bound shapes stay on hipBLASLt
 CALLS = {"gemm3": 0, "torch": 0}  # how many products took each path (tests check the encoder takes gemm3)
+FLOPS = [0]  # algorithmic 2*M*N*K of every product issued on gemm3 (bench.py's roofline counts them)
+EXECUTED_PER_ALGORITHMIC = 6  # bf16 MFMA products per fp32 product (the six split terms)
 
 
 def _bf16_mode():
@@ -40,8 +42,9 @@ def _rows_ok(t):
             and t.data_ptr() % 16 == 0 and t.stride(0) >= t.shape[1])
 
 
-def _use(M, K, *ops):
-    if not ENABLED or M < MIN_ROWS or K % 32 != 0 or not all(_rows_ok(t) for t in ops) or _bf16_mode():
+def _use(M, K, *ops, extra=True):
+    if (not extra or not ENABLED or M < MIN_ROWS or K % 32 != 0 or not all(_rows_ok(t) for t in ops)
+            or _bf16_mode()):
         CALLS["torch"] += 1
         return False
     CALLS["gemm3"] += 1
@@ -57,6 +60,7 @@ def split_planes(B, b_kc, N, K):
 
 def _gemm3p(a, planes, N, out, bias, epi):
     M, K = a.shape
+    FLOPS[0] += 2 * M * N * K
     _n.call("pdvc_gemm3p_f32", M, N, K, _n.ptr_any(a), a.stride(0), _n.ptr(planes), _n.ptr_any(out), out.stride(0),
             _n.ptr(bias), epi, _n.stream())
     return out
@@ -66,7 +70,7 @@ def addmm_nt(bias, x, W, relu=False):
     """torch.addmm(bias, x, W.t()) (bias may be None), + ReLU when relu=True."""
     M, K = x.shape
     N = W.shape[0]
-    if not _use(M, K, x, W) or not W.is_contiguous() or (bias is not None and not bias.is_contiguous()):
+    if not _use(M, K, x, W, extra=W.is_contiguous() and (bias is None or bias.is_contiguous())):
         if bias is None:
             y = torch.mm(x, W.t())
             return y.relu_() if relu else y
@@ -89,7 +93,7 @@ def mm_dgrad(dy, W, out=None):
     """dy @ W for dy (M, O) and W (O, I): the input gradient of y = x W^T.  out given (M, I): out += dy @ W."""
     M, K = dy.shape
     N = W.shape[1]
-    ok = _use(M, K, dy, W) and W.is_contiguous() and (out is None or (_rows_ok(out) and out.shape == (M, N)))
+    ok = _use(M, K, dy, W, extra=W.is_contiguous() and (out is None or (_rows_ok(out) and out.shape == (M, N))))
     if not ok:
         return torch.mm(dy, W) if out is None else out.addmm_(dy, W)
     planes = split_planes(W, 0, N, K)
@@ -110,14 +114,15 @@ def mm_wgrad(gy, x, out=None):
     in a fixed order).  out: a contiguous (O, I) destination (written, not accumulated)."""
     rows, O = gy.shape
     I = x.shape[1]
-    ok = (_use(rows, 32, gy, x) and O % 4 == 0 and I % 4 == 0 and rows % 32 == 0
-          and (out is None or (out.is_contiguous() and out.shape == (O, I))))
+    ok = _use(rows, 32, gy, x, extra=(O % 4 == 0 and I % 4 == 0 and rows % 32 == 0
+                                      and (out is None or (out.is_contiguous() and out.shape == (O, I)))))
     if not ok:
         return None
     if out is None:
         out = torch.empty((O, I), dtype=torch.float32, device=gy.device)
-    tiles = ((O + 255) // 256) * ((I + 127) // 128)
+    tiles = ((O + 255) // 256) * ((I + 255) // 256)  # gemm3w tiles
     splits = wgrad_splits(rows, tiles)
+    FLOPS[0] += 2 * rows * O * I
     ws = torch.empty(splits * O * I if splits > 1 else 0, dtype=torch.float32, device=gy.device)
     _n.call("pdvc_gemm3_f32", O, I, rows, _n.ptr_any(gy), gy.stride(0), 0, _n.ptr_any(x), x.stride(0), 0,
             _n.ptr_any(out), I, None, 0, splits, _n.ptr(ws) if splits > 1 else None, _n.stream())
