@@ -29,6 +29,7 @@ from torch import nn
 from pdvc import _native as _n
 from pdvc.ops.functions import CaptionDecodeFunction
 from pdvc.caption_tokens import DeferredLogprobs, pack_rows
+from pdvc.ops.functions.gemm3 import addmm_nt, mm_dgrad, mm_nt, mm_wgrad
 from pdvc.ops.functions.logprob import logprob_pick
 from pdvc.ops.modules import MSDeformAttnCap
 from pdvc.ops.modules.linear import Linear
@@ -71,7 +72,7 @@ class _WordGates(torch.autograd.Function):
     def forward(ctx, weight, W_x, idx, act):
         ctx.save_for_backward(weight, W_x, idx, act)
         xt = weight.index_select(0, idx.reshape(-1))
-        return torch.mm(xt, W_x.t()).view(*idx.shape, W_x.shape[0])
+        return mm_nt(xt, W_x).view(*idx.shape, W_x.shape[0])
 
     @staticmethod
     def backward(ctx, g):
@@ -82,8 +83,10 @@ class _WordGates(torch.autograd.Function):
         gs.masked_fill_((act >= N)[:, None], 0.0)  # padding entries: no contribution
         ids = idx.reshape(-1).index_select(0, a)
         xs = weight.index_select(0, ids)  # the embedding rows again (not saved: (n R, E) floats)
-        dW_x = torch.mm(gs.t(), xs)
-        dw = weight.new_zeros(weight.shape).index_add_(0, ids, torch.mm(gs, W_x))
+        dW_x = mm_wgrad(gs, xs)
+        if dW_x is None:
+            dW_x = torch.mm(gs.t(), xs)
+        dw = weight.new_zeros(weight.shape).index_add_(0, ids, mm_dgrad(gs, W_x))
         return dw, dW_x, None, None
 
 
@@ -285,7 +288,7 @@ class LSTMDSACaptioner(Captioner):
         v = value.view(Nv, S, M, D)
         if mask_u8 is not None:
             v = v.masked_fill(mask_u8.view(Nv, S, 1, 1).bool(), 0.0)
-        U = torch.addmm(core.ctx2att.bias, v.reshape(-1, D), core.ctx2att.weight.t())
+        U = addmm_nt(core.ctx2att.bias, v.reshape(-1, D), core.ctx2att.weight)
         return U.view(Nv, S, M, -1)
 
     def _step_fused(self, w, b, t, h, c, x_gates, hs_part, off_hs, value, mask_u8, row_video, ref_rows, rd1_rows,

@@ -23,6 +23,7 @@ from torch.autograd.function import once_differentiable
 
 from pdvc import _native as _n
 from pdvc.precision import bf16_active, fp32_gemms
+from .gemm3 import addmm_nt, mm_dgrad
 from .linear import colsum, tag_level_sums, wgrad_mm
 from .ms_deform_attn_func import NUM_SAMPLES, _levels
 
@@ -54,9 +55,15 @@ def _aligned16(*ptrs):
 
 
 def _gemm(inp, a, b, out, b16):
-    """out = inp + a @ b (inp None: a @ b), fp32 out; b16: a rounded to bf16 here, b already bf16."""
+    """out = inp + a @ b (inp None: a @ b), fp32 out; b16: a rounded to bf16 here, b already bf16.  inp is a bias
+    vector or `out` itself (accumulate).  fp32: b = W^T (a weight's transposed view) or W -- the forward product and
+    the input gradient of a projection -- on the split-bf16 GEMM (ops/functions/gemm3.py) where it takes the shape."""
     if b16 is None:
-        if inp is None:
+        if b.dim() == 2 and b.stride(0) == 1 and b.t().is_contiguous() and (inp is None or inp.dim() == 1):
+            addmm_nt(inp, a, b.t(), out=out)
+        elif b.is_contiguous() and (inp is None or inp is out):
+            mm_dgrad(a, b, out=out, accumulate=inp is not None)
+        elif inp is None:
             torch.mm(a, b, out=out)
         else:
             torch.addmm(inp, a, b, out=out)
@@ -132,7 +139,7 @@ class CaptionDecodeFunction(Function):
         if (CTX2ATT_GATHER and 32 <= A <= 512 and A & (A - 1) == 0 and n * R * M * NS > Nv * S * M
                 and u_bytes <= U_MAX_BYTES):
             vm = value if pad_mask is None else value.masked_fill(pad_mask.view(Nv, S, 1, 1).bool(), 0.0)
-            U = torch.addmm(b_ctx, vm.view(-1, D), W_ctx.t()).view(Nv, S, M, A)
+            U = addmm_nt(b_ctx, vm.view(-1, D), W_ctx).view(Nv, S, M, A)
         # the backward in the same form (U_GRAD): dATT is scattered onto the value rows once (dU), so dW_ctx = dU^T vm
         # and the value gradient's ctx2att part dU W_ctx are GEMMs over N*S rows instead of n*R*16, and the
         # location gradient of att is read off U at the sample corners (pdvc_cap_gather_backward2_f32)
@@ -328,11 +335,11 @@ class CaptionDecodeFunction(Function):
             dW_ctx = wgrad_mm(dU2, vm.reshape(-1, D))
             db_ctx = lsU.view(-1, A).sum(0)  # the weights of a sample sum to 1: sum dU = sum dATT
             if pad_mask is None:
-                gv.view(-1, D).addmm_(dU2, W_ctx)
+                mm_dgrad(dU2, W_ctx, out=gv.view(-1, D))
                 if lsums is not None:  # the level sums of gv gain those of dU W_ctx
                     lsums.view(-1, D).addmm_(lsU.view(-1, A), W_ctx)
             else:  # vm = value with its padded rows zeroed: no gradient reaches them
-                t = torch.mm(dU2, W_ctx).view(Nv, S, M, D)
+                t = mm_dgrad(dU2, W_ctx).view(Nv, S, M, D)
                 gv.add_(t.masked_fill_(pad_mask.view(Nv, S, 1, 1).bool(), 0.0))
                 lsums = None  # (the consumer falls back to a column sum)
         else:

@@ -66,18 +66,27 @@ def _gemm3p(a, planes, N, out, bias, epi):
     return out
 
 
-def addmm_nt(bias, x, W, relu=False):
-    """torch.addmm(bias, x, W.t()) (bias may be None), + ReLU when relu=True."""
+def addmm_nt(bias, x, W, relu=False, out=None):
+    """torch.addmm(bias, x, W.t()) (bias may be None), + ReLU when relu=True; out: an (M, N) row-strided
+    destination (written)."""
     M, K = x.shape
     N = W.shape[0]
-    if not _use(M, K, x, W, extra=W.is_contiguous() and (bias is None or bias.is_contiguous())):
+    ok_out = out is None or (_rows_ok(out) and out.shape == (M, N))
+    if not _use(M, K, x, W, extra=W.is_contiguous() and (bias is None or bias.is_contiguous()) and ok_out):
+        if out is not None:
+            if bias is None:
+                torch.mm(x, W.t(), out=out)
+            else:
+                torch.addmm(bias, x, W.t(), out=out)
+            return out.relu_() if relu else out
         if bias is None:
             y = torch.mm(x, W.t())
             return y.relu_() if relu else y
         if relu:
             return torch._addmm_activation(bias, x, W.t(), use_gelu=False)
         return torch.addmm(bias, x, W.t())
-    out = torch.empty((M, N), dtype=torch.float32, device=x.device)
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=x.device)
     epi = 0 if bias is None else (2 if relu else 1)
     if bias is None and relu:
         _gemm3p(x, split_planes(W, 1, N, K), N, out, None, 0)
@@ -85,21 +94,24 @@ def addmm_nt(bias, x, W, relu=False):
     return _gemm3p(x, split_planes(W, 1, N, K), N, out, bias, epi)
 
 
-def mm_nt(x, W):
-    return addmm_nt(None, x, W)
+def mm_nt(x, W, out=None):
+    return addmm_nt(None, x, W, out=out)
 
 
-def mm_dgrad(dy, W, out=None):
-    """dy @ W for dy (M, O) and W (O, I): the input gradient of y = x W^T.  out given (M, I): out += dy @ W."""
+def mm_dgrad(dy, W, out=None, accumulate=True):
+    """dy @ W for dy (M, O) and W (O, I): the input gradient of y = x W^T.  out given (M, I): out += dy @ W, or
+    out = dy @ W with accumulate=False."""
     M, K = dy.shape
     N = W.shape[1]
     ok = _use(M, K, dy, W, extra=W.is_contiguous() and (out is None or (_rows_ok(out) and out.shape == (M, N))))
     if not ok:
-        return torch.mm(dy, W) if out is None else out.addmm_(dy, W)
+        if out is None:
+            return torch.mm(dy, W)
+        return out.addmm_(dy, W) if accumulate else torch.mm(dy, W, out=out)
     planes = split_planes(W, 0, N, K)
     if out is None:
         return _gemm3p(dy, planes, N, torch.empty((M, N), dtype=torch.float32, device=dy.device), None, 0)
-    return _gemm3p(dy, planes, N, out, None, 3)
+    return _gemm3p(dy, planes, N, out, None, 3 if accumulate else 0)
 
 
 def wgrad_splits(rows, tiles):

@@ -178,7 +178,7 @@ class PackedLinearFunction(Function):
         r0 = 0
         for x, r in zip(xs, rows):
             x2 = x.reshape(-1, x.shape[-1])
-            y = torch.addmm(bias[r0:r0 + r], x2, weight[r0:r0 + r].t())
+            y = addmm_nt(bias[r0:r0 + r], x2, weight[r0:r0 + r])
             outs.append(y.view(*x.shape[:-1], r))
             r0 += r
         ctx.rows = rows
@@ -200,7 +200,7 @@ class PackedLinearFunction(Function):
                 continue
             g2 = g.reshape(-1, r).contiguous()
             w = weight[r0:r0 + r]
-            gxs.append(torch.mm(g2, w).view(shp) if ctx.needs_input_grad[3 + len(gxs)] else None)
+            gxs.append(mm_dgrad(g2, w).view(shp) if ctx.needs_input_grad[3 + len(gxs)] else None)
             wgrad_mm(g2, x2, out=gw[r0:r0 + r])
             colsum(g2, out=gb[r0:r0 + r])
             r0 += r
