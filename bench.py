@@ -792,7 +792,30 @@ def main():
             groof["traffic"] = g.get("bytes_per_step")
             groof["traffic_unit"] = "HBM bytes per step, every library GEMM launch (eager step)"
             groof["traffic_source"] = os.path.relpath(gfile, ROOT)
-        result["roofline"] = groof
+        g3 = groof.get("gemm3")
+        if g3 is not None:
+            # the dominant kernel family is the in-tree split-bf16 GEMM: `roofline` prices it -- algorithmic fp32
+            # flops (2mnk) over its device time, against the ceiling of the six-product scheme on the bf16 matrix
+            # cores (dense bf16 peak / 6); the fp32-input MFMA peak (157.3) and the whole GEMM mix ride beside it
+            g3file = latest_profile(f"gemm3_traffic_{a.workload}.json")
+            traffic = None
+            if g3file and B == WORKLOADS[a.workload].get("videos_per_gpu", 1024):
+                with open(g3file) as f:
+                    traffic = json.load(f).get("bytes_per_step")
+            from pdvc.ops.functions.gemm3 import EXECUTED_PER_ALGORITHMIC as X
+            top = {"kernel": g3["kernel"], "bound": "mfma", "achieved": g3["fp32_equivalent_tfs"],
+                   "peak": BF16_MFMA_PEAK_TFS / X, "unit": "TFLOP/s", "frac": g3["fp32_equivalent_tfs"] * X / BF16_MFMA_PEAK_TFS,
+                   "traffic": traffic, "traffic_unit": "HBM bytes per step over every gemm3 launch (PMC, eager step)",
+                   "traffic_source": os.path.relpath(g3file, ROOT) if traffic is not None else None,
+                   "peak_note": f"dense bf16 MFMA peak {BF16_MFMA_PEAK_TFS:.0f} / {X} bf16 products per fp32 product; "
+                                f"the f32-input MFMA peak is {F32_MFMA_PEAK_TFS} (achieved / that = "
+                                f"{g3['fp32_equivalent_tfs'] / F32_MFMA_PEAK_TFS:.3f})",
+                   "gflop_per_step": g3["gflop_per_step"], "device_ms_per_step": g3["device_ms_per_step"],
+                   "launches_per_step": g3["launches_per_step"], "timing": groof.get("timing"),
+                   "all_gemms": {k: v for k, v in groof.items() if k not in ("gemm3", "timing")}}
+            result["roofline"] = top
+        else:
+            result["roofline"] = groof
     elif "roofline_gather" in result:
         result["roofline"] = result["roofline_gather"]
     if dropin is not None:

@@ -22,6 +22,8 @@
 // lines for k-contiguous operands; 4 x 4 micro-blocks transposed in registers for mn-contiguous ones), split, and
 // written as three bf16 plane images [row][32 k] (64-B rows; the 16-B k-chunk index XOR-swizzled by (row >> 2) & 3,
 // so the 16-lane groups of a fragment read hit 16 distinct 16-B bank slots), double buffered: one barrier a stage.
+#include <type_traits>
+
 #include "pdvc_common.h"
 
 namespace pdvc {
@@ -454,11 +456,14 @@ __global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, cons
         else __builtin_amdgcn_s_waitcnt(0x0F70);
     }
     __syncthreads();
-    for (int s = 0; s < nst; ++s) {
+    // one stage; the staging work is compile-time unconditional in the main loop (MORE, MORE2 = true), so the split /
+    // store / DMA / load instructions share one basic block with the MFMAs and the scheduler can interleave them (as
+    // runtime branches they were separate blocks, each run with the matrix pipe idle); the last two stages are peeled
+    auto stage = [&](int s, auto MORE_, auto MORE2_) {
+        constexpr bool more = decltype(MORE_)::value, more2 = decltype(MORE2_)::value;
         const char* cur = lds + (s % NSTAGE) * STAGE;
         char* nx1 = lds + ((s + 1) % NSTAGE) * STAGE;
         char* nx2 = lds + ((s + 2) % NSTAGE) * STAGE;
-        const bool more = s + 1 < nst, more2 = s + 2 < nst;
         bf16x8 fa[4][3], fb[2][3];
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -480,13 +485,22 @@ __global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, cons
             }
             // stage s + 1's A rows split into its buffer (the compiler waits for them: loaded a stage ago, and with
             // them every older DMA -- stage s + 1's), then stage s + 2's DMAs and rows, two stages ahead
-            if (more && q >= 2 && q < 2 + NUA && (G3_ABLATE & 1) == 0) ra.store(q - 2, nx1);
-            if (more2 && q == 2 + NUA && (G3_ABLATE & 8) == 0) b_dma(nx2, (s + 2) * KS);
-            if (more2 && q == 2 + NUA && (G3_ABLATE & 2) == 0) ra.load(A, lda, m0, (s + 2) * KS, M);
+            if constexpr (more && (G3_ABLATE & 1) == 0)
+                if (q >= 2 && q < 2 + NUA) ra.store(q - 2, nx1);
+            if constexpr (more2 && (G3_ABLATE & 8) == 0)
+                if (q == 2 + NUA) b_dma(nx2, (s + 2) * KS);
+            if constexpr (more2 && (G3_ABLATE & 2) == 0)
+                if (q == 2 + NUA) ra.load(A, lda, m0, (s + 2) * KS, M);
         }
-        if (more && !more2) __builtin_amdgcn_s_waitcnt(0x0F70);  // the last stage's DMAs (no later rows to wait on)
+        if constexpr (more && !more2) __builtin_amdgcn_s_waitcnt(0x0F70);  // the last stage's DMAs (nothing later)
         __syncthreads();
-    }
+    };
+    using T_ = std::integral_constant<bool, true>;
+    using F_ = std::integral_constant<bool, false>;
+    int s = 0;
+    for (; s + 2 < nst; ++s) stage(s, T_{}, T_{});
+    if (s + 1 < nst) stage(s++, T_{}, F_{});
+    if (s < nst) stage(s, F_{}, F_{});
 
     const bool full = m0 + BM <= M && n0 + BN <= N;
     if (full) store_tile<EPI, true, 4, 2>(acc, C, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h);
@@ -551,14 +565,19 @@ struct Regs {  // one stage of both operands: float4 u = t + 512 i (i = 0, 1) is
 template <int EPI>
 __global__ __launch_bounds__(NT, 1) void gemm3w_kernel(int M, int N, int K, const float* __restrict__ A, long lda,
                                                        const float* __restrict__ B, long ldb, float* __restrict__ C,
-                                                       long ldc, int k_per_split, int tiles_n, long slab) {
+                                                       long ldc, int k_per_split, int tiles_n, long slab, int nsplit) {
     using namespace w3;
     __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    // one 1-D grid over (split, tile): the output tiles of one row chunk are consecutive logical blocks, so they run
+    // together on one XCD and read the chunk's rows of both operands from its L2 (a (tile, split) grid dealt them
+    // to different XCDs: every tile fetched its rows from HBM -- 7.0 GB per 512 x 512 launch for 4.0 of operands)
+    const int lid = xcd_remap(blockIdx.x, gridDim.x);
+    const int tiles = gridDim.x / nsplit;
+    const int zz = lid / tiles, tile = lid - zz * tiles;
     const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
-    const int kb = blockIdx.z * k_per_split;
+    const int kb = zz * k_per_split;
     const int nst = (min(K, kb + k_per_split) - kb) / KS;
     const int wm = (wid >> 2) * 128, wn = (wid & 3) * 64;
     const int l32 = lane & 31, h = lane >> 5;
@@ -579,10 +598,11 @@ __global__ __launch_bounds__(NT, 1) void gemm3w_kernel(int M, int N, int K, cons
         if (nst > 1) rg.load(A, lda, m0, M, B, ldb, n0, N, kb + KS);
     }
     __syncthreads();
-    for (int s = 0; s < nst; ++s) {
+    // the main loop's stages are branch-free (compile-time MORE / MORE2), the last two peeled (gemm3p)
+    auto stage = [&](int s, auto MORE_, auto MORE2_) {
+        constexpr bool more = decltype(MORE_)::value, more2 = decltype(MORE2_)::value;
         const char* cur = lds + (s & 1) * STAGE;
         char* nxt = lds + ((s + 1) & 1) * STAGE;
-        const bool more = s + 1 < nst, more2 = s + 2 < nst;
         bf16x8 fa[4][3], fb[2][3];
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -596,13 +616,21 @@ __global__ __launch_bounds__(NT, 1) void gemm3w_kernel(int M, int N, int K, cons
         for (int q = 0; q < 8; ++q) {
             const int i = q >> 1, j = q & 1;
             acc[i][j] = mfma6(fa[i], fb[j], acc[i][j]);
-            if (more && q >= 1 && q <= 4) rg.store(q - 1, nxt);  // stage s + 1 into the other buffer
-            if (more2 && q == 5) rg.load(A, lda, m0, M, B, ldb, n0, N, kb + (s + 2) * KS);
+            if constexpr (more)
+                if (q >= 1 && q <= 4) rg.store(q - 1, nxt);  // stage s + 1 into the other buffer
+            if constexpr (more2)
+                if (q == 5) rg.load(A, lda, m0, M, B, ldb, n0, N, kb + (s + 2) * KS);
         }
         __syncthreads();
-    }
+    };
+    using T_ = std::integral_constant<bool, true>;
+    using F_ = std::integral_constant<bool, false>;
+    int s = 0;
+    for (; s + 2 < nst; ++s) stage(s, T_{}, T_{});
+    if (s + 1 < nst) stage(s++, T_{}, F_{});
+    if (s < nst) stage(s, F_{}, F_{});
     (void)l32;
-    float* Cz = C + (EPI == EPI_SLAB ? (long)blockIdx.z * slab : 0);
+    float* Cz = C + (EPI == EPI_SLAB ? (long)zz * slab : 0);
     const bool full = m0 + BM <= M && n0 + BN <= N;
     if (full) store_tile<EPI, true, 4, 2>(acc, Cz, ldc, nullptr, m0 + wm, n0 + wn, M, N, l32, h);
     else store_tile<EPI, false, 4, 2>(acc, Cz, ldc, nullptr, m0 + wm, n0 + wn, M, N, l32, h);
@@ -689,11 +717,12 @@ extern "C" int pdvc_gemm3_f32(int M, int N, int K, const float* A, long lda, int
         int kpw = (K + splits - 1) / splits;
         kpw = (kpw + w3::KS - 1) / w3::KS * w3::KS;
         const int nzw = K == 0 ? 1 : (K + kpw - 1) / kpw;
-        const dim3 gw((unsigned)(wm_ * wn_), 1, (unsigned)nzw);
+        PDVC_CHECK_ARG(wm_ * wn_ * nzw < (1L << 31), "too many tiles");
+        const dim3 gw((unsigned)(wm_ * wn_ * nzw));
         float* dw = nzw > 1 ? workspace : C;
         const long ldw = nzw > 1 ? N : ldc;
-        if (nzw > 1) hipLaunchKernelGGL(gemm3w_kernel<EPI_SLAB>, gw, dim3(NT), 0, s, M, N, K, A, lda, B, ldb, dw, ldw, kpw, (int)wn_, slab_n);
-        else hipLaunchKernelGGL(gemm3w_kernel<EPI_STORE>, gw, dim3(NT), 0, s, M, N, K, A, lda, B, ldb, dw, ldw, kpw, (int)wn_, slab_n);
+        if (nzw > 1) hipLaunchKernelGGL(gemm3w_kernel<EPI_SLAB>, gw, dim3(NT), 0, s, M, N, K, A, lda, B, ldb, dw, ldw, kpw, (int)wn_, slab_n, nzw);
+        else hipLaunchKernelGGL(gemm3w_kernel<EPI_STORE>, gw, dim3(NT), 0, s, M, N, K, A, lda, B, ldb, dw, ldw, kpw, (int)wn_, slab_n, nzw);
         PDVC_CHECK_LAUNCH("gemm3w_kernel");
         if (nzw > 1) {
             const long n4 = slab_n / 4;

@@ -4,8 +4,9 @@ MI355X_MICROARCH.md section HBM: FETCH_SIZE counts half the bytes of a wide stre
 by (kernel, grid); the groups are printed by total bytes, and the JSON holds the per-step total over `steps` steps
 and the largest group's bytes per launch.
 
-    python tools/pmc_gemm.py DIR STEPS OUT.json
+    python tools/pmc_gemm.py DIR STEPS OUT.json [NAME_REGEX]   (default Cijk_; e.g. "gemm3" for the in-tree kernels)
 """
+import re
 import collections
 import csv
 import glob
@@ -14,12 +15,15 @@ import os
 import sys
 
 
+PAT = re.compile(sys.argv[4] if len(sys.argv) > 4 else "Cijk_")
+
+
 def read(root, sub, counter):
     vals, meta = collections.defaultdict(float), {}
     for f in glob.glob(os.path.join(root, sub, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             name = r.get("Kernel_Name", "")
-            if "Cijk_" not in name or r.get("Counter_Name") != counter:
+            if not PAT.search(name) or r.get("Counter_Name") != counter:
                 continue
             d = r.get("Dispatch_Id") or r.get("Correlation_Id")
             vals[d] += float(r["Counter_Value"])
@@ -46,7 +50,7 @@ def main():
     total = sum(r[0] for r in rows)
     for b, n, name, grid in rows[:12]:
         print(f"{b / 1e9:9.3f} GB  {n:4d} launches  {b / max(n, 1) / 1e6:9.1f} MB/launch  grid {grid}  {name}")
-    res = {"formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 bytes, Cijk_ kernels", "steps": steps,
+    res = {"formula": f"(2*FETCH_SIZE + WRITE_SIZE) * 1024 bytes, kernels matching {PAT.pattern!r}", "steps": steps,
            "bytes_per_step": total / max(steps, 1),
            "largest_group": {"kernel": rows[0][2], "grid": rows[0][3], "launches": rows[0][1],
                              "bytes_per_launch": rows[0][0] / max(rows[0][1], 1)} if rows else None}

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(pwd)}" || exit 1
 export TMPDIR=/tmp
 WL=${WL:-yc2_tsp_bf16}
 O=gpurun_out/${TAG:-pmc_$WL}; mkdir -p $O
-for k in msda1d_fwd msda1d_bwd Cijk_; do
+for k in msda1d_fwd msda1d_bwd Cijk_ gemm3; do
   for c in FETCH_SIZE WRITE_SIZE; do
     d=fetch; [ $c = WRITE_SIZE ] && d=write
     echo "[$(date +%T)] pmc $k $c"
@@ -21,4 +21,5 @@ python tools/pmc_traffic.py "$O/msda1d_bwd" msda1d_bwd_query_pyr "$O/msda1d_bwd_
 python tools/pmc_traffic.py "$O/msda1d_bwd" msda1d_bwd_query_dot "$O/msda1d_bwd_query_dot_traffic_$WL.json" --largest-grid | tail -2
 python tools/pmc_traffic.py "$O/msda1d_bwd" msda1d_bwd_value "$O/msda1d_bwd_value_enc_traffic_$WL.json" --large-launches | tail -2
 python tools/pmc_gemm.py "$O/Cijk_" 3 "$O/gemm_traffic_$WL.json" | tail -3
+python tools/pmc_gemm.py "$O/gemm3" 3 "$O/gemm3_traffic_$WL.json" "gemm3p?_kernel|gemm3w_kernel" | tail -3
 echo "[$(date +%T)] done"
