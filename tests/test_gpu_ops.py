@@ -471,6 +471,40 @@ def test_fused_msda1d_windowed_full_size_vs_oracle(offset_scale, ref_dim):
     close(p.grad, egp, 1e-4, "grad_proj")
 
 
+@pytest.mark.parametrize("ref_dim", [1, 2])
+def test_fused_msda1d_headline_encoder_backward_vs_oracle(ref_dim):
+    """The headline encoder call (T = 512: S = Lq = 960, M = 8, D = 64) over two videos with padded tails (the
+    whole-pyramid forward and backward-query kernels, the value gradient's counting sort and walk over 960 queries)
+    against the float64 oracle; masked rows get a zero gradient."""
+    from pdvc.ops.functions import MSDA1dFunction
+    rng = np.random.RandomState(50 + ref_dim)
+    T_l = [512, 256, 128, 64]
+    S = sum(T_l)
+    M, D, N, Lq = 8, 64, 2, S
+    value = rng.randn(N, S, M, D)
+    proj = np.concatenate([rng.randn(N, Lq, M * 16) * 3.0, rng.randn(N, Lq, M * 16)], -1)
+    centre = np.concatenate([(np.arange(t) + 0.5) / t for t in T_l])[None, :, None, None].repeat(4, 2)
+    centre = np.repeat(centre, N, 0)
+    ref = centre if ref_dim == 1 else np.concatenate([centre, rng.uniform(0.05, 0.5, size=(N, Lq, 4, 1))], -1)
+    proj = _away_from_cell_edges(proj, ref, T_l, M)
+    mask = np.zeros((N, S), bool)
+    mask[1, 400:512] = True
+    mask[1, 700:768] = True
+    mask[0, 950:960] = True
+    gout = rng.randn(N, Lq, M * D)
+    eo, egv, egp, egr = expected_msda1d(value, mask, proj, ref, T_l, M, gout)
+    v = cu(value, torch.float32).requires_grad_()
+    p = cu(proj, torch.float32).requires_grad_()
+    r = cu(ref, torch.float32).requires_grad_()
+    out = MSDA1dFunction.apply(v, cu(mask).view(torch.uint8), p, r, tuple(T_l), 0, M * 16)
+    close(out, eo, 1e-4, "out")
+    out.backward(cu(gout, torch.float32))
+    close(v.grad, egv, 1e-4, "grad_value")
+    close(p.grad, egp, 1e-4, "grad_proj")
+    close(r.grad, egr, 1e-4, "grad_ref")
+    assert float(v.grad[1, 400:512].abs().max()) == 0.0
+
+
 def _away_from_cell_edges(proj, ref, T_l, M, margin=2e-3):
     """Nudge the sampling offsets so that no sample's x = loc * T - 0.5 lies within `margin` of an integer: the
     location gradient T * a * (v[x0 + 1] - v[x0]) . g is a step function of x, so at T = 1024 an fp32 location a few
@@ -814,11 +848,13 @@ def test_module_msdeformattn_vs_golden(ref_dim):
 
 
 @pytest.mark.parametrize("D,T_l,Lq,masked", [(64, (40, 20, 10, 5), 37, True), (64, (128, 64, 32, 16), 240, False),
+                                             (64, (512, 256, 128, 64), 960, True), (64, (512, 256, 128, 64), 100, True),
                                              (64, (1024, 512, 256, 128), 1920, True), (32, (40, 20, 10, 5), 37, True)])
 def test_msda1d_value_level_sums(D, T_l, Lq, masked):
     """pdvc_msda1d_backward_ex_f32's per-(video, level) column sums of grad_value (the value bias gradient's
-    partials) against the sums of the grad_value it returns: formed inside the D = 64 value-gradient kernel
-    (one query chunk; two chunks at S = 1920, the second accumulating), by a second pass otherwise (D = 32)."""
+    partials) against the sums of the grad_value it returns: formed inside the D = 64 value-gradient kernel (one
+    query chunk at the encoder's Lq = 960 and the decoder's Lq = 100; two chunks at S = 1920, the second
+    accumulating), by a second pass otherwise (D = 32)."""
     from pdvc.ops.functions.ms_deform_attn_func import msda1d_backward, msda1d_forward
     rng = np.random.RandomState(D + Lq)
     M, N = 8 if D == 64 else 4, 2
