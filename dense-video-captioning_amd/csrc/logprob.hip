@@ -97,12 +97,13 @@ template <bool VEC4>
 __global__ __launch_bounds__(kLpThreads) void logprob_pick_bwd_kernel(const float* __restrict__ logp,
                                                                      const int64_t* __restrict__ target,
                                                                      const float* __restrict__ gpick, int V,
-                                                                     float* __restrict__ dx) {
+                                                                     float* __restrict__ dx, int ldo) {
     const long row = blockIdx.x;
     const float g = gpick[row];
     const int64_t t = target[row];
     const float* lr = logp + row * (long)V;
-    float* dr = dx + row * (long)V;
+    float* dr = dx + row * (long)ldo;
+    for (int j = V + threadIdx.x; j < ldo; j += kLpThreads) dr[j] = 0.f;  // a padded row's tail: zeros
     if (VEC4) {
         const int v4 = V / 4;
         const float4* l4 = reinterpret_cast<const float4*>(lr);
@@ -191,13 +192,14 @@ __global__ __launch_bounds__(kLpThreads) void logprob_pick_bwd_reg_kernel(const 
                                                                          const int64_t* __restrict__ target,
                                                                          const float* __restrict__ gpick, int V,
                                                                          float* __restrict__ dx,
-                                                                         uint16_t* __restrict__ dx16) {
+                                                                         uint16_t* __restrict__ dx16, int ldo) {
     const long row = blockIdx.x;
     const int v4 = V / 4;
     const float g = gpick[row];
     const int64_t t = target[row];
     const float4* l4 = reinterpret_cast<const float4*>(logp + row * (long)V);
-    float4* d4 = reinterpret_cast<float4*>(dx + row * (long)V);
+    float4* d4 = reinterpret_cast<float4*>(dx + row * (long)ldo);
+    for (int i = v4 + threadIdx.x; i < ldo / 4; i += kLpThreads) d4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 r[kLpKR];
 #pragma unroll
     for (int k = 0; k < kLpKR; ++k) {
@@ -301,24 +303,37 @@ extern "C" int pdvc_logprob_pick_forward_f32(const float* logits, const int64_t*
     return PDVC_OK;
 }
 
-extern "C" int pdvc_logprob_pick_backward_f32(const float* logp, const int64_t* target, const float* grad_picked,
-                                              int rows, int V, float* grad_logits, void* stream) {
-    PDVC_CHECK_ARG(rows >= 0 && V > 0, "invalid sizes (rows >= 0, V > 0)");
+static int logprob_pick_backward_impl(const float* logp, const int64_t* target, const float* grad_picked, int rows,
+                                      int V, int ldo, float* grad_logits, void* stream) {
+    PDVC_CHECK_ARG(rows >= 0 && V > 0 && ldo >= V, "invalid sizes (rows >= 0, V > 0, ld >= V)");
     PDVC_CHECK_ARG(rows == 0 || (logp && target && grad_picked && grad_logits), "null pointer");
     if (rows == 0) return PDVC_OK;
-    const bool vec4 = (V % 4) == 0 && ((uintptr_t)logp % 16) == 0 && ((uintptr_t)grad_logits % 16) == 0;
+    const bool vec4 = (V % 4) == 0 && (ldo % 4) == 0 && ((uintptr_t)logp % 16) == 0 &&
+                      ((uintptr_t)grad_logits % 16) == 0;
     hipStream_t s = (hipStream_t)stream;
     if (vec4 && V / 4 <= kLpThreads * kLpKR)
         hipLaunchKernelGGL(logprob_pick_bwd_reg_kernel, dim3((unsigned)rows), dim3(kLpThreads), 0, s, logp, target,
-                           grad_picked, V, grad_logits, (uint16_t*)nullptr);
+                           grad_picked, V, grad_logits, (uint16_t*)nullptr, ldo);
     else if (vec4)
         hipLaunchKernelGGL(logprob_pick_bwd_kernel<true>, dim3((unsigned)rows), dim3(kLpThreads), 0, s, logp,
-                           target, grad_picked, V, grad_logits);
+                           target, grad_picked, V, grad_logits, ldo);
     else
         hipLaunchKernelGGL(logprob_pick_bwd_kernel<false>, dim3((unsigned)rows), dim3(kLpThreads), 0, s, logp,
-                           target, grad_picked, V, grad_logits);
+                           target, grad_picked, V, grad_logits, ldo);
     PDVC_CHECK_LAUNCH("logprob_pick_bwd_kernel");
     return PDVC_OK;
+}
+
+extern "C" int pdvc_logprob_pick_backward_f32(const float* logp, const int64_t* target, const float* grad_picked,
+                                              int rows, int V, float* grad_logits, void* stream) {
+    return logprob_pick_backward_impl(logp, target, grad_picked, rows, V, V, grad_logits, stream);
+}
+
+// The same into rows of stride ld >= V whose columns [V, ld) are written as zeros: a K-padded operand for the logit
+// layer's input-gradient GEMM (pdvc/ops/functions/logprob.py LogitPickFunction)
+extern "C" int pdvc_logprob_pick_backward_ld_f32(const float* logp, const int64_t* target, const float* grad_picked,
+                                                 int rows, int V, int ld, float* grad_logits, void* stream) {
+    return logprob_pick_backward_impl(logp, target, grad_picked, rows, V, ld, grad_logits, stream);
 }
 
 // The bf16 mode's form (pdvc/precision.py): also writes grad_logits' bf16 rounding into grad16 -- the operand of
@@ -334,7 +349,7 @@ extern "C" int pdvc_logprob_pick_backward_f32_bf16out(const float* logp, const i
     if (!reg) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "bf16 shadow needs the register-resident row form");
     if (rows == 0) return PDVC_OK;
     hipLaunchKernelGGL(logprob_pick_bwd_reg_kernel, dim3((unsigned)rows), dim3(kLpThreads), 0, (hipStream_t)stream,
-                       logp, target, grad_picked, V, grad_logits, grad16);
+                       logp, target, grad_picked, V, grad_logits, grad16, V);
     PDVC_CHECK_LAUNCH("logprob_pick_bwd_reg_kernel");
     return PDVC_OK;
 }

@@ -30,7 +30,8 @@ from pdvc import _native as _n
 from pdvc.ops.functions import CaptionDecodeFunction
 from pdvc.caption_tokens import DeferredLogprobs, pack_rows
 from pdvc.ops.functions.gemm3 import addmm_nt, mm_dgrad, mm_nt, mm_wgrad
-from pdvc.ops.functions.logprob import logprob_pick
+from pdvc.ops.functions.linear import dense
+from pdvc.ops.functions.logprob import logit_pick
 from pdvc.ops.modules import MSDeformAttnCap
 from pdvc.ops.modules.linear import Linear
 
@@ -369,8 +370,8 @@ class LSTMDSACaptioner(Captioner):
             xe = _WordGates.apply(self.embed.weight, w["W_x"], seq[:, :n_steps].t().contiguous(), act)
         else:
             xt = embed_rows(self.embed, seq[:, :n_steps].t())  # (n, R, E): step-major, the recurrence's layout
-            xe = F.linear(xt, w["W_x"])  # loop-invariant gate parts: word part per step, event part per row
-        hs_g = F.linear(hs_rows, w["W_hs"])
+            xe = dense(xt, w["W_x"])  # loop-invariant gate parts: word part per step, event part per row
+        hs_g = dense(hs_rows, w["W_hs"])
         off_hs = F.linear(hs_rows, w["W_off_hs"], w["b_off"])
         Nv, S, _ = value.shape
         M = core.deformable_att.n_heads
@@ -385,14 +386,13 @@ class LSTMDSACaptioner(Captioner):
             R, n, H = Hd.shape
             Hp = pack_rows(Hd.reshape(R * n, H), tokens)
             tgt = pick_target[:, :n_steps].reshape(-1).index_select(0, index)
-            _, picked_p = logprob_pick(self.logit(Hp), tgt)
+            _, picked_p = logit_pick(Hp, self.logit, tgt)
             picked = Hp.new_zeros(R * n + 1).index_copy(0, scatter, picked_p)[:R * n].view(R, n)
             return DeferredLogprobs(Hd.detach(), self.logit.weight.detach().clone(),
                                     self.logit.bias.detach().clone()), picked
-        logits = self.logit(Hd)
         if pick_target is not None:
-            return logprob_pick(logits, pick_target[:, :n_steps])
-        return F.log_softmax(logits, dim=-1)
+            return logit_pick(Hd, self.logit, pick_target[:, :n_steps])
+        return F.log_softmax(self.logit(Hd), dim=-1)
 
     def decode_scheduled_sampling(self, hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten, level_T, seq,
                                   n_steps, generator=None, record=None):

@@ -60,6 +60,7 @@ SIGNATURES = {
     "pdvc_level_pos_rows_add_f32_bf16out": [_vp] * 5 + [_i] * 5 + [_vp] * 4,
     "pdvc_logprob_pick_forward_f32": [_vp, _vp, _i, _i, _vp, _vp, _vp],
     "pdvc_logprob_pick_backward_f32": [_vp, _vp, _vp, _i, _i, _vp, _vp],
+    "pdvc_logprob_pick_backward_ld_f32": [_vp, _vp, _vp, _i, _i, _i, _vp, _vp],
     "pdvc_logprob_argmax_f32": [_vp, _i, _i, _vp, _vp, _vp],
     "pdvc_seq_attention_forward_f32": [_vp, ctypes.c_long, _vp, ctypes.c_long, _vp, ctypes.c_long] + [_i] * 5
     + [_vp, _vp, _vp],

@@ -214,6 +214,9 @@ class TorchLinearFunction(Function):
     def forward(ctx, x, weight, bias, relu=False):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
+        # a strided weight view (the caption LSTM's word part W_ih[:, :E]) as a contiguous copy: the in-tree GEMMs
+        # take row-major operands (a 2048 x 512 copy against a 114688-row product)
+        weight = weight if weight.is_contiguous() else weight.contiguous()
         if relu and bias is not None and _RELU_EPILOGUE:
             y = addmm_nt(bias, x2, weight, relu=True)  # ReLU in the GEMM epilogue
         else:

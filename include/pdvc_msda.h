@@ -511,6 +511,9 @@ int pdvc_logprob_pick_forward_f32(const float* logits, const int64_t* target, in
                                   float* picked, void* stream);
 int pdvc_logprob_pick_backward_f32(const float* logp, const int64_t* target, const float* grad_picked, int rows,
                                    int V, float* grad_logits, void* stream);
+/* The same with grad_logits rows of stride ld >= V, columns [V, ld) written as zeros (a K-padded GEMM operand). */
+int pdvc_logprob_pick_backward_ld_f32(const float* logp, const int64_t* target, const float* grad_picked, int rows,
+                                      int V, int ld, float* grad_logits, void* stream);
 /* bf16 mode (pdvc/precision.py): the same, also writing grad16 = grad_logits rounded to bf16 (torch's RNE cast) --
  * only in the register-resident row form (V % 4 == 0, V <= 8192, 16-byte aligned rows; else PDVC_ERR_UNSUPPORTED
  * and nothing is launched). */

@@ -86,3 +86,36 @@ def test_logprob_argmax_matches_torch(V):
     _n.call("pdvc_logprob_argmax_f32", _n.ptr(x), R, V, _n.ptr(idx), _n.ptr(lp), _n.stream())
     assert torch.equal(idx, want_i)
     assert (lp - want_lp).abs().max().item() <= 1e-5
+
+
+@pytest.mark.parametrize("V,rows", [(5748, 9000), (1609, 8200), (37, 300)])
+def test_logit_pick_fused_matches_float64(V, rows):
+    """LogitPickFunction (the caption logit layer + logprob_pick as one node, its dlogits in rows padded to a multiple
+    of 32 columns so that dlogits @ W runs on the in-tree GEMM) against float64 torch: logp, picked and the
+    gradients of the input rows, the weight and the bias, with a gradient on logp as well."""
+    from pdvc.ops.functions.logprob import logit_pick
+    from pdvc.ops.modules.linear import Linear
+    g = torch.Generator().manual_seed(V + rows)
+    H = 512
+    layer = Linear(H, V).to(DEV)
+    with torch.no_grad():
+        layer.weight.copy_(torch.randn(V, H, generator=g) * 0.05)
+        layer.bias.copy_(torch.randn(V, generator=g) * 0.1)
+    x0 = torch.randn(rows, H, generator=g).to(DEV)
+    target = torch.randint(0, V, (rows,), generator=g).to(DEV)
+    gpick = torch.randn(rows, generator=g).to(DEV)
+    glogp = (torch.randn(rows, V, generator=g) * 1e-3).to(DEV)
+    x = x0.clone().requires_grad_(True)
+    logp, picked = logit_pick(x, layer, target)
+    ((picked * gpick).sum() + (logp * glogp).sum()).backward()
+    xr = x0.double().clone().requires_grad_(True)
+    Wr = layer.weight.detach().double().clone().requires_grad_(True)
+    br = layer.bias.detach().double().clone().requires_grad_(True)
+    lr = torch.log_softmax(xr @ Wr.t() + br, -1)
+    pr = lr.gather(1, target[:, None]).squeeze(1)
+    ((pr * gpick.double()).sum() + (lr * glogp.double()).sum()).backward()
+    close(logp, lr, TOL, "logp")
+    close(picked, pr, TOL, "picked")
+    close(x.grad, xr.grad, TOL, "grad x")
+    close(layer.weight.grad, Wr.grad, TOL, "grad W")
+    close(layer.bias.grad, br.grad, TOL, "grad b")
