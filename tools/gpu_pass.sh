@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU pass: each step writes its own timestamped log under gpurun_out/$PASS (a rerun never overwrites a failing
 # log); a step that fails, aborts or times out ends the pass (no GPU work after it).
-#   tools/r05_pass.sh PASS 'label|seconds|command' ...
+#   tools/gpu_pass.sh PASS 'label|seconds|command' ...
 PASS=$1; shift
 OUT=gpurun_out/$PASS
 mkdir -p "$OUT"
