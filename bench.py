@@ -255,6 +255,11 @@ def cpu_baseline(a, enc_layers=2, dec_layers=2):
     return {"value": 1.0 / med, "unit": "videos/s", "cores": info["threads"], "kind": "port",
             "cpu_model": info["cpu_model"], "physical_cores": info["physical_cores"],
             "usable_cpus": info["usable_cpus"], "ms_per_video": 1e3 * med,
+            "threads_note": (f"torch threads = min(usable CPUs {info['usable_cpus']}, OMP_NUM_THREADS "
+                             f"{os.environ.get('OMP_NUM_THREADS', 'unset')}): the GPU pool grants each job a CPU share "
+                             "and sets OMP_NUM_THREADS to it (16 for one GPU); the affinity mask still lists the "
+                             "whole host, whose other CPUs serve other jobs, so more threads would oversubscribe "
+                             "the share rather than add cores"),
             "sample": f"median of {info['runs']} runs (after {info['warmup']} warm-ups) of one video's MSDeformAttn "
                       f"call set ({info['calls']}), fwd+bwd, T={a.T}, M=8, D=64, L=4, P=4, fp32, "
                       f"torch.set_num_threads({info['threads']}): oracle/torch_core.py (grid_sample, border)"}

@@ -34,9 +34,12 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+#ifndef G3_AL2
+#define G3_AL2 0
+#endif
 #ifndef G3_ABLATE
 #define G3_ABLATE 0  // measurement-only builds (tools/variant_lib.sh): 1 no staging stores, 2 no staging loads, 4 no MFMA,
-                     // 8 no B-plane DMA (gemm3p)
+                     // 8 no B-plane DMA (gemm3p), 16 no gemm3p epilogue
 #endif
 
 constexpr int BK = 32;     // k per stage
@@ -374,7 +377,11 @@ struct ARegs {
 #pragma unroll
         for (int i = 0; i < NUA; ++i) {
             const int u = threadIdx.x + NT * i;
+#if G3_AL2  // measurement only: every tile reads the first 256 rows (L2-resident A)
+            const int row = (u >> 2) + 0 * m0;
+#else
             const int row = min(m0 + (u >> 2), M - 1);
+#endif
             v[i] = *reinterpret_cast<const float4*>(A + (long)row * lda + k0 + ((u & 3) << 2));
         }
     }
@@ -502,6 +509,13 @@ __global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, cons
     if (s + 1 < nst) stage(s++, T_{}, F_{});
     if (s < nst) stage(s, F_{}, F_{});
 
+    if constexpr ((G3_ABLATE & 16) != 0) {  // measurement only: no epilogue, the accumulators kept live
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[i][j]));
+        return;
+    }
     const bool full = m0 + BM <= M && n0 + BN <= N;
     if (full) store_tile<EPI, true, 4, 2>(acc, C, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h);
     else store_tile<EPI, false, 4, 2>(acc, C, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h);

@@ -63,7 +63,11 @@
  *   pdvc_gemm_f32                   <- the dense projections (nn.Linear forward/backward) of the layers
  *                                      above: MSDeformAttn value/offset/output projections
  *                                      (ms_deform_attn.py:79-126), the FFNs (deformable_transformer.py:150-156,
- *                                      240-243), fp32 on the f32-input matrix cores
+ *                                      240-243), fp32 on the f32-input matrix cores (round 1; an A/B form now)
+ *   pdvc_gemm3_f32 / pdvc_gemm3p_f32 <- the same nn.Linear products (ms_deform_attn.py:55-58,
+ *   / pdvc_split3_planes_f32           deformable_transformer.py:162-189, the caption head's gates and logits,
+ *                                      LSTM_DSA.py:112-116, 206-207): fp32 GEMM by exact three-term bf16 splitting
+ *                                      on the bf16 matrix cores, the default for encoder-scale products
  */
 #ifndef PDVC_MSDA_H
 #define PDVC_MSDA_H
