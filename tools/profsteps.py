@@ -43,10 +43,10 @@ def main():
     tot, gemm = [], []
     for w in rep:
         tot.append(sum(dur(r) for r in w))
-        gemm.append(sum(dur(r) for r in w if r["Kernel_Name"].startswith("Cijk")))
+        gemm.append(sum(dur(r) for r in w if r["Kernel_Name"].startswith("Cijk") or "pdvc::g3::" in r["Kernel_Name"]))
     med = statistics.median(tot)
     print(f"device time per replayed step: median {med:.2f} ms (min {min(tot):.2f}, max {max(tot):.2f})")
-    print(f"  GEMM {statistics.median(gemm):.2f} ms, non-GEMM {statistics.median([t - g for t, g in zip(tot, gemm)]):.2f} ms")
+    print(f"  GEMM (gemm3 + hipBLASLt) {statistics.median(gemm):.2f} ms, non-GEMM {statistics.median([t - g for t, g in zip(tot, gemm)]):.2f} ms")
     w = rep[sorted(range(len(rep)), key=lambda i: tot[i])[len(rep) // 2]]
     cat = collections.defaultdict(lambda: [0.0, 0])
     for r in w:
