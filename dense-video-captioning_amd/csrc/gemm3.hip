@@ -34,6 +34,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+#ifndef G3_ASPREAD
+#define G3_ASPREAD 1  // gemm3p: A pieces split and reloaded one per spread-out MFMA group (0: groups 2-3, reload at 4)
+#endif
 #ifndef G3_AL2
 #define G3_AL2 0
 #endif
@@ -177,6 +180,17 @@ __device__ __forceinline__ void store_tile(const f32x16 (&acc)[BI][BJ], float* _
         for (int i = 0; i < BI; ++i) {
             const int rbase = r0 + 32 * i + 4 * h;
             float* p0 = C + (long)rbase * ldc + col;
+            // accumulate: the block's 16 old values loaded before any store -- the rows are distinct (ldc >= N >= 1),
+            // but the compiler cannot prove a store leaves the next row's load alone, and interleaved it waited for
+            // every load in turn (load, vmcnt(0), add, store: 128 round trips per lane and tile)
+            float old[16];
+            if constexpr (EPI == EPI_ACCUM) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int dr = (r & 3) + 8 * (r >> 2);
+                    old[r] = (FULL || (colok && rbase + dr < M)) ? p0[(long)dr * ldc] : 0.f;
+                }
+            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int dr = (r & 3) + 8 * (r >> 2);
@@ -184,7 +198,7 @@ __device__ __forceinline__ void store_tile(const f32x16 (&acc)[BI][BJ], float* _
                     float v = acc[i][j][r] + bv;
                     if (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.f);
                     float* p = p0 + (long)dr * ldc;
-                    if (EPI == EPI_ACCUM) v += *p;
+                    if constexpr (EPI == EPI_ACCUM) v += old[r];
                     *p = v;
                 }
             }
@@ -375,7 +389,10 @@ struct ARegs {
     float4 v[NUA];
     __device__ __forceinline__ void load(const float* __restrict__ A, long lda, int m0, int k0, int M) {
 #pragma unroll
-        for (int i = 0; i < NUA; ++i) {
+        for (int i = 0; i < NUA; ++i) load1(i, A, lda, m0, k0, M);
+    }
+    __device__ __forceinline__ void load1(int i, const float* __restrict__ A, long lda, int m0, int k0, int M) {
+        {
             const int u = threadIdx.x + NT * i;
 #if G3_AL2  // measurement only: every tile reads the first 256 rows (L2-resident A)
             const int row = (u >> 2) + 0 * m0;
@@ -490,14 +507,26 @@ __global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, cons
 #pragma unroll
                 for (int p = 0; p < 3; ++p) asm volatile("" ::"v"(fa[i][p]), "v"(fb[j][p]));
             }
-            // stage s + 1's A rows split into its buffer (the compiler waits for them: loaded a stage ago, and with
-            // them every older DMA -- stage s + 1's), then stage s + 2's DMAs and rows, two stages ahead
+            // stage s + 1's A rows: piece i is split into its buffer at group QA(i) (the compiler waits for it: loaded
+            // one whole stage ago) and its register reloaded at once with stage s + 2's piece -- each piece gets a full
+            // stage to arrive and the split VALU spreads over the groups; stage s + 2's DMAs at group 4
+#if G3_ASPREAD
+            constexpr int QA0 = 1, QAS = 8 / NUA;  // pieces at groups 1, 5
+            if constexpr (more && (G3_ABLATE & 1) == 0)
+                if (q >= QA0 && (q - QA0) % QAS == 0 && (q - QA0) / QAS < NUA) ra.store((q - QA0) / QAS, nx1);
+            if constexpr (more2 && (G3_ABLATE & 2) == 0)
+                if (q >= QA0 && (q - QA0) % QAS == 0 && (q - QA0) / QAS < NUA)
+                    ra.load1((q - QA0) / QAS, A, lda, m0, (s + 2) * KS, M);
+            if constexpr (more2 && (G3_ABLATE & 8) == 0)
+                if (q == 4) b_dma(nx2, (s + 2) * KS);
+#else
             if constexpr (more && (G3_ABLATE & 1) == 0)
                 if (q >= 2 && q < 2 + NUA) ra.store(q - 2, nx1);
             if constexpr (more2 && (G3_ABLATE & 8) == 0)
                 if (q == 2 + NUA) b_dma(nx2, (s + 2) * KS);
             if constexpr (more2 && (G3_ABLATE & 2) == 0)
                 if (q == 2 + NUA) ra.load(A, lda, m0, (s + 2) * KS, M);
+#endif
         }
         if constexpr (more && !more2) __builtin_amdgcn_s_waitcnt(0x0F70);  // the last stage's DMAs (nothing later)
         __syncthreads();

@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--shapes", default="512x512,256x512,512x256", help="OxI list")
     ap.add_argument("--no-err", action="store_true")
     ap.add_argument("--mnk", default="", help="fwdp only at M,N,K (e.g. 245760,512,2048)")
+    ap.add_argument("--accum", action="store_true", help="with --mnk: also the accumulate epilogue")
     a = ap.parse_args()
     torch.manual_seed(0)
     dev = "cuda"
@@ -86,6 +87,9 @@ def main():
         planes = torch.empty(3 * Nx * Kx, dtype=torch.int16, device=dev)
         run("fwdp", Mx, Nx, Kx, lambda: gemm3p(Mx, Nx, Kx, x, Kx, W, Kx, 1, planes, y, Nx, b, 1),
             lambda: torch.addmm(b, x, W.t()), lambda: ({}, {}))
+        if a.accum:  # the accumulate epilogue (C += A B^T): the FFN's residual + input-gradient GEMM
+            run("fwdp_accum", Mx, Nx, Kx, lambda: gemm3p(Mx, Nx, Kx, x, Kx, W, Kx, 1, planes, y, Nx, None, 3),
+                lambda: y.addmm_(x, W.t()), lambda: ({}, {}))
         return
     for (O, I) in [tuple(int(v) for v in sh.split("x")) for sh in a.shapes.split(",")]:
         x = torch.randn(M, I, device=dev)
