@@ -328,6 +328,8 @@ __global__ __launch_bounds__(NT, 1) void gemm3_kernel(int M, int N, int K, const
 typedef __attribute__((address_space(3))) void g3_lds_t;
 
 // planes[p][n][k] (bf16 bits) of opB[n][k]; b_kc 1: B[n*ldb + k], 0: B[k*ldb + n].  One thread per 4 k of a row.
+// NP = 1: plane 0 only (the bf16 rounding, for the bf16 mode's product)
+template <int NP>
 __global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ B, long ldb, int b_kc, int N,
                                                            int K, uint16_t* __restrict__ planes) {
     const long n4 = (long)N * (K / 4);
@@ -341,10 +343,14 @@ __global__ __launch_bounds__(256) void split_planes_kernel(const float* __restri
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = B[(long)(k + j) * ldb + n];
         }
+        const long o = (long)n * K + k;
+        if constexpr (NP == 1) {
+            *reinterpret_cast<uint2*>(planes + o) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+            continue;
+        }
         uint2 p0, p1, p2;
         split2(v[0], v[1], p0.x, p1.x, p2.x);
         split2(v[2], v[3], p0.y, p1.y, p2.y);
-        const long o = (long)n * K + k;
         *reinterpret_cast<uint2*>(planes + o) = p0;
         *reinterpret_cast<uint2*>(planes + (long)N * K + o) = p1;
         *reinterpret_cast<uint2*>(planes + 2L * N * K + o) = p2;
@@ -376,9 +382,13 @@ __device__ __forceinline__ void planes_dma(char* dst, const uint16_t* __restrict
 // c ^ ((r >> 3) & 1), so the 16-lane groups of a fragment read and the DMA / A-row writes are conflict-free.
 namespace p3 {
 constexpr int BM = 256, BN = 256, KS = 16, RB = 32, NSTAGE = 3;
-constexpr int AIMG = 3 * BM * RB, BIMG = 3 * BN * RB, STAGE = AIMG + BIMG;  // 24 + 24 KiB
-constexpr int NUA = BM * KS / 4 / NT;                                    // A pieces (4 k of a row) per thread: 2
-constexpr int BDMA = 3 * BN * RB / 1024 / (NT / 64);                      // 1-KiB DMAs per wave per stage: 3
+constexpr int NUA = BM * KS / 4 / NT;  // A pieces (4 k of a row) per thread: 2
+// NP planes per operand: 3 = the exact fp32 product (six MFMA terms; images 24 + 24 KiB, 3 1-KiB DMAs per wave per
+// stage); 1 = the bf16 mode's product (operands rounded to bf16, one MFMA term; 8 + 8 KiB, one DMA)
+template <int NP> struct Geo {
+    static constexpr int AIMG = NP * BM * RB, BIMG = NP * BN * RB, STAGE = AIMG + BIMG;
+    static constexpr int BDMA = NP * BN * RB / 1024 / (NT / 64);
+};
 
 __device__ __forceinline__ int unit_off16(int row, int k4) {
     return row * RB + ((((k4 >> 1) ^ (row >> 3)) & 1) << 4) + ((k4 & 1) << 3);
@@ -402,9 +412,14 @@ struct ARegs {
             v[i] = *reinterpret_cast<const float4*>(A + (long)row * lda + k0 + ((u & 3) << 2));
         }
     }
+    template <int NP = 3>
     __device__ __forceinline__ void store(int i, char* __restrict__ img) const {
         const int u = threadIdx.x + NT * i;
         const int off = unit_off16(u >> 2, u & 3);
+        if constexpr (NP == 1) {  // the bf16 rounding only (v_cvt_pk_bf16_f32: RNE, torch's .to(bfloat16))
+            *reinterpret_cast<uint2*>(img + off) = make_uint2(pk_bf16(v[i].x, v[i].y), pk_bf16(v[i].z, v[i].w));
+            return;
+        }
         uint2 q0, q1, q2;
         split2(v[i].x, v[i].y, q0.x, q1.x, q2.x);
         split2(v[i].z, v[i].w, q0.y, q1.y, q2.y);
@@ -431,11 +446,12 @@ __device__ __forceinline__ void dma32(char* dst, const uint16_t* __restrict__ pl
 }
 }  // namespace p3
 
-template <int EPI>
+template <int EPI, int NP = 3>
 __global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, const float* __restrict__ A, long lda,
                                                        const uint16_t* __restrict__ planes, float* __restrict__ C,
                                                        long ldc, const float* __restrict__ bias, int tiles_n) {
     using namespace p3;
+    constexpr int AIMG = Geo<NP>::AIMG, STAGE = Geo<NP>::STAGE, BDMA = Geo<NP>::BDMA;
     __shared__ __attribute__((aligned(16))) char lds[NSTAGE * STAGE];
 
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -458,7 +474,7 @@ __global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, cons
     auto b_dma = [&](char* img, int k0) {
 #pragma unroll
         for (int q = 0; q < BDMA; ++q) {
-            const int g = wid * BDMA + q;  // 24 instructions: plane g / 8, rows 32 (g % 8) ..
+            const int g = wid * BDMA + q;  // 8 NP instructions: plane g / 8, rows 32 (g % 8) ..
             const int p = g / (BN / 32), r0 = (g % (BN / 32)) * 32;
             dma32(img + AIMG + p * BN * RB + r0 * RB, planes + p * pstride, K, n0 + r0, N, k0, lane);
         }
@@ -469,7 +485,7 @@ __global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, cons
     if (nst > 0) {
         ra.load(A, lda, m0, 0, M);
 #pragma unroll
-        for (int i = 0; i < NUA; ++i) ra.store(i, lds);  // (waits for the rows; nothing else is in flight)
+        for (int i = 0; i < NUA; ++i) ra.template store<NP>(i, lds);  // (waits for the rows; nothing else is in flight)
         b_dma(lds, 0);
         if (nst > 1) {
             b_dma(lds + STAGE, KS);
@@ -488,24 +504,27 @@ __global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, cons
         const char* cur = lds + (s % NSTAGE) * STAGE;
         char* nx1 = lds + ((s + 1) % NSTAGE) * STAGE;
         char* nx2 = lds + ((s + 2) % NSTAGE) * STAGE;
-        bf16x8 fa[4][3], fb[2][3];
+        bf16x8 fa[4][NP], fb[2][NP];
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int p = 0; p < 3; ++p)
+            for (int p = 0; p < NP; ++p)
                 fb[j][p] = *reinterpret_cast<const bf16x8*>(cur + AIMG + p * BN * RB + frag_off16(wn + 32 * j + l32, h));
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int p = 0; p < 3; ++p)
+            for (int p = 0; p < NP; ++p)
                 fa[i][p] = *reinterpret_cast<const bf16x8*>(cur + p * BM * RB + frag_off16(wm + 32 * i + l32, h));
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const int i = q >> 1, j = q & 1;
-            if constexpr ((G3_ABLATE & 4) == 0) acc[i][j] = mfma6(fa[i], fb[j], acc[i][j]);
-            else {
+            if constexpr ((G3_ABLATE & 4) != 0) {
 #pragma unroll
-                for (int p = 0; p < 3; ++p) asm volatile("" ::"v"(fa[i][p]), "v"(fb[j][p]));
+                for (int p = 0; p < NP; ++p) asm volatile("" ::"v"(fa[i][p]), "v"(fb[j][p]));
+            } else if constexpr (NP == 1) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
+            } else {
+                acc[i][j] = mfma6(fa[i], fb[j], acc[i][j]);
             }
             // stage s + 1's A rows: piece i is split into its buffer at group QA(i) (the compiler waits for it: loaded
             // one whole stage ago) and its register reloaded at once with stage s + 2's piece -- each piece gets a full
@@ -513,7 +532,7 @@ __global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, cons
 #if G3_ASPREAD
             constexpr int QA0 = 1, QAS = 8 / NUA;  // pieces at groups 1, 5
             if constexpr (more && (G3_ABLATE & 1) == 0)
-                if (q >= QA0 && (q - QA0) % QAS == 0 && (q - QA0) / QAS < NUA) ra.store((q - QA0) / QAS, nx1);
+                if (q >= QA0 && (q - QA0) % QAS == 0 && (q - QA0) / QAS < NUA) ra.template store<NP>((q - QA0) / QAS, nx1);
             if constexpr (more2 && (G3_ABLATE & 2) == 0)
                 if (q >= QA0 && (q - QA0) % QAS == 0 && (q - QA0) / QAS < NUA)
                     ra.load1((q - QA0) / QAS, A, lda, m0, (s + 2) * KS, M);
@@ -521,7 +540,7 @@ __global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, cons
                 if (q == 4) b_dma(nx2, (s + 2) * KS);
 #else
             if constexpr (more && (G3_ABLATE & 1) == 0)
-                if (q >= 2 && q < 2 + NUA) ra.store(q - 2, nx1);
+                if (q >= 2 && q < 2 + NUA) ra.template store<NP>(q - 2, nx1);
             if constexpr (more2 && (G3_ABLATE & 8) == 0)
                 if (q == 2 + NUA) b_dma(nx2, (s + 2) * KS);
             if constexpr (more2 && (G3_ABLATE & 2) == 0)
@@ -791,22 +810,23 @@ extern "C" int pdvc_gemm3_f32(int M, int N, int K, const float* A, long lda, int
     return PDVC_OK;
 }
 
-// C-ABI: see include/pdvc_msda.h
-extern "C" int pdvc_split3_planes_f32(const float* B, long ldb, int b_kc, int N, int K, uint16_t* planes,
-                                      void* stream) {
+namespace {
+int split_planes_impl(int np, const float* B, long ldb, int b_kc, int N, int K, uint16_t* planes, void* stream) {
     PDVC_CHECK_ARG(N > 0 && K > 0 && K % BK == 0, "N > 0 and K a positive multiple of 32");
     PDVC_CHECK_ARG(ldb >= (b_kc ? K : N), "leading dimension too small");
     PDVC_CHECK_ARG(!b_kc || ((uintptr_t)B % 16 == 0 && ldb % 4 == 0), "k-contiguous B: 16-byte aligned rows");
     PDVC_CHECK_ARG((uintptr_t)planes % 16 == 0, "planes must be 16-byte aligned");
     const long n4 = (long)N * (K / 4);
     const int blocks = (int)std::min<long>((n4 + 255) / 256, 4096);
-    hipLaunchKernelGGL(split_planes_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, B, ldb, b_kc, N, K, planes);
+    if (np == 1) hipLaunchKernelGGL(split_planes_kernel<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, B, ldb, b_kc, N, K, planes);
+    else hipLaunchKernelGGL(split_planes_kernel<3>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, B, ldb, b_kc, N, K, planes);
     PDVC_CHECK_LAUNCH("split_planes_kernel");
     return PDVC_OK;
 }
 
-extern "C" int pdvc_gemm3p_f32(int M, int N, int K, const float* A, long lda, const uint16_t* planes, float* C,
-                               long ldc, const float* bias, int epilogue, void* stream) {
+template <int NP>
+int gemmp_impl(int M, int N, int K, const float* A, long lda, const uint16_t* planes, float* C, long ldc,
+               const float* bias, int epilogue, void* stream) {
     PDVC_CHECK_ARG(M >= 0 && N > 0 && K >= 0 && K % BK == 0, "sizes: N > 0, K a multiple of 32");
     PDVC_CHECK_ARG(epilogue >= 0 && epilogue <= 3, "epilogue must be 0..3");
     PDVC_CHECK_ARG(epilogue != 1 && epilogue != 2 ? true : bias != nullptr, "bias epilogue needs a bias");
@@ -818,7 +838,7 @@ extern "C" int pdvc_gemm3p_f32(int M, int N, int K, const float* A, long lda, co
     PDVC_CHECK_ARG(tiles_m * tiles_n < (1L << 31), "too many tiles");
     const dim3 grid((unsigned)(tiles_m * tiles_n));
     hipStream_t s = (hipStream_t)stream;
-#define G3P_L(E) hipLaunchKernelGGL(gemm3p_kernel<E>, grid, dim3(NT), 0, s, M, N, K, A, lda, planes, C, ldc, bias, (int)tiles_n)
+#define G3P_L(E) hipLaunchKernelGGL((gemm3p_kernel<E, NP>), grid, dim3(NT), 0, s, M, N, K, A, lda, planes, C, ldc, bias, (int)tiles_n)
     switch (epilogue) {
         case 0: G3P_L(EPI_STORE); break;
         case 1: G3P_L(EPI_BIAS); break;
@@ -828,4 +848,26 @@ extern "C" int pdvc_gemm3p_f32(int M, int N, int K, const float* A, long lda, co
 #undef G3P_L
     PDVC_CHECK_LAUNCH("gemm3p_kernel");
     return PDVC_OK;
+}
+}  // namespace
+
+// C-ABI: see include/pdvc_msda.h
+extern "C" int pdvc_split3_planes_f32(const float* B, long ldb, int b_kc, int N, int K, uint16_t* planes,
+                                      void* stream) {
+    return split_planes_impl(3, B, ldb, b_kc, N, K, planes, stream);
+}
+
+extern "C" int pdvc_gemm3p_f32(int M, int N, int K, const float* A, long lda, const uint16_t* planes, float* C,
+                               long ldc, const float* bias, int epilogue, void* stream) {
+    return gemmp_impl<3>(M, N, K, A, lda, planes, C, ldc, bias, epilogue, stream);
+}
+
+// the bf16 mode's product: opB rounded to bf16 (one plane), A rounded in the kernel, one MFMA term, fp32 result
+extern "C" int pdvc_round_plane_f32(const float* B, long ldb, int b_kc, int N, int K, uint16_t* plane, void* stream) {
+    return split_planes_impl(1, B, ldb, b_kc, N, K, plane, stream);
+}
+
+extern "C" int pdvc_gemm1p_f32(int M, int N, int K, const float* A, long lda, const uint16_t* plane, float* C,
+                               long ldc, const float* bias, int epilogue, void* stream) {
+    return gemmp_impl<1>(M, N, K, A, lda, plane, C, ldc, bias, epilogue, stream);
 }

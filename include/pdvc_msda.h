@@ -574,6 +574,15 @@ int pdvc_split3_planes_f32(const float* B, long ldb, int b_kc, int N, int K, uin
 int pdvc_gemm3p_f32(int M, int N, int K, const float* A, long lda, const uint16_t* planes, float* C, long ldc,
                     const float* bias, int epilogue, void* stream);
 
+/* The bf16 mode's product (BASELINE configs[1]; pdvc/precision.py), the same call shape with one plane:
+ * pdvc_round_plane_f32 writes plane[n][k] = bf16(opB[n][k]) (round to nearest even, torch's .to(bfloat16)) and
+ * pdvc_gemm1p_f32 computes C (=|+=) sum_k bf16(A[m,k]) plane[n,k] (+ bias) (ReLU) with fp32 accumulation: A is
+ * rounded inside the kernel, so an fp32 activation needs no separate cast pass (replaces the cast + hipBLASLt bf16
+ * GEMM the mode issues for torch.addmm / mm). */
+int pdvc_round_plane_f32(const float* B, long ldb, int b_kc, int N, int K, uint16_t* plane, void* stream);
+int pdvc_gemm1p_f32(int M, int N, int K, const float* A, long lda, const uint16_t* plane, float* C, long ldc,
+                    const float* bias, int epilogue, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

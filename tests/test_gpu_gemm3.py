@@ -126,6 +126,40 @@ def test_gemm3p_matches_float64(M, N, K, bkc, epi):
     assert ours_e < 1e-6 and ours_e <= 2 * blas_e + 1e-8, (ours_e, blas_e)
 
 
+@pytest.mark.parametrize("M,N,K,bkc,epi", [(4096, 512, 512, 1, 1), (3000, 200, 96, 1, 2), (2500, 512, 256, 0, 3),
+                                           (700, 100, 64, 0, 0)])
+def test_gemm1p_is_the_bf16_operand_product(M, N, K, bkc, epi):
+    """pdvc_round_plane_f32 + pdvc_gemm1p_f32 (the bf16 mode's product): the plane is torch's RNE rounding bit for
+    bit, and C is the float64 product of the bf16-rounded operands up to fp32 accumulation (each bf16 x bf16 product
+    is exact in fp32; bound 1e-6 of sum_k |a||b|, as gemm3), and within the same bound of hipBLASLt's bf16 GEMM."""
+    _n = _lib()
+    torch.manual_seed(M + K + 1)
+    A = torch.randn(M, K + 4, device=DEV)
+    Bst = torch.randn((N, K) if bkc else (K, N), device=DEV)
+    b = Bst if bkc else Bst.t()
+    a = A[:, :K]
+    bias = torch.randn(N, device=DEV)
+    C0 = torch.randn(M, N, device=DEV)
+    C = C0.clone()
+    plane = torch.empty((N, K), dtype=torch.int16, device=DEV)
+    _n.call("pdvc_round_plane_f32", _n.ptr_any(Bst), Bst.stride(0), bkc, N, K, _n.ptr(plane), _n.stream())
+    assert torch.equal(plane.view(torch.bfloat16), b.to(torch.bfloat16))
+    _n.call("pdvc_gemm1p_f32", M, N, K, _n.ptr_any(A), K + 4, _n.ptr(plane), _n.ptr(C), N,
+            _n.ptr(bias) if epi in (1, 2) else None, epi, _n.stream())
+    a16, b16 = a.to(torch.bfloat16), b.to(torch.bfloat16)
+    ref = a16.double() @ b16.double().t()
+    scale = a16.double().abs() @ b16.double().abs().t()
+    theirs = torch.ops.aten.mm.dtype(a16, b16.t(), torch.float32)
+    if epi in (1, 2):
+        ref, theirs, scale = ref + bias.double(), theirs + bias, scale + bias.double().abs()
+    if epi == 2:
+        ref, theirs = ref.clamp_min(0), theirs.clamp_min(0)
+    if epi == 3:
+        ref, theirs, scale = ref + C0.double(), theirs + C0, scale + C0.double().abs()
+    assert scaled_err(C, ref, scale) < 1e-6
+    assert float(((C - theirs).abs().double() / scale.clamp_min(1e-300)).max()) < 1e-6
+
+
 def test_wgrad_split_is_deterministic_and_accurate():
     from pdvc.ops.functions.gemm3 import mm_wgrad
     torch.manual_seed(5)

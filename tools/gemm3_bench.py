@@ -28,6 +28,12 @@ def gemm3p(M, N, K, A, lda, B, ldb, bkc, planes, C, ldc, bias=None, epi=0):
             _n.stream())
 
 
+def gemm1p(M, N, K, A, lda, B, ldb, bkc, plane, C, ldc, bias=None, epi=0):
+    _n.call("pdvc_round_plane_f32", _n.ptr_any(B), ldb, bkc, N, K, _n.ptr_any(plane), _n.stream())
+    _n.call("pdvc_gemm1p_f32", M, N, K, _n.ptr_any(A), lda, _n.ptr_any(plane), _n.ptr_any(C), ldc, _n.ptr(bias), epi,
+            _n.stream())
+
+
 def timeit(fn, iters):
     for _ in range(3):
         fn()
@@ -57,6 +63,8 @@ def main():
     ap.add_argument("--no-err", action="store_true")
     ap.add_argument("--mnk", default="", help="fwdp only at M,N,K (e.g. 245760,512,2048)")
     ap.add_argument("--accum", action="store_true", help="with --mnk: also the accumulate epilogue")
+    ap.add_argument("--bf16", action="store_true",
+                    help="the bf16 mode's product: gemm1p against cast + hipBLASLt bf16 (fp32 result), M,N,K list")
     a = ap.parse_args()
     torch.manual_seed(0)
     dev = "cuda"
@@ -78,6 +86,57 @@ def main():
         res.append(r)
         print(json.dumps(r), flush=True)
 
+    if a.bf16:
+        aten = torch.ops.aten
+        for mnk in (a.mnk or "245760,512,512,0;245760,2048,512,0;245760,512,2048,3;245760,256,512,1").split(";"):
+            Mx, Nx, Kx, epi = (int(v) for v in mnk.split(","))
+            x = torch.randn(Mx, Kx, device=dev)
+            W = torch.randn(Nx, Kx, device=dev) / Kx ** 0.5
+            b = torch.randn(Nx, device=dev)
+            y = torch.randn(Mx, Nx, device=dev)
+            y0 = y.clone()
+            plane = torch.empty(Nx * Kx, dtype=torch.int16, device=dev)
+            bb = b if epi in (1, 2) else None
+            ours = lambda: gemm1p(Mx, Nx, Kx, x, Kx, W, Kx, 1, plane, y, Nx, bb, epi)  # noqa: E731
+            x16 = x.to(torch.bfloat16)
+
+            def theirs(cast=True):
+                xb = x.to(torch.bfloat16) if cast else x16
+                wb = W.to(torch.bfloat16)
+                if epi == 3:
+                    return aten.addmm.dtype_out(y, xb, wb.t(), torch.float32, out=y)
+                if epi == 0:
+                    return aten.mm.dtype(xb, wb.t(), torch.float32)
+                r = aten.addmm.dtype(b, xb, wb.t(), torch.float32)
+                return r.relu_() if epi == 2 else r
+            fl = 2.0 * Mx * Nx * Kx
+            r = {"op": f"bf16 epi{epi}", "M": Mx, "N": Nx, "K": Kx}
+            y.copy_(y0)
+            ours()
+            torch.cuda.synchronize()
+            sub = 4096
+            ref = x[:sub].to(torch.bfloat16).double() @ W.to(torch.bfloat16).double().t()
+            if epi in (1, 2):
+                ref = ref + b.double()
+            if epi == 2:
+                ref = ref.clamp_min(0)
+            if epi == 3:
+                ref = ref + y0[:sub].double()
+            scale = x[:sub].double().abs() @ W.double().abs().t()
+            r["err_ours_vs_bf16_operands"] = float(((y[:sub].double() - ref).abs() / scale).max())
+            r["ours_ms"] = timeit(ours, a.iters)
+            r["ours_tfs"] = fl / r["ours_ms"] / 1e9
+            r["blaslt_cast_ms"] = timeit(theirs, a.iters)
+            r["blaslt_precast_ms"] = timeit(lambda: theirs(False), a.iters)
+            r["blaslt_precast_tfs"] = fl / r["blaslt_precast_ms"] / 1e9
+            res.append(r)
+            print(json.dumps(r), flush=True)
+            del x, W, y, y0, x16
+            torch.cuda.empty_cache()
+        if a.out:
+            with open(a.out, "w") as f:
+                json.dump(res, f, indent=1)
+        return
     if a.mnk:
         Mx, Nx, Kx = (int(v) for v in a.mnk.split(","))
         x = torch.randn(Mx, Kx, device=dev)
