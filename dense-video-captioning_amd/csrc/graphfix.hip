@@ -87,3 +87,34 @@ extern "C" int pdvc_graph_replace_memsets(void* graph, int* replaced) {
     if (replaced) *replaced = done;
     return PDVC_OK;
 }
+
+// Events a captured graph records for work outside it (pdvc/distributed.py, the data-parallel overlap): torch's ROCm
+// build refuses torch.cuda.Event(external=True), so the step graph records these directly.  Recorded with
+// hipEventRecordExternal on a capturing stream, the record becomes an event-record node of the graph, and every
+// replay records the event when the node's dependencies have run; a stream outside the graph waits on it.
+extern "C" int pdvc_event_create(void** event) {
+    PDVC_CHECK_ARG(event != nullptr, "event is NULL");
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+        return pdvc_set_error(PDVC_ERR_LAUNCH, "hipEventCreateWithFlags");
+    *event = (void*)e;
+    return PDVC_OK;
+}
+
+extern "C" int pdvc_event_destroy(void* event) {
+    PDVC_CHECK_ARG(event != nullptr, "event is NULL");
+    return hipEventDestroy((hipEvent_t)event) == hipSuccess ? PDVC_OK
+                                                            : pdvc_set_error(PDVC_ERR_LAUNCH, "hipEventDestroy");
+}
+
+extern "C" int pdvc_event_record_external(void* event, void* stream) {
+    PDVC_CHECK_ARG(event != nullptr, "event is NULL");
+    const hipError_t e = hipEventRecordWithFlags((hipEvent_t)event, (hipStream_t)stream, hipEventRecordExternal);
+    return e == hipSuccess ? PDVC_OK : pdvc_set_error(PDVC_ERR_LAUNCH, "hipEventRecordWithFlags: %s", hipGetErrorString(e));
+}
+
+extern "C" int pdvc_stream_wait_event(void* stream, void* event) {
+    PDVC_CHECK_ARG(event != nullptr, "event is NULL");
+    const hipError_t e = hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0);
+    return e == hipSuccess ? PDVC_OK : pdvc_set_error(PDVC_ERR_LAUNCH, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+}

@@ -70,6 +70,10 @@ SIGNATURES = {
     "pdvc_level_pos_rows_backward_f32": [_vp, _vp] + [_i] * 4 + [_vp, _vp],
     "pdvc_level_pos_rows_add_f32": [_vp] * 5 + [_i] * 5 + [_vp, _vp, _vp],
     "pdvc_graph_replace_memsets": [_vp, _vp],
+    "pdvc_event_create": [_vp],
+    "pdvc_event_destroy": [_vp],
+    "pdvc_event_record_external": [_vp, _vp],
+    "pdvc_stream_wait_event": [_vp, _vp],
     "pdvc_box_refine_forward_f32": [_vp, _vp, ctypes.c_long, _i, _f, _vp, _vp],
     "pdvc_box_refine_backward_f32": [_vp, _vp, _vp, ctypes.c_long, _i, _f, _vp, _vp, _vp],
     "pdvc_match_cost_f32": [_vp] * 4 + [_i] * 4 + [_f] * 6 + [_vp, _vp],

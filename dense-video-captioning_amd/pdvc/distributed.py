@@ -18,11 +18,48 @@ per bucket, no set-to-None) keeps the views: backward's AccumulateGrad adds into
 all-reduce and one scale per bucket -- no concatenation, no copy back.  A caller that sets the gradients to None
 instead still gets the right result: a gradient that is not the bucket's view is copied into its slot at launch
 and the view is re-bound after the reduce (`copies` counts those copies; 0 on the resident path).
+
+Under a captured step (pdvc/step_graph.py) no host code runs during the backward, so the hooks cannot launch the
+collectives.  Instead the capture records an external event at each bucket's last gradient (begin_capture /
+end_capture: an event-record node of the graph), and after every replay finish_replay() queues bucket b's
+all-reduce on a side stream behind event b: the reduction of the buckets the backward finishes first runs while
+the replay is still computing the rest (the overlap torch DDP gets from its hooks in an eager step).
 """
+import ctypes
 import os
 
 import torch
 import torch.distributed as dist
+
+
+class GraphEvent:
+    """A HIP event that a captured graph records for streams outside it (csrc/graphfix.hip: hipEventRecordExternal
+    -- torch's ROCm build refuses torch.cuda.Event(external=True)).  record() on a capturing stream adds an
+    event-record node that every replay executes; wait(stream) queues a wait for the latest record."""
+
+    def __init__(self):
+        from pdvc import _native as _n
+        self._n = _n
+        h = ctypes.c_void_p()
+        _n.call("pdvc_event_create", ctypes.addressof(h))
+        self.handle = h
+
+    def record(self, stream=None):
+        s = stream if stream is not None else torch.cuda.current_stream()
+        self._n.call("pdvc_event_record_external", self.handle, ctypes.c_void_p(s.cuda_stream))
+
+    def wait(self, stream):
+        self._n.call("pdvc_stream_wait_event", ctypes.c_void_p(stream.cuda_stream), self.handle)
+
+    def __del__(self):
+        try:
+            self._n.call("pdvc_event_destroy", self.handle)
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
+
+def _graph_event():
+    return GraphEvent()
 
 
 def init_distributed(backend=None):
@@ -62,6 +99,9 @@ class GradAllReducer:
         self.suspended = False  # True while a step graph is captured: finish() then reduces every bucket
         self.flats = None  # one flat buffer per bucket once the active set is known
         self.copies = 0  # gradients copied into a bucket (not resident); stays 0 when zero_grad() is used
+        self.capturing = False  # inside begin_capture() .. end_capture(): bucket completions record events
+        self.events = None  # one external event per bucket, recorded by the captured step (finish_replay)
+        self._side = None
         self._hooks = []
         self._build(self.params)
 
@@ -138,6 +178,11 @@ class GradAllReducer:
         if bi is None or self.suspended:
             return
         self.pending[bi] -= 1
+        if self.capturing:  # the bucket's gradients are final at this point of the captured stream
+            if self.pending[bi] == 0:
+                self.events[bi].record()
+                self._recorded[bi] = True
+            return
         if self.active is not None:
             while self.next_launch < len(self.buckets) and self.pending[self.next_launch] == 0:
                 self._launch(self.next_launch)
@@ -178,3 +223,39 @@ class GradAllReducer:
                 if not self._resident(p):
                     p.grad = self.views[id(p)]
         self._reset()
+
+    # ---- captured steps ----------------------------------------------------------------------------
+    def begin_capture(self):
+        """Before capturing a step that ends with the buckets' gradients (after a finish(): the active set and
+        the flat buffers exist): bucket completions inside the capture record one external event each."""
+        assert self.flats is not None, "begin_capture() after the first finish()"
+        self.events = [_graph_event() for _ in self.buckets]
+        self._recorded = [False] * len(self.buckets)
+        self._reset()
+        self.capturing = True
+
+    def end_capture(self):
+        """Inside the capture, after the backward: a bucket left open by a gradient that did not arrive (a branch
+        not taken in the captured step) records its event here, where every gradient of the step is final."""
+        for bi, ev in enumerate(self.events):
+            if not self._recorded[bi]:
+                ev.record()
+        self.capturing = False
+        self._reset()
+
+    def finish_replay(self):
+        """After a replay of a step captured between begin_capture() and end_capture(): every bucket's all-reduce
+        in index order on a side stream, each behind its event, so a bucket is reduced as soon as the replay has
+        produced it; then the current stream waits for them and the rank mean is scaled in."""
+        if self._side is None:
+            self._side = torch.cuda.Stream()
+        works = []
+        with torch.cuda.stream(self._side):
+            for bi, flat in enumerate(self.flats):
+                self.events[bi].wait(self._side)
+                works.append((flat, dist.all_reduce(flat, group=self.group, async_op=True)))
+        inv = 1.0 / self.world
+        for flat, work in works:
+            work.wait()  # the current stream waits for the collective (and the side stream's position)
+            flat.mul_(inv)
+        torch.cuda.current_stream().wait_stream(self._side)

@@ -16,8 +16,9 @@ lengths: load() then also recomputes the caption rows' bookkeeping on the host a
 
 Dropout stays random per replay (torch's graph-safe Philox offsets; the HIP kernels draw their seeds on the
 device).  Gradients live in the graph's memory pool: do not set them to None between replays (the optimizer
-step and grad clipping run eagerly on them).  A GradAllReducer (data parallel) is suspended while capturing;
-replay() calls its finish() to average the gradients over ranks.  With a reducer the gradients are views into its
+step and grad clipping run eagerly on them).  A GradAllReducer (data parallel) records an event at each bucket's
+last gradient inside the capture, and replay() queues each bucket's all-reduce behind its event on a side stream
+(finish_replay: the reduction overlaps the rest of the replay).  With a reducer the gradients are views into its
 flat buckets (bucket-resident, pdvc/distributed.py): the captured step begins with the buckets' zero fill and the
 backward accumulates into them, so finish() is one all-reduce and one scale per bucket.
 
@@ -127,6 +128,58 @@ class rewriting_graphs:
         return False
 
 
+_DP_OVERLAP = []
+
+
+def dp_overlap_supported():
+    """Whether an event recorded inside a stream capture (GraphEvent, hipEventRecordExternal) gates a stream outside
+    the graph on this stack -- probed once: a captured chain of element-wise passes writes a marker, records the
+    event, then overwrites the marker; after each replay a side stream waits on the event and copies the marker,
+    which must be the first value every time (a wait that did not hold would read the zeroed or the final value).
+    A record that never fires is bounded by a host-side timeout.  PDVC_DP_OVERLAP=0 turns the overlap off."""
+    if os.environ.get("PDVC_DP_OVERLAP", "1") == "0":
+        return False
+    if not _DP_OVERLAP:
+        ok = False
+        try:
+            import time
+            from .distributed import GraphEvent
+            big = torch.ones(1 << 22, device="cuda")
+            mark = torch.zeros(1, device="cuda")
+            ev = GraphEvent()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(64):  # ~ms of work before the record
+                    big.mul_(1.0001).add_(1e-4)
+                mark.copy_(big[:1] * 0.0 + 7.0)
+                ev.record()
+                for _ in range(64):
+                    big.mul_(1.0001).add_(1e-4)
+                mark.fill_(3.0)
+            side = torch.cuda.Stream()
+            seen = []
+            for _ in range(3):
+                mark.zero_()
+                g.replay()
+                ev.wait(side)
+                with torch.cuda.stream(side):
+                    seen.append(mark.clone())
+                    done = torch.cuda.Event()
+                    done.record()
+                t0 = time.time()
+                while not done.query():
+                    if time.time() - t0 > 20.0:
+                        raise RuntimeError("the captured event never fired")
+                    time.sleep(0.001)
+            torch.cuda.synchronize()
+            ok = all(float(v) == 7.0 for v in seen)
+            del g
+        except Exception:  # noqa: BLE001 -- any failure: keep the serial reduction
+            ok = False
+        _DP_OVERLAP.append(ok)
+    return _DP_OVERLAP[0]
+
+
 class StepGraph:
     def __init__(self, model, criterion, dt, transformer_input_type="queries", warmup=2, reducer=None, debug_dot=None):
         self.model, self.criterion, self.dt, self.tit = model, criterion, dt, transformer_input_type
@@ -157,7 +210,13 @@ class StepGraph:
             self.graph.enable_debug_mode()
         from .precision import begin_capture
         begin_capture()  # bf16 mode: every operand rounding of the step becomes a node of the graph
-        if reducer is not None:
+        # data parallel: the capture records an event at each bucket's last gradient and every replay's all-reduces
+        # wait on those on a side stream (overlapped with the rest of the replay), when this build can record
+        # external events inside a capture; otherwise the reducer is suspended and finish() reduces after the replay
+        self.overlap = reducer is not None and reducer.flats is not None and dp_overlap_supported()
+        if self.overlap:
+            reducer.begin_capture()
+        elif reducer is not None:
             reducer.suspended = True
         # no garbage collection inside the capture.  Round 5 pinned the mechanism (tools/gc_capture_probe.py,
         # profiles/r05_gc_capture_probe.txt): a collection inside a capture that frees cyclic garbage holding
@@ -174,11 +233,14 @@ class StepGraph:
                 if reducer is not None and reducer.flats is not None:
                     reducer.zero_grad()  # every replay starts from zeroed buckets (a fill node per bucket)
                 self.total, self.losses = self._forward_backward()
+                if self.overlap:
+                    reducer.end_capture()
         finally:
             if gc_enabled:
                 gc.enable()
             if reducer is not None:
                 reducer.suspended = False
+                reducer.capturing = False
         if debug_dot:
             self.graph.debug_dump(debug_dot)
         # the captured outputs, detached: the storage is the graph's, but the autograd graph of the capture (and
@@ -288,5 +350,8 @@ class StepGraph:
     def replay(self):
         self.graph.replay()
         if self.reducer is not None:
-            self.reducer.finish()
+            if self.overlap:
+                self.reducer.finish_replay()
+            else:
+                self.reducer.finish()
         return self.total

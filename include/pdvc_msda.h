@@ -40,6 +40,8 @@
  *   pdvc_match_cost_f32             <- HungarianMatcher's cost matrix (pdvc/matcher.py:87-117), torch's op order
  *   pdvc_graph_replace_memsets      <- (no reference counterpart) the captured training-step graph's memset nodes
  *                                      rewritten as kernel nodes before instantiation (csrc/graphfix.hip)
+ *   pdvc_event_* / pdvc_stream_wait_event <- (no reference counterpart) the captured step's per-bucket events the
+ *                                      data-parallel all-reduces wait on (csrc/graphfix.hip)
  *   pdvc_box_refine_*               <- iterative box refinement sigmoid(tmp + inverse_sigmoid(ref)) of the
  *                                      decoder (deformable_transformer.py:303-313) and PDVC's box heads
  *                                      (pdvc/pdvc.py:245-253, misc/detr_utils/misc.py:540-544)
@@ -392,6 +394,15 @@ int pdvc_set_losses_backward_f32(const float* grad_losses, const float* dlogit, 
  * with the same dependencies; *replaced receives the count.  Small memset nodes did not re-apply on replays on this
  * ROCm stack. */
 int pdvc_graph_replace_memsets(void* graph, int* replaced);
+
+/* Events a captured graph records for streams outside it (the data-parallel all-reduce overlap, pdvc/distributed.py;
+ * no reference counterpart: the reference trains on one device).  pdvc_event_record_external records with
+ * hipEventRecordExternal: on a capturing stream it becomes an event-record node that every replay executes;
+ * pdvc_stream_wait_event makes `stream` wait for the event's latest record. */
+int pdvc_event_create(void** event);
+int pdvc_event_destroy(void* event);
+int pdvc_event_record_external(void* event, void* stream);
+int pdvc_stream_wait_event(void* stream, void* event);
 
 /* ---- box refinement: out = sigmoid(tmp + inverse_sigmoid(ref)) (deformable_transformer.py:303-313) ----------
  * tmp, out (rows, 2) (centre, length); ref (rows, rd), rd = 2, or 1 (only the centre refined); inverse_sigmoid clamps

@@ -40,11 +40,13 @@ def main():
         sg = StepGraph(model, criterion, dt, reducer=reducer)
         sg.replay()
         sg.replay()
+        overlap = sg.overlap
     else:
         model.zero_grad(set_to_none=True)
         _, loss = model(dt, criterion, "queries")
         sum(loss[k] * wd[k] for k in loss.keys() if k in wd).backward()
         reducer.finish()
+        overlap = False
     torch.cuda.synchronize()
     res = {}
     for n, p in model.named_parameters():
@@ -53,6 +55,7 @@ def main():
         else:
             res["grad." + n] = p.grad.detach().cpu().numpy()
     res["n_buckets"] = np.asarray(len(reducer.buckets))
+    res["overlap"] = np.asarray(int(overlap))  # graph mode: the all-reduces queued behind the capture's events
     np.savez(out, **res)
     dist.barrier()
     dist.destroy_process_group()

@@ -140,3 +140,86 @@ def test_grad_allreduce_is_mean_of_ranks(world):
             expect = sum(gs) / world
             for r in range(world):
                 torch.testing.assert_close(torch.from_numpy(results[r][step][name]), expect, rtol=1e-6, atol=1e-7)
+
+
+def test_capture_events_bookkeeping(monkeypatch):
+    """The step-graph form (GradAllReducer.begin_capture / end_capture / finish_replay, pdvc/distributed.py): inside
+    a capture each bucket records its event at its last gradient -- in the order the backward completes them --
+    a bucket left open by a gradient that did not arrive records at end_capture, and finish_replay queues every
+    bucket's all-reduce behind its event in index order.  CPU, one gloo rank; the graph events and torch.cuda's
+    streams are replaced by recorders (the GPU path is tests/test_gpu_dp.py)."""
+    from pdvc.distributed import GradAllReducer
+    log = []
+
+    class FakeEvent:
+        def __init__(self):
+            self.i = None
+
+        def record(self):
+            log.append(("record", self.i))
+
+        def wait(self, stream):
+            log.append(("wait", self.i))
+
+    class FakeStream:
+        def wait_stream(self, s):
+            pass
+
+    class Ctx:
+        def __init__(self, s):
+            pass
+
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *a):
+            return False
+
+    class Cur:
+        def wait_stream(self, s):
+            pass
+
+    real_ar = dist.all_reduce
+
+    def all_reduce(t, group=None, async_op=False):
+        log.append(("all_reduce", t.numel()))
+        return real_ar(t, group=group, async_op=async_op)
+
+    import pdvc.distributed as D
+    monkeypatch.setattr(D, "_graph_event", FakeEvent)
+    monkeypatch.setattr(torch.cuda, "Stream", FakeStream)
+    monkeypatch.setattr(torch.cuda, "stream", Ctx)
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda: Cur())
+    monkeypatch.setattr(dist, "all_reduce", all_reduce)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    try:
+        torch.manual_seed(0)
+        m = Toy()
+        x = torch.randn(4, 16)
+        params = [p for p in m.parameters()]
+        red = GradAllReducer(params, bucket_mb=0.001)  # ~1 KB buckets: several
+        m(x, True, 0).backward()
+        red.finish()  # first step: the active set (without `unused` and `late`) and the flat buffers
+        nb = len(red.buckets)
+        assert nb >= 3
+        red.zero_grad()
+        red.begin_capture()
+        for i, ev in enumerate(red.events):
+            ev.i = i
+        log.clear()
+        m(x, False, 0).backward()  # `branch` gets no gradient: its bucket stays open
+        during = [i for k, i in log if k == "record"]
+        open_b = red.bucket_of[id(m.branch.weight)]
+        assert open_b not in during and len(set(during)) == len(during) == nb - 1
+        red.end_capture()
+        assert [i for k, i in log if k == "record"] == during + [open_b]
+        assert not red.capturing and red.pending == [len(b) for b in red.buckets]
+        log.clear()
+        before = [f.clone() for f in red.flats]
+        red.finish_replay()
+        # index order: wait on bucket i's event, then its all-reduce; the world-1 mean leaves the buckets as they were
+        assert log == [e for i in range(nb) for e in (("wait", i), ("all_reduce", red.flats[i].numel()))]
+        for f, b in zip(red.flats, before):
+            assert torch.equal(f, b)
+    finally:
+        dist.destroy_process_group()

@@ -3,7 +3,8 @@ through the training step and GradAllReducer, end with the gradients one process
 union batch -- within 1e-4 * max|ref| + 1e-7 per tensor, with the same parameters left at grad None (the
 reference's never-used ones).  Ranks are fresh processes (tests/dp_worker.py) on cuda:0 over gloo (a 1-GPU
 box; the bench's N-GPU runs use RCCL with the same reducer); both the eager step and the StepGraph replay
-(forward + losses + backward as one hipGraph, the path bench.py times) are covered.  The union gradient is
+(forward + losses + backward as one hipGraph, the path bench.py times) are covered; the graph mode's all-reduces
+are queued behind the per-bucket events the capture records (GradAllReducer.finish_replay).  The union gradient is
 itself the mean of the reference's batch-1 gradients (tests/test_gpu_batch.py pins that)."""
 import os
 import socket
@@ -70,6 +71,8 @@ def test_two_ranks_equal_union_batch(tmp_path, union, mode):
     for r in range(world):
         g = np.load(outs[r], allow_pickle=False)
         assert int(g["n_buckets"]) >= 2
+        if mode == "graph":  # the replays' all-reduces ran behind the capture's per-bucket events (overlapped)
+            print(f"rank {r}: overlapped reduction {bool(int(g['overlap']))}")
         for n, ref in union.items():
             if ref is None:
                 assert "none." + n in g.files, f"rank {r}: {n} must stay None"
