@@ -107,10 +107,31 @@ extern "C" int pdvc_event_destroy(void* event) {
                                                             : pdvc_set_error(PDVC_ERR_LAUNCH, "hipEventDestroy");
 }
 
+// On a capturing stream the record is added to the capture's graph as an event-record node after the stream's
+// current dependency set (hipStreamGetCaptureInfo_v2), and the stream's later work is made to follow it
+// (hipEventRecordWithFlags(.., hipEventRecordExternal) is refused inside a capture on this stack: invalid argument).
+// On a stream that is not capturing it is a plain record.
 extern "C" int pdvc_event_record_external(void* event, void* stream) {
     PDVC_CHECK_ARG(event != nullptr, "event is NULL");
-    const hipError_t e = hipEventRecordWithFlags((hipEvent_t)event, (hipStream_t)stream, hipEventRecordExternal);
-    return e == hipSuccess ? PDVC_OK : pdvc_set_error(PDVC_ERR_LAUNCH, "hipEventRecordWithFlags: %s", hipGetErrorString(e));
+    hipStream_t s = (hipStream_t)stream;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t nd = 0;
+    hipError_t e = hipStreamGetCaptureInfo_v2(s, &st, &id, &g, &deps, &nd);
+    if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "hipStreamGetCaptureInfo_v2: %s", hipGetErrorString(e));
+    if (st != hipStreamCaptureStatusActive) {
+        e = hipEventRecord((hipEvent_t)event, s);
+        return e == hipSuccess ? PDVC_OK : pdvc_set_error(PDVC_ERR_LAUNCH, "hipEventRecord: %s", hipGetErrorString(e));
+    }
+    std::vector<hipGraphNode_t> dv(deps, deps + nd);  // copied: the stream's array may change with the update below
+    hipGraphNode_t node;
+    e = hipGraphAddEventRecordNode(&node, g, nd ? dv.data() : nullptr, nd, (hipEvent_t)event);
+    if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "hipGraphAddEventRecordNode: %s", hipGetErrorString(e));
+    e = hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies);
+    return e == hipSuccess ? PDVC_OK
+                           : pdvc_set_error(PDVC_ERR_LAUNCH, "hipStreamUpdateCaptureDependencies: %s", hipGetErrorString(e));
 }
 
 extern "C" int pdvc_stream_wait_event(void* stream, void* event) {

@@ -396,9 +396,10 @@ int pdvc_set_losses_backward_f32(const float* grad_losses, const float* dlogit, 
 int pdvc_graph_replace_memsets(void* graph, int* replaced);
 
 /* Events a captured graph records for streams outside it (the data-parallel all-reduce overlap, pdvc/distributed.py;
- * no reference counterpart: the reference trains on one device).  pdvc_event_record_external records with
- * hipEventRecordExternal: on a capturing stream it becomes an event-record node that every replay executes;
- * pdvc_stream_wait_event makes `stream` wait for the event's latest record. */
+ * no reference counterpart: the reference trains on one device).  pdvc_event_record_external on a capturing stream
+ * adds an event-record node after the stream's current dependencies (every replay executes it, and the stream's later
+ * captured work follows it); on any other stream it is a plain record.  pdvc_stream_wait_event makes `stream` wait
+ * for the event's latest record. */
 int pdvc_event_create(void** event);
 int pdvc_event_destroy(void* event);
 int pdvc_event_record_external(void* event, void* stream);
