@@ -9,20 +9,10 @@
 // in one pass over (dh_d, h_d), in place, which also sums the columns of dh (linear1's bias gradient) into
 // per-slab partial rows (the layout of colsum.hip) -- torch's masked_scale + threshold_backward + sum were three.
 // HBM-bound: forward 8 bytes / element, backward 12 bytes / element.
+#include "ffn_hash.h"
 #include "pdvc_common.h"
 
 namespace pdvc {
-
-__device__ __forceinline__ uint32_t ffn_mix(uint32_t x) {
-    x ^= x >> 16; x *= 0x21f0aaadU; x ^= x >> 15; x *= 0x735a2d97U; x ^= x >> 15;
-    return x;
-}
-
-// keep with probability 1 - p (24-bit uniform) for element (row, col)
-__device__ __forceinline__ bool ffn_keep(uint64_t seed, uint32_t row, uint32_t col, uint32_t thresh) {
-    const uint32_t h = ffn_mix(ffn_mix(row * 0x9e3779b1U ^ (uint32_t)seed) + col * 0xc2b2ae35U + (uint32_t)(seed >> 32));
-    return (h >> 8) >= thresh;
-}
 
 __global__ __launch_bounds__(256) void relu_dropout_fwd_kernel(float* __restrict__ h, long rows, int cols, float p,
                                                                uint32_t thresh, float scale, uint64_t seed0,
@@ -125,13 +115,6 @@ __global__ __launch_bounds__(256) void ffn_colsum_final_kernel(const float* __re
         }
         reinterpret_cast<float4*>(out)[c4] = t;
     }
-}
-
-static uint32_t ffn_threshold(float p) {
-    double t = (double)p * 16777216.0;
-    if (t < 0) t = 0;
-    if (t > 16777216.0) t = 16777216.0;
-    return (uint32_t)t;
 }
 
 }  // namespace pdvc

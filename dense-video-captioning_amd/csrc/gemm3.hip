@@ -24,6 +24,7 @@
 // so the 16-lane groups of a fragment read hit 16 distinct 16-B bank slots), double buffered: one barrier a stage.
 #include <type_traits>
 
+#include "ffn_hash.h"
 #include "pdvc_common.h"
 
 namespace pdvc {
@@ -49,7 +50,15 @@ constexpr int BK = 32;     // k per stage
 constexpr int ROWB = 64;   // bytes per LDS image row (BK bf16)
 constexpr int NT = 512;    // threads per workgroup
 
-enum { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_RELU = 2, EPI_ACCUM = 3, EPI_SLAB = 4 };
+enum { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_RELU = 2, EPI_ACCUM = 3, EPI_SLAB = 4, EPI_BIAS_RELU_DROP = 5 };
+
+// EPI_BIAS_RELU_DROP: the feed-forward block's relu -> dropout in the epilogue of linear1 (ffn.hip's forward pass,
+// the same keep mask bit for bit: ffn_hash.h); seed read on the device (graph-safe), scale = 1 / (1 - p)
+struct Drop {
+    const uint64_t* seed;
+    uint32_t thresh;
+    float scale;
+};
 
 __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
     const bf16x2 h = __builtin_convertvector((f32x2){a, b}, bf16x2);  // v_cvt_pk_bf16_f32, round to nearest even
@@ -170,12 +179,14 @@ __device__ __forceinline__ f32x16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[
 template <int EPI, bool FULL, int BI = 2, int BJ = 2>
 __device__ __forceinline__ void store_tile(const f32x16 (&acc)[BI][BJ], float* __restrict__ C, long ldc,
                                            const float* __restrict__ bias, int r0, int c0, int M, int N, int l32,
-                                           int h) {
+                                           int h, Drop drp = Drop{nullptr, 0u, 1.f}) {
+    constexpr bool BIASED = EPI == EPI_BIAS || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_RELU_DROP;
+    const uint64_t seed = EPI == EPI_BIAS_RELU_DROP ? *drp.seed : 0;
 #pragma unroll
     for (int j = 0; j < BJ; ++j) {
         const int col = c0 + 32 * j + l32;
         const bool colok = FULL || col < N;
-        const float bv = (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) ? bias[colok ? col : 0] : 0.f;
+        const float bv = BIASED ? bias[colok ? col : 0] : 0.f;
 #pragma unroll
         for (int i = 0; i < BI; ++i) {
             const int rbase = r0 + 32 * i + 4 * h;
@@ -196,7 +207,9 @@ __device__ __forceinline__ void store_tile(const f32x16 (&acc)[BI][BJ], float* _
                 const int dr = (r & 3) + 8 * (r >> 2);
                 if (FULL || (colok && rbase + dr < M)) {
                     float v = acc[i][j][r] + bv;
-                    if (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+                    if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_RELU_DROP) v = fmaxf(v, 0.f);
+                    if (EPI == EPI_BIAS_RELU_DROP)
+                        v = ffn_keep(seed, (uint32_t)(rbase + dr), (uint32_t)col, drp.thresh) ? v * drp.scale : 0.f;
                     float* p = p0 + (long)dr * ldc;
                     if constexpr (EPI == EPI_ACCUM) v += old[r];
                     *p = v;
@@ -449,7 +462,8 @@ __device__ __forceinline__ void dma32(char* dst, const uint16_t* __restrict__ pl
 template <int EPI, int NP = 3>
 __global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, const float* __restrict__ A, long lda,
                                                        const uint16_t* __restrict__ planes, float* __restrict__ C,
-                                                       long ldc, const float* __restrict__ bias, int tiles_n) {
+                                                       long ldc, const float* __restrict__ bias, int tiles_n,
+                                                       Drop drp) {
     using namespace p3;
     constexpr int AIMG = Geo<NP>::AIMG, STAGE = Geo<NP>::STAGE, BDMA = Geo<NP>::BDMA;
     __shared__ __attribute__((aligned(16))) char lds[NSTAGE * STAGE];
@@ -565,8 +579,8 @@ __global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, cons
         return;
     }
     const bool full = m0 + BM <= M && n0 + BN <= N;
-    if (full) store_tile<EPI, true, 4, 2>(acc, C, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h);
-    else store_tile<EPI, false, 4, 2>(acc, C, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h);
+    if (full) store_tile<EPI, true, 4, 2>(acc, C, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h, drp);
+    else store_tile<EPI, false, 4, 2>(acc, C, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h, drp);
 }
 
 // ---- both operands mn-contiguous (the weight gradient dW = dy^T x: the reduction runs over the rows of both) ----
@@ -826,10 +840,11 @@ int split_planes_impl(int np, const float* B, long ldb, int b_kc, int N, int K, 
 
 template <int NP>
 int gemmp_impl(int M, int N, int K, const float* A, long lda, const uint16_t* planes, float* C, long ldc,
-               const float* bias, int epilogue, void* stream) {
+               const float* bias, int epilogue, void* stream, Drop drp = Drop{nullptr, 0u, 1.f}) {
     PDVC_CHECK_ARG(M >= 0 && N > 0 && K >= 0 && K % BK == 0, "sizes: N > 0, K a multiple of 32");
-    PDVC_CHECK_ARG(epilogue >= 0 && epilogue <= 3, "epilogue must be 0..3");
-    PDVC_CHECK_ARG(epilogue != 1 && epilogue != 2 ? true : bias != nullptr, "bias epilogue needs a bias");
+    PDVC_CHECK_ARG((epilogue >= 0 && epilogue <= 3) || (epilogue == EPI_BIAS_RELU_DROP && drp.seed != nullptr),
+                   "epilogue must be 0..3 (5: through pdvc_gemm3p_relu_dropout_f32)");
+    PDVC_CHECK_ARG(epilogue == 0 || epilogue == 3 || bias != nullptr, "bias epilogue needs a bias");
     PDVC_CHECK_ARG(lda >= K && ldc >= N, "leading dimensions too small");
     PDVC_CHECK_ARG((uintptr_t)A % 16 == 0 && lda % 4 == 0 && (uintptr_t)planes % 16 == 0,
                    "A rows and the planes must be 16-byte aligned");
@@ -838,12 +853,15 @@ int gemmp_impl(int M, int N, int K, const float* A, long lda, const uint16_t* pl
     PDVC_CHECK_ARG(tiles_m * tiles_n < (1L << 31), "too many tiles");
     const dim3 grid((unsigned)(tiles_m * tiles_n));
     hipStream_t s = (hipStream_t)stream;
-#define G3P_L(E) hipLaunchKernelGGL((gemm3p_kernel<E, NP>), grid, dim3(NT), 0, s, M, N, K, A, lda, planes, C, ldc, bias, (int)tiles_n)
+#define G3P_L(E) hipLaunchKernelGGL((gemm3p_kernel<E, NP>), grid, dim3(NT), 0, s, M, N, K, A, lda, planes, C, ldc, bias, (int)tiles_n, drp)
     switch (epilogue) {
         case 0: G3P_L(EPI_STORE); break;
         case 1: G3P_L(EPI_BIAS); break;
         case 2: G3P_L(EPI_BIAS_RELU); break;
-        default: G3P_L(EPI_ACCUM); break;
+        case 3: G3P_L(EPI_ACCUM); break;
+        default:
+            if constexpr (NP == 3) G3P_L(EPI_BIAS_RELU_DROP);
+            break;
     }
 #undef G3P_L
     PDVC_CHECK_LAUNCH("gemm3p_kernel");
@@ -860,6 +878,18 @@ extern "C" int pdvc_split3_planes_f32(const float* B, long ldb, int b_kc, int N,
 extern "C" int pdvc_gemm3p_f32(int M, int N, int K, const float* A, long lda, const uint16_t* planes, float* C,
                                long ldc, const float* bias, int epilogue, void* stream) {
     return gemmp_impl<3>(M, N, K, A, lda, planes, C, ldc, bias, epilogue, stream);
+}
+
+// linear1 of the feed-forward block with its relu -> dropout in the epilogue (C = dropout(relu(A opB^T + bias)), the
+// keep mask of pdvc_relu_dropout_forward_f32 for element (row, col) of C and the same seed: bit-identical to the GEMM
+// followed by that pass)
+extern "C" int pdvc_gemm3p_relu_dropout_f32(int M, int N, int K, const float* A, long lda, const uint16_t* planes,
+                                            float* C, long ldc, const float* bias, float p, const uint64_t* seed_dev,
+                                            void* stream) {
+    PDVC_CHECK_ARG(p > 0.f && p < 1.f, "dropout p must be in (0, 1) (p = 0: the bias + ReLU epilogue)");
+    PDVC_CHECK_ARG(seed_dev != nullptr && bias != nullptr, "a device seed and a bias are required");
+    const Drop drp{seed_dev, ffn_threshold(p), 1.f / (1.f - p)};
+    return gemmp_impl<3>(M, N, K, A, lda, planes, C, ldc, bias, EPI_BIAS_RELU_DROP, stream, drp);
 }
 
 // the bf16 mode's product: opB rounded to bf16 (one plane), A rounded in the kernel, one MFMA term, fp32 result

@@ -3,14 +3,17 @@
 (reference: DeformableTransformerEncoderLayer.forward_ffn, deformable_transformer.py:140-145; the decoder's
 forward_ffn, :233-237).  Same arithmetic as the module chain; what changes is where the passes over the
 (rows x d_ffn) and (rows x d) tensors go:
-  * relu + dropout is one in-place HIP pass (csrc/ffn.hip), its backward one pass that also sums linear1's
-    bias gradient (no byte mask: the forward output itself says where relu passed and dropout kept);
+  * relu + dropout runs in linear1's gemm3 epilogue when linear1 takes gemm3 (pdvc_gemm3p_relu_dropout_f32),
+    else as one in-place HIP pass (csrc/ffn.hip) -- the same mask bits either way; its backward is one pass that
+    also sums linear1's bias gradient (no byte mask: the forward output itself says where relu passed and dropout
+    kept);
   * the residual gradient from the layer norm and linear1's input gradient meet in the dgrad GEMM's epilogue
     (dx = dx_residual + dh W1, beta = 1) instead of an autograd add;
   * the residual epilogue is pdvc_add_dropout_layernorm (csrc/addnorm.hip).
 Both dropout masks are counter hashes of seeds drawn on the GPU (graph-safe), regenerated in the backward.
 """
 import ctypes
+import os
 
 import torch
 import torch.nn.functional as F
@@ -21,8 +24,12 @@ from pdvc import _native as _n
 from pdvc.precision import attach_bf16, shadow_for
 from .addnorm import BWD_PARTS, an_backward, an_forward
 from . import linear as _lin
-from .gemm3 import addmm_nt, mm_dgrad
+from .gemm3 import addmm_nt, addmm_relu_dropout_nt, mm_dgrad
 from .linear import CU, wgrad_mm
+
+
+# False (or PDVC_FFN_FUSE=0): linear1, then the relu-dropout pass (the A/B and the bit-identity test)
+FUSE_RELU_DROPOUT = os.environ.get("PDVC_FFN_FUSE", "1") != "0"
 
 
 def _seed_ptrs(seeds):
@@ -46,9 +53,16 @@ class FFNBlockFunction(Function):
         x2 = x.reshape(-1, d).contiguous()
         rows = x2.shape[0]
         seed_act, seed_out = _seed_ptrs(seeds)
-        h = addmm_nt(b1, x2, w1)
-        h16 = shadow_for(h)  # bf16 mode: linear2's operand written by the same pass
-        if h16 is None:
+        h = None
+        if FUSE_RELU_DROPOUT and p_act > 0:  # relu -> dropout in linear1's gemm3 epilogue (same mask bits)
+            h = addmm_relu_dropout_nt(b1, x2, w1, float(p_act), seed_act)
+        fused = h is not None
+        if h is None:
+            h = addmm_nt(b1, x2, w1)
+        h16 = None if fused else shadow_for(h)  # bf16 mode: linear2's operand written by the same pass
+        if fused:
+            pass
+        elif h16 is None:
             _n.call("pdvc_relu_dropout_forward_f32", _n.ptr(h), rows, h.shape[1], float(p_act), 0, seed_act,
                     _n.stream())
         else:

@@ -94,6 +94,24 @@ def addmm_nt(bias, x, W, relu=False, out=None):
     return _gemm3p(x, split_planes(W, 1, N, K), N, out, bias, epi)
 
 
+def addmm_relu_dropout_nt(bias, x, W, p, seed_ptr):
+    """dropout(relu(torch.addmm(bias, x, W.t())), p) with the keep mask of pdvc_relu_dropout_forward_f32 for the
+    device seed at seed_ptr, as one gemm3 launch (the epilogue does the relu and the mask), or None when the shape
+    does not take gemm3 (the caller then runs the GEMM and the relu-dropout pass)."""
+    M, K = x.shape
+    N = W.shape[0]
+    if not (0.0 < p < 1.0) or seed_ptr is None or bias is None or M >= 2 ** 32:
+        return None
+    if not _use(M, K, x, W, extra=W.is_contiguous() and bias.is_contiguous()):
+        return None
+    out = torch.empty((M, N), dtype=torch.float32, device=x.device)
+    FLOPS[0] += 2 * M * N * K
+    planes = split_planes(W, 1, N, K)
+    _n.call("pdvc_gemm3p_relu_dropout_f32", M, N, K, _n.ptr_any(x), x.stride(0), _n.ptr(planes), _n.ptr(out), N,
+            _n.ptr(bias), float(p), seed_ptr, _n.stream())
+    return out
+
+
 def mm_nt(x, W, out=None):
     return addmm_nt(None, x, W, out=out)
 

@@ -585,6 +585,12 @@ int pdvc_gemm3_f32(int M, int N, int K, const float* A, long lda, int a_kc, cons
 int pdvc_split3_planes_f32(const float* B, long ldb, int b_kc, int N, int K, uint16_t* planes, void* stream);
 int pdvc_gemm3p_f32(int M, int N, int K, const float* A, long lda, const uint16_t* planes, float* C, long ldc,
                     const float* bias, int epilogue, void* stream);
+/* linear1 of the transformer feed-forward block with its relu -> dropout in the epilogue (DeformableTransformer
+ * EncoderLayer.forward_ffn, deformable_transformer.py:162-165: dropout(relu(linear1(x)))): C = keep(row, col) ?
+ * relu(A opB^T + bias) / (1 - p) : 0, the keep mask of pdvc_relu_dropout_forward_f32 for the same device seed, bit for
+ * bit (0 < p < 1; p = 0 is pdvc_gemm3p_f32's bias + ReLU epilogue). */
+int pdvc_gemm3p_relu_dropout_f32(int M, int N, int K, const float* A, long lda, const uint16_t* planes, float* C,
+                                 long ldc, const float* bias, float p, const uint64_t* seed_dev, void* stream);
 
 /* The bf16 mode's product (BASELINE configs[1]; pdvc/precision.py), the same call shape with one plane:
  * pdvc_round_plane_f32 writes plane[n][k] = bf16(opB[n][k]) (round to nearest even, torch's .to(bfloat16)) and

@@ -225,3 +225,30 @@ def test_batched_step_on_gemm3_equals_reference(monkeypatch):
     before = G.CALLS["gemm3"]
     TB.test_batched_step_equals_mean_of_reference_batch1_steps(TB.TM.load(TB.NAME))
     assert G.CALLS["gemm3"] > before + 20
+
+
+def test_ffn_relu_dropout_epilogue_is_bit_identical(monkeypatch):
+    """linear1's relu -> dropout in the gemm3 epilogue (pdvc_gemm3p_relu_dropout_f32) against linear1 on gemm3
+    followed by the relu-dropout pass (ffn.py FUSE_RELU_DROPOUT off): the same mask bits and arithmetic, so the
+    block's output and every gradient are bit-identical; ragged rows (not a multiple of the 256-row tile)."""
+    _on_gemm3(monkeypatch)
+    import pdvc.ops.functions.ffn as F
+    from pdvc.ops.functions.ffn import FFNBlockFunction
+    torch.manual_seed(3)
+    rows, d, f, p = 3000, 256, 512, 0.3
+    x = torch.randn(rows, d, device=DEV)
+    lin1, lin2 = torch.nn.Linear(d, f).to(DEV), torch.nn.Linear(f, d).to(DEV)
+    norm = torch.nn.LayerNorm(d).to(DEV)
+    params = [lin1.weight, lin1.bias, lin2.weight, lin2.bias, norm.weight, norm.bias]
+    seeds = torch.tensor([1234567, 7654321], dtype=torch.int64, device=DEV)
+    g = torch.randn(rows, d, device=DEV)
+    res = []
+    for fuse in (True, False):
+        monkeypatch.setattr(F, "FUSE_RELU_DROPOUT", fuse)
+        xa = x.clone().requires_grad_()
+        out = FFNBlockFunction.apply(xa, *params, p, 0.1, norm.eps, seeds)
+        res.append([out.detach()] + list(torch.autograd.grad(out, [xa] + params, g)))
+    for i, (a, b) in enumerate(zip(*res)):
+        assert torch.equal(a, b), f"tensor {i} differs between the fused epilogue and the separate pass"
+    kept = (res[0][0] != 0).float().mean()  # sanity: dropout active
+    assert kept > 0
