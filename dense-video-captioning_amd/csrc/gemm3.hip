@@ -181,7 +181,38 @@ __device__ __forceinline__ void store_tile(const f32x16 (&acc)[BI][BJ], float* _
                                            const float* __restrict__ bias, int r0, int c0, int M, int N, int l32,
                                            int h, Drop drp = Drop{nullptr, 0u, 1.f}) {
     constexpr bool BIASED = EPI == EPI_BIAS || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_RELU_DROP;
-    const uint64_t seed = EPI == EPI_BIAS_RELU_DROP ? *drp.seed : 0;
+    if constexpr (EPI == EPI_BIAS_RELU_DROP) {
+        // ffn_keep's hash split by what it depends on: the inner mix of the row once per row (rows outer, the column
+        // blocks inner), the column term once per column block -- the v_mul_lo_u32 of the mask are quarter-rate
+        const uint64_t seed = *drp.seed;
+        uint32_t cterm[BJ];
+        float bvs[BJ];
+#pragma unroll
+        for (int j = 0; j < BJ; ++j) {
+            const int col = c0 + 32 * j + l32;
+            cterm[j] = (uint32_t)col * 0xc2b2ae35U + (uint32_t)(seed >> 32);
+            bvs[j] = bias[(FULL || col < N) ? col : 0];
+        }
+#pragma unroll
+        for (int i = 0; i < BI; ++i) {
+            const int rbase = r0 + 32 * i + 4 * h;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int dr = (r & 3) + 8 * (r >> 2), row = rbase + dr;
+                const uint32_t rm = ffn_mix((uint32_t)row * 0x9e3779b1U ^ (uint32_t)seed);
+#pragma unroll
+                for (int j = 0; j < BJ; ++j) {
+                    const int col = c0 + 32 * j + l32;
+                    if (FULL || (col < N && row < M)) {
+                        const float v = fmaxf(acc[i][j][r] + bvs[j], 0.f);
+                        const bool keep = (ffn_mix(rm + cterm[j]) >> 8) >= drp.thresh;
+                        C[(long)row * ldc + col] = keep ? v * drp.scale : 0.f;
+                    }
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < BJ; ++j) {
         const int col = c0 + 32 * j + l32;
@@ -207,9 +238,7 @@ __device__ __forceinline__ void store_tile(const f32x16 (&acc)[BI][BJ], float* _
                 const int dr = (r & 3) + 8 * (r >> 2);
                 if (FULL || (colok && rbase + dr < M)) {
                     float v = acc[i][j][r] + bv;
-                    if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_RELU_DROP) v = fmaxf(v, 0.f);
-                    if (EPI == EPI_BIAS_RELU_DROP)
-                        v = ffn_keep(seed, (uint32_t)(rbase + dr), (uint32_t)col, drp.thresh) ? v * drp.scale : 0.f;
+                    if (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.f);
                     float* p = p0 + (long)dr * ldc;
                     if constexpr (EPI == EPI_ACCUM) v += old[r];
                     *p = v;

@@ -126,10 +126,34 @@ def mm_dgrad(dy, W, out=None, accumulate=True):
         if out is None:
             return torch.mm(dy, W)
         return out.addmm_(dy, W) if accumulate else torch.mm(dy, W, out=out)
+    splits = dgrad_splits(M, N, K)
+    if splits > 1 and (out is None or out.is_contiguous()):
+        # few output tiles over a deep reduction (the caption logit layer's input gradient: ~8 K rows x 512 over
+        # K = 5 760): gemm3p would run one workgroup per tile on a quarter of the CUs, so the reduction is split
+        # over workgroups on the generic kernel and the slabs summed in a fixed order (deterministic)
+        if out is None:
+            out = torch.empty((M, N), dtype=torch.float32, device=dy.device)
+            epi = 0
+        else:
+            epi = 3 if accumulate else 0
+        FLOPS[0] += 2 * M * N * K
+        ws = torch.empty(splits * M * N, dtype=torch.float32, device=dy.device)
+        _n.call("pdvc_gemm3_f32", M, N, K, _n.ptr_any(dy), dy.stride(0), 1, _n.ptr_any(W), W.stride(0), 0,
+                _n.ptr(out), N, None, epi, splits, _n.ptr(ws), _n.stream())
+        return out
     planes = split_planes(W, 0, N, K)
     if out is None:
         return _gemm3p(dy, planes, N, torch.empty((M, N), dtype=torch.float32, device=dy.device), None, 0)
     return _gemm3p(dy, planes, N, out, None, 3 if accumulate else 0)
+
+
+def dgrad_splits(M, N, K):
+    """Split-K factor of a data-gradient product: 1 when gemm3p's 256 x 256 tiles already give >= 128 workgroups or
+    the reduction is short; else enough K chunks of >= 512 for ~512 workgroups of the generic 256 x 128 tile."""
+    if ((M + 255) // 256) * ((N + 255) // 256) >= 128 or K < 1024 or N % 4:
+        return 1
+    tiles = ((M + 255) // 256) * ((N + 127) // 128)
+    return max(1, min((512 + tiles - 1) // tiles, K // 512, 64))
 
 
 def wgrad_splits(rows, tiles):

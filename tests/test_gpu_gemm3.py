@@ -252,3 +252,29 @@ def test_ffn_relu_dropout_epilogue_is_bit_identical(monkeypatch):
         assert torch.equal(a, b), f"tensor {i} differs between the fused epilogue and the separate pass"
     kept = (res[0][0] != 0).float().mean()  # sanity: dropout active
     assert kept > 0
+
+
+@pytest.mark.parametrize("accumulate", [None, False, True])
+def test_dgrad_split_k_few_tiles_deep_reduction(monkeypatch, accumulate):
+    """mm_dgrad on a product with few output tiles and a deep reduction (the caption logit layer's input gradient:
+    rows x 512 over K = the padded vocabulary) takes the split-K generic kernel (dgrad_splits > 1): float64 bound as
+    every gemm3 product, and deterministic (the slabs are summed in a fixed order)."""
+    G = _on_gemm3(monkeypatch)
+    torch.manual_seed(11)
+    M, N, K = 3000, 512, 5760
+    assert G.dgrad_splits(M, N, K) > 1
+    dy = torch.randn(M, K, device=DEV)
+    W = torch.randn(K, N, device=DEV) / K ** 0.5
+    ref = dy.double() @ W.double()
+    scale = dy.double().abs() @ W.double().abs()
+    if accumulate is None:
+        out = G.mm_dgrad(dy, W)
+        again = G.mm_dgrad(dy, W)
+        assert torch.equal(out, again), "split-K must be deterministic"
+    else:
+        base = torch.randn(M, N, device=DEV)
+        out = base.clone()
+        G.mm_dgrad(dy, W, out=out, accumulate=accumulate)
+        if accumulate:
+            ref, scale = ref + base.double(), scale + base.double().abs()
+    assert scaled_err(out, ref, scale) < 1e-6
