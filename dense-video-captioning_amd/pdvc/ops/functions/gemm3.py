@@ -158,9 +158,14 @@ def dgrad_splits(M, N, K):
 
 def wgrad_splits(rows, tiles):
     """Row chunks of a weight gradient's reduction: about two workgroups per CU over the output tiles, chunks of
-    at least 2048 rows (64 stages)."""
+    at least WGRAD_MIN_CHUNK rows."""
     want = max(1, (512 + tiles - 1) // tiles)
-    return max(1, min(want, rows // 2048, 1024))
+    return max(1, min(want, rows // WGRAD_MIN_CHUNK, 1024))
+
+
+# 1024 rows (64 stages of 16): the caption decoder's per-step weight gradients (8 192 rows) had 200-workgroup grids
+# at 2048-row chunks, under one wave of the 256 CUs
+WGRAD_MIN_CHUNK = int(os.environ.get("PDVC_WGRAD_MIN_CHUNK", "1024"))
 
 
 def mm_wgrad(gy, x, out=None):
