@@ -243,16 +243,18 @@ class GradAllReducer:
         self.capturing = False
         self._reset()
 
-    def finish_replay(self):
+    def finish_replay(self, events=None):
         """After a replay of a step captured between begin_capture() and end_capture(): every bucket's all-reduce
         in index order on a side stream, each behind its event, so a bucket is reduced as soon as the replay has
-        produced it; then the current stream waits for them and the rank mean is scaled in."""
+        produced it; then the current stream waits for them and the rank mean is scaled in.  events: the ones that
+        graph's capture recorded (StepGraph keeps them; a later capture with this reducer makes new ones)."""
+        events = self.events if events is None else events
         if self._side is None:
             self._side = torch.cuda.Stream()
         works = []
         with torch.cuda.stream(self._side):
             for bi, flat in enumerate(self.flats):
-                self.events[bi].wait(self._side)
+                events[bi].wait(self._side)
                 works.append((flat, dist.all_reduce(flat, group=self.group, async_op=True)))
         inv = 1.0 / self.world
         for flat, work in works:

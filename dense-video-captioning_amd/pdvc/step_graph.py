@@ -247,6 +247,9 @@ class StepGraph:
                 self.total, self.losses = self._forward_backward()
                 if self.overlap:
                     reducer.end_capture()
+                    # this graph's event-record nodes refer to these events: kept as long as the graph (a later
+                    # capture with the same reducer makes its own, and destroying these would leave dangling nodes)
+                    self.events = list(reducer.events)
         finally:
             if gc_enabled:
                 gc.enable()
@@ -363,7 +366,7 @@ class StepGraph:
         self.graph.replay()
         if self.reducer is not None:
             if self.overlap:
-                self.reducer.finish_replay()
+                self.reducer.finish_replay(self.events)
             else:
                 self.reducer.finish()
         return self.total
