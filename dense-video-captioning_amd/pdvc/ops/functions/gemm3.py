@@ -156,16 +156,28 @@ def dgrad_splits(M, N, K):
     return max(1, min((512 + tiles - 1) // tiles, K // 512, 64))
 
 
-def wgrad_splits(rows, tiles):
-    """Row chunks of a weight gradient's reduction: about two workgroups per CU over the output tiles, chunks of
-    at least WGRAD_MIN_CHUNK rows."""
-    want = max(1, (512 + tiles - 1) // tiles)
-    return max(1, min(want, rows // WGRAD_MIN_CHUNK, 1024))
+def wgrad_splits(rows, tiles, O=256, I=256):
+    """Row chunks of a weight gradient's reduction, by a cost model of gemm3w's launch: one workgroup per CU, so a
+    grid of tiles x splits workgroups runs in ceil(/256) waves of ceil(rows / splits / 16) stages each (≈1.9 µs a
+    stage, measured at the encoder's shapes), plus the slabs' write and fixed-order sum (8 B per output element and
+    split at ≈5 TB/s).  Chunks of at least WGRAD_MIN_CHUNK rows.  (A fixed two-workgroups-per-CU rule left the
+    decoder's 8 192-row products at 200 workgroups, 0.78 of a wave, and doubling them to 400 only moved the loss
+    into a second wave.)"""
+    smax = max(1, min(rows // WGRAD_MIN_CHUNK, 1024))
+    if not WGRAD_MODEL:  # the A/B baseline: about two workgroups per CU over the output tiles
+        return max(1, min((512 + tiles - 1) // tiles, smax))
+    best, best_t = 1, None
+    for s in range(1, smax + 1):
+        waves = (tiles * s + 255) // 256
+        stages = (-(-rows // s) + 15) // 16
+        t = waves * stages * 1.9 + (s * O * I * 8 / 5e6 if s > 1 else 0.0)
+        if best_t is None or t < best_t - 1e-9:
+            best, best_t = s, t
+    return best
 
 
-# 1024 rows (64 stages of 16): the caption decoder's per-step weight gradients (8 192 rows) had 200-workgroup grids
-# at 2048-row chunks, under one wave of the 256 CUs
 WGRAD_MIN_CHUNK = int(os.environ.get("PDVC_WGRAD_MIN_CHUNK", "1024"))
+WGRAD_MODEL = os.environ.get("PDVC_WGRAD_MODEL", "1") != "0"
 
 
 def mm_wgrad(gy, x, out=None):
@@ -180,7 +192,7 @@ def mm_wgrad(gy, x, out=None):
     if out is None:
         out = torch.empty((O, I), dtype=torch.float32, device=gy.device)
     tiles = ((O + 255) // 256) * ((I + 255) // 256)  # gemm3w tiles
-    splits = wgrad_splits(rows, tiles)
+    splits = wgrad_splits(rows, tiles, O, I)
     FLOPS[0] += 2 * rows * O * I
     ws = torch.empty(splits * O * I if splits > 1 else 0, dtype=torch.float32, device=gy.device)
     _n.call("pdvc_gemm3_f32", O, I, rows, _n.ptr_any(gy), gy.stride(0), 0, _n.ptr_any(x), x.stride(0), 0,
