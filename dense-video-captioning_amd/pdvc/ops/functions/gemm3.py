@@ -91,7 +91,28 @@ def addmm_nt(bias, x, W, relu=False, out=None):
     if bias is None and relu:
         _gemm3p(x, split_planes(W, 1, N, K), N, out, None, 0)
         return out.relu_()
+    if generic_wins(M, N, K):  # gemm3p's 256 x 256 tiles would leave the last wave mostly empty
+        FLOPS[0] += 2 * M * N * K
+        _n.call("pdvc_gemm3_f32", M, N, K, _n.ptr_any(x), x.stride(0), 1, _n.ptr_any(W), W.stride(0), 1,
+                _n.ptr_any(out), out.stride(0), _n.ptr(bias), epi, 1, None, _n.stream())
+        return out
     return _gemm3p(x, split_planes(W, 1, N, K), N, out, bias, epi)
+
+
+GENERIC_STAGE_COST = 1.14  # gemm3_kernel's 256 x 128 x 32 stage against gemm3p's 256 x 256 x 16 (same flops)
+TILE_MODEL = os.environ.get("PDVC_GEMM3_TILE_MODEL", "1") != "0"
+
+
+def generic_wins(M, N, K):
+    """Launch cost model (one workgroup per CU, whole waves): gemm3p takes ceil(tiles / 256) waves of K / 16
+    stages, the generic kernel's 256 x 128 tiles ceil(tiles / 256) waves of K / 32 slower stages.  The generic tile
+    wins only where gemm3p's last wave is mostly empty (e.g. 352 tiles: 2 waves against 3 waves of half-depth
+    stages) -- at whole or nearly whole waves gemm3p's faster stage decides."""
+    if not TILE_MODEL:
+        return False
+    wp = (((M + 255) // 256) * ((N + 255) // 256) + 255) // 256
+    wg = (((M + 255) // 256) * ((N + 127) // 128) + 255) // 256
+    return wg * (K / 32) * GENERIC_STAGE_COST < 0.9 * wp * (K / 16)
 
 
 def addmm_relu_dropout_nt(bias, x, W, p, seed_ptr):

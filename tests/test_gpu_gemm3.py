@@ -278,3 +278,22 @@ def test_dgrad_split_k_few_tiles_deep_reduction(monkeypatch, accumulate):
         if accumulate:
             ref, scale = ref + base.double(), scale + base.double().abs()
     assert scaled_err(out, ref, scale) < 1e-6
+
+
+def test_addmm_generic_tile_when_gemm3p_waves_are_ragged(monkeypatch):
+    """addmm_nt on a shape whose 256 x 256 tiles leave gemm3p's last wave mostly empty (8 192 x 2 816: 352 tiles)
+    takes the generic 256 x 128 kernel (generic_wins): same float64 bound, bias and ReLU epilogues."""
+    G = _on_gemm3(monkeypatch)
+    torch.manual_seed(13)
+    M, N, K = 8192, 2816, 512
+    assert G.generic_wins(M, N, K) and not G.generic_wins(983040, 512, 512)
+    x = torch.randn(M, K, device=DEV)
+    W = torch.randn(N, K, device=DEV) / K ** 0.5
+    b = torch.randn(N, device=DEV)
+    for relu in (False, True):
+        y = G.addmm_nt(b, x, W, relu=relu)
+        ref = x.double() @ W.double().t() + b.double()
+        if relu:
+            ref = ref.clamp_min(0)
+        scale = x.double().abs() @ W.double().abs().t() + b.double().abs()
+        assert scaled_err(y, ref, scale) < 1e-6
