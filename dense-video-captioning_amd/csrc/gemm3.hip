@@ -50,7 +50,8 @@ constexpr int BK = 32;     // k per stage
 constexpr int ROWB = 64;   // bytes per LDS image row (BK bf16)
 constexpr int NT = 512;    // threads per workgroup
 
-enum { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_RELU = 2, EPI_ACCUM = 3, EPI_SLAB = 4, EPI_BIAS_RELU_DROP = 5 };
+enum { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_RELU = 2, EPI_ACCUM = 3, EPI_SLAB = 4, EPI_BIAS_RELU_DROP = 5,
+       EPI_DMASK = 6 };
 
 // EPI_BIAS_RELU_DROP: the feed-forward block's relu -> dropout in the epilogue of linear1 (ffn.hip's forward pass,
 // the same keep mask bit for bit: ffn_hash.h); seed read on the device (graph-safe), scale = 1 / (1 - p)
@@ -58,6 +59,7 @@ struct Drop {
     const uint64_t* seed;
     uint32_t thresh;
     float scale;
+    const float* hd;  // EPI_DMASK: the forward's relu -> dropout output (C's shape and ldc); C = hd > 0 ? acc * scale : 0
 };
 
 __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
@@ -179,7 +181,7 @@ __device__ __forceinline__ f32x16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[
 template <int EPI, bool FULL, int BI = 2, int BJ = 2>
 __device__ __forceinline__ void store_tile(const f32x16 (&acc)[BI][BJ], float* __restrict__ C, long ldc,
                                            const float* __restrict__ bias, int r0, int c0, int M, int N, int l32,
-                                           int h, Drop drp = Drop{nullptr, 0u, 1.f}) {
+                                           int h, Drop drp = Drop{nullptr, 0u, 1.f, nullptr}) {
     constexpr bool BIASED = EPI == EPI_BIAS || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_RELU_DROP;
     if constexpr (EPI == EPI_BIAS_RELU_DROP) {
         // ffn_keep's hash split by what it depends on: the inner mix of the row once per row (rows outer, the column
@@ -226,11 +228,12 @@ __device__ __forceinline__ void store_tile(const f32x16 (&acc)[BI][BJ], float* _
             // but the compiler cannot prove a store leaves the next row's load alone, and interleaved it waited for
             // every load in turn (load, vmcnt(0), add, store: 128 round trips per lane and tile)
             float old[16];
-            if constexpr (EPI == EPI_ACCUM) {
+            if constexpr (EPI == EPI_ACCUM || EPI == EPI_DMASK) {  // (EPI_DMASK: the forward output's values)
+                const float* q0 = EPI == EPI_DMASK ? drp.hd + ((long)rbase * ldc + col) : p0;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int dr = (r & 3) + 8 * (r >> 2);
-                    old[r] = (FULL || (colok && rbase + dr < M)) ? p0[(long)dr * ldc] : 0.f;
+                    old[r] = (FULL || (colok && rbase + dr < M)) ? q0[(long)dr * ldc] : 0.f;
                 }
             }
 #pragma unroll
@@ -241,6 +244,7 @@ __device__ __forceinline__ void store_tile(const f32x16 (&acc)[BI][BJ], float* _
                     if (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.f);
                     float* p = p0 + (long)dr * ldc;
                     if constexpr (EPI == EPI_ACCUM) v += old[r];
+                    if constexpr (EPI == EPI_DMASK) v = old[r] > 0.f ? v * drp.scale : 0.f;
                     *p = v;
                 }
             }
@@ -869,11 +873,13 @@ int split_planes_impl(int np, const float* B, long ldb, int b_kc, int N, int K, 
 
 template <int NP>
 int gemmp_impl(int M, int N, int K, const float* A, long lda, const uint16_t* planes, float* C, long ldc,
-               const float* bias, int epilogue, void* stream, Drop drp = Drop{nullptr, 0u, 1.f}) {
+               const float* bias, int epilogue, void* stream, Drop drp = Drop{nullptr, 0u, 1.f, nullptr}) {
     PDVC_CHECK_ARG(M >= 0 && N > 0 && K >= 0 && K % BK == 0, "sizes: N > 0, K a multiple of 32");
-    PDVC_CHECK_ARG((epilogue >= 0 && epilogue <= 3) || (epilogue == EPI_BIAS_RELU_DROP && drp.seed != nullptr),
-                   "epilogue must be 0..3 (5: through pdvc_gemm3p_relu_dropout_f32)");
-    PDVC_CHECK_ARG(epilogue == 0 || epilogue == 3 || bias != nullptr, "bias epilogue needs a bias");
+    PDVC_CHECK_ARG((epilogue >= 0 && epilogue <= 3) || (epilogue == EPI_BIAS_RELU_DROP && drp.seed != nullptr) ||
+                       (epilogue == EPI_DMASK && drp.hd != nullptr),
+                   "epilogue must be 0..3 (5, 6: through pdvc_gemm3p_relu_dropout_f32 / _dmask_f32)");
+    PDVC_CHECK_ARG(epilogue == 0 || epilogue == 3 || epilogue == EPI_DMASK || bias != nullptr,
+                   "bias epilogue needs a bias");
     PDVC_CHECK_ARG(lda >= K && ldc >= N, "leading dimensions too small");
     PDVC_CHECK_ARG((uintptr_t)A % 16 == 0 && lda % 4 == 0 && (uintptr_t)planes % 16 == 0,
                    "A rows and the planes must be 16-byte aligned");
@@ -888,8 +894,11 @@ int gemmp_impl(int M, int N, int K, const float* A, long lda, const uint16_t* pl
         case 1: G3P_L(EPI_BIAS); break;
         case 2: G3P_L(EPI_BIAS_RELU); break;
         case 3: G3P_L(EPI_ACCUM); break;
-        default:
+        case EPI_BIAS_RELU_DROP:
             if constexpr (NP == 3) G3P_L(EPI_BIAS_RELU_DROP);
+            break;
+        default:
+            if constexpr (NP == 3) G3P_L(EPI_DMASK);
             break;
     }
 #undef G3P_L
@@ -917,8 +926,18 @@ extern "C" int pdvc_gemm3p_relu_dropout_f32(int M, int N, int K, const float* A,
                                             void* stream) {
     PDVC_CHECK_ARG(p > 0.f && p < 1.f, "dropout p must be in (0, 1) (p = 0: the bias + ReLU epilogue)");
     PDVC_CHECK_ARG(seed_dev != nullptr && bias != nullptr, "a device seed and a bias are required");
-    const Drop drp{seed_dev, ffn_threshold(p), 1.f / (1.f - p)};
+    const Drop drp{seed_dev, ffn_threshold(p), 1.f / (1.f - p), nullptr};
     return gemmp_impl<3>(M, N, K, A, lda, planes, C, ldc, bias, EPI_BIAS_RELU_DROP, stream, drp);
+}
+
+// the feed-forward block's backward through relu -> dropout in the data gradient of linear2's input: C = hd > 0 ?
+// (A opB^T) / (1 - p) : 0 with hd the forward's output (C's shape and ldc) -- pdvc_relu_dropout_backward_f32's
+// arithmetic on the GEMM's result, without its pass over the (rows x d_ffn) gradient
+extern "C" int pdvc_gemm3p_dmask_f32(int M, int N, int K, const float* A, long lda, const uint16_t* planes, float* C,
+                                     long ldc, const float* hd, float p, void* stream) {
+    PDVC_CHECK_ARG(p >= 0.f && p < 1.f && hd != nullptr, "dropout p in [0, 1) and the forward output required");
+    const Drop drp{nullptr, 0u, p > 0.f ? 1.f / (1.f - p) : 1.f, hd};
+    return gemmp_impl<3>(M, N, K, A, lda, planes, C, ldc, nullptr, EPI_DMASK, stream, drp);
 }
 
 // the bf16 mode's product: opB rounded to bf16 (one plane), A rounded in the kernel, one MFMA term, fp32 result

@@ -24,8 +24,8 @@ from pdvc import _native as _n
 from pdvc.precision import attach_bf16, shadow_for
 from .addnorm import BWD_PARTS, an_backward, an_forward
 from . import linear as _lin
-from .gemm3 import addmm_nt, addmm_relu_dropout_nt, mm_dgrad
-from .linear import CU, wgrad_mm
+from .gemm3 import addmm_nt, addmm_relu_dropout_nt, mm_dgrad, mm_dgrad_dmask
+from .linear import CU, colsum, wgrad_mm
 
 
 # False (or PDVC_FFN_FUSE=0): linear1, then the relu-dropout pass (the A/B and the bit-identity test)
@@ -95,10 +95,18 @@ class FFNBlockFunction(Function):
         db2 = torch.empty_like(gamma)  # linear2's bias gradient = column sums of dy, summed by the same pass
         an_backward(x2, y, gamma, mean, rstd, dout2, p_out, 0, seed_out, dx, dy, dgamma, dbeta, db2, ws)
         dw2 = wgrad_mm(dy, h)
+        db1 = torch.empty(fdim, dtype=h.dtype, device=h.device)
+        dh = None
+        if FUSE_RELU_DROPOUT and shadow_for(h) is None:  # relu -> dropout backward in the dgrad epilogue
+            dh = mm_dgrad_dmask(dy, w2, h, p_act)
+        if dh is not None:
+            colsum(dh, out=db1)  # linear1's bias gradient
+            dw1 = wgrad_mm(dh, x2)
+            mm_dgrad(dh, w1, out=dx)
+            return dx.view(shape), dw1, db1, dw2, db2, dgamma, dbeta, None, None, None, None
         dh = mm_dgrad(dy, w2)
         parts = _parts(rows, fdim)
         ws1 = torch.empty(parts * fdim, dtype=h.dtype, device=h.device)
-        db1 = torch.empty(fdim, dtype=h.dtype, device=h.device)
         dh16 = shadow_for(dh)  # bf16 mode: the operand of linear1's two gradient GEMMs, written by the same pass
         if dh16 is None:
             _n.call("pdvc_relu_dropout_backward_f32", _n.ptr(h), _n.ptr(dh), rows, fdim, p_act, parts, _n.ptr(ws1),

@@ -168,6 +168,24 @@ def mm_dgrad(dy, W, out=None, accumulate=True):
     return _gemm3p(dy, planes, N, out, None, 3 if accumulate else 0)
 
 
+def mm_dgrad_dmask(dy, W, hd, p):
+    """dy @ W masked as the feed-forward block's relu -> dropout backward: hd > 0 ? (dy @ W) / (1 - p) : 0, with hd
+    the forward's relu -> dropout output (M, I) -- one gemm3p launch (pdvc_gemm3p_dmask_f32) -- or None when the
+    product does not take gemm3p (the caller runs the GEMM and the relu-dropout backward pass)."""
+    M, K = dy.shape
+    N = W.shape[1]
+    if not (0.0 <= p < 1.0) or dgrad_splits(M, N, K) > 1:
+        return None
+    if not _use(M, K, dy, W, extra=W.is_contiguous() and hd.is_contiguous() and hd.shape == (M, N)):
+        return None
+    out = torch.empty((M, N), dtype=torch.float32, device=dy.device)
+    FLOPS[0] += 2 * M * N * K
+    planes = split_planes(W, 0, N, K)
+    _n.call("pdvc_gemm3p_dmask_f32", M, N, K, _n.ptr_any(dy), dy.stride(0), _n.ptr(planes), _n.ptr(out), N,
+            _n.ptr(hd), float(p), _n.stream())
+    return out
+
+
 def dgrad_splits(M, N, K):
     """Split-K factor of a data-gradient product: 1 when gemm3p's 256 x 256 tiles already give >= 128 workgroups or
     the reduction is short; else enough K chunks of >= 512 for ~512 workgroups of the generic 256 x 128 tile."""

@@ -591,6 +591,11 @@ int pdvc_gemm3p_f32(int M, int N, int K, const float* A, long lda, const uint16_
  * bit (0 < p < 1; p = 0 is pdvc_gemm3p_f32's bias + ReLU epilogue). */
 int pdvc_gemm3p_relu_dropout_f32(int M, int N, int K, const float* A, long lda, const uint16_t* planes, float* C,
                                  long ldc, const float* bias, float p, const uint64_t* seed_dev, void* stream);
+/* Its backward in the data gradient of linear2's input: C = hd[m, n] > 0 ? (A opB^T)[m, n] / (1 - p) : 0, hd the
+ * forward's output (C's shape and ldc) -- pdvc_relu_dropout_backward_f32's arithmetic on the GEMM result (the bias
+ * gradient, its column sums, is the caller's). */
+int pdvc_gemm3p_dmask_f32(int M, int N, int K, const float* A, long lda, const uint16_t* planes, float* C, long ldc,
+                          const float* hd, float p, void* stream);
 
 /* The bf16 mode's product (BASELINE configs[1]; pdvc/precision.py), the same call shape with one plane:
  * pdvc_round_plane_f32 writes plane[n][k] = bf16(opB[n][k]) (round to nearest even, torch's .to(bfloat16)) and

@@ -228,9 +228,10 @@ def test_batched_step_on_gemm3_equals_reference(monkeypatch):
 
 
 def test_ffn_relu_dropout_epilogue_is_bit_identical(monkeypatch):
-    """linear1's relu -> dropout in the gemm3 epilogue (pdvc_gemm3p_relu_dropout_f32) against linear1 on gemm3
-    followed by the relu-dropout pass (ffn.py FUSE_RELU_DROPOUT off): the same mask bits and arithmetic, so the
-    block's output and every gradient are bit-identical; ragged rows (not a multiple of the 256-row tile)."""
+    """linear1's relu -> dropout in the gemm3 epilogue (pdvc_gemm3p_relu_dropout_f32) and its backward in linear2's
+    data-gradient epilogue (pdvc_gemm3p_dmask_f32) against the GEMMs followed by the relu-dropout passes (ffn.py
+    FUSE_RELU_DROPOUT off): the same mask bits and arithmetic, so the block's output and every gradient are
+    bit-identical -- except linear1's bias gradient, the same column sums in another summation order; ragged rows."""
     _on_gemm3(monkeypatch)
     import pdvc.ops.functions.ffn as F
     from pdvc.ops.functions.ffn import FFNBlockFunction
@@ -249,7 +250,10 @@ def test_ffn_relu_dropout_epilogue_is_bit_identical(monkeypatch):
         out = FFNBlockFunction.apply(xa, *params, p, 0.1, norm.eps, seeds)
         res.append([out.detach()] + list(torch.autograd.grad(out, [xa] + params, g)))
     for i, (a, b) in enumerate(zip(*res)):
-        assert torch.equal(a, b), f"tensor {i} differs between the fused epilogue and the separate pass"
+        if i == 3:  # linear1's bias gradient: the column sums of the same dh, summed in another order
+            assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-7
+            continue
+        assert torch.equal(a, b), f"tensor {i} differs between the fused epilogues and the separate passes"
     kept = (res[0][0] != 0).float().mean()  # sanity: dropout active
     assert kept > 0
 
