@@ -4,9 +4,10 @@
 forward_ffn, :233-237).  Same arithmetic as the module chain; what changes is where the passes over the
 (rows x d_ffn) and (rows x d) tensors go:
   * relu + dropout runs in linear1's gemm3 epilogue when linear1 takes gemm3 (pdvc_gemm3p_relu_dropout_f32),
-    else as one in-place HIP pass (csrc/ffn.hip) -- the same mask bits either way; its backward is one pass that
-    also sums linear1's bias gradient (no byte mask: the forward output itself says where relu passed and dropout
-    kept);
+    else as one in-place HIP pass (csrc/ffn.hip) -- the same mask bits either way; its backward runs in linear2's
+    data-gradient epilogue (pdvc_gemm3p_dmask_f32) with linear1's bias gradient a column sum, else as one pass
+    that also sums that gradient (no byte mask either way: the forward output itself says where relu passed and
+    dropout kept);
   * the residual gradient from the layer norm and linear1's input gradient meet in the dgrad GEMM's epilogue
     (dx = dx_residual + dh W1, beta = 1) instead of an autograd add;
   * the residual epilogue is pdvc_add_dropout_layernorm (csrc/addnorm.hip).
@@ -21,7 +22,7 @@ from torch.autograd import Function
 from torch.autograd.function import once_differentiable
 
 from pdvc import _native as _n
-from pdvc.precision import attach_bf16, shadow_for
+from pdvc.precision import attach_bf16, bf16_active, shadow_for
 from .addnorm import BWD_PARTS, an_backward, an_forward
 from . import linear as _lin
 from .gemm3 import addmm_nt, addmm_relu_dropout_nt, mm_dgrad, mm_dgrad_dmask
@@ -56,19 +57,16 @@ class FFNBlockFunction(Function):
         h = None
         if FUSE_RELU_DROPOUT and p_act > 0:  # relu -> dropout in linear1's gemm3 epilogue (same mask bits)
             h = addmm_relu_dropout_nt(b1, x2, w1, float(p_act), seed_act)
-        fused = h is not None
         if h is None:
             h = addmm_nt(b1, x2, w1)
-        h16 = None if fused else shadow_for(h)  # bf16 mode: linear2's operand written by the same pass
-        if fused:
-            pass
-        elif h16 is None:
-            _n.call("pdvc_relu_dropout_forward_f32", _n.ptr(h), rows, h.shape[1], float(p_act), 0, seed_act,
-                    _n.stream())
-        else:
-            _n.call("pdvc_relu_dropout_forward_f32_bf16out", _n.ptr(h), rows, h.shape[1], float(p_act), 0, seed_act,
-                    _n.ptr(h16), _n.stream())
-            attach_bf16(h, h16)
+            h16 = shadow_for(h)  # bf16 mode: linear2's operand written by the same pass
+            if h16 is None:
+                _n.call("pdvc_relu_dropout_forward_f32", _n.ptr(h), rows, h.shape[1], float(p_act), 0, seed_act,
+                        _n.stream())
+            else:
+                _n.call("pdvc_relu_dropout_forward_f32_bf16out", _n.ptr(h), rows, h.shape[1], float(p_act), 0,
+                        seed_act, _n.ptr(h16), _n.stream())
+                attach_bf16(h, h16)
         y = addmm_nt(b2, h, w2)
         out = torch.empty_like(x2)
         mean = torch.empty(rows, dtype=x.dtype, device=x.device)
@@ -97,7 +95,7 @@ class FFNBlockFunction(Function):
         dw2 = wgrad_mm(dy, h)
         db1 = torch.empty(fdim, dtype=h.dtype, device=h.device)
         dh = None
-        if FUSE_RELU_DROPOUT and shadow_for(h) is None:  # relu -> dropout backward in the dgrad epilogue
+        if FUSE_RELU_DROPOUT and not bf16_active():  # relu -> dropout backward in the dgrad epilogue
             dh = mm_dgrad_dmask(dy, w2, h, p_act)
         if dh is not None:
             colsum(dh, out=db1)  # linear1's bias gradient
