@@ -510,30 +510,37 @@ def launch_ranks(a, script=None, argv=None):
                                       stdout=None if r == 0 else subprocess.DEVNULL))
     log(f"launched {a.gpus} rank processes (pids {[p.pid for p in procs]}), master port {port}")
     status = 0
-    live = {p.pid: p for p in procs}
+    live = {r: p for r, p in enumerate(procs)}
+    # an overall bound (a rank stuck in a collective must not hang the launcher): PDVC_LAUNCH_TIMEOUT seconds
+    limit = time.time() + float(os.environ.get("PDVC_LAUNCH_TIMEOUT", "3600"))
     deadline = None  # set once a rank failed: the others get 20 s after SIGTERM, then SIGKILL
     while live:
-        # reap in exit order (os.waitpid on any child): the FIRST failing rank's status is the job's, not that of a
-        # peer that then lost its collective connection and exited in the same instant
-        pid, wst = os.waitpid(-1, 0 if deadline is None else os.WNOHANG)
-        if pid == 0:  # (WNOHANG) nobody exited yet
-            if time.time() > deadline:
+        # poll only the rank processes (a waitpid(-1) would also reap children this process did not start); the
+        # first failing rank seen sets the job's status, not a peer that then lost its collective connection
+        exited = [(r, p.poll()) for r, p in list(live.items())]
+        exited = [(r, rc) for r, rc in exited if rc is not None]
+        for r, rc in exited:
+            live.pop(r)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 1
+                log(f"rank {r} (pid {procs[r].pid}) exited with {rc}: stopping the other ranks")
                 for q in live.values():
-                    q.kill()
-                deadline = float("inf")
-            time.sleep(0.1)
-            continue
-        p = live.pop(pid, None)
-        if p is None:
-            continue
-        rc = os.waitstatus_to_exitcode(wst)
-        p.returncode = rc
-        if rc != 0 and status == 0:
-            status = rc if rc > 0 else 1
-            log(f"rank pid {pid} exited with {rc}: stopping the other ranks")
+                    q.terminate()
+                deadline = time.time() + 20
+        if not live:
+            break
+        now = time.time()
+        if deadline is None and now > limit:
+            log(f"ranks still running after PDVC_LAUNCH_TIMEOUT: stopping them")
+            status = 124
             for q in live.values():
                 q.terminate()
-            deadline = time.time() + 20
+            deadline = now + 20
+        if deadline is not None and now > deadline:
+            for q in live.values():
+                q.kill()
+            deadline = float("inf")
+        time.sleep(0.1)
     return status
 
 
@@ -702,7 +709,7 @@ def main():
         "value": videos / el, "unit": "videos/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": 1000.0 * el / a.steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "bf16" if bf16 else "f32", "data": "synthetic",
-        "config": {"workload": f"{os.path.basename(a.cfg)[:-4]} training step (fwd+loss+bwd+allreduce+AdamW): " +
+        "config": {"workload": f"{os.path.basename(a.cfg)[:-4]} training step (fwd+loss+bwd" + ("+allreduce" if world > 1 else "") + "+AdamW): " +
                                ("dual-modality MHA front-end (clips + sound, 768-d, 32 heads) + " if a.frontend
                                 else "") +
                                f"T={a.T} C={a.C} L=4 Q={a.Q} {args.enc_layers} enc/{args.dec_layers} dec layers, " +

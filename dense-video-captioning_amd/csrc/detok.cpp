@@ -27,6 +27,7 @@ extern "C" int pdvc_detokenize(const int64_t* seqs, int rows, int len, const cha
                 return pdvc_set_error(PDVC_ERR_INVALID_ARG, "pdvc_detokenize: word id %lld outside [1, %d)", (long long)w,
                                       num_words);
             const int64_t a = word_off[w], b = word_off[w + 1];
+            if (b < a) return pdvc_set_error(PDVC_ERR_INVALID_ARG, "pdvc_detokenize: word_off decreases at id %lld", (long long)w);
             if (pos + (b - a) + 2 > out_cap) return pdvc_set_error(PDVC_ERR_INVALID_ARG, "pdvc_detokenize: output full");
             if (i) out[pos++] = ' ';
             std::memcpy(out + pos, words + a, (size_t)(b - a));

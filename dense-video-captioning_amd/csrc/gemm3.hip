@@ -31,6 +31,7 @@ namespace pdvc {
 namespace g3 {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -178,10 +179,27 @@ __device__ __forceinline__ f32x16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[
     return x;
 }
 
-template <int EPI, bool FULL, int BI = 2, int BJ = 2>
-__device__ __forceinline__ void store_tile(const f32x16 (&acc)[BI][BJ], float* __restrict__ C, long ldc,
-                                           const float* __restrict__ bias, int r0, int c0, int M, int N, int l32,
-                                           int h, Drop drp = Drop{nullptr, 0u, 1.f, nullptr}) {
+// accumulator layouts: SZ = 32, v_mfma_f32_32x32x16_bf16 (register r of lane l: row (r & 3) + 8 (r >> 2) + 4 (l >> 5),
+// column l & 31); SZ = 16, v_mfma_f32_16x16x32_bf16 (row r + 4 (l >> 4), column l & 15; a 16 x 16 x 32 form of
+// gemm3p / gemm3w measured slower, profiles/r06_gemm3_mf16_rejected.txt).  lrow / lcol: the lane's row offset and
+// column
+template <int SZ> struct Lay;
+template <> struct Lay<32> {
+    typedef f32x16 acc_t;
+    static constexpr int NR = 16;
+    __device__ static constexpr int dr(int r) { return (r & 3) + 8 * (r >> 2); }
+};
+template <> struct Lay<16> {
+    typedef f32x4 acc_t;
+    static constexpr int NR = 4;
+    __device__ static constexpr int dr(int r) { return r; }
+};
+
+template <int EPI, bool FULL, int BI = 2, int BJ = 2, int SZ = 32>
+__device__ __forceinline__ void store_tile(const typename Lay<SZ>::acc_t (&acc)[BI][BJ], float* __restrict__ C,
+                                           long ldc, const float* __restrict__ bias, int r0, int c0, int M, int N,
+                                           int lcol, int lrow, Drop drp = Drop{nullptr, 0u, 1.f, nullptr}) {
+    constexpr int NR = Lay<SZ>::NR;
     constexpr bool BIASED = EPI == EPI_BIAS || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_RELU_DROP;
     if constexpr (EPI == EPI_BIAS_RELU_DROP) {
         // ffn_keep's hash split by what it depends on: the inner mix of the row once per row (rows outer, the column
@@ -191,20 +209,20 @@ __device__ __forceinline__ void store_tile(const f32x16 (&acc)[BI][BJ], float* _
         float bvs[BJ];
 #pragma unroll
         for (int j = 0; j < BJ; ++j) {
-            const int col = c0 + 32 * j + l32;
+            const int col = c0 + SZ * j + lcol;
             cterm[j] = (uint32_t)col * 0xc2b2ae35U + (uint32_t)(seed >> 32);
             bvs[j] = bias[(FULL || col < N) ? col : 0];
         }
 #pragma unroll
         for (int i = 0; i < BI; ++i) {
-            const int rbase = r0 + 32 * i + 4 * h;
+            const int rbase = r0 + SZ * i + lrow;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int dr = (r & 3) + 8 * (r >> 2), row = rbase + dr;
+            for (int r = 0; r < NR; ++r) {
+                const int dr = Lay<SZ>::dr(r), row = rbase + dr;
                 const uint32_t rm = ffn_mix((uint32_t)row * 0x9e3779b1U ^ (uint32_t)seed);
 #pragma unroll
                 for (int j = 0; j < BJ; ++j) {
-                    const int col = c0 + 32 * j + l32;
+                    const int col = c0 + SZ * j + lcol;
                     if (FULL || (col < N && row < M)) {
                         const float v = fmaxf(acc[i][j][r] + bvs[j], 0.f);
                         const bool keep = (ffn_mix(rm + cterm[j]) >> 8) >= drp.thresh;
@@ -217,28 +235,28 @@ __device__ __forceinline__ void store_tile(const f32x16 (&acc)[BI][BJ], float* _
     }
 #pragma unroll
     for (int j = 0; j < BJ; ++j) {
-        const int col = c0 + 32 * j + l32;
+        const int col = c0 + SZ * j + lcol;
         const bool colok = FULL || col < N;
         const float bv = BIASED ? bias[colok ? col : 0] : 0.f;
 #pragma unroll
         for (int i = 0; i < BI; ++i) {
-            const int rbase = r0 + 32 * i + 4 * h;
+            const int rbase = r0 + SZ * i + lrow;
             float* p0 = C + (long)rbase * ldc + col;
             // accumulate: the block's 16 old values loaded before any store -- the rows are distinct (ldc >= N >= 1),
             // but the compiler cannot prove a store leaves the next row's load alone, and interleaved it waited for
             // every load in turn (load, vmcnt(0), add, store: 128 round trips per lane and tile)
-            float old[16];
+            float old[NR];
             if constexpr (EPI == EPI_ACCUM || EPI == EPI_DMASK) {  // (EPI_DMASK: the forward output's values)
                 const float* q0 = EPI == EPI_DMASK ? drp.hd + ((long)rbase * ldc + col) : p0;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int dr = (r & 3) + 8 * (r >> 2);
+                for (int r = 0; r < NR; ++r) {
+                    const int dr = Lay<SZ>::dr(r);
                     old[r] = (FULL || (colok && rbase + dr < M)) ? q0[(long)dr * ldc] : 0.f;
                 }
             }
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int dr = (r & 3) + 8 * (r >> 2);
+            for (int r = 0; r < NR; ++r) {
+                const int dr = Lay<SZ>::dr(r);
                 if (FULL || (colok && rbase + dr < M)) {
                     float v = acc[i][j][r] + bv;
                     if (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.f);
@@ -361,9 +379,9 @@ __global__ __launch_bounds__(NT, 1) void gemm3_kernel(int M, int N, int K, const
     float* Cz = C + (EPI == EPI_SLAB ? (long)blockIdx.z * slab : 0);
     const bool full = m0 + BM <= M && n0 + BN <= N;  // whole tile inside C: no per-element checks
     if (full) {
-        store_tile<EPI, true>(acc, Cz, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h);
+        store_tile<EPI, true>(acc, Cz, ldc, bias, m0 + wm, n0 + wn, M, N, l32, 4 * h);
     } else {
-        store_tile<EPI, false>(acc, Cz, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h);
+        store_tile<EPI, false>(acc, Cz, ldc, bias, m0 + wm, n0 + wn, M, N, l32, 4 * h);
     }
 }
 
@@ -612,8 +630,8 @@ __global__ __launch_bounds__(NT, 1) void gemm3p_kernel(int M, int N, int K, cons
         return;
     }
     const bool full = m0 + BM <= M && n0 + BN <= N;
-    if (full) store_tile<EPI, true, 4, 2>(acc, C, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h, drp);
-    else store_tile<EPI, false, 4, 2>(acc, C, ldc, bias, m0 + wm, n0 + wn, M, N, l32, h, drp);
+    if (full) store_tile<EPI, true, 4, 2>(acc, C, ldc, bias, m0 + wm, n0 + wn, M, N, l32, 4 * h, drp);
+    else store_tile<EPI, false, 4, 2>(acc, C, ldc, bias, m0 + wm, n0 + wn, M, N, l32, 4 * h, drp);
 }
 
 // ---- both operands mn-contiguous (the weight gradient dW = dy^T x: the reduction runs over the rows of both) ----
@@ -741,8 +759,8 @@ __global__ __launch_bounds__(NT, 1) void gemm3w_kernel(int M, int N, int K, cons
     (void)l32;
     float* Cz = C + (EPI == EPI_SLAB ? (long)zz * slab : 0);
     const bool full = m0 + BM <= M && n0 + BN <= N;
-    if (full) store_tile<EPI, true, 4, 2>(acc, Cz, ldc, nullptr, m0 + wm, n0 + wn, M, N, l32, h);
-    else store_tile<EPI, false, 4, 2>(acc, Cz, ldc, nullptr, m0 + wm, n0 + wn, M, N, l32, h);
+    if (full) store_tile<EPI, true, 4, 2>(acc, Cz, ldc, nullptr, m0 + wm, n0 + wn, M, N, l32, 4 * h);
+    else store_tile<EPI, false, 4, 2>(acc, Cz, ldc, nullptr, m0 + wm, n0 + wn, M, N, l32, 4 * h);
 }
 
 // out[i] (=|+=) sum_z ws[z * n + i], float4 lanes (n % 4 == 0)

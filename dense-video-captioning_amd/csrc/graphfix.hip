@@ -134,8 +134,62 @@ extern "C" int pdvc_event_record_external(void* event, void* stream) {
                            : pdvc_set_error(PDVC_ERR_LAUNCH, "hipStreamUpdateCaptureDependencies: %s", hipGetErrorString(e));
 }
 
+extern "C" int pdvc_event_record_captured(void* event, void* stream) {
+    PDVC_CHECK_ARG(event != nullptr, "event is NULL");
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    const hipError_t e = hipStreamIsCapturing((hipStream_t)stream, &st);
+    if (e != hipSuccess) return pdvc_set_error(PDVC_ERR_LAUNCH, "hipStreamIsCapturing: %s", hipGetErrorString(e));
+    PDVC_CHECK_ARG(st == hipStreamCaptureStatusActive,
+                   "pdvc_event_record_captured: the stream is not capturing (a bucket event recorded outside the "
+                   "captured step would not gate the replays' all-reduces)");
+    return pdvc_event_record_external(event, stream);
+}
+
 extern "C" int pdvc_stream_wait_event(void* stream, void* event) {
     PDVC_CHECK_ARG(event != nullptr, "event is NULL");
     const hipError_t e = hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0);
     return e == hipSuccess ? PDVC_OK : pdvc_set_error(PDVC_ERR_LAUNCH, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+}
+
+// ---- the overlap probe's gate: a host flag the device polls (fine-grained, coherent pinned memory) ----
+namespace {
+__global__ void spin_until_flag_kernel(const int* flag, int value, unsigned long long ticks) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+    // system-scope loads: vector loads past the caches, each one a read of the host's int
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != value) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) return;  // bounded: the grid always drains
+        __builtin_amdgcn_s_sleep(32);
+    }
+}
+}  // namespace
+
+extern "C" int pdvc_host_flag_alloc(void** host, void** dev) {
+    PDVC_CHECK_ARG(host != nullptr && dev != nullptr, "host / dev is NULL");
+    void* h = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+        return pdvc_set_error(PDVC_ERR_LAUNCH, "hipHostMalloc");
+    *reinterpret_cast<volatile int*>(h) = 0;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+        (void)hipHostFree(h);
+        return pdvc_set_error(PDVC_ERR_LAUNCH, "hipHostGetDevicePointer");
+    }
+    *host = h;
+    *dev = d;
+    return PDVC_OK;
+}
+
+extern "C" int pdvc_host_flag_free(void* host) {
+    PDVC_CHECK_ARG(host != nullptr, "host is NULL");
+    return hipHostFree(host) == hipSuccess ? PDVC_OK : pdvc_set_error(PDVC_ERR_LAUNCH, "hipHostFree");
+}
+
+extern "C" int pdvc_spin_until_flag(const int* dev_flag, int value, int timeout_ms, void* stream) {
+    PDVC_CHECK_ARG(dev_flag != nullptr, "flag is NULL");
+    PDVC_CHECK_ARG(timeout_ms > 0 && timeout_ms <= 10000, "timeout_ms must be in (0, 10000]");
+    hipLaunchKernelGGL(spin_until_flag_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, dev_flag, value,
+                       (unsigned long long)timeout_ms * 100000ull);
+    PDVC_CHECK_LAUNCH("spin_until_flag_kernel");
+    return PDVC_OK;
 }

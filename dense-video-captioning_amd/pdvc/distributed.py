@@ -44,9 +44,12 @@ class GraphEvent:
         _n.call("pdvc_event_create", ctypes.addressof(h))
         self.handle = h
 
-    def record(self, stream=None):
+    def record(self, stream=None, captured=False):
+        """captured=True: an error unless the stream is capturing (pdvc_event_record_captured) -- the reducer's
+        bucket records, which would otherwise be plain records that every replay's all-reduce races past."""
         s = stream if stream is not None else torch.cuda.current_stream()
-        self._n.call("pdvc_event_record_external", self.handle, ctypes.c_void_p(s.cuda_stream))
+        fn = "pdvc_event_record_captured" if captured else "pdvc_event_record_external"
+        self._n.call(fn, self.handle, ctypes.c_void_p(s.cuda_stream))
 
     def wait(self, stream):
         self._n.call("pdvc_stream_wait_event", ctypes.c_void_p(stream.cuda_stream), self.handle)
@@ -180,7 +183,7 @@ class GradAllReducer:
         self.pending[bi] -= 1
         if self.capturing:  # the bucket's gradients are final at this point of the captured stream
             if self.pending[bi] == 0:
-                self.events[bi].record()
+                self.events[bi].record(captured=True)
                 self._recorded[bi] = True
             return
         if self.active is not None:
@@ -239,7 +242,7 @@ class GradAllReducer:
         not taken in the captured step) records its event here, where every gradient of the step is final."""
         for bi, ev in enumerate(self.events):
             if not self._recorded[bi]:
-                ev.record()
+                ev.record(captured=True)
         self.capturing = False
         self._reset()
 

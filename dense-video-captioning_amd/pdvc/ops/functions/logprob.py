@@ -116,7 +116,9 @@ class LogitPickFunction(Function):
             Wp[:V] = weight
             gx = mm_dgrad(G, Wp).view(*ctx.lead, weight.shape[1])
         if ctx.needs_input_grad[1]:
-            gw = wgrad_mm(Gv, x2)
+            # on the padded (rows, Vp) buffer (zeros past V): its width qualifies for gemm3w, where the strided
+            # (rows, V) view made wgrad_mm fall back to a reshaped copy and a library GEMM
+            gw = wgrad_mm(G, x2)[:V]
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = colsum(G)[:V]
         return gx, gw, gb, None

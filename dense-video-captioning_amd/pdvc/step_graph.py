@@ -133,61 +133,82 @@ _DP_OVERLAP = []
 
 def dp_overlap_supported():
     """Whether an event recorded inside a stream capture (GraphEvent, hipEventRecordExternal) gates a stream outside
-    the graph on this stack -- probed once: the marker is zeroed, then a replay runs a chain of element-wise passes,
-    writes 7 into the marker, records the event, runs more passes and writes 3; a side stream waits on the event
-    right after the replay is queued and copies the marker: it must never read the zero (a wait that did not hold
-    runs at once, while the replay is still in its first passes; tools/probe_external_event.py shows that control).
-    A record that never fires is bounded by a host-side timeout.  PDVC_DP_OVERLAP=0 turns the overlap off."""
+    the graph on this stack -- probed once, deterministically.  The probe graph first runs a kernel that holds its
+    stream until the host sets a flag (pdvc_spin_until_flag: fine-grained pinned memory, bounded at 5 s), then writes
+    7 into a marker, records the event and writes 3.  After each replay is queued, a control stream that does NOT
+    wait copies the marker, and a side stream waits on the event and copies it.  While the flag is held the control
+    copy must finish and read 0 (the side streams do run beside a held replay) and the waiting copy must not have
+    finished; released, it must read 7 or 3.  A record that does not gate fails the second test every time, not by
+    timing (the earlier probe's ungated control could read 3 when the replay happened to finish
+    first).  PDVC_DP_OVERLAP=0 turns the overlap off."""
     if os.environ.get("PDVC_DP_OVERLAP", "1") == "0":
         return False
     if not _DP_OVERLAP:
         ok = False
+        host = ctypes.c_void_p()
+        dev = ctypes.c_void_p()
+        from . import _native as _n
         try:
             import time
             from .distributed import GraphEvent
-            big = torch.ones(1 << 22, device="cuda")
+            _n.call("pdvc_host_flag_alloc", ctypes.byref(host), ctypes.byref(dev))
+            flag = ctypes.c_int.from_address(host.value)
             mark = torch.zeros(1, device="cuda")
             ev = GraphEvent()
             g = torch.cuda.CUDAGraph()
             recorded = True
             with torch.cuda.graph(g):
-                for _ in range(64):  # ~ms of work before the record
-                    big.mul_(1.0001).add_(1e-4)
-                mark.copy_(big[:1] * 0.0 + 7.0)
+                _n.call("pdvc_spin_until_flag", dev, 1, 5000, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                mark.fill_(7.0)
                 try:  # a refused record must not raise out of the capture (a torch graph whose capture raised
-                    ev.record()  # aborts the process when it is destroyed)
+                    ev.record(captured=True)  # aborts the process when it is destroyed)
                 except Exception:  # noqa: BLE001
                     recorded = False
-                for _ in range(64):
-                    big.mul_(1.0001).add_(1e-4)
                 mark.fill_(3.0)
             if not recorded:
                 raise RuntimeError("the event record was refused inside the capture")
-            side = torch.cuda.Stream()
-            seen = []
-            for _ in range(3):
+            side, ctrl = torch.cuda.Stream(), torch.cuda.Stream()
+            trials = []
+            for _ in range(2):
+                flag.value = 0
                 mark.zero_()
+                torch.cuda.synchronize()
                 g.replay()
+                with torch.cuda.stream(ctrl):
+                    seen_ctrl = mark.clone()
+                    ctrl_done = torch.cuda.Event()
+                    ctrl_done.record()
                 ev.wait(side)
                 with torch.cuda.stream(side):
-                    seen.append(mark.clone())
+                    seen = mark.clone()
                     done = torch.cuda.Event()
                     done.record()
+                t0 = time.time()
+                while not ctrl_done.query() and time.time() - t0 < 2.0:
+                    time.sleep(0.001)
+                ctrl_ran = ctrl_done.query()
+                held = not done.query()
+                flag.value = 1
                 t0 = time.time()
                 while not done.query():
                     if time.time() - t0 > 20.0:
                         raise RuntimeError("the captured event never fired")
                     time.sleep(0.001)
-            torch.cuda.synchronize()
-            ok = all(float(v) in (7.0, 3.0) for v in seen)
+                torch.cuda.synchronize()
+                trials.append((ctrl_ran, held, float(seen_ctrl), float(seen)))
+            ok = all(c and h and vc == 0.0 and v in (7.0, 3.0) for c, h, vc, v in trials)
             if os.environ.get("PDVC_DP_OVERLAP_DEBUG"):
-                print("dp_overlap_supported: markers read behind the event", [float(v) for v in seen])
+                print("dp_overlap_supported: (control ran, waiting copy held, control read, waiting read)", trials)
             del g
-        except Exception as e:  # noqa: BLE001 -- any failure: keep the serial reduction
+        except Exception:  # noqa: BLE001 -- any failure: keep the serial reduction
             if os.environ.get("PDVC_DP_OVERLAP_DEBUG"):
                 import traceback
                 traceback.print_exc()
             ok = False
+        finally:
+            if host.value:
+                torch.cuda.synchronize()
+                _n.call("pdvc_host_flag_free", host)
         _DP_OVERLAP.append(ok)
     return _DP_OVERLAP[0]
 

@@ -404,6 +404,18 @@ int pdvc_event_create(void** event);
 int pdvc_event_destroy(void* event);
 int pdvc_event_record_external(void* event, void* stream);
 int pdvc_stream_wait_event(void* stream, void* event);
+/* The same record, but an error unless `stream` is capturing (PDVC_ERR_INVALID_ARG): the reducer's bucket hooks use it, so a
+ * hook that runs on a stream outside the capture fails the capture instead of recording a plain (already satisfied)
+ * event that every replay's all-reduce would race past. */
+int pdvc_event_record_captured(void* event, void* stream);
+
+/* The overlap probe's gate (pdvc/step_graph.py dp_overlap_supported): a fine-grained host flag (coherent pinned
+ * memory; *host and *dev address the same int) and a one-thread kernel that holds `stream` until the flag reads
+ * `value` or timeout_ms elapses.  Captured before the probe's event record, it keeps the record from firing while
+ * the host checks that a stream waiting on the event has not run -- the probe is then deterministic. */
+int pdvc_host_flag_alloc(void** host, void** dev);
+int pdvc_host_flag_free(void* host);
+int pdvc_spin_until_flag(const int* dev_flag, int value, int timeout_ms, void* stream);
 
 /* ---- box refinement: out = sigmoid(tmp + inverse_sigmoid(ref)) (deformable_transformer.py:303-313) ----------
  * tmp, out (rows, 2) (centre, length); ref (rows, rd), rd = 2, or 1 (only the centre refined); inverse_sigmoid clamps

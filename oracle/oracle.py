@@ -38,6 +38,9 @@ def build(force=False):
 def _load():
     global _lib
     if _lib is None:
+        if os.environ.get("PDVC_ORACLE_LIB"):  # the sanitizer pass's build (tools/sanitize/run.sh)
+            _lib = ctypes.CDLL(os.environ["PDVC_ORACLE_LIB"])
+            return _lib
         build()
         _lib = ctypes.CDLL(_LIB_PATH)
     return _lib

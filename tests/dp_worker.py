@@ -41,12 +41,14 @@ def main():
         sg.replay()
         sg.replay()
         overlap = sg.overlap
+        event_nodes = int(sg.node_counts.get("event_record", 0))
     else:
         model.zero_grad(set_to_none=True)
         _, loss = model(dt, criterion, "queries")
         sum(loss[k] * wd[k] for k in loss.keys() if k in wd).backward()
         reducer.finish()
         overlap = False
+        event_nodes = 0
     torch.cuda.synchronize()
     res = {}
     for n, p in model.named_parameters():
@@ -55,7 +57,8 @@ def main():
         else:
             res["grad." + n] = p.grad.detach().cpu().numpy()
     res["n_buckets"] = np.asarray(len(reducer.buckets))
-    res["overlap"] = np.asarray(int(overlap))  # graph mode: the all-reduces queued behind the capture's events
+    res["overlap"] = np.asarray(int(overlap))
+    res["event_nodes"] = np.asarray(event_nodes)  # graph mode: one event-record node per bucket in the replayed graph  # graph mode: the all-reduces queued behind the capture's events
     np.savez(out, **res)
     dist.barrier()
     dist.destroy_process_group()

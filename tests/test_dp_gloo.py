@@ -155,7 +155,8 @@ def test_capture_events_bookkeeping(monkeypatch):
         def __init__(self):
             self.i = None
 
-        def record(self):
+        def record(self, captured=False):
+            assert captured, "bucket events must be recorded with captured=True"
             log.append(("record", self.i))
 
         def wait(self, stream):

@@ -73,6 +73,8 @@ def test_two_ranks_equal_union_batch(tmp_path, union, mode):
         assert int(g["n_buckets"]) >= 2
         if mode == "graph":  # the replays' all-reduces ran behind the capture's per-bucket events (overlapped)
             assert int(g["overlap"]) == 1, "the capture's bucket events were not usable: reduction not overlapped"
+            assert int(g["event_nodes"]) == int(g["n_buckets"]), \
+                "the replayed graph must hold one event-record node per bucket (ADVICE round 5)"
         for n, ref in union.items():
             if ref is None:
                 assert "none." + n in g.files, f"rank {r}: {n} must stay None"
