@@ -415,8 +415,9 @@ def log(msg):
 
 def eval_main(a):
     """Evaluation throughput: forward with greedy captions for all Q queries (LSTM_DSA.py:118-186, the loop stops
-    when every row has finished, one host check per step as the reference) + PostProcess (pdvc.py:493-546,
-    captions detokenised on the host).  Eager: the decode's length is data-dependent.  One GPU."""
+    when every row has finished: tested on the device, read back a few steps late, the decode cut at the reference's
+    exit step) + PostProcess (pdvc.py:493-546, captions detokenised on the host on a worker thread while the next
+    batch is queued; drained inside the timed region).  Eager: the decode's length is data-dependent.  One GPU."""
     import types
     from pdvc.data import synthetic_videos, collate, to_device
     from data.video_dataset import Translator
@@ -444,6 +445,7 @@ def eval_main(a):
     log(f"eval: {B} videos, warm-up")
     for _ in range(a.warmup):
         step()
+    post.drain()
     torch.cuda.synchronize()
     # every step timed on its own: host wall time (the greedy loop checks for finished rows on the host once per
     # decode step, LSTM_DSA.py:172-179) beside the device time between two events on the step's stream, so a slow
@@ -459,6 +461,7 @@ def eval_main(a):
         torch.cuda.synchronize()
         walls.append(1e3 * (time.perf_counter() - w0))
         devs.append(e0.elapsed_time(e1))
+    post.drain()  # the last steps' deferred host halves (captions) are part of the timed work
     el = time.perf_counter() - t0
     ws, ds = sorted(walls), sorted(devs)
     med = ws[len(ws) // 2] if len(ws) % 2 else 0.5 * (ws[len(ws) // 2 - 1] + ws[len(ws) // 2])

@@ -11,6 +11,7 @@
 // registers, summed over the workgroup in LDS and over workgroups by a second small kernel.
 // The same kernels serve NewModel's front-end (NewModel.py:41-65, `ln(h) + residual`, d = 768): no s term, the
 // residual added after the affine (pdvc_layernorm_residual_*).
+#include "an_hash.h"
 #include "pdvc_common.h"
 
 namespace pdvc {
@@ -18,16 +19,6 @@ namespace pdvc {
 constexpr int kAND = 768;              // max row width
 constexpr int kANW = 4;                // waves per workgroup
 
-__device__ __forceinline__ uint32_t an_mix(uint32_t x) {
-    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
-    return x;
-}
-
-// keep with probability 1 - p: 24-bit uniform from (seed, row, col)
-__device__ __forceinline__ bool an_keep(uint64_t seed, uint32_t row, uint32_t col, uint32_t thresh) {
-    const uint32_t h = an_mix(an_mix(row * 0x9e3779b9U ^ (uint32_t)seed) + col * 0x85ebca6bU + (uint32_t)(seed >> 32));
-    return (h >> 8) >= thresh;
-}
 
 __device__ __forceinline__ float an_wave_sum(float v) {
 #pragma unroll
@@ -347,12 +338,6 @@ __global__ __launch_bounds__(256) void addnorm_colsum_kernel(const float* __rest
     }
 }
 
-static uint32_t an_threshold(float p) {
-    double t = (double)p * 16777216.0;
-    if (t < 0) t = 0;
-    if (t > 16777216.0) t = 16777216.0;
-    return (uint32_t)t;
-}
 
 static int an_grid(int rows, int cap) {
     const int want = (rows + kANW - 1) / kANW;

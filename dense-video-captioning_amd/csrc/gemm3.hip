@@ -24,6 +24,7 @@
 // so the 16-lane groups of a fragment read hit 16 distinct 16-B bank slots), double buffered: one barrier a stage.
 #include <type_traits>
 
+#include "an_hash.h"
 #include "ffn_hash.h"
 #include "pdvc_common.h"
 
@@ -52,7 +53,7 @@ constexpr int ROWB = 64;   // bytes per LDS image row (BK bf16)
 constexpr int NT = 512;    // threads per workgroup
 
 enum { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_RELU = 2, EPI_ACCUM = 3, EPI_SLAB = 4, EPI_BIAS_RELU_DROP = 5,
-       EPI_DMASK = 6 };
+       EPI_DMASK = 6, EPI_RESID_DROP = 7 };
 
 // EPI_BIAS_RELU_DROP: the feed-forward block's relu -> dropout in the epilogue of linear1 (ffn.hip's forward pass,
 // the same keep mask bit for bit: ffn_hash.h); seed read on the device (graph-safe), scale = 1 / (1 - p)
@@ -61,6 +62,7 @@ struct Drop {
     uint32_t thresh;
     float scale;
     const float* hd;  // EPI_DMASK: the forward's relu -> dropout output (C's shape and ldc); C = hd > 0 ? acc * scale : 0
+                      // EPI_RESID_DROP: the residual x (C's shape and ldc); C = x + keep ? (acc + bias) * scale : 0
 };
 
 __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
@@ -181,7 +183,7 @@ __device__ __forceinline__ f32x16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[
 
 // accumulator layouts: SZ = 32, v_mfma_f32_32x32x16_bf16 (register r of lane l: row (r & 3) + 8 (r >> 2) + 4 (l >> 5),
 // column l & 31); SZ = 16, v_mfma_f32_16x16x32_bf16 (row r + 4 (l >> 4), column l & 15; a 16 x 16 x 32 form of
-// gemm3p / gemm3w measured slower, profiles/r06_gemm3_mf16_rejected.txt).  lrow / lcol: the lane's row offset and
+// gemm3p / gemm3w measured slower, profiles/r06_gemm3_rejected.txt).  lrow / lcol: the lane's row offset and
 // column
 template <int SZ> struct Lay;
 template <> struct Lay<32> {
@@ -201,6 +203,51 @@ __device__ __forceinline__ void store_tile(const typename Lay<SZ>::acc_t (&acc)[
                                            int lcol, int lrow, Drop drp = Drop{nullptr, 0u, 1.f, nullptr}) {
     constexpr int NR = Lay<SZ>::NR;
     constexpr bool BIASED = EPI == EPI_BIAS || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_RELU_DROP;
+    if constexpr (EPI == EPI_RESID_DROP) {
+        // the residual sub-layer's sum t = x + dropout(acc + bias) for the add-norm pass that then reads t alone:
+        // the keep mask of addnorm.hip's forward (an_hash.h) for element (row, col), its row part once per row;
+        // seed == NULL: no dropout (p = 0).  The block row's residual values are loaded before its stores (as the
+        // accumulate epilogue: interleaved, every load would wait for the stores before it)
+        const bool drop = drp.seed != nullptr;
+        const uint64_t seed = drop ? *drp.seed : 0ull;
+        uint32_t cterm[BJ];
+        float bvs[BJ];
+#pragma unroll
+        for (int j = 0; j < BJ; ++j) {
+            const int col = c0 + SZ * j + lcol;
+            cterm[j] = an_col(seed, (uint32_t)col);
+            bvs[j] = bias[(FULL || col < N) ? col : 0];
+        }
+#pragma unroll
+        for (int i = 0; i < BI; ++i) {
+            const int rbase = r0 + SZ * i + lrow;
+            float old[BJ][NR];
+#pragma unroll
+            for (int j = 0; j < BJ; ++j) {
+                const int col = c0 + SZ * j + lcol;
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const int row = rbase + Lay<SZ>::dr(r);
+                    old[j][r] = (FULL || (col < N && row < M)) ? drp.hd[(long)row * ldc + col] : 0.f;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int row = rbase + Lay<SZ>::dr(r);
+                const uint32_t rm = an_row(seed, (uint32_t)row);
+#pragma unroll
+                for (int j = 0; j < BJ; ++j) {
+                    const int col = c0 + SZ * j + lcol;
+                    if (FULL || (col < N && row < M)) {
+                        float v = acc[i][j][r] + bvs[j];
+                        if (drop) v = (an_mix(rm + cterm[j]) >> 8) >= drp.thresh ? v * drp.scale : 0.f;
+                        C[(long)row * ldc + col] = old[j][r] + v;
+                    }
+                }
+            }
+        }
+        return;
+    }
     if constexpr (EPI == EPI_BIAS_RELU_DROP) {
         // ffn_keep's hash split by what it depends on: the inner mix of the row once per row (rows outer, the column
         // blocks inner), the column term once per column block -- the v_mul_lo_u32 of the mask are quarter-rate
@@ -894,7 +941,7 @@ int gemmp_impl(int M, int N, int K, const float* A, long lda, const uint16_t* pl
                const float* bias, int epilogue, void* stream, Drop drp = Drop{nullptr, 0u, 1.f, nullptr}) {
     PDVC_CHECK_ARG(M >= 0 && N > 0 && K >= 0 && K % BK == 0, "sizes: N > 0, K a multiple of 32");
     PDVC_CHECK_ARG((epilogue >= 0 && epilogue <= 3) || (epilogue == EPI_BIAS_RELU_DROP && drp.seed != nullptr) ||
-                       (epilogue == EPI_DMASK && drp.hd != nullptr),
+                       ((epilogue == EPI_DMASK || epilogue == EPI_RESID_DROP) && drp.hd != nullptr),
                    "epilogue must be 0..3 (5, 6: through pdvc_gemm3p_relu_dropout_f32 / _dmask_f32)");
     PDVC_CHECK_ARG(epilogue == 0 || epilogue == 3 || epilogue == EPI_DMASK || bias != nullptr,
                    "bias epilogue needs a bias");
@@ -914,6 +961,9 @@ int gemmp_impl(int M, int N, int K, const float* A, long lda, const uint16_t* pl
         case 3: G3P_L(EPI_ACCUM); break;
         case EPI_BIAS_RELU_DROP:
             if constexpr (NP == 3) G3P_L(EPI_BIAS_RELU_DROP);
+            break;
+        case EPI_RESID_DROP:
+            if constexpr (NP == 3) G3P_L(EPI_RESID_DROP);
             break;
         default:
             if constexpr (NP == 3) G3P_L(EPI_DMASK);
@@ -956,6 +1006,20 @@ extern "C" int pdvc_gemm3p_dmask_f32(int M, int N, int K, const float* A, long l
     PDVC_CHECK_ARG(p >= 0.f && p < 1.f && hd != nullptr, "dropout p in [0, 1) and the forward output required");
     const Drop drp{nullptr, 0u, p > 0.f ? 1.f / (1.f - p) : 1.f, hd};
     return gemmp_impl<3>(M, N, K, A, lda, planes, C, ldc, nullptr, EPI_DMASK, stream, drp);
+}
+
+// the residual sub-layer's sum before its LayerNorm: C = R + dropout(A opB^T + bias) with the keep mask of
+// pdvc_add_dropout_layernorm_forward_f32 (an_hash.h) for element (row, col) of C and the same seed (p = 0: no
+// dropout, seed_dev may be NULL); R has C's shape and ldc.  The add-norm pass then reads C alone (s = NULL): its
+// forward and backward are those of the unfused pair, bit for bit
+extern "C" int pdvc_gemm3p_resid_dropout_f32(int M, int N, int K, const float* A, long lda, const uint16_t* planes,
+                                             float* C, long ldc, const float* bias, const float* R, float p,
+                                             const uint64_t* seed_dev, void* stream) {
+    PDVC_CHECK_ARG(p >= 0.f && p < 1.f, "dropout p must be in [0, 1)");
+    PDVC_CHECK_ARG(p == 0.f || seed_dev != nullptr, "p > 0 needs a device seed");
+    PDVC_CHECK_ARG(bias != nullptr && R != nullptr, "a bias and the residual R are required");
+    const Drop drp{p > 0.f ? seed_dev : nullptr, an_threshold(p), p > 0.f ? 1.f / (1.f - p) : 1.f, R};
+    return gemmp_impl<3>(M, N, K, A, lda, planes, C, ldc, bias, EPI_RESID_DROP, stream, drp);
 }
 
 // the bf16 mode's product: opB rounded to bf16 (one plane), A rounded in the kernel, one MFMA term, fp32 result

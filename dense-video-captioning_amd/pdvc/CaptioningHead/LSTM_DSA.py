@@ -201,6 +201,20 @@ class ShowAttendTellCore(nn.Module):
             self.alpha_net = nn.Linear(self.att_hid_size, 1)
 
 
+# the greedy loop's exit test on the device (decode_greedy): a count read every CHECK_EVERY steps, CHECK_LAG steps late
+CHECK_EVERY = 2
+CHECK_LAG = 4
+_PINNED = {}
+
+
+def _pinned_counts(n):
+    """A pinned host buffer of n int64 (per size, reused; each decode's copies are ordered by its own events)."""
+    b = _PINNED.get(n)
+    if b is None:
+        b = _PINNED[n] = torch.empty(n, dtype=torch.long, pin_memory=torch.cuda.is_available())
+    return b
+
+
 class LSTMDSACaptioner(Captioner):
     def __init__(self, opt):
         super().__init__(opt)
@@ -457,6 +471,15 @@ class LSTMDSACaptioner(Captioner):
         it = torch.zeros(R, dtype=torch.long, device=hs_rows.device)
         seq, seqlp = [], []
         unfinished = None
+        # the reference leaves the loop at the first step whose rows have all finished (LSTM_DSA.py:178-179).  Its
+        # test stays on the device: each step's count of unfinished rows goes into alive[t], and the host reads one
+        # count per CHECK_EVERY steps, CHECK_LAG steps late (an async copy into pinned memory), so the launches run
+        # ahead of the decode instead of waiting for every step's read-back; the steps decoded past the reference's
+        # exit are cut off after the loop from the counts (one read): seq and seqlp are exactly the reference's
+        dev = hs_rows.device
+        alive = torch.ones(max_len + 2, dtype=torch.long, device=dev)
+        host = _pinned_counts(max_len + 2)
+        pending = []  # (step, event) of the counts copied to the host, oldest first
         for t in range(max_len + 1):
             if t > 0:
                 if sample_max and logprobs is None:  # fused: argmax and its log-probability from the logits
@@ -483,10 +506,28 @@ class LSTMDSACaptioner(Captioner):
             logprobs = None if (fused and sample_max) else F.log_softmax(logits, dim=1)
             if t >= 1:
                 unfinished = (it > 0) if t == 1 else (unfinished & (it > 0))
-                if int(unfinished.sum()) == 0:
-                    break
+                torch.sum(unfinished, 0, out=alive[t])
                 seq.append(it * unfinished.type_as(it))
                 seqlp.append(sample_lp.view(-1))
+                if not alive.is_cuda:  # (CPU: the reference's immediate test)
+                    if int(alive[t]) == 0:
+                        break
+                elif t % CHECK_EVERY == 0:
+                    host[t].copy_(alive[t], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    pending.append((t, ev))
+                if pending and pending[0][0] <= t - CHECK_LAG:
+                    tc, ev = pending.pop(0)
+                    ev.synchronize()
+                    if int(host[tc]) == 0:
+                        break
+        if seq:  # the reference's exit: the first step with no unfinished row (its tokens are not appended)
+            counts = alive[1:len(seq) + 1].cpu()
+            zero = (counts == 0).nonzero()
+            if len(zero):
+                keep = int(zero[0, 0])
+                seq, seqlp = seq[:keep], seqlp[:keep]
         if not seq:
             return None, None
         return torch.stack(seq, 1), torch.stack(seqlp, 1)

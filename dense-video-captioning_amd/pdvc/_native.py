@@ -89,6 +89,7 @@ SIGNATURES = {
     "pdvc_gemm3p_f32": [_i, _i, _i, _vp, ctypes.c_long, _vp, _vp, ctypes.c_long, _vp, _i, _vp],
     "pdvc_gemm3p_relu_dropout_f32": [_i, _i, _i, _vp, ctypes.c_long, _vp, _vp, ctypes.c_long, _vp, _f, _vp, _vp],
     "pdvc_gemm3p_dmask_f32": [_i, _i, _i, _vp, ctypes.c_long, _vp, _vp, ctypes.c_long, _vp, _f, _vp],
+    "pdvc_gemm3p_resid_dropout_f32": [_i, _i, _i, _vp, ctypes.c_long, _vp, _vp, ctypes.c_long, _vp, _vp, _f, _vp, _vp],
     "pdvc_round_plane_f32": [_vp, ctypes.c_long, _i, _i, _i, _vp, _vp],
     "pdvc_gemm1p_f32": [_i, _i, _i, _vp, ctypes.c_long, _vp, _vp, ctypes.c_long, _vp, _i, _vp],
     "pdvc_gemm3_f32": [_i, _i, _i, _vp, ctypes.c_long, _i, _vp, ctypes.c_long, _i, _vp, ctypes.c_long, _vp, _i, _i,

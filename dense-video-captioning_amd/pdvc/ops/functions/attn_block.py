@@ -6,6 +6,8 @@ gradients of src meet:
   * src's three gradient paths (residual from the layer norm, value projection, query projection) accumulate in
     the epilogues of the two input-gradient GEMMs (beta = 1) instead of two autograd adds over (N*S, d);
   * output_proj's bias gradient comes out of the layer-norm backward pass (pdvc_add_dropout_layernorm ds_colsum);
+  * the residual sum src + dropout(output_proj(...)) is formed in output_proj's gemm3 epilogue
+    (pdvc_gemm3p_resid_dropout_f32), so the add-norm pass reads one tensor instead of two each way;
   * with a level-position handle (ops/functions/posembed.py) the position gradient is returned as per-(video,
     level) sums, sum_rows(d_proj) @ W_q, so the (N*S, d) position gradient is never formed nor accumulated over
     layers.
@@ -16,7 +18,7 @@ from torch.autograd.function import once_differentiable
 
 from pdvc import _native as _n
 from .addnorm import BWD_PARTS, an_backward, an_forward
-from .gemm3 import addmm_nt, mm_dgrad
+from .gemm3 import addmm_nt, addmm_resid_dropout_nt, mm_dgrad
 from .linear import colsum, wgrad_mm
 from .ms_deform_attn_func import NUM_SAMPLES, msda1d_backward, msda1d_forward
 from .posembed import LevelPos, level_row_sums
@@ -36,16 +38,26 @@ class EncoderAttnBlockFunction(Function):
         ref = ref.contiguous()
         out, save_attn, save_loc = msda1d_forward(value.view(N, S, M, D), pad_mask, proj.view(N, S, -1), ref,
                                                   level_T, 0, nq)
-        s2 = addmm_nt(bo, out.view(R, d), Wo)
         y = torch.empty_like(src2)
         mean = torch.empty(R, dtype=src.dtype, device=src.device)
         rstd = torch.empty_like(mean)
         seed_dev = seed if isinstance(seed, torch.Tensor) else None
         seed_int = 0 if seed_dev is not None else int(seed)
-        an_forward(src2, s2, gamma, beta, p, seed_int, seed_dev, eps, y, mean, rstd)
+        # output_proj's epilogue forms src + dropout(s2) (the add-norm pass's mask bits, device seed), and the pass
+        # reads that sum alone each way; s2 then holds the sum
+        s2 = None
+        if seed_dev is not None or p == 0:
+            s2 = addmm_resid_dropout_nt(bo, out.view(R, d), Wo, src2, float(p),
+                                        _n.ptr(seed_dev) if seed_dev is not None else None)
+        fused_sum = s2 is not None
+        if fused_sum:
+            an_forward(s2, None, gamma, beta, 0.0, 0, None, eps, y, mean, rstd)
+        else:
+            s2 = addmm_nt(bo, out.view(R, d), Wo)
+            an_forward(src2, s2, gamma, beta, p, seed_int, seed_dev, eps, y, mean, rstd)
         ctx.save_for_backward(src2, q, value, proj, ref, pad_mask, save_attn, save_loc, out, s2, Wv, Wq, Wo, gamma,
                               mean, rstd, seed_dev)
-        ctx.meta = (N, S, d, M, float(p), seed_int, tuple(level_T), handle is not None)
+        ctx.meta = (N, S, d, M, float(p), seed_int, tuple(level_T), handle is not None, fused_sum)
         return y.view(N, S, d)
 
     @staticmethod
@@ -53,7 +65,7 @@ class EncoderAttnBlockFunction(Function):
     def backward(ctx, dy):
         (src2, q, value, proj, ref, pad_mask, save_attn, save_loc, out, s2, Wv, Wq, Wo, gamma, mean, rstd,
          seed_dev) = ctx.saved_tensors
-        N, S, d, M, p, seed_int, level_T, has_handle = ctx.meta
+        N, S, d, M, p, seed_int, level_T, has_handle, fused_sum = ctx.meta
         R = N * S
         D = d // M
         dy2 = dy.reshape(R, d).contiguous()
@@ -63,7 +75,10 @@ class EncoderAttnBlockFunction(Function):
         dbeta = torch.empty_like(gamma)
         dbo = torch.empty_like(gamma)
         ws = torch.empty(3 * BWD_PARTS * d, dtype=src2.dtype, device=src2.device)
-        an_backward(src2, s2, gamma, mean, rstd, dy2, p, seed_int, seed_dev, d_src, d_s2, dgamma, dbeta, dbo, ws)
+        if fused_sum:  # s2 holds src + dropout(output_proj(out))
+            an_backward(s2, None, gamma, mean, rstd, dy2, p, seed_int, seed_dev, d_src, d_s2, dgamma, dbeta, dbo, ws)
+        else:
+            an_backward(src2, s2, gamma, mean, rstd, dy2, p, seed_int, seed_dev, d_src, d_s2, dgamma, dbeta, dbo, ws)
         dWo = wgrad_mm(d_s2, out.view(R, d))
         d_out = mm_dgrad(d_s2, Wo)
         nq = M * NUM_SAMPLES

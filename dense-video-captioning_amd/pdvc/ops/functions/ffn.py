@@ -10,7 +10,9 @@ forward_ffn, :233-237).  Same arithmetic as the module chain; what changes is wh
     dropout kept);
   * the residual gradient from the layer norm and linear1's input gradient meet in the dgrad GEMM's epilogue
     (dx = dx_residual + dh W1, beta = 1) instead of an autograd add;
-  * the residual epilogue is pdvc_add_dropout_layernorm (csrc/addnorm.hip).
+  * the residual sum x + dropout(linear2(h)) is formed in linear2's gemm3 epilogue (pdvc_gemm3p_resid_dropout_f32,
+    the add-norm pass's mask bits) and the residual epilogue pdvc_add_dropout_layernorm (csrc/addnorm.hip) reads it
+    alone each way.
 Both dropout masks are counter hashes of seeds drawn on the GPU (graph-safe), regenerated in the backward.
 """
 import ctypes
@@ -25,7 +27,7 @@ from pdvc import _native as _n
 from pdvc.precision import attach_bf16, bf16_active, shadow_for
 from .addnorm import BWD_PARTS, an_backward, an_forward
 from . import linear as _lin
-from .gemm3 import addmm_nt, addmm_relu_dropout_nt, mm_dgrad, mm_dgrad_dmask
+from .gemm3 import addmm_nt, addmm_relu_dropout_nt, addmm_resid_dropout_nt, mm_dgrad, mm_dgrad_dmask
 from .linear import CU, colsum, wgrad_mm
 
 
@@ -67,20 +69,27 @@ class FFNBlockFunction(Function):
                 _n.call("pdvc_relu_dropout_forward_f32_bf16out", _n.ptr(h), rows, h.shape[1], float(p_act), 0,
                         seed_act, _n.ptr(h16), _n.stream())
                 attach_bf16(h, h16)
-        y = addmm_nt(b2, h, w2)
         out = torch.empty_like(x2)
         mean = torch.empty(rows, dtype=x.dtype, device=x.device)
         rstd = torch.empty_like(mean)
-        an_forward(x2, y, gamma, beta, p_out, 0, seed_out, eps, out, mean, rstd)
+        # the residual sum t = x + dropout(linear2(h)) in linear2's epilogue, then the add-norm pass on t alone (one
+        # tensor fewer read each way); y is then t, and the backward's add-norm pass takes it with s = None
+        t = addmm_resid_dropout_nt(b2, h, w2, x2, float(p_out), seed_out)
+        if t is not None:
+            y = t
+            an_forward(t, None, gamma, beta, 0.0, 0, None, eps, out, mean, rstd)
+        else:
+            y = addmm_nt(b2, h, w2)
+            an_forward(x2, y, gamma, beta, p_out, 0, seed_out, eps, out, mean, rstd)
         ctx.save_for_backward(x2, h, y, w1, w2, gamma, mean, rstd, seeds)
-        ctx.meta = (shape, float(p_act), float(p_out))
+        ctx.meta = (shape, float(p_act), float(p_out), t is not None)
         return out.view(shape)
 
     @staticmethod
     @once_differentiable
     def backward(ctx, dout):
         x2, h, y, w1, w2, gamma, mean, rstd, seeds = ctx.saved_tensors
-        shape, p_act, p_out = ctx.meta
+        shape, p_act, p_out, fused_sum = ctx.meta
         rows, d = x2.shape
         fdim = h.shape[1]
         _, seed_out = _seed_ptrs(seeds)
@@ -91,7 +100,10 @@ class FFNBlockFunction(Function):
         dbeta = torch.empty_like(gamma)
         ws = torch.empty(3 * BWD_PARTS * d, dtype=x2.dtype, device=x2.device)
         db2 = torch.empty_like(gamma)  # linear2's bias gradient = column sums of dy, summed by the same pass
-        an_backward(x2, y, gamma, mean, rstd, dout2, p_out, 0, seed_out, dx, dy, dgamma, dbeta, db2, ws)
+        if fused_sum:  # y holds t = x + dropout(linear2(h)): the pass reads it alone
+            an_backward(y, None, gamma, mean, rstd, dout2, p_out, 0, seed_out, dx, dy, dgamma, dbeta, db2, ws)
+        else:
+            an_backward(x2, y, gamma, mean, rstd, dout2, p_out, 0, seed_out, dx, dy, dgamma, dbeta, db2, ws)
         dw2 = wgrad_mm(dy, h)
         db1 = torch.empty(fdim, dtype=h.dtype, device=h.device)
         dh = None

@@ -133,6 +133,31 @@ def addmm_relu_dropout_nt(bias, x, W, p, seed_ptr):
     return out
 
 
+RESID_EPILOGUE = os.environ.get("PDVC_RESID_FUSE", "1") != "0"
+
+
+def addmm_resid_dropout_nt(bias, x, W, resid, p, seed_ptr):
+    """resid + dropout(torch.addmm(bias, x, W.t()), p) -- the residual sub-layer's sum before its LayerNorm -- as one
+    gemm3p launch whose epilogue applies the add-norm pass's keep mask for the device seed at seed_ptr
+    (pdvc_gemm3p_resid_dropout_f32; p = 0: no mask), or None when the product does not take gemm3p (the caller then
+    runs the GEMM and the two-input add-norm pass)."""
+    M, K = x.shape
+    N = W.shape[0]
+    if not RESID_EPILOGUE or bias is None or M >= 2 ** 31 or not (0.0 <= p < 1.0) or (p > 0 and seed_ptr is None):
+        return None
+    if not _use(M, K, x, W, extra=(W.is_contiguous() and bias.is_contiguous() and resid.is_contiguous()
+                                   and resid.shape == (M, N))):
+        return None
+    if generic_wins(M, N, K):
+        return None
+    out = torch.empty((M, N), dtype=torch.float32, device=x.device)
+    FLOPS[0] += 2 * M * N * K
+    planes = split_planes(W, 1, N, K)
+    _n.call("pdvc_gemm3p_resid_dropout_f32", M, N, K, _n.ptr_any(x), x.stride(0), _n.ptr(planes), _n.ptr(out), N,
+            _n.ptr(bias), _n.ptr(resid), float(p), seed_ptr if p > 0 else None, _n.stream())
+    return out
+
+
 def mm_nt(x, W, out=None):
     return addmm_nt(None, x, W, out=out)
 

@@ -533,6 +533,61 @@ class PDVC(nn.Module):
         return out, loss
 
 
+_POOL = []
+_PENDING = []
+
+
+def _host_pool():
+    if not _POOL:
+        import concurrent.futures
+        _POOL.append(concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="pdvc-postprocess"))
+    return _POOL[0]
+
+
+def _host_captions(ev, host_scores, host_seq, tr, N, Q):
+    """The host half of PostProcess: the ranked tokens detokenised (Translator.rtranslate, data/video_dataset.py:
+    172-180) and the caption scores as per-video lists.  ev: the event behind the device -> pinned copies."""
+    if ev is not None:
+        ev.synchronize()
+    host_seq = host_seq.numpy().astype("int")
+    if hasattr(tr, "rtranslate_batch"):  # data.video_dataset.Translator: one vectorised pass
+        flat = tr.rtranslate_batch(host_seq.reshape(N * Q, -1))
+        caps = [flat[b * Q:(b + 1) * Q] for b in range(N)]
+    else:
+        caps = [[tr.rtranslate(s) for s in vid] for vid in host_seq]
+    return caps, [list(row) for row in host_scores.numpy()]
+
+
+class DeferredRow:
+    """One video's captions (part 0) or caption scores (part 1) of a deferred PostProcess host half: a read-only list
+    that waits for the worker on first use."""
+
+    def __init__(self, fut, part, b):
+        self._fut, self._part, self._b = fut, part, b
+
+    def value(self):
+        return self._fut.result()[self._part][self._b]
+
+    def __len__(self):
+        return len(self.value())
+
+    def __getitem__(self, i):
+        return self.value()[i]
+
+    def __iter__(self):
+        return iter(self.value())
+
+    def __eq__(self, other):
+        return list(self.value()) == (other.value() if isinstance(other, DeferredRow) else list(other))
+
+    def __repr__(self):
+        return repr(self.value())
+
+    def __array__(self, dtype=None, copy=None):
+        import numpy as np
+        return np.asarray(self.value(), dtype=dtype)
+
+
 class PostProcess(nn.Module):
     """Eval outputs of a batch -> one result dict per video, in the reference's format (pdvc/pdvc.py:493-546).
 
@@ -546,9 +601,17 @@ class PostProcess(nn.Module):
     The caption scores and tokens reach the host in one copy; captions are detokenised there by the
     loader's translator (`loader.dataset.translator.rtranslate`, data/video_dataset.py:172-180)."""
 
-    def __init__(self, opt):
+    def __init__(self, opt, defer_host=None):
         super().__init__()
         self.opt = opt
+        # the captions' host half on a worker thread (DeferredRow results; PostProcess.drain() waits for all)
+        self.defer_host = os.environ.get("PDVC_POST_DEFER", "1") != "0" if defer_host is None else bool(defer_host)
+
+    @staticmethod
+    def drain():
+        """Wait for every deferred host half (captions, caption scores) queued so far; re-raise its error."""
+        while _PENDING:
+            _PENDING.pop(0).result()
 
     @torch.no_grad()
     def forward(self, outputs, target_sizes, loader):
@@ -567,14 +630,21 @@ class PostProcess(nn.Module):
             cap_scores = (outputs["caption_probs"]["cap_prob_eval"] * (seq > 0)).sum(2).gather(1, query_id)
             seq_ranked = seq.gather(1, query_id[..., None].expand(N, Q, seq.shape[2]))
             tr = loader.dataset.translator
-            host_scores = cap_scores.double().cpu().numpy()
-            host_seq = seq_ranked.cpu().numpy().astype("int")
-            if hasattr(tr, "rtranslate_batch"):  # data.video_dataset.Translator: one vectorised pass
-                flat = tr.rtranslate_batch(host_seq.reshape(N * Q, -1))
-                caps = [flat[b * Q:(b + 1) * Q] for b in range(N)]
+            if self.defer_host and seq.is_cuda:
+                # the host half (captions detokenised, scores as lists) runs on a worker thread behind an event on
+                # the device copies, while the caller queues its next batch: the device does not idle through it
+                hs = torch.empty(cap_scores.shape, dtype=torch.float64, pin_memory=True)
+                hq = torch.empty(seq_ranked.shape, dtype=torch.long, pin_memory=True)
+                hs.copy_(cap_scores.double(), non_blocking=True)
+                hq.copy_(seq_ranked, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                fut = _host_pool().submit(_host_captions, ev, hs, hq, tr, N, Q)
+                _PENDING.append(fut)
+                caps = [DeferredRow(fut, 0, b) for b in range(N)]
+                cap_scores = [DeferredRow(fut, 1, b) for b in range(N)]
             else:
-                caps = [[tr.rtranslate(s) for s in vid] for vid in host_seq]
-            cap_scores = [list(row) for row in host_scores]
+                caps, cap_scores = _host_captions(None, cap_scores.double().cpu(), seq_ranked.cpu(), tr, N, Q)
         else:  # no caption decoded (every query finished at once)
             cap_scores = [[-1e5] * Q for _ in range(N)]
             caps = [[""] * Q for _ in range(N)]

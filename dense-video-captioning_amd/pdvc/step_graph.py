@@ -135,9 +135,9 @@ def dp_overlap_supported():
     """Whether an event recorded inside a stream capture (GraphEvent, hipEventRecordExternal) gates a stream outside
     the graph on this stack -- probed once, deterministically.  The probe graph first runs a kernel that holds its
     stream until the host sets a flag (pdvc_spin_until_flag: fine-grained pinned memory, bounded at 5 s), then writes
-    7 into a marker, records the event and writes 3.  After each replay is queued, a control stream that does NOT
-    wait copies the marker, and a side stream waits on the event and copies it.  While the flag is held the control
-    copy must finish and read 0 (the side streams do run beside a held replay) and the waiting copy must not have
+    7 into a marker, records the event and writes 3.  After each replay is queued, a side stream copies the marker
+    (the control, no wait), then waits on the event and copies it again.  While the flag is held the control copy
+    must finish and read 0 (the side stream does run beside a held replay) and the waited copy must not have
     finished; released, it must read 7 or 3.  A record that does not gate fails the second test every time, not by
     timing (the earlier probe's ungated control could read 3 when the replay happened to finish
     first).  PDVC_DP_OVERLAP=0 turns the overlap off."""
@@ -167,14 +167,17 @@ def dp_overlap_supported():
                 mark.fill_(3.0)
             if not recorded:
                 raise RuntimeError("the event record was refused inside the capture")
-            side, ctrl = torch.cuda.Stream(), torch.cuda.Stream()
+            side = torch.cuda.Stream()
             trials = []
             for _ in range(2):
                 flag.value = 0
                 mark.zero_()
                 torch.cuda.synchronize()
                 g.replay()
-                with torch.cuda.stream(ctrl):
+                # on ONE side stream: the control copy, then the wait, then the waited copy -- the control proves this
+                # stream runs beside the held replay (a stream that shares the replay's hardware queue would not, and
+                # would then hold the waited copy whether or not the event gates it)
+                with torch.cuda.stream(side):
                     seen_ctrl = mark.clone()
                     ctrl_done = torch.cuda.Event()
                     ctrl_done.record()
@@ -187,6 +190,10 @@ def dp_overlap_supported():
                 while not ctrl_done.query() and time.time() - t0 < 2.0:
                     time.sleep(0.001)
                 ctrl_ran = ctrl_done.query()
+                # a waited copy that the event does not hold runs right behind the control: give it 50 ms to show
+                t0 = time.time()
+                while not done.query() and time.time() - t0 < 0.05:
+                    time.sleep(0.001)
                 held = not done.query()
                 flag.value = 1
                 t0 = time.time()

@@ -608,6 +608,14 @@ int pdvc_gemm3p_relu_dropout_f32(int M, int N, int K, const float* A, long lda, 
  * gradient, its column sums, is the caller's). */
 int pdvc_gemm3p_dmask_f32(int M, int N, int K, const float* A, long lda, const uint16_t* planes, float* C, long ldc,
                           const float* hd, float p, void* stream);
+/* The residual sub-layer's sum before its LayerNorm, t = R + dropout(A opB^T + bias) (deformable_transformer.py:
+ * 150-156 / :253-271: norm(src + dropout(src2)), src2 = a Linear): the keep mask of
+ * pdvc_add_dropout_layernorm_forward_f32 for element (row, col) and the same device seed (p = 0: no dropout, seed_dev
+ * may be NULL); R has C's shape and ldc.  The add-norm pass then takes t as x with s = NULL, forward and backward:
+ * bit-identical to the unfused pair, one (rows x d) tensor fewer read each way. */
+int pdvc_gemm3p_resid_dropout_f32(int M, int N, int K, const float* A, long lda, const uint16_t* planes, float* C,
+                                  long ldc, const float* bias, const float* R, float p, const uint64_t* seed_dev,
+                                  void* stream);
 
 /* The bf16 mode's product (BASELINE configs[1]; pdvc/precision.py), the same call shape with one plane:
  * pdvc_round_plane_f32 writes plane[n][k] = bf16(opB[n][k]) (round to nearest even, torch's .to(bfloat16)) and

@@ -258,6 +258,74 @@ def test_ffn_relu_dropout_epilogue_is_bit_identical(monkeypatch):
     assert kept > 0
 
 
+@pytest.mark.parametrize("p_out", [0.0, 0.25])
+def test_ffn_residual_sum_epilogue_is_bit_identical(monkeypatch, p_out):
+    """x + dropout(linear2(h)) formed in linear2's gemm3 epilogue (pdvc_gemm3p_resid_dropout_f32) and the add-norm
+    pass on that sum alone (s = NULL) against linear2 followed by the two-input add-norm pass (RESID_EPILOGUE off):
+    the same mask bits and the same operations, so the block's output and every gradient are bit-identical;
+    ragged rows; dropout off and on."""
+    G = _on_gemm3(monkeypatch)
+    from pdvc.ops.functions.ffn import FFNBlockFunction
+    torch.manual_seed(5)
+    rows, d, f = 3000, 256, 512
+    x = torch.randn(rows, d, device=DEV)
+    lin1, lin2 = torch.nn.Linear(d, f).to(DEV), torch.nn.Linear(f, d).to(DEV)
+    norm = torch.nn.LayerNorm(d).to(DEV)
+    with torch.no_grad():
+        norm.weight.add_(0.1 * torch.randn_like(norm.weight))
+        norm.bias.add_(0.1 * torch.randn_like(norm.bias))
+    params = [lin1.weight, lin1.bias, lin2.weight, lin2.bias, norm.weight, norm.bias]
+    seeds = torch.tensor([1234567, 7654321], dtype=torch.int64, device=DEV)
+    g = torch.randn(rows, d, device=DEV)
+    res = []
+    for fuse in (True, False):
+        monkeypatch.setattr(G, "RESID_EPILOGUE", fuse)
+        calls = G.CALLS["gemm3"]
+        xa = x.clone().requires_grad_()
+        out = FFNBlockFunction.apply(xa, *params, 0.1, p_out, norm.eps, seeds)
+        res.append([out.detach()] + list(torch.autograd.grad(out, [xa] + params, g)))
+        assert G.CALLS["gemm3"] > calls
+    for i, (a, b) in enumerate(zip(*res)):
+        assert torch.equal(a, b), f"tensor {i} differs between the fused residual sum and the two-input pass"
+
+
+@pytest.mark.parametrize("p", [0.0, 0.2])
+def test_attn_block_residual_sum_epilogue_is_bit_identical(monkeypatch, p):
+    """The encoder self-attention node with src + dropout(output_proj(...)) formed in output_proj's gemm3 epilogue
+    against the two-input add-norm pass (dropout off and on): the layer output and every gradient that does not pass
+    through the MSDA value-gradient walk bit-identical; the rest within 1e-5 of their scale (the walk's counting sort
+    places a row's entries by LDS atomics, so its sums are not bitwise reproducible run to run either)."""
+    from parity import assert_close
+    G = _on_gemm3(monkeypatch)
+    from pdvc.deformable_transformer import DeformableTransformerEncoder, DeformableTransformerEncoderLayer
+    torch.manual_seed(9)
+    d, heads, level_T, N = 256, 8, (64, 32, 16, 8), 2
+    S = sum(level_T)
+    layer = DeformableTransformerEncoderLayer(d, 2 * d, p, "relu", 4, heads, 4).to(DEV).train()
+    src = torch.randn(N, S, d, device=DEV)
+    pos = torch.randn(N, S, d, device=DEV)
+    ref_pts = DeformableTransformerEncoder.get_reference_points(level_T, torch.ones(N, 4, device=DEV), DEV)
+    lsi = torch.tensor([0, 64, 96, 112], device=DEV)
+    g = torch.randn(N, S, d, device=DEV)
+    res = []
+    for fuse in (True, False):
+        monkeypatch.setattr(G, "RESID_EPILOGUE", fuse)
+        torch.manual_seed(77)  # the same dropout seeds drawn on the device for both runs
+        a, b = src.clone().requires_grad_(), pos.clone().requires_grad_()
+        layer.zero_grad(set_to_none=True)
+        out = layer(a, b, ref_pts, level_T, lsi, None)
+        out.backward(g)
+        res.append([("out", out.detach()), ("src", a.grad), ("pos", b.grad)] +
+                   [(n, q.grad.clone()) for n, q in layer.named_parameters()])
+    exact = ("out", "self_attn.output_proj.weight", "self_attn.output_proj.bias", "norm1.weight", "norm1.bias",
+             "linear1.weight", "linear1.bias", "linear2.weight", "linear2.bias", "norm2.weight", "norm2.bias")
+    for (n, x1), (_, x2) in zip(*res):
+        if n in exact:
+            assert torch.equal(x1, x2), f"{n} differs between the fused residual sum and the two-input pass"
+        else:
+            assert_close(x1, x2, f"{n} (fused residual sum vs two-input pass)", 1e-5)
+
+
 @pytest.mark.parametrize("accumulate", [None, False, True])
 def test_dgrad_split_k_few_tiles_deep_reduction(monkeypatch, accumulate):
     """mm_dgrad on a product with few output tiles and a deep reduction (the caption logit layer's input gradient:
