@@ -1031,3 +1031,4 @@ extern "C" int pdvc_gemm1p_f32(int M, int N, int K, const float* A, long lda, co
                                long ldc, const float* bias, int epilogue, void* stream) {
     return gemmp_impl<1>(M, N, K, A, lda, plane, C, ldc, bias, epilogue, stream);
 }
+

@@ -82,7 +82,7 @@ class Translator:
         w2i = self.vocab["word_to_ix"]
         return np.array([0] + [w2i[w] for w in words][:max_len - 2] + [0])
 
-    def rtranslate_batch(self, seqs):
+    def rtranslate_batch(self, seqs, yield_every=0):
         """rtranslate of every row of an int array (R, L), in one native pass (pdvc_detokenize: the first-zero
         cut, the word lookup and the joins in C, one byte buffer for all rows)."""
         from pdvc import _native
@@ -102,7 +102,7 @@ class Translator:
             off[1:] = np.cumsum([len(e) for e in enc])
             tab = (np.frombuffer(b"".join(enc), dtype=np.uint8).copy(), off, n)
             self._word_table = tab
-        return _native.detokenize(seqs.astype(np.int64, copy=False), tab[0], tab[1])
+        return _native.detokenize(seqs.astype(np.int64, copy=False), tab[0], tab[1], yield_every)
 
     def rtranslate(self, sent_ids):
         """Ids up to the first 0 -> 'w1 w2 ... wn.' ('' when the caption is empty)."""

@@ -129,6 +129,7 @@ class rewriting_graphs:
 
 
 _DP_OVERLAP = []
+_DP_TRIALS = []
 
 
 def dp_overlap_supported():
@@ -204,6 +205,7 @@ def dp_overlap_supported():
                 torch.cuda.synchronize()
                 trials.append((ctrl_ran, held, float(seen_ctrl), float(seen)))
             ok = all(c and h and vc == 0.0 and v in (7.0, 3.0) for c, h, vc, v in trials)
+            _DP_TRIALS[:] = trials  # (tests/test_gpu_dp_probe.py reads what the probe saw)
             if os.environ.get("PDVC_DP_OVERLAP_DEBUG"):
                 print("dp_overlap_supported: (control ran, waiting copy held, control read, waiting read)", trials)
             del g

@@ -8,8 +8,9 @@ import sys
 
 
 def main():
-    path = sys.argv[1]
-    cut = sys.argv[2] if len(sys.argv) > 2 else "lsap_kernel"
+    path = [a for a in sys.argv[1:] if not a.startswith("--")][0]
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    cut = args[1] if len(args) > 1 else "lsap_kernel"
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     wins, cur = [], []
     for r in rows:
@@ -33,6 +34,14 @@ def main():
                 gap, at = g, j
             end = max(end, int(w[j]["End_Timestamp"]))
         over1 += n1
+        if "--all" in sys.argv:
+            end = int(w[0]["End_Timestamp"])
+            for j in range(1, len(w)):
+                g = int(w[j]["Start_Timestamp"]) - end
+                if g > 1_000_000:
+                    print(f"      gap {g / 1e6:7.2f} ms after launch {j - 1}: "
+                          f"{w[j - 1]['Kernel_Name'].split('(')[0][:60]} -> {w[j]['Kernel_Name'].split('(')[0][:60]}")
+                end = max(end, int(w[j]["End_Timestamp"]))
         name = lambda r: r["Kernel_Name"].split("(")[0].replace("void ", "")[:70]  # noqa: E731
         print(f"window {i:2d}: span {(e1 - s0) / 1e6:8.2f} ms  kernels {busy / 1e6:8.2f} ms  launches {len(w):5d}  "
               f"largest gap {gap / 1e6:7.2f} ms after launch {at - 1} ({name(w[at - 1]) if at else '-'} -> "
