@@ -548,7 +548,8 @@ class LSTMDSACaptioner(Captioner):
             rd1 = vid_num * query_num
         ref = ref[:, :, :L].reshape(vid_num * query_num, L, 2)
         row_video = torch.arange(vid_num, device=hs.device, dtype=torch.int32).repeat_interleave(query_num)
-        T = tuple(int(x) for x in others.get("level_T", others["spatial_shapes"].tolist()))[:L]
+        lt = others.get("level_T")  # (a .get default would read the device tensor back even when level_T is given)
+        T = tuple(int(x) for x in (lt if lt is not None else others["spatial_shapes"].tolist()))[:L]
         return hs.reshape(vid_num * query_num, -1), ref, rd1, row_video, T
 
     def forward(self, hs, reference, others, cap_tensor):

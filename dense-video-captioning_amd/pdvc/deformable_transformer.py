@@ -107,6 +107,7 @@ class DeformableTransformer(nn.Module):
             lvl_pos = torch.cat(lvl_pos, 1)
         temporal_shapes = hostio.const(("level_T", tuple(level_T)), lambda: torch.tensor(level_T, dtype=torch.long),
                                        src_flatten.device)
+        temporal_shapes.__dict__["_pdvc_level_T"] = tuple(level_T)  # _level_T reads it: no device read-back
         level_start_index = torch.cat((temporal_shapes.new_zeros((1,)), temporal_shapes.cumsum(0)[:-1]))
         valid_ratios = torch.stack([self.get_valid_ratio(m) for m in masks], 1)
         self.last_level_T = tuple(level_T)
@@ -141,6 +142,9 @@ class DeformableTransformer(nn.Module):
 
 def _level_T(temporal_shapes):
     if isinstance(temporal_shapes, torch.Tensor):
+        known = temporal_shapes.__dict__.get("_pdvc_level_T")  # the host tuple it was built from (no read-back)
+        if known is not None:
+            return known
         return tuple(int(x) for x in temporal_shapes.tolist())
     return tuple(int(x) for x in temporal_shapes)
 

@@ -29,6 +29,9 @@ def level_lengths(input_spatial_shapes):
     """Temporal length of every level as a tuple of ints.  The model passes tuples (no host sync);
     a tensor (the reference's calling convention) is read back once."""
     if isinstance(input_spatial_shapes, torch.Tensor):
+        known = input_spatial_shapes.__dict__.get("_pdvc_level_T")  # the model's level table: its host tuple
+        if known is not None and input_spatial_shapes.dim() == 1:
+            return tuple(known)
         v = input_spatial_shapes.detach().reshape(-1).tolist()
         return tuple(int(x) for x in v)
     return tuple(int(x) for x in input_spatial_shapes)
