@@ -442,6 +442,9 @@ def eval_main(a):
         steps_seen.append(out["seq"].shape[-1] if len(out["seq"]) else 0)
         return res
 
+    # PostProcess's host half runs on a worker thread (pdvc.py DeferredRow) while this thread queues the next batch;
+    # a short GIL switch interval keeps the queueing thread from waiting a whole default interval (5 ms) for it
+    sys.setswitchinterval(float(os.environ.get("PDVC_EVAL_SWITCH_INTERVAL", "0.0005")))
     log(f"eval: {B} videos, warm-up")
     for _ in range(a.warmup):
         step()
