@@ -9,6 +9,7 @@ videos are decoded in one recurrence, and all Hungarian matchings share one devi
 import copy
 import math
 import os
+import threading
 import time
 
 import torch
@@ -207,6 +208,7 @@ class PDVC(nn.Module):
         # changes nothing, so the kernels get none and skip its per-corner byte loads
         kmask = None if self.__dict__.get("_no_padding", False) else mask_flatten
         memory = tr.forward_encoder(src_flatten, level_T, lsi, valid_ratios, lvl_pos, kmask)
+        _HOST_GATE.set()  # the encoder's GEMMs queued: a deferred PostProcess host half may take the GIL now
         self._project_memory(memory)
         two_stage = proposals is not None
         if two_stage:
@@ -536,6 +538,12 @@ class PDVC(nn.Module):
 
 _POOL = []
 _PENDING = []
+# A deferred PostProcess host half (Python work, the GIL) waits behind this gate until the next batch's forward has
+# queued its encoder (trunk), so that it does not compete with the launches of a step whose device queue is still
+# empty; drain() and a DeferredRow read open it, and a 0.25 s timeout bounds the wait when no forward follows.
+_HOST_GATE = threading.Event()
+_HOST_GATE.set()
+_GATED = os.environ.get("PDVC_POST_GATE", "1") != "0"
 
 
 def _host_pool():
@@ -550,6 +558,7 @@ def _host_captions(ev, host_scores, host_seq, tr, N, Q):
     172-180) and the caption scores as per-video lists.  ev: the event behind the device -> pinned copies."""
     if ev is not None:
         ev.synchronize()
+        _HOST_GATE.wait(0.25)
     host_seq = host_seq.numpy().astype("int")
     if hasattr(tr, "rtranslate_batch"):  # data.video_dataset.Translator: one vectorised pass
         flat = tr.rtranslate_batch(host_seq.reshape(N * Q, -1), yield_every=2048 if ev is not None else 0)
@@ -569,6 +578,8 @@ class DeferredRow:
         self._fut, self._part, self._b = fut, part, b
 
     def value(self):
+        if not self._fut.done():
+            _HOST_GATE.set()
         return self._fut.result()[self._part][self._b]
 
     def __len__(self):
@@ -613,6 +624,7 @@ class PostProcess(nn.Module):
     @staticmethod
     def drain():
         """Wait for every deferred host half (captions, caption scores) queued so far; re-raise its error."""
+        _HOST_GATE.set()
         while _PENDING:
             _PENDING.pop(0).result()
 
@@ -642,6 +654,8 @@ class PostProcess(nn.Module):
                 hq.copy_(seq_ranked, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record()
+                if _GATED:
+                    _HOST_GATE.clear()
                 fut = _host_pool().submit(_host_captions, ev, hs, hq, tr, N, Q)
                 _PENDING.append(fut)
                 caps = [DeferredRow(fut, 0, b) for b in range(N)]
