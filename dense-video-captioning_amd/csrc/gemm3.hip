@@ -736,10 +736,14 @@ struct Regs {  // one stage of both operands: float4 u = t + 512 i (i = 0, 1) is
 };
 }  // namespace w3
 
-template <int EPI>
+// CS: also the column sums of A over this split's reduction rows (the bias gradient sum_k dy[k][m] of the layer whose
+// weight gradient this is), taken from the float4s each thread loads anyway: colpart[z * M + m] for split z, written by
+// the tiles of column block 0 (deterministic: fixed per-thread order, then the 8 waves summed in order through LDS)
+template <int EPI, bool CS = false>
 __global__ __launch_bounds__(NT, 1) void gemm3w_kernel(int M, int N, int K, const float* __restrict__ A, long lda,
                                                        const float* __restrict__ B, long ldb, float* __restrict__ C,
-                                                       long ldc, int k_per_split, int tiles_n, long slab, int nsplit) {
+                                                       long ldc, int k_per_split, int tiles_n, long slab, int nsplit,
+                                                       float* __restrict__ colpart) {
     using namespace w3;
     __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -765,8 +769,19 @@ __global__ __launch_bounds__(NT, 1) void gemm3w_kernel(int M, int N, int K, cons
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     Regs rg;
+    float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);  // CS: this thread's A column chunk summed over its rows
+    auto cadd = [&](int i) {
+        if constexpr (CS) {
+            csum.x += rg.a[i].x;
+            csum.y += rg.a[i].y;
+            csum.z += rg.a[i].z;
+            csum.w += rg.a[i].w;
+        }
+    };
     if (nst > 0) {
         rg.load(A, lda, m0, M, B, ldb, n0, N, kb);
+        cadd(0);
+        cadd(1);
 #pragma unroll
         for (int q = 0; q < 4; ++q) rg.store(q, lds);
         if (nst > 1) rg.load(A, lda, m0, M, B, ldb, n0, N, kb + KS);
@@ -790,8 +805,10 @@ __global__ __launch_bounds__(NT, 1) void gemm3w_kernel(int M, int N, int K, cons
         for (int q = 0; q < 8; ++q) {
             const int i = q >> 1, j = q & 1;
             acc[i][j] = mfma6(fa[i], fb[j], acc[i][j]);
-            if constexpr (more)
+            if constexpr (more) {
                 if (q >= 1 && q <= 4) rg.store(q - 1, nxt);  // stage s + 1 into the other buffer
+                if (q == 1 || q == 2) cadd(q - 1);
+            }
             if constexpr (more2)
                 if (q == 5) rg.load(A, lda, m0, M, B, ldb, n0, N, kb + (s + 2) * KS);
         }
@@ -804,6 +821,26 @@ __global__ __launch_bounds__(NT, 1) void gemm3w_kernel(int M, int N, int K, cons
     if (s + 1 < nst) stage(s++, T_{}, F_{});
     if (s < nst) stage(s, F_{}, F_{});
     (void)l32;
+    if constexpr (CS) {
+        if (tn == 0) {  // (block-uniform) LDS is free: the last stage ended with a barrier
+            float4* red = reinterpret_cast<float4*>(lds);
+            red[threadIdx.x] = csum;  // [wave][column chunk]: the chunk is threadIdx.x % 64 in every stage
+            __syncthreads();
+            if (threadIdx.x < 64) {
+                float4 t = red[threadIdx.x];
+#pragma unroll
+                for (int w = 1; w < NT / 64; ++w) {
+                    const float4 v = red[w * 64 + threadIdx.x];
+                    t.x += v.x;
+                    t.y += v.y;
+                    t.z += v.z;
+                    t.w += v.w;
+                }
+                const int m = m0 + 4 * threadIdx.x;
+                if (m < M) *reinterpret_cast<float4*>(colpart + (long)zz * M + m) = t;  // (the clamped loads beyond M dropped)
+            }
+        }
+    }
     float* Cz = C + (EPI == EPI_SLAB ? (long)zz * slab : 0);
     const bool full = m0 + BM <= M && n0 + BN <= N;
     if (full) store_tile<EPI, true, 4, 2>(acc, Cz, ldc, nullptr, m0 + wm, n0 + wn, M, N, l32, 4 * h);
@@ -852,6 +889,48 @@ void launch_epi(int epi, dim3 grid, hipStream_t s, int M, int N, int K, const fl
 
 }  // namespace
 
+namespace {
+
+// gemm3w over the reduction split into ceil(K / kpw) slabs (summed by slab_sum_kernel), optionally with the column
+// sums of A (db[m] = sum_k A[k][m]; per-slab partials in db_ws when there is more than one slab)
+int wgrad_launch(int M, int N, int K, const float* A, long lda, const float* B, long ldb, float* C, long ldc,
+                 int epilogue, int splits, float* workspace, float* db, float* db_ws, hipStream_t s) {
+    const long wm_ = (M + w3::BM - 1) / w3::BM, wn_ = (N + w3::BN - 1) / w3::BN;
+    int kpw = (K + splits - 1) / splits;
+    kpw = (kpw + w3::KS - 1) / w3::KS * w3::KS;
+    const int nzw = K == 0 ? 1 : (K + kpw - 1) / kpw;
+    PDVC_CHECK_ARG(wm_ * wn_ * nzw < (1L << 31), "too many tiles");
+    const dim3 gw((unsigned)(wm_ * wn_ * nzw));
+    float* dw = nzw > 1 ? workspace : C;
+    const long ldw = nzw > 1 ? N : ldc;
+    const long slab_n = (long)M * N;
+    float* cp = nzw > 1 ? db_ws : db;
+    if (db != nullptr) {
+        if (nzw > 1) hipLaunchKernelGGL((gemm3w_kernel<EPI_SLAB, true>), gw, dim3(NT), 0, s, M, N, K, A, lda, B, ldb, dw, ldw, kpw, (int)wn_, slab_n, nzw, cp);
+        else hipLaunchKernelGGL((gemm3w_kernel<EPI_STORE, true>), gw, dim3(NT), 0, s, M, N, K, A, lda, B, ldb, dw, ldw, kpw, (int)wn_, slab_n, nzw, cp);
+    } else {
+        if (nzw > 1) hipLaunchKernelGGL(gemm3w_kernel<EPI_SLAB>, gw, dim3(NT), 0, s, M, N, K, A, lda, B, ldb, dw, ldw, kpw, (int)wn_, slab_n, nzw, nullptr);
+        else hipLaunchKernelGGL(gemm3w_kernel<EPI_STORE>, gw, dim3(NT), 0, s, M, N, K, A, lda, B, ldb, dw, ldw, kpw, (int)wn_, slab_n, nzw, nullptr);
+    }
+    PDVC_CHECK_LAUNCH("gemm3w_kernel");
+    if (nzw > 1) {
+        const long n4 = slab_n / 4;
+        const int blocks = (int)std::min<long>((n4 + 255) / 256, 2048);
+        if (epilogue == 3) hipLaunchKernelGGL(slab_sum_kernel<true>, dim3(blocks), dim3(256), 0, s, workspace, nzw, n4, C);
+        else hipLaunchKernelGGL(slab_sum_kernel<false>, dim3(blocks), dim3(256), 0, s, workspace, nzw, n4, C);
+        PDVC_CHECK_LAUNCH("slab_sum_kernel");
+        if (db != nullptr) {
+            const long m4 = M / 4;
+            const int bl = (int)std::min<long>((m4 + 255) / 256, 2048);
+            hipLaunchKernelGGL(slab_sum_kernel<false>, dim3(bl), dim3(256), 0, s, db_ws, nzw, m4, db);
+            PDVC_CHECK_LAUNCH("slab_sum_kernel");
+        }
+    }
+    return PDVC_OK;
+}
+
+}  // namespace
+
 // C-ABI: see include/pdvc_msda.h ("fp32 GEMM on the bf16 matrix cores")
 extern "C" int pdvc_gemm3_f32(int M, int N, int K, const float* A, long lda, int a_kc, const float* B, long ldb,
                               int b_kc, float* C, long ldc, const float* bias, int epilogue, int splits,
@@ -886,27 +965,8 @@ extern "C" int pdvc_gemm3_f32(int M, int N, int K, const float* A, long lda, int
     const long ld = slab ? N : ldc;
     const int epi = slab ? (int)EPI_SLAB : epilogue;
     const long slab_n = (long)M * N;
-    if (!a_kc && !b_kc && (epi == EPI_STORE || epi == EPI_SLAB)) {  // the weight-gradient form: gemm3w's tile
-        const long wm_ = (M + w3::BM - 1) / w3::BM, wn_ = (N + w3::BN - 1) / w3::BN;
-        int kpw = (K + splits - 1) / splits;
-        kpw = (kpw + w3::KS - 1) / w3::KS * w3::KS;
-        const int nzw = K == 0 ? 1 : (K + kpw - 1) / kpw;
-        PDVC_CHECK_ARG(wm_ * wn_ * nzw < (1L << 31), "too many tiles");
-        const dim3 gw((unsigned)(wm_ * wn_ * nzw));
-        float* dw = nzw > 1 ? workspace : C;
-        const long ldw = nzw > 1 ? N : ldc;
-        if (nzw > 1) hipLaunchKernelGGL(gemm3w_kernel<EPI_SLAB>, gw, dim3(NT), 0, s, M, N, K, A, lda, B, ldb, dw, ldw, kpw, (int)wn_, slab_n, nzw);
-        else hipLaunchKernelGGL(gemm3w_kernel<EPI_STORE>, gw, dim3(NT), 0, s, M, N, K, A, lda, B, ldb, dw, ldw, kpw, (int)wn_, slab_n, nzw);
-        PDVC_CHECK_LAUNCH("gemm3w_kernel");
-        if (nzw > 1) {
-            const long n4 = slab_n / 4;
-            const int blocks = (int)std::min<long>((n4 + 255) / 256, 2048);
-            if (epilogue == 3) hipLaunchKernelGGL(slab_sum_kernel<true>, dim3(blocks), dim3(256), 0, s, workspace, nzw, n4, C);
-            else hipLaunchKernelGGL(slab_sum_kernel<false>, dim3(blocks), dim3(256), 0, s, workspace, nzw, n4, C);
-            PDVC_CHECK_LAUNCH("slab_sum_kernel");
-        }
-        return PDVC_OK;
-    }
+    if (!a_kc && !b_kc && (epi == EPI_STORE || epi == EPI_SLAB))  // the weight-gradient form: gemm3w's tile
+        return wgrad_launch(M, N, K, A, lda, B, ldb, C, ldc, epilogue, splits, workspace, nullptr, nullptr, s);
     if (a_kc && b_kc) launch_epi<BM, BN, true, true>(epi, grid, s, M, N, K, A, lda, B, ldb, dst, ld, bias, kps, (int)tiles_n, slab_n);
     else if (a_kc) launch_epi<BM, BN, true, false>(epi, grid, s, M, N, K, A, lda, B, ldb, dst, ld, bias, kps, (int)tiles_n, slab_n);
     else if (b_kc) launch_epi<BM, BN, false, true>(epi, grid, s, M, N, K, A, lda, B, ldb, dst, ld, bias, kps, (int)tiles_n, slab_n);
@@ -920,6 +980,26 @@ extern "C" int pdvc_gemm3_f32(int M, int N, int K, const float* A, long lda, int
         PDVC_CHECK_LAUNCH("slab_sum_kernel");
     }
     return PDVC_OK;
+}
+
+// C-ABI: see include/pdvc_msda.h -- the weight gradient C = A^T B of pdvc_gemm3_f32 (a_kc = b_kc = 0, epilogue 0) and
+// the bias gradient db = the column sums of A, from one pass over A
+extern "C" int pdvc_gemm3_wgrad_bias_f32(int M, int N, int K, const float* A, long lda, const float* B, long ldb,
+                                         float* C, long ldc, int epilogue, int splits, float* workspace, float* db,
+                                         float* db_ws, void* stream) {
+    PDVC_CHECK_ARG(M >= 4 && N >= 4 && K >= 0 && M % 4 == 0 && N % 4 == 0, "M, N: multiples of 4, at least 4");
+    PDVC_CHECK_ARG(epilogue == 0, "epilogue must be 0 (store)");
+    PDVC_CHECK_ARG(splits >= 1 && splits <= 65535, "splits out of range");
+    PDVC_CHECK_ARG(lda >= M && ldb >= N && ldc >= N, "leading dimensions too small");
+    PDVC_CHECK_ARG((uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0,
+                   "operands must be 16-byte aligned with leading dimensions divisible by 4");
+    PDVC_CHECK_ARG(K % BK == 0, "K must be a multiple of 32");
+    PDVC_CHECK_ARG(db != nullptr && (uintptr_t)db % 16 == 0, "db: a 16-byte aligned (M,) destination");
+    PDVC_CHECK_ARG(splits == 1 || (workspace != nullptr && db_ws != nullptr && (uintptr_t)db_ws % 16 == 0 &&
+                                   ldc == N && (uintptr_t)C % 16 == 0),
+                   "splits > 1: a workspace of splits * M * N floats, a 16-byte aligned db_ws of splits * M floats "
+                   "and a dense, 16-byte aligned C");
+    return wgrad_launch(M, N, K, A, lda, B, ldb, C, ldc, epilogue, splits, workspace, db, db_ws, (hipStream_t)stream);
 }
 
 namespace {

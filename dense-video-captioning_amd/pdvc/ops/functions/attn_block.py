@@ -19,7 +19,7 @@ from torch.autograd.function import once_differentiable
 from pdvc import _native as _n
 from .addnorm import BWD_PARTS, an_backward, an_forward
 from .gemm3 import addmm_nt, addmm_resid_dropout_nt, mm_dgrad
-from .linear import colsum, wgrad_mm
+from .linear import wgrad_mm
 from .ms_deform_attn_func import NUM_SAMPLES, msda1d_backward, msda1d_forward
 from .posembed import LevelPos, level_row_sums
 
@@ -88,10 +88,14 @@ class EncoderAttnBlockFunction(Function):
         gv2 = gv.view(R, d)
         gp2 = gp.view(R, -1)
         # the value bias gradient from the value-gradient kernel's per-(video, level) row sums
-        dbv = vsums.view(-1, d).sum(0) if vsums is not None else colsum(gv2)
-        dWv = wgrad_mm(gv2, src2)
-        dbq = colsum(gp2)
-        dWq = wgrad_mm(gp2, q)
+        if vsums is not None:
+            dbv = vsums.view(-1, d).sum(0)
+            dWv = wgrad_mm(gv2, src2)
+        else:
+            dbv = gv2.new_empty(d)
+            dWv = wgrad_mm(gv2, src2, db=dbv)
+        dbq = gp2.new_empty(gp2.shape[1])  # the sampling / attention-weight bias gradient, from dWq's pass over gp2
+        dWq = wgrad_mm(gp2, q, db=dbq)
         d_pos = d_handle = None
         if has_handle:
             d_handle = torch.matmul(level_row_sums(gp.view(N, S, -1), level_T), Wq)

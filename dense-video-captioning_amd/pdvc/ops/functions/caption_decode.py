@@ -344,8 +344,8 @@ class CaptionDecodeFunction(Function):
                 lsums = None  # (the consumer falls back to a column sum)
         else:
             dA2 = dATT.view(-1, A)
-            dW_ctx = wgrad_mm(dA2, CLIP.view(-1, D))
-            db_ctx = colsum(dA2)
+            db_ctx = dA2.new_empty(A)
+            dW_ctx = wgrad_mm(dA2, CLIP.view(-1, D), db=db_ctx)
         dalpha_w = colsum(GAW.view(-1, A))
         dalpha_b = GAB.sum().reshape(1)
         dW_att = wgrad_mm(d_gates.reshape(-1, G), RES.view(-1, M * D))

@@ -58,10 +58,11 @@ class ConvS2RowsFunction(Function):
             mm_dgrad(dz2, w0, out=dX2[:, C:])
             gx = dX2.view(N, T, C)[:, :Tin]
         if ctx.needs_input_grad[1]:
-            g12 = wgrad_mm(dy2, X2)
+            gb = dy2.new_empty(dy2.shape[1]) if ctx.needs_input_grad[2] else None
+            g12 = wgrad_mm(dy2, X2, db=gb)  # (the bias gradient from the same pass over dy)
             g0 = wgrad_mm(dz2, X2[:, C:])
             gw = torch.stack([g0, g12[:, :C], g12[:, C:]], 2)
-        if ctx.needs_input_grad[2]:
+        elif ctx.needs_input_grad[2]:
             gb = colsum(dy2)
         return gx, gw, gb
 

@@ -28,7 +28,7 @@ from pdvc.precision import attach_bf16, bf16_active, shadow_for
 from .addnorm import BWD_PARTS, an_backward, an_forward
 from . import linear as _lin
 from .gemm3 import addmm_nt, addmm_relu_dropout_nt, addmm_resid_dropout_nt, mm_dgrad, mm_dgrad_dmask
-from .linear import CU, colsum, wgrad_mm
+from .linear import CU, wgrad_mm
 
 
 # False (or PDVC_FFN_FUSE=0): linear1, then the relu-dropout pass (the A/B and the bit-identity test)
@@ -110,8 +110,7 @@ class FFNBlockFunction(Function):
         if FUSE_RELU_DROPOUT and not bf16_active():  # relu -> dropout backward in the dgrad epilogue
             dh = mm_dgrad_dmask(dy, w2, h, p_act)
         if dh is not None:
-            colsum(dh, out=db1)  # linear1's bias gradient
-            dw1 = wgrad_mm(dh, x2)
+            dw1 = wgrad_mm(dh, x2, db=db1)  # with linear1's bias gradient from the same pass over dh
             mm_dgrad(dh, w1, out=dx)
             return dx.view(shape), dw1, db1, dw2, db2, dgamma, dbeta, None, None, None, None
         dh = mm_dgrad(dy, w2)

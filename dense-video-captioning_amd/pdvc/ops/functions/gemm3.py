@@ -244,21 +244,43 @@ WGRAD_MIN_CHUNK = int(os.environ.get("PDVC_WGRAD_MIN_CHUNK", "1024"))
 WGRAD_MODEL = os.environ.get("PDVC_WGRAD_MODEL", "1") != "0"
 
 
-def mm_wgrad(gy, x, out=None):
+# the bias gradient (column sums of gy) taken by the weight-gradient GEMM from the rows it loads (A/B switch)
+WGRAD_BIAS = os.environ.get("PDVC_WGRAD_BIAS", "1") != "0"
+
+
+def wgrad_bias_ok(gy, x, db):
+    """Whether mm_wgrad can take gy.sum(0) into db in the same pass (pdvc_gemm3_wgrad_bias_f32's layout rules)."""
+    return (WGRAD_BIAS and db.is_cuda and db.dtype == torch.float32 and db.is_contiguous()
+            and db.shape == (gy.shape[1],) and db.data_ptr() % 16 == 0 and gy.stride(1) == 1 and x.stride(1) == 1
+            and gy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0 and gy.stride(0) % 4 == 0
+            and x.stride(0) % 4 == 0 and gy.shape[1] >= 4 and x.shape[1] >= 4)
+
+
+def mm_wgrad(gy, x, out=None, db=None):
     """gy^T x for gy (rows, O) and x (rows, I): the weight gradient of y = x W^T, deterministic (row chunks summed
-    in a fixed order).  out: a contiguous (O, I) destination (written, not accumulated)."""
+    in a fixed order).  out: a contiguous (O, I) destination (written, not accumulated).  db: a contiguous (O,)
+    destination for gy.sum(0) (the bias gradient, wgrad_bias_ok), computed by the same kernel from the gy rows it
+    loads (pdvc_gemm3_wgrad_bias_f32).  None (nothing written) when the shapes leave gemm3w."""
     rows, O = gy.shape
     I = x.shape[1]
     ok = _use(rows, 32, gy, x, extra=(O % 4 == 0 and I % 4 == 0 and rows % 32 == 0
                                       and (out is None or (out.is_contiguous() and out.shape == (O, I)))))
     if not ok:
         return None
+    if db is not None and not wgrad_bias_ok(gy, x, db):
+        raise ValueError("mm_wgrad: db needs wgrad_bias_ok(gy, x, db)")
     if out is None:
         out = torch.empty((O, I), dtype=torch.float32, device=gy.device)
     tiles = ((O + 255) // 256) * ((I + 255) // 256)  # gemm3w tiles
     splits = wgrad_splits(rows, tiles, O, I)
     FLOPS[0] += 2 * rows * O * I
     ws = torch.empty(splits * O * I if splits > 1 else 0, dtype=torch.float32, device=gy.device)
-    _n.call("pdvc_gemm3_f32", O, I, rows, _n.ptr_any(gy), gy.stride(0), 0, _n.ptr_any(x), x.stride(0), 0,
-            _n.ptr_any(out), I, None, 0, splits, _n.ptr(ws) if splits > 1 else None, _n.stream())
+    if db is None:
+        _n.call("pdvc_gemm3_f32", O, I, rows, _n.ptr_any(gy), gy.stride(0), 0, _n.ptr_any(x), x.stride(0), 0,
+                _n.ptr_any(out), I, None, 0, splits, _n.ptr(ws) if splits > 1 else None, _n.stream())
+        return out
+    dws = torch.empty(splits * O if splits > 1 else 0, dtype=torch.float32, device=gy.device)
+    _n.call("pdvc_gemm3_wgrad_bias_f32", O, I, rows, _n.ptr_any(gy), gy.stride(0), _n.ptr_any(x), x.stride(0),
+            _n.ptr_any(out), I, 0, splits, _n.ptr(ws) if splits > 1 else None, _n.ptr(db),
+            _n.ptr(dws) if splits > 1 else None, _n.stream())
     return out

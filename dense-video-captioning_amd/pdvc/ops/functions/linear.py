@@ -147,17 +147,26 @@ def add_row_bias(x, bias):
     return AddRowBias.apply(x, bias)
 
 
-def wgrad_mm(gy, x, out=None):
+def wgrad_mm(gy, x, out=None, db=None):
     """gy^T x for row-major gy (rows, O) and x (rows, I): the weight-gradient product, split over K.  out: a
-    contiguous (O, I) destination (a row block of a packed weight's gradient)."""
+    contiguous (O, I) destination (a row block of a packed weight's gradient).  db: an (O,) destination for the
+    bias gradient gy.sum(0) -- taken by gemm3w from the gy rows it loads when the layout allows (wgrad_bias_ok),
+    else a colsum pass."""
     rows = gy.shape[0]
     if gy.shape[1] == 1:  # a 1-wide layer: a weighted column sum, not an (M = 1) GEMM (~1 TB/s on hipBLASLt)
         r = colsum((x * gy).contiguous()).view(1, -1)
+        if db is not None:
+            colsum(gy, out=db)
         return r if out is None else out.copy_(r)
-    from .gemm3 import mm_wgrad
-    r = mm_wgrad(gy, x, out)  # fp32 on the bf16 matrix cores when the shape allows it
+    from .gemm3 import mm_wgrad, wgrad_bias_ok
+    fuse = db is not None and wgrad_bias_ok(gy, x, db)
+    r = mm_wgrad(gy, x, out, db if fuse else None)  # fp32 on the bf16 matrix cores when the shape allows it
     if r is not None:
+        if db is not None and not fuse:
+            colsum(gy, out=db)
         return r
+    if db is not None:
+        colsum(gy, out=db)
     s = wgrad_splits(rows)
     if s == 1:
         return torch.mm(gy.t(), x) if out is None else torch.mm(gy.t(), x, out=out)
@@ -201,8 +210,7 @@ class PackedLinearFunction(Function):
             g2 = g.reshape(-1, r).contiguous()
             w = weight[r0:r0 + r]
             gxs.append(mm_dgrad(g2, w).view(shp) if ctx.needs_input_grad[3 + len(gxs)] else None)
-            wgrad_mm(g2, x2, out=gw[r0:r0 + r])
-            colsum(g2, out=gb[r0:r0 + r])
+            wgrad_mm(g2, x2, out=gw[r0:r0 + r], db=gb[r0:r0 + r])
             r0 += r
         return (gw, gb, None) + tuple(gxs)
 
@@ -237,9 +245,11 @@ class TorchLinearFunction(Function):
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             gx = mm_dgrad(gy2, weight).view(*gy.shape[:-1], weight.shape[1])
+        want_gb = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
-            gw = wgrad_mm(gy2, x2)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = gy2.new_empty(O) if want_gb else None
+            gw = wgrad_mm(gy2, x2, db=gb)  # (the bias gradient from the same pass over gy)
+        elif want_gb:
             gb = colsum(gy2.contiguous())
         return gx, gw, gb, None
 
@@ -292,8 +302,11 @@ class MultiLinearFunction(Function):
             # (MSDA1dFunction): the bias gradient from those instead of another pass over g
             ls = level_sums_of(g)
             LEVEL_SUM_USES[0] += ls is not None
-            gb = ls.view(-1, ls.shape[-1]).sum(0) if ls is not None and ls.shape[-1] == w.shape[0] else colsum(g2)
-            gwb += [wgrad_mm(g2, x2), gb]
+            if ls is not None and ls.shape[-1] == w.shape[0]:
+                gwb += [wgrad_mm(g2, x2), ls.view(-1, ls.shape[-1]).sum(0)]
+            else:
+                gb = g2.new_empty(w.shape[0])
+                gwb += [wgrad_mm(g2, x2, db=gb), gb]
         if gx is None:
             gx = torch.zeros_like(x2)
         return (gx.view(ctx.shape), *gwb)

@@ -115,11 +115,15 @@ class LogitPickFunction(Function):
             Wp = weight.new_zeros(Vp, weight.shape[1])
             Wp[:V] = weight
             gx = mm_dgrad(G, Wp).view(*ctx.lead, weight.shape[1])
+        want_gb = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
             # on the padded (rows, Vp) buffer (zeros past V): its width qualifies for gemm3w, where the strided
-            # (rows, V) view made wgrad_mm fall back to a reshaped copy and a library GEMM
-            gw = wgrad_mm(G, x2)[:V]
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+            # (rows, V) view made wgrad_mm fall back to a reshaped copy and a library GEMM; the
+            # bias gradient from the same pass over G
+            gbp = G.new_empty(G.shape[1]) if want_gb else None
+            gw = wgrad_mm(G, x2, db=gbp)[:V]
+            gb = gbp[:V] if want_gb else None
+        elif want_gb:
             gb = colsum(G)[:V]
         return gx, gw, gb, None
 

@@ -590,6 +590,15 @@ int pdvc_gemm_f32(int M, int N, int K, const float* A, int lda, int trans_a, con
 int pdvc_gemm3_f32(int M, int N, int K, const float* A, long lda, int a_kc, const float* B, long ldb, int b_kc,
                    float* C, long ldc, const float* bias, int epilogue, int splits, float* workspace, void* stream);
 
+/* The weight gradient and the bias gradient of one nn.Linear from one pass over dy (the reference's autograd
+ * backward of nn.Linear: grad_weight = dy^T x, grad_bias = dy.sum(0)): pdvc_gemm3_f32 with a_kc = b_kc = 0 and
+ * epilogue 0 (C[M,N] = sum_k A[k*lda + m] B[k*ldb + n]), plus db[m] = sum_k A[k*lda + m], taken from the A rows the
+ * GEMM loads (deterministic order).  M, N multiples of 4; db 16-byte aligned; splits > 1: workspace of
+ * splits * M * N floats, db_ws of splits * M floats (16-byte aligned) and a dense C (ldc == N). */
+int pdvc_gemm3_wgrad_bias_f32(int M, int N, int K, const float* A, long lda, const float* B, long ldb, float* C,
+                              long ldc, int epilogue, int splits, float* workspace, float* db, float* db_ws,
+                              void* stream);
+
 /* The weight operand split once per call: planes[p][n][k] (bf16 bits, p = 0..2) of opB[n][k] (b_kc 1: B[n*ldb + k],
  * 0: B[k*ldb + n]); K a multiple of 32.  pdvc_gemm3p_f32 then computes C[M,N] (=|+=) sum_k A[m*lda + k] opB[n,k]
  * (+ bias) (ReLU) -- epilogues as pdvc_gemm3_f32 -- with the planes streamed into LDS by LDS-DMA, so that only A is

@@ -180,6 +180,58 @@ def test_wgrad_split_is_deterministic_and_accurate():
     assert scaled_err(w1, ref, scale) < 1e-6
 
 
+@pytest.mark.parametrize("rows,O,I,lead", [(65536, 256, 512, 0), (4096, 132, 200, 8), (8192, 516, 64, 4),
+                                           (96, 512, 512, 0)])
+def test_wgrad_bias_is_the_column_sum(rows, O, I, lead):
+    """pdvc_gemm3_wgrad_bias_f32 (mm_wgrad(..., db=)): dW as the plain weight-gradient launch, bit for bit, and db =
+    gy.sum(0) within fp32 summation error of float64 (|err| <= 1e-6 sum |gy|: the rounding of a sum of `rows` terms
+    in a fixed order is ~sqrt(rows) 2^-24 of it), deterministic; O not a multiple of the 256-wide tile, strided
+    rows, one split (rows = 96) and many."""
+    from pdvc.ops.functions.gemm3 import mm_wgrad
+    import pdvc.ops.functions.gemm3 as G
+    torch.manual_seed(rows + O)
+    base = torch.randn(rows, O + lead, device=DEV)
+    base[:, :O] *= torch.exp2(torch.randint(-6, 6, (O,), device=DEV).float())  # columns of different magnitudes
+    gy = base[:, :O]
+    x = torch.randn(rows, I + 4, device=DEV)[:, :I]
+    old = G.MIN_ROWS
+    G.MIN_ROWS = 0
+    try:
+        w0 = mm_wgrad(gy, x)
+        db1 = torch.full((O,), float("nan"), device=DEV)
+        w1 = mm_wgrad(gy, x, db=db1)
+        db2 = torch.empty(O, device=DEV)
+        mm_wgrad(gy, x, db=db2)
+    finally:
+        G.MIN_ROWS = old
+    assert w0 is not None and torch.equal(w0, w1), "the fused bias sum must leave dW unchanged"
+    assert torch.equal(db1, db2), "the bias sum must be deterministic"
+    ref = gy.double().sum(0)
+    assert float(((db1.double() - ref).abs() / gy.double().abs().sum(0)).max()) < 1e-6
+
+
+def test_linear_bias_gradients_through_the_fused_wgrad(monkeypatch):
+    """The nn.Linear backward (TorchLinearFunction) takes its bias gradient from the weight-gradient pass: dW
+    unchanged, db within fp32 summation error of float64 (1e-6 of sum |gy|) as the separate colsum pass it replaces
+    (PDVC_WGRAD_BIAS A/B switch)."""
+    G = _on_gemm3(monkeypatch)
+    from pdvc.ops.functions import linear as L
+    torch.manual_seed(3)
+    x = torch.randn(4096, 256, device=DEV, requires_grad=True)
+    lin = torch.nn.Linear(256, 384).to(DEV)
+    gy = torch.randn(4096, 384, device=DEV)
+    grads = {}
+    for fused in (True, False):
+        monkeypatch.setattr(G, "WGRAD_BIAS", fused)
+        lin.zero_grad()
+        L.TorchLinearFunction.apply(x, lin.weight, lin.bias, False).backward(gy)
+        grads[fused] = (lin.weight.grad.clone(), lin.bias.grad.clone())
+    assert torch.equal(grads[True][0], grads[False][0])
+    ref, scale = gy.double().sum(0), gy.double().abs().sum(0)  # fp32 sums in two orders: bound relative to sum |gy|
+    for fused in (True, False):
+        assert float(((grads[fused][1].double() - ref).abs() / scale).max()) < 1e-6
+
+
 def test_gemm3_argument_errors():
     _n = _lib()
     A = torch.randn(64, 48, device=DEV)
