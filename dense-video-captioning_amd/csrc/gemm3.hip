@@ -770,8 +770,9 @@ __global__ __launch_bounds__(NT, 1) void gemm3w_kernel(int M, int N, int K, cons
 
     Regs rg;
     float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);  // CS: this thread's A column chunk summed over its rows
+    const bool csb = CS && tn == 0;                  // (only column block 0's tiles write the sums)
     auto cadd = [&](int i) {
-        if constexpr (CS) {
+        if (csb) {
             csum.x += rg.a[i].x;
             csum.y += rg.a[i].y;
             csum.z += rg.a[i].z;
@@ -822,7 +823,7 @@ __global__ __launch_bounds__(NT, 1) void gemm3w_kernel(int M, int N, int K, cons
     if (s < nst) stage(s, F_{}, F_{});
     (void)l32;
     if constexpr (CS) {
-        if (tn == 0) {  // (block-uniform) LDS is free: the last stage ended with a barrier
+        if (csb) {  // (block-uniform) LDS is free: the last stage ended with a barrier
             float4* red = reinterpret_cast<float4*>(lds);
             red[threadIdx.x] = csum;  // [wave][column chunk]: the chunk is threadIdx.x % 64 in every stage
             __syncthreads();
@@ -847,20 +848,25 @@ __global__ __launch_bounds__(NT, 1) void gemm3w_kernel(int M, int N, int K, cons
     else store_tile<EPI, false, 4, 2>(acc, Cz, ldc, nullptr, m0 + wm, n0 + wn, M, N, l32, 4 * h);
 }
 
-// out[i] (=|+=) sum_z ws[z * n + i], float4 lanes (n % 4 == 0)
+// out[i] (=|+=) sum_z ws[z * n + i], float4 lanes (n % 4 == 0); then, in the same launch, out2[i] = sum_z ws2[z * n2 + i]
+// over a second region (the bias-gradient partials of gemm3w<CS>; n2 = 0: none)
 template <bool ACC>
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ ws, int splits, long n4,
-                                                       float* __restrict__ out) {
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-        float4 s = ACC ? reinterpret_cast<const float4*>(out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+                                                       float* __restrict__ out, const float* __restrict__ ws2,
+                                                       long n42, float* __restrict__ out2) {
+    for (long t = blockIdx.x * 256L + threadIdx.x; t < n4 + n42; t += (long)gridDim.x * 256) {
+        const bool first = t < n4;
+        const long i = first ? t : t - n4, n = first ? n4 : n42;
+        const float4* src = reinterpret_cast<const float4*>(first ? ws : ws2);
+        float4 s = ACC && first ? reinterpret_cast<const float4*>(out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
         for (int z = 0; z < splits; ++z) {
-            const float4 v = reinterpret_cast<const float4*>(ws)[(long)z * n4 + i];
+            const float4 v = src[(long)z * n + i];
             s.x += v.x;
             s.y += v.y;
             s.z += v.z;
             s.w += v.w;
         }
-        reinterpret_cast<float4*>(out)[i] = s;
+        reinterpret_cast<float4*>(first ? out : out2)[i] = s;
     }
 }
 
@@ -913,18 +919,12 @@ int wgrad_launch(int M, int N, int K, const float* A, long lda, const float* B, 
         else hipLaunchKernelGGL(gemm3w_kernel<EPI_STORE>, gw, dim3(NT), 0, s, M, N, K, A, lda, B, ldb, dw, ldw, kpw, (int)wn_, slab_n, nzw, nullptr);
     }
     PDVC_CHECK_LAUNCH("gemm3w_kernel");
-    if (nzw > 1) {
-        const long n4 = slab_n / 4;
-        const int blocks = (int)std::min<long>((n4 + 255) / 256, 2048);
-        if (epilogue == 3) hipLaunchKernelGGL(slab_sum_kernel<true>, dim3(blocks), dim3(256), 0, s, workspace, nzw, n4, C);
-        else hipLaunchKernelGGL(slab_sum_kernel<false>, dim3(blocks), dim3(256), 0, s, workspace, nzw, n4, C);
+    if (nzw > 1) {  // dW's slabs, and db's partials in the same launch
+        const long n4 = slab_n / 4, m4 = db != nullptr ? M / 4 : 0;
+        const int blocks = (int)std::min<long>((n4 + m4 + 255) / 256, 2048);
+        if (epilogue == 3) hipLaunchKernelGGL(slab_sum_kernel<true>, dim3(blocks), dim3(256), 0, s, workspace, nzw, n4, C, db_ws, m4, db);
+        else hipLaunchKernelGGL(slab_sum_kernel<false>, dim3(blocks), dim3(256), 0, s, workspace, nzw, n4, C, db_ws, m4, db);
         PDVC_CHECK_LAUNCH("slab_sum_kernel");
-        if (db != nullptr) {
-            const long m4 = M / 4;
-            const int bl = (int)std::min<long>((m4 + 255) / 256, 2048);
-            hipLaunchKernelGGL(slab_sum_kernel<false>, dim3(bl), dim3(256), 0, s, db_ws, nzw, m4, db);
-            PDVC_CHECK_LAUNCH("slab_sum_kernel");
-        }
     }
     return PDVC_OK;
 }
@@ -975,8 +975,8 @@ extern "C" int pdvc_gemm3_f32(int M, int N, int K, const float* A, long lda, int
     if (slab) {
         const long n4 = slab_n / 4;
         const int blocks = (int)std::min<long>((n4 + 255) / 256, 2048);
-        if (epilogue == 3) hipLaunchKernelGGL(slab_sum_kernel<true>, dim3(blocks), dim3(256), 0, s, workspace, nz, n4, C);
-        else hipLaunchKernelGGL(slab_sum_kernel<false>, dim3(blocks), dim3(256), 0, s, workspace, nz, n4, C);
+        if (epilogue == 3) hipLaunchKernelGGL(slab_sum_kernel<true>, dim3(blocks), dim3(256), 0, s, workspace, nz, n4, C, nullptr, 0L, nullptr);
+        else hipLaunchKernelGGL(slab_sum_kernel<false>, dim3(blocks), dim3(256), 0, s, workspace, nz, n4, C, nullptr, 0L, nullptr);
         PDVC_CHECK_LAUNCH("slab_sum_kernel");
     }
     return PDVC_OK;
