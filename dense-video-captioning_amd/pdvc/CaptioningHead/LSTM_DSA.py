@@ -20,6 +20,7 @@ The teacher-forced loop length is computed on the host from the caption lengths 
 first all-zero token column, LSTM_DSA.py:103-104): the same steps are computed, without a per-step sync.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -39,6 +40,8 @@ from pdvc.ops.modules.linear import Linear
 # greedy decoding: ctx2att of the samples as a gather of the once-projected memory rows (LSTMDSACaptioner.
 # _ctx2att_rows) instead of a GEMM per step; False keeps the GEMM (tests compare the two)
 GREEDY_CTX2ATT_GATHER = True
+# the greedy step's word / h / attention-gate products on gemm3 (A/B switch: PDVC_GREEDY_GEMM3=0 keeps torch's)
+GREEDY_GEMM3 = os.environ.get("PDVC_GREEDY_GEMM3", "1") != "0"
 
 
 class _EmbeddingRows(torch.autograd.Function):
@@ -326,7 +329,10 @@ class LSTMDSACaptioner(Captioner):
         lvl, nl = _levels(level_T)
         st = _n.stream()
         HP = b["HP"]
-        torch.addmm(w["b_h"], h, w["W_h"].t(), out=HP)
+        if GREEDY_GEMM3:
+            addmm_nt(w["b_h"], h, w["W_h"], out=HP)
+        else:
+            torch.addmm(w["b_h"], h, w["W_h"].t(), out=HP)
         ref = ref_rows.contiguous()
         _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(mask_u8), _n.ptr(row_video), _n.ptr(HP), Ph, 0,
                 _n.ptr(off_hs.contiguous()), _n.ptr(ref), ref.shape[2], int(rd1_rows), lvl, nl, Nv, R, M, D,
@@ -340,7 +346,10 @@ class LSTMDSACaptioner(Captioner):
         ah, ldh = _n.rows(HP[:, n_off:n_off + A])
         _n.call("pdvc_softattn_forward_f32", _n.ptr(b["ATT"]), ah, ldh, _n.ptr(core.alpha_net.weight.view(-1)),
                 _n.ptr(core.alpha_net.bias), _n.ptr(b["CLIP"]), R, M, A, D, _n.ptr(b["RES"]), _n.ptr(b["PROBS"]), st)
-        torch.mm(b["RES"], w["W_att"].t(), out=b["GATT"])
+        if GREEDY_GEMM3:
+            mm_nt(b["RES"], w["W_att"], out=b["GATT"])
+        else:
+            torch.mm(b["RES"], w["W_att"].t(), out=b["GATT"])
         xg = x_gates.contiguous()
         gh, ldg = _n.rows(HP[:, n_off + A:])
         h_out, c_out = b["H"][t % 2], b["C"][t % 2]
@@ -463,6 +472,9 @@ class LSTMDSACaptioner(Captioner):
         c = hs_rows.new_zeros(R, w["H"])
         fused = self._fused_step_ok(hs_rows, value, w)
         if fused:
+            # the per-step products on the in-tree fp32 GEMM (gemm3, row-major weights: the word and attention
+            # parts of W_ih as contiguous copies, once per decode) where the row count takes it, else torch's
+            w = dict(w, W_x=w["W_x"].contiguous(), W_att=w["W_att"].contiguous())
             value = value.contiguous()
             step_bufs = self._greedy_buffers(R, value, w)
             A = w["A"]  # the gather kernel's widths: powers of two in [32, 512] (else ctx2att stays a GEMM)
@@ -494,7 +506,10 @@ class LSTMDSACaptioner(Captioner):
                     it = torch.multinomial(prob, 1, generator=generator)
                     sample_lp = logprobs.gather(1, it)
                     it = it.view(-1)
-            x_gates = F.linear(self.embed(it), w["W_x"])
+            if fused and GREEDY_GEMM3:
+                x_gates = mm_nt(self.embed(it), w["W_x"])
+            else:
+                x_gates = F.linear(self.embed(it), w["W_x"])
             if fused:
                 h, c = self._step_fused(w, step_bufs, t, h, c, x_gates, hs_part, off_hs, value, mask_u8, row_video,
                                         ref_rows, rd1_rows, level_T)

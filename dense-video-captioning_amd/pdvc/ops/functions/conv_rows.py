@@ -7,6 +7,8 @@
     the W0 tap of the previous odd row, added shifted by one output row (zero at t = 0: the padding);
   * GroupNorm(G, C) on rows: pdvc_groupnorm_rows_* (csrc/groupnorm.hip).
 Same parameters (nn.Conv1d / nn.GroupNorm), same math."""
+import os
+
 import torch
 import torch.nn.functional as F
 from torch.autograd import Function
@@ -17,6 +19,8 @@ from .gemm3 import addmm_nt, mm_dgrad, mm_nt
 from .linear import colsum, dense, wgrad_mm
 
 GN_ROWS = 64  # rows per stats chunk (csrc/groupnorm.hip kGnRows)
+# the stride-2 conv's previous-odd-row tap in an accumulate epilogue (A/B switch: PDVC_CONV_TAP_EPILOGUE=0)
+_TAP_EPILOGUE = os.environ.get("PDVC_CONV_TAP_EPILOGUE", "1") != "0"
 
 
 class ConvS2RowsFunction(Function):
@@ -36,9 +40,18 @@ class ConvS2RowsFunction(Function):
         w12 = torch.cat([weight[:, :, 1], weight[:, :, 2]], 1)  # (O, 2C): taps on x[2t], x[2t+1]
         w0 = weight[:, :, 0].contiguous()                       # (O, C): tap on x[2t-1]
         y = addmm_nt(bias, X2, w12)
-        z = mm_nt(X2[:, C:], w0)                         # x[2t+1] W0^T feeds output row t+1
         yv = y.view(N, L, O)
-        yv[:, 1:] += z.view(N, L, O)[:, :-1]
+        if _TAP_EPILOGUE and N * L > 1:
+            # x[2t+1] W0^T added to output row t+1 by the accumulate epilogue of one GEMM over the rows shifted by
+            # one (out = y[1:]); the rows it also reaches across a video boundary (each video's row 0, whose tap is
+            # the zero padding) are restored from a copy taken before -- the same values as the separate product
+            # and add, without the (N, L, O) intermediate and its add pass
+            first = yv[1:, 0].clone()
+            mm_dgrad(X2[:-1, C:], w0.t().contiguous(), out=y[1:])
+            yv[1:, 0] = first
+        else:
+            z = mm_nt(X2[:, C:], w0)                     # x[2t+1] W0^T feeds output row t+1
+            yv[:, 1:] += z.view(N, L, O)[:, :-1]
         ctx.save_for_backward(X2, w12, w0)
         ctx.shape = (N, T, C, L, O, Tin)
         return yv
@@ -49,8 +62,9 @@ class ConvS2RowsFunction(Function):
         X2, w12, w0 = ctx.saved_tensors
         N, T, C, L, O, Tin = ctx.shape
         dy2 = dy.reshape(N * L, O).contiguous()
-        dz = torch.zeros_like(dy2).view(N, L, O)
+        dz = torch.empty_like(dy2).view(N, L, O)  # dy shifted up one row per video, zero at the last (one write)
         dz[:, :-1] = dy2.view(N, L, O)[:, 1:]
+        dz[:, -1] = 0.0
         dz2 = dz.view(N * L, O)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:

@@ -158,10 +158,17 @@ def test_batched_step_graph_equals_reference(fixture):
         _check_grads(d, model.named_parameters(), "step graph")
 
 
-def test_batched_eval_and_postprocess_match_reference(fixture):
+@pytest.mark.parametrize("on_gemm3", [False, True])
+def test_batched_eval_and_postprocess_match_reference(fixture, on_gemm3, monkeypatch):
     """Eval forward (greedy captions) of the 3-video batch and our PostProcess on it against each video's
-    reference eval forward and reference PostProcess (pdvc/pdvc.py:493-546)."""
+    reference eval forward and reference PostProcess (pdvc/pdvc.py:493-546).  on_gemm3: every eligible product on
+    the in-tree fp32 GEMM at these small row counts (MIN_ROWS = 0) -- the greedy step's word, h and attention-gate
+    products among them, as at the bench's row counts."""
     from data.video_dataset import Translator
+    if on_gemm3:
+        import pdvc.ops.functions.gemm3 as G
+        monkeypatch.setattr(G, "MIN_ROWS", 0)
+        monkeypatch.setattr(G, "ENABLED", True)
     d = fixture
     nv = int(d["n_videos"])
     model, criterion = TM.build_filled(d)

@@ -85,3 +85,34 @@ def test_base_encoder_flat_buffer_matches_per_level(T, monkeypatch):
     for k in gp0:
         err = (gp1[k] - gp0[k]).abs().max().item()
         assert err <= 1e-5 * (gp0[k].abs().max().item() + 1.0), (k, err)
+
+
+@pytest.mark.parametrize("N,T", [(64, 512), (5, 37), (1, 256)])
+def test_conv_s2_tap_epilogue_matches_conv1d(N, T, monkeypatch):
+    """The stride-2 conv with its previous-odd-row tap accumulated in a GEMM epilogue over the shifted rows (each
+    video's row 0 restored: its tap is the zero padding) against nn.Conv1d in float64 and against the separate
+    product + add (PDVC_CONV_TAP_EPILOGUE=0), every product on gemm3 (MIN_ROWS = 0); ragged T and N = 1 included."""
+    import pdvc.ops.functions.gemm3 as G
+    import pdvc.ops.functions.conv_rows as CR
+    monkeypatch.setattr(G, "MIN_ROWS", 0)
+    torch.manual_seed(N + T)
+    C, O = 512, 512
+    x = torch.randn(N, T, C, device=DEV)
+    w = torch.randn(O, C, 3, device=DEV) * C ** -0.5
+    b = torch.randn(O, device=DEV)
+    g = torch.randn(N, (T + 1) // 2, O, device=DEV)
+    outs = {}
+    for tap in (True, False):
+        monkeypatch.setattr(CR, "_TAP_EPILOGUE", tap)
+        xx, ww, bb = (t.clone().requires_grad_() for t in (x, w, b))
+        y = CR.ConvS2RowsFunction.apply(xx, ww, bb)
+        y.backward(g)
+        outs[tap] = (y.detach(), xx.grad, ww.grad, bb.grad)
+    ref = F.conv1d(x.double().transpose(1, 2), w.double(), b.double(), stride=2, padding=1).transpose(1, 2)
+    scale = F.conv1d(x.double().abs().transpose(1, 2), w.double().abs(), b.double().abs(), stride=2,
+                     padding=1).transpose(1, 2)
+    for tap in (True, False):
+        assert float(((outs[tap][0].double() - ref).abs() / scale).max()) < 1e-6, tap
+    torch.testing.assert_close(outs[True][0], outs[False][0], rtol=1e-6, atol=1e-5)
+    for a, c in zip(outs[True][1:], outs[False][1:]):
+        assert torch.equal(a, c), "the backward does not depend on the forward's form"
