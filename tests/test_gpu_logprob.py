@@ -67,11 +67,11 @@ def test_logprob_pick_bad_target_poisons_and_empty_rows():
     assert logp.shape == (0, 3, 16) and picked.shape == (0, 3)
 
 
-@pytest.mark.parametrize("V", [5749, 1609, 37])
+@pytest.mark.parametrize("V", [5749, 1609, 37, 8192, 9000])
 def test_logprob_argmax_matches_torch(V):
     """pdvc_logprob_argmax_f32 (greedy decoding's word choice, LSTM_DSA.py:149-151) against torch.max over
     log_softmax: identical indices (ties to the first maximal index, rows with repeated maxima included), the
-    log-probabilities within 1e-5."""
+    log-probabilities within 1e-5; the register-resident kernel (V <= 8 192) and the streaming one (9 000)."""
     from pdvc import _native as _n
     torch.manual_seed(V)
     R = 300

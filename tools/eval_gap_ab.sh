@@ -12,5 +12,6 @@ for spec in "${ARMS[@]}"; do
       2> "$OUT/$arm.err" || { echo "$arm failed"; tail -20 "$OUT/$arm.err"; exit 1; }
   kt=$(find "$OUT/$arm" -name "*kernel_trace.csv" | head -1)
   echo "== $arm ($E)"; tail -1 "$OUT/$arm.json" | cut -c1-120; python tools/gaps.py "$kt" | tail -7
+  python tools/evalbreak.py "$kt" 25 > "$OUT/${arm}_kernels.txt"
   rm -f "$kt"
 done
