@@ -42,6 +42,8 @@ from pdvc.ops.modules.linear import Linear
 GREEDY_CTX2ATT_GATHER = True
 # the greedy step's word / h / attention-gate products on gemm3 (A/B switch: PDVC_GREEDY_GEMM3=0 keeps torch's)
 GREEDY_GEMM3 = os.environ.get("PDVC_GREEDY_GEMM3", "1") != "0"
+# the greedy step's gathers and soft attention in one launch, samples and att not written (A/B: PDVC_GREEDY_FUSED_ATT=0)
+GREEDY_FUSED_ATT = os.environ.get("PDVC_GREEDY_FUSED_ATT", "1") != "0"
 
 
 class _EmbeddingRows(torch.autograd.Function):
@@ -285,8 +287,8 @@ class LSTMDSACaptioner(Captioner):
         D = value.shape[-1] // M
         Ph = w["W_h"].shape[0]
         kw = dict(dtype=value.dtype, device=value.device)
-        return dict(HP=torch.empty((R, Ph), **kw), CLIP=torch.empty((R, M, 16, D), **kw),
-                    LOC=torch.empty((R, M, 16), **kw), ATT=torch.empty((R * M * 16, w["A"]), **kw),
+        # (CLIP and ATT, the samples and att rows, only for the three-launch step: allocated there on first use)
+        return dict(HP=torch.empty((R, Ph), **kw), CLIP=None, LOC=torch.empty((R, M, 16), **kw), ATT=None,
                     PROBS=torch.empty((R, M, 16), **kw), RES=torch.empty((R, M * D), **kw),
                     GATT=torch.empty((R, 4 * w["H"]), **kw), ACTS=torch.empty((R, 4 * w["H"]), **kw),
                     H=[torch.empty((R, w["H"]), **kw) for _ in range(2)],
@@ -334,6 +336,41 @@ class LSTMDSACaptioner(Captioner):
         else:
             torch.addmm(w["b_h"], h, w["W_h"].t(), out=HP)
         ref = ref_rows.contiguous()
+        alpha_w = core.alpha_net.weight.view(-1)
+        if (GREEDY_FUSED_ATT and b["U"] is not None and A == D == 512 and Ph % 4 == 0 and n_off % 4 == 0
+                and all(q.data_ptr() % 16 == 0 for q in (value, b["U"], HP, alpha_w))):
+            # the two gathers and the soft attention in one launch (the teacher-forced recurrence's kernel), the
+            # samples and att never written: nothing reads them back in a greedy decode
+            ah, ldh = _n.rows(HP[:, n_off:n_off + A])
+            _n.call("pdvc_cap_softattn_forward_f32", _n.ptr(value), _n.ptr(mask_u8), _n.ptr(b["U"]),
+                    _n.ptr(row_video), _n.ptr(HP), Ph, 0, _n.ptr(off_hs.contiguous()), _n.ptr(ref), ref.shape[2],
+                    int(rd1_rows), lvl, nl, Nv, R, M, D, NUM_SAMPLES // nl, ah, ldh, _n.ptr(alpha_w),
+                    _n.ptr(core.alpha_net.bias), None, _n.ptr(b["LOC"]), None, _n.ptr(b["PROBS"]), _n.ptr(b["RES"]),
+                    st)
+        else:
+            self._gather_softattn(b, value, mask_u8, row_video, HP, Ph, off_hs, ref, rd1_rows, lvl, nl, Nv, R, M, D,
+                                  A, n_off, st)
+        if GREEDY_GEMM3:
+            mm_nt(b["RES"], w["W_att"], out=b["GATT"])
+        else:
+            torch.mm(b["RES"], w["W_att"].t(), out=b["GATT"])
+        xg = x_gates.contiguous()
+        gh, ldg = _n.rows(HP[:, n_off + A:])
+        h_out, c_out = b["H"][t % 2], b["C"][t % 2]
+        _n.call("pdvc_lstm_cell_forward_f32", _n.ptr(xg), G, _n.ptr(b["GATT"]), G, gh, ldg,
+                _n.ptr(hs_part.contiguous()), G, _n.ptr(c.contiguous()), R, H, _n.ptr(h_out), H, _n.ptr(c_out),
+                _n.ptr(b["ACTS"]), st)
+        return h_out, c_out
+
+    def _gather_softattn(self, b, value, mask_u8, row_video, HP, Ph, off_hs, ref, rd1_rows, lvl, nl, Nv, R, M, D, A,
+                         n_off, st):
+        """The greedy step's samples, att and soft attention as three launches (gather, gather or ctx2att GEMM, soft
+        attention): the heads the fused kernel does not take."""
+        from pdvc.ops.functions.ms_deform_attn_func import NUM_SAMPLES
+        core = self.core
+        if b["CLIP"] is None:
+            b["CLIP"] = torch.empty((R, M, NUM_SAMPLES, D), dtype=value.dtype, device=value.device)
+            b["ATT"] = torch.empty((R * M * NUM_SAMPLES, A), dtype=value.dtype, device=value.device)
         _n.call("pdvc_cap_gather_forward_f32", _n.ptr(value), _n.ptr(mask_u8), _n.ptr(row_video), _n.ptr(HP), Ph, 0,
                 _n.ptr(off_hs.contiguous()), _n.ptr(ref), ref.shape[2], int(rd1_rows), lvl, nl, Nv, R, M, D,
                 NUM_SAMPLES // nl, _n.ptr(b["CLIP"]), _n.ptr(b["LOC"]), st)
@@ -346,17 +383,6 @@ class LSTMDSACaptioner(Captioner):
         ah, ldh = _n.rows(HP[:, n_off:n_off + A])
         _n.call("pdvc_softattn_forward_f32", _n.ptr(b["ATT"]), ah, ldh, _n.ptr(core.alpha_net.weight.view(-1)),
                 _n.ptr(core.alpha_net.bias), _n.ptr(b["CLIP"]), R, M, A, D, _n.ptr(b["RES"]), _n.ptr(b["PROBS"]), st)
-        if GREEDY_GEMM3:
-            mm_nt(b["RES"], w["W_att"], out=b["GATT"])
-        else:
-            torch.mm(b["RES"], w["W_att"].t(), out=b["GATT"])
-        xg = x_gates.contiguous()
-        gh, ldg = _n.rows(HP[:, n_off + A:])
-        h_out, c_out = b["H"][t % 2], b["C"][t % 2]
-        _n.call("pdvc_lstm_cell_forward_f32", _n.ptr(xg), G, _n.ptr(b["GATT"]), G, gh, ldg,
-                _n.ptr(hs_part.contiguous()), G, _n.ptr(c.contiguous()), R, H, _n.ptr(h_out), H, _n.ptr(c_out),
-                _n.ptr(b["ACTS"]), st)
-        return h_out, c_out
 
     def decode_teacher_forced(self, hs_rows, ref_rows, rd1_rows, row_video, memory, mask_flatten, level_T, seq,
                               n_steps, video_csr=None, pick_target=None, tokens=None, step_ranges=None):
