@@ -44,6 +44,8 @@ GREEDY_CTX2ATT_GATHER = True
 GREEDY_GEMM3 = os.environ.get("PDVC_GREEDY_GEMM3", "1") != "0"
 # the greedy step's gathers and soft attention in one launch, samples and att not written (A/B: PDVC_GREEDY_FUSED_ATT=0)
 GREEDY_FUSED_ATT = os.environ.get("PDVC_GREEDY_FUSED_ATT", "1") != "0"
+# the greedy step's word gates as rows of a per-decode (vocabulary x 4H) table (A/B: PDVC_GREEDY_WORD_TABLE=0)
+GREEDY_WORD_TABLE = os.environ.get("PDVC_GREEDY_WORD_TABLE", "1") != "0"
 
 
 class _EmbeddingRows(torch.autograd.Function):
@@ -506,6 +508,11 @@ class LSTMDSACaptioner(Captioner):
             A = w["A"]  # the gather kernel's widths: powers of two in [32, 512] (else ctx2att stays a GEMM)
             gather = GREEDY_CTX2ATT_GATHER and 32 <= A <= 512 and A & (A - 1) == 0
             step_bufs["U"] = self._ctx2att_rows(value, mask_u8) if gather else None
+        # the word part of the gates for every vocabulary entry, once per decode ((V + 1) x 4H, the embedding table
+        # through W_x): each step then gathers its rows instead of embedding and projecting R rows
+        xtab = None
+        if fused and GREEDY_WORD_TABLE and self.embed.padding_idx is None and self.embed.max_norm is None:
+            xtab = mm_nt(self.embed.weight, w["W_x"])
         it = torch.zeros(R, dtype=torch.long, device=hs_rows.device)
         seq, seqlp = [], []
         unfinished = None
@@ -532,7 +539,9 @@ class LSTMDSACaptioner(Captioner):
                     it = torch.multinomial(prob, 1, generator=generator)
                     sample_lp = logprobs.gather(1, it)
                     it = it.view(-1)
-            if fused and GREEDY_GEMM3:
+            if xtab is not None:
+                x_gates = xtab.index_select(0, it)
+            elif fused and GREEDY_GEMM3:
                 x_gates = mm_nt(self.embed(it), w["W_x"])
             else:
                 x_gates = F.linear(self.embed(it), w["W_x"])
