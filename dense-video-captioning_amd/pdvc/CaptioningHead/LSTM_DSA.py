@@ -46,6 +46,8 @@ GREEDY_GEMM3 = os.environ.get("PDVC_GREEDY_GEMM3", "1") != "0"
 GREEDY_FUSED_ATT = os.environ.get("PDVC_GREEDY_FUSED_ATT", "1") != "0"
 # the greedy step's word gates as rows of a per-decode (vocabulary x 4H) table (A/B: PDVC_GREEDY_WORD_TABLE=0)
 GREEDY_WORD_TABLE = os.environ.get("PDVC_GREEDY_WORD_TABLE", "1") != "0"
+# the teacher-forced word gates the same way, with a sorted (atomic-free) backward (A/B: PDVC_WORD_TABLE=0)
+WORD_TABLE = os.environ.get("PDVC_WORD_TABLE", "1") != "0"
 
 
 class _EmbeddingRows(torch.autograd.Function):
@@ -96,6 +98,41 @@ class _WordGates(torch.autograd.Function):
             dW_x = torch.mm(gs.t(), xs)
         dw = weight.new_zeros(weight.shape).index_add_(0, ids, mm_dgrad(gs, W_x))
         return dw, dW_x, None, None
+
+
+class _WordTable(torch.autograd.Function):
+    """xe = W_x embed(idx) (idx (n, R) step-major) as rows of the batch's word-gate table T = embed.weight W_x^T
+    ((V + 1) x 4H): one (V + 1)-row GEMM and a row gather instead of an (n R)-row GEMM.  Backward: the gathered rows'
+    gradients summed per word in a fixed order (a stable sort of idx, pdvc_sorted_row_sums_f32: no atomics), then
+    d embed.weight = dT W_x and dW_x = dT^T embed.weight -- two (V + 1)-row GEMMs where the per-position form ran two
+    (n R)-row GEMMs and an atomic scatter-add into the embedding.  The same sums as LSTM_DSA.py:229-231 (embed, then
+    W_ih over [xt, ...]) in another order."""
+
+    @staticmethod
+    def forward(ctx, weight, W_x, idx):
+        ctx.save_for_backward(weight, W_x, idx)
+        table = mm_nt(weight, W_x)
+        return table.index_select(0, idx.reshape(-1)).view(*idx.shape, W_x.shape[0])
+
+    @staticmethod
+    def backward(ctx, g):
+        weight, W_x, idx = ctx.saved_tensors
+        flat = idx.reshape(-1)
+        keys, order = torch.sort(flat, stable=True)
+        G = g.reshape(flat.numel(), -1)
+        if G.stride(1) != 1 or G.stride(0) % 4 or G.data_ptr() % 16:
+            G = G.contiguous()
+        V, C4 = weight.shape[0], G.shape[1]
+        dT = torch.empty((V, C4), dtype=G.dtype, device=G.device)
+        _n.call("pdvc_sorted_row_sums_f32", _n.ptr_any(G), G.stride(0), C4, _n.ptr(keys), _n.ptr(order), flat.numel(),
+                V, _n.ptr(dT), C4, _n.stream())
+        dw = mm_dgrad(dT, W_x) if ctx.needs_input_grad[0] else None
+        dW_x = None
+        if ctx.needs_input_grad[1]:
+            dW_x = mm_wgrad(dT, weight)
+            if dW_x is None:
+                dW_x = torch.mm(dT.t(), weight)
+        return dw, dW_x, None
 
 
 def embed_rows(embedding, idx):
@@ -419,6 +456,10 @@ class LSTMDSACaptioner(Captioner):
             act = torch.where(live, (sc % n_) * R_ + torch.div(sc, n_, rounding_mode="floor"),
                               torch.full_like(sc, R_ * n_))
             xe = _WordGates.apply(self.embed.weight, w["W_x"], seq[:, :n_steps].t().contiguous(), act)
+        elif (WORD_TABLE and seq.is_cuda and hs_rows.dtype == torch.float32 and self.embed.padding_idx is None
+              and self.embed.max_norm is None and w["W_x"].shape[0] % 4 == 0):
+            # the word part of the gates as rows of the batch's (V + 1) x 4H table (_WordTable)
+            xe = _WordTable.apply(self.embed.weight, w["W_x"], seq[:, :n_steps].t().contiguous())
         else:
             xt = embed_rows(self.embed, seq[:, :n_steps].t())  # (n, R, E): step-major, the recurrence's layout
             xe = dense(xt, w["W_x"])  # loop-invariant gate parts: word part per step, event part per row

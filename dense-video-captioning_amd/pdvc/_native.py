@@ -94,6 +94,7 @@ SIGNATURES = {
     "pdvc_gemm1p_f32": [_i, _i, _i, _vp, ctypes.c_long, _vp, _vp, ctypes.c_long, _vp, _i, _vp],
     "pdvc_gemm3_f32": [_i, _i, _i, _vp, ctypes.c_long, _i, _vp, ctypes.c_long, _i, _vp, ctypes.c_long, _vp, _i, _i,
                        _vp, _vp],
+    "pdvc_sorted_row_sums_f32": [_vp, ctypes.c_long, _i, _vp, _vp, ctypes.c_long, _i, _vp, ctypes.c_long, _vp],
     "pdvc_gemm3_wgrad_bias_f32": [_i, _i, _i, _vp, ctypes.c_long, _vp, ctypes.c_long, _vp, ctypes.c_long, _i, _i,
                                   _vp, _vp, _vp, _vp],
     "pdvc_mha_forward_f32": [_vp, _vp, _u8p] + [_i] * 4 + [_f, _u64] + [_vp] * 4,
