@@ -81,6 +81,9 @@ class _WordGates(torch.autograd.Function):
     @staticmethod
     def forward(ctx, weight, W_x, idx, act):
         ctx.save_for_backward(weight, W_x, idx, act)
+        ctx.table = WORD_TABLE and idx.is_cuda and W_x.shape[0] % 4 == 0
+        if ctx.table:  # rows of the batch's (V + 1) x 4H word-gate table (_WordTable)
+            return mm_nt(weight, W_x).index_select(0, idx.reshape(-1)).view(*idx.shape, W_x.shape[0])
         xt = weight.index_select(0, idx.reshape(-1))
         return mm_nt(xt, W_x).view(*idx.shape, W_x.shape[0])
 
@@ -90,8 +93,18 @@ class _WordGates(torch.autograd.Function):
         N = idx.numel()
         a = act.clamp(max=N - 1)
         gs = g.reshape(N, -1).index_select(0, a)
-        gs.masked_fill_((act >= N)[:, None], 0.0)  # padding entries: no contribution
         ids = idx.reshape(-1).index_select(0, a)
+        if ctx.table:  # the listed positions' gradients summed per word (padding entries keyed past the table)
+            V = weight.shape[0]
+            keys, order = torch.sort(torch.where(act >= N, torch.full_like(ids, V), ids), stable=True)
+            dT = torch.empty((V, gs.shape[1]), dtype=gs.dtype, device=gs.device)
+            _n.call("pdvc_sorted_row_sums_f32", _n.ptr(gs), gs.stride(0), gs.shape[1], _n.ptr(keys), _n.ptr(order),
+                    ids.numel(), V, _n.ptr(dT), dT.stride(0), _n.stream())
+            dW_x = mm_wgrad(dT, weight)
+            if dW_x is None:
+                dW_x = torch.mm(dT.t(), weight)
+            return mm_dgrad(dT, W_x), dW_x, None, None
+        gs.masked_fill_((act >= N)[:, None], 0.0)  # padding entries: no contribution
         xs = weight.index_select(0, ids)  # the embedding rows again (not saved: (n R, E) floats)
         dW_x = mm_wgrad(gs, xs)
         if dW_x is None:

@@ -74,3 +74,32 @@ def test_word_table_matches_per_position_gates(monkeypatch):
     assert float((dw1 - dw0).abs().max()) <= 1e-5 * (float(dw0.abs().max()) + 1.0)
     x2, de2, dw2 = run(True)
     assert torch.equal(de1, de2) and torch.equal(dw1, dw2), "the table's backward is deterministic"
+
+
+@pytest.mark.parametrize("table", [True, False])
+def test_word_gates_over_listed_positions_gpu(table, monkeypatch):
+    """_WordGates on the GPU (the packed-token stream's word gates): the table form (rows of the batch's word-gate
+    table, the listed positions' gradients summed per word, padding entries keyed past the table) and the
+    per-position form both equal the full autograd backward when the gate gradient is zero off the listed
+    positions; fp32 operands, float64 reference, bound 1e-5 of each gradient's scale."""
+    import torch.nn.functional as F
+    import pdvc.CaptioningHead.LSTM_DSA as L
+    monkeypatch.setattr(L, "WORD_TABLE", table)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    n, R, V, E, G = 13, 640, 5749, 512, 2048
+    idx = torch.randint(0, V, (n, R), device=DEV, generator=g)
+    idx[0] = 0
+    weight = torch.randn(V, E, device=DEV, generator=g).requires_grad_()
+    W_ih = torch.randn(G, 2 * E, device=DEV, generator=g).mul_(E ** -0.5).requires_grad_()
+    keep = torch.rand(n, R, device=DEV, generator=g) < 0.5
+    up = torch.randn(n, R, G, device=DEV, generator=g) * keep[..., None]
+    wd, Wd = weight.detach().double().requires_grad_(), W_ih.detach().double().requires_grad_()
+    ref_out = F.linear(wd[idx], Wd[:, :E])
+    ref = torch.autograd.grad((ref_out * up.double()).sum(), (wd, Wd))
+    act = torch.nonzero(keep.reshape(-1)).view(-1)
+    act = torch.cat([act, torch.full((5,), n * R, device=DEV)])
+    out = L._WordGates.apply(weight, W_ih[:, :E], idx, act)
+    assert float((out.detach().double() - ref_out.detach()).abs().max()) <= 1e-5 * float(ref_out.detach().abs().max())
+    got = torch.autograd.grad((out * up).sum(), (weight, W_ih))
+    for a, e in zip(got, ref):
+        assert float((a.double() - e).abs().max()) <= 1e-5 * (float(e.abs().max()) + 1.0)
