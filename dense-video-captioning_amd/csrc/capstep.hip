@@ -337,20 +337,24 @@ static bool sa_vec4(const void* const* ptrs, int n, int A, int D, int ld1, int l
 }
 
 // gates = a + b + c + d (each (R,4H) with its own row stride; b, c or d may be NULL); acts <- (i,f,g,o) activations
+// GATHER: gates_a's row of output row r is a_rows[r] (the greedy decode's word-gate table rows, no gathered copy);
+// acts may be NULL (no backward follows: greedy decoding)
+template <bool GATHER>
 __global__ __launch_bounds__(256) void lstm_fwd_kernel(const float* __restrict__ ga, int lda, const float* __restrict__ gb,
                                                        int ldb, const float* __restrict__ gc, int ldc,
                                                        const float* __restrict__ gd, int ldd,
                                                        const float* __restrict__ c_prev, int R, int H,
                                                        float* __restrict__ h_out, int ldho, float* __restrict__ c_out,
-                                                       float* __restrict__ acts) {
+                                                       float* __restrict__ acts, const int64_t* __restrict__ a_rows) {
     const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (long)R * H) return;
     const int r = (int)(idx / H), u = (int)(idx - (long)r * H);
+    const size_t ra = GATHER ? (size_t)a_rows[r] : (size_t)r;
     float z[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int col = q * H + u;
-        float v = ga[(size_t)r * lda + col];
+        float v = ga[ra * lda + col];
         if (gb) v += gb[(size_t)r * ldb + col];
         if (gc) v += gc[(size_t)r * ldc + col];
         if (gd) v += gd[(size_t)r * ldd + col];
@@ -361,11 +365,13 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(const float* __restrict__
     const float h = o * tanhf(c);
     c_out[idx] = c;
     h_out[(size_t)r * ldho + u] = h;
-    float* a = acts + (size_t)r * 4 * H;
-    a[u] = i;
-    a[H + u] = f;
-    a[2 * H + u] = g;
-    a[3 * H + u] = o;
+    if (acts) {
+        float* a = acts + (size_t)r * 4 * H;
+        a[u] = i;
+        a[H + u] = f;
+        a[2 * H + u] = g;
+        a[3 * H + u] = o;
+    }
 }
 
 // dh (R,H) [+ dh2 (R, ld2) if given], dc_next (R,H) or NULL, acts, c_prev, c -> dgates (R,4H), dc_prev (R,H)
@@ -451,9 +457,28 @@ extern "C" int pdvc_lstm_cell_forward_f32(const float* gates_a, int lda, const f
     PDVC_CHECK_ARG(rows >= 0 && hidden > 0 && lda >= 4 * hidden, "invalid sizes");
     const long n = (long)rows * hidden;
     if (n == 0) return PDVC_OK;
-    hipLaunchKernelGGL(lstm_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, gates_a,
-                       lda, gates_b, ldb, gates_c, ldc, gates_d, ldd, c_prev, rows, hidden, h_out, ld_h_out, c_out,
-                       acts);
+    PDVC_CHECK_ARG(acts != nullptr, "acts (rows, 4 hidden) is required");
+    hipLaunchKernelGGL(lstm_fwd_kernel<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       gates_a, lda, gates_b, ldb, gates_c, ldc, gates_d, ldd, c_prev, rows, hidden, h_out, ld_h_out,
+                       c_out, acts, (const int64_t*)nullptr);
+    PDVC_CHECK_LAUNCH("lstm_fwd_kernel");
+    return PDVC_OK;
+}
+
+// The same with gates_a read through a row index (gates_a[a_rows[r]], e.g. a vocabulary table's rows) and acts
+// optional (NULL: not written -- greedy decoding, no backward)
+extern "C" int pdvc_lstm_cell_forward_gather_f32(const float* gates_a, int lda, const int64_t* a_rows,
+                                                 const float* gates_b, int ldb, const float* gates_c, int ldc,
+                                                 const float* gates_d, int ldd, const float* c_prev, int rows,
+                                                 int hidden, float* h_out, int ld_h_out, float* c_out, float* acts,
+                                                 void* stream) {
+    PDVC_CHECK_ARG(rows >= 0 && hidden > 0 && lda >= 4 * hidden, "invalid sizes");
+    PDVC_CHECK_ARG(rows == 0 || (gates_a && a_rows && c_prev && h_out && c_out), "null pointer");
+    const long n = (long)rows * hidden;
+    if (n == 0) return PDVC_OK;
+    hipLaunchKernelGGL(lstm_fwd_kernel<true>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       gates_a, lda, gates_b, ldb, gates_c, ldc, gates_d, ldd, c_prev, rows, hidden, h_out, ld_h_out,
+                       c_out, acts, a_rows);
     PDVC_CHECK_LAUNCH("lstm_fwd_kernel");
     return PDVC_OK;
 }

@@ -46,6 +46,8 @@ GREEDY_GEMM3 = os.environ.get("PDVC_GREEDY_GEMM3", "1") != "0"
 GREEDY_FUSED_ATT = os.environ.get("PDVC_GREEDY_FUSED_ATT", "1") != "0"
 # the greedy step's word gates as rows of a per-decode (vocabulary x 4H) table (A/B: PDVC_GREEDY_WORD_TABLE=0)
 GREEDY_WORD_TABLE = os.environ.get("PDVC_GREEDY_WORD_TABLE", "1") != "0"
+# ... read by the LSTM cell kernel through the word ids, its activations not written (A/B: PDVC_GREEDY_LSTM_GATHER=0)
+GREEDY_LSTM_GATHER = os.environ.get("PDVC_GREEDY_LSTM_GATHER", "1") != "0"
 # the teacher-forced word gates the same way, with a sorted (atomic-free) backward (A/B: PDVC_WORD_TABLE=0)
 WORD_TABLE = os.environ.get("PDVC_WORD_TABLE", "1") != "0"
 
@@ -406,12 +408,18 @@ class LSTMDSACaptioner(Captioner):
             mm_nt(b["RES"], w["W_att"], out=b["GATT"])
         else:
             torch.mm(b["RES"], w["W_att"].t(), out=b["GATT"])
-        xg = x_gates.contiguous()
         gh, ldg = _n.rows(HP[:, n_off + A:])
         h_out, c_out = b["H"][t % 2], b["C"][t % 2]
-        _n.call("pdvc_lstm_cell_forward_f32", _n.ptr(xg), G, _n.ptr(b["GATT"]), G, gh, ldg,
-                _n.ptr(hs_part.contiguous()), G, _n.ptr(c.contiguous()), R, H, _n.ptr(h_out), H, _n.ptr(c_out),
-                _n.ptr(b["ACTS"]), st)
+        if isinstance(x_gates, tuple):  # (word-gate table, word ids): rows read by id, no activations kept
+            xtab, ids = x_gates
+            _n.call("pdvc_lstm_cell_forward_gather_f32", _n.ptr(xtab), xtab.stride(0), _n.ptr(ids.contiguous()),
+                    _n.ptr(b["GATT"]), G, gh, ldg, _n.ptr(hs_part.contiguous()), G, _n.ptr(c.contiguous()), R, H,
+                    _n.ptr(h_out), H, _n.ptr(c_out), None, st)
+        else:
+            xg = x_gates.contiguous()
+            _n.call("pdvc_lstm_cell_forward_f32", _n.ptr(xg), G, _n.ptr(b["GATT"]), G, gh, ldg,
+                    _n.ptr(hs_part.contiguous()), G, _n.ptr(c.contiguous()), R, H, _n.ptr(h_out), H, _n.ptr(c_out),
+                    _n.ptr(b["ACTS"]), st)
         return h_out, c_out
 
     def _gather_softattn(self, b, value, mask_u8, row_video, HP, Ph, off_hs, ref, rd1_rows, lvl, nl, Nv, R, M, D, A,
@@ -593,8 +601,8 @@ class LSTMDSACaptioner(Captioner):
                     it = torch.multinomial(prob, 1, generator=generator)
                     sample_lp = logprobs.gather(1, it)
                     it = it.view(-1)
-            if xtab is not None:
-                x_gates = xtab.index_select(0, it)
+            if xtab is not None:  # read through the word ids by the LSTM cell kernel: no gathered copy
+                x_gates = (xtab, it) if GREEDY_LSTM_GATHER else xtab.index_select(0, it)
             elif fused and GREEDY_GEMM3:
                 x_gates = mm_nt(self.embed(it), w["W_x"])
             else:

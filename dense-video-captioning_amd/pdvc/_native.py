@@ -43,6 +43,8 @@ SIGNATURES = {
     "pdvc_softattn_forward_f32": [_vp, _vp, _i, _vp, _vp, _vp] + [_i] * 4 + [_vp] * 3,
     "pdvc_softattn_backward_f32": [_vp, _vp, _i, _vp, _vp, _vp, _vp] + [_i] * 4 + [_vp, _vp, _i, _vp, _vp, _vp, _vp],
     "pdvc_lstm_cell_forward_f32": [_vp, _i, _vp, _i, _vp, _i, _vp, _i, _vp, _i, _i, _vp, _i, _vp, _vp, _vp],
+    "pdvc_lstm_cell_forward_gather_f32": [_vp, _i, _vp, _vp, _i, _vp, _i, _vp, _i, _vp, _i, _i, _vp, _i, _vp, _vp,
+                                          _vp],
     "pdvc_lstm_cell_backward_f32": [_vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _i, _vp, _vp],
     "pdvc_add_dropout_layernorm_forward_f32": [_vp] * 4 + [_i, _i, _f, _u64, _vp, _f] + [_vp] * 4,
     "pdvc_add_dropout_layernorm_backward_f32": [_vp] * 6 + [_i, _i, _f, _u64] + [_vp] * 8,

@@ -314,6 +314,13 @@ int pdvc_softattn_backward_f32(const float* att, const float* att_h, int ld_att_
 int pdvc_lstm_cell_forward_f32(const float* gates_a, int lda, const float* gates_b, int ldb, const float* gates_c,
                                int ldc, const float* gates_d, int ldd, const float* c_prev, int rows, int hidden, float* h_out, int ld_h_out,
                                float* c_out, float* acts, void* stream);
+/* The same with gates_a read through a row index -- row r adds gates_a[a_rows[r]] (a vocabulary table's rows: the
+ * greedy decode's word gates, LSTM_DSA.py:229-231 embed then W_ih, without a gathered copy) -- and acts optional
+ * (NULL: not written; greedy decoding has no backward). */
+int pdvc_lstm_cell_forward_gather_f32(const float* gates_a, int lda, const int64_t* a_rows, const float* gates_b,
+                                      int ldb, const float* gates_c, int ldc, const float* gates_d, int ldd,
+                                      const float* c_prev, int rows, int hidden, float* h_out, int ld_h_out,
+                                      float* c_out, float* acts, void* stream);
 /* grad_gates (R, ld_grad_gates >= 4H; the first 4H columns written), grad_c_prev (R,H) from grad_h (+ grad_h2
  * if not NULL) and grad_c_next (or NULL). */
 int pdvc_lstm_cell_backward_f32(const float* grad_h, int ld_grad_h, const float* grad_h2, int ld_grad_h2,
