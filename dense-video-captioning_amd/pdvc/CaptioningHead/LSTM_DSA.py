@@ -71,6 +71,11 @@ class _EmbeddingRows(torch.autograd.Function):
         return gw, None
 
 
+def _row_sums_ws(n, cols, device):
+    """The workspace of pdvc_sorted_row_sums_f32: two rows of `cols` floats per 64 sorted positions."""
+    return torch.empty(2 * ((n + 63) // 64) * cols, dtype=torch.float32, device=device)
+
+
 class _WordGates(torch.autograd.Function):
     """xe = W_x embed(idx) for the teacher-forced recurrence (idx (n, R) step-major) with a backward over the
     positions that carry a gradient only: `act` (K,) lists them as flat step-major positions (entries >= n * R are
@@ -101,7 +106,8 @@ class _WordGates(torch.autograd.Function):
             keys, order = torch.sort(torch.where(act >= N, torch.full_like(ids, V), ids), stable=True)
             dT = torch.empty((V, gs.shape[1]), dtype=gs.dtype, device=gs.device)
             _n.call("pdvc_sorted_row_sums_f32", _n.ptr(gs), gs.stride(0), gs.shape[1], _n.ptr(keys), _n.ptr(order),
-                    ids.numel(), V, _n.ptr(dT), dT.stride(0), _n.stream())
+                    ids.numel(), V, _n.ptr(dT), dT.stride(0), _n.ptr(_row_sums_ws(ids.numel(), gs.shape[1], gs.device)),
+                    _n.stream())
             dW_x = mm_wgrad(dT, weight)
             if dW_x is None:
                 dW_x = torch.mm(dT.t(), weight)
@@ -140,7 +146,7 @@ class _WordTable(torch.autograd.Function):
         V, C4 = weight.shape[0], G.shape[1]
         dT = torch.empty((V, C4), dtype=G.dtype, device=G.device)
         _n.call("pdvc_sorted_row_sums_f32", _n.ptr_any(G), G.stride(0), C4, _n.ptr(keys), _n.ptr(order), flat.numel(),
-                V, _n.ptr(dT), C4, _n.stream())
+                V, _n.ptr(dT), C4, _n.ptr(_row_sums_ws(flat.numel(), C4, G.device)), _n.stream())
         dw = mm_dgrad(dT, W_x) if ctx.needs_input_grad[0] else None
         dW_x = None
         if ctx.needs_input_grad[1]:

@@ -96,7 +96,8 @@ SIGNATURES = {
     "pdvc_gemm1p_f32": [_i, _i, _i, _vp, ctypes.c_long, _vp, _vp, ctypes.c_long, _vp, _i, _vp],
     "pdvc_gemm3_f32": [_i, _i, _i, _vp, ctypes.c_long, _i, _vp, ctypes.c_long, _i, _vp, ctypes.c_long, _vp, _i, _i,
                        _vp, _vp],
-    "pdvc_sorted_row_sums_f32": [_vp, ctypes.c_long, _i, _vp, _vp, ctypes.c_long, _i, _vp, ctypes.c_long, _vp],
+    "pdvc_sorted_row_sums_f32": [_vp, ctypes.c_long, _i, _vp, _vp, ctypes.c_long, _i, _vp, ctypes.c_long, _vp,
+                                 _vp],
     "pdvc_gemm3_wgrad_bias_f32": [_i, _i, _i, _vp, ctypes.c_long, _vp, ctypes.c_long, _vp, ctypes.c_long, _i, _i,
                                   _vp, _vp, _vp, _vp],
     "pdvc_mha_forward_f32": [_vp, _vp, _u8p] + [_i] * 4 + [_f, _u64] + [_vp] * 4,
@@ -128,6 +129,8 @@ def lib():
         L.pdvc_mha_workspace_floats.restype = ctypes.c_long
         L.pdvc_ms_deform_attn_workspace_floats.argtypes = [ctypes.c_int] * 5
         L.pdvc_ms_deform_attn_workspace_floats.restype = ctypes.c_size_t
+        L.pdvc_sorted_row_sums_workspace.argtypes = [ctypes.c_long, ctypes.c_int]
+        L.pdvc_sorted_row_sums_workspace.restype = ctypes.c_long
         L.pdvc_last_error.restype = ctypes.c_char_p
         L.pdvc_abi_version.restype = ctypes.c_int
         _lib = L

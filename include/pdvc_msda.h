@@ -607,13 +607,16 @@ int pdvc_gemm3_wgrad_bias_f32(int M, int N, int K, const float* A, long lda, con
                               void* stream);
 
 /* Destination-sorted row sums (csrc/rowsum.hip): dst[v][c] = sum of src[order[j]][c] over the run of j with
- * sorted_keys[j] == v, for v < n_dst and c < cols, in the run's order (deterministic, no atomics; an empty run
- * writes zeros; keys outside [0, n_dst) are ignored).  sorted_keys ascending (n entries), order the positions in
- * that order (a stable sort's permutation).  Replaces the scatter-add (index_add_) of the backward of a row
- * gather -- the caption head's per-batch word-gate table, LSTM_DSA.py:229-231 (embed then W_ih) in the
- * reference.  cols a multiple of 4, src / dst 16-byte aligned, ld / ldd multiples of 4. */
+ * sorted_keys[j] == v, for v < n_dst and c < cols (deterministic: a reduce-by-key over fixed chunks of the sorted
+ * positions, the pieces of a run that crosses chunks added in chunk order; no atomics; an empty run writes zeros;
+ * keys outside [0, n_dst) are ignored).  sorted_keys ascending (n entries), order the positions in that order (a
+ * stable sort's permutation).  workspace: pdvc_sorted_row_sums_workspace(n, cols) floats, 16-byte aligned.
+ * Replaces the scatter-add (index_add_) of the backward of a row gather -- the caption head's per-batch word-gate
+ * table, LSTM_DSA.py:229-231 (embed then W_ih) in the reference.  cols a multiple of 4, src / dst 16-byte aligned,
+ * ld / ldd multiples of 4. */
+long pdvc_sorted_row_sums_workspace(long n, int cols);
 int pdvc_sorted_row_sums_f32(const float* src, long ld, int cols, const int64_t* sorted_keys, const int64_t* order,
-                             long n, int n_dst, float* dst, long ldd, void* stream);
+                             long n, int n_dst, float* dst, long ldd, float* workspace, void* stream);
 
 /* The weight operand split once per call: planes[p][n][k] (bf16 bits, p = 0..2) of opB[n][k] (b_kc 1: B[n*ldb + k],
  * 0: B[k*ldb + n]); K a multiple of 32.  pdvc_gemm3p_f32 then computes C[M,N] (=|+=) sum_k A[m*lda + k] opB[n,k]

@@ -18,22 +18,26 @@ def _row_sums(src, keys_flat, n_dst):
     from pdvc import _native as _n
     keys, order = torch.sort(keys_flat, stable=True)
     dst = torch.full((n_dst, src.shape[1]), float("nan"), device=DEV)
+    ws = torch.full((int(_n.lib().pdvc_sorted_row_sums_workspace(keys_flat.numel(), src.shape[1])) + 4,), float("nan"),
+                    device=DEV)
     _n.call("pdvc_sorted_row_sums_f32", _n.ptr_any(src), src.stride(0), src.shape[1], _n.ptr(keys), _n.ptr(order),
-            keys_flat.numel(), n_dst, _n.ptr(dst), dst.stride(0), _n.stream())
+            keys_flat.numel(), n_dst, _n.ptr(dst), dst.stride(0), _n.ptr(ws), _n.stream())
     return dst
 
 
 @pytest.mark.parametrize("n,cols,n_dst,lead", [(114688, 2048, 5749, 0), (1000, 36, 50, 8), (7, 256, 11, 0),
-                                               (0, 64, 5, 0)])
+                                               (0, 64, 5, 0), (4096, 300, 3, 4), (129, 64, 1, 0)])
 def test_sorted_row_sums_match_index_add(n, cols, n_dst, lead):
     g = torch.Generator(device=DEV).manual_seed(n + cols)
     base = torch.randn(n, cols + lead, device=DEV, generator=g)
     src = base[:, :cols]
     keys = torch.randint(0, n_dst, (n,), device=DEV, generator=g)
+    empty = n >= 1000 and n_dst > 8
     if n >= 1000:
-        keys[: n // 2] = 3                       # one heavy word
+        keys[: n // 2] = min(3, n_dst - 1)       # one heavy word: a run over many 64-position chunks
         keys[n // 2: n // 2 + 5] = n_dst + 4     # out of range: ignored
         keys[n // 2 + 5: n // 2 + 9] = -1
+    if empty:
         keys[keys == 7] = 8                      # an empty run
     dst = _row_sums(src, keys, n_dst)
     ok = (keys >= 0) & (keys < n_dst)
@@ -41,7 +45,7 @@ def test_sorted_row_sums_match_index_add(n, cols, n_dst, lead):
     scale = torch.zeros(n_dst, cols, dtype=torch.float64, device=DEV).index_add_(0, keys[ok], src[ok].double().abs())
     assert not torch.isnan(dst).any(), "every destination row is written"
     assert float(((dst.double() - ref).abs() / scale.clamp_min(1e-30)).max()) < 1e-5
-    if n >= 1000:
+    if empty:
         assert float(dst[7].abs().max()) == 0.0
     assert torch.equal(dst, _row_sums(src, keys, n_dst)), "deterministic"
 
