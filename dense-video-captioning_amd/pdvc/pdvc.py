@@ -26,7 +26,7 @@ from .CaptioningHead.LSTM_DSA import caption_steps
 from .criterion import SetCriterion
 from .deformable_transformer import build_deforamble_transformer
 from .batch_layout import caption_layout, caption_layout_to_device, live_rows, step_ranges
-from .caption_tokens import DeferredLogprobs, LazyProbs, pack_tokens, token_count
+from .caption_tokens import DeferredLogprobs, LazyProbs, RowSelect, pack_tokens, token_count
 from .matcher import LazyIndices, build_matcher
 
 
@@ -492,10 +492,9 @@ class PDVC(nn.Module):
                 tuple(R["last_range"]) if R["last_range"] is not None else last_sel, n_last))
         else:
             if R["last_range"] is not None:
-                last_lp = logprobs.narrow(0, R["last_range"][0], R["last_range"][1])
-            else:
-                last_lp = logprobs.index_select(0, last_sel)
-            probs = {"cap_prob_train": last_lp[:, :n_last]}
+                probs = {"cap_prob_train": logprobs.narrow(0, R["last_range"][0], R["last_range"][1])[:, :n_last]}
+            else:  # a gather of the last layer's rows: formed only if read
+                probs = LazyProbs(cap_prob_train=RowSelect(logprobs, last_sel, n_last))
         out.update({"caption_probs": probs, "seq": seq_rows.index_select(0, last_sel)})
         return out, loss
 
