@@ -413,6 +413,17 @@ def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def freeze_gc():
+    """After warm-up, before the timed steps: the objects alive then (model, buffers, captured graphs) moved out of
+    Python's collector generations (gc.freeze), so a full collection during the timed steps walks only the steps' own
+    garbage -- unfrozen, the eval line paid 70-110 ms for each such collection (2 of 12 steps,
+    profiles/r06_eval_gc_freeze_ab.txt).  PDVC_GC_FREEZE=0 leaves the collector as it is."""
+    if os.environ.get("PDVC_GC_FREEZE", "1") != "0":
+        import gc
+        gc.collect()
+        gc.freeze()
+
+
 def eval_main(a):
     """Evaluation throughput: forward with greedy captions for all Q queries (LSTM_DSA.py:118-186, the loop stops
     when every row has finished: tested on the device, read back a few steps late, the decode cut at the reference's
@@ -450,6 +461,7 @@ def eval_main(a):
         step()
     post.drain()
     torch.cuda.synchronize()
+    freeze_gc()
     # every step timed on its own: host wall time (the greedy loop checks for finished rows on the host once per
     # decode step, LSTM_DSA.py:172-179) beside the device time between two events on the step's stream, so a slow
     # step is attributed to the host (wall >> device) or to the device
@@ -655,6 +667,7 @@ def main():
     log(f"{B} videos/GPU, {world} rank(s): warm-up")
     for _ in range(a.warmup):
         step()
+    freeze_gc()
     log("timed steps")
     names = ["pdvc_msda1d_forward_f32", "pdvc_msda1d_backward_ex_f32", "pdvc_cap_gather_forward_f32",
              "pdvc_cap_gather_backward_f32", "pdvc_cap_gather_backward2_f32", "pdvc_cap_softattn_forward_f32", "pdvc_cap_softattn_backward_f32",
