@@ -67,23 +67,26 @@ def test_logprob_pick_bad_target_poisons_and_empty_rows():
     assert logp.shape == (0, 3, 16) and picked.shape == (0, 3)
 
 
-@pytest.mark.parametrize("V", [5749, 1609, 37, 8192, 9000])
-def test_logprob_argmax_matches_torch(V):
+@pytest.mark.parametrize("off", [0, 1])
+@pytest.mark.parametrize("V", [5749, 1609, 37, 8192, 9000, 3, 4])
+def test_logprob_argmax_matches_torch(V, off):
     """pdvc_logprob_argmax_f32 (greedy decoding's word choice, LSTM_DSA.py:149-151) against torch.max over
     log_softmax: identical indices (ties to the first maximal index, rows with repeated maxima included), the
-    log-probabilities within 1e-5; the register-resident kernel (V <= 8 192) and the streaming one (9 000)."""
+    log-probabilities within 1e-5; the register-resident kernel (V <= 8 192) and the streaming one (9 000), V = 3 and
+    4, logits 16-byte aligned or not (off)."""
     from pdvc import _native as _n
     torch.manual_seed(V)
     R = 300
-    x = torch.randn(R, V, device="cuda") * 3
+    x = (torch.randn(R * V + off, device="cuda") * 3)[off:].view(R, V)
     x[5, :] = 0.25                      # all tied: index 0
     x[6, V // 2] = x[6].max() + 1.0     # a clear winner in the middle
     x[7, V - 1] = x[7].max() + 1.0      # ... at the end
-    x[8, 3] = x[8, V - 2] = x[8].max() + 2.0  # tie between two entries: the first
+    if V > 4:
+        x[8, 3] = x[8, V - 2] = x[8].max() + 2.0  # tie between two entries: the first
     want_lp, want_i = torch.max(torch.log_softmax(x, 1), 1)
     idx = torch.empty(R, dtype=torch.long, device="cuda")
     lp = torch.empty(R, device="cuda")
-    _n.call("pdvc_logprob_argmax_f32", _n.ptr(x), R, V, _n.ptr(idx), _n.ptr(lp), _n.stream())
+    _n.call("pdvc_logprob_argmax_f32", _n.ptr_any(x), R, V, _n.ptr(idx), _n.ptr(lp), _n.stream())
     assert torch.equal(idx, want_i)
     assert (lp - want_lp).abs().max().item() <= 1e-5
 
