@@ -19,6 +19,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--videos", type=int, default=256)
     ap.add_argument("--top", type=int, default=50)
+    ap.add_argument("--bf16", action="store_true", help="the yc2_tsp_bf16 workload: cfgs/yc2_tsp_pdvc.yml, T=256, "
+                    "8 events x 9 words, every GEMM on bf16 operands (pdvc/precision.py)")
     a = ap.parse_args()
     import opts
     from pdvc import gemm_tuning
@@ -26,20 +28,23 @@ def main():
     from pdvc.pdvc import build
     gemm_tuning.enable()
     torch.manual_seed(0)
-    args = opts.parse_opts(["--cfg_path", "cfgs/anet_tsp_pdvc.yml", "--device", "cuda"], cfg_root=PKG,
+    cfg, T, E, W = ("cfgs/yc2_tsp_pdvc.yml", 256, 8, 9) if a.bf16 else ("cfgs/anet_tsp_pdvc.yml", 512, 4, 13)
+    args = opts.parse_opts(["--cfg_path", cfg, "--device", "cuda"], cfg_root=PKG,
                            feature_dim=768, num_queries=100, frame_embedding_num=512)
     model, criterion, _ = build(args)
     model = model.cuda().train()
-    dt = to_device(collate(synthetic_videos(a.videos, 512, 768, 4, 13, args.vocab_size + 1, seed=1000)), "cuda")
+    dt = to_device(collate(synthetic_videos(a.videos, T, 768, E, W, args.vocab_size + 1, seed=1000)), "cuda")
+    from pdvc.precision import bf16_matmul
     params = [p for p in model.parameters() if p.requires_grad]
     opt = torch.optim.AdamW(params, lr=args.lr, weight_decay=args.weight_decay, fused=True)
     wd = criterion.weight_dict
 
     def step():
-        out, loss = model(dt, criterion, "queries")
-        total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
-        opt.zero_grad(set_to_none=True)
-        total.backward()
+        with bf16_matmul(a.bf16):
+            out, loss = model(dt, criterion, "queries")
+            total = sum(loss[k] * wd[k] for k in loss.keys() if k in wd)
+            opt.zero_grad(set_to_none=True)
+            total.backward()
         torch.nn.utils.clip_grad_norm_(params, args.grad_clip)
         opt.step()
 
