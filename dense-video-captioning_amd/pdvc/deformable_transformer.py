@@ -9,6 +9,7 @@ host read-back of `temporal_shapes` (the reference's `assert spatial_shapes.sum(
 """
 import copy
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -126,8 +127,12 @@ class DeformableTransformer(nn.Module):
         # the Q reference points are the same for every video: one (Q, d) x (d, 1) product, then broadcast
         # (the reference applies the Linear to the expanded (bs, Q, d) tensor: the same values, bs times the work)
         reference_points = self.reference_points(query_embed).sigmoid().unsqueeze(0).expand(bs, -1, -1).contiguous()
+        pos_rows, tgt_rows = query_embed, tgt
         query_embed = query_embed.unsqueeze(0).expand(bs, -1, -1)
         tgt = tgt.unsqueeze(0).expand(bs, -1, -1)
+        # the (Q, d) rows every video repeats, for the first decoder layer's in_proj (see _shared_rows)
+        query_embed.__dict__["_pdvc_rows"] = pos_rows
+        tgt.__dict__["_pdvc_rows"] = tgt_rows
         return reference_points, tgt, reference_points, query_embed
 
     def prepare_decoder_input_proposal(self, gt_reference_points):
@@ -220,6 +225,17 @@ class DeformableTransformerEncoder(nn.Module):
         return output
 
 
+# The first decoder layer's self-attention input is the same Q query rows for every video (tgt and query_pos are
+# prepare_decoder_input_query's expands): its in_proj runs on the Q rows once and the products are broadcast, where
+# the reference projects the bs x Q expanded rows (the same values, bs times the work, forward and backward).
+SHARED_QUERY_ROWS = os.environ.get("PDVC_SHARED_QUERY_ROWS", "1") != "0"
+
+
+def _shared_rows(t):
+    """The (Q, d) rows a decoder input repeats for every video (prepare_decoder_input_query), or None."""
+    return None if t is None else t.__dict__.get("_pdvc_rows")
+
+
 class QuerySelfAttention(nn.Module):
     """nn.MultiheadAttention(d_model, n_heads, dropout) with identical parameters (in_proj_weight,
     in_proj_bias, out_proj) and forward semantics for the decoder's (batch-first) use; the attention core
@@ -238,9 +254,10 @@ class QuerySelfAttention(nn.Module):
         constant_(self.in_proj_bias, 0.)
         constant_(self.out_proj.bias, 0.)
 
-    def forward(self, qk_in, v_in, key_padding_mask=None):
+    def forward(self, qk_in, v_in, key_padding_mask=None, batch=None):
         """qk_in (N, Q, E) = tgt + query_pos (query and key input); v_in (N, Q, E) = tgt;
-        key_padding_mask (N, Q) True = ignore.  Returns (N, Q, E)."""
+        key_padding_mask (N, Q) True = ignore.  Returns (N, Q, E).  batch: qk_in and v_in are (Q, E) rows shared
+        by `batch` videos (projected once, the products broadcast to (batch, Q, *))."""
         E = self.embed_dim
         w, b = self.in_proj_weight, self.in_proj_bias
         if qk_in.is_cuda and qk_in.dtype == torch.float32 and _lin.BACKEND != "hip":
@@ -249,6 +266,9 @@ class QuerySelfAttention(nn.Module):
         else:
             qk = dense(qk_in, w[:2 * E], b[:2 * E])
             v = dense(v_in, w[2 * E:], b[2 * E:])
+        if batch is not None:
+            qk = qk.unsqueeze(0).expand(batch, -1, -1).contiguous()
+            v = v.unsqueeze(0).expand(batch, -1, -1).contiguous()
         p = self.dropout if self.training else 0.0
         out = query_self_attention(qk, v, key_padding_mask, self.num_heads, p)
         return self.out_proj(out)
@@ -286,9 +306,12 @@ class DeformableTransformerDecoderLayer(nn.Module):
 
     def forward(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,
                 src_padding_mask=None, query_mask=None):
-        q = self.with_pos_embed(tgt, query_pos)
         kpm = None if query_mask is None else ~query_mask
-        tgt2 = self.self_attn(q, tgt, key_padding_mask=kpm)
+        t_rows, p_rows = _shared_rows(tgt), _shared_rows(query_pos)
+        if SHARED_QUERY_ROWS and t_rows is not None and p_rows is not None:
+            tgt2 = self.self_attn(t_rows + p_rows, t_rows, key_padding_mask=kpm, batch=tgt.shape[0])
+        else:
+            tgt2 = self.self_attn(self.with_pos_embed(tgt, query_pos), tgt, key_padding_mask=kpm)
         tgt = add_dropout_layernorm(tgt, tgt2, self.norm2, self.dropout2.p, self.training)
         tgt2 = self.cross_attn(self.with_pos_embed(tgt, query_pos), reference_points, src, src_temporal_shapes,
                                level_start_index, src_padding_mask)

@@ -230,6 +230,43 @@ def test_decoder_layer_vs_golden():
         close(p.grad, d["grad." + n], 1e-4, n)
 
 
+def test_decoder_layer_shared_query_rows_match_the_expanded_rows():
+    """The first decoder layer's in_proj over the Q query rows every video repeats (prepare_decoder_input_query's
+    expands, tagged with their (Q, d) rows): projected once and broadcast, against the same layer on materialised
+    (N, Q, d) copies of the rows -- output, the rows' gradients (summed over the videos by the expand) and every
+    parameter gradient."""
+    from pdvc.deformable_transformer import DeformableTransformerDecoderLayer
+    d = load("module_decoder_layer")
+    layer = DeformableTransformerDecoderLayer(64, 48, 0.0, "relu", 4, 4, 4).to(DEV)
+    fill(layer)
+    T_l = tuple(int(t) for t in d["T_l"])
+    lsi = torch.tensor([0, 16, 24, 28], device=DEV)
+    ref, src = cu(d["ref"]), cu(d["src"])
+    N, Q, C = d["tgt"].shape
+    torch.manual_seed(11)
+    rows = [torch.randn(Q, C, device=DEV) for _ in range(2)]
+    g = torch.randn(N, Q, C, device=DEV)
+    seen = []
+    fwd = layer.self_attn.forward
+    layer.self_attn.forward = lambda *a, **k: (seen.append(k.get("batch")), fwd(*a, **k))[1]
+    results = []
+    for shared in (True, False):
+        layer.zero_grad()
+        t_rows, p_rows = (r.clone().requires_grad_() for r in rows)
+        tgt, pos = (r.unsqueeze(0).expand(N, -1, -1) for r in (t_rows, p_rows))
+        if shared:
+            tgt.__dict__["_pdvc_rows"], pos.__dict__["_pdvc_rows"] = t_rows, p_rows
+        else:
+            tgt, pos = tgt.contiguous(), pos.contiguous()
+        out = layer(tgt, pos, ref, src, T_l, lsi, cu(d["pad"]), cu(d["query_mask"]))
+        out.backward(g)
+        results.append([out, t_rows.grad, p_rows.grad] + [p.grad.clone() for p in layer.parameters()])
+    assert seen == [N, None]
+    names = ["out", "grad tgt rows", "grad pos rows"] + [n for n, _ in layer.named_parameters()]
+    for name, a, b in zip(names, *results):
+        close(a, b, 1e-5, name)
+
+
 def test_decoder_layer_parameters_named_like_nn_multiheadattention():
     from pdvc.deformable_transformer import DeformableTransformerDecoderLayer
     names = [n for n, _ in DeformableTransformerDecoderLayer(64, 48, 0.0, "relu", 4, 4, 4).named_parameters()]
