@@ -2483,8 +2483,10 @@ static int msda1d_backward_impl(const float* value, const uint8_t* value_pad_mas
         for (int l = 0; l < kL; ++l) Tm = lv.T[l] > Tm ? lv.T[l] : Tm;
         const bool g4ok = head_dim == 64 && value_g4() && (long)num_query * num_heads * head_dim * 4 < (1L << 31) &&
                           num_query < 65536 && Tm < 65535;
-        if (bq_blocks <= 0 || !g4ok || proj_stride != 2 * NSM || (uintptr_t)gv16 % 8 || (uintptr_t)gp16 % 2)
-            return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "bf16 gradients only on the encoder's pyramid path");
+        // grad_proj's rounding needs the encoder's pyramid backward-query kernel; grad_value's alone (gp16 null: the
+        // decoder's cross-attention, whose query side runs the dot kernel) only the 16-lane value walk
+        if (!g4ok || (uintptr_t)gv16 % 8 || (gp16 && (bq_blocks <= 0 || proj_stride != 2 * NSM || (uintptr_t)gp16 % 2)))
+            return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "bf16 gradients: grad_proj's only on the encoder's pyramid path");
     }
     if (bq_blocks > 0) {
         if ((rc = bwdq_pyr_attrs())) return rc;
@@ -2652,7 +2654,7 @@ extern "C" int pdvc_msda1d_backward_ex_f32_bf16out(const float* value, const uin
                                                    float* grad_value, float* grad_proj, float* grad_ref,
                                                    float* grad_value_level_sums, uint16_t* grad_value16,
                                                    uint16_t* grad_proj16, void* stream) {
-    PDVC_CHECK_ARG(grad_value16 != nullptr && grad_proj16 != nullptr, "both bf16 buffers are required");
+    PDVC_CHECK_ARG(grad_value16 != nullptr, "grad_value16 is required (grad_proj16 may be null)");
     return msda1d_backward_impl(value, value_pad_mask, ref, ref_dim, proj, proj_stride, off_base, logit_base, level_T,
                                 num_levels, batch, num_query, num_heads, head_dim, num_point, grad_output, output,
                                 save_attn, save_loc, grad_value, grad_proj, grad_ref, grad_value_level_sums,

@@ -215,6 +215,41 @@ class PackedLinearFunction(Function):
         return (gw, gb, None) + tuple(gxs)
 
 
+def tag_relu_masked(g, y):
+    """Mark g (a gradient w.r.t. the ReLU output y) as already masked by y > 0 -- the data-gradient GEMM that made it
+    applied the mask in its epilogue -- so y's producer skips its threshold_backward pass.  Tagged with g's version
+    counter like tag_level_sums: a gradient autograd later accumulates into in place loses the tag."""
+    g._pdvc_relu_masked = (y, g._version)
+    return g
+
+
+def relu_masked(g, y):
+    """Whether g carries tag_relu_masked for exactly this ReLU output y and is unchanged since."""
+    ent = getattr(g, "_pdvc_relu_masked", None)
+    return (ent is not None and ent[1] == g._version and ent[0].data_ptr() == y.data_ptr()
+            and ent[0].shape == y.shape and g.shape[-1] == y.shape[-1])
+
+
+def tag_colsum(g, sums):
+    """Hand g's column sums (the consuming layer's bias gradient), formed by the kernel that wrote g, to that layer's
+    backward (TorchLinearFunction), tagged with g's version counter like tag_level_sums."""
+    g._pdvc_colsum = (sums, g._version)
+    return g
+
+
+def colsum_of(g):
+    """The column sums tag_colsum attached to g, or None when absent or stale."""
+    ent = getattr(g, "_pdvc_colsum", None)
+    if ent is None or ent[1] != g._version or ent[0].shape != (g.shape[-1],):
+        return None
+    return ent[0]
+
+
+# the box MLP's ReLU backward in the next layer's data-gradient epilogue (pdvc_gemm3p_dmask_f32 with p = 0: hd > 0 ?
+# g : 0, bit for bit threshold_backward) instead of a pass over (rows, O); PDVC_RELU_DMASK=0 is the A/B switch
+_RELU_DMASK = os.environ.get("PDVC_RELU_DMASK", "1") != "0"
+
+
 class TorchLinearFunction(Function):
     """nn.Linear (+ fused ReLU) on hipBLASLt with a split-K weight gradient (see wgrad_splits)."""
 
@@ -231,22 +266,39 @@ class TorchLinearFunction(Function):
             y = addmm_nt(bias, x2, weight)
             if relu:
                 y.relu_()
-        ctx.save_for_backward(x2, weight, y if relu else None)
+        # x is the output of another ReLU layer of this kind: the input gradient can be masked in its GEMM epilogue
+        relu_in = x.__dict__.get("_pdvc_relu_out")
+        ctx.save_for_backward(x2, weight, y if relu else None, relu_in)
         ctx.has_bias = bias is not None
-        return y.view(*shape[:-1], weight.shape[0])
+        out = y.view(*shape[:-1], weight.shape[0])
+        if relu:
+            out.__dict__["_pdvc_relu_out"] = y  # (the saved y: its backward checks the tag against it)
+        return out
 
     @staticmethod
     def backward(ctx, gy):
-        x2, weight, y = ctx.saved_tensors
+        x2, weight, y, relu_in = ctx.saved_tensors
         O = weight.shape[0]
         gy2 = gy.reshape(-1, O)
-        if y is not None:
+        if y is not None and not relu_masked(gy, y):
             gy2 = torch.ops.aten.threshold_backward(gy2, y, 0.0)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = mm_dgrad(gy2, weight).view(*gy.shape[:-1], weight.shape[1])
+            gx = None
+            if _RELU_DMASK and relu_in is not None and relu_in.shape == (gy2.shape[0], weight.shape[1]):
+                from .gemm3 import mm_dgrad_dmask
+                gx = mm_dgrad_dmask(gy2.contiguous(), weight, relu_in, 0.0)
+                if gx is not None:
+                    gx = tag_relu_masked(gx.view(*gy.shape[:-1], weight.shape[1]), relu_in)
+            if gx is None:
+                gx = mm_dgrad(gy2, weight).view(*gy.shape[:-1], weight.shape[1])
         want_gb = ctx.has_bias and ctx.needs_input_grad[2]
-        if ctx.needs_input_grad[1]:
+        cs = colsum_of(gy) if want_gb and y is None else None  # summed by the kernel that wrote gy (bf16 mode logits)
+        if cs is not None:
+            gb = cs
+            if ctx.needs_input_grad[1]:
+                gw = wgrad_mm(gy2, x2)
+        elif ctx.needs_input_grad[1]:
             gb = gy2.new_empty(O) if want_gb else None
             gw = wgrad_mm(gy2, x2, db=gb)  # (the bias gradient from the same pass over gy)
         elif want_gb:

@@ -130,6 +130,10 @@ def msda1d_forward(value, pad_mask, proj, ref, level_T, off_base, logit_base, sa
 _DELTA_FROM_OUT = os.environ.get("PDVC_MSDA_DELTA_OUT", "0") == "1"
 
 
+# bf16 mode: the decoder's value gradient written with its bf16 rounding too (PDVC_MSDA_DEC_BF16OUT=0: cast pass, A/B)
+_DEC_BF16OUT = os.environ.get("PDVC_MSDA_DEC_BF16OUT", "1") != "0"
+
+
 def msda1d_backward(value, pad_mask, proj, ref, save_attn, save_loc, out, grad_out, level_T, off_base, logit_base,
                     need_ref=False, level_sums=False):
     """pdvc_msda1d_backward_ex_f32: returns (grad_value, grad_proj, grad_ref or None), plus with `level_sums` the
@@ -148,9 +152,11 @@ def msda1d_backward(value, pad_mask, proj, ref, save_attn, save_loc, out, grad_o
             _n.ptr(save_loc), _n.ptr(gv), _n.ptr(gp), _n.ptr(gr), _n.ptr(ls))
     meta = (N, Lq, S, M, D, NUM_SAMPLES)
     done = False
-    gv16 = shadow_for(gv) if Lq == S else None  # bf16 mode, encoder: the projections' gradient-GEMM operands
+    # bf16 mode: the projections' gradient-GEMM operands written beside the gradients -- grad_value's everywhere (the
+    # decoder's cross-attention value gradient feeds the memory projections' GEMMs), grad_proj's on the encoder
+    gv16 = shadow_for(gv) if (Lq == S or _DEC_BF16OUT) else None
     if gv16 is not None:
-        gp16 = shadow_for(gp)
+        gp16 = shadow_for(gp) if Lq == S else None
         try:
             _n.call("pdvc_msda1d_backward_ex_f32_bf16out", *args, _n.ptr(gv16), _n.ptr(gp16), _n.stream(), meta=meta)
             attach_bf16(gv, gv16)

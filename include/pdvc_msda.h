@@ -186,9 +186,10 @@ int pdvc_msda1d_backward_ex_f32(const float* value, const uint8_t* value_pad_mas
                                 const float* save_attn, const float* save_loc, float* grad_value, float* grad_proj,
                                 float* grad_ref, float* grad_value_level_sums, void* stream);
 /* bf16 mode (pdvc/precision.py): the same passes, also writing the bf16 roundings (torch's RNE cast) of output /
- * grad_value / grad_proj, the operands of the projections' GEMMs -- only on the encoder's pyramid path (Lq = S,
- * head_dim 64, level 0 <= 512 positions; the backward also needs proj_stride = 2 * num_heads * 16); any other
- * call returns PDVC_ERR_UNSUPPORTED before launching anything. */
+ * grad_value / grad_proj, the operands of the projections' GEMMs -- output16 and grad_proj16 only on the encoder's
+ * pyramid path (Lq = S, head_dim 64, level 0 <= 512 positions; grad_proj16 also needs proj_stride = 2 * num_heads *
+ * 16); grad_value16 alone (grad_proj16 NULL: the decoder's cross-attention) wherever head_dim is 64 and the levels
+ * are shorter than 65 535 positions.  Any other call returns PDVC_ERR_UNSUPPORTED before launching anything. */
 int pdvc_msda1d_forward_f32_bf16out(const float* value, const uint8_t* value_pad_mask, const float* proj,
                                     int proj_stride, int off_base, int logit_base, const float* ref, int ref_dim,
                                     const int32_t* level_T, int num_levels, int batch, int num_query, int num_heads,
@@ -554,6 +555,13 @@ int pdvc_logprob_pick_backward_ld_f32(const float* logp, const int64_t* target, 
  * and nothing is launched). */
 int pdvc_logprob_pick_backward_f32_bf16out(const float* logp, const int64_t* target, const float* grad_picked,
                                            int rows, int V, float* grad_logits, uint16_t* grad16, void* stream);
+/* The same plus column partials of grad_logits for the logit layer's bias gradient (its column sum): col_parts
+ * (parts, V), 1 <= parts <= rows, row i = the sum of grad_logits' rows i, i + parts, i + 2 parts, ... (fixed order:
+ * deterministic).  Replaces the bias gradient's column-sum pass over the (rows, V) gradient in the bf16 mode
+ * (reference: the logit nn.Linear's bias gradient, LSTM_DSA.py:112-116). */
+int pdvc_logprob_pick_backward_f32_bf16out_colparts(const float* logp, const int64_t* target,
+                                                    const float* grad_picked, int rows, int V, float* grad_logits,
+                                                    uint16_t* grad16, int parts, float* col_parts, void* stream);
 /* greedy decoding's word choice (LSTM_DSA.py:149-151, torch.max over log_softmax(logits)): index[r] = the first index
  * of the largest logit of row r, logp_max[r] = its log-probability (x_max - max) - log(sum exp(x - max)); one read
  * of the logits, the (rows, V) log-probabilities are not written. */

@@ -465,3 +465,103 @@ def test_cfg2_bf16_step_with_producer_shadows_equals_cast_passes():
         assert (r is None) == (g1[n] is None), n
         if r is not None:
             assert rel(g1[n], r) <= bound, f"grad {n}: {rel(g1[n], r):.2e} relative, run-to-run noise {noise:.2e}"
+
+
+def test_msda_bf16out_decoder_grad_value_only():
+    """The decoder's cross-attention shape (Lq = 100 queries on a T = 256 pyramid, the dot backward-query kernel):
+    pdvc_msda1d_backward_ex_f32_bf16out with grad_proj16 NULL writes grad_value's bf16 rounding bit for bit beside the
+    same fp32 gradients as the plain form; asking for grad_proj16 there is refused with nothing launched."""
+    from pdvc import _native as _n
+    from pdvc.ops.functions.ms_deform_attn_func import NUM_SAMPLES, _levels
+    g = torch.Generator(device=DEV).manual_seed(6)
+    T_l = (256, 128, 64, 32)
+    N, S, M, D, Lq = 3, sum(T_l), 8, 64, 100
+    lvl, nl = _levels(T_l)
+    value = torch.randn(N, S, M, D, device=DEV, generator=g)
+    proj = torch.cat([torch.randn(N, Lq, M * 16, device=DEV, generator=g) * 2,
+                      torch.randn(N, Lq, M * 16, device=DEV, generator=g)], -1).contiguous()
+    ref = torch.rand(N, Lq, 1, 2, device=DEV, generator=g).expand(N, Lq, 4, 2).contiguous() * 0.8 + 0.1
+    C = proj.shape[2]
+    out = torch.empty(N, Lq, M * D, device=DEV)
+    sa = torch.empty(N, M, nl, Lq, NUM_SAMPLES // nl, device=DEV)
+    sl = torch.empty_like(sa)
+    _n.call("pdvc_msda1d_forward_f32", _n.ptr(value), None, _n.ptr(proj), C, 0, M * 16, _n.ptr(ref), 2, lvl, nl, N, Lq,
+            M, D, NUM_SAMPLES // nl, _n.ptr(out), _n.ptr(sa), _n.ptr(sl), _n.stream())
+    gout = torch.randn(N, Lq, M * D, device=DEV, generator=g)
+
+    def bwd(bf, gp16=None):
+        gv = torch.empty_like(value)
+        gp = torch.empty_like(proj)
+        a = (_n.ptr(value), None, _n.ptr(ref), 2, _n.ptr(proj), C, 0, M * 16, lvl, nl, N, Lq, M, D, NUM_SAMPLES // nl,
+             _n.ptr(gout), None, _n.ptr(sa), _n.ptr(sl), _n.ptr(gv), _n.ptr(gp), None, None)
+        gv16 = torch.empty(gv.shape, device=DEV, dtype=torch.bfloat16)
+        if bf:
+            _n.call("pdvc_msda1d_backward_ex_f32_bf16out", *a, _n.ptr(gv16), _n.ptr(gp16), _n.stream())
+        else:
+            _n.call("pdvc_msda1d_backward_ex_f32", *a, _n.stream())
+        return gv, gp, gv16
+
+    gv0, gp0, _ = bwd(False)
+    gv1, gp1, gv16 = bwd(True)
+    assert (gv1 - gv0).abs().max().item() <= 1e-6 * gv0.abs().max().item()
+    assert (gp1 - gp0).abs().max().item() <= 1e-5 * gp0.abs().max().item()
+    assert torch.equal(_bits(gv16), _bits(gv1.to(torch.bfloat16)))
+    with pytest.raises(_n.NativeError):
+        bwd(True, torch.empty(proj.shape, device=DEV, dtype=torch.bfloat16))
+
+
+@pytest.mark.parametrize("rows,parts", [(9000, 2048), (333, 333), (5000, 7)])
+def test_logprob_backward_colparts_sum_to_the_bias_gradient(rows, parts):
+    """pdvc_logprob_pick_backward_f32_bf16out_colparts: grad_logits and its bf16 rounding bit for bit as the
+    bf16out form, and column partials whose column sum is grad_logits.sum(0) (the logit layer's bias gradient) to
+    fp32 summation accuracy -- the partials in a fixed order, identical across two calls."""
+    from pdvc import _native as _n
+    g = torch.Generator(device=DEV).manual_seed(11)
+    V = 5748
+    logp = torch.log_softmax(torch.randn(rows, V, device=DEV, generator=g) * 4, -1).contiguous()
+    tgt = torch.randint(0, V, (rows,), device=DEV, generator=g)
+    gp = torch.randn(rows, device=DEV, generator=g)
+    ref = torch.empty_like(logp)
+    r16 = torch.empty(rows, V, device=DEV, dtype=torch.bfloat16)
+    _n.call("pdvc_logprob_pick_backward_f32_bf16out", _n.ptr(logp), _n.ptr(tgt), _n.ptr(gp), rows, V, _n.ptr(ref),
+            _n.ptr(r16), _n.stream())
+    outs = []
+    for _ in range(2):
+        got = torch.empty_like(logp)
+        g16 = torch.empty(rows, V, device=DEV, dtype=torch.bfloat16)
+        cp = torch.empty(parts, V, device=DEV)
+        _n.call("pdvc_logprob_pick_backward_f32_bf16out_colparts", _n.ptr(logp), _n.ptr(tgt), _n.ptr(gp), rows, V,
+                _n.ptr(got), _n.ptr(g16), parts, _n.ptr(cp), _n.stream())
+        assert torch.equal(got, ref) and torch.equal(_bits(g16), _bits(r16))
+        outs.append(cp)
+    assert torch.equal(outs[0], outs[1])
+    want = ref.double().sum(0)
+    scale = ref.double().abs().sum(0).clamp_min(1e-30)
+    assert float(((outs[0].double().sum(0) - want).abs() / scale).max()) < 1e-5
+    with pytest.raises(_n.NativeError):
+        _n.call("pdvc_logprob_pick_backward_f32_bf16out_colparts", _n.ptr(logp), _n.ptr(tgt), _n.ptr(gp), rows, V,
+                _n.ptr(got), _n.ptr(g16), rows + 1, _n.ptr(cp), _n.stream())
+
+
+def test_logit_layer_bias_gradient_from_colparts(monkeypatch):
+    """The bf16 mode's caption logit layer (Linear -> logprob_pick): with the column partials the layer's bias
+    gradient comes from the logprob backward (tagged hand-over, no column-sum pass) and equals the column-sum path's
+    to fp32 summation accuracy; every other gradient is bit-identical."""
+    import pdvc.ops.functions.logprob as LP
+    from pdvc.ops.functions.linear import dense
+    from pdvc.precision import bf16_matmul
+    torch.manual_seed(2)
+    rows, H, V = 9000, 512, 5748
+    x = torch.randn(rows, H, device=DEV)
+    lin = torch.nn.Linear(H, V).to(DEV)
+    tgt = torch.randint(0, V, (rows,), device=DEV)
+    res = []
+    for on in (True, False):
+        monkeypatch.setattr(LP, "COLPARTS", on)
+        xa = x.clone().requires_grad_()
+        with bf16_matmul():
+            _, picked = LP.logprob_pick(dense(xa, lin.weight, lin.bias), tgt)
+            res.append(torch.autograd.grad(picked.sum(), [xa, lin.weight, lin.bias]))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    db, ref = res[0][2].double(), res[1][2].double()
+    assert float((db - ref).abs().max()) <= 1e-5 * float(ref.abs().max())

@@ -421,3 +421,38 @@ def test_addmm_generic_tile_when_gemm3p_waves_are_ragged(monkeypatch):
             ref = ref.clamp_min(0)
         scale = x.double().abs() @ W.double().abs().t() + b.double().abs()
         assert scaled_err(y, ref, scale) < 1e-6
+
+
+@pytest.mark.parametrize("consumers", [1, 2])
+def test_relu_mask_in_next_layers_dgrad_epilogue_is_bit_identical(monkeypatch, consumers):
+    """The box MLP (pdvc.py MLP: Linear-ReLU-Linear-ReLU-Linear through TorchLinearFunction): a ReLU layer's backward
+    mask (threshold_backward) taken by the next layer's data-gradient epilogue (pdvc_gemm3p_dmask_f32, p = 0) and
+    handed over as a tagged gradient (linear.py tag_relu_masked) against the separate threshold_backward passes --
+    bit-identical output and gradients.  consumers = 2: the ReLU output also feeds a second product, so autograd
+    sums the two gradients and the producer must mask that sum itself (the tag does not survive the sum)."""
+    _on_gemm3(monkeypatch)
+    import pdvc.ops.functions.linear as L
+    torch.manual_seed(5)
+    rows, d = 3000, 256
+    x = torch.randn(rows, d, device=DEV)
+    lins = [torch.nn.Linear(d, d).to(DEV), torch.nn.Linear(d, d).to(DEV), torch.nn.Linear(d, 64).to(DEV)]
+    extra = torch.nn.Linear(d, 32).to(DEV)
+    params = [p for lin in lins + [extra] for p in (lin.weight, lin.bias)]
+    g = torch.randn(rows, 64, device=DEV)
+    g2 = torch.randn(rows, 32, device=DEV)
+    res = []
+    for fuse in (True, False):
+        monkeypatch.setattr(L, "_RELU_DMASK", fuse)
+        xa = x.clone().requires_grad_()
+        h = L.dense(xa, lins[0].weight, lins[0].bias, relu=True)
+        h = L.dense(h, lins[1].weight, lins[1].bias, relu=True)
+        out = L.dense(h, lins[2].weight, lins[2].bias)
+        outs, gs = [out], [g]
+        if consumers == 2:
+            outs.append(L.dense(h, extra.weight, extra.bias))
+            gs.append(g2)
+        used = [xa] + params[:6] + (params[6:] if consumers == 2 else [])
+        res.append([out.detach()] + list(torch.autograd.grad(outs, used, gs)))
+    for i, (a, b) in enumerate(zip(*res)):
+        assert torch.equal(a, b), f"tensor {i} differs between the epilogue mask and threshold_backward"
+    assert float(res[0][1].abs().max()) > 0

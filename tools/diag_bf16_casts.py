@@ -33,8 +33,26 @@ def main():
     vocab = args.vocab_size + 1
     dt = to_device(collate(synthetic_videos(videos, a.T, a.C, a.events, a.words, vocab, seed=1000)), dev)
     wd = criterion.weight_dict
+    # the column-sum passes (bias gradients) the step makes, by call site: in the bf16 mode gemm3w's fused bias sums
+    # are off, so every bias gradient not summed by a producing kernel is a pass of its own
+    from pdvc import _native as _n
+    colsums = []
+    real_call = _n.call
+
+    def call(name, *a, **kw):
+        if name == "pdvc_colsum_f32" and P.CAST_LOG is not None:
+            f, where = sys._getframe(1), []
+            while f is not None and len(where) < 3:
+                fn = f.f_code.co_filename
+                if "/torch/" not in fn and fn != __file__:
+                    where.append(f"{os.path.basename(fn)}:{f.f_lineno} {f.f_code.co_name}")
+                f = f.f_back
+            colsums.append(((a[1], a[2]), " < ".join(where) or "autograd"))
+        return real_call(name, *a, **kw)
+    _n.call = call
     for step in range(2):  # the first step warms lazy state; the second is logged
         P.CAST_LOG.clear()
+        colsums.clear()
         P.STATS_CAST[:] = [0, 0, 0]
         with P.bf16_matmul():
             _, loss = model(dt, criterion, "queries")
@@ -59,7 +77,16 @@ def main():
     print(f"{'MB@1024':>9} {'n':>3}  shape  <- where")
     for (where, shape), (cnt, b) in rows:
         print(f"{b * scale / 1e6:9.1f} {cnt:3d}  {shape}  <- {where}")
+    cs = {}
+    for shape, where in colsums:
+        g = cs.setdefault((where, shape), [0, 0])
+        g[0] += 1
+        g[1] += shape[0] * shape[1] * 4
+    print(f"column-sum passes: {len(colsums)}")
+    for (where, shape), (cnt, b) in sorted(cs.items(), key=lambda kv: -kv[1][1]):
+        print(f"{b * scale / 1e6:9.1f} {cnt:3d}  {shape}  <- {where}")
 
 
 if __name__ == "__main__":
     main()
+
