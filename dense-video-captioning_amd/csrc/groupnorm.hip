@@ -228,6 +228,168 @@ __global__ __launch_bounds__(256) void gn_bwd_dx_kernel(const float* __restrict_
     reinterpret_cast<float4*>(dx)[i] = o;
 }
 
+// Single-pass forms for T <= kGnFRows: one 1024-thread workgroup per (video, 64-channel block) holds the block's
+// T x 64 values in registers (64 row slots x 16 float4 lanes, up to 8 rows per thread), so the group statistics
+// (forward) and the group sums s1, s2 (backward) come from registers and the pass reads x (and dy) once -- the
+// chunked forms above read them twice (stats or sums pass, then the apply or dx pass).  A 64-channel block holds
+// whole groups (C/G a power of two <= 64 channels).  The forward's statistics are two-pass over the registers (mean,
+// then the sum of squared deviations), the backward's column partials one row per video.
+constexpr int kGnFRows = 512;
+constexpr int kGnFThreads = 1024;
+constexpr int kGnFSlots = kGnFThreads / 16;   // row slots
+constexpr int kGnFRpt = kGnFRows / kGnFSlots;  // rows per thread (8)
+
+// sums v over the lanes of a group (cpg4 consecutive float4 lanes of a 16-lane row) and over the 64 row slots; every
+// thread gets its group's total.  red: kGnFSlots * 16 floats of LDS; the caller separates two uses by a barrier.
+__device__ __forceinline__ float gnf_group_sum(float v, int cpg4, float* red) {
+    for (int d = 1; d < cpg4; d <<= 1) v += __shfl_xor(v, d, PDVC_WAVE);
+    const int c4l = threadIdx.x & 15, rr = threadIdx.x >> 4;
+    red[rr * 16 + c4l] = v;
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        float t = 0.f;
+        for (int k = 0; k < kGnFSlots; ++k) t += red[k * 16 + threadIdx.x];
+        red[kGnFSlots * 16 + threadIdx.x] = t;
+    }
+    __syncthreads();
+    return red[kGnFSlots * 16 + (c4l & ~(cpg4 - 1))];
+}
+
+__global__ __launch_bounds__(kGnFThreads) void gn_fwd_fused_kernel(const float* __restrict__ x, int T, int C, int G,
+                                                                    float eps, const float* __restrict__ gamma,
+                                                                    const float* __restrict__ beta,
+                                                                    float* __restrict__ y, long ys,
+                                                                    float* __restrict__ y2, float* __restrict__ mean,
+                                                                    float* __restrict__ rstd) {
+    __shared__ float red[kGnFSlots * 16 + 16];
+    const int n = blockIdx.x, cb = blockIdx.y;
+    const int c4l = threadIdx.x & 15, rr = threadIdx.x >> 4;
+    const int c4 = C / 4, cg = cb * 16 + c4l;  // this lane's float4 column
+    const int cpg4 = (C / G) / 4;
+    const float4* xs = reinterpret_cast<const float4*>(x + (size_t)n * T * C) + cg;
+    float4 v[kGnFRpt];
+    float sm = 0.f;
+#pragma unroll
+    for (int k = 0; k < kGnFRpt; ++k) {
+        const int r = rr + k * kGnFSlots;
+        v[k] = r < T ? xs[(size_t)r * c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        sm += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+    }
+    const float cnt = (float)T * (float)(C / G);
+    const float mu = gnf_group_sum(sm, cpg4, red) / cnt;
+    float sq = 0.f;
+#pragma unroll
+    for (int k = 0; k < kGnFRpt; ++k) {
+        if (rr + k * kGnFSlots < T) {
+            const float a = v[k].x - mu, b = v[k].y - mu, c = v[k].z - mu, d = v[k].w - mu;
+            sq += (a * a + b * b) + (c * c + d * d);
+        }
+    }
+    __syncthreads();  // red reused
+    const float rs = rsqrtf(gnf_group_sum(sq, cpg4, red) / cnt + eps);
+    if (rr == 0 && (c4l & (cpg4 - 1)) == 0) {
+        const int g = (cg * 4) / (C / G);
+        mean[n * G + g] = mu;
+        rstd[n * G + g] = rs;
+    }
+    const float4 ga = reinterpret_cast<const float4*>(gamma)[cg], be = reinterpret_cast<const float4*>(beta)[cg];
+#pragma unroll
+    for (int k = 0; k < kGnFRpt; ++k) {
+        const int r = rr + k * kGnFSlots;
+        if (r < T) {
+            float4 o;
+            o.x = (v[k].x - mu) * rs * ga.x + be.x;
+            o.y = (v[k].y - mu) * rs * ga.y + be.y;
+            o.z = (v[k].z - mu) * rs * ga.z + be.z;
+            o.w = (v[k].w - mu) * rs * ga.w + be.w;
+            reinterpret_cast<float4*>(y + (size_t)n * ys + (size_t)r * C)[cg] = o;
+            if (y2) reinterpret_cast<float4*>(y2 + ((size_t)n * T + r) * C)[cg] = o;
+        }
+    }
+}
+
+// backward: col_partials (N, 2, C) -- per video dgamma = sum dy*xhat, dbeta = sum dy over its rows
+__global__ __launch_bounds__(kGnFThreads) void gn_bwd_fused_kernel(const float* __restrict__ x,
+                                                                    const float* __restrict__ dy,
+                                                                    const float* __restrict__ mean,
+                                                                    const float* __restrict__ rstd,
+                                                                    const float* __restrict__ gamma, int T, int C,
+                                                                    int G, long dys, const float* __restrict__ dy2,
+                                                                    float* __restrict__ cpart,
+                                                                    float* __restrict__ dx) {
+    __shared__ float red[kGnFSlots * 16 + 16];
+    __shared__ float4 redc[2][kGnFSlots][16];
+    const int n = blockIdx.x, cb = blockIdx.y;
+    const int c4l = threadIdx.x & 15, rr = threadIdx.x >> 4;
+    const int c4 = C / 4, cg = cb * 16 + c4l;
+    const int cpg4 = (C / G) / 4;
+    const int g = (cg * 4) / (C / G);
+    const float mu = mean[n * G + g], rs = rstd[n * G + g];
+    const float4 ga = reinterpret_cast<const float4*>(gamma)[cg];
+    const float4* xs = reinterpret_cast<const float4*>(x + (size_t)n * T * C) + cg;
+    const float4* ds = reinterpret_cast<const float4*>(dy + (size_t)n * dys) + cg;
+    const float4* ds2 = dy2 ? reinterpret_cast<const float4*>(dy2 + (size_t)n * T * C) + cg : nullptr;
+    float4 h[kGnFRpt], d[kGnFRpt];
+    float s1 = 0.f, s2 = 0.f;
+    float4 dg = make_float4(0.f, 0.f, 0.f, 0.f), db = dg;
+#pragma unroll
+    for (int k = 0; k < kGnFRpt; ++k) {
+        const int r = rr + k * kGnFSlots;
+        if (r < T) {
+            const float4 v = xs[(size_t)r * c4];
+            d[k] = ds[(size_t)r * c4];
+            if (ds2) {
+                const float4 e = ds2[(size_t)r * c4];
+                d[k].x += e.x; d[k].y += e.y; d[k].z += e.z; d[k].w += e.w;
+            }
+            h[k] = make_float4((v.x - mu) * rs, (v.y - mu) * rs, (v.z - mu) * rs, (v.w - mu) * rs);
+        } else {
+            d[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            h[k] = d[k];
+        }
+        s1 += d[k].x * ga.x + d[k].y * ga.y + d[k].z * ga.z + d[k].w * ga.w;
+        s2 += d[k].x * ga.x * h[k].x + d[k].y * ga.y * h[k].y + d[k].z * ga.z * h[k].z + d[k].w * ga.w * h[k].w;
+        dg.x += d[k].x * h[k].x; dg.y += d[k].y * h[k].y; dg.z += d[k].z * h[k].z; dg.w += d[k].w * h[k].w;
+        db.x += d[k].x; db.y += d[k].y; db.z += d[k].z; db.w += d[k].w;
+    }
+    redc[0][rr][c4l] = dg;
+    redc[1][rr][c4l] = db;
+    s1 = gnf_group_sum(s1, cpg4, red);  // (its barriers also publish redc)
+    if (threadIdx.x < 32) {  // the column partials: 16 float4 columns x (dgamma, dbeta)
+        const int which = threadIdx.x >> 4, col = threadIdx.x & 15;
+        float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int k = 0; k < kGnFSlots; ++k) {
+            const float4 a = redc[which][k][col];
+            t.x += a.x; t.y += a.y; t.z += a.z; t.w += a.w;
+        }
+        reinterpret_cast<float4*>(cpart + (size_t)n * 2 * C + (size_t)which * C)[cb * 16 + col] = t;
+    }
+    __syncthreads();  // red reused
+    s2 = gnf_group_sum(s2, cpg4, red);
+    const float inv_n = 1.f / ((float)T * (float)(C / G));
+#pragma unroll
+    for (int k = 0; k < kGnFRpt; ++k) {
+        const int r = rr + k * kGnFSlots;
+        if (r < T) {
+            float4 o;
+            o.x = rs * (d[k].x * ga.x - (s1 + h[k].x * s2) * inv_n);
+            o.y = rs * (d[k].y * ga.y - (s1 + h[k].y * s2) * inv_n);
+            o.z = rs * (d[k].z * ga.z - (s1 + h[k].z * s2) * inv_n);
+            o.w = rs * (d[k].w * ga.w - (s1 + h[k].w * s2) * inv_n);
+            reinterpret_cast<float4*>(dx + ((size_t)n * T + r) * C)[cg] = o;
+        }
+    }
+}
+
+// whether the single-pass forms serve this shape
+static bool gn_fused_ok(int T, int C, int G) {
+    static const bool on = [] {
+        const char* e = getenv("PDVC_GN_FUSED");  // A/B switch: 0 = the chunked two-pass kernels
+        return !(e && e[0] == '0');
+    }();
+    return on && T <= kGnFRows && C % 64 == 0 && (C / G) <= 64;
+}
+
 static int gn_check(int N, int T, int C, int G) {
     PDVC_CHECK_ARG(N >= 0 && T > 0 && C > 0 && G > 0 && C % G == 0, "invalid GroupNorm sizes");
     const int cpg = C / G;
@@ -306,4 +468,42 @@ extern "C" int pdvc_groupnorm_rows_backward_f32(const float* x, const float* dy,
                                                 float* col_partials, float* dx, void* stream) {
     return pdvc_groupnorm_rows_backward_strided_f32(x, dy, (long)T * C, nullptr, mean, rstd, gamma, N, T, C, G,
                                                     group_ws, col_partials, dx, stream);
+}
+
+// Single-pass forms (gn_fwd_fused_kernel / gn_bwd_fused_kernel): T <= 512, C a multiple of 64, C / G <= 64 channels
+// per group; any other shape (or PDVC_GN_FUSED=0) returns PDVC_ERR_UNSUPPORTED before launching anything (the caller
+// takes the chunked forms).  Forward: as pdvc_groupnorm_rows_forward_out_f32 without a workspace.  Backward: as
+// pdvc_groupnorm_rows_backward_strided_f32 with col_partials (N, 2, C) -- one row of (dgamma, dbeta) partials per
+// video -- and no group workspace.
+extern "C" int pdvc_groupnorm_rows_forward_fused_f32(const float* x, int N, int T, int C, int G, float eps,
+                                                     const float* gamma, const float* beta, float* y,
+                                                     long y_video_stride, float* y_copy, float* mean, float* rstd,
+                                                     void* stream) {
+    int rc = gn_check(N, T, C, G);
+    if (rc) return rc;
+    PDVC_CHECK_ARG(y_video_stride >= (long)T * C && y_video_stride % 4 == 0, "invalid output video stride %ld",
+                   y_video_stride);
+    if (!gn_fused_ok(T, C, G)) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "single-pass GroupNorm: shape not served");
+    if (N == 0) return PDVC_OK;
+    hipLaunchKernelGGL(gn_fwd_fused_kernel, dim3((unsigned)N, (unsigned)(C / 64)), dim3(kGnFThreads), 0,
+                       (hipStream_t)stream, x, T, C, G, eps, gamma, beta, y, y_video_stride, y_copy, mean, rstd);
+    PDVC_CHECK_LAUNCH("gn_fwd_fused_kernel");
+    return PDVC_OK;
+}
+
+extern "C" int pdvc_groupnorm_rows_backward_fused_f32(const float* x, const float* dy, long dy_video_stride,
+                                                      const float* dy_add, const float* mean, const float* rstd,
+                                                      const float* gamma, int N, int T, int C, int G,
+                                                      float* col_partials, float* dx, void* stream) {
+    int rc = gn_check(N, T, C, G);
+    if (rc) return rc;
+    PDVC_CHECK_ARG(dy_video_stride >= (long)T * C && dy_video_stride % 4 == 0, "invalid gradient video stride %ld",
+                   dy_video_stride);
+    if (!gn_fused_ok(T, C, G)) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "single-pass GroupNorm: shape not served");
+    if (N == 0) return PDVC_OK;
+    hipLaunchKernelGGL(gn_bwd_fused_kernel, dim3((unsigned)N, (unsigned)(C / 64)), dim3(kGnFThreads), 0,
+                       (hipStream_t)stream, x, dy, mean, rstd, gamma, T, C, G, dy_video_stride, dy_add, col_partials,
+                       dx);
+    PDVC_CHECK_LAUNCH("gn_bwd_fused_kernel");
+    return PDVC_OK;
 }

@@ -87,6 +87,9 @@ SIGNATURES = {
     "pdvc_groupnorm_rows_forward_out_f32": [_vp, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp, ctypes.c_long, _vp, _vp,
                                             _vp, _vp],
     "pdvc_groupnorm_rows_backward_strided_f32": [_vp, _vp, ctypes.c_long] + [_vp] * 4 + [_i] * 4 + [_vp] * 4,
+    "pdvc_groupnorm_rows_forward_fused_f32": [_vp, _i, _i, _i, _i, _f, _vp, _vp, _vp, ctypes.c_long, _vp, _vp, _vp,
+                                              _vp],
+    "pdvc_groupnorm_rows_backward_fused_f32": [_vp, _vp, ctypes.c_long] + [_vp] * 4 + [_i] * 4 + [_vp] * 3,
     "pdvc_gemm_f32": [_i, _i, _i, _vp, _i, _i, _vp, _i, _i, _vp, _i, _vp, _i, _i, _vp],
     "pdvc_split3_planes_f32": [_vp, ctypes.c_long, _i, _i, _i, _vp, _vp],
     "pdvc_gemm3p_f32": [_i, _i, _i, _vp, ctypes.c_long, _vp, _vp, ctypes.c_long, _vp, _i, _vp],

@@ -81,6 +81,29 @@ class ConvS2RowsFunction(Function):
         return gx, gw, gb
 
 
+def _fused_forward(x, N, T, C, G, eps, weight, bias, y, ys, y2, mean, rstd):
+    """The single-pass GroupNorm forward (pdvc_groupnorm_rows_forward_fused_f32: x read once, statistics from
+    registers) into y (video stride ys) / y2 / mean / rstd; False (nothing launched) for shapes it does not serve."""
+    try:
+        _n.call("pdvc_groupnorm_rows_forward_fused_f32", _n.ptr(x), N, T, C, G, float(eps), _n.ptr(weight),
+                _n.ptr(bias), _n.ptr_any(y), ys, _n.ptr(y2), _n.ptr(mean), _n.ptr(rstd), _n.stream())
+        return True
+    except _n.NativeError:
+        return False
+
+
+def _fused_backward(x, dy, dys, dy_add, mean, rstd, weight, N, T, C, G, dx):
+    """The single-pass GroupNorm backward (pdvc_groupnorm_rows_backward_fused_f32: x and dy read once) into dx;
+    returns its (N, 2C) [dgamma | dbeta] partials, or None (nothing launched) for shapes it does not serve."""
+    cpart = torch.empty(N, 2 * C, dtype=x.dtype, device=x.device)
+    try:
+        _n.call("pdvc_groupnorm_rows_backward_fused_f32", _n.ptr(x), _n.ptr_any(dy), dys, _n.ptr(dy_add),
+                _n.ptr(mean), _n.ptr(rstd), _n.ptr(weight), N, T, C, G, _n.ptr(cpart), _n.ptr(dx), _n.stream())
+        return cpart
+    except _n.NativeError:
+        return None
+
+
 class GroupNormRowsFunction(Function):
     """nn.GroupNorm(G, C) of x (N, T, C) rows (statistics per video and group over T x C/G values)."""
 
@@ -90,12 +113,13 @@ class GroupNormRowsFunction(Function):
         N, T, C = x.shape
         chunks = (T + GN_ROWS - 1) // GN_ROWS
         kw = dict(dtype=x.dtype, device=x.device)
-        ws = torch.empty(N * chunks * groups * 3, **kw)
         y = torch.empty_like(x)
         mean = torch.empty(N * groups, **kw)
         rstd = torch.empty(N * groups, **kw)
-        _n.call("pdvc_groupnorm_rows_forward_f32", _n.ptr(x), N, T, C, groups, float(eps), _n.ptr(weight),
-                _n.ptr(bias), _n.ptr(ws), _n.ptr(y), _n.ptr(mean), _n.ptr(rstd), _n.stream())
+        if not _fused_forward(x, N, T, C, groups, eps, weight, bias, y, T * C, None, mean, rstd):
+            ws = torch.empty(N * chunks * groups * 3, **kw)
+            _n.call("pdvc_groupnorm_rows_forward_f32", _n.ptr(x), N, T, C, groups, float(eps), _n.ptr(weight),
+                    _n.ptr(bias), _n.ptr(ws), _n.ptr(y), _n.ptr(mean), _n.ptr(rstd), _n.stream())
         ctx.save_for_backward(x, weight, mean, rstd)
         ctx.groups = groups
         return y
@@ -109,11 +133,13 @@ class GroupNormRowsFunction(Function):
         G = ctx.groups
         chunks = (T + GN_ROWS - 1) // GN_ROWS
         kw = dict(dtype=x.dtype, device=x.device)
-        gws = torch.empty(N * chunks * G * 2 + N * G * 2, **kw)
-        cpart = torch.empty(N * chunks, 2 * C, **kw)
         dx = torch.empty_like(x)
-        _n.call("pdvc_groupnorm_rows_backward_f32", _n.ptr(x), _n.ptr(dy), _n.ptr(mean), _n.ptr(rstd), _n.ptr(weight),
-                N, T, C, G, _n.ptr(gws), _n.ptr(cpart), _n.ptr(dx), _n.stream())
+        cpart = _fused_backward(x, dy, T * C, None, mean, rstd, weight, N, T, C, G, dx)
+        if cpart is None:
+            gws = torch.empty(N * chunks * G * 2 + N * G * 2, **kw)
+            cpart = torch.empty(N * chunks, 2 * C, **kw)
+            _n.call("pdvc_groupnorm_rows_backward_f32", _n.ptr(x), _n.ptr(dy), _n.ptr(mean), _n.ptr(rstd),
+                    _n.ptr(weight), N, T, C, G, _n.ptr(gws), _n.ptr(cpart), _n.ptr(dx), _n.stream())
         gsum = colsum(cpart)
         return dx, gsum[:C].contiguous(), gsum[C:].contiguous(), None, None
 
@@ -132,13 +158,14 @@ class GroupNormFlatFunction(Function):
         S = flat.shape[1]
         chunks = (T + GN_ROWS - 1) // GN_ROWS
         kw = dict(dtype=x.dtype, device=x.device)
-        ws = torch.empty(N * chunks * groups * 3, **kw)
         y2 = torch.empty_like(x) if want_copy else None
         mean = torch.empty(N * groups, **kw)
         rstd = torch.empty(N * groups, **kw)
-        _n.call("pdvc_groupnorm_rows_forward_out_f32", _n.ptr(x), N, T, C, groups, float(eps), _n.ptr(weight),
-                _n.ptr(bias), _n.ptr(ws), _n.ptr_any(flat[:, start:start + T]), S * C, _n.ptr(y2), _n.ptr(mean),
-                _n.ptr(rstd), _n.stream())
+        if not _fused_forward(x, N, T, C, groups, eps, weight, bias, flat[:, start:start + T], S * C, y2, mean, rstd):
+            ws = torch.empty(N * chunks * groups * 3, **kw)
+            _n.call("pdvc_groupnorm_rows_forward_out_f32", _n.ptr(x), N, T, C, groups, float(eps), _n.ptr(weight),
+                    _n.ptr(bias), _n.ptr(ws), _n.ptr_any(flat[:, start:start + T]), S * C, _n.ptr(y2), _n.ptr(mean),
+                    _n.ptr(rstd), _n.stream())
         ctx.mark_dirty(flat)
         ctx.save_for_backward(x, weight, mean, rstd)
         ctx.meta = (groups, start, S, want_copy)
@@ -154,12 +181,14 @@ class GroupNormFlatFunction(Function):
         d_copy = d_copy.contiguous() if d_copy is not None else None
         chunks = (T + GN_ROWS - 1) // GN_ROWS
         kw = dict(dtype=x.dtype, device=x.device)
-        gws = torch.empty(N * chunks * G * 2 + N * G * 2, **kw)
-        cpart = torch.empty(N * chunks, 2 * C, **kw)
         dx = torch.empty_like(x)
-        _n.call("pdvc_groupnorm_rows_backward_strided_f32", _n.ptr(x), _n.ptr_any(d_flat[:, start:start + T]), S * C,
-                _n.ptr(d_copy), _n.ptr(mean), _n.ptr(rstd), _n.ptr(weight), N, T, C, G, _n.ptr(gws), _n.ptr(cpart),
-                _n.ptr(dx), _n.stream())
+        cpart = _fused_backward(x, d_flat[:, start:start + T], S * C, d_copy, mean, rstd, weight, N, T, C, G, dx)
+        if cpart is None:
+            gws = torch.empty(N * chunks * G * 2 + N * G * 2, **kw)
+            cpart = torch.empty(N * chunks, 2 * C, **kw)
+            _n.call("pdvc_groupnorm_rows_backward_strided_f32", _n.ptr(x), _n.ptr_any(d_flat[:, start:start + T]),
+                    S * C, _n.ptr(d_copy), _n.ptr(mean), _n.ptr(rstd), _n.ptr(weight), N, T, C, G, _n.ptr(gws),
+                    _n.ptr(cpart), _n.ptr(dx), _n.stream())
         gsum = colsum(cpart)
         # the slice [start, start + T) of the incoming flat was overwritten: only the earlier levels' functions
         # (which read their own slices) consume this gradient, so it passes through unmasked

@@ -458,6 +458,17 @@ int pdvc_groupnorm_rows_backward_strided_f32(const float* x, const float* dy, lo
                                              const float* dy_add, const float* mean, const float* rstd,
                                              const float* gamma, int N, int T, int C, int G, float* group_ws,
                                              float* col_partials, float* dx, void* stream);
+/* Single-pass forms: one workgroup per (video, 64-channel block) holds the block in registers, so x (and dy) are
+ * read once -- the forms above read them twice (statistics / group sums, then apply / dx).  T <= 512, C a multiple
+ * of 64, C/G <= 64; any other shape returns PDVC_ERR_UNSUPPORTED before launching anything (use the forms above).
+ * No workspaces; the backward's col_partials are (N, 2, C): one row of [dgamma | dbeta] partials per video. */
+int pdvc_groupnorm_rows_forward_fused_f32(const float* x, int N, int T, int C, int G, float eps, const float* gamma,
+                                          const float* beta, float* y, long y_video_stride, float* y_copy,
+                                          float* mean, float* rstd, void* stream);
+int pdvc_groupnorm_rows_backward_fused_f32(const float* x, const float* dy, long dy_video_stride,
+                                           const float* dy_add, const float* mean, const float* rstd,
+                                           const float* gamma, int N, int T, int C, int G, float* col_partials,
+                                           float* dx, void* stream);
 
 /* ---- column sums (bias gradients) ---------------------------------------------------------------------
  * out[c] = sum_r x[r*cols + c] for a row-major (rows, cols) fp32 matrix, cols % 4 == 0, 16-byte aligned;

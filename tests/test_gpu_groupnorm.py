@@ -10,7 +10,7 @@ DEV = "cuda"
 
 
 @pytest.mark.parametrize("N,T,C,G", [(3, 512, 512, 32), (2, 37, 512, 32), (4, 64, 256, 16), (1, 1, 512, 32),
-                                     (2, 130, 128, 8)])
+                                     (2, 130, 128, 8), (2, 100, 512, 8), (2, 600, 512, 32), (2, 64, 32, 8)])
 def test_groupnorm_rows_matches_torch(N, T, C, G):
     from pdvc.ops.functions.conv_rows import GroupNormRowsFunction
     torch.manual_seed(N * T + C)
@@ -116,3 +116,38 @@ def test_conv_s2_tap_epilogue_matches_conv1d(N, T, monkeypatch):
     torch.testing.assert_close(outs[True][0], outs[False][0], rtol=1e-6, atol=1e-5)
     for a, c in zip(outs[True][1:], outs[False][1:]):
         assert torch.equal(a, c), "the backward does not depend on the forward's form"
+
+
+def test_groupnorm_single_pass_forms_serve_the_pyramid_shapes():
+    """The single-pass kernels (pdvc_groupnorm_rows_*_fused_f32) take every base-encoder level shape (T <= 512, C = 512,
+    32 groups) and refuse the rest (T > 512, C not a multiple of 64) with nothing written, so the chunked forms run
+    there; the backward's (N, 2C) partials sum to [dgamma | dbeta]."""
+    from pdvc import _native as _n
+    torch.manual_seed(1)
+    for T, C, ok in ((512, 512, True), (64, 512, True), (513, 512, False), (64, 32, False)):
+        N, G = 2, 32 if C == 512 else 8
+        x = torch.randn(N, T, C, device=DEV)
+        w, b = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+        y = torch.full_like(x, 7.0)
+        mean, rstd = torch.empty(N * G, device=DEV), torch.empty(N * G, device=DEV)
+        args = (_n.ptr(x), N, T, C, G, 1e-5, _n.ptr(w), _n.ptr(b), _n.ptr(y), T * C, None, _n.ptr(mean), _n.ptr(rstd),
+                _n.stream())
+        if not ok:
+            with pytest.raises(_n.NativeError):
+                _n.call("pdvc_groupnorm_rows_forward_fused_f32", *args)
+            assert bool((y == 7.0).all())
+            continue
+        _n.call("pdvc_groupnorm_rows_forward_fused_f32", *args)
+        ref = F.group_norm(x.double().transpose(1, 2), G, w.double(), b.double(), 1e-5).transpose(1, 2)
+        assert (y.double() - ref).abs().max().item() < 2e-5
+        dy = torch.randn_like(x)
+        dx = torch.empty_like(x)
+        cp = torch.empty(N, 2 * C, device=DEV)
+        _n.call("pdvc_groupnorm_rows_backward_fused_f32", _n.ptr(x), _n.ptr(dy), T * C, None, _n.ptr(mean),
+                _n.ptr(rstd), _n.ptr(w), N, T, C, G, _n.ptr(cp), _n.ptr(dx), _n.stream())
+        xh = ((x.double().view(N, T, G, -1) - mean.double().view(N, 1, G, 1)) * rstd.double().view(N, 1, G, 1))
+        dg = (dy.double() * xh.view(N, T, C)).sum((0, 1))
+        db = dy.double().sum((0, 1))
+        got = cp.double().sum(0)
+        assert (got[:C] - dg).abs().max().item() <= 1e-4 * (dg.abs().max().item() + 1.0)
+        assert (got[C:] - db).abs().max().item() <= 1e-4 * (db.abs().max().item() + 1.0)
