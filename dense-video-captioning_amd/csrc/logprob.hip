@@ -221,57 +221,6 @@ __global__ __launch_bounds__(kLpThreads) void logprob_pick_bwd_reg_kernel(const 
     }
 }
 
-// The bf16 mode's backward with the logit layer's bias gradient folded in: workgroups stride over the rows (a lane
-// keeps the same columns in every row), so each lane sums its columns' dlogits over its workgroup's rows in registers
-// and writes them once -- column partials (gridDim.x, V) that one small column sum reduces, in a fixed order
-// (deterministic) -- instead of a separate column-sum pass re-reading the (rows, V) gradient.
-__global__ __launch_bounds__(kLpThreads) void logprob_pick_bwd_reg_cs_kernel(const float* __restrict__ logp,
-                                                                            const int64_t* __restrict__ target,
-                                                                            const float* __restrict__ gpick, int V,
-                                                                            long rows, float* __restrict__ dx,
-                                                                            uint16_t* __restrict__ dx16,
-                                                                            float* __restrict__ col_parts) {
-    const int v4 = V / 4;
-    float4 cs[kLpKR];
-#pragma unroll
-    for (int k = 0; k < kLpKR; ++k) cs[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (long row = blockIdx.x; row < rows; row += gridDim.x) {
-        const float g = gpick[row];
-        const int64_t t = target[row];
-        const float4* l4 = reinterpret_cast<const float4*>(logp + row * (long)V);
-        float4* d4 = reinterpret_cast<float4*>(dx + row * (long)V);
-        float4 r[kLpKR];
-#pragma unroll
-        for (int k = 0; k < kLpKR; ++k) {
-            const int i = threadIdx.x + k * kLpThreads;
-            if (i < v4) r[k] = l4[i];
-        }
-#pragma unroll
-        for (int k = 0; k < kLpKR; ++k) {
-            const int i = threadIdx.x + k * kLpThreads;
-            if (i < v4) {
-                const int j = 4 * i;
-                const float4 o = make_float4(g * ((j == t ? 1.f : 0.f) - expf(r[k].x)),
-                                             g * ((j + 1 == t ? 1.f : 0.f) - expf(r[k].y)),
-                                             g * ((j + 2 == t ? 1.f : 0.f) - expf(r[k].z)),
-                                             g * ((j + 3 == t ? 1.f : 0.f) - expf(r[k].w)));
-                d4[i] = o;
-                store_bf16x4(dx16 + row * (long)V + j, o.x, o.y, o.z, o.w);
-                cs[k].x += o.x;
-                cs[k].y += o.y;
-                cs[k].z += o.z;
-                cs[k].w += o.w;
-            }
-        }
-    }
-    float4* p4 = reinterpret_cast<float4*>(col_parts + (long)blockIdx.x * V);
-#pragma unroll
-    for (int k = 0; k < kLpKR; ++k) {
-        const int i = threadIdx.x + k * kLpThreads;
-        if (i < v4) p4[i] = cs[k];
-    }
-}
-
 // Greedy decoding's word choice (LSTM_DSA.py:149-151: sampleLogprobs, it = torch.max(logprobs, 1) over
 // logprobs = log_softmax(logits)): per row the first index of the largest logit and its log-probability
 // (x_max - max) - log(sum exp(x - max)) = -log(sum exp(x - max)), from ONE read of the logits -- the (rows, V)
@@ -468,25 +417,5 @@ extern "C" int pdvc_logprob_pick_backward_f32_bf16out(const float* logp, const i
     hipLaunchKernelGGL(logprob_pick_bwd_reg_kernel, dim3((unsigned)rows), dim3(kLpThreads), 0, (hipStream_t)stream,
                        logp, target, grad_picked, V, grad_logits, grad16, V);
     PDVC_CHECK_LAUNCH("logprob_pick_bwd_reg_kernel");
-    return PDVC_OK;
-}
-
-// pdvc_logprob_pick_backward_f32_bf16out plus the column partials of grad_logits: col_parts (parts, V), parts in
-// [1, rows], each row of it the sum of grad_logits' rows parts apart (row i of col_parts: rows i, i + parts, ...);
-// their column sum is the logit layer's bias gradient.  Same conditions as the bf16out form.
-extern "C" int pdvc_logprob_pick_backward_f32_bf16out_colparts(const float* logp, const int64_t* target,
-                                                               const float* grad_picked, int rows, int V,
-                                                               float* grad_logits, uint16_t* grad16, int parts,
-                                                               float* col_parts, void* stream) {
-    PDVC_CHECK_ARG(rows >= 0 && V > 0, "invalid sizes (rows >= 0, V > 0)");
-    PDVC_CHECK_ARG(rows == 0 || (logp && target && grad_picked && grad_logits && grad16 && col_parts), "null pointer");
-    PDVC_CHECK_ARG(rows == 0 || (parts >= 1 && parts <= rows), "parts must be in [1, rows], got %d", parts);
-    const bool reg = (V % 4) == 0 && ((uintptr_t)logp % 16) == 0 && ((uintptr_t)grad_logits % 16) == 0 &&
-                     ((uintptr_t)grad16 % 8) == 0 && ((uintptr_t)col_parts % 16) == 0 && V / 4 <= kLpThreads * kLpKR;
-    if (!reg) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "bf16 shadow needs the register-resident row form");
-    if (rows == 0) return PDVC_OK;
-    hipLaunchKernelGGL(logprob_pick_bwd_reg_cs_kernel, dim3((unsigned)parts), dim3(kLpThreads), 0, (hipStream_t)stream,
-                       logp, target, grad_picked, V, (long)rows, grad_logits, grad16, col_parts);
-    PDVC_CHECK_LAUNCH("logprob_pick_bwd_reg_cs_kernel");
     return PDVC_OK;
 }

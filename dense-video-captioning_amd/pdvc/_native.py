@@ -59,7 +59,6 @@ SIGNATURES = {
     "pdvc_relu_dropout_forward_f32_bf16out": [_vp, ctypes.c_long, _i, _f, _u64, _vp, _vp, _vp],
     "pdvc_relu_dropout_backward_f32_bf16out": [_vp, _vp, _i, _i, _f, _i, _vp, _vp, _vp, _vp],
     "pdvc_logprob_pick_backward_f32_bf16out": [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp],
-    "pdvc_logprob_pick_backward_f32_bf16out_colparts": [_vp, _vp, _vp, _i, _i, _vp, _vp, _i, _vp, _vp],
     "pdvc_level_pos_rows_add_f32_bf16out": [_vp] * 5 + [_i] * 5 + [_vp] * 4,
     "pdvc_logprob_pick_forward_f32": [_vp, _vp, _i, _i, _vp, _vp, _vp],
     "pdvc_logprob_pick_backward_f32": [_vp, _vp, _vp, _i, _i, _vp, _vp],

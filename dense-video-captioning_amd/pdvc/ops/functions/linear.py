@@ -230,21 +230,6 @@ def relu_masked(g, y):
             and ent[0].shape == y.shape and g.shape[-1] == y.shape[-1])
 
 
-def tag_colsum(g, sums):
-    """Hand g's column sums (the consuming layer's bias gradient), formed by the kernel that wrote g, to that layer's
-    backward (TorchLinearFunction), tagged with g's version counter like tag_level_sums."""
-    g._pdvc_colsum = (sums, g._version)
-    return g
-
-
-def colsum_of(g):
-    """The column sums tag_colsum attached to g, or None when absent or stale."""
-    ent = getattr(g, "_pdvc_colsum", None)
-    if ent is None or ent[1] != g._version or ent[0].shape != (g.shape[-1],):
-        return None
-    return ent[0]
-
-
 # the box MLP's ReLU backward in the next layer's data-gradient epilogue (pdvc_gemm3p_dmask_f32 with p = 0: hd > 0 ?
 # g : 0, bit for bit threshold_backward) instead of a pass over (rows, O); PDVC_RELU_DMASK=0 is the A/B switch
 _RELU_DMASK = os.environ.get("PDVC_RELU_DMASK", "1") != "0"
@@ -293,12 +278,7 @@ class TorchLinearFunction(Function):
             if gx is None:
                 gx = mm_dgrad(gy2, weight).view(*gy.shape[:-1], weight.shape[1])
         want_gb = ctx.has_bias and ctx.needs_input_grad[2]
-        cs = colsum_of(gy) if want_gb and y is None else None  # summed by the kernel that wrote gy (bf16 mode logits)
-        if cs is not None:
-            gb = cs
-            if ctx.needs_input_grad[1]:
-                gw = wgrad_mm(gy2, x2)
-        elif ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1]:
             gb = gy2.new_empty(O) if want_gb else None
             gw = wgrad_mm(gy2, x2, db=gb)  # (the bias gradient from the same pass over gy)
         elif want_gb:

@@ -6,19 +6,11 @@ backward in one pass over logp (dlogits = g_picked * (onehot(target) - exp(logp)
 scatter or log_softmax_backward.  A gradient arriving on logp itself (only if a caller differentiates the
 returned caption_probs) is added with the closed-form log_softmax backward.
 """
-import os
-
 import torch
 from torch.autograd import Function
 
 from pdvc import _native as _n
 from pdvc.precision import attach_bf16, bf16_active, shadow_for
-
-
-# bf16 mode: the backward also sums dlogits' columns (the logit layer's bias gradient) over COLPARTS_ROWS row
-# partials (pdvc_logprob_pick_backward_f32_bf16out_colparts); PDVC_LOGPROB_COLPARTS=0 is the A/B switch
-COLPARTS = os.environ.get("PDVC_LOGPROB_COLPARTS", "1") != "0"
-COLPARTS_ROWS = 2048
 
 
 class LogProbPickFunction(Function):
@@ -51,22 +43,10 @@ class LogProbPickFunction(Function):
         g16 = shadow_for(grad) if g_logp is None else None  # bf16 mode: the logit GEMMs' operand, same pass
         done = False
         if g16 is not None:
-            rows = tgt.numel()
             try:
-                if COLPARTS and rows >= 4 * COLPARTS_ROWS:
-                    # the logit layer's bias gradient from the same pass: column partials, one small column sum,
-                    # handed to the layer's backward (linear.py tag_colsum) instead of its pass over (rows, V)
-                    from .linear import colsum, tag_colsum
-                    parts = min(rows, COLPARTS_ROWS)
-                    cp = torch.empty(parts, V, dtype=logp.dtype, device=logp.device)
-                    _n.call("pdvc_logprob_pick_backward_f32_bf16out_colparts", _n.ptr(logp), _n.ptr(tgt),
-                            _n.ptr(g_picked), rows, V, _n.ptr(grad), _n.ptr(g16), parts, _n.ptr(cp), _n.stream())
-                    attach_bf16(grad, g16)
-                    tag_colsum(grad, colsum(cp))
-                else:
-                    _n.call("pdvc_logprob_pick_backward_f32_bf16out", _n.ptr(logp), _n.ptr(tgt), _n.ptr(g_picked),
-                            rows, V, _n.ptr(grad), _n.ptr(g16), _n.stream())
-                    attach_bf16(grad, g16)
+                _n.call("pdvc_logprob_pick_backward_f32_bf16out", _n.ptr(logp), _n.ptr(tgt), _n.ptr(g_picked),
+                        tgt.numel(), V, _n.ptr(grad), _n.ptr(g16), _n.stream())
+                attach_bf16(grad, g16)
                 done = True
             except _n.NativeError:  # not the register-resident row form: the GEMMs cast grad themselves
                 pass

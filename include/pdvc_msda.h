@@ -566,13 +566,6 @@ int pdvc_logprob_pick_backward_ld_f32(const float* logp, const int64_t* target, 
  * and nothing is launched). */
 int pdvc_logprob_pick_backward_f32_bf16out(const float* logp, const int64_t* target, const float* grad_picked,
                                            int rows, int V, float* grad_logits, uint16_t* grad16, void* stream);
-/* The same plus column partials of grad_logits for the logit layer's bias gradient (its column sum): col_parts
- * (parts, V), 1 <= parts <= rows, row i = the sum of grad_logits' rows i, i + parts, i + 2 parts, ... (fixed order:
- * deterministic).  Replaces the bias gradient's column-sum pass over the (rows, V) gradient in the bf16 mode
- * (reference: the logit nn.Linear's bias gradient, LSTM_DSA.py:112-116). */
-int pdvc_logprob_pick_backward_f32_bf16out_colparts(const float* logp, const int64_t* target,
-                                                    const float* grad_picked, int rows, int V, float* grad_logits,
-                                                    uint16_t* grad16, int parts, float* col_parts, void* stream);
 /* greedy decoding's word choice (LSTM_DSA.py:149-151, torch.max over log_softmax(logits)): index[r] = the first index
  * of the largest logit of row r, logp_max[r] = its log-probability (x_max - max) - log(sum exp(x - max)); one read
  * of the logits, the (rows, V) log-probabilities are not written. */

@@ -508,60 +508,3 @@ def test_msda_bf16out_decoder_grad_value_only():
     assert torch.equal(_bits(gv16), _bits(gv1.to(torch.bfloat16)))
     with pytest.raises(_n.NativeError):
         bwd(True, torch.empty(proj.shape, device=DEV, dtype=torch.bfloat16))
-
-
-@pytest.mark.parametrize("rows,parts", [(9000, 2048), (333, 333), (5000, 7)])
-def test_logprob_backward_colparts_sum_to_the_bias_gradient(rows, parts):
-    """pdvc_logprob_pick_backward_f32_bf16out_colparts: grad_logits and its bf16 rounding bit for bit as the
-    bf16out form, and column partials whose column sum is grad_logits.sum(0) (the logit layer's bias gradient) to
-    fp32 summation accuracy -- the partials in a fixed order, identical across two calls."""
-    from pdvc import _native as _n
-    g = torch.Generator(device=DEV).manual_seed(11)
-    V = 5748
-    logp = torch.log_softmax(torch.randn(rows, V, device=DEV, generator=g) * 4, -1).contiguous()
-    tgt = torch.randint(0, V, (rows,), device=DEV, generator=g)
-    gp = torch.randn(rows, device=DEV, generator=g)
-    ref = torch.empty_like(logp)
-    r16 = torch.empty(rows, V, device=DEV, dtype=torch.bfloat16)
-    _n.call("pdvc_logprob_pick_backward_f32_bf16out", _n.ptr(logp), _n.ptr(tgt), _n.ptr(gp), rows, V, _n.ptr(ref),
-            _n.ptr(r16), _n.stream())
-    outs = []
-    for _ in range(2):
-        got = torch.empty_like(logp)
-        g16 = torch.empty(rows, V, device=DEV, dtype=torch.bfloat16)
-        cp = torch.empty(parts, V, device=DEV)
-        _n.call("pdvc_logprob_pick_backward_f32_bf16out_colparts", _n.ptr(logp), _n.ptr(tgt), _n.ptr(gp), rows, V,
-                _n.ptr(got), _n.ptr(g16), parts, _n.ptr(cp), _n.stream())
-        assert torch.equal(got, ref) and torch.equal(_bits(g16), _bits(r16))
-        outs.append(cp)
-    assert torch.equal(outs[0], outs[1])
-    want = ref.double().sum(0)
-    scale = ref.double().abs().sum(0).clamp_min(1e-30)
-    assert float(((outs[0].double().sum(0) - want).abs() / scale).max()) < 1e-5
-    with pytest.raises(_n.NativeError):
-        _n.call("pdvc_logprob_pick_backward_f32_bf16out_colparts", _n.ptr(logp), _n.ptr(tgt), _n.ptr(gp), rows, V,
-                _n.ptr(got), _n.ptr(g16), rows + 1, _n.ptr(cp), _n.stream())
-
-
-def test_logit_layer_bias_gradient_from_colparts(monkeypatch):
-    """The bf16 mode's caption logit layer (Linear -> logprob_pick): with the column partials the layer's bias
-    gradient comes from the logprob backward (tagged hand-over, no column-sum pass) and equals the column-sum path's
-    to fp32 summation accuracy; every other gradient is bit-identical."""
-    import pdvc.ops.functions.logprob as LP
-    from pdvc.ops.functions.linear import dense
-    from pdvc.precision import bf16_matmul
-    torch.manual_seed(2)
-    rows, H, V = 9000, 512, 5748
-    x = torch.randn(rows, H, device=DEV)
-    lin = torch.nn.Linear(H, V).to(DEV)
-    tgt = torch.randint(0, V, (rows,), device=DEV)
-    res = []
-    for on in (True, False):
-        monkeypatch.setattr(LP, "COLPARTS", on)
-        xa = x.clone().requires_grad_()
-        with bf16_matmul():
-            _, picked = LP.logprob_pick(dense(xa, lin.weight, lin.bias), tgt)
-            res.append(torch.autograd.grad(picked.sum(), [xa, lin.weight, lin.bias]))
-    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
-    db, ref = res[0][2].double(), res[1][2].double()
-    assert float((db - ref).abs().max()) <= 1e-5 * float(ref.abs().max())
