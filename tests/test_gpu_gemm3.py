@@ -430,8 +430,16 @@ def test_relu_mask_in_next_layers_dgrad_epilogue_is_bit_identical(monkeypatch, c
     handed over as a tagged gradient (linear.py tag_relu_masked) against the separate threshold_backward passes --
     bit-identical output and gradients.  consumers = 2: the ReLU output also feeds a second product, so autograd
     sums the two gradients and the producer must mask that sum itself (the tag does not survive the sum)."""
-    _on_gemm3(monkeypatch)
+    G = _on_gemm3(monkeypatch)
     import pdvc.ops.functions.linear as L
+    fused = []
+    real = G.mm_dgrad_dmask
+
+    def counting(*a, **k):
+        r = real(*a, **k)
+        fused.append(r is not None)
+        return r
+    monkeypatch.setattr(G, "mm_dgrad_dmask", counting)
     torch.manual_seed(5)
     rows, d = 3000, 256
     x = torch.randn(rows, d, device=DEV)
@@ -456,3 +464,4 @@ def test_relu_mask_in_next_layers_dgrad_epilogue_is_bit_identical(monkeypatch, c
     for i, (a, b) in enumerate(zip(*res)):
         assert torch.equal(a, b), f"tensor {i} differs between the epilogue mask and threshold_backward"
     assert float(res[0][1].abs().max()) > 0
+    assert sum(fused) == (2 if consumers == 1 else 3), "the masked data gradients did not run on the fused arm"
