@@ -267,7 +267,8 @@ __global__ __launch_bounds__(kCVW * 64) void cap_value_grad_kernel(
     const uint8_t* __restrict__ vmask, CapLevels lv, int S, int M, int D, int R, int s0, int ns, int accumulate,
     const int32_t* __restrict__ vr_start, const int32_t* __restrict__ vr_rows, const float* __restrict__ save_loc,
     const float* __restrict__ gsamp, float* __restrict__ grad_value, float* __restrict__ level_sums,
-    const int32_t* __restrict__ step_rows, const float* __restrict__ grow, const float* __restrict__ gscale) {
+    const int32_t* __restrict__ step_rows, const float* __restrict__ grow, const float* __restrict__ gscale,
+    uint16_t* __restrict__ gv16) {
     extern __shared__ __attribute__((aligned(16))) int lds_c[];
     __shared__ int wsum[kCVW];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -364,6 +365,8 @@ __global__ __launch_bounds__(kCVW * 64) void cap_value_grad_kernel(
     for (int c = 0; c < CW; ++c) psum[c] = 0.f;
     if (r0 < r1) {
     float* ob = grad_value + ((size_t)b * S + st) * MD + (size_t)m * D;
+    // bf16 mode: every row's rounding too, at the same offsets (the last chunk of steps writes the final rows)
+    uint16_t* ob16 = gv16 ? gv16 + ((size_t)b * S + st) * MD + (size_t)m * D : nullptr;
     float accp[CW], acch[CW];
 #pragma unroll
     for (int c = 0; c < CW; ++c) accp[c] = acch[c] = 0.f;
@@ -380,6 +383,7 @@ __global__ __launch_bounds__(kCVW * 64) void cap_value_grad_kernel(
                     psum[c] += v;
                     if (accumulate) v += orow[ch];
                     orow[ch] = v;
+                    if (ob16) ob16[(size_t)r * MD + ch] = (uint16_t)bf16_bits(v);
                 }
             }
         }
@@ -901,7 +905,7 @@ static int cap_value_grad_impl(const uint8_t* value_pad_mask, const int32_t* lev
                                int max_rows_per_video, const int32_t* video_row_start, const int32_t* video_rows,
                                const int32_t* step_rows, const float* save_loc, const float* grad_samples,
                                const float* grad_rows, const float* grad_scale, float* grad_value,
-                               float* grad_value_level_sums, void* stream) {
+                               float* grad_value_level_sums, uint16_t* gv16, void* stream) {
     float* level_sums = grad_value_level_sums;
     CapLevels lv;
     int S = 0;
@@ -919,7 +923,9 @@ static int cap_value_grad_impl(const uint8_t* value_pad_mask, const int32_t* lev
     const long nblk = (long)batch * num_heads * cL;
     if (nblk == 0) return PDVC_OK;
     if (steps == 0 || max_rows_per_video == 0) {
-        hipError_t e = zero_async(grad_value, (size_t)batch * S * num_heads * head_dim, s);
+        const size_t nv = (size_t)batch * S * num_heads * head_dim;
+        hipError_t e = zero_async(grad_value, nv, s);
+        if (e == hipSuccess && gv16) e = zero_async(reinterpret_cast<float*>(gv16), nv / 2, s);  // (nv even: checked)
         if (e == hipSuccess && level_sums) e = zero_async(level_sums, (size_t)batch * cL * num_heads * head_dim, s);
         return e == hipSuccess ? PDVC_OK : pdvc_set_error(PDVC_ERR_LAUNCH, "memset: %s", hipGetErrorString(e));
     }
@@ -946,7 +952,7 @@ static int cap_value_grad_impl(const uint8_t* value_pad_mask, const int32_t* lev
         const dim3 grid((unsigned)nblk), block(kCVW * 64);
 #define CVG(CW) hipLaunchKernelGGL((cap_value_grad_kernel<CW>), grid, block, lds, s, value_pad_mask, lv, S, num_heads, \
                                    head_dim, rows, s0, ns, acc, video_row_start, video_rows, save_loc, grad_samples,     \
-                                   grad_value, level_sums, step_rows, grad_rows, grad_scale)
+                                   grad_value, level_sums, step_rows, grad_rows, grad_scale, gv16)
         if (cw == 1) CVG(1);
         else if (cw == 2) CVG(2);
         else if (cw == 4) CVG(4);
@@ -966,7 +972,7 @@ extern "C" int pdvc_cap_value_grad_ranged_f32(const uint8_t* value_pad_mask, con
     PDVC_CHECK_ARG(grad_samples != nullptr, "grad_samples must not be NULL");
     return cap_value_grad_impl(value_pad_mask, level_T, num_levels, batch, num_heads, head_dim, num_point, rows, steps,
                                max_rows_per_video, video_row_start, video_rows, step_rows, save_loc, grad_samples,
-                               nullptr, nullptr, grad_value, grad_value_level_sums, stream);
+                               nullptr, nullptr, grad_value, grad_value_level_sums, nullptr, stream);
 }
 
 // The same pass with rank-1 sample gradients: sample s = (step, row, head, k) has gradient grad_scale[s] *
@@ -981,7 +987,7 @@ extern "C" int pdvc_cap_value_grad_rank1_f32(const uint8_t* value_pad_mask, cons
     PDVC_CHECK_ARG(grad_rows != nullptr && grad_scale != nullptr, "grad_rows and grad_scale must not be NULL");
     return cap_value_grad_impl(value_pad_mask, level_T, num_levels, batch, num_heads, head_dim, num_point, rows, steps,
                                max_rows_per_video, video_row_start, video_rows, step_rows, save_loc, nullptr,
-                               grad_rows, grad_scale, grad_value, grad_value_level_sums, stream);
+                               grad_rows, grad_scale, grad_value, grad_value_level_sums, nullptr, stream);
 }
 
 extern "C" int pdvc_cap_value_grad_f32(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels,
@@ -1082,4 +1088,22 @@ extern "C" int pdvc_cap_softattn_backward_f32(const float* value, const uint8_t*
                        grad_alpha_b_part, grad_offsets, grad_ref);
     PDVC_CHECK_LAUNCH("cap_softattn_bwd_kernel");
     return PDVC_OK;
+}
+
+// pdvc_cap_value_grad_ranged_f32 plus the bf16 rounding of grad_value at the same offsets (the bf16 mode: the caption
+// head's value-gradient operand of the projections' GEMMs, written by the pass that writes grad_value)
+extern "C" int pdvc_cap_value_grad_ranged_f32_bf16out(const uint8_t* value_pad_mask, const int32_t* level_T,
+                                                      int num_levels, int batch, int num_heads, int head_dim,
+                                                      int num_point, int rows, int steps, int max_rows_per_video,
+                                                      const int32_t* video_row_start, const int32_t* video_rows,
+                                                      const int32_t* step_rows, const float* save_loc,
+                                                      const float* grad_samples, float* grad_value,
+                                                      float* grad_value_level_sums, uint16_t* grad_value16,
+                                                      void* stream) {
+    PDVC_CHECK_ARG(grad_samples != nullptr, "grad_samples must not be NULL");
+    PDVC_CHECK_ARG(grad_value16 != nullptr && ((uintptr_t)grad_value16 % 4) == 0 && (num_heads * head_dim) % 2 == 0,
+                   "grad_value16: a 4-byte aligned bf16 buffer, num_heads * head_dim even");
+    return cap_value_grad_impl(value_pad_mask, level_T, num_levels, batch, num_heads, head_dim, num_point, rows, steps,
+                               max_rows_per_video, video_row_start, video_rows, step_rows, save_loc, grad_samples,
+                               nullptr, nullptr, grad_value, grad_value_level_sums, grad_value16, stream);
 }

@@ -260,7 +260,8 @@ __global__ __launch_bounds__(kGnFThreads) void gn_fwd_fused_kernel(const float* 
                                                                     const float* __restrict__ beta,
                                                                     float* __restrict__ y, long ys,
                                                                     float* __restrict__ y2, float* __restrict__ mean,
-                                                                    float* __restrict__ rstd) {
+                                                                    float* __restrict__ rstd,
+                                                                    uint16_t* __restrict__ y16) {
     __shared__ float red[kGnFSlots * 16 + 16];
     const int n = blockIdx.x, cb = blockIdx.y;
     const int c4l = threadIdx.x & 15, rr = threadIdx.x >> 4;
@@ -304,6 +305,7 @@ __global__ __launch_bounds__(kGnFThreads) void gn_fwd_fused_kernel(const float* 
             o.w = (v[k].w - mu) * rs * ga.w + be.w;
             reinterpret_cast<float4*>(y + (size_t)n * ys + (size_t)r * C)[cg] = o;
             if (y2) reinterpret_cast<float4*>(y2 + ((size_t)n * T + r) * C)[cg] = o;
+            if (y16) store_bf16x4(y16 + (size_t)n * ys + (size_t)r * C + cg * 4, o.x, o.y, o.z, o.w);
         }
     }
 }
@@ -472,13 +474,14 @@ extern "C" int pdvc_groupnorm_rows_backward_f32(const float* x, const float* dy,
 
 // Single-pass forms (gn_fwd_fused_kernel / gn_bwd_fused_kernel): T <= 512, C a multiple of 64, C / G <= 64 channels
 // per group; any other shape (or PDVC_GN_FUSED=0) returns PDVC_ERR_UNSUPPORTED before launching anything (the caller
-// takes the chunked forms).  Forward: as pdvc_groupnorm_rows_forward_out_f32 without a workspace.  Backward: as
+// takes the chunked forms).  Forward: as pdvc_groupnorm_rows_forward_out_f32 without a workspace, plus y16 (NULL for
+// none): y's bf16 rounding at y's offsets (the bf16 mode's operand of the encoder's first projections).  Backward: as
 // pdvc_groupnorm_rows_backward_strided_f32 with col_partials (N, 2, C) -- one row of (dgamma, dbeta) partials per
 // video -- and no group workspace.
 extern "C" int pdvc_groupnorm_rows_forward_fused_f32(const float* x, int N, int T, int C, int G, float eps,
                                                      const float* gamma, const float* beta, float* y,
                                                      long y_video_stride, float* y_copy, float* mean, float* rstd,
-                                                     void* stream) {
+                                                     uint16_t* y16, void* stream) {
     int rc = gn_check(N, T, C, G);
     if (rc) return rc;
     PDVC_CHECK_ARG(y_video_stride >= (long)T * C && y_video_stride % 4 == 0, "invalid output video stride %ld",
@@ -486,7 +489,8 @@ extern "C" int pdvc_groupnorm_rows_forward_fused_f32(const float* x, int N, int 
     if (!gn_fused_ok(T, C, G)) return pdvc_set_error(PDVC_ERR_UNSUPPORTED, "single-pass GroupNorm: shape not served");
     if (N == 0) return PDVC_OK;
     hipLaunchKernelGGL(gn_fwd_fused_kernel, dim3((unsigned)N, (unsigned)(C / 64)), dim3(kGnFThreads), 0,
-                       (hipStream_t)stream, x, T, C, G, eps, gamma, beta, y, y_video_stride, y_copy, mean, rstd);
+                       (hipStream_t)stream, x, T, C, G, eps, gamma, beta, y, y_video_stride, y_copy, mean, rstd,
+                       y16);
     PDVC_CHECK_LAUNCH("gn_fwd_fused_kernel");
     return PDVC_OK;
 }

@@ -39,6 +39,7 @@ SIGNATURES = {
     "pdvc_cap_value_grad_f32": [_u8p, _vp] + [_i] * 8 + [_vp] * 6,
     "pdvc_cap_value_grad_ex_f32": [_u8p, _vp] + [_i] * 8 + [_vp] * 7,
     "pdvc_cap_value_grad_ranged_f32": [_u8p, _vp] + [_i] * 8 + [_vp] * 8,
+    "pdvc_cap_value_grad_ranged_f32_bf16out": [_u8p, _vp] + [_i] * 8 + [_vp] * 9,
     "pdvc_cap_value_grad_rank1_f32": [_u8p, _vp] + [_i] * 8 + [_vp] * 9,
     "pdvc_softattn_forward_f32": [_vp, _vp, _i, _vp, _vp, _vp] + [_i] * 4 + [_vp] * 3,
     "pdvc_softattn_backward_f32": [_vp, _vp, _i, _vp, _vp, _vp, _vp] + [_i] * 4 + [_vp, _vp, _i, _vp, _vp, _vp, _vp],
@@ -87,7 +88,7 @@ SIGNATURES = {
                                             _vp, _vp],
     "pdvc_groupnorm_rows_backward_strided_f32": [_vp, _vp, ctypes.c_long] + [_vp] * 4 + [_i] * 4 + [_vp] * 4,
     "pdvc_groupnorm_rows_forward_fused_f32": [_vp, _i, _i, _i, _i, _f, _vp, _vp, _vp, ctypes.c_long, _vp, _vp, _vp,
-                                              _vp],
+                                              _vp, _vp],
     "pdvc_groupnorm_rows_backward_fused_f32": [_vp, _vp, ctypes.c_long] + [_vp] * 4 + [_i] * 4 + [_vp] * 3,
     "pdvc_gemm_f32": [_i, _i, _i, _vp, _i, _i, _vp, _i, _i, _vp, _i, _vp, _i, _i, _vp],
     "pdvc_split3_planes_f32": [_vp, ctypes.c_long, _i, _i, _i, _vp, _vp],

@@ -7,12 +7,18 @@ channels-last rows (N, T, C) end to end -- convolutions as GEMMs over row views 
 GroupNorm on rows (csrc/groupnorm.hip) -- so neither the input features nor the levels are ever transposed.
 Same nn.Conv1d / nn.GroupNorm parameters (state_dict unchanged).
 """
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
 
 from .ops.functions.conv_rows import conv1d_rows, group_norm_rows, group_norm_rows_into, group_norm_rows_ok
 from .position_encoding import PositionEmbeddingSine, PyramidPosEmbed
+from .precision import attach_bf16, shadow_for
+
+# bf16 mode: the GroupNorm levels write the flat buffer's bf16 rounding (PDVC_GN_SHADOW=0: the GEMM casts it, A/B)
+_FLAT_SHADOW = os.environ.get("PDVC_GN_SHADOW", "1") != "0"
 
 
 class BaseEncoder(nn.Module):
@@ -75,17 +81,21 @@ class BaseEncoder(nn.Module):
         for _ in range(1, self.num_feature_levels):
             Ts.append((Ts[-1] + 1) // 2)  # Conv1d(k=3, s=2, p=1)
         flat = x.new_empty(N, sum(Ts), self.hidden_dim)
+        # bf16 mode: every level also writes its rows' bf16 rounding, attached to the finished buffer -- the operand of
+        # the first encoder layer's projections, which would otherwise be a cast pass over (N, sum T_l, d)
+        flat16 = shadow_for(flat) if _FLAT_SHADOW else None
         start, prev, masks = 0, None, [mask]
         for lvl in range(self.num_feature_levels):
             conv, gn = self.input_proj[lvl][0], self.input_proj[lvl][1]
             c = conv1d_rows(conv, x if lvl <= 1 else prev)
             assert c.shape[1] == Ts[lvl]
             want = 0 < lvl < self.num_feature_levels - 1  # the next level's conv input
-            out = group_norm_rows_into(gn, c, flat, start, want)
+            out = group_norm_rows_into(gn, c, flat, start, want, flat16)
             flat, prev = out if want else (out, None)
             start += Ts[lvl]
             if lvl:
                 masks.append(F.interpolate(mask[None].float(), size=Ts[lvl]).to(torch.bool)[0])
+        attach_bf16(flat, flat16)
         levels, start = [], 0
         for t in Ts:
             v = flat[:, start:start + t].transpose(1, 2)

@@ -22,7 +22,7 @@ from torch.autograd import Function
 from torch.autograd.function import once_differentiable
 
 from pdvc import _native as _n
-from pdvc.precision import bf16_active, fp32_gemms
+from pdvc.precision import attach_bf16, bf16_active, fp32_gemms, shadow_for
 from .gemm3 import addmm_nt, mm_dgrad
 from .linear import colsum, tag_level_sums, wgrad_mm
 from .ms_deform_attn_func import NUM_SAMPLES, _levels
@@ -72,6 +72,9 @@ def _gemm(inp, a, b, out, b16):
     else:
         torch.ops.aten.addmm.dtype_out(inp, a.to(_BF16), b16, torch.float32, out=out)
 
+
+# bf16 mode: the caption dU written with its bf16 rounding by its value-gradient pass (PDVC_CAP_DU_SHADOW=0: cast, A/B)
+_DU_SHADOW = os.environ.get("PDVC_CAP_DU_SHADOW", "1") != "0"
 
 class CaptionDecodeFunction(Function):
     """value (Nv,S,M,D) = value_proj(memory); xe (n,R,4H); hs_g (R,4H); off_hs (R, M*16); ref (R,L,1|2) (first rd1_rows rows
@@ -328,9 +331,14 @@ class CaptionDecodeFunction(Function):
             # the bias), with its per-(video, level) row sums
             dU = torch.empty((Nv, S, M, A), **kw)
             lsU = torch.empty((Nv, nl, M * A), **kw)
-            _n.call("pdvc_cap_value_grad_ranged_f32", None, lvl, nl, Nv, M, A, NS // nl, R, n, int(max_rows),
-                    _n.ptr(vr_start), _n.ptr(vr_rows), _n.ptr(sr_dev), _n.ptr(LOC), _n.ptr(dATT), _n.ptr(dU),
-                    _n.ptr(lsU), st)
+            dU16 = shadow_for(dU) if _DU_SHADOW else None  # bf16 mode: dU's two GEMMs' operand, from the same pass
+            args = (None, lvl, nl, Nv, M, A, NS // nl, R, n, int(max_rows), _n.ptr(vr_start), _n.ptr(vr_rows),
+                    _n.ptr(sr_dev), _n.ptr(LOC), _n.ptr(dATT), _n.ptr(dU), _n.ptr(lsU))
+            if dU16 is None:
+                _n.call("pdvc_cap_value_grad_ranged_f32", *args, st)
+            else:
+                _n.call("pdvc_cap_value_grad_ranged_f32_bf16out", *args, _n.ptr(dU16), st)
+                attach_bf16(dU, dU16)
             dU2 = dU.view(-1, A)
             dW_ctx = wgrad_mm(dU2, vm.reshape(-1, D))
             db_ctx = lsU.view(-1, A).sum(0)  # the weights of a sample sum to 1: sum dU = sum dATT

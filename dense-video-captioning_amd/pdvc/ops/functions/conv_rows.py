@@ -81,12 +81,14 @@ class ConvS2RowsFunction(Function):
         return gx, gw, gb
 
 
-def _fused_forward(x, N, T, C, G, eps, weight, bias, y, ys, y2, mean, rstd):
+def _fused_forward(x, N, T, C, G, eps, weight, bias, y, ys, y2, mean, rstd, y16=None):
     """The single-pass GroupNorm forward (pdvc_groupnorm_rows_forward_fused_f32: x read once, statistics from
-    registers) into y (video stride ys) / y2 / mean / rstd; False (nothing launched) for shapes it does not serve."""
+    registers) into y (video stride ys) / y2 / mean / rstd, and y's bf16 rounding into y16 (same offsets) when given;
+    False (nothing launched) for shapes it does not serve."""
     try:
         _n.call("pdvc_groupnorm_rows_forward_fused_f32", _n.ptr(x), N, T, C, G, float(eps), _n.ptr(weight),
-                _n.ptr(bias), _n.ptr_any(y), ys, _n.ptr(y2), _n.ptr(mean), _n.ptr(rstd), _n.stream())
+                _n.ptr(bias), _n.ptr_any(y), ys, _n.ptr(y2), _n.ptr(mean), _n.ptr(rstd),
+                None if y16 is None else _n.ptr_any(y16), _n.stream())
         return True
     except _n.NativeError:
         return False
@@ -152,7 +154,7 @@ class GroupNormFlatFunction(Function):
     the slice's inside the backward kernels instead of by autograd."""
 
     @staticmethod
-    def forward(ctx, flat, x, weight, bias, groups, eps, start, want_copy):
+    def forward(ctx, flat, x, weight, bias, groups, eps, start, want_copy, flat16=None):
         x = x.contiguous()
         N, T, C = x.shape
         S = flat.shape[1]
@@ -161,11 +163,15 @@ class GroupNormFlatFunction(Function):
         y2 = torch.empty_like(x) if want_copy else None
         mean = torch.empty(N * groups, **kw)
         rstd = torch.empty(N * groups, **kw)
-        if not _fused_forward(x, N, T, C, groups, eps, weight, bias, flat[:, start:start + T], S * C, y2, mean, rstd):
+        s16 = None if flat16 is None else flat16[:, start:start + T]
+        if not _fused_forward(x, N, T, C, groups, eps, weight, bias, flat[:, start:start + T], S * C, y2, mean, rstd,
+                              s16):
             ws = torch.empty(N * chunks * groups * 3, **kw)
             _n.call("pdvc_groupnorm_rows_forward_out_f32", _n.ptr(x), N, T, C, groups, float(eps), _n.ptr(weight),
                     _n.ptr(bias), _n.ptr(ws), _n.ptr_any(flat[:, start:start + T]), S * C, _n.ptr(y2), _n.ptr(mean),
                     _n.ptr(rstd), _n.stream())
+            if s16 is not None:  # the chunked forms write no bf16 copy: the slice is rounded here
+                s16.copy_(flat[:, start:start + T])
         ctx.mark_dirty(flat)
         ctx.save_for_backward(x, weight, mean, rstd)
         ctx.meta = (groups, start, S, want_copy)
@@ -192,7 +198,7 @@ class GroupNormFlatFunction(Function):
         gsum = colsum(cpart)
         # the slice [start, start + T) of the incoming flat was overwritten: only the earlier levels' functions
         # (which read their own slices) consume this gradient, so it passes through unmasked
-        return d_flat, dx, gsum[:C].contiguous(), gsum[C:].contiguous(), None, None, None, None
+        return d_flat, dx, gsum[:C].contiguous(), gsum[C:].contiguous(), None, None, None, None, None
 
 
 def group_norm_rows_ok(gn, x):
@@ -202,10 +208,11 @@ def group_norm_rows_ok(gn, x):
             and cpg % 4 == 0 and (cpg // 4) & (cpg // 4 - 1) == 0)
 
 
-def group_norm_rows_into(gn, x, flat, start, want_copy):
-    """group_norm_rows(gn, x) written into flat[:, start:start + T] (see GroupNormFlatFunction).  Returns the new
-    flat (and the contiguous result when want_copy)."""
-    return GroupNormFlatFunction.apply(flat, x, gn.weight, gn.bias, gn.num_groups, gn.eps, start, want_copy)
+def group_norm_rows_into(gn, x, flat, start, want_copy, flat16=None):
+    """group_norm_rows(gn, x) written into flat[:, start:start + T] (see GroupNormFlatFunction), and its bf16 rounding
+    into the same rows of flat16 when given (the bf16 mode).  Returns the new flat (and the contiguous result when
+    want_copy)."""
+    return GroupNormFlatFunction.apply(flat, x, gn.weight, gn.bias, gn.num_groups, gn.eps, start, want_copy, flat16)
 
 
 def conv1d_rows(conv, x):

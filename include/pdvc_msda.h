@@ -461,10 +461,11 @@ int pdvc_groupnorm_rows_backward_strided_f32(const float* x, const float* dy, lo
 /* Single-pass forms: one workgroup per (video, 64-channel block) holds the block in registers, so x (and dy) are
  * read once -- the forms above read them twice (statistics / group sums, then apply / dx).  T <= 512, C a multiple
  * of 64, C/G <= 64; any other shape returns PDVC_ERR_UNSUPPORTED before launching anything (use the forms above).
- * No workspaces; the backward's col_partials are (N, 2, C): one row of [dgamma | dbeta] partials per video. */
+ * No workspaces; the backward's col_partials are (N, 2, C): one row of [dgamma | dbeta] partials per video.  y16
+ * (NULL for none, 8-byte aligned): the forward also writes y's bf16 rounding (torch's RNE cast) at y's offsets. */
 int pdvc_groupnorm_rows_forward_fused_f32(const float* x, int N, int T, int C, int G, float eps, const float* gamma,
                                           const float* beta, float* y, long y_video_stride, float* y_copy,
-                                          float* mean, float* rstd, void* stream);
+                                          float* mean, float* rstd, uint16_t* y16, void* stream);
 int pdvc_groupnorm_rows_backward_fused_f32(const float* x, const float* dy, long dy_video_stride,
                                            const float* dy_add, const float* mean, const float* rstd,
                                            const float* gamma, int N, int T, int C, int G, float* col_partials,
@@ -502,6 +503,14 @@ int pdvc_cap_value_grad_ranged_f32(const uint8_t* value_pad_mask, const int32_t*
                                    int max_rows_per_video, const int32_t* video_row_start, const int32_t* video_rows,
                                    const int32_t* step_rows, const float* save_loc, const float* grad_samples,
                                    float* grad_value, float* grad_value_level_sums, void* stream);
+/* bf16 mode (pdvc/precision.py): pdvc_cap_value_grad_ranged_f32 also writing grad_value's bf16 rounding (torch's RNE
+ * cast) into grad_value16 (same layout, 4-byte aligned; num_heads * head_dim even). */
+int pdvc_cap_value_grad_ranged_f32_bf16out(const uint8_t* value_pad_mask, const int32_t* level_T, int num_levels,
+                                           int batch, int num_heads, int head_dim, int num_point, int rows, int steps,
+                                           int max_rows_per_video, const int32_t* video_row_start,
+                                           const int32_t* video_rows, const int32_t* step_rows, const float* save_loc,
+                                           const float* grad_samples, float* grad_value, float* grad_value_level_sums,
+                                           uint16_t* grad_value16, void* stream);
 /* pdvc_cap_value_grad_ranged_f32 with rank-1 sample gradients: sample (step, row, head, k) has gradient
  * grad_scale[step, row, head, k] * grad_rows[step, row, head, :] -- grad_rows (steps, rows, heads, head_dim),
  * grad_scale (steps, rows, heads, 16) (the caption step's probabilities times its attended-row gradient). */

@@ -508,3 +508,24 @@ def test_msda_bf16out_decoder_grad_value_only():
     assert torch.equal(_bits(gv16), _bits(gv1.to(torch.bfloat16)))
     with pytest.raises(_n.NativeError):
         bwd(True, torch.empty(proj.shape, device=DEV, dtype=torch.bfloat16))
+
+
+@pytest.mark.parametrize("T", [256, 600])
+def test_base_encoder_flat_buffer_bf16_shadow(T):
+    """bf16 mode: the base encoder's levels write their bf16 rounding beside the flattened (N, sum T_l, d) buffer (the
+    single-pass GroupNorm's y16; T = 600 puts level 0 on the chunked forms, whose slice is rounded by a cast) and the
+    finished buffer carries it as its cached rounding: torch's bf16 cast of the buffer, bit for bit."""
+    from pdvc.base_encoder import BaseEncoder
+    from pdvc.precision import bf16_matmul
+    torch.manual_seed(T)
+    enc = BaseEncoder(4, 768, 512).to(DEV)
+    N = 3
+    vf = torch.randn(N, T, 768, device=DEV)
+    mask = torch.zeros(N, T, dtype=torch.bool, device=DEV)
+    dur = torch.tensor([100.0, 37.0, 12.0], device=DEV)
+    with bf16_matmul():
+        srcs, _, _ = enc(vf, mask, dur)
+    flat = srcs[0]._pdvc_flat[0]
+    ent = flat.__dict__.get("_pdvc_bf16")
+    assert ent is not None and ent[0] == flat._version
+    assert torch.equal(_bits(ent[1]), _bits(flat.to(torch.bfloat16)))

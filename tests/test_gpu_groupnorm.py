@@ -131,7 +131,7 @@ def test_groupnorm_single_pass_forms_serve_the_pyramid_shapes():
         y = torch.full_like(x, 7.0)
         mean, rstd = torch.empty(N * G, device=DEV), torch.empty(N * G, device=DEV)
         args = (_n.ptr(x), N, T, C, G, 1e-5, _n.ptr(w), _n.ptr(b), _n.ptr(y), T * C, None, _n.ptr(mean), _n.ptr(rstd),
-                _n.stream())
+                None, _n.stream())
         if not ok:
             with pytest.raises(_n.NativeError):
                 _n.call("pdvc_groupnorm_rows_forward_fused_f32", *args)

@@ -807,6 +807,44 @@ def test_cap_value_grad_rank1_matches_materialised(D, M, masked):
     assert out[0][0].abs().max().item() > 0
 
 
+@pytest.mark.parametrize("n,R", [(3, 10), (25, 600)])
+def test_cap_value_grad_bf16out_rounds_like_torch(n, R):
+    """pdvc_cap_value_grad_ranged_f32_bf16out (the bf16 mode's caption dU): grad_value and its level sums as the plain
+    form (to the counting sort's rounding), and beside grad_value its bf16 rounding, bit for bit torch's cast of the
+    grad_value it wrote; 25 steps of ~200 rows per video split the samples into several accumulating chunks of steps
+    (the LDS budget: the last chunk writes the final rows)."""
+    from pdvc import _native as _n
+    rng = np.random.RandomState(n)
+    T_l = [24, 12, 6, 3]
+    S, Nv, M, D = sum(T_l), 3, 1, 512
+    rv = rng.randint(0, Nv, size=R)
+    order = np.argsort(rv, kind="stable")
+    starts = np.concatenate([[0], np.cumsum(np.bincount(rv, minlength=Nv))]).astype(np.int32)
+    loc = cu(rng.uniform(-0.1, 1.1, size=(n, R, M, 16)), torch.float32)
+    gs = cu(rng.randn(n, R, M, 16, D), torch.float32)
+    vs, vr = cu(starts), cu(order.astype(np.int32))
+    max_rows = int(np.bincount(rv, minlength=Nv).max())
+    lvl = _n.int_array(T_l)
+    out = []
+    for bf in (False, True):
+        gv = torch.full((Nv, S, M, D), 3.0, device=DEV)
+        ls = torch.empty(Nv, 4, M * D, device=DEV)
+        g16 = torch.zeros(gv.shape, device=DEV, dtype=torch.bfloat16)
+        args = (None, lvl, 4, Nv, M, D, 4, R, n, max_rows, _n.ptr(vs), _n.ptr(vr), None, _n.ptr(loc), _n.ptr(gs),
+                _n.ptr(gv), _n.ptr(ls))
+        if bf:
+            _n.call("pdvc_cap_value_grad_ranged_f32_bf16out", *args, _n.ptr(g16), _n.stream())
+        else:
+            _n.call("pdvc_cap_value_grad_ranged_f32", *args, _n.stream())
+        torch.cuda.synchronize()
+        out.append((gv, ls, g16))
+    for a, b in zip(out[0][:2], out[1][:2]):
+        assert (a - b).abs().max().item() <= 1e-6 * (a.abs().max().item() + 1.0)
+    gv1, g16 = out[1][0], out[1][2]
+    assert torch.equal(g16.view(torch.int16), gv1.to(torch.bfloat16).view(torch.int16))
+    assert gv1.abs().max().item() > 0
+
+
 def test_cap_softattn_forward_rejects_other_widths():
     """the fused step is the 512-wide form only: any other head width is PDVC_ERR_UNSUPPORTED, not a wrong answer"""
     from pdvc import _native as _n
