@@ -838,8 +838,10 @@ def test_cap_value_grad_bf16out_rounds_like_torch(n, R):
             _n.call("pdvc_cap_value_grad_ranged_f32", *args, _n.stream())
         torch.cuda.synchronize()
         out.append((gv, ls, g16))
+    # the counting sort places a row's samples in atomic order: the two runs' sums agree to fp32 rounding of sums of up
+    # to a few thousand terms at the (25, 600) size (measured 1.1e-6 of the magnitude), not bitwise
     for a, b in zip(out[0][:2], out[1][:2]):
-        assert (a - b).abs().max().item() <= 1e-6 * (a.abs().max().item() + 1.0)
+        assert (a - b).abs().max().item() <= 1e-5 * (a.abs().max().item() + 1.0)
     gv1, g16 = out[1][0], out[1][2]
     assert torch.equal(g16.view(torch.int16), gv1.to(torch.bfloat16).view(torch.int16))
     assert gv1.abs().max().item() > 0
