@@ -21,6 +21,8 @@ from .linear import colsum, dense, wgrad_mm
 GN_ROWS = 64  # rows per stats chunk (csrc/groupnorm.hip kGnRows)
 # the stride-2 conv's previous-odd-row tap in an accumulate epilogue (A/B switch: PDVC_CONV_TAP_EPILOGUE=0)
 _TAP_EPILOGUE = os.environ.get("PDVC_CONV_TAP_EPILOGUE", "1") != "0"
+# its backward on row-shifted views instead of a shifted copy of the gradient (A/B switch: PDVC_CONV_SHIFT_VIEWS=0)
+_SHIFT_VIEWS = os.environ.get("PDVC_CONV_SHIFT_VIEWS", "1") != "0"
 
 
 class ConvS2RowsFunction(Function):
@@ -62,6 +64,9 @@ class ConvS2RowsFunction(Function):
         X2, w12, w0 = ctx.saved_tensors
         N, T, C, L, O, Tin = ctx.shape
         dy2 = dy.reshape(N * L, O).contiguous()
+        R = N * L
+        if _SHIFT_VIEWS and R >= 64 and R % 32 == 0 and O % 32 == 0 and C % 4 == 0:
+            return ConvS2RowsFunction._backward_views(ctx, dy2, X2, w12, w0, N, T, C, L, O, Tin)
         dz = torch.empty_like(dy2).view(N, L, O)  # dy shifted up one row per video, zero at the last (one write)
         dz[:, :-1] = dy2.view(N, L, O)[:, 1:]
         dz[:, -1] = 0.0
@@ -75,6 +80,37 @@ class ConvS2RowsFunction(Function):
             gb = dy2.new_empty(dy2.shape[1]) if ctx.needs_input_grad[2] else None
             g12 = wgrad_mm(dy2, X2, db=gb)  # (the bias gradient from the same pass over dy)
             g0 = wgrad_mm(dz2, X2[:, C:])
+            gw = torch.stack([g0, g12[:, :C], g12[:, C:]], 2)
+        elif ctx.needs_input_grad[2]:
+            gb = colsum(dy2)
+        return gx, gw, gb
+
+    @staticmethod
+    def _backward_views(ctx, dy2, X2, w12, w0, N, T, C, L, O, Tin):
+        """The backward without the shifted gradient dz (dz[r] = dy[r + 1] within a video, 0 at its last row): the W0
+        tap's products run on views shifted by one row -- dy2[1:] against the rows before -- and the pairs that cross
+        a video boundary are taken out again: the data gradient's rows they reach (each video's last odd row) are
+        restored from a copy, and the weight gradient subtracts their (N - 1)-row product.  No (N, L, O) copy."""
+        R = N * L
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            dX2 = mm_dgrad(dy2, w12)
+            d3 = dX2.view(N, L, 2 * C)
+            keep = d3[:-1, -1, C:].clone() if N > 1 else None  # each video's last odd row: its tap is the padding
+            mm_dgrad(dy2[1:], w0, out=dX2[:-1, C:])
+            if keep is not None:
+                d3[:-1, -1, C:] = keep
+            gx = d3.view(N, T, C)[:, :Tin]
+        if ctx.needs_input_grad[1]:
+            gb = dy2.new_empty(O) if ctx.needs_input_grad[2] else None
+            g12 = wgrad_mm(dy2, X2, db=gb)  # (the bias gradient from the same pass over dy)
+            # g0 = sum over rows r < R - 1 of dy2[r + 1]^T x_odd[r], minus the cross-video pairs: the first R - 32 rows
+            # as one split-K product (its row count a multiple of 32), the last 31 and the corrections as small ones
+            xo = X2[:, C:]
+            g0 = wgrad_mm(dy2[1:R - 31], xo[:R - 32])
+            g0.addmm_(dy2[R - 31:].t(), xo[R - 32:R - 1])
+            if N > 1:
+                g0.addmm_(dy2.view(N, L, O)[1:, 0].t(), xo.view(N, L, C)[:-1, -1], alpha=-1.0)
             gw = torch.stack([g0, g12[:, :C], g12[:, C:]], 2)
         elif ctx.needs_input_grad[2]:
             gb = colsum(dy2)

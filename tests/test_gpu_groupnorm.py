@@ -151,3 +151,34 @@ def test_groupnorm_single_pass_forms_serve_the_pyramid_shapes():
         got = cp.double().sum(0)
         assert (got[:C] - dg).abs().max().item() <= 1e-4 * (dg.abs().max().item() + 1.0)
         assert (got[C:] - db).abs().max().item() <= 1e-4 * (db.abs().max().item() + 1.0)
+
+
+@pytest.mark.parametrize("N,T", [(64, 512), (5, 37), (1, 256), (3, 64)])
+def test_conv_s2_backward_on_shifted_views(N, T, monkeypatch):
+    """The stride-2 conv's backward on row-shifted views (conv_rows.py _backward_views: no shifted copy of dy; the
+    W0 tap's cross-video pairs restored / subtracted) against nn.Conv1d's gradients in float64 and against the
+    shifted-copy backward (PDVC_CONV_SHIFT_VIEWS=0), every product on gemm3 (MIN_ROWS = 0); ragged T, N = 1 included
+    (shapes whose N * ceil(T/2) rows are not a multiple of 32 take the copy form)."""
+    import pdvc.ops.functions.gemm3 as G
+    import pdvc.ops.functions.conv_rows as CR
+    monkeypatch.setattr(G, "MIN_ROWS", 0)
+    torch.manual_seed(N * 7 + T)
+    C, O = 512, 512
+    x = torch.randn(N, T, C, device=DEV)
+    w = torch.randn(O, C, 3, device=DEV) * C ** -0.5
+    b = torch.randn(O, device=DEV)
+    g = torch.randn(N, (T + 1) // 2, O, device=DEV)
+    got = {}
+    for views in (True, False):
+        monkeypatch.setattr(CR, "_SHIFT_VIEWS", views)
+        xx, ww, bb = (t.clone().requires_grad_() for t in (x, w, b))
+        CR.ConvS2RowsFunction.apply(xx, ww, bb).backward(g)
+        got[views] = (xx.grad, ww.grad, bb.grad)
+    xd, wd, bd = (t.double().requires_grad_() for t in (x, w, b))
+    F.conv1d(xd.transpose(1, 2), wd, bd, stride=2, padding=1).transpose(1, 2).backward(g.double())
+    for views in (True, False):
+        for a, r, name in zip(got[views], (xd.grad, wd.grad, bd.grad), ("dx", "dw", "db")):
+            err = (a.double() - r).abs().max().item()
+            assert err <= 1e-5 * (r.abs().max().item() + 1.0), (views, name, err)
+    for a, c in zip(got[True], got[False]):
+        assert (a - c).abs().max().item() <= 1e-5 * (c.abs().max().item() + 1.0)
