@@ -21,7 +21,7 @@ from .ops.functions import add_dropout_layernorm
 
 from .box_ops import inverse_sigmoid
 from .ops.functions import linear as _lin
-from .ops.functions.linear import PackedLinearFunction, add_row_bias, dense
+from .ops.functions.linear import PackedLinearFunction, add_row_bias, dense, expand_rows
 from .ops.modules import MSDeformAttn
 from .ops.modules.linear import Linear
 from .ops.functions.attention import query_self_attention
@@ -128,8 +128,8 @@ class DeformableTransformer(nn.Module):
         # (the reference applies the Linear to the expanded (bs, Q, d) tensor: the same values, bs times the work)
         reference_points = self.reference_points(query_embed).sigmoid().unsqueeze(0).expand(bs, -1, -1).contiguous()
         pos_rows, tgt_rows = query_embed, tgt
-        query_embed = query_embed.unsqueeze(0).expand(bs, -1, -1)
-        tgt = tgt.unsqueeze(0).expand(bs, -1, -1)
+        query_embed = expand_rows(query_embed, bs)
+        tgt = expand_rows(tgt, bs)
         # the (Q, d) rows every video repeats, for the first decoder layer's in_proj (see _shared_rows)
         query_embed.__dict__["_pdvc_rows"] = pos_rows
         tgt.__dict__["_pdvc_rows"] = tgt_rows
@@ -267,8 +267,8 @@ class QuerySelfAttention(nn.Module):
             qk = dense(qk_in, w[:2 * E], b[:2 * E])
             v = dense(v_in, w[2 * E:], b[2 * E:])
         if batch is not None:
-            qk = qk.unsqueeze(0).expand(batch, -1, -1).contiguous()
-            v = v.unsqueeze(0).expand(batch, -1, -1).contiguous()
+            qk = expand_rows(qk, batch).contiguous()
+            v = expand_rows(v, batch).contiguous()
         p = self.dropout if self.training else 0.0
         out = query_self_attention(qk, v, key_padding_mask, self.num_heads, p)
         return self.out_proj(out)

@@ -147,6 +147,32 @@ def add_row_bias(x, bias):
     return AddRowBias.apply(x, bias)
 
 
+class ExpandRowsFunction(Function):
+    """t (Q, C) broadcast to (bs, Q, C) -- the decoder's query embedding and target rows, the same for every video
+    (deformable_transformer.py:186-188 in the reference: query_embed.unsqueeze(0).expand(bs, -1, -1)).  Forward is
+    torch's expand (a view); the backward sums the bs gradient slices as one column sum over the (bs, Q*C) view
+    (colsum) instead of torch's reduction over the batch dimension."""
+
+    @staticmethod
+    def forward(ctx, t, bs):
+        ctx.shape = t.shape
+        return t.unsqueeze(0).expand(bs, *t.shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        return colsum(g.reshape(g.shape[0], -1).contiguous()).view(ctx.shape), None
+
+
+def expand_rows(t, bs):
+    """t.unsqueeze(0).expand(bs, ...) with a column-sum backward (ExpandRowsFunction) for fp32 GPU rows."""
+    if not (t.is_cuda and t.dtype == torch.float32 and t.requires_grad and _EXPAND_COLSUM):
+        return t.unsqueeze(0).expand(bs, *t.shape)
+    return ExpandRowsFunction.apply(t, bs)
+
+
+_EXPAND_COLSUM = os.environ.get("PDVC_EXPAND_COLSUM", "1") != "0"  # A/B switch
+
+
 def wgrad_mm(gy, x, out=None, db=None):
     """gy^T x for row-major gy (rows, O) and x (rows, I): the weight-gradient product, split over K.  out: a
     contiguous (O, I) destination (a row block of a packed weight's gradient).  db: an (O,) destination for the
