@@ -73,6 +73,8 @@ def _gemm(inp, a, b, out, b16):
         torch.ops.aten.addmm.dtype_out(inp, a.to(_BF16), b16, torch.float32, out=out)
 
 
+# the per-step gradients' sums over the steps as one contiguous reduction (PDVC_STEP_SUM_WHOLE=0: two strided ones, A/B)
+_STEP_SUM_WHOLE = os.environ.get("PDVC_STEP_SUM_WHOLE", "1") != "0"
 # bf16 mode: the caption dU written with its bf16 rounding by its value-gradient pass (PDVC_CAP_DU_SHADOW=0: cast, A/B)
 _DU_SHADOW = os.environ.get("PDVC_CAP_DU_SHADOW", "1") != "0"
 
@@ -319,8 +321,12 @@ class CaptionDecodeFunction(Function):
                         _n.ptr(dCLIP_all), _n.ptr(gv), _n.ptr(lsums), st)
         # weight gradients: one GEMM each over every (step, row)
         d_gates = dHP[..., n_off + A:]                       # (n, R, 4H), row stride Ph: xe's gradient as is
-        d_hs_g = d_gates.sum(0)
-        d_off_hs = dHP[..., :n_off].sum(0)
+        if _STEP_SUM_WHOLE:  # one reduction over the steps of the contiguous (n, R * Ph) buffer, both slices of it
+            d_all = dHP.sum(0)
+            d_hs_g, d_off_hs = d_all[:, n_off + A:], d_all[:, :n_off]
+        else:  # two reductions over strided column slices (A/B)
+            d_hs_g = d_gates.sum(0)
+            d_off_hs = dHP[..., :n_off].sum(0)
         if n > 1:
             dW_h = wgrad_mm(dHP[1:].reshape(-1, Ph), HS[:, :-1].transpose(0, 1).reshape(-1, H))
         else:
